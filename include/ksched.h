@@ -1,0 +1,259 @@
+/*
+ * ksched.h — C ABI of the MI355X Filter/Score evaluator (libksched.so).
+ *
+ * Drop-in boundary for the debuggable scheduler's per-(pod, node, plugin) hot
+ * path.  Today the upstream framework calls, per pod and per node, the wrapped
+ * in-tree plugins:
+ *   PreFilter       simulator/scheduler/plugin/wrappedplugin.go:491 (-> :504)
+ *   Filter          simulator/scheduler/plugin/wrappedplugin.go:523 (-> :535)
+ *   PreScore        simulator/scheduler/plugin/wrappedplugin.go:459 (-> :472)
+ *   Score           simulator/scheduler/plugin/wrappedplugin.go:420 (-> :433)
+ *   NormalizeScore  simulator/scheduler/plugin/wrappedplugin.go:388 (-> :400)
+ *   Reserve/assume  simulator/scheduler/plugin/wrappedplugin.go:622 (AddSelectedNode)
+ * and each call lands in Store (resultstore/store.go:423,461,481,522,537,562).
+ * A cgo shim calls ksg_eval() ONCE per pod at PreFilter time,
+ * stashes the returned SoA in CycleState, and answers every Filter / Score /
+ * NormalizeScore call from it; Reserve calls ksg_commit().  ksg_run_queue()
+ * runs a whole pod queue on the device (filter -> score -> normalise ->
+ * weighted sum -> selectHost -> assume) without returning to the host.
+ *
+ * Conventions: all inputs are caller-owned and copied during the call; all
+ * outputs go to caller-allocated buffers; no pointer is retained after return
+ * (cgo pointer rules).  Every function returns 0 on success or a negative
+ * KSG_E_* code; ksg_last_error() gives the message.  A context is not
+ * thread-safe: the shim serialises calls (one call per pod).  No C++ exception
+ * crosses this boundary.
+ */
+#ifndef KSCHED_H
+#define KSCHED_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSG_ABI_VERSION 1
+
+#define KSG_OK 0
+#define KSG_E_INVALID (-1)     /* bad argument / inconsistent sizes            */
+#define KSG_E_DEVICE (-2)      /* HIP runtime error                            */
+#define KSG_E_NOMEM (-3)       /* device or host allocation failed             */
+#define KSG_E_STATE (-4)       /* call out of order (e.g. eval before load)    */
+#define KSG_E_UNSUPPORTED (-5) /* input outside what the kernels implement     */
+#define KSG_E_SCORE (-6)       /* a normalised score left [0,100] (framework error) */
+
+/* Plugin ids (stable; profile.py uses the same numbering). */
+enum {
+  KSG_PL_NODE_UNSCHEDULABLE = 0,
+  KSG_PL_NODE_NAME = 1,
+  KSG_PL_TAINT_TOLERATION = 2,
+  KSG_PL_NODE_AFFINITY = 3,
+  KSG_PL_NODE_PORTS = 4,
+  KSG_PL_NODE_RESOURCES_FIT = 5,
+  KSG_PL_VOLUME_RESTRICTIONS = 6,
+  KSG_PL_NODE_VOLUME_LIMITS = 7,
+  KSG_PL_VOLUME_BINDING = 8,
+  KSG_PL_VOLUME_ZONE = 9,
+  KSG_PL_POD_TOPOLOGY_SPREAD = 10,
+  KSG_PL_INTER_POD_AFFINITY = 11,
+  KSG_PL_BALANCED_ALLOCATION = 12,
+  KSG_PL_IMAGE_LOCALITY = 13,
+  KSG_NPLUGINS = 14
+};
+
+#define KSG_MAX_RES 8      /* resource columns: 0 cpu (milli), 1 memory, 2 ephemeral, 3.. scalars */
+#define KSG_RES_CPU 0
+#define KSG_RES_MEM 1
+#define KSG_RES_EPH 2
+
+/* Taint effects (taint vocabulary). */
+#define KSG_EFFECT_NO_SCHEDULE 1
+#define KSG_EFFECT_PREFER_NO_SCHEDULE 2
+#define KSG_EFFECT_NO_EXECUTE 3
+
+/* ---- per-node filter status word --------------------------------------
+ * bits 0..7  : 0 = passed every filter that ran; else failing plugin id + 1
+ * bits 8..31 : reason payload
+ *   NodeResourcesFit : bit0 "Too many pods", bit1 cpu, bit2 memory, bit3
+ *                      ephemeral-storage, bit(4+j) scalar column 3+j
+ *   TaintToleration  : taint slot index on the node (message names the taint)
+ *   NodeAffinity     : 1 = pod's affinity/selector
+ *   PodTopologySpread: 1 = missing required label, 2 = skew
+ *   InterPodAffinity : 1 affinity, 2 anti-affinity, 3 existing pods' anti-affinity
+ * KSG_FS_NOT_EVALUATED: node outside the PreFilterResult node set (absent
+ * from filter-result) or pod rejected at PreFilter.                         */
+#define KSG_FS_NOT_EVALUATED 0xFFu
+
+/* ---- cluster snapshot (SoA; column c of node i at [c * n_nodes + i]) ---- */
+typedef struct ksg_nodes {
+  int32_t n_nodes;
+  int32_t n_res;                 /* <= KSG_MAX_RES                                 */
+  const int64_t* alloc;          /* [n_res][n_nodes] allocatable                   */
+  const int64_t* requested;      /* [n_res][n_nodes] NodeInfo.Requested            */
+  const int64_t* nonzero;        /* [2][n_nodes]   NodeInfo.NonZeroRequested cpu,mem */
+  const int32_t* allowed_pods;   /* [n_nodes]                                      */
+  const int32_t* pod_count;      /* [n_nodes] len(NodeInfo.Pods)                   */
+  const uint8_t* unschedulable;  /* [n_nodes] spec.unschedulable                   */
+  int32_t n_label_cols;          /* label keys referenced by any selector / topology */
+  const uint32_t* label_val;     /* [n_label_cols][n_nodes] value id, 0 = absent   */
+  const int64_t* label_num;      /* [n_label_cols][n_nodes] strconv.ParseInt value */
+  const uint8_t* label_num_ok;   /* [n_label_cols][n_nodes] parse succeeded        */
+  int32_t max_taints;
+  const uint32_t* taints;        /* [max_taints][n_nodes] taint-vocab id + 1 in node order, 0 = end */
+  int32_t n_taint_vocab;
+  const uint8_t* taint_effect;   /* [n_taint_vocab] KSG_EFFECT_*                   */
+  int32_t max_images;
+  const uint32_t* images;        /* [max_images][n_nodes] ascending image id + 1, 0 = end */
+  int32_t n_images;              /* image vocabulary size                          */
+} ksg_nodes;
+
+/* ---- topology tables for PodTopologySpread / InterPodAffinity ----------- */
+#define KSG_TMPL_REQ_ANTI 0      /* existing pods' required anti-affinity term     */
+#define KSG_TMPL_REQ_AFF 1       /* existing pods' required affinity term          */
+#define KSG_TMPL_PREF 2          /* existing pods' preferred (anti-)affinity term  */
+typedef struct ksg_topology {
+  int32_t n_selectors;           /* pod label-selector ids (namespace-scoped)      */
+  int32_t n_templates;           /* term templates owned by pods                   */
+  const int32_t* tmpl_col;       /* [n_templates] label column of the topology key */
+  const int32_t* tmpl_kind;      /* [n_templates] KSG_TMPL_*                       */
+  const int32_t* tmpl_weight;    /* [n_templates] signed weight (PREF) or 1        */
+  const int32_t* col_vocab;      /* [n_label_cols] value ids are < col_vocab[c]     */
+  const uint8_t* col_unique;     /* [n_label_cols] every value on at most one node */
+  const double* log_table;       /* [log_n] Go math.Log(float64(i)), i < log_n     */
+  int32_t log_n;
+} ksg_topology;
+
+/* ---- pods ----------------------------------------------------------------
+ * Encoded pod (144 B).  Variable-length parts live in a shared int32 program
+ * pool; offsets are word indices into it, -1 = absent.  See encoder.py for
+ * the program grammar.                                                      */
+#define KSG_POD_TOL_UNSCHED (1u << 0)   /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
+#define KSG_POD_NA_REQUIRED (1u << 1)   /* has nodeSelector or required node affinity */
+#define KSG_POD_BEST_EFFORT (1u << 2)   /* all BalancedAllocation resource requests zero */
+#define KSG_POD_PREFILTER_REJECT (1u << 3) /* rejected at PreFilter: nothing evaluated */
+typedef struct ksg_pod {
+  int64_t req[KSG_MAX_RES];  /* PodRequests per resource column               */
+  int64_t nz_cpu;            /* non-zero request (100m default per container)   */
+  int64_t nz_mem;            /* non-zero request (200Mi default per container)  */
+  uint32_t flags;            /* KSG_POD_*                                      */
+  uint32_t filter_skip;      /* bit p: plugin p's PreFilter returned Skip      */
+  uint32_t score_skip;       /* bit p: plugin p's PreScore returns Skip (host-decidable part) */
+  int32_t node_name;         /* spec.nodeName as node index; -1 unset; -2 no such node */
+  int32_t n_containers;      /* init + regular containers (ImageLocality)       */
+  int32_t tol;               /* toleration bitmaps: [filter words][prefer words] */
+  int32_t na_req;            /* required node affinity program                 */
+  int32_t na_pref;           /* preferred node affinity program                */
+  int32_t img;               /* ImageLocality program                          */
+  int32_t node_set;          /* PreFilterResult node bitmap (n_nodes bits)      */
+  int32_t pts;               /* PodTopologySpread program                      */
+  int32_t ipa;               /* InterPodAffinity program                       */
+  int32_t commit;            /* selectors matched + templates owned (assume)   */
+  int32_t blob;              /* tol..commit programs are contiguous:           */
+  int32_t blob_len;          /*   prog[blob, blob + blob_len) (staged into LDS) */
+  int32_t pad;
+} ksg_pod;
+
+typedef struct ksg_workload {
+  const ksg_pod* pods;
+  int32_t n_pods;
+  const int32_t* prog;
+  int64_t prog_len;
+} ksg_workload;
+
+/* ---- profile ------------------------------------------------------------ */
+#define KSG_LEAST_ALLOCATED 0
+#define KSG_MOST_ALLOCATED 1
+#define KSG_PROF_BA_SKIP_BEST_EFFORT (1u << 0)
+#define KSG_PROF_IPA_IGNORE_EXISTING_PREF (1u << 1)
+typedef struct ksg_profile {
+  int32_t n_filter;
+  int32_t filter_order[KSG_NPLUGINS];  /* Filter plugins in MultiPoint order      */
+  uint32_t score_mask;                 /* bit p: plugin p runs at Score           */
+  int32_t weight[KSG_NPLUGINS];        /* getScorePluginWeight (0 -> 1)           */
+  int32_t fit_strategy;                /* KSG_LEAST_ALLOCATED / KSG_MOST_ALLOCATED */
+  int32_t fit_n;
+  int32_t fit_res[KSG_MAX_RES];        /* resource columns scored by Fit          */
+  int64_t fit_w[KSG_MAX_RES];
+  int32_t ba_n;
+  int32_t ba_res[KSG_MAX_RES];         /* resource columns of BalancedAllocation  */
+  int32_t hard_pod_affinity_weight;
+  uint32_t flags;                      /* KSG_PROF_*                              */
+  uint32_t fit_ignored_res;            /* bit r: scalar column r ignored by the Fit filter */
+  int32_t pad;
+} ksg_profile;
+
+/* ---- per-pod results ------------------------------------------------------ */
+#define KSG_ST_SCORED (1u << 0)          /* >= 2 feasible nodes: PreScore/Score ran */
+#define KSG_ST_IPA_PREFILTER_SKIP (1u << 1)
+#define KSG_ST_IPA_PRESCORE_SKIP (1u << 2)
+#define KSG_ST_SCORE_ERROR (1u << 3)     /* normalised score outside [0,100]       */
+typedef struct ksg_result {
+  int32_t selected;     /* node index; -1 = unschedulable                      */
+  int32_t n_feasible;
+  uint32_t status;      /* KSG_ST_*                                             */
+  uint32_t score_skip;  /* final PreScore Skip mask (host part | device part)   */
+} ksg_result;
+
+/* Optional capture of everything the wrapped plugins would record.  Arrays are
+ * per pod; ksg_run_queue() writes pod k at offset k * (stride of the array). */
+typedef struct ksg_capture {
+  uint32_t* fstatus;    /* [n_nodes]                 filter status word       */
+  int64_t* raw;         /* [KSG_NPLUGINS][n_nodes]   Score() value            */
+  int64_t* norm;        /* [KSG_NPLUGINS][n_nodes]   after NormalizeScore     */
+  int64_t* total;       /* [n_nodes]                 Σ normalised × weight    */
+} ksg_capture;
+
+/* Mutable node state, for read-back and checkpoints. */
+typedef struct ksg_node_state {
+  int64_t* requested;   /* [n_res][n_nodes] */
+  int64_t* nonzero;     /* [2][n_nodes]     */
+  int32_t* pod_count;   /* [n_nodes]        */
+} ksg_node_state;
+
+typedef struct ksg_replica_summary {
+  int32_t scheduled;
+  int32_t unschedulable;
+  uint64_t placement_hash;   /* FNV-1a over the replica's placements  */
+  int64_t cpu_requested;     /* Σ requested cpu over nodes after the run */
+  int64_t mem_requested;
+} ksg_replica_summary;
+
+typedef struct ksg_ctx ksg_ctx;
+
+int ksg_abi_version(void);
+int ksg_open(int device, ksg_ctx** out);
+int ksg_close(ksg_ctx* ctx);
+const char* ksg_last_error(ksg_ctx* ctx);
+
+int ksg_set_profile(ksg_ctx* ctx, const ksg_profile* prof);
+int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nodes, const ksg_topology* topo);
+int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl);
+
+/* Evaluate pod `pod` (index into the loaded workload) against the current
+ * node state; no state change.  `cap` may be NULL. */
+int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap);
+/* Assume pod `pod` onto node `node` (NodeInfo.AddPod + count tables). */
+int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node);
+/* Schedule pods [first, first+count) in order on the device.  placements
+ * [count]; results [count] may be NULL; cap may be NULL (else per-pod arrays
+ * of count * n_nodes entries). */
+int ksg_run_queue(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placements,
+                  ksg_result* results, ksg_capture* cap);
+/* What-if replicas: each replica starts from the loaded node state, uses its
+ * own profile and schedules the same pods [first, first+count).
+ * placements [n_replicas][count]; summaries [n_replicas] may be NULL. */
+int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replicas,
+                     int32_t first, int32_t count, int32_t* placements,
+                     ksg_replica_summary* summaries);
+int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out);
+/* Restore the node state captured at the last ksg_load_nodes(). */
+int ksg_reset_state(ksg_ctx* ctx);
+/* Timing of the last ksg_run_queue / ksg_run_replicas kernel: milliseconds
+ * between HIP events recorded on the stream the kernel was launched on. */
+int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSCHED_H */

@@ -1,0 +1,244 @@
+// Device-side data layout and per-node plugin arithmetic for gfx950.
+//
+// One workgroup owns one scheduling replica.  The pod's programs (tolerations,
+// node-affinity programs, images, topology terms) are staged into LDS once
+// per pod and read by every lane; node columns are read coalesced (lane i of
+// a wave touches node base+i of the same column).  Nothing in this path is a
+// dense contraction, so MFMA is not used: the per-node work is int64 compares,
+// int64 divides and a handful of float64 ops, bound by L2/HBM bytes and by the
+// per-pod barrier latency.
+//
+// Arithmetic restated from the upstream plugins [upstream k8s.io/kubernetes
+// v1.32 pkg/scheduler/framework/plugins/...], identical to oracle/oracle.cpp;
+// compiled with -ffp-contract=off so float64 follows Go's (unfused) operation
+// order.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ksched.h"
+
+#define KSG_BLOB_MAX 4096          // LDS words for one pod's programs
+#define KSG_HIST_MAX 8192          // LDS words for per-pod domain histograms
+
+struct DevCluster {
+  int32_t N, R, L, T, I, V, W;     // W = toleration bitmap words
+  const int64_t* alloc;            // [R][N]
+  const int32_t* allowed;          // [N]
+  const uint8_t* unsched;          // [N]
+  const uint32_t* label_val;       // [L][N]
+  const int64_t* label_num;        // [L][N]
+  const uint8_t* label_num_ok;     // [L][N]
+  const uint32_t* taints;          // [T][N]
+  const uint8_t* taint_effect;     // [V]
+  const uint32_t* images;          // [I][N]
+  // topology
+  int32_t S, n_tmpl;
+  const int32_t* tmpl_col;
+  const int32_t* tmpl_kind;
+  const int32_t* tmpl_weight;
+  const int32_t* tmpl_off;         // [n_tmpl] offset of the template's domain table
+  const int32_t* col_vocab;        // [L]
+  const uint8_t* col_unique;       // [L]
+  const double* log_table;
+  int32_t log_n;
+};
+
+// Mutable per-replica state.  Replica r's arrays start at base + r * stride.
+struct DevState {
+  int64_t* requested;   // [R][N]
+  int64_t* nonzero;     // [2][N]
+  int32_t* pod_count;   // [N]
+  int32_t* cnt;         // [S][N]   pods on node n matching selector s
+  int32_t* tab;         // [Σ template table sizes]  per-domain template tables
+  int32_t* tmpl_total;  // [n_tmpl] pods that contributed to template t
+  // scratch (per replica)
+  int64_t* partial;     // [N] Σ weight × score of un-normalised plugins, -1 = infeasible
+  int64_t* sraw;        // [4][N] raw scores of normalised plugins (taint, NA, PTS, IPA)
+  size_t stride_req, stride_nz, stride_pc, stride_cnt, stride_tab, stride_tt, stride_part, stride_sraw;
+};
+
+__device__ __forceinline__ int64_t ld64(const int32_t* w) {
+  return (int64_t)(((uint64_t)(uint32_t)w[1] << 32) | (uint32_t)w[0]);
+}
+
+// ---- requirement programs (encoder.py grammar); P = pod blob in LDS -------
+__device__ __forceinline__ bool eval_req(const DevCluster& c, const int32_t*& w, int n) {
+  const int col = w[0], op = w[1], nv = w[2];
+  const int32_t* vals = w + 3;
+  w += 3 + nv;
+  if (op == 6) return false;
+  const uint32_t v = c.label_val[(size_t)col * c.N + n];
+  if (op == 0 || op == 1) {
+    bool hit = false;
+    for (int i = 0; i < nv; i++) hit |= ((uint32_t)vals[i] == v);
+    if (op == 0) return v != 0 && hit;
+    return v == 0 || !hit;
+  }
+  if (op == 2) return v != 0;
+  if (op == 3) return v == 0;
+  if (v == 0) return false;
+  const size_t k = (size_t)col * c.N + n;
+  if (!c.label_num_ok[k]) return false;
+  const int64_t bound = ld64(vals), x = c.label_num[k];
+  return op == 4 ? x > bound : x < bound;
+}
+
+__device__ __forceinline__ bool eval_term(const DevCluster& c, const int32_t*& w, int n) {
+  const int nr = *w++;
+  bool ok = nr > 0;
+  for (int i = 0; i < nr; i++) ok = eval_req(c, w, n) && ok;
+  return ok;
+}
+
+__device__ __forceinline__ bool na_required_match(const DevCluster& c, const int32_t* P, int na_req, int n) {
+  if (na_req < 0) return true;
+  const int32_t* w = P + na_req;
+  const int nsel = *w++;
+  bool ok = true;
+  for (int i = 0; i < nsel; i++) ok = eval_req(c, w, n) && ok;
+  if (!ok) return false;
+  const int nterms = *w++;
+  if (nterms < 0) return true;
+  bool any = false;
+  for (int t = 0; t < nterms; t++) any = eval_term(c, w, n) || any;
+  return any;
+}
+
+__device__ __forceinline__ int64_t na_pref_score(const DevCluster& c, const int32_t* P, int na_pref, int n) {
+  const int32_t* w = P + na_pref;
+  const int nterms = *w++;
+  int64_t s = 0;
+  for (int t = 0; t < nterms; t++) {
+    const int weight = *w++;
+    if (eval_term(c, w, n)) s += weight;
+  }
+  return s;
+}
+
+__device__ __forceinline__ bool tol_bit(const int32_t* tolp, uint32_t vid) {
+  return (((uint32_t)tolp[vid >> 5]) >> (vid & 31)) & 1u;
+}
+
+// FindMatchingUntoleratedTaint (NoSchedule | NoExecute): slot or -1.
+__device__ __forceinline__ int untolerated_slot(const DevCluster& c, const int32_t* tolf, int n) {
+  for (int s = 0; s < c.T; s++) {
+    const uint32_t id = c.taints[(size_t)s * c.N + n];
+    if (!id) break;
+    const uint32_t vid = id - 1;
+    const uint8_t e = c.taint_effect[vid];
+    if (e != KSG_EFFECT_NO_SCHEDULE && e != KSG_EFFECT_NO_EXECUTE) continue;
+    if (!tol_bit(tolf, vid)) return s;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int64_t taint_score(const DevCluster& c, const int32_t* tolp, int n) {
+  int64_t k = 0;
+  for (int s = 0; s < c.T; s++) {
+    const uint32_t id = c.taints[(size_t)s * c.N + n];
+    if (!id) break;
+    const uint32_t vid = id - 1;
+    if (c.taint_effect[vid] != KSG_EFFECT_PREFER_NO_SCHEDULE) continue;
+    k += !tol_bit(tolp, vid);
+  }
+  return k;
+}
+
+__device__ __forceinline__ uint32_t fit_filter(const DevCluster& c, const ksg_pod& p, const int64_t* requested,
+                                               int32_t pod_count, uint32_t ignored, int n) {
+  uint32_t bits = 0;
+  if ((int64_t)pod_count + 1 > (int64_t)c.allowed[n]) bits |= 1u;
+  for (int r = 0; r < c.R; r++) {
+    const int64_t q = p.req[r];
+    if (q <= 0) continue;
+    if (r >= 3 && ((ignored >> r) & 1u)) continue;
+    const int64_t a = c.alloc[(size_t)r * c.N + n], u = requested[(size_t)r * c.N + n];
+    if (q > a - u) bits |= 1u << (r + 1);
+  }
+  return bits;
+}
+
+// resourceAllocationScorer.calculateResourceAllocatableRequest
+__device__ __forceinline__ void alloc_req(const DevCluster& c, const ksg_pod& p, const int64_t* requested,
+                                          const int64_t* nonzero, int r, int n, bool use_requested,
+                                          int64_t& a, int64_t& q) {
+  int64_t pr;
+  if (use_requested) pr = p.req[r];
+  else pr = r == KSG_RES_CPU ? p.nz_cpu : (r == KSG_RES_MEM ? p.nz_mem : p.req[r]);
+  a = 0;
+  q = 0;
+  if (pr == 0 && r >= 3) return;
+  a = c.alloc[(size_t)r * c.N + n];
+  int64_t base;
+  if (!use_requested && r == KSG_RES_CPU) base = nonzero[n];
+  else if (!use_requested && r == KSG_RES_MEM) base = nonzero[(size_t)c.N + n];
+  else base = requested[(size_t)r * c.N + n];
+  q = base + pr;
+}
+
+__device__ __forceinline__ int64_t fit_score(const DevCluster& c, const ksg_profile& prof, const ksg_pod& p,
+                                             const int64_t* requested, const int64_t* nonzero, int n) {
+  int64_t num = 0, wsum = 0;
+  for (int i = 0; i < prof.fit_n; i++) {
+    int64_t a, q;
+    alloc_req(c, p, requested, nonzero, prof.fit_res[i], n, false, a, q);
+    if (a == 0) continue;
+    int64_t s;
+    if (prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : ((a - q) * 100) / a;
+    else s = ((q > a ? a : q) * 100) / a;
+    num += s * prof.fit_w[i];
+    wsum += prof.fit_w[i];
+  }
+  return wsum == 0 ? 0 : num / wsum;
+}
+
+__device__ __forceinline__ int64_t ba_score(const DevCluster& c, const ksg_profile& prof, const ksg_pod& p,
+                                            const int64_t* requested, const int64_t* nonzero, int n) {
+  double fr[KSG_MAX_RES];
+  int k = 0;
+  double total = 0.0;
+  for (int i = 0; i < prof.ba_n; i++) {
+    int64_t a, q;
+    alloc_req(c, p, requested, nonzero, prof.ba_res[i], n, true, a, q);
+    if (a == 0) continue;
+    double f = (double)q / (double)a;
+    if (f > 1) f = 1;
+    total += f;
+    fr[k++] = f;
+  }
+  double sd = 0.0;
+  if (k == 2) {
+    sd = fabs((fr[0] - fr[1]) / 2);
+  } else if (k > 2) {
+    const double mean = total / (double)k;
+    double sum = 0.0;
+    for (int i = 0; i < k; i++) sum = sum + (fr[i] - mean) * (fr[i] - mean);
+    sd = sqrt(sum / (double)k);
+  }
+  return (int64_t)((1 - sd) * (double)100);
+}
+
+__device__ __forceinline__ int64_t image_score(const DevCluster& c, const int32_t* P, int img, int n_containers,
+                                               int n) {
+  int64_t sum = 0;
+  if (img >= 0) {
+    const int32_t* w = P + img;
+    const int cnt = *w++;
+    for (int i = 0; i < cnt; i++, w += 3) {
+      const uint32_t id = (uint32_t)w[0];
+      const int64_t contrib = ld64(w + 1);
+      for (int s = 0; s < c.I; s++) {
+        const uint32_t x = c.images[(size_t)s * c.N + n];
+        if (!x || x > id) break;
+        if (x == id) { sum += contrib; break; }
+      }
+    }
+  }
+  const int64_t mb = 1024 * 1024, minT = 23 * mb;
+  const int64_t mx = 1000 * mb * (int64_t)n_containers;
+  if (sum < minT) sum = minT;
+  else if (sum > mx) sum = mx;
+  return 100 * (sum - minT) / (mx - minT);
+}

@@ -1,0 +1,258 @@
+"""Debuggable-scheduler mirror over the device evaluator.
+
+`DebuggableScheduler` plays the role of the upstream framework + the
+simulator's wrapped plugins for the Filter/Score path:
+
+- one `Engine.eval()` per pod replaces the N x F wrapped `Filter` calls and
+  N x S wrapped `Score` calls (wrappedplugin.go:523, :420) and the
+  `NormalizeScore` calls (:388);
+- the device result (filter status words, raw and normalised scores) is
+  written into `annotations.ResultStore` exactly as the wrappers would have
+  written it: `"passed"` / rejection message per (node, plugin) up to the
+  first rejection (store.go:423), raw score + raw*weight (store.go:461),
+  normalised*weight overwrite for plugins with ScoreExtensions (store.go:481),
+  PreFilter / PreScore statuses with Skip recorded as "" (store.go:522, :537);
+- Reserve records the selected node (wrappedplugin.go:622 -> store.go:562) and
+  `Engine.commit()` assumes the pod.
+
+`DevicePlugin` shows the per-plugin shape a cgo shim presents to the
+framework (Name / Filter / Score / NormalizeScore answering from the per-pod
+device result in CycleState).  The Go version of that shim is INTEGRATION.md.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import annotations as A
+from . import encoder as E
+from . import model as m
+from . import native
+from . import profile as P
+
+FS_NOT_EVALUATED = E.FS_NOT_EVALUATED
+
+MSG_UNSCHEDULABLE = "node(s) were unschedulable"
+MSG_NODE_NAME = "node(s) didn't match the requested node name"
+MSG_NODE_AFFINITY = "node(s) didn't match Pod's node affinity/selector"
+MSG_NA_CONFLICT = "pod affinity terms conflict"
+MSG_PTS = "node(s) didn't match pod topology spread constraints"
+MSG_PTS_LABEL = MSG_PTS + " (missing required label)"
+MSG_IPA = {1: "node(s) didn't match pod affinity rules",
+           2: "node(s) didn't match pod anti-affinity rules",
+           3: "node(s) didn't satisfy existing pods anti-affinity rules"}
+
+
+def fit_reasons(bits: int, res_names: Sequence[str]) -> List[str]:
+    """noderesources.fitsRequest reason order: pods, cpu, memory, ephemeral,
+    then scalar resources (Go map order; sorted by column here)."""
+    out = []
+    if bits & 1:
+        out.append("Too many pods")
+    names = {0: "cpu", 1: "memory", 2: "ephemeral-storage"}
+    for r in range(len(res_names)):
+        if bits & (1 << (r + 1)):
+            out.append("Insufficient " + names.get(r, res_names[r]))
+    return out
+
+
+class Decoder:
+    """Turns status words back into the upstream message strings."""
+
+    def __init__(self, enc: E.Encoder):
+        self.enc = enc
+        self.cl = enc.cluster
+        self.taints = enc.cluster.arrays["taints"]
+
+    def message(self, st: int, node: int) -> str:
+        pl = (st & 0xFF) - 1
+        reason = st >> 8
+        if pl == P.NODE_UNSCHEDULABLE:
+            return MSG_UNSCHEDULABLE
+        if pl == P.NODE_NAME:
+            return MSG_NODE_NAME
+        if pl == P.TAINT_TOLERATION:
+            t = self.cl.taint_vocab[int(self.taints[reason, node]) - 1]
+            return f"node(s) had untolerated taint {{{t.key}: {t.value}}}"
+        if pl == P.NODE_AFFINITY:
+            return MSG_NODE_AFFINITY
+        if pl == P.NODE_RESOURCES_FIT:
+            return ", ".join(fit_reasons(reason, self.cl.res_names))
+        if pl == P.POD_TOPOLOGY_SPREAD:
+            return MSG_PTS_LABEL if reason == 1 else MSG_PTS
+        if pl == P.INTER_POD_AFFINITY:
+            return MSG_IPA[reason]
+        raise ValueError(f"unexpected status word {st:#x}")
+
+
+@dataclass
+class PodCycle:
+    """Everything the device computed for one pod (one CycleState)."""
+    pod: int
+    selected: int
+    n_feasible: int
+    status: int
+    score_skip: int
+    fstatus: np.ndarray
+    raw: np.ndarray
+    norm: np.ndarray
+    total: np.ndarray
+
+
+class DebuggableScheduler:
+    """Framework loop + wrapped-plugin recording, with the evaluator on the GPU."""
+
+    def __init__(self, nodes: Sequence[m.Node], pods: Sequence[m.Pod], prof: P.Profile,
+                 engine: Optional[native.Engine] = None, bound: Sequence = ()):
+        """`pods` holds every pod that will ever be bound or scheduled;
+        `bound` = [(pod_index, node_index)] already running at start."""
+        self.nodes = list(nodes)
+        self.pods = list(pods)
+        self.prof = prof
+        self.enc = E.Encoder(self.nodes, self.pods, prof)
+        self.engine = engine if engine is not None else native.Engine()
+        self.engine.load(self.enc, E.encode_profile(prof, self.enc.cluster.res_names))
+        for pi, ni in bound:
+            self.engine.commit(pi, ni)
+        self.store = A.ResultStore(prof.weights())
+        self.decoder = Decoder(self.enc)
+        self.node_names = self.enc.cluster.node_names
+        self.enabled = set(prof.enabled_ids())
+        self.names_enabled = {n for n, _ in prof.plugins}
+
+    # ---- one cycle --------------------------------------------------------
+    def evaluate(self, pi: int) -> PodCycle:
+        cap = native.CaptureBuffers(len(self.nodes), 1)
+        r = self.engine.eval(pi, cap)
+        return PodCycle(pi, r.selected, r.n_feasible, r.status, r.score_skip, cap.fstatus[0], cap.raw[0],
+                        cap.norm[0], cap.total[0])
+
+    def schedule_one(self, pi: int, record: bool = True) -> int:
+        cyc = self.evaluate(pi)
+        if record:
+            self.record(cyc)
+        if cyc.selected >= 0:
+            self.engine.commit(pi, cyc.selected)
+        return cyc.selected
+
+    def run_queue(self, first: int, count: int):
+        """Device-resident queue: no per-pod host round trip."""
+        return self.engine.run_queue(first, count)
+
+    # ---- recording (what the wrapped plugins write to the Store) ---------
+    def record(self, cyc: PodCycle):
+        pod = self.pods[cyc.pod]
+        rec = self.enc.workload.pods[cyc.pod]
+        ns, name = pod.namespace, pod.name
+        st = self.store
+        fskip = int(rec["filter_skip"])
+        if cyc.status & native.ST_IPA_PREFILTER_SKIP:
+            fskip |= 1 << P.INTER_POD_AFFINITY
+        rejected = bool(rec["flags"] & E.POD_FLAG_PREFILTER_REJECT)
+        # PreFilter (wrappedplugin.go:504-512): RunPreFilterPlugins stops at an
+        # UnschedulableAndUnresolvable rejection.
+        for pid in self.prof.prefilter_order():
+            pname = P.PLUGIN_NAMES[pid]
+            if pid == P.NODE_AFFINITY and rejected:
+                st.AddPreFilterResult(ns, name, pname, MSG_NA_CONFLICT)
+                break
+            node_names = None
+            if pid == P.NODE_AFFINITY and int(rec["node_set"]) >= 0:
+                node_names = self.enc.prefilter_node_names[cyc.pod]
+            st.AddPreFilterResult(ns, name, pname, "" if (fskip >> pid) & 1 else A.SUCCESS, node_names)
+        # Filter
+        order = [p for p in self.prof.filter_order() if not (fskip >> p) & 1]
+        evaluated = []
+        for n in range(len(self.nodes)):
+            s = int(cyc.fstatus[n])
+            if s == FS_NOT_EVALUATED:
+                continue
+            evaluated.append(n)
+            node = self.node_names[n]
+            fail = (s & 0xFF) - 1
+            for pid in order:
+                if pid == fail:
+                    st.AddFilterResult(ns, name, node, P.PLUGIN_NAMES[pid], self.decoder.message(s, n))
+                    break
+                st.AddFilterResult(ns, name, node, P.PLUGIN_NAMES[pid], A.PASSED)
+        if cyc.n_feasible == 0:
+            # DefaultPreemption PostFilter (wrappedplugin.go:562-577): with every
+            # pod at equal priority there is never a victim, so nothing is
+            # nominated and every explicitly evaluated node gets an empty entry.
+            if "DefaultPreemption" in self.names_enabled:
+                st.AddPostFilterResult(ns, name, "", "DefaultPreemption",
+                                       [self.node_names[n] for n in evaluated])
+            return
+        if cyc.n_feasible >= 2:
+            sskip = cyc.score_skip
+            for pid in self.prof.prescore_order():
+                st.AddPreScoreResult(ns, name, P.PLUGIN_NAMES[pid], "" if (sskip >> pid) & 1 else A.SUCCESS)
+            feas = [n for n in range(len(self.nodes)) if cyc.fstatus[n] == 0]
+            for pid in self.prof.score_order():
+                if (sskip >> pid) & 1:
+                    continue
+                pname = P.PLUGIN_NAMES[pid]
+                for n in feas:
+                    st.AddScoreResult(ns, name, self.node_names[n], pname, int(cyc.raw[pid, n]))
+                if P.EXT[pid][4]:
+                    for n in feas:
+                        st.AddNormalizedScoreResult(ns, name, self.node_names[n], pname, int(cyc.norm[pid, n]))
+        if cyc.selected < 0:
+            return
+        # Reserve / Permit / PreBind / Bind of the default plugins.
+        st.AddSelectedNode(ns, name, self.node_names[cyc.selected])
+        if P.VOLUME_BINDING in self.enabled:
+            st.AddReserveResult(ns, name, "VolumeBinding", A.SUCCESS)
+            st.AddPreBindResult(ns, name, "VolumeBinding", A.SUCCESS)
+        if "DefaultBinder" in self.names_enabled:
+            st.AddBindResult(ns, name, "DefaultBinder", A.SUCCESS)
+
+    def annotations(self, pi: int) -> Optional[Dict[str, str]]:
+        pod = self.pods[pi]
+        return self.store.GetStoredResult(pod.namespace, pod.name)
+
+
+class Status:
+    """framework.Status subset: code + reasons (Message joins with ", ")."""
+    SUCCESS, ERROR, UNSCHEDULABLE, UNSCHEDULABLE_AND_UNRESOLVABLE, SKIP = 0, 1, 2, 3, 7
+
+    def __init__(self, code: int = 0, *reasons: str):
+        self.code = code
+        self.reasons = list(reasons)
+
+    def is_success(self) -> bool:
+        return self.code == Status.SUCCESS
+
+    def message(self) -> str:
+        return ", ".join(self.reasons)
+
+
+class DevicePlugin:
+    """One in-tree plugin as the framework sees it, answered from the
+    device's per-pod result.  `Name()` returns the in-tree name so the
+    simulator's wrapper and Store key results exactly as before
+    (wrappedplugin.go:406,438,542)."""
+
+    def __init__(self, sched: DebuggableScheduler, pid: int):
+        self.s = sched
+        self.pid = pid
+
+    def Name(self) -> str:
+        return P.PLUGIN_NAMES[self.pid]
+
+    def Filter(self, cyc: PodCycle, node: int) -> Status:
+        st = int(cyc.fstatus[node])
+        if (st & 0xFF) - 1 == self.pid:
+            code = Status.UNSCHEDULABLE
+            return Status(code, self.s.decoder.message(st, node))
+        return Status()
+
+    def Score(self, cyc: PodCycle, node: int):
+        return int(cyc.raw[self.pid, node]), Status()
+
+    def NormalizeScore(self, cyc: PodCycle, scores: Dict[int, int]) -> Status:
+        for n in scores:
+            scores[n] = int(cyc.norm[self.pid, n])
+        return Status()

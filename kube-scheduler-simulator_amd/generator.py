@@ -1,0 +1,214 @@
+"""Seeded synthetic clusters and pod queues (numpy PCG64).
+
+C1 (seed 1): 100 nodes x 1,000 pods, default profile, Z=4, no taints, 20 % nodeSelector.
+C2 (seed 2): 5,000 x 50,000, Fit(LeastAllocated) + BA + Taint + NodeAffinity;
+             10 % nodes NoSchedule dedicated=<pool>, 10 % PreferNoSchedule spot=true;
+             30 % pods tolerate; 25 % required zone affinity; 25 % preferred
+             instance-type affinity (weights 1-100).
+C3 (seed 3): 15,000 x 150,000, Z=16, 500 apps (Zipf 1.2); every pod: PTS {zone
+             maxSkew 5 ScheduleAnyway, hostname maxSkew 1 DoNotSchedule}; 30 %
+             preferred anti-affinity hostname(same app); 10 % required affinity
+             zone(other app).
+C4 (seed 4): R what-if replicas of the C2 cluster/queue; per replica weights in
+             [1,5] per score plugin and strategy in {LeastAllocated, MostAllocated}
+             drawn from seed 4+r.
+C5 (seed 5): 100,000 nodes; amd.com/gpu on 30 % of nodes, 10 % pods request 1-8;
+             64 taints/node from a 1,024-entry vocabulary (>= 95 % PreferNoSchedule);
+             10,000 images (10 MiB-2 GiB log-uniform), 50 per node Zipf(1.1); pods
+             with 1-3 containers over the same vocabulary.
+
+Every config can be scaled down (n_nodes / n_pods) for parity tests.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import model as m
+from . import profile as P
+
+GI = 1024 ** 3
+MI = 1024 ** 2
+CPU_CHOICES = [100, 250, 500, 1000, 2000, 4000]
+MEM_CHOICES = [128 * MI * (2 ** k) for k in range(7)]   # 128Mi .. 8Gi
+INSTANCE_TYPES = [f"m{k}.{s}" for k in (5, 6) for s in ("large", "xlarge", "2xlarge", "4xlarge")]
+POOLS = [f"pool-{k:02d}" for k in range(32)]
+
+
+def _node(i: int, rng, zones: int, extra_alloc=None) -> m.Node:
+    z = i % zones
+    labels = {
+        m.LABEL_HOSTNAME: f"node-{i:06d}",
+        m.LABEL_ZONE: f"zone-{z}",
+        m.LABEL_REGION: f"region-{z // 4}",
+        "node.kubernetes.io/instance-type": INSTANCE_TYPES[int(rng.integers(len(INSTANCE_TYPES)))],
+        "pool": POOLS[int(rng.integers(len(POOLS)))],
+    }
+    alloc = {
+        m.CPU: int(rng.choice([16, 32, 64, 96])) * 1000,
+        m.MEMORY: int(rng.choice([64, 128, 256, 512])) * GI,
+        m.EPHEMERAL: 200 * GI,
+        m.PODS: 110,
+    }
+    if extra_alloc:
+        alloc.update(extra_alloc)
+    return m.Node(name=f"node-{i:06d}", labels=labels, allocatable=alloc)
+
+
+def _pod(j: int, rng, best_effort_frac=0.05, image: str = "registry.k8s.io/pause:3.10") -> m.Pod:
+    if rng.random() < best_effort_frac:
+        req = {}
+    else:
+        req = {m.CPU: int(rng.choice(CPU_CHOICES)), m.MEMORY: int(rng.choice(MEM_CHOICES))}
+    return m.Pod(name=f"pod-{j:06d}", containers=[m.Container(image=image, requests=req)])
+
+
+def config1(n_nodes: int = 100, n_pods: int = 1000, seed: int = 1):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    Z = 4
+    nodes = [_node(i, rng, Z) for i in range(n_nodes)]
+    pods = []
+    for j in range(n_pods):
+        p = _pod(j, rng)
+        if rng.random() < 0.20:
+            p.node_selector = {m.LABEL_ZONE: f"zone-{int(rng.integers(Z))}"}
+        pods.append(p)
+    return nodes, pods, P.default_profile()
+
+
+def config2(n_nodes: int = 5000, n_pods: int = 50000, seed: int = 2, zones: int = 8):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = [_node(i, rng, zones) for i in range(n_nodes)]
+    for n in nodes:
+        u = rng.random()
+        if u < 0.10:
+            n.taints.append(m.Taint("dedicated", n.labels["pool"], m.NO_SCHEDULE))
+        elif u < 0.20:
+            n.taints.append(m.Taint("spot", "true", m.PREFER_NO_SCHEDULE))
+    pods = []
+    for j in range(n_pods):
+        p = _pod(j, rng)
+        if rng.random() < 0.30:
+            if rng.random() < 0.5:
+                p.tolerations = [m.Toleration("dedicated", m.OP_EQUAL, POOLS[int(rng.integers(len(POOLS)))],
+                                              m.NO_SCHEDULE)]
+            else:
+                p.tolerations = [m.Toleration("spot", m.OP_EXISTS, "", ""),
+                                 m.Toleration("dedicated", m.OP_EXISTS, "", m.NO_SCHEDULE)]
+        if rng.random() < 0.25:
+            k = int(rng.integers(1, 4))
+            zs = tuple(sorted({f"zone-{int(z)}" for z in rng.integers(0, zones, size=k)}))
+            p.node_affinity_required = [m.NodeSelectorTerm(
+                match_expressions=(m.Requirement(m.LABEL_ZONE, m.IN, zs),))]
+        if rng.random() < 0.25:
+            it = INSTANCE_TYPES[int(rng.integers(len(INSTANCE_TYPES)))]
+            p.node_affinity_preferred = [m.PreferredSchedulingTerm(
+                int(rng.integers(1, 101)),
+                m.NodeSelectorTerm(match_expressions=(
+                    m.Requirement("node.kubernetes.io/instance-type", m.IN, (it,)),)))]
+        pods.append(p)
+    return nodes, pods, P.config2_profile()
+
+
+def _zipf_choice(rng, n: int, a: float, size: int):
+    w = 1.0 / np.arange(1, n + 1) ** a
+    w /= w.sum()
+    return rng.choice(n, size=size, p=w)
+
+
+def config3(n_nodes: int = 15000, n_pods: int = 150000, seed: int = 3, zones: int = 16, apps: int = 500):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = [_node(i, rng, zones) for i in range(n_nodes)]
+    app_of = _zipf_choice(rng, apps, 1.2, n_pods)
+    pods = []
+    for j in range(n_pods):
+        p = _pod(j, rng)
+        a = int(app_of[j])
+        p.labels = {"app": f"app-{a:03d}"}
+        sel = m.LabelSelector(match_labels=(("app", f"app-{a:03d}"),))
+        p.topology_spread_constraints = [
+            m.TopologySpreadConstraint(5, m.LABEL_ZONE, m.SCHEDULE_ANYWAY, sel),
+            m.TopologySpreadConstraint(1, m.LABEL_HOSTNAME, m.DO_NOT_SCHEDULE, sel),
+        ]
+        if rng.random() < 0.30:
+            p.pod_anti_affinity_preferred = [m.WeightedPodAffinityTerm(
+                int(rng.integers(1, 101)), m.PodAffinityTerm(sel, m.LABEL_HOSTNAME))]
+        if rng.random() < 0.10:
+            b = int(rng.integers(apps))
+            if b == a:
+                b = (b + 1) % apps
+            osel = m.LabelSelector(match_labels=(("app", f"app-{b:03d}"),))
+            p.pod_affinity_required = [m.PodAffinityTerm(osel, m.LABEL_ZONE)]
+        pods.append(p)
+    return nodes, pods, P.config3_profile()
+
+
+def replica_profiles(n_replicas: int, seed: int = 4) -> List[P.Profile]:
+    """C4: per-replica weights in [1,5] per score plugin and Fit strategy."""
+    out = []
+    for r in range(n_replicas):
+        rng = np.random.Generator(np.random.PCG64(seed + r))
+        w = {k: int(rng.integers(1, 6)) for k in
+             ("TaintToleration", "NodeAffinity", "NodeResourcesFit", "NodeResourcesBalancedAllocation")}
+        strat = P.LEAST_ALLOCATED if rng.random() < 0.5 else P.MOST_ALLOCATED
+        out.append(P.config2_profile(strategy=strat, weights=w))
+    return out
+
+
+def config4(n_replicas: int = 1024, n_nodes: int = 5000, n_pods: int = 50000):
+    nodes, pods, base = config2(n_nodes, n_pods, seed=2)
+    return nodes, pods, base, replica_profiles(n_replicas)
+
+
+def config5(n_nodes: int = 100000, n_pods: int = 100000, seed: int = 5, n_images: int = 10000,
+            taint_vocab: int = 1024, taints_per_node: int = 64, images_per_node: int = 50):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = np.exp(rng.uniform(np.log(10 * MI), np.log(2 * GI), size=n_images)).astype(np.int64)
+    img_names = [f"registry.example.com/img-{k:05d}:v1" for k in range(n_images)]
+    vocab = []
+    for k in range(taint_vocab):
+        eff = m.PREFER_NO_SCHEDULE if rng.random() < 0.97 else m.NO_SCHEDULE
+        vocab.append(m.Taint(f"t{k % 97}.example.com/k{k}", f"v{k % 13}", eff))
+    nodes = []
+    for i in range(n_nodes):
+        extra = {"amd.com/gpu": int(rng.choice([4, 8]))} if rng.random() < 0.30 else None
+        n = _node(i, rng, 16, extra)
+        ts = rng.choice(taint_vocab, size=taints_per_node, replace=False)
+        n.taints = [vocab[int(t)] for t in ts]
+        ims = np.unique(_zipf_choice(rng, n_images, 1.1, images_per_node))
+        n.images = [m.ImageState((img_names[int(k)],), int(sizes[int(k)])) for k in ims]
+        nodes.append(n)
+    pods = []
+    for j in range(n_pods):
+        nc = int(rng.integers(1, 4))
+        conts = []
+        for c in range(nc):
+            req = {m.CPU: int(rng.choice(CPU_CHOICES)), m.MEMORY: int(rng.choice(MEM_CHOICES))}
+            if c == 0 and rng.random() < 0.10:
+                req["amd.com/gpu"] = int(rng.integers(1, 9))
+            conts.append(m.Container(image=img_names[int(_zipf_choice(rng, n_images, 1.1, 1)[0])],
+                                     requests=req))
+        p = m.Pod(name=f"pod-{j:06d}", containers=conts)
+        k = int(rng.integers(0, 8))
+        p.tolerations = [m.Toleration(vocab[int(t)].key, m.OP_EXISTS) for t in
+                         rng.choice(taint_vocab, size=k, replace=False)]
+        pods.append(p)
+    prof = P.Profile(plugins=[("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0),
+                              ("TaintToleration", 3), ("NodeAffinity", 2), ("NodeResourcesFit", 1),
+                              ("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1),
+                              ("DefaultBinder", 0)],
+                     fit_resources=[(m.CPU, 1), (m.MEMORY, 1), ("amd.com/gpu", 1)])
+    return nodes, pods, prof
+
+
+def readme_kat() -> Tuple[List[m.Node], List[m.Pod], P.Profile]:
+    """The README.md:56-81 example: two template nodes (4 CPU / 32Gi / 110 pods,
+    web/components/lib/templates/node.yaml:6-13) and a pause:3.5 pod requesting
+    100m / 16Gi (web/components/lib/templates/pod.yaml:8-15)."""
+    nodes = [m.Node(name=nm, labels={m.LABEL_HOSTNAME: nm},
+                    allocatable={m.CPU: 4000, m.MEMORY: 32 * GI, m.PODS: 110})
+             for nm in ("node-282x7", "node-gp9t4")]
+    pod = m.Pod(name="hoge-pod", containers=[m.Container(
+        image="registry.k8s.io/pause:3.5", requests={m.CPU: 100, m.MEMORY: 16 * GI})])
+    return nodes, [pod], P.default_profile()

@@ -1,0 +1,65 @@
+"""Algorithmic byte counts for the roofline.
+
+Bytes per node-eval = every SoA column the enabled plugins must read for one
+node, each counted once, plus the per-node bytes written (none in
+placement-only mode).  The pod spec (staged once per pod in LDS) and LDS
+table lookups are not counted.  `achieved` = bytes/node-eval x node-evals per
+launch / launch time.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+from . import encoder as E
+from . import profile as P
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E vendor peak (MI355X_MICROARCH.md, chip table)
+
+
+def bytes_per_node_eval(enc: E.Encoder, prof: P.Profile) -> Dict[str, int]:
+    en = set(prof.enabled_ids())
+    R = len(enc.cluster.res_names)
+    cols: Dict[str, int] = {}
+    if P.NODE_UNSCHEDULABLE in en:
+        cols["unschedulable"] = 1
+    if P.NODE_RESOURCES_FIT in en or P.BALANCED_ALLOCATION in en:
+        cols["alloc"] = 8 * R
+        cols["requested"] = 8 * R
+        cols["allowed_pods"] = 4
+        cols["pod_count"] = 4
+    if P.NODE_RESOURCES_FIT in en:
+        cols["nonzero"] = 16
+    if P.TAINT_TOLERATION in en:
+        cols["taints"] = 4 * enc.cluster.max_taints
+    if P.NODE_AFFINITY in en:
+        # label columns referenced by node-affinity programs (all label columns
+        # that are not pure topology keys)
+        na_keys = set()
+        for p in enc.pods:
+            if p.node_selector:
+                na_keys.update(p.node_selector)
+            for t in (p.node_affinity_required or []):
+                na_keys.update(r.key for r in t.match_expressions)
+            for pt in (p.node_affinity_preferred or []):
+                na_keys.update(r.key for r in pt.preference.match_expressions)
+        cols["labels"] = 4 * len(na_keys)
+    if P.IMAGE_LOCALITY in en:
+        cols["images"] = 4 * enc.cluster.max_images
+    if P.POD_TOPOLOGY_SPREAD in en or P.INTER_POD_AFFINITY in en:
+        topo = set()
+        for p in enc.pods:
+            for c in p.topology_spread_constraints:
+                topo.add(c.topology_key)
+            for t in p.pod_affinity_required + p.pod_anti_affinity_required:
+                topo.add(t.topology_key)
+            for w in p.pod_affinity_preferred + p.pod_anti_affinity_preferred:
+                topo.add(w.term.topology_key)
+        cols["topology_labels"] = 4 * len(topo)
+        cols["selector_counts"] = 4     # one per-node count lookup per constraint/term
+    return cols
+
+
+def roofline(bytes_per_eval: int, node_evals_per_launch: int, launch_ms: float) -> Dict[str, float]:
+    achieved = bytes_per_eval * node_evals_per_launch / (launch_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS}

@@ -1,0 +1,286 @@
+"""ctypes binding of the C ABI in include/ksched.h (libksched.so).
+
+The shared library is built in-tree by `__graft_entry__.build()` (hipcc,
+--offload-arch=gfx950).  There is no fallback: if the library cannot be loaded
+the import of `Lib` fails loudly, so no GPU test can pass on a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import encoder as E
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libksched.so")
+
+NPLUGINS = 14
+MAX_RES = 8
+
+i32p = C.POINTER(C.c_int32)
+u32p = C.POINTER(C.c_uint32)
+i64p = C.POINTER(C.c_int64)
+u8p = C.POINTER(C.c_uint8)
+f64p = C.POINTER(C.c_double)
+
+
+class KsgNodes(C.Structure):
+    _fields_ = [("n_nodes", C.c_int32), ("n_res", C.c_int32), ("alloc", i64p), ("requested", i64p),
+                ("nonzero", i64p), ("allowed_pods", i32p), ("pod_count", i32p), ("unschedulable", u8p),
+                ("n_label_cols", C.c_int32), ("label_val", u32p), ("label_num", i64p), ("label_num_ok", u8p),
+                ("max_taints", C.c_int32), ("taints", u32p), ("n_taint_vocab", C.c_int32), ("taint_effect", u8p),
+                ("max_images", C.c_int32), ("images", u32p), ("n_images", C.c_int32)]
+
+
+class KsgTopology(C.Structure):
+    _fields_ = [("n_selectors", C.c_int32), ("n_templates", C.c_int32), ("tmpl_col", i32p),
+                ("tmpl_kind", i32p), ("tmpl_weight", i32p), ("col_vocab", i32p), ("col_unique", u8p),
+                ("log_table", f64p), ("log_n", C.c_int32)]
+
+
+class KsgWorkload(C.Structure):
+    _fields_ = [("pods", C.c_void_p), ("n_pods", C.c_int32), ("prog", i32p), ("prog_len", C.c_int64)]
+
+
+class KsgProfile(C.Structure):
+    _fields_ = [("n_filter", C.c_int32), ("filter_order", C.c_int32 * NPLUGINS), ("score_mask", C.c_uint32),
+                ("weight", C.c_int32 * NPLUGINS), ("fit_strategy", C.c_int32), ("fit_n", C.c_int32),
+                ("fit_res", C.c_int32 * MAX_RES), ("fit_w", C.c_int64 * MAX_RES), ("ba_n", C.c_int32),
+                ("ba_res", C.c_int32 * MAX_RES), ("hard_pod_affinity_weight", C.c_int32),
+                ("flags", C.c_uint32), ("fit_ignored_res", C.c_uint32), ("pad", C.c_int32)]
+
+
+class KsgResult(C.Structure):
+    _fields_ = [("selected", C.c_int32), ("n_feasible", C.c_int32), ("status", C.c_uint32),
+                ("score_skip", C.c_uint32)]
+
+
+RESULT_DTYPE = np.dtype([("selected", "<i4"), ("n_feasible", "<i4"), ("status", "<u4"), ("score_skip", "<u4")])
+
+
+class KsgCapture(C.Structure):
+    _fields_ = [("fstatus", u32p), ("raw", i64p), ("norm", i64p), ("total", i64p)]
+
+
+class KsgNodeState(C.Structure):
+    _fields_ = [("requested", i64p), ("nonzero", i64p), ("pod_count", i32p)]
+
+
+class KsgReplicaSummary(C.Structure):
+    _fields_ = [("scheduled", C.c_int32), ("unschedulable", C.c_int32), ("placement_hash", C.c_uint64),
+                ("cpu_requested", C.c_int64), ("mem_requested", C.c_int64)]
+
+
+SUMMARY_DTYPE = np.dtype([("scheduled", "<i4"), ("unschedulable", "<i4"), ("placement_hash", "<u8"),
+                          ("cpu_requested", "<i8"), ("mem_requested", "<i8")])
+assert SUMMARY_DTYPE.itemsize == C.sizeof(KsgReplicaSummary)
+
+ST_SCORED = 1
+ST_IPA_PREFILTER_SKIP = 2
+ST_IPA_PRESCORE_SKIP = 4
+ST_SCORE_ERROR = 8
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+class Marshalled:
+    """Keeps the numpy buffers behind the C structs alive."""
+
+    def __init__(self, enc: "E.Encoder"):
+        ec = enc.cluster
+        a = ec.arrays
+        self.keep = {}
+
+        def keep(name, arr, dtype):
+            arr = np.ascontiguousarray(arr, dtype=dtype)
+            self.keep[name] = arr
+            return arr
+
+        N = len(ec.node_names)
+        self.n_nodes = N
+        self.nodes = KsgNodes(
+            n_nodes=N, n_res=len(ec.res_names),
+            alloc=_ptr(keep("alloc", a["alloc"], np.int64), i64p),
+            requested=_ptr(keep("requested", a["requested"], np.int64), i64p),
+            nonzero=_ptr(keep("nonzero", a["nonzero"], np.int64), i64p),
+            allowed_pods=_ptr(keep("allowed", a["allowed_pods"], np.int32), i32p),
+            pod_count=_ptr(keep("pod_count", a["pod_count"], np.int32), i32p),
+            unschedulable=_ptr(keep("unsched", a["unschedulable"], np.uint8), u8p),
+            n_label_cols=len(ec.label_cols),
+            label_val=_ptr(keep("label_val", a["label_val"], np.uint32), u32p),
+            label_num=_ptr(keep("label_num", a["label_num"], np.int64), i64p),
+            label_num_ok=_ptr(keep("label_num_ok", a["label_num_ok"], np.uint8), u8p),
+            max_taints=ec.max_taints, taints=_ptr(keep("taints", a["taints"], np.uint32), u32p),
+            n_taint_vocab=len(ec.taint_vocab),
+            taint_effect=_ptr(keep("taint_effect", a["taint_effect"], np.uint8), u8p),
+            max_images=ec.max_images, images=_ptr(keep("images", a["images"], np.uint32), u32p),
+            n_images=ec.n_images)
+        self.topo = KsgTopology(
+            n_selectors=ec.n_selectors, n_templates=ec.n_templates,
+            tmpl_col=_ptr(keep("tmpl_col", a["tmpl_col"], np.int32), i32p),
+            tmpl_kind=_ptr(keep("tmpl_kind", a["tmpl_kind"], np.int32), i32p),
+            tmpl_weight=_ptr(keep("tmpl_weight", a["tmpl_weight"], np.int32), i32p),
+            col_vocab=_ptr(keep("col_vocab", a["col_vocab"], np.int32), i32p),
+            col_unique=_ptr(keep("col_unique", a["col_unique"], np.uint8), u8p),
+            log_table=_ptr(keep("log_table", a["log_table"], np.float64), f64p),
+            log_n=int(len(a["log_table"])))
+        wl = enc.workload
+        pods = keep("pods", wl.pods, E.POD_DTYPE)
+        prog = keep("prog", wl.prog, np.int32)
+        self.n_pods = len(pods)
+        self.workload = KsgWorkload(pods=pods.ctypes.data, n_pods=len(pods),
+                                    prog=_ptr(prog, i32p), prog_len=len(prog))
+
+
+def make_profile(fields: dict) -> KsgProfile:
+    p = KsgProfile()
+    for k, v in fields.items():
+        attr = getattr(p, k)
+        if isinstance(v, (list, tuple)):
+            for i, x in enumerate(v):
+                attr[i] = x
+        else:
+            setattr(p, k, v)
+    return p
+
+
+class CaptureBuffers:
+    """Host buffers for `count` pods of capture output."""
+
+    def __init__(self, n_nodes: int, count: int = 1):
+        self.fstatus = np.zeros((count, n_nodes), np.uint32)
+        self.raw = np.zeros((count, NPLUGINS, n_nodes), np.int64)
+        self.norm = np.zeros((count, NPLUGINS, n_nodes), np.int64)
+        self.total = np.zeros((count, n_nodes), np.int64)
+        self.struct = KsgCapture(_ptr(self.fstatus, u32p), _ptr(self.raw, i64p), _ptr(self.norm, i64p),
+                                 _ptr(self.total, i64p))
+
+
+def _bind(lib, prefix: str):
+    def f(name, restype, *argtypes):
+        fn = getattr(lib, prefix + name)
+        fn.restype = restype
+        fn.argtypes = list(argtypes)
+        return fn
+    return f
+
+
+class KschedError(RuntimeError):
+    pass
+
+
+class Engine:
+    """One evaluator context (ksg_ctx) behind the C ABI."""
+
+    PREFIX = "ksg_"
+
+    def __init__(self, lib_path: Optional[str] = None, device: int = 0):
+        path = lib_path or LIB_PATH
+        if not os.path.exists(path):
+            raise KschedError(f"{path} not found: run __graft_entry__.build() (no CPU fallback exists)")
+        self.lib = C.CDLL(path)
+        self._declare()
+        self.ctx = C.c_void_p()
+        self._check(self._open(device, C.byref(self.ctx)))
+        self._m: Optional[Marshalled] = None
+
+    def _declare(self):
+        f = _bind(self.lib, self.PREFIX)
+        vp = C.c_void_p
+        self._open = f("open", C.c_int, C.c_int, C.POINTER(C.c_void_p))
+        self._close = f("close", C.c_int, vp)
+        self._err = f("last_error", C.c_char_p, vp)
+        self._set_profile = f("set_profile", C.c_int, vp, C.POINTER(KsgProfile))
+        self._load_nodes = f("load_nodes", C.c_int, vp, C.POINTER(KsgNodes), C.POINTER(KsgTopology))
+        self._load_workload = f("load_workload", C.c_int, vp, C.POINTER(KsgWorkload))
+        self._eval = f("eval", C.c_int, vp, C.c_int32, C.POINTER(KsgResult), C.POINTER(KsgCapture))
+        self._commit = f("commit", C.c_int, vp, C.c_int32, C.c_int32)
+        self._run_queue = f("run_queue", C.c_int, vp, C.c_int32, C.c_int32, i32p, vp, C.POINTER(KsgCapture))
+        self._read_state = f("read_state", C.c_int, vp, C.POINTER(KsgNodeState))
+        self._reset_state = f("reset_state", C.c_int, vp)
+        self._declare_extra(f)
+
+    def _declare_extra(self, f):
+        vp = C.c_void_p
+        self._run_replicas = f("run_replicas", C.c_int, vp, C.POINTER(KsgProfile), C.c_int32, C.c_int32,
+                               C.c_int32, i32p, vp)
+        self._last_ms = f("last_kernel_ms", C.c_int, vp, C.POINTER(C.c_double))
+        self.abi_version = f("abi_version", C.c_int)()
+
+    def _check(self, rc: int):
+        if rc != 0:
+            msg = self._err(self.ctx).decode() if self.ctx else ""
+            raise KschedError(f"{self.PREFIX} call failed rc={rc}: {msg}")
+
+    def close(self):
+        if self.ctx:
+            self._close(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- loading --------------------------------------------------------
+    def load(self, enc: "E.Encoder", prof_fields: dict):
+        self._m = Marshalled(enc)
+        self.set_profile(prof_fields)
+        self._check(self._load_nodes(self.ctx, C.byref(self._m.nodes), C.byref(self._m.topo)))
+        self._check(self._load_workload(self.ctx, C.byref(self._m.workload)))
+
+    def set_profile(self, prof_fields: dict):
+        self._check(self._set_profile(self.ctx, C.byref(make_profile(prof_fields))))
+
+    @property
+    def n_nodes(self) -> int:
+        return self._m.n_nodes
+
+    # -- evaluation -----------------------------------------------------
+    def eval(self, pod: int, capture: Optional[CaptureBuffers] = None) -> KsgResult:
+        r = KsgResult()
+        self._check(self._eval(self.ctx, pod, C.byref(r), C.byref(capture.struct) if capture else None))
+        return r
+
+    def commit(self, pod: int, node: int):
+        self._check(self._commit(self.ctx, pod, node))
+
+    def run_queue(self, first: int, count: int, capture: Optional[CaptureBuffers] = None,
+                  results: bool = True):
+        pl = np.zeros(count, np.int32)
+        res = np.zeros(count, RESULT_DTYPE) if results else None
+        self._check(self._run_queue(self.ctx, first, count, _ptr(pl, i32p),
+                                    res.ctypes.data if res is not None else None,
+                                    C.byref(capture.struct) if capture else None))
+        return pl, res
+
+    def run_replicas(self, profiles, first: int, count: int):
+        R = len(profiles)
+        arr = (KsgProfile * R)(*[make_profile(p) for p in profiles])
+        pl = np.zeros((R, count), np.int32)
+        sums = np.zeros(R, SUMMARY_DTYPE)
+        self._check(self._run_replicas(self.ctx, arr, R, first, count, _ptr(pl, i32p), sums.ctypes.data))
+        return pl, sums
+
+    def last_kernel_ms(self) -> float:
+        v = C.c_double()
+        self._check(self._last_ms(self.ctx, C.byref(v)))
+        return v.value
+
+    def read_state(self, n_res: int):
+        N = self.n_nodes
+        req = np.zeros((n_res, N), np.int64)
+        nz = np.zeros((2, N), np.int64)
+        pc = np.zeros(N, np.int32)
+        st = KsgNodeState(_ptr(req, i64p), _ptr(nz, i64p), _ptr(pc, i32p))
+        self._check(self._read_state(self.ctx, C.byref(st)))
+        return req, nz, pc
+
+    def reset_state(self):
+        self._check(self._reset_state(self.ctx))

@@ -1,0 +1,166 @@
+"""Scheduler profile: which plugins run, in which order, with which weights/args.
+
+Mirrors what the debuggable scheduler derives from a KubeSchedulerConfiguration:
+- the MultiPoint plugin order after `ConvertForSimulator`
+  (`simulator/scheduler/plugin/plugins.go:174-197`; the converted default
+  profile is pinned at `simulator/scheduler/scheduler_test.go:519-541`),
+- the score-weight map of `getScorePluginWeight` (`plugins.go:289-304`: weight
+  0 maps to 1, key is the plugin name without the `Wrapped` suffix),
+- the default plugin args pinned at `plugins_test.go:876-1000`
+  (LeastAllocated cpu=1/memory=1, BalancedAllocation cpu=1/memory=1,
+  hardPodAffinityWeight=1, PodTopologySpread defaultingType System).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from . import model as m
+
+PLUGIN_SUFFIX = "Wrapped"  # wrappedplugin.go:242-248
+
+# Stable plugin ids shared with include/ksched.h (KSG_PL_*).
+NODE_UNSCHEDULABLE = 0
+NODE_NAME = 1
+TAINT_TOLERATION = 2
+NODE_AFFINITY = 3
+NODE_PORTS = 4
+NODE_RESOURCES_FIT = 5
+VOLUME_RESTRICTIONS = 6
+NODE_VOLUME_LIMITS = 7
+VOLUME_BINDING = 8
+VOLUME_ZONE = 9
+POD_TOPOLOGY_SPREAD = 10
+INTER_POD_AFFINITY = 11
+BALANCED_ALLOCATION = 12
+IMAGE_LOCALITY = 13
+N_PLUGINS = 14
+
+PLUGIN_NAMES = [
+    "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts",
+    "NodeResourcesFit", "VolumeRestrictions", "NodeVolumeLimits", "VolumeBinding",
+    "VolumeZone", "PodTopologySpread", "InterPodAffinity",
+    "NodeResourcesBalancedAllocation", "ImageLocality",
+]
+PLUGIN_ID = {n: i for i, n in enumerate(PLUGIN_NAMES)}
+
+# Plugins of the default profile that take part in neither Filter nor Score.
+NON_EVAL_PLUGINS = ("SchedulingGates", "PrioritySort", "DefaultPreemption", "DefaultBinder")
+
+# Extension points each in-tree plugin implements in kube-scheduler v1.32
+# [upstream, TO VERIFY — source not in container, SURVEY.md §8(c)].
+# (prefilter, filter, prescore, score, normalize)
+EXT = {
+    NODE_UNSCHEDULABLE: (False, True, False, False, False),
+    NODE_NAME: (False, True, False, False, False),
+    TAINT_TOLERATION: (False, True, True, True, True),
+    NODE_AFFINITY: (True, True, True, True, True),
+    NODE_PORTS: (True, True, False, False, False),
+    NODE_RESOURCES_FIT: (True, True, True, True, False),
+    VOLUME_RESTRICTIONS: (True, True, False, False, False),
+    NODE_VOLUME_LIMITS: (True, True, False, False, False),
+    VOLUME_BINDING: (True, True, True, True, False),
+    VOLUME_ZONE: (True, True, False, False, False),
+    POD_TOPOLOGY_SPREAD: (True, True, True, True, True),
+    INTER_POD_AFFINITY: (True, True, True, True, True),
+    BALANCED_ALLOCATION: (False, False, True, True, False),
+    IMAGE_LOCALITY: (False, False, False, True, False),
+}
+
+LEAST_ALLOCATED = 0
+MOST_ALLOCATED = 1
+STRATEGY_NAMES = {"LeastAllocated": LEAST_ALLOCATED, "MostAllocated": MOST_ALLOCATED}
+
+DEFAULT_MULTIPOINT: List[Tuple[str, int]] = [
+    ("SchedulingGates", 0), ("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0),
+    ("TaintToleration", 3), ("NodeAffinity", 2), ("NodePorts", 0), ("NodeResourcesFit", 1),
+    ("VolumeRestrictions", 0), ("NodeVolumeLimits", 0), ("VolumeBinding", 0), ("VolumeZone", 0),
+    ("PodTopologySpread", 2), ("InterPodAffinity", 2), ("DefaultPreemption", 0),
+    ("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1), ("DefaultBinder", 0),
+]
+
+
+@dataclass
+class Profile:
+    """One KubeSchedulerProfile as the debuggable scheduler runs it."""
+    plugins: List[Tuple[str, int]] = field(default_factory=lambda: list(DEFAULT_MULTIPOINT))
+    fit_strategy: int = LEAST_ALLOCATED
+    fit_resources: List[Tuple[str, int]] = field(default_factory=lambda: [(m.CPU, 1), (m.MEMORY, 1)])
+    ba_resources: List[Tuple[str, int]] = field(default_factory=lambda: [(m.CPU, 1), (m.MEMORY, 1)])
+    fit_ignored_resources: Tuple[str, ...] = ()
+    fit_ignored_resource_groups: Tuple[str, ...] = ()
+    hard_pod_affinity_weight: int = 1
+    ignore_preferred_terms_of_existing_pods: bool = False
+    # PodTopologySpreadArgs.defaultingType == System (no explicit defaultConstraints)
+    pts_system_defaulted: bool = True
+    # BalancedAllocation PreScore Skip for best-effort pods [upstream; believed
+    # to land after v1.32 — TO VERIFY, SURVEY.md Appendix A.2]
+    ba_skip_best_effort: bool = False
+
+    # -- derived views ---------------------------------------------------
+    def enabled_ids(self) -> List[int]:
+        """Filter/score-relevant plugin ids in MultiPoint order."""
+        out = []
+        for name, _ in self.plugins:
+            name = name[:-len(PLUGIN_SUFFIX)] if name.endswith(PLUGIN_SUFFIX) else name
+            if name in PLUGIN_ID:
+                out.append(PLUGIN_ID[name])
+            elif name not in NON_EVAL_PLUGINS:
+                raise ValueError(f"plugin {name!r} is not an in-tree Filter/Score plugin")
+        return out
+
+    def filter_order(self) -> List[int]:
+        return [p for p in self.enabled_ids() if EXT[p][1]]
+
+    def prefilter_order(self) -> List[int]:
+        return [p for p in self.enabled_ids() if EXT[p][0]]
+
+    def prescore_order(self) -> List[int]:
+        return [p for p in self.enabled_ids() if EXT[p][2]]
+
+    def score_order(self) -> List[int]:
+        return [p for p in self.enabled_ids() if EXT[p][3]]
+
+    def weights(self) -> Dict[str, int]:
+        """getScorePluginWeight (plugins.go:289-304): every enabled
+        MultiPoint plugin gets an entry; weight 0 is replaced by 1."""
+        out = {}
+        for name, w in self.plugins:
+            key = name[:-len(PLUGIN_SUFFIX)] if name.endswith(PLUGIN_SUFFIX) else name
+            out[key] = w if w != 0 else 1
+        return out
+
+    def weight_of(self, pid: int) -> int:
+        return self.weights().get(PLUGIN_NAMES[pid], 0)
+
+    def simulator_plugin_names(self) -> List[str]:
+        """Names after ConvertForSimulator (plugins.go:174-197)."""
+        return [n if n.endswith(PLUGIN_SUFFIX) else n + PLUGIN_SUFFIX for n, _ in self.plugins]
+
+
+def default_profile() -> Profile:
+    return Profile()
+
+
+def config2_profile(strategy: int = LEAST_ALLOCATED, weights: Optional[Dict[str, int]] = None) -> Profile:
+    """BASELINE.json configs[1]: NodeResourcesFit + BalancedAllocation +
+    TaintToleration + NodeAffinity (plus the cheap always-on filters)."""
+    w = {"TaintToleration": 3, "NodeAffinity": 2, "NodeResourcesFit": 1,
+         "NodeResourcesBalancedAllocation": 1}
+    if weights:
+        w.update(weights)
+    plugins = [("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0),
+               ("TaintToleration", w["TaintToleration"]), ("NodeAffinity", w["NodeAffinity"]),
+               ("NodeResourcesFit", w["NodeResourcesFit"]),
+               ("NodeResourcesBalancedAllocation", w["NodeResourcesBalancedAllocation"]),
+               ("DefaultBinder", 0)]
+    return Profile(plugins=plugins, fit_strategy=strategy)
+
+
+def config3_profile() -> Profile:
+    """BASELINE.json configs[2]: config 2 plus PodTopologySpread and InterPodAffinity."""
+    plugins = [("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0),
+               ("TaintToleration", 3), ("NodeAffinity", 2), ("NodeResourcesFit", 1),
+               ("PodTopologySpread", 2), ("InterPodAffinity", 2),
+               ("NodeResourcesBalancedAllocation", 1), ("DefaultBinder", 0)]
+    return Profile(plugins=plugins)

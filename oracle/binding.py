@@ -1,0 +1,52 @@
+"""ORACLE — test infrastructure only: ctypes binding of liboracle.so (kso_*).
+
+Same structs and call shapes as the product binding (native.Engine), so the
+tests drive the oracle and the HIP library identically.  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import importlib
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+native = importlib.import_module("kube-scheduler-simulator_amd.native")
+
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "oracle.cpp")
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+    return LIB
+
+
+class Oracle(native.Engine):
+    PREFIX = "kso_"
+
+    def __init__(self, nthreads: int = 1):
+        build()
+        super().__init__(lib_path=LIB, device=nthreads)
+
+    def _declare_extra(self, f):
+        self._set_threads = f("set_threads", C.c_int, C.c_void_p, C.c_int)
+        self.abi_version = native.NPLUGINS and 1
+
+    def set_threads(self, n: int):
+        self._check(self._set_threads(self.ctx, n))
+
+    def run_replicas(self, profiles, first: int, count: int):
+        """Sequential what-if replicas: reset, switch profile, run the queue."""
+        import numpy as np
+        R = len(profiles)
+        pl = np.zeros((R, count), np.int32)
+        for r, prof in enumerate(profiles):
+            self.reset_state()
+            self.set_profile(prof)
+            pl[r], _ = self.run_queue(first, count, results=False)
+        return pl, None

@@ -1,0 +1,912 @@
+"""ORACLE — test infrastructure only.  Never imported by the product path.
+
+Independent pure-Python restatement of the kube-scheduler v1.32 Filter/Score
+cycle as the debuggable scheduler records it.  It works on the object model
+(`model.Pod`/`model.Node`, strings and maps), i.e. *before* the snapshot
+encoder, so it checks the encoder, the C++ oracle (`oracle/oracle.cpp`) and
+the HIP path at the same time.  Pure Python loops: small cases only.
+
+Parity status: the upstream plugin source (k8s.io/kubernetes v1.32.5) is not
+in this container and no Go toolchain exists; the plugin
+arithmetic below is restated from the upstream design
+and pinned only by the README known-answer test (README.md:56-81, SURVEY.md
+Appendix C) and by the wrapper/store contract tests of the reference
+(wrappedplugin_test.go, store_test.go).  Parity against the Go binary is
+therefore *unpinned* for the plugin arithmetic.
+
+Recording rules restated from the reference:
+- PreFilter: `"success"` or `Status.Message()` (Skip -> "")  wrappedplugin.go:504-512
+- Filter: `"passed"` or the rejection message              wrappedplugin.go:535-542
+- PreScore: as PreFilter                                   wrappedplugin.go:472-478
+- Score: raw score; finalscore = raw*weight               wrappedplugin.go:433-438, store.go:461-478
+- NormalizeScore: finalscore = normalized*weight           wrappedplugin.go:400-406, store.go:481-507
+- Reserve: selected node                                   wrappedplugin.go:622-623
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+from typing import Dict, List, Optional
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import importlib  # noqa: E402
+
+_pkg = importlib.import_module("kube-scheduler-simulator_amd")
+m = importlib.import_module("kube-scheduler-simulator_amd.model")
+P = importlib.import_module("kube-scheduler-simulator_amd.profile")
+
+MAX_NODE_SCORE = 100
+MB = 1024 * 1024
+MIN_THRESHOLD = 23 * MB
+MAX_CONTAINER_THRESHOLD = 1000 * MB
+MAX_INT32 = 2 ** 31 - 1
+
+SKIP = "__skip__"
+
+
+# ---------------------------------------------------------------- selectors
+class Sel:
+    """labels.Selector built by metav1.LabelSelectorAsSelector."""
+
+    def __init__(self, ls: Optional[m.LabelSelector], extra=None):
+        self.nothing = ls is None
+        self.reqs = []
+        if ls is not None:
+            for k, v in ls.match_labels:
+                self.reqs.append((k, m.IN, (v,)))
+            for r in ls.match_expressions:
+                self.reqs.append((r.key, r.operator, tuple(r.values)))
+        if extra:
+            for k, v in extra.items():
+                self.reqs.append((k, m.IN, (v,)))
+
+    def empty(self) -> bool:
+        return (not self.nothing) and not self.reqs
+
+    def matches(self, labels: Dict[str, str]) -> bool:
+        if self.nothing:
+            return False
+        for k, op, vals in self.reqs:
+            if not label_req_matches(k, op, vals, labels):
+                return False
+        return True
+
+
+def label_req_matches(k, op, vals, labels) -> bool:
+    """labels.Requirement.Matches [upstream apimachinery/pkg/labels/selector.go]."""
+    has = k in labels
+    if op == m.IN:
+        return has and labels[k] in vals
+    if op == m.NOT_IN:
+        return (not has) or labels[k] not in vals
+    if op == m.EXISTS:
+        return has
+    if op == m.DOES_NOT_EXIST:
+        return not has
+    if op in (m.GT, m.LT):
+        if not has:
+            return False
+        lv = parse_int64(labels[k])
+        if lv is None or len(vals) != 1:
+            return False
+        rv = parse_int64(vals[0])
+        if rv is None:
+            return False
+        return lv > rv if op == m.GT else lv < rv
+    return False
+
+
+def parse_int64(s: str):
+    """strconv.ParseInt(s, 10, 64)."""
+    if not s:
+        return None
+    body = s[1:] if s[0] in "+-" else s
+    if not body or not body.isdigit() or not body.isascii():
+        return None
+    v = int(s)
+    if v < -(2 ** 63) or v >= 2 ** 63:
+        return None
+    return v
+
+
+def node_term_matches(term: m.NodeSelectorTerm, node: m.Node) -> bool:
+    """nodeaffinity nodeSelectorTerm.match: an empty term matches nothing;
+    an unparsable requirement makes the term never match."""
+    if not term.match_expressions and not term.match_fields:
+        return False
+    for r in term.match_expressions:
+        if r.operator in (m.IN, m.NOT_IN) and not r.values:
+            return False
+        if r.operator in (m.EXISTS, m.DOES_NOT_EXIST) and r.values:
+            return False
+        if r.operator in (m.GT, m.LT) and (len(r.values) != 1 or parse_int64(r.values[0]) is None):
+            return False
+        if not label_req_matches(r.key, r.operator, r.values, node.labels):
+            return False
+    for r in term.match_fields:
+        if r.key != m.OBJECT_NAME_FIELD or r.operator not in (m.IN, m.NOT_IN) or len(r.values) != 1:
+            return False
+        if not label_req_matches(r.key, r.operator, r.values, {m.OBJECT_NAME_FIELD: node.name}):
+            return False
+    return True
+
+
+def required_node_affinity_match(pod: m.Pod, node: m.Node) -> bool:
+    """nodeaffinity.GetRequiredNodeAffinity(pod).Match(node)."""
+    if pod.node_selector:
+        for k, v in pod.node_selector.items():
+            if node.labels.get(k) != v or k not in node.labels:
+                return False
+    if pod.node_affinity_required is not None:
+        return any(node_term_matches(t, node) for t in pod.node_affinity_required)
+    return True
+
+
+def find_untolerated(taints, tols, effects):
+    for t in taints:
+        if t.effect not in effects:
+            continue
+        if not m.tolerations_tolerate(tols, t):
+            return t
+    return None
+
+
+# ---------------------------------------------------------------- NodeInfo
+class NodeInfo:
+    def __init__(self, node: m.Node, res_names):
+        self.node = node
+        self.pods: List[m.Pod] = []
+        self.requested = {r: 0 for r in res_names}
+        self.nz_cpu = 0
+        self.nz_mem = 0
+        self.image_states = {}  # normalized name -> (size, num_nodes)
+
+    def add_pod(self, pod: m.Pod):
+        """NodeInfo.AddPod / update(sign=+1) [upstream framework/types.go]."""
+        req = m.pod_requests(pod)
+        nz = m.pod_requests(pod, non_zero=True)
+        for k, v in req.items():
+            if k in (m.CPU, m.MEMORY, m.EPHEMERAL) or m.is_scalar_resource(k):
+                self.requested[k] = self.requested.get(k, 0) + v
+        self.nz_cpu += nz.get(m.CPU, 0)
+        self.nz_mem += nz.get(m.MEMORY, 0)
+        self.pods.append(pod)
+
+    def used_ports(self):
+        out = []
+        for p in self.pods:
+            out.extend(p.host_ports())
+        return out
+
+
+def build_snapshot(nodes: List[m.Node], bound):
+    res_names = {m.CPU, m.MEMORY, m.EPHEMERAL}
+    for n in nodes:
+        res_names.update(k for k in n.allocatable if m.is_scalar_resource(k))
+    infos = [NodeInfo(n, res_names) for n in nodes]
+    by_name = {n.name: i for i, n in enumerate(nodes)}
+    # cache.addNodeImageStates: first reporter's size, set of nodes per name
+    states = {}
+    for n in nodes:
+        for img in n.images:
+            for name in img.names:
+                if name not in states:
+                    states[name] = [img.size_bytes, set()]
+                states[name][1].add(n.name)
+    for ni in infos:
+        for img in ni.node.images:
+            for name in img.names:
+                st = states[name]
+                ni.image_states[name] = (st[0], len(st[1]))
+    for pod, node_name in bound:
+        infos[by_name[node_name]].add_pod(pod)
+    return infos
+
+
+# ---------------------------------------------------------------- plugins
+def fit_request(pod):
+    req = m.pod_requests(pod)
+    return req
+
+
+def fits_request(pod, ni: NodeInfo, prof: P.Profile):
+    """noderesources.fitsRequest."""
+    reasons = []
+    alloc = ni.node.allocatable
+    if len(ni.pods) + 1 > alloc.get(m.PODS, 0):
+        reasons.append("Too many pods")
+    req = fit_request(pod)
+    scal = {k: v for k, v in req.items() if m.is_scalar_resource(k)}
+    cpu, mem, eph = req.get(m.CPU, 0), req.get(m.MEMORY, 0), req.get(m.EPHEMERAL, 0)
+    if cpu == 0 and mem == 0 and eph == 0 and not scal:
+        return reasons
+    if cpu > 0 and cpu > alloc.get(m.CPU, 0) - ni.requested[m.CPU]:
+        reasons.append("Insufficient cpu")
+    if mem > 0 and mem > alloc.get(m.MEMORY, 0) - ni.requested[m.MEMORY]:
+        reasons.append("Insufficient memory")
+    if eph > 0 and eph > alloc.get(m.EPHEMERAL, 0) - ni.requested[m.EPHEMERAL]:
+        reasons.append("Insufficient ephemeral-storage")
+    for r in sorted(scal):   # Go map order; the encoder limits pods to <=1 such reason
+        q = scal[r]
+        if q == 0:
+            continue
+        if "/" in r and (r in prof.fit_ignored_resources or r.split("/")[0] in prof.fit_ignored_resource_groups):
+            continue
+        if q > alloc.get(r, 0) - ni.requested.get(r, 0):
+            reasons.append(f"Insufficient {r}")
+    return reasons
+
+
+def score_pod_request(pod, rname, use_requested):
+    req = m.pod_requests(pod, non_zero=not use_requested)
+    return req.get(rname, 0)
+
+
+def alloc_req(ni: NodeInfo, rname, pod_req, use_requested):
+    """resourceAllocationScorer.calculateResourceAllocatableRequest."""
+    if pod_req == 0 and m.is_scalar_resource(rname):
+        return 0, 0
+    alloc = ni.node.allocatable
+    if rname == m.CPU:
+        base = ni.requested[m.CPU] if use_requested else ni.nz_cpu
+        return alloc.get(m.CPU, 0), base + pod_req
+    if rname == m.MEMORY:
+        base = ni.requested[m.MEMORY] if use_requested else ni.nz_mem
+        return alloc.get(m.MEMORY, 0), base + pod_req
+    if rname == m.EPHEMERAL:
+        return alloc.get(m.EPHEMERAL, 0), ni.requested[m.EPHEMERAL] + pod_req
+    if rname in alloc:
+        return alloc[rname], ni.requested.get(rname, 0) + pod_req
+    return 0, 0
+
+
+def go_div(a: int, b: int) -> int:
+    """Go int64 division truncates toward zero."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def fit_score(pod, ni, prof: P.Profile):
+    num = 0
+    wsum = 0
+    for rname, w in prof.fit_resources:
+        a, r = alloc_req(ni, rname, score_pod_request(pod, rname, False), False)
+        if a == 0:
+            continue
+        if prof.fit_strategy == P.LEAST_ALLOCATED:
+            s = 0 if r > a else go_div((a - r) * MAX_NODE_SCORE, a)
+        else:
+            s = go_div(min(r, a) * MAX_NODE_SCORE, a)
+        num += s * w
+        wsum += w
+    return go_div(num, wsum) if wsum else 0
+
+
+def ba_score(pod, ni, prof: P.Profile):
+    fr = []
+    total = 0.0
+    for rname, _ in prof.ba_resources:
+        a, r = alloc_req(ni, rname, score_pod_request(pod, rname, True), True)
+        if a == 0:
+            continue
+        f = float(r) / float(a)
+        if f > 1:
+            f = 1.0
+        total += f
+        fr.append(f)
+    std = 0.0
+    if len(fr) == 2:
+        std = abs((fr[0] - fr[1]) / 2)
+    elif len(fr) > 2:
+        mean = total / float(len(fr))
+        s = 0.0
+        for f in fr:
+            s = s + (f - mean) * (f - mean)
+        std = math.sqrt(s / float(len(fr)))
+    return int((1 - std) * float(MAX_NODE_SCORE))
+
+
+def image_score(pod, ni, total_nodes):
+    s = 0
+    for c in list(pod.init_containers) + list(pod.containers):
+        st = ni.image_states.get(m.normalized_image_name(c.image))
+        if st is not None:
+            spread = float(st[1]) / float(total_nodes)
+            s += int(float(st[0]) * spread)
+    ncont = len(pod.init_containers) + len(pod.containers)
+    max_t = MAX_CONTAINER_THRESHOLD * ncont
+    if s < MIN_THRESHOLD:
+        s = MIN_THRESHOLD
+    elif s > max_t:
+        s = max_t
+    return go_div(MAX_NODE_SCORE * (s - MIN_THRESHOLD), max_t - MIN_THRESHOLD)
+
+
+def default_normalize(scores: List[int], reverse: bool) -> List[int]:
+    mx = 0
+    for s in scores:
+        if s > mx:
+            mx = s
+    if mx == 0:
+        return [MAX_NODE_SCORE] * len(scores) if reverse else list(scores)
+    out = []
+    for s in scores:
+        v = go_div(MAX_NODE_SCORE * s, mx)
+        out.append(MAX_NODE_SCORE - v if reverse else v)
+    return out
+
+
+# ---------------------------------------------------------------- PodTopologySpread
+class TSC:
+    def __init__(self, c: m.TopologySpreadConstraint, pod: m.Pod, default_sel=None):
+        self.max_skew = c.max_skew
+        self.key = c.topology_key
+        if default_sel is not None:
+            self.sel = default_sel
+        else:
+            extra = None
+            if c.match_label_keys:
+                extra = {k: pod.labels[k] for k in c.match_label_keys if k in pod.labels}
+            self.sel = Sel(c.label_selector, extra or None)
+        self.min_domains = c.min_domains if c.min_domains is not None else 1
+        self.na_policy = c.node_affinity_policy or m.POLICY_HONOR
+        self.nt_policy = c.node_taints_policy or m.POLICY_IGNORE
+
+    def match_inclusion(self, pod, node):
+        if self.na_policy == m.POLICY_HONOR and not required_node_affinity_match(pod, node):
+            return False
+        if self.nt_policy == m.POLICY_HONOR and find_untolerated(node.taints, pod.tolerations,
+                                                                  (m.NO_SCHEDULE, m.NO_EXECUTE)):
+            return False
+        return True
+
+
+SYSTEM_DEFAULT_CONSTRAINTS = [
+    m.TopologySpreadConstraint(3, m.LABEL_HOSTNAME, m.SCHEDULE_ANYWAY, None),
+    m.TopologySpreadConstraint(5, m.LABEL_ZONE, m.SCHEDULE_ANYWAY, None),
+]
+
+
+def pts_constraints(pod: m.Pod, action: str, prof: P.Profile):
+    if pod.topology_spread_constraints:
+        return [TSC(c, pod) for c in pod.topology_spread_constraints if c.when_unsatisfiable == action]
+    if not prof.pts_system_defaulted:
+        return []
+    cs = [c for c in SYSTEM_DEFAULT_CONSTRAINTS if c.when_unsatisfiable == action]
+    if not cs or pod.default_spread_selector is None:
+        return []
+    sel = Sel(pod.default_spread_selector)
+    if sel.empty():
+        return []
+    return [TSC(c, pod, default_sel=sel) for c in cs]
+
+
+def count_matching(pods, sel: Sel, ns):
+    if sel.empty():
+        return 0
+    n = 0
+    for p in pods:
+        if p.terminating or p.namespace != ns:
+            continue
+        if sel.matches(p.labels):
+            n += 1
+    return n
+
+
+def pts_prefilter(pod, infos, prof):
+    cons = pts_constraints(pod, m.DO_NOT_SCHEDULE, prof)
+    if not cons:
+        return None
+    tp = [dict() for _ in cons]
+    for ni in infos:
+        node = ni.node
+        if not all(c.key in node.labels for c in cons):
+            continue
+        for i, c in enumerate(cons):
+            if not c.match_inclusion(pod, node):
+                continue
+            v = node.labels[c.key]
+            tp[i][v] = tp[i].get(v, 0) + count_matching(ni.pods, c.sel, pod.namespace)
+    mins = []
+    for i, c in enumerate(cons):
+        mn = min(tp[i].values()) if tp[i] else MAX_INT32
+        if len(tp[i]) < c.min_domains:
+            mn = 0
+        mins.append(mn)
+    return cons, tp, mins
+
+
+def pts_filter(state, pod, ni):
+    cons, tp, mins = state
+    for i, c in enumerate(cons):
+        if c.key not in ni.node.labels:
+            return "node(s) didn't match pod topology spread constraints (missing required label)"
+        self_match = 1 if c.sel.matches(pod.labels) else 0
+        cnt = tp[i].get(ni.node.labels[c.key], 0)
+        if cnt + self_match - mins[i] > c.max_skew:
+            return "node(s) didn't match pod topology spread constraints"
+    return None
+
+
+def pts_prescore(pod, infos, feasible, prof):
+    cons = pts_constraints(pod, m.SCHEDULE_ANYWAY, prof)
+    if not cons:
+        return None
+    require_all = bool(pod.topology_spread_constraints) or not prof.pts_system_defaulted
+    ignored = set()
+    counts = [dict() for _ in cons]
+    topo_size = [0] * len(cons)
+    for ni in feasible:
+        node = ni.node
+        if require_all and not all(c.key in node.labels for c in cons):
+            ignored.add(node.name)
+            continue
+        for i, c in enumerate(cons):
+            if c.key == m.LABEL_HOSTNAME:
+                continue
+            v = node.labels.get(c.key, "")
+            if v not in counts[i]:
+                counts[i][v] = 0
+                topo_size[i] += 1
+    weights = []
+    for i, c in enumerate(cons):
+        sz = topo_size[i]
+        if c.key == m.LABEL_HOSTNAME:
+            sz = len(feasible) - len(ignored)
+        weights.append(math.log(float(sz + 2)))
+    for ni in infos:
+        node = ni.node
+        if require_all and not all(c.key in node.labels for c in cons):
+            continue
+        for i, c in enumerate(cons):
+            if not c.match_inclusion(pod, node):
+                continue
+            v = node.labels.get(c.key, "")
+            if v not in counts[i]:
+                continue
+            counts[i][v] += count_matching(ni.pods, c.sel, pod.namespace)
+    return cons, ignored, counts, weights
+
+
+def pts_score(state, pod, ni):
+    cons, ignored, counts, weights = state
+    if ni.node.name in ignored:
+        return 0
+    score = 0.0
+    for i, c in enumerate(cons):
+        if c.key in ni.node.labels:
+            if c.key == m.LABEL_HOSTNAME:
+                cnt = count_matching(ni.pods, c.sel, pod.namespace)
+            else:
+                cnt = counts[i][ni.node.labels[c.key]]
+            score += float(cnt) * weights[i] + float(c.max_skew - 1)
+    return go_round(score)
+
+
+def go_round(x: float) -> int:
+    """math.Round: half away from zero."""
+    return int(math.floor(x + 0.5)) if x >= 0 else -int(math.floor(-x + 0.5))
+
+
+def pts_normalize(state, names, scores):
+    _, ignored, _, _ = state
+    mn, mx = 2 ** 63 - 1, 0
+    for nm, s in zip(names, scores):
+        if nm in ignored:
+            continue
+        mn = min(mn, s)
+        mx = max(mx, s)
+    out = []
+    for nm, s in zip(names, scores):
+        if nm in ignored:
+            out.append(0)
+        elif mx == 0:
+            out.append(MAX_NODE_SCORE)
+        else:
+            out.append(go_div(MAX_NODE_SCORE * (mx + mn - s), mx))
+    return out
+
+
+# ---------------------------------------------------------------- InterPodAffinity
+class ATerm:
+    """framework.AffinityTerm."""
+
+    def __init__(self, t: m.PodAffinityTerm, owner: m.Pod, weight=0):
+        self.sel = Sel(t.label_selector)
+        self.key = t.topology_key
+        ns = set(t.namespaces)
+        if not t.namespaces and t.namespace_selector is None:
+            ns = {owner.namespace}
+        self.namespaces = ns
+        self.ns_all = t.namespace_selector is not None and t.namespace_selector.empty()
+        if t.namespace_selector is not None and not t.namespace_selector.empty():
+            raise NotImplementedError("namespaceSelector with requirements is not modelled")
+        self.weight = weight
+
+    def matches(self, pod: m.Pod) -> bool:
+        if pod.namespace in self.namespaces or self.ns_all:
+            return self.sel.matches(pod.labels)
+        return False
+
+
+def terms_of(pod):
+    ra = [ATerm(t, pod) for t in pod.pod_affinity_required]
+    rn = [ATerm(t, pod) for t in pod.pod_anti_affinity_required]
+    pa = [ATerm(w.term, pod, w.weight) for w in pod.pod_affinity_preferred]
+    pn = [ATerm(w.term, pod, w.weight) for w in pod.pod_anti_affinity_preferred]
+    return ra, rn, pa, pn
+
+
+def _upd(mp, node, key, val):
+    if key in node.labels:
+        pr = (key, node.labels[key])
+        mp[pr] = mp.get(pr, 0) + val
+        if mp[pr] == 0:
+            del mp[pr]
+
+
+def ipa_prefilter(pod, infos):
+    ra, rn, _, _ = terms_of(pod)
+    existing_anti = {}
+    for ni in infos:
+        for ep in ni.pods:
+            if not ep.pod_anti_affinity_required:
+                continue
+            for t in terms_of(ep)[1]:
+                if t.matches(pod):
+                    _upd(existing_anti, ni.node, t.key, 1)
+    aff, anti = {}, {}
+    if ra or rn:
+        for ni in infos:
+            for ep in ni.pods:
+                if ra and all(t.matches(ep) for t in ra):
+                    for t in ra:
+                        _upd(aff, ni.node, t.key, 1)
+                for t in rn:
+                    if t.matches(ep):
+                        _upd(anti, ni.node, t.key, 1)
+    if not existing_anti and not ra and not rn:
+        return None
+    return ra, rn, existing_anti, aff, anti
+
+
+def ipa_filter(state, pod, ni):
+    ra, rn, existing_anti, aff, anti = state
+    labels = ni.node.labels
+    pods_exist = True
+    ok = True
+    for t in ra:
+        if t.key in labels:
+            if aff.get((t.key, labels[t.key]), 0) <= 0:
+                pods_exist = False
+        else:
+            ok = False
+            break
+    if ok and not pods_exist:
+        ok = (not aff) and bool(ra) and all(t.matches(pod) for t in ra)
+    if not ok:
+        return "node(s) didn't match pod affinity rules"
+    if anti:
+        for t in rn:
+            if t.key in labels and anti.get((t.key, labels[t.key]), 0) > 0:
+                return "node(s) didn't match pod anti-affinity rules"
+    if existing_anti:
+        for k, v in labels.items():
+            if existing_anti.get((k, v), 0) > 0:
+                return "node(s) didn't satisfy existing pods anti-affinity rules"
+    return None
+
+
+def ipa_prescore(pod, infos, prof):
+    ra, rn, pa, pn = terms_of(pod)
+    has_cons = bool(pa) or bool(pn)
+    if prof.ignore_preferred_terms_of_existing_pods and not has_cons:
+        return None
+    topo = {}
+
+    def proc(term: ATerm, weight, target, node, mult):
+        if term.matches(target) and term.key in node.labels:
+            d = topo.setdefault(term.key, {})
+            v = node.labels[term.key]
+            d[v] = d.get(v, 0) + weight * mult
+
+    for ni in infos:
+        pods = ni.pods if has_cons else [p for p in ni.pods if p.has_pod_affinity()]
+        node = ni.node
+        for ep in pods:
+            if not node.labels:
+                continue
+            for t in pa:
+                proc(t, t.weight, ep, node, 1)
+            for t in pn:
+                proc(t, t.weight, ep, node, -1)
+            era, _, epa, epn = terms_of(ep)
+            if prof.hard_pod_affinity_weight > 0:
+                for t in era:
+                    proc(t, prof.hard_pod_affinity_weight, pod, node, 1)
+            for t in epa:
+                proc(t, t.weight, pod, node, 1)
+            for t in epn:
+                proc(t, t.weight, pod, node, -1)
+    if not topo:
+        return None
+    return topo
+
+
+def ipa_score(topo, ni):
+    s = 0
+    for k, vals in topo.items():
+        if k in ni.node.labels:
+            s += vals.get(ni.node.labels[k], 0)
+    return s
+
+
+def ipa_normalize(scores):
+    mn = min(scores)
+    mx = max(scores)
+    diff = mx - mn
+    out = []
+    for s in scores:
+        f = 0.0
+        if diff > 0:
+            f = float(MAX_NODE_SCORE) * (float(s - mn) / float(diff))
+        out.append(int(f))
+    return out
+
+
+# ---------------------------------------------------------------- framework
+def pod_prefilter(pod, infos, prof):
+    """Returns (statuses {plugin:str}, states, rejected, node_set)."""
+    st = {}
+    states = {}
+    skip = set()
+    node_set = None
+    rejected = None
+    for pid in prof.prefilter_order():
+        name = P.PLUGIN_NAMES[pid]
+        if pid == P.NODE_AFFINITY:
+            no_aff = pod.node_affinity_required is None
+            if no_aff and pod.node_selector is None:
+                st[name] = ""
+                skip.add(pid)
+                continue
+            if not no_aff and pod.node_affinity_required:
+                names = None
+                conflict = False
+                for term in pod.node_affinity_required:
+                    tn = None
+                    for r in term.match_fields:
+                        if r.key == m.OBJECT_NAME_FIELD and r.operator == m.IN:
+                            s = set(r.values)
+                            tn = s if tn is None else (tn & s)
+                    if tn is None:
+                        names = None
+                        break
+                    names = tn if names is None else (names | tn)
+                else:
+                    if names is not None and not names:
+                        conflict = True
+                if conflict:
+                    st[name] = "pod affinity terms conflict"
+                    rejected = name
+                    break
+                if names:
+                    node_set = sorted(names)
+            st[name] = "success"
+        elif pid == P.NODE_PORTS:
+            if not pod.host_ports():
+                st[name] = ""
+                skip.add(pid)
+            else:
+                st[name] = "success"
+        elif pid == P.NODE_RESOURCES_FIT:
+            st[name] = "success"
+        elif pid in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE):
+            st[name] = ""          # volume-less pods: Skip
+            skip.add(pid)
+        elif pid == P.POD_TOPOLOGY_SPREAD:
+            s = pts_prefilter(pod, infos, prof)
+            if s is None:
+                st[name] = ""
+                skip.add(pid)
+            else:
+                states[pid] = s
+                st[name] = "success"
+        elif pid == P.INTER_POD_AFFINITY:
+            s = ipa_prefilter(pod, infos)
+            if s is None:
+                st[name] = ""
+                skip.add(pid)
+            else:
+                states[pid] = s
+                st[name] = "success"
+    return st, states, skip, rejected, node_set
+
+
+def run_filters(pod, ni, prof, states, skip, total_nodes):
+    """Returns (ordered [(plugin, msg)], passed)."""
+    out = []
+    for pid in prof.filter_order():
+        if pid in skip:
+            continue
+        name = P.PLUGIN_NAMES[pid]
+        msg = None
+        node = ni.node
+        if pid == P.NODE_UNSCHEDULABLE:
+            if node.unschedulable and not m.tolerations_tolerate(
+                    pod.tolerations, m.Taint(m.TAINT_NODE_UNSCHEDULABLE, "", m.NO_SCHEDULE)):
+                msg = "node(s) were unschedulable"
+        elif pid == P.NODE_NAME:
+            if pod.node_name and pod.node_name != node.name:
+                msg = "node(s) didn't match the requested node name"
+        elif pid == P.TAINT_TOLERATION:
+            t = find_untolerated(node.taints, pod.tolerations, (m.NO_SCHEDULE, m.NO_EXECUTE))
+            if t is not None:
+                msg = f"node(s) had untolerated taint {{{t.key}: {t.value}}}"
+        elif pid == P.NODE_AFFINITY:
+            if not required_node_affinity_match(pod, node):
+                msg = "node(s) didn't match Pod's node affinity/selector"
+        elif pid == P.NODE_PORTS:
+            used = ni.used_ports()
+            for (ip, proto, port) in pod.host_ports():
+                for (uip, uproto, uport) in used:
+                    if uport == port and uproto == proto and (uip == ip or uip == "0.0.0.0" or ip == "0.0.0.0"):
+                        msg = "node(s) didn't have free ports for the requested pod ports"
+        elif pid == P.NODE_RESOURCES_FIT:
+            r = fits_request(pod, ni, prof)
+            if r:
+                msg = ", ".join(r)
+        elif pid == P.POD_TOPOLOGY_SPREAD:
+            msg = pts_filter(states[pid], pod, ni)
+        elif pid == P.INTER_POD_AFFINITY:
+            msg = ipa_filter(states[pid], pod, ni)
+        # volume plugins pass for volume-less pods
+        if msg is None:
+            out.append((name, "passed"))
+        else:
+            out.append((name, msg))
+            return out, False
+    return out, True
+
+
+def schedule_one(pod: m.Pod, infos: List[NodeInfo], prof: P.Profile):
+    rec = {"prefilter_status": {}, "prefilter_result": {}, "filter": {}, "prescore": {},
+           "score": {}, "finalscore": {}, "selected": "", "selected_index": -1,
+           "raw": {}, "norm": {}, "n_feasible": 0}
+    st, states, skip, rejected, node_set = pod_prefilter(pod, infos, prof)
+    rec["prefilter_status"] = st
+    if node_set is not None:
+        rec["prefilter_result"]["NodeAffinity"] = node_set
+    if rejected:
+        return rec
+    total_nodes = len(infos)
+    feasible = []
+    for idx, ni in enumerate(infos):
+        if node_set is not None and ni.node.name not in node_set:
+            continue
+        res, ok = run_filters(pod, ni, prof, states, skip, total_nodes)
+        if res:
+            rec["filter"][ni.node.name] = dict(res)
+        if ok:
+            feasible.append(idx)
+    rec["n_feasible"] = len(feasible)
+    if not feasible:
+        return rec
+    if len(feasible) == 1:
+        rec["selected_index"] = feasible[0]
+        rec["selected"] = infos[feasible[0]].node.name
+        return rec
+    fnodes = [infos[i] for i in feasible]
+    names = [ni.node.name for ni in fnodes]
+    # PreScore
+    skip_score = set()
+    pstate = {}
+    for pid in prof.prescore_order():
+        name = P.PLUGIN_NAMES[pid]
+        if pid == P.TAINT_TOLERATION or pid == P.NODE_RESOURCES_FIT:
+            rec["prescore"][name] = "success"
+        elif pid == P.NODE_AFFINITY:
+            if pod.node_affinity_preferred is None:
+                rec["prescore"][name] = ""
+                skip_score.add(pid)
+            else:
+                rec["prescore"][name] = "success"
+        elif pid == P.VOLUME_BINDING:
+            rec["prescore"][name] = ""
+            skip_score.add(pid)
+        elif pid == P.BALANCED_ALLOCATION:
+            req = m.pod_requests(pod)
+            be = all(req.get(r, 0) == 0 for r, _ in prof.ba_resources)
+            if prof.ba_skip_best_effort and be:
+                rec["prescore"][name] = ""
+                skip_score.add(pid)
+            else:
+                rec["prescore"][name] = "success"
+        elif pid == P.POD_TOPOLOGY_SPREAD:
+            s = pts_prescore(pod, infos, fnodes, prof)
+            if s is None:
+                rec["prescore"][name] = ""
+                skip_score.add(pid)
+            else:
+                pstate[pid] = s
+                rec["prescore"][name] = "success"
+        elif pid == P.INTER_POD_AFFINITY:
+            s = ipa_prescore(pod, infos, prof)
+            if s is None:
+                rec["prescore"][name] = ""
+                skip_score.add(pid)
+            else:
+                pstate[pid] = s
+                rec["prescore"][name] = "success"
+    weights = prof.weights()
+    total = [0] * len(fnodes)
+    for pid in prof.score_order():
+        if pid in skip_score:
+            continue
+        name = P.PLUGIN_NAMES[pid]
+        raw = []
+        for ni in fnodes:
+            if pid == P.NODE_RESOURCES_FIT:
+                s = fit_score(pod, ni, prof)
+            elif pid == P.BALANCED_ALLOCATION:
+                s = ba_score(pod, ni, prof)
+            elif pid == P.TAINT_TOLERATION:
+                tols = [t for t in pod.tolerations if t.effect in ("", m.PREFER_NO_SCHEDULE)]
+                s = sum(1 for t in ni.node.taints if t.effect == m.PREFER_NO_SCHEDULE
+                        and not m.tolerations_tolerate(tols, t))
+            elif pid == P.NODE_AFFINITY:
+                s = 0
+                for pt in pod.node_affinity_preferred:
+                    if pt.weight == 0:
+                        continue
+                    if node_term_matches(pt.preference, ni.node):
+                        s += pt.weight
+            elif pid == P.IMAGE_LOCALITY:
+                s = image_score(pod, ni, total_nodes)
+            elif pid == P.POD_TOPOLOGY_SPREAD:
+                s = pts_score(pstate[pid], pod, ni)
+            elif pid == P.INTER_POD_AFFINITY:
+                s = ipa_score(pstate[pid], ni)
+            else:   # VolumeBinding has no scorer in v1.32 defaults (PreScore Skip)
+                s = 0
+            raw.append(s)
+        w = weights.get(name, 1)
+        for nm, s in zip(names, raw):
+            rec["score"].setdefault(nm, {})[name] = str(s)
+            rec["finalscore"].setdefault(nm, {})[name] = str(s * w)
+        norm = raw
+        if pid == P.TAINT_TOLERATION:
+            norm = default_normalize(raw, True)
+        elif pid == P.NODE_AFFINITY:
+            norm = default_normalize(raw, False)
+        elif pid == P.POD_TOPOLOGY_SPREAD:
+            norm = pts_normalize(pstate[pid], names, raw)
+        elif pid == P.INTER_POD_AFFINITY:
+            norm = ipa_normalize(raw)
+        if P.EXT[pid][4]:
+            for nm, s in zip(names, norm):
+                rec["finalscore"][nm][name] = str(s * w)
+        for i, s in enumerate(norm):
+            if s > MAX_NODE_SCORE or s < 0:
+                raise ValueError(f"plugin {name} returns an invalid score {s}")
+            total[i] += s * w
+        rec["raw"][name] = {feasible[i]: raw[i] for i in range(len(raw))}
+        rec["norm"][name] = {feasible[i]: norm[i] for i in range(len(norm))}
+    best = max(range(len(fnodes)), key=lambda i: (total[i], -feasible[i]))
+    rec["selected_index"] = feasible[best]
+    rec["selected"] = names[best]
+    rec["total"] = {feasible[i]: total[i] for i in range(len(total))}
+    return rec
+
+
+def run_queue(nodes, bound, queue, prof, capture=True):
+    """Schedules `queue` in order; unschedulable pods are attempted once."""
+    infos = build_snapshot(nodes, bound)
+    recs = []
+    for pod in queue:
+        rec = schedule_one(pod, infos, prof)
+        if rec["selected_index"] >= 0:
+            infos[rec["selected_index"]].add_pod(pod)
+        recs.append(rec if capture else rec["selected_index"])
+    return recs

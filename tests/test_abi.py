@@ -1,0 +1,57 @@
+"""The C-ABI library loads and exports every entry point include/ksched.h declares."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT, pkg
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "ksched.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ksg_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    for s in ("ksg_open", "ksg_eval", "ksg_commit", "ksg_run_queue", "ksg_run_replicas", "ksg_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_symbol(built):
+    native = pkg("native")
+    lib = ctypes.CDLL(native.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    lib.ksg_abi_version.restype = ctypes.c_int
+    assert lib.ksg_abi_version() == 1
+
+
+def test_struct_layouts_match(tmp_path):
+    """ctypes / numpy mirrors of the ABI structs have the C compiler's layout."""
+    import subprocess
+    native = pkg("native")
+    E = pkg("encoder")
+    src = tmp_path / "sz.c"
+    names = ["ksg_nodes", "ksg_topology", "ksg_pod", "ksg_workload", "ksg_profile", "ksg_result",
+             "ksg_capture", "ksg_node_state", "ksg_replica_summary"]
+    src.write_text('#include <stdio.h>\n#include "ksched.h"\nint main(void){' +
+                   "".join(f'printf("%zu\\n", sizeof({n}));' for n in names) + "return 0;}")
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    sizes = dict(zip(names, map(int, subprocess.check_output([str(exe)]).split())))
+    assert sizes["ksg_pod"] == E.POD_DTYPE.itemsize
+    assert sizes["ksg_nodes"] == ctypes.sizeof(native.KsgNodes)
+    assert sizes["ksg_topology"] == ctypes.sizeof(native.KsgTopology)
+    assert sizes["ksg_workload"] == ctypes.sizeof(native.KsgWorkload)
+    assert sizes["ksg_profile"] == ctypes.sizeof(native.KsgProfile)
+    assert sizes["ksg_result"] == ctypes.sizeof(native.KsgResult) == native.RESULT_DTYPE.itemsize
+    assert sizes["ksg_capture"] == ctypes.sizeof(native.KsgCapture)
+    assert sizes["ksg_node_state"] == ctypes.sizeof(native.KsgNodeState)
+    assert sizes["ksg_replica_summary"] == ctypes.sizeof(native.KsgReplicaSummary)
+
+
+def test_product_path_fails_loudly_without_library(tmp_path):
+    native = pkg("native")
+    import pytest
+    with pytest.raises(native.KschedError):
+        native.Engine(lib_path=str(tmp_path / "missing.so"))
