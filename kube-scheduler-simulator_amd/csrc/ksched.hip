@@ -1,25 +1,35 @@
 // libksched.so — MI355X (gfx950) Filter/Score evaluator behind the C ABI of
 // include/ksched.h.
 //
-// Kernel structure:
-//   ksg_queue_kernel<BLOCK>: one workgroup per scheduling replica, persistent
-//   over the pod queue.  Per pod:
-//     stage   pod record + its program blob -> LDS (one coalesced copy)
-//     sweep A every lane walks nodes n = tid, tid+BLOCK, ...: Filter plugins in
-//             profile order with first-rejection exit (RunFilterPlugins), then
-//             raw scores; un-normalised plugins (Fit, BalancedAllocation,
-//             ImageLocality) are weighted into a partial total on the spot;
-//             normalised plugins (TaintToleration, NodeAffinity) keep their raw
-//             score and feed block-wide max reductions
-//     reduce  wave shuffles + one LDS round: feasible count, first feasible
-//             node, per-plugin maxima
-//     sweep B (>= 2 feasible nodes) DefaultNormalizeScore, weighted sum,
-//             packed (total << 32 | ~node) argmax = selectHost with the
-//             lowest-index tie-break
-//     assume  one lane commits the pod into the selected node's columns
-//   A replica never talks to another workgroup, so there is no inter-workgroup
-//   synchronisation at all (the per-pod dependency is inside one CU).
-//   ksg_commit_kernel: NodeInfo.AddPod for ksg_commit().
+// Two execution schemes, both bit-exact with the sequential
+// upstream cycle:
+//
+// 1. ksg_queue_kernel<BLOCK> — one workgroup per scheduling replica,
+//    persistent over the pod queue.  Per pod: stage the pod into LDS; sweep A
+//    (every lane walks nodes tid, tid+BLOCK, ...: filters in profile order with
+//    first-rejection exit, raw scores); block reduction (feasible count, first
+//    feasible node, normalisation maxima); sweep B (normalise, weight,
+//    packed-key argmax = selectHost with lowest-index tie-break); one lane
+//    assumes the pod.  Used for replica sweeps (config 4: one CU per
+//    replica, no inter-workgroup traffic), for capture (annotation) runs and
+//    for ksg_eval.
+//
+// 2. Batched speculate-and-repair, for a single replica's placement-only queue
+//    when every enabled plugin is node-local (Fit, BalancedAllocation,
+//    TaintToleration, NodeAffinity, ImageLocality, NodeUnschedulable,
+//    NodeName): assuming a pod changes the columns of exactly one node, so
+//    pod j of a batch sees the batch-start state everywhere except at the
+//    <= j nodes chosen earlier in the batch.
+//      ksg_batch_phase1  grid (node tiles, B pods): every (pod, node) of the
+//                        batch against the batch-start state, packed into one
+//                        8-byte record; per-pod normalisation maxima by atomics.
+//      ksg_batch_phase2  one workgroup walks the batch in order: re-evaluates
+//                        only the changed nodes against the live state, scans
+//                        the records of the others, normalises with the live
+//                        maxima (a second scan only if a max holder dropped
+//                        out), selects and assumes.
+//    Only the changed nodes are ever recomputed, so the result is the
+//    sequential result exactly.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,9 +38,13 @@
 #include <string>
 #include <vector>
 
-#include "ksched_device.h"
+#include "ksched_kernels.h"
+
+#define KSG_BATCH_MAX 256
 
 namespace {
+
+using namespace ksg;
 
 struct Red {
   int64_t max_t;   // TaintToleration raw max over feasible nodes
@@ -54,64 +68,6 @@ struct QueueArgs {
   int64_t* cap_norm;
   int64_t* cap_total;           // [count][N]
 };
-
-constexpr uint32_t bit(int p) { return 1u << p; }
-
-__device__ __forceinline__ int64_t wave_max64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (int64_t)__shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t w = __shfl_xor(v, o, 64);
-    v = w > v ? w : v;
-  }
-  return v;
-}
-__device__ __forceinline__ int32_t wave_sum32(int32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ int32_t wave_min32(int32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-  return v;
-}
-
-// NodeInfo.AddPod restricted to the columns the plugins read, plus the
-// PodTopologySpread / InterPodAffinity count tables.
-__device__ void commit_node(const DevCluster& c, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
-                            int32_t* cnt, int32_t* tab, int32_t* tmpl_total, const ksg_pod& p,
-                            const int32_t* commit_prog, int n) {
-  const int N = c.N;
-  for (int r = 0; r < c.R; r++) requested[(size_t)r * N + n] += p.req[r];
-  nonzero[n] += p.nz_cpu;
-  nonzero[(size_t)N + n] += p.nz_mem;
-  pod_count[n] += 1;
-  if (commit_prog) {
-    const int32_t* w = commit_prog;
-    const int ns = *w++;
-    for (int i = 0; i < ns; i++) cnt[(size_t)w[i] * N + n] += 1;
-    w += ns;
-    const int nt = *w++;
-    for (int i = 0; i < nt; i++) {
-      const int t = w[i];
-      const int col = c.tmpl_col[t];
-      const uint32_t v = c.label_val[(size_t)col * N + n];
-      if (!v) continue;
-      tab[c.tmpl_off[t] + v] += c.tmpl_kind[t] == KSG_TMPL_PREF ? c.tmpl_weight[t] : 1;
-      tmpl_total[t] += 1;
-    }
-  }
-}
 
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
@@ -143,30 +99,11 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
   for (int k = 0; k < a.count; k++) {
     const int pi = a.first + k;
     __syncthreads();  // previous pod fully consumed; its commit is visible
-    if (tid < (int)(sizeof(ksg_pod) / 4))
-      reinterpret_cast<int32_t*>(&s_pod)[tid] = reinterpret_cast<const int32_t*>(a.pods + pi)[tid];
-    {
-      const int boff = a.pods[pi].blob, blen = a.pods[pi].blob_len;
-      for (int i = tid; i < blen; i += BLOCK) s_blob[i] = a.prog[boff + i];
-    }
+    stage_pod<BLOCK>(a.pods, a.prog, pi, &s_pod, s_blob);
     __syncthreads();
     const ksg_pod& p = s_pod;
     const ksg_profile& prof = s_prof;
-    const int boff = p.blob;
-    auto rb = [boff](int off) { return off < 0 ? -1 : off - boff; };
-    const int32_t* P = s_blob;
-    const int tol = rb(p.tol), na_req = rb(p.na_req), na_pref = rb(p.na_pref), img = rb(p.img);
-    const int32_t* tolf = P + tol;
-    const int32_t* tolp = P + tol + c.W;
-    const bool reject = (p.flags & KSG_POD_PREFILTER_REJECT) != 0;
-    const uint32_t fskip = p.filter_skip | bit(KSG_PL_INTER_POD_AFFINITY) | bit(KSG_PL_POD_TOPOLOGY_SPREAD);
-    const uint32_t smask = prof.score_mask & ~p.score_skip &
-                           ~(bit(KSG_PL_INTER_POD_AFFINITY) | bit(KSG_PL_POD_TOPOLOGY_SPREAD));
-    const int64_t w_fit = prof.weight[KSG_PL_NODE_RESOURCES_FIT];
-    const int64_t w_ba = prof.weight[KSG_PL_BALANCED_ALLOCATION];
-    const int64_t w_img = prof.weight[KSG_PL_IMAGE_LOCALITY];
-    const int64_t w_t = prof.weight[KSG_PL_TAINT_TOLERATION];
-    const int64_t w_a = prof.weight[KSG_PL_NODE_AFFINITY];
+    const PodView v = make_view(c, prof, p, s_blob, a.prog);
     uint32_t* cfs = cap ? a.cap_fstatus + (size_t)k * N : nullptr;
     int64_t* craw = cap ? a.cap_raw + (size_t)k * KSG_NPLUGINS * N : nullptr;
     int64_t* cnorm = cap ? a.cap_norm + (size_t)k * KSG_NPLUGINS * N : nullptr;
@@ -174,76 +111,20 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
     // ---- sweep A: filters + raw scores ------------------------------------
     Red r{0, 0, 0, 0x7fffffff};
     for (int n = tid; n < N; n += BLOCK) {
-      uint32_t st = 0;
-      if (reject || (p.node_set >= 0 && !((((uint32_t)a.prog[p.node_set + (n >> 5)]) >> (n & 31)) & 1u))) {
-        st = KSG_FS_NOT_EVALUATED;
-      } else {
-        for (int kf = 0; kf < prof.n_filter && !st; kf++) {
-          const int pl = prof.filter_order[kf];
-          if ((fskip >> pl) & 1u) continue;
-          switch (pl) {
-            case KSG_PL_NODE_UNSCHEDULABLE:
-              if (c.unsched[n] && !(p.flags & KSG_POD_TOL_UNSCHED)) st = pl + 1;
-              break;
-            case KSG_PL_NODE_NAME:
-              if (p.node_name != -1 && p.node_name != n) st = pl + 1;
-              break;
-            case KSG_PL_TAINT_TOLERATION: {
-              const int s = untolerated_slot(c, tolf, n);
-              if (s >= 0) st = (uint32_t)(pl + 1) | ((uint32_t)s << 8);
-              break;
-            }
-            case KSG_PL_NODE_AFFINITY:
-              if (!na_required_match(c, P, na_req, n)) st = (uint32_t)(pl + 1) | (1u << 8);
-              break;
-            case KSG_PL_NODE_RESOURCES_FIT: {
-              const uint32_t b = fit_filter(c, p, requested, pod_count[n], prof.fit_ignored_res, n);
-              if (b) st = (uint32_t)(pl + 1) | (b << 8);
-              break;
-            }
-            default:
-              break;
-          }
-        }
-      }
-      if (cap) cfs[n] = st;
-      if (st == 0) {
+      const NodeEval e = eval_node(c, prof, v, requested, nonzero, pod_count, n, craw, cnorm);
+      if (cap) cfs[n] = e.st;
+      if (e.st == 0) {
         r.nfeas += 1;
         r.minidx = min(r.minidx, n);
-        int64_t part = 0;
-        if (smask & bit(KSG_PL_NODE_RESOURCES_FIT)) {
-          const int64_t s = fit_score(c, prof, p, requested, nonzero, n);
-          part += s * w_fit;
-          if (cap) { craw[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = s; cnorm[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = s; }
-        }
-        if (smask & bit(KSG_PL_BALANCED_ALLOCATION)) {
-          const int64_t s = ba_score(c, prof, p, requested, nonzero, n);
-          part += s * w_ba;
-          if (cap) { craw[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; cnorm[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; }
-        }
-        if (smask & bit(KSG_PL_IMAGE_LOCALITY)) {
-          const int64_t s = image_score(c, P, img, p.n_containers, n);
-          part += s * w_img;
-          if (cap) { craw[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; cnorm[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; }
-        }
-        if (smask & bit(KSG_PL_TAINT_TOLERATION)) {
-          const int64_t s = taint_score(c, tolp, n);
-          sraw[n] = s;
-          r.max_t = max(r.max_t, s);
-          if (cap) craw[(size_t)KSG_PL_TAINT_TOLERATION * N + n] = s;
-        }
-        if (smask & bit(KSG_PL_NODE_AFFINITY)) {
-          const int64_t s = na_pref_score(c, P, na_pref, n);
-          sraw[(size_t)N + n] = s;
-          r.max_a = max(r.max_a, s);
-          if (cap) craw[(size_t)KSG_PL_NODE_AFFINITY * N + n] = s;
-        }
-        partial[n] = part;
+        r.max_t = max(r.max_t, e.rt);
+        r.max_a = max(r.max_a, e.ra);
+        sraw[n] = e.rt;
+        sraw[(size_t)N + n] = e.ra;
+        partial[n] = e.part;
       } else {
         partial[n] = -1;
       }
     }
-    // ---- reduce ------------------------------------------------------------
     {
       Red w;
       w.max_t = wave_max64(r.max_t);
@@ -276,25 +157,14 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
       for (int n = tid; n < N; n += BLOCK) {
         const int64_t part = partial[n];
         if (part < 0) continue;
-        int64_t total = part;
-        if (smask & bit(KSG_PL_TAINT_TOLERATION)) {
-          const int64_t s = sraw[n];
-          int64_t v = 100;
-          if (g.max_t != 0) v = 100 - 100 * s / g.max_t;
-          err |= (v < 0 || v > 100);
-          total += v * w_t;
-          if (cap) cnorm[(size_t)KSG_PL_TAINT_TOLERATION * N + n] = v;
+        int64_t nt = 0, na = 0;
+        const int64_t total = total_score(v, part, sraw[n], sraw[(size_t)N + n], g.max_t, g.max_a, err, &nt, &na);
+        if (cap) {
+          ctot[n] = total;
+          if (v.smask & bit(KSG_PL_TAINT_TOLERATION)) cnorm[(size_t)KSG_PL_TAINT_TOLERATION * N + n] = nt;
+          if (v.smask & bit(KSG_PL_NODE_AFFINITY)) cnorm[(size_t)KSG_PL_NODE_AFFINITY * N + n] = na;
         }
-        if (smask & bit(KSG_PL_NODE_AFFINITY)) {
-          const int64_t s = sraw[(size_t)N + n];
-          int64_t v = s;
-          if (g.max_a != 0) v = 100 * s / g.max_a;
-          err |= (v < 0 || v > 100);
-          total += v * w_a;
-          if (cap) cnorm[(size_t)KSG_PL_NODE_AFFINITY * N + n] = v;
-        }
-        if (cap) ctot[n] = total;
-        const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xffffffffu - (uint32_t)n);
+        const uint64_t key = argmax_key(total, n);
         best = key > best ? key : best;
       }
       best = wave_max_u64(best);
@@ -309,21 +179,239 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
         ge |= s_err[i];
       }
       if (ge) status |= KSG_ST_SCORE_ERROR;
-      else selected = (int)(0xffffffffu - (uint32_t)(gb & 0xffffffffu));
+      else selected = key_node(gb);
     }
+    uint32_t score_skip;
+    ipa_skip_bits(prof, p, status, score_skip);
     if (tid == 0) {
-      if (a.do_commit && selected >= 0) {
-        const int32_t* cp = p.commit >= 0 ? P + rb(p.commit) : nullptr;
-        commit_node(c, requested, nonzero, pod_count, cnt, tab, tmpl_total, p, cp, selected);
-      }
+      if (a.do_commit && selected >= 0)
+        commit_node(c, requested, nonzero, pod_count, cnt, tab, tmpl_total, p,
+                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected);
       a.placements[(size_t)rep * a.count + k] = selected;
       if (a.results) {
         ksg_result res;
         res.selected = selected;
         res.n_feasible = g.nfeas;
         res.status = status;
-        res.score_skip = p.score_skip;
+        res.score_skip = score_skip;
         a.results[(size_t)rep * a.count + k] = res;
+      }
+    }
+  }
+}
+
+// ---- batched speculate-and-repair --------------------------------------------
+struct BatchArgs {
+  DevCluster c;
+  DevState st;              // replica 0
+  const ksg_pod* pods;
+  const int32_t* prog;
+  const ksg_profile* prof;
+  int32_t b0, nb;           // batch = pods [b0, b0 + nb)
+  int32_t out0;             // output index of pod b0
+  uint64_t* rec;            // [KSG_BATCH_MAX][N] packed phase-1 records
+  int32_t* pmax;            // [KSG_BATCH_MAX][2] phase-1 maxima (taint, node affinity)
+  int32_t* placements;
+  ksg_result* results;      // or null
+};
+
+// record: bit 63 feasible | rt (8 bits) << 48 | ra (16 bits) << 32 | partial (32 bits)
+__device__ __forceinline__ uint64_t pack_rec(const NodeEval& e) {
+  if (e.st != 0) return 0;
+  return (1ull << 63) | ((uint64_t)(e.rt & 0xff) << 48) | ((uint64_t)(e.ra & 0xffff) << 32) | (uint32_t)e.part;
+}
+
+__global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
+  __shared__ int32_t s_blob[KSG_BLOB_MAX];
+  __shared__ ksg_pod s_pod;
+  __shared__ ksg_profile s_prof;
+  __shared__ int32_t s_mt[4], s_ma[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = blockIdx.y;
+  const DevCluster& c = a.c;
+  const int N = c.N;
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
+  __syncthreads();
+  const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog);
+  const int n = blockIdx.x * 256 + tid;
+  int32_t mt = 0, ma = 0;
+  if (n < N) {
+    const NodeEval e = eval_node(c, s_prof, v, a.st.requested, a.st.nonzero, a.st.pod_count, n, nullptr, nullptr);
+    a.rec[(size_t)j * N + n] = pack_rec(e);
+    if (e.st == 0) { mt = (int32_t)e.rt; ma = (int32_t)e.ra; }
+  }
+  mt = (int32_t)wave_max64(mt);
+  ma = (int32_t)wave_max64(ma);
+  if (lane == 0) { s_mt[wv] = mt; s_ma[wv] = ma; }
+  __syncthreads();
+  if (tid == 0) {
+    int32_t bt = 0, ba = 0;
+    for (int i = 0; i < 4; i++) { bt = max(bt, s_mt[i]); ba = max(ba, s_ma[i]); }
+    if (bt) atomicMax(&a.pmax[2 * j], bt);
+    if (ba) atomicMax(&a.pmax[2 * j + 1], ba);
+  }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
+  constexpr int NW = BLOCK / 64;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_cmask[];   // changed-node bitmap, N bits
+  __shared__ int32_t s_blob[KSG_BLOB_MAX];
+  __shared__ ksg_pod s_pod;
+  __shared__ ksg_profile s_prof;
+  __shared__ int32_t s_clist[KSG_BATCH_MAX];
+  __shared__ NodeEval s_ce[KSG_BATCH_MAX];
+  __shared__ int32_t s_nc;
+  __shared__ Red s_red[NW];
+  __shared__ uint64_t s_best[NW];
+  __shared__ uint32_t s_err[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const DevCluster& c = a.c;
+  const int N = c.N;
+  int64_t* requested = a.st.requested;
+  int64_t* nonzero = a.st.nonzero;
+  int32_t* pod_count = a.st.pod_count;
+  const int words = (N + 31) / 32;
+  for (int i = tid; i < words; i += BLOCK) s_cmask[i] = 0;
+  if (tid == 0) s_nc = 0;
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+
+  for (int j = 0; j < a.nb; j++) {
+    const int pi = a.b0 + j;
+    __syncthreads();
+    stage_pod<BLOCK>(a.pods, a.prog, pi, &s_pod, s_blob);
+    __syncthreads();
+    const ksg_pod& p = s_pod;
+    const ksg_profile& prof = s_prof;
+    const PodView v = make_view(c, prof, p, s_blob, a.prog);
+    const int nc = s_nc;
+    // re-evaluate the nodes assumed onto earlier in this batch, on live state
+    for (int i = tid; i < nc; i += BLOCK)
+      s_ce[i] = eval_node(c, prof, v, requested, nonzero, pod_count, s_clist[i], nullptr, nullptr);
+    __syncthreads();
+    const int64_t mt1 = a.pmax[2 * j], ma1 = a.pmax[2 * j + 1];
+    const uint64_t* rec = a.rec + (size_t)j * N;
+    Red r{0, 0, 0, 0x7fffffff};
+    uint64_t best = 0;
+    uint32_t err = 0;
+    for (int n = tid; n < N; n += BLOCK) {
+      if ((s_cmask[n >> 5] >> (n & 31)) & 1u) continue;
+      const uint64_t x = rec[n];
+      if (!(x >> 63)) continue;
+      const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
+      r.nfeas += 1;
+      r.minidx = min(r.minidx, n);
+      r.max_t = max(r.max_t, rt);
+      r.max_a = max(r.max_a, ra);
+      const uint64_t key = argmax_key(total_score(v, part, rt, ra, mt1, ma1, err, nullptr, nullptr), n);
+      best = key > best ? key : best;
+    }
+    for (int i = tid; i < nc; i += BLOCK) {
+      const NodeEval e = s_ce[i];
+      if (e.st != 0) continue;
+      const int n = s_clist[i];
+      r.nfeas += 1;
+      r.minidx = min(r.minidx, n);
+      r.max_t = max(r.max_t, e.rt);
+      r.max_a = max(r.max_a, e.ra);
+      const uint64_t key = argmax_key(total_score(v, e.part, e.rt, e.ra, mt1, ma1, err, nullptr, nullptr), n);
+      best = key > best ? key : best;
+    }
+    {
+      Red w;
+      w.max_t = wave_max64(r.max_t);
+      w.max_a = wave_max64(r.max_a);
+      w.nfeas = wave_sum32(r.nfeas);
+      w.minidx = wave_min32(r.minidx);
+      best = wave_max_u64(best);
+      err = wave_or32(err);
+      if (lane == 0) { s_red[wv] = w; s_best[wv] = best; s_err[wv] = err; }
+    }
+    __syncthreads();
+    Red g{0, 0, 0, 0x7fffffff};
+    uint64_t gb = 0;
+    uint32_t ge = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      const Red w = s_red[i];
+      g.max_t = max(g.max_t, w.max_t);
+      g.max_a = max(g.max_a, w.max_a);
+      g.nfeas += w.nfeas;
+      g.minidx = min(g.minidx, w.minidx);
+      gb = s_best[i] > gb ? s_best[i] : gb;
+      ge |= s_err[i];
+    }
+    const bool stale_t = (v.smask & bit(KSG_PL_TAINT_TOLERATION)) && g.max_t != mt1;
+    const bool stale_a = (v.smask & bit(KSG_PL_NODE_AFFINITY)) && g.max_a != ma1;
+    if (g.nfeas >= 2 && (stale_t || stale_a)) {
+      // a holder of a phase-1 maximum was assumed full: renormalise with the
+      // live maxima (second scan; rare)
+      __syncthreads();
+      best = 0;
+      err = 0;
+      for (int n = tid; n < N; n += BLOCK) {
+        if ((s_cmask[n >> 5] >> (n & 31)) & 1u) continue;
+        const uint64_t x = rec[n];
+        if (!(x >> 63)) continue;
+        const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
+        const uint64_t key = argmax_key(total_score(v, part, rt, ra, g.max_t, g.max_a, err, nullptr, nullptr), n);
+        best = key > best ? key : best;
+      }
+      for (int i = tid; i < nc; i += BLOCK) {
+        const NodeEval e = s_ce[i];
+        if (e.st != 0) continue;
+        const uint64_t key =
+            argmax_key(total_score(v, e.part, e.rt, e.ra, g.max_t, g.max_a, err, nullptr, nullptr), s_clist[i]);
+        best = key > best ? key : best;
+      }
+      best = wave_max_u64(best);
+      err = wave_or32(err);
+      if (lane == 0) { s_best[wv] = best; s_err[wv] = err; }
+      __syncthreads();
+      gb = 0;
+      ge = 0;
+#pragma unroll
+      for (int i = 0; i < NW; i++) {
+        gb = s_best[i] > gb ? s_best[i] : gb;
+        ge |= s_err[i];
+      }
+    }
+    int selected = -1;
+    uint32_t status = 0;
+    if (g.nfeas == 1) {
+      selected = g.minidx;
+    } else if (g.nfeas >= 2) {
+      status |= KSG_ST_SCORED;
+      if (ge) status |= KSG_ST_SCORE_ERROR;
+      else selected = key_node(gb);
+    }
+    uint32_t score_skip;
+    ipa_skip_bits(prof, p, status, score_skip);
+    if (tid == 0) {
+      if (selected >= 0) {
+        commit_node(c, requested, nonzero, pod_count, a.st.cnt, a.st.tab, a.st.tmpl_total, p,
+                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected);
+        if (!((s_cmask[selected >> 5] >> (selected & 31)) & 1u)) {
+          s_cmask[selected >> 5] |= 1u << (selected & 31);
+          s_clist[s_nc] = selected;
+          s_nc = s_nc + 1;
+        }
+      }
+      a.pmax[2 * j] = 0;   // ready for the next batch's phase 1
+      a.pmax[2 * j + 1] = 0;
+      const int o = a.out0 + j;
+      a.placements[o] = selected;
+      if (a.results) {
+        ksg_result res;
+        res.selected = selected;
+        res.n_feasible = g.nfeas;
+        res.status = status;
+        res.score_skip = score_skip;
+        a.results[o] = res;
       }
     }
   }
@@ -348,6 +436,7 @@ struct ksg_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
+  int last_path = 0;   // 1 = queue kernel, 2 = batched
   ksg_profile prof{};
   bool have_prof = false, have_nodes = false, have_wl = false;
   // cluster
@@ -357,8 +446,8 @@ struct ksg_ctx {
   ksg_pod* d_pods = nullptr;
   int32_t* d_prog = nullptr;
   std::vector<ksg_pod> h_pods;
+  std::vector<int32_t> h_na_pref_sum;   // per pod Σ preferred node-affinity weights
   int32_t max_blob = 0;
-  bool any_topology = false;
   // state (replica 0 = the ctx's own state)
   DevState st{};
   size_t tab_words = 0;
@@ -366,7 +455,10 @@ struct ksg_ctx {
   int64_t* d_req0 = nullptr;
   int64_t* d_nz0 = nullptr;
   int32_t* d_pc0 = nullptr;
-  void* wl_allocs[2] = {nullptr, nullptr};
+  // batched-path buffers (lazily allocated)
+  uint64_t* d_rec = nullptr;
+  int32_t* d_pmax = nullptr;
+  int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
 };
 
 namespace {
@@ -411,9 +503,10 @@ int upc(ksg_ctx* ctx, const T*& field, const T* src, size_t count) {
 void free_all(ksg_ctx* ctx) {
   for (void* p : ctx->allocs) (void)hipFree(p);
   ctx->allocs.clear();
+  ctx->d_rec = nullptr;
+  ctx->d_pmax = nullptr;
 }
 
-// Which kernel configuration to launch.
 int launch_queue(ksg_ctx* ctx, QueueArgs& a, int n_replicas, int block) {
   (void)hipGetLastError();
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
@@ -436,22 +529,41 @@ int check_ready(ksg_ctx* ctx) {
   return KSG_OK;
 }
 
-// PodTopologySpread / InterPodAffinity kernels are not in this build yet: refuse
-// pods that need them instead of computing something else.
+bool profile_has(const ksg_profile& prof, int pl) {
+  if ((prof.score_mask >> pl) & 1u) return true;
+  for (int k = 0; k < prof.n_filter; k++)
+    if (prof.filter_order[k] == pl) return true;
+  return false;
+}
+
+// PodTopologySpread / InterPodAffinity terms are not implemented in this
+// build: refuse pods that need them instead of computing something else.
 int check_supported(ksg_ctx* ctx, const ksg_profile& prof, int first, int count) {
-  bool pts = false, ipa = false;
-  for (int k = 0; k < prof.n_filter; k++) {
-    pts |= prof.filter_order[k] == KSG_PL_POD_TOPOLOGY_SPREAD;
-    ipa |= prof.filter_order[k] == KSG_PL_INTER_POD_AFFINITY;
-  }
-  pts |= (prof.score_mask >> KSG_PL_POD_TOPOLOGY_SPREAD) & 1u;
-  ipa |= (prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u;
+  const bool pts = profile_has(prof, KSG_PL_POD_TOPOLOGY_SPREAD), ipa = profile_has(prof, KSG_PL_INTER_POD_AFFINITY);
   for (int i = first; i < first + count; i++) {
     const ksg_pod& p = ctx->h_pods[i];
     if ((pts && p.pts >= 0) || (ipa && p.ipa >= 0))
       return fail(ctx, KSG_E_UNSUPPORTED, "PodTopologySpread/InterPodAffinity terms are not implemented in this build");
   }
   return KSG_OK;
+}
+
+// The batched path packs raw scores into 8-byte records; use it only when the
+// values provably fit.
+bool batch_eligible(ksg_ctx* ctx, int first, int count) {
+  const ksg_profile& prof = ctx->prof;
+  if (ctx->c.T > 255) return false;
+  if (ctx->c.N > (1 << 19)) return false;   // changed-node bitmap must fit LDS
+  int64_t wsum = 0;
+  for (int pl : {KSG_PL_NODE_RESOURCES_FIT, KSG_PL_BALANCED_ALLOCATION, KSG_PL_IMAGE_LOCALITY})
+    if ((prof.score_mask >> pl) & 1u) {
+      if (prof.weight[pl] < 0) return false;
+      wsum += prof.weight[pl];
+    }
+  if (wsum * 100 >= (1ll << 31)) return false;
+  for (int i = first; i < first + count; i++)
+    if (ctx->h_na_pref_sum[i] > 0xffff || ctx->h_na_pref_sum[i] < 0) return false;
+  return true;
 }
 
 QueueArgs base_args(ksg_ctx* ctx) {
@@ -461,6 +573,130 @@ QueueArgs base_args(ksg_ctx* ctx) {
   a.pods = ctx->d_pods;
   a.prog = ctx->d_prog;
   return a;
+}
+
+struct Tmp {
+  std::vector<void*> ptrs;
+  ~Tmp() { for (void* p : ptrs) (void)hipFree(p); }
+  template <typename T>
+  hipError_t alloc(T** p, size_t bytes) {
+    hipError_t e = hipMalloc((void**)p, std::max<size_t>(bytes, 8));
+    if (e == hipSuccess) ptrs.push_back(*p);
+    return e;
+  }
+};
+#define TA(tmp, p, bytes)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (tmp).alloc((p), (bytes));                                         \
+    if (_e != hipSuccess) return fail(ctx, KSG_E_NOMEM, hipGetErrorString(_e));        \
+  } while (0)
+
+int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
+                const ksg_profile* d_prof) {
+  const int N = ctx->c.N;
+  if (!ctx->d_rec) {
+    int rc;
+    if ((rc = dalloc(ctx, &ctx->d_rec, (size_t)KSG_BATCH_MAX * N))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_pmax, (size_t)2 * KSG_BATCH_MAX))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_pmax, 0, sizeof(int32_t) * 2 * KSG_BATCH_MAX, ctx->stream));
+  }
+  BatchArgs b{};
+  b.c = ctx->c;
+  b.st = ctx->st;
+  b.pods = ctx->d_pods;
+  b.prog = ctx->d_prog;
+  b.prof = d_prof;
+  b.rec = ctx->d_rec;
+  b.pmax = ctx->d_pmax;
+  b.placements = d_pl;
+  b.results = d_res;
+  const size_t cmask_bytes = sizeof(uint32_t) * ((N + 31) / 32);
+  (void)hipGetLastError();
+  HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  for (int off = 0; off < count; off += KSG_BATCH_MAX) {
+    b.b0 = first + off;
+    b.out0 = off;
+    b.nb = std::min(KSG_BATCH_MAX, count - off);
+    hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, b);
+    hipLaunchKernelGGL(ksg_batch_phase2<1024>, dim3(1), dim3(1024), cmask_bytes, ctx->stream, b);
+  }
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  return KSG_OK;
+}
+
+int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int32_t* placements,
+                 ksg_result* results, ksg_capture* cap) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (first < 0 || count < 0 || first + count > ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod range");
+  if ((rc = check_supported(ctx, ctx->prof, first, count))) return rc;
+  if (count == 0) return KSG_OK;
+  HIPC(ctx, hipSetDevice(ctx->device));
+  const size_t N = ctx->c.N;
+  Tmp tmp;
+  ksg_profile* d_prof = nullptr;
+  int32_t* d_pl = nullptr;
+  ksg_result* d_res = nullptr;
+  TA(tmp, &d_prof, sizeof(ksg_profile));
+  TA(tmp, &d_pl, sizeof(int32_t) * count);
+  if (results) TA(tmp, &d_res, sizeof(ksg_result) * count);
+  HIPC(ctx, hipMemcpyAsync(d_prof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream));
+  const bool want_cap = cap && (cap->fstatus || cap->raw || cap->norm || cap->total);
+  QueueArgs a = base_args(ctx);
+  if (want_cap) {
+    TA(tmp, &a.cap_fstatus, sizeof(uint32_t) * N * count);
+    TA(tmp, &a.cap_raw, sizeof(int64_t) * N * KSG_NPLUGINS * count);
+    TA(tmp, &a.cap_norm, sizeof(int64_t) * N * KSG_NPLUGINS * count);
+    TA(tmp, &a.cap_total, sizeof(int64_t) * N * count);
+    HIPC(ctx, hipMemsetAsync(a.cap_raw, 0, sizeof(int64_t) * N * KSG_NPLUGINS * count, ctx->stream));
+    HIPC(ctx, hipMemsetAsync(a.cap_norm, 0, sizeof(int64_t) * N * KSG_NPLUGINS * count, ctx->stream));
+    HIPC(ctx, hipMemsetAsync(a.cap_total, 0, sizeof(int64_t) * N * count, ctx->stream));
+  }
+  bool batched = do_commit && !want_cap && batch_eligible(ctx, first, count);
+  if (ctx->force_path == 1) batched = false;
+  if (ctx->force_path == 2 && do_commit && !want_cap) batched = batch_eligible(ctx, first, count);
+  if (batched) {
+    ctx->last_path = 2;
+    if ((rc = run_batched(ctx, first, count, d_pl, d_res, d_prof))) return rc;
+  } else {
+    ctx->last_path = 1;
+    a.first = first;
+    a.count = count;
+    a.do_commit = do_commit;
+    a.profiles = d_prof;
+    a.placements = d_pl;
+    a.results = d_res;
+    const int block = N >= 2048 ? 1024 : (N >= 512 ? 512 : 256);
+    if ((rc = launch_queue(ctx, a, 1, block))) return rc;
+  }
+  if (placements) HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * count, hipMemcpyDeviceToHost, ctx->stream));
+  if (results) HIPC(ctx, hipMemcpyAsync(results, d_res, sizeof(ksg_result) * count, hipMemcpyDeviceToHost, ctx->stream));
+  if (want_cap) {
+    if (cap->fstatus) HIPC(ctx, hipMemcpyAsync(cap->fstatus, a.cap_fstatus, sizeof(uint32_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
+    if (cap->raw) HIPC(ctx, hipMemcpyAsync(cap->raw, a.cap_raw, sizeof(int64_t) * N * KSG_NPLUGINS * count, hipMemcpyDeviceToHost, ctx->stream));
+    if (cap->norm) HIPC(ctx, hipMemcpyAsync(cap->norm, a.cap_norm, sizeof(int64_t) * N * KSG_NPLUGINS * count, hipMemcpyDeviceToHost, ctx->stream));
+    if (cap->total) HIPC(ctx, hipMemcpyAsync(cap->total, a.cap_total, sizeof(int64_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->last_ms = ms;
+  return KSG_OK;
+}
+
+int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, int off) {
+  // na_pref := n_terms { weight n_reqs requirement[n_reqs] }
+  if (off < 0) return 0;
+  size_t w = off;
+  const int nt = prog[w++];
+  int64_t s = 0;
+  for (int t = 0; t < nt; t++) {
+    s += prog[w++];
+    const int nr = prog[w++];
+    for (int r = 0; r < nr; r++) w += 3 + prog[w + 2];
+  }
+  return s > 0x7fffffff ? 0x7fffffff : (int32_t)s;
 }
 
 }  // namespace
@@ -482,6 +718,7 @@ int ksg_open(int device, ksg_ctx** out) {
     delete ctx;
     return KSG_E_DEVICE;
   }
+  if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
   *out = ctx;
   return KSG_OK;
 }
@@ -544,7 +781,6 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
   UP(col_unique, tp->col_unique, L);
   UP(log_table, tp->log_table, tp->log_n);
   c.log_n = tp->log_n;
-  // template tables: one segment of col_vocab[col] words per template
   std::vector<int32_t> off(nt, 0);
   size_t total = 0;
   for (int t = 0; t < tp->n_templates; t++) {
@@ -554,7 +790,6 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
   ctx->tab_words = std::max<size_t>(total, 1);
   UP(tmpl_off, off.data(), nt);
 #undef UP
-  // replica-0 state
   DevState& st = ctx->st;
   st = DevState{};
   if ((rc = upload(ctx, &st.requested, nd->requested, (size_t)R * N))) return rc;
@@ -581,13 +816,17 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "load nodes before the workload");
   HIPC(ctx, hipSetDevice(ctx->device));
   ctx->h_pods.assign(wl->pods, wl->pods + wl->n_pods);
+  std::vector<int32_t> prog(wl->prog, wl->prog + wl->prog_len);
   ctx->max_blob = 0;
-  for (const ksg_pod& p : ctx->h_pods) {
+  ctx->h_na_pref_sum.assign(wl->n_pods, 0);
+  for (int i = 0; i < wl->n_pods; i++) {
+    const ksg_pod& p = ctx->h_pods[i];
     ctx->max_blob = std::max(ctx->max_blob, p.blob_len);
     if (p.blob < 0 || (int64_t)p.blob + p.blob_len > wl->prog_len)
       return fail(ctx, KSG_E_INVALID, "pod blob outside the program pool");
     if (p.node_set >= 0 && (int64_t)p.node_set + (ctx->c.N + 31) / 32 > wl->prog_len)
       return fail(ctx, KSG_E_INVALID, "node set outside the program pool");
+    ctx->h_na_pref_sum[i] = na_pref_weight_sum(prog, p.na_pref);
   }
   int rc;
   if ((rc = upload(ctx, &ctx->d_pods, wl->pods, std::max(wl->n_pods, 1)))) return rc;
@@ -595,73 +834,6 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_pods = wl->n_pods;
   ctx->have_wl = true;
-  return KSG_OK;
-}
-
-static int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int32_t* placements,
-                        ksg_result* results, ksg_capture* cap) {
-  int rc = check_ready(ctx);
-  if (rc) return rc;
-  if (first < 0 || count < 0 || first + count > ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod range");
-  if ((rc = check_supported(ctx, ctx->prof, first, count))) return rc;
-  if (count == 0) return KSG_OK;
-  HIPC(ctx, hipSetDevice(ctx->device));
-  const size_t N = ctx->c.N;
-  QueueArgs a = base_args(ctx);
-  a.first = first;
-  a.count = count;
-  a.do_commit = do_commit;
-  ksg_profile* d_prof = nullptr;
-  int32_t* d_pl = nullptr;
-  ksg_result* d_res = nullptr;
-  std::vector<void*> tmp;
-  auto cleanup = [&]() { for (void* p : tmp) (void)hipFree(p); };
-  auto talloc = [&](void** p, size_t bytes) -> hipError_t {
-    hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 8));
-    if (e == hipSuccess) tmp.push_back(*p);
-    return e;
-  };
-#define TA(p, bytes) do { hipError_t _e = talloc((void**)(p), (bytes)); if (_e != hipSuccess) { cleanup(); return fail(ctx, KSG_E_NOMEM, hipGetErrorString(_e)); } } while (0)
-  TA(&d_prof, sizeof(ksg_profile));
-  TA(&d_pl, sizeof(int32_t) * count);
-  if (results) TA(&d_res, sizeof(ksg_result) * count);
-  a.profiles = d_prof;
-  a.placements = d_pl;
-  a.results = d_res;
-  const bool want_cap = cap && (cap->fstatus || cap->raw || cap->norm || cap->total);
-  if (want_cap) {
-    TA(&a.cap_fstatus, sizeof(uint32_t) * N * count);
-    TA(&a.cap_raw, sizeof(int64_t) * N * KSG_NPLUGINS * count);
-    TA(&a.cap_norm, sizeof(int64_t) * N * KSG_NPLUGINS * count);
-    TA(&a.cap_total, sizeof(int64_t) * N * count);
-    (void)hipMemsetAsync(a.cap_raw, 0, sizeof(int64_t) * N * KSG_NPLUGINS * count, ctx->stream);
-    (void)hipMemsetAsync(a.cap_norm, 0, sizeof(int64_t) * N * KSG_NPLUGINS * count, ctx->stream);
-    (void)hipMemsetAsync(a.cap_total, 0, sizeof(int64_t) * N * count, ctx->stream);
-  }
-#undef TA
-  hipError_t e = hipMemcpyAsync(d_prof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream);
-  if (e != hipSuccess) { cleanup(); return fail(ctx, KSG_E_DEVICE, hipGetErrorString(e)); }
-  const int block = N >= 2048 ? 1024 : (N >= 512 ? 512 : 256);
-  rc = launch_queue(ctx, a, 1, block);
-  if (rc) { cleanup(); return rc; }
-  auto d2h = [&](void* dst, const void* src, size_t bytes) -> bool {
-    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess;
-  };
-  bool ok = true;
-  if (placements) ok &= d2h(placements, d_pl, sizeof(int32_t) * count);
-  if (results) ok &= d2h(results, d_res, sizeof(ksg_result) * count);
-  if (want_cap) {
-    if (cap->fstatus) ok &= d2h(cap->fstatus, a.cap_fstatus, sizeof(uint32_t) * N * count);
-    if (cap->raw) ok &= d2h(cap->raw, a.cap_raw, sizeof(int64_t) * N * KSG_NPLUGINS * count);
-    if (cap->norm) ok &= d2h(cap->norm, a.cap_norm, sizeof(int64_t) * N * KSG_NPLUGINS * count);
-    if (cap->total) ok &= d2h(cap->total, a.cap_total, sizeof(int64_t) * N * count);
-  }
-  e = hipStreamSynchronize(ctx->stream);
-  float ms = 0;
-  if (e == hipSuccess) (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-  ctx->last_ms = ms;
-  cleanup();
-  if (e != hipSuccess || !ok) return fail(ctx, KSG_E_DEVICE, std::string("queue kernel: ") + hipGetErrorString(e));
   return KSG_OK;
 }
 
@@ -704,73 +876,61 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   a.first = first;
   a.count = count;
   a.do_commit = 1;
-  std::vector<void*> tmp;
-  auto cleanup = [&]() { for (void* p : tmp) (void)hipFree(p); };
-  auto talloc = [&](void** p, size_t bytes) -> hipError_t {
-    hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 8));
-    if (e == hipSuccess) tmp.push_back(*p);
-    return e;
-  };
-#define TA(p, bytes) do { hipError_t _e = talloc((void**)(p), (bytes)); if (_e != hipSuccess) { cleanup(); return fail(ctx, KSG_E_NOMEM, hipGetErrorString(_e)); } } while (0)
+  Tmp tmp;
   DevState& s = a.st;
   s.stride_req = R * N; s.stride_nz = 2 * N; s.stride_pc = N; s.stride_cnt = S * N; s.stride_tab = ctx->tab_words;
   s.stride_tt = NT; s.stride_part = N; s.stride_sraw = 4 * N;
-  TA(&s.requested, 8 * RR * s.stride_req);
-  TA(&s.nonzero, 8 * RR * s.stride_nz);
-  TA(&s.pod_count, 4 * RR * s.stride_pc);
-  TA(&s.cnt, 4 * RR * s.stride_cnt);
-  TA(&s.tab, 4 * RR * s.stride_tab);
-  TA(&s.tmpl_total, 4 * RR * s.stride_tt);
-  TA(&s.partial, 8 * RR * s.stride_part);
-  TA(&s.sraw, 8 * RR * s.stride_sraw);
+  TA(tmp, &s.requested, 8 * RR * s.stride_req);
+  TA(tmp, &s.nonzero, 8 * RR * s.stride_nz);
+  TA(tmp, &s.pod_count, 4 * RR * s.stride_pc);
+  TA(tmp, &s.cnt, 4 * RR * s.stride_cnt);
+  TA(tmp, &s.tab, 4 * RR * s.stride_tab);
+  TA(tmp, &s.tmpl_total, 4 * RR * s.stride_tt);
+  TA(tmp, &s.partial, 8 * RR * s.stride_part);
+  TA(tmp, &s.sraw, 8 * RR * s.stride_sraw);
   ksg_profile* d_prof;
   int32_t* d_pl;
-  TA(&d_prof, sizeof(ksg_profile) * RR);
-  TA(&d_pl, sizeof(int32_t) * RR * count);
-#undef TA
-  bool ok = true;
+  TA(tmp, &d_prof, sizeof(ksg_profile) * RR);
+  TA(tmp, &d_pl, sizeof(int32_t) * RR * count);
   for (size_t r = 0; r < RR; r++) {  // every replica starts from the ctx's current state
-    ok &= hipMemcpyAsync(s.requested + r * s.stride_req, ctx->st.requested, 8 * s.stride_req, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess;
-    ok &= hipMemcpyAsync(s.nonzero + r * s.stride_nz, ctx->st.nonzero, 8 * s.stride_nz, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess;
-    ok &= hipMemcpyAsync(s.pod_count + r * s.stride_pc, ctx->st.pod_count, 4 * s.stride_pc, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess;
-    ok &= hipMemcpyAsync(s.cnt + r * s.stride_cnt, ctx->st.cnt, 4 * s.stride_cnt, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess;
-    ok &= hipMemcpyAsync(s.tab + r * s.stride_tab, ctx->st.tab, 4 * s.stride_tab, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess;
-    ok &= hipMemcpyAsync(s.tmpl_total + r * s.stride_tt, ctx->st.tmpl_total, 4 * s.stride_tt, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess;
+    HIPC(ctx, hipMemcpyAsync(s.requested + r * s.stride_req, ctx->st.requested, 8 * s.stride_req, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(ctx, hipMemcpyAsync(s.nonzero + r * s.stride_nz, ctx->st.nonzero, 8 * s.stride_nz, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(ctx, hipMemcpyAsync(s.pod_count + r * s.stride_pc, ctx->st.pod_count, 4 * s.stride_pc, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(ctx, hipMemcpyAsync(s.cnt + r * s.stride_cnt, ctx->st.cnt, 4 * s.stride_cnt, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(ctx, hipMemcpyAsync(s.tab + r * s.stride_tab, ctx->st.tab, 4 * s.stride_tab, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(ctx, hipMemcpyAsync(s.tmpl_total + r * s.stride_tt, ctx->st.tmpl_total, 4 * s.stride_tt, hipMemcpyDeviceToDevice, ctx->stream));
   }
-  ok &= hipMemcpyAsync(d_prof, profiles, sizeof(ksg_profile) * RR, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
-  if (!ok) { cleanup(); return fail(ctx, KSG_E_DEVICE, "replica state copy"); }
+  HIPC(ctx, hipMemcpyAsync(d_prof, profiles, sizeof(ksg_profile) * RR, hipMemcpyHostToDevice, ctx->stream));
   a.profiles = d_prof;
   a.placements = d_pl;
   a.results = nullptr;
   const int block = N >= 8192 ? 512 : 256;
-  rc = launch_queue(ctx, a, (int)RR, block);
-  if (rc) { cleanup(); return rc; }
-  ok = hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * RR * count, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess;
-  std::vector<int64_t> req_cpu, req_mem;
+  if ((rc = launch_queue(ctx, a, (int)RR, block))) return rc;
+  ctx->last_path = 1;
+  HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * RR * count, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<int64_t> req;
   if (summaries) {
-    req_cpu.resize(RR * s.stride_req);
-    ok &= hipMemcpyAsync(req_cpu.data(), s.requested, 8 * RR * s.stride_req, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess;
+    req.resize(RR * s.stride_req);
+    HIPC(ctx, hipMemcpyAsync(req.data(), s.requested, 8 * RR * s.stride_req, hipMemcpyDeviceToHost, ctx->stream));
   }
-  hipError_t e = hipStreamSynchronize(ctx->stream);
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
   float ms = 0;
-  if (e == hipSuccess) (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+  HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
-  cleanup();
-  if (e != hipSuccess || !ok) return fail(ctx, KSG_E_DEVICE, std::string("replica kernel: ") + hipGetErrorString(e));
   if (summaries) {
     for (size_t r = 0; r < RR; r++) {
       ksg_replica_summary& sm = summaries[r];
       sm = ksg_replica_summary{};
       uint64_t h = 1469598103934665603ull;
       for (int k = 0; k < count; k++) {
-        int32_t v = placements[r * count + k];
+        const int32_t v = placements[r * count + k];
         (v >= 0 ? sm.scheduled : sm.unschedulable) += 1;
         for (int b = 0; b < 4; b++) { h ^= (uint8_t)(((uint32_t)v) >> (8 * b)); h *= 1099511628211ull; }
       }
       sm.placement_hash = h;
       for (size_t n = 0; n < N; n++) {
-        sm.cpu_requested += req_cpu[r * s.stride_req + n];
-        sm.mem_requested += req_cpu[r * s.stride_req + N + n];
+        sm.cpu_requested += req[r * s.stride_req + n];
+        sm.mem_requested += req[r * s.stride_req + N + n];
       }
     }
   }

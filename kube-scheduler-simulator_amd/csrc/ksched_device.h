@@ -63,6 +63,21 @@ __device__ __forceinline__ int64_t ld64(const int32_t* w) {
   return (int64_t)(((uint64_t)(uint32_t)w[1] << 32) | (uint32_t)w[0]);
 }
 
+// Exact Go int64 division x / a for 0 <= x, 0 < a (every division on this
+// path: dividends are scores x 100 or byte counts x 100, divisors are
+// allocatable amounts or maxima).  gfx950 has no int64 divide instruction;
+// the compiler's software divide is ~100 instructions.  Below 2^52 the f64
+// quotient is within one of the truth, and one integer multiply-subtract
+// corrects it, so the result is exact.
+__device__ __forceinline__ int64_t div_nonneg(int64_t x, int64_t a) {
+  if ((uint64_t)x >= (1ull << 52) || (uint64_t)(a - 1) >= (1ull << 52)) return x / a;
+  int64_t q = (int64_t)((double)x / (double)a);
+  int64_t r = x - q * a;
+  if (r < 0) { q -= 1; r += a; }
+  if (r >= a) { q += 1; }
+  return q;
+}
+
 // ---- requirement programs (encoder.py grammar); P = pod blob in LDS -------
 __device__ __forceinline__ bool eval_req(const DevCluster& c, const int32_t*& w, int n) {
   const int col = w[0], op = w[1], nv = w[2];
@@ -186,12 +201,12 @@ __device__ __forceinline__ int64_t fit_score(const DevCluster& c, const ksg_prof
     alloc_req(c, p, requested, nonzero, prof.fit_res[i], n, false, a, q);
     if (a == 0) continue;
     int64_t s;
-    if (prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : ((a - q) * 100) / a;
-    else s = ((q > a ? a : q) * 100) / a;
+    if (prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : div_nonneg((a - q) * 100, a);
+    else s = div_nonneg((q > a ? a : q) * 100, a);
     num += s * prof.fit_w[i];
     wsum += prof.fit_w[i];
   }
-  return wsum == 0 ? 0 : num / wsum;
+  return wsum == 0 ? 0 : div_nonneg(num, wsum);
 }
 
 __device__ __forceinline__ int64_t ba_score(const DevCluster& c, const ksg_profile& prof, const ksg_pod& p,
@@ -240,5 +255,5 @@ __device__ __forceinline__ int64_t image_score(const DevCluster& c, const int32_
   const int64_t mx = 1000 * mb * (int64_t)n_containers;
   if (sum < minT) sum = minT;
   else if (sum > mx) sum = mx;
-  return 100 * (sum - minT) / (mx - minT);
+  return div_nonneg(100 * (sum - minT), mx - minT);
 }

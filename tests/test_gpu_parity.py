@@ -55,6 +55,30 @@ def test_queue_capture_matches_oracle(gpu, oracle, name, make):
     assert (pl >= 0).any()
 
 
+@pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
+def test_placement_queue_matches_oracle(gpu, oracle, name, make):
+    """Placement-only queue (no capture): the batched speculate-and-repair path."""
+    nodes, pods, prof = make()
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    oracle.load(enc, pf)
+    pg, rg = gpu.run_queue(0, len(pods))
+    po, ro = oracle.run_queue(0, len(pods))
+    np.testing.assert_array_equal(pg, po)
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
+    R = len(enc.cluster.res_names)
+    for a, b in zip(gpu.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(a, b)
+    # second half of the queue after a reset + split: batches straddling calls
+    gpu.reset_state()
+    half = len(pods) // 2
+    p1, _ = gpu.run_queue(0, half)
+    p2, _ = gpu.run_queue(half, len(pods) - half)
+    np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
+
+
 def test_annotations_bytes_gpu_vs_pyoracle(gpu):
     nodes, pods, prof = G.config2(n_nodes=40, n_pods=60, seed=21)
     want, _ = pyoracle_annotations(nodes, pods, prof)
