@@ -18,6 +18,10 @@ native = importlib.import_module("kube-scheduler-simulator_amd.native")
 
 LIB = os.path.join(HERE, "liboracle.so")
 
+# Worker threads spin between the per-pod parallel phases instead of sleeping
+# (libgomp reads this once, when the library loads).
+os.environ.setdefault("OMP_WAIT_POLICY", "ACTIVE")
+
 
 def build(force: bool = False) -> str:
     src = os.path.join(HERE, "oracle.cpp")

@@ -598,7 +598,10 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
     IpaPre ipre;
     ipre.skip = true;
     if (p.ipa >= 0 && in_filter(c, KSG_PL_INTER_POD_AFFINITY)) ipre = ipa_prefilter(c, p, ig);
-    if (ipre.skip) { fskip |= 1u << KSG_PL_INTER_POD_AFFINITY; res->status |= KSG_ST_IPA_PREFILTER_SKIP; }
+    if (ipre.skip) {
+      fskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
+      if (in_filter(c, KSG_PL_INTER_POD_AFFINITY)) res->status |= KSG_ST_IPA_PREFILTER_SKIP;
+    }
     const int32_t* node_set = p.node_set >= 0 ? c.prog.data() + p.node_set : nullptr;
 #pragma omp parallel for num_threads(c.nthreads) schedule(static)
     for (int n = 0; n < N; n++) {
@@ -674,13 +677,19 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
   const size_t F = feas.size();
   std::vector<int64_t> total(F, 0);
   std::vector<int64_t> raw(F), norm(F);
-  for (int pl = 0; pl < KSG_NPLUGINS; pl++) {
-    if (!((c.prof.score_mask >> pl) & 1u) || ((sskip >> pl) & 1u)) continue;
+  // RunScorePlugins: Score() of every plugin for every feasible node (one
+  // parallel pass over nodes, like the upstream Parallelizer), then
+  // NormalizeScore per plugin.
+  int plugins[KSG_NPLUGINS], np = 0;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if (((c.prof.score_mask >> pl) & 1u) && !((sskip >> pl) & 1u)) plugins[np++] = pl;
+  std::vector<int64_t> rawm((size_t)np * F);
 #pragma omp parallel for num_threads(c.nthreads) schedule(static)
-    for (size_t i = 0; i < F; i++) {
-      int n = feas[i];
+  for (size_t i = 0; i < F; i++) {
+    const int n = feas[i];
+    for (int k = 0; k < np; k++) {
       int64_t s = 0;
-      switch (pl) {
+      switch (plugins[k]) {
         case KSG_PL_NODE_RESOURCES_FIT: s = fit_score(c, p, n); break;
         case KSG_PL_BALANCED_ALLOCATION: s = ba_score(c, p, n); break;
         case KSG_PL_TAINT_TOLERATION: s = taint_score(c, p, n); break;
@@ -690,54 +699,60 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
         case KSG_PL_INTER_POD_AFFINITY: s = ipa_score(c, ist, n); break;
         default: s = 0; break;
       }
-      raw[i] = s;
-    }
-    // NormalizeScore
-    norm = raw;
-    if (pl == KSG_PL_TAINT_TOLERATION || pl == KSG_PL_NODE_AFFINITY) {
-      bool reverse = pl == KSG_PL_TAINT_TOLERATION;
-      int64_t mx = 0;
-      for (size_t i = 0; i < F; i++) mx = std::max(mx, raw[i]);
-      if (mx == 0) {
-        if (reverse) for (size_t i = 0; i < F; i++) norm[i] = kMaxNodeScore;
-      } else {
-        for (size_t i = 0; i < F; i++) {
-          int64_t s = kMaxNodeScore * raw[i] / mx;
-          norm[i] = reverse ? kMaxNodeScore - s : s;
-        }
-      }
-    } else if (pl == KSG_PL_POD_TOPOLOGY_SPREAD) {
-      int64_t mn = INT64_MAX, mx = 0;
-      for (size_t i = 0; i < F; i++) {
-        if (pst.ignored[feas[i]]) continue;
-        mn = std::min(mn, raw[i]);
-        mx = std::max(mx, raw[i]);
-      }
-      for (size_t i = 0; i < F; i++) {
-        if (pst.ignored[feas[i]]) norm[i] = 0;
-        else if (mx == 0) norm[i] = kMaxNodeScore;
-        else norm[i] = kMaxNodeScore * (mx + mn - raw[i]) / mx;
-      }
-    } else if (pl == KSG_PL_INTER_POD_AFFINITY) {
-      int64_t mn = INT64_MAX, mx = INT64_MIN;
-      for (size_t i = 0; i < F; i++) { mn = std::min(mn, raw[i]); mx = std::max(mx, raw[i]); }
-      int64_t diff = mx - mn;
-      for (size_t i = 0; i < F; i++) {
-        double f = 0;
-        if (diff > 0) f = (double)kMaxNodeScore * ((double)(raw[i] - mn) / (double)diff);
-        norm[i] = (int64_t)f;
-      }
-    }
-    int64_t w = c.prof.weight[pl];
-    for (size_t i = 0; i < F; i++) {
-      if (norm[i] > kMaxNodeScore || norm[i] < 0) res->status |= KSG_ST_SCORE_ERROR;
-      total[i] += norm[i] * w;
-      if (cap && cap->raw) {
-        cap->raw[(size_t)pl * N + feas[i]] = raw[i];
-        cap->norm[(size_t)pl * N + feas[i]] = norm[i];
-      }
+      rawm[(size_t)k * F + i] = s;
     }
   }
+  // NormalizeScore statistics per plugin (serial, no division) ...
+  int64_t s_min[KSG_NPLUGINS], s_max[KSG_NPLUGINS];
+  for (int k = 0; k < np; k++) {
+    const int pl = plugins[k];
+    const int64_t* r = rawm.data() + (size_t)k * F;
+    int64_t mn = INT64_MAX, mx = pl == KSG_PL_INTER_POD_AFFINITY ? INT64_MIN : 0;
+    for (size_t i = 0; i < F; i++) {
+      if (pl == KSG_PL_POD_TOPOLOGY_SPREAD && pst.ignored[feas[i]]) continue;
+      mn = std::min(mn, r[i]);
+      mx = std::max(mx, r[i]);
+    }
+    s_min[k] = mn;
+    s_max[k] = mx;
+  }
+  // ... then normalise, weight and sum per node (parallel).
+  uint32_t err = 0;
+#pragma omp parallel for num_threads(c.nthreads) schedule(static) reduction(| : err)
+  for (size_t i = 0; i < F; i++) {
+    int64_t t = 0;
+    for (int k = 0; k < np; k++) {
+      const int pl = plugins[k];
+      const int64_t x = rawm[(size_t)k * F + i], mn = s_min[k], mx = s_max[k];
+      int64_t v = x;
+      if (pl == KSG_PL_TAINT_TOLERATION || pl == KSG_PL_NODE_AFFINITY) {
+        // helper.DefaultNormalizeScore(MaxNodeScore, reverse)
+        const bool reverse = pl == KSG_PL_TAINT_TOLERATION;
+        if (mx == 0) v = reverse ? kMaxNodeScore : x;
+        else {
+          const int64_t sc = kMaxNodeScore * x / mx;
+          v = reverse ? kMaxNodeScore - sc : sc;
+        }
+      } else if (pl == KSG_PL_POD_TOPOLOGY_SPREAD) {
+        if (pst.ignored[feas[i]]) v = 0;
+        else if (mx == 0) v = kMaxNodeScore;
+        else v = kMaxNodeScore * (mx + mn - x) / mx;
+      } else if (pl == KSG_PL_INTER_POD_AFFINITY) {
+        const int64_t diff = mx - mn;
+        double f = 0;
+        if (diff > 0) f = (double)kMaxNodeScore * ((double)(x - mn) / (double)diff);
+        v = (int64_t)f;
+      }
+      if (v > kMaxNodeScore || v < 0) err |= 1u;
+      t += v * c.prof.weight[pl];
+      if (cap && cap->raw) {
+        cap->raw[(size_t)pl * N + feas[i]] = x;
+        cap->norm[(size_t)pl * N + feas[i]] = v;
+      }
+    }
+    total[i] = t;
+  }
+  if (err) res->status |= KSG_ST_SCORE_ERROR;
   if (res->status & KSG_ST_SCORE_ERROR) return KSG_OK;  // framework error: no placement
   size_t best = 0;
   for (size_t i = 1; i < F; i++)
