@@ -417,6 +417,408 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
   }
 }
 
+// ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (int64_t)__shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
+  constexpr int NW = BLOCK / 64;
+  constexpr long long BIG = 0x7fffffffffffffffll;
+  __shared__ int32_t s_blob[KSG_BLOB_MAX];
+  __shared__ __attribute__((aligned(16))) int32_t s_hist[KSG_HIST_MAX];
+  __shared__ ksg_pod s_pod;
+  __shared__ ksg_profile s_prof;
+  __shared__ TopoProg s_g;
+  __shared__ TopoShared s_t;
+  __shared__ Red s_red[NW];
+  __shared__ uint64_t s_best[NW];
+  __shared__ uint32_t s_err[NW];
+  __shared__ long long s_r64[NW][4];
+  __shared__ int s_size[kMaxSoft];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int rep = blockIdx.x;
+  const DevCluster& c = a.c;
+  const int N = c.N;
+  int64_t* requested = a.st.requested + rep * a.st.stride_req;
+  int64_t* nonzero = a.st.nonzero + rep * a.st.stride_nz;
+  int32_t* pod_count = a.st.pod_count + rep * a.st.stride_pc;
+  int32_t* cnt = a.st.cnt + rep * a.st.stride_cnt;
+  int32_t* tab = a.st.tab + rep * a.st.stride_tab;
+  int32_t* tmpl_total = a.st.tmpl_total + rep * a.st.stride_tt;
+  int64_t* partial = a.st.partial + rep * a.st.stride_part;
+  int64_t* sraw = a.st.sraw + rep * a.st.stride_sraw;
+  const bool cap = a.cap_fstatus != nullptr && rep == 0;
+
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles + rep)[tid];
+  __syncthreads();
+  const ksg_profile& prof = s_prof;
+  bool ipa_in_filter = false;
+  for (int kf = 0; kf < prof.n_filter; kf++) ipa_in_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
+  const bool ipa_in_score = (prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u;
+
+  for (int k = 0; k < a.count; k++) {
+    const int pi = a.first + k;
+    __syncthreads();
+    stage_pod<BLOCK>(a.pods, a.prog, pi, &s_pod, s_blob);
+    __syncthreads();
+    const ksg_pod& p = s_pod;
+    if (tid == 0) {
+      const PodView v0 = make_view(c, prof, p, s_blob, a.prog, true);
+      parse_topo(p, s_blob, v0.fskip, v0.smask, s_g);
+      layout_slots(c, s_g, s_t);
+      long long ma = 0, mh = 0, mp = 0;
+      for (int i = 0; i < s_g.n_ma; i++) ma += tmpl_total[s_g.m_anti[i]];
+      for (int i = 0; i < s_g.n_mh; i++) mh += tmpl_total[s_g.m_hard[i]];
+      for (int i = 0; i < s_g.n_mp; i++) mp += tmpl_total[s_g.m_pref[i]];
+      s_t.ipa_skip_filter = !s_g.ipa || (ma == 0 && s_g.n_aff == 0 && s_g.n_anti == 0);
+      // PreScore Skip unless some term contributes (pref_any added after the pre-pass)
+      s_t.ipa_skip_score = !s_g.ipa || !((prof.hard_pod_affinity_weight > 0 && mh > 0) || mp > 0);
+      for (int i = 0; i < kMaxHard; i++) { s_t.hard_min[i] = BIG; s_t.hard_dom[i] = 0; }
+      for (int i = 0; i < kMaxSoft; i++) {
+        s_t.soft_empty[i] = 0; s_t.soft_present[i] = 0; s_t.soft_empty_seen[i] = 0; s_size[i] = 0;
+      }
+      s_t.n_ignored = 0;
+      s_t.aff_total = 0;
+      s_t.pref_any = 0;
+    }
+    __syncthreads();
+    const bool ok = s_t.ok;
+    for (int i = tid; i < s_t.words; i += BLOCK) s_hist[i] = 0;
+    PodView v = make_view(c, prof, p, s_blob, a.prog, true);
+    if (s_t.ipa_skip_filter) v.fskip |= bit(KSG_PL_INTER_POD_AFFINITY);
+    const TopoProg& g = s_g;
+    const TopoCtx tc{&s_g, &s_t, s_hist, cnt, tab};
+    __syncthreads();
+
+    // ---- pre-pass: per-domain counts ------------------------------------
+    const bool pre = ok && (g.pts_filter || g.pts_score || g.ipa);
+    if (pre) {
+      long long lmin[kMaxHard], ldom[kMaxHard], lempty[kMaxSoft], laff = 0, lany = 0;
+      for (int i = 0; i < kMaxHard; i++) { lmin[i] = BIG; ldom[i] = 0; }
+      for (int i = 0; i < kMaxSoft; i++) lempty[i] = 0;
+      for (int n = tid; n < N; n += BLOCK) {
+        if (g.pts_filter && has_all(c, g.hard, g.n_hard, 7, n)) {
+          for (int i = 0; i < g.n_hard; i++) {
+            const int32_t* h = g.hard + 7 * i;
+            if (!inclusion(c, v, h[5], h[6], n)) continue;
+            const Slot& sl = s_t.hard[i];
+            const int32_t x = cnt_at(cnt, N, sl.sel, n);
+            if (sl.unique) {
+              lmin[i] = min(lmin[i], (long long)x);
+              ldom[i] += 1;
+            } else {
+              const uint32_t val = lab(c, sl.col, n);
+              atomicAdd(&s_hist[sl.hist + val], x);
+              atomicOr((uint32_t*)&s_hist[sl.pres + (val >> 5)], 1u << (val & 31));
+            }
+          }
+        }
+        if (g.pts_score && (!g.require_all || has_all(c, g.soft, g.n_soft, 6, n))) {
+          for (int i = 0; i < g.n_soft; i++) {
+            const int32_t* sc = g.soft + 6 * i;
+            if (sc[5] || !inclusion(c, v, sc[3], sc[4], n)) continue;
+            const Slot& sl = s_t.soft[i];
+            uint32_t val = lab(c, sl.col, n);
+            if (!val) val = 1;   // node.Labels[key] of a missing key is ""
+            const int32_t x = cnt_at(cnt, N, sl.sel, n);
+            if (sl.unique) {
+              if (val == 1) lempty[i] += x;
+            } else {
+              atomicAdd(&s_hist[sl.hist + val], x);
+            }
+          }
+        }
+        if (g.ipa) {
+          if (g.n_aff > 0) {
+            const int32_t x = cnt_at(cnt, N, g.sel_all, n);
+            for (int i = 0; i < g.n_aff; i++) {
+              const Slot& sl = s_t.aff[i];
+              const uint32_t val = lab(c, sl.col, n);
+              if (!val) continue;
+              laff += x;
+              if (!sl.unique) {
+                atomicAdd(&s_hist[sl.hist + val], x);
+                atomicOr((uint32_t*)&s_hist[sl.pres + (val >> 5)], 1u << (val & 31));
+              }
+            }
+          }
+          for (int i = 0; i < g.n_anti; i++) {
+            const Slot& sl = s_t.anti[i];
+            const uint32_t val = lab(c, sl.col, n);
+            if (!val || sl.unique) continue;
+            atomicAdd(&s_hist[sl.hist + val], cnt_at(cnt, N, sl.sel, n));
+            atomicOr((uint32_t*)&s_hist[sl.pres + (val >> 5)], 1u << (val & 31));
+          }
+          for (int i = 0; i < g.n_pref; i++) {
+            const Slot& sl = s_t.pref[i];
+            const uint32_t val = lab(c, sl.col, n);
+            if (!val) continue;
+            const int32_t x = cnt_at(cnt, N, sl.sel, n);
+            lany |= x > 0;
+            if (!sl.unique) {
+              atomicAdd(&s_hist[sl.hist + val], x);
+              atomicOr((uint32_t*)&s_hist[sl.pres + (val >> 5)], 1u << (val & 31));
+            }
+          }
+        }
+      }
+      for (int i = 0; i < g.n_hard; i++) {
+        const long long m = wave_min64(lmin[i]), d = wave_sum64(ldom[i]);
+        if (lane == 0 && s_t.hard[i].unique) {
+          atomicMin((unsigned long long*)&s_t.hard_min[i], (unsigned long long)m);
+          atomicAdd(&s_t.hard_dom[i], (int)d);
+        }
+      }
+      for (int i = 0; i < g.n_soft; i++) {
+        const long long e = wave_sum64(lempty[i]);
+        if (lane == 0 && e) atomicAdd((unsigned long long*)&s_t.soft_empty[i], (unsigned long long)e);
+      }
+      laff = wave_sum64(laff);
+      lany = wave_sum64(lany);
+      if (lane == 0) {
+        if (laff) atomicAdd((unsigned long long*)&s_t.aff_total, (unsigned long long)laff);
+        if (lany) atomicOr(&s_t.pref_any, 1);
+      }
+      __syncthreads();
+      // minimum over present domains of the non-unique hard slots
+      for (int i = 0; i < g.n_hard; i++) {
+        const Slot& sl = s_t.hard[i];
+        if (sl.unique) continue;
+        long long m = BIG, d = 0;
+        for (int val = tid; val < sl.V; val += BLOCK)
+          if (bit_get(s_hist, sl.pres, val)) { m = min(m, (long long)s_hist[sl.hist + val]); d += 1; }
+        m = wave_min64(m);
+        d = wave_sum64(d);
+        if (lane == 0) {
+          atomicMin((unsigned long long*)&s_t.hard_min[i], (unsigned long long)m);
+          atomicAdd(&s_t.hard_dom[i], (int)d);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        for (int i = 0; i < g.n_hard; i++)   // minMatchNum: 0 when fewer domains than minDomains
+          if (s_t.hard_dom[i] < g.hard[7 * i + 3]) s_t.hard_min[i] = 0;
+        if (s_t.pref_any) s_t.ipa_skip_score = 0;
+      }
+      __syncthreads();
+    }
+
+    uint32_t* cfs = cap ? a.cap_fstatus + (size_t)k * N : nullptr;
+    int64_t* craw = cap ? a.cap_raw + (size_t)k * KSG_NPLUGINS * N : nullptr;
+    int64_t* cnorm = cap ? a.cap_norm + (size_t)k * KSG_NPLUGINS * N : nullptr;
+
+    // ---- sweep A: filters + node-local raw scores ----------------------------
+    Red r{0, 0, 0, 0x7fffffff};
+    int lpres[kMaxSoft] = {0, 0, 0, 0}, lseen[kMaxSoft] = {0, 0, 0, 0}, lign = 0;
+    for (int n = tid; n < N && ok; n += BLOCK) {
+      const NodeEval e = eval_node(c, prof, v, requested, nonzero, pod_count, n, craw, cnorm, &tc);
+      if (cap) cfs[n] = e.st;
+      if (e.st != 0) {
+        partial[n] = -1;
+        continue;
+      }
+      r.nfeas += 1;
+      r.minidx = min(r.minidx, n);
+      r.max_t = max(r.max_t, e.rt);
+      r.max_a = max(r.max_a, e.ra);
+      sraw[n] = e.rt;
+      sraw[(size_t)N + n] = e.ra;
+      partial[n] = e.part;
+      if (g.pts_score) {
+        if (g.require_all && !has_all(c, g.soft, g.n_soft, 6, n)) {
+          lign += 1;
+        } else {
+          for (int i = 0; i < g.n_soft; i++) {
+            if (g.soft[6 * i + 5]) continue;
+            const Slot& sl = s_t.soft[i];
+            uint32_t val = lab(c, sl.col, n);
+            if (!val) val = 1;
+            if (sl.unique) {
+              if (val == 1) lseen[i] = 1;
+              else lpres[i] += 1;
+            } else {
+              atomicOr((uint32_t*)&s_hist[sl.mark + (val >> 5)], 1u << (val & 31));
+            }
+          }
+        }
+      }
+    }
+    {
+      Red w;
+      w.max_t = wave_max64(r.max_t);
+      w.max_a = wave_max64(r.max_a);
+      w.nfeas = wave_sum32(r.nfeas);
+      w.minidx = wave_min32(r.minidx);
+      if (lane == 0) s_red[wv] = w;
+      if (g.pts_score) {
+        for (int i = 0; i < g.n_soft; i++) {
+          const int pr = wave_sum32(lpres[i]), se = (int)wave_or32((uint32_t)lseen[i]);
+          if (lane == 0) {
+            if (pr) atomicAdd(&s_t.soft_present[i], pr);
+            if (se) atomicOr(&s_t.soft_empty_seen[i], 1);
+          }
+        }
+        lign = wave_sum32(lign);
+        if (lane == 0 && lign) atomicAdd(&s_t.n_ignored, lign);
+      }
+    }
+    __syncthreads();
+    Red gr{0, 0, 0, 0x7fffffff};
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      const Red w = s_red[i];
+      gr.max_t = max(gr.max_t, w.max_t);
+      gr.max_a = max(gr.max_a, w.max_a);
+      gr.nfeas += w.nfeas;
+      gr.minidx = min(gr.minidx, w.minidx);
+    }
+    const bool scored = gr.nfeas >= 2;
+    const bool do_pts = scored && g.pts_score;
+    const bool do_ipa = scored && ipa_in_score && !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u) &&
+                        !s_t.ipa_skip_score;
+    if (do_pts) {
+      // topology sizes: distinct domains among feasible, non-ignored nodes
+      for (int i = 0; i < g.n_soft; i++) {
+        const Slot& sl = s_t.soft[i];
+        if (g.soft[6 * i + 5] || sl.unique) continue;
+        int bits = 0;
+        for (int wd = tid; wd < (sl.V + 31) / 32; wd += BLOCK) bits += __popc((uint32_t)s_hist[sl.mark + wd]);
+        bits = wave_sum32(bits);
+        if (lane == 0 && bits) atomicAdd(&s_size[i], bits);
+      }
+      __syncthreads();
+      if (tid == 0)
+        for (int i = 0; i < g.n_soft; i++) {
+          const Slot& sl = s_t.soft[i];
+          int sz;
+          if (g.soft[6 * i + 5]) sz = gr.nfeas - s_t.n_ignored;
+          else if (sl.unique) sz = s_t.soft_present[i] + s_t.soft_empty_seen[i];
+          else sz = s_size[i];
+          s_t.soft_w[i] = c.log_table[sz + 2];   // topologyNormalizingWeight = math.Log(size + 2)
+        }
+      __syncthreads();
+    }
+    // ---- sweep B: PodTopologySpread / InterPodAffinity raw scores -------------
+    long long pmin = BIG, pmax = 0, imin = BIG, imax = -BIG - 1;
+    if (do_pts || do_ipa) {
+      for (int n = tid; n < N; n += BLOCK) {
+        if (partial[n] < 0) continue;
+        if (do_pts) {
+          const int64_t x = pts_score_node(c, v, tc, n);
+          sraw[2 * (size_t)N + n] = x;
+          if (x >= 0) { pmin = min(pmin, (long long)x); pmax = max(pmax, (long long)x); }
+          if (cap) craw[(size_t)KSG_PL_POD_TOPOLOGY_SPREAD * N + n] = x < 0 ? 0 : x;
+        }
+        if (do_ipa) {
+          const int64_t y = ipa_score_node(c, prof, tc, n);
+          sraw[3 * (size_t)N + n] = y;
+          imin = min(imin, (long long)y);
+          imax = max(imax, (long long)y);
+          if (cap) craw[(size_t)KSG_PL_INTER_POD_AFFINITY * N + n] = y;
+        }
+      }
+      pmin = wave_min64(pmin); pmax = wave_max64(pmax); imin = wave_min64(imin); imax = wave_max64(imax);
+      if (lane == 0) { s_r64[wv][0] = pmin; s_r64[wv][1] = pmax; s_r64[wv][2] = imin; s_r64[wv][3] = imax; }
+      __syncthreads();
+      for (int i = 0; i < NW; i++) {
+        pmin = min(pmin, s_r64[i][0]); pmax = max(pmax, s_r64[i][1]);
+        imin = min(imin, s_r64[i][2]); imax = max(imax, s_r64[i][3]);
+      }
+    }
+    // ---- sweep C: normalise, weight, argmax ------------------------------------
+    int selected = -1;
+    uint32_t status = 0;
+    if (!ok) {
+      status |= KSG_ST_SCORE_ERROR;
+    } else if (gr.nfeas == 1) {
+      selected = gr.minidx;
+    } else if (scored) {
+      status |= KSG_ST_SCORED;
+      uint64_t best = 0;
+      uint32_t err = 0;
+      int64_t* ctot = cap ? a.cap_total + (size_t)k * N : nullptr;
+      const int64_t w_pts = prof.weight[KSG_PL_POD_TOPOLOGY_SPREAD], w_ipa = prof.weight[KSG_PL_INTER_POD_AFFINITY];
+      for (int n = tid; n < N; n += BLOCK) {
+        const int64_t part = partial[n];
+        if (part < 0) continue;
+        int64_t nt = 0, na = 0;
+        int64_t total = total_score(v, part, sraw[n], sraw[(size_t)N + n], gr.max_t, gr.max_a, err, &nt, &na);
+        if (cap) {
+          if (v.smask & bit(KSG_PL_TAINT_TOLERATION)) cnorm[(size_t)KSG_PL_TAINT_TOLERATION * N + n] = nt;
+          if (v.smask & bit(KSG_PL_NODE_AFFINITY)) cnorm[(size_t)KSG_PL_NODE_AFFINITY * N + n] = na;
+        }
+        if (do_pts) {   // PodTopologySpread.NormalizeScore
+          const int64_t x = sraw[2 * (size_t)N + n];
+          int64_t s;
+          if (x < 0) s = 0;
+          else if (pmax == 0) s = 100;
+          else s = div_nonneg(100 * (pmax + pmin - x), pmax);
+          err |= (s < 0 || s > 100);
+          total += s * w_pts;
+          if (cap) cnorm[(size_t)KSG_PL_POD_TOPOLOGY_SPREAD * N + n] = s;
+        }
+        if (do_ipa) {   // InterPodAffinity.NormalizeScore (float64 min-max)
+          const int64_t y = sraw[3 * (size_t)N + n];
+          const int64_t diff = imax - imin;
+          double f = 0;
+          if (diff > 0) f = (double)100 * ((double)(y - imin) / (double)diff);
+          const int64_t s = (int64_t)f;
+          err |= (s < 0 || s > 100);
+          total += s * w_ipa;
+          if (cap) cnorm[(size_t)KSG_PL_INTER_POD_AFFINITY * N + n] = s;
+        }
+        if (cap) ctot[n] = total;
+        const uint64_t key = argmax_key(total, n);
+        best = key > best ? key : best;
+      }
+      best = wave_max_u64(best);
+      err = wave_or32(err);
+      if (lane == 0) { s_best[wv] = best; s_err[wv] = err; }
+      __syncthreads();
+      uint64_t gb = 0;
+      uint32_t ge = 0;
+#pragma unroll
+      for (int i = 0; i < NW; i++) {
+        gb = s_best[i] > gb ? s_best[i] : gb;
+        ge |= s_err[i];
+      }
+      if (ge) status |= KSG_ST_SCORE_ERROR;
+      else selected = key_node(gb);
+    }
+    uint32_t score_skip = p.score_skip;
+    if (ipa_in_filter && s_t.ipa_skip_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
+    if (scored && ipa_in_score && !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u) && s_t.ipa_skip_score) {
+      status |= KSG_ST_IPA_PRESCORE_SKIP;
+      score_skip |= bit(KSG_PL_INTER_POD_AFFINITY);
+    }
+    if (tid == 0) {
+      if (a.do_commit && selected >= 0)
+        commit_node(c, requested, nonzero, pod_count, cnt, tab, tmpl_total, p,
+                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected);
+      a.placements[(size_t)rep * a.count + k] = selected;
+      if (a.results) {
+        ksg_result res;
+        res.selected = selected;
+        res.n_feasible = gr.nfeas;
+        res.status = status;
+        res.score_skip = score_skip;
+        a.results[(size_t)rep * a.count + k] = res;
+      }
+    }
+  }
+}
+
 __global__ void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods, const int32_t* prog, int pod,
                                   int node) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -447,6 +849,9 @@ struct ksg_ctx {
   int32_t* d_prog = nullptr;
   std::vector<ksg_pod> h_pods;
   std::vector<int32_t> h_na_pref_sum;   // per pod Σ preferred node-affinity weights
+  std::vector<int32_t> h_prog;
+  std::vector<int32_t> h_col_vocab;
+  std::vector<uint8_t> h_col_unique;
   int32_t max_blob = 0;
   // state (replica 0 = the ctx's own state)
   DevState st{};
@@ -507,15 +912,43 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_pmax = nullptr;
 }
 
-int launch_queue(ksg_ctx* ctx, QueueArgs& a, int n_replicas, int block) {
+bool profile_has(const ksg_profile& prof, int pl) {
+  if ((prof.score_mask >> pl) & 1u) return true;
+  for (int k = 0; k < prof.n_filter; k++)
+    if (prof.filter_order[k] == pl) return true;
+  return false;
+}
+
+// Does any pod of [first, first+count) need the PodTopologySpread /
+// InterPodAffinity kernel under this profile?
+bool needs_topo(ksg_ctx* ctx, const ksg_profile& prof, int first, int count) {
+  const bool pts = profile_has(prof, KSG_PL_POD_TOPOLOGY_SPREAD), ipa = profile_has(prof, KSG_PL_INTER_POD_AFFINITY);
+  if (!pts && !ipa) return false;
+  for (int i = first; i < first + count; i++) {
+    const ksg_pod& p = ctx->h_pods[i];
+    if ((pts && p.pts >= 0) || (ipa && p.ipa >= 0)) return true;
+  }
+  return false;
+}
+
+int launch_queue(ksg_ctx* ctx, QueueArgs& a, int n_replicas, int block, bool topo) {
   (void)hipGetLastError();
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-  if (block == 1024)
-    hipLaunchKernelGGL(ksg_queue_kernel<1024>, dim3(n_replicas), dim3(1024), 0, ctx->stream, a);
-  else if (block == 512)
-    hipLaunchKernelGGL(ksg_queue_kernel<512>, dim3(n_replicas), dim3(512), 0, ctx->stream, a);
-  else
-    hipLaunchKernelGGL(ksg_queue_kernel<256>, dim3(n_replicas), dim3(256), 0, ctx->stream, a);
+  if (topo) {
+    if (block == 1024)
+      hipLaunchKernelGGL(ksg_queue_topo_kernel<1024>, dim3(n_replicas), dim3(1024), 0, ctx->stream, a);
+    else if (block == 512)
+      hipLaunchKernelGGL(ksg_queue_topo_kernel<512>, dim3(n_replicas), dim3(512), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL(ksg_queue_topo_kernel<256>, dim3(n_replicas), dim3(256), 0, ctx->stream, a);
+  } else {
+    if (block == 1024)
+      hipLaunchKernelGGL(ksg_queue_kernel<1024>, dim3(n_replicas), dim3(1024), 0, ctx->stream, a);
+    else if (block == 512)
+      hipLaunchKernelGGL(ksg_queue_kernel<512>, dim3(n_replicas), dim3(512), 0, ctx->stream, a);
+    else
+      hipLaunchKernelGGL(ksg_queue_kernel<256>, dim3(n_replicas), dim3(256), 0, ctx->stream, a);
+  }
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   return KSG_OK;
@@ -529,29 +962,58 @@ int check_ready(ksg_ctx* ctx) {
   return KSG_OK;
 }
 
-bool profile_has(const ksg_profile& prof, int pl) {
-  if ((prof.score_mask >> pl) & 1u) return true;
-  for (int k = 0; k < prof.n_filter; k++)
-    if (prof.filter_order[k] == pl) return true;
-  return false;
+// Host mirror of layout_slots(): words of LDS histograms a pod needs.
+int topo_words(ksg_ctx* ctx, const ksg_pod& p, bool pts, bool ipa) {
+  const std::vector<int32_t>& P = ctx->h_prog;
+  int words = 0;
+  auto slot = [&](int col, bool mark) {
+    if (col < 0 || col >= std::max(ctx->c.L, 1)) { words = 1 << 30; return; }
+    if (ctx->h_col_unique[col]) return;
+    const int V = ctx->h_col_vocab[col];
+    words += V + (V + 31) / 32 * (mark ? 2 : 1);
+  };
+  if (pts && p.pts >= 0) {
+    const int nh = P[p.pts], ns = P[p.pts + 1];
+    if (nh > ksg::kMaxHard || ns > ksg::kMaxSoft) return 1 << 30;
+    for (int i = 0; i < nh; i++) slot(P[p.pts + 3 + 7 * i], false);
+    for (int i = 0; i < ns; i++) slot(P[p.pts + 3 + 7 * nh + 6 * i], true);
+  }
+  if (ipa && p.ipa >= 0) {
+    size_t w = p.ipa;
+    const int na = P[w];
+    if (na > ksg::kMaxAff) return 1 << 30;
+    for (int i = 0; i < na; i++) slot(P[w + 3 + i], false);
+    w += 3 + na;
+    const int nn = P[w++];
+    if (nn > ksg::kMaxAnti) return 1 << 30;
+    for (int i = 0; i < nn; i++) slot(P[w + 2 * i], false);
+    w += 2 * nn;
+    const int np = P[w++];
+    if (np > ksg::kMaxPref) return 1 << 30;
+    for (int i = 0; i < np; i++) slot(P[w + 3 * i], false);
+  }
+  return words;
 }
 
-// PodTopologySpread / InterPodAffinity terms are not implemented in this
-// build: refuse pods that need them instead of computing something else.
+// Refuse inputs outside what the kernels implement instead of computing
+// something else.
 int check_supported(ksg_ctx* ctx, const ksg_profile& prof, int first, int count) {
   const bool pts = profile_has(prof, KSG_PL_POD_TOPOLOGY_SPREAD), ipa = profile_has(prof, KSG_PL_INTER_POD_AFFINITY);
+  if (!pts && !ipa) return KSG_OK;
   for (int i = first; i < first + count; i++) {
     const ksg_pod& p = ctx->h_pods[i];
-    if ((pts && p.pts >= 0) || (ipa && p.ipa >= 0))
-      return fail(ctx, KSG_E_UNSUPPORTED, "PodTopologySpread/InterPodAffinity terms are not implemented in this build");
+    if (topo_words(ctx, p, pts, ipa) > KSG_HIST_MAX)
+      return fail(ctx, KSG_E_UNSUPPORTED,
+                  "pod " + std::to_string(i) + ": topology terms exceed the LDS histogram budget");
   }
   return KSG_OK;
 }
 
-// The batched path packs raw scores into 8-byte records; use it only when the
-// values provably fit.
+// The batched path covers node-local plugins only and packs raw scores into
+// 8-byte records; use it only when the values provably fit.
 bool batch_eligible(ksg_ctx* ctx, int first, int count) {
   const ksg_profile& prof = ctx->prof;
+  if (needs_topo(ctx, prof, first, count)) return false;
   if (ctx->c.T > 255) return false;
   if (ctx->c.N > (1 << 19)) return false;   // changed-node bitmap must fit LDS
   int64_t wsum = 0;
@@ -668,7 +1130,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     a.placements = d_pl;
     a.results = d_res;
     const int block = N >= 2048 ? 1024 : (N >= 512 ? 512 : 256);
-    if ((rc = launch_queue(ctx, a, 1, block))) return rc;
+    if ((rc = launch_queue(ctx, a, 1, block, needs_topo(ctx, ctx->prof, first, count)))) return rc;
   }
   if (placements) HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * count, hipMemcpyDeviceToHost, ctx->stream));
   if (results) HIPC(ctx, hipMemcpyAsync(results, d_res, sizeof(ksg_result) * count, hipMemcpyDeviceToHost, ctx->stream));
@@ -779,6 +1241,8 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
   UP(tmpl_weight, tp->tmpl_weight, nt);
   UP(col_vocab, tp->col_vocab, L);
   UP(col_unique, tp->col_unique, L);
+  ctx->h_col_vocab.assign(tp->col_vocab, tp->col_vocab + L);
+  ctx->h_col_unique.assign(tp->col_unique, tp->col_unique + L);
   UP(log_table, tp->log_table, tp->log_n);
   c.log_n = tp->log_n;
   std::vector<int32_t> off(nt, 0);
@@ -828,6 +1292,7 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
       return fail(ctx, KSG_E_INVALID, "node set outside the program pool");
     ctx->h_na_pref_sum[i] = na_pref_weight_sum(prog, p.na_pref);
   }
+  ctx->h_prog = std::move(prog);
   int rc;
   if ((rc = upload(ctx, &ctx->d_pods, wl->pods, std::max(wl->n_pods, 1)))) return rc;
   if ((rc = upload(ctx, &ctx->d_prog, wl->prog, (size_t)std::max<int64_t>(wl->prog_len, 1)))) return rc;
@@ -905,7 +1370,9 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   a.placements = d_pl;
   a.results = nullptr;
   const int block = N >= 8192 ? 512 : 256;
-  if ((rc = launch_queue(ctx, a, (int)RR, block))) return rc;
+  bool topo = false;
+  for (size_t r = 0; r < RR && !topo; r++) topo = needs_topo(ctx, profiles[r], first, count);
+  if ((rc = launch_queue(ctx, a, (int)RR, block, topo))) return rc;
   ctx->last_path = 1;
   HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * RR * count, hipMemcpyDeviceToHost, ctx->stream));
   std::vector<int64_t> req;

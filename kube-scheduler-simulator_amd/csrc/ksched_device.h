@@ -161,23 +161,55 @@ __device__ __forceinline__ int64_t taint_score(const DevCluster& c, const int32_
   return k;
 }
 
-__device__ __forceinline__ uint32_t fit_filter(const DevCluster& c, const ksg_pod& p, const int64_t* requested,
-                                               int32_t pod_count, uint32_t ignored, int n) {
+// A node's resource columns, gathered with independent loads up front so
+// their latencies overlap (the plugin code below branches on them).
+struct NodeCols {
+  int64_t alloc[KSG_MAX_RES];
+  int64_t req[KSG_MAX_RES];     // NodeInfo.Requested
+  int64_t nz_cpu, nz_mem;       // NodeInfo.NonZeroRequested
+  int32_t pod_count, allowed;
+};
+
+__device__ __forceinline__ void load_cols(const DevCluster& c, const int64_t* requested, const int64_t* nonzero,
+                                          const int32_t* pod_count, int n, NodeCols& L) {
+  const size_t N = c.N;
+#pragma unroll
+  for (int r = 0; r < KSG_MAX_RES; r++) {
+    L.alloc[r] = r < c.R ? c.alloc[r * N + n] : 0;
+    L.req[r] = r < c.R ? requested[r * N + n] : 0;
+  }
+  L.nz_cpu = nonzero[n];
+  L.nz_mem = nonzero[N + n];
+  L.pod_count = pod_count[n];
+  L.allowed = c.allowed[n];
+}
+
+// a[r] for a runtime r without dynamic register indexing (keeps a[] in VGPRs)
+__device__ __forceinline__ int64_t pick(const int64_t (&a)[KSG_MAX_RES], int r) {
+  int64_t v = a[0];
+#pragma unroll
+  for (int i = 1; i < KSG_MAX_RES; i++) v = r == i ? a[i] : v;
+  return v;
+}
+
+// noderesources.fitsRequest: bit0 pods, bit(r+1) resource column r
+__device__ __forceinline__ uint32_t fit_filter(const DevCluster& c, const ksg_pod& p, const NodeCols& L,
+                                               uint32_t ignored) {
   uint32_t bits = 0;
-  if ((int64_t)pod_count + 1 > (int64_t)c.allowed[n]) bits |= 1u;
-  for (int r = 0; r < c.R; r++) {
+  if ((int64_t)L.pod_count + 1 > (int64_t)L.allowed) bits |= 1u;
+#pragma unroll
+  for (int r = 0; r < KSG_MAX_RES; r++) {
+    if (r >= c.R) break;
     const int64_t q = p.req[r];
     if (q <= 0) continue;
     if (r >= 3 && ((ignored >> r) & 1u)) continue;
-    const int64_t a = c.alloc[(size_t)r * c.N + n], u = requested[(size_t)r * c.N + n];
-    if (q > a - u) bits |= 1u << (r + 1);
+    if (q > L.alloc[r] - L.req[r]) bits |= 1u << (r + 1);
   }
   return bits;
 }
 
 // resourceAllocationScorer.calculateResourceAllocatableRequest
-__device__ __forceinline__ void alloc_req(const DevCluster& c, const ksg_pod& p, const int64_t* requested,
-                                          const int64_t* nonzero, int r, int n, bool use_requested,
+__device__ __forceinline__ void alloc_req(const ksg_pod& p, const NodeCols& L, int r, bool use_requested,
                                           int64_t& a, int64_t& q) {
   int64_t pr;
   if (use_requested) pr = p.req[r];
@@ -185,20 +217,19 @@ __device__ __forceinline__ void alloc_req(const DevCluster& c, const ksg_pod& p,
   a = 0;
   q = 0;
   if (pr == 0 && r >= 3) return;
-  a = c.alloc[(size_t)r * c.N + n];
+  a = pick(L.alloc, r);
   int64_t base;
-  if (!use_requested && r == KSG_RES_CPU) base = nonzero[n];
-  else if (!use_requested && r == KSG_RES_MEM) base = nonzero[(size_t)c.N + n];
-  else base = requested[(size_t)r * c.N + n];
+  if (!use_requested && r == KSG_RES_CPU) base = L.nz_cpu;
+  else if (!use_requested && r == KSG_RES_MEM) base = L.nz_mem;
+  else base = pick(L.req, r);
   q = base + pr;
 }
 
-__device__ __forceinline__ int64_t fit_score(const DevCluster& c, const ksg_profile& prof, const ksg_pod& p,
-                                             const int64_t* requested, const int64_t* nonzero, int n) {
+__device__ __forceinline__ int64_t fit_score(const ksg_profile& prof, const ksg_pod& p, const NodeCols& L) {
   int64_t num = 0, wsum = 0;
   for (int i = 0; i < prof.fit_n; i++) {
     int64_t a, q;
-    alloc_req(c, p, requested, nonzero, prof.fit_res[i], n, false, a, q);
+    alloc_req(p, L, prof.fit_res[i], false, a, q);
     if (a == 0) continue;
     int64_t s;
     if (prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : div_nonneg((a - q) * 100, a);
@@ -209,27 +240,36 @@ __device__ __forceinline__ int64_t fit_score(const DevCluster& c, const ksg_prof
   return wsum == 0 ? 0 : div_nonneg(num, wsum);
 }
 
-__device__ __forceinline__ int64_t ba_score(const DevCluster& c, const ksg_profile& prof, const ksg_pod& p,
-                                            const int64_t* requested, const int64_t* nonzero, int n) {
-  double fr[KSG_MAX_RES];
+// balancedResourceScorer, in Go's float64 operation order.  Fractions are
+// recomputed in the second pass instead of stored (no private-memory array).
+__device__ __forceinline__ int64_t ba_score(const ksg_profile& prof, const ksg_pod& p, const NodeCols& L) {
   int k = 0;
-  double total = 0.0;
+  double total = 0.0, f0 = 0.0, f1 = 0.0;
   for (int i = 0; i < prof.ba_n; i++) {
     int64_t a, q;
-    alloc_req(c, p, requested, nonzero, prof.ba_res[i], n, true, a, q);
+    alloc_req(p, L, prof.ba_res[i], true, a, q);
     if (a == 0) continue;
     double f = (double)q / (double)a;
     if (f > 1) f = 1;
     total += f;
-    fr[k++] = f;
+    if (k == 0) f0 = f;
+    else if (k == 1) f1 = f;
+    k++;
   }
   double sd = 0.0;
   if (k == 2) {
-    sd = fabs((fr[0] - fr[1]) / 2);
+    sd = fabs((f0 - f1) / 2);
   } else if (k > 2) {
     const double mean = total / (double)k;
     double sum = 0.0;
-    for (int i = 0; i < k; i++) sum = sum + (fr[i] - mean) * (fr[i] - mean);
+    for (int i = 0; i < prof.ba_n; i++) {
+      int64_t a, q;
+      alloc_req(p, L, prof.ba_res[i], true, a, q);
+      if (a == 0) continue;
+      double f = (double)q / (double)a;
+      if (f > 1) f = 1;
+      sum = sum + (f - mean) * (f - mean);
+    }
     sd = sqrt(sum / (double)k);
   }
   return (int64_t)((1 - sd) * (double)100);

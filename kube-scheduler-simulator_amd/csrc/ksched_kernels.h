@@ -52,8 +52,11 @@ struct PodView {
   int64_t w_fit, w_ba, w_img, w_t, w_a;
 };
 
+// topo = false: PodTopologySpread / InterPodAffinity reach this evaluator only
+// for pods without terms (host check), i.e. they Skip.  topo = true: the
+// topology kernel evaluates them (IPA Skip decided on the device).
 __device__ __forceinline__ PodView make_view(const DevCluster& c, const ksg_profile& prof, const ksg_pod& p,
-                                             const int32_t* P, const int32_t* gprog) {
+                                             const int32_t* P, const int32_t* gprog, bool topo = false) {
   PodView v;
   const int boff = p.blob;
   auto rb = [boff](int off) { return off < 0 ? -1 : off - boff; };
@@ -67,16 +70,277 @@ __device__ __forceinline__ PodView make_view(const DevCluster& c, const ksg_prof
   v.tolp = v.tolf + c.W;
   v.node_set = p.node_set >= 0 ? gprog + p.node_set : nullptr;
   v.reject = (p.flags & KSG_POD_PREFILTER_REJECT) != 0;
-  // PodTopologySpread / InterPodAffinity reach this evaluator only for pods
-  // without terms (host check), i.e. they Skip.
-  v.fskip = p.filter_skip | bit(KSG_PL_INTER_POD_AFFINITY) | bit(KSG_PL_POD_TOPOLOGY_SPREAD);
-  v.smask = prof.score_mask & ~p.score_skip & ~(bit(KSG_PL_INTER_POD_AFFINITY) | bit(KSG_PL_POD_TOPOLOGY_SPREAD));
+  if (topo) {
+    v.fskip = p.filter_skip;
+    v.smask = prof.score_mask & ~p.score_skip;
+  } else {
+    v.fskip = p.filter_skip | bit(KSG_PL_INTER_POD_AFFINITY) | bit(KSG_PL_POD_TOPOLOGY_SPREAD);
+    v.smask = prof.score_mask & ~p.score_skip & ~(bit(KSG_PL_INTER_POD_AFFINITY) | bit(KSG_PL_POD_TOPOLOGY_SPREAD));
+  }
   v.w_fit = prof.weight[KSG_PL_NODE_RESOURCES_FIT];
   v.w_ba = prof.weight[KSG_PL_BALANCED_ALLOCATION];
   v.w_img = prof.weight[KSG_PL_IMAGE_LOCALITY];
   v.w_t = prof.weight[KSG_PL_TAINT_TOLERATION];
   v.w_a = prof.weight[KSG_PL_NODE_AFFINITY];
   return v;
+}
+
+// ============================================================================
+// PodTopologySpread / InterPodAffinity.
+//
+// The upstream plugins rescan every pod on every node in each PreFilter /
+// PreScore [upstream podtopologyspread/filtering.go calPreFilterState,
+// scoring.go PreScore; interpodaffinity/filtering.go PreFilter, scoring.go
+// PreScore].  Here the scan is replaced by state maintained at assume time
+// (commit_node):
+//   cnt[s][n]      pods on node n matching selector s (namespace-scoped; one
+//                  selector id per distinct PTS selector, IPA term selector and
+//                  conjunction of a pod's required affinity terms)
+//   tab[t][v]      per-domain table of term template t owned by existing pods
+//                  (required anti-affinity / required affinity counts,
+//                  preferred (anti-)affinity weight sums)
+//   tmpl_total[t]  pods that contributed to template t
+// and, per pod, a pre-pass over nodes folds cnt[s][.] into per-domain counts:
+// directly per node when the topology column is unique (hostname), otherwise
+// through LDS histograms indexed by the column's value id.
+// ============================================================================
+constexpr int kMaxHard = 4, kMaxSoft = 4, kMaxAff = 4, kMaxAnti = 4, kMaxPref = 8;
+
+struct TopoProg {
+  int n_hard, n_soft, require_all;
+  const int32_t* hard;   // {col sel max_skew min_domains self_match na nt} x n_hard
+  const int32_t* soft;   // {col sel max_skew na nt is_hostname} x n_soft
+  int n_aff, sel_all, self_all;
+  const int32_t* aff_cols;
+  int n_anti;
+  const int32_t* anti;   // {col sel}
+  int n_pref;
+  const int32_t* pref;   // {col sel weight}
+  int n_ma, n_mh, n_mp;
+  const int32_t *m_anti, *m_hard, *m_pref;
+  bool pts_filter, pts_score, ipa;
+};
+
+// One LDS histogram slot: counts (V words) + presence bitmap + optional mark bitmap.
+struct Slot {
+  int col, sel, unique, V, hist, pres, mark;
+};
+
+struct TopoShared {
+  Slot hard[kMaxHard], soft[kMaxSoft], aff[kMaxAff], anti[kMaxAnti], pref[kMaxPref];
+  long long hard_min[kMaxHard];
+  int hard_dom[kMaxHard];
+  long long soft_empty[kMaxSoft];     // unique soft column: count of the "" domain
+  int soft_present[kMaxSoft];         // unique soft column: feasible non-ignored nodes with a value
+  int soft_empty_seen[kMaxSoft];
+  double soft_w[kMaxSoft];
+  int n_ignored;
+  long long aff_total;
+  int pref_any;
+  int ipa_skip_filter;                // InterPodAffinity PreFilter Skip
+  int ipa_skip_score;                 // InterPodAffinity PreScore Skip
+  int words;
+  int ok;
+};
+
+struct TopoCtx {
+  const TopoProg* g;
+  const TopoShared* s;
+  const int32_t* hist;   // LDS
+  const int32_t* cnt;    // replica's cnt[S][N]
+  const int32_t* tab;    // replica's template tables
+};
+
+__device__ __forceinline__ void parse_topo(const ksg_pod& p, const int32_t* P, uint32_t fskip, uint32_t smask,
+                                           TopoProg& g) {
+  g = TopoProg{};
+  const int boff = p.blob;
+  if (p.pts >= 0) {
+    const int32_t* w = P + (p.pts - boff);
+    g.n_hard = w[0];
+    g.n_soft = w[1];
+    g.require_all = w[2];
+    g.hard = w + 3;
+    g.soft = g.hard + 7 * g.n_hard;
+  }
+  g.pts_filter = g.n_hard > 0 && !((fskip >> KSG_PL_POD_TOPOLOGY_SPREAD) & 1u);
+  g.pts_score = g.n_soft > 0 && ((smask >> KSG_PL_POD_TOPOLOGY_SPREAD) & 1u);
+  if (p.ipa >= 0) {
+    const int32_t* w = P + (p.ipa - boff);
+    g.n_aff = w[0];
+    g.sel_all = w[1];
+    g.self_all = w[2];
+    g.aff_cols = w + 3;
+    w += 3 + g.n_aff;
+    g.n_anti = *w++;
+    g.anti = w;
+    w += 2 * g.n_anti;
+    g.n_pref = *w++;
+    g.pref = w;
+    w += 3 * g.n_pref;
+    g.n_ma = *w++;
+    g.m_anti = w;
+    w += g.n_ma;
+    g.n_mh = *w++;
+    g.m_hard = w;
+    w += g.n_mh;
+    g.n_mp = *w++;
+    g.m_pref = w;
+    g.ipa = true;
+  }
+}
+
+// One thread: lay out this pod's LDS histograms.
+__device__ __forceinline__ void layout_slots(const DevCluster& c, const TopoProg& g, TopoShared& s) {
+  int words = 0;
+  const bool ok = g.n_hard <= kMaxHard && g.n_soft <= kMaxSoft && g.n_aff <= kMaxAff && g.n_anti <= kMaxAnti &&
+                  g.n_pref <= kMaxPref;
+  auto mk = [&](Slot& sl, int col, int sel, bool need_mark) {
+    sl.col = col;
+    sl.sel = sel;
+    sl.unique = c.col_unique[col];
+    sl.V = c.col_vocab[col];
+    sl.hist = sl.pres = sl.mark = -1;
+    if (!sl.unique) {
+      sl.hist = words;
+      words += sl.V;
+      sl.pres = words;
+      words += (sl.V + 31) / 32;
+      if (need_mark) {
+        sl.mark = words;
+        words += (sl.V + 31) / 32;
+      }
+    }
+  };
+  if (ok) {
+    for (int i = 0; i < g.n_hard; i++) mk(s.hard[i], g.hard[7 * i], g.hard[7 * i + 1], false);
+    for (int i = 0; i < g.n_soft; i++) mk(s.soft[i], g.soft[6 * i], g.soft[6 * i + 1], true);
+    for (int i = 0; i < g.n_aff; i++) mk(s.aff[i], g.aff_cols[i], g.sel_all, false);
+    for (int i = 0; i < g.n_anti; i++) mk(s.anti[i], g.anti[2 * i], g.anti[2 * i + 1], false);
+    for (int i = 0; i < g.n_pref; i++) mk(s.pref[i], g.pref[3 * i], g.pref[3 * i + 1], false);
+  }
+  s.words = words;
+  s.ok = ok && words <= KSG_HIST_MAX;
+}
+
+__device__ __forceinline__ int32_t cnt_at(const int32_t* cnt, int N, int sel, int n) {
+  return sel < 0 ? 0 : cnt[(size_t)sel * N + n];
+}
+__device__ __forceinline__ uint32_t lab(const DevCluster& c, int col, int n) {
+  return c.label_val[(size_t)col * c.N + n];
+}
+__device__ __forceinline__ bool has_all(const DevCluster& c, const int32_t* cons, int ncons, int stride, int n) {
+  for (int i = 0; i < ncons; i++)
+    if (!lab(c, cons[stride * i], n)) return false;
+  return true;
+}
+// topologySpreadConstraint.matchNodeInclusionPolicies
+__device__ __forceinline__ bool inclusion(const DevCluster& c, const PodView& v, int na, int nt, int n) {
+  if (na && !na_required_match(c, v.P, v.na_req, n)) return false;
+  if (nt && untolerated_slot(c, v.tolf, n) >= 0) return false;
+  return true;
+}
+__device__ __forceinline__ bool bit_get(const int32_t* h, int base, uint32_t v) {
+  return ((((uint32_t)h[base + (v >> 5)]) >> (v & 31)) & 1u) != 0;
+}
+// count in the domain of node n for a non-unique slot (0 when the domain is absent)
+__device__ __forceinline__ int64_t hist_at(const int32_t* h, const Slot& sl, uint32_t v) {
+  return bit_get(h, sl.pres, v) ? (int64_t)h[sl.hist + v] : 0;
+}
+
+// PodTopologySpread.Filter: 0 pass, 1 missing required label, 2 skew.
+__device__ __forceinline__ uint32_t pts_filter_node(const DevCluster& c, const PodView& v, const TopoCtx& t, int n) {
+  const TopoProg& g = *t.g;
+  const TopoShared& s = *t.s;
+  const bool all = has_all(c, g.hard, g.n_hard, 7, n);
+  for (int i = 0; i < g.n_hard; i++) {
+    const int32_t* h = g.hard + 7 * i;
+    const uint32_t val = lab(c, h[0], n);
+    if (!val) return 1;
+    const Slot& sl = s.hard[i];
+    int64_t m;
+    if (sl.unique) m = (all && inclusion(c, v, h[5], h[6], n)) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
+    else m = hist_at(t.hist, sl, val);
+    if (m + h[4] - s.hard_min[i] > h[2]) return 2;
+  }
+  return 0;
+}
+
+// InterPodAffinity.Filter: 0 pass, 1 affinity, 2 anti-affinity, 3 existing pods' anti-affinity.
+__device__ __forceinline__ uint32_t ipa_filter_node(const DevCluster& c, const TopoCtx& t, int n) {
+  const TopoProg& g = *t.g;
+  const TopoShared& s = *t.s;
+  bool pods_exist = true;
+  for (int i = 0; i < g.n_aff; i++) {
+    const Slot& sl = s.aff[i];
+    const uint32_t val = lab(c, sl.col, n);
+    if (!val) return 1;
+    const int64_t m = sl.unique ? cnt_at(t.cnt, c.N, g.sel_all, n) : hist_at(t.hist, sl, val);
+    if (m <= 0) pods_exist = false;
+  }
+  if (!pods_exist && !(s.aff_total == 0 && g.n_aff > 0 && g.self_all)) return 1;
+  for (int i = 0; i < g.n_anti; i++) {
+    const Slot& sl = s.anti[i];
+    const uint32_t val = lab(c, sl.col, n);
+    if (!val) continue;
+    const int64_t m = sl.unique ? cnt_at(t.cnt, c.N, sl.sel, n) : hist_at(t.hist, sl, val);
+    if (m > 0) return 2;
+  }
+  for (int i = 0; i < g.n_ma; i++) {
+    const int tm = g.m_anti[i];
+    const uint32_t val = lab(c, c.tmpl_col[tm], n);
+    if (val && t.tab[c.tmpl_off[tm] + val] > 0) return 3;
+  }
+  return 0;
+}
+
+// PodTopologySpread.Score; -1 for IgnoredNodes.
+__device__ __forceinline__ int64_t pts_score_node(const DevCluster& c, const PodView& v, const TopoCtx& t, int n) {
+  const TopoProg& g = *t.g;
+  const TopoShared& s = *t.s;
+  if (g.require_all && !has_all(c, g.soft, g.n_soft, 6, n)) return -1;
+  double score = 0.0;
+  for (int i = 0; i < g.n_soft; i++) {
+    const int32_t* sc = g.soft + 6 * i;
+    const uint32_t val = lab(c, sc[0], n);
+    if (!val) continue;
+    const Slot& sl = s.soft[i];
+    int64_t m;
+    if (sc[5]) m = cnt_at(t.cnt, c.N, sl.sel, n);                    // hostname: this node's pods
+    else if (!sl.unique) m = t.hist[sl.hist + val];
+    else if (val == 1) m = s.soft_empty[i];
+    else m = inclusion(c, v, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
+    const double x = (double)m * s.soft_w[i];
+    score += x + (double)(sc[2] - 1);
+  }
+  return (int64_t)round(score);
+}
+
+// InterPodAffinity.Score
+__device__ __forceinline__ int64_t ipa_score_node(const DevCluster& c, const ksg_profile& prof, const TopoCtx& t,
+                                                  int n) {
+  const TopoProg& g = *t.g;
+  const TopoShared& s = *t.s;
+  int64_t sc = 0;
+  for (int i = 0; i < g.n_pref; i++) {
+    const Slot& sl = s.pref[i];
+    const uint32_t val = lab(c, sl.col, n);
+    if (!val) continue;
+    const int64_t m = sl.unique ? cnt_at(t.cnt, c.N, sl.sel, n) : hist_at(t.hist, sl, val);
+    sc += (int64_t)g.pref[3 * i + 2] * m;
+  }
+  if (prof.hard_pod_affinity_weight > 0)
+    for (int i = 0; i < g.n_mh; i++) {
+      const int tm = g.m_hard[i];
+      const uint32_t val = lab(c, c.tmpl_col[tm], n);
+      if (val) sc += (int64_t)prof.hard_pod_affinity_weight * t.tab[c.tmpl_off[tm] + val];
+    }
+  for (int i = 0; i < g.n_mp; i++) {
+    const int tm = g.m_pref[i];
+    const uint32_t val = lab(c, c.tmpl_col[tm], n);
+    if (val) sc += t.tab[c.tmpl_off[tm] + val];
+  }
+  return sc;
 }
 
 struct NodeEval {
@@ -90,10 +354,13 @@ struct NodeEval {
 // enabled score plugin, for one (pod, node).  craw/cnorm: optional capture rows.
 __device__ __forceinline__ NodeEval eval_node(const DevCluster& c, const ksg_profile& prof, const PodView& v,
                                               const int64_t* requested, const int64_t* nonzero,
-                                              const int32_t* pod_count, int n, int64_t* craw, int64_t* cnorm) {
+                                              const int32_t* pod_count, int n, int64_t* craw, int64_t* cnorm,
+                                              const TopoCtx* tc = nullptr) {
   const ksg_pod& p = *v.p;
   const int N = c.N;
   NodeEval e{0, 0, 0, 0};
+  NodeCols L;
+  load_cols(c, requested, nonzero, pod_count, n, L);
   uint32_t st = 0;
   if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) {
     st = KSG_FS_NOT_EVALUATED;
@@ -117,10 +384,22 @@ __device__ __forceinline__ NodeEval eval_node(const DevCluster& c, const ksg_pro
           if (!na_required_match(c, v.P, v.na_req, n)) st = (uint32_t)(pl + 1) | (1u << 8);
           break;
         case KSG_PL_NODE_RESOURCES_FIT: {
-          const uint32_t b = fit_filter(c, p, requested, pod_count[n], prof.fit_ignored_res, n);
+          const uint32_t b = fit_filter(c, p, L, prof.fit_ignored_res);
           if (b) st = (uint32_t)(pl + 1) | (b << 8);
           break;
         }
+        case KSG_PL_POD_TOPOLOGY_SPREAD:
+          if (tc && tc->g->pts_filter) {
+            const uint32_t r = pts_filter_node(c, v, *tc, n);
+            if (r) st = (uint32_t)(pl + 1) | (r << 8);
+          }
+          break;
+        case KSG_PL_INTER_POD_AFFINITY:
+          if (tc && tc->g->ipa) {
+            const uint32_t r = ipa_filter_node(c, *tc, n);
+            if (r) st = (uint32_t)(pl + 1) | (r << 8);
+          }
+          break;
         default:
           break;
       }
@@ -129,12 +408,12 @@ __device__ __forceinline__ NodeEval eval_node(const DevCluster& c, const ksg_pro
   e.st = st;
   if (st != 0) return e;
   if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) {
-    const int64_t s = fit_score(c, prof, p, requested, nonzero, n);
+    const int64_t s = fit_score(prof, p, L);
     e.part += s * v.w_fit;
     if (craw) { craw[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = s; cnorm[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = s; }
   }
   if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) {
-    const int64_t s = ba_score(c, prof, p, requested, nonzero, n);
+    const int64_t s = ba_score(prof, p, L);
     e.part += s * v.w_ba;
     if (craw) { craw[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; cnorm[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; }
   }

@@ -40,7 +40,9 @@ CASES = [
     ("c5-small", lambda: G.config5(n_nodes=400, n_pods=300, n_images=200, taint_vocab=128,
                                    taints_per_node=16, images_per_node=20)),
     ("readme-kat", G.readme_kat),
-]
+    ("c3-60x400", lambda: G.config3(n_nodes=60, n_pods=400, apps=12, zones=4)),
+    ("c3-600x3000", lambda: G.config3(n_nodes=600, n_pods=3000, apps=40, zones=8)),
+] + [(f"zoo-{s}", (lambda s=s: __import__("zoo").zoo(s))) for s in range(8)]
 
 
 @pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
@@ -77,6 +79,15 @@ def test_placement_queue_matches_oracle(gpu, oracle, name, make):
     p1, _ = gpu.run_queue(0, half)
     p2, _ = gpu.run_queue(half, len(pods) - half)
     np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
+
+
+@pytest.mark.parametrize("seed", [0, 3, 5])
+def test_zoo_annotation_bytes_gpu_vs_pyoracle(gpu, seed):
+    from zoo import zoo
+    nodes, pods, prof = zoo(seed, n_pods=80)
+    want, _ = pyoracle_annotations(nodes, pods, prof)
+    got = scheduler_annotations(nodes, pods, prof, gpu)
+    assert want == got
 
 
 def test_annotations_bytes_gpu_vs_pyoracle(gpu):

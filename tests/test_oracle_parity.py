@@ -39,3 +39,24 @@ def test_readme_kat_annotation_bytes():
     assert got[A.SELECTED_NODE] == "node-282x7"
     assert got[A.BIND] == '{"DefaultBinder":"success"}'
     assert got[A.RESERVE] == '{"VolumeBinding":"success"}'
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_zoo_annotations_pyoracle_vs_oracle(seed):
+    """Randomised edge-case workloads (tests/zoo.py): every byte of every
+    annotation from the C++ oracle equals the pure-Python restatement."""
+    import binding
+    from zoo import zoo
+    nodes, pods, prof = zoo(seed)
+    want, _ = pyoracle_annotations(nodes, pods, prof)
+    got = scheduler_annotations(nodes, pods, prof, binding.Oracle(2))
+    for i, (w, g) in enumerate(zip(want, got)):
+        assert w == g, f"zoo seed {seed}: pod {i} annotations differ"
+
+
+def test_config3_small_annotations():
+    import binding
+    nodes, pods, prof = G.config3(n_nodes=40, n_pods=200, apps=10, zones=4)
+    want, _ = pyoracle_annotations(nodes, pods, prof)
+    got = scheduler_annotations(nodes, pods, prof, binding.Oracle(2))
+    assert want == got

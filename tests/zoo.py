@@ -1,0 +1,152 @@
+"""Randomised small workloads that exercise the edge cases of every plugin:
+hard and soft PodTopologySpread on zone / hostname / region, minDomains,
+nodeAffinityPolicy / nodeTaintsPolicy, matchLabelKeys, system-default
+spreading, InterPodAffinity required / preferred terms both ways, namespaces
+and namespace selectors, node selectors with Gt/Lt/NotIn/DoesNotExist,
+matchFields, nodes without labels, unschedulable nodes, NoExecute taints,
+nodeName, init containers and sidecars, scalar resources, images."""
+import numpy as np
+
+from conftest import pkg
+
+m = pkg("model")
+P = pkg("profile")
+
+GI = 1024 ** 3
+MI = 1024 ** 2
+
+
+def _sel(rng, apps):
+    k = int(rng.integers(4))
+    if k == 0:
+        return m.LabelSelector(match_labels=(("app", f"a{int(rng.integers(apps))}"),))
+    if k == 1:
+        return m.LabelSelector(match_expressions=(m.Requirement("app", m.IN, tuple(
+            f"a{int(x)}" for x in rng.integers(0, apps, size=2))),))
+    if k == 2:
+        return m.LabelSelector(match_labels=(("tier", "web"),),
+                               match_expressions=(m.Requirement("app", m.EXISTS),))
+    return m.LabelSelector(match_expressions=(m.Requirement("app", m.NOT_IN, (f"a{int(rng.integers(apps))}",)),))
+
+
+def zoo(seed: int, n_nodes: int = 24, n_pods: int = 160, apps: int = 5, zones: int = 3):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = []
+    for i in range(n_nodes):
+        labels = {m.LABEL_HOSTNAME: f"n{i}", "rank": str(int(rng.integers(0, 20)))}
+        if rng.random() > 0.1:
+            labels[m.LABEL_ZONE] = f"z{int(rng.integers(zones))}"
+        if rng.random() > 0.3:
+            labels[m.LABEL_REGION] = f"r{int(rng.integers(2))}"
+        if rng.random() < 0.05:
+            labels = {}
+        taints = []
+        u = rng.random()
+        if u < 0.15:
+            taints.append(m.Taint("dedicated", "gpu", m.NO_SCHEDULE))
+        elif u < 0.25:
+            taints.append(m.Taint("flaky", "", m.NO_EXECUTE))
+        if rng.random() < 0.3:
+            taints.append(m.Taint("spot", "true", m.PREFER_NO_SCHEDULE))
+        alloc = {m.CPU: int(rng.choice([2000, 4000, 8000])), m.MEMORY: int(rng.choice([4, 8, 16])) * GI,
+                 m.EPHEMERAL: 20 * GI, m.PODS: int(rng.choice([8, 16, 110]))}
+        if rng.random() < 0.3:
+            alloc["example.com/fpga"] = int(rng.integers(1, 4))
+        images = []
+        if rng.random() < 0.6:
+            images.append(m.ImageState(("registry/app:v1",), int(rng.integers(50, 900)) * MI))
+        if rng.random() < 0.3:
+            images.append(m.ImageState(("registry/db:v2", "registry/db@sha256:x"), 600 * MI))
+        nodes.append(m.Node(name=f"n{i}", labels=labels, taints=taints, allocatable=alloc,
+                            unschedulable=bool(rng.random() < 0.05), images=images))
+    pods = []
+    for j in range(n_pods):
+        ns = "default" if rng.random() < 0.8 else "other"
+        app = f"a{int(rng.integers(apps))}"
+        labels = {"app": app}
+        if rng.random() < 0.5:
+            labels["tier"] = "web"
+        req = {}
+        if rng.random() > 0.1:
+            req = {m.CPU: int(rng.choice([100, 250, 500, 1000])), m.MEMORY: int(rng.choice([256, 512, 1024])) * MI}
+        if rng.random() < 0.1:
+            req["example.com/fpga"] = 1
+        if rng.random() < 0.1:
+            req[m.EPHEMERAL] = GI
+        conts = [m.Container(image=str(rng.choice(["registry/app:v1", "registry/app", "registry/db:v2"])),
+                             requests=req)]
+        inits = []
+        if rng.random() < 0.1:
+            inits.append(m.Container(image="busybox", requests={m.CPU: 1500}))
+        if rng.random() < 0.05:
+            inits.append(m.Container(image="registry/db:v2", requests={m.MEMORY: 64 * MI}, restartable=True))
+        p = m.Pod(name=f"p{j}", namespace=ns, labels=labels, containers=conts, init_containers=inits)
+        if rng.random() < 0.15:
+            p.tolerations.append(m.Toleration("dedicated", m.OP_EQUAL, "gpu", m.NO_SCHEDULE))
+        if rng.random() < 0.1:
+            p.tolerations.append(m.Toleration("", m.OP_EXISTS))
+        if rng.random() < 0.1:
+            p.tolerations.append(m.Toleration("spot", m.OP_EXISTS, "", m.PREFER_NO_SCHEDULE))
+        if rng.random() < 0.05:
+            p.tolerations.append(m.Toleration(m.TAINT_NODE_UNSCHEDULABLE, m.OP_EXISTS, "", m.NO_SCHEDULE))
+        if rng.random() < 0.1:
+            p.node_selector = {m.LABEL_REGION: f"r{int(rng.integers(2))}"}
+        if rng.random() < 0.15:
+            op = rng.choice([m.GT, m.LT, m.NOT_IN, m.DOES_NOT_EXIST, m.IN])
+            if op in (m.GT, m.LT):
+                r = m.Requirement("rank", str(op), (str(int(rng.integers(0, 20))),))
+            elif op == m.DOES_NOT_EXIST:
+                r = m.Requirement(m.LABEL_REGION, m.DOES_NOT_EXIST)
+            else:
+                r = m.Requirement(m.LABEL_ZONE, str(op), (f"z{int(rng.integers(zones))}",))
+            terms = [m.NodeSelectorTerm(match_expressions=(r,))]
+            if rng.random() < 0.3:
+                terms.append(m.NodeSelectorTerm(match_fields=(m.Requirement(
+                    m.OBJECT_NAME_FIELD, m.IN, (f"n{int(rng.integers(n_nodes))}",)),)))
+            p.node_affinity_required = terms
+        if rng.random() < 0.15:
+            p.node_affinity_preferred = [m.PreferredSchedulingTerm(int(rng.integers(1, 100)), m.NodeSelectorTerm(
+                match_expressions=(m.Requirement(m.LABEL_ZONE, m.IN, (f"z{int(rng.integers(zones))}",)),)))]
+        if rng.random() < 0.03:
+            p.node_name = f"n{int(rng.integers(n_nodes))}"
+        # PodTopologySpread
+        u = rng.random()
+        if u < 0.35:
+            cons = []
+            for _ in range(int(rng.integers(1, 3))):
+                key = str(rng.choice([m.LABEL_ZONE, m.LABEL_HOSTNAME, m.LABEL_REGION]))
+                when = m.DO_NOT_SCHEDULE if rng.random() < 0.5 else m.SCHEDULE_ANYWAY
+                cons.append(m.TopologySpreadConstraint(
+                    int(rng.integers(1, 4)), key, when,
+                    m.LabelSelector(match_labels=(("app", app),)) if rng.random() < 0.8 else _sel(rng, apps),
+                    min_domains=int(rng.integers(1, 5)) if (when == m.DO_NOT_SCHEDULE and rng.random() < 0.3) else None,
+                    node_affinity_policy=m.POLICY_IGNORE if rng.random() < 0.2 else None,
+                    node_taints_policy=m.POLICY_HONOR if rng.random() < 0.3 else None,
+                    match_label_keys=("tier",) if rng.random() < 0.2 else ()))
+            p.topology_spread_constraints = cons
+        elif u < 0.45:
+            p.default_spread_selector = m.LabelSelector(match_labels=(("app", app),))
+        # InterPodAffinity
+        if rng.random() < 0.15:
+            p.pod_affinity_required = [m.PodAffinityTerm(_sel(rng, apps), str(rng.choice(
+                [m.LABEL_ZONE, m.LABEL_HOSTNAME])))]
+        if rng.random() < 0.15:
+            t = m.PodAffinityTerm(m.LabelSelector(match_labels=(("app", app),)), m.LABEL_HOSTNAME,
+                                  namespaces=("default", "other") if rng.random() < 0.3 else ())
+            p.pod_anti_affinity_required = [t]
+        if rng.random() < 0.2:
+            p.pod_affinity_preferred = [m.WeightedPodAffinityTerm(int(rng.integers(1, 100)), m.PodAffinityTerm(
+                _sel(rng, apps), m.LABEL_ZONE,
+                namespace_selector=m.LabelSelector() if rng.random() < 0.3 else None))]
+        if rng.random() < 0.2:
+            p.pod_anti_affinity_preferred = [m.WeightedPodAffinityTerm(int(rng.integers(1, 100)), m.PodAffinityTerm(
+                m.LabelSelector(match_labels=(("app", app),)), str(rng.choice([m.LABEL_ZONE, m.LABEL_HOSTNAME]))))]
+        pods.append(p)
+    prof = P.default_profile()
+    if seed % 3 == 1:
+        prof.fit_strategy = P.MOST_ALLOCATED
+        prof.fit_resources = [(m.CPU, 2), (m.MEMORY, 1), ("example.com/fpga", 3)]
+        prof.ba_resources = [(m.CPU, 1), (m.MEMORY, 1), (m.EPHEMERAL, 1)]
+    if seed % 4 == 2:
+        prof.hard_pod_affinity_weight = 5
+    return nodes, pods, prof
