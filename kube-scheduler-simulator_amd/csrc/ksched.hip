@@ -209,6 +209,7 @@ struct BatchArgs {
   const ksg_profile* prof;
   int32_t b0, nb;           // batch = pods [b0, b0 + nb)
   int32_t out0;             // output index of pod b0
+  int32_t prog_lo, prog_len;  // program range covering the batch's blobs
   uint64_t* rec;            // [KSG_BATCH_MAX][N] packed phase-1 records
   int32_t* pmax;            // [KSG_BATCH_MAX][2] phase-1 maxima (taint, node affinity)
   int32_t* placements;
@@ -254,15 +255,21 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
   }
 }
 
+// Phase 2: one workgroup walks the batch in queue order.  The batch's pod
+// records and program range are preloaded into LDS in one coalesced copy;
+// each pod's phase-1 records are prefetched into registers while the changed
+// nodes are re-evaluated, so a pod costs one re-evaluation latency plus three
+// barriers.
+constexpr int kRPT = 10;  // phase-1 records held in registers per lane (N <= 5120 at 512 lanes)
+
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
   constexpr int NW = BLOCK / 64;
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_cmask[];   // changed-node bitmap, N bits
-  __shared__ int32_t s_blob[KSG_BLOB_MAX];
-  __shared__ ksg_pod s_pod;
+  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
   __shared__ ksg_profile s_prof;
   __shared__ int32_t s_clist[KSG_BATCH_MAX];
   __shared__ NodeEval s_ce[KSG_BATCH_MAX];
+  __shared__ int32_t s_pmax[2 * KSG_BATCH_MAX];
   __shared__ int32_t s_nc;
   __shared__ Red s_red[NW];
   __shared__ uint64_t s_best[NW];
@@ -274,53 +281,85 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
   int64_t* requested = a.st.requested;
   int64_t* nonzero = a.st.nonzero;
   int32_t* pod_count = a.st.pod_count;
-  const int words = (N + 31) / 32;
-  for (int i = tid; i < words; i += BLOCK) s_cmask[i] = 0;
-  if (tid == 0) s_nc = 0;
+  const int cm_words = (((N + 31) / 32) + 3) & ~3;
+  constexpr int POD_WORDS = sizeof(ksg_pod) / 4;
+  uint32_t* s_cmask = reinterpret_cast<uint32_t*>(s_dyn);
+  ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
+  int32_t* s_prog = s_dyn + cm_words + a.nb * POD_WORDS;
+
+  for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
+  for (int i = tid; i < a.nb * POD_WORDS; i += BLOCK)
+    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
+  for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
+  for (int i = tid; i < 2 * a.nb; i += BLOCK) s_pmax[i] = a.pmax[i];
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  if (tid == 0) s_nc = 0;
+
+  uint64_t rr[kRPT];
+  auto prefetch = [&](int j) {
+    const uint64_t* rec = a.rec + (size_t)j * N;
+#pragma unroll
+    for (int q = 0; q < kRPT; q++) {
+      const int n = tid + q * BLOCK;
+      rr[q] = n < N ? rec[n] : 0;
+    }
+  };
+  prefetch(0);
+  __syncthreads();
 
   for (int j = 0; j < a.nb; j++) {
-    const int pi = a.b0 + j;
-    __syncthreads();
-    stage_pod<BLOCK>(a.pods, a.prog, pi, &s_pod, s_blob);
-    __syncthreads();
-    const ksg_pod& p = s_pod;
+    const ksg_pod& p = s_pods[j];
     const ksg_profile& prof = s_prof;
-    const PodView v = make_view(c, prof, p, s_blob, a.prog);
+    const PodView v = make_view(c, prof, p, s_prog + (p.blob - a.prog_lo), a.prog);
     const int nc = s_nc;
     // re-evaluate the nodes assumed onto earlier in this batch, on live state
     for (int i = tid; i < nc; i += BLOCK)
       s_ce[i] = eval_node(c, prof, v, requested, nonzero, pod_count, s_clist[i], nullptr, nullptr);
     __syncthreads();
-    const int64_t mt1 = a.pmax[2 * j], ma1 = a.pmax[2 * j + 1];
+    const int64_t mt1 = s_pmax[2 * j], ma1 = s_pmax[2 * j + 1];
     const uint64_t* rec = a.rec + (size_t)j * N;
     Red r{0, 0, 0, 0x7fffffff};
     uint64_t best = 0;
     uint32_t err = 0;
-    for (int n = tid; n < N; n += BLOCK) {
-      if ((s_cmask[n >> 5] >> (n & 31)) & 1u) continue;
-      const uint64_t x = rec[n];
-      if (!(x >> 63)) continue;
+    auto visit = [&](uint64_t x, int n, int64_t mt, int64_t ma, bool stats) {
+      if (!(x >> 63)) return;
       const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
-      r.nfeas += 1;
-      r.minidx = min(r.minidx, n);
-      r.max_t = max(r.max_t, rt);
-      r.max_a = max(r.max_a, ra);
-      const uint64_t key = argmax_key(total_score(v, part, rt, ra, mt1, ma1, err, nullptr, nullptr), n);
+      if (stats) {
+        r.nfeas += 1;
+        r.minidx = min(r.minidx, n);
+        r.max_t = max(r.max_t, rt);
+        r.max_a = max(r.max_a, ra);
+      }
+      const uint64_t key = argmax_key(total_score(v, part, rt, ra, mt, ma, err, nullptr, nullptr), n);
       best = key > best ? key : best;
-    }
-    for (int i = tid; i < nc; i += BLOCK) {
-      const NodeEval e = s_ce[i];
-      if (e.st != 0) continue;
-      const int n = s_clist[i];
-      r.nfeas += 1;
-      r.minidx = min(r.minidx, n);
-      r.max_t = max(r.max_t, e.rt);
-      r.max_a = max(r.max_a, e.ra);
-      const uint64_t key = argmax_key(total_score(v, e.part, e.rt, e.ra, mt1, ma1, err, nullptr, nullptr), n);
-      best = key > best ? key : best;
-    }
+    };
+    auto visit_changed = [&](int64_t mt, int64_t ma, bool stats) {
+      for (int i = tid; i < nc; i += BLOCK) {
+        const NodeEval e = s_ce[i];
+        if (e.st != 0) continue;
+        const int n = s_clist[i];
+        if (stats) {
+          r.nfeas += 1;
+          r.minidx = min(r.minidx, n);
+          r.max_t = max(r.max_t, e.rt);
+          r.max_a = max(r.max_a, e.ra);
+        }
+        const uint64_t key = argmax_key(total_score(v, e.part, e.rt, e.ra, mt, ma, err, nullptr, nullptr), n);
+        best = key > best ? key : best;
+      }
+    };
+    auto scan = [&](int64_t mt, int64_t ma, bool stats) {
+#pragma unroll
+      for (int q = 0; q < kRPT; q++) {
+        const int n = tid + q * BLOCK;
+        if (n < N && !((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rr[q], n, mt, ma, stats);
+      }
+      for (int n = tid + kRPT * BLOCK; n < N; n += BLOCK)
+        if (!((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rec[n], n, mt, ma, stats);
+      visit_changed(mt, ma, stats);
+    };
+    scan(mt1, ma1, true);
     {
       Red w;
       w.max_t = wave_max64(r.max_t);
@@ -353,21 +392,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
       __syncthreads();
       best = 0;
       err = 0;
-      for (int n = tid; n < N; n += BLOCK) {
-        if ((s_cmask[n >> 5] >> (n & 31)) & 1u) continue;
-        const uint64_t x = rec[n];
-        if (!(x >> 63)) continue;
-        const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
-        const uint64_t key = argmax_key(total_score(v, part, rt, ra, g.max_t, g.max_a, err, nullptr, nullptr), n);
-        best = key > best ? key : best;
-      }
-      for (int i = tid; i < nc; i += BLOCK) {
-        const NodeEval e = s_ce[i];
-        if (e.st != 0) continue;
-        const uint64_t key =
-            argmax_key(total_score(v, e.part, e.rt, e.ra, g.max_t, g.max_a, err, nullptr, nullptr), s_clist[i]);
-        best = key > best ? key : best;
-      }
+      scan(g.max_t, g.max_a, false);
       best = wave_max_u64(best);
       err = wave_or32(err);
       if (lane == 0) { s_best[wv] = best; s_err[wv] = err; }
@@ -380,6 +405,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
         ge |= s_err[i];
       }
     }
+    if (j + 1 < a.nb) prefetch(j + 1);   // overlaps the commit barrier
     int selected = -1;
     uint32_t status = 0;
     if (g.nfeas == 1) {
@@ -394,15 +420,13 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
     if (tid == 0) {
       if (selected >= 0) {
         commit_node(c, requested, nonzero, pod_count, a.st.cnt, a.st.tab, a.st.tmpl_total, p,
-                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected);
+                    v.commit >= 0 ? v.P + v.commit : nullptr, selected);
         if (!((s_cmask[selected >> 5] >> (selected & 31)) & 1u)) {
           s_cmask[selected >> 5] |= 1u << (selected & 31);
           s_clist[s_nc] = selected;
           s_nc = s_nc + 1;
         }
       }
-      a.pmax[2 * j] = 0;   // ready for the next batch's phase 1
-      a.pmax[2 * j + 1] = 0;
       const int o = a.out0 + j;
       a.placements[o] = selected;
       if (a.results) {
@@ -414,7 +438,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
         a.results[o] = res;
       }
     }
+    __syncthreads();
   }
+  for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
 }
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
@@ -1072,15 +1098,43 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   b.pmax = ctx->d_pmax;
   b.placements = d_pl;
   b.results = d_res;
-  const size_t cmask_bytes = sizeof(uint32_t) * ((N + 31) / 32);
+  // Plan batches so that phase 2's LDS preload (changed-node bitmap + pod
+  // records + the program range of the batch) fits the dynamic LDS budget.
+  constexpr size_t kLdsBudget = 120 * 1024;
+  const size_t cm_bytes = 4 * (size_t)((((N + 31) / 32) + 3) & ~3);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBudget));
+    attr_set = true;
+  }
   (void)hipGetLastError();
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-  for (int off = 0; off < count; off += KSG_BATCH_MAX) {
+  for (int off = 0; off < count;) {
+    int nb = std::min(KSG_BATCH_MAX, count - off);
+    int64_t lo = 0, hi = 0;
+    size_t bytes = 0;
+    for (;;) {
+      lo = ctx->h_pods[first + off].blob;
+      hi = lo;
+      for (int k = 0; k < nb; k++) {
+        const ksg_pod& q = ctx->h_pods[first + off + k];
+        lo = std::min<int64_t>(lo, q.blob);
+        hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
+      }
+      bytes = cm_bytes + (size_t)nb * sizeof(ksg_pod) + 4 * (size_t)(hi - lo);
+      if (bytes <= kLdsBudget || nb == 1) break;
+      nb = std::max(1, nb / 2);
+    }
+    if (bytes > kLdsBudget) return fail(ctx, KSG_E_UNSUPPORTED, "batch does not fit the LDS budget");
     b.b0 = first + off;
     b.out0 = off;
-    b.nb = std::min(KSG_BATCH_MAX, count - off);
+    b.nb = nb;
+    b.prog_lo = (int32_t)lo;
+    b.prog_len = (int32_t)(hi - lo);
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, b);
-    hipLaunchKernelGGL(ksg_batch_phase2<1024>, dim3(1), dim3(1024), cmask_bytes, ctx->stream, b);
+    hipLaunchKernelGGL(ksg_batch_phase2<512>, dim3(1), dim3(512), bytes, ctx->stream, b);
+    off += nb;
   }
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
@@ -1129,7 +1183,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     a.profiles = d_prof;
     a.placements = d_pl;
     a.results = d_res;
-    const int block = N >= 2048 ? 1024 : (N >= 512 ? 512 : 256);
+    const int block = N >= 512 ? 512 : 256;   // 512 lanes: <= 256 VGPRs per lane, no spills
     if ((rc = launch_queue(ctx, a, 1, block, needs_topo(ctx, ctx->prof, first, count)))) return rc;
   }
   if (placements) HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * count, hipMemcpyDeviceToHost, ctx->stream));

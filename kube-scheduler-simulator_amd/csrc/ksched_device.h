@@ -184,12 +184,20 @@ __device__ __forceinline__ void load_cols(const DevCluster& c, const int64_t* re
   L.allowed = c.allowed[n];
 }
 
-// a[r] for a runtime r without dynamic register indexing (keeps a[] in VGPRs)
+// a[r] for a wave-uniform runtime r without dynamic register indexing (a
+// uniform branch per column keeps a[] in VGPRs; an indexed access would put
+// the whole array in scratch memory).
 __device__ __forceinline__ int64_t pick(const int64_t (&a)[KSG_MAX_RES], int r) {
-  int64_t v = a[0];
-#pragma unroll
-  for (int i = 1; i < KSG_MAX_RES; i++) v = r == i ? a[i] : v;
-  return v;
+  switch (r) {
+    case 0: return a[0];
+    case 1: return a[1];
+    case 2: return a[2];
+    case 3: return a[3];
+    case 4: return a[4];
+    case 5: return a[5];
+    case 6: return a[6];
+    default: return a[7];
+  }
 }
 
 // noderesources.fitsRequest: bit0 pods, bit(r+1) resource column r
