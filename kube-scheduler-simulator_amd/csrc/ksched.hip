@@ -210,6 +210,7 @@ struct BatchArgs {
   int32_t b0, nb;           // batch = pods [b0, b0 + nb)
   int32_t out0;             // output index of pod b0
   int32_t prog_lo, prog_len;  // program range covering the batch's blobs
+  unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
   uint64_t* rec;            // [KSG_BATCH_MAX][N] packed phase-1 records
   int32_t* pmax;            // [KSG_BATCH_MAX][2] phase-1 maxima (taint, node affinity)
   int32_t* placements;
@@ -260,6 +261,19 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
 // each pod's phase-1 records are prefetched into registers while the changed
 // nodes are re-evaluated, so a pod costs one re-evaluation latency plus three
 // barriers.
+// Diagnostic build (-DKSG_STAMPS): lane 0 of wave 0 sums s_memtime deltas per
+// segment of the phase-2 loop.  Never compiled into the measured library.
+#ifdef KSG_STAMPS
+#define KSG_STAMP(seg)                                                   \
+  do {                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();          \
+    if (tid == 0) { st_acc[seg] += _t - st_last; st_last = _t; }         \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+  } while (0)
+#else
+#define KSG_STAMP(seg) do {} while (0)
+#endif
 constexpr int kRPT = 10;  // phase-1 records held in registers per lane (N <= 5120 at 512 lanes)
 
 template <int BLOCK>
@@ -308,6 +322,10 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
   prefetch(0);
   __syncthreads();
 
+#ifdef KSG_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
+  KSG_STAMP(0);
   for (int j = 0; j < a.nb; j++) {
     const ksg_pod& p = s_pods[j];
     const ksg_profile& prof = s_prof;
@@ -316,7 +334,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
     // re-evaluate the nodes assumed onto earlier in this batch, on live state
     for (int i = tid; i < nc; i += BLOCK)
       s_ce[i] = eval_node(c, prof, v, requested, nonzero, pod_count, s_clist[i], nullptr, nullptr);
+    KSG_STAMP(1);
     __syncthreads();
+    KSG_STAMP(2);
     const int64_t mt1 = s_pmax[2 * j], ma1 = s_pmax[2 * j + 1];
     const uint64_t* rec = a.rec + (size_t)j * N;
     Red r{0, 0, 0, 0x7fffffff};
@@ -360,6 +380,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
       visit_changed(mt, ma, stats);
     };
     scan(mt1, ma1, true);
+    KSG_STAMP(3);
     {
       Red w;
       w.max_t = wave_max64(r.max_t);
@@ -405,6 +426,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
         ge |= s_err[i];
       }
     }
+    KSG_STAMP(4);
     if (j + 1 < a.nb) prefetch(j + 1);   // overlaps the commit barrier
     int selected = -1;
     uint32_t status = 0;
@@ -439,8 +461,13 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
       }
     }
     __syncthreads();
+    KSG_STAMP(5);
   }
   for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
+#ifdef KSG_STAMPS
+  if (tid == 0 && a.stamps)
+    for (int i = 0; i < 6; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+#endif
 }
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
@@ -890,6 +917,7 @@ struct ksg_ctx {
   uint64_t* d_rec = nullptr;
   int32_t* d_pmax = nullptr;
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
+  unsigned long long* d_stamps = nullptr;   // KSG_STAMPS diagnostic build only
 };
 
 namespace {
@@ -936,6 +964,7 @@ void free_all(ksg_ctx* ctx) {
   ctx->allocs.clear();
   ctx->d_rec = nullptr;
   ctx->d_pmax = nullptr;
+  ctx->d_stamps = nullptr;
 }
 
 bool profile_has(const ksg_profile& prof, int pl) {
@@ -1098,6 +1127,14 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   b.pmax = ctx->d_pmax;
   b.placements = d_pl;
   b.results = d_res;
+#ifdef KSG_STAMPS
+  if (!ctx->d_stamps) {
+    int rc;
+    if ((rc = dalloc(ctx, &ctx->d_stamps, 8))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 64, ctx->stream));
+  }
+  b.stamps = ctx->d_stamps;
+#endif
   // Plan batches so that phase 2's LDS preload (changed-node bitmap + pod
   // records + the program range of the batch) fits the dynamic LDS budget.
   constexpr size_t kLdsBudget = 120 * 1024;
@@ -1484,6 +1521,15 @@ int ksg_reset_state(ksg_ctx* ctx) {
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
   return KSG_OK;
 }
+
+#ifdef KSG_STAMPS
+// Diagnostic build only: cycle sums per phase-2 segment since load.
+int ksg_debug_stamps(ksg_ctx* ctx, unsigned long long* out6) {
+  if (!ctx || !out6 || !ctx->d_stamps) return KSG_E_STATE;
+  HIPC(ctx, hipMemcpy(out6, ctx->d_stamps, 48, hipMemcpyDeviceToHost));
+  return KSG_OK;
+}
+#endif
 
 int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms) {
   if (!ctx || !ms) return KSG_E_INVALID;

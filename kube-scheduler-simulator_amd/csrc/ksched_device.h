@@ -78,13 +78,67 @@ __device__ __forceinline__ int64_t div_nonneg(int64_t x, int64_t a) {
   return q;
 }
 
+// ---- node sources ------------------------------------------------------------
+// The plugin code reads a node's static columns through an accessor: GNode
+// reads the SoA columns in global memory, LNode a copy of the node in an LDS
+// slot (phase 2 of the batched path keeps the nodes it re-evaluates there).
+struct GNode {
+  const DevCluster* c;
+  int n;
+  __device__ __forceinline__ uint32_t label(int col) const { return c->label_val[(size_t)col * c->N + n]; }
+  __device__ __forceinline__ bool num(int col, int64_t& x) const {
+    const size_t k = (size_t)col * c->N + n;
+    if (!c->label_num_ok[k]) return false;
+    x = c->label_num[k];
+    return true;
+  }
+  __device__ __forceinline__ uint32_t taint(int s) const { return c->taints[(size_t)s * c->N + n]; }
+  __device__ __forceinline__ uint32_t image(int s) const { return c->images[(size_t)s * c->N + n]; }
+  __device__ __forceinline__ bool unsched() const { return c->unsched[n] != 0; }
+};
+
+// LDS slot layout of a cached node (int32 words; the same for every slot).
+struct SlotLayout {
+  int alloc, req, nz, pc, allowed, unsched, lab, num, numok, taint, img, words;
+};
+__device__ __forceinline__ SlotLayout slot_layout(const DevCluster& c) {
+  SlotLayout s;
+  s.alloc = 0;
+  s.req = 2 * c.R;
+  s.nz = 4 * c.R;
+  s.pc = s.nz + 4;
+  s.allowed = s.pc + 1;
+  s.unsched = s.allowed + 1;
+  s.lab = s.unsched + 1;
+  s.num = s.lab + c.L;
+  s.numok = s.num + 2 * c.L;
+  s.taint = s.numok + c.L;
+  s.img = s.taint + c.T;
+  s.words = (s.img + c.I + 1) & ~1;   // keep int64 fields 8-byte aligned
+  return s;
+}
+struct LNode {
+  const int32_t* w;        // slot base (LDS)
+  const SlotLayout* lay;
+  __device__ __forceinline__ uint32_t label(int col) const { return (uint32_t)w[lay->lab + col]; }
+  __device__ __forceinline__ bool num(int col, int64_t& x) const {
+    if (!w[lay->numok + col]) return false;
+    x = (int64_t)(((uint64_t)(uint32_t)w[lay->num + 2 * col + 1] << 32) | (uint32_t)w[lay->num + 2 * col]);
+    return true;
+  }
+  __device__ __forceinline__ uint32_t taint(int s) const { return (uint32_t)w[lay->taint + s]; }
+  __device__ __forceinline__ uint32_t image(int s) const { return (uint32_t)w[lay->img + s]; }
+  __device__ __forceinline__ bool unsched() const { return w[lay->unsched] != 0; }
+};
+
 // ---- requirement programs (encoder.py grammar); P = pod blob in LDS -------
-__device__ __forceinline__ bool eval_req(const DevCluster& c, const int32_t*& w, int n) {
+template <class Src>
+__device__ __forceinline__ bool eval_req(const Src& nd, const int32_t*& w) {
   const int col = w[0], op = w[1], nv = w[2];
   const int32_t* vals = w + 3;
   w += 3 + nv;
   if (op == 6) return false;
-  const uint32_t v = c.label_val[(size_t)col * c.N + n];
+  const uint32_t v = nd.label(col);
   if (op == 0 || op == 1) {
     bool hit = false;
     for (int i = 0; i < nv; i++) hit |= ((uint32_t)vals[i] == v);
@@ -94,40 +148,43 @@ __device__ __forceinline__ bool eval_req(const DevCluster& c, const int32_t*& w,
   if (op == 2) return v != 0;
   if (op == 3) return v == 0;
   if (v == 0) return false;
-  const size_t k = (size_t)col * c.N + n;
-  if (!c.label_num_ok[k]) return false;
-  const int64_t bound = ld64(vals), x = c.label_num[k];
+  int64_t x;
+  if (!nd.num(col, x)) return false;
+  const int64_t bound = ld64(vals);
   return op == 4 ? x > bound : x < bound;
 }
 
-__device__ __forceinline__ bool eval_term(const DevCluster& c, const int32_t*& w, int n) {
+template <class Src>
+__device__ __forceinline__ bool eval_term(const Src& nd, const int32_t*& w) {
   const int nr = *w++;
   bool ok = nr > 0;
-  for (int i = 0; i < nr; i++) ok = eval_req(c, w, n) && ok;
+  for (int i = 0; i < nr; i++) ok = eval_req(nd, w) && ok;
   return ok;
 }
 
-__device__ __forceinline__ bool na_required_match(const DevCluster& c, const int32_t* P, int na_req, int n) {
+template <class Src>
+__device__ __forceinline__ bool na_required_match(const Src& nd, const int32_t* P, int na_req) {
   if (na_req < 0) return true;
   const int32_t* w = P + na_req;
   const int nsel = *w++;
   bool ok = true;
-  for (int i = 0; i < nsel; i++) ok = eval_req(c, w, n) && ok;
+  for (int i = 0; i < nsel; i++) ok = eval_req(nd, w) && ok;
   if (!ok) return false;
   const int nterms = *w++;
   if (nterms < 0) return true;
   bool any = false;
-  for (int t = 0; t < nterms; t++) any = eval_term(c, w, n) || any;
+  for (int t = 0; t < nterms; t++) any = eval_term(nd, w) || any;
   return any;
 }
 
-__device__ __forceinline__ int64_t na_pref_score(const DevCluster& c, const int32_t* P, int na_pref, int n) {
+template <class Src>
+__device__ __forceinline__ int64_t na_pref_score(const Src& nd, const int32_t* P, int na_pref) {
   const int32_t* w = P + na_pref;
   const int nterms = *w++;
   int64_t s = 0;
   for (int t = 0; t < nterms; t++) {
     const int weight = *w++;
-    if (eval_term(c, w, n)) s += weight;
+    if (eval_term(nd, w)) s += weight;
   }
   return s;
 }
@@ -137,9 +194,10 @@ __device__ __forceinline__ bool tol_bit(const int32_t* tolp, uint32_t vid) {
 }
 
 // FindMatchingUntoleratedTaint (NoSchedule | NoExecute): slot or -1.
-__device__ __forceinline__ int untolerated_slot(const DevCluster& c, const int32_t* tolf, int n) {
+template <class Src>
+__device__ __forceinline__ int untolerated_slot(const DevCluster& c, const Src& nd, const int32_t* tolf) {
   for (int s = 0; s < c.T; s++) {
-    const uint32_t id = c.taints[(size_t)s * c.N + n];
+    const uint32_t id = nd.taint(s);
     if (!id) break;
     const uint32_t vid = id - 1;
     const uint8_t e = c.taint_effect[vid];
@@ -149,10 +207,11 @@ __device__ __forceinline__ int untolerated_slot(const DevCluster& c, const int32
   return -1;
 }
 
-__device__ __forceinline__ int64_t taint_score(const DevCluster& c, const int32_t* tolp, int n) {
+template <class Src>
+__device__ __forceinline__ int64_t taint_score(const DevCluster& c, const Src& nd, const int32_t* tolp) {
   int64_t k = 0;
   for (int s = 0; s < c.T; s++) {
-    const uint32_t id = c.taints[(size_t)s * c.N + n];
+    const uint32_t id = nd.taint(s);
     if (!id) break;
     const uint32_t vid = id - 1;
     if (c.taint_effect[vid] != KSG_EFFECT_PREFER_NO_SCHEDULE) continue;
@@ -283,8 +342,9 @@ __device__ __forceinline__ int64_t ba_score(const ksg_profile& prof, const ksg_p
   return (int64_t)((1 - sd) * (double)100);
 }
 
-__device__ __forceinline__ int64_t image_score(const DevCluster& c, const int32_t* P, int img, int n_containers,
-                                               int n) {
+template <class Src>
+__device__ __forceinline__ int64_t image_score(const DevCluster& c, const Src& nd, const int32_t* P, int img,
+                                               int n_containers) {
   int64_t sum = 0;
   if (img >= 0) {
     const int32_t* w = P + img;
@@ -293,7 +353,7 @@ __device__ __forceinline__ int64_t image_score(const DevCluster& c, const int32_
       const uint32_t id = (uint32_t)w[0];
       const int64_t contrib = ld64(w + 1);
       for (int s = 0; s < c.I; s++) {
-        const uint32_t x = c.images[(size_t)s * c.N + n];
+        const uint32_t x = nd.image(s);
         if (!x || x > id) break;
         if (x == id) { sum += contrib; break; }
       }

@@ -236,8 +236,9 @@ __device__ __forceinline__ bool has_all(const DevCluster& c, const int32_t* cons
 }
 // topologySpreadConstraint.matchNodeInclusionPolicies
 __device__ __forceinline__ bool inclusion(const DevCluster& c, const PodView& v, int na, int nt, int n) {
-  if (na && !na_required_match(c, v.P, v.na_req, n)) return false;
-  if (nt && untolerated_slot(c, v.tolf, n) >= 0) return false;
+  const GNode nd{&c, n};
+  if (na && !na_required_match(nd, v.P, v.na_req)) return false;
+  if (nt && untolerated_slot(c, nd, v.tolf) >= 0) return false;
   return true;
 }
 __device__ __forceinline__ bool bit_get(const int32_t* h, int base, uint32_t v) {
@@ -352,15 +353,15 @@ struct NodeEval {
 
 // RunFilterPlugins (first rejection ends the node) + the raw Score() of every
 // enabled score plugin, for one (pod, node).  craw/cnorm: optional capture rows.
-__device__ __forceinline__ NodeEval eval_node(const DevCluster& c, const ksg_profile& prof, const PodView& v,
-                                              const int64_t* requested, const int64_t* nonzero,
-                                              const int32_t* pod_count, int n, int64_t* craw, int64_t* cnorm,
-                                              const TopoCtx* tc = nullptr) {
+// Src: GNode (columns in global memory) or LNode (a node cached in LDS); L:
+// the node's resource columns, already gathered by the caller.
+template <class Src>
+__device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg_profile& prof, const PodView& v,
+                                                  const Src& nd, const NodeCols& L, int n, int64_t* craw,
+                                                  int64_t* cnorm, const TopoCtx* tc = nullptr) {
   const ksg_pod& p = *v.p;
   const int N = c.N;
   NodeEval e{0, 0, 0, 0};
-  NodeCols L;
-  load_cols(c, requested, nonzero, pod_count, n, L);
   uint32_t st = 0;
   if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) {
     st = KSG_FS_NOT_EVALUATED;
@@ -370,18 +371,18 @@ __device__ __forceinline__ NodeEval eval_node(const DevCluster& c, const ksg_pro
       if ((v.fskip >> pl) & 1u) continue;
       switch (pl) {
         case KSG_PL_NODE_UNSCHEDULABLE:
-          if (c.unsched[n] && !(p.flags & KSG_POD_TOL_UNSCHED)) st = pl + 1;
+          if (nd.unsched() && !(p.flags & KSG_POD_TOL_UNSCHED)) st = pl + 1;
           break;
         case KSG_PL_NODE_NAME:
           if (p.node_name != -1 && p.node_name != n) st = pl + 1;
           break;
         case KSG_PL_TAINT_TOLERATION: {
-          const int s = untolerated_slot(c, v.tolf, n);
+          const int s = untolerated_slot(c, nd, v.tolf);
           if (s >= 0) st = (uint32_t)(pl + 1) | ((uint32_t)s << 8);
           break;
         }
         case KSG_PL_NODE_AFFINITY:
-          if (!na_required_match(c, v.P, v.na_req, n)) st = (uint32_t)(pl + 1) | (1u << 8);
+          if (!na_required_match(nd, v.P, v.na_req)) st = (uint32_t)(pl + 1) | (1u << 8);
           break;
         case KSG_PL_NODE_RESOURCES_FIT: {
           const uint32_t b = fit_filter(c, p, L, prof.fit_ignored_res);
@@ -418,19 +419,28 @@ __device__ __forceinline__ NodeEval eval_node(const DevCluster& c, const ksg_pro
     if (craw) { craw[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; cnorm[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; }
   }
   if (v.smask & bit(KSG_PL_IMAGE_LOCALITY)) {
-    const int64_t s = image_score(c, v.P, v.img, p.n_containers, n);
+    const int64_t s = image_score(c, nd, v.P, v.img, p.n_containers);
     e.part += s * v.w_img;
     if (craw) { craw[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; cnorm[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; }
   }
   if (v.smask & bit(KSG_PL_TAINT_TOLERATION)) {
-    e.rt = taint_score(c, v.tolp, n);
+    e.rt = taint_score(c, nd, v.tolp);
     if (craw) craw[(size_t)KSG_PL_TAINT_TOLERATION * N + n] = e.rt;
   }
   if (v.smask & bit(KSG_PL_NODE_AFFINITY)) {
-    e.ra = na_pref_score(c, v.P, v.na_pref, n);
+    e.ra = na_pref_score(nd, v.P, v.na_pref);
     if (craw) craw[(size_t)KSG_PL_NODE_AFFINITY * N + n] = e.ra;
   }
   return e;
+}
+
+__device__ __forceinline__ NodeEval eval_node(const DevCluster& c, const ksg_profile& prof, const PodView& v,
+                                              const int64_t* requested, const int64_t* nonzero,
+                                              const int32_t* pod_count, int n, int64_t* craw, int64_t* cnorm,
+                                              const TopoCtx* tc = nullptr) {
+  NodeCols L;
+  load_cols(c, requested, nonzero, pod_count, n, L);
+  return eval_node_src(c, prof, v, GNode{&c, n}, L, n, craw, cnorm, tc);
 }
 
 // DefaultNormalizeScore (reverse for TaintToleration) + weighted sum.  err set
