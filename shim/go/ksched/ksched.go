@@ -1,0 +1,206 @@
+// Package ksched is the cgo binding of libksched.so (include/ksched.h) for the
+// debuggable scheduler in simulator/scheduler.  Source only: this image has no
+// Go toolchain, so it is not compiled here (DESIGN.md §1).
+//
+// Build: CGO_ENABLED=1, CGO_CFLAGS=-I<repo>/include,
+// CGO_LDFLAGS="-L<repo>/kube-scheduler-simulator_amd -lksched -Wl,-rpath,<dir>".
+package ksched
+
+/*
+#cgo LDFLAGS: -lksched
+#include <stdlib.h>
+#include "ksched.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"sync"
+	"unsafe"
+)
+
+// Plugin ids, identical to include/ksched.h.
+const (
+	NodeUnschedulable  = C.KSG_PL_NODE_UNSCHEDULABLE
+	NodeName           = C.KSG_PL_NODE_NAME
+	TaintToleration    = C.KSG_PL_TAINT_TOLERATION
+	NodeAffinity       = C.KSG_PL_NODE_AFFINITY
+	NodePorts          = C.KSG_PL_NODE_PORTS
+	NodeResourcesFit   = C.KSG_PL_NODE_RESOURCES_FIT
+	PodTopologySpread  = C.KSG_PL_POD_TOPOLOGY_SPREAD
+	InterPodAffinity   = C.KSG_PL_INTER_POD_AFFINITY
+	BalancedAllocation = C.KSG_PL_BALANCED_ALLOCATION
+	ImageLocality      = C.KSG_PL_IMAGE_LOCALITY
+	NPlugins           = C.KSG_NPLUGINS
+)
+
+// Error carries a KSG_E_* code and the context's message.
+type Error struct {
+	Code int
+	Msg  string
+}
+
+func (e *Error) Error() string { return fmt.Sprintf("ksched: %d: %s", e.Code, e.Msg) }
+
+// Ctx owns one device context.  Calls are serialised (a ksg_ctx is not
+// thread-safe, and the framework calls plugins from 16 goroutines).
+type Ctx struct {
+	mu  sync.Mutex
+	c   *C.ksg_ctx
+	nN  int
+}
+
+func (x *Ctx) check(rc C.int) error {
+	if rc == 0 {
+		return nil
+	}
+	return &Error{Code: int(rc), Msg: C.GoString(C.ksg_last_error(x.c))}
+}
+
+// Open creates a context on HIP device dev.
+func Open(dev int) (*Ctx, error) {
+	x := &Ctx{}
+	if rc := C.ksg_open(C.int(dev), &x.c); rc != 0 {
+		return nil, &Error{Code: int(rc), Msg: "ksg_open"}
+	}
+	return x, nil
+}
+
+// Close releases the device context.
+func (x *Ctx) Close() error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	rc := C.ksg_close(x.c)
+	x.c = nil
+	return x.check(rc)
+}
+
+// Nodes is the SoA snapshot produced by the encoder (see encoder.py for the
+// column rules); Go slices are passed without copying for the duration of
+// the call only (cgo pointer rules: ksched copies them).
+type Nodes struct {
+	NNodes, NRes                  int
+	Alloc, Requested, Nonzero     []int64
+	AllowedPods, PodCount         []int32
+	Unschedulable                 []uint8
+	NLabelCols                    int
+	LabelVal                      []uint32
+	LabelNum                      []int64
+	LabelNumOK                    []uint8
+	MaxTaints                     int
+	Taints                        []uint32
+	TaintEffect                   []uint8
+	MaxImages                     int
+	Images                        []uint32
+	NImages                       int
+}
+
+func p64(s []int64) *C.int64_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.int64_t)(unsafe.Pointer(&s[0]))
+}
+func p32(s []int32) *C.int32_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.int32_t)(unsafe.Pointer(&s[0]))
+}
+func pu32(s []uint32) *C.uint32_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint32_t)(unsafe.Pointer(&s[0]))
+}
+func pu8(s []uint8) *C.uint8_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(unsafe.Pointer(&s[0]))
+}
+
+// LoadNodes uploads the snapshot (topology tables may be nil when neither
+// PodTopologySpread nor InterPodAffinity is enabled).
+func (x *Ctx) LoadNodes(n *Nodes, topo *C.ksg_topology) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	cn := C.ksg_nodes{
+		n_nodes: C.int32_t(n.NNodes), n_res: C.int32_t(n.NRes),
+		alloc: p64(n.Alloc), requested: p64(n.Requested), nonzero: p64(n.Nonzero),
+		allowed_pods: p32(n.AllowedPods), pod_count: p32(n.PodCount), unschedulable: pu8(n.Unschedulable),
+		n_label_cols: C.int32_t(n.NLabelCols), label_val: pu32(n.LabelVal), label_num: p64(n.LabelNum),
+		label_num_ok: pu8(n.LabelNumOK), max_taints: C.int32_t(n.MaxTaints), taints: pu32(n.Taints),
+		n_taint_vocab: C.int32_t(len(n.TaintEffect)), taint_effect: pu8(n.TaintEffect),
+		max_images: C.int32_t(n.MaxImages), images: pu32(n.Images), n_images: C.int32_t(n.NImages),
+	}
+	x.nN = n.NNodes
+	return x.check(C.ksg_load_nodes(x.c, &cn, topo))
+}
+
+// SetProfile installs the encoded scheduler profile (MultiPoint order,
+// weights from getScorePluginWeight, plugin args).
+func (x *Ctx) SetProfile(p *C.ksg_profile) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	return x.check(C.ksg_set_profile(x.c, p))
+}
+
+// LoadWorkload uploads encoded pods and their program pool.
+func (x *Ctx) LoadWorkload(pods []C.ksg_pod, prog []int32) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	wl := C.ksg_workload{n_pods: C.int32_t(len(pods)), prog: p32(prog), prog_len: C.int64_t(len(prog))}
+	if len(pods) > 0 {
+		wl.pods = &pods[0]
+	}
+	return x.check(C.ksg_load_workload(x.c, &wl))
+}
+
+// PodEval is everything the wrapped plugins record for one pod, in SoA form.
+type PodEval struct {
+	Selected, NFeasible int
+	Status, ScoreSkip   uint32
+	FStatus             []uint32 // [n_nodes]
+	Raw, Norm           []int64  // [NPlugins][n_nodes]
+	Total               []int64  // [n_nodes]
+}
+
+// Eval runs the full per-pod sweep (filters in profile order with
+// first-rejection exit, raw scores, normalisation, weighted totals, selectHost)
+// without changing node state.  One call per pod, at PreFilter time.
+func (x *Ctx) Eval(pod int) (*PodEval, error) {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	n := x.nN
+	e := &PodEval{
+		FStatus: make([]uint32, n), Raw: make([]int64, NPlugins*n),
+		Norm: make([]int64, NPlugins*n), Total: make([]int64, n),
+	}
+	var res C.ksg_result
+	cap := C.ksg_capture{fstatus: pu32(e.FStatus), raw: p64(e.Raw), norm: p64(e.Norm), total: p64(e.Total)}
+	if err := x.check(C.ksg_eval(x.c, C.int32_t(pod), &res, &cap)); err != nil {
+		return nil, err
+	}
+	e.Selected, e.NFeasible = int(res.selected), int(res.n_feasible)
+	e.Status, e.ScoreSkip = uint32(res.status), uint32(res.score_skip)
+	return e, nil
+}
+
+// Commit assumes pod onto node (Reserve).
+func (x *Ctx) Commit(pod, node int) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	return x.check(C.ksg_commit(x.c, C.int32_t(pod), C.int32_t(node)))
+}
+
+// RunQueue schedules pods [first, first+count) on the device in queue order.
+func (x *Ctx) RunQueue(first, count int) ([]int32, error) {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	pl := make([]int32, count)
+	if count == 0 {
+		return pl, nil
+	}
+	return pl, x.check(C.ksg_run_queue(x.c, C.int32_t(first), C.int32_t(count), p32(pl), nil, nil))
+}
