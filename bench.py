@@ -93,9 +93,16 @@ def main():
     eng.load(enc, pf)   # inputs resident in HBM from here on
     P = len(pods)
 
+    gather_out = None
+    if dist:
+        gather_out = [torch.empty(P, dtype=torch.int32, device=f"cuda:{local_rank}") for _ in range(world)]
+
     def step():
         eng.reset_state()
         pl, _ = eng.run_queue(0, P, results=False)
+        if dist:
+            # the one exchange of the replica sweep: every replica's placements to every rank (RCCL)
+            dist.all_gather(gather_out, torch.from_numpy(pl).to(f"cuda:{local_rank}"))
         return pl
 
     for _ in range(args.warmup):

@@ -200,7 +200,27 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
   }
 }
 
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (int64_t)__shfl_xor(v, o, 64);
+  return v;
+}
+
 // ---- batched speculate-and-repair --------------------------------------------
+// Phase-1 statistics of pod j of a batch (against the batch-start state).
+struct P1Stats {
+  int32_t nfeas, minidx;   // feasible nodes, lowest feasible index
+  int32_t mt, ma;          // max raw TaintToleration / NodeAffinity score over feasible nodes
+  int32_t ht, ha;          // feasible nodes holding mt / ma
+  int32_t err;             // some normalised score left [0, 100]
+  int32_t K;               // |top set| = min(j + 1, nfeas)
+};
+
 struct BatchArgs {
   DevCluster c;
   DevState st;              // replica 0
@@ -212,15 +232,20 @@ struct BatchArgs {
   int32_t prog_lo, prog_len;  // program range covering the batch's blobs
   unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
   uint64_t* rec;            // [KSG_BATCH_MAX][N] packed phase-1 records
+  int32_t* img;             // [KSG_BATCH_MAX][N] weight x ImageLocality score of feasible nodes
   int32_t* pmax;            // [KSG_BATCH_MAX][2] phase-1 maxima (taint, node affinity)
+  P1Stats* p1;              // [KSG_BATCH_MAX]
+  uint64_t* top;            // [KSG_BATCH_MAX][KSG_BATCH_MAX] top-set argmax keys
   int32_t* placements;
   ksg_result* results;      // or null
 };
 
 // record: bit 63 feasible | rt (8 bits) << 48 | ra (16 bits) << 32 | partial (32 bits)
+__device__ __forceinline__ uint64_t pack_rec(int64_t part, int64_t rt, int64_t ra) {
+  return (1ull << 63) | ((uint64_t)(rt & 0xff) << 48) | ((uint64_t)(ra & 0xffff) << 32) | (uint32_t)part;
+}
 __device__ __forceinline__ uint64_t pack_rec(const NodeEval& e) {
-  if (e.st != 0) return 0;
-  return (1ull << 63) | ((uint64_t)(e.rt & 0xff) << 48) | ((uint64_t)(e.ra & 0xffff) << 32) | (uint32_t)e.part;
+  return e.st != 0 ? 0 : pack_rec(e.part, e.rt, e.ra);
 }
 
 __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
@@ -242,6 +267,7 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
   if (n < N) {
     const NodeEval e = eval_node(c, s_prof, v, a.st.requested, a.st.nonzero, a.st.pod_count, n, nullptr, nullptr);
     a.rec[(size_t)j * N + n] = pack_rec(e);
+    a.img[(size_t)j * N + n] = e.st == 0 ? (int32_t)e.img : 0;
     if (e.st == 0) { mt = (int32_t)e.rt; ma = (int32_t)e.ra; }
   }
   mt = (int32_t)wave_max64(mt);
@@ -256,13 +282,174 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
   }
 }
 
-// Phase 2: one workgroup walks the batch in queue order.  The batch's pod
-// records and program range are preloaded into LDS in one coalesced copy;
-// each pod's phase-1 records are prefetched into registers while the changed
-// nodes are re-evaluated, so a pod costs one re-evaluation latency plus three
-// barriers.
-// Diagnostic build (-DKSG_STAMPS): lane 0 of wave 0 sums s_memtime deltas per
-// segment of the phase-2 loop.  Never compiled into the measured library.
+// Phase 1b, one workgroup per pod j: the statistics phase 2 needs to update
+// pod j's result incrementally, and the top set T_j = the min(j + 1, nfeas)
+// best nodes by (total, lowest index) under the phase-1 maxima.  At most j
+// nodes change before pod j, so T_j always contains the best unchanged node.
+// The K-th largest key is found by a binary search over a dense key
+// ((total - tmin) * N + N - 1 - n), one block count per step.
+constexpr int kTopQ = 16;   // keys held in registers per lane (N <= 8192 at 512 lanes)
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
+  constexpr int NW = BLOCK / 64;
+  constexpr long long BIG = 0x7fffffffffffffffll;
+  __shared__ ksg_profile s_prof;
+  __shared__ long long s_r[NW][4];
+  __shared__ int32_t s_i[NW][6];
+  __shared__ int32_t s_cnt[3];
+  __shared__ int32_t s_pos;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int j = blockIdx.x;
+  const DevCluster& c = a.c;
+  const int N = c.N;
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  if (tid < 3) s_cnt[tid] = 0;
+  if (tid == 0) s_pos = 0;
+  __syncthreads();
+  const ksg_pod& p = a.pods[a.b0 + j];
+  const PodView v = make_view(c, s_prof, p, nullptr, a.prog);
+  const int64_t mt = a.pmax[2 * j], ma = a.pmax[2 * j + 1];
+  const uint64_t* rec = a.rec + (size_t)j * N;
+
+  int32_t nfeas = 0, minidx = 0x7fffffff, ht = 0, ha = 0;
+  uint32_t err = 0;
+  int64_t tmin = BIG, tmax = -BIG;
+  auto total_of = [&](uint64_t x, uint32_t& e) -> int64_t {
+    const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
+    return total_score(v, part, rt, ra, mt, ma, e, nullptr, nullptr);
+  };
+  int64_t tot[kTopQ];
+#pragma unroll
+  for (int q = 0; q < kTopQ; q++) {
+    const int n = tid + q * BLOCK;
+    tot[q] = BIG;   // BIG = infeasible
+    if (n >= N) continue;
+    const uint64_t x = rec[n];
+    if (!(x >> 63)) continue;
+    const int64_t t = total_of(x, err);
+    tot[q] = t;
+  }
+  auto stats = [&](uint64_t x, int n, int64_t t) {
+    nfeas += 1;
+    minidx = min(minidx, n);
+    ht += ((int64_t)((x >> 48) & 0xff) == mt);
+    ha += ((int64_t)((x >> 32) & 0xffff) == ma);
+    tmin = min(tmin, t);
+    tmax = max(tmax, t);
+  };
+#pragma unroll
+  for (int q = 0; q < kTopQ; q++) {
+    const int n = tid + q * BLOCK;
+    if (tot[q] != BIG) stats(rec[n], n, tot[q]);
+  }
+  for (int n = tid + kTopQ * BLOCK; n < N; n += BLOCK) {
+    const uint64_t x = rec[n];
+    if (x >> 63) stats(x, n, total_of(x, err));
+  }
+  {
+    const int64_t w0 = wave_min64(tmin), w1 = -wave_min64(-tmax);
+    const int32_t i0 = wave_sum32(nfeas), i1 = wave_min32(minidx), i2 = wave_sum32(ht), i3 = wave_sum32(ha);
+    const uint32_t i4 = wave_or32(err);
+    if (lane == 0) {
+      s_r[wv][0] = w0;
+      s_r[wv][1] = w1;
+      s_i[wv][0] = i0;
+      s_i[wv][1] = i1;
+      s_i[wv][2] = i2;
+      s_i[wv][3] = i3;
+      s_i[wv][4] = (int32_t)i4;
+    }
+  }
+  __syncthreads();
+  int64_t gmin = BIG, gmax = -BIG;
+  int32_t gn = 0, gidx = 0x7fffffff, ght = 0, gha = 0, gerr = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) {
+    gmin = min(gmin, (int64_t)s_r[i][0]);
+    gmax = max(gmax, (int64_t)s_r[i][1]);
+    gn += s_i[i][0];
+    gidx = min(gidx, s_i[i][1]);
+    ght += s_i[i][2];
+    gha += s_i[i][3];
+    gerr |= s_i[i][4];
+  }
+  const int K = min(j + 1, gn);
+  if (tid == 0) {
+    P1Stats s;
+    s.nfeas = gn;
+    s.minidx = gidx;
+    s.mt = (int32_t)mt;
+    s.ma = (int32_t)ma;
+    s.ht = ght;
+    s.ha = gha;
+    s.err = gerr;
+    s.K = K;
+    a.p1[j] = s;
+  }
+  if (K == 0) return;
+  // dense key: larger = better (higher total, then lower node index)
+  auto dkey = [&](int64_t t, int n) -> int64_t { return (t - gmin) * (int64_t)N + (N - 1 - n); };
+  auto count_ge = [&](int64_t th) -> int32_t {
+    int32_t k = 0;
+#pragma unroll
+    for (int q = 0; q < kTopQ; q++) {
+      const int n = tid + q * BLOCK;
+      k += (tot[q] != BIG && dkey(tot[q], n) >= th);
+    }
+    for (int n = tid + kTopQ * BLOCK; n < N; n += BLOCK) {
+      const uint64_t x = rec[n];
+      uint32_t e = 0;
+      if (x >> 63) k += dkey(total_of(x, e), n) >= th;
+    }
+    return k;
+  };
+  int64_t lo = 0, hi = dkey(gmax, 0);
+  for (int it = 0; lo < hi; it++) {
+    const int64_t mid = lo + (hi - lo + 1) / 2;
+    const int32_t k = wave_sum32(count_ge(mid));
+    if (lane == 0) atomicAdd(&s_cnt[it % 3], k);
+    __syncthreads();
+    const int32_t tot_k = s_cnt[it % 3];
+    if (tid == 0) s_cnt[(it + 2) % 3] = 0;
+    if (tot_k >= K) lo = mid;
+    else hi = mid - 1;
+  }
+  uint64_t* out = a.top + (size_t)j * KSG_BATCH_MAX;
+  auto emit = [&](int64_t t, int n) {
+    if (dkey(t, n) >= lo) {
+      const int pos = atomicAdd(&s_pos, 1);
+      if (pos < KSG_BATCH_MAX) out[pos] = argmax_key(t, n);
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kTopQ; q++) {
+    const int n = tid + q * BLOCK;
+    if (tot[q] != BIG) emit(tot[q], n);
+  }
+  for (int n = tid + kTopQ * BLOCK; n < N; n += BLOCK) {
+    const uint64_t x = rec[n];
+    uint32_t e = 0;
+    if (x >> 63) emit(total_of(x, e), n);
+  }
+}
+
+// Phase 2: one workgroup walks the batch in queue order and keeps every node
+// assumed onto during the batch (the changed set C, |C| <= j before pod j) in
+// an LDS slot holding its live resource columns.  Per pod j:
+//   A  lanes 0..255     re-evaluate C: static filters/scores from the phase-1
+//                       record (they do not depend on the assumed pods),
+//                       NodeResourcesFit + BalancedAllocation from the slot;
+//      lanes 256..511   best key of T_j \ C (= the best unchanged node);
+//      lanes 512..767   best two keys of T_{j+1} \ C (prediction of pod j+1's
+//                       choice, so its columns are fetched a pod ahead);
+//   B  feasible count = phase-1 count corrected over C; the normalisation
+//      maxima are unchanged while a holder survives (else, or on a range
+//      error, a full rescan of the records, rare); select; the last wave
+//      assumes the pod into its slot and stores the node's new columns.
+// Two barriers per pod; the next pod's records and top set are fetched into
+// registers during A and written to LDS during B.
 #ifdef KSG_STAMPS
 #define KSG_STAMP(seg)                                                   \
   do {                                                                   \
@@ -274,52 +461,96 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
 #else
 #define KSG_STAMP(seg) do {} while (0)
 #endif
-constexpr int kRPT = 10;  // phase-1 records held in registers per lane (N <= 5120 at 512 lanes)
 
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
-  constexpr int NW = BLOCK / 64;
+struct WRed {
+  uint64_t k0, k1;
+  int32_t feas1, live, lost_t, lost_a, cmin, err;
+};
+
+__device__ __forceinline__ void top2_merge(uint64_t& a, uint64_t& b, uint64_t oa, uint64_t ob) {
+  const uint64_t hi = a > oa ? a : oa, lo = a > oa ? oa : a;
+  uint64_t s = b > ob ? b : ob;
+  s = s > lo ? s : lo;
+  a = hi;
+  b = s;
+}
+
+__device__ __forceinline__ void slot_cols(const int64_t* sl, int R, NodeCols& L) {
+#pragma unroll
+  for (int r = 0; r < KSG_MAX_RES; r++) {
+    L.alloc[r] = r < R ? sl[r] : 0;
+    L.req[r] = r < R ? sl[R + r] : 0;
+  }
+  L.nz_cpu = sl[2 * R];
+  L.nz_mem = sl[2 * R + 1];
+  L.pod_count = (int32_t)sl[2 * R + 2];
+  L.allowed = (int32_t)sl[2 * R + 3];
+}
+
+constexpr int kP2Block = 768;   // three groups of 256 lanes; the last wave also assumes pods
+
+__global__ __launch_bounds__(kP2Block) void ksg_batch_phase2(BatchArgs a) {
+  constexpr int BLOCK = kP2Block, NW = BLOCK / 64;
+  constexpr int LOADER = NW - 1;   // wave that assumes pods and fetches node columns (after its A work)
   extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
   __shared__ ksg_profile s_prof;
+  __shared__ P1Stats s_p1[KSG_BATCH_MAX];
   __shared__ int32_t s_clist[KSG_BATCH_MAX];
-  __shared__ NodeEval s_ce[KSG_BATCH_MAX];
-  __shared__ int32_t s_pmax[2 * KSG_BATCH_MAX];
+  __shared__ uint64_t s_top[2][KSG_BATCH_MAX];
+  __shared__ uint64_t s_crec[2][KSG_BATCH_MAX];
+  __shared__ int32_t s_cimg[2][KSG_BATCH_MAX];
+  __shared__ uint64_t s_ce[KSG_BATCH_MAX];     // live record of each changed node (rescan path)
+  __shared__ WRed s_w[NW];
   __shared__ int32_t s_nc;
-  __shared__ Red s_red[NW];
-  __shared__ uint64_t s_best[NW];
-  __shared__ uint32_t s_err[NW];
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, grp = tid >> 8, gi = tid & 255;
   const DevCluster& c = a.c;
-  const int N = c.N;
-  int64_t* requested = a.st.requested;
-  int64_t* nonzero = a.st.nonzero;
-  int32_t* pod_count = a.st.pod_count;
+  const int N = c.N, R = c.R, S = 2 * R + 4;
   const int cm_words = (((N + 31) / 32) + 3) & ~3;
   constexpr int POD_WORDS = sizeof(ksg_pod) / 4;
   uint32_t* s_cmask = reinterpret_cast<uint32_t*>(s_dyn);
   ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
   int32_t* s_prog = s_dyn + cm_words + a.nb * POD_WORDS;
+  int64_t* s_slot = reinterpret_cast<int64_t*>(s_dyn + ((cm_words + a.nb * POD_WORDS + a.prog_len + 3) & ~3));
 
   for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
   for (int i = tid; i < a.nb * POD_WORDS; i += BLOCK)
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
   for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
-  for (int i = tid; i < 2 * a.nb; i += BLOCK) s_pmax[i] = a.pmax[i];
+  for (int i = tid; i < a.nb * (int)(sizeof(P1Stats) / 4); i += BLOCK)
+    reinterpret_cast<int32_t*>(s_p1)[i] = reinterpret_cast<const int32_t*>(a.p1)[i];
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  if (tid < KSG_BATCH_MAX) {
+    s_top[0][tid] = a.top[tid];
+    if (a.nb > 1) s_top[1][tid] = a.top[KSG_BATCH_MAX + tid];
+  }
   if (tid == 0) s_nc = 0;
 
-  uint64_t rr[kRPT];
-  auto prefetch = [&](int j) {
-    const uint64_t* rec = a.rec + (size_t)j * N;
-#pragma unroll
-    for (int q = 0; q < kRPT; q++) {
-      const int n = tid + q * BLOCK;
-      rr[q] = n < N ? rec[n] : 0;
-    }
+  bool fit_filter_on = false;
+  for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
+
+  // loader wave: columns of the predicted next choice.  Lane l < S holds slot
+  // word l (alloc[R], requested[R], nonzero[2], pod_count, allowed); lane S
+  // the record and lane S + 1 the image part of the pod after it.
+  int spec_node = -1;
+  int64_t spec_val = 0;
+  auto fetch = [&](int n, int jrec, int64_t& val) {
+    val = 0;
+    if (lane < R) val = c.alloc[(size_t)lane * N + n];
+    else if (lane < 2 * R) val = a.st.requested[(size_t)(lane - R) * N + n];
+    else if (lane < 2 * R + 2) val = a.st.nonzero[(size_t)(lane - 2 * R) * N + n];
+    else if (lane == 2 * R + 2) val = a.st.pod_count[n];
+    else if (lane == 2 * R + 3) val = c.allowed[n];
+    else if (lane == S && jrec < a.nb) val = (int64_t)a.rec[(size_t)jrec * N + n];
+    else if (lane == S + 1 && jrec < a.nb) val = a.img[(size_t)jrec * N + n];
   };
-  prefetch(0);
+  if (wv == LOADER) {
+    if (a.p1[0].K > 0) {
+      spec_node = key_node(a.top[0]);
+      fetch(spec_node, 1, spec_val);
+    }
+  }
   __syncthreads();
 
 #ifdef KSG_STAMPS
@@ -330,136 +561,263 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
     const ksg_pod& p = s_pods[j];
     const ksg_profile& prof = s_prof;
     const PodView v = make_view(c, prof, p, s_prog + (p.blob - a.prog_lo), a.prog);
+    const P1Stats s1 = s_p1[j];
     const int nc = s_nc;
-    // re-evaluate the nodes assumed onto earlier in this batch, on live state
-    for (int i = tid; i < nc; i += BLOCK)
-      s_ce[i] = eval_node(c, prof, v, requested, nonzero, pod_count, s_clist[i], nullptr, nullptr);
+    const int cur = j & 1, nxt = cur ^ 1;
+    const int64_t mt1 = s1.mt, ma1 = s1.ma;
+    auto changed = [&](int n) { return ((s_cmask[n >> 5] >> (n & 31)) & 1u) != 0; };
+
+    // ---- A --------------------------------------------------------------
+    uint64_t pre_rec = 0;   // grp 0: next pod's record of changed node gi; grp 1: T_{j+2} entry gi
+    int32_t pre_img = 0;
+    if (grp == 0) {
+      WRed w{0, 0, 0, 0, 0, 0, 0x7fffffff, 0};
+      if (gi < nc) {
+        const int n = s_clist[gi];
+        if (j + 1 < a.nb) {
+          pre_rec = a.rec[(size_t)(j + 1) * N + n];
+          pre_img = a.img[(size_t)(j + 1) * N + n];
+        }
+        const uint64_t x = s_crec[cur][gi];
+        uint64_t live = 0;
+        if (x >> 63) {
+          w.feas1 = 1;
+          const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff;
+          NodeCols L;
+          slot_cols(s_slot + (size_t)gi * S, R, L);
+          const bool fits = !(fit_filter_on && !((v.fskip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) &&
+                              fit_filter(c, p, L, prof.fit_ignored_res) != 0);
+          if (!fits) {
+            w.lost_t = rt == mt1;
+            w.lost_a = ra == ma1;
+          } else {
+            int64_t part = s_cimg[cur][gi];
+            if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) part += fit_score(prof, p, L) * v.w_fit;
+            if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) part += ba_score(prof, p, L) * v.w_ba;
+            uint32_t e = 0;
+            w.k0 = argmax_key(total_score(v, part, rt, ra, mt1, ma1, e, nullptr, nullptr), n);
+            w.err = (int32_t)e;
+            w.live = 1;
+            w.cmin = n;
+            live = pack_rec(part, rt, ra);
+          }
+        }
+        s_ce[gi] = live;
+      }
+      w.k0 = wave_max_u64(w.k0);
+      w.feas1 = wave_sum32(w.feas1);
+      w.live = wave_sum32(w.live);
+      w.lost_t = wave_sum32(w.lost_t);
+      w.lost_a = wave_sum32(w.lost_a);
+      w.cmin = wave_min32(w.cmin);
+      w.err = (int32_t)wave_or32((uint32_t)w.err);
+      if (lane == 0) s_w[wv] = w;
+    } else if (grp == 1) {
+      uint64_t best = 0;
+      if (gi < s1.K) {
+        const uint64_t key = s_top[cur][gi];
+        if (!changed(key_node(key))) best = key;
+      }
+      if (j + 2 < a.nb && gi < s_p1[j + 2].K) pre_rec = a.top[(size_t)(j + 2) * KSG_BATCH_MAX + gi];
+      best = wave_max_u64(best);
+      if (lane == 0) s_w[wv].k0 = best;
+    } else if (grp == 2) {
+      uint64_t t1 = 0, t2 = 0;
+      if (j + 1 < a.nb && gi < s_p1[j + 1].K) {
+        const uint64_t key = s_top[nxt][gi];
+        if (!changed(key_node(key))) t1 = key;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t o1 = __shfl_xor(t1, o, 64), o2 = __shfl_xor(t2, o, 64);
+        top2_merge(t1, t2, o1, o2);
+      }
+      if (lane == 0) { s_w[wv].k0 = t1; s_w[wv].k1 = t2; }
+    }
     KSG_STAMP(1);
     __syncthreads();
     KSG_STAMP(2);
-    const int64_t mt1 = s_pmax[2 * j], ma1 = s_pmax[2 * j + 1];
-    const uint64_t* rec = a.rec + (size_t)j * N;
-    Red r{0, 0, 0, 0x7fffffff};
-    uint64_t best = 0;
-    uint32_t err = 0;
-    auto visit = [&](uint64_t x, int n, int64_t mt, int64_t ma, bool stats) {
-      if (!(x >> 63)) return;
-      const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
-      if (stats) {
-        r.nfeas += 1;
-        r.minidx = min(r.minidx, n);
-        r.max_t = max(r.max_t, rt);
-        r.max_a = max(r.max_a, ra);
-      }
-      const uint64_t key = argmax_key(total_score(v, part, rt, ra, mt, ma, err, nullptr, nullptr), n);
-      best = key > best ? key : best;
-    };
-    auto visit_changed = [&](int64_t mt, int64_t ma, bool stats) {
-      for (int i = tid; i < nc; i += BLOCK) {
-        const NodeEval e = s_ce[i];
-        if (e.st != 0) continue;
-        const int n = s_clist[i];
-        if (stats) {
-          r.nfeas += 1;
-          r.minidx = min(r.minidx, n);
-          r.max_t = max(r.max_t, e.rt);
-          r.max_a = max(r.max_a, e.ra);
+
+    // ---- B --------------------------------------------------------------
+    WRed g{0, 0, 0, 0, 0, 0, 0x7fffffff, 0};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const WRed w = s_w[i];
+      g.k0 = w.k0 > g.k0 ? w.k0 : g.k0;
+      g.feas1 += w.feas1;
+      g.live += w.live;
+      g.lost_t += w.lost_t;
+      g.lost_a += w.lost_a;
+      g.cmin = min(g.cmin, w.cmin);
+      g.err |= w.err;
+    }
+    const int unch = s1.nfeas - g.feas1;          // unchanged feasible nodes
+    int nfeas = unch + g.live;
+    const bool stale = nfeas >= 2 && (((v.smask & bit(KSG_PL_TAINT_TOLERATION)) && s1.ht - g.lost_t <= 0) ||
+                                      ((v.smask & bit(KSG_PL_NODE_AFFINITY)) && s1.ha - g.lost_a <= 0));
+    const bool rescan = nfeas >= 2 && (s1.err || g.err || stale);
+    uint64_t bu = 0, s1k = 0, s2k = 0;   // loader: best of T_j \ C; best two of T_{j+1} \ C
+    if (wv == LOADER) {
+#pragma unroll
+      for (int i = 4; i < 8; i++) bu = s_w[i].k0 > bu ? s_w[i].k0 : bu;
+#pragma unroll
+      for (int i = 8; i < 12; i++) top2_merge(s1k, s2k, s_w[i].k0, s_w[i].k1);
+    }
+    int selected = -1;
+    uint32_t status = 0;
+    if (rescan) {
+      // full pass over pod j's records with the live maxima (rare)
+      const uint64_t* rec = a.rec + (size_t)j * N;
+      Red r{0, 0, 0, 0x7fffffff};
+      for (int pass = 0; pass < 2; pass++) {
+        uint64_t best = 0;
+        uint32_t err = 0;
+        auto visit = [&](uint64_t x, int n) {
+          if (!(x >> 63)) return;
+          const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
+          if (pass == 0) {
+            r.nfeas += 1;
+            r.minidx = min(r.minidx, n);
+            r.max_t = max(r.max_t, rt);
+            r.max_a = max(r.max_a, ra);
+          } else {
+            const uint64_t key = argmax_key(total_score(v, part, rt, ra, r.max_t, r.max_a, err, nullptr, nullptr), n);
+            best = key > best ? key : best;
+          }
+        };
+        for (int n = tid; n < N; n += BLOCK)
+          if (!changed(n)) visit(rec[n], n);
+        for (int i = tid; i < nc; i += BLOCK) visit(s_ce[i], s_clist[i]);
+        __syncthreads();   // s_w reads of this pod are done / previous pass consumed
+        if (pass == 0) {
+          WRed w{0, 0, 0, 0, 0, 0, 0, 0};
+          w.k0 = (uint64_t)wave_max64(r.max_t);
+          w.k1 = (uint64_t)wave_max64(r.max_a);
+          w.live = wave_sum32(r.nfeas);
+          w.cmin = wave_min32(r.minidx);
+          if (lane == 0) s_w[wv] = w;
+          __syncthreads();
+          r = Red{0, 0, 0, 0x7fffffff};
+#pragma unroll
+          for (int i = 0; i < NW; i++) {
+            const WRed w2 = s_w[i];
+            r.max_t = max(r.max_t, (int64_t)w2.k0);
+            r.max_a = max(r.max_a, (int64_t)w2.k1);
+            r.nfeas += w2.live;
+            r.minidx = min(r.minidx, w2.cmin);
+          }
+        } else {
+          WRed w{0, 0, 0, 0, 0, 0, 0, 0};
+          w.k0 = wave_max_u64(best);
+          w.err = (int32_t)wave_or32(err);
+          if (lane == 0) s_w[wv] = w;
+          __syncthreads();
+          uint64_t gb = 0;
+          uint32_t ge = 0;
+#pragma unroll
+          for (int i = 0; i < NW; i++) {
+            gb = s_w[i].k0 > gb ? s_w[i].k0 : gb;
+            ge |= (uint32_t)s_w[i].err;
+          }
+          nfeas = r.nfeas;
+          status |= KSG_ST_SCORED;
+          if (ge) status |= KSG_ST_SCORE_ERROR;
+          else selected = key_node(gb);
         }
-        const uint64_t key = argmax_key(total_score(v, e.part, e.rt, e.ra, mt, ma, err, nullptr, nullptr), n);
-        best = key > best ? key : best;
       }
-    };
-    auto scan = [&](int64_t mt, int64_t ma, bool stats) {
-#pragma unroll
-      for (int q = 0; q < kRPT; q++) {
-        const int n = tid + q * BLOCK;
-        if (n < N && !((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rr[q], n, mt, ma, stats);
-      }
-      for (int n = tid + kRPT * BLOCK; n < N; n += BLOCK)
-        if (!((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rec[n], n, mt, ma, stats);
-      visit_changed(mt, ma, stats);
-    };
-    scan(mt1, ma1, true);
+    } else if (nfeas == 1) {
+      selected = unch == 1 ? -2 : g.cmin;   // -2: the unchanged best (resolved below)
+    } else if (nfeas >= 2) {
+      status |= KSG_ST_SCORED;
+      selected = -3;                          // max(best unchanged, best changed)
+    }
     KSG_STAMP(3);
-    {
-      Red w;
-      w.max_t = wave_max64(r.max_t);
-      w.max_a = wave_max64(r.max_a);
-      w.nfeas = wave_sum32(r.nfeas);
-      w.minidx = wave_min32(r.minidx);
-      best = wave_max_u64(best);
-      err = wave_or32(err);
-      if (lane == 0) { s_red[wv] = w; s_best[wv] = best; s_err[wv] = err; }
+    if (grp == 0 && gi < nc && j + 1 < a.nb) {
+      s_crec[nxt][gi] = pre_rec;
+      s_cimg[nxt][gi] = pre_img;
+    } else if (grp == 1 && j + 2 < a.nb && gi < s_p1[j + 2].K) {
+      s_top[cur][gi] = pre_rec;
     }
-    __syncthreads();
-    Red g{0, 0, 0, 0x7fffffff};
-    uint64_t gb = 0;
-    uint32_t ge = 0;
-#pragma unroll
-    for (int i = 0; i < NW; i++) {
-      const Red w = s_red[i];
-      g.max_t = max(g.max_t, w.max_t);
-      g.max_a = max(g.max_a, w.max_a);
-      g.nfeas += w.nfeas;
-      g.minidx = min(g.minidx, w.minidx);
-      gb = s_best[i] > gb ? s_best[i] : gb;
-      ge |= s_err[i];
-    }
-    const bool stale_t = (v.smask & bit(KSG_PL_TAINT_TOLERATION)) && g.max_t != mt1;
-    const bool stale_a = (v.smask & bit(KSG_PL_NODE_AFFINITY)) && g.max_a != ma1;
-    if (g.nfeas >= 2 && (stale_t || stale_a)) {
-      // a holder of a phase-1 maximum was assumed full: renormalise with the
-      // live maxima (second scan; rare)
-      __syncthreads();
-      best = 0;
-      err = 0;
-      scan(g.max_t, g.max_a, false);
-      best = wave_max_u64(best);
-      err = wave_or32(err);
-      if (lane == 0) { s_best[wv] = best; s_err[wv] = err; }
-      __syncthreads();
-      gb = 0;
-      ge = 0;
-#pragma unroll
-      for (int i = 0; i < NW; i++) {
-        gb = s_best[i] > gb ? s_best[i] : gb;
-        ge |= s_err[i];
+    if (wv == LOADER) {
+      if (selected == -2) selected = key_node(bu);
+      else if (selected == -3) selected = key_node(bu > g.k0 ? bu : g.k0);
+      uint32_t score_skip;
+      ipa_skip_bits(prof, p, status, score_skip);
+      if (selected >= 0) {
+        // assume: live columns of the selected node into its slot + global
+        int idx = -1;
+        if (changed(selected)) {
+          for (int b = 0; b < nc; b += 64) {
+            const uint64_t m = __ballot(b + lane < nc && s_clist[b + lane] == selected);
+            if (m) { idx = b + __builtin_ctzll(m); break; }
+          }
+        }
+        int64_t val;
+        if (idx >= 0) {
+          val = lane < S ? s_slot[(size_t)idx * S + lane] : 0;
+        } else if (selected == spec_node) {
+          val = spec_val;
+        } else {
+          fetch(selected, j + 1, val);
+        }
+        if (lane < S) {
+          int64_t d = 0;
+          if (lane >= R && lane < 2 * R) d = p.req[lane - R];
+          else if (lane == 2 * R) d = p.nz_cpu;
+          else if (lane == 2 * R + 1) d = p.nz_mem;
+          else if (lane == 2 * R + 2) d = 1;
+          val += d;
+          const int slot = idx >= 0 ? idx : nc;
+          s_slot[(size_t)slot * S + lane] = val;
+          if (lane >= R && lane < 2 * R) a.st.requested[(size_t)(lane - R) * N + selected] = val;
+          else if (lane == 2 * R || lane == 2 * R + 1) a.st.nonzero[(size_t)(lane - 2 * R) * N + selected] = val;
+          else if (lane == 2 * R + 2) a.st.pod_count[selected] = (int32_t)val;
+        }
+        if (idx < 0) {
+          if (lane == S) s_crec[nxt][nc] = (uint64_t)val;
+          if (lane == S + 1) s_cimg[nxt][nc] = (int32_t)val;
+          if (lane == 0) {
+            s_cmask[selected >> 5] |= 1u << (selected & 31);
+            s_clist[nc] = selected;
+            s_nc = nc + 1;
+          }
+        }
+        if (lane == 0 && v.commit >= 0) {   // PodTopologySpread / InterPodAffinity count tables
+          const int32_t* w = v.P + v.commit;
+          const int ns = *w++;
+          for (int i = 0; i < ns; i++) a.st.cnt[(size_t)w[i] * N + selected] += 1;
+          w += ns;
+          const int nt = *w++;
+          for (int i = 0; i < nt; i++) {
+            const int t = w[i];
+            const uint32_t lv = c.label_val[(size_t)c.tmpl_col[t] * N + selected];
+            if (!lv) continue;
+            a.st.tab[c.tmpl_off[t] + lv] += c.tmpl_kind[t] == KSG_TMPL_PREF ? c.tmpl_weight[t] : 1;
+            a.st.tmpl_total[t] += 1;
+          }
+        }
+      }
+      if (lane == 0) {
+        const int o = a.out0 + j;
+        a.placements[o] = selected;
+        if (a.results) {
+          ksg_result res;
+          res.selected = selected;
+          res.n_feasible = nfeas;
+          res.status = status;
+          res.score_skip = score_skip;
+          a.results[o] = res;
+        }
+      }
+      // predict pod j+1's choice: its best unchanged node once `selected` is in C
+      spec_node = -1;
+      if (j + 1 < a.nb) {
+        const int n1 = s1k ? key_node(s1k) : -1, n2 = s2k ? key_node(s2k) : -1;
+        spec_node = n1 != selected ? n1 : n2;
+        if (spec_node >= 0) fetch(spec_node, j + 2, spec_val);
       }
     }
     KSG_STAMP(4);
-    if (j + 1 < a.nb) prefetch(j + 1);   // overlaps the commit barrier
-    int selected = -1;
-    uint32_t status = 0;
-    if (g.nfeas == 1) {
-      selected = g.minidx;
-    } else if (g.nfeas >= 2) {
-      status |= KSG_ST_SCORED;
-      if (ge) status |= KSG_ST_SCORE_ERROR;
-      else selected = key_node(gb);
-    }
-    uint32_t score_skip;
-    ipa_skip_bits(prof, p, status, score_skip);
-    if (tid == 0) {
-      if (selected >= 0) {
-        commit_node(c, requested, nonzero, pod_count, a.st.cnt, a.st.tab, a.st.tmpl_total, p,
-                    v.commit >= 0 ? v.P + v.commit : nullptr, selected);
-        if (!((s_cmask[selected >> 5] >> (selected & 31)) & 1u)) {
-          s_cmask[selected >> 5] |= 1u << (selected & 31);
-          s_clist[s_nc] = selected;
-          s_nc = s_nc + 1;
-        }
-      }
-      const int o = a.out0 + j;
-      a.placements[o] = selected;
-      if (a.results) {
-        ksg_result res;
-        res.selected = selected;
-        res.n_feasible = g.nfeas;
-        res.status = status;
-        res.score_skip = score_skip;
-        a.results[o] = res;
-      }
-    }
     __syncthreads();
     KSG_STAMP(5);
   }
@@ -471,17 +829,6 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2(BatchArgs a) {
 }
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
-__device__ __forceinline__ int64_t wave_min64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += (int64_t)__shfl_xor(v, o, 64);
-  return v;
-}
-
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
   constexpr int NW = BLOCK / 64;
@@ -915,7 +1262,10 @@ struct ksg_ctx {
   int32_t* d_pc0 = nullptr;
   // batched-path buffers (lazily allocated)
   uint64_t* d_rec = nullptr;
+  int32_t* d_img = nullptr;
   int32_t* d_pmax = nullptr;
+  P1Stats* d_p1 = nullptr;
+  uint64_t* d_top = nullptr;
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
   unsigned long long* d_stamps = nullptr;   // KSG_STAMPS diagnostic build only
 };
@@ -963,7 +1313,10 @@ void free_all(ksg_ctx* ctx) {
   for (void* p : ctx->allocs) (void)hipFree(p);
   ctx->allocs.clear();
   ctx->d_rec = nullptr;
+  ctx->d_img = nullptr;
   ctx->d_pmax = nullptr;
+  ctx->d_p1 = nullptr;
+  ctx->d_top = nullptr;
   ctx->d_stamps = nullptr;
 }
 
@@ -1114,7 +1467,10 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   if (!ctx->d_rec) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rec, (size_t)KSG_BATCH_MAX * N))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_img, (size_t)KSG_BATCH_MAX * N))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_pmax, (size_t)2 * KSG_BATCH_MAX))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_p1, (size_t)KSG_BATCH_MAX))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_top, (size_t)KSG_BATCH_MAX * KSG_BATCH_MAX))) return rc;
     HIPC(ctx, hipMemsetAsync(ctx->d_pmax, 0, sizeof(int32_t) * 2 * KSG_BATCH_MAX, ctx->stream));
   }
   BatchArgs b{};
@@ -1124,7 +1480,10 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   b.prog = ctx->d_prog;
   b.prof = d_prof;
   b.rec = ctx->d_rec;
+  b.img = ctx->d_img;
   b.pmax = ctx->d_pmax;
+  b.p1 = ctx->d_p1;
+  b.top = ctx->d_top;
   b.placements = d_pl;
   b.results = d_res;
 #ifdef KSG_STAMPS
@@ -1136,12 +1495,14 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   b.stamps = ctx->d_stamps;
 #endif
   // Plan batches so that phase 2's LDS preload (changed-node bitmap + pod
-  // records + the program range of the batch) fits the dynamic LDS budget.
+  // records + the program range of the batch + one slot of live resource
+  // columns per pod) fits the dynamic LDS budget.
   constexpr size_t kLdsBudget = 120 * 1024;
-  const size_t cm_bytes = 4 * (size_t)((((N + 31) / 32) + 3) & ~3);
+  const size_t cm_words = (size_t)((((N + 31) / 32) + 3) & ~3);
+  const size_t slot_bytes = 8 * (size_t)(2 * ctx->c.R + 4);
   static bool attr_set = false;
   if (!attr_set) {
-    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)kLdsBudget));
     attr_set = true;
   }
@@ -1159,7 +1520,8 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
         lo = std::min<int64_t>(lo, q.blob);
         hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
       }
-      bytes = cm_bytes + (size_t)nb * sizeof(ksg_pod) + 4 * (size_t)(hi - lo);
+      const size_t words = (cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3;
+      bytes = 4 * words + (size_t)nb * slot_bytes;
       if (bytes <= kLdsBudget || nb == 1) break;
       nb = std::max(1, nb / 2);
     }
@@ -1170,7 +1532,8 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     b.prog_lo = (int32_t)lo;
     b.prog_len = (int32_t)(hi - lo);
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, b);
-    hipLaunchKernelGGL(ksg_batch_phase2<512>, dim3(1), dim3(512), bytes, ctx->stream, b);
+    hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
+    hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
     off += nb;
   }
   HIPC(ctx, hipGetLastError());

@@ -79,9 +79,8 @@ __device__ __forceinline__ int64_t div_nonneg(int64_t x, int64_t a) {
 }
 
 // ---- node sources ------------------------------------------------------------
-// The plugin code reads a node's static columns through an accessor: GNode
-// reads the SoA columns in global memory, LNode a copy of the node in an LDS
-// slot (phase 2 of the batched path keeps the nodes it re-evaluates there).
+// The plugin code reads a node's static columns through an accessor (GNode:
+// the SoA columns in global memory), so a kernel can substitute its own copy.
 struct GNode {
   const DevCluster* c;
   int n;
@@ -95,40 +94,6 @@ struct GNode {
   __device__ __forceinline__ uint32_t taint(int s) const { return c->taints[(size_t)s * c->N + n]; }
   __device__ __forceinline__ uint32_t image(int s) const { return c->images[(size_t)s * c->N + n]; }
   __device__ __forceinline__ bool unsched() const { return c->unsched[n] != 0; }
-};
-
-// LDS slot layout of a cached node (int32 words; the same for every slot).
-struct SlotLayout {
-  int alloc, req, nz, pc, allowed, unsched, lab, num, numok, taint, img, words;
-};
-__device__ __forceinline__ SlotLayout slot_layout(const DevCluster& c) {
-  SlotLayout s;
-  s.alloc = 0;
-  s.req = 2 * c.R;
-  s.nz = 4 * c.R;
-  s.pc = s.nz + 4;
-  s.allowed = s.pc + 1;
-  s.unsched = s.allowed + 1;
-  s.lab = s.unsched + 1;
-  s.num = s.lab + c.L;
-  s.numok = s.num + 2 * c.L;
-  s.taint = s.numok + c.L;
-  s.img = s.taint + c.T;
-  s.words = (s.img + c.I + 1) & ~1;   // keep int64 fields 8-byte aligned
-  return s;
-}
-struct LNode {
-  const int32_t* w;        // slot base (LDS)
-  const SlotLayout* lay;
-  __device__ __forceinline__ uint32_t label(int col) const { return (uint32_t)w[lay->lab + col]; }
-  __device__ __forceinline__ bool num(int col, int64_t& x) const {
-    if (!w[lay->numok + col]) return false;
-    x = (int64_t)(((uint64_t)(uint32_t)w[lay->num + 2 * col + 1] << 32) | (uint32_t)w[lay->num + 2 * col]);
-    return true;
-  }
-  __device__ __forceinline__ uint32_t taint(int s) const { return (uint32_t)w[lay->taint + s]; }
-  __device__ __forceinline__ uint32_t image(int s) const { return (uint32_t)w[lay->img + s]; }
-  __device__ __forceinline__ bool unsched() const { return w[lay->unsched] != 0; }
 };
 
 // ---- requirement programs (encoder.py grammar); P = pod blob in LDS -------

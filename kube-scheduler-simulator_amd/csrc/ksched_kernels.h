@@ -349,6 +349,7 @@ struct NodeEval {
   int64_t part;   // Σ weight x score over Fit, BalancedAllocation, ImageLocality
   int64_t rt;     // TaintToleration raw score
   int64_t ra;     // NodeAffinity raw score
+  int64_t img;    // weight x ImageLocality score (part of `part`)
 };
 
 // RunFilterPlugins (first rejection ends the node) + the raw Score() of every
@@ -361,7 +362,7 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
                                                   int64_t* cnorm, const TopoCtx* tc = nullptr) {
   const ksg_pod& p = *v.p;
   const int N = c.N;
-  NodeEval e{0, 0, 0, 0};
+  NodeEval e{0, 0, 0, 0, 0};
   uint32_t st = 0;
   if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) {
     st = KSG_FS_NOT_EVALUATED;
@@ -420,7 +421,8 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
   }
   if (v.smask & bit(KSG_PL_IMAGE_LOCALITY)) {
     const int64_t s = image_score(c, nd, v.P, v.img, p.n_containers);
-    e.part += s * v.w_img;
+    e.img = s * v.w_img;
+    e.part += e.img;
     if (craw) { craw[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; cnorm[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; }
   }
   if (v.smask & bit(KSG_PL_TAINT_TOLERATION)) {

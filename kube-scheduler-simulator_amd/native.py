@@ -237,6 +237,7 @@ class Engine:
 
     def set_profile(self, prof_fields: dict):
         self._check(self._set_profile(self.ctx, C.byref(make_profile(prof_fields))))
+        self.profile_fields = prof_fields
 
     @property
     def n_nodes(self) -> int:

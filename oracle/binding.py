@@ -49,8 +49,19 @@ class Oracle(native.Engine):
         import numpy as np
         R = len(profiles)
         pl = np.zeros((R, count), np.int32)
+        sums = np.zeros(R, native.SUMMARY_DTYPE)
+        n_res = int(self._m.nodes.n_res)
+        own = getattr(self, "profile_fields", None)
         for r, prof in enumerate(profiles):
             self.reset_state()
             self.set_profile(prof)
             pl[r], _ = self.run_queue(first, count, results=False)
-        return pl, None
+            req, _, _ = self.read_state(n_res)
+            h = 0xcbf29ce484222325
+            for b in pl[r].astype("<i4").tobytes():
+                h = ((h ^ b) * 0x100000001b3) & 0xffffffffffffffff
+            sums[r] = (int((pl[r] >= 0).sum()), int((pl[r] < 0).sum()), h, int(req[0].sum()), int(req[1].sum()))
+        self.reset_state()
+        if own is not None:
+            self.set_profile(own)
+        return pl, sums

@@ -23,8 +23,8 @@ fn = eng.lib.ksg_debug_stamps
 fn.argtypes = [C.c_void_p, C.c_void_p]
 assert fn(eng.ctx, st) == 0
 tot = sum(st[1:])
-names = ["(start)", "recompute changed nodes", "barrier after recompute", "scan records",
-         "reduce + barrier (+stale rescan)", "commit + barrier"]
+names = ["(start)", "A: changed nodes + top sets", "barrier 1", "B: decide (+rescan)",
+         "B: next-pod LDS writes", "barrier 2 (waits for the assume)"]
 print(f"{n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build)")
 for i in range(1, 6):
     print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")

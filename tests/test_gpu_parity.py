@@ -130,9 +130,16 @@ def test_replicas_match_sequential_oracle(gpu, oracle):
     gpu.load(enc, profs[0])
     oracle.load(enc, profs[0])
     pl, sums = gpu.run_replicas(profs, 0, len(pods))
-    want, _ = oracle.run_replicas(profs, 0, len(pods))
+    want, wsums = oracle.run_replicas(profs, 0, len(pods))
     np.testing.assert_array_equal(pl, want)
     assert (sums["scheduled"] + sums["unschedulable"] == len(pods)).all()
+    for f in wsums.dtype.names:
+        np.testing.assert_array_equal(sums[f], wsums[f], err_msg=f)
+    # the sweep entry point (world 1: no collective) returns the same
+    replicas = pkg("replicas")
+    spl, ssm = replicas.run_sweep(gpu, profs, 0, len(pods))
+    np.testing.assert_array_equal(spl, want)
+    np.testing.assert_array_equal(ssm[:, 0], wsums["scheduled"])
     # replicas start from (and do not modify) the context's own state
     R = len(enc.cluster.res_names)
     assert int(gpu.read_state(R)[2].sum()) == 0
