@@ -253,6 +253,44 @@ int ksg_reset_state(ksg_ctx* ctx);
  * between HIP events recorded on the stream the kernel was launched on. */
 int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
 
+/* ---- bulk result-store serialiser (host code; no device needed) ---------
+ * Emits the filter-result, score-result and finalscore-result annotation
+ * values of one pod straight from its capture SoA, byte-identical to
+ * resultstore.Store.GetStoredResult (store.go:133-198) after the wrapped
+ * plugins' AddFilterResult (store.go:423), AddScoreResult (:461) and
+ * AddNormalizedScoreResult (:481) calls, i.e. Go encoding/json of the maps. */
+typedef struct ksg_names {
+  int32_t n_nodes;
+  const char* const* node;         /* [n_nodes] node names (UTF-8)                    */
+  const char* const* plugin;       /* [KSG_NPLUGINS] names the Store keys plugins by  */
+  int32_t n_res;
+  const char* const* res;          /* [n_res] resource names ("Insufficient <name>")  */
+  int32_t n_taint_vocab;
+  const char* const* taint;        /* [n_taint_vocab] "{<key>: <value>}"               */
+  int32_t max_taints;
+  const uint32_t* taints;          /* [max_taints][n_nodes] as in ksg_nodes.taints    */
+} ksg_names;
+
+typedef struct ksg_annotate_in {
+  int32_t n_filter;
+  const int32_t* filter_order;     /* Filter plugins that ran (PreFilter not Skip), in run order */
+  int32_t n_score;
+  const int32_t* score_order;      /* Score plugins that ran (PreScore not Skip)      */
+  uint32_t normalize_mask;         /* bit p: plugin p has ScoreExtensions             */
+  const int64_t* weight;           /* [KSG_NPLUGINS] Store score weight (0 = missing) */
+  int32_t n_feasible;              /* < 2: no score / finalscore entries              */
+  const uint32_t* fstatus;         /* [n_nodes]  one pod's capture (ksg_capture)       */
+  const int64_t* raw;              /* [KSG_NPLUGINS][n_nodes]                          */
+  const int64_t* norm;             /* [KSG_NPLUGINS][n_nodes]                          */
+} ksg_annotate_in;
+
+typedef struct ksg_annotator ksg_annotator;
+int ksg_annotator_new(const ksg_names* names, ksg_annotator** out);
+int ksg_annotator_free(ksg_annotator* a);
+/* json[0..2] / len[0..2]: filter-result, score-result, finalscore-result.  The
+ * strings are owned by the annotator and valid until its next call. */
+int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const char** json, int64_t* len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,7 +91,7 @@ class _PodResult:
     """resultstore.result (store.go:37-90)."""
     __slots__ = ("selected_node", "prescore", "score", "finalscore", "prefilter_status",
                  "prefilter_result", "filter", "postfilter", "permit", "permit_timeout",
-                 "reserve", "prebind", "bind", "custom")
+                 "reserve", "prebind", "bind", "custom", "serialized")
 
     def __init__(self):
         self.selected_node = ""
@@ -108,6 +108,7 @@ class _PodResult:
         self.prebind: Dict[str, str] = {}
         self.bind: Dict[str, str] = {}
         self.custom: Dict[str, str] = {}
+        self.serialized: Dict[str, str] = {}   # annotation key -> JSON emitted by the native serialiser
 
 
 class ResultStore:
@@ -184,6 +185,11 @@ class ResultStore:
     def AddCustomResult(self, namespace, pod, key, result):
         self._get(namespace, pod).custom[key] = result
 
+    def AddSerializedResult(self, namespace, pod, key, value: str):
+        """Annotation value already serialised from the capture SoA
+        (native.Annotator, byte-identical to marshalling the map)."""
+        self._get(namespace, pod).serialized[key] = value
+
     def DeleteData(self, namespace, pod):
         self.results.pop(namespace + "/" + pod, None)
 
@@ -206,6 +212,7 @@ class ResultStore:
             PREBIND: go_marshal(r.prebind),
             BIND: go_marshal(r.bind),
         }
+        a.update(r.serialized)
         for k, v in r.custom.items():
             a.setdefault(k, v)
         a[SELECTED_NODE] = r.selected_node

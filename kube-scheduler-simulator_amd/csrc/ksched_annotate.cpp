@@ -1,0 +1,287 @@
+// Bulk result-store serialiser, host code in libksched.so.
+//
+// The wrapped plugins write one map entry per (node, plugin) into
+// resultstore.Store under a global mutex (store.go:423 AddFilterResult, :461
+// AddScoreResult, :481 AddNormalizedScoreResult), and GetStoredResult
+// json.Marshals the maps (store.go:133-198, add*ResultToMap :200-420).  Here
+// the three O(N) annotations (filter-result, score-result, finalscore-result)
+// are emitted straight from one pod's capture SoA, byte-identical to Go's
+// encoding/json output: map keys sorted bytewise, HTML-safe escaping of < > &,
+// U+2028/U+2029 escaped, invalid UTF-8 replaced by U+FFFD, \b \f \n \r \t
+// short escapes, other control characters as \u00XX.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ksched.h"
+
+namespace {
+
+void go_string(std::string& o, const char* s) {
+  static const char* hex = "0123456789abcdef";
+  o.push_back('"');
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(s);
+  while (*p) {
+    const unsigned char c = *p;
+    if (c < 0x80) {
+      switch (c) {
+        case '"': o += "\\\""; break;
+        case '\\': o += "\\\\"; break;
+        case '\n': o += "\\n"; break;
+        case '\r': o += "\\r"; break;
+        case '\t': o += "\\t"; break;
+        case '\b': o += "\\b"; break;
+        case '\f': o += "\\f"; break;
+        case '<': o += "\\u003c"; break;
+        case '>': o += "\\u003e"; break;
+        case '&': o += "\\u0026"; break;
+        default:
+          if (c < 0x20) {
+            o += "\\u00";
+            o.push_back(hex[c >> 4]);
+            o.push_back(hex[c & 15]);
+          } else {
+            o.push_back((char)c);
+          }
+      }
+      p++;
+      continue;
+    }
+    // decode one UTF-8 sequence (utf8.DecodeRuneInString rules)
+    int len = 0;
+    uint32_t cp = 0, lo = 0;
+    if (c >= 0xC2 && c <= 0xDF) { len = 2; cp = c & 0x1F; lo = 0x80; }
+    else if (c >= 0xE0 && c <= 0xEF) { len = 3; cp = c & 0x0F; lo = 0x800; }
+    else if (c >= 0xF0 && c <= 0xF4) { len = 4; cp = c & 0x07; lo = 0x10000; }
+    bool ok = len > 0;
+    for (int i = 1; ok && i < len; i++) {
+      if ((p[i] & 0xC0) != 0x80) ok = false;
+      else cp = (cp << 6) | (p[i] & 0x3F);
+    }
+    if (ok && (cp < lo || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF))) ok = false;
+    if (!ok) {
+      o += "\xEF\xBF\xBD";   // U+FFFD, one invalid byte consumed
+      p++;
+      continue;
+    }
+    if (cp == 0x2028) o += "\\u2028";
+    else if (cp == 0x2029) o += "\\u2029";
+    else o.append(reinterpret_cast<const char*>(p), len);
+    p += len;
+  }
+  o.push_back('"');
+}
+
+void go_int(std::string& o, int64_t v) {
+  char b[24];
+  int n = 0;
+  uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+  do { b[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+  o.push_back('"');
+  if (v < 0) o.push_back('-');
+  while (n) o.push_back(b[--n]);
+  o.push_back('"');
+}
+
+const char* kFitRes[3] = {"cpu", "memory", "ephemeral-storage"};
+
+}  // namespace
+
+struct ksg_annotator {
+  int32_t N = 0;
+  std::vector<std::string> node_json;     // escaped, quoted node names
+  std::vector<int32_t> node_order;        // node indices sorted bytewise by name
+  std::string plugin[KSG_NPLUGINS];       // escaped, quoted plugin names
+  std::string plugin_raw[KSG_NPLUGINS];
+  std::vector<std::string> res;           // resource names
+  std::vector<std::string> taint;         // "{key: value}" per taint-vocab id
+  int32_t max_taints = 0;
+  std::vector<uint32_t> taints;           // [max_taints][N]
+  std::string out[3];
+};
+
+extern "C" int ksg_annotator_new(const ksg_names* names, ksg_annotator** out) {
+  if (!names || !out || names->n_nodes < 0 || (names->n_nodes > 0 && !names->node) || !names->plugin)
+    return KSG_E_INVALID;
+  ksg_annotator* a = new (std::nothrow) ksg_annotator();
+  if (!a) return KSG_E_NOMEM;
+  a->N = names->n_nodes;
+  a->node_json.resize(a->N);
+  a->node_order.resize(a->N);
+  for (int i = 0; i < a->N; i++) {
+    go_string(a->node_json[i], names->node[i] ? names->node[i] : "");
+    a->node_order[i] = i;
+  }
+  std::stable_sort(a->node_order.begin(), a->node_order.end(), [&](int x, int y) {
+    return std::strcmp(names->node[x], names->node[y]) < 0;   // bytewise (unsigned) like Go's string <
+  });
+  for (int p = 0; p < KSG_NPLUGINS; p++) {
+    const char* s = names->plugin[p] ? names->plugin[p] : "";
+    a->plugin_raw[p] = s;
+    go_string(a->plugin[p], s);
+  }
+  for (int r = 0; r < names->n_res; r++) a->res.emplace_back(names->res[r] ? names->res[r] : "");
+  for (int t = 0; t < names->n_taint_vocab; t++) a->taint.emplace_back(names->taint[t] ? names->taint[t] : "");
+  a->max_taints = names->max_taints;
+  if (names->max_taints > 0 && names->taints)
+    a->taints.assign(names->taints, names->taints + (size_t)names->max_taints * a->N);
+  *out = a;
+  return KSG_OK;
+}
+
+extern "C" int ksg_annotator_free(ksg_annotator* a) {
+  delete a;
+  return KSG_OK;
+}
+
+namespace {
+
+// framework.py Decoder.message restated: status word -> upstream message.
+bool filter_message(const ksg_annotator* a, uint32_t st, int n, std::string& msg) {
+  const int pl = (int)(st & 0xFF) - 1;
+  const uint32_t reason = st >> 8;
+  msg.clear();
+  switch (pl) {
+    case KSG_PL_NODE_UNSCHEDULABLE: msg = "node(s) were unschedulable"; return true;
+    case KSG_PL_NODE_NAME: msg = "node(s) didn't match the requested node name"; return true;
+    case KSG_PL_TAINT_TOLERATION: {
+      if ((int)reason >= a->max_taints) return false;
+      const uint32_t id = a->taints[(size_t)reason * a->N + n];
+      if (id == 0 || id > a->taint.size()) return false;
+      msg = "node(s) had untolerated taint " + a->taint[id - 1];
+      return true;
+    }
+    case KSG_PL_NODE_AFFINITY: msg = "node(s) didn't match Pod's node affinity/selector"; return true;
+    case KSG_PL_NODE_RESOURCES_FIT: {
+      // noderesources.fitsRequest order: pods, cpu, memory, ephemeral, scalars by column
+      bool first = true;
+      auto add = [&](const std::string& s) {
+        if (!first) msg += ", ";
+        msg += s;
+        first = false;
+      };
+      if (reason & 1u) add("Too many pods");
+      for (int r = 0; r < (int)a->res.size(); r++)
+        if (reason & (1u << (r + 1))) add(std::string("Insufficient ") + (r < 3 ? kFitRes[r] : a->res[r].c_str()));
+      return true;
+    }
+    case KSG_PL_POD_TOPOLOGY_SPREAD:
+      msg = reason == 1 ? "node(s) didn't match pod topology spread constraints (missing required label)"
+                        : "node(s) didn't match pod topology spread constraints";
+      return true;
+    case KSG_PL_INTER_POD_AFFINITY:
+      if (reason == 1) msg = "node(s) didn't match pod affinity rules";
+      else if (reason == 2) msg = "node(s) didn't match pod anti-affinity rules";
+      else if (reason == 3) msg = "node(s) didn't satisfy existing pods anti-affinity rules";
+      else return false;
+      return true;
+    default:
+      return false;
+  }
+}
+
+std::vector<int> sorted_plugins(const ksg_annotator* a, const int32_t* ids, int n) {
+  std::vector<int> v(ids, ids + n);
+  std::sort(v.begin(), v.end(), [&](int x, int y) { return a->plugin_raw[x] < a->plugin_raw[y]; });
+  return v;
+}
+
+}  // namespace
+
+extern "C" int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const char** json, int64_t* len) {
+  if (!a || !in || !json || !len || !in->fstatus) return KSG_E_INVALID;
+  if (in->n_filter < 0 || in->n_filter > KSG_NPLUGINS || in->n_score < 0 || in->n_score > KSG_NPLUGINS)
+    return KSG_E_INVALID;
+  for (int i = 0; i < in->n_filter; i++)
+    if (in->filter_order[i] < 0 || in->filter_order[i] >= KSG_NPLUGINS) return KSG_E_INVALID;
+  for (int i = 0; i < in->n_score; i++)
+    if (in->score_order[i] < 0 || in->score_order[i] >= KSG_NPLUGINS) return KSG_E_INVALID;
+  const int N = a->N;
+  // ---- filter-result (store.go:423; nodes outside PreFilterResult absent)
+  std::string& f = a->out[0];
+  f.clear();
+  f.push_back('{');
+  if (in->n_filter > 0) {
+    // position of each plugin in run order; a node's entries are the plugins
+    // up to and including the first rejecting one
+    int pos[KSG_NPLUGINS];
+    for (int p = 0; p < KSG_NPLUGINS; p++) pos[p] = -1;
+    for (int i = 0; i < in->n_filter; i++) pos[in->filter_order[i]] = i;
+    const std::vector<int> by_name = sorted_plugins(a, in->filter_order, in->n_filter);
+    std::string msg;
+    bool first_node = true;
+    for (int k = 0; k < N; k++) {
+      const int n = a->node_order[k];
+      const uint32_t st = in->fstatus[n];
+      if (st == KSG_FS_NOT_EVALUATED) continue;
+      const int fail = st == 0 ? -1 : (int)(st & 0xFF) - 1;
+      const int last = fail < 0 ? in->n_filter : (fail < KSG_NPLUGINS ? pos[fail] : -1);
+      if (last < 0) return KSG_E_INVALID;   // rejected by a plugin that did not run
+      if (fail >= 0 && !filter_message(a, st, n, msg)) return KSG_E_INVALID;
+      if (!first_node) f.push_back(',');
+      first_node = false;
+      f += a->node_json[n];
+      f += ":{";
+      bool first = true;
+      for (int p : by_name) {
+        if (pos[p] > last) continue;
+        if (!first) f.push_back(',');
+        first = false;
+        f += a->plugin[p];
+        f.push_back(':');
+        if (p == fail) go_string(f, msg.c_str());
+        else f += "\"passed\"";
+      }
+      f.push_back('}');
+    }
+  }
+  f.push_back('}');
+  // ---- score-result / finalscore-result (store.go:461, :481, :504-507)
+  std::string& s = a->out[1];
+  std::string& t = a->out[2];
+  s.clear();
+  t.clear();
+  s.push_back('{');
+  t.push_back('{');
+  if (in->n_feasible >= 2 && in->n_score > 0) {
+    if (!in->raw || !in->weight) return KSG_E_INVALID;
+    const std::vector<int> by_name = sorted_plugins(a, in->score_order, in->n_score);
+    bool first_node = true;
+    for (int k = 0; k < N; k++) {
+      const int n = a->node_order[k];
+      if (in->fstatus[n] != 0) continue;
+      if (!first_node) { s.push_back(','); t.push_back(','); }
+      first_node = false;
+      s += a->node_json[n];
+      s += ":{";
+      t += a->node_json[n];
+      t += ":{";
+      bool first = true;
+      for (int p : by_name) {
+        if (!first) { s.push_back(','); t.push_back(','); }
+        first = false;
+        s += a->plugin[p];
+        s.push_back(':');
+        t += a->plugin[p];
+        t.push_back(':');
+        const int64_t raw = in->raw[(size_t)p * N + n];
+        go_int(s, raw);
+        const bool normed = ((in->normalize_mask >> p) & 1u) && in->norm;
+        const uint64_t v = (uint64_t)(normed ? in->norm[(size_t)p * N + n] : raw) * (uint64_t)in->weight[p];
+        go_int(t, (int64_t)v);   // Go int64 multiplication wraps
+      }
+      s.push_back('}');
+      t.push_back('}');
+    }
+  }
+  s.push_back('}');
+  t.push_back('}');
+  for (int i = 0; i < 3; i++) {
+    json[i] = a->out[i].c_str();
+    len[i] = (int64_t)a->out[i].size();
+  }
+  return KSG_OK;
+}

@@ -105,9 +105,11 @@ class DebuggableScheduler:
     """Framework loop + wrapped-plugin recording, with the evaluator on the GPU."""
 
     def __init__(self, nodes: Sequence[m.Node], pods: Sequence[m.Pod], prof: P.Profile,
-                 engine: Optional[native.Engine] = None, bound: Sequence = ()):
+                 engine: Optional[native.Engine] = None, bound: Sequence = (), native_annotations: bool = True):
         """`pods` holds every pod that will ever be bound or scheduled;
-        `bound` = [(pod_index, node_index)] already running at start."""
+        `bound` = [(pod_index, node_index)] already running at start.
+        `native_annotations`: emit filter/score/finalscore-result with the
+        native serialiser (ksg_annotate) instead of per-entry Store writes."""
         self.nodes = list(nodes)
         self.pods = list(pods)
         self.prof = prof
@@ -121,6 +123,14 @@ class DebuggableScheduler:
         self.node_names = self.enc.cluster.node_names
         self.enabled = set(prof.enabled_ids())
         self.names_enabled = {n for n, _ in prof.plugins}
+        self.annotator = None
+        if native_annotations:
+            cl = self.enc.cluster
+            self.annotator = native.Annotator(
+                cl.node_names, P.PLUGIN_NAMES, cl.res_names,
+                [f"{{{t.key}: {t.value}}}" for t in cl.taint_vocab], cl.arrays["taints"])
+            self._weights = np.array([self.store.score_plugin_weight.get(n, 0) for n in P.PLUGIN_NAMES], np.int64)
+            self._norm_mask = sum(1 << pid for pid in range(len(P.PLUGIN_NAMES)) if P.EXT[pid][4])
 
     # ---- one cycle --------------------------------------------------------
     def evaluate(self, pi: int) -> PodCycle:
@@ -164,6 +174,8 @@ class DebuggableScheduler:
             st.AddPreFilterResult(ns, name, pname, "" if (fskip >> pid) & 1 else A.SUCCESS, node_names)
         # Filter
         order = [p for p in self.prof.filter_order() if not (fskip >> p) & 1]
+        if self.annotator is not None:
+            return self._record_native(cyc, ns, name, order)
         evaluated = []
         for n in range(len(self.nodes)):
             s = int(cyc.fstatus[n])
@@ -199,6 +211,31 @@ class DebuggableScheduler:
                 if P.EXT[pid][4]:
                     for n in feas:
                         st.AddNormalizedScoreResult(ns, name, self.node_names[n], pname, int(cyc.norm[pid, n]))
+        self._record_bind(cyc, ns, name)
+
+    def _record_native(self, cyc: PodCycle, ns: str, name: str, order: List[int]):
+        """Filter/Score/NormalizeScore entries serialised in one native call."""
+        st = self.store
+        score_order: List[int] = []
+        if cyc.n_feasible >= 2:
+            score_order = [p for p in self.prof.score_order() if not (cyc.score_skip >> p) & 1]
+        f, s, t = self.annotator.annotate(order, score_order, self._norm_mask, self._weights, cyc.n_feasible,
+                                          cyc.fstatus, cyc.raw, cyc.norm)
+        st.AddSerializedResult(ns, name, A.FILTER, f)
+        st.AddSerializedResult(ns, name, A.SCORE, s)
+        st.AddSerializedResult(ns, name, A.FINALSCORE, t)
+        if cyc.n_feasible == 0:
+            if "DefaultPreemption" in self.names_enabled:
+                evaluated = np.nonzero(cyc.fstatus != FS_NOT_EVALUATED)[0]
+                st.AddPostFilterResult(ns, name, "", "DefaultPreemption", [self.node_names[n] for n in evaluated])
+            return
+        if cyc.n_feasible >= 2:
+            for pid in self.prof.prescore_order():
+                st.AddPreScoreResult(ns, name, P.PLUGIN_NAMES[pid], "" if (cyc.score_skip >> pid) & 1 else A.SUCCESS)
+        self._record_bind(cyc, ns, name)
+
+    def _record_bind(self, cyc: PodCycle, ns: str, name: str):
+        st = self.store
         if cyc.selected < 0:
             return
         # Reserve / Permit / PreBind / Bind of the default plugins.

@@ -285,3 +285,78 @@ class Engine:
 
     def reset_state(self):
         self._check(self._reset_state(self.ctx))
+
+
+# ---- bulk result-store serialiser (host code in libksched.so) ----------------
+class KsgNames(C.Structure):
+    _fields_ = [("n_nodes", C.c_int32), ("node", C.POINTER(C.c_char_p)), ("plugin", C.POINTER(C.c_char_p)),
+                ("n_res", C.c_int32), ("res", C.POINTER(C.c_char_p)), ("n_taint_vocab", C.c_int32),
+                ("taint", C.POINTER(C.c_char_p)), ("max_taints", C.c_int32), ("taints", u32p)]
+
+
+class KsgAnnotateIn(C.Structure):
+    _fields_ = [("n_filter", C.c_int32), ("filter_order", i32p), ("n_score", C.c_int32), ("score_order", i32p),
+                ("normalize_mask", C.c_uint32), ("weight", i64p), ("n_feasible", C.c_int32),
+                ("fstatus", u32p), ("raw", i64p), ("norm", i64p)]
+
+
+def _cstrs(items):
+    arr = (C.c_char_p * max(len(items), 1))()
+    for i, s in enumerate(items):
+        arr[i] = s.encode("utf-8", errors="surrogatepass")
+    return arr
+
+
+class Annotator:
+    """ksg_annotator: filter-result / score-result / finalscore-result JSON of
+    one pod straight from its capture SoA (resultstore.Store output bytes)."""
+
+    def __init__(self, node_names, plugin_names, res_names, taint_strings, taints: np.ndarray,
+                 lib_path: Optional[str] = None):
+        path = lib_path or LIB_PATH
+        if not os.path.exists(path):
+            raise KschedError(f"{path} not found: run __graft_entry__.build()")
+        self.lib = C.CDLL(path)
+        f = _bind(self.lib, "ksg_")
+        self._new = f("annotator_new", C.c_int, C.POINTER(KsgNames), C.POINTER(C.c_void_p))
+        self._free = f("annotator_free", C.c_int, C.c_void_p)
+        self._annotate = f("annotate", C.c_int, C.c_void_p, C.POINTER(KsgAnnotateIn),
+                           C.POINTER(C.c_char_p), C.POINTER(C.c_int64))
+        self._keep = [_cstrs(node_names), _cstrs(plugin_names), _cstrs(res_names), _cstrs(taint_strings),
+                      np.ascontiguousarray(taints, np.uint32)]
+        names = KsgNames(len(node_names), self._keep[0], self._keep[1], len(res_names), self._keep[2],
+                         len(taint_strings), self._keep[3], int(self._keep[4].shape[0]),
+                         _ptr(self._keep[4], u32p))
+        self.h = C.c_void_p()
+        rc = self._new(C.byref(names), C.byref(self.h))
+        if rc != 0:
+            raise KschedError(f"ksg_annotator_new rc={rc}")
+        self.n_nodes = len(node_names)
+
+    def annotate(self, filter_order, score_order, normalize_mask: int, weight, n_feasible: int,
+                 fstatus: np.ndarray, raw: np.ndarray, norm: np.ndarray):
+        fo = np.ascontiguousarray(filter_order, np.int32)
+        so = np.ascontiguousarray(score_order, np.int32)
+        w = np.ascontiguousarray(weight, np.int64)
+        fs = np.ascontiguousarray(fstatus, np.uint32)
+        rw = np.ascontiguousarray(raw, np.int64)
+        nm = np.ascontiguousarray(norm, np.int64)
+        inp = KsgAnnotateIn(len(fo), _ptr(fo, i32p), len(so), _ptr(so, i32p), normalize_mask, _ptr(w, i64p),
+                            n_feasible, _ptr(fs, u32p), _ptr(rw, i64p), _ptr(nm, i64p))
+        out = (C.c_char_p * 3)()
+        ln = (C.c_int64 * 3)()
+        rc = self._annotate(self.h, C.byref(inp), out, ln)
+        if rc != 0:
+            raise KschedError(f"ksg_annotate rc={rc}")
+        return tuple(C.string_at(out[i], ln[i]).decode("utf-8") for i in range(3))
+
+    def close(self):
+        if self.h:
+            self._free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
