@@ -282,6 +282,223 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
   }
 }
 
+// Diagnostic build (-DKSG_STAMPS): lane 0 of wave 0 sums s_memtime deltas per
+// segment of the phase-2 loop.  Never compiled into the measured library.
+#ifdef KSG_STAMPS
+#define KSG_STAMP(seg)                                                   \
+  do {                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();          \
+    if (tid == 0) { st_acc[seg] += _t - st_last; st_last = _t; }         \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+  } while (0)
+#else
+#define KSG_STAMP(seg) do {} while (0)
+#endif
+
+// Phase 2, scan variant (KSG_BATCH_MODE=scan): one workgroup walks the batch
+// in queue order, re-evaluates the changed nodes from global memory and scans
+// all N phase-1 records of every pod (three barriers per pod).  Kept as the
+// reference implementation of the batched scheme next to the top-set variant
+// below.
+// Diagnostic build (-DKSG_STAMPS): lane 0 of wave 0 sums s_memtime deltas per
+// segment of the phase-2 loop.  Never compiled into the measured library.
+constexpr int kRPT = 10;  // phase-1 records held in registers per lane (N <= 5120 at 512 lanes)
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2_scan(BatchArgs a) {
+  constexpr int NW = BLOCK / 64;
+  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
+  __shared__ ksg_profile s_prof;
+  __shared__ int32_t s_clist[KSG_BATCH_MAX];
+  __shared__ NodeEval s_ce[KSG_BATCH_MAX];
+  __shared__ int32_t s_pmax[2 * KSG_BATCH_MAX];
+  __shared__ int32_t s_nc;
+  __shared__ Red s_red[NW];
+  __shared__ uint64_t s_best[NW];
+  __shared__ uint32_t s_err[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const DevCluster& c = a.c;
+  const int N = c.N;
+  int64_t* requested = a.st.requested;
+  int64_t* nonzero = a.st.nonzero;
+  int32_t* pod_count = a.st.pod_count;
+  const int cm_words = (((N + 31) / 32) + 3) & ~3;
+  constexpr int POD_WORDS = sizeof(ksg_pod) / 4;
+  uint32_t* s_cmask = reinterpret_cast<uint32_t*>(s_dyn);
+  ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
+  int32_t* s_prog = s_dyn + cm_words + a.nb * POD_WORDS;
+
+  for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
+  for (int i = tid; i < a.nb * POD_WORDS; i += BLOCK)
+    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
+  for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
+  for (int i = tid; i < 2 * a.nb; i += BLOCK) s_pmax[i] = a.pmax[i];
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  if (tid == 0) s_nc = 0;
+
+  uint64_t rr[kRPT];
+  auto prefetch = [&](int j) {
+    const uint64_t* rec = a.rec + (size_t)j * N;
+#pragma unroll
+    for (int q = 0; q < kRPT; q++) {
+      const int n = tid + q * BLOCK;
+      rr[q] = n < N ? rec[n] : 0;
+    }
+  };
+  prefetch(0);
+  __syncthreads();
+
+#ifdef KSG_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
+  KSG_STAMP(0);
+  for (int j = 0; j < a.nb; j++) {
+    const ksg_pod& p = s_pods[j];
+    const ksg_profile& prof = s_prof;
+    const PodView v = make_view(c, prof, p, s_prog + (p.blob - a.prog_lo), a.prog);
+    const int nc = s_nc;
+    // re-evaluate the nodes assumed onto earlier in this batch, on live state
+    for (int i = tid; i < nc; i += BLOCK)
+      s_ce[i] = eval_node(c, prof, v, requested, nonzero, pod_count, s_clist[i], nullptr, nullptr);
+    KSG_STAMP(1);
+    __syncthreads();
+    KSG_STAMP(2);
+    const int64_t mt1 = s_pmax[2 * j], ma1 = s_pmax[2 * j + 1];
+    const uint64_t* rec = a.rec + (size_t)j * N;
+    Red r{0, 0, 0, 0x7fffffff};
+    uint64_t best = 0;
+    uint32_t err = 0;
+    auto visit = [&](uint64_t x, int n, int64_t mt, int64_t ma, bool stats) {
+      if (!(x >> 63)) return;
+      const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
+      if (stats) {
+        r.nfeas += 1;
+        r.minidx = min(r.minidx, n);
+        r.max_t = max(r.max_t, rt);
+        r.max_a = max(r.max_a, ra);
+      }
+      const uint64_t key = argmax_key(total_score(v, part, rt, ra, mt, ma, err, nullptr, nullptr), n);
+      best = key > best ? key : best;
+    };
+    auto visit_changed = [&](int64_t mt, int64_t ma, bool stats) {
+      for (int i = tid; i < nc; i += BLOCK) {
+        const NodeEval e = s_ce[i];
+        if (e.st != 0) continue;
+        const int n = s_clist[i];
+        if (stats) {
+          r.nfeas += 1;
+          r.minidx = min(r.minidx, n);
+          r.max_t = max(r.max_t, e.rt);
+          r.max_a = max(r.max_a, e.ra);
+        }
+        const uint64_t key = argmax_key(total_score(v, e.part, e.rt, e.ra, mt, ma, err, nullptr, nullptr), n);
+        best = key > best ? key : best;
+      }
+    };
+    auto scan = [&](int64_t mt, int64_t ma, bool stats) {
+#pragma unroll
+      for (int q = 0; q < kRPT; q++) {
+        const int n = tid + q * BLOCK;
+        if (n < N && !((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rr[q], n, mt, ma, stats);
+      }
+      for (int n = tid + kRPT * BLOCK; n < N; n += BLOCK)
+        if (!((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rec[n], n, mt, ma, stats);
+      visit_changed(mt, ma, stats);
+    };
+    scan(mt1, ma1, true);
+    KSG_STAMP(3);
+    {
+      Red w;
+      w.max_t = wave_max64(r.max_t);
+      w.max_a = wave_max64(r.max_a);
+      w.nfeas = wave_sum32(r.nfeas);
+      w.minidx = wave_min32(r.minidx);
+      best = wave_max_u64(best);
+      err = wave_or32(err);
+      if (lane == 0) { s_red[wv] = w; s_best[wv] = best; s_err[wv] = err; }
+    }
+    __syncthreads();
+    Red g{0, 0, 0, 0x7fffffff};
+    uint64_t gb = 0;
+    uint32_t ge = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      const Red w = s_red[i];
+      g.max_t = max(g.max_t, w.max_t);
+      g.max_a = max(g.max_a, w.max_a);
+      g.nfeas += w.nfeas;
+      g.minidx = min(g.minidx, w.minidx);
+      gb = s_best[i] > gb ? s_best[i] : gb;
+      ge |= s_err[i];
+    }
+    const bool stale_t = (v.smask & bit(KSG_PL_TAINT_TOLERATION)) && g.max_t != mt1;
+    const bool stale_a = (v.smask & bit(KSG_PL_NODE_AFFINITY)) && g.max_a != ma1;
+    if (g.nfeas >= 2 && (stale_t || stale_a)) {
+      // a holder of a phase-1 maximum was assumed full: renormalise with the
+      // live maxima (second scan; rare)
+      __syncthreads();
+      best = 0;
+      err = 0;
+      scan(g.max_t, g.max_a, false);
+      best = wave_max_u64(best);
+      err = wave_or32(err);
+      if (lane == 0) { s_best[wv] = best; s_err[wv] = err; }
+      __syncthreads();
+      gb = 0;
+      ge = 0;
+#pragma unroll
+      for (int i = 0; i < NW; i++) {
+        gb = s_best[i] > gb ? s_best[i] : gb;
+        ge |= s_err[i];
+      }
+    }
+    KSG_STAMP(4);
+    if (j + 1 < a.nb) prefetch(j + 1);   // overlaps the commit barrier
+    int selected = -1;
+    uint32_t status = 0;
+    if (g.nfeas == 1) {
+      selected = g.minidx;
+    } else if (g.nfeas >= 2) {
+      status |= KSG_ST_SCORED;
+      if (ge) status |= KSG_ST_SCORE_ERROR;
+      else selected = key_node(gb);
+    }
+    uint32_t score_skip;
+    ipa_skip_bits(prof, p, status, score_skip);
+    if (tid == 0) {
+      if (selected >= 0) {
+        commit_node(c, requested, nonzero, pod_count, a.st.cnt, a.st.tab, a.st.tmpl_total, p,
+                    v.commit >= 0 ? v.P + v.commit : nullptr, selected);
+        if (!((s_cmask[selected >> 5] >> (selected & 31)) & 1u)) {
+          s_cmask[selected >> 5] |= 1u << (selected & 31);
+          s_clist[s_nc] = selected;
+          s_nc = s_nc + 1;
+        }
+      }
+      const int o = a.out0 + j;
+      a.placements[o] = selected;
+      if (a.results) {
+        ksg_result res;
+        res.selected = selected;
+        res.n_feasible = g.nfeas;
+        res.status = status;
+        res.score_skip = score_skip;
+        a.results[o] = res;
+      }
+    }
+    __syncthreads();
+    KSG_STAMP(5);
+  }
+  for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
+#ifdef KSG_STAMPS
+  if (tid == 0 && a.stamps)
+    for (int i = 0; i < 6; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+#endif
+}
+
 // Phase 1b, one workgroup per pod j: the statistics phase 2 needs to update
 // pod j's result incrementally, and the top set T_j = the min(j + 1, nfeas)
 // best nodes by (total, lowest index) under the phase-1 maxima.  At most j
@@ -450,17 +667,6 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
 //      assumes the pod into its slot and stores the node's new columns.
 // Two barriers per pod; the next pod's records and top set are fetched into
 // registers during A and written to LDS during B.
-#ifdef KSG_STAMPS
-#define KSG_STAMP(seg)                                                   \
-  do {                                                                   \
-    __builtin_amdgcn_sched_barrier(0);                                   \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();          \
-    if (tid == 0) { st_acc[seg] += _t - st_last; st_last = _t; }         \
-    __builtin_amdgcn_sched_barrier(0);                                   \
-  } while (0)
-#else
-#define KSG_STAMP(seg) do {} while (0)
-#endif
 
 struct WRed {
   uint64_t k0, k1;
@@ -1267,6 +1473,7 @@ struct ksg_ctx {
   P1Stats* d_p1 = nullptr;
   uint64_t* d_top = nullptr;
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
+  int batch_mode = 0;  // env KSG_BATCH_MODE: 0 "scan" (default), 1 "topset"
   unsigned long long* d_stamps = nullptr;   // KSG_STAMPS diagnostic build only
 };
 
@@ -1500,10 +1707,13 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   constexpr size_t kLdsBudget = 120 * 1024;
   const size_t cm_words = (size_t)((((N + 31) / 32) + 3) & ~3);
   const size_t slot_bytes = 8 * (size_t)(2 * ctx->c.R + 4);
+  const bool topset = ctx->batch_mode == 1;
   static bool attr_set = false;
   if (!attr_set) {
     HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)kLdsBudget));
+    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
     attr_set = true;
   }
   (void)hipGetLastError();
@@ -1521,7 +1731,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
         hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
       }
       const size_t words = (cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3;
-      bytes = 4 * words + (size_t)nb * slot_bytes;
+      bytes = 4 * words + (topset ? (size_t)nb * slot_bytes : 0);
       if (bytes <= kLdsBudget || nb == 1) break;
       nb = std::max(1, nb / 2);
     }
@@ -1532,8 +1742,12 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     b.prog_lo = (int32_t)lo;
     b.prog_len = (int32_t)(hi - lo);
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, b);
-    hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
-    hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
+    if (topset) {
+      hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
+      hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
+    } else {
+      hipLaunchKernelGGL(ksg_batch_phase2_scan<512>, dim3(1), dim3(512), bytes, ctx->stream, b);
+    }
     off += nb;
   }
   HIPC(ctx, hipGetLastError());
@@ -1635,6 +1849,7 @@ int ksg_open(int device, ksg_ctx** out) {
     return KSG_E_DEVICE;
   }
   if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
+  if (const char* f = getenv("KSG_BATCH_MODE")) ctx->batch_mode = std::string(f) == "topset" ? 1 : 0;
   *out = ctx;
   return KSG_OK;
 }

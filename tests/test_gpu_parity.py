@@ -24,6 +24,26 @@ def gpu(built):
     return native.Engine(device=0)
 
 
+def _engine_with_batch_mode(mode):
+    import os
+    old = os.environ.get("KSG_BATCH_MODE")
+    os.environ["KSG_BATCH_MODE"] = mode
+    try:
+        return native.Engine(device=0)   # the mode is read at ksg_open
+    finally:
+        if old is None:
+            del os.environ["KSG_BATCH_MODE"]
+        else:
+            os.environ["KSG_BATCH_MODE"] = old
+
+
+@pytest.fixture(scope="module")
+def gpu_batched(built):
+    """The batched placement path (default phase-2 variant, "scan").  The
+    "topset" variant has its own opt-in tests (tests/test_gpu_topset.py)."""
+    return _engine_with_batch_mode("scan")
+
+
 @pytest.fixture(scope="module")
 def oracle():
     import binding
@@ -58,8 +78,9 @@ def test_queue_capture_matches_oracle(gpu, oracle, name, make):
 
 
 @pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
-def test_placement_queue_matches_oracle(gpu, oracle, name, make):
+def test_placement_queue_matches_oracle(gpu_batched, oracle, name, make):
     """Placement-only queue (no capture): the batched speculate-and-repair path."""
+    gpu = gpu_batched
     nodes, pods, prof = make()
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
@@ -146,8 +167,9 @@ def test_replicas_match_sequential_oracle(gpu, oracle):
 
 
 @pytest.mark.slow
-def test_full_config2_placements(gpu, oracle):
+def test_full_config2_placements(gpu_batched, oracle):
     """BASELINE configs[1] at full size: 5,000 nodes x 50,000 pods."""
+    gpu = gpu_batched
     nodes, pods, prof = G.config2()
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)

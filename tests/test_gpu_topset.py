@@ -1,0 +1,66 @@
+"""Opt-in GPU tests of the experimental "topset" phase-2 variant of the
+batched path (KSG_BATCH_MODE=topset).  Not the default path
+and not yet validated on hardware, so these are kept out of `-m gpu`; run
+them with `python -m pytest tests -m topset` on a GPU box.  Same parity bar
+as the default path: placements, per-pod results and node state bit-exact
+against the C++ oracle."""
+import numpy as np
+import pytest
+
+from conftest import pkg
+from test_gpu_parity import CASES, _engine_with_batch_mode
+
+G = pkg("generator")
+E = pkg("encoder")
+
+
+def _have_gpu():
+    try:
+        import torch
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+pytestmark = [pytest.mark.topset, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
+
+
+@pytest.fixture(scope="module")
+def topset(built):
+    return _engine_with_batch_mode("topset")
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import binding
+    return binding.Oracle(8)
+
+
+def _check(gpu, oracle, nodes, pods, prof, split=True):
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    oracle.load(enc, pf)
+    pg, rg = gpu.run_queue(0, len(pods))
+    po, ro = oracle.run_queue(0, len(pods))
+    np.testing.assert_array_equal(pg, po)
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
+    R = len(enc.cluster.res_names)
+    for a, b in zip(gpu.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(a, b)
+    if split:
+        gpu.reset_state()
+        half = len(pods) // 2
+        p1, _ = gpu.run_queue(0, half)
+        p2, _ = gpu.run_queue(half, len(pods) - half)
+        np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
+
+
+@pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
+def test_topset_placements_match_oracle(topset, oracle, name, make):
+    _check(topset, oracle, *make())
+
+
+def test_topset_full_config2(topset, oracle):
+    _check(topset, oracle, *G.config2(), split=False)
