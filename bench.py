@@ -124,6 +124,15 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     scheduled = int((pl >= 0).sum())
+    # one extra, untimed step with per-kernel HIP-event timing (ksg_set_timing)
+    kstats = []
+    try:
+        eng.set_timing(True)
+        step()
+        kstats = eng.kernel_stats()
+        eng.set_timing(False)
+    except Exception as e:   # timing is diagnostic; never lose the bench line over it
+        log(f"[rank {rank}] per-kernel timing unavailable: {e}")
 
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
@@ -132,7 +141,15 @@ def main():
         per_eval = metrics.bytes_per_node_eval(enc, prof)
         bpe = sum(per_eval.values())
         kms = float(np.mean(kernel_ms))
-        roof = metrics.roofline(bpe, P * len(nodes), kms)
+        try:
+            roof = metrics.dominant_kernel_roofline(kstats, bpe)
+        except Exception as e:
+            log(f"per-kernel roofline unavailable: {e}")
+            roof = None
+        if roof is None:   # no per-kernel timing: whole step as one launch
+            roof = metrics.roofline(bpe, P * len(nodes), kms)
+        roof["step"] = metrics.roofline(bpe, P * len(nodes), kms)
+        roof["step"]["kernel_ms"] = kms
         roof["traffic"] = None
         pmc = os.path.join(ROOT, "profiles", "pmc_config2.json")
         if os.path.exists(pmc):
@@ -140,7 +157,6 @@ def main():
                 roof["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
                 pass
-        roof["kernel_ms"] = kms
         roof["bytes_per_node_eval"] = bpe
         roof["node_evals_per_launch"] = P * len(nodes)
         out = {

@@ -253,6 +253,33 @@ int ksg_reset_state(ksg_ctx* ctx);
  * between HIP events recorded on the stream the kernel was launched on. */
 int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
 
+/* Per-kernel timing of the next runs (off by default: it adds one event
+ * record per launch).  With timing on, ksg_kernel_stats() returns, per kernel
+ * that ran in the last ksg_run_queue / ksg_run_replicas call, the number of
+ * launches, the summed launch durations (HIP events on the launch stream,
+ * between consecutive launches) and the algorithmic units processed:
+ * (pod, node) pairs for the sweeping kernels; for the top-set phase 2,
+ * Σ_j (j + 1) = top-set entries + changed-node records of a batch.
+ * *n = number of kernels (may exceed max). */
+enum {
+  KSG_K_QUEUE = 0,
+  KSG_K_QUEUE_TOPO = 1,
+  KSG_K_BATCH_PHASE1 = 2,
+  KSG_K_BATCH_TOPK = 3,
+  KSG_K_BATCH_PHASE2 = 4,
+  KSG_K_BATCH_PHASE2_SCAN = 5,
+  KSG_NKERNELS = 6
+};
+typedef struct ksg_kernel_stat {
+  char name[48];
+  int32_t kind;      /* KSG_K_* */
+  int32_t calls;
+  double total_ms;
+  double units;      /* (pod, node) pairs processed over all launches */
+} ksg_kernel_stat;
+int ksg_set_timing(ksg_ctx* ctx, int on);
+int ksg_kernel_stats(ksg_ctx* ctx, ksg_kernel_stat* out, int32_t max, int32_t* n);
+
 /* ---- bulk result-store serialiser (host code; no device needed) ---------
  * Emits the filter-result, score-result and finalscore-result annotation
  * values of one pod straight from its capture SoA, byte-identical to

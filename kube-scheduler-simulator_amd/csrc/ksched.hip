@@ -1474,6 +1474,15 @@ struct ksg_ctx {
   uint64_t* d_top = nullptr;
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
   int batch_mode = 0;  // env KSG_BATCH_MODE: 0 "scan" (default), 1 "topset"
+  // per-kernel timing (ksg_set_timing): one event before the first and after
+  // every launch of a run, on the launch stream
+  bool timing = false;
+  std::vector<hipEvent_t> tev;
+  int tev_used = 0;
+  std::vector<std::pair<int, double>> tlaunch;   // (kernel kind, algorithmic units)
+  double kstat_ms[KSG_NKERNELS] = {};
+  double kstat_units[KSG_NKERNELS] = {};
+  int32_t kstat_calls[KSG_NKERNELS] = {};
   unsigned long long* d_stamps = nullptr;   // KSG_STAMPS diagnostic build only
 };
 
@@ -1527,6 +1536,51 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_stamps = nullptr;
 }
 
+// ---- per-kernel timing -------------------------------------------------------
+const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_batch_phase1",
+                                          "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan"};
+
+int tmark(ksg_ctx* ctx) {
+  if (!ctx->timing) return KSG_OK;
+  if (ctx->tev_used == (int)ctx->tev.size()) {
+    hipEvent_t e;
+    HIPC(ctx, hipEventCreate(&e));
+    ctx->tev.push_back(e);
+  }
+  HIPC(ctx, hipEventRecord(ctx->tev[ctx->tev_used++], ctx->stream));
+  return KSG_OK;
+}
+
+int tlaunched(ksg_ctx* ctx, int kind, double units) {
+  if (!ctx->timing) return KSG_OK;
+  ctx->tlaunch.emplace_back(kind, units);
+  return tmark(ctx);
+}
+
+void treset(ksg_ctx* ctx) {
+  ctx->tev_used = 0;
+  ctx->tlaunch.clear();
+  for (int k = 0; k < KSG_NKERNELS; k++) {
+    ctx->kstat_ms[k] = 0;
+    ctx->kstat_units[k] = 0;
+    ctx->kstat_calls[k] = 0;
+  }
+}
+
+// after the stream has been synchronised
+int tcollect(ksg_ctx* ctx) {
+  if (!ctx->timing) return KSG_OK;
+  for (size_t i = 0; i < ctx->tlaunch.size() && (int)i + 1 < ctx->tev_used; i++) {
+    float ms = 0;
+    HIPC(ctx, hipEventElapsedTime(&ms, ctx->tev[i], ctx->tev[i + 1]));
+    const int k = ctx->tlaunch[i].first;
+    ctx->kstat_ms[k] += ms;
+    ctx->kstat_units[k] += ctx->tlaunch[i].second;
+    ctx->kstat_calls[k] += 1;
+  }
+  return KSG_OK;
+}
+
 bool profile_has(const ksg_profile& prof, int pl) {
   if ((prof.score_mask >> pl) & 1u) return true;
   for (int k = 0; k < prof.n_filter; k++)
@@ -1548,7 +1602,10 @@ bool needs_topo(ksg_ctx* ctx, const ksg_profile& prof, int first, int count) {
 
 int launch_queue(ksg_ctx* ctx, QueueArgs& a, int n_replicas, int block, bool topo) {
   (void)hipGetLastError();
+  treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  int rc;
+  if ((rc = tmark(ctx))) return rc;
   if (topo) {
     if (block == 1024)
       hipLaunchKernelGGL(ksg_queue_topo_kernel<1024>, dim3(n_replicas), dim3(1024), 0, ctx->stream, a);
@@ -1565,6 +1622,7 @@ int launch_queue(ksg_ctx* ctx, QueueArgs& a, int n_replicas, int block, bool top
       hipLaunchKernelGGL(ksg_queue_kernel<256>, dim3(n_replicas), dim3(256), 0, ctx->stream, a);
   }
   HIPC(ctx, hipGetLastError());
+  if ((rc = tlaunched(ctx, topo ? KSG_K_QUEUE_TOPO : KSG_K_QUEUE, (double)n_replicas * a.count * a.c.N))) return rc;
   HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   return KSG_OK;
 }
@@ -1717,7 +1775,10 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     attr_set = true;
   }
   (void)hipGetLastError();
+  treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  int trc;
+  if ((trc = tmark(ctx))) return trc;
   for (int off = 0; off < count;) {
     int nb = std::min(KSG_BATCH_MAX, count - off);
     int64_t lo = 0, hi = 0;
@@ -1741,12 +1802,18 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     b.nb = nb;
     b.prog_lo = (int32_t)lo;
     b.prog_len = (int32_t)(hi - lo);
+    const double units = (double)b.nb * N;   // (pod, node) pairs of the batch
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, b);
+    if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return trc;
     if (topset) {
       hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
+      if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
       hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
+      // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
+      if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2, 0.5 * b.nb * (b.nb + 1)))) return trc;
     } else {
       hipLaunchKernelGGL(ksg_batch_phase2_scan<512>, dim3(1), dim3(512), bytes, ctx->stream, b);
+      if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2_SCAN, units))) return trc;
     }
     off += nb;
   }
@@ -1812,6 +1879,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   float ms = 0;
   HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
+  if ((rc = tcollect(ctx))) return rc;
   return KSG_OK;
 }
 
@@ -1859,6 +1927,7 @@ int ksg_close(ksg_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   free_all(ctx);
+  for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2053,6 +2122,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   float ms = 0;
   HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
+  if ((rc = tcollect(ctx))) return rc;
   if (summaries) {
     for (size_t r = 0; r < RR; r++) {
       ksg_replica_summary& sm = summaries[r];
@@ -2108,6 +2178,33 @@ int ksg_debug_stamps(ksg_ctx* ctx, unsigned long long* out6) {
   return KSG_OK;
 }
 #endif
+
+int ksg_set_timing(ksg_ctx* ctx, int on) {
+  if (!ctx) return KSG_E_INVALID;
+  ctx->timing = on != 0;
+  treset(ctx);
+  return KSG_OK;
+}
+
+int ksg_kernel_stats(ksg_ctx* ctx, ksg_kernel_stat* out, int32_t max, int32_t* n) {
+  if (!ctx || !n || (max > 0 && !out)) return KSG_E_INVALID;
+  int k = 0;
+  for (int i = 0; i < KSG_NKERNELS; i++) {
+    if (!ctx->kstat_calls[i]) continue;
+    if (k < max) {
+      ksg_kernel_stat& st = out[k];
+      st = ksg_kernel_stat{};
+      std::snprintf(st.name, sizeof(st.name), "%s", kKernelNames[i]);
+      st.kind = i;
+      st.calls = ctx->kstat_calls[i];
+      st.total_ms = ctx->kstat_ms[i];
+      st.units = ctx->kstat_units[i];
+    }
+    k++;
+  }
+  *n = k;
+  return KSG_OK;
+}
 
 int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms) {
   if (!ctx || !ms) return KSG_E_INVALID;

@@ -63,3 +63,39 @@ def roofline(bytes_per_eval: int, node_evals_per_launch: int, launch_ms: float) 
     achieved = bytes_per_eval * node_evals_per_launch / (launch_ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS}
+
+
+# Algorithmic bytes per unit of each kernel (units as ksg_kernel_stats counts them).
+#   queue kernels, batch phase 1: one node-eval per (pod, node) = the column
+#     schema above; phase 1 also writes its 8-byte record + 4-byte image part
+#   topk / scan phase 2: one 8-byte record read per (pod, node)
+#   top-set phase 2: per unit one 8-byte top key + 8-byte record + 4-byte image part
+def kernel_bytes_per_unit(name: str, bytes_per_eval: int) -> int:
+    if name in ("ksg_queue_kernel", "ksg_queue_topo_kernel"):
+        return bytes_per_eval
+    if name == "ksg_batch_phase1":
+        return bytes_per_eval + 12
+    if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
+        return 8
+    if name == "ksg_batch_phase2":
+        return 20
+    raise KeyError(name)
+
+
+def dominant_kernel_roofline(kstats, bytes_per_eval: int):
+    """Roofline of the kernel with the largest summed time: algorithmic bytes
+    per launch / average launch duration; every kernel listed under "kernels"."""
+    if not kstats:
+        return None
+    rows = []
+    for k in kstats:
+        bpu = kernel_bytes_per_unit(k["name"], bytes_per_eval)
+        per_launch = bpu * k["units"] / max(k["calls"], 1)
+        r = roofline(1, per_launch, k["avg_ms"]) if k["avg_ms"] > 0 else {"achieved": 0.0, "frac": 0.0}
+        rows.append({"name": k["name"], "calls": k["calls"], "avg_ms": k["avg_ms"], "total_ms": k["total_ms"],
+                     "bytes_per_launch": per_launch, "bytes_per_unit": bpu,
+                     "achieved": r["achieved"], "frac": r["frac"]})
+    dom = max(rows, key=lambda r: r["total_ms"])
+    return {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": dom["frac"], "kernel": dom["name"], "avg_launch_ms": dom["avg_ms"],
+            "bytes_per_launch": dom["bytes_per_launch"], "kernels": rows}

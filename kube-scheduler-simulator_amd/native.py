@@ -170,6 +170,11 @@ def _bind(lib, prefix: str):
     return f
 
 
+class KsgKernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 48), ("kind", C.c_int32), ("calls", C.c_int32), ("total_ms", C.c_double),
+                ("units", C.c_double)]
+
+
 class KschedError(RuntimeError):
     pass
 
@@ -210,6 +215,9 @@ class Engine:
         self._run_replicas = f("run_replicas", C.c_int, vp, C.POINTER(KsgProfile), C.c_int32, C.c_int32,
                                C.c_int32, i32p, vp)
         self._last_ms = f("last_kernel_ms", C.c_int, vp, C.POINTER(C.c_double))
+        self._set_timing = f("set_timing", C.c_int, vp, C.c_int)
+        self._kernel_stats = f("kernel_stats", C.c_int, vp, C.POINTER(KsgKernelStat), C.c_int32,
+                               C.POINTER(C.c_int32))
         self.abi_version = f("abi_version", C.c_int)()
 
     def _check(self, rc: int):
@@ -268,6 +276,22 @@ class Engine:
         sums = np.zeros(R, SUMMARY_DTYPE)
         self._check(self._run_replicas(self.ctx, arr, R, first, count, _ptr(pl, i32p), sums.ctypes.data))
         return pl, sums
+
+    def set_timing(self, on: bool):
+        """Per-kernel HIP-event timing of the following runs (ksg_set_timing)."""
+        self._check(self._set_timing(self.ctx, 1 if on else 0))
+
+    def kernel_stats(self):
+        """[{name, calls, total_ms, avg_ms, units}] of the last run (timing on)."""
+        buf = (KsgKernelStat * 16)()
+        n = C.c_int32()
+        self._check(self._kernel_stats(self.ctx, buf, 16, C.byref(n)))
+        out = []
+        for i in range(min(n.value, 16)):
+            k = buf[i]
+            out.append({"name": k.name.decode(), "calls": k.calls, "total_ms": k.total_ms,
+                        "avg_ms": k.total_ms / max(k.calls, 1), "units": k.units})
+        return out
 
     def last_kernel_ms(self) -> float:
         v = C.c_double()

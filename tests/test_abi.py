@@ -33,7 +33,8 @@ def test_struct_layouts_match(tmp_path):
     E = pkg("encoder")
     src = tmp_path / "sz.c"
     names = ["ksg_nodes", "ksg_topology", "ksg_pod", "ksg_workload", "ksg_profile", "ksg_result",
-             "ksg_capture", "ksg_node_state", "ksg_replica_summary"]
+             "ksg_capture", "ksg_node_state", "ksg_replica_summary", "ksg_kernel_stat", "ksg_names",
+             "ksg_annotate_in"]
     src.write_text('#include <stdio.h>\n#include "ksched.h"\nint main(void){' +
                    "".join(f'printf("%zu\\n", sizeof({n}));' for n in names) + "return 0;}")
     exe = tmp_path / "sz"
@@ -48,6 +49,9 @@ def test_struct_layouts_match(tmp_path):
     assert sizes["ksg_capture"] == ctypes.sizeof(native.KsgCapture)
     assert sizes["ksg_node_state"] == ctypes.sizeof(native.KsgNodeState)
     assert sizes["ksg_replica_summary"] == ctypes.sizeof(native.KsgReplicaSummary)
+    assert sizes["ksg_kernel_stat"] == ctypes.sizeof(native.KsgKernelStat)
+    assert sizes["ksg_names"] == ctypes.sizeof(native.KsgNames)
+    assert sizes["ksg_annotate_in"] == ctypes.sizeof(native.KsgAnnotateIn)
 
 
 def test_product_path_fails_loudly_without_library(tmp_path):
