@@ -179,3 +179,19 @@ def test_full_config2_placements(gpu_batched, oracle):
     po, ro = oracle.run_queue(0, len(pods))
     np.testing.assert_array_equal(pg, po)
     np.testing.assert_array_equal(rg["n_feasible"], ro["n_feasible"])
+
+
+def test_kernel_timing_accounts_for_the_run(gpu_batched):
+    """ksg_set_timing: per-kernel HIP-event durations cover the run (bench.py's roofline input)."""
+    gpu = gpu_batched
+    nodes, pods, prof = G.config2(n_nodes=500, n_pods=700, seed=9)
+    enc = E.Encoder(nodes, pods, prof)
+    gpu.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    gpu.set_timing(True)
+    gpu.run_queue(0, len(pods), results=False)
+    stats = {k["name"]: k for k in gpu.kernel_stats()}
+    gpu.set_timing(False)
+    assert "ksg_batch_phase1" in stats and "ksg_batch_phase2_scan" in stats
+    assert stats["ksg_batch_phase1"]["units"] == len(pods) * len(nodes)
+    total = sum(k["total_ms"] for k in stats.values())
+    assert 0 < total <= gpu.last_kernel_ms() * 1.05 + 0.05
