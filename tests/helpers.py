@@ -65,10 +65,11 @@ def scheduler_annotations(nodes, pods, prof, engine):
     return out
 
 
-def pyoracle_annotations(nodes, pods, prof):
+def pyoracle_annotations(nodes, pods, prof, bound=()):
+    """`pods` = the queue; `bound` = [(pod, node name)] already running."""
     import pyoracle
     store = A.ResultStore(prof.weights())
-    recs = pyoracle.run_queue(nodes, [], pods, prof)
+    recs = pyoracle.run_queue(nodes, list(bound), pods, prof)
     names = set(n for n, _ in prof.plugins)
     for pod, r in zip(pods, recs):
         ns, nm = pod.namespace, pod.name

@@ -1,0 +1,197 @@
+"""Snapshot / record ingest: quantities, object
+conversion, scheduler-config profiles, and round trips generator -> k8s JSON
+-> ingest -> identical SoA encoding and identical placements."""
+import json
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from conftest import pkg
+
+G = pkg("generator")
+E = pkg("encoder")
+I = pkg("ingest")
+P = pkg("profile")
+m = pkg("model")
+
+
+@pytest.mark.parametrize("s,milli,val", [
+    ("100m", 100, 1), ("0.5", 500, 1), ("4", 4000, 4), ("1Gi", 2 ** 30 * 1000, 2 ** 30),
+    ("16Gi", 16 * 2 ** 30 * 1000, 16 * 2 ** 30), ("1.5Gi", 3 * 2 ** 29 * 1000, 3 * 2 ** 29),
+    ("1G", 10 ** 12, 10 ** 9), ("2k", 2 * 10 ** 6, 2000), ("1e3", 10 ** 6, 1000), ("0.0001", 1, 1),
+    ("1.0001m", 2, 1), ("200Mi", 200 * 2 ** 20 * 1000, 200 * 2 ** 20), ("110", 110000, 110), (".5", 500, 1),
+    ("5E-3", 5, 1), ("-1", -1000, -1), ("+3", 3000, 3), (3, 3000, 3),
+])
+def test_parse_quantity(s, milli, val):
+    q = I.parse_quantity(s)
+    assert I.milli_value(q) == milli
+    assert I.value(q) == val
+
+
+@pytest.mark.parametrize("bad", ["", "m", "1.2.3", "1Qi", "abc", "1 Gi"])
+def test_parse_quantity_rejects(bad):
+    with pytest.raises(ValueError):
+        I.parse_quantity(bad)
+
+
+def test_readme_templates():
+    """The web UI's node/pod templates (web/components/lib/templates/node.yaml,
+    pod.yaml), i.e. the README example's objects, as ingested."""
+    node = I.node_from_k8s({"metadata": {"name": "node-282x7", "labels": {}}, "spec": {},
+                            "status": {"capacity": {"cpu": "4", "memory": "32Gi", "pods": "110"},
+                                       "allocatable": {"cpu": "4", "memory": "32Gi", "pods": "110"}}})
+    assert node.allocatable == {"cpu": 4000, "memory": 32 * 2 ** 30, "pods": 110}
+    pod = I.pod_from_k8s({"metadata": {"name": "hoge-pod", "namespace": "default", "labels": {}},
+                          "spec": {"containers": [{"name": "pause", "image": "registry.k8s.io/pause:3.5",
+                                                   "resources": {"limits": {"cpu": "100m", "memory": "16Gi"},
+                                                                 "requests": {"cpu": "100m", "memory": "16Gi"}}}]}})
+    assert m.pod_requests(pod) == {"cpu": 100, "memory": 16 * 2 ** 30}
+
+
+def test_limits_default_requests():
+    pod = I.pod_from_k8s({"metadata": {"name": "p"}, "spec": {"containers": [
+        {"resources": {"limits": {"cpu": "2", "example.com/fpga": "1"}, "requests": {"cpu": "1"}}}]}})
+    assert pod.containers[0].requests == {"cpu": 1000, "example.com/fpga": 1}
+
+
+def test_profile_from_config_multipoint_merge():
+    cfg = {"profiles": [{"plugins": {"multiPoint": {
+        "enabled": [{"name": "NodeResourcesFit", "weight": 5}, {"name": "ImageLocality", "weight": 3}],
+        "disabled": [{"name": "TaintToleration"}]}},
+        "pluginConfig": [{"name": "NodeResourcesFit", "args": {"scoringStrategy": {
+            "type": "MostAllocated", "resources": [{"name": "cpu", "weight": 2}, {"name": "memory", "weight": 1}]}}},
+            {"name": "InterPodAffinity", "args": {"hardPodAffinityWeight": 4}}]}],
+        "percentageOfNodesToScore": 100}
+    prof, pct = I.profile_from_config(cfg)
+    names = [n for n, _ in prof.plugins]
+    assert "TaintToleration" not in names
+    assert dict(prof.plugins)["NodeResourcesFit"] == 5 and dict(prof.plugins)["ImageLocality"] == 3
+    # re-configured defaults keep their default position (mergePluginSet)
+    assert names.index("NodeResourcesFit") < names.index("VolumeRestrictions")
+    assert prof.fit_strategy == P.MOST_ALLOCATED and prof.fit_resources == [("cpu", 2), ("memory", 1)]
+    assert prof.hard_pod_affinity_weight == 4 and pct == 100
+    assert prof.weights()["NodeResourcesFit"] == 5
+
+
+def test_profile_from_config_refuses_unmodelled():
+    with pytest.raises(NotImplementedError):
+        I.profile_from_config({"profiles": [{"plugins": {"filter": {"disabled": [{"name": "NodeAffinity"}]}}}]})
+    with pytest.raises(NotImplementedError):
+        I.profile_from_config({"profiles": [{"pluginConfig": [{"name": "NodeResourcesFit", "args": {
+            "scoringStrategy": {"type": "RequestedToCapacityRatio"}}}]}]})
+    with pytest.raises(ValueError):
+        I.profile_from_config({"profiles": [{"plugins": {"multiPoint": {"enabled": [{"name": "NodeNumber"}]}}}]})
+
+
+def _same_encoding(a, b):
+    assert a.cluster.node_names == b.cluster.node_names
+    assert sorted(a.cluster.arrays) == sorted(b.cluster.arrays)
+    for k in a.cluster.arrays:
+        np.testing.assert_array_equal(a.cluster.arrays[k], b.cluster.arrays[k], err_msg=k)
+    np.testing.assert_array_equal(a.workload.pods, b.workload.pods)
+    np.testing.assert_array_equal(a.workload.prog, b.workload.prog)
+
+
+ROUND_TRIP = {
+    "readme-kat": G.readme_kat,
+    "c1": lambda: G.config1(n_nodes=40, n_pods=120),
+    "c2": lambda: G.config2(n_nodes=60, n_pods=150, seed=21),
+    "c2-most": lambda: (lambda n, p, _: (n, p, P.config2_profile(strategy=P.MOST_ALLOCATED)))(
+        *G.config2(n_nodes=50, n_pods=80, seed=12)),
+    "c3": lambda: G.config3(n_nodes=40, n_pods=150, apps=8, zones=4),
+    "c5": lambda: G.config5(n_nodes=60, n_pods=40, n_images=50, taint_vocab=64, taints_per_node=8,
+                            images_per_node=10),
+}
+
+
+@pytest.mark.parametrize("name", sorted(ROUND_TRIP))
+def test_snapshot_round_trip(name):
+    import binding
+    nodes, pods, prof = ROUND_TRIP[name]()
+    doc = json.loads(json.dumps(I.snapshot_document(nodes, pods, prof)))
+    snap = I.load_snapshot(doc)
+    assert not snap.bound and snap.queue == list(range(len(pods)))
+    assert snap.profile.plugins == prof.plugins
+    direct = E.Encoder(nodes, pods, prof)
+    via = E.Encoder(snap.nodes, snap.pods, snap.profile)
+    _same_encoding(direct, via)
+    o = binding.Oracle(2)
+    o.load(via, E.encode_profile(snap.profile, via.cluster.res_names))
+    pl_via, _ = o.run_queue(0, len(pods))
+    o.load(direct, E.encode_profile(prof, direct.cluster.res_names))
+    pl_direct, _ = o.run_queue(0, len(pods))
+    np.testing.assert_array_equal(pl_via, pl_direct)
+
+
+def test_bound_pods_and_priority_order():
+    nodes, pods, prof = G.config2(n_nodes=20, n_pods=30, seed=4)
+    doc = I.snapshot_document(nodes, pods, prof)
+    doc["pods"][3]["spec"]["nodeName"] = nodes[5].name        # already running
+    doc["pods"][7]["spec"]["nodeName"] = "gone-node"           # bound to a node not in the snapshot
+    doc["pods"][10]["spec"]["priority"] = 100
+    doc["priorityClasses"] = [{"metadata": {"name": "hi"}, "value": 50}]
+    doc["pods"][12]["spec"]["priorityClassName"] = "hi"
+    snap = I.load_snapshot(doc)
+    assert snap.bound == [(0, 5)] and snap.pods[0].name == pods[3].name
+    assert snap.skipped == [pods[7].name]
+    q = [snap.pods[i].name for i in snap.queue]
+    assert q[0] == pods[10].name and q[1] == pods[12].name
+    assert len(q) == 28
+
+
+def test_namespace_selector_resolved():
+    doc = {"nodes": [], "namespaces": [{"metadata": {"name": "a", "labels": {"team": "x"}}},
+                                       {"metadata": {"name": "b", "labels": {"team": "y"}}}],
+           "pods": [{"metadata": {"name": "p", "namespace": "a"}, "spec": {"containers": [{}], "affinity": {
+               "podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                   {"labelSelector": {"matchLabels": {"app": "z"}}, "topologyKey": "zone",
+                    "namespaceSelector": {"matchLabels": {"team": "y"}}},
+                   {"labelSelector": {"matchLabels": {"app": "z"}}, "topologyKey": "zone",
+                    "namespaceSelector": {"matchLabels": {"team": "none"}}}]}}}}]}
+    snap = I.load_snapshot(doc)
+    t0, t1 = snap.pods[0].pod_affinity_required
+    assert t0.namespaces == ("b",) and t0.namespace_selector is None
+    assert t1.namespaces == (I.NO_NAMESPACE,)
+
+
+def test_replay_records():
+    nodes, pods, prof = G.config1(n_nodes=5, n_pods=6)
+    doc = I.snapshot_document(nodes, pods, prof)
+    recs = [{"time": "t", "event": "Add", "resource": o} for o in doc["nodes"] + doc["pods"]]
+    upd = json.loads(json.dumps(doc["nodes"][1]))
+    upd["metadata"]["labels"]["extra"] = "1"
+    recs.append({"time": "t", "event": "Update", "resource": upd})
+    recs.append({"time": "t", "event": "Delete", "resource": doc["pods"][2]})
+    out = I.replay_records(json.dumps(recs))
+    assert [n["metadata"]["name"] for n in out["nodes"]] == [n.name for n in nodes]
+    assert out["nodes"][1]["metadata"]["labels"]["extra"] == "1"
+    assert [p["metadata"]["name"] for p in out["pods"]] == [p.name for i, p in enumerate(pods) if i != 2]
+    snap = I.load_snapshot(out)
+    assert len(snap.queue) == 5
+
+
+def test_snapshot_with_running_pods_end_to_end():
+    """A snapshot whose first pods already run: the mirror (C++ oracle engine,
+    native serialiser) and the Python restatement agree on every annotation."""
+    import binding
+    import pyoracle
+    F = pkg("framework")
+    A = pkg("annotations")
+    nodes, pods, prof = G.config3(n_nodes=30, n_pods=90, apps=6, zones=3)
+    doc = I.snapshot_document(nodes, pods, prof)
+    for k in range(30):                      # the first 30 pods already run, round robin
+        doc["pods"][k]["spec"]["nodeName"] = nodes[k % len(nodes)].name
+    snap = I.load_snapshot(doc)
+    assert len(snap.bound) == 30 and len(snap.queue) == 60
+    s = F.DebuggableScheduler(snap.nodes, snap.pods, snap.profile, engine=binding.Oracle(2), bound=snap.bound)
+    got = []
+    for i in snap.queue:
+        s.schedule_one(i)
+        got.append(s.annotations(i))
+    from helpers import pyoracle_annotations
+    bound = [(snap.pods[pi], snap.nodes[ni].name) for pi, ni in snap.bound]
+    queue = [snap.pods[i] for i in snap.queue]
+    want, _ = pyoracle_annotations(snap.nodes, queue, snap.profile, bound)
+    assert want == got
+    assert any(a[A.SELECTED_NODE] for a in got)
