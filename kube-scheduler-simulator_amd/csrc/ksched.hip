@@ -1473,7 +1473,7 @@ struct ksg_ctx {
   P1Stats* d_p1 = nullptr;
   uint64_t* d_top = nullptr;
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
-  int batch_mode = 0;  // env KSG_BATCH_MODE: 0 "scan" (default), 1 "topset"
+  int batch_mode = 1;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset" (default)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
   bool timing = false;
@@ -1917,7 +1917,7 @@ int ksg_open(int device, ksg_ctx** out) {
     return KSG_E_DEVICE;
   }
   if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
-  if (const char* f = getenv("KSG_BATCH_MODE")) ctx->batch_mode = std::string(f) == "topset" ? 1 : 0;
+  if (const char* f = getenv("KSG_BATCH_MODE")) ctx->batch_mode = std::string(f) == "scan" ? 0 : 1;
   *out = ctx;
   return KSG_OK;
 }
@@ -2127,7 +2127,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     for (size_t r = 0; r < RR; r++) {
       ksg_replica_summary& sm = summaries[r];
       sm = ksg_replica_summary{};
-      uint64_t h = 1469598103934665603ull;
+      uint64_t h = 14695981039346656037ull;  // FNV-1a 64 offset basis
       for (int k = 0; k < count; k++) {
         const int32_t v = placements[r * count + k];
         (v >= 0 ? sm.scheduled : sm.unschedulable) += 1;

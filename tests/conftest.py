@@ -18,7 +18,6 @@ def pkg(mod: str = ""):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libksched.so)")
     config.addinivalue_line("markers", "slow: long-running case")
-    config.addinivalue_line("markers", "topset: opt-in GPU tests of the experimental topset phase-2 variant")
 
 
 @pytest.fixture(scope="session")

@@ -1,9 +1,7 @@
-"""Opt-in GPU tests of the experimental "topset" phase-2 variant of the
-batched path (KSG_BATCH_MODE=topset).  Not the default path
-and not yet validated on hardware, so these are kept out of `-m gpu`; run
-them with `python -m pytest tests -m topset` on a GPU box.  Same parity bar
+"""GPU parity of every phase-2 variant of the batched placement path
+(KSG_BATCH_MODE): "topset" (default) and "scan".  Same bar
 as the default path: placements, per-pod results and node state bit-exact
-against the C++ oracle."""
+against the C++ oracle, including split calls."""
 import numpy as np
 import pytest
 
@@ -22,12 +20,14 @@ def _have_gpu():
         return False
 
 
-pytestmark = [pytest.mark.topset, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
+
+MODES = ["topset", "scan"]
 
 
-@pytest.fixture(scope="module")
-def topset(built):
-    return _engine_with_batch_mode("topset")
+@pytest.fixture(scope="module", params=MODES)
+def variant(request, built):
+    return _engine_with_batch_mode(request.param)
 
 
 @pytest.fixture(scope="module")
@@ -58,9 +58,9 @@ def _check(gpu, oracle, nodes, pods, prof, split=True):
 
 
 @pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
-def test_topset_placements_match_oracle(topset, oracle, name, make):
-    _check(topset, oracle, *make())
+def test_variant_placements_match_oracle(variant, oracle, name, make):
+    _check(variant, oracle, *make())
 
 
-def test_topset_full_config2(topset, oracle):
-    _check(topset, oracle, *G.config2(), split=False)
+def test_variant_full_config2(variant, oracle):
+    _check(variant, oracle, *G.config2(), split=False)

@@ -39,9 +39,9 @@ def _engine_with_batch_mode(mode):
 
 @pytest.fixture(scope="module")
 def gpu_batched(built):
-    """The batched placement path (default phase-2 variant, "scan").  The
-    "topset" variant has its own opt-in tests (tests/test_gpu_topset.py)."""
-    return _engine_with_batch_mode("scan")
+    """The batched placement path (default phase-2 variant, "topset").  Every
+    variant also runs the full case list in tests/test_gpu_batch_variants.py."""
+    return _engine_with_batch_mode("topset")
 
 
 @pytest.fixture(scope="module")
