@@ -268,7 +268,8 @@ enum {
   KSG_K_BATCH_TOPK = 3,
   KSG_K_BATCH_PHASE2 = 4,
   KSG_K_BATCH_PHASE2_SCAN = 5,
-  KSG_NKERNELS = 6
+  KSG_K_BATCH_PHASE2S = 6,
+  KSG_NKERNELS = 7
 };
 typedef struct ksg_kernel_stat {
   char name[48];

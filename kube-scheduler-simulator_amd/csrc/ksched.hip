@@ -219,6 +219,8 @@ struct P1Stats {
   int32_t ht, ha;          // feasible nodes holding mt / ma
   int32_t err;             // some normalised score left [0, 100]
   int32_t K;               // |top set| = min(j + 1, nfeas)
+  float inv_mt, inv_ma;    // 1 / mt, 1 / ma (qdiv estimates; 1 when the maximum is 0)
+  int32_t pad;
 };
 
 struct BatchArgs {
@@ -603,6 +605,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
     s.ha = gha;
     s.err = gerr;
     s.K = K;
+    s.inv_mt = mt ? 1.0f / (float)mt : 1.0f;
+    s.inv_ma = ma ? 1.0f / (float)ma : 1.0f;
+    s.pad = 0;
     a.p1[j] = s;
   }
   if (K == 0) return;
@@ -633,11 +638,15 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
     if (tot_k >= K) lo = mid;
     else hi = mid - 1;
   }
-  uint64_t* out = a.top + (size_t)j * KSG_BATCH_MAX;
+  // collect the K keys (dense keys are distinct, so exactly K pass) and sort
+  // them descending in LDS: phase 2 takes the first entry outside C.
+  __shared__ uint64_t s_keys[KSG_BATCH_MAX];
+  for (int i = tid; i < KSG_BATCH_MAX; i += BLOCK) s_keys[i] = 0;
+  __syncthreads();
   auto emit = [&](int64_t t, int n) {
     if (dkey(t, n) >= lo) {
       const int pos = atomicAdd(&s_pos, 1);
-      if (pos < KSG_BATCH_MAX) out[pos] = argmax_key(t, n);
+      if (pos < KSG_BATCH_MAX) s_keys[pos] = argmax_key(t, n);
     }
   };
 #pragma unroll
@@ -650,6 +659,21 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
     uint32_t e = 0;
     if (x >> 63) emit(total_of(x, e), n);
   }
+  __syncthreads();
+  static_assert(BLOCK >= KSG_BATCH_MAX / 2, "one compare-exchange per lane per step");
+  for (int k = 2; k <= KSG_BATCH_MAX; k <<= 1) {     // bitonic sort, descending
+    for (int m = k >> 1; m > 0; m >>= 1) {
+      if (tid < KSG_BATCH_MAX / 2) {
+        const int i = 2 * tid - (tid & (m - 1)), l = i + m;   // i has bit m clear
+        const uint64_t x = s_keys[i], y = s_keys[l];
+        const bool desc = (i & k) == 0;
+        if (desc ? x < y : x > y) { s_keys[i] = y; s_keys[l] = x; }
+      }
+      __syncthreads();
+    }
+  }
+  uint64_t* out = a.top + (size_t)j * KSG_BATCH_MAX;
+  for (int i = tid; i < K; i += BLOCK) out[i] = s_keys[i];
 }
 
 // Phase 2: one workgroup walks the batch in queue order and keeps every node
@@ -1023,6 +1047,550 @@ __global__ __launch_bounds__(kP2Block) void ksg_batch_phase2(BatchArgs a) {
         if (spec_node >= 0) fetch(spec_node, j + 2, spec_val);
       }
     }
+    KSG_STAMP(4);
+    __syncthreads();
+    KSG_STAMP(5);
+  }
+  for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
+#ifdef KSG_STAMPS
+  if (tid == 0 && a.stamps)
+    for (int i = 0; i < 6; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+#endif
+}
+
+// Phase 2, slot-parallel variant (KSG_BATCH_MODE=slot, default).  256 lanes;
+// lane i owns changed slot i (the i-th node assumed onto in this batch) and
+// keeps that node's phase-1 records in registers, one pod ahead.  Per pod j:
+//   X  every lane: spec = the first entry of the sorted top set T_j outside C
+//      (ballot over the first 64 entries: the best unchanged node unless all
+//      64 are changed); issue pod j+1's loads (records of C, of spec for the
+//      next slot's owner, the top set T_{j+1}; wave 0 also spec's columns),
+//      all unconditional and unconverted so that nothing waits on them
+//      before Y; re-evaluate the lane's changed node on its live slot (one
+//      bulk LDS read of the slot, branch-free filter, reciprocal-multiply
+//      divisions with an exact correction, Go's float64 BalancedAllocation);
+//      DPP reductions; one partial per wave into LDS.
+//   -- barrier --
+//   Y  every wave folds the four partials and takes the same decision; wave
+//      0 assumes the pod into its slot (LDS) and stores the node's new columns
+//      (global); the next slot's owner keeps spec's records (or reloads on a
+//      miss); the prefetched top set goes to LDS.
+//   -- barrier --
+// The selected node is either the best unchanged node or a changed one, so
+// outside the rare renormalisation every load pod j+1 needs is issued a pod
+// early.  RM bounds the resource columns (slot layout fixed at compile time).
+constexpr int kP2SBlock = KSG_BATCH_MAX;   // one lane per possible changed slot
+
+// slot row (int64 words): alloc/requested pairs of columns 0..RM-1, then
+// nonzero cpu, nonzero memory, pod count, allowed pods, f32 1/alloc of cpu and
+// memory (qdiv estimates), f64 alloc of cpu and memory (BalancedAllocation).
+template <int RM>
+struct SlotLayout {
+  static constexpr int NZC = 2 * RM, NZM = 2 * RM + 1, PODS = 2 * RM + 2, ALLOWED = 2 * RM + 3;
+  static constexpr int INVC = 2 * RM + 4, INVM = 2 * RM + 5, DAC = 2 * RM + 6, DAM = 2 * RM + 7;
+  static constexpr int W = 2 * RM + 8;
+};
+
+struct P2Part {
+  uint64_t k0, bu;           // best changed key, best unchanged key (in T_j \ C)
+  uint32_t cnt_lo, cnt_hi;   // feas1 | live << 16, lost_t | lost_a << 16
+  int32_t cmin, err;
+  int32_t kidx, cidx;        // slot of k0 / of cmin, -1 if not in this wave
+};
+
+// floor(x / a) for 0 <= x, 0 < a, quotient below 2^20 (every division on the
+// changed-node path: scores x 100 over allocatable amounts, weight sums or
+// maxima).  inv = (float)(1 / a).  The f32 estimate is within 2^-21 relative
+// of x / a, i.e. within one of the quotient; one integer multiply-subtract
+// corrects it, so the result is exact.
+__device__ __forceinline__ int64_t qdiv(int64_t x, int64_t a, float inv) {
+  const float xf = __builtin_fmaf((float)(uint32_t)((uint64_t)x >> 32), 4294967296.0f, (float)(uint32_t)x);
+  int64_t q = (int32_t)(xf * inv);
+  const int64_t r = x - q * a;
+  q += r < 0 ? -1 : (r >= a ? 1 : 0);
+  return q;
+}
+
+// x / a in float64, bit-identical to the compiler's division for 0 <= x and
+// 1 <= a < 2^53 (integers): the same rcp + two Newton steps + residual fma
+// sequence without v_div_scale / v_div_fmas / v_div_fixup, which are identities
+// in that range.  No VCC use, so two divisions interleave.
+__device__ __forceinline__ double ddiv(double x, double a) {
+  double r = __builtin_amdgcn_rcp(a);
+  double e = __builtin_fma(-a, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-a, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = x * r;
+  const double rem = __builtin_fma(-a, q, x);
+  return __builtin_fma(rem, r, q);
+}
+
+// Batch-uniform profile facts for the compact evaluator.
+struct CmProf {
+  bool fast;        // Fit and BalancedAllocation both score exactly {cpu, memory}
+  bool least;
+  int64_t wc, wm;   // Fit resource weights of cpu / memory
+  float inv_ws, inv_wc, inv_wm;   // 1 / (wc + wm), 1 / wc, 1 / wm
+};
+
+__device__ __forceinline__ CmProf cm_prof(const ksg_profile& prof) {
+  CmProf m{false, prof.fit_strategy == KSG_LEAST_ALLOCATED, 0, 0, 1.0f, 1.0f, 1.0f};
+  bool ok = prof.fit_n == 2 && prof.ba_n == 2;
+  if (ok) {
+    const int r0 = prof.fit_res[0], r1 = prof.fit_res[1];
+    ok = (r0 == KSG_RES_CPU && r1 == KSG_RES_MEM) || (r0 == KSG_RES_MEM && r1 == KSG_RES_CPU);
+    m.wc = r0 == KSG_RES_CPU ? prof.fit_w[0] : prof.fit_w[1];
+    m.wm = r0 == KSG_RES_CPU ? prof.fit_w[1] : prof.fit_w[0];
+    const int b0 = prof.ba_res[0], b1 = prof.ba_res[1];
+    ok = ok && ((b0 == KSG_RES_CPU && b1 == KSG_RES_MEM) || (b0 == KSG_RES_MEM && b1 == KSG_RES_CPU));
+    ok = ok && m.wc > 0 && m.wm > 0;
+  }
+  m.fast = ok;
+  if (ok) {
+    m.inv_ws = 1.0f / (float)(m.wc + m.wm);
+    m.inv_wc = 1.0f / (float)m.wc;
+    m.inv_wm = 1.0f / (float)m.wm;
+  }
+  return m;
+}
+
+// Per-pod values of the changed-node evaluation, read from LDS in one batch.
+template <int RM>
+struct PodHot {
+  int64_t req[RM];
+  int64_t nz_cpu, nz_mem;
+  uint32_t req_mask;   // bit r: NodeResourcesFit filter checks column r for this pod
+  bool fit_on;         // NodeResourcesFit filter runs for this pod
+  int64_t w_fit, w_ba, w_t, w_a;   // weight if the plugin scores this pod, else 0
+};
+
+template <int RM>
+__device__ __forceinline__ PodHot<RM> pod_hot(const ksg_pod& p, const ksg_profile& prof, bool fit_filter_on, int R) {
+  PodHot<RM> h;
+  uint32_t m = 0;
+#pragma unroll
+  for (int r = 0; r < RM; r++) {
+    h.req[r] = p.req[r];
+    const bool chk = r < R && h.req[r] > 0 && !(r >= 3 && ((prof.fit_ignored_res >> r) & 1u));
+    m |= chk ? 1u << r : 0u;
+  }
+  h.nz_cpu = p.nz_cpu;
+  h.nz_mem = p.nz_mem;
+  h.req_mask = m;
+  h.fit_on = fit_filter_on && !((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u);
+  const uint32_t smask = prof.score_mask & ~p.score_skip;
+  h.w_fit = (smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? prof.weight[KSG_PL_NODE_RESOURCES_FIT] : 0;
+  h.w_ba = (smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? prof.weight[KSG_PL_BALANCED_ALLOCATION] : 0;
+  h.w_t = (smask & bit(KSG_PL_TAINT_TOLERATION)) ? prof.weight[KSG_PL_TAINT_TOLERATION] : 0;
+  h.w_a = (smask & bit(KSG_PL_NODE_AFFINITY)) ? prof.weight[KSG_PL_NODE_AFFINITY] : 0;
+  return h;
+}
+
+// NodeResourcesFit score + BalancedAllocation score of a changed node from its
+// slot row w, when both score {cpu, memory}: the results of fit_score /
+// ba_score, computed without branches (a column with zero allocatable is left
+// out by selects) so that the two chains interleave.
+template <int RM>
+__device__ __forceinline__ void cm_scores(const CmProf& m, const PodHot<RM>& h, const int64_t (&w)[SlotLayout<RM>::W],
+                                          int64_t& fit, int64_t& ba) {
+  using SL = SlotLayout<RM>;
+  const int64_t ac = w[2 * KSG_RES_CPU], am = w[2 * KSG_RES_MEM];
+  const bool hc = ac > 0, hm = am > 0;
+  const int64_t sac = hc ? ac : 1, sam = hm ? am : 1;
+  const float ic = __int_as_float((int32_t)w[SL::INVC]), im = __int_as_float((int32_t)w[SL::INVM]);
+  const int64_t qc = w[SL::NZC] + h.nz_cpu, qm = w[SL::NZM] + h.nz_mem;
+  int64_t xc, xm;
+  if (m.least) {
+    xc = qc > ac ? 0 : (ac - qc) * 100;
+    xm = qm > am ? 0 : (am - qm) * 100;
+  } else {
+    xc = (qc > ac ? ac : qc) * 100;
+    xm = (qm > am ? am : qm) * 100;
+  }
+  const int64_t sc = qdiv(xc, sac, ic), sm = qdiv(xm, sam, im);
+  const int64_t num = (hc ? sc * m.wc : 0) + (hm ? sm * m.wm : 0);
+  const int64_t ws = (hc ? m.wc : 0) + (hm ? m.wm : 0);
+  const float i_ws = m.inv_ws, i_wc = m.inv_wc, i_wm = m.inv_wm;
+  float iws = __builtin_amdgcn_readfirstlane(0) ? 0.0f : i_wm;   // (selects on values, not on
+  iws = hc ? i_wc : iws;                                         //  member addresses: no scratch)
+  iws = hc && hm ? i_ws : iws;
+  fit = ws == 0 ? 0 : qdiv(num, ws, iws);
+  const double dac = hc ? __longlong_as_double(w[SL::DAC]) : 1.0, dam = hm ? __longlong_as_double(w[SL::DAM]) : 1.0;
+  double fc = ddiv((double)(w[2 * KSG_RES_CPU + 1] + h.req[KSG_RES_CPU]), dac);
+  double fm = ddiv((double)(w[2 * KSG_RES_MEM + 1] + h.req[KSG_RES_MEM]), dam);
+  fc = fc > 1 ? 1 : fc;
+  fm = fm > 1 ? 1 : fm;
+  const double sd = hc && hm ? fabs((fc - fm) / 2) : 0.0;   // |f0 - f1| is symmetric in the column order
+  ba = (int32_t)((1 - sd) * (double)100);
+}
+
+template <int RM>
+__device__ __forceinline__ void slot_row_cols(const int64_t (&w)[SlotLayout<RM>::W], NodeCols& L) {
+  using SL = SlotLayout<RM>;
+#pragma unroll
+  for (int r = 0; r < KSG_MAX_RES; r++) {
+    L.alloc[r] = r < RM ? w[2 * (r < RM ? r : 0)] : 0;
+    L.req[r] = r < RM ? w[2 * (r < RM ? r : 0) + 1] : 0;
+  }
+  L.nz_cpu = w[SL::NZC];
+  L.nz_mem = w[SL::NZM];
+  L.pod_count = (int32_t)w[SL::PODS];
+  L.allowed = (int32_t)w[SL::ALLOWED];
+}
+
+// Slot word `lane` of node n, loaded without branches (every lane issues the
+// same two loads from valid addresses); decode with slot_word_value().
+template <int RM>
+struct SlotFetch {
+  int64_t v64;
+  int32_t v32;
+};
+template <int RM>
+__device__ __forceinline__ SlotFetch<RM> slot_word_fetch(const DevCluster& c, const DevState& st, int lane, int R,
+                                                          int n) {
+  using SL = SlotLayout<RM>;
+  const size_t N = c.N;
+  const int r = lane >> 1;
+  const int64_t* p64 = c.alloc + n;   // harmless default
+  if (lane < 2 * RM && r < R) p64 = ((lane & 1) ? st.requested : c.alloc) + (size_t)r * N + n;
+  else if (lane == SL::NZC || lane == SL::NZM) p64 = st.nonzero + (size_t)(lane - SL::NZC) * N + n;
+  else if (lane == SL::INVC || lane == SL::DAC) p64 = c.alloc + (size_t)KSG_RES_CPU * N + n;
+  else if (lane == SL::INVM || lane == SL::DAM) p64 = c.alloc + (size_t)KSG_RES_MEM * N + n;
+  const int32_t* p32 = lane == SL::PODS ? st.pod_count + n : c.allowed + n;
+  return SlotFetch<RM>{*p64, *p32};
+}
+template <int RM>
+__device__ __forceinline__ int64_t slot_word_value(const SlotFetch<RM>& f, int lane, int R) {
+  using SL = SlotLayout<RM>;
+  if (lane == SL::PODS || lane == SL::ALLOWED) return (int64_t)f.v32;
+  if (lane < 2 * RM) return (lane >> 1) < R ? f.v64 : 0;
+  if (lane == SL::INVC || lane == SL::INVM)
+    return (int64_t)(uint32_t)__float_as_int(f.v64 > 0 ? 1.0f / (float)f.v64 : 1.0f);
+  if (lane == SL::DAC || lane == SL::DAM) return __double_as_longlong((double)f.v64);
+  return lane < SL::W ? f.v64 : 0;
+}
+
+template <int RM>
+__global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
+  using SL = SlotLayout<RM>;
+  constexpr int BLOCK = kP2SBlock, NW = BLOCK / 64, SW = SL::W;
+  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
+  __shared__ ksg_profile s_prof;
+  __shared__ P1Stats s_p1[KSG_BATCH_MAX];
+  __shared__ int32_t s_clist[KSG_BATCH_MAX];
+  __shared__ uint64_t s_top[KSG_BATCH_MAX];    // T_j, sorted descending
+  __shared__ uint64_t s_ce[KSG_BATCH_MAX];     // live record of changed slot i (renormalisation)
+  __shared__ P2Part s_part[NW];
+  __shared__ WRed s_w[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const DevCluster& c = a.c;
+  const int N = c.N, R = c.R;
+  const int cm_words = (((N + 31) / 32) + 3) & ~3;
+  constexpr int POD_WORDS = sizeof(ksg_pod) / 4;
+  uint32_t* s_cmask = reinterpret_cast<uint32_t*>(s_dyn);
+  ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
+  int32_t* s_prog = s_dyn + cm_words + a.nb * POD_WORDS;
+  int64_t* s_slot = reinterpret_cast<int64_t*>(s_dyn + ((cm_words + a.nb * POD_WORDS + a.prog_len + 3) & ~3));
+
+  for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
+  for (int i = tid; i < a.nb * POD_WORDS; i += BLOCK)
+    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
+  for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
+  for (int i = tid; i < a.nb * (int)(sizeof(P1Stats) / 4); i += BLOCK)
+    reinterpret_cast<int32_t*>(s_p1)[i] = reinterpret_cast<const int32_t*>(a.p1)[i];
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  s_top[tid] = a.top[tid];
+  bool fit_filter_on = false;
+  for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
+  __syncthreads();
+  const CmProf cm = cm_prof(s_prof);
+
+  auto changed = [&](int n) { return ((s_cmask[n >> 5] >> (n & 31)) & 1u) != 0; };
+  int nc = 0;                  // |C|, block-uniform
+  int my_node = 0;             // node of slot tid (tid < nc)
+  uint64_t my_rec = 0;         // pod j's phase-1 record at my_node
+  int32_t my_img = 0;
+#ifdef KSG_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
+  KSG_STAMP(0);
+  for (int j = 0; j < a.nb; j++) {
+    const ksg_pod& p = s_pods[j];
+    const ksg_profile& prof = s_prof;
+    const P1Stats s1 = s_p1[j];
+    const PodHot<RM> h = pod_hot<RM>(p, prof, fit_filter_on, R);
+    const int64_t mt1 = s1.mt, ma1 = s1.ma;
+    const bool more = j + 1 < a.nb;
+    const int jn = more ? j + 1 : j;   // row of the next-pod loads (always a valid row)
+
+    // ---- X1: speculated best unchanged node (sorted T_j, first 64 entries) --
+    int spec = -1;
+    {
+      uint64_t key = 0;
+      bool ok = false;
+      if (lane < s1.K) {
+        key = s_top[lane];
+        ok = !changed(key_node(key));
+      }
+      const uint64_t m = __ballot(ok);
+      if (m) spec = key_node(readlane64(key, __builtin_ctzll(m)));
+    }
+    // ---- X2: pod j+1's loads (consumed in Y) ----------------------------------
+    const int K1 = more ? s_p1[j + 1].K : 0;
+    const int nn = tid < nc ? my_node : (spec >= 0 ? spec : 0);
+    uint64_t nx_rec = a.rec[(size_t)jn * N + nn];
+    int32_t nx_img = a.img[(size_t)jn * N + nn];
+    uint64_t nx_top = a.top[(size_t)jn * KSG_BATCH_MAX + tid];
+    SlotFetch<RM> col = slot_word_fetch<RM>(c, a.st, lane, R, spec >= 0 ? spec : 0);
+    KSG_STAMP(1);
+
+    // ---- X3: my changed node on its live slot ---------------------------------
+    P2Part w{0, 0, 0, 0, 0x7fffffff, 0, -1, -1};
+    uint64_t live = 0, my_key = 0;
+    if (tid < nc && (my_rec >> 63)) {
+      int64_t sw[SW];
+      {
+        const int4* src = reinterpret_cast<const int4*>(s_slot + (size_t)tid * SW);
+#pragma unroll
+        for (int k = 0; k < SW / 2; k++) reinterpret_cast<int4*>(sw)[k] = src[k];
+      }
+      const uint64_t x = my_rec;
+      w.cnt_lo = 1;
+      const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff;
+      bool fits = true;
+      if (h.fit_on) {
+        fits = sw[SL::PODS] + 1 <= sw[SL::ALLOWED];
+#pragma unroll
+        for (int r = 0; r < RM; r++) fits = fits && (!((h.req_mask >> r) & 1u) || h.req[r] <= sw[2 * r] - sw[2 * r + 1]);
+      }
+      if (!fits) {
+        w.cnt_hi = (rt == mt1 ? 1u : 0u) + (ra == ma1 ? 0x10000u : 0u);
+      } else {
+        int64_t fs = 0, bs = 0;
+        if (cm.fast) {
+          cm_scores<RM>(cm, h, sw, fs, bs);
+        } else {
+          NodeCols L;
+          slot_row_cols<RM>(sw, L);
+          fs = fit_score(prof, p, L);
+          bs = ba_score(prof, p, L);
+        }
+        const int64_t part = my_img + fs * h.w_fit + bs * h.w_ba;
+        const int64_t nt = mt1 != 0 ? 100 - qdiv(100 * rt, mt1, s1.inv_mt) : 100;
+        const int64_t na = ma1 != 0 ? qdiv(100 * ra, ma1, s1.inv_ma) : ra;
+        my_key = argmax_key(part + nt * h.w_t + na * h.w_a, my_node);
+        w.cnt_lo += 0x10000u;
+        live = pack_rec(part, rt, ra);
+      }
+    }
+    if (tid < nc) s_ce[tid] = live;
+    {
+      const uint64_t k0 = wreduce(my_key, OpMaxU64{});
+      const uint32_t lo = wreduce(w.cnt_lo, OpAdd32{}), hi = wreduce(w.cnt_hi, OpAdd32{});
+      const int32_t cmin = wreduce(live ? my_node : 0x7fffffff, OpMin32{});
+      const uint64_t mk = __ballot(k0 != 0 && my_key == k0), mc = __ballot(live != 0 && my_node == cmin);
+      // best unchanged: this wave's slice of T_j
+      uint64_t tk = 0;
+      if (tid < s1.K) {
+        const uint64_t key = s_top[tid];
+        if (!changed(key_node(key))) tk = key;
+      }
+      const uint64_t bu = wreduce(tk, OpMaxU64{});
+      if (lane == 0) {
+        P2Part o;
+        o.k0 = k0;
+        o.bu = bu;
+        o.cnt_lo = lo;
+        o.cnt_hi = hi;
+        o.cmin = cmin;
+        o.err = 0;
+        o.kidx = mk ? wv * 64 + __builtin_ctzll(mk) : -1;
+        o.cidx = mc ? wv * 64 + __builtin_ctzll(mc) : -1;
+        s_part[wv] = o;
+      }
+    }
+    KSG_STAMP(2);
+    __syncthreads();
+
+    // ---- Y: decide (every wave, identically) -------------------------------
+    uint64_t k0 = 0, bu = 0;
+    uint32_t lo = 0, hi = 0;
+    int32_t cmin = 0x7fffffff, kidx = -1, cidx = -1;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      const P2Part o = s_part[i];
+      if (o.k0 > k0) { k0 = o.k0; kidx = o.kidx; }
+      bu = o.bu > bu ? o.bu : bu;
+      lo += o.cnt_lo;
+      hi += o.cnt_hi;
+      if (o.cmin < cmin) { cmin = o.cmin; cidx = o.cidx; }
+    }
+    const int feas1 = lo & 0xffff, live_n = lo >> 16;
+    const int lost_t = hi & 0xffff, lost_a = hi >> 16;
+    const int unch = s1.nfeas - feas1;   // unchanged feasible nodes
+    int nfeas = unch + live_n;
+    // a phase-1 maximum whose every holder became infeasible, or a range error:
+    // renormalise with the live maxima over all of pod j's records (rare)
+    const bool renorm = nfeas >= 2 && (s1.err || (h.w_t && s1.ht - lost_t <= 0) || (h.w_a && s1.ha - lost_a <= 0));
+    int selected = -1, idx = -1;   // idx: slot of the selected node if it is in C
+    uint32_t status = 0;
+    if (renorm) {
+      const PodView v = make_view(c, prof, p, s_prog + (p.blob - a.prog_lo), a.prog);
+      const uint64_t* rec = a.rec + (size_t)j * N;
+      Red r{0, 0, 0, 0x7fffffff};
+      for (int pass = 0; pass < 2; pass++) {
+        uint64_t best = 0;
+        uint32_t err = 0;
+        auto visit = [&](uint64_t x, int n) {
+          if (!(x >> 63)) return;
+          const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
+          if (pass == 0) {
+            r.nfeas += 1;
+            r.max_t = max(r.max_t, rt);
+            r.max_a = max(r.max_a, ra);
+          } else {
+            const uint64_t key = argmax_key(total_score(v, part, rt, ra, r.max_t, r.max_a, err, nullptr, nullptr), n);
+            best = key > best ? key : best;
+          }
+        };
+        for (int n = tid; n < N; n += BLOCK)
+          if (!changed(n)) visit(rec[n], n);
+        if (tid < nc) visit(s_ce[tid], my_node);
+        if (pass == 0) {
+          WRed o{0, 0, 0, 0, 0, 0, 0, 0};
+          o.k0 = (uint64_t)wreduce(r.max_t, OpMax64{});
+          o.k1 = (uint64_t)wreduce(r.max_a, OpMax64{});
+          o.live = (int32_t)wreduce((uint32_t)r.nfeas, OpAdd32{});
+          if (lane == 0) s_w[wv] = o;
+          __syncthreads();
+          r = Red{0, 0, 0, 0x7fffffff};
+#pragma unroll
+          for (int i = 0; i < NW; i++) {
+            const WRed o2 = s_w[i];
+            r.max_t = max(r.max_t, (int64_t)o2.k0);
+            r.max_a = max(r.max_a, (int64_t)o2.k1);
+            r.nfeas += o2.live;
+          }
+          __syncthreads();
+        } else {
+          WRed o{0, 0, 0, 0, 0, 0, 0, 0};
+          o.k0 = wreduce(best, OpMaxU64{});
+          o.err = (int32_t)wreduce(err, OpOr32{});
+          if (lane == 0) s_w[wv] = o;
+          __syncthreads();
+          uint64_t gb = 0;
+          uint32_t ge = 0;
+#pragma unroll
+          for (int i = 0; i < NW; i++) {
+            gb = s_w[i].k0 > gb ? s_w[i].k0 : gb;
+            ge |= (uint32_t)s_w[i].err;
+          }
+          nfeas = r.nfeas;
+          status |= KSG_ST_SCORED;
+          if (ge) status |= KSG_ST_SCORE_ERROR;
+          else selected = key_node(gb);
+          if (selected >= 0 && changed(selected)) {
+            const uint64_t mk = __ballot(tid < nc && my_node == selected);
+            if (mk) s_w[wv].cmin = wv * 64 + __builtin_ctzll(mk);
+            else if (lane == 0) s_w[wv].cmin = -1;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NW; i++) idx = max(idx, s_w[i].cmin);
+          }
+        }
+      }
+    } else if (nfeas == 1) {
+      if (unch == 1) {
+        selected = key_node(bu);
+      } else {
+        selected = cmin;
+        idx = cidx;
+      }
+    } else if (nfeas >= 2) {
+      status |= KSG_ST_SCORED;
+      if (bu > k0) {
+        selected = key_node(bu);
+      } else {
+        selected = key_node(k0);
+        idx = kidx;
+      }
+    }
+    KSG_STAMP(3);
+
+    // ---- Y: assume ----------------------------------------------------------
+    const bool added = selected >= 0 && idx < 0;
+    if (added && selected != spec) {   // speculation missed: dependent loads
+      if (wv == 0) col = slot_word_fetch<RM>(c, a.st, lane, R, selected);
+      if (tid == nc) {
+        nx_rec = a.rec[(size_t)jn * N + selected];
+        nx_img = a.img[(size_t)jn * N + selected];
+      }
+    }
+    // pod j+1's state into place (waits for X2's loads, before this pod's
+    // stores are issued, so the wait never covers a store)
+    if (added && tid == nc) my_node = selected;
+    if (tid < nc + (added ? 1 : 0)) {
+      my_rec = nx_rec;
+      my_img = nx_img;
+    }
+    if (tid < K1) s_top[tid] = nx_top;
+    const int64_t col_val = slot_word_value<RM>(col, lane, R);
+    if (wv == 0 && selected >= 0) {
+      const int slot = added ? nc : idx;
+      int64_t* row = s_slot + (size_t)slot * SW;
+      if (lane < SW) {
+        int64_t val = added ? col_val : row[lane];
+        if (lane < SL::INVC) {
+          int64_t d = 0;
+          if (lane < 2 * RM) d = (lane & 1) && (lane >> 1) < R ? p.req[lane >> 1] : 0;
+          else if (lane == SL::NZC) d = p.nz_cpu;
+          else if (lane == SL::NZM) d = p.nz_mem;
+          else if (lane == SL::PODS) d = 1;
+          val += d;
+          const int r = lane >> 1;
+          if (lane < 2 * RM && (lane & 1) && r < R) a.st.requested[(size_t)r * N + selected] = val;
+          else if (lane == SL::NZC || lane == SL::NZM) a.st.nonzero[(size_t)(lane - SL::NZC) * N + selected] = val;
+          else if (lane == SL::PODS) a.st.pod_count[selected] = (int32_t)val;
+        }
+        row[lane] = val;
+      }
+      if (lane == 0 && p.commit >= 0) {   // PodTopologySpread / InterPodAffinity count tables
+        const int32_t* cw = s_prog + (p.commit - a.prog_lo);
+        const int ns = *cw++;
+        for (int i = 0; i < ns; i++) a.st.cnt[(size_t)cw[i] * N + selected] += 1;
+        cw += ns;
+        const int nt = *cw++;
+        for (int i = 0; i < nt; i++) {
+          const int t = cw[i];
+          const uint32_t lv = c.label_val[(size_t)c.tmpl_col[t] * N + selected];
+          if (!lv) continue;
+          a.st.tab[c.tmpl_off[t] + lv] += c.tmpl_kind[t] == KSG_TMPL_PREF ? c.tmpl_weight[t] : 1;
+          a.st.tmpl_total[t] += 1;
+        }
+      }
+      if (lane == 0 && added) {
+        s_cmask[selected >> 5] |= 1u << (selected & 31);
+        s_clist[nc] = selected;
+      }
+    }
+    if (tid == 0) {
+      uint32_t score_skip;
+      ipa_skip_bits(prof, p, status, score_skip);
+      const int o = a.out0 + j;
+      a.placements[o] = selected;
+      if (a.results) {
+        ksg_result res;
+        res.selected = selected;
+        res.n_feasible = nfeas;
+        res.status = status;
+        res.score_skip = score_skip;
+        a.results[o] = res;
+      }
+    }
+    nc += added ? 1 : 0;
     KSG_STAMP(4);
     __syncthreads();
     KSG_STAMP(5);
@@ -1473,7 +2041,7 @@ struct ksg_ctx {
   P1Stats* d_p1 = nullptr;
   uint64_t* d_top = nullptr;
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
-  int batch_mode = 1;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset" (default)
+  int batch_mode = 2;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
   bool timing = false;
@@ -1538,7 +2106,8 @@ void free_all(ksg_ctx* ctx) {
 
 // ---- per-kernel timing -------------------------------------------------------
 const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_batch_phase1",
-                                          "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan"};
+                                          "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan",
+                                          "ksg_batch_phase2s"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -1764,13 +2333,18 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   // columns per pod) fits the dynamic LDS budget.
   constexpr size_t kLdsBudget = 120 * 1024;
   const size_t cm_words = (size_t)((((N + 31) / 32) + 3) & ~3);
-  const size_t slot_bytes = 8 * (size_t)(2 * ctx->c.R + 4);
-  const bool topset = ctx->batch_mode == 1;
+  const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;   // ksg_batch_phase2s<RM> instance
+  const size_t slot_bytes = ctx->batch_mode == 2 ? 8 * (size_t)(2 * slot_rm + 8) : 8 * (size_t)(2 * ctx->c.R + 4);
+  const bool topset = ctx->batch_mode >= 1;   // top-set variants keep one slot per pod
   static bool attr_set = false;
   if (!attr_set) {
     HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)kLdsBudget));
     HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
+    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2s<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBudget));
+    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2s<KSG_MAX_RES>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
     attr_set = true;
   }
@@ -1808,9 +2382,15 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     if (topset) {
       hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
       if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
-      hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
       // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
-      if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2, 0.5 * b.nb * (b.nb + 1)))) return trc;
+      if (ctx->batch_mode == 2) {
+        if (slot_rm == 4) hipLaunchKernelGGL(ksg_batch_phase2s<4>, dim3(1), dim3(kP2SBlock), bytes, ctx->stream, b);
+        else hipLaunchKernelGGL(ksg_batch_phase2s<KSG_MAX_RES>, dim3(1), dim3(kP2SBlock), bytes, ctx->stream, b);
+        if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2S, 0.5 * b.nb * (b.nb + 1)))) return trc;
+      } else {
+        hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
+        if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2, 0.5 * b.nb * (b.nb + 1)))) return trc;
+      }
     } else {
       hipLaunchKernelGGL(ksg_batch_phase2_scan<512>, dim3(1), dim3(512), bytes, ctx->stream, b);
       if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2_SCAN, units))) return trc;
@@ -1917,7 +2497,10 @@ int ksg_open(int device, ksg_ctx** out) {
     return KSG_E_DEVICE;
   }
   if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
-  if (const char* f = getenv("KSG_BATCH_MODE")) ctx->batch_mode = std::string(f) == "scan" ? 0 : 1;
+  if (const char* f = getenv("KSG_BATCH_MODE")) {
+    const std::string m(f);
+    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : 2;
+  }
   *out = ctx;
   return KSG_OK;
 }

@@ -38,6 +38,49 @@ __device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
   return v;
 }
 
+// ---- DPP wave reductions, result uniform (in SGPRs) ------------------------
+// Quad swaps, half-row and row mirrors reduce each 16-lane row in four DPP
+// moves; the four row values are combined through v_readlane.  No LDS
+// traffic (a __shfl_xor step is a ds_bpermute round trip).  Call with all 64
+// lanes active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  return ((uint64_t)dpp32<CTRL>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+template <class T, class Op>
+__device__ __forceinline__ T wreduce(T v, Op op) {
+  if constexpr (sizeof(T) == 8) {
+    v = op(v, (T)dpp64<0xB1>((uint64_t)v));    // quad_perm [1,0,3,2]
+    v = op(v, (T)dpp64<0x4E>((uint64_t)v));    // quad_perm [2,3,0,1]
+    v = op(v, (T)dpp64<0x141>((uint64_t)v));   // row_half_mirror
+    v = op(v, (T)dpp64<0x140>((uint64_t)v));   // row_mirror
+    const T r0 = (T)readlane64((uint64_t)v, 0), r1 = (T)readlane64((uint64_t)v, 16);
+    const T r2 = (T)readlane64((uint64_t)v, 32), r3 = (T)readlane64((uint64_t)v, 48);
+    return op(op(r0, r1), op(r2, r3));
+  } else {
+    v = op(v, (T)dpp32<0xB1>((uint32_t)v));
+    v = op(v, (T)dpp32<0x4E>((uint32_t)v));
+    v = op(v, (T)dpp32<0x141>((uint32_t)v));
+    v = op(v, (T)dpp32<0x140>((uint32_t)v));
+    const T r0 = (T)__builtin_amdgcn_readlane((int)v, 0), r1 = (T)__builtin_amdgcn_readlane((int)v, 16);
+    const T r2 = (T)__builtin_amdgcn_readlane((int)v, 32), r3 = (T)__builtin_amdgcn_readlane((int)v, 48);
+    return op(op(r0, r1), op(r2, r3));
+  }
+}
+struct OpMaxU64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; } };
+struct OpMax64 { __device__ int64_t operator()(int64_t a, int64_t b) const { return a > b ? a : b; } };
+struct OpAdd32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpMin32 { __device__ int32_t operator()(int32_t a, int32_t b) const { return a < b ? a : b; } };
+struct OpOr32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
+
 // Per-pod values every lane needs, derived once from the LDS copy of the pod.
 struct PodView {
   const ksg_pod* p;

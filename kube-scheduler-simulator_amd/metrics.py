@@ -69,7 +69,7 @@ def roofline(bytes_per_eval: int, node_evals_per_launch: int, launch_ms: float) 
 #   queue kernels, batch phase 1: one node-eval per (pod, node) = the column
 #     schema above; phase 1 also writes its 8-byte record + 4-byte image part
 #   topk / scan phase 2: one 8-byte record read per (pod, node)
-#   top-set phase 2: per unit one 8-byte top key + 8-byte record + 4-byte image part
+#   top-set phase 2 (both variants): per unit one 8-byte top key + 8-byte record + 4-byte image part
 def kernel_bytes_per_unit(name: str, bytes_per_eval: int) -> int:
     if name in ("ksg_queue_kernel", "ksg_queue_topo_kernel"):
         return bytes_per_eval
@@ -77,7 +77,7 @@ def kernel_bytes_per_unit(name: str, bytes_per_eval: int) -> int:
         return bytes_per_eval + 12
     if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
         return 8
-    if name == "ksg_batch_phase2":
+    if name in ("ksg_batch_phase2", "ksg_batch_phase2s"):
         return 20
     raise KeyError(name)
 

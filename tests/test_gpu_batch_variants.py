@@ -1,5 +1,5 @@
 """GPU parity of every phase-2 variant of the batched placement path
-(KSG_BATCH_MODE): "topset" (default) and "scan".  Same bar
+(KSG_BATCH_MODE): "slot" (default), "topset" and "scan".  Same bar
 as the default path: placements, per-pod results and node state bit-exact
 against the C++ oracle, including split calls."""
 import numpy as np
@@ -22,7 +22,7 @@ def _have_gpu():
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
 
-MODES = ["topset", "scan"]
+MODES = ["slot", "topset", "scan"]
 
 
 @pytest.fixture(scope="module", params=MODES)
