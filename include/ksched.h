@@ -269,7 +269,9 @@ enum {
   KSG_K_BATCH_PHASE2 = 4,
   KSG_K_BATCH_PHASE2_SCAN = 5,
   KSG_K_BATCH_PHASE2S = 6,
-  KSG_NKERNELS = 7
+  KSG_K_SWEEP_STATIC = 7,
+  KSG_K_SWEEP = 8,
+  KSG_NKERNELS = 9
 };
 typedef struct ksg_kernel_stat {
   char name[48];

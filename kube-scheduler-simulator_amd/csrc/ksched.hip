@@ -1602,6 +1602,8 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
 #endif
 }
 
+#include "ksched_sweep.h"
+
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
@@ -2012,7 +2014,7 @@ struct ksg_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
-  int last_path = 0;   // 1 = queue kernel, 2 = batched
+  int last_path = 0;   // 1 = queue kernel, 2 = batched, 3 = replica sweep
   ksg_profile prof{};
   bool have_prof = false, have_nodes = false, have_wl = false;
   // cluster
@@ -2107,7 +2109,7 @@ void free_all(ksg_ctx* ctx) {
 // ---- per-kernel timing -------------------------------------------------------
 const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_batch_phase1",
                                           "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan",
-                                          "ksg_batch_phase2s"};
+                                          "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2402,6 +2404,100 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   return KSG_OK;
 }
 
+// The replica sweep packs the replica-independent plugin results into 8-byte
+// static records and the per-replica result into pack_rec(); use it when
+// every replica profile is node-local and the values provably fit.
+bool sweep_eligible(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first, int count) {
+  if (ctx->c.T > 255) return false;
+  for (int r = 0; r < R; r++) {
+    const ksg_profile& prof = profiles[r];
+    if (needs_topo(ctx, prof, first, count)) return false;
+    int64_t wsum = 0;
+    for (int pl : {KSG_PL_NODE_RESOURCES_FIT, KSG_PL_BALANCED_ALLOCATION, KSG_PL_IMAGE_LOCALITY})
+      if ((prof.score_mask >> pl) & 1u) {
+        if (prof.weight[pl] < 0) return false;
+        wsum += prof.weight[pl];
+      }
+    if (wsum * 100 >= (1ll << 31)) return false;
+  }
+  for (int i = first; i < first + count; i++)
+    if (ctx->h_na_pref_sum[i] > 0xffff || ctx->h_na_pref_sum[i] < 0) return false;
+  return true;
+}
+
+template <int BLOCK, int KN>
+void launch_sweep(const SweepArgs& s, int R, hipStream_t st) {
+  hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true>), dim3(R), dim3(BLOCK), 0, st, s);
+}
+
+// Host mirror of cm_prof().fast: Fit and BalancedAllocation both score exactly
+// {cpu, memory}, Fit with positive weights.
+bool profile_cm_fast(const ksg_profile& prof) {
+  if (prof.fit_n != 2 || prof.ba_n != 2) return false;
+  auto cpumem = [](int a, int b) {
+    return (a == KSG_RES_CPU && b == KSG_RES_MEM) || (a == KSG_RES_MEM && b == KSG_RES_CPU);
+  };
+  return cpumem(prof.fit_res[0], prof.fit_res[1]) && cpumem(prof.ba_res[0], prof.ba_res[1]) &&
+         prof.fit_w[0] > 0 && prof.fit_w[1] > 0;
+}
+
+// R replicas of pods [first, first + count) on the state already copied into
+// a.st (replica strides set); placements [R][count] on the device.
+int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, const ksg_profile* d_prof, int R,
+              int first, int count, int32_t* d_pl, Tmp& tmp) {
+  bool fast = true;
+  for (int r = 0; r < R; r++) fast = fast && profile_cm_fast(profiles[r]);
+  const int N = ctx->c.N;
+  constexpr int kBatch = 64;
+  SweepArgs s{};
+  s.c = ctx->c;
+  s.st = a.st;
+  s.pods = ctx->d_pods;
+  s.prog = ctx->d_prog;
+  s.profiles = d_prof;
+  s.count = count;
+  s.placements = d_pl;
+  TA(tmp, &s.srec, sizeof(uint64_t) * (size_t)kBatch * N);
+  // (BLOCK, KN): KN nodes per lane in registers; KN = 0 streams them through
+  // a per-replica scratch row instead (N > 32,768, or a profile outside the
+  // cpu/memory fast path)
+  int block = N <= 16384 ? 256 : 1024, kn = 0;
+  const struct { int block, kn; } shapes[] = {{256, 8}, {256, 16}, {256, 20}, {256, 24}, {256, 32},
+                                              {512, 32}, {1024, 32}};
+  if (fast)
+    for (const auto& sh : shapes)
+      if (N <= sh.block * sh.kn) { block = sh.block; kn = sh.kn; break; }
+  if (kn == 0) TA(tmp, &s.scratch, sizeof(uint64_t) * (size_t)R * N);
+  (void)hipGetLastError();
+  treset(ctx);
+  HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  int rc;
+  if ((rc = tmark(ctx))) return rc;
+  for (int off = 0; off < count; off += kBatch) {
+    s.b0 = first + off;
+    s.nb = std::min(kBatch, count - off);
+    s.out0 = off;
+    hipLaunchKernelGGL(ksg_sweep_static, dim3((N + 255) / 256, s.nb), dim3(256), 0, ctx->stream, s);
+    if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)s.nb * N))) return rc;
+    switch (fast ? block * 100 + kn : -block) {
+      case 25608: launch_sweep<256, 8>(s, R, ctx->stream); break;
+      case 25616: launch_sweep<256, 16>(s, R, ctx->stream); break;
+      case 25620: launch_sweep<256, 20>(s, R, ctx->stream); break;
+      case 25624: launch_sweep<256, 24>(s, R, ctx->stream); break;
+      case 25632: launch_sweep<256, 32>(s, R, ctx->stream); break;
+      case 51232: launch_sweep<512, 32>(s, R, ctx->stream); break;
+      case 102432: launch_sweep<1024, 32>(s, R, ctx->stream); break;
+      case 102400: launch_sweep<1024, 0>(s, R, ctx->stream); break;
+      case -256: hipLaunchKernelGGL((ksg_sweep<256, 0, false>), dim3(R), dim3(256), 0, ctx->stream, s); break;
+      default: hipLaunchKernelGGL((ksg_sweep<1024, 0, false>), dim3(R), dim3(1024), 0, ctx->stream, s); break;
+    }
+    if ((rc = tlaunched(ctx, KSG_K_SWEEP, (double)R * s.nb * N))) return rc;
+  }
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  return KSG_OK;
+}
+
 int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int32_t* placements,
                  ksg_result* results, ksg_capture* cap) {
   int rc = check_ready(ctx);
@@ -2690,11 +2786,18 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   a.profiles = d_prof;
   a.placements = d_pl;
   a.results = nullptr;
-  const int block = N >= 8192 ? 512 : 256;
-  bool topo = false;
-  for (size_t r = 0; r < RR && !topo; r++) topo = needs_topo(ctx, profiles[r], first, count);
-  if ((rc = launch_queue(ctx, a, (int)RR, block, topo))) return rc;
-  ctx->last_path = 1;
+  bool sweep = sweep_eligible(ctx, profiles, (int)RR, first, count) && count > 0;
+  if (ctx->force_path == 1) sweep = false;
+  if (sweep) {
+    if ((rc = run_sweep(ctx, a, profiles, d_prof, (int)RR, first, count, d_pl, tmp))) return rc;
+    ctx->last_path = 3;
+  } else {
+    const int block = N >= 8192 ? 512 : 256;
+    bool topo = false;
+    for (size_t r = 0; r < RR && !topo; r++) topo = needs_topo(ctx, profiles[r], first, count);
+    if ((rc = launch_queue(ctx, a, (int)RR, block, topo))) return rc;
+    ctx->last_path = 1;
+  }
   HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * RR * count, hipMemcpyDeviceToHost, ctx->stream));
   std::vector<int64_t> req;
   if (summaries) {

@@ -1,0 +1,358 @@
+// Replica sweep (configs 4/5: R what-if scheduler profiles over one queue on
+// one cluster), included by ksched.hip inside its anonymous namespace.
+//
+// Of the per-(pod, node) work, everything except NodeResourcesFit and
+// BalancedAllocation is independent of the replica: the NodeUnschedulable,
+// NodeName, TaintToleration and NodeAffinity verdicts and the raw
+// TaintToleration, NodeAffinity and ImageLocality scores depend on the pod and
+// the node's static columns only (the profiles change which plugins run and
+// their weights, not what a plugin computes).  So:
+//
+//   ksg_sweep_static   grid (node tiles, batch pods): one 8-byte static record
+//                      per (pod, node), computed once for all replicas;
+//   ksg_sweep<BLOCK,KN> one workgroup per replica, persistent over the batch:
+//                      per pod, one sweep over the replica's nodes reads the
+//                      static record and the Fit/BalancedAllocation columns
+//                      (every load of a node issued before any use, no
+//                      data-dependent branches), keeps the packed result of
+//                      each of its KN nodes in registers, reduces (DPP + LDS),
+//                      normalises from the registers, takes the argmax and the
+//                      lane that owns the selected node assumes the pod.
+//
+// The owner lane of node n is n % BLOCK for every pod, so a node's mutable
+// columns are only ever read and written by one lane: an assume needs no
+// barrier.  Results equal ksg_queue_kernel's bit for bit (same plugin
+// arithmetic, same reductions), which the GPU tests check against the oracle.
+
+// static record: bits 0-4 filter verdicts (1 = rejects), 8-15 raw
+// TaintToleration, 16-31 raw NodeAffinity, 32-39 raw ImageLocality.
+constexpr uint32_t kSrUnsched = 1u, kSrNodeName = 2u, kSrTaint = 4u, kSrNodeAff = 8u, kSrNotEval = 16u;
+
+struct SweepArgs {
+  DevCluster c;
+  DevState st;                  // replica r's arrays at base + r * stride
+  const ksg_pod* pods;
+  const int32_t* prog;
+  const ksg_profile* profiles;  // [R]
+  int32_t b0, nb;               // batch = pods [b0, b0 + nb)
+  int32_t out0, count;          // placements[r * count + out0 + j]
+  uint64_t* srec;               // [nb][N] static records
+  uint64_t* scratch;            // KN == 0 only: [R][N] packed per-node results
+  int32_t* placements;
+};
+
+__global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
+  __shared__ int32_t s_blob[KSG_BLOB_MAX];
+  __shared__ ksg_pod s_pod;
+  __shared__ ksg_profile s_prof;
+  const int tid = threadIdx.x;
+  const int j = blockIdx.y;
+  const DevCluster& c = a.c;
+  const int N = c.N;
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles)[tid];
+  stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
+  __syncthreads();
+  const ksg_pod& p = s_pod;
+  const PodView v = make_view(c, s_prof, p, s_blob, a.prog);
+  const int n = blockIdx.x * 256 + tid;
+  if (n >= N) return;
+  const GNode nd{&c, n};
+  uint32_t bits = 0;
+  if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) bits |= kSrNotEval;
+  if (nd.unsched() && !(p.flags & KSG_POD_TOL_UNSCHED)) bits |= kSrUnsched;
+  if (p.node_name != -1 && p.node_name != n) bits |= kSrNodeName;
+  if (untolerated_slot(c, nd, v.tolf) >= 0) bits |= kSrTaint;
+  if (!na_required_match(nd, v.P, v.na_req)) bits |= kSrNodeAff;
+  const uint64_t rt = (uint64_t)taint_score(c, nd, v.tolp);
+  const uint64_t ra = v.na_pref >= 0 ? (uint64_t)na_pref_score(nd, v.P, v.na_pref) : 0;
+  const uint64_t im = (uint64_t)image_score(c, nd, v.P, v.img, p.n_containers);
+  a.srec[(size_t)j * N + n] = bits | ((rt & 0xff) << 8) | ((ra & 0xffff) << 16) | ((im & 0xff) << 32);
+}
+
+// Replica-uniform facts of a profile for the sweep.
+struct SweepProf {
+  bool f_unsched, f_nodename, f_taint, f_na, f_fit;   // filter enabled
+  CmProf cm;
+};
+
+__device__ __forceinline__ SweepProf sweep_prof(const ksg_profile& prof) {
+  SweepProf s{};
+  for (int k = 0; k < prof.n_filter; k++) {
+    const int pl = prof.filter_order[k];
+    s.f_unsched |= pl == KSG_PL_NODE_UNSCHEDULABLE;
+    s.f_nodename |= pl == KSG_PL_NODE_NAME;
+    s.f_taint |= pl == KSG_PL_TAINT_TOLERATION;
+    s.f_na |= pl == KSG_PL_NODE_AFFINITY;
+    s.f_fit |= pl == KSG_PL_NODE_RESOURCES_FIT;
+  }
+  s.cm = cm_prof(prof);
+  return s;
+}
+
+// Pod-uniform values of one replica's evaluation of pod p.
+struct SweepPod {
+  uint32_t fmask;      // static-record bits that reject
+  bool fit_on;
+  uint32_t req_mask;   // resource columns the Fit filter checks
+  int64_t w_fit, w_ba, w_img, w_t, w_a;
+  uint32_t smask;
+};
+
+__device__ __forceinline__ SweepPod sweep_pod(const SweepProf& sp, const ksg_profile& prof, const ksg_pod& p, int R) {
+  SweepPod q;
+  const uint32_t fs = p.filter_skip;
+  auto on = [&](bool en, int pl) { return en && !((fs >> pl) & 1u); };
+  q.fmask = kSrNotEval | (on(sp.f_unsched, KSG_PL_NODE_UNSCHEDULABLE) ? kSrUnsched : 0u) |
+            (on(sp.f_nodename, KSG_PL_NODE_NAME) ? kSrNodeName : 0u) |
+            (on(sp.f_taint, KSG_PL_TAINT_TOLERATION) ? kSrTaint : 0u) |
+            (on(sp.f_na, KSG_PL_NODE_AFFINITY) ? kSrNodeAff : 0u);
+  q.fit_on = on(sp.f_fit, KSG_PL_NODE_RESOURCES_FIT);
+  uint32_t m = 0;
+  for (int r = 0; r < R && r < KSG_MAX_RES; r++)
+    if (p.req[r] > 0 && !(r >= 3 && ((prof.fit_ignored_res >> r) & 1u))) m |= 1u << r;
+  q.req_mask = m;
+  q.smask = prof.score_mask & ~p.score_skip & ~(bit(KSG_PL_INTER_POD_AFFINITY) | bit(KSG_PL_POD_TOPOLOGY_SPREAD));
+  auto w = [&](int pl) { return (q.smask & bit(pl)) ? (int64_t)prof.weight[pl] : (int64_t)0; };
+  q.w_fit = w(KSG_PL_NODE_RESOURCES_FIT);
+  q.w_ba = w(KSG_PL_BALANCED_ALLOCATION);
+  q.w_img = w(KSG_PL_IMAGE_LOCALITY);
+  q.w_t = w(KSG_PL_TAINT_TOLERATION);
+  q.w_a = w(KSG_PL_NODE_AFFINITY);
+  return q;
+}
+
+// Fit (cpu + memory) and BalancedAllocation (cpu + memory) scores from loaded
+// values: fit_score / ba_score restated without branches (cm_scores' arithmetic).
+__device__ __forceinline__ void sweep_cm_scores(const CmProf& m, const ksg_pod& p, int64_t ac, int64_t am, int64_t rc,
+                                                int64_t rm, int64_t zc, int64_t zm, int64_t& fit, int64_t& ba) {
+  const bool hc = ac > 0, hm = am > 0;
+  const int64_t sac = hc ? ac : 1, sam = hm ? am : 1;
+  const float ic = __builtin_amdgcn_rcpf((float)sac), im = __builtin_amdgcn_rcpf((float)sam);
+  const int64_t qc = zc + p.nz_cpu, qm = zm + p.nz_mem;
+  int64_t xc, xm;
+  if (m.least) {
+    xc = qc > ac ? 0 : (ac - qc) * 100;
+    xm = qm > am ? 0 : (am - qm) * 100;
+  } else {
+    xc = (qc > ac ? ac : qc) * 100;
+    xm = (qm > am ? am : qm) * 100;
+  }
+  const int64_t sc = qdiv(xc, sac, ic), sm = qdiv(xm, sam, im);
+  const int64_t num = (hc ? sc * m.wc : 0) + (hm ? sm * m.wm : 0);
+  const int64_t ws = (hc ? m.wc : 0) + (hm ? m.wm : 0);
+  float iws = m.inv_wm;
+  iws = hc ? m.inv_wc : iws;
+  iws = hc && hm ? m.inv_ws : iws;
+  fit = ws == 0 ? 0 : qdiv(num, ws, iws);
+  const double dac = (double)sac, dam = (double)sam;
+  double fc = ddiv((double)(rc + p.req[KSG_RES_CPU]), dac);
+  double fm = ddiv((double)(rm + p.req[KSG_RES_MEM]), dam);
+  fc = fc > 1 ? 1 : fc;
+  fm = fm > 1 ? 1 : fm;
+  const double sd = hc && hm ? fabs((fc - fm) / 2) : 0.0;
+  ba = (int32_t)((1 - sd) * (double)100);
+}
+
+struct OpMaxI32 { __device__ int32_t operator()(int32_t a, int32_t b) const { return a > b ? a : b; } };
+
+struct SweepPart {
+  uint32_t nfeas;
+  int32_t minidx, mt, ma;
+};
+
+// KN > 0: node n = tid + k * BLOCK, k < KN, results kept in registers.
+// KN == 0: nodes tid, tid + BLOCK, ... < N, results in the replica's scratch row.
+// FAST: every replica's Fit and BalancedAllocation score exactly {cpu, memory}
+// with positive weights (CmProf::fast; the host checks it for all replicas).
+template <int BLOCK, int KN, bool FAST>
+__global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) {   // 16 waves per CU
+  constexpr int NW = BLOCK / 64;
+  constexpr int U = !FAST ? 1 : (KN >= 20 ? 2 : 4);   // nodes whose loads are in flight together
+  __shared__ ksg_profile s_prof;
+  __shared__ SweepPart s_part[2][NW];
+  __shared__ uint64_t s_best[2][NW];
+  __shared__ uint32_t s_err[2][NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int rep = blockIdx.x;
+  const DevCluster& c = a.c;
+  const int N = c.N, R = c.R;
+  const size_t NN = (size_t)N;
+  int64_t* requested = a.st.requested + rep * a.st.stride_req;
+  int64_t* nonzero = a.st.nonzero + rep * a.st.stride_nz;
+  int32_t* pod_count = a.st.pod_count + rep * a.st.stride_pc;
+  uint64_t* scratch = KN == 0 ? a.scratch + (size_t)rep * N : nullptr;
+  if (tid < (int)(sizeof(ksg_profile) / 4))
+    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles + rep)[tid];
+  __syncthreads();
+  const ksg_profile& prof = s_prof;
+  const SweepProf sp = sweep_prof(prof);
+  constexpr int KR = KN > 0 ? KN : 1;
+  uint64_t recs[KR];
+
+  for (int j = 0; j < a.nb; j++) {
+    const ksg_pod& p = a.pods[a.b0 + j];
+    const SweepPod q = sweep_pod(sp, prof, p, R);
+    const uint64_t* srec = a.srec + (size_t)j * N;
+    const int par = j & 1;
+
+    // ---- sweep A: filters + raw scores of this lane's nodes ------------------
+    uint32_t nfeas = 0;
+    int32_t minidx = 0x7fffffff, mt = 0, ma = 0;
+    auto eval = [&](int n, uint64_t sr, int64_t ac, int64_t am, int64_t rc, int64_t rm, int64_t zc, int64_t zm,
+                    int32_t pc, int32_t al) -> uint64_t {
+      bool ok = (sr & q.fmask) == 0;
+      if (q.fit_on) {
+        ok = ok && pc + 1 <= al;
+        ok = ok && (!(q.req_mask & 1u) || p.req[KSG_RES_CPU] <= ac - rc);
+        ok = ok && (!(q.req_mask & 2u) || p.req[KSG_RES_MEM] <= am - rm);
+        for (int r = 2; r < R && r < KSG_MAX_RES; r++)   // pod-uniform: loads only for requested columns
+          if ((q.req_mask >> r) & 1u) ok = ok && p.req[r] <= c.alloc[r * NN + n] - requested[r * NN + n];
+      }
+      if (!ok) return 0;
+      int64_t fs = 0, bs = 0;
+      if constexpr (FAST) {
+        sweep_cm_scores(sp.cm, p, ac, am, rc, rm, zc, zm, fs, bs);
+      } else {
+        NodeCols L;
+        load_cols(c, requested, nonzero, pod_count, n, L);
+        fs = fit_score(prof, p, L);
+        bs = ba_score(prof, p, L);
+      }
+      const int64_t rt = (sr >> 8) & 0xff, ra = (sr >> 16) & 0xffff, im = (sr >> 32) & 0xff;
+      const int64_t part = im * q.w_img + ((q.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? fs * q.w_fit : 0) +
+                           ((q.smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? bs * q.w_ba : 0);
+      return pack_rec(part, rt, ra);
+    };
+    auto account = [&](int n, uint64_t x) {
+      if (x >> 63) {
+        nfeas += 1;
+        minidx = min(minidx, n);
+        mt = max(mt, (int32_t)((x >> 48) & 0xff));
+        ma = max(ma, (int32_t)((x >> 32) & 0xffff));
+      }
+    };
+    const int iters = KN > 0 ? KN : (N + BLOCK - 1) / BLOCK;
+    // opaque per pod: keeps the per-node addresses from being hoisted out of
+    // the pod loop (KN x 9 live 64-bit pointers would not fit the VGPR budget)
+    int tb = tid;
+    asm volatile("" : "+v"(tb));
+    auto group = [&](const int k0) {
+      uint64_t sr[U];
+      int64_t ac[U], am[U], rc[U], rm[U], zc[U], zm[U];
+      int32_t pc[U], al[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int n = tb + (k0 + u) * BLOCK;
+        const int nl = n < N ? n : 0;   // clamped: every lane loads from a valid address
+        sr[u] = srec[nl];
+        ac[u] = c.alloc[KSG_RES_CPU * NN + nl];
+        am[u] = c.alloc[KSG_RES_MEM * NN + nl];
+        rc[u] = requested[KSG_RES_CPU * NN + nl];
+        rm[u] = requested[KSG_RES_MEM * NN + nl];
+        zc[u] = nonzero[nl];
+        zm[u] = nonzero[NN + nl];
+        pc[u] = pod_count[nl];
+        al[u] = c.allowed[nl];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int n = tb + (k0 + u) * BLOCK;
+        uint64_t x = 0;
+        if (k0 + u < iters && n < N) x = eval(n, sr[u], ac[u], am[u], rc[u], rm[u], zc[u], zm[u], pc[u], al[u]);
+        account(n, x);
+        if constexpr (KN > 0) {
+          if (k0 + u < KN) recs[k0 + u < KR ? k0 + u : 0] = x;
+        } else {
+          if (n < N) scratch[n] = x;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one group's loads in flight at a time (register budget)
+    };
+    if constexpr (KN > 0) {
+#pragma unroll
+      for (int k0 = 0; k0 < KN; k0 += U) group(k0);
+    } else {
+      for (int k0 = 0; k0 < iters; k0 += U) group(k0);
+    }
+    {
+      SweepPart w;
+      w.nfeas = wreduce(nfeas, OpAdd32{});
+      w.minidx = wreduce(minidx, OpMin32{});
+      w.mt = wreduce(mt, OpMaxI32{});
+      w.ma = wreduce(ma, OpMaxI32{});
+      if (lane == 0) s_part[par][wv] = w;
+    }
+    __syncthreads();
+    uint32_t gn = 0;
+    int32_t gmin = 0x7fffffff, gmt = 0, gma = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      const SweepPart w = s_part[par][i];
+      gn += w.nfeas;
+      gmin = min(gmin, w.minidx);
+      gmt = max(gmt, w.mt);
+      gma = max(gma, w.ma);
+    }
+    int selected = -1;
+    if (gn == 1) {
+      selected = gmin;
+    } else if (gn >= 2) {
+      // ---- sweep B: normalise, weight, argmax (registers only) ---------------
+      const float inv_t = gmt ? __builtin_amdgcn_rcpf((float)gmt) : 1.0f;
+      const float inv_a = gma ? __builtin_amdgcn_rcpf((float)gma) : 1.0f;
+      uint64_t best = 0;
+      uint32_t err = 0;
+      auto score = [&](int n, uint64_t x) {
+        if (!(x >> 63)) return;
+        const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
+        int64_t total = part;
+        if (q.smask & bit(KSG_PL_TAINT_TOLERATION)) {
+          const int64_t s = gmt != 0 ? 100 - qdiv(100 * rt, gmt, inv_t) : 100;
+          err |= (s < 0 || s > 100);
+          total += s * q.w_t;
+        }
+        if (q.smask & bit(KSG_PL_NODE_AFFINITY)) {
+          const int64_t s = gma != 0 ? qdiv(100 * ra, gma, inv_a) : ra;
+          err |= (s < 0 || s > 100);
+          total += s * q.w_a;
+        }
+        const uint64_t key = argmax_key(total, n);
+        best = key > best ? key : best;
+      };
+      if constexpr (KN > 0) {
+#pragma unroll
+        for (int k = 0; k < KN; k++) {
+          score(tb + k * BLOCK, recs[k]);
+          if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        for (int n = tid; n < N; n += BLOCK) score(n, scratch[n]);
+      }
+      best = wreduce(best, OpMaxU64{});
+      err = wreduce(err, OpOr32{});
+      if (lane == 0) {
+        s_best[par][wv] = best;
+        s_err[par][wv] = err;
+      }
+      __syncthreads();
+      uint64_t gb = 0;
+      bool gerr = false;
+#pragma unroll
+      for (int i = 0; i < NW; i++) {
+        gb = s_best[par][i] > gb ? s_best[par][i] : gb;
+        gerr |= s_err[par][i] != 0;
+      }
+      if (!gerr) selected = key_node(gb);
+    }
+    // ---- assume: the lane that owns the selected node ------------------------
+    if (selected >= 0 && (selected % BLOCK) == tid) {
+      for (int r = 0; r < R; r++) requested[(size_t)r * N + selected] += p.req[r];
+      nonzero[selected] += p.nz_cpu;
+      nonzero[NN + selected] += p.nz_mem;
+      pod_count[selected] += 1;
+    }
+    if (tid == 0) a.placements[(size_t)rep * a.count + a.out0 + j] = selected;
+  }
+}

@@ -70,7 +70,16 @@ def roofline(bytes_per_eval: int, node_evals_per_launch: int, launch_ms: float) 
 #     schema above; phase 1 also writes its 8-byte record + 4-byte image part
 #   topk / scan phase 2: one 8-byte record read per (pod, node)
 #   top-set phase 2 (both variants): per unit one 8-byte top key + 8-byte record + 4-byte image part
-def kernel_bytes_per_unit(name: str, bytes_per_eval: int) -> int:
+#   replica sweep, static records (unit = (pod, node)): the replica-independent
+#     columns (unschedulable, taints, labels, images) + the 8-byte record written
+#   replica sweep (unit = (replica, pod, node)): the 8-byte static record + the
+#     Fit / BalancedAllocation columns it reads: allocatable and requested of
+#     cpu and memory, non-zero requested, pod count, allowed pods
+STATIC_COLS = ("unschedulable", "taints", "labels", "images")
+
+
+def kernel_bytes_per_unit(name: str, cols) -> int:
+    bytes_per_eval = sum(cols.values()) if isinstance(cols, dict) else int(cols)
     if name in ("ksg_queue_kernel", "ksg_queue_topo_kernel"):
         return bytes_per_eval
     if name == "ksg_batch_phase1":
@@ -79,10 +88,17 @@ def kernel_bytes_per_unit(name: str, bytes_per_eval: int) -> int:
         return 8
     if name in ("ksg_batch_phase2", "ksg_batch_phase2s"):
         return 20
+    if name in ("ksg_sweep_static", "ksg_sweep"):
+        if not isinstance(cols, dict):
+            raise TypeError("the replica-sweep kernels need the per-column byte counts")
+        if name == "ksg_sweep_static":
+            return sum(cols.get(k, 0) for k in STATIC_COLS) + 8
+        fit = 32 if "alloc" in cols else 0
+        return 8 + fit + sum(cols.get(k, 0) for k in ("nonzero", "pod_count", "allowed_pods"))
     raise KeyError(name)
 
 
-def dominant_kernel_roofline(kstats, bytes_per_eval: int):
+def dominant_kernel_roofline(kstats, bytes_per_eval):
     """Roofline of the kernel with the largest summed time: algorithmic bytes
     per launch / average launch duration; every kernel listed under "kernels"."""
     if not kstats:

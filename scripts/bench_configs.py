@@ -1,0 +1,108 @@
+"""Measure the non-headline configs of BASELINE.json on one MI355X.
+
+  python scripts/bench_configs.py --config 4 [--replicas 1024] [--pods 2000]
+  python scripts/bench_configs.py --config 3 [--pods 20000]
+  python scripts/bench_configs.py --config 5 [--replicas 64] [--pods 500]
+
+Config 4 / 5 run one what-if replica sweep (ksg_run_replicas: R replicas of
+the queue, one workgroup per replica); config 3 runs the single-replica queue
+with PodTopologySpread + InterPodAffinity.  Prints one JSON line with pods/s
+(replica-pods for sweeps), node-evals/s and the per-kernel roofline from HIP
+events on the library's stream.  Pods are a prefix of the config's queue (the
+full queue at configs[3]'s 1,024 x 50,000 would run for minutes per sample);
+the prefix is stated in the output.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "kube-scheduler-simulator_amd"
+G = importlib.import_module(PKG + ".generator")
+E = importlib.import_module(PKG + ".encoder")
+native = importlib.import_module(PKG + ".native")
+metrics = importlib.import_module(PKG + ".metrics")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, required=True, choices=(3, 4, 5))
+    ap.add_argument("--replicas", type=int, default=None)
+    ap.add_argument("--pods", type=int, default=None)
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--reps", type=int, default=2, help="timed repetitions (after one warmup)")
+    args = ap.parse_args()
+
+    t0 = time.time()
+    profiles = None
+    if args.config == 4:
+        R = args.replicas or 1024
+        P = args.pods or 2000
+        nodes, pods, prof, rprofs = G.config4(n_replicas=R, n_nodes=args.nodes or 5000, n_pods=P)
+        workload = f"configs[3]: {R} replicas x {len(nodes)} nodes, first {P} pods of the config-2 queue"
+    elif args.config == 3:
+        P = args.pods or 20000
+        nodes, pods, prof = G.config3(n_nodes=args.nodes or 15000, n_pods=P)
+        R = 1
+        workload = f"configs[2]: {len(nodes)} nodes x {P} pods, PTS + IPA (config3 profile)"
+    else:
+        R = args.replicas or 64
+        P = args.pods or 500
+        nodes, pods, prof = G.config5(n_nodes=args.nodes or 100000, n_pods=P)
+        rprofs = [prof] * R
+        workload = f"configs[4]: {R} replicas x {len(nodes)} nodes, 64 taints/node, 10k images, GPU scalar, {P} pods"
+    log(f"generated in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    log(f"encoded in {time.time() - t0:.1f}s")
+    if args.config in (4, 5):
+        profiles = [E.encode_profile(p, enc.cluster.res_names) for p in rprofs]
+
+    eng = native.Engine(device=0)
+    eng.load(enc, pf)
+
+    def run():
+        if profiles is not None:
+            pl, _ = eng.run_replicas(profiles, 0, P)
+        else:
+            eng.reset_state()
+            pl, _ = eng.run_queue(0, P, results=False)
+        return pl
+
+    run()   # warmup
+    ms = []
+    for _ in range(args.reps):
+        t = time.perf_counter()
+        pl = run()
+        ms.append((time.perf_counter() - t) * 1e3)
+        log(f"rep: wall {ms[-1]:.1f} ms, device {eng.last_kernel_ms():.1f} ms")
+    kms = eng.last_kernel_ms()
+    eng.set_timing(True)
+    run()
+    ks = eng.kernel_stats()
+    eng.set_timing(False)
+    per_eval = metrics.bytes_per_node_eval(enc, prof)
+    bpe = sum(per_eval.values())
+    roof = metrics.dominant_kernel_roofline(ks, per_eval)
+    evals = R * P * len(nodes)
+    out = {
+        "config": args.config, "workload": workload, "replicas": R, "nodes": len(nodes), "pods": P,
+        "device_ms": kms, "wall_ms": min(ms),
+        "pods_per_s": R * P / (kms * 1e-3), "node_evals_per_s": evals / (kms * 1e-3),
+        "scheduled": int((pl >= 0).sum()), "bytes_per_node_eval": bpe, "columns": per_eval,
+        "roofline": roof,
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

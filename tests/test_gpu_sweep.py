@@ -1,0 +1,105 @@
+"""GPU parity of the replica sweep (ksg_run_replicas): the
+static-record + per-replica sweep kernels against the C++ oracle run replica by
+replica, bit-exact placements and summaries.  Cases cover every (BLOCK, KN)
+shape the host picks (registers: N <= 2,048 ... 32,768; scratch row: N >
+32,768), the generic (non cpu/memory) profile path, mixed strategies and
+weights, nodeName / unschedulable / taint / affinity edge cases from the zoo
+under node-local profiles, and profiles that fall back to the queue kernel."""
+import numpy as np
+import pytest
+
+from conftest import pkg
+
+G = pkg("generator")
+E = pkg("encoder")
+P = pkg("profile")
+m = pkg("model")
+native = pkg("native")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu(built):
+    return native.Engine(device=0)
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import binding
+    return binding.Oracle(8)
+
+
+NODE_LOCAL = [("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0), ("TaintToleration", 3),
+              ("NodeAffinity", 2), ("NodeResourcesFit", 1), ("NodeResourcesBalancedAllocation", 1),
+              ("ImageLocality", 1), ("DefaultBinder", 0)]
+
+
+def _zoo_profiles(k):
+    rng = np.random.Generator(np.random.PCG64(100 + k))
+    out = []
+    for r in range(k):
+        plugins = [(n, int(rng.integers(1, 6)) if w else 0) for n, w in NODE_LOCAL]
+        strat = P.LEAST_ALLOCATED if r % 2 == 0 else P.MOST_ALLOCATED
+        out.append(P.Profile(plugins=plugins, fit_strategy=strat))
+    return out
+
+
+def _c2(n_nodes, n_pods, seed=2):
+    nodes, pods, base = G.config2(n_nodes=n_nodes, n_pods=n_pods, seed=seed)
+    return nodes, pods, base
+
+
+CASES = [
+    # (name, workload, replica profiles)
+    ("c2-150x300-r6", lambda: _c2(150, 300), lambda: G.replica_profiles(6)),
+    ("c2-tight-r4", lambda: _c2(7, 120, seed=11), lambda: G.replica_profiles(4)),
+    ("c2-3000x200-r8", lambda: _c2(3000, 200), lambda: G.replica_profiles(8)),      # KN 16
+    ("c2-5000x150-r8", lambda: _c2(5000, 150), lambda: G.replica_profiles(8)),      # KN 20
+    ("c2-6000x80-r3", lambda: _c2(6000, 80), lambda: G.replica_profiles(3)),        # KN 24
+    ("c2-8000x60-r3", lambda: _c2(8000, 60), lambda: G.replica_profiles(3)),        # KN 32
+    ("c2-12000x50-r2", lambda: _c2(12000, 50), lambda: G.replica_profiles(2)),      # 512 lanes
+    ("c2-20000x40-r2", lambda: _c2(20000, 40), lambda: G.replica_profiles(2)),      # 1024 lanes
+    ("c2-33000x30-r2", lambda: _c2(33000, 30), lambda: G.replica_profiles(2)),      # scratch row
+    ("c5-generic-r3", lambda: G.config5(n_nodes=400, n_pods=300, n_images=200, taint_vocab=128,
+                                        taints_per_node=16, images_per_node=20), None),
+    ("c1-default-r2", lambda: G.config1(n_nodes=100, n_pods=300), None),            # PTS/IPA: queue kernel
+] + [(f"zoo-{s}-r4", (lambda s=s: __import__("zoo").zoo(s)), (lambda: _zoo_profiles(4))) for s in range(6)]
+
+
+@pytest.mark.parametrize("name,make,profs", CASES, ids=[c[0] for c in CASES])
+def test_sweep_matches_oracle(gpu, oracle, name, make, profs):
+    nodes, pods, base = make()
+    enc = E.Encoder(nodes, pods, base)
+    if profs is None:   # the workload's own profile, with varied weights / strategy
+        plist = []
+        for r in range(3 if name.startswith("c5") else 2):
+            plugins = [(n, (w + r) if w else 0) for n, w in base.plugins]
+            plist.append(P.Profile(plugins=plugins, fit_strategy=r % 2, fit_resources=base.fit_resources,
+                                   ba_resources=base.ba_resources))
+    else:
+        plist = profs()
+    pf = [E.encode_profile(p, enc.cluster.res_names) for p in plist]
+    gpu.load(enc, pf[0])
+    oracle.load(enc, pf[0])
+    pl, sums = gpu.run_replicas(pf, 0, len(pods))
+    want, wsums = oracle.run_replicas(pf, 0, len(pods))
+    for r in range(len(pf)):
+        bad = np.nonzero(pl[r] != want[r])[0]
+        assert bad.size == 0, f"{name} replica {r}: first mismatch at pod {bad[:5]}: gpu {pl[r][bad[:5]]} " \
+                              f"oracle {want[r][bad[:5]]}"
+    for f in wsums.dtype.names:
+        np.testing.assert_array_equal(sums[f], wsums[f], err_msg=f)
+    assert (pl >= 0).any()
+
+
+def test_sweep_queue_subrange(gpu, oracle):
+    """A sub-range of the queue (batches not aligned to the first pod)."""
+    nodes, pods, base = _c2(400, 300)
+    enc = E.Encoder(nodes, pods, base)
+    pf = [E.encode_profile(p, enc.cluster.res_names) for p in G.replica_profiles(5)]
+    gpu.load(enc, pf[0])
+    oracle.load(enc, pf[0])
+    pl, _ = gpu.run_replicas(pf, 100, 150)
+    want, _ = oracle.run_replicas(pf, 100, 150)
+    np.testing.assert_array_equal(pl, want)
