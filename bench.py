@@ -150,11 +150,17 @@ def main():
             roof = metrics.roofline(bpe, P * len(nodes), kms)
         roof["step"] = metrics.roofline(bpe, P * len(nodes), kms)
         roof["step"]["kernel_ms"] = kms
+        # HBM bytes per launch of the dominant kernel from the committed PMC
+        # passes (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE
+        # + WRITE_SIZE per dispatch, gfx950-corrected), null when not collected
         roof["traffic"] = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_config2.json")
-        if os.path.exists(pmc):
+        pmc = os.path.join(ROOT, "profiles", "r1", "pmc_config2.json")
+        if os.path.exists(pmc) and roof.get("kernel"):
             try:
-                roof["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                row = json.load(open(pmc)).get(roof["kernel"])
+                if row:
+                    roof["traffic"] = row["hbm_bytes_per_dispatch"]
+                    roof["traffic_source"] = "profiles/r1/pmc_config2.json"
             except Exception:
                 pass
         roof["bytes_per_node_eval"] = bpe

@@ -36,6 +36,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "ksched_kernels.h"
@@ -1995,6 +1996,36 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
   }
 }
 
+// dst[r * stride + i] = src[i] for every replica r = blockIdx.y (replica state
+// initialisation: one launch per array instead of one copy per replica).
+template <typename T>
+__global__ __launch_bounds__(256) void ksg_broadcast(const T* __restrict__ src, T* __restrict__ dst, size_t len,
+                                                     size_t stride) {
+  T* d = dst + (size_t)blockIdx.y * stride;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (size_t)gridDim.x * 256) d[i] = src[i];
+}
+
+// Per replica: Σ requested cpu and Σ requested memory over the nodes (summaries).
+__global__ __launch_bounds__(256) void ksg_replica_sums(const int64_t* requested, size_t stride, int N,
+                                                        int64_t* out) {
+  __shared__ int64_t s_p[2][4];
+  const int64_t* q = requested + (size_t)blockIdx.x * stride;
+  int64_t a = 0, b = 0;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    a += q[n];
+    b += q[(size_t)N + n];
+  }
+  a = wave_sum64(a);
+  b = wave_sum64(b);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { s_p[0][wv] = a; s_p[1][wv] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = s_p[0][0] + s_p[0][1] + s_p[0][2] + s_p[0][3];
+    out[2 * blockIdx.x + 1] = s_p[1][0] + s_p[1][1] + s_p[1][2] + s_p[1][3];
+  }
+}
+
 __global__ void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods, const int32_t* prog, int pod,
                                   int node) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -2762,32 +2793,46 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   DevState& s = a.st;
   s.stride_req = R * N; s.stride_nz = 2 * N; s.stride_pc = N; s.stride_cnt = S * N; s.stride_tab = ctx->tab_words;
   s.stride_tt = NT; s.stride_part = N; s.stride_sraw = 4 * N;
+  bool sweep = sweep_eligible(ctx, profiles, (int)RR, first, count) && count > 0;
+  if (ctx->force_path == 1) sweep = false;
+  // the sweep reads and writes only the Fit columns; the queue kernels also
+  // keep the PodTopologySpread / InterPodAffinity tables and per-node scratch
   TA(tmp, &s.requested, 8 * RR * s.stride_req);
   TA(tmp, &s.nonzero, 8 * RR * s.stride_nz);
   TA(tmp, &s.pod_count, 4 * RR * s.stride_pc);
-  TA(tmp, &s.cnt, 4 * RR * s.stride_cnt);
-  TA(tmp, &s.tab, 4 * RR * s.stride_tab);
-  TA(tmp, &s.tmpl_total, 4 * RR * s.stride_tt);
-  TA(tmp, &s.partial, 8 * RR * s.stride_part);
-  TA(tmp, &s.sraw, 8 * RR * s.stride_sraw);
+  if (!sweep) {
+    TA(tmp, &s.cnt, 4 * RR * s.stride_cnt);
+    TA(tmp, &s.tab, 4 * RR * s.stride_tab);
+    TA(tmp, &s.tmpl_total, 4 * RR * s.stride_tt);
+    TA(tmp, &s.partial, 8 * RR * s.stride_part);
+    TA(tmp, &s.sraw, 8 * RR * s.stride_sraw);
+  }
   ksg_profile* d_prof;
   int32_t* d_pl;
+  int64_t* d_sums;
   TA(tmp, &d_prof, sizeof(ksg_profile) * RR);
   TA(tmp, &d_pl, sizeof(int32_t) * RR * count);
-  for (size_t r = 0; r < RR; r++) {  // every replica starts from the ctx's current state
-    HIPC(ctx, hipMemcpyAsync(s.requested + r * s.stride_req, ctx->st.requested, 8 * s.stride_req, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPC(ctx, hipMemcpyAsync(s.nonzero + r * s.stride_nz, ctx->st.nonzero, 8 * s.stride_nz, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPC(ctx, hipMemcpyAsync(s.pod_count + r * s.stride_pc, ctx->st.pod_count, 4 * s.stride_pc, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPC(ctx, hipMemcpyAsync(s.cnt + r * s.stride_cnt, ctx->st.cnt, 4 * s.stride_cnt, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPC(ctx, hipMemcpyAsync(s.tab + r * s.stride_tab, ctx->st.tab, 4 * s.stride_tab, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPC(ctx, hipMemcpyAsync(s.tmpl_total + r * s.stride_tt, ctx->st.tmpl_total, 4 * s.stride_tt, hipMemcpyDeviceToDevice, ctx->stream));
+  TA(tmp, &d_sums, sizeof(int64_t) * 2 * RR);
+  // every replica starts from the ctx's current state
+  auto bcast = [&](auto* src, auto* dst, size_t len, size_t stride) {
+    using T = std::remove_pointer_t<decltype(dst)>;
+    const unsigned bx = (unsigned)std::min<size_t>((len + 255) / 256, 64);
+    hipLaunchKernelGGL(ksg_broadcast<T>, dim3(std::max(bx, 1u), (unsigned)RR), dim3(256), 0, ctx->stream,
+                       (const T*)src, dst, len, stride);
+  };
+  bcast(ctx->st.requested, s.requested, s.stride_req, s.stride_req);
+  bcast(ctx->st.nonzero, s.nonzero, s.stride_nz, s.stride_nz);
+  bcast(ctx->st.pod_count, s.pod_count, s.stride_pc, s.stride_pc);
+  if (!sweep) {
+    bcast(ctx->st.cnt, s.cnt, s.stride_cnt, s.stride_cnt);
+    bcast(ctx->st.tab, s.tab, s.stride_tab, s.stride_tab);
+    bcast(ctx->st.tmpl_total, s.tmpl_total, s.stride_tt, s.stride_tt);
   }
+  HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipMemcpyAsync(d_prof, profiles, sizeof(ksg_profile) * RR, hipMemcpyHostToDevice, ctx->stream));
   a.profiles = d_prof;
   a.placements = d_pl;
   a.results = nullptr;
-  bool sweep = sweep_eligible(ctx, profiles, (int)RR, first, count) && count > 0;
-  if (ctx->force_path == 1) sweep = false;
   if (sweep) {
     if ((rc = run_sweep(ctx, a, profiles, d_prof, (int)RR, first, count, d_pl, tmp))) return rc;
     ctx->last_path = 3;
@@ -2799,10 +2844,12 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     ctx->last_path = 1;
   }
   HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * RR * count, hipMemcpyDeviceToHost, ctx->stream));
-  std::vector<int64_t> req;
+  std::vector<int64_t> sums(2 * RR);
   if (summaries) {
-    req.resize(RR * s.stride_req);
-    HIPC(ctx, hipMemcpyAsync(req.data(), s.requested, 8 * RR * s.stride_req, hipMemcpyDeviceToHost, ctx->stream));
+    hipLaunchKernelGGL(ksg_replica_sums, dim3((unsigned)RR), dim3(256), 0, ctx->stream, (const int64_t*)s.requested,
+                       s.stride_req, (int)N, d_sums);
+    HIPC(ctx, hipGetLastError());
+    HIPC(ctx, hipMemcpyAsync(sums.data(), d_sums, sizeof(int64_t) * 2 * RR, hipMemcpyDeviceToHost, ctx->stream));
   }
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
   float ms = 0;
@@ -2820,10 +2867,8 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
         for (int b = 0; b < 4; b++) { h ^= (uint8_t)(((uint32_t)v) >> (8 * b)); h *= 1099511628211ull; }
       }
       sm.placement_hash = h;
-      for (size_t n = 0; n < N; n++) {
-        sm.cpu_requested += req[r * s.stride_req + n];
-        sm.mem_requested += req[r * s.stride_req + N + n];
-      }
+      sm.cpu_requested = sums[2 * r];
+      sm.mem_requested = sums[2 * r + 1];
     }
   }
   return KSG_OK;

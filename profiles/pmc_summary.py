@@ -1,0 +1,55 @@
+"""Fold rocprofv3 outputs of profiles/run_pmc.sh into per-kernel summaries.
+
+  python profiles/pmc_summary.py <run_pmc out dir> <dest dir>
+
+Writes <dest>/{bench,sweep}_kernel_stats.csv (the --stats summaries, copied)
+and <dest>/pmc_{config2,config4}.json: per kernel, dispatches, average
+FETCH_SIZE and WRITE_SIZE per dispatch (KB as rocprofv3 reports them) and HBM
+bytes per dispatch = 2 x FETCH_SIZE + WRITE_SIZE (x 1024): the gfx950
+correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE counts half the bytes of
+wide coalesced reads; WRITE_SIZE exact).  The sweep/bench kernels read 8-byte
+words per lane, a width the guide leaves uncalibrated, so the raw counters are
+kept beside the corrected figure.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def counters(path):
+    """{kernel: [values per dispatch]} from a counter_collection.csv."""
+    out = defaultdict(list)
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
+                name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1)
+                name = name.split("(")[0].split("<")[0].strip()
+                out[name].append(float(row["Counter_Value"]))
+    return out
+
+
+def main():
+    src, dest = sys.argv[1], sys.argv[2]
+    os.makedirs(dest, exist_ok=True)
+    for tag, cfg in (("bench", "config2"), ("sweep", "config4")):
+        for f in glob.glob(os.path.join(src, f"{tag}_kt", "**", "*kernel_stats.csv"), recursive=True):
+            shutil.copy(f, os.path.join(dest, f"{tag}_kernel_stats.csv"))
+        fetch, write = counters(os.path.join(src, f"{tag}_fetch")), counters(os.path.join(src, f"{tag}_write"))
+        res = {}
+        for k in sorted(set(fetch) | set(write)):
+            fv, wv = fetch.get(k, []), write.get(k, [])
+            fa = sum(fv) / len(fv) if fv else None
+            wa = sum(wv) / len(wv) if wv else None
+            res[k] = {"dispatches": max(len(fv), len(wv)), "fetch_size_kb": fa, "write_size_kb": wa,
+                      "hbm_bytes_per_dispatch": None if fa is None or wa is None else (2 * fa + wa) * 1024}
+        json.dump(res, open(os.path.join(dest, f"pmc_{cfg}.json"), "w"), indent=1)
+        print(cfg, json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

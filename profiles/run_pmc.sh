@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-1 profiles on one MI355X (run from the repo root on the GPU box):
+#   1. rocprofv3 --kernel-trace --stats of the default bench (config 2)
+#   2. PMC passes FETCH_SIZE and WRITE_SIZE (separate runs) of the same bench
+#   3. the same three for the config-4 replica sweep (scripts/bench_configs.py)
+# Summaries are folded by profiles/pmc_summary.py into profiles/r1/.
+set -uo pipefail
+OUT=${1:-gpurun_out/pmc}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1"
+S="python3 scripts/bench_configs.py --config 4 --replicas 1024 --pods 256 --reps 1"
+SP="$S --no-timing"
+run() {  # name, rocprof args..., -- command
+  local name=$1; shift
+  timeout -k 10 240 rocprofv3 "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit 1; }
+}
+if [ -z "${SKIP_BENCH:-}" ]; then
+run bench_kt --kernel-trace --stats --output-format csv -d "$OUT/bench_kt" -o run -- $B
+run bench_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/bench_fetch" -o run -- $B
+run bench_write --pmc WRITE_SIZE --output-format csv -d "$OUT/bench_write" -o run -- $B
+fi
+run sweep_kt --kernel-trace --stats --output-format csv -d "$OUT/sweep_kt" -o run -- $S
+run sweep_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/sweep_fetch" -o run -- $SP
+run sweep_write --pmc WRITE_SIZE --output-format csv -d "$OUT/sweep_write" -o run -- $SP
+find "$OUT" -name "*.csv" | sort

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--reps", type=int, default=2, help="timed repetitions (after one warmup)")
+    ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event run (PMC passes)")
     args = ap.parse_args()
 
     t0 = time.time()
@@ -86,13 +87,15 @@ def main():
         ms.append((time.perf_counter() - t) * 1e3)
         log(f"rep: wall {ms[-1]:.1f} ms, device {eng.last_kernel_ms():.1f} ms")
     kms = eng.last_kernel_ms()
-    eng.set_timing(True)
-    run()
-    ks = eng.kernel_stats()
-    eng.set_timing(False)
     per_eval = metrics.bytes_per_node_eval(enc, prof)
     bpe = sum(per_eval.values())
-    roof = metrics.dominant_kernel_roofline(ks, per_eval)
+    roof = None
+    if not args.no_timing:
+        eng.set_timing(True)
+        run()
+        ks = eng.kernel_stats()
+        eng.set_timing(False)
+        roof = metrics.dominant_kernel_roofline(ks, per_eval)
     evals = R * P * len(nodes)
     out = {
         "config": args.config, "workload": workload, "replicas": R, "nodes": len(nodes), "pods": P,
