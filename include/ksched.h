@@ -271,7 +271,8 @@ enum {
   KSG_K_BATCH_PHASE2S = 6,
   KSG_K_SWEEP_STATIC = 7,
   KSG_K_SWEEP = 8,
-  KSG_NKERNELS = 9
+  KSG_K_TOPO_COOP = 9,
+  KSG_NKERNELS = 10
 };
 typedef struct ksg_kernel_stat {
   char name[48];

@@ -1996,6 +1996,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
   }
 }
 
+#include "ksched_topo_coop.h"
+
 // dst[r * stride + i] = src[i] for every replica r = blockIdx.y (replica state
 // initialisation: one launch per array instead of one copy per replica).
 template <typename T>
@@ -2045,7 +2047,7 @@ struct ksg_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
-  int last_path = 0;   // 1 = queue kernel, 2 = batched, 3 = replica sweep
+  int last_path = 0;   // 1 = queue kernel, 2 = batched, 3 = replica sweep, 4 = chip-wide topology
   ksg_profile prof{};
   bool have_prof = false, have_nodes = false, have_wl = false;
   // cluster
@@ -2073,6 +2075,11 @@ struct ksg_ctx {
   int32_t* d_pmax = nullptr;
   P1Stats* d_p1 = nullptr;
   uint64_t* d_top = nullptr;
+  // chip-wide topology path buffers (lazily allocated)
+  CoopAcc* d_coop_acc = nullptr;
+  unsigned* d_coop_flags = nullptr;   // [0] barrier counter, [1] timeout
+  int coop_gmax = 0;                  // co-resident workgroups of ksg_topo_coop
+  bool topo_coop = true;              // env KSG_TOPO_COOP=0 disables
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
   int batch_mode = 2;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default)
   // per-kernel timing (ksg_set_timing): one event before the first and after
@@ -2135,12 +2142,15 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_p1 = nullptr;
   ctx->d_top = nullptr;
   ctx->d_stamps = nullptr;
+  ctx->d_coop_acc = nullptr;
+  ctx->d_coop_flags = nullptr;
 }
 
 // ---- per-kernel timing -------------------------------------------------------
 const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_batch_phase1",
                                           "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan",
-                                          "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep"};
+                                          "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
+                                          "ksg_topo_coop"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2529,6 +2539,72 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   return KSG_OK;
 }
 
+template <int KN>
+int launch_coop(ksg_ctx* ctx, const CoopArgs& a, int* gmax_out) {
+  int occ = 0, cus = 0;
+  HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)ksg_topo_coop<KN>, 256, 0));
+  HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  *gmax_out = occ * cus;
+  if (a.G > occ * cus) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: grid exceeds co-resident workgroups");
+  hipLaunchKernelGGL(ksg_topo_coop<KN>, dim3(a.G), dim3(256), 0, ctx->stream, a);
+  return KSG_OK;
+}
+
+// Single replica, PodTopologySpread / InterPodAffinity, no capture: the queue
+// on G co-resident workgroups (ksched_topo_coop.h).
+int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
+                  const ksg_profile* d_prof) {
+  const int N = ctx->c.N;
+  int rc;
+  if (!ctx->d_coop_acc) {
+    if ((rc = dalloc(ctx, &ctx->d_coop_acc, 2))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 4))) return rc;
+  }
+  if (!ctx->coop_gmax) {
+    int occ = 0, cus = 0;
+    HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)ksg_topo_coop<1>, 256, 0));
+    HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    ctx->coop_gmax = std::min(occ * cus, cus);   // one workgroup per CU: lanes wait on memory, not issue
+  }
+  int kn = 1;
+  while ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N && kn < 32) kn *= 2;
+  if ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: too many nodes");
+  CoopArgs a{};
+  a.c = ctx->c;
+  a.st = ctx->st;
+  a.pods = ctx->d_pods;
+  a.prog = ctx->d_prog;
+  a.profile = d_prof;
+  a.first = first;
+  a.count = count;
+  a.G = (int)((N + 256 * kn - 1) / (256 * kn));
+  a.placements = d_pl;
+  a.results = d_res;
+  a.acc = ctx->d_coop_acc;
+  a.bar = ctx->d_coop_flags;
+  a.timeout = ctx->d_coop_flags + 1;
+  HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 16, ctx->stream));
+  hipLaunchKernelGGL(ksg_topo_coop_init, dim3(2), dim3(256), 0, ctx->stream, ctx->d_coop_acc);
+  (void)hipGetLastError();
+  treset(ctx);
+  HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  if ((rc = tmark(ctx))) return rc;
+  int gmax = 0;
+  switch (kn) {
+    case 1: rc = launch_coop<1>(ctx, a, &gmax); break;
+    case 2: rc = launch_coop<2>(ctx, a, &gmax); break;
+    case 4: rc = launch_coop<4>(ctx, a, &gmax); break;
+    case 8: rc = launch_coop<8>(ctx, a, &gmax); break;
+    case 16: rc = launch_coop<16>(ctx, a, &gmax); break;
+    default: rc = launch_coop<32>(ctx, a, &gmax); break;
+  }
+  if (rc) return rc;
+  HIPC(ctx, hipGetLastError());
+  if ((rc = tlaunched(ctx, KSG_K_TOPO_COOP, (double)count * N))) return rc;
+  HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  return KSG_OK;
+}
+
 int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int32_t* placements,
                  ksg_result* results, ksg_capture* cap) {
   int rc = check_ready(ctx);
@@ -2572,7 +2648,13 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     a.placements = d_pl;
     a.results = d_res;
     const int block = N >= 512 ? 512 : 256;   // 512 lanes: <= 256 VGPRs per lane, no spills
-    if ((rc = launch_queue(ctx, a, 1, block, needs_topo(ctx, ctx->prof, first, count)))) return rc;
+    const bool topo = needs_topo(ctx, ctx->prof, first, count);
+    if (topo && !want_cap && ctx->topo_coop && ctx->force_path != 1) {
+      ctx->last_path = 4;
+      if ((rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof))) return rc;
+    } else if ((rc = launch_queue(ctx, a, 1, block, topo))) {
+      return rc;
+    }
   }
   if (placements) HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * count, hipMemcpyDeviceToHost, ctx->stream));
   if (results) HIPC(ctx, hipMemcpyAsync(results, d_res, sizeof(ksg_result) * count, hipMemcpyDeviceToHost, ctx->stream));
@@ -2587,6 +2669,11 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
   if ((rc = tcollect(ctx))) return rc;
+  if (ctx->last_path == 4) {
+    unsigned flags[2] = {0, 0};
+    HIPC(ctx, hipMemcpy(flags, ctx->d_coop_flags, sizeof(flags), hipMemcpyDeviceToHost));
+    if (flags[1]) return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
+  }
   return KSG_OK;
 }
 
@@ -2624,6 +2711,7 @@ int ksg_open(int device, ksg_ctx** out) {
     return KSG_E_DEVICE;
   }
   if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
+  if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : 2;

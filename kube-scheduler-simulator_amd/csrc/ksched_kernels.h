@@ -192,6 +192,12 @@ struct TopoCtx {
   const int32_t* hist;   // LDS
   const int32_t* cnt;    // replica's cnt[S][N]
   const int32_t* tab;    // replica's template tables
+  bool coherent;         // tab is written by other workgroups of this launch (ksg_topo_coop):
+                         // read it with agent-scope atomic loads, never from a cache line
+  __device__ __forceinline__ int32_t tabv(int idx) const {
+    if (coherent) return __hip_atomic_load(const_cast<int32_t*>(tab) + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return tab[idx];
+  }
 };
 
 __device__ __forceinline__ void parse_topo(const ksg_pod& p, const int32_t* P, uint32_t fskip, uint32_t smask,
@@ -333,7 +339,7 @@ __device__ __forceinline__ uint32_t ipa_filter_node(const DevCluster& c, const T
   for (int i = 0; i < g.n_ma; i++) {
     const int tm = g.m_anti[i];
     const uint32_t val = lab(c, c.tmpl_col[tm], n);
-    if (val && t.tab[c.tmpl_off[tm] + val] > 0) return 3;
+    if (val && t.tabv(c.tmpl_off[tm] + val) > 0) return 3;
   }
   return 0;
 }
@@ -377,12 +383,12 @@ __device__ __forceinline__ int64_t ipa_score_node(const DevCluster& c, const ksg
     for (int i = 0; i < g.n_mh; i++) {
       const int tm = g.m_hard[i];
       const uint32_t val = lab(c, c.tmpl_col[tm], n);
-      if (val) sc += (int64_t)prof.hard_pod_affinity_weight * t.tab[c.tmpl_off[tm] + val];
+      if (val) sc += (int64_t)prof.hard_pod_affinity_weight * t.tabv(c.tmpl_off[tm] + val);
     }
   for (int i = 0; i < g.n_mp; i++) {
     const int tm = g.m_pref[i];
     const uint32_t val = lab(c, c.tmpl_col[tm], n);
-    if (val) sc += t.tab[c.tmpl_off[tm] + val];
+    if (val) sc += t.tabv(c.tmpl_off[tm] + val);
   }
   return sc;
 }

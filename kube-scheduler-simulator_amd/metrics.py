@@ -80,7 +80,7 @@ STATIC_COLS = ("unschedulable", "taints", "labels", "images")
 
 def kernel_bytes_per_unit(name: str, cols) -> int:
     bytes_per_eval = sum(cols.values()) if isinstance(cols, dict) else int(cols)
-    if name in ("ksg_queue_kernel", "ksg_queue_topo_kernel"):
+    if name in ("ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_topo_coop"):
         return bytes_per_eval
     if name == "ksg_batch_phase1":
         return bytes_per_eval + 12

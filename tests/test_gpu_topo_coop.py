@@ -1,0 +1,59 @@
+"""GPU parity of the chip-wide PodTopologySpread / InterPodAffinity path
+(ksg_topo_coop): G workgroups share each pod through grid
+barriers.  Placements, per-pod results and the node state after the queue are
+compared bit for bit with the C++ oracle at sizes that spread a pod over many
+workgroups (G = N / 256), including the zoo's edge cases (several soft
+constraints: the extra-barrier branch; minDomains; namespaces; existing pods'
+terms) and split calls."""
+import numpy as np
+import pytest
+
+from conftest import pkg
+
+G = pkg("generator")
+E = pkg("encoder")
+native = pkg("native")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu(built):
+    return native.Engine(device=0)
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import binding
+    return binding.Oracle(8)
+
+
+CASES = [
+    ("c3-4000x1200", lambda: G.config3(n_nodes=4000, n_pods=1200, apps=60, zones=8)),
+    ("c3-15000x300", lambda: G.config3(n_nodes=15000, n_pods=300)),
+    ("c1-2000x800", lambda: G.config1(n_nodes=2000, n_pods=800)),
+] + [(f"zoo-big-{s}", (lambda s=s: __import__("zoo").zoo(s, n_nodes=700, n_pods=400, apps=7, zones=5)))
+     for s in range(4)]
+
+
+@pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
+def test_topo_coop_matches_oracle(gpu, oracle, name, make):
+    nodes, pods, prof = make()
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    oracle.load(enc, pf)
+    pg, rg = gpu.run_queue(0, len(pods))
+    po, ro = oracle.run_queue(0, len(pods))
+    bad = np.nonzero(pg != po)[0]
+    assert bad.size == 0, f"{name}: first mismatches at pods {bad[:5]}: gpu {pg[bad[:5]]} oracle {po[bad[:5]]}"
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
+    R = len(enc.cluster.res_names)
+    for a, b in zip(gpu.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(a, b)
+    gpu.reset_state()
+    third = len(pods) // 3
+    p1, _ = gpu.run_queue(0, third)
+    p2, _ = gpu.run_queue(third, len(pods) - third)
+    np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
