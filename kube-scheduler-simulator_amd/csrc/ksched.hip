@@ -2077,7 +2077,10 @@ struct ksg_ctx {
   uint64_t* d_top = nullptr;
   // chip-wide topology path buffers (lazily allocated)
   CoopAcc* d_coop_acc = nullptr;
-  unsigned* d_coop_flags = nullptr;   // [0] barrier counter, [1] timeout
+  unsigned* d_coop_flags = nullptr;   // [0] barrier counter, [4] timeout
+  CoopPart* d_coop_parts = nullptr;   // [256] per-workgroup partials
+  int32_t* d_coop_phist = nullptr;    // [256][kCoopPHist] per-workgroup partial histograms
+  uint64_t* d_coop_srec = nullptr;    // [kCoopBatch][N] static records of the current batch
   int coop_gmax = 0;                  // co-resident workgroups of ksg_topo_coop
   bool topo_coop = true;              // env KSG_TOPO_COOP=0 disables
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
@@ -2144,6 +2147,9 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_stamps = nullptr;
   ctx->d_coop_acc = nullptr;
   ctx->d_coop_flags = nullptr;
+  ctx->d_coop_parts = nullptr;
+  ctx->d_coop_phist = nullptr;
+  ctx->d_coop_srec = nullptr;
 }
 
 // ---- per-kernel timing -------------------------------------------------------
@@ -2366,8 +2372,8 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
 #ifdef KSG_STAMPS
   if (!ctx->d_stamps) {
     int rc;
-    if ((rc = dalloc(ctx, &ctx->d_stamps, 8))) return rc;
-    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 64, ctx->stream));
+    if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 128, ctx->stream));
   }
   b.stamps = ctx->d_stamps;
 #endif
@@ -2539,68 +2545,99 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   return KSG_OK;
 }
 
+// Single replica, PodTopologySpread / InterPodAffinity, no capture: the queue
+// on G co-resident workgroups (ksched_topo_coop.h), in batches of kCoopBatch
+// pods, each preceded by its static records (ksg_sweep_static).
 template <int KN>
-int launch_coop(ksg_ctx* ctx, const CoopArgs& a, int* gmax_out) {
-  int occ = 0, cus = 0;
-  HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)ksg_topo_coop<KN>, 256, 0));
-  HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  *gmax_out = occ * cus;
-  if (a.G > occ * cus) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: grid exceeds co-resident workgroups");
-  hipLaunchKernelGGL(ksg_topo_coop<KN>, dim3(a.G), dim3(256), 0, ctx->stream, a);
+int coop_occupancy(ksg_ctx* ctx, int* occ) {
+  HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ksg_topo_coop<KN>, 256, 0));
   return KSG_OK;
 }
 
-// Single replica, PodTopologySpread / InterPodAffinity, no capture: the queue
-// on G co-resident workgroups (ksched_topo_coop.h).
 int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
                   const ksg_profile* d_prof) {
   const int N = ctx->c.N;
   int rc;
-  if (!ctx->d_coop_acc) {
-    if ((rc = dalloc(ctx, &ctx->d_coop_acc, 2))) return rc;
-    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 4))) return rc;
-  }
-  if (!ctx->coop_gmax) {
-    int occ = 0, cus = 0;
-    HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)ksg_topo_coop<1>, 256, 0));
-    HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    ctx->coop_gmax = std::min(occ * cus, cus);   // one workgroup per CU: lanes wait on memory, not issue
-  }
+  int cus = 0;
+  HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  if (!ctx->coop_gmax) ctx->coop_gmax = std::min(cus, 256);   // one workgroup per CU: lanes wait on memory
   int kn = 1;
   while ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N && kn < 32) kn *= 2;
   if ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: too many nodes");
+  const int G = (int)((N + 256 * kn - 1) / (256 * kn));
+  int occ = 0;
+  switch (kn) {
+    case 1: rc = coop_occupancy<1>(ctx, &occ); break;
+    case 2: rc = coop_occupancy<2>(ctx, &occ); break;
+    case 4: rc = coop_occupancy<4>(ctx, &occ); break;
+    case 8: rc = coop_occupancy<8>(ctx, &occ); break;
+    case 16: rc = coop_occupancy<16>(ctx, &occ); break;
+    default: rc = coop_occupancy<32>(ctx, &occ); break;
+  }
+  if (rc) return rc;
+  if (G > occ * cus) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: grid exceeds co-resident workgroups");
+  if (!ctx->d_coop_acc) {
+    if ((rc = dalloc(ctx, &ctx->d_coop_acc, 2))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [0] barrier (own 16 B), [4] timeout
+    if ((rc = dalloc(ctx, &ctx->d_coop_parts, 256))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_coop_phist, (size_t)256 * kCoopPHist))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_coop_srec, (size_t)kCoopBatch * N))) return rc;
+  }
   CoopArgs a{};
   a.c = ctx->c;
   a.st = ctx->st;
   a.pods = ctx->d_pods;
   a.prog = ctx->d_prog;
   a.profile = d_prof;
-  a.first = first;
-  a.count = count;
-  a.G = (int)((N + 256 * kn - 1) / (256 * kn));
+  a.G = G;
   a.placements = d_pl;
   a.results = d_res;
+  a.srec = ctx->d_coop_srec;
+  a.parts = ctx->d_coop_parts;
+  a.phist = ctx->d_coop_phist;
   a.acc = ctx->d_coop_acc;
   a.bar = ctx->d_coop_flags;
-  a.timeout = ctx->d_coop_flags + 1;
-  HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 16, ctx->stream));
-  hipLaunchKernelGGL(ksg_topo_coop_init, dim3(2), dim3(256), 0, ctx->stream, ctx->d_coop_acc);
+  a.timeout = ctx->d_coop_flags + 4;
+  SweepArgs sa{};
+  sa.c = ctx->c;
+  sa.pods = ctx->d_pods;
+  sa.prog = ctx->d_prog;
+  sa.profiles = d_prof;
+  sa.srec = ctx->d_coop_srec;
+  HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 32, ctx->stream));
+#ifdef KSG_STAMPS
+  if (!ctx->d_stamps) {
+    if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 128, ctx->stream));
+  }
+  a.stamps = ctx->d_stamps;
+#endif
   (void)hipGetLastError();
   treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   if ((rc = tmark(ctx))) return rc;
-  int gmax = 0;
-  switch (kn) {
-    case 1: rc = launch_coop<1>(ctx, a, &gmax); break;
-    case 2: rc = launch_coop<2>(ctx, a, &gmax); break;
-    case 4: rc = launch_coop<4>(ctx, a, &gmax); break;
-    case 8: rc = launch_coop<8>(ctx, a, &gmax); break;
-    case 16: rc = launch_coop<16>(ctx, a, &gmax); break;
-    default: rc = launch_coop<32>(ctx, a, &gmax); break;
+  for (int off = 0; off < count; off += kCoopBatch) {
+    const int nb = std::min(kCoopBatch, count - off);
+    sa.b0 = first + off;
+    sa.nb = nb;
+    hipLaunchKernelGGL(ksg_sweep_static, dim3((N + 255) / 256, nb), dim3(256), 0, ctx->stream, sa);
+    if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)nb * N))) return rc;
+    a.first = first + off;
+    a.count = nb;
+    a.out0 = off;
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 16, ctx->stream));   // barrier counter (timeout kept)
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_acc, 0, 2 * sizeof(CoopAcc), ctx->stream));
+    switch (kn) {
+      case 1: hipLaunchKernelGGL(ksg_topo_coop<1>, dim3(G), dim3(256), 0, ctx->stream, a); break;
+      case 2: hipLaunchKernelGGL(ksg_topo_coop<2>, dim3(G), dim3(256), 0, ctx->stream, a); break;
+      case 4: hipLaunchKernelGGL(ksg_topo_coop<4>, dim3(G), dim3(256), 0, ctx->stream, a); break;
+      case 8: hipLaunchKernelGGL(ksg_topo_coop<8>, dim3(G), dim3(256), 0, ctx->stream, a); break;
+      case 16: hipLaunchKernelGGL(ksg_topo_coop<16>, dim3(G), dim3(256), 0, ctx->stream, a); break;
+      default: hipLaunchKernelGGL(ksg_topo_coop<32>, dim3(G), dim3(256), 0, ctx->stream, a); break;
+    }
+    if ((rc = tlaunched(ctx, KSG_K_TOPO_COOP, (double)nb * N))) return rc;
   }
-  if (rc) return rc;
   HIPC(ctx, hipGetLastError());
-  if ((rc = tlaunched(ctx, KSG_K_TOPO_COOP, (double)count * N))) return rc;
   HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   return KSG_OK;
 }
@@ -2670,9 +2707,9 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   ctx->last_ms = ms;
   if ((rc = tcollect(ctx))) return rc;
   if (ctx->last_path == 4) {
-    unsigned flags[2] = {0, 0};
+    unsigned flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPC(ctx, hipMemcpy(flags, ctx->d_coop_flags, sizeof(flags), hipMemcpyDeviceToHost));
-    if (flags[1]) return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
+    if (flags[4]) return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
   }
   return KSG_OK;
 }
@@ -2991,9 +3028,9 @@ int ksg_reset_state(ksg_ctx* ctx) {
 
 #ifdef KSG_STAMPS
 // Diagnostic build only: cycle sums per phase-2 segment since load.
-int ksg_debug_stamps(ksg_ctx* ctx, unsigned long long* out6) {
-  if (!ctx || !out6 || !ctx->d_stamps) return KSG_E_STATE;
-  HIPC(ctx, hipMemcpy(out6, ctx->d_stamps, 48, hipMemcpyDeviceToHost));
+int ksg_debug_stamps(ksg_ctx* ctx, unsigned long long* out8) {   // 16 segment sums
+  if (!ctx || !out8 || !ctx->d_stamps) return KSG_E_STATE;
+  HIPC(ctx, hipMemcpy(out8, ctx->d_stamps, 128, hipMemcpyDeviceToHost));
   return KSG_OK;
 }
 #endif

@@ -186,6 +186,11 @@ struct TopoShared {
   int ok;
 };
 
+// Static record of a (pod, node) (ksg_sweep_static): bits 0-4 filter verdicts
+// (1 = rejects), 8-15 raw TaintToleration, 16-31 raw NodeAffinity, 32-39 raw
+// ImageLocality.
+constexpr uint32_t kSrUnsched = 1u, kSrNodeName = 2u, kSrTaint = 4u, kSrNodeAff = 8u, kSrNotEval = 16u;
+
 struct TopoCtx {
   const TopoProg* g;
   const TopoShared* s;
@@ -194,6 +199,8 @@ struct TopoCtx {
   const int32_t* tab;    // replica's template tables
   bool coherent;         // tab is written by other workgroups of this launch (ksg_topo_coop):
                          // read it with agent-scope atomic loads, never from a cache line
+  bool has_rec;          // rec = the node's static record: inclusion() reads its verdict bits
+  uint64_t rec;
   __device__ __forceinline__ int32_t tabv(int idx) const {
     if (coherent) return __hip_atomic_load(const_cast<int32_t*>(tab) + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return tab[idx];
@@ -290,6 +297,13 @@ __device__ __forceinline__ bool inclusion(const DevCluster& c, const PodView& v,
   if (nt && untolerated_slot(c, nd, v.tolf) >= 0) return false;
   return true;
 }
+// the same from the node's static record when the context carries one (the
+// record's NodeAffinity / TaintToleration bits are these two evaluations)
+__device__ __forceinline__ bool inclusion(const DevCluster& c, const PodView& v, const TopoCtx& t, int na, int nt,
+                                          int n) {
+  if (t.has_rec) return !(na && (t.rec & kSrNodeAff)) && !(nt && (t.rec & kSrTaint));
+  return inclusion(c, v, na, nt, n);
+}
 __device__ __forceinline__ bool bit_get(const int32_t* h, int base, uint32_t v) {
   return ((((uint32_t)h[base + (v >> 5)]) >> (v & 31)) & 1u) != 0;
 }
@@ -309,7 +323,7 @@ __device__ __forceinline__ uint32_t pts_filter_node(const DevCluster& c, const P
     if (!val) return 1;
     const Slot& sl = s.hard[i];
     int64_t m;
-    if (sl.unique) m = (all && inclusion(c, v, h[5], h[6], n)) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
+    if (sl.unique) m = (all && inclusion(c, v, t, h[5], h[6], n)) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
     else m = hist_at(t.hist, sl, val);
     if (m + h[4] - s.hard_min[i] > h[2]) return 2;
   }
@@ -359,7 +373,7 @@ __device__ __forceinline__ int64_t pts_score_node(const DevCluster& c, const Pod
     if (sc[5]) m = cnt_at(t.cnt, c.N, sl.sel, n);                    // hostname: this node's pods
     else if (!sl.unique) m = t.hist[sl.hist + val];
     else if (val == 1) m = s.soft_empty[i];
-    else m = inclusion(c, v, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
+    else m = inclusion(c, v, t, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
     const double x = (double)m * s.soft_w[i];
     score += x + (double)(sc[2] - 1);
   }

@@ -24,9 +24,7 @@
 // barrier.  Results equal ksg_queue_kernel's bit for bit (same plugin
 // arithmetic, same reductions), which the GPU tests check against the oracle.
 
-// static record: bits 0-4 filter verdicts (1 = rejects), 8-15 raw
-// TaintToleration, 16-31 raw NodeAffinity, 32-39 raw ImageLocality.
-constexpr uint32_t kSrUnsched = 1u, kSrNodeName = 2u, kSrTaint = 4u, kSrNodeAff = 8u, kSrNotEval = 16u;
+// static record layout: kSr* in ksched_kernels.h
 
 struct SweepArgs {
   DevCluster c;

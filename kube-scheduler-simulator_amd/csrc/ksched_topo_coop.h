@@ -6,23 +6,32 @@
 // sweep, 1.2 ms per pod.  Here G co-resident workgroups share each pod: lane
 // (wg, tid) owns nodes (k * G + wg) * 256 + tid, k < KN, for the whole queue,
 // so a node's mutable columns (requested, non-zero, pod count, selector
-// counts) are only ever read and written by one lane.  Per pod:
+// counts) are only ever read and written by one lane.
+//
+// The queue runs in batches of kCoopBatch pods.  Per batch, ksg_sweep_static
+// first computes every (pod, node)'s replica-independent plugin results
+// (NodeUnschedulable, NodeName, TaintToleration, NodeAffinity verdicts, raw
+// taint / node-affinity / image scores) in one massively parallel launch, so
+// the per-pod critical path below reads one 8-byte record per node instead of
+// walking taint, toleration, image and requirement lists.  Then
+// ksg_topo_coop<KN> walks the batch; per pod:
 //
 //   setup      every workgroup stages the pod and lays out its LDS histograms
 //   phase 1    pre-pass over the lane's nodes: per-domain counts into the LDS
-//              histograms, merged into a global accumulator set (atomics)
+//              histograms; the workgroup publishes its partial histogram and
+//              partial scalars in its own slot (plain stores, no contention)
 //   -- grid barrier --
-//   phase 2    every workgroup copies the merged histograms back into LDS;
+//   phase 2    every workgroup folds the G partial slots into its LDS copy;
 //              sweep A (filters incl. PTS/IPA, node-local scores), the IPA raw
 //              score and, with one soft PTS constraint, the extremes of its
-//              per-node count; reductions into the accumulator set
+//              per-node count; partial reductions into the slot
 //   -- grid barrier --  (+ one more for >= 2 soft PTS constraints: their raw
 //                         scores' min/max)
-//   phase 3    normalise, weight, argmax; atomicMax of the packed key
+//   phase 3    fold the phase-2 partials; normalise, weight, argmax
 //   -- grid barrier --
-//   phase 4    every workgroup reads the selection; the owner lane of the
-//              selected node assumes the pod (node columns, selector counts;
-//              domain tables by atomics)
+//   phase 4    fold the argmax partials; the owner lane of the selected node
+//              assumes the pod (node columns, selector counts; domain tables
+//              by atomics); workgroup 0 writes the result
 //
 // With one soft constraint the PodTopologySpread raw score of a node is
 // round(m * w + maxSkew - 1) for a node with the topology key (0 without it),
@@ -30,66 +39,58 @@
 // min / max over the feasible nodes follow from the min / max of m, so the
 // sizes and the min / max need no extra barrier.
 //
-// Accumulator sets alternate by pod parity; workgroup 0 resets the set of pod
-// j - 1 in phase 2 of pod j (every workgroup has read it by then).  Grid
-// barrier: a monotonic arrival counter; every storing wave drains its stores,
-// one lane releases (agent scope), arrives, polls relaxed with s_sleep, and
-// acquires (agent scope); every cross-workgroup word is read with agent-scope
-// atomic loads (MI355X guide, Guideline 16).  The poll is bounded: on timeout
-// the kernel records an error and every workgroup leaves.
+// Partial slots are rewritten in full every pod, and each is read only between
+// the barrier after its write and the next write (always two barriers later),
+// so one set suffices.  A pod whose histograms exceed the partial-slot budget
+// merges them with atomics into an accumulator set instead (two sets by pod
+// parity; workgroup 0 resets the set of pod j - 1 in phase 2 of pod j).
+// Grid barrier: a monotonic arrival counter; every storing wave drains its
+// stores, one lane releases (agent scope), arrives, polls relaxed with
+// s_sleep, and acquires (agent scope); every cross-workgroup word is read with
+// agent-scope atomic loads (MI355X guide, Guideline 16).  The poll is bounded:
+// on timeout the kernel records an error and every workgroup leaves.
 
-struct CoopAcc {
+constexpr int kCoopBatch = 64;      // pods per launch (static records [kCoopBatch][N])
+constexpr int kCoopPHist = 512;     // partial-histogram words per workgroup slot
+
+struct CoopPart {   // one workgroup's partial results of the current pod
   // phase 1
-  unsigned long long hard_min[kMaxHard];   // order-preserving encoding (enc64)
+  long long hard_min[kMaxHard];
   int32_t hard_dom[kMaxHard];
   long long soft_empty[kMaxSoft];
   long long aff_total;
   int32_t pref_any;
   // phase 2
-  int32_t nfeas;
-  int32_t minidx;                           // atomicMin
-  int32_t soft_present[kMaxSoft], soft_empty_seen[kMaxSoft], n_ignored;
-  int32_t has_val, has_zero, err;
-  unsigned long long max_t, max_a;          // atomicMax (non-negative)
-  unsigned long long mmin, mmax;            // one soft constraint: extremes of m (enc64)
-  unsigned long long imin, imax;            // IPA raw extremes (enc64)
-  unsigned long long pmin, pmax;            // >= 2 soft constraints: raw extremes (enc64)
+  int32_t nfeas, minidx, n_ignored, has_val, has_zero;
+  int32_t soft_present[kMaxSoft], soft_seen[kMaxSoft];
+  long long max_t, max_a, mmin, mmax, imin, imax;
+  // phase 2b (>= 2 soft constraints)
+  long long pmin, pmax;
   // phase 3
   unsigned long long best;
-  int32_t hist[KSG_HIST_MAX];               // merged LDS histograms (counts added, bitmaps or-ed)
+  int32_t err;
 };
 
-__device__ __forceinline__ unsigned long long enc64(long long x) { return (unsigned long long)x ^ (1ull << 63); }
-__device__ __forceinline__ long long dec64(unsigned long long x) { return (long long)(x ^ (1ull << 63)); }
+struct CoopAcc {    // atomics fallback for large histograms
+  int32_t hist[KSG_HIST_MAX];
+};
 
 template <class T>
 __device__ __forceinline__ T ald(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ void coop_acc_init(CoopAcc* a, int words) {
-  // called by one workgroup; plain stores, published by the next grid barrier
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    for (int i = 0; i < kMaxHard; i++) { a->hard_min[i] = enc64(0x7fffffffffffffffll); a->hard_dom[i] = 0; }
-    for (int i = 0; i < kMaxSoft; i++) { a->soft_empty[i] = 0; a->soft_present[i] = 0; a->soft_empty_seen[i] = 0; }
-    a->aff_total = 0;
-    a->pref_any = 0;
-    a->nfeas = 0;
-    a->minidx = 0x7fffffff;
-    a->n_ignored = 0;
-    a->has_val = a->has_zero = a->err = 0;
-    a->max_t = a->max_a = 0;
-    a->mmin = a->imin = a->pmin = enc64(0x7fffffffffffffffll);
-    a->mmax = a->imax = a->pmax = enc64(-0x7fffffffffffffffll - 1);
-    a->best = 0;
-  }
-  for (int i = tid; i < words; i += blockDim.x) a->hist[i] = 0;
-}
-
-__global__ void ksg_topo_coop_init(CoopAcc* acc) {
-  coop_acc_init(acc + blockIdx.x, KSG_HIST_MAX);
-}
+#ifdef KSG_STAMPS
+#define KSG_CSTAMP(seg)                                                     \
+  do {                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();             \
+    if (tid == 0 && wg == 0) { st_acc[seg] += _t - st_last; st_last = _t; } \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+  } while (0)
+#else
+#define KSG_CSTAMP(seg) do {} while (0)
+#endif
 
 struct CoopArgs {
   DevCluster c;
@@ -97,29 +98,33 @@ struct CoopArgs {
   const ksg_pod* pods;
   const int32_t* prog;
   const ksg_profile* profile;
-  int32_t first, count, G;
+  int32_t first, count, G;     // pods [first, first + count): one batch
+  int32_t out0;                // output index of pod `first`
   int32_t* placements;
-  ksg_result* results;      // or null
-  CoopAcc* acc;             // [2]
-  unsigned* bar;            // arrival counter, zeroed before the launch
-  unsigned* timeout;        // set when a barrier poll gave up
+  ksg_result* results;         // or null
+  const uint64_t* srec;        // [count][N] static records of the batch
+  CoopPart* parts;             // [G]
+  int32_t* phist;              // [G][kCoopPHist]
+  CoopAcc* acc;                // [2], zeroed before the launch
+  unsigned* bar;               // arrival counter, zeroed before the launch
+  unsigned* timeout;           // set when a barrier poll gave up
+  unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
 };
 
-__device__ __forceinline__ bool coop_barrier(const CoopArgs& a, unsigned& target) {
+__device__ __forceinline__ bool coop_barrier(unsigned* bar, unsigned* timeout, int G, unsigned& target) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
   __syncthreads();
-  target += (unsigned)a.G;
+  target += (unsigned)G;
   __shared__ int s_timeout;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(a.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     int to = 0;
-    while (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 25) ||
-          __hip_atomic_load(a.timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        __hip_atomic_store(a.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26) || __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         to = 1;
         break;
       }
@@ -147,7 +152,7 @@ __device__ __forceinline__ int pts_soft1_m(const DevCluster& c, const PodView& v
   if (sc[5]) m = cnt_at(t.cnt, c.N, sl.sel, n);
   else if (!sl.unique) m = t.hist[sl.hist + val];
   else if (val == 1) m = s.soft_empty[0];
-  else m = inclusion(c, v, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
+  else m = inclusion(c, v, t, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
   return 0;
 }
 
@@ -158,10 +163,73 @@ __device__ __forceinline__ int64_t pts_soft1_score(const TopoProg& g, const Topo
   return (int64_t)round(score);
 }
 
+// eval_node_src with the replica-independent plugins read from the node's
+// static record (t.rec): RunFilterPlugins (feasibility; the coop path records
+// no per-node status word) + the raw scores.
+__device__ __forceinline__ NodeEval eval_node_rec(const DevCluster& c, const ksg_profile& prof, const PodView& v,
+                                                  const NodeCols& L, int n, const TopoCtx& t) {
+  const ksg_pod& p = *v.p;
+  const uint64_t sr = t.rec;
+  NodeEval e{0, 0, 0, 0, 0};
+  uint32_t st = 0;
+  if (sr & kSrNotEval) {
+    st = KSG_FS_NOT_EVALUATED;
+  } else {
+    for (int kf = 0; kf < prof.n_filter && !st; kf++) {
+      const int pl = prof.filter_order[kf];
+      if ((v.fskip >> pl) & 1u) continue;
+      switch (pl) {
+        case KSG_PL_NODE_UNSCHEDULABLE:
+          if (sr & kSrUnsched) st = pl + 1;
+          break;
+        case KSG_PL_NODE_NAME:
+          if (sr & kSrNodeName) st = pl + 1;
+          break;
+        case KSG_PL_TAINT_TOLERATION:
+          if (sr & kSrTaint) st = pl + 1;
+          break;
+        case KSG_PL_NODE_AFFINITY:
+          if (sr & kSrNodeAff) st = (uint32_t)(pl + 1) | (1u << 8);
+          break;
+        case KSG_PL_NODE_RESOURCES_FIT: {
+          const uint32_t b = fit_filter(c, p, L, prof.fit_ignored_res);
+          if (b) st = (uint32_t)(pl + 1) | (b << 8);
+          break;
+        }
+        case KSG_PL_POD_TOPOLOGY_SPREAD:
+          if (t.g->pts_filter) {
+            const uint32_t r = pts_filter_node(c, v, t, n);
+            if (r) st = (uint32_t)(pl + 1) | (r << 8);
+          }
+          break;
+        case KSG_PL_INTER_POD_AFFINITY:
+          if (t.g->ipa) {
+            const uint32_t r = ipa_filter_node(c, t, n);
+            if (r) st = (uint32_t)(pl + 1) | (r << 8);
+          }
+          break;
+        default:
+          break;
+      }
+    }
+  }
+  e.st = st;
+  if (st != 0) return e;
+  if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) e.part += fit_score(prof, p, L) * v.w_fit;
+  if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) e.part += ba_score(prof, p, L) * v.w_ba;
+  if (v.smask & bit(KSG_PL_IMAGE_LOCALITY)) {
+    e.img = (int64_t)((sr >> 32) & 0xff) * v.w_img;
+    e.part += e.img;
+  }
+  if (v.smask & bit(KSG_PL_TAINT_TOLERATION)) e.rt = (int64_t)((sr >> 8) & 0xff);
+  if (v.smask & bit(KSG_PL_NODE_AFFINITY)) e.ra = (int64_t)((sr >> 16) & 0xffff);
+  return e;
+}
+
 // NodeInfo.AddPod for node n by the lane that owns it: node columns and
 // selector counts with plain stores, domain tables with atomics.
-__device__ void coop_commit(const DevCluster& c, const DevState& st, const ksg_pod& p, const int32_t* commit_prog,
-                            int n) {
+__device__ __forceinline__ void coop_commit(const DevCluster& c, const DevState& st, const ksg_pod& p,
+                                            const int32_t* commit_prog, int n) {
   const int N = c.N;
   for (int r = 0; r < c.R; r++) st.requested[(size_t)r * N + n] += p.req[r];
   st.nonzero[n] += p.nz_cpu;
@@ -184,6 +252,13 @@ __device__ void coop_commit(const DevCluster& c, const DevState& st, const ksg_p
   }
 }
 
+struct OpMinL { __device__ long long operator()(long long a, long long b) const { return a < b ? a : b; } };
+struct OpMaxL { __device__ long long operator()(long long a, long long b) const { return a > b ? a : b; } };
+struct OpAddL { __device__ long long operator()(long long a, long long b) const { return a + b; } };
+struct OpAddI { __device__ int32_t operator()(int32_t a, int32_t b) const { return a + b; } };
+struct OpMinI { __device__ int32_t operator()(int32_t a, int32_t b) const { return a < b ? a : b; } };
+struct OpOrI { __device__ int32_t operator()(int32_t a, int32_t b) const { return a | b; } };
+
 template <int KN>
 __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   constexpr int BLOCK = 256, NW = BLOCK / 64;
@@ -194,10 +269,12 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ ksg_profile s_prof;
   __shared__ TopoProg s_g;
   __shared__ TopoShared s_t;
-  __shared__ long long s_r[NW][8];
+  __shared__ long long s_l[NW][16];
+  __shared__ int32_t s_i[NW][16];
   __shared__ int s_size[kMaxSoft];
+  __shared__ long long s_tt[4];
 
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
   const DevCluster& c = a.c;
   const int N = c.N;
@@ -210,14 +287,39 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   for (int kf = 0; kf < prof.n_filter; kf++) ipa_in_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
   const bool ipa_in_score = (prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u;
   unsigned target = 0;
-  int prev_words = KSG_HIST_MAX;
+  int prev_fallback_words = 0;   // words of the previous pod's atomics-merged histograms (0: partial slots)
+  CoopPart* const mine = a.parts + wg;
+  int32_t* const myhist = a.phist + (size_t)wg * kCoopPHist;
+#ifdef KSG_STAMPS
+  unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
 
   auto node_of = [&](int k) { return (k * G + wg) * BLOCK + tid; };
+  // block-wide fold of one value per lane: DPP within waves, partials in LDS
+  auto bfold_l = [&](long long x, auto op, int slot) {
+    x = wreduce(x, op);
+    if (lane == 0) s_l[wv][slot] = x;
+  };
+  auto bfold_i = [&](int32_t x, auto op, int slot) {
+    x = wreduce(x, op);
+    if (lane == 0) s_i[wv][slot] = x;
+  };
+  auto get_l = [&](int slot, auto op) {
+    long long x = s_l[0][slot];
+    for (int i = 1; i < NW; i++) x = op(x, s_l[i][slot]);
+    return x;
+  };
+  auto get_i = [&](int slot, auto op) {
+    int32_t x = s_i[0][slot];
+    for (int i = 1; i < NW; i++) x = op(x, s_i[i][slot]);
+    return x;
+  };
 
   for (int kq = 0; kq < a.count; kq++) {
     const int pi = a.first + kq;
     CoopAcc* acc = a.acc + (kq & 1);
     CoopAcc* nxt = a.acc + ((kq + 1) & 1);
+    const uint64_t* srow = a.srec + (size_t)kq * N;
     __syncthreads();
     stage_pod<BLOCK>(a.pods, a.prog, pi, &s_pod, s_blob);
     __syncthreads();
@@ -233,29 +335,45 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       s_t.n_ignored = 0;
       s_t.aff_total = 0;
       s_t.pref_any = 0;
+      s_tt[0] = s_tt[1] = s_tt[2] = 0;
+    }
+    uint64_t srk[KN];
+#pragma unroll
+    for (int k = 0; k < KN; k++) {
+      const int n = node_of(k);
+      srk[k] = srow[n < N ? n : 0];
     }
     __syncthreads();
     const bool ok = s_t.ok;
     const int words = ok ? s_t.words : 0;
+    const bool pmode = words <= kCoopPHist && words * G <= 32768;
     for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
     PodView v = make_view(c, prof, p, s_blob, a.prog, true);
     const TopoProg& g = s_g;
-    const TopoCtx tc{&s_g, &s_t, s_hist, st.cnt, st.tab, true};
+    const TopoCtx tc{&s_g, &s_t, s_hist, st.cnt, st.tab, true, false, 0};
     __syncthreads();
+    KSG_CSTAMP(0);
 
     // ---- phase 1: pre-pass over this lane's nodes -------------------------
     const bool pre = ok && (g.pts_filter || g.pts_score || g.ipa);
     if (pre) {
       long long lmin[kMaxHard], ldom[kMaxHard], lempty[kMaxSoft], laff = 0, lany = 0;
+#pragma unroll
       for (int i = 0; i < kMaxHard; i++) { lmin[i] = BIG; ldom[i] = 0; }
+#pragma unroll
       for (int i = 0; i < kMaxSoft; i++) lempty[i] = 0;
       for (int k = 0; k < KN; k++) {
         const int n = node_of(k);
         if (n >= N) break;
+        TopoCtx tn = tc;
+        tn.has_rec = true;
+        tn.rec = srk[k];
         if (g.pts_filter && has_all(c, g.hard, g.n_hard, 7, n)) {
-          for (int i = 0; i < g.n_hard; i++) {
+#pragma unroll
+          for (int i = 0; i < kMaxHard; i++) {
+            if (i >= g.n_hard) break;
             const int32_t* h = g.hard + 7 * i;
-            if (!inclusion(c, v, h[5], h[6], n)) continue;
+            if (!inclusion(c, v, tn, h[5], h[6], n)) continue;
             const Slot& sl = s_t.hard[i];
             const int32_t x = cnt_at(st.cnt, N, sl.sel, n);
             if (sl.unique) {
@@ -269,9 +387,11 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           }
         }
         if (g.pts_score && (!g.require_all || has_all(c, g.soft, g.n_soft, 6, n))) {
-          for (int i = 0; i < g.n_soft; i++) {
+#pragma unroll
+          for (int i = 0; i < kMaxSoft; i++) {
+            if (i >= g.n_soft) break;
             const int32_t* sc = g.soft + 6 * i;
-            if (sc[5] || !inclusion(c, v, sc[3], sc[4], n)) continue;
+            if (sc[5] || !inclusion(c, v, tn, sc[3], sc[4], n)) continue;
             const Slot& sl = s_t.soft[i];
             uint32_t val = lab(c, sl.col, n);
             if (!val) val = 1;   // node.Labels[key] of a missing key is ""
@@ -317,64 +437,113 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           }
         }
       }
-      for (int i = 0; i < g.n_hard; i++) {
-        const long long m = wave_min64(lmin[i]), d = wave_sum64(ldom[i]);
-        if (lane == 0 && s_t.hard[i].unique) {
-          atomicMin((unsigned long long*)&s_t.hard_min[i], (unsigned long long)m);
-          atomicAdd(&s_t.hard_dom[i], (int)d);
-        }
+#pragma unroll
+      for (int i = 0; i < kMaxHard; i++) {
+        bfold_l(lmin[i], OpMinL{}, i);
+        bfold_l(ldom[i], OpAddL{}, 4 + i);
       }
-      for (int i = 0; i < g.n_soft; i++) {
-        const long long e = wave_sum64(lempty[i]);
-        if (lane == 0 && e) atomicAdd((unsigned long long*)&s_t.soft_empty[i], (unsigned long long)e);
-      }
-      laff = wave_sum64(laff);
-      lany = wave_sum64(lany);
-      if (lane == 0) {
-        if (laff) atomicAdd((unsigned long long*)&s_t.aff_total, (unsigned long long)laff);
-        if (lany) atomicOr(&s_t.pref_any, 1);
-      }
+#pragma unroll
+      for (int i = 0; i < kMaxSoft; i++) bfold_l(lempty[i], OpAddL{}, 8 + i);
+      bfold_l(laff, OpAddL{}, 12);
+      bfold_l(lany, OpAddL{}, 13);
       __syncthreads();
-      // merge this workgroup's part into the pod's accumulator set
-      auto merge_slot = [&](const Slot& sl) {
-        if (sl.unique) return;
-        for (int i = tid; i < sl.V; i += BLOCK)
-          if (s_hist[sl.hist + i]) atomicAdd(&acc->hist[sl.hist + i], s_hist[sl.hist + i]);
-        const int bw = (sl.V + 31) / 32;
-        for (int i = tid; i < bw; i += BLOCK)
-          if (s_hist[sl.pres + i]) atomicOr((uint32_t*)&acc->hist[sl.pres + i], (uint32_t)s_hist[sl.pres + i]);
-      };
-      for (int i = 0; i < g.n_hard; i++) merge_slot(s_t.hard[i]);
-      for (int i = 0; i < g.n_soft; i++) merge_slot(s_t.soft[i]);
-      for (int i = 0; i < g.n_aff; i++) merge_slot(s_t.aff[i]);
-      for (int i = 0; i < g.n_anti; i++) merge_slot(s_t.anti[i]);
-      for (int i = 0; i < g.n_pref; i++) merge_slot(s_t.pref[i]);
-      if (tid == 0) {
-        for (int i = 0; i < g.n_hard; i++)
-          if (s_t.hard[i].unique) {
-            if (s_t.hard_dom[i]) atomicMin(&acc->hard_min[i], enc64(s_t.hard_min[i]));
-            if (s_t.hard_dom[i]) atomicAdd(&acc->hard_dom[i], s_t.hard_dom[i]);
-          }
-        for (int i = 0; i < g.n_soft; i++)
-          if (s_t.soft_empty[i]) atomicAdd((unsigned long long*)&acc->soft_empty[i], (unsigned long long)s_t.soft_empty[i]);
-        if (s_t.aff_total) atomicAdd((unsigned long long*)&acc->aff_total, (unsigned long long)s_t.aff_total);
-        if (s_t.pref_any) atomicOr(&acc->pref_any, 1);
+      // publish this workgroup's partial
+      if (pmode) {
+        for (int i = tid; i < words; i += BLOCK) myhist[i] = s_hist[i];
+      } else {
+        auto merge_slot = [&](const Slot& sl) {
+          if (sl.unique) return;
+          for (int i = tid; i < sl.V; i += BLOCK)
+            if (s_hist[sl.hist + i]) atomicAdd(&acc->hist[sl.hist + i], s_hist[sl.hist + i]);
+          const int bw = (sl.V + 31) / 32;
+          for (int i = tid; i < bw; i += BLOCK)
+            if (s_hist[sl.pres + i]) atomicOr((uint32_t*)&acc->hist[sl.pres + i], (uint32_t)s_hist[sl.pres + i]);
+        };
+        for (int i = 0; i < g.n_hard; i++) merge_slot(s_t.hard[i]);
+        for (int i = 0; i < g.n_soft; i++) merge_slot(s_t.soft[i]);
+        for (int i = 0; i < g.n_aff; i++) merge_slot(s_t.aff[i]);
+        for (int i = 0; i < g.n_anti; i++) merge_slot(s_t.anti[i]);
+        for (int i = 0; i < g.n_pref; i++) merge_slot(s_t.pref[i]);
+      }
+      if (tid < kMaxHard) {
+        mine->hard_min[tid] = get_l(tid, OpMinL{});
+        mine->hard_dom[tid] = (int32_t)get_l(4 + tid, OpAddL{});
+      } else if (tid >= 64 && tid < 64 + kMaxSoft) {
+        mine->soft_empty[tid - 64] = get_l(8 + tid - 64, OpAddL{});
+      } else if (tid == 128) {
+        mine->aff_total = get_l(12, OpAddL{});
+        mine->pref_any = get_l(13, OpAddL{}) != 0;
       }
     }
-    if (!coop_barrier(a, target)) return;
+    KSG_CSTAMP(1);
+    if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+    KSG_CSTAMP(2);
 
-    // ---- phase 2: merged counts back into LDS; sweep A ----------------------
+    // ---- phase 2: fold the partials into LDS; sweep A --------------------------
     if (pre) {
-      for (int i = tid; i < words; i += BLOCK) s_hist[i] = ald(&acc->hist[i]);
+      if (pmode) {
+        for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
+        __syncthreads();
+        // (word, workgroup) pairs over the lanes: counts add, presence bitmaps or
+        auto fold_slot = [&](const Slot& sl) {
+          if (sl.unique) return;
+          for (int x = tid; x < sl.V * G; x += BLOCK) {
+            const int w = x / G, q = x - w * G;
+            const int32_t y = ald(a.phist + (size_t)q * kCoopPHist + sl.hist + w);
+            if (y) atomicAdd(&s_hist[sl.hist + w], y);
+          }
+          const int bw = (sl.V + 31) / 32;
+          for (int x = tid; x < bw * G; x += BLOCK) {
+            const int w = x / G, q = x - w * G;
+            const int32_t y = ald(a.phist + (size_t)q * kCoopPHist + sl.pres + w);
+            if (y) atomicOr((uint32_t*)&s_hist[sl.pres + w], (uint32_t)y);
+          }
+        };
+        for (int i = 0; i < g.n_hard; i++) fold_slot(s_t.hard[i]);
+        for (int i = 0; i < g.n_soft; i++) fold_slot(s_t.soft[i]);
+        for (int i = 0; i < g.n_aff; i++) fold_slot(s_t.aff[i]);
+        for (int i = 0; i < g.n_anti; i++) fold_slot(s_t.anti[i]);
+        for (int i = 0; i < g.n_pref; i++) fold_slot(s_t.pref[i]);
+      } else {
+        for (int i = tid; i < words; i += BLOCK) s_hist[i] = ald(&acc->hist[i]);
+      }
+      // scalars: lane q folds workgroup q's slot
+      {
+        long long hm[kMaxHard], hd[kMaxHard], se[kMaxSoft], af = 0, pa = 0;
+#pragma unroll
+        for (int i = 0; i < kMaxHard; i++) { hm[i] = BIG; hd[i] = 0; }
+#pragma unroll
+        for (int i = 0; i < kMaxSoft; i++) se[i] = 0;
+        if (tid < G) {
+          const CoopPart* q = a.parts + tid;
+#pragma unroll
+          for (int i = 0; i < kMaxHard; i++) { hm[i] = ald(&q->hard_min[i]); hd[i] = ald(&q->hard_dom[i]); }
+#pragma unroll
+          for (int i = 0; i < kMaxSoft; i++) se[i] = ald(&q->soft_empty[i]);
+          af = ald(&q->aff_total);
+          pa = ald(&q->pref_any);
+        }
+        __syncthreads();   // every wave is past its phase-1 get_*() reads
+#pragma unroll
+        for (int i = 0; i < kMaxHard; i++) {
+          bfold_l(hm[i], OpMinL{}, i);
+          bfold_l(hd[i], OpAddL{}, 4 + i);
+        }
+#pragma unroll
+        for (int i = 0; i < kMaxSoft; i++) bfold_l(se[i], OpAddL{}, 8 + i);
+        bfold_l(af, OpAddL{}, 12);
+        bfold_l(pa, OpAddL{}, 13);
+      }
+      __syncthreads();
       if (tid == 0) {
         for (int i = 0; i < g.n_hard; i++)
           if (s_t.hard[i].unique) {
-            s_t.hard_min[i] = dec64(ald(&acc->hard_min[i]));
-            s_t.hard_dom[i] = ald(&acc->hard_dom[i]);
+            s_t.hard_min[i] = get_l(i, OpMinL{});
+            s_t.hard_dom[i] = (int)get_l(4 + i, OpAddL{});
           }
-        for (int i = 0; i < g.n_soft; i++) s_t.soft_empty[i] = ald(&acc->soft_empty[i]);
-        s_t.aff_total = ald(&acc->aff_total);
-        s_t.pref_any = ald(&acc->pref_any);
+        for (int i = 0; i < g.n_soft; i++) s_t.soft_empty[i] = get_l(8 + i, OpAddL{});
+        s_t.aff_total = get_l(12, OpAddL{});
+        s_t.pref_any = get_l(13, OpAddL{}) != 0;
       }
       __syncthreads();
       for (int i = 0; i < g.n_hard; i++) {   // minimum over present domains of the non-unique hard slots
@@ -391,14 +560,22 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         }
       }
     }
-    if (wg == 0) coop_acc_init(nxt, prev_words);   // the set of pod kq - 1, read by everyone by now
-    prev_words = words;
+    KSG_CSTAMP(3);
+    if (wg == 0 && prev_fallback_words)   // the set of pod kq - 1, read by everyone by now
+      for (int i = tid; i < prev_fallback_words; i += BLOCK) nxt->hist[i] = 0;
+    prev_fallback_words = pmode ? 0 : words;
+    {   // existing pods' terms matching this pod: totals, one template per lane
+      const int n_t = g.ipa ? g.n_ma + g.n_mh + g.n_mp : 0;
+      for (int i = tid; i < n_t; i += BLOCK) {
+        const int which = i < g.n_ma ? 0 : (i < g.n_ma + g.n_mh ? 1 : 2);
+        const int tm = which == 0 ? g.m_anti[i] : (which == 1 ? g.m_hard[i - g.n_ma] : g.m_pref[i - g.n_ma - g.n_mh]);
+        const int32_t x = ald(&st.tmpl_total[tm]);
+        if (x) atomicAdd((unsigned long long*)&s_tt[which], (unsigned long long)x);
+      }
+    }
     __syncthreads();
     if (tid == 0) {
-      long long ma = 0, mh = 0, mp = 0;
-      for (int i = 0; i < g.n_ma; i++) ma += ald(&st.tmpl_total[g.m_anti[i]]);
-      for (int i = 0; i < g.n_mh; i++) mh += ald(&st.tmpl_total[g.m_hard[i]]);
-      for (int i = 0; i < g.n_mp; i++) mp += ald(&st.tmpl_total[g.m_pref[i]]);
+      const long long ma = s_tt[0], mh = s_tt[1], mp = s_tt[2];
       s_t.ipa_skip_filter = !g.ipa || (ma == 0 && g.n_aff == 0 && g.n_anti == 0);
       s_t.ipa_skip_score = !g.ipa || !((prof.hard_pod_affinity_weight > 0 && mh > 0) || mp > 0);
       if (pre) {
@@ -408,6 +585,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     __syncthreads();
+    KSG_CSTAMP(4);
     if (s_t.ipa_skip_filter) v.fskip |= bit(KSG_PL_INTER_POD_AFFINITY);
     const bool ipa_may_score = ipa_in_score && !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u) &&
                                !s_t.ipa_skip_score;
@@ -416,26 +594,33 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     NodeEval ev[KN];
     int64_t yv[KN];
     int32_t nfeas = 0, minidx = 0x7fffffff, lign = 0, has_val = 0, has_zero = 0;
-    int64_t max_t = 0, max_a = 0;
+    long long max_t = 0, max_a = 0;
     long long mmin = BIG, mmax = -BIG - 1, imin = BIG, imax = -BIG - 1;
-    int lpres[kMaxSoft] = {0, 0, 0, 0}, lseen[kMaxSoft] = {0, 0, 0, 0};
+    int32_t lpres[kMaxSoft] = {0, 0, 0, 0}, lseen[kMaxSoft] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < KN; k++) {
       const int n = node_of(k);
       ev[k].st = 1;
       yv[k] = 0;
       if (n >= N || !ok) continue;
-      ev[k] = eval_node(c, prof, v, st.requested, st.nonzero, st.pod_count, n, nullptr, nullptr, &tc);
+      TopoCtx tn = tc;
+      tn.has_rec = true;
+      tn.rec = srk[k];
+      NodeCols L;
+      load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
+      ev[k] = eval_node_rec(c, prof, v, L, n, tn);
       if (ev[k].st != 0) continue;
       nfeas += 1;
       minidx = min(minidx, n);
-      max_t = max(max_t, ev[k].rt);
-      max_a = max(max_a, ev[k].ra);
+      max_t = max(max_t, (long long)ev[k].rt);
+      max_a = max(max_a, (long long)ev[k].ra);
       if (g.pts_score) {
         if (g.require_all && !has_all(c, g.soft, g.n_soft, 6, n)) {
           lign += 1;
         } else {
-          for (int i = 0; i < g.n_soft; i++) {
+#pragma unroll
+          for (int i = 0; i < kMaxSoft; i++) {
+            if (i >= g.n_soft) break;
             if (g.soft[6 * i + 5]) continue;
             const Slot& sl = s_t.soft[i];
             uint32_t val = lab(c, sl.col, n);
@@ -450,135 +635,195 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         }
         if (soft1) {
           int64_t m = 0;
-          const int r = pts_soft1_m(c, v, tc, n, m);
+          const int r = pts_soft1_m(c, v, tn, n, m);
           if (r == 0) { has_val = 1; mmin = min(mmin, (long long)m); mmax = max(mmax, (long long)m); }
           else if (r == 1) has_zero = 1;
         }
       }
       if (ipa_may_score) {
-        yv[k] = ipa_score_node(c, prof, tc, n);
+        yv[k] = ipa_score_node(c, prof, tn, n);
         imin = min(imin, (long long)yv[k]);
         imax = max(imax, (long long)yv[k]);
       }
     }
-    {
-      nfeas = wave_sum32(nfeas);
-      minidx = wave_min32(minidx);
-      max_t = wave_max64(max_t);
-      max_a = wave_max64(max_a);
-      lign = wave_sum32(lign);
-      has_val = wave_sum32(has_val);
-      has_zero = wave_sum32(has_zero);
-      mmin = wave_min64(mmin); mmax = wave_max64(mmax);
-      imin = wave_min64(imin); imax = wave_max64(imax);
-      if (lane == 0) {
-        if (nfeas) {
-          atomicAdd(&acc->nfeas, nfeas);
-          atomicMin(&acc->minidx, minidx);
-          atomicMax(&acc->max_t, (unsigned long long)max_t);
-          atomicMax(&acc->max_a, (unsigned long long)max_a);
-        }
-        if (lign) atomicAdd(&acc->n_ignored, lign);
-        if (has_val) {
-          atomicOr(&acc->has_val, 1);
-          atomicMin(&acc->mmin, enc64(mmin));
-          atomicMax(&acc->mmax, enc64(mmax));
-        }
-        if (has_zero) atomicOr(&acc->has_zero, 1);
-        if (imin <= imax) {
-          atomicMin(&acc->imin, enc64(imin));
-          atomicMax(&acc->imax, enc64(imax));
-        }
-      }
-      if (g.pts_score) {
-        for (int i = 0; i < g.n_soft; i++) {
-          const int pr = wave_sum32(lpres[i]), se = (int)wave_or32((uint32_t)lseen[i]);
-          if (lane == 0) {
-            if (pr) atomicAdd(&acc->soft_present[i], pr);
-            if (se) atomicOr(&acc->soft_empty_seen[i], 1);
-          }
-        }
-      }
+    KSG_CSTAMP(5);
+    bfold_i(nfeas, OpAddI{}, 0);
+    bfold_i(minidx, OpMinI{}, 1);
+    bfold_i(lign, OpAddI{}, 2);
+    bfold_i(has_val, OpOrI{}, 3);
+    bfold_i(has_zero, OpOrI{}, 4);
+#pragma unroll
+    for (int i = 0; i < kMaxSoft; i++) {
+      bfold_i(lpres[i], OpAddI{}, 5 + i);
+      bfold_i(lseen[i], OpOrI{}, 9 + i);
     }
+    bfold_l(max_t, OpMaxL{}, 0);
+    bfold_l(max_a, OpMaxL{}, 1);
+    bfold_l(mmin, OpMinL{}, 2);
+    bfold_l(mmax, OpMaxL{}, 3);
+    bfold_l(imin, OpMinL{}, 4);
+    bfold_l(imax, OpMaxL{}, 5);
     __syncthreads();
+    if (tid == 0) {
+      mine->nfeas = get_i(0, OpAddI{});
+      mine->minidx = get_i(1, OpMinI{});
+      mine->n_ignored = get_i(2, OpAddI{});
+      mine->has_val = get_i(3, OpOrI{});
+      mine->has_zero = get_i(4, OpOrI{});
+      for (int i = 0; i < kMaxSoft; i++) {
+        mine->soft_present[i] = get_i(5 + i, OpAddI{});
+        mine->soft_seen[i] = get_i(9 + i, OpOrI{});
+      }
+      mine->max_t = get_l(0, OpMaxL{});
+      mine->max_a = get_l(1, OpMaxL{});
+      mine->mmin = get_l(2, OpMinL{});
+      mine->mmax = get_l(3, OpMaxL{});
+      mine->imin = get_l(4, OpMinL{});
+      mine->imax = get_l(5, OpMaxL{});
+    }
     if (g.pts_score && ok)   // domains seen among feasible nodes (non-unique soft slots)
       for (int i = 0; i < g.n_soft; i++) {
         const Slot& sl = s_t.soft[i];
         if (g.soft[6 * i + 5] || sl.unique) continue;
-        for (int wd = tid; wd < (sl.V + 31) / 32; wd += BLOCK)
-          if (s_hist[sl.mark + wd]) atomicOr((uint32_t*)&acc->hist[sl.mark + wd], (uint32_t)s_hist[sl.mark + wd]);
+        for (int wd = tid; wd < (sl.V + 31) / 32; wd += BLOCK) {
+          if (pmode) myhist[sl.mark + wd] = s_hist[sl.mark + wd];
+          else if (s_hist[sl.mark + wd]) atomicOr((uint32_t*)&acc->hist[sl.mark + wd], (uint32_t)s_hist[sl.mark + wd]);
+        }
       }
-    if (!coop_barrier(a, target)) return;
+    KSG_CSTAMP(6);
+    if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+    KSG_CSTAMP(7);
 
-    // ---- phase 3: sizes, normalisation, argmax --------------------------------
-    const int gnfeas = ald(&acc->nfeas);
+    // ---- phase 3: fold phase 2; sizes, normalisation, argmax --------------------
+    {
+      int32_t f_n = 0, f_min = 0x7fffffff, f_ign = 0, f_hv = 0, f_hz = 0;
+      int32_t f_pr[kMaxSoft] = {0, 0, 0, 0}, f_se[kMaxSoft] = {0, 0, 0, 0};
+      long long f_mt = 0, f_ma = 0, f_mmin = BIG, f_mmax = -BIG - 1, f_imin = BIG, f_imax = -BIG - 1;
+      if (tid < G) {
+        const CoopPart* q = a.parts + tid;
+        f_n = ald(&q->nfeas);
+        f_min = ald(&q->minidx);
+        f_ign = ald(&q->n_ignored);
+        f_hv = ald(&q->has_val);
+        f_hz = ald(&q->has_zero);
+#pragma unroll
+        for (int i = 0; i < kMaxSoft; i++) { f_pr[i] = ald(&q->soft_present[i]); f_se[i] = ald(&q->soft_seen[i]); }
+        f_mt = ald(&q->max_t);
+        f_ma = ald(&q->max_a);
+        f_mmin = ald(&q->mmin);
+        f_mmax = ald(&q->mmax);
+        f_imin = ald(&q->imin);
+        f_imax = ald(&q->imax);
+      }
+      bfold_i(f_n, OpAddI{}, 0);
+      bfold_i(f_min, OpMinI{}, 1);
+      bfold_i(f_ign, OpAddI{}, 2);
+      bfold_i(f_hv, OpOrI{}, 3);
+      bfold_i(f_hz, OpOrI{}, 4);
+#pragma unroll
+      for (int i = 0; i < kMaxSoft; i++) {
+        bfold_i(f_pr[i], OpAddI{}, 5 + i);
+        bfold_i(f_se[i], OpOrI{}, 9 + i);
+      }
+      bfold_l(f_mt, OpMaxL{}, 0);
+      bfold_l(f_ma, OpMaxL{}, 1);
+      bfold_l(f_mmin, OpMinL{}, 2);
+      bfold_l(f_mmax, OpMaxL{}, 3);
+      bfold_l(f_imin, OpMinL{}, 4);
+      bfold_l(f_imax, OpMaxL{}, 5);
+    }
+    __syncthreads();
+    const int gnfeas = get_i(0, OpAddI{});
+    const int gminidx = get_i(1, OpMinI{});
     const bool scored = ok && gnfeas >= 2;
     const bool do_pts = scored && g.pts_score;
     const bool do_ipa = scored && ipa_may_score;
-    long long pmin = BIG, pmax = 0, gimin = BIG, gimax = -BIG - 1;
+    const int64_t gmax_t = get_l(0, OpMaxL{}), gmax_a = get_l(1, OpMaxL{});
+    const long long gimin = get_l(4, OpMinL{}), gimax = get_l(5, OpMaxL{});
+    long long pmin = BIG, pmax = 0;
     if (do_pts) {
       for (int i = 0; i < g.n_soft; i++) {
         const Slot& sl = s_t.soft[i];
         if (g.soft[6 * i + 5] || sl.unique) continue;
+        const int bw = (sl.V + 31) / 32;
+        if (pmode) {   // (word, workgroup) pairs over the lanes, or-ed into this workgroup's own marks
+          for (int x = tid; x < bw * G; x += BLOCK) {
+            const int w = x / G, q = x - w * G;
+            const uint32_t y = (uint32_t)ald(a.phist + (size_t)q * kCoopPHist + sl.mark + w);
+            if (y) atomicOr((uint32_t*)&s_hist[sl.mark + w], y);
+          }
+        } else {
+          for (int wd = tid; wd < bw; wd += BLOCK) s_hist[sl.mark + wd] = ald(&acc->hist[sl.mark + wd]);
+        }
+      }
+      __syncthreads();
+      for (int i = 0; i < g.n_soft; i++) {
+        const Slot& sl = s_t.soft[i];
+        if (g.soft[6 * i + 5] || sl.unique) continue;
         int bits = 0;
-        for (int wd = tid; wd < (sl.V + 31) / 32; wd += BLOCK) bits += __popc(ald((uint32_t*)&acc->hist[sl.mark + wd]));
+        for (int wd = tid; wd < (sl.V + 31) / 32; wd += BLOCK) bits += __popc((uint32_t)s_hist[sl.mark + wd]);
         bits = wave_sum32(bits);
         if (lane == 0 && bits) atomicAdd(&s_size[i], bits);
       }
       __syncthreads();
       if (tid == 0) {
-        const int n_ign = ald(&acc->n_ignored);
+        const int n_ign = get_i(2, OpAddI{});
         for (int i = 0; i < g.n_soft; i++) {
           const Slot& sl = s_t.soft[i];
           int sz;
           if (g.soft[6 * i + 5]) sz = gnfeas - n_ign;
-          else if (sl.unique) sz = ald(&acc->soft_present[i]) + ald(&acc->soft_empty_seen[i]);
+          else if (sl.unique) sz = get_i(5 + i, OpAddI{}) + get_i(9 + i, OpOrI{});
           else sz = s_size[i];
           s_t.soft_w[i] = c.log_table[sz + 2];   // topologyNormalizingWeight = math.Log(size + 2)
         }
-        long long lo = BIG, hi = 0;
-        if (soft1) {
-          if (ald(&acc->has_val)) {
-            lo = pts_soft1_score(g, s_t, dec64(ald(&acc->mmin)));
-            hi = pts_soft1_score(g, s_t, dec64(ald(&acc->mmax)));
-          }
-          if (ald(&acc->has_zero)) { lo = min(lo, 0ll); hi = max(hi, 0ll); }
-        }
-        s_r[0][0] = lo;
-        s_r[0][1] = hi;
       }
       __syncthreads();
-      pmin = s_r[0][0];
-      pmax = s_r[0][1];
-      if (!soft1) {   // >= 2 soft constraints: raw scores first, then their extremes
+      if (soft1) {
         long long lo = BIG, hi = 0;
+        if (get_i(3, OpOrI{})) {
+          lo = pts_soft1_score(g, s_t, get_l(2, OpMinL{}));
+          hi = pts_soft1_score(g, s_t, get_l(3, OpMaxL{}));
+        }
+        if (get_i(4, OpOrI{})) { lo = min(lo, 0ll); hi = max(hi, 0ll); }
+        pmin = lo;
+        pmax = hi;
+      } else {   // >= 2 soft constraints: raw scores first, then their extremes
+        long long lo = BIG, hi = -BIG - 1;
 #pragma unroll
         for (int k = 0; k < KN; k++) {
           const int n = node_of(k);
           if (n >= N || ev[k].st != 0) continue;
-          const int64_t x = pts_score_node(c, v, tc, n);
+          TopoCtx tn = tc;
+          tn.has_rec = true;
+          tn.rec = srk[k];
+          const int64_t x = pts_score_node(c, v, tn, n);
           if (x >= 0) { lo = min(lo, (long long)x); hi = max(hi, (long long)x); }
         }
-        lo = wave_min64(lo);
-        hi = wave_max64(hi);
-        if (lane == 0 && lo <= hi) {
-          atomicMin(&acc->pmin, enc64(lo));
-          atomicMax(&acc->pmax, enc64(hi));
+        bfold_l(lo, OpMinL{}, 6);
+        bfold_l(hi, OpMaxL{}, 7);
+        __syncthreads();
+        if (tid == 0) {
+          mine->pmin = get_l(6, OpMinL{});
+          mine->pmax = get_l(7, OpMaxL{});
         }
-        if (!coop_barrier(a, target)) return;
-        const long long l2 = dec64(ald(&acc->pmin)), h2 = dec64(ald(&acc->pmax));
+        if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+        long long l2 = BIG, h2 = -BIG - 1;
+        if (tid < G) {
+          l2 = ald(&a.parts[tid].pmin);
+          h2 = ald(&a.parts[tid].pmax);
+        }
+        bfold_l(l2, OpMinL{}, 8);
+        bfold_l(h2, OpMaxL{}, 9);
+        __syncthreads();
+        l2 = get_l(8, OpMinL{});
+        h2 = get_l(9, OpMaxL{});
         pmin = l2;
         pmax = l2 <= h2 ? h2 : 0;
       }
     }
-    if (do_ipa) {
-      gimin = dec64(ald(&acc->imin));
-      gimax = dec64(ald(&acc->imax));
-    }
-    const int64_t gmax_t = (int64_t)ald(&acc->max_t), gmax_a = (int64_t)ald(&acc->max_a);
+    uint64_t best = 0;
+    uint32_t err = 0;
     if (scored) {
-      uint64_t best = 0;
-      uint32_t err = 0;
       const int64_t w_pts = prof.weight[KSG_PL_POD_TOPOLOGY_SPREAD], w_ipa = prof.weight[KSG_PL_INTER_POD_AFFINITY];
 #pragma unroll
       for (int k = 0; k < KN; k++) {
@@ -586,7 +831,10 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         if (n >= N || ev[k].st != 0) continue;
         int64_t total = total_score(v, ev[k].part, ev[k].rt, ev[k].ra, gmax_t, gmax_a, err, nullptr, nullptr);
         if (do_pts) {   // PodTopologySpread.NormalizeScore
-          const int64_t x = pts_score_node(c, v, tc, n);
+          TopoCtx tn = tc;
+          tn.has_rec = true;
+          tn.rec = srk[k];
+          const int64_t x = pts_score_node(c, v, tn, n);
           int64_t s;
           if (x < 0) s = 0;
           else if (pmax == 0) s = 100;
@@ -606,26 +854,49 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         const uint64_t key = argmax_key(total, n);
         best = key > best ? key : best;
       }
-      best = wave_max_u64(best);
-      err = wave_or32(err);
-      if (lane == 0) {
-        if (best) atomicMax(&acc->best, (unsigned long long)best);
-        if (err) atomicOr(&acc->err, 1);
-      }
     }
-    if (!coop_barrier(a, target)) return;
+    best = wreduce(best, OpMaxU64{});
+    err = wreduce(err, OpOr32{});
+    __syncthreads();   // every wave is past its get_*() reads of s_l / s_i
+    if (lane == 0) { s_l[wv][10] = (long long)best; s_i[wv][13] = (int32_t)err; }
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long b = 0;
+      int32_t e = 0;
+      for (int i = 0; i < NW; i++) { b = max(b, (unsigned long long)s_l[i][10]); e |= s_i[i][13]; }
+      mine->best = b;
+      mine->err = e;
+    }
+    KSG_CSTAMP(8);
+    if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+    KSG_CSTAMP(9);
 
     // ---- phase 4: select and assume --------------------------------------------
+    {
+      unsigned long long b = 0;
+      int32_t e = 0;
+      if (tid < G) {
+        b = ald(&a.parts[tid].best);
+        e = ald(&a.parts[tid].err);
+      }
+      b = wreduce(b, OpMaxU64{});
+      e = wreduce(e, OpOrI{});
+      if (lane == 0) { s_l[wv][11] = (long long)b; s_i[wv][14] = e; }
+    }
+    __syncthreads();
     int selected = -1;
     uint32_t status = 0;
     if (!ok) {
       status |= KSG_ST_SCORE_ERROR;
     } else if (gnfeas == 1) {
-      selected = ald(&acc->minidx);
+      selected = gminidx;
     } else if (scored) {
       status |= KSG_ST_SCORED;
-      if (ald(&acc->err)) status |= KSG_ST_SCORE_ERROR;
-      else selected = key_node(ald(&acc->best));
+      unsigned long long b = 0;
+      int32_t e = 0;
+      for (int i = 0; i < NW; i++) { b = max(b, (unsigned long long)s_l[i][11]); e |= s_i[i][14]; }
+      if (e) status |= KSG_ST_SCORE_ERROR;
+      else selected = key_node(b);
     }
     if (selected >= 0 && ((selected / BLOCK) % G) == wg && (selected % BLOCK) == tid)
       coop_commit(c, st, p, p.commit >= 0 ? s_blob + (p.commit - p.blob) : nullptr, selected);
@@ -636,15 +907,20 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         status |= KSG_ST_IPA_PRESCORE_SKIP;
         score_skip |= bit(KSG_PL_INTER_POD_AFFINITY);
       }
-      a.placements[kq] = selected;
+      a.placements[a.out0 + kq] = selected;
       if (a.results) {
         ksg_result res;
         res.selected = selected;
         res.n_feasible = ok ? gnfeas : 0;
         res.status = status;
         res.score_skip = score_skip;
-        a.results[kq] = res;
+        a.results[a.out0 + kq] = res;
       }
     }
+    KSG_CSTAMP(10);
   }
+#ifdef KSG_STAMPS
+  if (tid == 0 && wg == 0 && a.stamps)
+    for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+#endif
 }

@@ -18,7 +18,7 @@ eng = native.Engine(lib_path=os.path.join(ROOT, "kube-scheduler-simulator_amd", 
 eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
 eng.run_queue(0, n_pods, results=False)
 ms = eng.last_kernel_ms()
-st = (C.c_ulonglong * 6)()
+st = (C.c_ulonglong * 16)()
 fn = eng.lib.ksg_debug_stamps
 fn.argtypes = [C.c_void_p, C.c_void_p]
 assert fn(eng.ctx, st) == 0

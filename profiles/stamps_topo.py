@@ -1,0 +1,32 @@
+"""Diagnostic: per-pod segment shares of the chip-wide topology path
+(ksg_topo_coop) from the KSG_STAMPS build, workgroup 0's clock (never the
+measured library).  Run on the GPU box: python profiles/stamps_topo.py [pods]"""
+import ctypes as C
+import importlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+G = importlib.import_module("kube-scheduler-simulator_amd.generator")
+E = importlib.import_module("kube-scheduler-simulator_amd.encoder")
+native = importlib.import_module("kube-scheduler-simulator_amd.native")
+
+n_pods = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+nodes, pods, prof = G.config3(n_pods=n_pods)
+enc = E.Encoder(nodes, pods, prof)
+eng = native.Engine(lib_path=os.path.join(ROOT, "kube-scheduler-simulator_amd", "libksched_stamps.so"))
+eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+eng.run_queue(0, n_pods, results=False)
+ms = eng.last_kernel_ms()
+st = (C.c_ulonglong * 16)()
+fn = eng.lib.ksg_debug_stamps
+fn.argtypes = [C.c_void_p, C.c_void_p]
+assert fn(eng.ctx, st) == 0
+tot = sum(st)
+names = ["setup (stage pod, layout)", "phase 1 (pre-pass + merge)", "barrier 1", "2a: merged counts to LDS",
+         "2b: reset next set, IPA skips", "2c: sweep A", "2d: reductions, marks", "barrier 2",
+         "phase 3 (normalise, argmax)", "barrier 3", "phase 4 (select, assume)"]
+print(f"[topo coop] {n_pods} pods x {len(nodes)} nodes, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped)")
+for i in range(11):
+    print(f"  {names[i]:30s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / max(tot, 1):5.1f} %")
