@@ -1020,10 +1020,10 @@ __global__ __launch_bounds__(kP2Block) void ksg_batch_phase2(BatchArgs a) {
           w += ns;
           const int nt = *w++;
           for (int i = 0; i < nt; i++) {
-            const int t = w[i];
+            const int t = w[2 * i];
             const uint32_t lv = c.label_val[(size_t)c.tmpl_col[t] * N + selected];
             if (!lv) continue;
-            a.st.tab[c.tmpl_off[t] + lv] += c.tmpl_kind[t] == KSG_TMPL_PREF ? c.tmpl_weight[t] : 1;
+            a.st.tab[c.tmpl_off[t] + lv] += c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1;
             a.st.tmpl_total[t] += 1;
           }
         }
@@ -1565,10 +1565,10 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
         cw += ns;
         const int nt = *cw++;
         for (int i = 0; i < nt; i++) {
-          const int t = cw[i];
+          const int t = cw[2 * i];
           const uint32_t lv = c.label_val[(size_t)c.tmpl_col[t] * N + selected];
           if (!lv) continue;
-          a.st.tab[c.tmpl_off[t] + lv] += c.tmpl_kind[t] == KSG_TMPL_PREF ? c.tmpl_weight[t] : 1;
+          a.st.tab[c.tmpl_off[t] + lv] += c.tmpl_kind[t] == KSG_TMPL_PREF ? cw[2 * i + 1] : 1;
           a.st.tmpl_total[t] += 1;
         }
       }

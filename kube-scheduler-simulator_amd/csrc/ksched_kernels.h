@@ -569,11 +569,11 @@ __device__ void commit_node(const DevCluster& c, int64_t* requested, int64_t* no
     w += ns;
     const int nt = *w++;
     for (int i = 0; i < nt; i++) {
-      const int t = w[i];
+      const int t = w[2 * i];
       const int col = c.tmpl_col[t];
       const uint32_t val = c.label_val[(size_t)col * N + n];
       if (!val) continue;
-      tab[c.tmpl_off[t] + val] += c.tmpl_kind[t] == KSG_TMPL_PREF ? c.tmpl_weight[t] : 1;
+      tab[c.tmpl_off[t] + val] += c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1;
       tmpl_total[t] += 1;
     }
   }

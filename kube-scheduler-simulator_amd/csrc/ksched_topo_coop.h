@@ -242,10 +242,10 @@ __device__ __forceinline__ void coop_commit(const DevCluster& c, const DevState&
     w += ns;
     const int nt = *w++;
     for (int i = 0; i < nt; i++) {
-      const int t = w[i];
+      const int t = w[2 * i];
       const uint32_t val = c.label_val[(size_t)c.tmpl_col[t] * N + n];
       if (!val) continue;
-      __hip_atomic_fetch_add(st.tab + c.tmpl_off[t] + val, c.tmpl_kind[t] == KSG_TMPL_PREF ? c.tmpl_weight[t] : 1,
+      __hip_atomic_fetch_add(st.tab + c.tmpl_off[t] + val, c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(st.tmpl_total + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

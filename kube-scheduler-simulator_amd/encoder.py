@@ -38,7 +38,8 @@ Program grammar (int32 words; offsets are word indices, -1 = absent):
                   n_anti { col sel }[n_anti]
                   n_pref { col sel weight }[n_pref]          (weight < 0: anti)
                   n_m_anti tmpl[n_m_anti]  n_m_hard tmpl[n_m_hard]  n_m_pref tmpl[n_m_pref]
-  commit       := n_sel sel[n_sel] n_tmpl tmpl[n_tmpl]
+  commit       := n_sel sel[n_sel] n_tmpl {tmpl weight}[n_tmpl]   (weight: the term's signed
+                  preferred weight, 1 for required terms)
 
 A pod's tol..commit programs are contiguous: [blob, blob + blob_len).
 """
@@ -411,7 +412,7 @@ class Encoder:
         idx = _PodIndex(pods)
         self.pts_sel: Dict[tuple, int] = {}      # (canon, namespace) -> id
         self.ipa_sel: Dict[tuple, int] = {}      # tuple of scopes (conjunction) -> id
-        self.templates: Dict[tuple, int] = {}    # (kind, scope, col, weight) -> id
+        self.templates: Dict[tuple, int] = {}    # (kind, scope, col) -> id; weights ride in commit programs
         self.owned_templates: Dict[int, List[int]] = defaultdict(list)
         for i, p in enumerate(pods):
             hard, soft = self._pts_cache[i]
@@ -431,9 +432,12 @@ class Encoder:
                                 (TMPL_PREF, [(w.term, w.weight) for w in p.pod_affinity_preferred]
                                  + [(w.term, -w.weight) for w in p.pod_anti_affinity_preferred])):
                 for t, wt in terms:
-                    key = (kind, self._term_scope(t, p), self.col_index[t.topology_key], wt)
+                    # one template per (kind, scope, topology key): terms that differ only
+                    # in weight share its domain table (each assume adds its own weight),
+                    # so an incoming pod looks up one table instead of one per weight
+                    key = (kind, self._term_scope(t, p), self.col_index[t.topology_key])
                     tid = self.templates.setdefault(key, len(self.templates))
-                    self.owned_templates[i].append(tid)
+                    self.owned_templates[i].append((tid, wt))
         n_pts = len(self.pts_sel)
         # selector ids: PTS selectors first, then IPA selectors
         self.ipa_sel = {k: n_pts + v for k, v in self.ipa_sel.items()}
@@ -452,16 +456,16 @@ class Encoder:
                 self.pod_selectors[j].append(sid)
         # which templates match which (incoming) pod
         self.pod_tmpl_match: Dict[int, Tuple[List[int], List[int], List[int]]] = defaultdict(lambda: ([], [], []))
-        for (kind, (canon, ns, ns_all), col, wt), tid in sorted(self.templates.items(), key=lambda kv: kv[1]):
+        for (kind, (canon, ns, ns_all), col), tid in sorted(self.templates.items(), key=lambda kv: kv[1]):
             for j in idx.matching(canon, lambda q, ns=ns, ns_all=ns_all: ns_all or q.namespace in ns):
                 self.pod_tmpl_match[j][kind].append(tid)
         self.tmpl_col = np.zeros(max(len(self.templates), 1), np.int32)
         self.tmpl_kind = np.zeros(max(len(self.templates), 1), np.int32)
         self.tmpl_weight = np.zeros(max(len(self.templates), 1), np.int32)
-        for (kind, _, col, wt), tid in self.templates.items():
+        for (kind, _, col), tid in self.templates.items():
             self.tmpl_col[tid] = col
             self.tmpl_kind[tid] = kind
-            self.tmpl_weight[tid] = wt
+            self.tmpl_weight[tid] = 1   # unused: per-term weights are in the owners' commit programs
 
     # -------------------------------------------------------------- programs
     def _emit(self, words: Sequence[int], intern: bool = False) -> int:
@@ -619,7 +623,7 @@ class Encoder:
         tm = self.owned_templates.get(i, [])
         if not sels and not tm:
             return -1
-        return self._emit([len(sels)] + sels + [len(tm)] + tm)
+        return self._emit([len(sels)] + sels + [len(tm)] + [x for pair in tm for x in pair])
 
     # -------------------------------------------------------------- encode
     def _encode_cluster(self) -> EncodedCluster:

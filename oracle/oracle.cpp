@@ -281,7 +281,7 @@ int64_t image_score(const Ctx& c, const ksg_pod& p, int n) {
 // ---- selectors / templates -------------------------------------------------
 struct CommitProg {
   const int32_t* sels = nullptr; int nsel = 0;
-  const int32_t* tmpls = nullptr; int ntmpl = 0;
+  const int32_t* tmpls = nullptr; int ntmpl = 0;   // ntmpl {template id, weight} pairs
 };
 CommitProg commit_prog(const Ctx& c, int pod) {
   CommitProg cp;
@@ -478,7 +478,7 @@ IpaPre ipa_prefilter(const Ctx& c, const ksg_pod& p, const IpaProg& g) {
     for (int q : c.pods_on[n]) {
       CommitProg cp = commit_prog(c, q);
       for (int k = 0; k < cp.ntmpl; k++) {
-        int tid = cp.tmpls[k];
+        int tid = cp.tmpls[2 * k];
         if (c.tmpl_kind[tid] != KSG_TMPL_REQ_ANTI) continue;
         if (!std::binary_search(g.m_anti.begin(), g.m_anti.end(), tid)) continue;
         uint32_t v = lv(c, c.tmpl_col[tid], n);
@@ -544,7 +544,7 @@ IpaScore ipa_prescore(const Ctx& c, const ksg_pod& p, const IpaProg& g) {
           if (v) { part[t][{pr.col, v}] += pr.w; any[t] = 1; }
         }
       for (int k = 0; k < cp.ntmpl; k++) {
-        int tid = cp.tmpls[k];
+        int tid = cp.tmpls[2 * k];
         int kind = c.tmpl_kind[tid];
         int64_t add;
         if (kind == KSG_TMPL_REQ_AFF) {
@@ -552,7 +552,7 @@ IpaScore ipa_prescore(const Ctx& c, const ksg_pod& p, const IpaProg& g) {
           add = hw;
         } else if (kind == KSG_TMPL_PREF) {
           if (!std::binary_search(g.m_pref.begin(), g.m_pref.end(), tid)) continue;
-          add = c.tmpl_weight[tid];
+          add = cp.tmpls[2 * k + 1];   // the owning term's signed weight
         } else {
           continue;
         }
