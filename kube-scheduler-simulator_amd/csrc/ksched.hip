@@ -1093,10 +1093,10 @@ struct SlotLayout {
 };
 
 struct P2Part {
-  uint64_t k0, bu;           // best changed key, best unchanged key (in T_j \ C)
-  uint32_t cnt_lo, cnt_hi;   // feas1 | live << 16, lost_t | lost_a << 16
-  int32_t cmin, err;
-  int32_t kidx, cidx;        // slot of k0 / of cmin, -1 if not in this wave
+  uint64_t k0, bu;           // best changed key, best unchanged key (in T_j \ C; only when
+                             // the first 64 entries of T_j are all changed)
+  uint32_t cnt;              // this wave's feas1 | live << 8 | lost_t << 16 | lost_a << 24 (each <= 64)
+  int32_t kidx;              // slot of k0, -1 if not in this wave
 };
 
 // floor(x / a) for 0 <= x, 0 < a, quotient below 2^20 (every division on the
@@ -1284,6 +1284,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
   __shared__ uint64_t s_ce[KSG_BATCH_MAX];     // live record of changed slot i (renormalisation)
   __shared__ P2Part s_part[NW];
   __shared__ WRed s_w[NW];
+  __shared__ ksg_result s_res[KSG_BATCH_MAX];  // per-pod results, stored after the walk
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const DevCluster& c = a.c;
@@ -1328,7 +1329,12 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     const int jn = more ? j + 1 : j;   // row of the next-pod loads (always a valid row)
 
     // ---- X1: speculated best unchanged node (sorted T_j, first 64 entries) --
+    // T_j is sorted, so its first entry outside C is the best unchanged key;
+    // every wave computes it identically.  Only when all of the first 64
+    // entries are changed does the best unchanged key need a block reduction.
     int spec = -1;
+    uint64_t bu_key = 0;
+    bool bu_full = false;
     {
       uint64_t key = 0;
       bool ok = false;
@@ -1337,7 +1343,11 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
         ok = !changed(key_node(key));
       }
       const uint64_t m = __ballot(ok);
-      if (m) spec = key_node(readlane64(key, __builtin_ctzll(m)));
+      if (m) {
+        bu_key = readlane64(key, __builtin_ctzll(m));
+        spec = key_node(bu_key);
+      }
+      bu_full = m == 0 && s1.K > 64;
     }
     // ---- X2: pod j+1's loads (consumed in Y) ----------------------------------
     const int K1 = more ? s_p1[j + 1].K : 0;
@@ -1349,7 +1359,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     KSG_STAMP(1);
 
     // ---- X3: my changed node on its live slot ---------------------------------
-    P2Part w{0, 0, 0, 0, 0x7fffffff, 0, -1, -1};
+    uint32_t cnt = 0;   // feas1 | live << 8 | lost_t << 16 | lost_a << 24
     uint64_t live = 0, my_key = 0;
     if (tid < nc && (my_rec >> 63)) {
       int64_t sw[SW];
@@ -1359,7 +1369,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
         for (int k = 0; k < SW / 2; k++) reinterpret_cast<int4*>(sw)[k] = src[k];
       }
       const uint64_t x = my_rec;
-      w.cnt_lo = 1;
+      cnt = 1;
       const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff;
       bool fits = true;
       if (h.fit_on) {
@@ -1368,7 +1378,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
         for (int r = 0; r < RM; r++) fits = fits && (!((h.req_mask >> r) & 1u) || h.req[r] <= sw[2 * r] - sw[2 * r + 1]);
       }
       if (!fits) {
-        w.cnt_hi = (rt == mt1 ? 1u : 0u) + (ra == ma1 ? 0x10000u : 0u);
+        cnt += (rt == mt1 ? 1u << 16 : 0u) + (ra == ma1 ? 1u << 24 : 0u);
       } else {
         int64_t fs = 0, bs = 0;
         if (cm.fast) {
@@ -1383,33 +1393,30 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
         const int64_t nt = mt1 != 0 ? 100 - qdiv(100 * rt, mt1, s1.inv_mt) : 100;
         const int64_t na = ma1 != 0 ? qdiv(100 * ra, ma1, s1.inv_ma) : ra;
         my_key = argmax_key(part + nt * h.w_t + na * h.w_a, my_node);
-        w.cnt_lo += 0x10000u;
+        cnt += 1u << 8;
         live = pack_rec(part, rt, ra);
       }
     }
     if (tid < nc) s_ce[tid] = live;
     {
       const uint64_t k0 = wreduce(my_key, OpMaxU64{});
-      const uint32_t lo = wreduce(w.cnt_lo, OpAdd32{}), hi = wreduce(w.cnt_hi, OpAdd32{});
-      const int32_t cmin = wreduce(live ? my_node : 0x7fffffff, OpMin32{});
-      const uint64_t mk = __ballot(k0 != 0 && my_key == k0), mc = __ballot(live != 0 && my_node == cmin);
-      // best unchanged: this wave's slice of T_j
-      uint64_t tk = 0;
-      if (tid < s1.K) {
-        const uint64_t key = s_top[tid];
-        if (!changed(key_node(key))) tk = key;
+      const uint32_t wc = wreduce(cnt, OpAdd32{});
+      const uint64_t mk = __ballot(k0 != 0 && my_key == k0);
+      uint64_t bu = 0;
+      if (bu_full) {   // best unchanged: this wave's slice of T_j (rare)
+        uint64_t tk = 0;
+        if (tid < s1.K) {
+          const uint64_t key = s_top[tid];
+          if (!changed(key_node(key))) tk = key;
+        }
+        bu = wreduce(tk, OpMaxU64{});
       }
-      const uint64_t bu = wreduce(tk, OpMaxU64{});
       if (lane == 0) {
         P2Part o;
         o.k0 = k0;
         o.bu = bu;
-        o.cnt_lo = lo;
-        o.cnt_hi = hi;
-        o.cmin = cmin;
-        o.err = 0;
+        o.cnt = wc;
         o.kidx = mk ? wv * 64 + __builtin_ctzll(mk) : -1;
-        o.cidx = mc ? wv * 64 + __builtin_ctzll(mc) : -1;
         s_part[wv] = o;
       }
     }
@@ -1417,20 +1424,19 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     __syncthreads();
 
     // ---- Y: decide (every wave, identically) -------------------------------
-    uint64_t k0 = 0, bu = 0;
-    uint32_t lo = 0, hi = 0;
-    int32_t cmin = 0x7fffffff, kidx = -1, cidx = -1;
+    uint64_t k0 = 0, bu = bu_key;
+    int32_t kidx = -1;
+    int feas1 = 0, live_n = 0, lost_t = 0, lost_a = 0;
 #pragma unroll
     for (int i = 0; i < NW; i++) {
       const P2Part o = s_part[i];
       if (o.k0 > k0) { k0 = o.k0; kidx = o.kidx; }
-      bu = o.bu > bu ? o.bu : bu;
-      lo += o.cnt_lo;
-      hi += o.cnt_hi;
-      if (o.cmin < cmin) { cmin = o.cmin; cidx = o.cidx; }
+      if (bu_full) bu = o.bu > bu ? o.bu : bu;
+      feas1 += o.cnt & 0xff;
+      live_n += (o.cnt >> 8) & 0xff;
+      lost_t += (o.cnt >> 16) & 0xff;
+      lost_a += o.cnt >> 24;
     }
-    const int feas1 = lo & 0xffff, live_n = lo >> 16;
-    const int lost_t = hi & 0xffff, lost_a = hi >> 16;
     const int unch = s1.nfeas - feas1;   // unchanged feasible nodes
     int nfeas = unch + live_n;
     // a phase-1 maximum whose every holder became infeasible, or a range error:
@@ -1506,9 +1512,12 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     } else if (nfeas == 1) {
       if (unch == 1) {
         selected = key_node(bu);
-      } else {
-        selected = cmin;
-        idx = cidx;
+      } else {   // the one live changed node (rare): its wave publishes its slot
+        const uint64_t mb = __ballot(tid < nc && live != 0);
+        if (mb && lane == 0) s_w[0].live = wv * 64 + __builtin_ctzll(mb);
+        __syncthreads();
+        idx = s_w[0].live;
+        selected = s_clist[idx];
       }
     } else if (nfeas >= 2) {
       status |= KSG_ST_SCORED;
@@ -1550,11 +1559,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
           else if (lane == SL::NZC) d = p.nz_cpu;
           else if (lane == SL::NZM) d = p.nz_mem;
           else if (lane == SL::PODS) d = 1;
-          val += d;
-          const int r = lane >> 1;
-          if (lane < 2 * RM && (lane & 1) && r < R) a.st.requested[(size_t)r * N + selected] = val;
-          else if (lane == SL::NZC || lane == SL::NZM) a.st.nonzero[(size_t)(lane - SL::NZC) * N + selected] = val;
-          else if (lane == SL::PODS) a.st.pod_count[selected] = (int32_t)val;
+          val += d;   // the live columns stay in the row; global memory gets them after the walk
         }
         row[lane] = val;
       }
@@ -1580,21 +1585,31 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     if (tid == 0) {
       uint32_t score_skip;
       ipa_skip_bits(prof, p, status, score_skip);
-      const int o = a.out0 + j;
-      a.placements[o] = selected;
-      if (a.results) {
-        ksg_result res;
-        res.selected = selected;
-        res.n_feasible = nfeas;
-        res.status = status;
-        res.score_skip = score_skip;
-        a.results[o] = res;
-      }
+      ksg_result res;
+      res.selected = selected;
+      res.n_feasible = nfeas;
+      res.status = status;
+      res.score_skip = score_skip;
+      s_res[j] = res;
     }
     nc += added ? 1 : 0;
     KSG_STAMP(4);
     __syncthreads();
     KSG_STAMP(5);
+  }
+  // No store is on the per-pod path: nothing in the walk reads a changed
+  // node's columns from global memory (they live in its LDS row), so the rows
+  // and the results go out once, here.
+  for (int i = tid; i < nc * SW; i += BLOCK) {
+    const int slot = i / SW, w = i - slot * SW, node = s_clist[slot];
+    const int64_t val = s_slot[(size_t)slot * SW + w];
+    if (w < 2 * RM && (w & 1) && (w >> 1) < R) a.st.requested[(size_t)(w >> 1) * N + node] = val;
+    else if (w == SL::NZC || w == SL::NZM) a.st.nonzero[(size_t)(w - SL::NZC) * N + node] = val;
+    else if (w == SL::PODS) a.st.pod_count[node] = (int32_t)val;
+  }
+  for (int i = tid; i < a.nb; i += BLOCK) {
+    a.placements[a.out0 + i] = s_res[i].selected;
+    if (a.results) a.results[a.out0 + i] = s_res[i];
   }
   for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
 #ifdef KSG_STAMPS
