@@ -1266,8 +1266,8 @@ __device__ __forceinline__ int64_t slot_word_value(const SlotFetch<RM>& f, int l
   using SL = SlotLayout<RM>;
   if (lane == SL::PODS || lane == SL::ALLOWED) return (int64_t)f.v32;
   if (lane < 2 * RM) return (lane >> 1) < R ? f.v64 : 0;
-  if (lane == SL::INVC || lane == SL::INVM)
-    return (int64_t)(uint32_t)__float_as_int(f.v64 > 0 ? 1.0f / (float)f.v64 : 1.0f);
+  if (lane == SL::INVC || lane == SL::INVM)   // qdiv's estimate: v_rcp_f32 (1 ulp) is within its correction
+    return (int64_t)(uint32_t)__float_as_int(f.v64 > 0 ? __builtin_amdgcn_rcpf((float)f.v64) : 1.0f);
   if (lane == SL::DAC || lane == SL::DAM) return __double_as_longlong((double)f.v64);
   return lane < SL::W ? f.v64 : 0;
 }
@@ -1309,6 +1309,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
   for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
   __syncthreads();
   const CmProf cm = cm_prof(s_prof);
+  const bool ipa_filter = ipa_in_filter(s_prof);
 
   auto changed = [&](int n) { return ((s_cmask[n >> 5] >> (n & 31)) & 1u) != 0; };
   int nc = 0;                  // |C|, block-uniform
@@ -1316,7 +1317,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
   uint64_t my_rec = 0;         // pod j's phase-1 record at my_node
   int32_t my_img = 0;
 #ifdef KSG_STAMPS
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
 #endif
   KSG_STAMP(0);
   for (int j = 0; j < a.nb; j++) {
@@ -1324,6 +1325,19 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     const ksg_profile& prof = s_prof;
     const P1Stats s1 = s_p1[j];
     const PodHot<RM> h = pod_hot<RM>(p, prof, fit_filter_on, R);
+    // this lane's word of the assume (row word `lane` += delta), computed off the critical path
+    int64_t row_delta = 0;
+    if (lane < 2 * RM) row_delta = (lane & 1) && (lane >> 1) < R ? p.req[lane >> 1] : 0;
+    else if (lane == SL::NZC) row_delta = p.nz_cpu;
+    else if (lane == SL::NZM) row_delta = p.nz_mem;
+    else if (lane == SL::PODS) row_delta = 1;
+    const bool has_commit = p.commit >= 0;
+    uint32_t pod_status = 0, pod_skip = 0;   // ipa_skip_bits for an unscored / scored result
+    uint32_t pod_status_s = KSG_ST_SCORED, pod_skip_s = 0;
+    if (tid == 0) {
+      ipa_skip_bits(prof, ipa_filter, p, pod_status, pod_skip);
+      ipa_skip_bits(prof, ipa_filter, p, pod_status_s, pod_skip_s);
+    }
     const int64_t mt1 = s1.mt, ma1 = s1.ma;
     const bool more = j + 1 < a.nb;
     const int jn = more ? j + 1 : j;   // row of the next-pod loads (always a valid row)
@@ -1547,23 +1561,15 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
       my_img = nx_img;
     }
     if (tid < K1) s_top[tid] = nx_top;
+    KSG_STAMP(6);
     const int64_t col_val = slot_word_value<RM>(col, lane, R);
+    KSG_STAMP(7);
     if (wv == 0 && selected >= 0) {
       const int slot = added ? nc : idx;
       int64_t* row = s_slot + (size_t)slot * SW;
-      if (lane < SW) {
-        int64_t val = added ? col_val : row[lane];
-        if (lane < SL::INVC) {
-          int64_t d = 0;
-          if (lane < 2 * RM) d = (lane & 1) && (lane >> 1) < R ? p.req[lane >> 1] : 0;
-          else if (lane == SL::NZC) d = p.nz_cpu;
-          else if (lane == SL::NZM) d = p.nz_mem;
-          else if (lane == SL::PODS) d = 1;
-          val += d;   // the live columns stay in the row; global memory gets them after the walk
-        }
-        row[lane] = val;
-      }
-      if (lane == 0 && p.commit >= 0) {   // PodTopologySpread / InterPodAffinity count tables
+      if (lane < SW)   // the live columns stay in the row; global memory gets them after the walk
+        row[lane] = (added ? col_val : row[lane]) + row_delta;
+      if (lane == 0 && has_commit) {   // PodTopologySpread / InterPodAffinity count tables
         const int32_t* cw = s_prog + (p.commit - a.prog_lo);
         const int ns = *cw++;
         for (int i = 0; i < ns; i++) a.st.cnt[(size_t)cw[i] * N + selected] += 1;
@@ -1583,13 +1589,12 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
       }
     }
     if (tid == 0) {
-      uint32_t score_skip;
-      ipa_skip_bits(prof, p, status, score_skip);
+      const bool sc = (status & KSG_ST_SCORED) != 0;
       ksg_result res;
       res.selected = selected;
       res.n_feasible = nfeas;
-      res.status = status;
-      res.score_skip = score_skip;
+      res.status = status | (sc ? pod_status_s : pod_status);
+      res.score_skip = sc ? pod_skip_s : pod_skip;
       s_res[j] = res;
     }
     nc += added ? 1 : 0;
@@ -1614,7 +1619,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
   for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
 #ifdef KSG_STAMPS
   if (tid == 0 && a.stamps)
-    for (int i = 0; i < 6; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+    for (int i = 0; i < 8; i++) atomicAdd(&a.stamps[i], st_acc[i]);
 #endif
 }
 

@@ -538,18 +538,26 @@ __device__ __forceinline__ int key_node(uint64_t key) { return (int)(0xffffffffu
 
 // InterPodAffinity without any term of, or matching, this pod: PreFilter and
 // PreScore both return Skip [upstream interpodaffinity/filtering.go, scoring.go].
-__device__ __forceinline__ void ipa_skip_bits(const ksg_profile& prof, const ksg_pod& p, uint32_t& status,
-                                              uint32_t& score_skip) {
-  score_skip = p.score_skip;
-  if (p.ipa >= 0) return;
+__device__ __forceinline__ bool ipa_in_filter(const ksg_profile& prof) {
   bool ipa_filter = false;
   for (int kf = 0; kf < prof.n_filter; kf++) ipa_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
+  return ipa_filter;
+}
+// ipa_filter: ipa_in_filter(prof), hoisted out of per-pod loops by callers on a critical path
+__device__ __forceinline__ void ipa_skip_bits(const ksg_profile& prof, bool ipa_filter, const ksg_pod& p,
+                                              uint32_t& status, uint32_t& score_skip) {
+  score_skip = p.score_skip;
+  if (p.ipa >= 0) return;
   if (ipa_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
   if ((status & KSG_ST_SCORED) && ((prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) &&
       !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u)) {
     status |= KSG_ST_IPA_PRESCORE_SKIP;
     score_skip |= bit(KSG_PL_INTER_POD_AFFINITY);
   }
+}
+__device__ __forceinline__ void ipa_skip_bits(const ksg_profile& prof, const ksg_pod& p, uint32_t& status,
+                                              uint32_t& score_skip) {
+  ipa_skip_bits(prof, ipa_in_filter(prof), p, status, score_skip);
 }
 
 // NodeInfo.AddPod restricted to the columns the plugins read, plus the

@@ -26,10 +26,11 @@ tot = sum(st[1:])
 mode = os.environ.get("KSG_BATCH_MODE", "slot")
 if mode == "slot":
     names = ["(start)", "X: speculate + issue next-pod loads", "X: changed node + DPP reductions",
-             "Y: barrier 1 + decide (+renorm)", "Y: assume + next-pod state", "barrier 2"]
+             "Y: barrier 1 + decide (+renorm)", "Y: row update + results", "barrier 2",
+             "Y: next-pod records + top set (waits)", "Y: fetched column decode"]
 else:
     names = ["(start)", "A: changed nodes + top sets", "barrier 1", "B: decide (+rescan)",
              "B: next-pod LDS writes", "barrier 2 (waits for the assume)"]
 print(f"[{mode}] {n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build)")
-for i in range(1, 6):
+for i in range(1, 8 if mode == "slot" else 6):
     print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
