@@ -2103,6 +2103,7 @@ struct ksg_ctx {
   uint64_t* d_coop_srec = nullptr;    // [kCoopBatch][N] static records of the current batch
   int coop_gmax = 0;                  // co-resident workgroups of ksg_topo_coop
   bool topo_coop = true;              // env KSG_TOPO_COOP=0 disables
+  unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
   int batch_mode = 2;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default)
   // per-kernel timing (ksg_set_timing): one event before the first and after
@@ -2492,9 +2493,17 @@ bool sweep_eligible(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first,
   return true;
 }
 
+template <int BLOCK, int KN, bool MULTI>
+void launch_sweep(const SweepArgs& s, int grid, bool fast, hipStream_t st) {
+  if (fast) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
+  else hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, false, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
+}
+
 template <int BLOCK, int KN>
-void launch_sweep(const SweepArgs& s, int R, hipStream_t st) {
-  hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true>), dim3(R), dim3(BLOCK), 0, st, s);
+int sweep_occupancy(ksg_ctx* ctx, bool fast, int* occ) {   // the MULTI instances
+  if (fast) HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ksg_sweep<BLOCK, KN, true, true>, BLOCK, 0));
+  else HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ksg_sweep<BLOCK, KN, false, true>, BLOCK, 0));
+  return KSG_OK;
 }
 
 // Host mirror of cm_prof().fast: Fit and BalancedAllocation both score exactly
@@ -2525,16 +2534,48 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   s.count = count;
   s.placements = d_pl;
   TA(tmp, &s.srec, sizeof(uint64_t) * (size_t)kBatch * N);
-  // (BLOCK, KN): KN nodes per lane in registers; KN = 0 streams them through
-  // a per-replica scratch row instead (N > 32,768, or a profile outside the
-  // cpu/memory fast path)
-  int block = N <= 16384 ? 256 : 1024, kn = 0;
-  const struct { int block, kn; } shapes[] = {{256, 8}, {256, 16}, {256, 20}, {256, 24}, {256, 32},
-                                              {512, 32}, {1024, 32}};
-  if (fast)
-    for (const auto& sh : shapes)
-      if (N <= sh.block * sh.kn) { block = sh.block; kn = sh.kn; break; }
+  // Workgroups per replica: with few replicas of a large cluster, S > 1 spreads
+  // each replica over S co-resident workgroups (two group barriers per pod);
+  // aim at ~4 workgroups per CU and at least ~8 nodes per lane.
+  int cus = 0;
+  HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  int S = 1;
+  if (R < 4 * cus) S = std::min({std::max(1, 4 * cus / R), std::max(1, N / 2048), 64});
+  // (BLOCK, KN): KN nodes per lane in registers; KN = 0 streams them through a
+  // per-replica scratch row instead.  The instances that fit 128 VGPRs without
+  // spilling: every fast shape for one workgroup per replica; KN = 8 for
+  // several (runtime stride) and for the generic arithmetic.
+  struct Shape { int block, kn; };
+  static const Shape fast1[] = {{256, 8}, {256, 16}, {256, 20}, {256, 24}, {256, 32}, {512, 32}, {1024, 32}};
+  static const Shape fastm[] = {{256, 8}};
+  static const Shape gen[] = {{256, 8}};
+  int block = 1024, kn = 0;
+  for (;;) {
+    const int neff = (N + S - 1) / S;
+    const Shape* list = fast ? (S == 1 ? fast1 : fastm) : gen;
+    const int nl = fast && S == 1 ? 7 : 1;
+    block = S > 1 || neff <= 16384 ? 256 : 1024;
+    kn = 0;
+    for (int i = 0; i < nl; i++)
+      if (neff <= list[i].block * list[i].kn) { block = list[i].block; kn = list[i].kn; break; }
+    if (S == 1) break;
+    int occ = 0, rc0 = 0;
+    switch (block * 100 + kn) {
+      case 25608: rc0 = sweep_occupancy<256, 8>(ctx, fast, &occ); break;
+      default: rc0 = sweep_occupancy<256, 0>(ctx, fast, &occ); break;
+    }
+    if (rc0) return rc0;
+    if ((long long)R * S <= (long long)occ * cus) break;   // every workgroup of a group co-resident
+    S = S / 2;
+  }
+  s.S = S;
   if (kn == 0) TA(tmp, &s.scratch, sizeof(uint64_t) * (size_t)R * N);
+  if (S > 1) {
+    TA(tmp, &s.slots, sizeof(SweepSlot) * 2 * (size_t)R * S);
+    TA(tmp, &s.gbar, sizeof(unsigned) * ((size_t)R + 4));
+    TA(tmp, &s.timeout, 16);
+    HIPC(ctx, hipMemsetAsync(s.timeout, 0, 16, ctx->stream));
+  }
   (void)hipGetLastError();
   treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
@@ -2546,20 +2587,29 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     s.out0 = off;
     hipLaunchKernelGGL(ksg_sweep_static, dim3((N + 255) / 256, s.nb), dim3(256), 0, ctx->stream, s);
     if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)s.nb * N))) return rc;
-    switch (fast ? block * 100 + kn : -block) {
-      case 25608: launch_sweep<256, 8>(s, R, ctx->stream); break;
-      case 25616: launch_sweep<256, 16>(s, R, ctx->stream); break;
-      case 25620: launch_sweep<256, 20>(s, R, ctx->stream); break;
-      case 25624: launch_sweep<256, 24>(s, R, ctx->stream); break;
-      case 25632: launch_sweep<256, 32>(s, R, ctx->stream); break;
-      case 51232: launch_sweep<512, 32>(s, R, ctx->stream); break;
-      case 102432: launch_sweep<1024, 32>(s, R, ctx->stream); break;
-      case 102400: launch_sweep<1024, 0>(s, R, ctx->stream); break;
-      case -256: hipLaunchKernelGGL((ksg_sweep<256, 0, false>), dim3(R), dim3(256), 0, ctx->stream, s); break;
-      default: hipLaunchKernelGGL((ksg_sweep<1024, 0, false>), dim3(R), dim3(1024), 0, ctx->stream, s); break;
+    if (S > 1) HIPC(ctx, hipMemsetAsync(s.gbar, 0, sizeof(unsigned) * (size_t)R, ctx->stream));
+    const int grid = R * S;
+    if (S > 1) {
+      switch (block * 100 + kn) {
+        case 25608: launch_sweep<256, 8, true>(s, grid, fast, ctx->stream); break;
+        default: launch_sweep<256, 0, true>(s, grid, fast, ctx->stream); break;
+      }
+    } else {
+      switch (block * 100 + kn) {
+        case 25608: launch_sweep<256, 8, false>(s, grid, fast, ctx->stream); break;
+        case 25616: launch_sweep<256, 16, false>(s, grid, fast, ctx->stream); break;
+        case 25620: launch_sweep<256, 20, false>(s, grid, fast, ctx->stream); break;
+        case 25624: launch_sweep<256, 24, false>(s, grid, fast, ctx->stream); break;
+        case 25632: launch_sweep<256, 32, false>(s, grid, fast, ctx->stream); break;
+        case 51232: launch_sweep<512, 32, false>(s, grid, fast, ctx->stream); break;
+        case 102432: launch_sweep<1024, 32, false>(s, grid, fast, ctx->stream); break;
+        case 25600: launch_sweep<256, 0, false>(s, grid, fast, ctx->stream); break;
+        default: launch_sweep<1024, 0, false>(s, grid, fast, ctx->stream); break;
+      }
     }
     if ((rc = tlaunched(ctx, KSG_K_SWEEP, (double)R * s.nb * N))) return rc;
   }
+  ctx->sweep_timeout = S > 1 ? s.timeout : nullptr;
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   return KSG_OK;
@@ -3001,6 +3051,12 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
   if ((rc = tcollect(ctx))) return rc;
+  if (ctx->last_path == 3 && ctx->sweep_timeout) {
+    unsigned to = 0;
+    HIPC(ctx, hipMemcpy(&to, ctx->sweep_timeout, sizeof(to), hipMemcpyDeviceToHost));
+    ctx->sweep_timeout = nullptr;
+    if (to) return fail(ctx, KSG_E_DEVICE, "replica sweep: group barrier timed out");
+  }
   if (summaries) {
     for (size_t r = 0; r < RR; r++) {
       ksg_replica_summary& sm = summaries[r];

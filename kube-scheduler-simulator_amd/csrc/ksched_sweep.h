@@ -10,7 +10,7 @@
 //
 //   ksg_sweep_static   grid (node tiles, batch pods): one 8-byte static record
 //                      per (pod, node), computed once for all replicas;
-//   ksg_sweep<BLOCK,KN> one workgroup per replica, persistent over the batch:
+//   ksg_sweep<BLOCK,KN> S workgroups per replica, persistent over the batch:
 //                      per pod, one sweep over the replica's nodes reads the
 //                      static record and the Fit/BalancedAllocation columns
 //                      (every load of a node issued before any use, no
@@ -19,12 +19,25 @@
 //                      normalises from the registers, takes the argmax and the
 //                      lane that owns the selected node assumes the pod.
 //
-// The owner lane of node n is n % BLOCK for every pod, so a node's mutable
-// columns are only ever read and written by one lane: an assume needs no
-// barrier.  Results equal ksg_queue_kernel's bit for bit (same plugin
-// arithmetic, same reductions), which the GPU tests check against the oracle.
+// Node n of a replica is owned by workgroup (n / BLOCK) mod S of the replica's
+// group and lane n mod BLOCK for every pod, so a node's mutable columns are
+// only ever read and written by one lane: an assume needs no barrier.  With
+// many replicas S = 1 (config 4: 1,024 replicas fill the chip); with few
+// replicas of a large cluster (config 5: 64 replicas x 100,000 nodes, or 8 per
+// GPU of an 8-GPU sweep) the S workgroups of a replica exchange their partial
+// reductions through per-workgroup slots and a group barrier, two per pod.
+// Results equal ksg_queue_kernel's bit for bit (same plugin arithmetic, same
+// reductions), which the GPU tests check against the oracle.
 
 // static record layout: kSr* in ksched_kernels.h
+
+struct SweepSlot {          // one workgroup's partials of the current pod (S > 1)
+  uint32_t nfeas;
+  int32_t minidx, mt, ma;
+  uint64_t best;
+  uint32_t err;
+  int32_t pad;
+};
 
 struct SweepArgs {
   DevCluster c;
@@ -37,7 +50,48 @@ struct SweepArgs {
   uint64_t* srec;               // [nb][N] static records
   uint64_t* scratch;            // KN == 0 only: [R][N] packed per-node results
   int32_t* placements;
+  int32_t S;                    // workgroups per replica (>= 1)
+  SweepSlot* slots;             // S > 1: [2][R * S] partials by pod parity
+  unsigned* gbar;               // S > 1: [R] arrival counters, zeroed before the launch
+  unsigned* timeout;            // S > 1: set when a group barrier poll gave up
 };
+
+template <class T>
+__device__ __forceinline__ T ald(const T* p) {   // agent-scope load of a word another workgroup wrote
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Arrive at a counter shared by `arrivals` co-resident workgroups and wait for
+// all of them (monotonic counter: the k-th barrier completes at k * arrivals).
+// Every storing wave drains its stores, one lane releases at agent scope,
+// arrives, polls relaxed with s_sleep and acquires at agent scope (MI355X
+// guide, Guideline 16).  Bounded: after a timeout it records one (for every
+// waiter and for the host) and returns false.
+__device__ __forceinline__ bool arrive_and_wait(unsigned* bar, unsigned* timeout, int arrivals, unsigned& target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  target += (unsigned)arrivals;
+  __shared__ int s_timeout;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    int to = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26) || __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        to = 1;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_timeout = to;
+  }
+  __syncthreads();
+  return s_timeout == 0;
+}
 
 __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
@@ -159,11 +213,16 @@ struct SweepPart {
   int32_t minidx, mt, ma;
 };
 
-// KN > 0: node n = tid + k * BLOCK, k < KN, results kept in registers.
-// KN == 0: nodes tid, tid + BLOCK, ... < N, results in the replica's scratch row.
+// KN > 0: the lane's nodes are base + k * S * BLOCK, k < KN (base = sub * BLOCK +
+// tid), results kept in registers.  KN == 0: the same nodes for k while < N,
+// results in the replica's scratch row.
 // FAST: every replica's Fit and BalancedAllocation score exactly {cpu, memory}
-// with positive weights (CmProf::fast; the host checks it for all replicas).
-template <int BLOCK, int KN, bool FAST>
+// with positive weights (CmProf::fast; the host checks it for all replicas);
+// otherwise the generic plugin arithmetic on the loaded columns.
+// MULTI: S > 1 workgroups per replica (runtime stride S * BLOCK between a
+// lane's nodes); without it S == 1 and the stride is the constant BLOCK, which
+// keeps the node offsets in the load instructions' immediates.
+template <int BLOCK, int KN, bool FAST, bool MULTI>
 __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) {   // 16 waves per CU
   constexpr int NW = BLOCK / 64;
   constexpr int U = !FAST ? 1 : (KN >= 20 ? 2 : 4);   // nodes whose loads are in flight together
@@ -171,9 +230,14 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
   __shared__ SweepPart s_part[2][NW];
   __shared__ uint64_t s_best[2][NW];
   __shared__ uint32_t s_err[2][NW];
+  __shared__ SweepPart s_grp[2];        // S > 1: the replica's totals
+  __shared__ uint64_t s_gbest[2];
+  __shared__ uint32_t s_gerr[2];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int rep = blockIdx.x;
+  const int S = MULTI ? a.S : 1;
+  const int rep = MULTI ? blockIdx.x / S : blockIdx.x, sub = MULTI ? blockIdx.x - rep * S : 0;
+  const int stride = MULTI ? S * BLOCK : BLOCK;   // between a lane's nodes
   const DevCluster& c = a.c;
   const int N = c.N, R = c.R;
   const size_t NN = (size_t)N;
@@ -188,18 +252,26 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
   const SweepProf sp = sweep_prof(prof);
   constexpr int KR = KN > 0 ? KN : 1;
   uint64_t recs[KR];
+  unsigned target = 0;
+  const size_t slot_base = (size_t)rep * S;   // this replica's slots within a parity set
 
   for (int j = 0; j < a.nb; j++) {
     const ksg_pod& p = a.pods[a.b0 + j];
     const SweepPod q = sweep_pod(sp, prof, p, R);
     const uint64_t* srec = a.srec + (size_t)j * N;
     const int par = j & 1;
+    SweepSlot* slots = a.slots + (size_t)par * gridDim.x;
 
     // ---- sweep A: filters + raw scores of this lane's nodes ------------------
     uint32_t nfeas = 0;
     int32_t minidx = 0x7fffffff, mt = 0, ma = 0;
-    auto eval = [&](int n, uint64_t sr, int64_t ac, int64_t am, int64_t rc, int64_t rm, int64_t zc, int64_t zm,
-                    int32_t pc, int32_t al) -> uint64_t {
+    auto feasible = [&](int n, uint64_t sr, const NodeCols& L) {
+      bool ok = (sr & q.fmask) == 0;
+      if (q.fit_on) ok = ok && fit_filter(c, p, L, prof.fit_ignored_res) == 0;
+      return ok;
+    };
+    auto eval_fast = [&](int n, uint64_t sr, int64_t ac, int64_t am, int64_t rc, int64_t rm, int64_t zc, int64_t zm,
+                         int32_t pc, int32_t al) -> uint64_t {
       bool ok = (sr & q.fmask) == 0;
       if (q.fit_on) {
         ok = ok && pc + 1 <= al;
@@ -210,14 +282,15 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       }
       if (!ok) return 0;
       int64_t fs = 0, bs = 0;
-      if constexpr (FAST) {
-        sweep_cm_scores(sp.cm, p, ac, am, rc, rm, zc, zm, fs, bs);
-      } else {
-        NodeCols L;
-        load_cols(c, requested, nonzero, pod_count, n, L);
-        fs = fit_score(prof, p, L);
-        bs = ba_score(prof, p, L);
-      }
+      sweep_cm_scores(sp.cm, p, ac, am, rc, rm, zc, zm, fs, bs);
+      const int64_t rt = (sr >> 8) & 0xff, ra = (sr >> 16) & 0xffff, im = (sr >> 32) & 0xff;
+      const int64_t part = im * q.w_img + ((q.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? fs * q.w_fit : 0) +
+                           ((q.smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? bs * q.w_ba : 0);
+      return pack_rec(part, rt, ra);
+    };
+    auto eval_generic = [&](int n, uint64_t sr, const NodeCols& L) -> uint64_t {
+      if (!feasible(n, sr, L)) return 0;
+      const int64_t fs = fit_score(prof, p, L), bs = ba_score(prof, p, L);
       const int64_t rt = (sr >> 8) & 0xff, ra = (sr >> 16) & 0xffff, im = (sr >> 32) & 0xff;
       const int64_t part = im * q.w_img + ((q.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? fs * q.w_fit : 0) +
                            ((q.smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? bs * q.w_ba : 0);
@@ -231,37 +304,53 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
         ma = max(ma, (int32_t)((x >> 32) & 0xffff));
       }
     };
-    const int iters = KN > 0 ? KN : (N + BLOCK - 1) / BLOCK;
+    const int iters = KN > 0 ? KN : (N + stride - 1) / stride;
     // opaque per pod: keeps the per-node addresses from being hoisted out of
     // the pod loop (KN x 9 live 64-bit pointers would not fit the VGPR budget)
-    int tb = tid;
+    int tb = sub * BLOCK + tid;
     asm volatile("" : "+v"(tb));
     auto group = [&](const int k0) {
-      uint64_t sr[U];
-      int64_t ac[U], am[U], rc[U], rm[U], zc[U], zm[U];
-      int32_t pc[U], al[U];
+      if constexpr (FAST) {
+        uint64_t sr[U];
+        int64_t ac[U], am[U], rc[U], rm[U], zc[U], zm[U];
+        int32_t pc[U], al[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int n = tb + (k0 + u) * BLOCK;
-        const int nl = n < N ? n : 0;   // clamped: every lane loads from a valid address
-        sr[u] = srec[nl];
-        ac[u] = c.alloc[KSG_RES_CPU * NN + nl];
-        am[u] = c.alloc[KSG_RES_MEM * NN + nl];
-        rc[u] = requested[KSG_RES_CPU * NN + nl];
-        rm[u] = requested[KSG_RES_MEM * NN + nl];
-        zc[u] = nonzero[nl];
-        zm[u] = nonzero[NN + nl];
-        pc[u] = pod_count[nl];
-        al[u] = c.allowed[nl];
-      }
+        for (int u = 0; u < U; u++) {
+          const int n = tb + (k0 + u) * stride;
+          const int nl = n < N ? n : 0;   // clamped: every lane loads from a valid address
+          sr[u] = srec[nl];
+          ac[u] = c.alloc[KSG_RES_CPU * NN + nl];
+          am[u] = c.alloc[KSG_RES_MEM * NN + nl];
+          rc[u] = requested[KSG_RES_CPU * NN + nl];
+          rm[u] = requested[KSG_RES_MEM * NN + nl];
+          zc[u] = nonzero[nl];
+          zm[u] = nonzero[NN + nl];
+          pc[u] = pod_count[nl];
+          al[u] = c.allowed[nl];
+        }
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int n = tb + (k0 + u) * BLOCK;
+        for (int u = 0; u < U; u++) {
+          const int n = tb + (k0 + u) * stride;
+          uint64_t x = 0;
+          if (k0 + u < iters && n < N) x = eval_fast(n, sr[u], ac[u], am[u], rc[u], rm[u], zc[u], zm[u], pc[u], al[u]);
+          account(n, x);
+          if constexpr (KN > 0) {
+            if (k0 + u < KN) recs[k0 + u < KR ? k0 + u : 0] = x;
+          } else {
+            if (n < N) scratch[n] = x;
+          }
+        }
+      } else {   // U == 1: one node's record and every resource column in flight
+        const int n = tb + k0 * stride;
+        const int nl = n < N ? n : 0;
+        const uint64_t sr = srec[nl];
+        NodeCols L;
+        load_cols(c, requested, nonzero, pod_count, nl, L);
         uint64_t x = 0;
-        if (k0 + u < iters && n < N) x = eval(n, sr[u], ac[u], am[u], rc[u], rm[u], zc[u], zm[u], pc[u], al[u]);
+        if (k0 < iters && n < N) x = eval_generic(n, sr, L);
         account(n, x);
         if constexpr (KN > 0) {
-          if (k0 + u < KN) recs[k0 + u < KR ? k0 + u : 0] = x;
+          recs[k0 < KR ? k0 : 0] = x;
         } else {
           if (n < N) scratch[n] = x;
         }
@@ -293,6 +382,37 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       gmt = max(gmt, w.mt);
       gma = max(gma, w.ma);
     }
+    if (MULTI) {   // the replica's totals over its S workgroups
+      if (tid == 0) {
+        SweepSlot& o = slots[slot_base + sub];
+        o.nfeas = gn;
+        o.minidx = gmin;
+        o.mt = gmt;
+        o.ma = gma;
+      }
+      if (!arrive_and_wait(a.gbar + rep, a.timeout, S, target)) return;
+      if (wv == 0) {
+        uint32_t n_ = 0;
+        int32_t mi = 0x7fffffff, t_ = 0, a_ = 0;
+        for (int qi = lane; qi < S; qi += 64) {
+          const SweepSlot* o = slots + slot_base + qi;
+          n_ += ald(&o->nfeas);
+          mi = min(mi, ald(&o->minidx));
+          t_ = max(t_, ald(&o->mt));
+          a_ = max(a_, ald(&o->ma));
+        }
+        n_ = wreduce(n_, OpAdd32{});
+        mi = wreduce(mi, OpMin32{});
+        t_ = wreduce(t_, OpMaxI32{});
+        a_ = wreduce(a_, OpMaxI32{});
+        if (lane == 0) s_grp[par] = SweepPart{n_, mi, t_, a_};
+      }
+      __syncthreads();
+      gn = s_grp[par].nfeas;
+      gmin = s_grp[par].minidx;
+      gmt = s_grp[par].mt;
+      gma = s_grp[par].ma;
+    }
     int selected = -1;
     if (gn == 1) {
       selected = gmin;
@@ -322,11 +442,11 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       if constexpr (KN > 0) {
 #pragma unroll
         for (int k = 0; k < KN; k++) {
-          score(tb + k * BLOCK, recs[k]);
+          score(tb + k * stride, recs[k]);
           if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
       } else {
-        for (int n = tid; n < N; n += BLOCK) score(n, scratch[n]);
+        for (int n = sub * BLOCK + tid; n < N; n += stride) score(n, scratch[n]);
       }
       best = wreduce(best, OpMaxU64{});
       err = wreduce(err, OpOr32{});
@@ -342,15 +462,39 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
         gb = s_best[par][i] > gb ? s_best[par][i] : gb;
         gerr |= s_err[par][i] != 0;
       }
+      if (MULTI) {   // the replica's argmax over its S workgroups
+        if (tid == 0) {
+          SweepSlot& o = slots[slot_base + sub];
+          o.best = gb;
+          o.err = gerr ? 1u : 0u;
+        }
+        if (!arrive_and_wait(a.gbar + rep, a.timeout, S, target)) return;
+        if (wv == 0) {
+          uint64_t b_ = 0;
+          uint32_t e_ = 0;
+          for (int qi = lane; qi < S; qi += 64) {
+            const SweepSlot* o = slots + slot_base + qi;
+            const uint64_t ob = ald(&o->best);
+            b_ = ob > b_ ? ob : b_;
+            e_ |= ald(&o->err);
+          }
+          b_ = wreduce(b_, OpMaxU64{});
+          e_ = wreduce(e_, OpOr32{});
+          if (lane == 0) { s_gbest[par] = b_; s_gerr[par] = e_; }
+        }
+        __syncthreads();
+        gb = s_gbest[par];
+        gerr = s_gerr[par] != 0;
+      }
       if (!gerr) selected = key_node(gb);
     }
     // ---- assume: the lane that owns the selected node ------------------------
-    if (selected >= 0 && (selected % BLOCK) == tid) {
+    if (selected >= 0 && (!MULTI || ((selected / BLOCK) % S) == sub) && (selected % BLOCK) == tid) {
       for (int r = 0; r < R; r++) requested[(size_t)r * N + selected] += p.req[r];
       nonzero[selected] += p.nz_cpu;
       nonzero[NN + selected] += p.nz_mem;
       pod_count[selected] += 1;
     }
-    if (tid == 0) a.placements[(size_t)rep * a.count + a.out0 + j] = selected;
+    if (sub == 0 && tid == 0) a.placements[(size_t)rep * a.count + a.out0 + j] = selected;
   }
 }

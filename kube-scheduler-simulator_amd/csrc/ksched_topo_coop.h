@@ -75,10 +75,7 @@ struct CoopAcc {    // atomics fallback for large histograms
   int32_t hist[KSG_HIST_MAX];
 };
 
-template <class T>
-__device__ __forceinline__ T ald(const T* p) {
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// ald(), arrive_and_wait(): ksched_sweep.h
 
 #ifdef KSG_STAMPS
 #define KSG_CSTAMP(seg)                                                     \
@@ -112,29 +109,7 @@ struct CoopArgs {
 };
 
 __device__ __forceinline__ bool coop_barrier(unsigned* bar, unsigned* timeout, int G, unsigned& target) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
-  __syncthreads();
-  target += (unsigned)G;
-  __shared__ int s_timeout;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    int to = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 26) || __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        to = 1;
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_timeout = to;
-  }
-  __syncthreads();
-  return s_timeout == 0;
+  return arrive_and_wait(bar, timeout, G, target);
 }
 
 // PodTopologySpread with one soft constraint: the per-node count m of

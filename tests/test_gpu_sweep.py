@@ -2,7 +2,8 @@
 static-record + per-replica sweep kernels against the C++ oracle run replica by
 replica, bit-exact placements and summaries.  Cases cover every (BLOCK, KN)
 shape the host picks (registers: N <= 2,048 ... 32,768; scratch row: N >
-32,768), the generic (non cpu/memory) profile path, mixed strategies and
+32,768; S > 1 workgroups per replica from 4,096 nodes with few replicas),
+the generic (non cpu/memory) profile path, mixed strategies and
 weights, nodeName / unschedulable / taint / affinity edge cases from the zoo
 under node-local profiles, and profiles that fall back to the queue kernel."""
 import numpy as np
@@ -63,6 +64,8 @@ CASES = [
     ("c2-33000x30-r2", lambda: _c2(33000, 30), lambda: G.replica_profiles(2)),      # scratch row
     ("c5-generic-r3", lambda: G.config5(n_nodes=400, n_pods=300, n_images=200, taint_vocab=128,
                                         taints_per_node=16, images_per_node=20), None),
+    ("c5-generic-6000-r3", lambda: G.config5(n_nodes=6000, n_pods=60, n_images=500, taint_vocab=256,
+                                             taints_per_node=16, images_per_node=20), None),   # S = 2, generic
     ("c1-default-r2", lambda: G.config1(n_nodes=100, n_pods=300), None),            # PTS/IPA: queue kernel
 ] + [(f"zoo-{s}-r4", (lambda s=s: __import__("zoo").zoo(s)), (lambda: _zoo_profiles(4))) for s in range(6)]
 
