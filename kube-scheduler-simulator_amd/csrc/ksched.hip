@@ -1099,33 +1099,7 @@ struct P2Part {
   int32_t kidx;              // slot of k0, -1 if not in this wave
 };
 
-// floor(x / a) for 0 <= x, 0 < a, quotient below 2^20 (every division on the
-// changed-node path: scores x 100 over allocatable amounts, weight sums or
-// maxima).  inv = (float)(1 / a).  The f32 estimate is within 2^-21 relative
-// of x / a, i.e. within one of the quotient; one integer multiply-subtract
-// corrects it, so the result is exact.
-__device__ __forceinline__ int64_t qdiv(int64_t x, int64_t a, float inv) {
-  const float xf = __builtin_fmaf((float)(uint32_t)((uint64_t)x >> 32), 4294967296.0f, (float)(uint32_t)x);
-  int64_t q = (int32_t)(xf * inv);
-  const int64_t r = x - q * a;
-  q += r < 0 ? -1 : (r >= a ? 1 : 0);
-  return q;
-}
-
-// x / a in float64, bit-identical to the compiler's division for 0 <= x and
-// 1 <= a < 2^53 (integers): the same rcp + two Newton steps + residual fma
-// sequence without v_div_scale / v_div_fmas / v_div_fixup, which are identities
-// in that range.  No VCC use, so two divisions interleave.
-__device__ __forceinline__ double ddiv(double x, double a) {
-  double r = __builtin_amdgcn_rcp(a);
-  double e = __builtin_fma(-a, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-a, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  const double q = x * r;
-  const double rem = __builtin_fma(-a, q, x);
-  return __builtin_fma(rem, r, q);
-}
+// qdiv(), ddiv(): ksched_device.h
 
 // Batch-uniform profile facts for the compact evaluator.
 struct CmProf {
@@ -1960,7 +1934,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
           int64_t s;
           if (x < 0) s = 0;
           else if (pmax == 0) s = 100;
-          else s = div_nonneg(100 * (pmax + pmin - x), pmax);
+          else s = div_small(100 * (pmax + pmin - x), pmax);
           err |= (s < 0 || s > 100);
           total += s * w_pts;
           if (cap) cnorm[(size_t)KSG_PL_POD_TOPOLOGY_SPREAD * N + n] = s;
@@ -2572,7 +2546,7 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   if (kn == 0) TA(tmp, &s.scratch, sizeof(uint64_t) * (size_t)R * N);
   if (S > 1) {
     TA(tmp, &s.slots, sizeof(SweepSlot) * 2 * (size_t)R * S);
-    TA(tmp, &s.gbar, sizeof(unsigned) * ((size_t)R + 4));
+    TA(tmp, &s.gbar, sizeof(unsigned) * 16 * (size_t)R);
     TA(tmp, &s.timeout, 16);
     HIPC(ctx, hipMemsetAsync(s.timeout, 0, 16, ctx->stream));
   }
@@ -2587,7 +2561,7 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     s.out0 = off;
     hipLaunchKernelGGL(ksg_sweep_static, dim3((N + 255) / 256, s.nb), dim3(256), 0, ctx->stream, s);
     if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)s.nb * N))) return rc;
-    if (S > 1) HIPC(ctx, hipMemsetAsync(s.gbar, 0, sizeof(unsigned) * (size_t)R, ctx->stream));
+    if (S > 1) HIPC(ctx, hipMemsetAsync(s.gbar, 0, sizeof(unsigned) * 16 * (size_t)R, ctx->stream));
     const int grid = R * S;
     if (S > 1) {
       switch (block * 100 + kn) {

@@ -78,6 +78,41 @@ __device__ __forceinline__ int64_t div_nonneg(int64_t x, int64_t a) {
   return q;
 }
 
+// floor(x / a) for 0 <= x, 0 < a, quotient below 2^20 (every division on the
+// changed-node path: scores x 100 over allocatable amounts, weight sums or
+// maxima).  inv = (float)(1 / a).  The f32 estimate is within 2^-21 relative
+// of x / a, i.e. within one of the quotient; one integer multiply-subtract
+// corrects it, so the result is exact.
+__device__ __forceinline__ int64_t qdiv(int64_t x, int64_t a, float inv) {
+  const float xf = __builtin_fmaf((float)(uint32_t)((uint64_t)x >> 32), 4294967296.0f, (float)(uint32_t)x);
+  int64_t q = (int32_t)(xf * inv);
+  const int64_t r = x - q * a;
+  q += r < 0 ? -1 : (r >= a ? 1 : 0);
+  return q;
+}
+
+// x / a in float64, bit-identical to the compiler's division for 0 <= x and
+// 1 <= a < 2^53 (integers): the same rcp + two Newton steps + residual fma
+// sequence without v_div_scale / v_div_fmas / v_div_fixup, which are identities
+// in that range.  No VCC use, so two divisions interleave.
+__device__ __forceinline__ double ddiv(double x, double a) {
+  double r = __builtin_amdgcn_rcp(a);
+  double e = __builtin_fma(-a, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-a, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = x * r;
+  const double rem = __builtin_fma(-a, q, x);
+  return __builtin_fma(rem, r, q);
+}
+
+// floor(x / a) for a quotient known to be at most 100 (scores, normalisation):
+// qdiv with its own reciprocal estimate; div_nonneg outside qdiv's domain.
+__device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
+  if (x < 0 || a <= 0) return x / a;
+  return qdiv(x, a, __builtin_amdgcn_rcpf((float)a));
+}
+
 // ---- node sources ------------------------------------------------------------
 // The plugin code reads a node's static columns through an accessor (GNode:
 // the SoA columns in global memory), so a kernel can substitute its own copy.
@@ -264,12 +299,12 @@ __device__ __forceinline__ int64_t fit_score(const ksg_profile& prof, const ksg_
     alloc_req(p, L, prof.fit_res[i], false, a, q);
     if (a == 0) continue;
     int64_t s;
-    if (prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : div_nonneg((a - q) * 100, a);
-    else s = div_nonneg((q > a ? a : q) * 100, a);
+    if (prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : div_small((a - q) * 100, a);
+    else s = div_small((q > a ? a : q) * 100, a);
     num += s * prof.fit_w[i];
     wsum += prof.fit_w[i];
   }
-  return wsum == 0 ? 0 : div_nonneg(num, wsum);
+  return wsum == 0 ? 0 : div_small(num, wsum);
 }
 
 // balancedResourceScorer, in Go's float64 operation order.  Fractions are
@@ -281,7 +316,7 @@ __device__ __forceinline__ int64_t ba_score(const ksg_profile& prof, const ksg_p
     int64_t a, q;
     alloc_req(p, L, prof.ba_res[i], true, a, q);
     if (a == 0) continue;
-    double f = (double)q / (double)a;
+    double f = ddiv((double)q, (double)a);   // IEEE-exact for integer q >= 0, a >= 1
     if (f > 1) f = 1;
     total += f;
     if (k == 0) f0 = f;
@@ -298,7 +333,7 @@ __device__ __forceinline__ int64_t ba_score(const ksg_profile& prof, const ksg_p
       int64_t a, q;
       alloc_req(p, L, prof.ba_res[i], true, a, q);
       if (a == 0) continue;
-      double f = (double)q / (double)a;
+      double f = ddiv((double)q, (double)a);   // IEEE-exact for integer q >= 0, a >= 1
       if (f > 1) f = 1;
       sum = sum + (f - mean) * (f - mean);
     }
@@ -328,5 +363,5 @@ __device__ __forceinline__ int64_t image_score(const DevCluster& c, const Src& n
   const int64_t mx = 1000 * mb * (int64_t)n_containers;
   if (sum < minT) sum = minT;
   else if (sum > mx) sum = mx;
-  return div_nonneg(100 * (sum - minT), mx - minT);
+  return div_small(100 * (sum - minT), mx - minT);
 }

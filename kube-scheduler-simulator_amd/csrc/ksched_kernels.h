@@ -515,14 +515,14 @@ __device__ __forceinline__ int64_t total_score(const PodView& v, int64_t part, i
   int64_t total = part;
   if (v.smask & bit(KSG_PL_TAINT_TOLERATION)) {
     int64_t s = 100;
-    if (max_t != 0) s = 100 - div_nonneg(100 * rt, max_t);
+    if (max_t != 0) s = 100 - div_small(100 * rt, max_t);
     err |= (s < 0 || s > 100);
     total += s * v.w_t;
     if (nt) *nt = s;
   }
   if (v.smask & bit(KSG_PL_NODE_AFFINITY)) {
     int64_t s = ra;
-    if (max_a != 0) s = div_nonneg(100 * ra, max_a);
+    if (max_a != 0) s = div_small(100 * ra, max_a);
     err |= (s < 0 || s > 100);
     total += s * v.w_a;
     if (na) *na = s;

@@ -52,7 +52,7 @@ struct SweepArgs {
   int32_t* placements;
   int32_t S;                    // workgroups per replica (>= 1)
   SweepSlot* slots;             // S > 1: [2][R * S] partials by pod parity
-  unsigned* gbar;               // S > 1: [R] arrival counters, zeroed before the launch
+  unsigned* gbar;               // S > 1: [R][16] arrival counters (one 64-B line each), zeroed before the launch
   unsigned* timeout;            // S > 1: set when a group barrier poll gave up
 };
 
@@ -225,7 +225,7 @@ struct SweepPart {
 template <int BLOCK, int KN, bool FAST, bool MULTI>
 __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) {   // 16 waves per CU
   constexpr int NW = BLOCK / 64;
-  constexpr int U = !FAST ? 1 : (KN >= 20 ? 2 : 4);   // nodes whose loads are in flight together
+  constexpr int U = !FAST ? (KN == 0 ? 2 : 1) : (KN >= 20 ? 2 : 4);   // nodes whose loads are in flight together
   __shared__ ksg_profile s_prof;
   __shared__ SweepPart s_part[2][NW];
   __shared__ uint64_t s_best[2][NW];
@@ -340,19 +340,27 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
             if (n < N) scratch[n] = x;
           }
         }
-      } else {   // U == 1: one node's record and every resource column in flight
-        const int n = tb + k0 * stride;
-        const int nl = n < N ? n : 0;
-        const uint64_t sr = srec[nl];
-        NodeCols L;
-        load_cols(c, requested, nonzero, pod_count, nl, L);
-        uint64_t x = 0;
-        if (k0 < iters && n < N) x = eval_generic(n, sr, L);
-        account(n, x);
-        if constexpr (KN > 0) {
-          recs[k0 < KR ? k0 : 0] = x;
-        } else {
-          if (n < N) scratch[n] = x;
+      } else {   // U nodes' records and every resource column in flight
+        uint64_t sr[U];
+        NodeCols L[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int n = tb + (k0 + u) * stride;
+          const int nl = n < N ? n : 0;
+          sr[u] = srec[nl];
+          load_cols(c, requested, nonzero, pod_count, nl, L[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int n = tb + (k0 + u) * stride;
+          uint64_t x = 0;
+          if (k0 + u < iters && n < N) x = eval_generic(n, sr[u], L[u]);
+          account(n, x);
+          if constexpr (KN > 0) {
+            if (k0 + u < KN) recs[k0 + u < KR ? k0 + u : 0] = x;
+          } else {
+            if (n < N) scratch[n] = x;
+          }
         }
       }
       __builtin_amdgcn_sched_barrier(0);   // one group's loads in flight at a time (register budget)
@@ -390,7 +398,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
         o.mt = gmt;
         o.ma = gma;
       }
-      if (!arrive_and_wait(a.gbar + rep, a.timeout, S, target)) return;
+      if (!arrive_and_wait(a.gbar + 16 * rep, a.timeout, S, target)) return;
       if (wv == 0) {
         uint32_t n_ = 0;
         int32_t mi = 0x7fffffff, t_ = 0, a_ = 0;
@@ -445,8 +453,17 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
           score(tb + k * stride, recs[k]);
           if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
-      } else {
-        for (int n = sub * BLOCK + tid; n < N; n += stride) score(n, scratch[n]);
+      } else {   // four scratch words in flight per step
+        int n = sub * BLOCK + tid;
+        for (; n + 3 * stride < N; n += 4 * stride) {
+          const uint64_t x0 = scratch[n], x1 = scratch[n + stride], x2 = scratch[n + 2 * stride],
+                         x3 = scratch[n + 3 * stride];
+          score(n, x0);
+          score(n + stride, x1);
+          score(n + 2 * stride, x2);
+          score(n + 3 * stride, x3);
+        }
+        for (; n < N; n += stride) score(n, scratch[n]);
       }
       best = wreduce(best, OpMaxU64{});
       err = wreduce(err, OpOr32{});
@@ -468,7 +485,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
           o.best = gb;
           o.err = gerr ? 1u : 0u;
         }
-        if (!arrive_and_wait(a.gbar + rep, a.timeout, S, target)) return;
+        if (!arrive_and_wait(a.gbar + 16 * rep, a.timeout, S, target)) return;
         if (wv == 0) {
           uint64_t b_ = 0;
           uint32_t e_ = 0;

@@ -813,7 +813,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           int64_t s;
           if (x < 0) s = 0;
           else if (pmax == 0) s = 100;
-          else s = div_nonneg(100 * (pmax + pmin - x), pmax);
+          else s = div_small(100 * (pmax + pmin - x), pmax);
           err |= (s < 0 || s > 100);
           total += s * w_pts;
         }
