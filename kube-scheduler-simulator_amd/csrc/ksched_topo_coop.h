@@ -270,6 +270,28 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
 #endif
 
   auto node_of = [&](int k) { return (k * G + wg) * BLOCK + tid; };
+  // LDS words [base, base + nw) += (or |=) the same words of every workgroup's
+  // partial slot: (word, workgroup) pairs over the lanes, four loads in flight
+  auto fold_words = [&](int base, int nw, bool bits) {
+    const int total = nw * G;
+    for (int x0 = tid; x0 < total; x0 += 4 * BLOCK) {
+      int32_t y[4];
+      int w[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int x = x0 + u * BLOCK;
+        w[u] = x / G;
+        const int qg = x - w[u] * G;
+        y[u] = x < total ? ald(a.phist + (size_t)qg * kCoopPHist + base + w[u]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (!y[u]) continue;
+        if (bits) atomicOr((uint32_t*)&s_hist[base + w[u]], (uint32_t)y[u]);
+        else atomicAdd(&s_hist[base + w[u]], y[u]);
+      }
+    }
+  };
   // block-wide fold of one value per lane: DPP within waves, partials in LDS
   auto bfold_l = [&](long long x, auto op, int slot) {
     x = wreduce(x, op);
@@ -327,6 +349,12 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const TopoProg& g = s_g;
     const TopoCtx tc{&s_g, &s_t, s_hist, st.cnt, st.tab, true, false, 0};
     __syncthreads();
+    // which partial values this pod needs at all (pod-uniform): folds of the
+    // others are skipped
+    bool need_hmin = false, need_se = false;
+    for (int i = 0; i < g.n_hard; i++) need_hmin |= s_t.hard[i].unique != 0;
+    for (int i = 0; i < g.n_soft; i++) need_se |= s_t.soft[i].unique && !g.soft[6 * i + 5];
+    const bool need_aff = g.ipa && g.n_aff > 0, need_pref = g.ipa && g.n_pref > 0;
     KSG_CSTAMP(0);
 
     // ---- phase 1: pre-pass over this lane's nodes -------------------------
@@ -412,15 +440,23 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           }
         }
       }
+      if (need_hmin) {
 #pragma unroll
-      for (int i = 0; i < kMaxHard; i++) {
-        bfold_l(lmin[i], OpMinL{}, i);
-        bfold_l(ldom[i], OpAddL{}, 4 + i);
+        for (int i = 0; i < kMaxHard; i++) {
+          if (i >= g.n_hard) break;
+          bfold_l(lmin[i], OpMinL{}, i);
+          bfold_i((int32_t)ldom[i], OpAddI{}, 4 + i);
+        }
       }
+      if (need_se) {
 #pragma unroll
-      for (int i = 0; i < kMaxSoft; i++) bfold_l(lempty[i], OpAddL{}, 8 + i);
-      bfold_l(laff, OpAddL{}, 12);
-      bfold_l(lany, OpAddL{}, 13);
+        for (int i = 0; i < kMaxSoft; i++) {
+          if (i >= g.n_soft) break;
+          bfold_l(lempty[i], OpAddL{}, 8 + i);
+        }
+      }
+      if (need_aff) bfold_l(laff, OpAddL{}, 12);
+      if (need_pref) bfold_i((int32_t)lany, OpOrI{}, 13);
       __syncthreads();
       // publish this workgroup's partial
       if (pmode) {
@@ -440,14 +476,14 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         for (int i = 0; i < g.n_anti; i++) merge_slot(s_t.anti[i]);
         for (int i = 0; i < g.n_pref; i++) merge_slot(s_t.pref[i]);
       }
-      if (tid < kMaxHard) {
+      if (need_hmin && tid < g.n_hard) {
         mine->hard_min[tid] = get_l(tid, OpMinL{});
-        mine->hard_dom[tid] = (int32_t)get_l(4 + tid, OpAddL{});
-      } else if (tid >= 64 && tid < 64 + kMaxSoft) {
+        mine->hard_dom[tid] = get_i(4 + tid, OpAddI{});
+      } else if (need_se && tid >= 64 && tid < 64 + g.n_soft) {
         mine->soft_empty[tid - 64] = get_l(8 + tid - 64, OpAddL{});
       } else if (tid == 128) {
-        mine->aff_total = get_l(12, OpAddL{});
-        mine->pref_any = get_l(13, OpAddL{}) != 0;
+        if (need_aff) mine->aff_total = get_l(12, OpAddL{});
+        if (need_pref) mine->pref_any = get_i(13, OpOrI{}) != 0;
       }
     }
     KSG_CSTAMP(1);
@@ -462,17 +498,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         // (word, workgroup) pairs over the lanes: counts add, presence bitmaps or
         auto fold_slot = [&](const Slot& sl) {
           if (sl.unique) return;
-          for (int x = tid; x < sl.V * G; x += BLOCK) {
-            const int w = x / G, q = x - w * G;
-            const int32_t y = ald(a.phist + (size_t)q * kCoopPHist + sl.hist + w);
-            if (y) atomicAdd(&s_hist[sl.hist + w], y);
-          }
-          const int bw = (sl.V + 31) / 32;
-          for (int x = tid; x < bw * G; x += BLOCK) {
-            const int w = x / G, q = x - w * G;
-            const int32_t y = ald(a.phist + (size_t)q * kCoopPHist + sl.pres + w);
-            if (y) atomicOr((uint32_t*)&s_hist[sl.pres + w], (uint32_t)y);
-          }
+          fold_words(sl.hist, sl.V, false);
+          fold_words(sl.pres, (sl.V + 31) / 32, true);
         };
         for (int i = 0; i < g.n_hard; i++) fold_slot(s_t.hard[i]);
         for (int i = 0; i < g.n_soft; i++) fold_slot(s_t.soft[i]);
@@ -483,8 +510,9 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         for (int i = tid; i < words; i += BLOCK) s_hist[i] = ald(&acc->hist[i]);
       }
       // scalars: lane q folds workgroup q's slot
-      {
-        long long hm[kMaxHard], hd[kMaxHard], se[kMaxSoft], af = 0, pa = 0;
+      if (need_hmin || need_se || need_aff || need_pref) {
+        long long hm[kMaxHard], se[kMaxSoft], af = 0;
+        int32_t hd[kMaxHard], pa = 0;
 #pragma unroll
         for (int i = 0; i < kMaxHard; i++) { hm[i] = BIG; hd[i] = 0; }
 #pragma unroll
@@ -492,35 +520,47 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         if (tid < G) {
           const CoopPart* q = a.parts + tid;
 #pragma unroll
-          for (int i = 0; i < kMaxHard; i++) { hm[i] = ald(&q->hard_min[i]); hd[i] = ald(&q->hard_dom[i]); }
+          for (int i = 0; i < kMaxHard; i++)
+            if (need_hmin && i < g.n_hard) { hm[i] = ald(&q->hard_min[i]); hd[i] = ald(&q->hard_dom[i]); }
 #pragma unroll
-          for (int i = 0; i < kMaxSoft; i++) se[i] = ald(&q->soft_empty[i]);
-          af = ald(&q->aff_total);
-          pa = ald(&q->pref_any);
+          for (int i = 0; i < kMaxSoft; i++)
+            if (need_se && i < g.n_soft) se[i] = ald(&q->soft_empty[i]);
+          if (need_aff) af = ald(&q->aff_total);
+          if (need_pref) pa = ald(&q->pref_any);
         }
         __syncthreads();   // every wave is past its phase-1 get_*() reads
+        if (need_hmin) {
 #pragma unroll
-        for (int i = 0; i < kMaxHard; i++) {
-          bfold_l(hm[i], OpMinL{}, i);
-          bfold_l(hd[i], OpAddL{}, 4 + i);
-        }
-#pragma unroll
-        for (int i = 0; i < kMaxSoft; i++) bfold_l(se[i], OpAddL{}, 8 + i);
-        bfold_l(af, OpAddL{}, 12);
-        bfold_l(pa, OpAddL{}, 13);
-      }
-      __syncthreads();
-      if (tid == 0) {
-        for (int i = 0; i < g.n_hard; i++)
-          if (s_t.hard[i].unique) {
-            s_t.hard_min[i] = get_l(i, OpMinL{});
-            s_t.hard_dom[i] = (int)get_l(4 + i, OpAddL{});
+          for (int i = 0; i < kMaxHard; i++) {
+            if (i >= g.n_hard) break;
+            bfold_l(hm[i], OpMinL{}, i);
+            bfold_i(hd[i], OpAddI{}, 4 + i);
           }
-        for (int i = 0; i < g.n_soft; i++) s_t.soft_empty[i] = get_l(8 + i, OpAddL{});
-        s_t.aff_total = get_l(12, OpAddL{});
-        s_t.pref_any = get_l(13, OpAddL{}) != 0;
+        }
+        if (need_se) {
+#pragma unroll
+          for (int i = 0; i < kMaxSoft; i++) {
+            if (i >= g.n_soft) break;
+            bfold_l(se[i], OpAddL{}, 8 + i);
+          }
+        }
+        if (need_aff) bfold_l(af, OpAddL{}, 12);
+        if (need_pref) bfold_i(pa, OpOrI{}, 13);
+        __syncthreads();
+        if (tid == 0) {
+          if (need_hmin)
+            for (int i = 0; i < g.n_hard; i++)
+              if (s_t.hard[i].unique) {
+                s_t.hard_min[i] = get_l(i, OpMinL{});
+                s_t.hard_dom[i] = get_i(4 + i, OpAddI{});
+              }
+          if (need_se)
+            for (int i = 0; i < g.n_soft; i++) s_t.soft_empty[i] = get_l(8 + i, OpAddL{});
+          if (need_aff) s_t.aff_total = get_l(12, OpAddL{});
+          if (need_pref) s_t.pref_any = get_i(13, OpOrI{}) != 0;
+        }
+        __syncthreads();
       }
-      __syncthreads();
       for (int i = 0; i < g.n_hard; i++) {   // minimum over present domains of the non-unique hard slots
         const Slot& sl = s_t.hard[i];
         if (sl.unique) continue;
@@ -568,6 +608,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
 
     NodeEval ev[KN];
     int64_t yv[KN];
+    int64_t pm[KN];   // one soft PTS constraint: the node's count m ...
+    int32_t pr[KN];   // ... and pts_soft1_m's case (0 m valid, 1 no key, 2 ignored)
     int32_t nfeas = 0, minidx = 0x7fffffff, lign = 0, has_val = 0, has_zero = 0;
     long long max_t = 0, max_a = 0;
     long long mmin = BIG, mmax = -BIG - 1, imin = BIG, imax = -BIG - 1;
@@ -577,6 +619,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       const int n = node_of(k);
       ev[k].st = 1;
       yv[k] = 0;
+      pm[k] = 0;
+      pr[k] = 2;
       if (n >= N || !ok) continue;
       TopoCtx tn = tc;
       tn.has_rec = true;
@@ -611,6 +655,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         if (soft1) {
           int64_t m = 0;
           const int r = pts_soft1_m(c, v, tn, n, m);
+          pm[k] = m;
+          pr[k] = r;
           if (r == 0) { has_val = 1; mmin = min(mmin, (long long)m); mmax = max(mmax, (long long)m); }
           else if (r == 1) has_zero = 1;
         }
@@ -622,39 +668,52 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     KSG_CSTAMP(5);
+    const bool need_ign = g.pts_score && g.require_all;
     bfold_i(nfeas, OpAddI{}, 0);
     bfold_i(minidx, OpMinI{}, 1);
-    bfold_i(lign, OpAddI{}, 2);
-    bfold_i(has_val, OpOrI{}, 3);
-    bfold_i(has_zero, OpOrI{}, 4);
-#pragma unroll
-    for (int i = 0; i < kMaxSoft; i++) {
-      bfold_i(lpres[i], OpAddI{}, 5 + i);
-      bfold_i(lseen[i], OpOrI{}, 9 + i);
+    bfold_i((int32_t)max_t, OpMaxI32{}, 6);   // raw taint <= 255, raw node affinity <= 65535
+    bfold_i((int32_t)max_a, OpMaxI32{}, 7);
+    if (need_ign) bfold_i(lign, OpAddI{}, 2);
+    if (soft1) {
+      bfold_i(has_val, OpOrI{}, 3);
+      bfold_i(has_zero, OpOrI{}, 4);
+      bfold_l(mmin, OpMinL{}, 2);
+      bfold_l(mmax, OpMaxL{}, 3);
     }
-    bfold_l(max_t, OpMaxL{}, 0);
-    bfold_l(max_a, OpMaxL{}, 1);
-    bfold_l(mmin, OpMinL{}, 2);
-    bfold_l(mmax, OpMaxL{}, 3);
-    bfold_l(imin, OpMinL{}, 4);
-    bfold_l(imax, OpMaxL{}, 5);
+    if (need_se) {
+#pragma unroll
+      for (int i = 0; i < kMaxSoft; i++) {
+        if (i >= g.n_soft) break;
+        bfold_i(lpres[i], OpAddI{}, 8 + i);
+        bfold_i(lseen[i], OpOrI{}, 12 + i);
+      }
+    }
+    if (ipa_may_score) {
+      bfold_l(imin, OpMinL{}, 4);
+      bfold_l(imax, OpMaxL{}, 5);
+    }
     __syncthreads();
     if (tid == 0) {
       mine->nfeas = get_i(0, OpAddI{});
       mine->minidx = get_i(1, OpMinI{});
-      mine->n_ignored = get_i(2, OpAddI{});
-      mine->has_val = get_i(3, OpOrI{});
-      mine->has_zero = get_i(4, OpOrI{});
-      for (int i = 0; i < kMaxSoft; i++) {
-        mine->soft_present[i] = get_i(5 + i, OpAddI{});
-        mine->soft_seen[i] = get_i(9 + i, OpOrI{});
+      mine->max_t = get_i(6, OpMaxI32{});
+      mine->max_a = get_i(7, OpMaxI32{});
+      if (need_ign) mine->n_ignored = get_i(2, OpAddI{});
+      if (soft1) {
+        mine->has_val = get_i(3, OpOrI{});
+        mine->has_zero = get_i(4, OpOrI{});
+        mine->mmin = get_l(2, OpMinL{});
+        mine->mmax = get_l(3, OpMaxL{});
       }
-      mine->max_t = get_l(0, OpMaxL{});
-      mine->max_a = get_l(1, OpMaxL{});
-      mine->mmin = get_l(2, OpMinL{});
-      mine->mmax = get_l(3, OpMaxL{});
-      mine->imin = get_l(4, OpMinL{});
-      mine->imax = get_l(5, OpMaxL{});
+      if (need_se)
+        for (int i = 0; i < g.n_soft; i++) {
+          mine->soft_present[i] = get_i(8 + i, OpAddI{});
+          mine->soft_seen[i] = get_i(12 + i, OpOrI{});
+        }
+      if (ipa_may_score) {
+        mine->imin = get_l(4, OpMinL{});
+        mine->imax = get_l(5, OpMaxL{});
+      }
     }
     if (g.pts_score && ok)   // domains seen among feasible nodes (non-unique soft slots)
       for (int i = 0; i < g.n_soft; i++) {
@@ -671,41 +730,54 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
 
     // ---- phase 3: fold phase 2; sizes, normalisation, argmax --------------------
     {
-      int32_t f_n = 0, f_min = 0x7fffffff, f_ign = 0, f_hv = 0, f_hz = 0;
+      int32_t f_n = 0, f_min = 0x7fffffff, f_ign = 0, f_hv = 0, f_hz = 0, f_mt = 0, f_ma = 0;
       int32_t f_pr[kMaxSoft] = {0, 0, 0, 0}, f_se[kMaxSoft] = {0, 0, 0, 0};
-      long long f_mt = 0, f_ma = 0, f_mmin = BIG, f_mmax = -BIG - 1, f_imin = BIG, f_imax = -BIG - 1;
+      long long f_mmin = BIG, f_mmax = -BIG - 1, f_imin = BIG, f_imax = -BIG - 1;
       if (tid < G) {
         const CoopPart* q = a.parts + tid;
         f_n = ald(&q->nfeas);
         f_min = ald(&q->minidx);
-        f_ign = ald(&q->n_ignored);
-        f_hv = ald(&q->has_val);
-        f_hz = ald(&q->has_zero);
+        f_mt = (int32_t)ald(&q->max_t);
+        f_ma = (int32_t)ald(&q->max_a);
+        if (need_ign) f_ign = ald(&q->n_ignored);
+        if (soft1) {
+          f_hv = ald(&q->has_val);
+          f_hz = ald(&q->has_zero);
+          f_mmin = ald(&q->mmin);
+          f_mmax = ald(&q->mmax);
+        }
+        if (need_se)
 #pragma unroll
-        for (int i = 0; i < kMaxSoft; i++) { f_pr[i] = ald(&q->soft_present[i]); f_se[i] = ald(&q->soft_seen[i]); }
-        f_mt = ald(&q->max_t);
-        f_ma = ald(&q->max_a);
-        f_mmin = ald(&q->mmin);
-        f_mmax = ald(&q->mmax);
-        f_imin = ald(&q->imin);
-        f_imax = ald(&q->imax);
+          for (int i = 0; i < kMaxSoft; i++)
+            if (i < g.n_soft) { f_pr[i] = ald(&q->soft_present[i]); f_se[i] = ald(&q->soft_seen[i]); }
+        if (ipa_may_score) {
+          f_imin = ald(&q->imin);
+          f_imax = ald(&q->imax);
+        }
       }
       bfold_i(f_n, OpAddI{}, 0);
       bfold_i(f_min, OpMinI{}, 1);
-      bfold_i(f_ign, OpAddI{}, 2);
-      bfold_i(f_hv, OpOrI{}, 3);
-      bfold_i(f_hz, OpOrI{}, 4);
-#pragma unroll
-      for (int i = 0; i < kMaxSoft; i++) {
-        bfold_i(f_pr[i], OpAddI{}, 5 + i);
-        bfold_i(f_se[i], OpOrI{}, 9 + i);
+      bfold_i(f_mt, OpMaxI32{}, 6);
+      bfold_i(f_ma, OpMaxI32{}, 7);
+      if (need_ign) bfold_i(f_ign, OpAddI{}, 2);
+      if (soft1) {
+        bfold_i(f_hv, OpOrI{}, 3);
+        bfold_i(f_hz, OpOrI{}, 4);
+        bfold_l(f_mmin, OpMinL{}, 2);
+        bfold_l(f_mmax, OpMaxL{}, 3);
       }
-      bfold_l(f_mt, OpMaxL{}, 0);
-      bfold_l(f_ma, OpMaxL{}, 1);
-      bfold_l(f_mmin, OpMinL{}, 2);
-      bfold_l(f_mmax, OpMaxL{}, 3);
-      bfold_l(f_imin, OpMinL{}, 4);
-      bfold_l(f_imax, OpMaxL{}, 5);
+      if (need_se) {
+#pragma unroll
+        for (int i = 0; i < kMaxSoft; i++) {
+          if (i >= g.n_soft) break;
+          bfold_i(f_pr[i], OpAddI{}, 8 + i);
+          bfold_i(f_se[i], OpOrI{}, 12 + i);
+        }
+      }
+      if (ipa_may_score) {
+        bfold_l(f_imin, OpMinL{}, 4);
+        bfold_l(f_imax, OpMaxL{}, 5);
+      }
     }
     __syncthreads();
     const int gnfeas = get_i(0, OpAddI{});
@@ -713,20 +785,16 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const bool scored = ok && gnfeas >= 2;
     const bool do_pts = scored && g.pts_score;
     const bool do_ipa = scored && ipa_may_score;
-    const int64_t gmax_t = get_l(0, OpMaxL{}), gmax_a = get_l(1, OpMaxL{});
-    const long long gimin = get_l(4, OpMinL{}), gimax = get_l(5, OpMaxL{});
+    const int64_t gmax_t = get_i(6, OpMaxI32{}), gmax_a = get_i(7, OpMaxI32{});
+    const long long gimin = do_ipa ? get_l(4, OpMinL{}) : 0, gimax = do_ipa ? get_l(5, OpMaxL{}) : 0;
     long long pmin = BIG, pmax = 0;
     if (do_pts) {
       for (int i = 0; i < g.n_soft; i++) {
         const Slot& sl = s_t.soft[i];
         if (g.soft[6 * i + 5] || sl.unique) continue;
         const int bw = (sl.V + 31) / 32;
-        if (pmode) {   // (word, workgroup) pairs over the lanes, or-ed into this workgroup's own marks
-          for (int x = tid; x < bw * G; x += BLOCK) {
-            const int w = x / G, q = x - w * G;
-            const uint32_t y = (uint32_t)ald(a.phist + (size_t)q * kCoopPHist + sl.mark + w);
-            if (y) atomicOr((uint32_t*)&s_hist[sl.mark + w], y);
-          }
+        if (pmode) {   // or-ed into this workgroup's own marks
+          fold_words(sl.mark, bw, true);
         } else {
           for (int wd = tid; wd < bw; wd += BLOCK) s_hist[sl.mark + wd] = ald(&acc->hist[sl.mark + wd]);
         }
@@ -742,12 +810,12 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
       __syncthreads();
       if (tid == 0) {
-        const int n_ign = get_i(2, OpAddI{});
+        const int n_ign = need_ign ? get_i(2, OpAddI{}) : 0;
         for (int i = 0; i < g.n_soft; i++) {
           const Slot& sl = s_t.soft[i];
           int sz;
           if (g.soft[6 * i + 5]) sz = gnfeas - n_ign;
-          else if (sl.unique) sz = get_i(5 + i, OpAddI{}) + get_i(9 + i, OpOrI{});
+          else if (sl.unique) sz = get_i(8 + i, OpAddI{}) + get_i(12 + i, OpOrI{});
           else sz = s_size[i];
           s_t.soft_w[i] = c.log_table[sz + 2];   // topologyNormalizingWeight = math.Log(size + 2)
         }
@@ -806,10 +874,15 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         if (n >= N || ev[k].st != 0) continue;
         int64_t total = total_score(v, ev[k].part, ev[k].rt, ev[k].ra, gmax_t, gmax_a, err, nullptr, nullptr);
         if (do_pts) {   // PodTopologySpread.NormalizeScore
-          TopoCtx tn = tc;
-          tn.has_rec = true;
-          tn.rec = srk[k];
-          const int64_t x = pts_score_node(c, v, tn, n);
+          int64_t x;
+          if (soft1) {   // from the count kept since sweep A: no loads
+            x = pr[k] == 2 ? -1 : (pr[k] == 1 ? 0 : pts_soft1_score(g, s_t, pm[k]));
+          } else {
+            TopoCtx tn = tc;
+            tn.has_rec = true;
+            tn.rec = srk[k];
+            x = pts_score_node(c, v, tn, n);
+          }
           int64_t s;
           if (x < 0) s = 0;
           else if (pmax == 0) s = 100;
