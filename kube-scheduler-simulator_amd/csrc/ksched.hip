@@ -2467,21 +2467,46 @@ bool sweep_eligible(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first,
   return true;
 }
 
+// mode: 0 generic arithmetic, 1 fast (Fit/BA over {cpu, memory}), 2 fast with
+// one scalar Fit column (instantiated for the spill-free shapes only)
 template <int BLOCK, int KN, bool MULTI>
-void launch_sweep(const SweepArgs& s, int grid, bool fast, hipStream_t st) {
-  if (fast) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
+void launch_sweep(const SweepArgs& s, int grid, int mode, hipStream_t st) {
+  if (mode == 1) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
   else hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, false, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
+}
+template <int BLOCK, int KN, bool MULTI>
+void launch_sweep_ex(const SweepArgs& s, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, true>), dim3(grid), dim3(BLOCK), 0, st, s);
 }
 
 template <int BLOCK, int KN>
-int sweep_occupancy(ksg_ctx* ctx, bool fast, int* occ) {   // the MULTI instances
-  if (fast) HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ksg_sweep<BLOCK, KN, true, true>, BLOCK, 0));
-  else HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ksg_sweep<BLOCK, KN, false, true>, BLOCK, 0));
+int sweep_occupancy(ksg_ctx* ctx, int mode, int* occ) {   // the MULTI instances
+  const void* f = mode == 2 ? (const void*)ksg_sweep<BLOCK, KN, true, true, true>
+                  : mode == 1 ? (const void*)ksg_sweep<BLOCK, KN, true, true> : (const void*)ksg_sweep<BLOCK, KN, false, true>;
+  HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, f, BLOCK, 0));
   return KSG_OK;
 }
 
 // Host mirror of cm_prof().fast: Fit and BalancedAllocation both score exactly
 // {cpu, memory}, Fit with positive weights.
+// Host mirror of the sweep's extended fast form (SweepProf::ex): Fit over
+// {cpu, memory, one scalar column}, BalancedAllocation over {cpu, memory},
+// positive weights.
+bool profile_ex_fast(const ksg_profile& prof) {
+  if (prof.fit_n != 3 || prof.ba_n != 2) return false;
+  int nc = 0, nm = 0, nx = 0;
+  for (int i = 0; i < 3; i++) {
+    const int r = prof.fit_res[i];
+    nc += r == KSG_RES_CPU;
+    nm += r == KSG_RES_MEM;
+    nx += r >= 3;
+    if (prof.fit_w[i] <= 0) return false;
+  }
+  const int b0 = prof.ba_res[0], b1 = prof.ba_res[1];
+  return nc == 1 && nm == 1 && nx == 1 &&
+         ((b0 == KSG_RES_CPU && b1 == KSG_RES_MEM) || (b0 == KSG_RES_MEM && b1 == KSG_RES_CPU));
+}
+
 bool profile_cm_fast(const ksg_profile& prof) {
   if (prof.fit_n != 2 || prof.ba_n != 2) return false;
   auto cpumem = [](int a, int b) {
@@ -2495,8 +2520,13 @@ bool profile_cm_fast(const ksg_profile& prof) {
 // a.st (replica strides set); placements [R][count] on the device.
 int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, const ksg_profile* d_prof, int R,
               int first, int count, int32_t* d_pl, Tmp& tmp) {
-  bool fast = true;
-  for (int r = 0; r < R; r++) fast = fast && profile_cm_fast(profiles[r]);
+  bool fast = true, ex = false;
+  for (int r = 0; r < R; r++) {
+    const bool cm = profile_cm_fast(profiles[r]), exf = !cm && profile_ex_fast(profiles[r]);
+    fast = fast && (cm || exf);
+    ex = ex || exf;
+  }
+  const int mode = !fast ? 0 : (ex ? 2 : 1);
   const int N = ctx->c.N;
   constexpr int kBatch = 64;
   SweepArgs s{};
@@ -2526,8 +2556,8 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   int block = 1024, kn = 0;
   for (;;) {
     const int neff = (N + S - 1) / S;
-    const Shape* list = fast ? (S == 1 ? fast1 : fastm) : gen;
-    const int nl = fast && S == 1 ? 7 : 1;
+    const Shape* list = mode == 1 ? (S == 1 ? fast1 : fastm) : gen;
+    const int nl = mode == 1 && S == 1 ? 7 : 1;
     block = S > 1 || neff <= 16384 ? 256 : 1024;
     kn = 0;
     for (int i = 0; i < nl; i++)
@@ -2535,8 +2565,8 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     if (S == 1) break;
     int occ = 0, rc0 = 0;
     switch (block * 100 + kn) {
-      case 25608: rc0 = sweep_occupancy<256, 8>(ctx, fast, &occ); break;
-      default: rc0 = sweep_occupancy<256, 0>(ctx, fast, &occ); break;
+      case 25608: rc0 = sweep_occupancy<256, 8>(ctx, mode, &occ); break;
+      default: rc0 = sweep_occupancy<256, 0>(ctx, mode, &occ); break;
     }
     if (rc0) return rc0;
     if ((long long)R * S <= (long long)occ * cus) break;   // every workgroup of a group co-resident
@@ -2563,22 +2593,32 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)s.nb * N))) return rc;
     if (S > 1) HIPC(ctx, hipMemsetAsync(s.gbar, 0, sizeof(unsigned) * 16 * (size_t)R, ctx->stream));
     const int grid = R * S;
-    if (S > 1) {
-      switch (block * 100 + kn) {
-        case 25608: launch_sweep<256, 8, true>(s, grid, fast, ctx->stream); break;
-        default: launch_sweep<256, 0, true>(s, grid, fast, ctx->stream); break;
+    const int key = block * 100 + kn;
+    if (mode == 2) {
+      if (S > 1) {
+        if (key == 25608) launch_sweep_ex<256, 8, true>(s, grid, ctx->stream);
+        else launch_sweep_ex<256, 0, true>(s, grid, ctx->stream);
+      } else {
+        if (key == 25608) launch_sweep_ex<256, 8, false>(s, grid, ctx->stream);
+        else if (key == 25600) launch_sweep_ex<256, 0, false>(s, grid, ctx->stream);
+        else launch_sweep_ex<1024, 0, false>(s, grid, ctx->stream);
+      }
+    } else if (S > 1) {
+      switch (key) {
+        case 25608: launch_sweep<256, 8, true>(s, grid, mode, ctx->stream); break;
+        default: launch_sweep<256, 0, true>(s, grid, mode, ctx->stream); break;
       }
     } else {
-      switch (block * 100 + kn) {
-        case 25608: launch_sweep<256, 8, false>(s, grid, fast, ctx->stream); break;
-        case 25616: launch_sweep<256, 16, false>(s, grid, fast, ctx->stream); break;
-        case 25620: launch_sweep<256, 20, false>(s, grid, fast, ctx->stream); break;
-        case 25624: launch_sweep<256, 24, false>(s, grid, fast, ctx->stream); break;
-        case 25632: launch_sweep<256, 32, false>(s, grid, fast, ctx->stream); break;
-        case 51232: launch_sweep<512, 32, false>(s, grid, fast, ctx->stream); break;
-        case 102432: launch_sweep<1024, 32, false>(s, grid, fast, ctx->stream); break;
-        case 25600: launch_sweep<256, 0, false>(s, grid, fast, ctx->stream); break;
-        default: launch_sweep<1024, 0, false>(s, grid, fast, ctx->stream); break;
+      switch (key) {
+        case 25608: launch_sweep<256, 8, false>(s, grid, mode, ctx->stream); break;
+        case 25616: launch_sweep<256, 16, false>(s, grid, mode, ctx->stream); break;
+        case 25620: launch_sweep<256, 20, false>(s, grid, mode, ctx->stream); break;
+        case 25624: launch_sweep<256, 24, false>(s, grid, mode, ctx->stream); break;
+        case 25632: launch_sweep<256, 32, false>(s, grid, mode, ctx->stream); break;
+        case 51232: launch_sweep<512, 32, false>(s, grid, mode, ctx->stream); break;
+        case 102432: launch_sweep<1024, 32, false>(s, grid, mode, ctx->stream); break;
+        case 25600: launch_sweep<256, 0, false>(s, grid, mode, ctx->stream); break;
+        default: launch_sweep<1024, 0, false>(s, grid, mode, ctx->stream); break;
       }
     }
     if ((rc = tlaunched(ctx, KSG_K_SWEEP, (double)R * s.nb * N))) return rc;

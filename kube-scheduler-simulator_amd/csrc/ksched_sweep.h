@@ -125,9 +125,15 @@ __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
 // Replica-uniform facts of a profile for the sweep.
 struct SweepProf {
   bool f_unsched, f_nodename, f_taint, f_na, f_fit;   // filter enabled
-  CmProf cm;
+  CmProf cm;     // Fit over {cpu, memory} (+ ex), BalancedAllocation over {cpu, memory}
+  int ex;        // a third, scalar Fit column (config 5: amd.com/gpu), -1 if none
+  int64_t w_ex;
 };
 
+// The "fast" sweep arithmetic covers Fit over exactly {cpu, memory} or
+// {cpu, memory, one scalar column} with positive weights, and
+// BalancedAllocation over exactly {cpu, memory}; sweep_fast_profile() is the
+// host mirror.
 __device__ __forceinline__ SweepProf sweep_prof(const ksg_profile& prof) {
   SweepProf s{};
   for (int k = 0; k < prof.n_filter; k++) {
@@ -139,6 +145,16 @@ __device__ __forceinline__ SweepProf sweep_prof(const ksg_profile& prof) {
     s.f_fit |= pl == KSG_PL_NODE_RESOURCES_FIT;
   }
   s.cm = cm_prof(prof);
+  s.ex = -1;
+  s.w_ex = 0;
+  if (!s.cm.fast && prof.fit_n == 3) {
+    for (int i = 0; i < 3; i++) {
+      const int r = prof.fit_res[i];
+      if (r == KSG_RES_CPU) s.cm.wc = prof.fit_w[i];
+      else if (r == KSG_RES_MEM) s.cm.wm = prof.fit_w[i];
+      else { s.ex = r; s.w_ex = prof.fit_w[i]; }
+    }
+  }
   return s;
 }
 
@@ -146,6 +162,7 @@ __device__ __forceinline__ SweepProf sweep_prof(const ksg_profile& prof) {
 struct SweepPod {
   uint32_t fmask;      // static-record bits that reject
   bool fit_on;
+  bool ex_on;          // Fit scores the scalar column sp.ex (the pod requests it)
   uint32_t req_mask;   // resource columns the Fit filter checks
   int64_t w_fit, w_ba, w_img, w_t, w_a;
   uint32_t smask;
@@ -160,6 +177,7 @@ __device__ __forceinline__ SweepPod sweep_pod(const SweepProf& sp, const ksg_pro
             (on(sp.f_taint, KSG_PL_TAINT_TOLERATION) ? kSrTaint : 0u) |
             (on(sp.f_na, KSG_PL_NODE_AFFINITY) ? kSrNodeAff : 0u);
   q.fit_on = on(sp.f_fit, KSG_PL_NODE_RESOURCES_FIT);
+  q.ex_on = sp.ex >= 0 && p.req[sp.ex] > 0;   // alloc_req: a scalar the pod does not request is skipped
   uint32_t m = 0;
   for (int r = 0; r < R && r < KSG_MAX_RES; r++)
     if (p.req[r] > 0 && !(r >= 3 && ((prof.fit_ignored_res >> r) & 1u))) m |= 1u << r;
@@ -174,10 +192,13 @@ __device__ __forceinline__ SweepPod sweep_pod(const SweepProf& sp, const ksg_pro
   return q;
 }
 
-// Fit (cpu + memory) and BalancedAllocation (cpu + memory) scores from loaded
-// values: fit_score / ba_score restated without branches (cm_scores' arithmetic).
+// Fit (cpu + memory [+ ex]) and BalancedAllocation (cpu + memory) scores from
+// loaded values: fit_score / ba_score restated without branches (cm_scores'
+// arithmetic).  ex_on: Fit also scores the scalar column with allocatable ae,
+// requested re, pod request qx and weight w_ex.
 __device__ __forceinline__ void sweep_cm_scores(const CmProf& m, const ksg_pod& p, int64_t ac, int64_t am, int64_t rc,
-                                                int64_t rm, int64_t zc, int64_t zm, int64_t& fit, int64_t& ba) {
+                                                int64_t rm, int64_t zc, int64_t zm, bool ex_on, int64_t ae,
+                                                int64_t re, int64_t qx, int64_t w_ex, int64_t& fit, int64_t& ba) {
   const bool hc = ac > 0, hm = am > 0;
   const int64_t sac = hc ? ac : 1, sam = hm ? am : 1;
   const float ic = __builtin_amdgcn_rcpf((float)sac), im = __builtin_amdgcn_rcpf((float)sam);
@@ -191,12 +212,17 @@ __device__ __forceinline__ void sweep_cm_scores(const CmProf& m, const ksg_pod& 
     xm = (qm > am ? am : qm) * 100;
   }
   const int64_t sc = qdiv(xc, sac, ic), sm = qdiv(xm, sam, im);
-  const int64_t num = (hc ? sc * m.wc : 0) + (hm ? sm * m.wm : 0);
-  const int64_t ws = (hc ? m.wc : 0) + (hm ? m.wm : 0);
-  float iws = m.inv_wm;
-  iws = hc ? m.inv_wc : iws;
-  iws = hc && hm ? m.inv_ws : iws;
-  fit = ws == 0 ? 0 : qdiv(num, ws, iws);
+  int64_t num = (hc ? sc * m.wc : 0) + (hm ? sm * m.wm : 0);
+  int64_t ws = (hc ? m.wc : 0) + (hm ? m.wm : 0);
+  if (ex_on) {
+    const bool he = ae > 0;
+    const int64_t sae = he ? ae : 1, qe = re + qx;
+    const int64_t xe = m.least ? (qe > ae ? 0 : (ae - qe) * 100) : (qe > ae ? ae : qe) * 100;
+    const int64_t se = qdiv(xe, sae, __builtin_amdgcn_rcpf((float)sae));
+    num += he ? se * w_ex : 0;
+    ws += he ? w_ex : 0;
+  }
+  fit = ws == 0 ? 0 : qdiv(num, ws, __builtin_amdgcn_rcpf((float)ws));
   const double dac = (double)sac, dam = (double)sam;
   double fc = ddiv((double)(rc + p.req[KSG_RES_CPU]), dac);
   double fm = ddiv((double)(rm + p.req[KSG_RES_MEM]), dam);
@@ -222,10 +248,11 @@ struct SweepPart {
 // MULTI: S > 1 workgroups per replica (runtime stride S * BLOCK between a
 // lane's nodes); without it S == 1 and the stride is the constant BLOCK, which
 // keeps the node offsets in the load instructions' immediates.
-template <int BLOCK, int KN, bool FAST, bool MULTI>
+// EX (with FAST): some replica's Fit also scores one scalar column (SweepProf::ex).
+template <int BLOCK, int KN, bool FAST, bool MULTI, bool EX = false>
 __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) {   // 16 waves per CU
   constexpr int NW = BLOCK / 64;
-  constexpr int U = !FAST ? (KN == 0 ? 2 : 1) : (KN >= 20 ? 2 : 4);   // nodes whose loads are in flight together
+  constexpr int U = !FAST ? (KN == 0 ? 2 : 1) : (KN >= 20 || EX ? 2 : 4);   // nodes whose loads are in flight together
   __shared__ ksg_profile s_prof;
   __shared__ SweepPart s_part[2][NW];
   __shared__ uint64_t s_best[2][NW];
@@ -271,7 +298,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       return ok;
     };
     auto eval_fast = [&](int n, uint64_t sr, int64_t ac, int64_t am, int64_t rc, int64_t rm, int64_t zc, int64_t zm,
-                         int32_t pc, int32_t al) -> uint64_t {
+                         int32_t pc, int32_t al, int64_t ae, int64_t re) -> uint64_t {
       bool ok = (sr & q.fmask) == 0;
       if (q.fit_on) {
         ok = ok && pc + 1 <= al;
@@ -282,7 +309,8 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       }
       if (!ok) return 0;
       int64_t fs = 0, bs = 0;
-      sweep_cm_scores(sp.cm, p, ac, am, rc, rm, zc, zm, fs, bs);
+      sweep_cm_scores(sp.cm, p, ac, am, rc, rm, zc, zm, EX && q.ex_on, ae, re, EX ? p.req[EX ? sp.ex : 0] : 0,
+                      sp.w_ex, fs, bs);
       const int64_t rt = (sr >> 8) & 0xff, ra = (sr >> 16) & 0xffff, im = (sr >> 32) & 0xff;
       const int64_t part = im * q.w_img + ((q.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? fs * q.w_fit : 0) +
                            ((q.smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? bs * q.w_ba : 0);
@@ -312,7 +340,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
     auto group = [&](const int k0) {
       if constexpr (FAST) {
         uint64_t sr[U];
-        int64_t ac[U], am[U], rc[U], rm[U], zc[U], zm[U];
+        int64_t ac[U], am[U], rc[U], rm[U], zc[U], zm[U], ae[U], re[U];
         int32_t pc[U], al[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -327,12 +355,21 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
           zm[u] = nonzero[NN + nl];
           pc[u] = pod_count[nl];
           al[u] = c.allowed[nl];
+          ae[u] = 0;
+          re[u] = 0;
+          if constexpr (EX) {
+            if (q.ex_on) {
+              ae[u] = c.alloc[(size_t)sp.ex * NN + nl];
+              re[u] = requested[(size_t)sp.ex * NN + nl];
+            }
+          }
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const int n = tb + (k0 + u) * stride;
           uint64_t x = 0;
-          if (k0 + u < iters && n < N) x = eval_fast(n, sr[u], ac[u], am[u], rc[u], rm[u], zc[u], zm[u], pc[u], al[u]);
+          if (k0 + u < iters && n < N)
+            x = eval_fast(n, sr[u], ac[u], am[u], rc[u], rm[u], zc[u], zm[u], pc[u], al[u], ae[u], re[u]);
           account(n, x);
           if constexpr (KN > 0) {
             if (k0 + u < KN) recs[k0 + u < KR ? k0 + u : 0] = x;

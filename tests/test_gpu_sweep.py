@@ -66,6 +66,8 @@ CASES = [
                                         taints_per_node=16, images_per_node=20), None),
     ("c5-generic-6000-r3", lambda: G.config5(n_nodes=6000, n_pods=60, n_images=500, taint_vocab=256,
                                              taints_per_node=16, images_per_node=20), None),   # S = 2, generic
+    ("c5-ex-6000-r2", lambda: G.config5(n_nodes=6000, n_pods=80, n_images=500, taint_vocab=256,
+                                        taints_per_node=16, images_per_node=20), None),   # S = 2, cpu/mem/gpu Fit
     ("c1-default-r2", lambda: G.config1(n_nodes=100, n_pods=300), None),            # PTS/IPA: queue kernel
 ] + [(f"zoo-{s}-r4", (lambda s=s: __import__("zoo").zoo(s)), (lambda: _zoo_profiles(4))) for s in range(6)]
 
@@ -78,8 +80,11 @@ def test_sweep_matches_oracle(gpu, oracle, name, make, profs):
         plist = []
         for r in range(3 if name.startswith("c5") else 2):
             plugins = [(n, (w + r) if w else 0) for n, w in base.plugins]
+            ba = base.ba_resources
+            if name.startswith("c5") and r == 2:   # BalancedAllocation over three columns: generic arithmetic
+                ba = list(base.ba_resources) + [("amd.com/gpu", 1)]
             plist.append(P.Profile(plugins=plugins, fit_strategy=r % 2, fit_resources=base.fit_resources,
-                                   ba_resources=base.ba_resources))
+                                   ba_resources=ba))
     else:
         plist = profs()
     pf = [E.encode_profile(p, enc.cluster.res_names) for p in plist]
