@@ -247,6 +247,26 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
                      int32_t first, int32_t count, int32_t* placements,
                      ksg_replica_summary* summaries);
 int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out);
+
+/* ---- DefaultPreemption PostFilter (wrappedplugin.go:550-583 wraps it; the
+ * plugin itself is upstream v1.32 defaultpreemption/default_preemption.go,
+ * not vendored) ------------------------------------------------------------ */
+/* SelectVictimsOnNode for n_cand candidate nodes at once, on the current
+ * node state.  Candidate k is node cand_node[k]; its potential victims (the
+ * pods on it with lower priority than `pod`, most important first:
+ * util.MoreImportantPod order) are vic_pod[vic_off[k] .. vic_off[k+1]).
+ * Per candidate: remove every potential victim, run NodeResourcesFit for
+ * `pod` (fits[k] = 0: the node cannot help), then reprieve the victims in
+ * order, each staying evicted (victim[i] = 1) only if `pod` no longer fits
+ * with it back.  The caller (framework.DebuggableScheduler.preempt) limits
+ * preemption to preemptors whose other filters do not depend on the pods of
+ * the node, so NodeResourcesFit is the only filter the dry run re-runs. */
+int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int32_t n_cand,
+                        const int32_t* vic_off, const int32_t* vic_pod, int32_t* fits, uint8_t* victim);
+/* A victim's deletion: the inverse of ksg_commit (NodeInfo.RemovePod and the
+ * count tables), applied by DefaultPreemption's prepareCandidate. */
+int ksg_uncommit(ksg_ctx* ctx, int32_t pod, int32_t node);
+
 /* Restore the node state captured at the last ksg_load_nodes(). */
 int ksg_reset_state(ksg_ctx* ctx);
 /* Timing of the last ksg_run_queue / ksg_run_replicas kernel: milliseconds

@@ -245,3 +245,13 @@ def reflect(store: ResultStore, namespace: str, pod: str, pod_annotations: Dict[
     update_result_history(pod_annotations, m)
     store.DeleteData(namespace, pod)
     return True
+
+
+def merged_reflection(pod_annotations: Dict[str, str], result_set: Optional[Dict[str, str]]) -> Dict[str, str]:
+    """The pod's annotations after one more reflection of `result_set`
+    (storeAllResultToPodFunc), without touching the inputs."""
+    out = dict(pod_annotations)
+    if result_set:
+        out.update(result_set)
+        update_result_history(out, result_set)
+    return out

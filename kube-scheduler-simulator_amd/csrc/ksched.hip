@@ -2023,11 +2023,53 @@ __global__ __launch_bounds__(256) void ksg_replica_sums(const int64_t* requested
 }
 
 __global__ void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods, const int32_t* prog, int pod,
-                                  int node) {
+                                  int node, int sign) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const ksg_pod& p = pods[pod];
   commit_node(c, st.requested, st.nonzero, st.pod_count, st.cnt, st.tab, st.tmpl_total, p,
-              p.commit >= 0 ? prog + p.commit : nullptr, node);
+              p.commit >= 0 ? prog + p.commit : nullptr, node, sign);
+}
+
+// DefaultPreemption dry run (SelectVictimsOnNode), one lane per candidate
+// node: the lane takes the node's live columns, removes every potential
+// victim, checks NodeResourcesFit for the preemptor, then reprieves the
+// victims most important first.  Only the Fit columns change, so a lane
+// works in registers on one NodeCols; victims of a node are few, and the
+// pass is off the per-pod critical path (it runs for pods with no feasible
+// node only).
+__global__ __launch_bounds__(256) void ksg_preempt_kernel(DevCluster c, DevState st, const ksg_pod* pods, int pod,
+                                                          uint32_t ignored, int fit_on, const int32_t* cand,
+                                                          int n_cand, const int32_t* off, const int32_t* vic,
+                                                          int32_t* fits, uint8_t* victim) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_cand) return;
+  const int n = cand[k];
+  NodeCols L;
+  load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
+  const ksg_pod& p = pods[pod];
+  const int b = off[k], e = off[k + 1];
+  auto move = [&](const ksg_pod& v, int sign) {
+#pragma unroll
+    for (int r = 0; r < KSG_MAX_RES; r++)
+      if (r < c.R) L.req[r] += sign * v.req[r];
+    L.nz_cpu += sign * v.nz_cpu;
+    L.nz_mem += sign * v.nz_mem;
+    L.pod_count += sign;
+  };
+  for (int i = b; i < e; i++) move(pods[vic[i]], -1);
+  const bool ok = !fit_on || fit_filter(c, p, L, ignored) == 0;
+  fits[k] = ok ? 1 : 0;
+  for (int i = b; i < e; i++) {
+    uint8_t out = 0;
+    if (ok) {
+      move(pods[vic[i]], +1);
+      if (fit_on && fit_filter(c, p, L, ignored) != 0) {
+        move(pods[vic[i]], -1);
+        out = 1;
+      }
+    }
+    victim[i] = out;
+  }
 }
 
 }  // namespace
@@ -2069,6 +2111,9 @@ struct ksg_ctx {
   int32_t* d_pmax = nullptr;
   P1Stats* d_p1 = nullptr;
   uint64_t* d_top = nullptr;
+  // DefaultPreemption dry-run scratch (grow-only)
+  int32_t* d_pre = nullptr;
+  size_t pre_words = 0;
   // chip-wide topology path buffers (lazily allocated)
   CoopAcc* d_coop_acc = nullptr;
   unsigned* d_coop_flags = nullptr;   // [0] barrier counter, [4] timeout
@@ -2970,14 +3015,64 @@ int ksg_run_queue(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placement
   return run_internal(ctx, first, count, 1, placements, results, cap);
 }
 
-int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node) {
+static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (pod < 0 || pod >= ctx->n_pods || node < 0 || node >= ctx->c.N) return fail(ctx, KSG_E_INVALID, "commit range");
   HIPC(ctx, hipSetDevice(ctx->device));
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
-                     ctx->d_prog, pod, node);
+                     ctx->d_prog, pod, node, sign);
   HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  return KSG_OK;
+}
+
+int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node) { return commit_signed(ctx, pod, node, 1); }
+
+int ksg_uncommit(ksg_ctx* ctx, int32_t pod, int32_t node) { return commit_signed(ctx, pod, node, -1); }
+
+int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int32_t n_cand, const int32_t* vic_off,
+                        const int32_t* vic_pod, int32_t* fits, uint8_t* victim) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (pod < 0 || pod >= ctx->n_pods || n_cand < 0 || (n_cand > 0 && (!cand_node || !vic_off || !fits)))
+    return fail(ctx, KSG_E_INVALID, "preempt arguments");
+  if (n_cand == 0) return KSG_OK;
+  const int32_t nv = vic_off[n_cand];
+  if (vic_off[0] != 0 || nv < 0 || (nv > 0 && (!vic_pod || !victim)))
+    return fail(ctx, KSG_E_INVALID, "preempt victim lists");
+  // host-side checks of every index the kernel dereferences
+  for (int k = 0; k < n_cand; k++) {
+    if (cand_node[k] < 0 || cand_node[k] >= ctx->c.N) return fail(ctx, KSG_E_INVALID, "preempt candidate node");
+    if (vic_off[k + 1] < vic_off[k]) return fail(ctx, KSG_E_INVALID, "preempt offsets not ascending");
+  }
+  for (int i = 0; i < nv; i++)
+    if (vic_pod[i] < 0 || vic_pod[i] >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "preempt victim pod");
+  const ksg_pod& p = ctx->h_pods[pod];
+  bool fit_on = false;
+  for (int kf = 0; kf < ctx->prof.n_filter; kf++) fit_on |= ctx->prof.filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
+  fit_on = fit_on && !((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u);
+  // one scratch block: cand | off | vic | fits | victim
+  const size_t words = (size_t)n_cand + (n_cand + 1) + nv + n_cand + (nv + 3) / 4;
+  if (words > ctx->pre_words) {
+    if ((rc = dalloc(ctx, &ctx->d_pre, words))) return rc;
+    ctx->pre_words = words;
+  }
+  int32_t* d_cand = ctx->d_pre;
+  int32_t* d_off = d_cand + n_cand;
+  int32_t* d_vic = d_off + n_cand + 1;
+  int32_t* d_fits = d_vic + nv;
+  uint8_t* d_victim = reinterpret_cast<uint8_t*>(d_fits + n_cand);
+  HIPC(ctx, hipSetDevice(ctx->device));
+  HIPC(ctx, hipMemcpyAsync(d_cand, cand_node, sizeof(int32_t) * n_cand, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(ctx, hipMemcpyAsync(d_off, vic_off, sizeof(int32_t) * (n_cand + 1), hipMemcpyHostToDevice, ctx->stream));
+  if (nv) HIPC(ctx, hipMemcpyAsync(d_vic, vic_pod, sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(ksg_preempt_kernel, dim3((n_cand + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
+                     ctx->d_pods, pod, ctx->prof.fit_ignored_res, fit_on ? 1 : 0, d_cand, n_cand, d_off, d_vic,
+                     d_fits, d_victim);
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipMemcpyAsync(fits, d_fits, sizeof(int32_t) * n_cand, hipMemcpyDeviceToHost, ctx->stream));
+  if (nv) HIPC(ctx, hipMemcpyAsync(victim, d_victim, nv, hipMemcpyDeviceToHost, ctx->stream));
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
   return KSG_OK;
 }

@@ -562,18 +562,20 @@ __device__ __forceinline__ void ipa_skip_bits(const ksg_profile& prof, const ksg
 
 // NodeInfo.AddPod restricted to the columns the plugins read, plus the
 // PodTopologySpread / InterPodAffinity count tables.
+// sign = +1: assume (NodeInfo.AddPod); sign = -1: a preemption victim's
+// deletion (NodeInfo.RemovePod), the exact inverse.
 __device__ void commit_node(const DevCluster& c, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
                             int32_t* cnt, int32_t* tab, int32_t* tmpl_total, const ksg_pod& p,
-                            const int32_t* commit_prog, int n) {
+                            const int32_t* commit_prog, int n, int sign = 1) {
   const int N = c.N;
-  for (int r = 0; r < c.R; r++) requested[(size_t)r * N + n] += p.req[r];
-  nonzero[n] += p.nz_cpu;
-  nonzero[(size_t)N + n] += p.nz_mem;
-  pod_count[n] += 1;
+  for (int r = 0; r < c.R; r++) requested[(size_t)r * N + n] += sign * p.req[r];
+  nonzero[n] += sign * p.nz_cpu;
+  nonzero[(size_t)N + n] += sign * p.nz_mem;
+  pod_count[n] += sign;
   if (commit_prog) {
     const int32_t* w = commit_prog;
     const int ns = *w++;
-    for (int i = 0; i < ns; i++) cnt[(size_t)w[i] * N + n] += 1;
+    for (int i = 0; i < ns; i++) cnt[(size_t)w[i] * N + n] += sign;
     w += ns;
     const int nt = *w++;
     for (int i = 0; i < nt; i++) {
@@ -581,8 +583,8 @@ __device__ void commit_node(const DevCluster& c, int64_t* requested, int64_t* no
       const int col = c.tmpl_col[t];
       const uint32_t val = c.label_val[(size_t)col * N + n];
       if (!val) continue;
-      tab[c.tmpl_off[t] + val] += c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1;
-      tmpl_total[t] += 1;
+      tab[c.tmpl_off[t] + val] += sign * (c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1);
+      tmpl_total[t] += sign;
     }
   }
 }

@@ -30,6 +30,7 @@ from . import annotations as A
 from . import encoder as E
 from . import model as m
 from . import native
+from . import preemption as PR
 from . import profile as P
 
 FS_NOT_EVALUATED = E.FS_NOT_EVALUATED
@@ -116,8 +117,17 @@ class DebuggableScheduler:
         self.enc = E.Encoder(self.nodes, self.pods, prof)
         self.engine = engine if engine is not None else native.Engine()
         self.engine.load(self.enc, E.encode_profile(prof, self.enc.cluster.res_names))
+        # NodeInfo.Pods per node (pod indices): DefaultPreemption's victims
+        self.on_node: List[List[int]] = [[] for _ in self.nodes]
         for pi, ni in bound:
             self.engine.commit(pi, ni)
+            self.on_node[ni].append(pi)
+        self.preemption_on = "DefaultPreemption" in {n for n, _ in prof.plugins}
+        # (preemptor, nominated node, victims) per preemption, in order
+        self.preemptions: List[tuple] = []
+        # annotations of a preemptor's first attempt, reflected onto the pod
+        # (storereflector) before its retry is recorded
+        self.reflected: Dict[int, Dict[str, str]] = {}
         self.store = A.ResultStore(prof.weights())
         self.decoder = Decoder(self.enc)
         self.node_names = self.enc.cluster.node_names
@@ -140,19 +150,104 @@ class DebuggableScheduler:
                         cap.norm[0], cap.total[0])
 
     def schedule_one(self, pi: int, record: bool = True) -> int:
+        return self._cycle(pi, record).selected
+
+    def _cycle(self, pi: int, record: bool) -> PodCycle:
         cyc = self.evaluate(pi)
+        nominated, victims = -1, []
+        if cyc.n_feasible == 0 and self.preemption_on:
+            nominated, victims = self.preempt(pi, cyc)
         if record:
-            self.record(cyc)
+            self.record(cyc, nominated)
+        if nominated >= 0:
+            # prepareCandidate: delete the victims; then the retry (module
+            # docstring of preemption.py, step 6)
+            for v in victims:
+                self.engine.uncommit(v, nominated)
+                self.on_node[nominated].remove(v)
+            self.preemptions.append((pi, nominated, list(victims)))
+            if record:
+                pod = self.pods[pi]
+                self.reflected[pi] = {}
+                A.reflect(self.store, pod.namespace, pod.name, self.reflected[pi])
+            cyc = self.evaluate(pi)
+            if int(cyc.fstatus[nominated]) == 0:   # evaluateNominatedNode: the only feasible node
+                only = np.full_like(cyc.fstatus, FS_NOT_EVALUATED)
+                only[nominated] = 0
+                cyc = PodCycle(pi, nominated, 1, cyc.status & ~native.ST_SCORED, cyc.score_skip, only,
+                               cyc.raw, cyc.norm, cyc.total)
+            if record:
+                self.record(cyc)
         if cyc.selected >= 0:
             self.engine.commit(pi, cyc.selected)
-        return cyc.selected
+            self.on_node[cyc.selected].append(pi)
+        return cyc
+
+    def preempt(self, pi: int, cyc: PodCycle):
+        """DefaultPreemption.PostFilter for a pod with no feasible node:
+        returns (nominated node or -1, victims most important first).  The
+        dry run over the candidate nodes is ksg_preempt_victims."""
+        pod = self.pods[pi]
+        if pod.preemption_policy == "Never":              # PodEligibleToPreemptOthers
+            return -1, []
+        potential = PR.potential_nodes(cyc.fstatus)
+        if not potential:
+            return -1, []
+        # nodes without a lower-priority pod fail SelectVictimsOnNode at once
+        lists = []
+        for n in potential:
+            low = [q for q in self.on_node[n] if self.pods[q].priority < pod.priority]
+            if low:
+                lists.append((n, sorted(low, key=lambda q: PR.importance_key(self.pods[q]))))
+        if not lists:
+            return -1, []
+        PR.check_scope(self.prof, pod, self.pods)
+        off = np.zeros(len(lists) + 1, np.int32)
+        off[1:] = np.cumsum([len(v) for _, v in lists])
+        vic = np.array([q for _, v in lists for q in v], np.int32)
+        fits, flags = self.engine.preempt_victims(pi, [n for n, _ in lists], off, vic)
+        # DryRunPreemption from offset 0: the first num_candidates candidates in node order
+        want = PR.num_candidates(len(potential), self.prof)
+        cands = []
+        for k, (n, v) in enumerate(lists):
+            chosen = [int(q) for q, f in zip(v, flags[off[k]:off[k + 1]]) if f]
+            if fits[k] and chosen:
+                cands.append((n, chosen))
+                if len(cands) >= want:
+                    break
+        if not cands:
+            return -1, []
+        node = PR.pick_one_node([(n, [self.pods[q] for q in v], 0) for n, v in cands])
+        return node, dict(cands)[node]
 
     def run_queue(self, first: int, count: int):
-        """Device-resident queue: no per-pod host round trip."""
-        return self.engine.run_queue(first, count)
+        """Device-resident queue: no per-pod host round trip.  With
+        DefaultPreemption enabled, the pods that could find a victim (those
+        of higher priority than some pod already placed or placed before
+        them) run as single cycles first; the rest go to ksg_run_queue."""
+        head = 0
+        if self.preemption_on:
+            low = min((self.pods[q].priority for v in self.on_node for q in v), default=None)
+            for k in range(count):
+                pod = self.pods[first + k]
+                if PR.may_preempt(pod, low):
+                    head = k + 1
+                low = pod.priority if low is None else min(low, pod.priority)
+        pl = np.zeros(count, np.int32)
+        res = np.zeros(count, native.RESULT_DTYPE)
+        for k in range(head):
+            cyc = self._cycle(first + k, record=False)
+            pl[k] = cyc.selected
+            res[k] = (cyc.selected, cyc.n_feasible, cyc.status, cyc.score_skip)
+        if head < count:
+            pl[head:], res[head:] = self.engine.run_queue(first + head, count - head)
+            for k in range(head, count):
+                if pl[k] >= 0:
+                    self.on_node[pl[k]].append(first + k)
+        return pl, res
 
     # ---- recording (what the wrapped plugins write to the Store) ---------
-    def record(self, cyc: PodCycle):
+    def record(self, cyc: PodCycle, nominated: int = -1):
         pod = self.pods[cyc.pod]
         rec = self.enc.workload.pods[cyc.pod]
         ns, name = pod.namespace, pod.name
@@ -175,7 +270,7 @@ class DebuggableScheduler:
         # Filter
         order = [p for p in self.prof.filter_order() if not (fskip >> p) & 1]
         if self.annotator is not None:
-            return self._record_native(cyc, ns, name, order)
+            return self._record_native(cyc, ns, name, order, nominated)
         evaluated = []
         for n in range(len(self.nodes)):
             s = int(cyc.fstatus[n])
@@ -194,8 +289,8 @@ class DebuggableScheduler:
             # pod at equal priority there is never a victim, so nothing is
             # nominated and every explicitly evaluated node gets an empty entry.
             if "DefaultPreemption" in self.names_enabled:
-                st.AddPostFilterResult(ns, name, "", "DefaultPreemption",
-                                       [self.node_names[n] for n in evaluated])
+                st.AddPostFilterResult(ns, name, self.node_names[nominated] if nominated >= 0 else "",
+                                       "DefaultPreemption", [self.node_names[n] for n in evaluated])
             return
         if cyc.n_feasible >= 2:
             sskip = cyc.score_skip
@@ -213,7 +308,7 @@ class DebuggableScheduler:
                         st.AddNormalizedScoreResult(ns, name, self.node_names[n], pname, int(cyc.norm[pid, n]))
         self._record_bind(cyc, ns, name)
 
-    def _record_native(self, cyc: PodCycle, ns: str, name: str, order: List[int]):
+    def _record_native(self, cyc: PodCycle, ns: str, name: str, order: List[int], nominated: int = -1):
         """Filter/Score/NormalizeScore entries serialised in one native call."""
         st = self.store
         score_order: List[int] = []
@@ -227,7 +322,8 @@ class DebuggableScheduler:
         if cyc.n_feasible == 0:
             if "DefaultPreemption" in self.names_enabled:
                 evaluated = np.nonzero(cyc.fstatus != FS_NOT_EVALUATED)[0]
-                st.AddPostFilterResult(ns, name, "", "DefaultPreemption", [self.node_names[n] for n in evaluated])
+                st.AddPostFilterResult(ns, name, self.node_names[nominated] if nominated >= 0 else "",
+                                       "DefaultPreemption", [self.node_names[n] for n in evaluated])
             return
         if cyc.n_feasible >= 2:
             for pid in self.prof.prescore_order():
@@ -247,8 +343,14 @@ class DebuggableScheduler:
             st.AddBindResult(ns, name, "DefaultBinder", A.SUCCESS)
 
     def annotations(self, pi: int) -> Optional[Dict[str, str]]:
+        """The stored result of the pod's cycle.  A preemptor has two: the
+        first attempt is already reflected onto the pod; the retry is merged
+        over it as the reflector's next pass would (with result-history)."""
         pod = self.pods[pi]
-        return self.store.GetStoredResult(pod.namespace, pod.name)
+        cur = self.store.GetStoredResult(pod.namespace, pod.name)
+        if pi not in self.reflected:
+            return cur
+        return A.merged_reflection(self.reflected[pi], cur)
 
 
 class Status:

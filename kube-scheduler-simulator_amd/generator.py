@@ -212,3 +212,57 @@ def readme_kat() -> Tuple[List[m.Node], List[m.Pod], P.Profile]:
     pod = m.Pod(name="hoge-pod", containers=[m.Container(
         image="registry.k8s.io/pause:3.5", requests={m.CPU: 100, m.MEMORY: 16 * GI})])
     return nodes, [pod], P.default_profile()
+
+
+def preemption_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, seed: int = 7):
+    """A cluster filled with lower-priority running pods and a queue of
+    higher-priority pods that only fit by preemption (DefaultPreemption
+    parity cases).  Small nodes (4-8 cores, 8-16 GiB, 6-12 pods) so that
+    both "Insufficient" and "Too many pods" rejections are preemptable; 10 %
+    of nodes NoSchedule-tainted (unresolvable, never candidates); 5 %
+    of queued pods preemptionPolicy Never; running pods' start times spread
+    over an hour, some unset.  Returns (nodes, pods, bound [(pod, node)],
+    profile); pods = running pods, then the queue in PrioritySort order."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = []
+    for i in range(n_nodes):
+        nd = _node(i, rng, 4)
+        nd.allocatable[m.CPU] = int(rng.choice([4, 6, 8])) * 1000
+        nd.allocatable[m.MEMORY] = int(rng.choice([8, 12, 16])) * GI
+        nd.allocatable[m.PODS] = int(rng.integers(6, 13))
+        if rng.random() < 0.10:
+            nd.taints = [m.Taint("dedicated", "infra", m.NO_SCHEDULE)]
+        nodes.append(nd)
+    t0 = 1_700_000_000 * 10 ** 9
+    pods, bound = [], []
+    free = [[nd.allocatable[m.CPU], nd.allocatable[m.MEMORY], nd.allocatable[m.PODS]] for nd in nodes]
+    for j in range(n_bound):
+        p = m.Pod(name=f"run-{j:05d}", containers=[m.Container(
+            image="registry.k8s.io/pause:3.10",
+            requests={m.CPU: int(rng.choice([250, 500, 1000, 1500])), m.MEMORY: int(rng.choice([1, 2, 3])) * GI})])
+        p.priority = int(rng.choice([0, 10, 10, 100, 500]))
+        p.start_time = None if rng.random() < 0.15 else t0 + int(rng.integers(0, 3600)) * 10 ** 9
+        ok = [i for i in range(n_nodes) if not nodes[i].taints and free[i][0] >= p.containers[0].requests[m.CPU]
+              and free[i][1] >= p.containers[0].requests[m.MEMORY] and free[i][2] >= 1]
+        if not ok:
+            continue
+        i = ok[int(rng.integers(len(ok)))]
+        free[i][0] -= p.containers[0].requests[m.CPU]
+        free[i][1] -= p.containers[0].requests[m.MEMORY]
+        free[i][2] -= 1
+        p.node_name = nodes[i].name
+        bound.append((len(pods), i))
+        pods.append(p)
+    queue = []
+    for j in range(n_queue):
+        p = _pod(j, rng, best_effort_frac=0.05)
+        if p.containers[0].requests:
+            p.containers[0].requests[m.CPU] = int(rng.choice([500, 1000, 2000, 3000]))
+            p.containers[0].requests[m.MEMORY] = int(rng.choice([1, 2, 4, 6])) * GI
+        p.priority = int(rng.choice([0, 10, 50, 200, 200, 1000]))
+        if rng.random() < 0.05:
+            p.preemption_policy = "Never"
+        queue.append(p)
+    queue.sort(key=lambda p: -p.priority)     # PrioritySort (stable: creation order within a priority)
+    pods.extend(queue)
+    return nodes, pods, bound, P.default_profile()

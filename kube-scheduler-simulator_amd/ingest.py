@@ -228,6 +228,34 @@ def pod_priority(obj: dict, classes: Dict[str, int], global_default: int) -> int
     return global_default
 
 
+def pod_preemption_policy(obj: dict, class_policy: Dict[str, str]) -> str:
+    """spec.preemptionPolicy, else the one the Priority admission plugin
+    copies from the pod's PriorityClass, else PreemptLowerPriority."""
+    spec = obj.get("spec") or {}
+    if spec.get("preemptionPolicy"):
+        return spec["preemptionPolicy"]
+    return class_policy.get(spec.get("priorityClassName") or "", "PreemptLowerPriority")
+
+
+def rfc3339_ns(ts: Optional[str]) -> Optional[int]:
+    """metav1.Time (RFC 3339, optional fraction) -> Unix nanoseconds."""
+    if not ts:
+        return None
+    import datetime
+    t = ts.strip().replace("z", "Z")
+    frac = 0
+    if "." in t:
+        head, rest = t.split(".", 1)
+        k = 0
+        while k < len(rest) and rest[k].isdigit():
+            k += 1
+        digits, tz = rest[:k], rest[k:]
+        frac = int((digits + "000000000")[:9]) if digits else 0
+        t = head + tz
+    dt = datetime.datetime.fromisoformat(t.replace("Z", "+00:00"))
+    return int(dt.timestamp()) * 1_000_000_000 + frac
+
+
 # ---------------------------------------------------------------------------
 # scheduler configuration -> Profile
 # ---------------------------------------------------------------------------
@@ -296,6 +324,9 @@ def profile_from_config(cfg: Optional[dict]) -> Tuple[P.Profile, Optional[int]]:
             if "hardPodAffinityWeight" in args:
                 prof.hard_pod_affinity_weight = int(args["hardPodAffinityWeight"])
             prof.ignore_preferred_terms_of_existing_pods = bool(args.get("ignorePreferredTermsOfExistingPods", False))
+        elif name == "DefaultPreemption":
+            prof.preemption_min_candidate_pct = int(args.get("minCandidateNodesPercentage", 10))
+            prof.preemption_min_candidate_abs = int(args.get("minCandidateNodesAbsolute", 100))
         elif name == "PodTopologySpread":
             dt = args.get("defaultingType", "System")
             if dt == "System":
@@ -326,9 +357,11 @@ def load_snapshot(doc, n_nodes_check: bool = True) -> Snapshot:
         doc = json.loads(doc)
     ns_labels = {(n.get("metadata") or {}).get("name"): dict((n.get("metadata") or {}).get("labels") or {})
                  for n in doc.get("namespaces") or ()}
-    classes, global_default = {}, 0
+    classes, global_default, class_policy = {}, 0, {}
     for pc in doc.get("priorityClasses") or ():
         classes[pc["metadata"]["name"]] = int(pc.get("value", 0))
+        if pc.get("preemptionPolicy"):
+            class_policy[pc["metadata"]["name"]] = pc["preemptionPolicy"]
         if pc.get("globalDefault"):
             global_default = int(pc.get("value", 0))
     nodes = [node_from_k8s(n) for n in doc.get("nodes") or ()]
@@ -350,6 +383,10 @@ def load_snapshot(doc, n_nodes_check: bool = True) -> Snapshot:
     queue_objs.sort(key=lambda t: t[:3])
     pods = [pod_from_k8s(o, ns_labels or None) for o in bound_objs] + \
            [pod_from_k8s(t[3], ns_labels or None) for t in queue_objs]
+    for p, o in zip(pods, bound_objs + [t[3] for t in queue_objs]):
+        p.priority = pod_priority(o, classes, global_default)
+        p.preemption_policy = pod_preemption_policy(o, class_policy)
+        p.start_time = rfc3339_ns((o.get("status") or {}).get("startTime"))
     bound = [(i, index[pods[i].node_name]) for i in range(len(bound_objs))]
     queue = list(range(len(bound_objs), len(pods)))
     prof, pct = profile_from_config(doc.get("schedulerConfig"))
@@ -504,10 +541,24 @@ def pod_to_k8s(p: m.Pod) -> dict:
                 d["matchLabelKeys"] = list(c.match_label_keys)
             cs.append(d)
         spec["topologySpreadConstraints"] = cs
+    if p.priority:
+        spec["priority"] = p.priority
+    if p.preemption_policy != "PreemptLowerPriority":
+        spec["preemptionPolicy"] = p.preemption_policy
     meta = {"name": p.name, "namespace": p.namespace, "labels": dict(p.labels)}
     if p.terminating:
         meta["deletionTimestamp"] = "2024-01-01T00:00:00Z"
-    return {"kind": "Pod", "apiVersion": "v1", "metadata": meta, "spec": spec}
+    out = {"kind": "Pod", "apiVersion": "v1", "metadata": meta, "spec": spec}
+    if p.start_time is not None:
+        out["status"] = {"startTime": ns_rfc3339(p.start_time)}
+    return out
+
+
+def ns_rfc3339(ns: int) -> str:
+    import datetime
+    sec, frac = divmod(int(ns), 1_000_000_000)
+    t = datetime.datetime.fromtimestamp(sec, datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%S")
+    return t + (f".{frac:09d}".rstrip("0") if frac else "") + "Z"
 
 
 def profile_to_config(prof: P.Profile) -> dict:

@@ -188,6 +188,13 @@ class Pod:
     # default constraints).  None = no such owner/service.
     default_spread_selector: Optional[LabelSelector] = None
     terminating: bool = False
+    # DefaultPreemption inputs: corev1helpers.PodPriority (spec.priority, 0
+    # when unset), spec.preemptionPolicy ("Never" or "PreemptLowerPriority")
+    # and status.startTime in Unix ns (None: not started, util.GetPodStartTime
+    # then answers "now", later than every recorded start).
+    priority: int = 0
+    preemption_policy: str = "PreemptLowerPriority"
+    start_time: Optional[int] = None
 
     def has_pod_affinity(self) -> bool:
         return bool(self.pod_affinity_required or self.pod_affinity_preferred

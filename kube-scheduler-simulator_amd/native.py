@@ -208,6 +208,9 @@ class Engine:
         self._run_queue = f("run_queue", C.c_int, vp, C.c_int32, C.c_int32, i32p, vp, C.POINTER(KsgCapture))
         self._read_state = f("read_state", C.c_int, vp, C.POINTER(KsgNodeState))
         self._reset_state = f("reset_state", C.c_int, vp)
+        self._uncommit = f("uncommit", C.c_int, vp, C.c_int32, C.c_int32)
+        self._preempt = f("preempt_victims", C.c_int, vp, C.c_int32, i32p, C.c_int32, i32p, i32p, i32p,
+                          C.POINTER(C.c_uint8))
         self._declare_extra(f)
 
     def _declare_extra(self, f):
@@ -259,6 +262,24 @@ class Engine:
 
     def commit(self, pod: int, node: int):
         self._check(self._commit(self.ctx, pod, node))
+
+    def uncommit(self, pod: int, node: int):
+        """A preemption victim's deletion (ksg_uncommit: NodeInfo.RemovePod)."""
+        self._check(self._uncommit(self.ctx, pod, node))
+
+    def preempt_victims(self, pod: int, cand_nodes, vic_off, vic_pod):
+        """SelectVictimsOnNode for every candidate node (ksg_preempt_victims).
+        Returns (fits[n_cand] bool, victim[len(vic_pod)] bool)."""
+        cand = np.ascontiguousarray(cand_nodes, np.int32)
+        off = np.ascontiguousarray(vic_off, np.int32)
+        vic = np.ascontiguousarray(vic_pod, np.int32)
+        if len(off) != len(cand) + 1:
+            raise ValueError("vic_off needs n_cand + 1 entries")
+        fits = np.zeros(len(cand), np.int32)
+        victim = np.zeros(max(len(vic), 1), np.uint8)
+        self._check(self._preempt(self.ctx, pod, _ptr(cand, i32p), len(cand), _ptr(off, i32p), _ptr(vic, i32p),
+                                  _ptr(fits, i32p), victim.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return fits.astype(bool), victim[:len(vic)].astype(bool)
 
     def run_queue(self, first: int, count: int, capture: Optional[CaptureBuffers] = None,
                   results: bool = True):

@@ -96,6 +96,10 @@ class Profile:
     # BalancedAllocation PreScore Skip for best-effort pods [upstream; believed
     # to land after v1.32 — TO VERIFY, SURVEY.md Appendix A.2]
     ba_skip_best_effort: bool = False
+    # DefaultPreemptionArgs (v1 defaults): candidate count =
+    # max(potential nodes * pct / 100, abs), at most the potential nodes
+    preemption_min_candidate_pct: int = 10
+    preemption_min_candidate_abs: int = 100
 
     # -- derived views ---------------------------------------------------
     def enabled_ids(self) -> List[int]:

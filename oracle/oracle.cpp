@@ -772,6 +772,52 @@ void commit(Ctx& c, int pi, int n) {
   c.pods_on[n].push_back(pi);
 }
 
+// NodeInfo.RemovePod for a preemption victim (the inverse of commit).
+void uncommit(Ctx& c, int pi, int n) {
+  const ksg_pod& p = c.pods[pi];
+  for (int r = 0; r < c.R; r++) c.requested[(size_t)r * c.N + n] -= p.req[r];
+  c.nonzero[n] -= p.nz_cpu;
+  c.nonzero[(size_t)c.N + n] -= p.nz_mem;
+  c.pod_count[n] -= 1;
+  auto& v = c.pods_on[n];
+  v.erase(std::find(v.begin(), v.end(), pi));
+}
+
+// defaultpreemption.SelectVictimsOnNode (upstream v1.32) with NodeResourcesFit
+// as the only pod-dependent filter: on a copy of the node (here: the node's
+// own columns, restored afterwards), remove every lower-priority pod, run the
+// filter, reprieve the pods most important first.
+void select_victims(Ctx& c, int pi, int n, const int32_t* vic, int nv, int32_t& fits, uint8_t* victim) {
+  const ksg_pod& p = c.pods[pi];
+  bool fit_on = false;
+  for (int k = 0; k < c.prof.n_filter; k++) fit_on |= c.prof.filter_order[k] == KSG_PL_NODE_RESOURCES_FIT;
+  fit_on = fit_on && !((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u);
+  std::vector<int64_t> save_req(c.R);
+  for (int r = 0; r < c.R; r++) save_req[r] = c.requested[(size_t)r * c.N + n];
+  const int32_t save_pc = c.pod_count[n];
+  auto remove = [&](int q) {
+    for (int r = 0; r < c.R; r++) c.requested[(size_t)r * c.N + n] -= c.pods[q].req[r];
+    c.pod_count[n] -= 1;
+  };
+  auto add = [&](int q) {
+    for (int r = 0; r < c.R; r++) c.requested[(size_t)r * c.N + n] += c.pods[q].req[r];
+    c.pod_count[n] += 1;
+  };
+  for (int i = 0; i < nv; i++) remove(vic[i]);
+  fits = (!fit_on || fit_filter(c, p, n) == 0) ? 1 : 0;
+  for (int i = 0; i < nv; i++) {
+    victim[i] = 0;
+    if (!fits) continue;
+    add(vic[i]);                                   // reprievePod
+    if (fit_on && fit_filter(c, p, n) != 0) {
+      remove(vic[i]);
+      victim[i] = 1;
+    }
+  }
+  for (int r = 0; r < c.R; r++) c.requested[(size_t)r * c.N + n] = save_req[r];
+  c.pod_count[n] = save_pc;
+}
+
 }  // namespace
 
 struct kso_ctx : Ctx {};
@@ -850,6 +896,26 @@ int kso_eval(kso_ctx* c, int32_t pod, ksg_result* res, ksg_capture* cap) {
 int kso_commit(kso_ctx* c, int32_t pod, int32_t node) {
   if (!c || pod < 0 || pod >= (int)c->pods.size() || node < 0 || node >= c->N) return KSG_E_INVALID;
   commit(*c, pod, node);
+  return KSG_OK;
+}
+
+int kso_uncommit(kso_ctx* c, int32_t pod, int32_t node) {
+  if (!c || pod < 0 || pod >= (int)c->pods.size() || node < 0 || node >= c->N) return KSG_E_INVALID;
+  auto& v = c->pods_on[node];
+  if (std::find(v.begin(), v.end(), pod) == v.end()) { c->err = "uncommit: pod not on node"; return KSG_E_INVALID; }
+  uncommit(*c, pod, node);
+  return KSG_OK;
+}
+
+int kso_preempt_victims(kso_ctx* c, int32_t pod, const int32_t* cand_node, int32_t n_cand, const int32_t* vic_off,
+                        const int32_t* vic_pod, int32_t* fits, uint8_t* victim) {
+  if (!c || !c->have_nodes || !c->have_wl || !c->have_prof) return KSG_E_STATE;
+  if (pod < 0 || pod >= (int)c->pods.size() || n_cand < 0) return KSG_E_INVALID;
+  for (int k = 0; k < n_cand; k++) {
+    const int n = cand_node[k];
+    if (n < 0 || n >= c->N) return KSG_E_INVALID;
+    select_victims(*c, pod, n, vic_pod + vic_off[k], vic_off[k + 1] - vic_off[k], fits[k], victim + vic_off[k]);
+  }
   return KSG_OK;
 }
 

@@ -173,6 +173,26 @@ class NodeInfo:
         self.nz_mem += nz.get(m.MEMORY, 0)
         self.pods.append(pod)
 
+    def remove_pod(self, pod: m.Pod):
+        """NodeInfo.RemovePod (update with sign -1)."""
+        req = m.pod_requests(pod)
+        nz = m.pod_requests(pod, non_zero=True)
+        for k, v in req.items():
+            if k in (m.CPU, m.MEMORY, m.EPHEMERAL) or m.is_scalar_resource(k):
+                self.requested[k] = self.requested.get(k, 0) - v
+        self.nz_cpu -= nz.get(m.CPU, 0)
+        self.nz_mem -= nz.get(m.MEMORY, 0)
+        self.pods = [p for p in self.pods if p is not pod]
+
+    def snapshot(self) -> "NodeInfo":
+        """NodeInfo.Snapshot: an independent copy."""
+        c = NodeInfo(self.node, list(self.requested))
+        c.requested = dict(self.requested)
+        c.nz_cpu, c.nz_mem = self.nz_cpu, self.nz_mem
+        c.image_states = self.image_states
+        c.pods = list(self.pods)
+        return c
+
     def used_ports(self):
         out = []
         for p in self.pods:
@@ -900,12 +920,129 @@ def schedule_one(pod: m.Pod, infos: List[NodeInfo], prof: P.Profile):
     return rec
 
 
+# ---------------------------------------------------------------- DefaultPreemption
+# Upstream v1.32 framework/preemption + plugins/defaultpreemption (not
+# vendored), restated on the object model; the deterministic choices (offset
+# 0, node-order candidates, lowest-index final tie, name order between equally
+# important pods, retry of the preemptor on its nominated node right away)
+# are the ones documented in kube-scheduler-simulator_amd/preemption.py.
+_NOW = 1 << 62
+
+
+def _filter_code(plugin: str, msg: str) -> str:
+    if plugin in ("NodeResourcesFit", "NodePorts"):
+        return "Unschedulable"
+    if plugin == "PodTopologySpread":
+        return "UnschedulableAndUnresolvable" if msg.endswith("(missing required label)") else "Unschedulable"
+    if plugin == "InterPodAffinity":
+        return ("UnschedulableAndUnresolvable" if msg == "node(s) didn't match pod affinity rules"
+                else "Unschedulable")
+    return "UnschedulableAndUnresolvable"
+
+
+def _more_important_first(pods):
+    return sorted(pods, key=lambda p: (-p.priority, p.start_time if p.start_time is not None else _NOW,
+                                       p.namespace, p.name))
+
+
+def _pick_one(cands):
+    """pickOneNodeForPreemption; cands = [(node index, victims)], no PDBs."""
+    def start(p):
+        return p.start_time if p.start_time is not None else _NOW
+
+    def earliest(vs):
+        top = max(v.priority for v in vs)
+        return min(start(v) for v in vs if v.priority == top)
+
+    keys = [lambda c: 0,
+            lambda c: -c[1][0].priority,
+            lambda c: -sum(v.priority + 2 ** 31 for v in c[1]),
+            lambda c: -len(c[1]),
+            lambda c: earliest(c[1])]
+    pool = sorted(cands, key=lambda c: c[0])
+    for k in keys:
+        hi = max(k(c) for c in pool)
+        pool = [c for c in pool if k(c) == hi]
+        if len(pool) == 1:
+            break
+    return pool[0]
+
+
+def preempt(pod, infos, prof: P.Profile, rec):
+    """DefaultPreemption.PostFilter -> (nominated node index or -1, victims)."""
+    if pod.preemption_policy == "Never":
+        return -1, []
+    potential = []
+    for idx, ni in enumerate(infos):
+        d = rec["filter"].get(ni.node.name)
+        if not d:
+            continue
+        bad = [(pl, msg) for pl, msg in d.items() if msg != "passed"]
+        if bad and _filter_code(*bad[0]) == "Unschedulable":
+            potential.append(idx)
+    if not potential:
+        return -1, []
+    want = min(max(len(potential) * prof.preemption_min_candidate_pct // 100, prof.preemption_min_candidate_abs),
+               len(potential))
+    _, states, skip, _, _ = pod_prefilter(pod, infos, prof)
+    cands = []
+    for idx in potential:
+        low = _more_important_first([q for q in infos[idx].pods if q.priority < pod.priority])
+        if not low:
+            continue      # "No preemption victims found for incoming pod"
+        trial = infos[idx].snapshot()
+        for q in low:
+            trial.remove_pod(q)
+        if not run_filters(pod, trial, prof, states, skip, len(infos))[1]:
+            continue
+        victims = []
+        for q in low:                              # reprievePod
+            trial.add_pod(q)
+            if not run_filters(pod, trial, prof, states, skip, len(infos))[1]:
+                trial.remove_pod(q)
+                victims.append(q)
+        if victims:
+            cands.append((idx, victims))
+            if len(cands) >= want:
+                break
+    if not cands:
+        return -1, []
+    return _pick_one(cands)
+
+
+def schedule_nominated(pod, infos, prof, nom):
+    """The preemptor's retry: evaluateNominatedNode, else a full cycle."""
+    st, states, skip, rejected, node_set = pod_prefilter(pod, infos, prof)
+    if not rejected:
+        res, ok = run_filters(pod, infos[nom], prof, states, skip, len(infos))
+        if ok:
+            rec = schedule_one(pod, infos, prof)     # same PreFilter records
+            rec.update({"filter": {infos[nom].node.name: dict(res)} if res else {}, "prescore": {}, "score": {},
+                        "finalscore": {}, "raw": {}, "norm": {}, "n_feasible": 1, "selected_index": nom,
+                        "selected": infos[nom].node.name})
+            rec.pop("total", None)
+            return rec
+    return schedule_one(pod, infos, prof)
+
+
 def run_queue(nodes, bound, queue, prof, capture=True):
-    """Schedules `queue` in order; unschedulable pods are attempted once."""
+    """Schedules `queue` in order; unschedulable pods are attempted once
+    (a preemptor is retried once, on its nominated node)."""
     infos = build_snapshot(nodes, bound)
+    preemption = any(n == "DefaultPreemption" for n, _ in prof.plugins)
     recs = []
     for pod in queue:
         rec = schedule_one(pod, infos, prof)
+        if rec["n_feasible"] == 0 and preemption:
+            nom, victims = preempt(pod, infos, prof, rec)
+            if nom >= 0:
+                rec["nominated"] = infos[nom].node.name
+                rec["victims"] = [(v.namespace, v.name) for v in victims]
+                for v in victims:
+                    infos[nom].remove_pod(v)
+                first = rec
+                rec = schedule_nominated(pod, infos, prof, nom)
+                rec["first_attempt"] = first
         if rec["selected_index"] >= 0:
             infos[rec["selected_index"]].add_pod(pod)
         recs.append(rec if capture else rec["selected_index"])

@@ -66,13 +66,15 @@ def scheduler_annotations(nodes, pods, prof, engine):
 
 
 def pyoracle_annotations(nodes, pods, prof, bound=()):
-    """`pods` = the queue; `bound` = [(pod, node name)] already running."""
+    """`pods` = the queue; `bound` = [(pod, node name)] already running.
+    A preemptor's first attempt is reflected onto the pod before its retry
+    is recorded (A.reflect / A.merged_reflection)."""
     import pyoracle
     store = A.ResultStore(prof.weights())
     recs = pyoracle.run_queue(nodes, list(bound), pods, prof)
     names = set(n for n, _ in prof.plugins)
-    for pod, r in zip(pods, recs):
-        ns, nm = pod.namespace, pod.name
+
+    def put(ns, nm, r):
         for pl, msg in r["prefilter_status"].items():
             store.AddPreFilterResult(ns, nm, pl, msg, r["prefilter_result"].get(pl))
         for node, d in r["filter"].items():
@@ -80,7 +82,7 @@ def pyoracle_annotations(nodes, pods, prof, bound=()):
                 store.AddFilterResult(ns, nm, node, pl, msg)
         if r["n_feasible"] == 0:
             if "DefaultPreemption" in names:
-                store.AddPostFilterResult(ns, nm, "", "DefaultPreemption", list(r["filter"].keys()))
+                store.AddPostFilterResult(ns, nm, r.get("nominated", ""), "DefaultPreemption", list(r["filter"].keys()))
         for pl, msg in r["prescore"].items():
             store.AddPreScoreResult(ns, nm, pl, msg)
         for node, d in r["score"].items():
@@ -98,4 +100,17 @@ def pyoracle_annotations(nodes, pods, prof, bound=()):
                 store.AddPreBindResult(ns, nm, "VolumeBinding", "success")
             if "DefaultBinder" in names:
                 store.AddBindResult(ns, nm, "DefaultBinder", "success")
-    return [store.GetStoredResult(p.namespace, p.name) for p in pods], recs
+
+    out = []
+    for pod, r in zip(pods, recs):
+        ns, nm = pod.namespace, pod.name
+        if "first_attempt" in r:
+            put(ns, nm, r["first_attempt"])
+            pod_ann = {}
+            A.reflect(store, ns, nm, pod_ann)
+            put(ns, nm, r)
+            out.append(A.merged_reflection(pod_ann, store.GetStoredResult(ns, nm)))
+        else:
+            put(ns, nm, r)
+            out.append(store.GetStoredResult(ns, nm))
+    return out, recs
