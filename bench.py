@@ -14,7 +14,10 @@ state the next pod reads), so N GPUs run N independent what-if replicas of the
 same queue (weak scaling, no data-path collective); value = pods scheduled by
 all ranks / max-over-ranks time.
 
-Prints ONE JSON line (rank 0).
+Prints ONE JSON line (rank 0).  At N=1 the line also carries
+`replica_sweep`: BASELINE configs[3] (1,024 what-if replicas of the first
+1,000 pods on the same cluster), the HBM-bound regime of the same path, with
+the roofline of its dominant kernel.
 """
 from __future__ import annotations
 
@@ -56,6 +59,32 @@ def cpu_baseline(enc, pf, n_threads: int, budget_s: float):
             "node_evals_per_sec": done * len(enc.cluster.node_names) / dt}
 
 
+def replica_sweep(eng, enc, prof, G, E, metrics, R: int, P: int):
+    """BASELINE configs[3] beside the headline: R what-if replicas (weights and
+    strategy per replica, generator.replica_profiles) of the first P pods of
+    the same queue on the same cluster, one ksg_run_replicas launch chain.
+    This is the HBM-bound regime of the path; device time from
+    HIP events on the library's stream, roofline of the dominant kernel."""
+    profiles = [E.encode_profile(p, enc.cluster.res_names) for p in G.replica_profiles(R)]
+    eng.run_replicas(profiles, 0, P)   # warmup
+    ms, walls = [], []
+    for _ in range(3):
+        t = time.perf_counter()
+        eng.run_replicas(profiles, 0, P)
+        walls.append((time.perf_counter() - t) * 1e3)
+        ms.append(eng.last_kernel_ms())
+    eng.set_timing(True)
+    eng.run_replicas(profiles, 0, P)
+    ks = eng.kernel_stats()
+    eng.set_timing(False)
+    kms = min(ms)
+    n = len(enc.cluster.node_names)
+    return {"workload": f"configs[3]: {R} replicas x {n} nodes, first {P} pods of the configs[1] queue",
+            "replica_pods_per_s": R * P / (kms * 1e-3), "node_evals_per_s": R * P * n / (kms * 1e-3),
+            "device_ms": kms, "wall_ms": min(walls),
+            "roofline": metrics.dominant_kernel_roofline(ks, metrics.bytes_per_node_eval(enc, prof))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -66,6 +95,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sweep-replicas", type=int, default=1024, help="configs[3] sidecar; 0 disables")
+    ap.add_argument("--sweep-pods", type=int, default=1000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,6 +210,12 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(enc, pf, args.cpu_threads, args.cpu_budget)
+        if args.sweep_replicas > 0 and world == 1:
+            try:
+                out["replica_sweep"] = replica_sweep(eng, enc, prof, G, E, metrics, args.sweep_replicas,
+                                                     min(args.sweep_pods, P))
+            except Exception as e:   # a sidecar; never lose the headline line over it
+                log(f"replica sweep unavailable: {e}")
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -125,9 +125,9 @@ class DebuggableScheduler:
         self.preemption_on = "DefaultPreemption" in {n for n, _ in prof.plugins}
         # (preemptor, nominated node, victims) per preemption, in order
         self.preemptions: List[tuple] = []
-        # annotations of a preemptor's first attempt, reflected onto the pod
-        # (storereflector) before its retry is recorded
-        self.reflected: Dict[int, Dict[str, str]] = {}
+        # result set of a preemptor's first attempt: the storereflector
+        # reflects it onto the pod before the retry is recorded
+        self.first_attempt: Dict[int, Dict[str, str]] = {}
         self.store = A.ResultStore(prof.weights())
         self.decoder = Decoder(self.enc)
         self.node_names = self.enc.cluster.node_names
@@ -152,6 +152,22 @@ class DebuggableScheduler:
     def schedule_one(self, pi: int, record: bool = True) -> int:
         return self._cycle(pi, record).selected
 
+    def schedule(self, pi: int, record: bool = True) -> PodCycle:
+        """One scheduling cycle (with DefaultPreemption and the preemptor's
+        retry); returns the final cycle."""
+        return self._cycle(pi, record)
+
+    @staticmethod
+    def rejecting_plugins(cyc: PodCycle, enc_pod) -> set:
+        """diagnosis.UnschedulablePlugins of a failed cycle: the plugin of
+        every node's first rejection (NodeAffinity for a PreFilter reject)."""
+        w = np.asarray(cyc.fstatus)
+        w = w[(w != 0) & (w != FS_NOT_EVALUATED)]
+        out = {int(x) for x in np.unique(w & 0xFF) - 1}
+        if int(enc_pod["flags"]) & E.POD_FLAG_PREFILTER_REJECT:
+            out.add(P.NODE_AFFINITY)
+        return out
+
     def _cycle(self, pi: int, record: bool) -> PodCycle:
         cyc = self.evaluate(pi)
         nominated, victims = -1, []
@@ -168,8 +184,8 @@ class DebuggableScheduler:
             self.preemptions.append((pi, nominated, list(victims)))
             if record:
                 pod = self.pods[pi]
-                self.reflected[pi] = {}
-                A.reflect(self.store, pod.namespace, pod.name, self.reflected[pi])
+                self.first_attempt[pi] = self.store.GetStoredResult(pod.namespace, pod.name) or {}
+                self.store.DeleteData(pod.namespace, pod.name)
             cyc = self.evaluate(pi)
             if int(cyc.fstatus[nominated]) == 0:   # evaluateNominatedNode: the only feasible node
                 only = np.full_like(cyc.fstatus, FS_NOT_EVALUATED)
@@ -348,9 +364,20 @@ class DebuggableScheduler:
         over it as the reflector's next pass would (with result-history)."""
         pod = self.pods[pi]
         cur = self.store.GetStoredResult(pod.namespace, pod.name)
-        if pi not in self.reflected:
+        if pi not in self.first_attempt:
             return cur
-        return A.merged_reflection(self.reflected[pi], cur)
+        return A.merged_reflection(A.merged_reflection({}, self.first_attempt[pi]), cur)
+
+    def reflect(self, pi: int, pod_annotations: Dict[str, str]) -> None:
+        """storereflector: merge every result set of the pod's last cycle into
+        its annotations (history appended, oldest first) and drop the stored
+        data, as after the reflector's pod update."""
+        pod = self.pods[pi]
+        first = self.first_attempt.pop(pi, None)
+        if first:
+            pod_annotations.update(first)
+            A.update_result_history(pod_annotations, first)
+        A.reflect(self.store, pod.namespace, pod.name, pod_annotations)
 
 
 class Status:
