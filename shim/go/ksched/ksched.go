@@ -194,6 +194,34 @@ func (x *Ctx) Commit(pod, node int) error {
 	return x.check(C.ksg_commit(x.c, C.int32_t(pod), C.int32_t(node)))
 }
 
+// Uncommit deletes a preemption victim from the node state (ksg_uncommit,
+// the inverse of Commit).
+func (x *Ctx) Uncommit(pod, node int) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	return x.check(C.ksg_uncommit(x.c, C.int32_t(pod), C.int32_t(node)))
+}
+
+// PreemptVictims runs DefaultPreemption's SelectVictimsOnNode for every
+// candidate node at once (ksg_preempt_victims).  cand[k]'s potential victims
+// are vic[off[k]:off[k+1]], most important first; fits[k] == 0 means the node
+// cannot help, victim[i] == 1 means vic[i] stays evicted.
+func (x *Ctx) PreemptVictims(pod int, cand, off, vic []int32) (fits []int32, victim []uint8, err error) {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	if len(off) != len(cand)+1 {
+		return nil, nil, fmt.Errorf("ksched: off needs len(cand)+1 entries")
+	}
+	fits = make([]int32, len(cand))
+	victim = make([]uint8, len(vic))
+	if len(cand) == 0 {
+		return fits, victim, nil
+	}
+	err = x.check(C.ksg_preempt_victims(x.c, C.int32_t(pod), p32(cand), C.int32_t(len(cand)), p32(off),
+		p32(vic), p32(fits), pu8(victim)))
+	return fits, victim, err
+}
+
 // RunQueue schedules pods [first, first+count) on the device in queue order.
 func (x *Ctx) RunQueue(first, count int) ([]int32, error) {
 	x.mu.Lock()
