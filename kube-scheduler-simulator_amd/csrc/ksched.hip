@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -1080,7 +1081,6 @@ __global__ __launch_bounds__(kP2Block) void ksg_batch_phase2(BatchArgs a) {
 // The selected node is either the best unchanged node or a changed one, so
 // outside the rare renormalisation every load pod j+1 needs is issued a pod
 // early.  RM bounds the resource columns (slot layout fixed at compile time).
-constexpr int kP2SBlock = KSG_BATCH_MAX;   // one lane per possible changed slot
 
 // slot row (int64 words): alloc/requested pairs of columns 0..RM-1, then
 // nonzero cpu, nonzero memory, pod count, allowed pods, f32 1/alloc of cpu and
@@ -1090,6 +1090,10 @@ struct SlotLayout {
   static constexpr int NZC = 2 * RM, NZM = 2 * RM + 1, PODS = 2 * RM + 2, ALLOWED = 2 * RM + 3;
   static constexpr int INVC = 2 * RM + 4, INVM = 2 * RM + 5, DAC = 2 * RM + 6, DAM = 2 * RM + 7;
   static constexpr int W = 2 * RM + 8;
+  // LDS row stride (int64 words): 2 words of padding put lane i's row 4i banks
+  // (mod 64) from lane 0's, so the per-lane 16-byte reads of a row hit disjoint
+  // banks instead of all lanes hitting the same bank
+  static constexpr int STRIDE = W + 2;
 };
 
 struct P2Part {
@@ -1246,10 +1250,11 @@ __device__ __forceinline__ int64_t slot_word_value(const SlotFetch<RM>& f, int l
   return lane < SL::W ? f.v64 : 0;
 }
 
-template <int RM>
-__global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
+template <int RM, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   using SL = SlotLayout<RM>;
-  constexpr int BLOCK = kP2SBlock, NW = BLOCK / 64, SW = SL::W;
+  constexpr int NW = BLOCK / 64, SW = SL::W;
+  static_assert(BLOCK % 64 == 0 && BLOCK <= KSG_BATCH_MAX, "one lane per changed slot of a batch of <= BLOCK pods");
   extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
   __shared__ ksg_profile s_prof;
   __shared__ P1Stats s_p1[KSG_BATCH_MAX];
@@ -1276,8 +1281,8 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
   for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
   for (int i = tid; i < a.nb * (int)(sizeof(P1Stats) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(s_p1)[i] = reinterpret_cast<const int32_t*>(a.p1)[i];
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  for (int i = tid; i < (int)(sizeof(ksg_profile) / 4); i += BLOCK)
+    reinterpret_cast<int32_t*>(&s_prof)[i] = reinterpret_cast<const int32_t*>(a.prof)[i];
   s_top[tid] = a.top[tid];
   bool fit_filter_on = false;
   for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
@@ -1352,7 +1357,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     if (tid < nc && (my_rec >> 63)) {
       int64_t sw[SW];
       {
-        const int4* src = reinterpret_cast<const int4*>(s_slot + (size_t)tid * SW);
+        const int4* src = reinterpret_cast<const int4*>(s_slot + (size_t)tid * SL::STRIDE);
 #pragma unroll
         for (int k = 0; k < SW / 2; k++) reinterpret_cast<int4*>(sw)[k] = src[k];
       }
@@ -1540,7 +1545,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
     KSG_STAMP(7);
     if (wv == 0 && selected >= 0) {
       const int slot = added ? nc : idx;
-      int64_t* row = s_slot + (size_t)slot * SW;
+      int64_t* row = s_slot + (size_t)slot * SL::STRIDE;
       if (lane < SW)   // the live columns stay in the row; global memory gets them after the walk
         row[lane] = (added ? col_val : row[lane]) + row_delta;
       if (lane == 0 && has_commit) {   // PodTopologySpread / InterPodAffinity count tables
@@ -1581,7 +1586,7 @@ __global__ __launch_bounds__(kP2SBlock) void ksg_batch_phase2s(BatchArgs a) {
   // and the results go out once, here.
   for (int i = tid; i < nc * SW; i += BLOCK) {
     const int slot = i / SW, w = i - slot * SW, node = s_clist[slot];
-    const int64_t val = s_slot[(size_t)slot * SW + w];
+    const int64_t val = s_slot[(size_t)slot * SL::STRIDE + w];
     if (w < 2 * RM && (w & 1) && (w >> 1) < R) a.st.requested[(size_t)(w >> 1) * N + node] = val;
     else if (w == SL::NZC || w == SL::NZM) a.st.nonzero[(size_t)(w - SL::NZC) * N + node] = val;
     else if (w == SL::PODS) a.st.pod_count[node] = (int32_t)val;
@@ -2125,6 +2130,7 @@ struct ksg_ctx {
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
   int batch_mode = 2;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default)
+  int slot_block = KSG_BATCH_MAX;  // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
   bool timing = false;
@@ -2384,6 +2390,15 @@ struct Tmp {
     if (_e != hipSuccess) return fail(ctx, KSG_E_NOMEM, hipGetErrorString(_e));        \
   } while (0)
 
+// ksg_batch_phase2s instances: (RM 4 | KSG_MAX_RES) x (64 | 128 | 256 lanes)
+static const std::array<const void*, 6>& slot_kernels() {
+  static const std::array<const void*, 6> k = {
+      (const void*)ksg_batch_phase2s<4, 64>,           (const void*)ksg_batch_phase2s<4, 128>,
+      (const void*)ksg_batch_phase2s<4, 256>,          (const void*)ksg_batch_phase2s<KSG_MAX_RES, 64>,
+      (const void*)ksg_batch_phase2s<KSG_MAX_RES, 128>, (const void*)ksg_batch_phase2s<KSG_MAX_RES, 256>};
+  return k;
+}
+
 int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
                 const ksg_profile* d_prof) {
   const int N = ctx->c.N;
@@ -2423,7 +2438,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   constexpr size_t kLdsBudget = 120 * 1024;
   const size_t cm_words = (size_t)((((N + 31) / 32) + 3) & ~3);
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;   // ksg_batch_phase2s<RM> instance
-  const size_t slot_bytes = ctx->batch_mode == 2 ? 8 * (size_t)(2 * slot_rm + 8) : 8 * (size_t)(2 * ctx->c.R + 4);
+  const size_t slot_bytes = ctx->batch_mode == 2 ? 8 * (size_t)(2 * slot_rm + 10) : 8 * (size_t)(2 * ctx->c.R + 4);
   const bool topset = ctx->batch_mode >= 1;   // top-set variants keep one slot per pod
   static bool attr_set = false;
   if (!attr_set) {
@@ -2431,10 +2446,8 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
                                   (int)kLdsBudget));
     HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
-    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2s<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kLdsBudget));
-    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2s<KSG_MAX_RES>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
+    for (const void* f : slot_kernels())
+      HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
     attr_set = true;
   }
   (void)hipGetLastError();
@@ -2443,7 +2456,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   int trc;
   if ((trc = tmark(ctx))) return trc;
   for (int off = 0; off < count;) {
-    int nb = std::min(KSG_BATCH_MAX, count - off);
+    int nb = std::min(ctx->batch_mode == 2 ? ctx->slot_block : KSG_BATCH_MAX, count - off);
     int64_t lo = 0, hi = 0;
     size_t bytes = 0;
     for (;;) {
@@ -2473,8 +2486,9 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
       if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
       // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
       if (ctx->batch_mode == 2) {
-        if (slot_rm == 4) hipLaunchKernelGGL(ksg_batch_phase2s<4>, dim3(1), dim3(kP2SBlock), bytes, ctx->stream, b);
-        else hipLaunchKernelGGL(ksg_batch_phase2s<KSG_MAX_RES>, dim3(1), dim3(kP2SBlock), bytes, ctx->stream, b);
+        const int si = (slot_rm == 4 ? 0 : 3) + (ctx->slot_block == 64 ? 0 : ctx->slot_block == 128 ? 1 : 2);
+        hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(slot_kernels()[si])), dim3(1),
+                           dim3(ctx->slot_block), bytes, ctx->stream, b);
         if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2S, 0.5 * b.nb * (b.nb + 1)))) return trc;
       } else {
         hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
@@ -2881,6 +2895,10 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : 2;
+  }
+  if (const char* f = getenv("KSG_SLOT_BLOCK")) {
+    const int v = atoi(f);
+    ctx->slot_block = v <= 64 ? 64 : v <= 128 ? 128 : KSG_BATCH_MAX;
   }
   *out = ctx;
   return KSG_OK;

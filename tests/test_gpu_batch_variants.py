@@ -22,12 +22,16 @@ def _have_gpu():
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
 
-MODES = ["slot", "topset", "scan"]
+# (mode, extra env): the slot variant at each of its block sizes (= batch sizes)
+MODES = {"slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
+         "slot128": ("slot", {"KSG_SLOT_BLOCK": 128}),
+         "topset": ("topset", {}), "scan": ("scan", {})}
 
 
-@pytest.fixture(scope="module", params=MODES)
+@pytest.fixture(scope="module", params=list(MODES))
 def variant(request, built):
-    return _engine_with_batch_mode(request.param)
+    mode, env = MODES[request.param]
+    return _engine_with_batch_mode(mode, **env)
 
 
 @pytest.fixture(scope="module")

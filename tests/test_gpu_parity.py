@@ -24,17 +24,21 @@ def gpu(built):
     return native.Engine(device=0)
 
 
-def _engine_with_batch_mode(mode):
+def _engine_with_batch_mode(mode, **env):
+    """Engine whose batched path runs phase-2 variant `mode`; `env` sets further
+    KSG_* knobs (e.g. KSG_SLOT_BLOCK).  All are read at ksg_open."""
     import os
-    old = os.environ.get("KSG_BATCH_MODE")
-    os.environ["KSG_BATCH_MODE"] = mode
+    env = {"KSG_BATCH_MODE": mode, **env}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
     try:
-        return native.Engine(device=0)   # the mode is read at ksg_open
+        return native.Engine(device=0)
     finally:
-        if old is None:
-            del os.environ["KSG_BATCH_MODE"]
-        else:
-            os.environ["KSG_BATCH_MODE"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
