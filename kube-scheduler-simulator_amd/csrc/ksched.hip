@@ -1296,7 +1296,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   uint64_t my_rec = 0;         // pod j's phase-1 record at my_node
   int32_t my_img = 0;
 #ifdef KSG_STAMPS
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+  unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
 #endif
   KSG_STAMP(0);
   for (int j = 0; j < a.nb; j++) {
@@ -1319,6 +1319,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     }
     const int64_t mt1 = s1.mt, ma1 = s1.ma;
     const bool more = j + 1 < a.nb;
+    KSG_STAMP(8);
     const int jn = more ? j + 1 : j;   // row of the next-pod loads (always a valid row)
 
     // ---- X1: speculated best unchanged node (sorted T_j, first 64 entries) --
@@ -1342,6 +1343,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
       }
       bu_full = m == 0 && s1.K > 64;
     }
+    KSG_STAMP(9);
     // ---- X2: pod j+1's loads (consumed in Y) ----------------------------------
     const int K1 = more ? s_p1[j + 1].K : 0;
     const int nn = tid < nc ? my_node : (spec >= 0 ? spec : 0);
@@ -1361,6 +1363,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 #pragma unroll
         for (int k = 0; k < SW / 2; k++) reinterpret_cast<int4*>(sw)[k] = src[k];
       }
+      KSG_STAMP(10);
       const uint64_t x = my_rec;
       cnt = 1;
       const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff;
@@ -1382,6 +1385,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
           fs = fit_score(prof, p, L);
           bs = ba_score(prof, p, L);
         }
+        KSG_STAMP(11);
         const int64_t part = my_img + fs * h.w_fit + bs * h.w_ba;
         const int64_t nt = mt1 != 0 ? 100 - qdiv(100 * rt, mt1, s1.inv_mt) : 100;
         const int64_t na = ma1 != 0 ? qdiv(100 * ra, ma1, s1.inv_ma) : ra;
@@ -1390,6 +1394,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
         live = pack_rec(part, rt, ra);
       }
     }
+    KSG_STAMP(12);
     if (tid < nc) s_ce[tid] = live;
     {
       const uint64_t k0 = wreduce(my_key, OpMaxU64{});
@@ -1598,7 +1603,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
 #ifdef KSG_STAMPS
   if (tid == 0 && a.stamps)
-    for (int i = 0; i < 8; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+    for (int i = 0; i < 16; i++) atomicAdd(&a.stamps[i], st_acc[i]);
 #endif
 }
 

@@ -23,14 +23,55 @@ native = importlib.import_module(PKG + ".native")
 import binding  # oracle/binding.py: the checker
 
 
+def replicas(a):
+    """Configs 4/5: one GPU replica sweep (ksg_run_replicas) of the first LIMIT
+    pods; an evenly spaced subset of the replicas re-run on the oracle."""
+    if a.config == 4:
+        R = a.replicas or 1024
+        nodes, pods, prof, rprofs = G.config4(n_replicas=R)
+    else:
+        R = a.replicas or 64
+        nodes, pods, prof = G.config5(n_pods=a.limit or 500)
+        rprofs = [prof] * R   # as scripts/bench_configs.py --config 5
+    P = min(a.limit or 500, len(pods))
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    profiles = [E.encode_profile(p, enc.cluster.res_names) for p in rprofs]
+    gpu = native.Engine(device=0)
+    gpu.load(enc, pf)
+    t = time.perf_counter()
+    pg, sg = gpu.run_replicas(profiles, 0, P)
+    t_gpu = time.perf_counter() - t
+    ora = binding.Oracle(nthreads=a.threads)
+    ora.load(enc, pf)
+    idx = sorted(set(np.linspace(0, R - 1, min(a.check, R)).astype(int).tolist()))
+    t = time.perf_counter()
+    bad = []
+    for k, r in enumerate(idx):
+        po, so = ora.run_replicas([profiles[r]], 0, P)
+        if not (np.array_equal(pg[r], po[0]) and sg[r].tobytes() == so[0].tobytes()):
+            bad.append(r)
+        print(f"oracle: replica {r} ({k + 1}/{len(idx)}), {time.perf_counter() - t:.0f}s", file=sys.stderr, flush=True)
+    out = {"config": a.config, "nodes": len(nodes), "pods": P, "replicas": R, "checked_replicas": idx,
+           "gpu_s": t_gpu, "oracle_s": time.perf_counter() - t, "oracle_threads": a.threads,
+           "mismatched_replicas": bad, "placements_and_summaries_equal": not bad}
+    print(json.dumps(out), flush=True)
+    sys.exit(0 if not bad else 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, choices=(2, 3), default=3)
+    ap.add_argument("--config", type=int, choices=(2, 3, 4, 5), default=3)
+    ap.add_argument("--replicas", type=int, default=None, help="configs 4/5: replicas on the GPU")
+    ap.add_argument("--check", type=int, default=16, help="configs 4/5: replicas re-run on the oracle (evenly spaced)")
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--chunk", type=int, default=2000)
     ap.add_argument("--limit", type=int, default=None, help="compare the first LIMIT pods of the queue")
     a = ap.parse_args()
+    if a.config in (4, 5):
+        replicas(a)
+        return
     make = {2: G.config2, 3: G.config3}[a.config]
     nodes, pods, prof = make(n_pods=a.pods) if a.pods else make()
     enc = E.Encoder(nodes, pods, prof)
