@@ -1289,6 +1289,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   __syncthreads();
   const CmProf cm = cm_prof(s_prof);
   const bool ipa_filter = ipa_in_filter(s_prof);
+  const bool ipa_score = ((s_prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) != 0;
 
   auto changed = [&](int n) { return ((s_cmask[n >> 5] >> (n & 31)) & 1u) != 0; };
   int nc = 0;                  // |C|, block-uniform
@@ -1304,19 +1305,25 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     const ksg_profile& prof = s_prof;
     const P1Stats s1 = s_p1[j];
     const PodHot<RM> h = pod_hot<RM>(p, prof, fit_filter_on, R);
+    // Every LDS read of the pod's setup is issued here, in straight-line code,
+    // so they share one round trip (branches on lane or tid would serialise them).
+    const int rl = (lane >> 1) < RM ? (lane >> 1) : 0;
+    const int64_t req_l = p.req[rl];
+    const int32_t p_commit = p.commit, p_ipa = p.ipa;
+    const uint32_t p_skip = p.score_skip;
     // this lane's word of the assume (row word `lane` += delta), computed off the critical path
-    int64_t row_delta = 0;
-    if (lane < 2 * RM) row_delta = (lane & 1) && (lane >> 1) < R ? p.req[lane >> 1] : 0;
-    else if (lane == SL::NZC) row_delta = p.nz_cpu;
-    else if (lane == SL::NZM) row_delta = p.nz_mem;
-    else if (lane == SL::PODS) row_delta = 1;
-    const bool has_commit = p.commit >= 0;
-    uint32_t pod_status = 0, pod_skip = 0;   // ipa_skip_bits for an unscored / scored result
-    uint32_t pod_status_s = KSG_ST_SCORED, pod_skip_s = 0;
-    if (tid == 0) {
-      ipa_skip_bits(prof, ipa_filter, p, pod_status, pod_skip);
-      ipa_skip_bits(prof, ipa_filter, p, pod_status_s, pod_skip_s);
-    }
+    const int64_t row_delta = lane < 2 * RM ? ((lane & 1) && (lane >> 1) < R ? req_l : 0)
+                              : lane == SL::NZC ? h.nz_cpu
+                              : lane == SL::NZM ? h.nz_mem
+                              : lane == SL::PODS ? 1 : 0;
+    const bool has_commit = p_commit >= 0;
+    // ipa_skip_bits for an unscored / scored result, without the call's branches
+    const bool ipa_none = p_ipa < 0;
+    const uint32_t st_pf = ipa_none && ipa_filter ? KSG_ST_IPA_PREFILTER_SKIP : 0u;
+    const bool ps_skip = ipa_none && ipa_score && !((p_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u);
+    const uint32_t pod_status = st_pf, pod_skip = p_skip;
+    const uint32_t pod_status_s = KSG_ST_SCORED | st_pf | (ps_skip ? KSG_ST_IPA_PRESCORE_SKIP : 0u);
+    const uint32_t pod_skip_s = p_skip | (ps_skip ? bit(KSG_PL_INTER_POD_AFFINITY) : 0u);
     const int64_t mt1 = s1.mt, ma1 = s1.ma;
     const bool more = j + 1 < a.nb;
     KSG_STAMP(8);
