@@ -2142,7 +2142,7 @@ struct ksg_ctx {
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
   int batch_mode = 2;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default)
-  int slot_block = KSG_BATCH_MAX;  // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256
+  int slot_block = 128;  // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (128: 1-2 % faster end to end than 256)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
   bool timing = false;

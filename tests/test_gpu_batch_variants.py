@@ -22,9 +22,9 @@ def _have_gpu():
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
 
-# (mode, extra env): the slot variant at each of its block sizes (= batch sizes)
+# (mode, extra env): the slot variant at each of its block sizes (= batch sizes; 128 is the default)
 MODES = {"slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
-         "slot128": ("slot", {"KSG_SLOT_BLOCK": 128}),
+         "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
          "topset": ("topset", {}), "scan": ("scan", {})}
 
 
