@@ -2611,11 +2611,16 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   TA(tmp, &s.srec, sizeof(uint64_t) * (size_t)kBatch * N);
   // Workgroups per replica: with few replicas of a large cluster, S > 1 spreads
   // each replica over S co-resident workgroups (two group barriers per pod);
-  // aim at ~4 workgroups per CU and at least ~8 nodes per lane.
+  // aim at ~2 workgroups per CU and at least ~8 nodes per lane (config 5,
+  // 64 replicas x 100k nodes: S = 8 runs 5 % faster than S = 16 and 1.2x
+  // faster than S = 4; profiles/r1/config5_group_size.json).
   int cus = 0;
   HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
   int S = 1;
-  if (R < 4 * cus) S = std::min({std::max(1, 4 * cus / R), std::max(1, N / 2048), 64});
+  if (R < 2 * cus) S = std::min({std::max(1, 2 * cus / R), std::max(1, N / 2048), 64});
+  // Measurement knob: force the group size (still halved below until every
+  // workgroup of a group is co-resident, so a forced S cannot deadlock).
+  if (const char* f = getenv("KSG_SWEEP_S")) S = std::max(1, std::min(atoi(f), 64));
   // (BLOCK, KN): KN nodes per lane in registers; KN = 0 streams them through a
   // per-replica scratch row instead.  The instances that fit 128 VGPRs without
   // spilling: every fast shape for one workgroup per replica; KN = 8 for
