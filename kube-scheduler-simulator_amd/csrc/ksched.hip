@@ -2721,6 +2721,8 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   int cus = 0;
   HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
   if (!ctx->coop_gmax) ctx->coop_gmax = std::min(cus, 256);   // one workgroup per CU: lanes wait on memory
+  // Measurement knob: cap on the group size (fewer workgroups, more nodes per lane).
+  if (const char* f = getenv("KSG_COOP_GMAX")) ctx->coop_gmax = std::max(1, std::min(atoi(f), std::min(cus, 256)));
   int kn = 1;
   while ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N && kn < 32) kn *= 2;
   if ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: too many nodes");
