@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KSG_ABI_VERSION 1
+#define KSG_ABI_VERSION 2
 
 #define KSG_OK 0
 #define KSG_E_INVALID (-1)     /* bad argument / inconsistent sizes            */
@@ -230,9 +230,21 @@ int ksg_set_profile(ksg_ctx* ctx, const ksg_profile* prof);
 int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nodes, const ksg_topology* topo);
 int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl);
 
+/* Append pods to the loaded workload (the scheduler's per-cycle path: a new
+ * pod is encoded against the loaded universe and appended; include/
+ * ksched_snapshot.h does both).  tail->pods' program offsets are absolute in
+ * the pool; tail->prog holds pool words [prog_base, prog_base +
+ * tail->prog_len), and prog_base must not cut into a program an earlier pod
+ * uses.  The new pods get indices n_pods, n_pods + 1, ... */
+int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base);
 /* Evaluate pod `pod` (index into the loaded workload) against the current
  * node state; no state change.  `cap` may be NULL. */
 int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap);
+/* Evaluate an encoded pod that is not part of the workload: `pod`'s program
+ * offsets index `prog[0 .. prog_len)`.  Same outputs as ksg_eval; the pod
+ * is not retained (ksg_append_pods it first to commit it). */
+int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t prog_len, ksg_result* res,
+                 ksg_capture* cap);
 /* Assume pod `pod` onto node `node` (NodeInfo.AddPod + count tables). */
 int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node);
 /* Schedule pods [first, first+count) in order on the device.  placements

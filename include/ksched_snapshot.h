@@ -1,0 +1,272 @@
+/*
+ * ksched_snapshot.h — native snapshot encoder of libksched.so (host code).
+ *
+ * North-star subsystem (1): NodeInfo / PodInfo -> the SoA columns, interned
+ * ids and compiled selector programs of ksched.h, built from flat C views of
+ * the v1.Node / v1.Pod fields the in-tree Filter/Score plugins read.  A cgo
+ * caller fills these views straight from the objects the framework hands to
+ * the wrapped plugins:
+ *   PreFilter(ctx, state, *v1.Pod)             wrappedplugin.go:491 (-> :504)
+ *   Filter(ctx, state, *v1.Pod, *NodeInfo)     wrappedplugin.go:523 (-> :535)
+ * and from handle.SnapshotSharedLister().NodeInfos().List() for the node set
+ * (INTEGRATION.md §3).  No Python is involved: the encoder, the device
+ * library and the status-message decoder are one native library.
+ *
+ * Views are read during the call only (cgo pointer rules); strings are
+ * NUL-terminated UTF-8.  Every function returns 0 or a negative KSG_E_* code;
+ * ksg_snapshot_error() gives the message.  A snapshot is not thread-safe.
+ *
+ * Life cycle:
+ *   ksg_snapshot_new(profile)            KubeSchedulerConfiguration profile 0
+ *   ksg_snapshot_add_node(...)           every node, in snapshot order
+ *   ksg_snapshot_add_pod(...)            every pod that is or will be bound
+ *   ksg_snapshot_bind(pod, node)         pods already running (NodeInfo.Pods)
+ *   ksg_snapshot_load(ctx)               encode + load into a device context,
+ *                                        replaying the bindings
+ * then per scheduling cycle:
+ *   ksg_snapshot_add_pod(new pod)        -> pod index
+ *   ksg_snapshot_sync(ctx)               appends the pod to the device
+ *                                        workload when the encoding universe
+ *                                        (label columns, value ids, selectors,
+ *                                        term templates) is unchanged, else
+ *                                        re-encodes and reloads everything
+ *   ksg_eval(ctx, pod, ...)              one sweep (ksched.h)
+ *   ksg_snapshot_assume(ctx, pod, node)  Reserve: ksg_commit + binding record
+ *   ksg_snapshot_status(...)             framework.Status code + message of a
+ *                                        node's filter status word
+ */
+#ifndef KSCHED_SNAPSHOT_H
+#define KSCHED_SNAPSHOT_H
+
+#include "ksched.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ksg_str_pair { const char* key; const char* value; } ksg_str_pair;
+
+/* A resource quantity: cpu in millicores (Quantity.MilliValue), every other
+ * resource in base units (Quantity.Value).  Also (name, weight) pairs of the
+ * plugin args' resource lists. */
+typedef struct ksg_quantity { const char* name; int64_t value; } ksg_quantity;
+
+typedef struct ksg_taint_view { const char* key; const char* value; const char* effect; } ksg_taint_view;
+
+/* operator: "" / "Equal" / "Exists"; effect "" = every effect */
+typedef struct ksg_toleration_view {
+  const char* key;
+  const char* op;
+  const char* value;
+  const char* effect;
+} ksg_toleration_view;
+
+/* NodeSelectorRequirement / LabelSelectorRequirement:
+ * op "In" "NotIn" "Exists" "DoesNotExist" "Gt" "Lt" */
+typedef struct ksg_requirement_view {
+  const char* key;
+  const char* op;
+  int32_t n_values;
+  const char* const* values;
+} ksg_requirement_view;
+
+typedef struct ksg_node_selector_term_view {
+  int32_t n_expr;
+  const ksg_requirement_view* expr;     /* matchExpressions */
+  int32_t n_fields;
+  const ksg_requirement_view* fields;   /* matchFields (metadata.name) */
+} ksg_node_selector_term_view;
+
+typedef struct ksg_preferred_term_view {
+  int32_t weight;
+  ksg_node_selector_term_view preference;
+} ksg_preferred_term_view;
+
+/* metav1.LabelSelector; is_set = 0 models a nil pointer */
+typedef struct ksg_label_selector_view {
+  int32_t is_set;
+  int32_t n_labels;
+  const ksg_str_pair* match_labels;
+  int32_t n_expr;
+  const ksg_requirement_view* expr;
+} ksg_label_selector_view;
+
+/* PodAffinityTerm (weight: WeightedPodAffinityTerm.weight, preferred terms only) */
+typedef struct ksg_affinity_term_view {
+  int32_t weight;
+  ksg_label_selector_view selector;
+  const char* topology_key;
+  int32_t n_namespaces;
+  const char* const* namespaces;
+  ksg_label_selector_view namespace_selector;   /* is_set 0 = nil */
+} ksg_affinity_term_view;
+
+/* TopologySpreadConstraint; min_domains 0 = nil; policies NULL/"" = nil */
+typedef struct ksg_spread_view {
+  int32_t max_skew;
+  const char* topology_key;
+  const char* when_unsatisfiable;   /* "DoNotSchedule" / "ScheduleAnyway" */
+  ksg_label_selector_view selector;
+  int32_t min_domains;
+  const char* node_affinity_policy;
+  const char* node_taints_policy;
+  int32_t n_match_label_keys;
+  const char* const* match_label_keys;
+} ksg_spread_view;
+
+typedef struct ksg_container_view {
+  const char* image;
+  int32_t n_requests;
+  const ksg_quantity* requests;
+  int32_t restartable;      /* init container with restartPolicy Always (sidecar) */
+  int32_t n_host_ports;     /* > 0: NodePorts with ports (refused: KSG_E_UNSUPPORTED) */
+} ksg_container_view;
+
+typedef struct ksg_image_view {
+  int32_t n_names;
+  const char* const* names;
+  int64_t size_bytes;
+} ksg_image_view;
+
+typedef struct ksg_node_view {
+  const char* name;
+  int32_t n_labels;
+  const ksg_str_pair* labels;
+  int32_t n_taints;
+  const ksg_taint_view* taints;
+  int32_t n_alloc;
+  const ksg_quantity* allocatable;   /* status.allocatable, "pods" included */
+  int32_t unschedulable;             /* spec.unschedulable */
+  int32_t n_images;
+  const ksg_image_view* images;      /* status.images */
+} ksg_node_view;
+
+typedef struct ksg_pod_view {
+  const char* namespace_;
+  const char* name;
+  int32_t n_labels;
+  const ksg_str_pair* labels;
+  int32_t n_containers;
+  const ksg_container_view* containers;
+  int32_t n_init_containers;
+  const ksg_container_view* init_containers;
+  int32_t has_overhead;
+  int32_t n_overhead;
+  const ksg_quantity* overhead;
+  const char* node_name;                     /* spec.nodeName ("" = unset) */
+  int32_t has_node_selector;                 /* spec.nodeSelector != nil */
+  int32_t n_node_selector;
+  const ksg_str_pair* node_selector;
+  int32_t has_na_required;                   /* requiredDuringScheduling... != nil */
+  int32_t n_na_required;
+  const ksg_node_selector_term_view* na_required;
+  int32_t has_na_preferred;                  /* preferredDuringScheduling... != nil */
+  int32_t n_na_preferred;
+  const ksg_preferred_term_view* na_preferred;
+  int32_t n_pod_affinity_required;
+  const ksg_affinity_term_view* pod_affinity_required;
+  int32_t n_pod_affinity_preferred;
+  const ksg_affinity_term_view* pod_affinity_preferred;
+  int32_t n_pod_anti_affinity_required;
+  const ksg_affinity_term_view* pod_anti_affinity_required;
+  int32_t n_pod_anti_affinity_preferred;
+  const ksg_affinity_term_view* pod_anti_affinity_preferred;
+  int32_t n_tolerations;
+  const ksg_toleration_view* tolerations;
+  int32_t n_spread;
+  const ksg_spread_view* spread;
+  /* helper.DefaultSelector over the Services / RCs / RSs / StatefulSets that
+   * select the pod (PodTopologySpread system defaults); is_set 0 = none */
+  ksg_label_selector_view default_spread_selector;
+  int32_t terminating;                       /* metadata.deletionTimestamp != nil */
+  int32_t priority;                          /* corev1helpers.PodPriority */
+} ksg_pod_view;
+
+typedef struct ksg_plugin_view { const char* name; int32_t weight; } ksg_plugin_view;
+
+/* Profile 0 after ConvertForSimulator (plugins.go:174-197): MultiPoint plugins
+ * in order (names with or without the "Wrapped" suffix), weights as written
+ * (getScorePluginWeight maps 0 to 1, plugins.go:289-304), and the plugin args
+ * the evaluator models (defaults: plugins_test.go:876-1000). */
+typedef struct ksg_profile_view {
+  int32_t n_plugins;
+  const ksg_plugin_view* plugins;
+  const char* fit_strategy;                  /* "LeastAllocated" / "MostAllocated" */
+  int32_t n_fit_resources;
+  const ksg_quantity* fit_resources;         /* (name, weight) */
+  int32_t n_ba_resources;
+  const ksg_quantity* ba_resources;
+  int32_t n_fit_ignored_resources;
+  const char* const* fit_ignored_resources;
+  int32_t n_fit_ignored_groups;
+  const char* const* fit_ignored_groups;
+  int32_t hard_pod_affinity_weight;
+  int32_t ignore_preferred_terms_of_existing_pods;
+  int32_t pts_system_defaulted;              /* PodTopologySpreadArgs.defaultingType == System */
+  int32_t ba_skip_best_effort;
+} ksg_profile_view;
+
+typedef struct ksg_snapshot ksg_snapshot;
+
+/* framework.Code values used by ksg_snapshot_status */
+#define KSG_CODE_SUCCESS 0
+#define KSG_CODE_UNSCHEDULABLE 2
+#define KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE 3
+#define KSG_CODE_SKIP 5
+
+int ksg_snapshot_new(const ksg_profile_view* profile, ksg_snapshot** out);
+int ksg_snapshot_free(ksg_snapshot* s);
+const char* ksg_snapshot_error(ksg_snapshot* s);
+
+int ksg_snapshot_add_node(ksg_snapshot* s, const ksg_node_view* node, int32_t* index);
+int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* pod, int32_t* index);
+/* Pod `pod` runs on `node` (NodeInfo.Pods): replayed as an assume at load. */
+int ksg_snapshot_bind(ksg_snapshot* s, int32_t pod, int32_t node);
+int ksg_snapshot_node_index(ksg_snapshot* s, const char* name, int32_t* index);
+
+/* Encode everything added so far (no device needed).  The views below point
+ * into the snapshot and stay valid until the next add / encode / sync. */
+int ksg_snapshot_encode(ksg_snapshot* s);
+int ksg_snapshot_view(ksg_snapshot* s, ksg_nodes* nodes, ksg_topology* topo, ksg_workload* workload,
+                      ksg_profile* profile);
+
+/* Encode only the pods added since the last encode: *appended = 1 when none
+ * of them extends the encoding universe (they are encoded against it,
+ * byte-identical to a full re-encode), 0 when a full re-encode ran. */
+int ksg_snapshot_encode_incremental(ksg_snapshot* s, int32_t* appended);
+
+/* Encode, ksg_set_profile + ksg_load_nodes + ksg_load_workload into `ctx`,
+ * then replay every binding / assume in order (ksg_commit). */
+int ksg_snapshot_load(ksg_snapshot* s, ksg_ctx* ctx);
+/* Bring `ctx` up to date after ksg_snapshot_add_pod: *appended = 1 when the new
+ * pods were appended (ksg_append_pods), 0 when a full reload was needed. */
+int ksg_snapshot_sync(ksg_snapshot* s, ksg_ctx* ctx, int32_t* appended);
+/* Reserve / assume: ksg_commit on the device and a binding record (replayed
+ * by a later reload). */
+int ksg_snapshot_assume(ksg_snapshot* s, ksg_ctx* ctx, int32_t pod, int32_t node);
+/* The inverse (a preemption victim's deletion): ksg_uncommit + record. */
+int ksg_snapshot_forget(ksg_snapshot* s, ksg_ctx* ctx, int32_t pod, int32_t node);
+
+/* framework.Status of `pod`'s Filter at `node` from its status word
+ * (ksg_capture.fstatus): *code = KSG_CODE_*, msg = Status.Message() (reasons
+ * joined with ", "), NUL-terminated, truncated to cap - 1 bytes; *len = full
+ * length.  Word 0 = Success (empty message). */
+int ksg_snapshot_status(ksg_snapshot* s, int32_t pod, uint32_t word, int32_t node, int32_t* code, char* msg,
+                        int32_t cap, int32_t* len);
+/* PreFilter of plugin `plugin` for `pod` (given the device result's status
+ * bits): *code = KSG_CODE_SUCCESS / SKIP / UNSCHEDULABLE_AND_UNRESOLVABLE
+ * (NodeAffinity "pod affinity terms conflict"); NodeAffinity's
+ * PreFilterResult node names (sorted) go to names[0..*n_names) when
+ * *has_result = 1 (names may be NULL to query the count). */
+int ksg_snapshot_prefilter(ksg_snapshot* s, int32_t pod, int32_t plugin, uint32_t result_status, int32_t* code,
+                           int32_t* has_result, const char** names, int32_t cap, int32_t* n_names);
+
+/* Decode tables of the current encoding (for ksg_annotator_new): node names,
+ * resource column names, taint strings "{key: value}". */
+int ksg_snapshot_counts(ksg_snapshot* s, int32_t* n_nodes, int32_t* n_pods, int32_t* n_res, int32_t* n_taint_vocab);
+int ksg_snapshot_names(ksg_snapshot* s, const char** node, const char** res, const char** taint);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSCHED_SNAPSHOT_H */

@@ -2112,6 +2112,8 @@ struct ksg_ctx {
   std::vector<ksg_pod> h_pods;
   std::vector<int32_t> h_na_pref_sum;   // per pod Σ preferred node-affinity weights
   std::vector<int32_t> h_prog;
+  size_t pod_cap = 0, prog_cap = 0;   // device capacity of d_pods / d_prog (ksg_append_pods grows them)
+  int64_t prog_used = 0;              // end of the last program word a loaded pod uses
   std::vector<int32_t> h_col_vocab;
   std::vector<uint8_t> h_col_unique;
   int32_t max_blob = 0;
@@ -2197,6 +2199,11 @@ int upc(ksg_ctx* ctx, const T*& field, const T* src, size_t count) {
 void free_all(ksg_ctx* ctx) {
   for (void* p : ctx->allocs) (void)hipFree(p);
   ctx->allocs.clear();
+  ctx->d_pods = nullptr;
+  ctx->d_prog = nullptr;
+  ctx->pod_cap = ctx->prog_cap = 0;
+  ctx->d_pre = nullptr;
+  ctx->pre_words = 0;
   ctx->d_rec = nullptr;
   ctx->d_img = nullptr;
   ctx->d_pmax = nullptr;
@@ -2848,7 +2855,9 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     a.results = d_res;
     const int block = N >= 512 ? 512 : 256;   // 512 lanes: <= 256 VGPRs per lane, no spills
     const bool topo = needs_topo(ctx, ctx->prof, first, count);
-    if (topo && !want_cap && ctx->topo_coop && ctx->force_path != 1) {
+    // the chip-wide path always assumes its pods: ksg_eval (do_commit = 0)
+    // takes the single-workgroup kernel
+    if (topo && !want_cap && do_commit && ctx->topo_coop && ctx->force_path != 1) {
       ctx->last_path = 4;
       if ((rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof))) return rc;
     } else if ((rc = launch_queue(ctx, a, 1, block, topo))) {
@@ -2873,6 +2882,72 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     HIPC(ctx, hipMemcpy(flags, ctx->d_coop_flags, sizeof(flags), hipMemcpyDeviceToHost));
     if (flags[4]) return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
   }
+  return KSG_OK;
+}
+
+// Grow a device array to `need` elements, keeping its first `used` ones.
+template <typename T>
+int dgrow(ksg_ctx* ctx, T** p, size_t* cap, size_t used, size_t need) {
+  if (need <= *cap && *p) return KSG_OK;
+  const size_t ncap = std::max(need, 2 * *cap);
+  T* np = nullptr;
+  int rc = dalloc(ctx, &np, ncap);
+  if (rc) return rc;
+  if (used && *p) HIPC(ctx, hipMemcpyAsync(np, *p, used * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  if (*p) {
+    auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)*p);
+    if (it != ctx->allocs.end()) ctx->allocs.erase(it);
+    (void)hipFree(*p);
+  }
+  *p = np;
+  *cap = ncap;
+  return KSG_OK;
+}
+
+// Extent of the program words a pod uses (blob and node set).
+int64_t pod_prog_end(const ksg_pod& p, int N) {
+  int64_t e = (int64_t)p.blob + p.blob_len;
+  if (p.node_set >= 0) e = std::max<int64_t>(e, (int64_t)p.node_set + (N + 31) / 32);
+  return e;
+}
+
+int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, int off);
+
+int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t* prog, int64_t prog_len,
+                    int64_t prog_base) {
+  if (!ctx->have_wl) return fail(ctx, KSG_E_STATE, "load a workload before appending");
+  if (n < 0 || prog_len < 0 || (n > 0 && !pods) || (prog_len > 0 && !prog)) return fail(ctx, KSG_E_INVALID, "append arguments");
+  if (prog_base < ctx->prog_used || prog_base > (int64_t)ctx->h_prog.size())
+    return fail(ctx, KSG_E_INVALID, "append: prog_base cuts into loaded programs or leaves a gap");
+  const int64_t new_len = prog_base + prog_len;
+  const int N = ctx->c.N;
+  int64_t used = ctx->prog_used;
+  int32_t max_blob = ctx->max_blob;
+  for (int i = 0; i < n; i++) {
+    const ksg_pod& p = pods[i];
+    if (p.blob < 0 || p.blob_len < 0 || pod_prog_end(p, N) > new_len)
+      return fail(ctx, KSG_E_INVALID, "appended pod program outside the pool");
+    used = std::max(used, pod_prog_end(p, N));
+    max_blob = std::max(max_blob, p.blob_len);
+  }
+  HIPC(ctx, hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = dgrow(ctx, &ctx->d_pods, &ctx->pod_cap, (size_t)ctx->n_pods, (size_t)ctx->n_pods + n))) return rc;
+  if ((rc = dgrow(ctx, &ctx->d_prog, &ctx->prog_cap, (size_t)prog_base, (size_t)std::max<int64_t>(new_len, 1)))) return rc;
+  if (n) HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->n_pods, pods, sizeof(ksg_pod) * n, hipMemcpyHostToDevice, ctx->stream));
+  if (prog_len)
+    HIPC(ctx, hipMemcpyAsync(ctx->d_prog + prog_base, prog, sizeof(int32_t) * prog_len, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->h_prog.resize(new_len);
+  if (prog_len) std::copy(prog, prog + prog_len, ctx->h_prog.begin() + prog_base);
+  for (int i = 0; i < n; i++) {
+    ctx->h_pods.push_back(pods[i]);
+    ctx->h_na_pref_sum.push_back(na_pref_weight_sum(ctx->h_prog, pods[i].na_pref));
+  }
+  ctx->n_pods += n;
+  ctx->prog_used = used;
+  ctx->max_blob = max_blob;
   return KSG_OK;
 }
 
@@ -3032,9 +3107,22 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
     ctx->h_na_pref_sum[i] = na_pref_weight_sum(prog, p.na_pref);
   }
   ctx->h_prog = std::move(prog);
+  ctx->prog_used = 0;
+  for (int i = 0; i < wl->n_pods; i++) ctx->prog_used = std::max(ctx->prog_used, pod_prog_end(ctx->h_pods[i], ctx->c.N));
   int rc;
+  if (ctx->d_pods) {   // a reload: drop the previous workload's buffers
+    for (void* q : {(void*)ctx->d_pods, (void*)ctx->d_prog}) {
+      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), q);
+      if (it != ctx->allocs.end()) ctx->allocs.erase(it);
+      (void)hipFree(q);
+    }
+    ctx->d_pods = nullptr;
+    ctx->d_prog = nullptr;
+  }
   if ((rc = upload(ctx, &ctx->d_pods, wl->pods, std::max(wl->n_pods, 1)))) return rc;
   if ((rc = upload(ctx, &ctx->d_prog, wl->prog, (size_t)std::max<int64_t>(wl->prog_len, 1)))) return rc;
+  ctx->pod_cap = std::max(wl->n_pods, 1);
+  ctx->prog_cap = (size_t)std::max<int64_t>(wl->prog_len, 1);
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_pods = wl->n_pods;
   ctx->have_wl = true;
@@ -3045,6 +3133,39 @@ int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   if (!res) return fail(ctx, KSG_E_INVALID, "null result");
   int32_t pl;
   return run_internal(ctx, pod, 1, 0, &pl, res, cap);
+}
+
+int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base) {
+  if (!ctx || !tail) return KSG_E_INVALID;
+  return append_internal(ctx, tail->pods, tail->n_pods, tail->prog, tail->prog_len, prog_base);
+}
+
+int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t prog_len, ksg_result* res,
+                 ksg_capture* cap) {
+  if (!ctx || !pod || !res) return KSG_E_INVALID;
+  if (!ctx->have_wl) return fail(ctx, KSG_E_STATE, "load a workload first");
+  // Stage the pod behind the loaded workload (offsets rebased), evaluate it,
+  // then drop it again: the device buffers keep the capacity.
+  const int64_t base = (int64_t)ctx->h_prog.size();
+  ksg_pod p = *pod;
+  for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob})
+    if (*f >= 0) *f = (int32_t)(*f + base);
+  const int32_t n0 = ctx->n_pods, blob0 = ctx->max_blob;
+  const int64_t used0 = ctx->prog_used;
+  int rc = append_internal(ctx, &p, 1, prog, prog_len, base);
+  if (!rc) {
+    int32_t pl;
+    rc = run_internal(ctx, n0, 1, 0, &pl, res, cap);
+  }
+  if (ctx->n_pods > n0) {
+    ctx->n_pods = n0;
+    ctx->h_pods.resize(n0);
+    ctx->h_na_pref_sum.resize(n0);
+    ctx->h_prog.resize(base);
+    ctx->prog_used = used0;
+    ctx->max_blob = blob0;
+  }
+  return rc;
 }
 
 int ksg_run_queue(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placements, ksg_result* results,

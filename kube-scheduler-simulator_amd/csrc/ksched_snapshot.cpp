@@ -1,0 +1,1768 @@
+// Native snapshot encoder (include/ksched_snapshot.h): NodeInfo / PodInfo
+// views -> the SoA columns, interned ids and compiled selector programs of
+// include/ksched.h.  Host code only (no device needed), part of libksched.so.
+//
+// The encoding is the one encoder.py documents (program grammar in its module
+// docstring); the two are independent restatements of the same contract and
+// tests/test_snapshot_native.py requires byte-identical output from both on
+// every workload family.  Upstream semantics restated here [upstream
+// k8s.io/kubernetes v1.32.5, not vendored — SURVEY.md §8(c)]:
+//   resourcehelper.PodRequests (non-missing cpu/memory defaults for the
+//   non-zero form), v1.Toleration.ToleratesTaint,
+//   metav1.LabelSelectorAsSelector, podtopologyspread
+//   filterTopologySpreadConstraints / buildDefaultConstraints,
+//   framework.AffinityTerm namespaces, imagelocality normalizedImageName and
+//   scaledImageScore, nodeaffinity PreFilter (matchFields metadata.name ->
+//   PreFilterResult), Go math.Log (src/math/log.go).
+// The framework.Status codes returned by ksg_snapshot_status follow the
+// plugins' Filter returns.
+#include "ksched_snapshot.h"
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <iterator>
+#include <map>
+#include <optional>
+#include <set>
+#include <string>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+namespace {
+
+// ---- plugin table (profile.py) ----------------------------------------------
+const char* const kPluginNames[KSG_NPLUGINS] = {
+    "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts",
+    "NodeResourcesFit", "VolumeRestrictions", "NodeVolumeLimits", "VolumeBinding",
+    "VolumeZone", "PodTopologySpread", "InterPodAffinity",
+    "NodeResourcesBalancedAllocation", "ImageLocality"};
+// extension points per plugin: prefilter, filter, prescore, score, normalize
+const bool kExt[KSG_NPLUGINS][5] = {
+    {false, true, false, false, false}, {false, true, false, false, false}, {false, true, true, true, true},
+    {true, true, true, true, true},     {true, true, false, false, false},  {true, true, true, true, false},
+    {true, true, false, false, false},  {true, true, false, false, false},  {true, true, true, true, false},
+    {true, true, false, false, false},  {true, true, true, true, true},     {true, true, true, true, true},
+    {false, false, true, true, false},  {false, false, false, true, false}};
+const char* const kNonEval[] = {"SchedulingGates", "PrioritySort", "DefaultPreemption", "DefaultBinder"};
+
+const std::string kCPU = "cpu", kMemory = "memory", kEphemeral = "ephemeral-storage", kPods = "pods";
+const std::string kHostname = "kubernetes.io/hostname", kZone = "topology.kubernetes.io/zone";
+const std::string kObjectName = "metadata.name";
+const std::string kUnschedTaint = "node.kubernetes.io/unschedulable";
+constexpr int64_t kDefaultMilliCPU = 100, kDefaultMemory = 200ll * 1024 * 1024;
+
+enum { OP_IN = 0, OP_NOT_IN, OP_EXISTS, OP_DNE, OP_GT, OP_LT, OP_NEVER };
+enum { TMPL_REQ_ANTI = 0, TMPL_REQ_AFF = 1, TMPL_PREF = 2 };
+
+int op_code(const std::string& s) {
+  if (s == "In") return OP_IN;
+  if (s == "NotIn") return OP_NOT_IN;
+  if (s == "Exists") return OP_EXISTS;
+  if (s == "DoesNotExist") return OP_DNE;
+  if (s == "Gt") return OP_GT;
+  if (s == "Lt") return OP_LT;
+  return -1;
+}
+
+int effect_code(const std::string& e) {
+  return e == "NoSchedule" ? KSG_EFFECT_NO_SCHEDULE
+         : e == "PreferNoSchedule" ? KSG_EFFECT_PREFER_NO_SCHEDULE
+         : e == "NoExecute" ? KSG_EFFECT_NO_EXECUTE : 0;
+}
+
+std::string S(const char* p) { return p ? std::string(p) : std::string(); }
+
+bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+
+// schedutil.IsScalarResourceName
+bool is_scalar(const std::string& n) {
+  if (starts_with(n, "hugepages-") || starts_with(n, "attachable-volumes-")) return true;
+  return n.find('/') != std::string::npos && !starts_with(n, "kubernetes.io/") && !starts_with(n, "requests.");
+}
+
+// strconv.ParseInt(s, 10, 64)
+bool parse_int64(const std::string& s, int64_t* out) {
+  if (s.empty()) return false;
+  size_t i = (s[0] == '+' || s[0] == '-') ? 1 : 0;
+  if (i == s.size()) return false;
+  const bool neg = s[0] == '-';
+  unsigned long long v = 0;
+  const unsigned long long lim = neg ? (1ull << 63) : (1ull << 63) - 1;
+  for (; i < s.size(); i++) {
+    const char ch = s[i];
+    if (ch < '0' || ch > '9') return false;
+    const unsigned d = ch - '0';
+    if (v > (lim - d) / 10) return false;
+    v = v * 10 + d;
+  }
+  *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+  return true;
+}
+
+// Go math.Log (src/math/log.go; FreeBSD e_log.c).  Built with
+// -ffp-contract=off: Go on amd64 does not fuse.
+double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (std::isnan(x) || (std::isinf(x) && x > 0)) return x;
+  if (x < 0) return std::nan("");
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = std::frexp(x, &ki);
+  if (f1 < std::sqrt(2.0) / 2) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1, k = (double)ki;
+  const double s = f / (2 + f), s2 = s * s, s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2, hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+int32_t s32(uint64_t x) { return (int32_t)(uint32_t)(x & 0xffffffffu); }
+
+// ---- object model (copies of the views) --------------------------------------
+using StrMap = std::map<std::string, std::string>;
+using ResMap = std::map<std::string, int64_t>;
+
+struct Req {
+  std::string key, op;
+  std::vector<std::string> values;
+};
+struct Sel {
+  bool set = false;
+  std::vector<std::pair<std::string, std::string>> labels;
+  std::vector<Req> expr;
+  bool empty() const { return labels.empty() && expr.empty(); }
+};
+struct Term {
+  std::vector<Req> expr, fields;
+};
+struct PrefTerm {
+  int32_t weight;
+  Term pref;
+};
+struct AffTerm {
+  int32_t weight;
+  Sel sel;
+  std::string key;
+  std::vector<std::string> ns;
+  Sel ns_sel;
+};
+struct Spread {
+  int32_t skew, min_domains;
+  std::string key, when, nap, ntp;
+  Sel sel;
+  std::vector<std::string> mlk;
+};
+struct Container {
+  std::string image;
+  ResMap req;
+  bool restartable;
+  int32_t host_ports;
+};
+struct Taint {
+  std::string key, value, effect;
+  bool operator<(const Taint& o) const { return std::tie(key, value, effect) < std::tie(o.key, o.value, o.effect); }
+};
+struct Tol {
+  std::string key, op, value, effect;
+  // v1.Toleration.ToleratesTaint
+  bool tolerates(const Taint& t) const {
+    if (!effect.empty() && effect != t.effect) return false;
+    if (!key.empty() && key != t.key) return false;
+    if (op.empty() || op == "Equal") return value == t.value;
+    return op == "Exists";
+  }
+};
+struct Image {
+  std::vector<std::string> names;
+  int64_t size;
+};
+struct Node {
+  std::string name;
+  StrMap labels;
+  std::vector<Taint> taints;
+  ResMap alloc;
+  bool unsched;
+  std::vector<Image> images;
+};
+struct Pod {
+  std::string ns, name, node_name;
+  StrMap labels;
+  std::vector<Container> containers, init;
+  bool has_overhead;
+  ResMap overhead;
+  bool has_node_selector, has_na_req, has_na_pref;
+  StrMap node_selector;
+  std::vector<Term> na_req;
+  std::vector<PrefTerm> na_pref;
+  std::vector<AffTerm> aff_req, aff_pref, anti_req, anti_pref;
+  std::vector<Tol> tols;
+  std::vector<Spread> spread;
+  Sel default_sel;
+  bool terminating;
+  int32_t priority;
+};
+
+std::vector<Req> copy_reqs(int32_t n, const ksg_requirement_view* v) {
+  std::vector<Req> out;
+  for (int32_t i = 0; i < n; i++) {
+    Req r{S(v[i].key), S(v[i].op), {}};
+    for (int32_t k = 0; k < v[i].n_values; k++) r.values.push_back(S(v[i].values[k]));
+    out.push_back(std::move(r));
+  }
+  return out;
+}
+Sel copy_sel(const ksg_label_selector_view& v) {
+  Sel s;
+  s.set = v.is_set != 0;
+  if (!s.set) return s;
+  for (int32_t i = 0; i < v.n_labels; i++) s.labels.emplace_back(S(v.match_labels[i].key), S(v.match_labels[i].value));
+  s.expr = copy_reqs(v.n_expr, v.expr);
+  return s;
+}
+Term copy_term(const ksg_node_selector_term_view& v) {
+  return Term{copy_reqs(v.n_expr, v.expr), copy_reqs(v.n_fields, v.fields)};
+}
+StrMap copy_pairs(int32_t n, const ksg_str_pair* p) {
+  StrMap m;
+  for (int32_t i = 0; i < n; i++) m[S(p[i].key)] = S(p[i].value);
+  return m;
+}
+ResMap copy_res(int32_t n, const ksg_quantity* q) {
+  ResMap m;
+  for (int32_t i = 0; i < n; i++) m[S(q[i].name)] = q[i].value;
+  return m;
+}
+std::vector<AffTerm> copy_aff(int32_t n, const ksg_affinity_term_view* v) {
+  std::vector<AffTerm> out;
+  for (int32_t i = 0; i < n; i++) {
+    AffTerm t;
+    t.weight = v[i].weight;
+    t.sel = copy_sel(v[i].selector);
+    t.key = S(v[i].topology_key);
+    for (int32_t k = 0; k < v[i].n_namespaces; k++) t.ns.push_back(S(v[i].namespaces[k]));
+    t.ns_sel = copy_sel(v[i].namespace_selector);
+    out.push_back(std::move(t));
+  }
+  return out;
+}
+std::vector<Container> copy_containers(int32_t n, const ksg_container_view* v) {
+  std::vector<Container> out;
+  for (int32_t i = 0; i < n; i++)
+    out.push_back(Container{S(v[i].image), copy_res(v[i].n_requests, v[i].requests), v[i].restartable != 0,
+                            v[i].n_host_ports});
+  return out;
+}
+
+// ---- resourcehelper.PodRequests -------------------------------------------------
+void add_to(ResMap& d, const ResMap& s) {
+  for (auto& kv : s) d[kv.first] += kv.second;
+}
+void max_to(ResMap& d, const ResMap& s) {
+  for (auto& kv : s) {
+    auto it = d.find(kv.first);
+    if (it == d.end() || kv.second > it->second) d[kv.first] = kv.second;
+  }
+}
+ResMap non_missing(const ResMap& r, bool nz) {
+  ResMap cp = r;
+  if (nz) {
+    if (!r.count(kCPU)) cp[kCPU] += kDefaultMilliCPU;
+    if (!r.count(kMemory)) cp[kMemory] += kDefaultMemory;
+  }
+  return cp;
+}
+ResMap pod_requests(const Pod& p, bool nz) {
+  ResMap reqs, restartable, init_reqs;
+  for (auto& c : p.containers) add_to(reqs, non_missing(c.req, nz));
+  for (auto& c : p.init) {
+    ResMap cr = non_missing(c.req, nz);
+    if (c.restartable) {
+      add_to(reqs, cr);
+      add_to(restartable, cr);
+      cr = restartable;
+    } else {
+      ResMap tmp;
+      add_to(tmp, cr);
+      add_to(tmp, restartable);
+      cr = tmp;
+    }
+    max_to(init_reqs, cr);
+  }
+  max_to(reqs, init_reqs);
+  if (p.has_overhead) add_to(reqs, p.overhead);
+  return reqs;
+}
+
+std::string normalized_image(std::string n) {
+  const auto c = n.rfind(':'), s = n.rfind('/');
+  const long ci = c == std::string::npos ? -1 : (long)c, si = s == std::string::npos ? -1 : (long)s;
+  if (ci <= si) n += ":latest";
+  return n;
+}
+
+// ---- canonical selectors (encoder.canon_selector) ---------------------------------
+using CReq = std::tuple<std::string, int, std::vector<std::string>>;
+using Canon = std::optional<std::vector<CReq>>;   // nullopt = labels.Nothing()
+
+struct EncodeError {
+  int code;
+  std::string msg;
+};
+
+Canon canon_selector(const Sel& ls, const StrMap* extra = nullptr) {
+  if (!ls.set) return std::nullopt;
+  std::set<CReq> reqs;
+  for (auto& kv : ls.labels) reqs.insert(CReq{kv.first, OP_IN, {kv.second}});
+  for (auto& r : ls.expr) {
+    const int op = op_code(r.op);
+    if (op < 0) throw EncodeError{KSG_E_INVALID, "label selector operator " + r.op};
+    std::set<std::string> vs(r.values.begin(), r.values.end());
+    reqs.insert(CReq{r.key, op, std::vector<std::string>(vs.begin(), vs.end())});
+  }
+  if (extra)
+    for (auto& kv : *extra) reqs.insert(CReq{kv.first, OP_IN, {kv.second}});
+  return std::vector<CReq>(reqs.begin(), reqs.end());
+}
+
+bool selector_matches(const Canon& c, const StrMap& labels) {
+  if (!c) return false;
+  for (auto& r : *c) {
+    const auto it = labels.find(std::get<0>(r));
+    const bool has = it != labels.end();
+    const auto& vals = std::get<2>(r);
+    switch (std::get<1>(r)) {
+      case OP_IN:
+        if (!has || !std::binary_search(vals.begin(), vals.end(), it->second)) return false;
+        break;
+      case OP_NOT_IN:
+        if (has && std::binary_search(vals.begin(), vals.end(), it->second)) return false;
+        break;
+      case OP_EXISTS:
+        if (!has) return false;
+        break;
+      case OP_DNE:
+        if (has) return false;
+        break;
+      default:
+        return false;
+    }
+  }
+  return true;
+}
+
+// framework.AffinityTerm scope: (selector, namespaces, all namespaces)
+struct Scope {
+  Canon canon;
+  std::vector<std::string> ns;
+  bool ns_all;
+  bool operator<(const Scope& o) const { return std::tie(canon, ns, ns_all) < std::tie(o.canon, o.ns, o.ns_all); }
+  bool operator==(const Scope& o) const { return canon == o.canon && ns == o.ns && ns_all == o.ns_all; }
+  bool ns_match(const std::string& n) const { return ns_all || std::binary_search(ns.begin(), ns.end(), n); }
+};
+
+Scope term_scope(const AffTerm& t, const Pod& owner) {
+  if (t.ns_sel.set && !t.ns_sel.empty())
+    throw EncodeError{KSG_E_UNSUPPORTED, "namespaceSelector with requirements is not modelled"};
+  Scope s;
+  s.canon = canon_selector(t.sel);
+  s.ns_all = t.ns_sel.set;
+  std::set<std::string> ns(t.ns.begin(), t.ns.end());
+  s.ns.assign(ns.begin(), ns.end());
+  if (t.ns.empty() && !t.ns_sel.set) s.ns = {owner.ns};
+  return s;
+}
+
+// (max_skew, key, canon, min_domains, na_honor, nt_honor)
+struct Constraint {
+  int32_t skew;
+  std::string key;
+  Canon canon;
+  int32_t min_domains;
+  bool na_honor, nt_honor;
+};
+
+// ---- the encoded snapshot ---------------------------------------------------------
+struct Encoded {
+  std::vector<std::string> res_names, label_cols;
+  std::map<std::string, int> res_col, col_index;
+  std::vector<std::map<std::string, int32_t>> vocab;   // per label column
+  std::vector<Taint> taint_vocab;
+  std::map<Taint, int> taint_id;
+  std::vector<std::string> image_vocab;
+  std::map<std::string, int> image_id;
+  std::map<std::string, std::pair<int64_t, int64_t>> image_state;   // name -> (size, numNodes)
+  int max_taints = 1, max_images = 1, tol_words = 1;
+  // topology universe
+  std::map<std::pair<std::vector<CReq>, std::string>, int> pts_sel;
+  std::vector<std::pair<std::vector<CReq>, std::string>> pts_order;
+  std::map<std::vector<Scope>, int> ipa_sel;   // ids offset by n_pts
+  std::vector<std::vector<Scope>> ipa_order;
+  std::map<std::tuple<int, Scope, int>, int> templates;
+  std::vector<std::tuple<int, Scope, int>> tmpl_order;
+  int n_selectors = 0;
+  // arrays
+  std::vector<int64_t> alloc, requested, nonzero, label_num;
+  std::vector<int32_t> allowed, pod_count;
+  std::vector<uint8_t> unsched, label_num_ok, taint_effect, col_unique;
+  std::vector<uint32_t> label_val, taints, images;
+  std::vector<int32_t> col_vocab, tmpl_col, tmpl_kind, tmpl_weight;
+  std::vector<double> log_table;
+  std::vector<ksg_pod> pods;
+  std::vector<int32_t> prog;            // program pool (the views hand out {0} when empty)
+  std::map<int, std::vector<std::string>> prefilter_names;
+  std::vector<std::string> taint_strings;
+  ksg_profile prof{};
+  int N = 0;
+};
+
+struct Profile {
+  std::vector<std::pair<std::string, int32_t>> plugins;
+  std::string fit_strategy;
+  std::vector<std::pair<std::string, int64_t>> fit_res, ba_res;
+  std::set<std::string> ignored, ignored_groups;
+  int32_t hard_weight;
+  bool ignore_pref, pts_system, ba_skip_be;
+  std::vector<int> enabled;   // plugin ids in MultiPoint order
+};
+
+}  // namespace
+
+struct ksg_snapshot {
+  std::string err;
+  Profile prof;
+  std::vector<Node> nodes;
+  std::map<std::string, int> node_index;
+  std::vector<Pod> pods;
+  std::vector<std::pair<int32_t, int32_t>> binds;   // (pod, node) in order: bound, then assumed
+  Encoded e;
+  bool encoded = false;     // e reflects nodes and pods [0, n_encoded)
+  int n_encoded = 0;
+  int epoch = 0;                    // bumped by every full encode
+  ksg_ctx* loaded_ctx = nullptr;   // the context e was last loaded into
+  int loaded_epoch = -1;            // the encoding that context holds
+  int n_loaded = 0;                 // pods on that context's workload
+  size_t prog_loaded = 0;           // program words on that context
+  // per-pod encode caches (full encode)
+  std::vector<std::pair<std::vector<Constraint>, std::vector<Constraint>>> pts_cache;
+  std::vector<std::vector<int>> pod_selectors;
+  std::vector<std::vector<std::pair<int, int>>> owned_templates;
+  std::vector<std::array<std::vector<int>, 3>> tmpl_match;
+  std::vector<std::pair<ResMap, ResMap>> req_cache;
+  // views handed out
+  std::vector<const char*> v_nodes, v_res, v_taints;
+};
+
+namespace {
+
+int fail(ksg_snapshot* s, int code, const std::string& m) {
+  if (s) s->err = m;
+  return code;
+}
+
+// PodTopologySpread constraints of a pod (encoder._pts_constraints)
+std::pair<std::vector<Constraint>, std::vector<Constraint>> pts_constraints(const Pod& p, const Profile& prof) {
+  std::vector<Constraint> hard, soft;
+  if (!p.spread.empty()) {
+    for (auto& c : p.spread) {
+      StrMap extra;
+      for (auto& k : c.mlk) {
+        auto it = p.labels.find(k);
+        if (it != p.labels.end()) extra[k] = it->second;
+      }
+      Constraint ent{c.skew, c.key, canon_selector(c.sel, extra.empty() ? nullptr : &extra),
+                     c.min_domains > 0 ? c.min_domains : 1, c.nap.empty() || c.nap == "Honor",
+                     !c.ntp.empty() && c.ntp == "Honor"};
+      if (c.when == "DoNotSchedule") hard.push_back(ent);
+      else if (c.when == "ScheduleAnyway") soft.push_back(ent);
+    }
+  } else if (prof.pts_system && p.default_sel.set) {
+    Canon canon = canon_selector(p.default_sel);
+    if (canon && !canon->empty()) {
+      soft.push_back(Constraint{3, kHostname, canon, 1, true, false});
+      soft.push_back(Constraint{5, kZone, canon, 1, true, false});
+    }
+  }
+  return {hard, soft};
+}
+
+// Encoding context of one pass: full (may extend the universe) or frozen
+// (an appended pod: any new column / value / selector / template sets miss).
+struct Pass {
+  ksg_snapshot* s;
+  bool frozen;
+  bool miss = false;
+  Encoded& e() { return s->e; }
+
+  int col(const std::string& key) {
+    auto it = e().col_index.find(key);
+    if (it == e().col_index.end()) {
+      miss = true;
+      return 0;
+    }
+    return it->second;
+  }
+  int32_t value_id(int c, const std::string& v) {
+    auto& voc = e().vocab[c];
+    auto it = voc.find(v);
+    if (it != voc.end()) return it->second;
+    if (frozen) {
+      miss = true;
+      return 0;
+    }
+    const int32_t id = (int32_t)voc.size() + 1;
+    voc[v] = id;
+    return id;
+  }
+  void emit(std::vector<int32_t>& out, const std::vector<int32_t>& w) { out.insert(out.end(), w.begin(), w.end()); }
+
+  std::vector<int32_t> requirement(const Req& r, bool field) {
+    int c;
+    if (field) {
+      if (r.key != kObjectName || (r.op != "In" && r.op != "NotIn") || r.values.size() != 1) return {0, OP_NEVER, 0};
+      c = col(kObjectName);
+    } else {
+      c = col(r.key);
+    }
+    if (miss) return {0, OP_NEVER, 0};
+    const int op = op_code(r.op);
+    if (op < 0) return {0, OP_NEVER, 0};
+    if (op == OP_IN || op == OP_NOT_IN) {
+      if (r.values.empty()) return {0, OP_NEVER, 0};
+      std::set<int32_t> ids;
+      for (auto& v : r.values) ids.insert(value_id(c, v));
+      std::vector<int32_t> out = {c, op, (int32_t)ids.size()};
+      out.insert(out.end(), ids.begin(), ids.end());
+      return out;
+    }
+    if (op == OP_EXISTS || op == OP_DNE) {
+      if (!r.values.empty()) return {0, OP_NEVER, 0};
+      return {c, op, 0};
+    }
+    int64_t v;
+    if (r.values.size() != 1 || !parse_int64(r.values[0], &v)) return {0, OP_NEVER, 0};
+    const uint64_t u = (uint64_t)v;
+    return {c, op, 2, s32(u), s32(u >> 32)};
+  }
+  std::vector<int32_t> term(const Term& t) {
+    std::vector<std::vector<int32_t>> reqs;
+    for (auto& r : t.expr) reqs.push_back(requirement(r, false));
+    for (auto& r : t.fields) reqs.push_back(requirement(r, true));
+    std::vector<int32_t> out = {(int32_t)reqs.size()};
+    for (auto& r : reqs) emit(out, r);
+    return out;
+  }
+};
+
+// ---- universe (full encode) ---------------------------------------------------
+void build_resources(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  std::set<std::string> scal;
+  for (auto& n : s->nodes)
+    for (auto& kv : n.alloc)
+      if (is_scalar(kv.first)) scal.insert(kv.first);
+  s->req_cache.clear();
+  for (auto& p : s->pods) {
+    s->req_cache.emplace_back(pod_requests(p, false), pod_requests(p, true));
+    for (auto& kv : s->req_cache.back().first)
+      if (is_scalar(kv.first)) scal.insert(kv.first);
+  }
+  for (auto& r : s->prof.fit_res)
+    if (is_scalar(r.first)) scal.insert(r.first);
+  for (auto& r : s->prof.ba_res)
+    if (is_scalar(r.first)) scal.insert(r.first);
+  e.res_names = {kCPU, kMemory, kEphemeral};
+  e.res_names.insert(e.res_names.end(), scal.begin(), scal.end());
+  if ((int)e.res_names.size() > KSG_MAX_RES)
+    throw EncodeError{KSG_E_UNSUPPORTED, "more than " + std::to_string(KSG_MAX_RES) + " resource columns"};
+  e.res_col.clear();
+  for (size_t i = 0; i < e.res_names.size(); i++) e.res_col[e.res_names[i]] = (int)i;
+}
+
+void build_label_columns(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  std::set<std::string> keys;
+  bool name_field = false;
+  s->pts_cache.clear();
+  for (auto& p : s->pods) {
+    if (p.has_node_selector)
+      for (auto& kv : p.node_selector) keys.insert(kv.first);
+    if (p.has_na_req)
+      for (auto& t : p.na_req) {
+        for (auto& r : t.expr) keys.insert(r.key);
+        name_field |= !t.fields.empty();
+      }
+    if (p.has_na_pref)
+      for (auto& pt : p.na_pref) {
+        for (auto& r : pt.pref.expr) keys.insert(r.key);
+        name_field |= !pt.pref.fields.empty();
+      }
+    s->pts_cache.push_back(pts_constraints(p, s->prof));
+    for (auto& c : s->pts_cache.back().first) keys.insert(c.key);
+    for (auto& c : s->pts_cache.back().second) keys.insert(c.key);
+    for (auto* v : {&p.aff_req, &p.anti_req, &p.aff_pref, &p.anti_pref})
+      for (auto& t : *v) keys.insert(t.key);
+  }
+  e.label_cols.assign(keys.begin(), keys.end());
+  if (name_field) e.label_cols.push_back(kObjectName);
+  e.col_index.clear();
+  for (size_t i = 0; i < e.label_cols.size(); i++) e.col_index[e.label_cols[i]] = (int)i;
+  const size_t L = e.label_cols.size(), N = s->nodes.size(), Lr = std::max<size_t>(L, 1);
+  e.vocab.assign(L, std::map<std::string, int32_t>{{"", 1}});
+  e.label_val.assign(Lr * N, 0);
+  e.label_num.assign(Lr * N, 0);
+  e.label_num_ok.assign(Lr * N, 0);
+  for (size_t c = 0; c < L; c++) {
+    auto& voc = e.vocab[c];
+    const std::string& key = e.label_cols[c];
+    for (size_t i = 0; i < N; i++) {
+      const Node& n = s->nodes[i];
+      std::string v;
+      if (key == kObjectName) {
+        v = n.name;
+      } else {
+        auto it = n.labels.find(key);
+        if (it == n.labels.end()) continue;
+        v = it->second;
+      }
+      auto vt = voc.find(v);
+      int32_t vid;
+      if (vt == voc.end()) {
+        vid = (int32_t)voc.size() + 1;
+        voc[v] = vid;
+      } else {
+        vid = vt->second;
+      }
+      e.label_val[c * N + i] = (uint32_t)vid;
+      int64_t num;
+      if (parse_int64(v, &num)) {
+        e.label_num[c * N + i] = num;
+        e.label_num_ok[c * N + i] = 1;
+      }
+    }
+  }
+}
+
+void build_taints(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  e.taint_vocab.clear();
+  e.taint_id.clear();
+  for (auto& n : s->nodes)
+    for (auto& t : n.taints)
+      if (!e.taint_id.count(t)) {
+        e.taint_id[t] = (int)e.taint_vocab.size();
+        e.taint_vocab.push_back(t);
+      }
+  size_t mt = 1;
+  for (auto& n : s->nodes) mt = std::max(mt, n.taints.size());
+  e.max_taints = (int)mt;
+  const size_t N = s->nodes.size();
+  e.taints.assign(mt * N, 0);
+  for (size_t i = 0; i < N; i++)
+    for (size_t k = 0; k < s->nodes[i].taints.size(); k++)
+      e.taints[k * N + i] = (uint32_t)e.taint_id[s->nodes[i].taints[k]] + 1;
+  e.taint_effect.clear();
+  for (auto& t : e.taint_vocab) e.taint_effect.push_back((uint8_t)effect_code(t.effect));
+  if (e.taint_effect.empty()) e.taint_effect.push_back(0);
+  e.tol_words = std::max<int>(1, ((int)e.taint_vocab.size() + 31) / 32);
+  e.taint_strings.clear();
+  for (auto& t : e.taint_vocab) e.taint_strings.push_back("{" + t.key + ": " + t.value + "}");
+}
+
+void build_images(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  std::map<std::string, int64_t> first;
+  std::map<std::string, std::set<std::string>> with;
+  for (auto& n : s->nodes)
+    for (auto& img : n.images)
+      for (auto& nm : img.names) {
+        if (!first.count(nm)) first[nm] = img.size;
+        with[nm].insert(n.name);
+      }
+  e.image_vocab.clear();
+  e.image_id.clear();
+  e.image_state.clear();
+  for (auto& kv : first) {
+    e.image_id[kv.first] = (int)e.image_vocab.size();
+    e.image_vocab.push_back(kv.first);
+    e.image_state[kv.first] = {kv.second, (int64_t)with[kv.first].size()};
+  }
+  const size_t N = s->nodes.size();
+  std::vector<std::vector<uint32_t>> per(N);
+  size_t mi = 1;
+  for (size_t i = 0; i < N; i++) {
+    std::set<int> ids;
+    for (auto& img : s->nodes[i].images)
+      for (auto& nm : img.names) ids.insert(e.image_id[nm]);
+    for (int id : ids) per[i].push_back((uint32_t)id + 1);
+    mi = std::max(mi, per[i].size());
+  }
+  e.max_images = (int)mi;
+  e.images.assign(mi * N, 0);
+  for (size_t i = 0; i < N; i++)
+    for (size_t k = 0; k < per[i].size(); k++) e.images[k * N + i] = per[i][k];
+}
+
+// encoder._PodIndex: (key, value) -> pods, to match selectors without a
+// pods x selectors scan; returns matching pods in ascending order.
+struct PodIndex {
+  const std::vector<Pod>& pods;
+  std::map<std::pair<std::string, std::string>, std::vector<int>> by_kv;
+  explicit PodIndex(const std::vector<Pod>& p) : pods(p) {
+    for (size_t i = 0; i < p.size(); i++)
+      for (auto& kv : p[i].labels) by_kv[{kv.first, kv.second}].push_back((int)i);
+  }
+  template <typename Pred>
+  std::vector<int> matching(const Canon& canon, Pred pred) const {
+    std::vector<int> out;
+    if (!canon) return out;
+    std::vector<int> tmp, best_store;
+    bool have = false;
+    for (auto& r : *canon) {
+      if (std::get<1>(r) != OP_IN) continue;
+      tmp.clear();
+      for (auto& v : std::get<2>(r)) {
+        auto it = by_kv.find({std::get<0>(r), v});
+        if (it != by_kv.end()) tmp.insert(tmp.end(), it->second.begin(), it->second.end());
+      }
+      if (!have || tmp.size() < best_store.size()) {
+        best_store = tmp;
+        have = true;
+      }
+    }
+    if (have) {
+      std::sort(best_store.begin(), best_store.end());
+      best_store.erase(std::unique(best_store.begin(), best_store.end()), best_store.end());
+      for (int i : best_store)
+        if (pred(pods[i]) && selector_matches(canon, pods[i].labels)) out.push_back(i);
+    } else {
+      for (size_t i = 0; i < pods.size(); i++)
+        if (pred(pods[i]) && selector_matches(canon, pods[i].labels)) out.push_back((int)i);
+    }
+    return out;
+  }
+};
+
+void build_topology_universe(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  const size_t P = s->pods.size();
+  e.pts_sel.clear();
+  e.pts_order.clear();
+  e.ipa_sel.clear();
+  e.ipa_order.clear();
+  e.templates.clear();
+  e.tmpl_order.clear();
+  s->owned_templates.assign(P, {});
+  for (size_t i = 0; i < P; i++) {
+    const Pod& p = s->pods[i];
+    auto& hs = s->pts_cache[i];
+    for (auto* lst : {&hs.first, &hs.second})
+      for (auto& c : *lst)
+        if (c.canon && !c.canon->empty()) {
+          auto key = std::make_pair(*c.canon, p.ns);
+          if (!e.pts_sel.count(key)) {
+            e.pts_sel[key] = (int)e.pts_order.size();
+            e.pts_order.push_back(key);
+          }
+        }
+    auto add_ipa = [&](std::vector<Scope> conj) {
+      if (!e.ipa_sel.count(conj)) {
+        e.ipa_sel[conj] = (int)e.ipa_order.size();
+        e.ipa_order.push_back(conj);
+      }
+    };
+    if (!p.aff_req.empty()) {
+      std::vector<Scope> conj;
+      for (auto& t : p.aff_req) conj.push_back(term_scope(t, p));
+      add_ipa(conj);
+    }
+    for (auto& t : p.anti_req) add_ipa({term_scope(t, p)});
+    for (auto& t : p.aff_pref) add_ipa({term_scope(t, p)});
+    for (auto& t : p.anti_pref) add_ipa({term_scope(t, p)});
+    auto own = [&](int kind, const AffTerm& t, int wt) {
+      auto key = std::make_tuple(kind, term_scope(t, p), e.col_index.at(t.key));
+      auto it = e.templates.find(key);
+      int tid;
+      if (it == e.templates.end()) {
+        tid = (int)e.tmpl_order.size();
+        e.templates[key] = tid;
+        e.tmpl_order.push_back(key);
+      } else {
+        tid = it->second;
+      }
+      s->owned_templates[i].emplace_back(tid, wt);
+    };
+    for (auto& t : p.anti_req) own(TMPL_REQ_ANTI, t, 1);
+    for (auto& t : p.aff_req) own(TMPL_REQ_AFF, t, 1);
+    for (auto& t : p.aff_pref) own(TMPL_PREF, t, t.weight);
+    for (auto& t : p.anti_pref) own(TMPL_PREF, t, -t.weight);
+  }
+  const int n_pts = (int)e.pts_order.size();
+  for (auto& kv : e.ipa_sel) kv.second += n_pts;
+  e.n_selectors = n_pts + (int)e.ipa_order.size();
+  PodIndex idx(s->pods);
+  s->pod_selectors.assign(P, {});
+  for (size_t k = 0; k < e.pts_order.size(); k++) {
+    const auto& key = e.pts_order[k];
+    const std::string& ns = key.second;
+    for (int j : idx.matching(Canon(key.first), [&](const Pod& q) { return q.ns == ns && !q.terminating; }))
+      s->pod_selectors[j].push_back((int)k);
+  }
+  for (size_t k = 0; k < e.ipa_order.size(); k++) {
+    const auto& conj = e.ipa_order[k];
+    std::vector<int> cand;
+    bool first = true;
+    for (auto& sc : conj) {
+      std::vector<int> mt = idx.matching(sc.canon, [&](const Pod& q) { return sc.ns_match(q.ns); });
+      if (first) {
+        cand = mt;
+        first = false;
+      } else {
+        std::vector<int> inter;
+        std::set_intersection(cand.begin(), cand.end(), mt.begin(), mt.end(), std::back_inserter(inter));
+        cand = inter;
+      }
+    }
+    for (int j : cand) s->pod_selectors[j].push_back(n_pts + (int)k);
+  }
+  s->tmpl_match.assign(P, {});
+  for (size_t t = 0; t < e.tmpl_order.size(); t++) {
+    const int kind = std::get<0>(e.tmpl_order[t]);
+    const Scope& sc = std::get<1>(e.tmpl_order[t]);
+    for (int j : idx.matching(sc.canon, [&](const Pod& q) { return sc.ns_match(q.ns); }))
+      s->tmpl_match[j][kind].push_back((int)t);
+  }
+  const size_t T = std::max<size_t>(e.tmpl_order.size(), 1);
+  e.tmpl_col.assign(T, 0);
+  e.tmpl_kind.assign(T, 0);
+  e.tmpl_weight.assign(T, 0);
+  for (size_t t = 0; t < e.tmpl_order.size(); t++) {
+    e.tmpl_col[t] = std::get<2>(e.tmpl_order[t]);
+    e.tmpl_kind[t] = std::get<0>(e.tmpl_order[t]);
+    e.tmpl_weight[t] = 1;   // unused: per-term weights ride in the owners' commit programs
+  }
+}
+
+// Selector / template membership of one pod against the current universe
+// (the incremental path: the full pass computes it with the pod index).
+void match_pod(ksg_snapshot* s, int i) {
+  Encoded& e = s->e;
+  const Pod& q = s->pods[i];
+  const int n_pts = (int)e.pts_order.size();
+  std::vector<int> sels;
+  for (size_t k = 0; k < e.pts_order.size(); k++)
+    if (q.ns == e.pts_order[k].second && !q.terminating && selector_matches(Canon(e.pts_order[k].first), q.labels))
+      sels.push_back((int)k);
+  for (size_t k = 0; k < e.ipa_order.size(); k++) {
+    bool all = true;
+    for (auto& sc : e.ipa_order[k]) all = all && sc.ns_match(q.ns) && selector_matches(sc.canon, q.labels);
+    if (all) sels.push_back(n_pts + (int)k);
+  }
+  s->pod_selectors[i] = sels;
+  std::array<std::vector<int>, 3> tm;
+  for (size_t t = 0; t < e.tmpl_order.size(); t++) {
+    const Scope& sc = std::get<1>(e.tmpl_order[t]);
+    if (sc.ns_match(q.ns) && selector_matches(sc.canon, q.labels)) tm[std::get<0>(e.tmpl_order[t])].push_back((int)t);
+  }
+  s->tmpl_match[i] = tm;
+}
+
+// Universe lookups of an appended pod (no insertion): owned templates,
+// PodTopologySpread constraints; sets pass.miss when the pod would extend it.
+void prepare_frozen(ksg_snapshot* s, int i, Pass& ps) {
+  Encoded& e = s->e;
+  const Pod& p = s->pods[i];
+  s->req_cache.emplace_back(pod_requests(p, false), pod_requests(p, true));
+  for (auto& kv : s->req_cache.back().first)
+    if (is_scalar(kv.first) && !e.res_col.count(kv.first)) ps.miss = true;
+  s->pts_cache.push_back(pts_constraints(p, s->prof));
+  auto& hs = s->pts_cache.back();
+  for (auto* lst : {&hs.first, &hs.second})
+    for (auto& c : *lst) {
+      if (!e.col_index.count(c.key)) ps.miss = true;
+      if (c.canon && !c.canon->empty() && !e.pts_sel.count({*c.canon, p.ns})) ps.miss = true;
+    }
+  auto has_ipa = [&](const std::vector<Scope>& conj) {
+    if (!e.ipa_sel.count(conj)) ps.miss = true;
+  };
+  if (!p.aff_req.empty()) {
+    std::vector<Scope> conj;
+    for (auto& t : p.aff_req) conj.push_back(term_scope(t, p));
+    has_ipa(conj);
+  }
+  for (auto* v : {&p.anti_req, &p.aff_pref, &p.anti_pref})
+    for (auto& t : *v) has_ipa({term_scope(t, p)});
+  std::vector<std::pair<int, int>> owned;
+  auto own = [&](int kind, const AffTerm& t, int wt) {
+    auto ct = e.col_index.find(t.key);
+    if (ct == e.col_index.end()) {
+      ps.miss = true;
+      return;
+    }
+    auto it = e.templates.find(std::make_tuple(kind, term_scope(t, p), ct->second));
+    if (it == e.templates.end()) {
+      ps.miss = true;
+      return;
+    }
+    owned.emplace_back(it->second, wt);
+  };
+  for (auto& t : p.anti_req) own(TMPL_REQ_ANTI, t, 1);
+  for (auto& t : p.aff_req) own(TMPL_REQ_AFF, t, 1);
+  for (auto& t : p.aff_pref) own(TMPL_PREF, t, t.weight);
+  for (auto& t : p.anti_pref) own(TMPL_PREF, t, -t.weight);
+  if (p.has_node_selector)
+    for (auto& kv : p.node_selector)
+      if (!e.col_index.count(kv.first)) ps.miss = true;
+  auto terms_ok = [&](const Term& t) {
+    for (auto& r : t.expr)
+      if (!e.col_index.count(r.key)) ps.miss = true;
+    if (!t.fields.empty() && !e.col_index.count(kObjectName)) ps.miss = true;
+  };
+  if (p.has_na_req)
+    for (auto& t : p.na_req) terms_ok(t);
+  if (p.has_na_pref)
+    for (auto& t : p.na_pref) terms_ok(t.pref);
+  s->owned_templates.push_back(owned);
+  s->pod_selectors.emplace_back();
+  s->tmpl_match.emplace_back();
+  if (!ps.miss) match_pod(s, i);
+}
+
+// ---- per-pod programs --------------------------------------------------------------
+void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
+  Encoded& e = s->e;
+  const Pod& p = s->pods[i];
+  const Profile& prof = s->prof;
+  std::vector<int32_t>& prog = e.prog;
+  for (auto& c : p.containers)
+    if (c.host_ports > 0) throw EncodeError{KSG_E_UNSUPPORTED, "hostPorts (NodePorts) are not encoded yet"};
+  const ResMap& r = s->req_cache[i].first;
+  const ResMap& nz = s->req_cache[i].second;
+  ksg_pod rec;
+  std::memset(&rec, 0, sizeof(rec));
+  for (auto& kv : r) {
+    auto it = e.res_col.find(kv.first);
+    if (it != e.res_col.end()) rec.req[it->second] = kv.second;
+  }
+  auto get = [](const ResMap& m, const std::string& k) {
+    auto it = m.find(k);
+    return it == m.end() ? (int64_t)0 : it->second;
+  };
+  rec.nz_cpu = get(nz, kCPU);
+  rec.nz_mem = get(nz, kMemory);
+  uint32_t flags = 0;
+  const Taint unsched{kUnschedTaint, "", "NoSchedule"};
+  for (auto& t : p.tols)
+    if (t.tolerates(unsched)) {
+      flags |= KSG_POD_TOL_UNSCHED;
+      break;
+    }
+  const bool na_required = p.has_node_selector || p.has_na_req;
+  if (na_required) flags |= KSG_POD_NA_REQUIRED;
+  bool best_effort = true;
+  for (auto& br : prof.ba_res)
+    if (e.res_col.count(br.first) && get(r, br.first) != 0) best_effort = false;
+  if (best_effort) flags |= KSG_POD_BEST_EFFORT;
+  uint32_t fskip = 0, sskip = 0;
+  if (!na_required) fskip |= 1u << KSG_PL_NODE_AFFINITY;
+  fskip |= 1u << KSG_PL_NODE_PORTS;
+  for (int v : {KSG_PL_VOLUME_RESTRICTIONS, KSG_PL_NODE_VOLUME_LIMITS, KSG_PL_VOLUME_BINDING, KSG_PL_VOLUME_ZONE})
+    fskip |= 1u << v;
+  const auto& hard = s->pts_cache[i].first;
+  const auto& soft = s->pts_cache[i].second;
+  if (hard.empty()) fskip |= 1u << KSG_PL_POD_TOPOLOGY_SPREAD;
+  if (soft.empty()) sskip |= 1u << KSG_PL_POD_TOPOLOGY_SPREAD;
+  if (!p.has_na_pref) sskip |= 1u << KSG_PL_NODE_AFFINITY;
+  sskip |= 1u << KSG_PL_VOLUME_BINDING;
+  if (prof.ba_skip_be && (flags & KSG_POD_BEST_EFFORT)) sskip |= 1u << KSG_PL_BALANCED_ALLOCATION;
+  const bool pref_pod_aff = !p.aff_pref.empty() || !p.anti_pref.empty();
+  if (prof.ignore_pref && !pref_pod_aff) sskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
+  // NodeAffinity PreFilter: matchFields metadata.name In -> PreFilterResult
+  rec.node_set = -1;
+  e.prefilter_names.erase(i);
+  if (p.has_na_req && !p.na_req.empty()) {
+    std::optional<std::set<std::string>> names_u;
+    bool all_named = true;
+    for (auto& term : p.na_req) {
+      std::optional<std::set<std::string>> tn;
+      for (auto& rq : term.fields)
+        if (rq.key == kObjectName && rq.op == "In") {
+          std::set<std::string> sv(rq.values.begin(), rq.values.end());
+          if (!tn) {
+            tn = sv;
+          } else {
+            std::set<std::string> inter;
+            std::set_intersection(tn->begin(), tn->end(), sv.begin(), sv.end(), std::inserter(inter, inter.begin()));
+            tn = inter;
+          }
+        }
+      if (!tn) {
+        all_named = false;
+        break;
+      }
+      if (!names_u) names_u = *tn;
+      else names_u->insert(tn->begin(), tn->end());
+    }
+    if (all_named && names_u) {
+      if (names_u->empty()) {
+        flags |= KSG_POD_PREFILTER_REJECT;
+      } else {
+        const int N = (int)s->nodes.size(), W = (N + 31) / 32;
+        std::vector<uint32_t> bits(W, 0);
+        for (auto& nm : *names_u) {
+          auto it = s->node_index.find(nm);
+          if (it != s->node_index.end()) bits[it->second / 32] |= 1u << (it->second % 32);
+        }
+        rec.node_set = (int32_t)prog.size();
+        for (uint32_t b : bits) prog.push_back((int32_t)b);
+        e.prefilter_names[i] = std::vector<std::string>(names_u->begin(), names_u->end());
+      }
+    }
+  }
+  rec.flags = flags;
+  rec.filter_skip = fskip;
+  rec.score_skip = sskip;
+  if (p.node_name.empty()) {
+    rec.node_name = -1;
+  } else {
+    auto it = s->node_index.find(p.node_name);
+    rec.node_name = it == s->node_index.end() ? -2 : it->second;
+  }
+  rec.n_containers = (int32_t)(p.containers.size() + p.init.size());
+  const int32_t blob = (int32_t)prog.size();
+  // tol := filter_bits[W] prefer_bits[W]
+  {
+    const int W = e.tol_words;
+    std::vector<uint32_t> fb(W, 0), pb(W, 0);
+    std::vector<const Tol*> pref;
+    for (auto& t : p.tols)
+      if (t.effect.empty() || t.effect == "PreferNoSchedule") pref.push_back(&t);
+    for (size_t v = 0; v < e.taint_vocab.size(); v++) {
+      const Taint& taint = e.taint_vocab[v];
+      bool f = false, pr = false;
+      for (auto& t : p.tols) f = f || t.tolerates(taint);
+      for (auto* t : pref) pr = pr || t->tolerates(taint);
+      if (f) fb[v / 32] |= 1u << (v % 32);
+      if (pr) pb[v / 32] |= 1u << (v % 32);
+    }
+    rec.tol = (int32_t)prog.size();
+    for (uint32_t x : fb) prog.push_back((int32_t)x);
+    for (uint32_t x : pb) prog.push_back((int32_t)x);
+  }
+  // na_req := n_sel requirement[n_sel] n_terms { n_reqs requirement[n_reqs] }
+  rec.na_req = -1;
+  if (na_required) {
+    std::vector<int32_t> w;
+    w.push_back((int32_t)p.node_selector.size());
+    for (auto& kv : p.node_selector) {   // std::map: sorted by key
+      const int c = ps.col(kv.first);
+      const int32_t id = ps.miss ? 0 : ps.value_id(c, kv.second);
+      w.insert(w.end(), {c, OP_IN, 1, id});
+    }
+    if (!p.has_na_req) {
+      w.push_back(-1);
+    } else {
+      w.push_back((int32_t)p.na_req.size());
+      for (auto& t : p.na_req) ps.emit(w, ps.term(t));
+    }
+    rec.na_req = (int32_t)prog.size();
+    ps.emit(prog, w);
+  }
+  // na_pref := n_terms { weight n_reqs requirement[n_reqs] }
+  rec.na_pref = -1;
+  if (p.has_na_pref) {
+    std::vector<int32_t> w = {0};
+    for (auto& pt : p.na_pref) {
+      if (pt.weight == 0 || (pt.pref.expr.empty() && pt.pref.fields.empty())) continue;
+      w[0]++;
+      w.push_back(pt.weight);
+      ps.emit(w, ps.term(pt.pref));
+    }
+    rec.na_pref = (int32_t)prog.size();
+    ps.emit(prog, w);
+  }
+  // img := n { image_id+1 contrib_lo contrib_hi }
+  {
+    std::vector<int32_t> ents;
+    const double total = (double)s->nodes.size();
+    auto one = [&](const Container& c) {
+      const std::string nm = normalized_image(c.image);
+      auto it = e.image_state.find(nm);
+      if (it == e.image_state.end()) return;
+      const int64_t contrib = (int64_t)((double)it->second.first * ((double)it->second.second / total));
+      const uint64_t u = (uint64_t)contrib;
+      ents.insert(ents.end(), {e.image_id[nm] + 1, s32(u), s32(u >> 32)});
+    };
+    for (auto& c : p.init) one(c);
+    for (auto& c : p.containers) one(c);
+    rec.img = (int32_t)prog.size();
+    prog.push_back((int32_t)(ents.size() / 3));
+    ps.emit(prog, ents);
+  }
+  // pts := n_hard n_soft require_all {hard}[..] {soft}[..]
+  rec.pts = -1;
+  if (!hard.empty() || !soft.empty()) {
+    const int require_all = (!p.spread.empty() || !prof.pts_system) ? 1 : 0;
+    std::vector<int32_t> w = {(int32_t)hard.size(), (int32_t)soft.size(), require_all};
+    auto sel_of = [&](const Canon& c) -> int32_t {
+      if (!c || c->empty()) return -1;
+      auto it = e.pts_sel.find({*c, p.ns});
+      if (it == e.pts_sel.end()) {
+        ps.miss = true;
+        return -1;
+      }
+      return it->second;
+    };
+    for (auto& c : hard) {
+      const int self = (c.canon && selector_matches(c.canon, p.labels)) ? 1 : 0;
+      w.insert(w.end(), {ps.col(c.key), sel_of(c.canon), c.skew, c.min_domains, self, c.na_honor ? 1 : 0,
+                         c.nt_honor ? 1 : 0});
+    }
+    for (auto& c : soft)
+      w.insert(w.end(), {ps.col(c.key), sel_of(c.canon), c.skew, c.na_honor ? 1 : 0, c.nt_honor ? 1 : 0,
+                         c.key == kHostname ? 1 : 0});
+    rec.pts = (int32_t)prog.size();
+    ps.emit(prog, w);
+  }
+  // ipa
+  rec.ipa = -1;
+  {
+    const auto& tm = s->tmpl_match[i];
+    const bool any = !p.aff_req.empty() || !p.anti_req.empty() || !p.aff_pref.empty() || !p.anti_pref.empty() ||
+                     !tm[0].empty() || !tm[1].empty() || !tm[2].empty();
+    if (any) {
+      std::vector<int32_t> w;
+      auto sel_id = [&](const std::vector<Scope>& conj) -> int32_t {
+        auto it = e.ipa_sel.find(conj);
+        if (it == e.ipa_sel.end()) {
+          ps.miss = true;
+          return -1;
+        }
+        return it->second;
+      };
+      if (!p.aff_req.empty()) {
+        std::vector<Scope> scopes;
+        for (auto& t : p.aff_req) scopes.push_back(term_scope(t, p));
+        bool self_all = true;
+        for (auto& sc : scopes) self_all = self_all && sc.ns_match(p.ns) && selector_matches(sc.canon, p.labels);
+        w.insert(w.end(), {(int32_t)p.aff_req.size(), sel_id(scopes), self_all ? 1 : 0});
+        for (auto& t : p.aff_req) w.push_back(ps.col(t.key));
+      } else {
+        w.insert(w.end(), {0, -1, 0});
+      }
+      w.push_back((int32_t)p.anti_req.size());
+      for (auto& t : p.anti_req) w.insert(w.end(), {ps.col(t.key), sel_id({term_scope(t, p)})});
+      w.push_back((int32_t)(p.aff_pref.size() + p.anti_pref.size()));
+      for (auto& t : p.aff_pref) w.insert(w.end(), {ps.col(t.key), sel_id({term_scope(t, p)}), t.weight});
+      for (auto& t : p.anti_pref) w.insert(w.end(), {ps.col(t.key), sel_id({term_scope(t, p)}), -t.weight});
+      for (int k = 0; k < 3; k++) {
+        w.push_back((int32_t)tm[k].size());
+        w.insert(w.end(), tm[k].begin(), tm[k].end());
+      }
+      rec.ipa = (int32_t)prog.size();
+      ps.emit(prog, w);
+    }
+  }
+  // commit := n_sel sel[n_sel] n_tmpl {tmpl weight}[n_tmpl]
+  rec.commit = -1;
+  {
+    std::vector<int> sels = s->pod_selectors[i];
+    std::sort(sels.begin(), sels.end());
+    const auto& tmo = s->owned_templates[i];
+    if (!sels.empty() || !tmo.empty()) {
+      rec.commit = (int32_t)prog.size();
+      prog.push_back((int32_t)sels.size());
+      prog.insert(prog.end(), sels.begin(), sels.end());
+      prog.push_back((int32_t)tmo.size());
+      for (auto& pr : tmo) prog.insert(prog.end(), {pr.first, pr.second});
+    }
+  }
+  rec.blob = blob;
+  rec.blob_len = (int32_t)prog.size() - blob;
+  if ((int)e.pods.size() <= i) e.pods.resize(i + 1);
+  e.pods[i] = rec;
+}
+
+// Requirement values may extend a column's vocabulary after the node columns
+// were built; ids stay below col_vocab either way.
+void finish_arrays(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  e.col_vocab.clear();
+  for (auto& v : e.vocab) e.col_vocab.push_back((int32_t)v.size() + 1);
+  if (e.col_vocab.empty()) e.col_vocab.push_back(1);
+}
+
+void encode_all(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  e = Encoded{};
+  const size_t N = s->nodes.size(), P = s->pods.size();
+  e.N = (int)N;
+  build_resources(s);
+  build_label_columns(s);
+  build_taints(s);
+  build_images(s);
+  build_topology_universe(s);
+  // node columns
+  const size_t R = e.res_names.size();
+  e.alloc.assign(R * N, 0);
+  for (size_t i = 0; i < N; i++)
+    for (auto& kv : s->nodes[i].alloc) {
+      auto it = e.res_col.find(kv.first);
+      if (it != e.res_col.end()) e.alloc[(size_t)it->second * N + i] = kv.second;
+    }
+  e.requested.assign(R * N, 0);
+  e.nonzero.assign(2 * N, 0);
+  e.allowed.assign(N, 0);
+  e.pod_count.assign(N, 0);
+  e.unsched.assign(N, 0);
+  for (size_t i = 0; i < N; i++) {
+    auto it = s->nodes[i].alloc.find(kPods);
+    e.allowed[i] = it == s->nodes[i].alloc.end() ? 0 : (int32_t)it->second;
+    e.unsched[i] = s->nodes[i].unsched ? 1 : 0;
+  }
+  const size_t Lc = e.label_cols.size();
+  e.col_unique.assign(std::max<size_t>(Lc, 1), 0);
+  for (size_t c = 0; c < Lc; c++) {
+    std::set<uint32_t> seen;
+    bool uniq = true;
+    for (size_t i = 0; i < N && uniq; i++) {
+      const uint32_t v = e.label_val[c * N + i];
+      if (v && !seen.insert(v).second) uniq = false;
+    }
+    e.col_unique[c] = uniq ? 1 : 0;
+  }
+  e.log_table.resize(N + 3);
+  for (size_t i = 0; i < N + 3; i++) e.log_table[i] = go_log((double)i);
+  // pods
+  e.pods.assign(P, ksg_pod{});
+  Pass ps{s, false};
+  for (size_t i = 0; i < P; i++) encode_pod(s, (int)i, ps);
+  finish_arrays(s);
+  s->encoded = true;
+  s->n_encoded = (int)P;
+  s->epoch++;
+}
+
+// ---- profile ---------------------------------------------------------------------
+int encode_profile(ksg_snapshot* s) {
+  const Profile& pr = s->prof;
+  Encoded& e = s->e;
+  ksg_profile& p = e.prof;
+  std::memset(&p, 0, sizeof(p));
+  std::map<std::string, int32_t> weights;
+  for (auto& pl : pr.plugins) {
+    std::string key = pl.first;
+    if (key.size() > 7 && key.compare(key.size() - 7, 7, "Wrapped") == 0) key.resize(key.size() - 7);
+    weights[key] = pl.second != 0 ? pl.second : 1;
+  }
+  for (int pid : pr.enabled)
+    if (kExt[pid][1]) p.filter_order[p.n_filter++] = pid;
+  for (int pid : pr.enabled)
+    if (kExt[pid][3]) {
+      p.score_mask |= 1u << pid;
+      auto it = weights.find(kPluginNames[pid]);
+      p.weight[pid] = it == weights.end() ? 1 : it->second;
+    }
+  p.fit_strategy = pr.fit_strategy == "MostAllocated" ? KSG_MOST_ALLOCATED : KSG_LEAST_ALLOCATED;
+  for (auto& r : pr.fit_res) {
+    auto it = e.res_col.find(r.first);
+    if (it == e.res_col.end()) continue;
+    p.fit_res[p.fit_n] = it->second;
+    p.fit_w[p.fit_n] = r.second;
+    p.fit_n++;
+  }
+  for (auto& r : pr.ba_res) {
+    auto it = e.res_col.find(r.first);
+    if (it != e.res_col.end()) p.ba_res[p.ba_n++] = it->second;
+  }
+  for (size_t c = 0; c < e.res_names.size(); c++) {
+    const std::string& r = e.res_names[c];
+    const auto slash = r.find('/');
+    if (slash == std::string::npos) continue;
+    if (pr.ignored.count(r) || pr.ignored_groups.count(r.substr(0, slash))) p.fit_ignored_res |= 1u << c;
+  }
+  p.hard_pod_affinity_weight = pr.hard_weight;
+  p.flags = (pr.ba_skip_be ? KSG_PROF_BA_SKIP_BEST_EFFORT : 0u) | (pr.ignore_pref ? KSG_PROF_IPA_IGNORE_EXISTING_PREF : 0u);
+  return KSG_OK;
+}
+
+int do_encode(ksg_snapshot* s) {
+  try {
+    encode_all(s);
+    encode_profile(s);
+  } catch (const EncodeError& x) {
+    s->encoded = false;
+    return fail(s, x.code, x.msg);
+  } catch (const std::exception& x) {
+    s->encoded = false;
+    return fail(s, KSG_E_INVALID, std::string("encode: ") + x.what());
+  }
+  return KSG_OK;
+}
+
+void fill_views(ksg_snapshot* s, ksg_nodes* nd, ksg_topology* tp, ksg_workload* wl, ksg_profile* pf) {
+  Encoded& e = s->e;
+  if (nd) {
+    *nd = ksg_nodes{};
+    nd->n_nodes = e.N;
+    nd->n_res = (int32_t)e.res_names.size();
+    nd->alloc = e.alloc.data();
+    nd->requested = e.requested.data();
+    nd->nonzero = e.nonzero.data();
+    nd->allowed_pods = e.allowed.data();
+    nd->pod_count = e.pod_count.data();
+    nd->unschedulable = e.unsched.data();
+    nd->n_label_cols = (int32_t)e.label_cols.size();
+    nd->label_val = e.label_val.data();
+    nd->label_num = e.label_num.data();
+    nd->label_num_ok = e.label_num_ok.data();
+    nd->max_taints = e.max_taints;
+    nd->taints = e.taints.data();
+    nd->n_taint_vocab = (int32_t)e.taint_vocab.size();
+    nd->taint_effect = e.taint_effect.data();
+    nd->max_images = e.max_images;
+    nd->images = e.images.data();
+    nd->n_images = (int32_t)e.image_vocab.size();
+  }
+  if (tp) {
+    *tp = ksg_topology{};
+    tp->n_selectors = e.n_selectors;
+    tp->n_templates = (int32_t)e.tmpl_order.size();
+    tp->tmpl_col = e.tmpl_col.data();
+    tp->tmpl_kind = e.tmpl_kind.data();
+    tp->tmpl_weight = e.tmpl_weight.data();
+    tp->col_vocab = e.col_vocab.data();
+    tp->col_unique = e.col_unique.data();
+    tp->log_table = e.log_table.data();
+    tp->log_n = (int32_t)e.log_table.size();
+  }
+  if (wl) {
+    *wl = ksg_workload{};
+    wl->pods = e.pods.data();
+    wl->n_pods = (int32_t)e.pods.size();
+    static const int32_t kEmpty[1] = {0};   // encoder.py: `prog or [0]`
+    wl->prog = e.prog.empty() ? kEmpty : e.prog.data();
+    wl->prog_len = std::max<int64_t>((int64_t)e.prog.size(), 1);
+  }
+  if (pf) *pf = e.prof;
+}
+
+// Encode the pods added since the last encode.  When none of them extends
+// the encoding universe (label columns, value ids, resource columns,
+// selectors, term templates) they are encoded against it and appended
+// (*appended = 1): byte-identical to a full re-encode, which is what runs
+// otherwise (*appended = 0).
+int encode_incremental(ksg_snapshot* s, int32_t* appended) {
+  if (appended) *appended = 0;
+  if (!s->encoded) return do_encode(s);
+  const int P = (int)s->pods.size();
+  if (s->n_encoded == P) {
+    if (appended) *appended = 1;
+    return KSG_OK;
+  }
+  Encoded& e = s->e;
+  const size_t prog0 = e.prog.size(), pods0 = e.pods.size(), caches0 = s->req_cache.size();
+  bool miss = false;
+  try {
+    for (int i = s->n_encoded; i < P && !miss; i++) {
+      Pass ps{s, true};
+      prepare_frozen(s, i, ps);
+      if (!ps.miss) encode_pod(s, i, ps);
+      miss = ps.miss;
+    }
+  } catch (const EncodeError& x) {
+    miss = true;
+  }
+  if (miss) {
+    e.prog.resize(prog0);
+    e.pods.resize(pods0);
+    for (auto* v : {&s->req_cache}) v->resize(caches0);
+    s->pts_cache.resize(caches0);
+    s->owned_templates.resize(caches0);
+    s->pod_selectors.resize(caches0);
+    s->tmpl_match.resize(caches0);
+    return do_encode(s);
+  }
+  finish_arrays(s);
+  s->n_encoded = P;
+  if (appended) *appended = 1;
+  return KSG_OK;
+}
+
+// Upload the current encoding and replay the bindings.
+int upload_all(ksg_snapshot* s, ksg_ctx* ctx) {
+  int rc;
+  ksg_nodes nd;
+  ksg_topology tp;
+  ksg_workload wl;
+  ksg_profile pf;
+  fill_views(s, &nd, &tp, &wl, &pf);
+  auto dev = [&](int r, const char* what) {
+    return fail(s, r, std::string(what) + ": " + ksg_last_error(ctx));
+  };
+  if ((rc = ksg_set_profile(ctx, &pf))) return dev(rc, "ksg_set_profile");
+  if ((rc = ksg_load_nodes(ctx, &nd, &tp))) return dev(rc, "ksg_load_nodes");
+  if ((rc = ksg_load_workload(ctx, &wl))) return dev(rc, "ksg_load_workload");
+  for (auto& b : s->binds)
+    if ((rc = ksg_commit(ctx, b.first, b.second))) return dev(rc, "ksg_commit (replayed binding)");
+  s->loaded_ctx = ctx;
+  s->loaded_epoch = s->epoch;
+  s->n_loaded = s->n_encoded;
+  s->prog_loaded = s->e.prog.size();
+  return KSG_OK;
+}
+
+int full_load(ksg_snapshot* s, ksg_ctx* ctx) {
+  const int rc = do_encode(s);
+  return rc ? rc : upload_all(s, ctx);
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+int ksg_snapshot_new(const ksg_profile_view* pv, ksg_snapshot** out) {
+  if (!pv || !out) return KSG_E_INVALID;
+  *out = nullptr;
+  ksg_snapshot* s = new ksg_snapshot();
+  Profile& p = s->prof;
+  for (int32_t i = 0; i < pv->n_plugins; i++) {
+    std::string name = S(pv->plugins[i].name);
+    p.plugins.emplace_back(name, pv->plugins[i].weight);
+    std::string key = name;
+    if (key.size() > 7 && key.compare(key.size() - 7, 7, "Wrapped") == 0) key.resize(key.size() - 7);
+    int pid = -1;
+    for (int k = 0; k < KSG_NPLUGINS; k++)
+      if (key == kPluginNames[k]) pid = k;
+    if (pid >= 0) {
+      p.enabled.push_back(pid);
+    } else {
+      bool known = false;
+      for (const char* n : kNonEval) known = known || key == n;
+      if (!known) {
+        delete s;
+        return KSG_E_UNSUPPORTED;   // not an in-tree Filter/Score plugin
+      }
+    }
+  }
+  p.fit_strategy = pv->fit_strategy ? S(pv->fit_strategy) : "LeastAllocated";
+  if (p.fit_strategy != "LeastAllocated" && p.fit_strategy != "MostAllocated") {
+    delete s;
+    return KSG_E_UNSUPPORTED;   // RequestedToCapacityRatio is not modelled
+  }
+  for (int32_t i = 0; i < pv->n_fit_resources; i++)
+    p.fit_res.emplace_back(S(pv->fit_resources[i].name), pv->fit_resources[i].value);
+  for (int32_t i = 0; i < pv->n_ba_resources; i++)
+    p.ba_res.emplace_back(S(pv->ba_resources[i].name), pv->ba_resources[i].value);
+  for (int32_t i = 0; i < pv->n_fit_ignored_resources; i++) p.ignored.insert(S(pv->fit_ignored_resources[i]));
+  for (int32_t i = 0; i < pv->n_fit_ignored_groups; i++) p.ignored_groups.insert(S(pv->fit_ignored_groups[i]));
+  p.hard_weight = pv->hard_pod_affinity_weight;
+  p.ignore_pref = pv->ignore_preferred_terms_of_existing_pods != 0;
+  p.pts_system = pv->pts_system_defaulted != 0;
+  p.ba_skip_be = pv->ba_skip_best_effort != 0;
+  *out = s;
+  return KSG_OK;
+}
+
+int ksg_snapshot_free(ksg_snapshot* s) {
+  delete s;
+  return KSG_OK;
+}
+
+const char* ksg_snapshot_error(ksg_snapshot* s) { return s ? s->err.c_str() : "null snapshot"; }
+
+int ksg_snapshot_add_node(ksg_snapshot* s, const ksg_node_view* v, int32_t* index) {
+  if (!s || !v || !v->name) return KSG_E_INVALID;
+  Node n;
+  n.name = v->name;
+  if (s->node_index.count(n.name)) return fail(s, KSG_E_INVALID, "duplicate node name " + n.name);
+  n.labels = copy_pairs(v->n_labels, v->labels);
+  for (int32_t i = 0; i < v->n_taints; i++)
+    n.taints.push_back(Taint{S(v->taints[i].key), S(v->taints[i].value), S(v->taints[i].effect)});
+  n.alloc = copy_res(v->n_alloc, v->allocatable);
+  n.unsched = v->unschedulable != 0;
+  for (int32_t i = 0; i < v->n_images; i++) {
+    Image im;
+    for (int32_t k = 0; k < v->images[i].n_names; k++) im.names.push_back(S(v->images[i].names[k]));
+    im.size = v->images[i].size_bytes;
+    n.images.push_back(std::move(im));
+  }
+  const int32_t idx = (int32_t)s->nodes.size();
+  s->node_index[n.name] = idx;
+  s->nodes.push_back(std::move(n));
+  s->encoded = false;
+  s->loaded_ctx = nullptr;   // the node set changed: the next sync reloads
+  if (index) *index = idx;
+  return KSG_OK;
+}
+
+int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index) {
+  if (!s || !v || !v->name) return KSG_E_INVALID;
+  Pod p;
+  p.ns = v->namespace_ ? S(v->namespace_) : "default";
+  p.name = S(v->name);
+  p.labels = copy_pairs(v->n_labels, v->labels);
+  p.containers = copy_containers(v->n_containers, v->containers);
+  p.init = copy_containers(v->n_init_containers, v->init_containers);
+  p.has_overhead = v->has_overhead != 0;
+  p.overhead = copy_res(v->n_overhead, v->overhead);
+  p.node_name = S(v->node_name);
+  p.has_node_selector = v->has_node_selector != 0;
+  p.node_selector = copy_pairs(v->n_node_selector, v->node_selector);
+  p.has_na_req = v->has_na_required != 0;
+  for (int32_t i = 0; i < v->n_na_required; i++) p.na_req.push_back(copy_term(v->na_required[i]));
+  p.has_na_pref = v->has_na_preferred != 0;
+  for (int32_t i = 0; i < v->n_na_preferred; i++)
+    p.na_pref.push_back(PrefTerm{v->na_preferred[i].weight, copy_term(v->na_preferred[i].preference)});
+  p.aff_req = copy_aff(v->n_pod_affinity_required, v->pod_affinity_required);
+  p.aff_pref = copy_aff(v->n_pod_affinity_preferred, v->pod_affinity_preferred);
+  p.anti_req = copy_aff(v->n_pod_anti_affinity_required, v->pod_anti_affinity_required);
+  p.anti_pref = copy_aff(v->n_pod_anti_affinity_preferred, v->pod_anti_affinity_preferred);
+  for (int32_t i = 0; i < v->n_tolerations; i++)
+    p.tols.push_back(Tol{S(v->tolerations[i].key), S(v->tolerations[i].op), S(v->tolerations[i].value),
+                         S(v->tolerations[i].effect)});
+  for (int32_t i = 0; i < v->n_spread; i++) {
+    const ksg_spread_view& c = v->spread[i];
+    Spread sp;
+    sp.skew = c.max_skew;
+    sp.key = S(c.topology_key);
+    sp.when = S(c.when_unsatisfiable);
+    sp.sel = copy_sel(c.selector);
+    sp.min_domains = c.min_domains;
+    sp.nap = S(c.node_affinity_policy);
+    sp.ntp = S(c.node_taints_policy);
+    for (int32_t k = 0; k < c.n_match_label_keys; k++) sp.mlk.push_back(S(c.match_label_keys[k]));
+    p.spread.push_back(std::move(sp));
+  }
+  p.default_sel = copy_sel(v->default_spread_selector);
+  p.terminating = v->terminating != 0;
+  p.priority = v->priority;
+  const int32_t idx = (int32_t)s->pods.size();
+  s->pods.push_back(std::move(p));
+  if (index) *index = idx;
+  return KSG_OK;
+}
+
+int ksg_snapshot_bind(ksg_snapshot* s, int32_t pod, int32_t node) {
+  if (!s) return KSG_E_INVALID;
+  if (pod < 0 || pod >= (int32_t)s->pods.size() || node < 0 || node >= (int32_t)s->nodes.size())
+    return fail(s, KSG_E_INVALID, "bind: index out of range");
+  s->binds.emplace_back(pod, node);
+  s->loaded_ctx = nullptr;   // bindings are replayed by the next load
+  return KSG_OK;
+}
+
+int ksg_snapshot_node_index(ksg_snapshot* s, const char* name, int32_t* index) {
+  if (!s || !name || !index) return KSG_E_INVALID;
+  auto it = s->node_index.find(name);
+  *index = it == s->node_index.end() ? -1 : it->second;
+  return KSG_OK;
+}
+
+int ksg_snapshot_encode(ksg_snapshot* s) {
+  if (!s) return KSG_E_INVALID;
+  if (s->nodes.empty()) return fail(s, KSG_E_STATE, "no nodes");
+  return do_encode(s);
+}
+
+int ksg_snapshot_view(ksg_snapshot* s, ksg_nodes* nd, ksg_topology* tp, ksg_workload* wl, ksg_profile* pf) {
+  if (!s) return KSG_E_INVALID;
+  if (!s->encoded || s->n_encoded != (int)s->pods.size())
+    return fail(s, KSG_E_STATE, "snapshot not encoded (pods added since the last encode)");
+  fill_views(s, nd, tp, wl, pf);
+  return KSG_OK;
+}
+
+int ksg_snapshot_load(ksg_snapshot* s, ksg_ctx* ctx) {
+  if (!s || !ctx) return KSG_E_INVALID;
+  if (s->nodes.empty()) return fail(s, KSG_E_STATE, "no nodes");
+  return full_load(s, ctx);
+}
+
+int ksg_snapshot_encode_incremental(ksg_snapshot* s, int32_t* appended) {
+  if (!s) return KSG_E_INVALID;
+  if (s->nodes.empty()) return fail(s, KSG_E_STATE, "no nodes");
+  return encode_incremental(s, appended);
+}
+
+int ksg_snapshot_sync(ksg_snapshot* s, ksg_ctx* ctx, int32_t* appended) {
+  if (!s || !ctx) return KSG_E_INVALID;
+  if (appended) *appended = 0;
+  if (s->nodes.empty()) return fail(s, KSG_E_STATE, "no nodes");
+  if (s->loaded_ctx != ctx) return full_load(s, ctx);
+  int rc = encode_incremental(s, nullptr);
+  if (rc) return rc;
+  if (s->loaded_epoch != s->epoch) return upload_all(s, ctx);   // the universe changed
+  const int P = s->n_encoded;
+  Encoded& e = s->e;
+  if (s->n_loaded < P) {
+    ksg_workload tail{};
+    tail.pods = e.pods.data() + s->n_loaded;
+    tail.n_pods = P - s->n_loaded;
+    tail.prog = e.prog.data() + s->prog_loaded;
+    tail.prog_len = (int64_t)(e.prog.size() - s->prog_loaded);
+    rc = ksg_append_pods(ctx, &tail, (int64_t)s->prog_loaded);
+    if (rc) return fail(s, rc, std::string("ksg_append_pods: ") + ksg_last_error(ctx));
+    s->n_loaded = P;
+    s->prog_loaded = e.prog.size();
+  }
+  if (appended) *appended = 1;
+  return KSG_OK;
+}
+
+int ksg_snapshot_assume(ksg_snapshot* s, ksg_ctx* ctx, int32_t pod, int32_t node) {
+  if (!s || !ctx) return KSG_E_INVALID;
+  if (s->loaded_ctx != ctx || pod >= s->n_loaded) return fail(s, KSG_E_STATE, "assume: sync the context first");
+  const int rc = ksg_commit(ctx, pod, node);
+  if (rc) return fail(s, rc, std::string("ksg_commit: ") + ksg_last_error(ctx));
+  s->binds.emplace_back(pod, node);
+  return KSG_OK;
+}
+
+int ksg_snapshot_forget(ksg_snapshot* s, ksg_ctx* ctx, int32_t pod, int32_t node) {
+  if (!s || !ctx) return KSG_E_INVALID;
+  auto it = std::find(s->binds.begin(), s->binds.end(), std::make_pair(pod, node));
+  if (it == s->binds.end()) return fail(s, KSG_E_INVALID, "forget: no such binding");
+  if (s->loaded_ctx == ctx) {
+    const int rc = ksg_uncommit(ctx, pod, node);
+    if (rc) return fail(s, rc, std::string("ksg_uncommit: ") + ksg_last_error(ctx));
+  }
+  s->binds.erase(it);
+  return KSG_OK;
+}
+
+int ksg_snapshot_status(ksg_snapshot* s, int32_t pod, uint32_t word, int32_t node, int32_t* code, char* msg,
+                        int32_t cap, int32_t* len) {
+  if (!s || !code) return KSG_E_INVALID;
+  if (!s->encoded || pod < 0 || pod >= (int32_t)s->e.pods.size() || node < 0 || node >= s->e.N)
+    return fail(s, KSG_E_INVALID, "status: index out of range");
+  const Encoded& e = s->e;
+  std::string m;
+  int c = KSG_CODE_SUCCESS;
+  const int pl = (int)(word & 0xffu) - 1;
+  const uint32_t reason = word >> 8;
+  if (word == KSG_FS_NOT_EVALUATED) return fail(s, KSG_E_INVALID, "status: node not evaluated");
+  switch (pl) {
+    case -1:
+      break;
+    case KSG_PL_NODE_UNSCHEDULABLE:
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      m = "node(s) were unschedulable";
+      break;
+    case KSG_PL_NODE_NAME:
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      m = "node(s) didn't match the requested node name";
+      break;
+    case KSG_PL_TAINT_TOLERATION: {
+      if ((int)reason >= e.max_taints) return fail(s, KSG_E_INVALID, "status: taint slot");
+      const uint32_t t = e.taints[(size_t)reason * e.N + node];
+      if (t == 0) return fail(s, KSG_E_INVALID, "status: empty taint slot");
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      m = "node(s) had untolerated taint " + e.taint_strings[t - 1];
+      break;
+    }
+    case KSG_PL_NODE_AFFINITY:
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      m = "node(s) didn't match Pod's node affinity/selector";
+      break;
+    case KSG_PL_NODE_RESOURCES_FIT: {
+      // fitsRequest reason order: pods, cpu, memory, ephemeral, scalars;
+      // Unresolvable when the request exceeds the allocatable outright.
+      c = KSG_CODE_UNSCHEDULABLE;
+      const ksg_pod& p = e.pods[pod];
+      std::vector<std::string> rs;
+      if (reason & 1u) rs.push_back("Too many pods");
+      for (size_t r = 0; r < e.res_names.size(); r++)
+        if (reason & (1u << (r + 1))) {
+          rs.push_back("Insufficient " + e.res_names[r]);
+          if (p.req[r] > e.alloc[r * e.N + node]) c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+        }
+      for (size_t k = 0; k < rs.size(); k++) m += (k ? ", " : "") + rs[k];
+      break;
+    }
+    case KSG_PL_POD_TOPOLOGY_SPREAD:
+      c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
+      m = reason == 1 ? "node(s) didn't match pod topology spread constraints (missing required label)"
+                      : "node(s) didn't match pod topology spread constraints";
+      break;
+    case KSG_PL_INTER_POD_AFFINITY:
+      c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
+      m = reason == 1   ? "node(s) didn't match pod affinity rules"
+          : reason == 2 ? "node(s) didn't match pod anti-affinity rules"
+                        : "node(s) didn't satisfy existing pods anti-affinity rules";
+      break;
+    default:
+      return fail(s, KSG_E_INVALID, "status: unexpected word");
+  }
+  *code = c;
+  if (len) *len = (int32_t)m.size();
+  if (msg && cap > 0) {
+    const size_t n = std::min<size_t>(m.size(), (size_t)cap - 1);
+    std::memcpy(msg, m.data(), n);
+    msg[n] = 0;
+  }
+  return KSG_OK;
+}
+
+int ksg_snapshot_prefilter(ksg_snapshot* s, int32_t pod, int32_t plugin, uint32_t result_status, int32_t* code,
+                           int32_t* has_result, const char** names, int32_t cap, int32_t* n_names) {
+  if (!s || !code) return KSG_E_INVALID;
+  if (!s->encoded || pod < 0 || pod >= (int32_t)s->e.pods.size() || plugin < 0 || plugin >= KSG_NPLUGINS)
+    return fail(s, KSG_E_INVALID, "prefilter: index out of range");
+  const ksg_pod& p = s->e.pods[pod];
+  if (has_result) *has_result = 0;
+  if (n_names) *n_names = 0;
+  uint32_t fskip = p.filter_skip;
+  if (result_status & KSG_ST_IPA_PREFILTER_SKIP) fskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
+  if (plugin == KSG_PL_NODE_AFFINITY && (p.flags & KSG_POD_PREFILTER_REJECT)) {
+    *code = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;   // "pod affinity terms conflict"
+    return KSG_OK;
+  }
+  if ((fskip >> plugin) & 1u) {
+    *code = KSG_CODE_SKIP;
+    return KSG_OK;
+  }
+  *code = KSG_CODE_SUCCESS;
+  if (plugin == KSG_PL_NODE_AFFINITY && p.node_set >= 0) {
+    const auto& nm = s->e.prefilter_names.at(pod);
+    if (has_result) *has_result = 1;
+    if (n_names) *n_names = (int32_t)nm.size();
+    if (names)
+      for (int32_t k = 0; k < cap && k < (int32_t)nm.size(); k++) names[k] = nm[k].c_str();
+  }
+  return KSG_OK;
+}
+
+int ksg_snapshot_counts(ksg_snapshot* s, int32_t* n_nodes, int32_t* n_pods, int32_t* n_res, int32_t* n_taint_vocab) {
+  if (!s) return KSG_E_INVALID;
+  if (n_nodes) *n_nodes = (int32_t)s->nodes.size();
+  if (n_pods) *n_pods = (int32_t)s->pods.size();
+  if (n_res) *n_res = s->encoded ? (int32_t)s->e.res_names.size() : 0;
+  if (n_taint_vocab) *n_taint_vocab = s->encoded ? (int32_t)s->e.taint_vocab.size() : 0;
+  return KSG_OK;
+}
+
+int ksg_snapshot_names(ksg_snapshot* s, const char** node, const char** res, const char** taint) {
+  if (!s) return KSG_E_INVALID;
+  if (!s->encoded) return fail(s, KSG_E_STATE, "snapshot not encoded");
+  if (node)
+    for (size_t i = 0; i < s->nodes.size(); i++) node[i] = s->nodes[i].name.c_str();
+  if (res)
+    for (size_t i = 0; i < s->e.res_names.size(); i++) res[i] = s->e.res_names[i].c_str();
+  if (taint)
+    for (size_t i = 0; i < s->e.taint_strings.size(); i++) taint[i] = s->e.taint_strings[i].c_str();
+  return KSG_OK;
+}
+
+}  // extern "C"

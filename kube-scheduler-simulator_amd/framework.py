@@ -88,6 +88,33 @@ class Decoder:
         raise ValueError(f"unexpected status word {st:#x}")
 
 
+def status_code(st: int, enc: E.Encoder, pod: int, node: int) -> int:
+    """framework.Code of the Filter rejection in status word `st` [upstream
+    v1.32 Filter returns, SURVEY.md Appendix A]: the node-static plugins
+    (NodeUnschedulable, NodeName, TaintToleration, NodeAffinity), a
+    PodTopologySpread missing label and an InterPodAffinity affinity
+    mismatch are UnschedulableAndUnresolvable (preemption cannot help);
+    NodeResourcesFit is Unschedulable unless a request exceeds the node's
+    allocatable outright (the InsufficientResource.Unresolvable flag);
+    skew and anti-affinity rejections are Unschedulable."""
+    pl = (st & 0xFF) - 1
+    reason = st >> 8
+    if pl < 0:
+        return Status.SUCCESS
+    if pl in (P.NODE_UNSCHEDULABLE, P.NODE_NAME, P.TAINT_TOLERATION, P.NODE_AFFINITY):
+        return Status.UNSCHEDULABLE_AND_UNRESOLVABLE
+    if pl == P.NODE_RESOURCES_FIT:
+        req = enc.workload.pods[pod]["req"]
+        alloc = enc.cluster.arrays["alloc"]
+        for r in range(len(enc.cluster.res_names)):
+            if reason & (1 << (r + 1)) and int(req[r]) > int(alloc[r, node]):
+                return Status.UNSCHEDULABLE_AND_UNRESOLVABLE
+        return Status.UNSCHEDULABLE
+    if pl in (P.POD_TOPOLOGY_SPREAD, P.INTER_POD_AFFINITY):
+        return Status.UNSCHEDULABLE_AND_UNRESOLVABLE if reason == 1 else Status.UNSCHEDULABLE
+    return Status.UNSCHEDULABLE
+
+
 @dataclass
 class PodCycle:
     """Everything the device computed for one pod (one CycleState)."""
@@ -206,7 +233,8 @@ class DebuggableScheduler:
         pod = self.pods[pi]
         if pod.preemption_policy == "Never":              # PodEligibleToPreemptOthers
             return -1, []
-        potential = PR.potential_nodes(cyc.fstatus)
+        potential = PR.potential_nodes(cyc.fstatus, self.enc.workload.pods[pi]["req"],
+                                       self.enc.cluster.arrays["alloc"])
         if not potential:
             return -1, []
         # nodes without a lower-priority pod fail SelectVictimsOnNode at once
@@ -382,7 +410,7 @@ class DebuggableScheduler:
 
 class Status:
     """framework.Status subset: code + reasons (Message joins with ", ")."""
-    SUCCESS, ERROR, UNSCHEDULABLE, UNSCHEDULABLE_AND_UNRESOLVABLE, SKIP = 0, 1, 2, 3, 7
+    SUCCESS, ERROR, UNSCHEDULABLE, UNSCHEDULABLE_AND_UNRESOLVABLE, SKIP = 0, 1, 2, 3, 5   # framework.Code
 
     def __init__(self, code: int = 0, *reasons: str):
         self.code = code
@@ -411,9 +439,23 @@ class DevicePlugin:
     def Filter(self, cyc: PodCycle, node: int) -> Status:
         st = int(cyc.fstatus[node])
         if (st & 0xFF) - 1 == self.pid:
-            code = Status.UNSCHEDULABLE
-            return Status(code, self.s.decoder.message(st, node))
+            return Status(status_code(st, self.s.enc, cyc.pod, node), self.s.decoder.message(st, node))
         return Status()
+
+    def PreFilter(self, cyc: PodCycle) -> Status:
+        """Skip for plugins whose PreFilter skips this pod (encoder
+        filter_skip, InterPodAffinity's from the device); NodeAffinity
+        rejects a pod whose matchFields name no node."""
+        rec = self.s.enc.workload.pods[cyc.pod]
+        if self.pid == P.NODE_AFFINITY and int(rec["flags"]) & E.POD_FLAG_PREFILTER_REJECT:
+            return Status(Status.UNSCHEDULABLE_AND_UNRESOLVABLE, MSG_NA_CONFLICT)
+        fskip = int(rec["filter_skip"])
+        if cyc.status & native.ST_IPA_PREFILTER_SKIP:
+            fskip |= 1 << P.INTER_POD_AFFINITY
+        return Status(Status.SKIP) if (fskip >> self.pid) & 1 else Status()
+
+    def PreScore(self, cyc: PodCycle) -> Status:
+        return Status(Status.SKIP) if (cyc.score_skip >> self.pid) & 1 else Status()
 
     def Score(self, cyc: PodCycle, node: int):
         return int(cyc.raw[self.pid, node]), Status()

@@ -21,6 +21,7 @@ Every config can be scaled down (n_nodes / n_pods) for parity tests.
 """
 from __future__ import annotations
 
+import functools
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -111,10 +112,21 @@ def config2(n_nodes: int = 5000, n_pods: int = 50000, seed: int = 2, zones: int 
     return nodes, pods, P.config2_profile()
 
 
-def _zipf_choice(rng, n: int, a: float, size: int):
+@functools.lru_cache(maxsize=None)
+def _zipf_cdf(n: int, a: float) -> np.ndarray:
     w = 1.0 / np.arange(1, n + 1) ** a
     w /= w.sum()
-    return rng.choice(n, size=size, p=w)
+    # Generator.choice(n, size, p=w) draws exactly this way (cdf of p,
+    # normalised by its last entry, searched with one uniform per sample);
+    # the cdf is built once per (n, a) instead of once per call.
+    cdf = w.cumsum()
+    cdf /= cdf[-1]
+    cdf.setflags(write=False)
+    return cdf
+
+
+def _zipf_choice(rng, n: int, a: float, size: int):
+    return _zipf_cdf(n, a).searchsorted(rng.random(size), side="right").astype(np.int64)
 
 
 def config3(n_nodes: int = 15000, n_pods: int = 150000, seed: int = 3, zones: int = 16, apps: int = 500):

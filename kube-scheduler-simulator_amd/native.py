@@ -193,6 +193,7 @@ class Engine:
         self.ctx = C.c_void_p()
         self._check(self._open(device, C.byref(self.ctx)))
         self._m: Optional[Marshalled] = None
+        self._nn = 0
 
     def _declare(self):
         f = _bind(self.lib, self.PREFIX)
@@ -211,12 +212,15 @@ class Engine:
         self._uncommit = f("uncommit", C.c_int, vp, C.c_int32, C.c_int32)
         self._preempt = f("preempt_victims", C.c_int, vp, C.c_int32, i32p, C.c_int32, i32p, i32p, i32p,
                           C.POINTER(C.c_uint8))
+        self._append = f("append_pods", C.c_int, vp, C.POINTER(KsgWorkload), C.c_int64)
         self._declare_extra(f)
 
     def _declare_extra(self, f):
         vp = C.c_void_p
         self._run_replicas = f("run_replicas", C.c_int, vp, C.POINTER(KsgProfile), C.c_int32, C.c_int32,
                                C.c_int32, i32p, vp)
+        self._eval_pod = f("eval_pod", C.c_int, vp, vp, i32p, C.c_int64, C.POINTER(KsgResult),
+                           C.POINTER(KsgCapture))
         self._last_ms = f("last_kernel_ms", C.c_int, vp, C.POINTER(C.c_double))
         self._set_timing = f("set_timing", C.c_int, vp, C.c_int)
         self._kernel_stats = f("kernel_stats", C.c_int, vp, C.POINTER(KsgKernelStat), C.c_int32,
@@ -250,14 +254,38 @@ class Engine:
         self._check(self._set_profile(self.ctx, C.byref(make_profile(prof_fields))))
         self.profile_fields = prof_fields
 
+    def _snapshot_loaded(self, snap):
+        """Loaded through the native snapshot encoder (snapshot.Snapshot)."""
+        n = C.c_int32()
+        snap.lib.ksg_snapshot_counts(snap.h, C.byref(n), None, None, None)
+        self._m = None
+        self._nn = n.value
+
     @property
     def n_nodes(self) -> int:
-        return self._m.n_nodes
+        return self._m.n_nodes if self._m is not None else self._nn
 
     # -- evaluation -----------------------------------------------------
     def eval(self, pod: int, capture: Optional[CaptureBuffers] = None) -> KsgResult:
         r = KsgResult()
         self._check(self._eval(self.ctx, pod, C.byref(r), C.byref(capture.struct) if capture else None))
+        return r
+
+    def append_pods(self, pods: np.ndarray, prog: np.ndarray, prog_base: int):
+        """ksg_append_pods: pods (POD_DTYPE, absolute program offsets) whose
+        programs are pool words [prog_base, prog_base + len(prog))."""
+        pods = np.ascontiguousarray(pods, E.POD_DTYPE)
+        prog = np.ascontiguousarray(prog, np.int32)
+        wl = KsgWorkload(pods=pods.ctypes.data, n_pods=len(pods), prog=_ptr(prog, i32p), prog_len=len(prog))
+        self._check(self._append(self.ctx, C.byref(wl), prog_base))
+
+    def eval_pod(self, pod: np.ndarray, prog: np.ndarray, capture: Optional[CaptureBuffers] = None) -> KsgResult:
+        """ksg_eval_pod: an encoded pod outside the workload (offsets into prog)."""
+        rec = np.ascontiguousarray(np.asarray(pod, E.POD_DTYPE).reshape(1))
+        prog = np.ascontiguousarray(prog, np.int32)
+        r = KsgResult()
+        self._check(self._eval_pod(self.ctx, rec.ctypes.data, _ptr(prog, i32p), len(prog), C.byref(r),
+                                   C.byref(capture.struct) if capture else None))
         return r
 
     def commit(self, pod: int, node: int):

@@ -54,16 +54,25 @@ INT32_SPAN = 1 << 31          # math.MaxInt32 + 1 (minSumPrioritiesScoreFunc)
 _STATIC_FILTERS = (P.NODE_UNSCHEDULABLE, P.NODE_NAME, P.TAINT_TOLERATION, P.NODE_AFFINITY)
 
 
-def status_code(word: int) -> int:
+def status_code(word: int, req=None, alloc=None) -> int:
     """framework.Code of a node's filter result from its device status word
     (plugin id + 1 in bits 0-7, reason above).  Nodes outside the PreFilter
-    node set (FS_NOT_EVALUATED) carry the absent-nodes status."""
+    node set (FS_NOT_EVALUATED) carry the absent-nodes status.  For
+    NodeResourcesFit, `req` (the pod's request per resource column) and
+    `alloc` (the node's allocatable) give InsufficientResource.Unresolvable:
+    a request above the allocatable outright (framework.status_code)."""
     if word == 0:
         return SUCCESS
     if word == E.FS_NOT_EVALUATED:
         return UNSCHEDULABLE_AND_UNRESOLVABLE
     pl, reason = (word & 0xFF) - 1, word >> 8
-    if pl in (P.NODE_RESOURCES_FIT, P.NODE_PORTS):
+    if pl == P.NODE_RESOURCES_FIT:
+        if req is not None:
+            for r in range(len(alloc)):
+                if reason & (1 << (r + 1)) and int(req[r]) > int(alloc[r]):
+                    return UNSCHEDULABLE_AND_UNRESOLVABLE
+        return UNSCHEDULABLE
+    if pl == P.NODE_PORTS:
         return UNSCHEDULABLE
     if pl == P.POD_TOPOLOGY_SPREAD:            # ErrReasonNodeLabelNotMatch is unresolvable
         return UNSCHEDULABLE_AND_UNRESOLVABLE if reason == 1 else UNSCHEDULABLE
@@ -140,8 +149,11 @@ def check_scope(prof: P.Profile, pod: m.Pod, pods: Sequence[m.Pod]) -> None:
             raise NotImplementedError("DefaultPreemption with pods carrying required anti-affinity")
 
 
-def potential_nodes(fstatus) -> List[int]:
-    return [n for n in range(len(fstatus)) if status_code(int(fstatus[n])) == UNSCHEDULABLE]
+def potential_nodes(fstatus, req=None, alloc=None) -> List[int]:
+    """nodesWherePreemptionMightHelp; req = the pod's request columns, alloc
+    = [n_res][n_nodes] allocatable."""
+    return [n for n in range(len(fstatus))
+            if status_code(int(fstatus[n]), req, None if alloc is None else alloc[:, n]) == UNSCHEDULABLE]
 
 
 def may_preempt(pod: m.Pod, placed_min_priority: Optional[int]) -> bool:

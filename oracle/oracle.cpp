@@ -881,6 +881,29 @@ int kso_load_workload(kso_ctx* c, const ksg_workload* wl) {
   return KSG_OK;
 }
 
+int kso_append_pods(kso_ctx* c, const ksg_workload* tail, int64_t prog_base) {
+  if (!c || !tail || !c->have_wl || prog_base < 0 || prog_base > (int64_t)c->prog.size()) return KSG_E_INVALID;
+  c->prog.resize(prog_base);
+  c->prog.insert(c->prog.end(), tail->prog, tail->prog + tail->prog_len);
+  c->pods.insert(c->pods.end(), tail->pods, tail->pods + tail->n_pods);
+  return KSG_OK;
+}
+
+int kso_eval_pod(kso_ctx* c, const ksg_pod* pod, const int32_t* prog, int64_t prog_len, ksg_result* res,
+                 ksg_capture* cap) {
+  if (!c || !pod || !res || !c->have_nodes || !c->have_wl || !c->have_prof) return KSG_E_STATE;
+  const int64_t base = (int64_t)c->prog.size();
+  ksg_pod p = *pod;
+  for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob})
+    if (*f >= 0) *f = (int32_t)(*f + base);
+  c->prog.insert(c->prog.end(), prog, prog + prog_len);
+  c->pods.push_back(p);
+  const int rc = eval_pod(*c, (int)c->pods.size() - 1, res, cap);
+  c->pods.pop_back();
+  c->prog.resize(base);
+  return rc;
+}
+
 int kso_reset_state(kso_ctx* c) {
   c->requested = c->requested0; c->nonzero = c->nonzero0; c->pod_count = c->pod_count0;
   c->pods_on.assign(c->N, {});

@@ -929,8 +929,18 @@ def schedule_one(pod: m.Pod, infos: List[NodeInfo], prof: P.Profile):
 _NOW = 1 << 62
 
 
-def _filter_code(plugin: str, msg: str) -> str:
-    if plugin in ("NodeResourcesFit", "NodePorts"):
+def _filter_code(plugin: str, msg: str, pod=None, node=None) -> str:
+    if plugin == "NodeResourcesFit":
+        # InsufficientResource.Unresolvable: the request exceeds the node's
+        # allocatable outright, so no preemption on that node can help
+        req = m.pod_requests(pod)
+        for reason in msg.split(", "):
+            if reason.startswith("Insufficient "):
+                r = reason[len("Insufficient "):]
+                if req.get(r, 0) > node.allocatable.get(r, 0):
+                    return "UnschedulableAndUnresolvable"
+        return "Unschedulable"
+    if plugin == "NodePorts":
         return "Unschedulable"
     if plugin == "PodTopologySpread":
         return "UnschedulableAndUnresolvable" if msg.endswith("(missing required label)") else "Unschedulable"
@@ -978,7 +988,7 @@ def preempt(pod, infos, prof: P.Profile, rec):
         if not d:
             continue
         bad = [(pl, msg) for pl, msg in d.items() if msg != "passed"]
-        if bad and _filter_code(*bad[0]) == "Unschedulable":
+        if bad and _filter_code(*bad[0], pod, ni.node) == "Unschedulable":
             potential.append(idx)
     if not potential:
         return -1, []

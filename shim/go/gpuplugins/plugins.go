@@ -2,12 +2,20 @@
 // Framework plugins, so the simulator's wrappedPlugin and resultstore.Store
 // stay unchanged (SURVEY.md §8(b)).  Source only (no Go toolchain here).
 //
-// Wiring: overlay these factories onto the in-tree registry returned at
+// Wiring: overlay Factories(ev) onto the in-tree registry returned at
 // simulator/scheduler/config/plugin.go:49-51 (plugins.go:50 looks in-tree up
 // first), or add an option next to debuggablescheduler.WithPlugin
 // (simulator/pkg/debuggablescheduler/command.go:64-68).  Name() returns the
 // in-tree name, so Store keys (wrappedplugin.go:406,438,542) and
 // getScorePluginWeight (plugins.go:295) see the same names as today.
+//
+// Each plugin implements exactly the extension points its upstream v1.32
+// counterpart implements: NewWrappedPlugin type-asserts every interface
+// (wrappedplugin.go:253-360) and records a result for each one it finds, so
+// an extra method (a Reserve on NodeResourcesFit, say) would add an
+// annotation entry the reference never writes.  Assumed pods therefore reach
+// the device through the next cycle's snapshot diff (Evaluator.syncCluster),
+// not through a Reserve plugin.
 package gpuplugins
 
 import (
@@ -16,7 +24,10 @@ import (
 	"sync"
 
 	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/labels"
 	"k8s.io/apimachinery/pkg/runtime"
+	"k8s.io/apimachinery/pkg/types"
+	"k8s.io/apimachinery/pkg/util/sets"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
 
 	"example.invalid/ksched-mi355x/shim/go/ksched"
@@ -24,181 +35,436 @@ import (
 
 const stateKey framework.StateKey = "ksched/eval"
 
-// podState is the per-pod SoA result, computed once at PreFilter time.
+const fsNotEvaluated = 0xFF // KSG_FS_NOT_EVALUATED
+
+// podState is the per-pod SoA result, computed once per scheduling cycle.
 type podState struct {
+	pod   int // snapshot pod index
 	ev    *ksched.PodEval
 	index map[string]int // node name -> column
 }
 
 func (s *podState) Clone() framework.StateData { return s }
 
-// Evaluator owns the device context and the host-side encoder (the Go
-// equivalent of encoder.py: NodeInfo/PodInfo -> SoA columns + pod programs).
+// DefaultSelectorFunc is helper.DefaultSelector over the handle's service /
+// RC / RS / StatefulSet listers (PodTopologySpread system defaults); nil
+// when PodTopologySpread is not system-defaulted.
+type DefaultSelectorFunc func(*v1.Pod) labels.Selector
+
+// Evaluator owns the device context and the native snapshot encoder.  The
+// framework calls plugins from 16 goroutines; every device call happens
+// under mu, once per pod.
 type Evaluator struct {
-	mu    sync.Mutex
-	ctx   *ksched.Ctx
-	enc   Encoder
-	names []string
+	mu         sync.Mutex
+	ctx        *ksched.Ctx
+	prof       *ksched.ProfileArgs
+	snap       *ksched.Snapshot
+	defaultSel DefaultSelectorFunc
+
+	nodes   []string          // column order of the loaded snapshot
+	nodeRV  map[string]string // node ResourceVersion at load
+	nodeGen map[string]int64  // NodeInfo.Generation at the last diff
+	podIdx  map[types.UID]int // pod -> snapshot index
+	podRV   map[types.UID]string
+	podNode map[types.UID]int // pods bound / assumed on the device -> column
 }
 
-// Encoder is the snapshot/pod encoder (encoder.py restated in Go).
-type Encoder interface {
-	// SyncNodes re-encodes the snapshot when it changed; returns node names in column order.
-	SyncNodes(ctx *ksched.Ctx, nodes []*framework.NodeInfo) ([]string, error)
-	// LoadPod encodes one pod as a single-pod workload (index 0).
-	LoadPod(ctx *ksched.Ctx, pod *v1.Pod) error
-	// Message rebuilds the upstream status message from a filter status word.
-	Message(plugin int, word uint32, node string) (framework.Code, string)
+// NewEvaluator opens device dev for profile 0.
+func NewEvaluator(dev int, prof *ksched.ProfileArgs, ds DefaultSelectorFunc) (*Evaluator, error) {
+	ctx, err := ksched.Open(dev)
+	if err != nil {
+		return nil, err
+	}
+	return &Evaluator{ctx: ctx, prof: prof, defaultSel: ds}, nil
 }
 
-func (e *Evaluator) evalPod(ctx context.Context, cs *framework.CycleState, pod *v1.Pod,
-	nodes []*framework.NodeInfo) (*podState, error) {
+func (e *Evaluator) selectorOf(p *v1.Pod) labels.Selector {
+	if e.defaultSel == nil {
+		return nil
+	}
+	return e.defaultSel(p)
+}
+
+// rebuild encodes the whole snapshot: every node, every pod on them (bound),
+// then loads it (bindings replayed as assumes).
+func (e *Evaluator) rebuild(infos []*framework.NodeInfo) error {
+	if e.snap != nil {
+		e.snap.Free()
+	}
+	snap, err := ksched.NewSnapshot(e.prof)
+	if err != nil {
+		return err
+	}
+	e.snap = snap
+	e.nodes = e.nodes[:0]
+	e.nodeRV, e.nodeGen = map[string]string{}, map[string]int64{}
+	e.podIdx, e.podRV, e.podNode = map[types.UID]int{}, map[types.UID]string{}, map[types.UID]int{}
+	for _, ni := range infos {
+		n := ni.Node()
+		if _, err := snap.AddNode(n); err != nil {
+			return err
+		}
+		e.nodes = append(e.nodes, n.Name)
+		e.nodeRV[n.Name] = n.ResourceVersion
+		e.nodeGen[n.Name] = ni.Generation
+	}
+	for col, ni := range infos {
+		for _, pi := range ni.Pods {
+			idx, err := snap.AddPod(pi.Pod, e.selectorOf(pi.Pod))
+			if err != nil {
+				return err
+			}
+			if err := snap.Bind(idx, col); err != nil {
+				return err
+			}
+			e.podIdx[pi.Pod.UID], e.podRV[pi.Pod.UID], e.podNode[pi.Pod.UID] = idx, pi.Pod.ResourceVersion, col
+		}
+	}
+	return snap.Load(e.ctx)
+}
+
+// syncCluster brings the device up to date with the framework's snapshot:
+// a changed node set or node object reloads everything; otherwise the pods
+// that appeared on / left a node since the last cycle (the previous cycle's
+// assume among them) are assumed / forgotten one by one.
+func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
+	same := e.snap != nil && len(infos) == len(e.nodes)
+	for i := 0; same && i < len(infos); i++ {
+		n := infos[i].Node()
+		same = n.Name == e.nodes[i] && n.ResourceVersion == e.nodeRV[n.Name]
+	}
+	if !same {
+		return e.rebuild(infos)
+	}
+	for col, ni := range infos {
+		name := e.nodes[col]
+		if ni.Generation == e.nodeGen[name] {
+			continue
+		}
+		present := make(map[types.UID]bool, len(ni.Pods))
+		for _, pi := range ni.Pods {
+			uid := pi.Pod.UID
+			present[uid] = true
+			if c, ok := e.podNode[uid]; ok && c == col {
+				continue
+			}
+			idx, known := e.podIdx[uid]
+			if known && e.podRV[uid] != pi.Pod.ResourceVersion && e.podNode[uid] >= 0 {
+				return e.rebuild(infos) // a bound pod changed: re-encode
+			}
+			if !known {
+				var err error
+				if idx, err = e.snap.AddPod(pi.Pod, e.selectorOf(pi.Pod)); err != nil {
+					return err
+				}
+				if _, err := e.snap.Sync(e.ctx); err != nil {
+					return err
+				}
+				e.podIdx[uid], e.podRV[uid] = idx, pi.Pod.ResourceVersion
+			}
+			if c, ok := e.podNode[uid]; ok && c >= 0 {
+				if err := e.snap.Forget(e.ctx, idx, c); err != nil {
+					return err
+				}
+			}
+			if err := e.snap.Assume(e.ctx, idx, col); err != nil {
+				return err
+			}
+			e.podNode[uid] = col
+		}
+		for uid, c := range e.podNode {
+			if c == col && !present[uid] {
+				if err := e.snap.Forget(e.ctx, e.podIdx[uid], col); err != nil {
+					return err
+				}
+				e.podNode[uid] = -1
+			}
+		}
+		e.nodeGen[name] = ni.Generation
+	}
+	return nil
+}
+
+// evalPod runs the whole sweep for the pod once per cycle (the first of the
+// shim's plugins to be called pays) and stashes it in CycleState.
+func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*framework.NodeInfo) (*podState, error) {
 	if d, err := cs.Read(stateKey); err == nil {
 		return d.(*podState), nil
 	}
 	e.mu.Lock()
 	defer e.mu.Unlock()
-	names, err := e.enc.SyncNodes(e.ctx, nodes)
+	if err := e.syncCluster(infos); err != nil {
+		return nil, err
+	}
+	idx, known := e.podIdx[pod.UID]
+	if known && e.podRV[pod.UID] != pod.ResourceVersion {
+		known = false // the pod object changed since it was encoded: encode it again
+	}
+	if !known {
+		var err error
+		if idx, err = e.snap.AddPod(pod, e.selectorOf(pod)); err != nil {
+			return nil, err
+		}
+		e.podIdx[pod.UID], e.podRV[pod.UID] = idx, pod.ResourceVersion
+		if _, ok := e.podNode[pod.UID]; !ok {
+			e.podNode[pod.UID] = -1
+		}
+	}
+	if _, err := e.snap.Sync(e.ctx); err != nil {
+		return nil, err
+	}
+	ev, err := e.ctx.Eval(idx)
 	if err != nil {
 		return nil, err
 	}
-	if err := e.enc.LoadPod(e.ctx, pod); err != nil {
-		return nil, err
-	}
-	ev, err := e.ctx.Eval(0)
-	if err != nil {
-		return nil, err
-	}
-	st := &podState{ev: ev, index: make(map[string]int, len(names))}
-	for i, n := range names {
+	st := &podState{pod: idx, ev: ev, index: make(map[string]int, len(e.nodes))}
+	for i, n := range e.nodes {
 		st.index[n] = i
 	}
 	cs.Write(stateKey, st)
 	return st, nil
 }
 
-// Plugin is one in-tree plugin backed by the shared per-pod evaluation.
-type Plugin struct {
+func (e *Evaluator) status(st *podState, id int, node string) *framework.Status {
+	col, ok := st.index[node]
+	if !ok {
+		return framework.AsStatus(fmt.Errorf("node %q not in the evaluated snapshot", node))
+	}
+	w := st.ev.FStatus[col]
+	if w == 0 || w == fsNotEvaluated || int(w&0xff)-1 != id {
+		return nil // passed this plugin (the framework stops at the first rejection, as the device does)
+	}
+	e.mu.Lock()
+	code, msg, err := e.snap.Status(st.pod, w, col)
+	e.mu.Unlock()
+	if err != nil {
+		return framework.AsStatus(err)
+	}
+	return framework.NewStatus(frameworkCode(code), msg)
+}
+
+func frameworkCode(c int) framework.Code {
+	switch c {
+	case ksched.CodeSuccess:
+		return framework.Success
+	case ksched.CodeUnschedulable:
+		return framework.Unschedulable
+	case ksched.CodeUnschedulableAndUnresolvable:
+		return framework.UnschedulableAndUnresolvable
+	case ksched.CodeSkip:
+		return framework.Skip
+	}
+	return framework.Error
+}
+
+// ---- plugin bodies shared by the per-extension-point types below ------------
+
+type base struct {
 	name string
 	id   int
-	norm bool // has ScoreExtensions (TaintToleration, NodeAffinity, PodTopologySpread, InterPodAffinity)
 	ev   *Evaluator
 	h    framework.Handle
 }
 
-func (p *Plugin) Name() string { return p.name }
+func (b *base) Name() string { return b.name }
 
-// PreFilter runs the whole sweep for the pod (first plugin to get here pays).
-func (p *Plugin) PreFilter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod) (*framework.PreFilterResult, *framework.Status) {
-	all, err := p.h.SnapshotSharedLister().NodeInfos().List()
+func (b *base) state(cs *framework.CycleState) (*podState, *framework.Status) {
+	d, err := cs.Read(stateKey)
 	if err != nil {
 		return nil, framework.AsStatus(err)
 	}
-	st, err := p.ev.evalPod(ctx, cs, pod, all)
+	return d.(*podState), nil
+}
+
+// run makes sure the pod was evaluated (plugins without a PreFilter can be
+// the first of the shim's plugins the framework calls).
+func (b *base) run(cs *framework.CycleState, pod *v1.Pod) (*podState, *framework.Status) {
+	if st, s := b.state(cs); s == nil {
+		return st, nil
+	}
+	infos, err := b.h.SnapshotSharedLister().NodeInfos().List()
 	if err != nil {
 		return nil, framework.AsStatus(err)
 	}
-	_ = st
-	// Skip decisions are host-decidable (encoder: filter_skip) except the
-	// InterPodAffinity one reported in ev.Status (KSG_ST_IPA_PREFILTER_SKIP).
+	st, err := b.ev.evalPod(cs, pod, infos)
+	if err != nil {
+		return nil, framework.AsStatus(err)
+	}
+	return st, nil
+}
+
+func (b *base) preFilter(cs *framework.CycleState, pod *v1.Pod) (*framework.PreFilterResult, *framework.Status) {
+	st, s := b.run(cs, pod)
+	if s != nil {
+		return nil, s
+	}
+	b.ev.mu.Lock()
+	code, names, err := b.ev.snap.PreFilter(st.pod, b.id, st.ev.Status)
+	b.ev.mu.Unlock()
+	if err != nil {
+		return nil, framework.AsStatus(err)
+	}
+	switch code {
+	case ksched.CodeSkip:
+		return nil, framework.NewStatus(framework.Skip) // recorded as "" (store.go:522)
+	case ksched.CodeUnschedulableAndUnresolvable: // nodeaffinity errReasonConflict
+		return nil, framework.NewStatus(framework.UnschedulableAndUnresolvable, "pod affinity terms conflict")
+	}
+	if names != nil {
+		return &framework.PreFilterResult{NodeNames: sets.New[string](names...)}, nil
+	}
 	return nil, nil
 }
 
-func (p *Plugin) PreFilterExtensions() framework.PreFilterExtensions { return nil }
-
-// Filter answers from the stashed status word: reject iff this plugin is
-// the first one that rejected the node (the framework stops there).
-func (p *Plugin) Filter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
-	d, err := cs.Read(stateKey)
-	if err != nil {
-		return framework.AsStatus(err)
+func (b *base) filter(cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
+	st, s := b.run(cs, pod)
+	if s != nil {
+		return s
 	}
-	st := d.(*podState)
-	i, ok := st.index[ni.Node().Name]
-	if !ok {
-		return framework.AsStatus(fmt.Errorf("node %q not in snapshot", ni.Node().Name))
-	}
-	w := st.ev.FStatus[i]
-	if w == 0 || int(w&0xff)-1 != p.id {
-		return nil
-	}
-	code, msg := p.ev.enc.Message(p.id, w, ni.Node().Name)
-	return framework.NewStatus(code, msg)
+	return b.ev.status(st, b.id, ni.Node().Name)
 }
 
-func (p *Plugin) PreScore(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, nodes []*framework.NodeInfo) *framework.Status {
-	d, err := cs.Read(stateKey)
-	if err != nil {
-		return framework.AsStatus(err)
+func (b *base) preScore(cs *framework.CycleState, pod *v1.Pod) *framework.Status {
+	st, s := b.run(cs, pod)
+	if s != nil {
+		return s
 	}
-	if d.(*podState).ev.ScoreSkip&(1<<uint(p.id)) != 0 {
+	if st.ev.ScoreSkip&(1<<uint(b.id)) != 0 {
 		return framework.NewStatus(framework.Skip)
 	}
 	return nil
 }
 
-// Score returns the raw Score() value computed on the device.
-func (p *Plugin) Score(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, nodeName string) (int64, *framework.Status) {
-	d, err := cs.Read(stateKey)
-	if err != nil {
-		return 0, framework.AsStatus(err)
+func (b *base) score(cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
+	st, s := b.run(cs, pod)
+	if s != nil {
+		return 0, s
 	}
-	st := d.(*podState)
 	n := len(st.ev.Total)
-	return st.ev.Raw[p.id*n+st.index[nodeName]], nil
+	return st.ev.Raw[b.id*n+st.index[node]], nil
 }
 
-func (p *Plugin) ScoreExtensions() framework.ScoreExtensions {
-	if p.norm {
-		return p
+func (b *base) normalize(cs *framework.CycleState, scores framework.NodeScoreList) *framework.Status {
+	st, s := b.state(cs)
+	if s != nil {
+		return s
 	}
-	return nil
-}
-
-// NormalizeScore overwrites the list with the device's normalised values.
-func (p *Plugin) NormalizeScore(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, scores framework.NodeScoreList) *framework.Status {
-	d, err := cs.Read(stateKey)
-	if err != nil {
-		return framework.AsStatus(err)
-	}
-	st := d.(*podState)
 	n := len(st.ev.Total)
 	for k := range scores {
-		scores[k].Score = st.ev.Norm[p.id*n+st.index[scores[k].Name]]
+		scores[k].Score = st.ev.Norm[b.id*n+st.index[scores[k].Name]]
 	}
 	return nil
 }
 
-// Reserve assumes the pod on the device (NodeInfo.AddPod restated).
-func (p *Plugin) Reserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, nodeName string) *framework.Status {
-	d, err := cs.Read(stateKey)
-	if err != nil {
-		return framework.AsStatus(err)
-	}
-	if err := p.ev.ctx.Commit(0, d.(*podState).index[nodeName]); err != nil {
-		return framework.AsStatus(err)
-	}
-	return nil
+// ---- one type per upstream extension-point set ---------------------------
+
+// filterOnly: NodeUnschedulable, NodeName.
+type filterOnly struct{ base }
+
+func (p *filterOnly) Filter(_ context.Context, cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
+	return p.filter(cs, pod, ni)
 }
 
-func (p *Plugin) Unreserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, nodeName string) {}
+// taintToleration: Filter, PreScore, Score + NormalizeScore.
+type taintToleration struct{ base }
 
-// Factories returns in-tree-named factories sharing one Evaluator.
+func (p *taintToleration) Filter(_ context.Context, cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
+	return p.filter(cs, pod, ni)
+}
+func (p *taintToleration) PreScore(_ context.Context, cs *framework.CycleState, pod *v1.Pod, _ []*framework.NodeInfo) *framework.Status {
+	return p.preScore(cs, pod)
+}
+func (p *taintToleration) Score(_ context.Context, cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
+	return p.score(cs, pod, node)
+}
+func (p *taintToleration) ScoreExtensions() framework.ScoreExtensions { return p }
+func (p *taintToleration) NormalizeScore(_ context.Context, cs *framework.CycleState, _ *v1.Pod, s framework.NodeScoreList) *framework.Status {
+	return p.normalize(cs, s)
+}
+
+// allPoints: NodeAffinity, PodTopologySpread, InterPodAffinity.
+type allPoints struct{ base }
+
+func (p *allPoints) PreFilter(_ context.Context, cs *framework.CycleState, pod *v1.Pod) (*framework.PreFilterResult, *framework.Status) {
+	return p.preFilter(cs, pod)
+}
+func (p *allPoints) PreFilterExtensions() framework.PreFilterExtensions { return nil }
+func (p *allPoints) Filter(_ context.Context, cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
+	return p.filter(cs, pod, ni)
+}
+func (p *allPoints) PreScore(_ context.Context, cs *framework.CycleState, pod *v1.Pod, _ []*framework.NodeInfo) *framework.Status {
+	return p.preScore(cs, pod)
+}
+func (p *allPoints) Score(_ context.Context, cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
+	return p.score(cs, pod, node)
+}
+func (p *allPoints) ScoreExtensions() framework.ScoreExtensions { return p }
+func (p *allPoints) NormalizeScore(_ context.Context, cs *framework.CycleState, _ *v1.Pod, s framework.NodeScoreList) *framework.Status {
+	return p.normalize(cs, s)
+}
+
+// fit: NodeResourcesFit (PreFilter, Filter, PreScore, Score; no normalise).
+type fit struct{ base }
+
+func (p *fit) PreFilter(_ context.Context, cs *framework.CycleState, pod *v1.Pod) (*framework.PreFilterResult, *framework.Status) {
+	return p.preFilter(cs, pod)
+}
+func (p *fit) PreFilterExtensions() framework.PreFilterExtensions { return nil }
+func (p *fit) Filter(_ context.Context, cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
+	return p.filter(cs, pod, ni)
+}
+func (p *fit) PreScore(_ context.Context, cs *framework.CycleState, pod *v1.Pod, _ []*framework.NodeInfo) *framework.Status {
+	return p.preScore(cs, pod)
+}
+func (p *fit) Score(_ context.Context, cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
+	return p.score(cs, pod, node)
+}
+func (p *fit) ScoreExtensions() framework.ScoreExtensions { return nil }
+
+// balanced: NodeResourcesBalancedAllocation (PreScore, Score).
+type balanced struct{ base }
+
+func (p *balanced) PreScore(_ context.Context, cs *framework.CycleState, pod *v1.Pod, _ []*framework.NodeInfo) *framework.Status {
+	return p.preScore(cs, pod)
+}
+func (p *balanced) Score(_ context.Context, cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
+	return p.score(cs, pod, node)
+}
+func (p *balanced) ScoreExtensions() framework.ScoreExtensions { return nil }
+
+// imageLocality: Score only.
+type imageLocality struct{ base }
+
+func (p *imageLocality) Score(_ context.Context, cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
+	return p.score(cs, pod, node)
+}
+func (p *imageLocality) ScoreExtensions() framework.ScoreExtensions { return nil }
+
+// Factories returns in-tree-named factories sharing one Evaluator (the
+// PluginFactory signature of k8s.io/kubernetes v1.32 runtime.Registry).
 func Factories(ev *Evaluator) map[string]func(context.Context, runtime.Object, framework.Handle) (framework.Plugin, error) {
-	mk := func(name string, id int, norm bool) func(context.Context, runtime.Object, framework.Handle) (framework.Plugin, error) {
-		return func(_ context.Context, _ runtime.Object, h framework.Handle) (framework.Plugin, error) {
-			return &Plugin{name: name, id: id, norm: norm, ev: ev, h: h}, nil
+	type mk func(b base) framework.Plugin
+	table := []struct {
+		name string
+		id   int
+		make mk
+	}{
+		{"NodeUnschedulable", ksched.NodeUnschedulable, func(b base) framework.Plugin { return &filterOnly{b} }},
+		{"NodeName", ksched.NodeName, func(b base) framework.Plugin { return &filterOnly{b} }},
+		{"TaintToleration", ksched.TaintToleration, func(b base) framework.Plugin { return &taintToleration{b} }},
+		{"NodeAffinity", ksched.NodeAffinity, func(b base) framework.Plugin { return &allPoints{b} }},
+		{"NodeResourcesFit", ksched.NodeResourcesFit, func(b base) framework.Plugin { return &fit{b} }},
+		{"PodTopologySpread", ksched.PodTopologySpread, func(b base) framework.Plugin { return &allPoints{b} }},
+		{"InterPodAffinity", ksched.InterPodAffinity, func(b base) framework.Plugin { return &allPoints{b} }},
+		{"NodeResourcesBalancedAllocation", ksched.BalancedAllocation, func(b base) framework.Plugin { return &balanced{b} }},
+		{"ImageLocality", ksched.ImageLocality, func(b base) framework.Plugin { return &imageLocality{b} }},
+	}
+	out := map[string]func(context.Context, runtime.Object, framework.Handle) (framework.Plugin, error){}
+	for _, t := range table {
+		t := t
+		out[t.name] = func(_ context.Context, _ runtime.Object, h framework.Handle) (framework.Plugin, error) {
+			return t.make(base{name: t.name, id: t.id, ev: ev, h: h}), nil
 		}
 	}
-	return map[string]func(context.Context, runtime.Object, framework.Handle) (framework.Plugin, error){
-		"NodeUnschedulable":  mk("NodeUnschedulable", ksched.NodeUnschedulable, false),
-		"NodeName":           mk("NodeName", ksched.NodeName, false),
-		"TaintToleration":    mk("TaintToleration", ksched.TaintToleration, true),
-		"NodeAffinity":       mk("NodeAffinity", ksched.NodeAffinity, true),
-		"NodeResourcesFit":   mk("NodeResourcesFit", ksched.NodeResourcesFit, false),
-		"PodTopologySpread":  mk("PodTopologySpread", ksched.PodTopologySpread, true),
-		"InterPodAffinity":   mk("InterPodAffinity", ksched.InterPodAffinity, true),
-		"NodeResourcesBalancedAllocation": mk("NodeResourcesBalancedAllocation", ksched.BalancedAllocation, false),
-		"ImageLocality":      mk("ImageLocality", ksched.ImageLocality, false),
-	}
+	return out
 }

@@ -1,0 +1,492 @@
+/*
+ * snapshot_c_test.c — the drop-in boundary exercised from C only: clusters are
+ * built from strings through include/ksched_snapshot.h (no Python encoder),
+ * encoded by libksched.so, and scheduled
+ *   --cpu : on the C++ oracle only (liboracle.so; test infrastructure):
+ *           README KAT scores, incremental-vs-full encoding bytes, oracle
+ *           placements of both encodings equal;
+ *   --gpu : on the MI355X through ksg_run_queue (whole queue) and through the
+ *           per-cycle path a cgo shim takes (add_pod -> sync -> ksg_eval ->
+ *           status words -> ksg_snapshot_assume), each compared with the
+ *           oracle's placements, results and per-node filter status words.
+ * Built by __graft_entry__.build() (gcc, links libksched.so + liboracle.so);
+ * run by tests/test_snapshot_c.py.  Exit 0 = every check passed.
+ */
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ksched_snapshot.h"
+
+/* ---- the CPU oracle's C ABI (oracle/oracle.cpp; the checker) ---- */
+typedef struct kso_ctx kso_ctx;
+int kso_open(int nthreads, kso_ctx** out);
+int kso_close(kso_ctx* c);
+int kso_set_profile(kso_ctx* c, const ksg_profile* p);
+int kso_load_nodes(kso_ctx* c, const ksg_nodes* nd, const ksg_topology* tp);
+int kso_load_workload(kso_ctx* c, const ksg_workload* wl);
+int kso_append_pods(kso_ctx* c, const ksg_workload* tail, int64_t prog_base);
+int kso_eval(kso_ctx* c, int32_t pod, ksg_result* res, ksg_capture* cap);
+int kso_commit(kso_ctx* c, int32_t pod, int32_t node);
+int kso_run_queue(kso_ctx* c, int32_t first, int32_t count, int32_t* placements, ksg_result* results,
+                  ksg_capture* cap);
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                                  \
+  do {                                                    \
+    if (!(cond)) {                                        \
+      fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      fprintf(stderr, __VA_ARGS__);                       \
+      fprintf(stderr, "\n");                              \
+      g_fail++;                                           \
+    }                                                     \
+  } while (0)
+#define OK(call)                                                                  \
+  do {                                                                            \
+    int _rc = (call);                                                             \
+    if (_rc != 0) {                                                               \
+      fprintf(stderr, "FATAL %s:%d: %s -> %d\n", __FILE__, __LINE__, #call, _rc); \
+      exit(2);                                                                    \
+    }                                                                             \
+  } while (0)
+
+/* ---- tiny arena: every string / array lives until exit ---- */
+static const char* S(const char* f, ...) {
+  char buf[256];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof buf, f, ap);
+  va_end(ap);
+  return strdup(buf);
+}
+static void* A(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
+
+static uint64_t g_rng = 88172645463325252ull;
+static uint32_t rnd(uint32_t n) {   /* xorshift64 */
+  g_rng ^= g_rng << 13;
+  g_rng ^= g_rng >> 7;
+  g_rng ^= g_rng << 17;
+  return (uint32_t)(g_rng % n);
+}
+
+#define GI (1024ll * 1024 * 1024)
+#define MI (1024ll * 1024)
+
+/* ---- scenario = nodes + pods + bindings + profile ---- */
+typedef struct {
+  const char* name;
+  ksg_profile_view prof;
+  int n_nodes, n_pods, n_bound;
+  ksg_node_view* nodes;
+  ksg_pod_view* pods;
+  int32_t* bound_node; /* pods [0, n_bound) run on these nodes */
+} scenario;
+
+static ksg_plugin_view* plugins(int n, const char** names, const int* w) {
+  ksg_plugin_view* p = A(n, sizeof *p);
+  for (int i = 0; i < n; i++) { p[i].name = names[i]; p[i].weight = w[i]; }
+  return p;
+}
+static void default_args(ksg_profile_view* pv) {
+  static ksg_quantity cm[2] = {{"cpu", 1}, {"memory", 1}};
+  pv->fit_strategy = "LeastAllocated";
+  pv->n_fit_resources = 2; pv->fit_resources = cm;
+  pv->n_ba_resources = 2; pv->ba_resources = cm;
+  pv->hard_pod_affinity_weight = 1;
+  pv->pts_system_defaulted = 1;
+}
+
+static ksg_node_view make_node(int i, int zones, int tainted) {
+  static const char* itype[] = {"m5.large", "m5.xlarge", "m6.2xlarge", "m6.4xlarge"};
+  ksg_node_view n;
+  memset(&n, 0, sizeof n);
+  n.name = S("node-%04d", i);
+  ksg_str_pair* l = A(4, sizeof *l);
+  l[0] = (ksg_str_pair){"kubernetes.io/hostname", n.name};
+  l[1] = (ksg_str_pair){"topology.kubernetes.io/zone", S("zone-%d", i % zones)};
+  l[2] = (ksg_str_pair){"node.kubernetes.io/instance-type", itype[rnd(4)]};
+  l[3] = (ksg_str_pair){"pool", S("pool-%d", rnd(6))};
+  n.n_labels = 4; n.labels = l;
+  ksg_quantity* q = A(4, sizeof *q);
+  static const int64_t cores[] = {8, 16, 32, 64}, mem[] = {32, 64, 128, 256};
+  q[0] = (ksg_quantity){"cpu", cores[rnd(4)] * 1000};
+  q[1] = (ksg_quantity){"memory", mem[rnd(4)] * GI};
+  q[2] = (ksg_quantity){"ephemeral-storage", 200 * GI};
+  q[3] = (ksg_quantity){"pods", 110};
+  n.n_alloc = 4; n.allocatable = q;
+  if (tainted) {
+    const uint32_t u = rnd(10);
+    if (u == 0 || u == 1) {
+      ksg_taint_view* t = A(1, sizeof *t);
+      if (u == 0) *t = (ksg_taint_view){"dedicated", l[3].value, "NoSchedule"};
+      else *t = (ksg_taint_view){"spot", "true", "PreferNoSchedule"};
+      n.n_taints = 1; n.taints = t;
+    }
+  }
+  if (rnd(3) == 0) {
+    ksg_image_view* im = A(1, sizeof *im);
+    const char** nm = A(1, sizeof *nm);
+    nm[0] = "registry.example.com/app:v1";
+    im->n_names = 1; im->names = nm; im->size_bytes = (100 + rnd(800)) * MI;
+    n.n_images = 1; n.images = im;
+  }
+  return n;
+}
+
+static ksg_container_view* one_container(int best_effort) {
+  static const int64_t cpu[] = {100, 250, 500, 1000, 2000}, mem[] = {128, 256, 512, 1024, 4096};
+  ksg_container_view* c = A(1, sizeof *c);
+  c->image = rnd(2) ? "registry.example.com/app:v1" : "registry.k8s.io/pause:3.10";
+  if (!best_effort) {
+    ksg_quantity* q = A(2, sizeof *q);
+    q[0] = (ksg_quantity){"cpu", cpu[rnd(5)]};
+    q[1] = (ksg_quantity){"memory", mem[rnd(5)] * MI};
+    c->n_requests = 2; c->requests = q;
+  }
+  return c;
+}
+
+static ksg_requirement_view* req_in(const char* key, int nv, const char** vals) {
+  ksg_requirement_view* r = A(1, sizeof *r);
+  r->key = key; r->op = "In"; r->n_values = nv; r->values = vals;
+  return r;
+}
+
+/* config-2 style: Fit + BalancedAllocation + TaintToleration + NodeAffinity */
+static scenario scenario_c2(int N, int P, int bound) {
+  scenario s;
+  memset(&s, 0, sizeof s);
+  s.name = "c2";
+  static const char* names[] = {"PrioritySort", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
+                                "NodeResourcesFit", "NodeResourcesBalancedAllocation", "DefaultBinder"};
+  static const int w[] = {0, 0, 0, 3, 2, 1, 1, 0};
+  s.prof.n_plugins = 8; s.prof.plugins = plugins(8, names, w);
+  default_args(&s.prof);
+  s.n_nodes = N; s.n_pods = P; s.n_bound = bound;
+  s.nodes = A(N, sizeof *s.nodes);
+  for (int i = 0; i < N; i++) s.nodes[i] = make_node(i, 4, 1);
+  s.pods = A(P, sizeof *s.pods);
+  s.bound_node = A(bound, sizeof *s.bound_node);
+  for (int j = 0; j < P; j++) {
+    ksg_pod_view* p = &s.pods[j];
+    p->namespace_ = "default";
+    p->name = S("pod-%05d", j);
+    p->n_containers = 1;
+    p->containers = one_container(rnd(20) == 0);
+    p->node_name = "";
+    if (rnd(10) < 3) {
+      ksg_toleration_view* t = A(2, sizeof *t);
+      if (rnd(2)) {
+        t[0] = (ksg_toleration_view){"dedicated", "Equal", S("pool-%d", rnd(6)), "NoSchedule"};
+        p->n_tolerations = 1;
+      } else {
+        t[0] = (ksg_toleration_view){"spot", "Exists", "", ""};
+        t[1] = (ksg_toleration_view){"dedicated", "Exists", "", "NoSchedule"};
+        p->n_tolerations = 2;
+      }
+      p->tolerations = t;
+    }
+    if (rnd(4) == 0) {
+      const char** z = A(2, sizeof *z);
+      z[0] = S("zone-%d", rnd(4));
+      z[1] = S("zone-%d", rnd(4));
+      ksg_node_selector_term_view* term = A(1, sizeof *term);
+      term->n_expr = 1; term->expr = req_in("topology.kubernetes.io/zone", 2, z);
+      p->has_na_required = 1; p->n_na_required = 1; p->na_required = term;
+    }
+    if (rnd(4) == 0) {
+      static const char* it[] = {"m5.large", "m6.4xlarge"};
+      ksg_preferred_term_view* pt = A(1, sizeof *pt);
+      pt->weight = 1 + rnd(100);
+      pt->preference.n_expr = 1;
+      pt->preference.expr = req_in("node.kubernetes.io/instance-type", 1, &it[rnd(2)]);
+      p->has_na_preferred = 1; p->n_na_preferred = 1; p->na_preferred = pt;
+    }
+    if (rnd(10) == 0) {
+      ksg_str_pair* ns = A(1, sizeof *ns);
+      *ns = (ksg_str_pair){"pool", S("pool-%d", rnd(6))};
+      p->has_node_selector = 1; p->n_node_selector = 1; p->node_selector = ns;
+    }
+    if (j < bound) {
+      s.bound_node[j] = (int32_t)rnd(N);
+      p->node_name = s.nodes[s.bound_node[j]].name;
+    }
+  }
+  return s;
+}
+
+/* config-3 style: PodTopologySpread + InterPodAffinity over zone / hostname */
+static scenario scenario_c3(int N, int P, int bound, int apps) {
+  scenario s = scenario_c2(N, P, 0);
+  s.name = "c3";
+  static const char* names[] = {"PrioritySort", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
+                                "NodeResourcesFit", "PodTopologySpread", "InterPodAffinity",
+                                "NodeResourcesBalancedAllocation", "DefaultBinder"};
+  static const int w[] = {0, 0, 0, 3, 2, 1, 2, 2, 1, 0};
+  s.prof.n_plugins = 10; s.prof.plugins = plugins(10, names, w);
+  s.n_bound = bound;
+  s.bound_node = A(bound, sizeof *s.bound_node);
+  for (int j = 0; j < P; j++) {
+    ksg_pod_view* p = &s.pods[j];
+    const int a = (int)rnd(apps);
+    ksg_str_pair* lab = A(1, sizeof *lab);
+    *lab = (ksg_str_pair){"app", S("app-%02d", a)};
+    p->n_labels = 1; p->labels = lab;
+    ksg_label_selector_view sel;
+    memset(&sel, 0, sizeof sel);
+    sel.is_set = 1; sel.n_labels = 1; sel.match_labels = lab;
+    ksg_spread_view* sp = A(2, sizeof *sp);
+    sp[0] = (ksg_spread_view){5, "topology.kubernetes.io/zone", "ScheduleAnyway", sel, 0, NULL, NULL, 0, NULL};
+    sp[1] = (ksg_spread_view){1 + (int)rnd(2), "kubernetes.io/hostname", "DoNotSchedule", sel, 0, NULL, NULL, 0, NULL};
+    p->n_spread = 2; p->spread = sp;
+    if (rnd(10) < 3) {
+      ksg_affinity_term_view* t = A(1, sizeof *t);
+      t->weight = 1 + rnd(100); t->selector = sel; t->topology_key = "kubernetes.io/hostname";
+      p->n_pod_anti_affinity_preferred = 1; p->pod_anti_affinity_preferred = t;
+    }
+    if (rnd(10) == 0) {
+      ksg_str_pair* o = A(1, sizeof *o);
+      *o = (ksg_str_pair){"app", S("app-%02d", (a + 1 + (int)rnd(apps - 1)) % apps)};
+      ksg_affinity_term_view* t = A(1, sizeof *t);
+      t->selector.is_set = 1; t->selector.n_labels = 1; t->selector.match_labels = o;
+      t->topology_key = "topology.kubernetes.io/zone";
+      p->n_pod_affinity_required = 1; p->pod_affinity_required = t;
+    }
+    if (j < bound) {
+      s.bound_node[j] = (int32_t)rnd(N);
+      p->node_name = s.nodes[s.bound_node[j]].name;
+    }
+  }
+  return s;
+}
+
+/* README.md:56-81 example: two 4-CPU / 32Gi nodes, a 100m / 16Gi pause pod,
+ * the default profile (scheduler_test.go:519-541 order and weights). */
+static scenario scenario_kat(void) {
+  scenario s;
+  memset(&s, 0, sizeof s);
+  s.name = "kat";
+  static const char* names[] = {"SchedulingGates", "PrioritySort", "NodeUnschedulable", "NodeName",
+                                "TaintToleration", "NodeAffinity", "NodePorts", "NodeResourcesFit",
+                                "VolumeRestrictions", "NodeVolumeLimits", "VolumeBinding", "VolumeZone",
+                                "PodTopologySpread", "InterPodAffinity", "DefaultPreemption",
+                                "NodeResourcesBalancedAllocation", "ImageLocality", "DefaultBinder"};
+  static const int w[] = {0, 0, 0, 0, 3, 2, 0, 1, 0, 0, 0, 0, 2, 2, 0, 1, 1, 0};
+  s.prof.n_plugins = 18; s.prof.plugins = plugins(18, names, w);
+  default_args(&s.prof);
+  s.n_nodes = 2; s.n_pods = 1;
+  s.nodes = A(2, sizeof *s.nodes);
+  for (int i = 0; i < 2; i++) {
+    ksg_node_view* n = &s.nodes[i];
+    n->name = i ? "node-gp9t4" : "node-282x7";
+    ksg_str_pair* l = A(1, sizeof *l);
+    *l = (ksg_str_pair){"kubernetes.io/hostname", n->name};
+    n->n_labels = 1; n->labels = l;
+    ksg_quantity* q = A(3, sizeof *q);
+    q[0] = (ksg_quantity){"cpu", 4000};
+    q[1] = (ksg_quantity){"memory", 32 * GI};
+    q[2] = (ksg_quantity){"pods", 110};
+    n->n_alloc = 3; n->allocatable = q;
+  }
+  s.pods = A(1, sizeof *s.pods);
+  ksg_container_view* c = A(1, sizeof *c);
+  ksg_quantity* rq = A(2, sizeof *rq);
+  rq[0] = (ksg_quantity){"cpu", 100};
+  rq[1] = (ksg_quantity){"memory", 16 * GI};
+  c->image = "registry.k8s.io/pause:3.5"; c->n_requests = 2; c->requests = rq;
+  s.pods[0].namespace_ = "default"; s.pods[0].name = "hoge-pod"; s.pods[0].node_name = "";
+  s.pods[0].n_containers = 1; s.pods[0].containers = c;
+  return s;
+}
+
+static ksg_snapshot* build(const scenario* s, int n_pods) {
+  ksg_snapshot* snap;
+  OK(ksg_snapshot_new(&s->prof, &snap));
+  for (int i = 0; i < s->n_nodes; i++) OK(ksg_snapshot_add_node(snap, &s->nodes[i], NULL));
+  for (int j = 0; j < n_pods; j++) OK(ksg_snapshot_add_pod(snap, &s->pods[j], NULL));
+  for (int j = 0; j < s->n_bound; j++) OK(ksg_snapshot_bind(snap, j, s->bound_node[j]));
+  return snap;
+}
+
+static kso_ctx* oracle_of(ksg_snapshot* snap, const scenario* s) {
+  ksg_nodes nd;
+  ksg_topology tp;
+  ksg_workload wl;
+  ksg_profile pf;
+  OK(ksg_snapshot_view(snap, &nd, &tp, &wl, &pf));
+  kso_ctx* o;
+  OK(kso_open(4, &o));
+  OK(kso_set_profile(o, &pf));
+  OK(kso_load_nodes(o, &nd, &tp));
+  OK(kso_load_workload(o, &wl));
+  for (int j = 0; j < s->n_bound; j++) OK(kso_commit(o, j, s->bound_node[j]));
+  return o;
+}
+
+/* README KAT (README.md:66,80): NodeResourcesFit raw 73, BalancedAllocation
+ * raw 76, TaintToleration normalised 100 (final 300 at weight 3). */
+static void check_kat(void) {
+  scenario s = scenario_kat();
+  ksg_snapshot* snap = build(&s, 1);
+  OK(ksg_snapshot_encode(snap));
+  kso_ctx* o = oracle_of(snap, &s);
+  uint32_t fs[2];
+  int64_t raw[KSG_NPLUGINS * 2], norm[KSG_NPLUGINS * 2], tot[2];
+  ksg_capture cap = {fs, raw, norm, tot};
+  ksg_result r;
+  OK(kso_eval(o, 0, &r, &cap));
+  CHECK(r.n_feasible == 2, "kat feasible %d", r.n_feasible);
+  CHECK(raw[KSG_PL_NODE_RESOURCES_FIT * 2] == 73, "kat Fit %lld", (long long)raw[KSG_PL_NODE_RESOURCES_FIT * 2]);
+  CHECK(raw[KSG_PL_BALANCED_ALLOCATION * 2] == 76, "kat BA %lld", (long long)raw[KSG_PL_BALANCED_ALLOCATION * 2]);
+  CHECK(norm[KSG_PL_TAINT_TOLERATION * 2] == 100, "kat taint norm %lld", (long long)norm[KSG_PL_TAINT_TOLERATION * 2]);
+  int32_t code, has, n;
+  OK(ksg_snapshot_prefilter(snap, 0, KSG_PL_POD_TOPOLOGY_SPREAD, r.status, &code, &has, NULL, 0, &n));
+  CHECK(code == KSG_CODE_SKIP, "kat PTS prefilter code %d", code);
+  OK(ksg_snapshot_prefilter(snap, 0, KSG_PL_NODE_RESOURCES_FIT, r.status, &code, &has, NULL, 0, &n));
+  CHECK(code == KSG_CODE_SUCCESS, "kat Fit prefilter code %d", code);
+  printf("ok kat: Fit 73, BalancedAllocation 76, TaintToleration 100\n");
+  kso_close(o);
+  ksg_snapshot_free(snap);
+}
+
+/* Incremental encoding (pods added after the first encode) against one full
+ * encode: identical pod records and program pool when appended. */
+static void check_incremental_bytes(const scenario* s) {
+  ksg_snapshot* full = build(s, s->n_pods);
+  OK(ksg_snapshot_encode(full));
+  ksg_snapshot* inc = build(s, s->n_bound + 1);
+  OK(ksg_snapshot_encode(inc));
+  int appended = 0, reloads = 0;
+  for (int j = s->n_bound + 1; j < s->n_pods; j++) {
+    int32_t ap;
+    OK(ksg_snapshot_add_pod(inc, &s->pods[j], NULL));
+    OK(ksg_snapshot_encode_incremental(inc, &ap));
+    appended += ap;
+    reloads += !ap;
+  }
+  ksg_workload a, b;
+  OK(ksg_snapshot_view(full, NULL, NULL, &a, NULL));
+  OK(ksg_snapshot_view(inc, NULL, NULL, &b, NULL));
+  CHECK(a.n_pods == b.n_pods && a.prog_len == b.prog_len, "%s: sizes differ", s->name);
+  CHECK(a.n_pods == b.n_pods && memcmp(a.pods, b.pods, sizeof(ksg_pod) * a.n_pods) == 0, "%s: pod records differ",
+        s->name);
+  CHECK(a.prog_len == b.prog_len && memcmp(a.prog, b.prog, 4 * a.prog_len) == 0, "%s: programs differ", s->name);
+  printf("ok %s incremental encoding: %d appended, %d full re-encodes, bytes identical\n", s->name, appended, reloads);
+  ksg_snapshot_free(full);
+  ksg_snapshot_free(inc);
+}
+
+static void oracle_queue(kso_ctx* o, const scenario* s, int32_t* pl, ksg_result* res) {
+  OK(kso_run_queue(o, s->n_bound, s->n_pods - s->n_bound, pl, res, NULL));
+}
+
+static int run_cpu(void) {
+  check_kat();
+  scenario sc[2] = {scenario_c2(96, 400, 24), scenario_c3(64, 300, 16, 8)};
+  for (int k = 0; k < 2; k++) {
+    const scenario* s = &sc[k];
+    check_incremental_bytes(s);
+    ksg_snapshot* snap = build(s, s->n_pods);
+    OK(ksg_snapshot_encode(snap));
+    kso_ctx* o = oracle_of(snap, s);
+    const int Q = s->n_pods - s->n_bound;
+    int32_t* pl = A(Q, 4);
+    ksg_result* res = A(Q, sizeof *res);
+    oracle_queue(o, s, pl, res);
+    int placed = 0;
+    for (int i = 0; i < Q; i++) placed += pl[i] >= 0;
+    CHECK(placed > Q / 2, "%s: only %d of %d placed", s->name, placed, Q);
+    printf("ok %s oracle queue: %d of %d pods placed\n", s->name, placed, Q);
+    kso_close(o);
+    ksg_snapshot_free(snap);
+  }
+  return g_fail;
+}
+
+static int run_gpu(void) {
+  scenario sc[2] = {scenario_c2(96, 400, 24), scenario_c3(64, 300, 16, 8)};
+  for (int k = 0; k < 2; k++) {
+    const scenario* s = &sc[k];
+    const int N = s->n_nodes, Q = s->n_pods - s->n_bound;
+    /* (1) whole queue on the device vs the oracle */
+    ksg_snapshot* snap = build(s, s->n_pods);
+    ksg_ctx* ctx;
+    OK(ksg_open(0, &ctx));
+    if (ksg_snapshot_load(snap, ctx)) {
+      fprintf(stderr, "load: %s\n", ksg_snapshot_error(snap));
+      return 2;
+    }
+    int32_t* pl = A(Q, 4);
+    int32_t* want = A(Q, 4);
+    ksg_result* res = A(Q, sizeof *res);
+    ksg_result* wres = A(Q, sizeof *wres);
+    OK(ksg_run_queue(ctx, s->n_bound, Q, pl, res, NULL));
+    kso_ctx* o = oracle_of(snap, s);
+    oracle_queue(o, s, want, wres);
+    int bad = 0;
+    for (int i = 0; i < Q; i++)
+      bad += pl[i] != want[i] || res[i].n_feasible != wres[i].n_feasible || res[i].status != wres[i].status ||
+             res[i].score_skip != wres[i].score_skip;
+    CHECK(bad == 0, "%s: %d of %d pods differ from the oracle (ksg_run_queue)", s->name, bad, Q);
+    printf("ok %s ksg_run_queue: %d pods identical to the oracle\n", s->name, Q);
+    kso_close(o);
+    ksg_close(ctx);
+
+    /* (2) the per-cycle path of the Go shim: add_pod -> sync -> ksg_eval ->
+     * status words / messages -> assume, one pod at a time */
+    ksg_snapshot* cyc = build(s, s->n_bound);
+    OK(ksg_open(0, &ctx));
+    if (ksg_snapshot_load(cyc, ctx)) {
+      fprintf(stderr, "load: %s\n", ksg_snapshot_error(cyc));
+      return 2;
+    }
+    o = oracle_of(snap, s);
+    uint32_t* fs = A(N, 4);
+    uint32_t* wfs = A(N, 4);
+    ksg_capture cap = {fs, NULL, NULL, NULL}, wcap = {wfs, NULL, NULL, NULL};
+    int appended = 0, mismatch = 0, msgs = 0;
+    char msg[512];
+    for (int j = s->n_bound; j < s->n_pods; j++) {
+      int32_t idx, ap;
+      OK(ksg_snapshot_add_pod(cyc, &s->pods[j], &idx));
+      if (ksg_snapshot_sync(cyc, ctx, &ap)) {
+        fprintf(stderr, "sync: %s\n", ksg_snapshot_error(cyc));
+        return 2;
+      }
+      appended += ap;
+      ksg_result r, wr;
+      OK(ksg_eval(ctx, idx, &r, &cap));
+      OK(kso_eval(o, j, &wr, &wcap));
+      if (r.selected != wr.selected || r.n_feasible != wr.n_feasible || memcmp(fs, wfs, 4 * N) != 0) mismatch++;
+      for (int n = 0; n < N; n++) {
+        if (fs[n] == 0 || fs[n] == KSG_FS_NOT_EVALUATED) continue;
+        int32_t code, len;
+        OK(ksg_snapshot_status(cyc, idx, fs[n], n, &code, msg, sizeof msg, &len));
+        CHECK(len > 0 && (code == KSG_CODE_UNSCHEDULABLE || code == KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE),
+              "%s: status of pod %d node %d: code %d '%s'", s->name, j, n, code, msg);
+        msgs++;
+      }
+      if (r.selected >= 0) {
+        OK(ksg_snapshot_assume(cyc, ctx, idx, r.selected));
+        OK(kso_commit(o, j, r.selected));
+      }
+    }
+    CHECK(mismatch == 0, "%s: %d of %d cycles differ from the oracle (per-cycle path)", s->name, mismatch, Q);
+    printf("ok %s per-cycle path: %d cycles (%d appended, %d reloads), status words identical, %d messages\n",
+           s->name, Q, appended, Q - appended, msgs);
+    kso_close(o);
+    ksg_close(ctx);
+    ksg_snapshot_free(cyc);
+    ksg_snapshot_free(snap);
+  }
+  return g_fail;
+}
+
+int main(int argc, char** argv) {
+  const int gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
+  const int rc = gpu ? run_gpu() : run_cpu();
+  printf(rc ? "FAILED (%d checks)\n" : "PASSED\n", rc);
+  return rc ? 1 : 0;
+}

@@ -1,4 +1,6 @@
-"""The C-ABI library loads and exports every entry point include/ksched.h declares."""
+"""The C-ABI library loads and exports every entry point include/*.h declares
+(ksched.h: device evaluator and annotator; ksched_snapshot.h: the native
+snapshot encoder), and the ctypes mirrors have the C compiler's layouts."""
 import ctypes
 import os
 import re
@@ -7,13 +9,20 @@ from conftest import ROOT, pkg
 
 
 def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "ksched.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ksg_\w+)\s*\(", src, re.M)))
+    out = set()
+    inc = os.path.join(ROOT, "include")
+    for h in sorted(os.listdir(inc)):
+        if h.endswith(".h"):
+            src = open(os.path.join(inc, h)).read()
+            out |= set(re.findall(r"^\s*(?:int|const char\*)\s+(ksg_\w+)\s*\(", src, re.M))
+    return sorted(out)
 
 
 def test_header_declares_entry_points():
     syms = declared_symbols()
-    for s in ("ksg_open", "ksg_eval", "ksg_commit", "ksg_run_queue", "ksg_run_replicas", "ksg_last_error"):
+    for s in ("ksg_open", "ksg_eval", "ksg_commit", "ksg_run_queue", "ksg_run_replicas", "ksg_last_error",
+              "ksg_append_pods", "ksg_eval_pod", "ksg_snapshot_new", "ksg_snapshot_add_pod", "ksg_snapshot_sync",
+              "ksg_snapshot_status", "ksg_snapshot_prefilter"):
         assert s in syms
 
 
@@ -23,7 +32,7 @@ def test_library_exports_every_symbol(built):
     missing = [s for s in declared_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     lib.ksg_abi_version.restype = ctypes.c_int
-    assert lib.ksg_abi_version() == 1
+    assert lib.ksg_abi_version() == 2
 
 
 def test_struct_layouts_match(tmp_path):
@@ -52,6 +61,27 @@ def test_struct_layouts_match(tmp_path):
     assert sizes["ksg_kernel_stat"] == ctypes.sizeof(native.KsgKernelStat)
     assert sizes["ksg_names"] == ctypes.sizeof(native.KsgNames)
     assert sizes["ksg_annotate_in"] == ctypes.sizeof(native.KsgAnnotateIn)
+
+
+def test_snapshot_view_layouts(tmp_path):
+    """ctypes mirrors of the ksched_snapshot.h views (snapshot.py)."""
+    import subprocess
+    S = pkg("snapshot")
+    pairs = {"ksg_str_pair": S.StrPair, "ksg_quantity": S.Quantity, "ksg_taint_view": S.TaintView,
+             "ksg_toleration_view": S.TolerationView, "ksg_requirement_view": S.RequirementView,
+             "ksg_node_selector_term_view": S.NodeSelectorTermView, "ksg_preferred_term_view": S.PreferredTermView,
+             "ksg_label_selector_view": S.LabelSelectorView, "ksg_affinity_term_view": S.AffinityTermView,
+             "ksg_spread_view": S.SpreadView, "ksg_container_view": S.ContainerView, "ksg_image_view": S.ImageView,
+             "ksg_node_view": S.NodeView, "ksg_pod_view": S.PodView, "ksg_plugin_view": S.PluginView,
+             "ksg_profile_view": S.ProfileView}
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "ksched_snapshot.h"\nint main(void){' +
+                   "".join(f'printf("%zu\\n", sizeof({n}));' for n in pairs) + "return 0;}")
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    sizes = list(map(int, subprocess.check_output([str(exe)]).split()))
+    for (n, t), sz in zip(pairs.items(), sizes):
+        assert sz == ctypes.sizeof(t), n
 
 
 def test_product_path_fails_loudly_without_library(tmp_path):

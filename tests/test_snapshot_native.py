@@ -1,0 +1,214 @@
+"""The native snapshot encoder (include/ksched_snapshot.h, C++) against the
+Python restatement (encoder.py): byte-identical SoA columns, pod records,
+program pool and profile on every workload family, through the C views only
+(no device needed).  Also: the incremental append path (a new pod encoded
+against the loaded universe) gives exactly the full re-encode's bytes, and
+the framework.Status codes / messages the Go shim returns."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import pkg
+
+E = pkg("encoder")
+G = pkg("generator")
+P = pkg("profile")
+m = pkg("model")
+S = pkg("snapshot")
+F = pkg("framework")
+
+import make_golden_loader as mg  # noqa: E402
+import zoo  # noqa: E402
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = json.load(open(os.path.join(HERE, "cases.json")))
+
+
+def _py_arrays(enc):
+    a = enc.cluster.arrays
+    L = max(len(enc.cluster.label_cols), 1)
+    out = {k: a[k] for k in ("alloc", "requested", "nonzero", "allowed_pods", "pod_count", "unschedulable",
+                             "taints", "taint_effect", "images", "tmpl_col", "tmpl_kind", "tmpl_weight",
+                             "log_table", "col_unique", "col_vocab")}
+    out["label_val"] = a["label_val"].reshape(L, -1)
+    out["label_num"] = a["label_num"].reshape(L, -1)
+    out["label_num_ok"] = a["label_num_ok"].reshape(L, -1)
+    out["pods"] = enc.workload.pods
+    out["prog"] = enc.workload.prog
+    return out
+
+
+def _assert_same(nodes, pods, prof, bound=()):
+    enc = E.Encoder(nodes, pods, prof)
+    snap = S.Snapshot(prof, nodes, pods, bound)
+    snap.encode()
+    got = snap.arrays()
+    want = _py_arrays(enc)
+    for k, v in want.items():
+        g = got[k]
+        assert g.dtype == np.asarray(v).dtype or k == "pods", k
+        if k == "log_table":
+            assert g.tobytes() == np.asarray(v, np.float64).tobytes(), k
+        else:
+            np.testing.assert_array_equal(g, np.asarray(v), err_msg=k)
+    assert got["pods"].tobytes() == enc.workload.pods.tobytes()
+    meta = got["meta"]
+    assert meta["n_label_cols"] == len(enc.cluster.label_cols)
+    assert meta["n_taint_vocab"] == len(enc.cluster.taint_vocab)
+    assert meta["n_images"] == enc.cluster.n_images
+    assert meta["n_selectors"] == enc.cluster.n_selectors
+    assert meta["n_templates"] == enc.cluster.n_templates
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    for k, v in pf.items():
+        assert got["profile"][k] == v, k
+    return snap, enc
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_zoo(built, seed):
+    nodes, pods, prof = zoo.zoo(seed)
+    _assert_same(nodes, pods, prof)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_golden_cases(built, name):
+    c = CASES[name]
+    nodes, pods, prof = mg.make(c["generator"], c["args"])
+    _assert_same(nodes, pods, prof)
+
+
+@pytest.mark.parametrize("make", [
+    lambda: G.config1(n_nodes=60, n_pods=200),
+    lambda: G.config2(n_nodes=300, n_pods=500),
+    lambda: G.config3(n_nodes=400, n_pods=1200),
+    lambda: G.config5(n_nodes=300, n_pods=200, n_images=300, taint_vocab=128, taints_per_node=16,
+                      images_per_node=20),
+    lambda: G.readme_kat(),
+], ids=["c1", "c2", "c3", "c5", "kat"])
+def test_configs(built, make):
+    nodes, pods, prof = make()
+    _assert_same(nodes, pods, prof)
+
+
+def test_preemption_case_with_bindings(built):
+    nodes, pods, bound, prof = G.preemption_case()
+    _assert_same(nodes, pods, prof, bound)
+
+
+def test_profiles_and_args(built):
+    nodes, pods, _ = zoo.zoo(3)
+    for prof in [P.Profile(fit_strategy=P.MOST_ALLOCATED, fit_resources=[(m.CPU, 3), (m.MEMORY, 1),
+                                                                            ("example.com/fpga", 2)],
+                           ba_resources=[(m.CPU, 1), (m.MEMORY, 1), ("example.com/fpga", 1)],
+                           fit_ignored_resources=("example.com/fpga",), hard_pod_affinity_weight=5,
+                           ignore_preferred_terms_of_existing_pods=True, ba_skip_best_effort=True),
+                 P.Profile(plugins=[(n + "Wrapped", w) for n, w in P.DEFAULT_MULTIPOINT], pts_system_defaulted=False,
+                           fit_ignored_resource_groups=("example.com",))]:
+        _assert_same(nodes, pods, prof)
+
+
+def test_unsupported_inputs_refused(built):
+    nodes, pods, prof = zoo.zoo(1)
+    pods = list(pods)
+    pods[3].containers[0].host_ports = (("", "TCP", 8080),)
+    snap = S.Snapshot(prof, nodes, pods)
+    with pytest.raises(S.SnapshotError, match="hostPorts"):
+        snap.encode()
+    with pytest.raises(S.SnapshotError):
+        S.Snapshot(P.Profile(plugins=[("NoSuchPlugin", 1)]))
+
+
+def _frozen_vs_full(nodes, pods, prof, split):
+    """Encode pods[:split], then the rest through the frozen (append) pass;
+    compare with one full encode of all pods."""
+    full = S.Snapshot(prof, nodes, pods)
+    full.encode()
+    want = full.arrays()
+    snap = S.Snapshot(prof, nodes, pods[:split])
+    snap.encode()
+    for p in pods[split:]:
+        snap.add_pod(p)
+    appended = snap.encode_incremental()
+    got = snap.arrays()
+    return appended, got, want
+
+
+def test_append_equals_full_encode(built):
+    """config 2: later pods reuse the universe (label columns, value ids,
+    taint vocabulary): the appended encoding is byte-identical."""
+    nodes, pods, prof = G.config2(n_nodes=200, n_pods=400)
+    appended, got, want = _frozen_vs_full(nodes, pods, prof, 300)
+    assert appended
+    assert got["pods"].tobytes() == want["pods"].tobytes()
+    np.testing.assert_array_equal(got["prog"], want["prog"])
+    np.testing.assert_array_equal(got["col_vocab"], want["col_vocab"])
+
+
+def test_append_config3_selectors(built):
+    """config 3: appended pods match existing selectors / templates (commit
+    and IPA programs computed against the loaded universe)."""
+    nodes, pods, prof = G.config3(n_nodes=200, n_pods=1500, apps=20)
+    appended, got, want = _frozen_vs_full(nodes, pods, prof, 1400)
+    assert appended
+    assert got["pods"].tobytes() == want["pods"].tobytes()
+    np.testing.assert_array_equal(got["prog"], want["prog"])
+
+
+def test_append_new_universe_falls_back(built):
+    """A pod with a new label key cannot be appended: the pass reports it."""
+    nodes, pods, prof = G.config2(n_nodes=50, n_pods=60)
+    pods = list(pods)
+    pods[-1].node_selector = {"brand-new-key": "x"}
+    appended, got, want = _frozen_vs_full(nodes, pods, prof, 59)
+    assert not appended
+    assert got["pods"].tobytes() == want["pods"].tobytes()
+
+
+def test_status_codes_and_messages(built):
+    """framework.Status of each filter word: the code the upstream plugin
+    returns (UnschedulableAndUnresolvable for the node-static plugins and
+    for affinity / missing-label rejections) and the Decoder's message."""
+    nodes, pods, prof = zoo.zoo(2)
+    enc = E.Encoder(nodes, pods, prof)
+    snap = S.Snapshot(prof, nodes, pods)
+    snap.encode()
+    dec = F.Decoder(enc)
+    import binding
+    o = binding.Oracle(1)
+    o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    seen = set()
+    for pi in range(40):
+        cap = pkg("native").CaptureBuffers(len(nodes), 1)
+        o.eval(pi, cap)
+        for n, w in enumerate(cap.fstatus[0]):
+            w = int(w)
+            if w in (0, E.FS_NOT_EVALUATED):
+                continue
+            code, msg = snap.status(pi, w, n)
+            assert msg == dec.message(w, n)
+            assert code == F.status_code(w, enc, pi, n)
+            seen.add((w & 0xFF) - 1)
+        o.commit(pi, max(0, int(np.argmin(cap.fstatus[0]))))
+    assert {P.TAINT_TOLERATION, P.NODE_RESOURCES_FIT} <= seen
+
+
+def test_prefilter_statuses(built):
+    nodes, pods, prof = zoo.zoo(4)
+    enc = E.Encoder(nodes, pods, prof)
+    snap = S.Snapshot(prof, nodes, pods)
+    snap.encode()
+    for pi, rec in enumerate(enc.workload.pods):
+        for pid in prof.prefilter_order():
+            code, names = snap.prefilter(pi, pid)
+            if pid == P.NODE_AFFINITY and rec["flags"] & E.POD_FLAG_PREFILTER_REJECT:
+                assert code == S.CODE_UNRESOLVABLE
+            elif (int(rec["filter_skip"]) >> pid) & 1:
+                assert code == S.CODE_SKIP
+            else:
+                assert code == S.CODE_SUCCESS
+            if pid == P.NODE_AFFINITY and int(rec["node_set"]) >= 0:
+                assert names == enc.prefilter_node_names[pi]
+            else:
+                assert names is None
