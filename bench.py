@@ -12,12 +12,21 @@ input already resident in HBM.
 Multi-GPU: the per-pod decision does not shard (every binding changes the
 state the next pod reads), so N GPUs run N independent what-if replicas of the
 same queue (weak scaling, no data-path collective); value = pods scheduled by
-all ranks / max-over-ranks time.
+all ranks / max-over-ranks time.  The process group is RCCL ("nccl") at every
+N, N = 1 included (a one-rank group on 127.0.0.1), so the collectives run on
+the box.
 
-Prints ONE JSON line (rank 0).  At N=1 the line also carries
-`replica_sweep`: BASELINE configs[3] (1,024 what-if replicas of the first
-1,000 pods on the same cluster), the HBM-bound regime of the same path, with
-the roofline of its dominant kernel.
+Prints ONE JSON line (rank 0).  The line also carries:
+* `replica_sweep`: BASELINE configs[3], 1,024 what-if replicas (weights and
+  strategy per replica) of the first 1,000 pods on the same cluster, sharded
+  over the N ranks by replicas.run_sweep (contiguous replica blocks, one
+  RCCL all_gather of placements + summaries at the end): aggregate
+  replica-pods/s over max-over-ranks time, the roofline of its dominant
+  kernel, and a digest of all 1,024 replicas' placements (identical at every
+  N);
+* `cpu_baseline` (rank 0, N = 1): the C++ restatement (oracle/) on a bounded
+  prefix of the same queue, at 16 threads (upstream parallelism) and at every
+  host core this process may use, with the CPU model.
 """
 from __future__ import annotations
 
@@ -35,6 +44,16 @@ PKG = "kube-scheduler-simulator_amd"
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(enc, pf, n_threads: int, budget_s: float):
@@ -59,30 +78,65 @@ def cpu_baseline(enc, pf, n_threads: int, budget_s: float):
             "node_evals_per_sec": done * len(enc.cluster.node_names) / dt}
 
 
-def replica_sweep(eng, enc, prof, G, E, metrics, R: int, P: int):
+def cpu_baselines(enc, pf, budget_s: float):
+    """16 threads (upstream parallelism: 16) and every host core
+    this process may run on (sched_getaffinity; nproc of the machine beside it)."""
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    out = cpu_baseline(enc, pf, 16, budget_s)
+    out["cpu_model"] = cpu_model()
+    out["nproc"] = os.cpu_count()
+    out["usable_cores"] = usable
+    if usable != 16:
+        allc = cpu_baseline(enc, pf, usable, budget_s)
+        out["all_cores"] = {k: allc[k] for k in ("value", "cores", "sample", "node_evals_per_sec")}
+    return out
+
+
+def replica_sweep(eng, enc, prof, G, E, metrics, replicas, R: int, P: int, rank: int, world: int, dist, dev):
     """BASELINE configs[3] beside the headline: R what-if replicas (weights and
     strategy per replica, generator.replica_profiles) of the first P pods of
-    the same queue on the same cluster, one ksg_run_replicas launch chain.
-    This is the HBM-bound regime of the path; device time from
-    HIP events on the library's stream, roofline of the dominant kernel."""
+    the same queue on the same cluster, sharded over the ranks by
+    replicas.run_sweep (one ksg_run_replicas launch chain per rank, then one
+    RCCL all_gather of placements + summaries).  The HBM-bound regime of the
+    path: max-over-ranks wall time of the sharded sweep,
+    device time of each rank's block from HIP events on the library's
+    stream, roofline of the dominant kernel."""
+    import hashlib
+    import numpy as np
+    import torch
     profiles = [E.encode_profile(p, enc.cluster.res_names) for p in G.replica_profiles(R)]
-    eng.run_replicas(profiles, 0, P)   # warmup
-    ms, walls = [], []
+    replicas.run_sweep(eng, profiles, 0, P, rank=rank, world=world, device=dev)   # warmup
+    walls, ms = [], []
     for _ in range(3):
+        dist.barrier()
+        torch.cuda.synchronize()
         t = time.perf_counter()
-        eng.run_replicas(profiles, 0, P)
-        walls.append((time.perf_counter() - t) * 1e3)
-        ms.append(eng.last_kernel_ms())
-    eng.set_timing(True)
-    eng.run_replicas(profiles, 0, P)
-    ks = eng.kernel_stats()
-    eng.set_timing(False)
-    kms = min(ms)
+        pl, sm = replicas.run_sweep(eng, profiles, 0, P, rank=rank, world=world, device=dev)
+        torch.cuda.synchronize()
+        w = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=dev)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        walls.append(float(w.item()) * 1e3)
+        k = torch.tensor([eng.last_kernel_ms()], dtype=torch.float64, device=dev)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        ms.append(float(k.item()))
+    lo, hi = replicas.shard(R, world, rank)
+    ks = []
+    if hi > lo:
+        eng.set_timing(True)
+        eng.run_replicas(profiles[lo:hi], 0, P)
+        ks = eng.kernel_stats()
+        eng.set_timing(False)
+    kms, wms = min(ms), min(walls)
     n = len(enc.cluster.node_names)
-    return {"workload": f"configs[3]: {R} replicas x {n} nodes, first {P} pods of the configs[1] queue",
-            "replica_pods_per_s": R * P / (kms * 1e-3), "node_evals_per_s": R * P * n / (kms * 1e-3),
-            "device_ms": kms, "wall_ms": min(walls),
-            "roofline": metrics.dominant_kernel_roofline(ks, metrics.bytes_per_node_eval(enc, prof))}
+    return {"workload": f"configs[3]: {R} replicas x {n} nodes, first {P} pods of the configs[1] queue, "
+                        f"sharded over {world} rank(s), RCCL all_gather of placements + summaries",
+            "replica_pods_per_s": R * P / (wms * 1e-3), "node_evals_per_s": R * P * n / (wms * 1e-3),
+            "wall_ms": wms, "device_ms_max_rank": kms,
+            "device_replica_pods_per_s": R * P / (kms * 1e-3),
+            "replicas_per_rank": hi - lo, "collective": "nccl (RCCL) all_gather",
+            "placements_sha256": hashlib.sha256(np.ascontiguousarray(pl).tobytes()).hexdigest(),
+            "scheduled_total": int(sm[:, 0].sum()),
+            "roofline": metrics.dominant_kernel_roofline(ks, metrics.bytes_per_node_eval(enc, prof)) if ks else None}
 
 
 def main():
@@ -92,7 +146,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods", type=int, default=50000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep-replicas", type=int, default=1024, help="configs[3] sidecar; 0 disables")
@@ -104,16 +157,24 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl", init_method="env://")
+    import torch.distributed as dist
+    if "MASTER_ADDR" not in os.environ:   # N = 1 without a launcher: a one-rank RCCL group
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]), RANK="0",
+                          WORLD_SIZE="1", LOCAL_RANK="0")
+        sk.close()
+    torch.cuda.set_device(local_rank)
+    dev = f"cuda:{local_rank}"
+    dist.init_process_group(backend="nccl", init_method="env://", world_size=world, rank=rank,
+                            device_id=torch.device(dev))
 
     G = importlib.import_module(PKG + ".generator")
     E = importlib.import_module(PKG + ".encoder")
     native = importlib.import_module(PKG + ".native")
     metrics = importlib.import_module(PKG + ".metrics")
+    replicas = importlib.import_module(PKG + ".replicas")
 
     t = time.perf_counter()
     nodes, pods, prof = G.config2(n_nodes=args.nodes, n_pods=args.pods)
@@ -124,36 +185,30 @@ def main():
     eng.load(enc, pf)   # inputs resident in HBM from here on
     P = len(pods)
 
-    gather_out = None
-    if dist:
-        gather_out = [torch.empty(P, dtype=torch.int32, device=f"cuda:{local_rank}") for _ in range(world)]
+    gather_out = [torch.empty(P, dtype=torch.int32, device=dev) for _ in range(world)]
 
     def step():
         eng.reset_state()
         pl, _ = eng.run_queue(0, P, results=False)
-        if dist:
-            # the one exchange of the replica sweep: every replica's placements to every rank (RCCL)
-            dist.all_gather(gather_out, torch.from_numpy(pl).to(f"cuda:{local_rank}"))
+        # the one exchange of the replica sweep: every replica's placements to every rank (RCCL)
+        dist.all_gather(gather_out, torch.from_numpy(pl).to(dev))
         return pl
 
     for _ in range(args.warmup):
         step()
     kernel_ms = []
-    if dist:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pl = step()
         kernel_ms.append(eng.last_kernel_ms())
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
     scheduled = int((pl >= 0).sum())
     # one extra, untimed step with per-kernel HIP-event timing (ksg_set_timing)
     kstats = []
@@ -164,6 +219,14 @@ def main():
         eng.set_timing(False)
     except Exception as e:   # timing is diagnostic; never lose the bench line over it
         log(f"[rank {rank}] per-kernel timing unavailable: {e}")
+
+    sweep = None
+    if args.sweep_replicas > 0:
+        try:
+            sweep = replica_sweep(eng, enc, prof, G, E, metrics, replicas, args.sweep_replicas,
+                                  min(args.sweep_pods, P), rank, world, dist, dev)
+        except Exception as e:   # a sidecar; never lose the headline line over it
+            log(f"[rank {rank}] replica sweep unavailable: {e}")
 
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
@@ -185,13 +248,13 @@ def main():
         # passes (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE
         # + WRITE_SIZE per dispatch, gfx950-corrected), null when not collected
         roof["traffic"] = None
-        pmc = os.path.join(ROOT, "profiles", "r1", "pmc_config2.json")
+        pmc = os.path.join(ROOT, "profiles", "r2", "pmc_config2.json")
         if os.path.exists(pmc) and roof.get("kernel"):
             try:
                 row = json.load(open(pmc)).get(roof["kernel"])
                 if row:
                     roof["traffic"] = row["hbm_bytes_per_dispatch"]
-                    roof["traffic_source"] = "profiles/r1/pmc_config2.json"
+                    roof["traffic_source"] = "profiles/r2/pmc_config2.json"
             except Exception:
                 pass
         roof["bytes_per_node_eval"] = bpe
@@ -208,17 +271,13 @@ def main():
             "node_evals_per_sec": node_evals,
             "roofline": roof,
         }
+        if sweep is not None:
+            out["replica_sweep"] = sweep
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(enc, pf, args.cpu_threads, args.cpu_budget)
-        if args.sweep_replicas > 0 and world == 1:
-            try:
-                out["replica_sweep"] = replica_sweep(eng, enc, prof, G, E, metrics, args.sweep_replicas,
-                                                     min(args.sweep_pods, P))
-            except Exception as e:   # a sidecar; never lose the headline line over it
-                log(f"replica sweep unavailable: {e}")
+            out["cpu_baseline"] = cpu_baselines(enc, pf, args.cpu_budget)
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -304,7 +304,9 @@ enum {
   KSG_K_SWEEP_STATIC = 7,
   KSG_K_SWEEP = 8,
   KSG_K_TOPO_COOP = 9,
-  KSG_NKERNELS = 10
+  KSG_K_BATCH_PHASE2P = 10,
+  KSG_K_SWEEP_NARROW = 11,
+  KSG_NKERNELS = 12
 };
 typedef struct ksg_kernel_stat {
   char name[48];

@@ -242,6 +242,12 @@ struct BatchArgs {
   uint64_t* top;            // [KSG_BATCH_MAX][KSG_BATCH_MAX] top-set argmax keys
   int32_t* placements;
   ksg_result* results;      // or null
+  // pipelined phase 2 (ksched_phase2p.h): the two-batch window
+  int32_t k_extra;          // top sets hold min(j + 1 + k_extra, nfeas) keys
+  const int32_t* carry;     // nodes the previous batch changed (slot order), or null
+  const int32_t* carry_n;   // their count (device), or null
+  int32_t* carry_out;       // this batch's changed nodes, for the next batch
+  int32_t* carry_out_n;
 };
 
 // record: bit 63 feasible | rt (8 bits) << 48 | ra (16 bits) << 32 | partial (32 bits)
@@ -596,7 +602,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
     gha += s_i[i][3];
     gerr |= s_i[i][4];
   }
-  const int K = min(j + 1, gn);
+  const int K = min(j + 1 + a.k_extra, gn);
   if (tid == 0) {
     P1Stats s;
     s.nfeas = gn;
@@ -1614,6 +1620,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 #endif
 }
 
+#include "ksched_phase2p.h"
 #include "ksched_sweep.h"
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
@@ -2130,6 +2137,17 @@ struct ksg_ctx {
   int32_t* d_pmax = nullptr;
   P1Stats* d_p1 = nullptr;
   uint64_t* d_top = nullptr;
+  // pipelined path (two buffer sets by batch parity, a second stream for
+  // phase 1 + top-k, the carried changed set)
+  uint64_t* d_prec[2] = {nullptr, nullptr};
+  int32_t* d_pimg[2] = {nullptr, nullptr};
+  int32_t* d_ppmax[2] = {nullptr, nullptr};
+  P1Stats* d_pp1[2] = {nullptr, nullptr};
+  uint64_t* d_ptop[2] = {nullptr, nullptr};
+  int32_t* d_carry = nullptr;          // [2][KSG_BATCH_MAX] slot node lists, then [2] counts
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_tk[2] = {nullptr, nullptr}, ev_p2[2] = {nullptr, nullptr};
+  int pipe_window = 1;                 // env KSG_PIPE_WINDOW=0: no overlap, no carried set
   // DefaultPreemption dry-run scratch (grow-only)
   int32_t* d_pre = nullptr;
   size_t pre_words = 0;
@@ -2142,8 +2160,12 @@ struct ksg_ctx {
   int coop_gmax = 0;                  // co-resident workgroups of ksg_topo_coop
   bool topo_coop = true;              // env KSG_TOPO_COOP=0 disables
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
-  int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched
-  int batch_mode = 2;  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default)
+  int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched, 3 int64 sweep state
+  bool last_narrow = false;   // the last replica sweep ran on the narrow records
+  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default), 3 "pipe"
+  // (the pipelined phase 2 is exact but measured slower than slot:
+  // profiles/r2/phase2_modes.log)
+  int batch_mode = 2;
   int slot_block = 128;  // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (128: 1-2 % faster end to end than 256)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
@@ -2209,6 +2231,14 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_pmax = nullptr;
   ctx->d_p1 = nullptr;
   ctx->d_top = nullptr;
+  for (int q = 0; q < 2; q++) {
+    ctx->d_prec[q] = nullptr;
+    ctx->d_pimg[q] = nullptr;
+    ctx->d_ppmax[q] = nullptr;
+    ctx->d_pp1[q] = nullptr;
+    ctx->d_ptop[q] = nullptr;
+  }
+  ctx->d_carry = nullptr;
   ctx->d_stamps = nullptr;
   ctx->d_coop_acc = nullptr;
   ctx->d_coop_flags = nullptr;
@@ -2221,7 +2251,7 @@ void free_all(ksg_ctx* ctx) {
 const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_batch_phase1",
                                           "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan",
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
-                                          "ksg_topo_coop"};
+                                          "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2524,6 +2554,137 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   return KSG_OK;
 }
 
+// ksg_batch_phase2p instances: (RM 4 | KSG_MAX_RES) x (SLOTS 128 | 256)
+static const std::array<const void*, 4>& pipe_kernels() {
+  static const std::array<const void*, 4> k = {
+      (const void*)ksg_batch_phase2p<4, 128>, (const void*)ksg_batch_phase2p<4, 256>,
+      (const void*)ksg_batch_phase2p<KSG_MAX_RES, 128>, (const void*)ksg_batch_phase2p<KSG_MAX_RES, 256>};
+  return k;
+}
+
+// Pipelined batched path (ksched_phase2p.h).  Batch b's phase 1 + top-k run on
+// a second stream while batch b - 1's phase 2 runs: phase 1 of batch b reads
+// the state at least as of the end of batch b - 2 (it waits for that phase 2),
+// and phase 2 of batch b carries batch b - 1's changed nodes as changed slots
+// (the two-batch window; top sets hold k_extra = |batch b - 1| extra keys).
+// With per-kernel timing on, every launch goes to one stream (same
+// arithmetic, no overlap) so that each launch is timed on its own.
+int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const ksg_profile* d_prof) {
+  const int N = ctx->c.N;
+  int rc;
+  if (!ctx->d_prec[0]) {
+    for (int q = 0; q < 2; q++) {
+      if ((rc = dalloc(ctx, &ctx->d_prec[q], (size_t)KSG_BATCH_MAX * N))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_pimg[q], (size_t)KSG_BATCH_MAX * N))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_ppmax[q], (size_t)2 * KSG_BATCH_MAX))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_pp1[q], (size_t)KSG_BATCH_MAX))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_ptop[q], (size_t)KSG_BATCH_MAX * KSG_BATCH_MAX))) return rc;
+      HIPC(ctx, hipMemsetAsync(ctx->d_ppmax[q], 0, sizeof(int32_t) * 2 * KSG_BATCH_MAX, ctx->stream));
+    }
+    if ((rc = dalloc(ctx, &ctx->d_carry, (size_t)2 * KSG_BATCH_MAX + 2))) return rc;
+  }
+  if (!ctx->stream2) {
+    HIPC(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    for (int q = 0; q < 2; q++) {
+      HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_tk[q], hipEventDisableTiming));
+      HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_p2[q], hipEventDisableTiming));
+    }
+  }
+  int32_t* carry_n = ctx->d_carry + 2 * KSG_BATCH_MAX;   // [2]
+  HIPC(ctx, hipMemsetAsync(carry_n, 0, 2 * sizeof(int32_t), ctx->stream));
+  const bool window = ctx->pipe_window != 0;
+  const bool overlap = window && !ctx->timing;
+  const int B = window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
+  const int slots = window ? 2 * B : B;   // carried + this batch's slots
+  const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
+  const void* kern = pipe_kernels()[(slot_rm == 4 ? 0 : 2) + (slots <= 128 ? 0 : 1)];
+  const int block = 2 * (slots <= 128 ? 128 : 256);
+  constexpr size_t kLdsBudget = 96 * 1024;
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (const void* f : pipe_kernels())
+      HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
+    attr_set = true;
+  }
+  BatchArgs b{};
+  b.c = ctx->c;
+  b.st = ctx->st;
+  b.pods = ctx->d_pods;
+  b.prog = ctx->d_prog;
+  b.prof = d_prof;
+  b.placements = d_pl;
+  b.results = d_res;
+  const size_t cm_words = (size_t)((((N + 31) / 32) + 3) & ~3);
+#ifdef KSG_STAMPS
+  if (!ctx->d_stamps) {
+    if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 128, ctx->stream));
+  }
+  b.stamps = ctx->d_stamps;
+#endif
+  hipStream_t s1 = overlap ? ctx->stream2 : ctx->stream, s2 = ctx->stream;
+  (void)hipGetLastError();
+  treset(ctx);
+  HIPC(ctx, hipEventRecord(ctx->ev0, s2));
+  if (overlap) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev0, 0));
+  if ((rc = tmark(ctx))) return rc;
+  int prev_nb = 0;
+  for (int off = 0, bi = 0; off < count; bi++) {
+    const int par = bi & 1;
+    int nb = std::min(B, count - off);
+    int64_t lo = 0, hi = 0;
+    size_t bytes = 0;
+    for (;;) {
+      lo = ctx->h_pods[first + off].blob;
+      hi = lo;
+      for (int k = 0; k < nb; k++) {
+        const ksg_pod& q = ctx->h_pods[first + off + k];
+        lo = std::min<int64_t>(lo, q.blob);
+        hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
+      }
+      bytes = 4 * ((2 * cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3);
+      if (bytes <= kLdsBudget || nb == 1) break;
+      nb = std::max(1, nb / 2);
+    }
+    if (bytes > kLdsBudget) return fail(ctx, KSG_E_UNSUPPORTED, "batch does not fit the LDS budget");
+    b.b0 = first + off;
+    b.out0 = off;
+    b.nb = nb;
+    b.prog_lo = (int32_t)lo;
+    b.prog_len = (int32_t)(hi - lo);
+    b.rec = ctx->d_prec[par];
+    b.img = ctx->d_pimg[par];
+    b.pmax = ctx->d_ppmax[par];
+    b.p1 = ctx->d_pp1[par];
+    b.top = ctx->d_ptop[par];
+    b.k_extra = window ? prev_nb : 0;
+    b.carry = window ? ctx->d_carry + (par ^ 1) * KSG_BATCH_MAX : nullptr;
+    b.carry_n = window ? carry_n + (par ^ 1) : nullptr;
+    b.carry_out = window ? ctx->d_carry + par * KSG_BATCH_MAX : nullptr;
+    b.carry_out_n = window ? carry_n + par : nullptr;
+    const double units = (double)nb * N;
+    // phase 1 of batch b reads the state as of the end of batch b - 2 at least,
+    // and reuses the buffers phase 2 of batch b - 2 read
+    if (overlap && bi >= 2) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev_p2[par], 0));
+    hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, nb), dim3(256), 0, s1, b);
+    if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return rc;
+    hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(nb), dim3(512), 0, s1, b);
+    if ((rc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return rc;
+    if (overlap) {
+      HIPC(ctx, hipEventRecord(ctx->ev_tk[par], s1));
+      HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
+    }
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(kern)), dim3(1), dim3(block), bytes, s2, b);
+    if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2P, 0.5 * nb * (nb + 1)))) return rc;
+    if (overlap) HIPC(ctx, hipEventRecord(ctx->ev_p2[par], s2));
+    prev_nb = nb;
+    off += nb;
+  }
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipEventRecord(ctx->ev1, s2));
+  return KSG_OK;
+}
+
 // The replica sweep packs the replica-independent plugin results into 8-byte
 // static records and the per-replica result into pack_rec(); use it when
 // every replica profile is node-local and the values provably fit.
@@ -2546,21 +2707,27 @@ bool sweep_eligible(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first,
 }
 
 // mode: 0 generic arithmetic, 1 fast (Fit/BA over {cpu, memory}), 2 fast with
-// one scalar Fit column (instantiated for the spill-free shapes only)
+// one scalar Fit column (instantiated for the spill-free shapes only);
+// narrow: the 16-byte records (fast modes only)
 template <int BLOCK, int KN, bool MULTI>
-void launch_sweep(const SweepArgs& s, int grid, int mode, hipStream_t st) {
-  if (mode == 1) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
+void launch_sweep(const SweepArgs& s, int grid, int mode, bool narrow, hipStream_t st) {
+  if (mode == 1 && narrow) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, false, true>), dim3(grid), dim3(BLOCK), 0, st, s);
+  else if (mode == 1) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
   else hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, false, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
 }
 template <int BLOCK, int KN, bool MULTI>
-void launch_sweep_ex(const SweepArgs& s, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, true>), dim3(grid), dim3(BLOCK), 0, st, s);
+void launch_sweep_ex(const SweepArgs& s, int grid, bool narrow, hipStream_t st) {
+  if (narrow) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, true, true>), dim3(grid), dim3(BLOCK), 0, st, s);
+  else hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, true>), dim3(grid), dim3(BLOCK), 0, st, s);
 }
 
 template <int BLOCK, int KN>
-int sweep_occupancy(ksg_ctx* ctx, int mode, int* occ) {   // the MULTI instances
-  const void* f = mode == 2 ? (const void*)ksg_sweep<BLOCK, KN, true, true, true>
-                  : mode == 1 ? (const void*)ksg_sweep<BLOCK, KN, true, true> : (const void*)ksg_sweep<BLOCK, KN, false, true>;
+int sweep_occupancy(ksg_ctx* ctx, int mode, bool narrow, int* occ) {   // the MULTI instances
+  const void* f = mode == 2 ? (narrow ? (const void*)ksg_sweep<BLOCK, KN, true, true, true, true>
+                                      : (const void*)ksg_sweep<BLOCK, KN, true, true, true>)
+                  : mode == 1 ? (narrow ? (const void*)ksg_sweep<BLOCK, KN, true, true, false, true>
+                                        : (const void*)ksg_sweep<BLOCK, KN, true, true>)
+                              : (const void*)ksg_sweep<BLOCK, KN, false, true>;
   HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, f, BLOCK, 0));
   return KSG_OK;
 }
@@ -2594,17 +2761,73 @@ bool profile_cm_fast(const ksg_profile& prof) {
          prof.fit_w[0] > 0 && prof.fit_w[1] > 0;
 }
 
-// R replicas of pods [first, first + count) on the state already copied into
-// a.st (replica strides set); placements [R][count] on the device.
-int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, const ksg_profile* d_prof, int R,
-              int first, int count, int32_t* d_pl, Tmp& tmp) {
+// The sweep's arithmetic form: 0 generic, 1 fast {cpu, memory}, 2 fast with
+// one scalar Fit column.
+int sweep_mode(const ksg_profile* profiles, int R) {
   bool fast = true, ex = false;
   for (int r = 0; r < R; r++) {
     const bool cm = profile_cm_fast(profiles[r]), exf = !cm && profile_ex_fast(profiles[r]);
     fast = fast && (cm || exf);
     ex = ex || exf;
   }
-  const int mode = !fast ? 0 : (ex ? 2 : 1);
+  return !fast ? 0 : (ex ? 2 : 1);
+}
+
+// Host half of the narrow-state check (the node half is ksg_narrow_init):
+// fast arithmetic; every replica filters with Fit and every pod runs it (so
+// the Fit filter bounds the requested sums and the pod count); the pods
+// request cpu, memory and at most one scalar column, the one every ex
+// replica scores (and no replica ignores); memory quantities in whole MiB.
+// Fills the pod-side bounds.
+bool narrow_candidate(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first, int count, int mode,
+                      NarrowBounds* b) {
+  if (mode == 0 || ctx->force_path == 3) return false;
+  int nx = -1;
+  for (int r = 0; r < R; r++) {
+    const ksg_profile& prof = profiles[r];
+    bool fit = false;
+    for (int k = 0; k < prof.n_filter; k++) fit |= prof.filter_order[k] == KSG_PL_NODE_RESOURCES_FIT;
+    if (!fit) return false;
+    if (mode == 2 && !profile_cm_fast(prof))
+      for (int i = 0; i < prof.fit_n; i++)
+        if (prof.fit_res[i] >= 3) {
+          if (nx >= 0 && nx != prof.fit_res[i]) return false;
+          nx = prof.fit_res[i];
+        }
+  }
+  if (mode == 2 && nx < 0) return false;
+  for (int r = 0; r < R; r++)
+    if (nx >= 0 && ((profiles[r].fit_ignored_res >> nx) & 1u)) return false;
+  constexpr int64_t kMiB = (int64_t)1 << kNarrowMemShift;
+  int64_t xc = 0, xm = 0;
+  for (int i = first; i < first + count; i++) {
+    const ksg_pod& p = ctx->h_pods[i];
+    if ((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) return false;
+    for (int r = 0; r < KSG_MAX_RES; r++)
+      if (p.req[r] < 0 || (r >= 2 && r != nx && p.req[r] != 0)) return false;
+    if (p.req[KSG_RES_CPU] > INT32_MAX || p.nz_cpu < 0 || p.nz_cpu > INT32_MAX) return false;
+    if (nx >= 0 && p.req[nx] > 255) return false;
+    if (((p.req[KSG_RES_MEM] | p.nz_mem) & (kMiB - 1)) != 0 || p.nz_mem < 0) return false;
+    if ((p.req[KSG_RES_MEM] >> kNarrowMemShift) > INT32_MAX) return false;
+    xc = std::max(xc, p.nz_cpu - p.req[KSG_RES_CPU]);
+    xm = std::max(xm, (p.nz_mem - p.req[KSG_RES_MEM]) >> kNarrowMemShift);
+  }
+  if (xc > INT32_MAX || xm >= ((int64_t)1 << 24)) return false;
+  b->xc = xc;
+  b->xm = xm;
+  b->nx = nx;
+  b->places = std::min(count, 255);
+  return true;
+}
+
+// R replicas of pods [first, first + count) on the state already copied into
+// a.st (replica strides set), or on the narrow records when nstat is set;
+// placements [R][count] on the device.
+int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, const ksg_profile* d_prof, int R,
+              int first, int count, int32_t* d_pl, Tmp& tmp, const int4* nstat = nullptr, int4* nmut = nullptr,
+              int nx = -1) {
+  const int mode = sweep_mode(profiles, R);
+  const bool narrow = nstat != nullptr;
   const int N = ctx->c.N;
   constexpr int kBatch = 64;
   SweepArgs s{};
@@ -2615,6 +2838,9 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   s.profiles = d_prof;
   s.count = count;
   s.placements = d_pl;
+  s.nstat = nstat;
+  s.nmut = nmut;
+  s.nx = nx;
   TA(tmp, &s.srec, sizeof(uint64_t) * (size_t)kBatch * N);
   // Workgroups per replica: with few replicas of a large cluster, S > 1 spreads
   // each replica over S co-resident workgroups (two group barriers per pod);
@@ -2648,8 +2874,8 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     if (S == 1) break;
     int occ = 0, rc0 = 0;
     switch (block * 100 + kn) {
-      case 25608: rc0 = sweep_occupancy<256, 8>(ctx, mode, &occ); break;
-      default: rc0 = sweep_occupancy<256, 0>(ctx, mode, &occ); break;
+      case 25608: rc0 = sweep_occupancy<256, 8>(ctx, mode, narrow, &occ); break;
+      default: rc0 = sweep_occupancy<256, 0>(ctx, mode, narrow, &occ); break;
     }
     if (rc0) return rc0;
     if ((long long)R * S <= (long long)occ * cus) break;   // every workgroup of a group co-resident
@@ -2679,32 +2905,32 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     const int key = block * 100 + kn;
     if (mode == 2) {
       if (S > 1) {
-        if (key == 25608) launch_sweep_ex<256, 8, true>(s, grid, ctx->stream);
-        else launch_sweep_ex<256, 0, true>(s, grid, ctx->stream);
+        if (key == 25608) launch_sweep_ex<256, 8, true>(s, grid, narrow, ctx->stream);
+        else launch_sweep_ex<256, 0, true>(s, grid, narrow, ctx->stream);
       } else {
-        if (key == 25608) launch_sweep_ex<256, 8, false>(s, grid, ctx->stream);
-        else if (key == 25600) launch_sweep_ex<256, 0, false>(s, grid, ctx->stream);
-        else launch_sweep_ex<1024, 0, false>(s, grid, ctx->stream);
+        if (key == 25608) launch_sweep_ex<256, 8, false>(s, grid, narrow, ctx->stream);
+        else if (key == 25600) launch_sweep_ex<256, 0, false>(s, grid, narrow, ctx->stream);
+        else launch_sweep_ex<1024, 0, false>(s, grid, narrow, ctx->stream);
       }
     } else if (S > 1) {
       switch (key) {
-        case 25608: launch_sweep<256, 8, true>(s, grid, mode, ctx->stream); break;
-        default: launch_sweep<256, 0, true>(s, grid, mode, ctx->stream); break;
+        case 25608: launch_sweep<256, 8, true>(s, grid, mode, narrow, ctx->stream); break;
+        default: launch_sweep<256, 0, true>(s, grid, mode, narrow, ctx->stream); break;
       }
     } else {
       switch (key) {
-        case 25608: launch_sweep<256, 8, false>(s, grid, mode, ctx->stream); break;
-        case 25616: launch_sweep<256, 16, false>(s, grid, mode, ctx->stream); break;
-        case 25620: launch_sweep<256, 20, false>(s, grid, mode, ctx->stream); break;
-        case 25624: launch_sweep<256, 24, false>(s, grid, mode, ctx->stream); break;
-        case 25632: launch_sweep<256, 32, false>(s, grid, mode, ctx->stream); break;
-        case 51232: launch_sweep<512, 32, false>(s, grid, mode, ctx->stream); break;
-        case 102432: launch_sweep<1024, 32, false>(s, grid, mode, ctx->stream); break;
-        case 25600: launch_sweep<256, 0, false>(s, grid, mode, ctx->stream); break;
-        default: launch_sweep<1024, 0, false>(s, grid, mode, ctx->stream); break;
+        case 25608: launch_sweep<256, 8, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25616: launch_sweep<256, 16, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25620: launch_sweep<256, 20, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25624: launch_sweep<256, 24, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25632: launch_sweep<256, 32, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 51232: launch_sweep<512, 32, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 102432: launch_sweep<1024, 32, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25600: launch_sweep<256, 0, false>(s, grid, mode, narrow, ctx->stream); break;
+        default: launch_sweep<1024, 0, false>(s, grid, mode, narrow, ctx->stream); break;
       }
     }
-    if ((rc = tlaunched(ctx, KSG_K_SWEEP, (double)R * s.nb * N))) return rc;
+    if ((rc = tlaunched(ctx, narrow ? KSG_K_SWEEP_NARROW : KSG_K_SWEEP, (double)R * s.nb * N))) return rc;
   }
   ctx->sweep_timeout = S > 1 ? s.timeout : nullptr;
   HIPC(ctx, hipGetLastError());
@@ -2844,7 +3070,11 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   if (ctx->force_path == 2 && do_commit && !want_cap) batched = batch_eligible(ctx, first, count);
   if (batched) {
     ctx->last_path = 2;
-    if ((rc = run_batched(ctx, first, count, d_pl, d_res, d_prof))) return rc;
+    if (ctx->batch_mode == 3) {
+      if ((rc = run_pipe(ctx, first, count, d_pl, d_res, d_prof))) return rc;
+    } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, d_prof))) {
+      return rc;
+    }
   } else {
     ctx->last_path = 1;
     a.first = first;
@@ -2988,8 +3218,9 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
-    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : 2;
+    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : 2;
   }
+  if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);
     ctx->slot_block = v <= 64 ? 64 : v <= 128 ? 128 : KSG_BATCH_MAX;
@@ -3004,6 +3235,12 @@ int ksg_close(ksg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   free_all(ctx);
   for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  for (int q = 0; q < 2; q++) {
+    if (ctx->ev_tk[q]) (void)hipEventDestroy(ctx->ev_tk[q]);
+    if (ctx->ev_p2[q]) (void)hipEventDestroy(ctx->ev_p2[q]);
+  }
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -3257,11 +3494,33 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   s.stride_tt = NT; s.stride_part = N; s.stride_sraw = 4 * N;
   bool sweep = sweep_eligible(ctx, profiles, (int)RR, first, count) && count > 0;
   if (ctx->force_path == 1) sweep = false;
+  // narrow records when every range check passes (host: pods and profiles,
+  // ksg_narrow_init: nodes), else the int64 columns
+  int4* nstat = nullptr;
+  int4* nmut = nullptr;
+  NarrowBounds nb{};
+  if (sweep && narrow_candidate(ctx, profiles, (int)RR, first, count, sweep_mode(profiles, (int)RR), &nb)) {
+    unsigned* d_bad;
+    TA(tmp, &nstat, sizeof(int4) * N);
+    TA(tmp, &nmut, sizeof(int4) * RR * N);
+    TA(tmp, &d_bad, 16);
+    HIPC(ctx, hipMemsetAsync(d_bad, 0, 16, ctx->stream));
+    hipLaunchKernelGGL(ksg_narrow_init, dim3((unsigned)((N + 255) / 256), (unsigned)std::min<size_t>(RR, 64)), dim3(256),
+                       0, ctx->stream, ctx->c, ctx->st, nstat, nmut, (int)RR, nb, d_bad);
+    HIPC(ctx, hipGetLastError());
+    unsigned bad = 0;
+    HIPC(ctx, hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(ctx, hipStreamSynchronize(ctx->stream));
+    if (bad) nstat = nullptr, nmut = nullptr;
+  }
+  ctx->last_narrow = nstat != nullptr;
   // the sweep reads and writes only the Fit columns; the queue kernels also
   // keep the PodTopologySpread / InterPodAffinity tables and per-node scratch
-  TA(tmp, &s.requested, 8 * RR * s.stride_req);
-  TA(tmp, &s.nonzero, 8 * RR * s.stride_nz);
-  TA(tmp, &s.pod_count, 4 * RR * s.stride_pc);
+  if (!nstat) {
+    TA(tmp, &s.requested, 8 * RR * s.stride_req);
+    TA(tmp, &s.nonzero, 8 * RR * s.stride_nz);
+    TA(tmp, &s.pod_count, 4 * RR * s.stride_pc);
+  }
   if (!sweep) {
     TA(tmp, &s.cnt, 4 * RR * s.stride_cnt);
     TA(tmp, &s.tab, 4 * RR * s.stride_tab);
@@ -3282,9 +3541,11 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     hipLaunchKernelGGL(ksg_broadcast<T>, dim3(std::max(bx, 1u), (unsigned)RR), dim3(256), 0, ctx->stream,
                        (const T*)src, dst, len, stride);
   };
-  bcast(ctx->st.requested, s.requested, s.stride_req, s.stride_req);
-  bcast(ctx->st.nonzero, s.nonzero, s.stride_nz, s.stride_nz);
-  bcast(ctx->st.pod_count, s.pod_count, s.stride_pc, s.stride_pc);
+  if (!nstat) {
+    bcast(ctx->st.requested, s.requested, s.stride_req, s.stride_req);
+    bcast(ctx->st.nonzero, s.nonzero, s.stride_nz, s.stride_nz);
+    bcast(ctx->st.pod_count, s.pod_count, s.stride_pc, s.stride_pc);
+  }
   if (!sweep) {
     bcast(ctx->st.cnt, s.cnt, s.stride_cnt, s.stride_cnt);
     bcast(ctx->st.tab, s.tab, s.stride_tab, s.stride_tab);
@@ -3296,7 +3557,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   a.placements = d_pl;
   a.results = nullptr;
   if (sweep) {
-    if ((rc = run_sweep(ctx, a, profiles, d_prof, (int)RR, first, count, d_pl, tmp))) return rc;
+    if ((rc = run_sweep(ctx, a, profiles, d_prof, (int)RR, first, count, d_pl, tmp, nstat, nmut, nb.nx))) return rc;
     ctx->last_path = 3;
   } else {
     const int block = N >= 8192 ? 512 : 256;
@@ -3307,7 +3568,12 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   }
   HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * RR * count, hipMemcpyDeviceToHost, ctx->stream));
   std::vector<int64_t> sums(2 * RR);
-  if (summaries) {
+  if (summaries && nmut) {
+    hipLaunchKernelGGL(ksg_narrow_sums, dim3((unsigned)RR), dim3(256), 0, ctx->stream, (const int4*)nmut, (int)N,
+                       nb.nx >= 0 ? 0xffffffu : 0xffffffffu, d_sums);
+    HIPC(ctx, hipGetLastError());
+    HIPC(ctx, hipMemcpyAsync(sums.data(), d_sums, sizeof(int64_t) * 2 * RR, hipMemcpyDeviceToHost, ctx->stream));
+  } else if (summaries) {
     hipLaunchKernelGGL(ksg_replica_sums, dim3((unsigned)RR), dim3(256), 0, ctx->stream, (const int64_t*)s.requested,
                        s.stride_req, (int)N, d_sums);
     HIPC(ctx, hipGetLastError());

@@ -54,7 +54,22 @@ struct SweepArgs {
   SweepSlot* slots;             // S > 1: [2][R * S] partials by pod parity
   unsigned* gbar;               // S > 1: [R][16] arrival counters (one 64-B line each), zeroed before the launch
   unsigned* timeout;            // S > 1: set when a group barrier poll gave up
+  // narrow state (NARROW instances; ranges checked by the host and by
+  // ksg_narrow_init): per node one 16-byte static record {alloc cpu milli,
+  // alloc memory MiB, allowed pods, alloc of column nx} and per (replica, node)
+  // one 16-byte mutable record {requested cpu milli (EX: 24 bits | requested
+  // nx << 24), non-zero cpu milli, requested memory MiB, non-zero memory MiB
+  // (24 bits) | pod count << 24}
+  const int4* nstat;            // [N]
+  int4* nmut;                   // [R][N]
+  int32_t nx;                   // EX: the one scalar column any pod of the run requests
 };
+
+// Memory in MiB: exact for the Fit and BalancedAllocation arithmetic when every
+// memory quantity is a multiple of 2^20 (quotients of equally scaled integers
+// are unchanged; float64 quotients of values scaled by a power of two are
+// bit-identical), which the host checks.
+constexpr int kNarrowMemShift = 20;
 
 template <class T>
 __device__ __forceinline__ T ald(const T* p) {   // agent-scope load of a word another workgroup wrote
@@ -192,17 +207,31 @@ __device__ __forceinline__ SweepPod sweep_pod(const SweepProf& sp, const ksg_pro
   return q;
 }
 
+// The pod's cpu / memory requests in the units of the columns (memory in MiB
+// on the narrow instances).
+struct PodCM {
+  int64_t req_c, req_m, nz_c, nz_m;
+};
+
+template <bool NARROW>
+__device__ __forceinline__ PodCM pod_cm(const ksg_pod& p) {
+  if constexpr (NARROW)
+    return PodCM{p.req[KSG_RES_CPU], p.req[KSG_RES_MEM] >> kNarrowMemShift, p.nz_cpu, p.nz_mem >> kNarrowMemShift};
+  else
+    return PodCM{p.req[KSG_RES_CPU], p.req[KSG_RES_MEM], p.nz_cpu, p.nz_mem};
+}
+
 // Fit (cpu + memory [+ ex]) and BalancedAllocation (cpu + memory) scores from
 // loaded values: fit_score / ba_score restated without branches (cm_scores'
 // arithmetic).  ex_on: Fit also scores the scalar column with allocatable ae,
 // requested re, pod request qx and weight w_ex.
-__device__ __forceinline__ void sweep_cm_scores(const CmProf& m, const ksg_pod& p, int64_t ac, int64_t am, int64_t rc,
+__device__ __forceinline__ void sweep_cm_scores(const CmProf& m, const PodCM& p, int64_t ac, int64_t am, int64_t rc,
                                                 int64_t rm, int64_t zc, int64_t zm, bool ex_on, int64_t ae,
                                                 int64_t re, int64_t qx, int64_t w_ex, int64_t& fit, int64_t& ba) {
   const bool hc = ac > 0, hm = am > 0;
   const int64_t sac = hc ? ac : 1, sam = hm ? am : 1;
   const float ic = __builtin_amdgcn_rcpf((float)sac), im = __builtin_amdgcn_rcpf((float)sam);
-  const int64_t qc = zc + p.nz_cpu, qm = zm + p.nz_mem;
+  const int64_t qc = zc + p.nz_c, qm = zm + p.nz_m;
   int64_t xc, xm;
   if (m.least) {
     xc = qc > ac ? 0 : (ac - qc) * 100;
@@ -224,8 +253,8 @@ __device__ __forceinline__ void sweep_cm_scores(const CmProf& m, const ksg_pod& 
   }
   fit = ws == 0 ? 0 : qdiv(num, ws, __builtin_amdgcn_rcpf((float)ws));
   const double dac = (double)sac, dam = (double)sam;
-  double fc = ddiv((double)(rc + p.req[KSG_RES_CPU]), dac);
-  double fm = ddiv((double)(rm + p.req[KSG_RES_MEM]), dam);
+  double fc = ddiv((double)(rc + p.req_c), dac);
+  double fm = ddiv((double)(rm + p.req_m), dam);
   fc = fc > 1 ? 1 : fc;
   fm = fm > 1 ? 1 : fm;
   const double sd = hc && hm ? fabs((fc - fm) / 2) : 0.0;
@@ -249,8 +278,13 @@ struct SweepPart {
 // lane's nodes); without it S == 1 and the stride is the constant BLOCK, which
 // keeps the node offsets in the load instructions' immediates.
 // EX (with FAST): some replica's Fit also scores one scalar column (SweepProf::ex).
-template <int BLOCK, int KN, bool FAST, bool MULTI, bool EX = false>
+// NARROW (with FAST): the 16-byte static and mutable records above instead of
+// the int64 columns (16 instead of 36 bytes of per-replica state per (replica,
+// pod, node)); the pods of the run request nothing beyond cpu, memory and
+// (EX) column a.nx.
+template <int BLOCK, int KN, bool FAST, bool MULTI, bool EX = false, bool NARROW = false>
 __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) {   // 16 waves per CU
+  static_assert(!NARROW || FAST, "narrow state: the fast cpu/memory arithmetic");
   constexpr int NW = BLOCK / 64;
   constexpr int U = !FAST ? (KN == 0 ? 2 : 1) : (KN >= 20 || EX ? 2 : 4);   // nodes whose loads are in flight together
   __shared__ ksg_profile s_prof;
@@ -271,6 +305,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
   int64_t* requested = a.st.requested + rep * a.st.stride_req;
   int64_t* nonzero = a.st.nonzero + rep * a.st.stride_nz;
   int32_t* pod_count = a.st.pod_count + rep * a.st.stride_pc;
+  int4* nmut = NARROW ? a.nmut + (size_t)rep * N : nullptr;
   uint64_t* scratch = KN == 0 ? a.scratch + (size_t)rep * N : nullptr;
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles + rep)[tid];
@@ -285,6 +320,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
   for (int j = 0; j < a.nb; j++) {
     const ksg_pod& p = a.pods[a.b0 + j];
     const SweepPod q = sweep_pod(sp, prof, p, R);
+    const PodCM pc4 = pod_cm<NARROW>(p);
     const uint64_t* srec = a.srec + (size_t)j * N;
     const int par = j & 1;
     SweepSlot* slots = a.slots + (size_t)par * gridDim.x;
@@ -302,14 +338,18 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       bool ok = (sr & q.fmask) == 0;
       if (q.fit_on) {
         ok = ok && pc + 1 <= al;
-        ok = ok && (!(q.req_mask & 1u) || p.req[KSG_RES_CPU] <= ac - rc);
-        ok = ok && (!(q.req_mask & 2u) || p.req[KSG_RES_MEM] <= am - rm);
-        for (int r = 2; r < R && r < KSG_MAX_RES; r++)   // pod-uniform: loads only for requested columns
-          if ((q.req_mask >> r) & 1u) ok = ok && p.req[r] <= c.alloc[r * NN + n] - requested[r * NN + n];
+        ok = ok && (!(q.req_mask & 1u) || pc4.req_c <= ac - rc);
+        ok = ok && (!(q.req_mask & 2u) || pc4.req_m <= am - rm);
+        if constexpr (NARROW) {
+          if (EX && ((q.req_mask >> a.nx) & 1u)) ok = ok && p.req[a.nx] <= ae - re;
+        } else {
+          for (int r = 2; r < R && r < KSG_MAX_RES; r++)   // pod-uniform: loads only for requested columns
+            if ((q.req_mask >> r) & 1u) ok = ok && p.req[r] <= c.alloc[r * NN + n] - requested[r * NN + n];
+        }
       }
       if (!ok) return 0;
       int64_t fs = 0, bs = 0;
-      sweep_cm_scores(sp.cm, p, ac, am, rc, rm, zc, zm, EX && q.ex_on, ae, re, EX ? p.req[EX ? sp.ex : 0] : 0,
+      sweep_cm_scores(sp.cm, pc4, ac, am, rc, rm, zc, zm, EX && q.ex_on, ae, re, EX ? p.req[EX ? sp.ex : 0] : 0,
                       sp.w_ex, fs, bs);
       const int64_t rt = (sr >> 8) & 0xff, ra = (sr >> 16) & 0xffff, im = (sr >> 32) & 0xff;
       const int64_t part = im * q.w_img + ((q.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? fs * q.w_fit : 0) +
@@ -347,17 +387,33 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
           const int n = tb + (k0 + u) * stride;
           const int nl = n < N ? n : 0;   // clamped: every lane loads from a valid address
           sr[u] = srec[nl];
-          ac[u] = c.alloc[KSG_RES_CPU * NN + nl];
-          am[u] = c.alloc[KSG_RES_MEM * NN + nl];
-          rc[u] = requested[KSG_RES_CPU * NN + nl];
-          rm[u] = requested[KSG_RES_MEM * NN + nl];
-          zc[u] = nonzero[nl];
-          zm[u] = nonzero[NN + nl];
-          pc[u] = pod_count[nl];
-          al[u] = c.allowed[nl];
-          ae[u] = 0;
-          re[u] = 0;
-          if constexpr (EX) {
+          if constexpr (NARROW) {
+            const int4 st4 = a.nstat[nl], mu = nmut[nl];
+            ac[u] = st4.x;
+            am[u] = st4.y;
+            al[u] = st4.z;
+            rc[u] = EX ? (int64_t)((uint32_t)mu.x & 0xffffffu) : (int64_t)mu.x;
+            zc[u] = mu.y;
+            rm[u] = mu.z;
+            zm[u] = (int64_t)((uint32_t)mu.w & 0xffffffu);
+            pc[u] = (int32_t)((uint32_t)mu.w >> 24);
+            ae[u] = EX ? st4.w : 0;
+            re[u] = EX ? (int64_t)((uint32_t)mu.x >> 24) : 0;
+          } else {
+            ac[u] = c.alloc[KSG_RES_CPU * NN + nl];
+            am[u] = c.alloc[KSG_RES_MEM * NN + nl];
+            rc[u] = requested[KSG_RES_CPU * NN + nl];
+            rm[u] = requested[KSG_RES_MEM * NN + nl];
+            zc[u] = nonzero[nl];
+            zm[u] = nonzero[NN + nl];
+            pc[u] = pod_count[nl];
+            al[u] = c.allowed[nl];
+          }
+          if constexpr (!NARROW) {
+            ae[u] = 0;
+            re[u] = 0;
+          }
+          if constexpr (EX && !NARROW) {
             if (q.ex_on) {
               ae[u] = c.alloc[(size_t)sp.ex * NN + nl];
               re[u] = requested[(size_t)sp.ex * NN + nl];
@@ -544,11 +600,86 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
     }
     // ---- assume: the lane that owns the selected node ------------------------
     if (selected >= 0 && (!MULTI || ((selected / BLOCK) % S) == sub) && (selected % BLOCK) == tid) {
-      for (int r = 0; r < R; r++) requested[(size_t)r * N + selected] += p.req[r];
-      nonzero[selected] += p.nz_cpu;
-      nonzero[NN + selected] += p.nz_mem;
-      pod_count[selected] += 1;
+      if constexpr (NARROW) {
+        // packed fields: the range checks bound every sum below its field
+        int4 mu = nmut[selected];
+        mu.x = (int32_t)((uint32_t)mu.x + (uint32_t)pc4.req_c + (EX ? (uint32_t)p.req[a.nx] << 24 : 0u));
+        mu.y = (int32_t)((uint32_t)mu.y + (uint32_t)pc4.nz_c);
+        mu.z = (int32_t)((uint32_t)mu.z + (uint32_t)pc4.req_m);
+        mu.w = (int32_t)((uint32_t)mu.w + (uint32_t)pc4.nz_m + (1u << 24));
+        nmut[selected] = mu;
+      } else {
+        for (int r = 0; r < R; r++) requested[(size_t)r * N + selected] += p.req[r];
+        nonzero[selected] += p.nz_cpu;
+        nonzero[NN + selected] += p.nz_mem;
+        pod_count[selected] += 1;
+      }
     }
     if (sub == 0 && tid == 0) a.placements[(size_t)rep * a.count + a.out0 + j] = selected;
+  }
+}
+
+// Narrow bounds the node side must meet (the pod side is checked on the host):
+// per placed pod, at most xc / xm (MiB) of non-zero request beyond its request.
+struct NarrowBounds {
+  int64_t xc, xm;
+  int32_t nx;      // EX column, -1 without
+  int32_t places;  // pods a node can still take: min(queue length, 255)
+};
+
+// Narrow state of every replica from the int64 columns (every replica starts
+// from the context's state): one static record per node, the mutable record
+// broadcast.  A node outside the ranges sets *bad; the host then runs the
+// int64 instances instead (nothing here writes the context's state).
+__global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st, int4* nstat, int4* nmut, int R,
+                                                       NarrowBounds b, unsigned* bad) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int N = c.N;
+  if (n >= N) return;
+  const size_t NN = N;
+  constexpr int64_t kMiB = (int64_t)1 << kNarrowMemShift, k24 = (int64_t)1 << 24;
+  const int64_t ac = c.alloc[KSG_RES_CPU * NN + n], am = c.alloc[KSG_RES_MEM * NN + n];
+  const int64_t rc = st.requested[KSG_RES_CPU * NN + n], rm = st.requested[KSG_RES_MEM * NN + n];
+  const int64_t zc = st.nonzero[n], zm = st.nonzero[NN + n];
+  const int32_t pc = st.pod_count[n], al = c.allowed[n];
+  const int64_t ae = b.nx >= 0 ? c.alloc[(size_t)b.nx * NN + n] : 0;
+  const int64_t re = b.nx >= 0 ? st.requested[(size_t)b.nx * NN + n] : 0;
+  const int64_t cmax = b.nx >= 0 ? k24 - 1 : (int64_t)INT32_MAX;
+  bool ok = ac >= 0 && rc >= 0 && am >= 0 && rm >= 0 && zc >= 0 && zm >= 0 && ae >= 0 && re >= 0;
+  ok = ok && ((am | rm | zm) & (kMiB - 1)) == 0;
+  ok = ok && ac <= cmax && rc <= cmax;                                   // requested cpu <= max(rc, ac)
+  ok = ok && zc + ac + b.places * b.xc <= (int64_t)INT32_MAX;            // Σ placed cpu requests <= ac
+  ok = ok && (am >> kNarrowMemShift) <= (int64_t)INT32_MAX && (rm >> kNarrowMemShift) <= (int64_t)INT32_MAX;
+  ok = ok && (zm >> kNarrowMemShift) + (am >> kNarrowMemShift) + b.places * b.xm < k24;
+  ok = ok && pc >= 0 && pc <= 255 && al >= 0 && al <= 255;              // pod count <= max(pc, al)
+  ok = ok && ae <= 255 && re <= 255;
+  if (!ok) {
+    atomicOr(bad, 1u);
+    return;
+  }
+  const int4 mu = make_int4((int32_t)(rc | (re << 24)), (int32_t)zc, (int32_t)(rm >> kNarrowMemShift),
+                            (int32_t)((zm >> kNarrowMemShift) | ((int64_t)pc << 24)));
+  if (blockIdx.y == 0) nstat[n] = make_int4((int32_t)ac, (int32_t)(am >> kNarrowMemShift), al, (int32_t)ae);
+  for (int r = blockIdx.y; r < R; r += gridDim.y) nmut[(size_t)r * N + n] = mu;
+}
+
+// Σ requested cpu / memory per replica from the narrow state (the summaries).
+__global__ __launch_bounds__(256) void ksg_narrow_sums(const int4* nmut, int N, uint32_t cpu_mask, int64_t* out) {
+  __shared__ int64_t s_p[2][4];
+  const int4* q = nmut + (size_t)blockIdx.x * N;
+  int64_t a = 0, b = 0;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const int4 m = q[n];
+    a += (uint32_t)m.x & cpu_mask;
+    b += (int64_t)m.z << kNarrowMemShift;
+  }
+  a = wave_sum64(a);
+  b = wave_sum64(b);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { s_p[0][wv] = a; s_p[1][wv] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = s_p[0][0] + s_p[0][1] + s_p[0][2] + s_p[0][3];
+    out[2 * blockIdx.x + 1] = s_p[1][0] + s_p[1][1] + s_p[1][2] + s_p[1][3];
   }
 }

@@ -69,12 +69,14 @@ def roofline(bytes_per_eval: int, node_evals_per_launch: int, launch_ms: float) 
 #   queue kernels, batch phase 1: one node-eval per (pod, node) = the column
 #     schema above; phase 1 also writes its 8-byte record + 4-byte image part
 #   topk / scan phase 2: one 8-byte record read per (pod, node)
-#   top-set phase 2 (both variants): per unit one 8-byte top key + 8-byte record + 4-byte image part
+#   top-set phase 2 (all variants): per unit one 8-byte top key + 8-byte record + 4-byte image part
 #   replica sweep, static records (unit = (pod, node)): the replica-independent
 #     columns (unschedulable, taints, labels, images) + the 8-byte record written
 #   replica sweep (unit = (replica, pod, node)): the 8-byte static record + the
 #     Fit / BalancedAllocation columns it reads: allocatable and requested of
 #     cpu and memory, non-zero requested, pod count, allowed pods
+#   narrow replica sweep: the 8-byte static record + the 16-byte per-node
+#     static record + the 16-byte per-(replica, node) record
 STATIC_COLS = ("unschedulable", "taints", "labels", "images")
 
 
@@ -86,7 +88,7 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
         return bytes_per_eval + 12
     if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
         return 8
-    if name in ("ksg_batch_phase2", "ksg_batch_phase2s"):
+    if name in ("ksg_batch_phase2", "ksg_batch_phase2s", "ksg_batch_phase2p"):
         return 20
     if name in ("ksg_sweep_static", "ksg_sweep"):
         if not isinstance(cols, dict):
@@ -95,6 +97,8 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
             return sum(cols.get(k, 0) for k in STATIC_COLS) + 8
         fit = 32 if "alloc" in cols else 0
         return 8 + fit + sum(cols.get(k, 0) for k in ("nonzero", "pod_count", "allowed_pods"))
+    if name == "ksg_sweep_narrow":
+        return 40
     raise KeyError(name)
 
 

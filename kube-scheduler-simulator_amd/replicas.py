@@ -47,6 +47,8 @@ def run_sweep(engine, profiles: Sequence[dict], first: int, count: int, rank: in
     `engine` is native.Engine (the HIP library) in production; any object with
     the same run_replicas() works (the CPU tests pass the oracle).
     `device`: where the gather buffers live ("cuda:<i>" for RCCL, None = CPU/gloo).
+    With a process group initialised the gather runs even at world size 1 (the
+    bench initialises RCCL at N = 1 too, so the collective executes).
     """
     R = len(profiles)
     lo, hi = shard(R, world, rank)
@@ -57,10 +59,10 @@ def run_sweep(engine, profiles: Sequence[dict], first: int, count: int, rank: in
     else:
         pl, sums = np.zeros((0, count), np.int32), None
     sm = _summary_matrix(sums, len(mine))
-    if world == 1:
+    import torch.distributed as dist
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return pl, sm
     import torch
-    import torch.distributed as dist
     block = -(-R // world)
     buf = torch.full((block, count + len(SUMMARY_FIELDS) * 2), -1, dtype=torch.int32)
     buf[:len(mine), :count] = torch.from_numpy(pl)

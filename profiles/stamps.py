@@ -23,7 +23,16 @@ fn = eng.lib.ksg_debug_stamps
 fn.argtypes = [C.c_void_p, C.c_void_p]
 assert fn(eng.ctx, st) == 0
 tot = sum(st[1:])
-mode = os.environ.get("KSG_BATCH_MODE", "slot")
+mode = os.environ.get("KSG_BATCH_MODE", "pipe")
+if mode == "pipe":
+    names = ["(unused)", "bu + candidate buffer reads", "evaluate pod j+1 (both versions)",
+             "candidates of pod j+1 + loads", "fold + decide", "contributions (reductions)",
+             "results (lane 0)", "assume + record rotation", "candidate stores (wait for loads)", "barrier"]
+    print(f"[pipe] {n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build)")
+    tot = sum(st[1:10])
+    for i in range(1, 10):
+        print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
+    sys.exit(0)
 if mode == "slot":
     names = ["(start)", "X: speculate + issue next-pod loads", "X: changed node + DPP reductions",
              "Y: barrier 1 + decide (+renorm)", "Y: row update + results", "barrier 2",

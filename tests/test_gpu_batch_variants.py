@@ -1,7 +1,9 @@
 """GPU parity of every phase-2 variant of the batched placement path
-(KSG_BATCH_MODE): "slot" (default), "topset" and "scan".  Same bar
-as the default path: placements, per-pod results and node state bit-exact
-against the C++ oracle, including split calls."""
+(KSG_BATCH_MODE): "slot" (default) at each block size,
+"pipe" (with and without the two-batch window, at 64- and 128-pod batches,
+and with per-kernel timing on, which runs the same arithmetic without
+overlap), "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
+state bit-exact against the C++ oracle, including split calls."""
 import numpy as np
 import pytest
 
@@ -23,7 +25,9 @@ def _have_gpu():
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
 
 # (mode, extra env): the slot variant at each of its block sizes (= batch sizes; 128 is the default)
-MODES = {"slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
+MODES = {"pipe": ("pipe", {}), "pipe64": ("pipe", {"KSG_SLOT_BLOCK": 64}),
+         "pipe-nowindow": ("pipe", {"KSG_PIPE_WINDOW": 0}), "pipe-timed": ("pipe", {"_timing": 1}),
+         "slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
          "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
          "topset": ("topset", {}), "scan": ("scan", {})}
 
@@ -31,7 +35,12 @@ MODES = {"slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
 @pytest.fixture(scope="module", params=list(MODES))
 def variant(request, built):
     mode, env = MODES[request.param]
-    return _engine_with_batch_mode(mode, **env)
+    env = dict(env)
+    timing = env.pop("_timing", 0)
+    eng = _engine_with_batch_mode(mode, **env)
+    if timing:
+        eng.set_timing(True)
+    return eng
 
 
 @pytest.fixture(scope="module")

@@ -111,3 +111,116 @@ def test_sweep_queue_subrange(gpu, oracle):
     pl, _ = gpu.run_replicas(pf, 100, 150)
     want, _ = oracle.run_replicas(pf, 100, 150)
     np.testing.assert_array_equal(pl, want)
+
+
+# ---- narrow records: 16-byte per-(replica, node) state ----
+
+def _engine_env(**env):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return native.Engine(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def timed(built):
+    eng = native.Engine(device=0)
+    eng.set_timing(True)
+    return eng
+
+
+@pytest.fixture(scope="module")
+def wide(built):
+    """The int64-column sweep instances (KSG_FORCE_PATH=3 skips the narrow records)."""
+    return _engine_env(KSG_FORCE_PATH=3)
+
+
+def _sweep_kernel(eng):
+    names = {k["name"] for k in eng.kernel_stats()}
+    assert names & {"ksg_sweep", "ksg_sweep_narrow"}, names
+    return "ksg_sweep_narrow" if "ksg_sweep_narrow" in names else "ksg_sweep"
+
+
+def _run(eng, oracle, nodes, pods, base, plist):
+    enc = E.Encoder(nodes, pods, base)
+    pf = [E.encode_profile(p, enc.cluster.res_names) for p in plist]
+    eng.load(enc, pf[0])
+    oracle.load(enc, pf[0])
+    pl, sums = eng.run_replicas(pf, 0, len(pods))
+    want, wsums = oracle.run_replicas(pf, 0, len(pods))
+    np.testing.assert_array_equal(pl, want)
+    for f in wsums.dtype.names:
+        np.testing.assert_array_equal(sums[f], wsums[f], err_msg=f)
+    return pl
+
+
+NARROW_CASES = [
+    ("c2-150x300-r6", lambda: _c2(150, 300), lambda b: G.replica_profiles(6), "ksg_sweep_narrow"),
+    ("c2-5000x150-r8", lambda: _c2(5000, 150), lambda b: G.replica_profiles(8), "ksg_sweep_narrow"),
+    ("c2-33000x30-r2", lambda: _c2(33000, 30), lambda b: G.replica_profiles(2), "ksg_sweep_narrow"),
+    ("c5-ex-6000-r2", lambda: G.config5(n_nodes=6000, n_pods=80, n_images=500, taint_vocab=256,
+                                        taints_per_node=16, images_per_node=20),
+     lambda b: [b, P.Profile(plugins=[(n, w + 1 if w else 0) for n, w in b.plugins], fit_strategy=1,
+                             fit_resources=b.fit_resources, ba_resources=b.ba_resources)], "ksg_sweep_narrow"),
+]
+
+
+@pytest.mark.parametrize("name,make,profs,kernel", NARROW_CASES, ids=[c[0] for c in NARROW_CASES])
+def test_narrow_sweep_runs_and_matches_wide(timed, wide, oracle, name, make, profs, kernel):
+    """The narrow instances run where the ranges allow and agree bit for bit
+    with the int64 instances and the oracle."""
+    nodes, pods, base = make()
+    plist = profs(base)
+    a = _run(timed, oracle, nodes, pods, base, plist)
+    assert _sweep_kernel(timed) == kernel
+    b = _run(wide, oracle, nodes, pods, base, plist)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_narrow_fallback_on_sub_mib_memory(timed, oracle):
+    """One node whose memory is not a whole number of MiB: the node-side check
+    (ksg_narrow_init) sends the run to the int64 instances."""
+    nodes, pods, base = _c2(300, 200)
+    nodes[17].allocatable[m.MEMORY] += 1000
+    _run(timed, oracle, nodes, pods, base, G.replica_profiles(4))
+    assert _sweep_kernel(timed) == "ksg_sweep"
+
+
+def test_narrow_fallback_on_third_column(timed, oracle):
+    """A pod requesting ephemeral storage: the host-side check keeps the int64
+    instances (the narrow record has no column for it)."""
+    nodes, pods, base = _c2(300, 200)
+    pods[5].containers[0].requests[m.EPHEMERAL] = 1 << 30
+    _run(timed, oracle, nodes, pods, base, G.replica_profiles(4))
+    assert _sweep_kernel(timed) == "ksg_sweep"
+
+
+def test_narrow_pod_count_field_at_255(timed, wide, oracle):
+    """allowed pods = 255 and tiny pods: the 8-bit pod count reaches its
+    maximum, after which Fit rejects the node (Too many pods)."""
+    nodes, pods, base = _c2(4, 1200, seed=7)
+    for n in nodes:
+        n.allocatable[m.PODS] = 255
+        n.taints = []
+    for p in pods:
+        p.containers[0].requests = {m.CPU: 1, m.MEMORY: 1 << 20}
+        p.node_affinity_required = None
+    a = _run(timed, oracle, nodes, pods, base, G.replica_profiles(3))
+    assert _sweep_kernel(timed) == "ksg_sweep_narrow"
+    assert (a >= 0).sum(axis=1).max() == 4 * 255
+    b = _run(wide, oracle, nodes, pods, base, G.replica_profiles(3))
+    np.testing.assert_array_equal(a, b)
+
+
+def test_narrow_fallback_on_allowed_above_255(timed, oracle):
+    nodes, pods, base = _c2(4, 300, seed=7)
+    nodes[2].allocatable[m.PODS] = 256
+    _run(timed, oracle, nodes, pods, base, G.replica_profiles(2))
+    assert _sweep_kernel(timed) == "ksg_sweep"
