@@ -771,7 +771,7 @@ def encode_profile(prof: P.Profile, res_names: Sequence[str]) -> dict:
     """KubeSchedulerProfile -> ksg_profile field values."""
     res_col = {r: i for i, r in enumerate(res_names)}
     order = prof.filter_order()
-    weights = prof.weights()
+    weights = prof.selection_weights()
     score_mask = 0
     w = [0] * NPLUGINS
     for pid in prof.score_order():

@@ -259,7 +259,7 @@ def rfc3339_ns(ts: Optional[str]) -> Optional[int]:
 # ---------------------------------------------------------------------------
 # scheduler configuration -> Profile
 # ---------------------------------------------------------------------------
-_POINTS_NOT_MODELLED = ("preFilter", "filter", "preScore", "score")
+_POINTS_MODELLED = ("preFilter", "filter", "preScore", "score")
 
 
 def _merge_plugin_set(default: List[Tuple[str, int]], custom: dict) -> List[Tuple[str, int]]:
@@ -299,12 +299,17 @@ def profile_from_config(cfg: Optional[dict]) -> Tuple[P.Profile, Optional[int]]:
         return prof, pct
     p0 = profiles[0]
     plugins = p0.get("plugins") or {}
-    for point in _POINTS_NOT_MODELLED:
+    prof.plugins = _merge_plugin_set(list(P.DEFAULT_MULTIPOINT), plugins.get("multiPoint") or {})
+    # per-point sets are kept as written (ConvertForSimulator, plugins.go:177-186;
+    # the in-tree MultiPoint set has nothing per point to merge with)
+    for point in _POINTS_MODELLED:
         ps = plugins.get(point) or {}
         if ps.get("enabled") or ps.get("disabled"):
-            raise NotImplementedError(f"per-extension-point plugin set {point!r}: configure through multiPoint")
-    prof.plugins = _merge_plugin_set(list(P.DEFAULT_MULTIPOINT), plugins.get("multiPoint") or {})
+            prof.points[point] = ([(e["name"], int(e.get("weight", 0) or 0)) for e in ps.get("enabled") or ()],
+                                  tuple(d["name"] for d in ps.get("disabled") or ()))
     prof.enabled_ids()   # refuses plugins outside the modelled in-tree set
+    for f in (prof.prefilter_order, prof.filter_order, prof.prescore_order, prof.score_order):
+        f()              # ... and per-point plugins the registry lacks (plugins.go:39-60)
     for pc in p0.get("pluginConfig") or ():
         name, args = pc.get("name"), pc.get("args") or {}
         if name == "NodeResourcesFit":

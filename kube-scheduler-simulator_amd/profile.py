@@ -8,7 +8,19 @@ Mirrors what the debuggable scheduler derives from a KubeSchedulerConfiguration:
   0 maps to 1, key is the plugin name without the `Wrapped` suffix),
 - the default plugin args pinned at `plugins_test.go:876-1000`
   (LeastAllocated cpu=1/memory=1, BalancedAllocation cpu=1/memory=1,
-  hardPodAffinityWeight=1, PodTopologySpread defaultingType System).
+  hardPodAffinityWeight=1, PodTopologySpread defaultingType System),
+- per-extension-point plugin sets (`Profile.points`): ConvertForSimulator keeps
+  them as written (`plugins.go:177-186`) beside the in-tree MultiPoint set
+  (`plugins.go:187-194`); the framework then expands MultiPoint into each
+  point [upstream v1.32 frameworkImpl.expandMultiPointPlugins, not vendored —
+  TO VERIFY, DESIGN.md §9]: the point's own plugins that MultiPoint also
+  lists first (in the point's order), then the remaining MultiPoint plugins
+  that implement the point and are not disabled there, then the point's other
+  plugins.  Score weights differ by consumer: the framework's selection takes
+  a point's own Score weight before the MultiPoint one [upstream
+  getScoreWeights, TO VERIFY], while the simulator's store map appends
+  MultiPoint after Score.Enabled, so the MultiPoint weight wins there
+  (`plugins.go:289-304`) and the finalscore annotations use it.
 """
 from __future__ import annotations
 
@@ -100,6 +112,9 @@ class Profile:
     # max(potential nodes * pct / 100, abs), at most the potential nodes
     preemption_min_candidate_pct: int = 10
     preemption_min_candidate_abs: int = 100
+    # per-extension-point sets: point ("preFilter", "filter", "preScore",
+    # "score") -> (enabled [(name, weight)], disabled names)
+    points: Dict[str, Tuple[List[Tuple[str, int]], Tuple[str, ...]]] = field(default_factory=dict)
 
     # -- derived views ---------------------------------------------------
     def enabled_ids(self) -> List[int]:
@@ -113,25 +128,55 @@ class Profile:
                 raise ValueError(f"plugin {name!r} is not an in-tree Filter/Score plugin")
         return out
 
+    def _expand(self, point: str, ext: int) -> List[int]:
+        """The framework's plugin list of one extension point (module docstring)."""
+        multi = [p for p in self.enabled_ids() if EXT[p][ext]]
+        if point not in self.points:
+            return multi
+        enabled, disabled = self.points[point]
+        own = [_plain(n) for n, _ in enabled]
+        for n in own:   # updatePluginList: the plugin must exist and implement the point
+            if n not in PLUGIN_ID:
+                raise ValueError(f"plugin {n!r} in {point!r} is not an in-tree Filter/Score plugin")
+            if not EXT[PLUGIN_ID[n]][ext]:
+                raise ValueError(f"plugin {n!r} does not extend {point!r}")
+        own_ids = [PLUGIN_ID[n] for n in own]
+        if len(set(own_ids)) != len(own_ids):
+            raise ValueError(f"plugin listed twice in {point!r}")
+        if "*" in disabled:
+            return own_ids
+        off = {PLUGIN_ID[_plain(n)] for n in disabled if _plain(n) in PLUGIN_ID}
+        override = [p for p in own_ids if p in multi]
+        rest_multi = [p for p in multi if p not in off and p not in own_ids]
+        return override + rest_multi + [p for p in own_ids if p not in multi]
+
     def filter_order(self) -> List[int]:
-        return [p for p in self.enabled_ids() if EXT[p][1]]
+        return self._expand("filter", 1)
 
     def prefilter_order(self) -> List[int]:
-        return [p for p in self.enabled_ids() if EXT[p][0]]
+        return self._expand("preFilter", 0)
 
     def prescore_order(self) -> List[int]:
-        return [p for p in self.enabled_ids() if EXT[p][2]]
+        return self._expand("preScore", 2)
 
     def score_order(self) -> List[int]:
-        return [p for p in self.enabled_ids() if EXT[p][3]]
+        return self._expand("score", 3)
 
     def weights(self) -> Dict[str, int]:
-        """getScorePluginWeight (plugins.go:289-304): every enabled
-        MultiPoint plugin gets an entry; weight 0 is replaced by 1."""
+        """getScorePluginWeight (plugins.go:289-304), the store's map:
+        Score.Enabled, then every enabled MultiPoint plugin (a later entry
+        replaces an earlier one); weight 0 is replaced by 1."""
         out = {}
-        for name, w in self.plugins:
-            key = name[:-len(PLUGIN_SUFFIX)] if name.endswith(PLUGIN_SUFFIX) else name
-            out[key] = w if w != 0 else 1
+        for name, w in list(self.points.get("score", ([], ()))[0]) + list(self.plugins):
+            out[_plain(name)] = w if w != 0 else 1
+        return out
+
+    def selection_weights(self) -> Dict[str, int]:
+        """The framework's Score weights (selection): a point's own Score
+        weight first, then MultiPoint's (the first entry wins); 0 -> 1."""
+        out: Dict[str, int] = {}
+        for name, w in list(self.points.get("score", ([], ()))[0]) + list(self.plugins):
+            out.setdefault(_plain(name), w if w != 0 else 1)
         return out
 
     def weight_of(self, pid: int) -> int:
@@ -140,6 +185,10 @@ class Profile:
     def simulator_plugin_names(self) -> List[str]:
         """Names after ConvertForSimulator (plugins.go:174-197)."""
         return [n if n.endswith(PLUGIN_SUFFIX) else n + PLUGIN_SUFFIX for n, _ in self.plugins]
+
+
+def _plain(name: str) -> str:
+    return name[:-len(PLUGIN_SUFFIX)] if name.endswith(PLUGIN_SUFFIX) else name
 
 
 def default_profile() -> Profile:

@@ -859,7 +859,8 @@ def schedule_one(pod: m.Pod, infos: List[NodeInfo], prof: P.Profile):
             else:
                 pstate[pid] = s
                 rec["prescore"][name] = "success"
-    weights = prof.weights()
+    weights = prof.weights()              # the store's map: finalscore annotations
+    sel_weights = prof.selection_weights()  # the framework's: the selection totals
     total = [0] * len(fnodes)
     for pid in prof.score_order():
         if pid in skip_score:
@@ -910,7 +911,7 @@ def schedule_one(pod: m.Pod, infos: List[NodeInfo], prof: P.Profile):
         for i, s in enumerate(norm):
             if s > MAX_NODE_SCORE or s < 0:
                 raise ValueError(f"plugin {name} returns an invalid score {s}")
-            total[i] += s * w
+            total[i] += s * sel_weights.get(name, 1)
         rec["raw"][name] = {feasible[i]: raw[i] for i in range(len(raw))}
         rec["norm"][name] = {feasible[i]: norm[i] for i in range(len(norm))}
     best = max(range(len(fnodes)), key=lambda i: (total[i], -feasible[i]))

@@ -76,8 +76,6 @@ def test_profile_from_config_multipoint_merge():
 
 def test_profile_from_config_refuses_unmodelled():
     with pytest.raises(NotImplementedError):
-        I.profile_from_config({"profiles": [{"plugins": {"filter": {"disabled": [{"name": "NodeAffinity"}]}}}]})
-    with pytest.raises(NotImplementedError):
         I.profile_from_config({"profiles": [{"pluginConfig": [{"name": "NodeResourcesFit", "args": {
             "scoringStrategy": {"type": "RequestedToCapacityRatio"}}}]}]})
     with pytest.raises(ValueError):
@@ -195,3 +193,106 @@ def test_snapshot_with_running_pods_end_to_end():
     want, _ = pyoracle_annotations(snap.nodes, queue, snap.profile, bound)
     assert want == got
     assert any(a[A.SELECTED_NODE] for a in got)
+
+
+# ---- the reference's own export sample (simulator/docs/api-samples/v1/export.md) ----
+
+def _export(case):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "export_md.json")) as f:
+        return json.load(f)[case]
+
+
+LEGACY = ("EBSLimits", "GCEPDLimits", "AzureDiskLimits")
+
+
+def export_config_loadable():
+    """case 1's schedulerConfig without the three volume-limit plugins the
+    simulator's registry (in-tree MultiPoint names only, plugins.go:39-60)
+    does not hold."""
+    import copy
+    cfg = copy.deepcopy(_export("case1")["schedulerConfig"])
+    flt = cfg["profiles"][0]["plugins"]["filter"]
+    flt["enabled"] = [e for e in flt["enabled"] if e["name"] not in LEGACY]
+    return cfg
+
+
+@pytest.mark.parametrize("case", ["case1", "case2"])
+def test_export_sample_refused_like_the_registry(case):
+    """Both samples name EBSLimits / GCEPDLimits / AzureDiskLimits under
+    filter; the simulator registers only the in-tree MultiPoint plugins, so
+    its framework cannot be built from this configuration either."""
+    with pytest.raises(ValueError, match="EBSLimits"):
+        I.load_snapshot(_export(case))
+
+
+def test_export_sample_priority_classes_and_empty_cluster():
+    doc = _export("case2")
+    doc["schedulerConfig"] = export_config_loadable()
+    snap = I.load_snapshot(doc)
+    assert snap.nodes == [] and snap.pods == [] and snap.queue == []
+
+
+def test_export_sample_per_point_expansion():
+    """The per-point sets of the sample expanded against the in-tree
+    MultiPoint set (profile.py docstring); weights: the framework takes the
+    Score point's own, the store map MultiPoint's."""
+    prof, pct = I.profile_from_config(export_config_loadable())
+    assert pct == 0
+    nm = lambda ids: [P.PLUGIN_NAMES[i] for i in ids]
+    assert nm(prof.filter_order()) == [
+        "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts", "NodeResourcesFit",
+        "VolumeRestrictions", "NodeVolumeLimits", "VolumeBinding", "VolumeZone", "PodTopologySpread",
+        "InterPodAffinity"]
+    assert nm(prof.prefilter_order()) == [
+        "NodeResourcesFit", "NodePorts", "VolumeRestrictions", "PodTopologySpread", "InterPodAffinity",
+        "VolumeBinding", "NodeAffinity", "NodeVolumeLimits", "VolumeZone"]
+    assert nm(prof.prescore_order()) == [
+        "InterPodAffinity", "PodTopologySpread", "TaintToleration", "NodeAffinity", "NodeResourcesFit",
+        "VolumeBinding", "NodeResourcesBalancedAllocation"]
+    assert nm(prof.score_order()) == [
+        "NodeResourcesBalancedAllocation", "ImageLocality", "InterPodAffinity", "NodeResourcesFit",
+        "NodeAffinity", "PodTopologySpread", "TaintToleration", "VolumeBinding"]
+    sel, store = prof.selection_weights(), prof.weights()
+    for k, v in {"TaintToleration": 1, "NodeAffinity": 1, "PodTopologySpread": 2, "InterPodAffinity": 1,
+                 "NodeResourcesFit": 1, "NodeResourcesBalancedAllocation": 1, "ImageLocality": 1}.items():
+        assert sel[k] == v, k
+    for k, v in {"TaintToleration": 3, "NodeAffinity": 2, "PodTopologySpread": 2, "InterPodAffinity": 2,
+                 "NodeResourcesFit": 1, "NodeResourcesBalancedAllocation": 1, "ImageLocality": 1}.items():
+        assert store[k] == v, k
+    assert prof.hard_pod_affinity_weight == 1 and prof.fit_strategy == P.LEAST_ALLOCATED
+
+
+def test_per_point_disable_and_errors():
+    prof, _ = I.profile_from_config({"profiles": [{"plugins": {"filter": {"disabled": [{"name": "NodeAffinity"}]}}}]})
+    assert "NodeAffinity" not in [P.PLUGIN_NAMES[i] for i in prof.filter_order()]
+    assert "NodeAffinity" in [P.PLUGIN_NAMES[i] for i in prof.score_order()]
+    prof, _ = I.profile_from_config({"profiles": [{"plugins": {"score": {
+        "enabled": [{"name": "ImageLocality", "weight": 7}], "disabled": [{"name": "*"}]}}}]})
+    assert prof.score_order() == [P.IMAGE_LOCALITY] and prof.selection_weights()["ImageLocality"] == 7
+    assert prof.weights()["ImageLocality"] == 1          # the store map: MultiPoint's weight wins
+    with pytest.raises(ValueError, match="does not extend"):
+        I.profile_from_config({"profiles": [{"plugins": {"filter": {"enabled": [{"name": "ImageLocality"}]}}}]})
+
+
+def test_export_profile_cpp_oracle_vs_pyoracle():
+    """The export sample's profile on a small config-3 cluster: the C++
+    oracle (selection on the Score point's weights, through encode_profile)
+    and pyoracle give the same annotation bytes (store weights = MultiPoint's)."""
+    import binding
+    from helpers import pyoracle_annotations
+    F = pkg("framework")
+    nodes, pods, _ = G.config3(n_nodes=30, n_pods=90, apps=6, zones=3)
+    doc = I.snapshot_document(nodes, pods, P.default_profile())
+    doc["schedulerConfig"] = export_config_loadable()
+    snap = I.load_snapshot(doc)
+    s = F.DebuggableScheduler(snap.nodes, snap.pods, snap.profile, engine=binding.Oracle(2))
+    got = []
+    for i in snap.queue:
+        s.schedule_one(i)
+        got.append(s.annotations(i))
+    want, _ = pyoracle_annotations(snap.nodes, [snap.pods[i] for i in snap.queue], snap.profile)
+    assert want == got
+    # the two weight maps really differ here, so the test separates them
+    assert snap.profile.weights()["TaintToleration"] != snap.profile.selection_weights()["TaintToleration"]
