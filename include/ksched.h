@@ -196,7 +196,9 @@ typedef struct ksg_result {
 } ksg_result;
 
 /* Optional capture of everything the wrapped plugins would record.  Arrays are
- * per pod; ksg_run_queue() writes pod k at offset k * (stride of the array). */
+ * per pod; ksg_run_queue() writes pod k at offset k * (stride of the array).
+ * raw / norm rows of plugins outside the profile's score set may be left
+ * untouched (the batched path writes only the score set's rows). */
 typedef struct ksg_capture {
   uint32_t* fstatus;    /* [n_nodes]                 filter status word       */
   int64_t* raw;         /* [KSG_NPLUGINS][n_nodes]   Score() value            */
@@ -306,7 +308,9 @@ enum {
   KSG_K_TOPO_COOP = 9,
   KSG_K_BATCH_PHASE2P = 10,
   KSG_K_SWEEP_NARROW = 11,
-  KSG_NKERNELS = 12
+  KSG_K_CAPTURE_EVAL = 12,
+  KSG_K_CAPTURE_NORM = 13,
+  KSG_NKERNELS = 14
 };
 typedef struct ksg_kernel_stat {
   char name[48];

@@ -148,6 +148,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
 
     int selected = -1;
     uint32_t status = 0;
+    if (cap && g.nfeas == 1 && tid == 0)   // one feasible node: no Score runs, nothing recorded
+      for (int q = 0; q < KSG_NPLUGINS; q++) craw[(size_t)q * N + g.minidx] = cnorm[(size_t)q * N + g.minidx] = 0;
     if (g.nfeas == 1) {
       selected = g.minidx;
     } else if (g.nfeas >= 2) {
@@ -1621,6 +1623,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 }
 
 #include "ksched_phase2p.h"
+#include "ksched_capture.h"
 #include "ksched_sweep.h"
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
@@ -1934,6 +1937,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
     // ---- sweep C: normalise, weight, argmax ------------------------------------
     int selected = -1;
     uint32_t status = 0;
+    if (cap && ok && gr.nfeas == 1 && tid == 0)   // one feasible node: no Score runs, nothing recorded
+      for (int q = 0; q < KSG_NPLUGINS; q++) craw[(size_t)q * N + gr.minidx] = cnorm[(size_t)q * N + gr.minidx] = 0;
     if (!ok) {
       status |= KSG_ST_SCORE_ERROR;
     } else if (gr.nfeas == 1) {
@@ -2251,7 +2256,8 @@ void free_all(ksg_ctx* ctx) {
 const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_batch_phase1",
                                           "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan",
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
-                                          "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow"};
+                                          "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
+                                          "ksg_capture_eval", "ksg_capture_norm"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2448,7 +2454,7 @@ static const std::array<const void*, 6>& slot_kernels() {
   return k;
 }
 
-int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
+int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const CapArgs* cap,
                 const ksg_profile* d_prof) {
   const int N = ctx->c.N;
   if (!ctx->d_rec) {
@@ -2546,6 +2552,18 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     } else {
       hipLaunchKernelGGL(ksg_batch_phase2_scan<512>, dim3(1), dim3(512), bytes, ctx->stream, b);
       if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2_SCAN, units))) return trc;
+    }
+    if (cap) {   // the batch's capture, on the post-batch state (ksched_capture.h)
+      CapArgs ca = *cap;
+      ca.b0 = b.b0;
+      ca.nb = b.nb;
+      ca.out0 = b.out0;
+      ca.rec = ctx->d_rec;
+      HIPC(ctx, hipMemsetAsync(ca.stats, 0, sizeof(int32_t) * 4 * b.nb, ctx->stream));
+      hipLaunchKernelGGL(ksg_capture_eval, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, ca);
+      if ((trc = tlaunched(ctx, KSG_K_CAPTURE_EVAL, units))) return trc;
+      hipLaunchKernelGGL(ksg_capture_norm, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, ca);
+      if ((trc = tlaunched(ctx, KSG_K_CAPTURE_NORM, units))) return trc;
     }
     off += nb;
   }
@@ -3056,7 +3074,28 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   HIPC(ctx, hipMemcpyAsync(d_prof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream));
   const bool want_cap = cap && (cap->fstatus || cap->raw || cap->norm || cap->total);
   QueueArgs a = base_args(ctx);
-  if (want_cap) {
+  bool batched = do_commit && batch_eligible(ctx, first, count);
+  if (ctx->force_path == 1) batched = false;
+  // captured queues take the batched path too (ksched_capture.h): the capture
+  // kernels write the profile's score rows only, in a compact layout
+  CapArgs ca{};
+  if (want_cap && batched) {
+    ca.c = ctx->c;
+    ca.st = ctx->st;
+    ca.pods = ctx->d_pods;
+    ca.prog = ctx->d_prog;
+    ca.prof = d_prof;
+    ca.placements = d_pl;
+    for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+      if ((ctx->prof.score_mask >> pl) & 1u) ca.rows[ca.n_rows++] = pl;
+    TA(tmp, &ca.stats, sizeof(int32_t) * 4 * KSG_BATCH_MAX);
+    TA(tmp, &ca.fstatus, sizeof(uint32_t) * N * count);
+    TA(tmp, &ca.total, sizeof(int64_t) * N * count);
+    if (ca.n_rows) {
+      TA(tmp, &ca.raw, sizeof(int64_t) * N * ca.n_rows * count);
+      TA(tmp, &ca.norm, sizeof(int64_t) * N * ca.n_rows * count);
+    }
+  } else if (want_cap) {
     TA(tmp, &a.cap_fstatus, sizeof(uint32_t) * N * count);
     TA(tmp, &a.cap_raw, sizeof(int64_t) * N * KSG_NPLUGINS * count);
     TA(tmp, &a.cap_norm, sizeof(int64_t) * N * KSG_NPLUGINS * count);
@@ -3065,14 +3104,11 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     HIPC(ctx, hipMemsetAsync(a.cap_norm, 0, sizeof(int64_t) * N * KSG_NPLUGINS * count, ctx->stream));
     HIPC(ctx, hipMemsetAsync(a.cap_total, 0, sizeof(int64_t) * N * count, ctx->stream));
   }
-  bool batched = do_commit && !want_cap && batch_eligible(ctx, first, count);
-  if (ctx->force_path == 1) batched = false;
-  if (ctx->force_path == 2 && do_commit && !want_cap) batched = batch_eligible(ctx, first, count);
   if (batched) {
     ctx->last_path = 2;
-    if (ctx->batch_mode == 3) {
+    if (ctx->batch_mode == 3 && !want_cap) {
       if ((rc = run_pipe(ctx, first, count, d_pl, d_res, d_prof))) return rc;
-    } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, d_prof))) {
+    } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, want_cap ? &ca : nullptr, d_prof))) {
       return rc;
     }
   } else {
@@ -3096,7 +3132,19 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   }
   if (placements) HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * count, hipMemcpyDeviceToHost, ctx->stream));
   if (results) HIPC(ctx, hipMemcpyAsync(results, d_res, sizeof(ksg_result) * count, hipMemcpyDeviceToHost, ctx->stream));
-  if (want_cap) {
+  if (want_cap && batched) {
+    if (cap->fstatus) HIPC(ctx, hipMemcpyAsync(cap->fstatus, ca.fstatus, sizeof(uint32_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
+    if (cap->total) HIPC(ctx, hipMemcpyAsync(cap->total, ca.total, sizeof(int64_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
+    for (int q = 0; q < ca.n_rows; q++) {   // compact row q -> the caller's plugin row, every pod
+      const size_t w = sizeof(int64_t) * N, hp = w * KSG_NPLUGINS, dp = w * ca.n_rows;
+      if (cap->raw)
+        HIPC(ctx, hipMemcpy2DAsync(cap->raw + (size_t)ca.rows[q] * N, hp, ca.raw + (size_t)q * N, dp, w, count,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+      if (cap->norm)
+        HIPC(ctx, hipMemcpy2DAsync(cap->norm + (size_t)ca.rows[q] * N, hp, ca.norm + (size_t)q * N, dp, w, count,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+    }
+  } else if (want_cap) {
     if (cap->fstatus) HIPC(ctx, hipMemcpyAsync(cap->fstatus, a.cap_fstatus, sizeof(uint32_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
     if (cap->raw) HIPC(ctx, hipMemcpyAsync(cap->raw, a.cap_raw, sizeof(int64_t) * N * KSG_NPLUGINS * count, hipMemcpyDeviceToHost, ctx->stream));
     if (cap->norm) HIPC(ctx, hipMemcpyAsync(cap->norm, a.cap_norm, sizeof(int64_t) * N * KSG_NPLUGINS * count, hipMemcpyDeviceToHost, ctx->stream));

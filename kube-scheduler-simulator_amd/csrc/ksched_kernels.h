@@ -416,13 +416,16 @@ struct NodeEval {
 };
 
 // RunFilterPlugins (first rejection ends the node) + the raw Score() of every
-// enabled score plugin, for one (pod, node).  craw/cnorm: optional capture rows.
+// enabled score plugin, for one (pod, node).  craw/cnorm: optional capture rows;
+// lraw: optional per-plugin raw scores of the node-local plugins ([KSG_NPLUGINS],
+// constant indices: registers).
 // Src: GNode (columns in global memory) or LNode (a node cached in LDS); L:
 // the node's resource columns, already gathered by the caller.
 template <class Src>
 __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg_profile& prof, const PodView& v,
                                                   const Src& nd, const NodeCols& L, int n, int64_t* craw,
-                                                  int64_t* cnorm, const TopoCtx* tc = nullptr) {
+                                                  int64_t* cnorm, const TopoCtx* tc = nullptr,
+                                                  int64_t* lraw = nullptr) {
   const ksg_pod& p = *v.p;
   const int N = c.N;
   NodeEval e{0, 0, 0, 0, 0};
@@ -475,25 +478,30 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
   if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) {
     const int64_t s = fit_score(prof, p, L);
     e.part += s * v.w_fit;
+    if (lraw) lraw[KSG_PL_NODE_RESOURCES_FIT] = s;
     if (craw) { craw[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = s; cnorm[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = s; }
   }
   if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) {
     const int64_t s = ba_score(prof, p, L);
     e.part += s * v.w_ba;
+    if (lraw) lraw[KSG_PL_BALANCED_ALLOCATION] = s;
     if (craw) { craw[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; cnorm[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; }
   }
   if (v.smask & bit(KSG_PL_IMAGE_LOCALITY)) {
     const int64_t s = image_score(c, nd, v.P, v.img, p.n_containers);
     e.img = s * v.w_img;
+    if (lraw) lraw[KSG_PL_IMAGE_LOCALITY] = s;
     e.part += e.img;
     if (craw) { craw[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; cnorm[(size_t)KSG_PL_IMAGE_LOCALITY * N + n] = s; }
   }
   if (v.smask & bit(KSG_PL_TAINT_TOLERATION)) {
     e.rt = taint_score(c, nd, v.tolp);
+    if (lraw) lraw[KSG_PL_TAINT_TOLERATION] = e.rt;
     if (craw) craw[(size_t)KSG_PL_TAINT_TOLERATION * N + n] = e.rt;
   }
   if (v.smask & bit(KSG_PL_NODE_AFFINITY)) {
     e.ra = na_pref_score(nd, v.P, v.na_pref);
+    if (lraw) lraw[KSG_PL_NODE_AFFINITY] = e.ra;
     if (craw) craw[(size_t)KSG_PL_NODE_AFFINITY * N + n] = e.ra;
   }
   return e;
