@@ -26,7 +26,13 @@ Prints ONE JSON line (rank 0).  The line also carries:
   N);
 * `cpu_baseline` (rank 0, N = 1): the C++ restatement (oracle/) on a bounded
   prefix of the same queue, at 16 threads (upstream parallelism) and at every
-  host core this process may use, with the CPU model.
+  host core this process may use, with the CPU model;
+* `annotations` (N = 1): the simulator's product for the first 2,000 pods of
+  the same queue: captured batched run + filter-result / score-result /
+  finalscore-result bytes from ksg_annotate (bulk.annotate_queue, device
+  capture of the next chunk overlapping the serialisation of this one);
+* `default_profile` (N = 1): the in-tree default profile (every Filter/Score
+  plugin, generator.config1) at the same 5,000 nodes.
 """
 from __future__ import annotations
 
@@ -139,6 +145,82 @@ def replica_sweep(eng, enc, prof, G, E, metrics, replicas, R: int, P: int, rank:
             "roofline": metrics.dominant_kernel_roofline(ks, metrics.bytes_per_node_eval(enc, prof)) if ks else None}
 
 
+def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threads: int):
+    """Annotation bytes for the first n_pods of the queue (bulk.annotate_queue):
+    end-to-end wall (device capture + D2H + ksg_annotate on `threads` workers),
+    the capture alone, and an xxh3 digest over every pod's three values."""
+    import numpy as np
+    import xxhash
+    digests = np.zeros(n_pods, np.uint64)
+    sizes = np.zeros(n_pods, np.int64)
+
+    def sink(i, vals):
+        h = xxhash.xxh3_64()
+        for v in vals:
+            h.update(v)
+        digests[i] = h.intdigest()
+        sizes[i] = sum(len(v) for v in vals)
+
+    bulk = B.BulkAnnotator(enc, prof, threads=threads)
+    try:
+        eng.reset_state()
+        B.annotate_queue(eng, bulk, 0, min(chunk, n_pods), sink, chunk=chunk)   # warmup
+        eng.reset_state()
+        t = time.perf_counter()
+        pl = B.annotate_queue(eng, bulk, 0, n_pods, sink, chunk=chunk)
+        wall = time.perf_counter() - t
+    finally:
+        bulk.close()
+    # the captured run alone (device + D2H of the capture arrays), same chunks
+    cap = native.CaptureBuffers(len(enc.cluster.node_names), min(chunk, n_pods))
+    eng.reset_state()
+    eng.set_timing(True)
+    t = time.perf_counter()
+    dev_ms = 0.0
+    ks = {}
+    for off in range(0, n_pods, chunk):
+        k = min(chunk, n_pods - off)
+        eng.run_queue(off, k, capture=cap)
+        dev_ms += eng.last_kernel_ms()
+        for r in eng.kernel_stats():
+            ks[r["name"]] = ks.get(r["name"], 0.0) + r["total_ms"]
+    cap_wall = time.perf_counter() - t
+    eng.set_timing(False)
+    h = xxhash.xxh3_64()
+    h.update(digests.tobytes())
+    return {"workload": f"configs[1] cluster, first {n_pods} pods, {chunk}-pod chunks, capture on the batched "
+                        f"path + ksg_annotate on {threads} threads",
+            "pods_per_s": n_pods / wall, "wall_s": wall, "annotation_bytes": int(sizes.sum()),
+            "annotation_MB_per_s": sizes.sum() / wall / 1e6,
+            "capture_only_pods_per_s": n_pods / cap_wall, "capture_device_ms": dev_ms,
+            "capture_kernels_ms": {k: round(v, 3) for k, v in ks.items()},
+            "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(), "threads": threads}
+
+
+def default_profile_line(native, G, E, n_nodes: int, n_pods: int, steps: int):
+    """The in-tree default profile at n_nodes (generator.config1): pods/s of
+    reset + one ksg_run_queue over n_pods, best of `steps`."""
+    nodes, pods, prof = G.config1(n_nodes=n_nodes, n_pods=n_pods)
+    enc = E.Encoder(nodes, pods, prof)
+    eng = native.Engine(device=0)
+    eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    best, kms = None, None
+    for _ in range(steps + 1):
+        eng.reset_state()
+        t = time.perf_counter()
+        pl, _ = eng.run_queue(0, n_pods, results=False)
+        dt = time.perf_counter() - t
+        if best is None or dt < best:
+            best, kms = dt, eng.last_kernel_ms()
+    eng.set_timing(True)
+    eng.reset_state()
+    eng.run_queue(0, n_pods, results=False)
+    names = sorted({k["name"] for k in eng.kernel_stats()})
+    return {"workload": f"default profile (every in-tree Filter/Score plugin), generator.config1: {n_nodes} nodes x "
+                        f"{n_pods} pods", "pods_per_s": n_pods / best, "device_pods_per_s": n_pods / (kms * 1e-3),
+            "scheduled": int((pl >= 0).sum()), "kernels": names}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,6 +232,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep-replicas", type=int, default=1024, help="configs[3] sidecar; 0 disables")
     ap.add_argument("--sweep-pods", type=int, default=1000)
+    ap.add_argument("--annotate-pods", type=int, default=2000, help="annotation sidecar; 0 disables")
+    ap.add_argument("--annotate-threads", type=int, default=16)
+    ap.add_argument("--default-pods", type=int, default=20000, help="default-profile line; 0 disables")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,6 +313,20 @@ def main():
         except Exception as e:   # a sidecar; never lose the headline line over it
             log(f"[rank {rank}] replica sweep unavailable: {e}")
 
+    ann = dflt = None
+    if world == 1 and args.annotate_pods > 0:
+        try:
+            B = importlib.import_module(PKG + ".bulk")
+            ann = annotation_sidecar(eng, enc, prof, native, B, min(args.annotate_pods, P), 256,
+                                     args.annotate_threads)
+        except Exception as e:
+            log(f"[rank {rank}] annotation sidecar unavailable: {e}")
+    if world == 1 and args.default_pods > 0:
+        try:
+            dflt = default_profile_line(native, G, E, args.nodes, args.default_pods, 2)
+        except Exception as e:
+            log(f"[rank {rank}] default-profile line unavailable: {e}")
+
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
         pods_per_s = world * P * args.steps / elapsed
@@ -273,6 +372,10 @@ def main():
         }
         if sweep is not None:
             out["replica_sweep"] = sweep
+        if ann is not None:
+            out["annotations"] = ann
+        if dflt is not None:
+            out["default_profile"] = dflt
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baselines(enc, pf, args.cpu_budget)
         print(json.dumps(out), flush=True)

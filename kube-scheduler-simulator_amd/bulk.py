@@ -1,0 +1,103 @@
+"""Bulk annotation: a whole queue's filter-result / score-result /
+finalscore-result values (store.go:423-507 as GetStoredResult serialises them,
+store.go:133-198) from one captured device run.
+
+`framework.DebuggableScheduler` mirrors the wrapper pod by pod (one ksg_eval,
+record, commit per cycle).  For a queue that needs no preemption the same
+three annotation values come out of one captured `ksg_run_queue` (the batched
+path with its capture kernels, ksched_capture.h) followed by one
+`ksg_annotate` per pod; `annotate_queue` runs that in chunks, with the device
+capture of chunk i + 1 overlapping the native serialisation of chunk i on a
+thread pool (ctypes releases the GIL in both calls).  The bytes are the
+per-pod path's, which tests/test_gpu_bulk_annotations.py checks.
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+from typing import Callable, List, Optional
+
+import numpy as np
+
+from . import encoder as E
+from . import native
+from . import profile as P
+
+
+class BulkAnnotator:
+    """Per-profile constants plus one native annotator per worker thread."""
+
+    def __init__(self, enc: E.Encoder, prof: P.Profile, threads: int = 1):
+        cl = enc.cluster
+        self.enc, self.prof = enc, prof
+        self.n_nodes = len(cl.node_names)
+        taints = [f"{{{t.key}: {t.value}}}" for t in cl.taint_vocab]
+        self.annotators = [native.Annotator(cl.node_names, P.PLUGIN_NAMES, cl.res_names, taints, cl.arrays["taints"])
+                           for _ in range(max(1, threads))]
+        store_w = prof.weights()
+        self.weights = np.array([store_w.get(n, 0) for n in P.PLUGIN_NAMES], np.int64)
+        self.norm_mask = sum(1 << pid for pid in range(len(P.PLUGIN_NAMES)) if P.EXT[pid][4])
+        self.filter_order = prof.filter_order()
+        self.score_order = prof.score_order()
+        self.pool = ThreadPoolExecutor(max_workers=len(self.annotators)) if len(self.annotators) > 1 else None
+
+    def close(self):
+        if self.pool:
+            self.pool.shutdown()
+        for a in self.annotators:
+            a.close()
+
+    def _pod(self, ann: native.Annotator, k: int, pi: int, res, cap: native.CaptureBuffers):
+        rec = self.enc.workload.pods[pi]
+        fskip = int(rec["filter_skip"])
+        if int(res["status"][k]) & native.ST_IPA_PREFILTER_SKIP:
+            fskip |= 1 << P.INTER_POD_AFFINITY
+        order = [p for p in self.filter_order if not (fskip >> p) & 1]
+        nf = int(res["n_feasible"][k])
+        sskip = int(res["score_skip"][k])
+        sorder = [p for p in self.score_order if not (sskip >> p) & 1] if nf >= 2 else []
+        return ann.annotate_bytes(order, sorder, self.norm_mask, self.weights, nf, cap.fstatus[k], cap.raw[k],
+                                  cap.norm[k])
+
+    def serialise(self, first: int, res, cap: native.CaptureBuffers, count: int,
+                  sink: Callable[[int, tuple], None]):
+        """ksg_annotate for pods first .. first + count of a captured chunk;
+        sink(pod index, (filter, score, finalscore) bytes) in pod order per worker."""
+        T = len(self.annotators)
+
+        def work(t):
+            for k in range(t, count, T):
+                sink(first + k, self._pod(self.annotators[t], k, first + k, res, cap))
+
+        if self.pool is None:
+            work(0)
+        else:
+            list(self.pool.map(work, range(T)))
+
+
+def annotate_queue(engine: native.Engine, bulk: BulkAnnotator, first: int, count: int,
+                   sink: Callable[[int, tuple], None], chunk: int = 256) -> np.ndarray:
+    """Schedule pods [first, first + count) in chunks with capture on, emitting
+    every pod's three annotation values through `sink`; returns placements.
+    The device capture of the next chunk overlaps the serialisation of the
+    current one."""
+    N = bulk.n_nodes
+    out = np.empty(count, np.int32)
+    io = ThreadPoolExecutor(max_workers=1)
+    caps = [native.CaptureBuffers(N, min(chunk, count)) for _ in range(2)]
+
+    def capture(off, buf):
+        k = min(chunk, count - off)
+        pl, res = engine.run_queue(first + off, k, capture=buf)
+        return off, k, pl, res, buf
+
+    pending: Optional[object] = io.submit(capture, 0, caps[0]) if count else None
+    i = 0
+    while pending is not None:
+        off, k, pl, res, buf = pending.result()
+        out[off:off + k] = pl
+        nxt = off + k
+        i ^= 1
+        pending = io.submit(capture, nxt, caps[i]) if nxt < count else None
+        bulk.serialise(first + off, res, buf, k, sink)
+    io.shutdown()
+    return out

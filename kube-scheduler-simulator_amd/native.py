@@ -408,6 +408,11 @@ class Annotator:
 
     def annotate(self, filter_order, score_order, normalize_mask: int, weight, n_feasible: int,
                  fstatus: np.ndarray, raw: np.ndarray, norm: np.ndarray):
+        return tuple(b.decode("utf-8") for b in self.annotate_bytes(
+            filter_order, score_order, normalize_mask, weight, n_feasible, fstatus, raw, norm))
+
+    def annotate_bytes(self, filter_order, score_order, normalize_mask: int, weight, n_feasible: int,
+                       fstatus: np.ndarray, raw: np.ndarray, norm: np.ndarray):
         fo = np.ascontiguousarray(filter_order, np.int32)
         so = np.ascontiguousarray(score_order, np.int32)
         w = np.ascontiguousarray(weight, np.int64)
@@ -421,7 +426,7 @@ class Annotator:
         rc = self._annotate(self.h, C.byref(inp), out, ln)
         if rc != 0:
             raise KschedError(f"ksg_annotate rc={rc}")
-        return tuple(C.string_at(out[i], ln[i]).decode("utf-8") for i in range(3))
+        return tuple(C.string_at(out[i], ln[i]) for i in range(3))
 
     def close(self):
         if self.h:
