@@ -98,6 +98,20 @@ def cpu_baselines(enc, pf, budget_s: float):
     return out
 
 
+def pmc_traffic(kernel, name):
+    """HBM bytes per dispatch of `kernel` from a committed PMC summary
+    (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    path = os.path.join(ROOT, "profiles", "r2", name)
+    try:
+        row = json.load(open(path)).get(kernel) if kernel else None
+    except (OSError, ValueError):
+        return None, None
+    if not row or row.get("hbm_bytes_per_dispatch") is None:
+        return None, None
+    return row["hbm_bytes_per_dispatch"], "profiles/r2/" + name
+
+
 def replica_sweep(eng, enc, prof, G, E, metrics, replicas, R: int, P: int, rank: int, world: int, dist, dev):
     """BASELINE configs[3] beside the headline: R what-if replicas (weights and
     strategy per replica, generator.replica_profiles) of the first P pods of
@@ -134,6 +148,10 @@ def replica_sweep(eng, enc, prof, G, E, metrics, replicas, R: int, P: int, rank:
         eng.set_timing(False)
     kms, wms = min(ms), min(walls)
     n = len(enc.cluster.node_names)
+    roof = metrics.dominant_kernel_roofline(ks, metrics.bytes_per_node_eval(enc, prof)) if ks else None
+    if roof is not None:
+        # PMC passes of the same sweep shape at 256 pods per call (64-pod launches, as here)
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(roof.get("kernel"), "pmc_config4.json")
     return {"workload": f"configs[3]: {R} replicas x {n} nodes, first {P} pods of the configs[1] queue, "
                         f"sharded over {world} rank(s), RCCL all_gather of placements + summaries",
             "replica_pods_per_s": R * P / (wms * 1e-3), "node_evals_per_s": R * P * n / (wms * 1e-3),
@@ -142,7 +160,7 @@ def replica_sweep(eng, enc, prof, G, E, metrics, replicas, R: int, P: int, rank:
             "replicas_per_rank": hi - lo, "collective": "nccl (RCCL) all_gather",
             "placements_sha256": hashlib.sha256(np.ascontiguousarray(pl).tobytes()).hexdigest(),
             "scheduled_total": int(sm[:, 0].sum()),
-            "roofline": metrics.dominant_kernel_roofline(ks, metrics.bytes_per_node_eval(enc, prof)) if ks else None}
+            "roofline": roof}
 
 
 def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threads: int):
@@ -346,16 +364,7 @@ def main():
         # HBM bytes per launch of the dominant kernel from the committed PMC
         # passes (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE
         # + WRITE_SIZE per dispatch, gfx950-corrected), null when not collected
-        roof["traffic"] = None
-        pmc = os.path.join(ROOT, "profiles", "r2", "pmc_config2.json")
-        if os.path.exists(pmc) and roof.get("kernel"):
-            try:
-                row = json.load(open(pmc)).get(roof["kernel"])
-                if row:
-                    roof["traffic"] = row["hbm_bytes_per_dispatch"]
-                    roof["traffic_source"] = "profiles/r2/pmc_config2.json"
-            except Exception:
-                pass
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(roof.get("kernel"), "pmc_config2.json")
         roof["bytes_per_node_eval"] = bpe
         roof["node_evals_per_launch"] = P * len(nodes)
         out = {

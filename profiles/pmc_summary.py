@@ -20,6 +20,19 @@ import sys
 from collections import defaultdict
 
 
+def kernel_key(name: str) -> str:
+    """The ksg_kernel_stats name of a rocprofv3 kernel name: template
+    arguments dropped, except that the narrow replica-sweep instances
+    (ksg_sweep<..., NARROW = true>, the sixth argument) are ksg_sweep_narrow."""
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0].strip()
+    base = name.split("<")[0].strip()
+    if base == "ksg_sweep" and "<" in name:
+        args = [a.strip() for a in name[name.index("<") + 1:name.rindex(">")].split(",")]
+        if len(args) >= 6 and args[5] == "true":
+            return "ksg_sweep_narrow"
+    return base
+
+
 def counters(path):
     """{kernel: [values per dispatch]} from a counter_collection.csv."""
     out = defaultdict(list)
@@ -27,8 +40,7 @@ def counters(path):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
-                name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1)
-                name = name.split("(")[0].split("<")[0].strip()
+                name = kernel_key(name)
                 out[name].append(float(row["Counter_Value"]))
     return out
 

@@ -1,15 +1,15 @@
 #!/bin/bash
-# Round-1 profiles on one MI355X (run from the repo root on the GPU box):
+# Profiles on one MI355X (run from the repo root on the GPU box):
 #   1. rocprofv3 --kernel-trace --stats of the default bench (config 2)
 #   2. PMC passes FETCH_SIZE and WRITE_SIZE (separate runs) of the same bench
 #   3. the same three for the config-4 replica sweep (scripts/bench_configs.py)
-# Summaries are folded by profiles/pmc_summary.py into profiles/r1/.
+# Summaries are folded by profiles/pmc_summary.py into profiles/rNN/.
 set -uo pipefail
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1"
-S="python3 scripts/bench_configs.py --config 4 --replicas 1024 --pods 256 --reps 1"
+B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0"
+S="python3 scripts/bench_configs.py --config 4 --replicas 1024 --pods 256 --reps 1 --no-cpu-baseline"
 SP="$S --no-timing"
 run() {  # name, rocprof args..., -- command
   local name=$1; shift

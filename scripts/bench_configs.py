@@ -10,7 +10,10 @@ with PodTopologySpread + InterPodAffinity.  Prints one JSON line with pods/s
 (replica-pods for sweeps), node-evals/s and the per-kernel roofline from HIP
 events on the library's stream.  Pods are a prefix of the config's queue (the
 full queue at configs[3]'s 1,024 x 50,000 would run for minutes per sample);
-the prefix is stated in the output.
+the prefix is stated in the output.  `cpu_baseline`: the C++ restatement
+(oracle/, "port") on a bounded sample of the same workload (whole replicas of
+the same pod prefix for 4 / 5, a prefix of the queue for 3), at 16 threads and
+at every core this process may use, with the CPU model.
 """
 import argparse
 import importlib
@@ -32,6 +35,55 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(enc, pf, profiles, P: int, threads: int, budget_s: float):
+    """Oracle throughput on a bounded sample: replicas one at a time (each the
+    full P-pod prefix) for sweeps, 100-pod chunks of the queue otherwise."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import binding
+    o = binding.Oracle(threads)
+    o.load(enc, pf)
+    N = len(enc.cluster.node_names)
+    t0 = time.perf_counter()
+    if profiles is not None:
+        done = 0
+        while done < len(profiles) and time.perf_counter() - t0 < budget_s:
+            o.run_replicas([profiles[done]], 0, P)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": done * P / dt, "unit": "replica-pods/s", "cores": threads, "kind": "port",
+                "sample": f"{done} of the {len(profiles)} replicas x {P} pods x {N} nodes ({dt:.1f} s)",
+                "node_evals_per_sec": done * P * N / dt}
+    done = 0
+    while done < P and time.perf_counter() - t0 < budget_s:
+        k = min(100, P - done)
+        o.run_queue(done, k, results=False)
+        done += k
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "pods/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} pods of the queue on the {N}-node cluster ({dt:.1f} s)",
+            "node_evals_per_sec": done * N / dt}
+
+
+def cpu_baselines(enc, pf, profiles, P, budget_s):
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    out = cpu_baseline(enc, pf, profiles, P, 16, budget_s)
+    out.update(cpu_model=cpu_model(), nproc=os.cpu_count(), usable_cores=usable)
+    if usable != 16:
+        allc = cpu_baseline(enc, pf, profiles, P, usable, budget_s)
+        out["all_cores"] = {k: allc[k] for k in ("value", "cores", "sample", "node_evals_per_sec")}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, required=True, choices=(3, 4, 5))
@@ -40,6 +92,8 @@ def main():
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--reps", type=int, default=2, help="timed repetitions (after one warmup)")
     ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event run (PMC passes)")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     t0 = time.time()
@@ -104,6 +158,8 @@ def main():
         "scheduled": int((pl >= 0).sum()), "bytes_per_node_eval": bpe, "columns": per_eval,
         "roofline": roof,
     }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baselines(enc, pf, profiles, P, args.cpu_budget)
     print(json.dumps(out), flush=True)
 
 
