@@ -2806,6 +2806,9 @@ bool narrow_candidate(ksg_ctx* ctx, const ksg_profile* profiles, int R, int firs
     bool fit = false;
     for (int k = 0; k < prof.n_filter; k++) fit |= prof.filter_order[k] == KSG_PL_NODE_RESOURCES_FIT;
     if (!fit) return false;
+    int64_t fw = 0;   // Fit's weighted score numerator stays below 2^30 (sweep_cm_scores32)
+    for (int i = 0; i < prof.fit_n; i++) fw += prof.fit_w[i] > 0 ? prof.fit_w[i] : 0;
+    if (fw * 100 >= (1 << 30)) return false;
     if (mode == 2 && !profile_cm_fast(prof))
       for (int i = 0; i < prof.fit_n; i++)
         if (prof.fit_res[i] >= 3) {
@@ -2842,8 +2845,8 @@ bool narrow_candidate(ksg_ctx* ctx, const ksg_profile* profiles, int R, int firs
 // a.st (replica strides set), or on the narrow records when nstat is set;
 // placements [R][count] on the device.
 int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, const ksg_profile* d_prof, int R,
-              int first, int count, int32_t* d_pl, Tmp& tmp, const int4* nstat = nullptr, int4* nmut = nullptr,
-              int nx = -1) {
+              int first, int count, int32_t* d_pl, Tmp& tmp, const int4* nstat = nullptr,
+              const double2* nrcp = nullptr, int4* nmut = nullptr, int nx = -1) {
   const int mode = sweep_mode(profiles, R);
   const bool narrow = nstat != nullptr;
   const int N = ctx->c.N;
@@ -2857,6 +2860,7 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   s.count = count;
   s.placements = d_pl;
   s.nstat = nstat;
+  s.nrcp = nrcp;
   s.nmut = nmut;
   s.nx = nx;
   TA(tmp, &s.srec, sizeof(uint64_t) * (size_t)kBatch * N);
@@ -3546,15 +3550,17 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   // ksg_narrow_init: nodes), else the int64 columns
   int4* nstat = nullptr;
   int4* nmut = nullptr;
+  double2* nrcp = nullptr;
   NarrowBounds nb{};
   if (sweep && narrow_candidate(ctx, profiles, (int)RR, first, count, sweep_mode(profiles, (int)RR), &nb)) {
     unsigned* d_bad;
     TA(tmp, &nstat, sizeof(int4) * N);
+    TA(tmp, &nrcp, sizeof(double2) * N);
     TA(tmp, &nmut, sizeof(int4) * RR * N);
     TA(tmp, &d_bad, 16);
     HIPC(ctx, hipMemsetAsync(d_bad, 0, 16, ctx->stream));
     hipLaunchKernelGGL(ksg_narrow_init, dim3((unsigned)((N + 255) / 256), (unsigned)std::min<size_t>(RR, 64)), dim3(256),
-                       0, ctx->stream, ctx->c, ctx->st, nstat, nmut, (int)RR, nb, d_bad);
+                       0, ctx->stream, ctx->c, ctx->st, nstat, nrcp, nmut, (int)RR, nb, d_bad);
     HIPC(ctx, hipGetLastError());
     unsigned bad = 0;
     HIPC(ctx, hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
@@ -3605,7 +3611,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   a.placements = d_pl;
   a.results = nullptr;
   if (sweep) {
-    if ((rc = run_sweep(ctx, a, profiles, d_prof, (int)RR, first, count, d_pl, tmp, nstat, nmut, nb.nx))) return rc;
+    if ((rc = run_sweep(ctx, a, profiles, d_prof, (int)RR, first, count, d_pl, tmp, nstat, nrcp, nmut, nb.nx))) return rc;
     ctx->last_path = 3;
   } else {
     const int block = N >= 8192 ? 512 : 256;

@@ -95,15 +95,28 @@ __device__ __forceinline__ int64_t qdiv(int64_t x, int64_t a, float inv) {
 // 1 <= a < 2^53 (integers): the same rcp + two Newton steps + residual fma
 // sequence without v_div_scale / v_div_fmas / v_div_fixup, which are identities
 // in that range.  No VCC use, so two divisions interleave.
-__device__ __forceinline__ double ddiv(double x, double a) {
+__device__ __forceinline__ double ddiv_rcp(double a) {   // ddiv's reciprocal of a
   double r = __builtin_amdgcn_rcp(a);
   double e = __builtin_fma(-a, r, 1.0);
   r = __builtin_fma(r, e, r);
   e = __builtin_fma(-a, r, 1.0);
-  r = __builtin_fma(r, e, r);
+  return __builtin_fma(r, e, r);
+}
+// ddiv with r = ddiv_rcp(a) computed once per divisor (same bits)
+__device__ __forceinline__ double ddiv_r(double x, double a, double r) {
   const double q = x * r;
   const double rem = __builtin_fma(-a, q, x);
   return __builtin_fma(rem, r, q);
+}
+__device__ __forceinline__ double ddiv(double x, double a) { return ddiv_r(x, a, ddiv_rcp(a)); }
+
+// qdiv in 32 bits: floor(x / a) for 0 <= x < 2^30, a >= 1 and a quotient of
+// at most ~100 (the one-step correction covers the float estimate's error).
+__device__ __forceinline__ int32_t qdiv32(int32_t x, int32_t a, float inv) {
+  int32_t q = (int32_t)((float)x * inv);
+  const int32_t r = x - q * a;
+  q += r < 0 ? -1 : (r >= a ? 1 : 0);
+  return q;
 }
 
 // floor(x / a) for a quotient known to be at most 100 (scores, normalisation):

@@ -61,6 +61,7 @@ struct SweepArgs {
   // nx << 24), non-zero cpu milli, requested memory MiB, non-zero memory MiB
   // (24 bits) | pod count << 24}
   const int4* nstat;            // [N]
+  const double2* nrcp;          // [N] ddiv_rcp of the cpu / memory allocatable (1 when 0)
   int4* nmut;                   // [R][N]
   int32_t nx;                   // EX: the one scalar column any pod of the run requests
 };
@@ -261,6 +262,47 @@ __device__ __forceinline__ void sweep_cm_scores(const CmProf& m, const PodCM& p,
   ba = (int32_t)((1 - sd) * (double)100);
 }
 
+// sweep_cm_scores on the narrow records, in 32-bit integers: the range checks
+// (narrow_candidate, ksg_narrow_init) bound every product below 2^30, so the
+// quotients equal the int64 ones; BalancedAllocation's float64 quotients use
+// the per-node reciprocals (ddiv_r: the same bits as ddiv).
+__device__ __forceinline__ void sweep_cm_scores32(const CmProf& m, const PodCM& p, int32_t ac, int32_t am,
+                                                  int32_t rc, int32_t rm, int32_t zc, int32_t zm, double2 rcp,
+                                                  bool ex_on, int32_t ae, int32_t re, int32_t qx, int32_t w_ex,
+                                                  int64_t& fit, int64_t& ba) {
+  const bool hc = ac > 0, hm = am > 0;
+  const int32_t sac = hc ? ac : 1, sam = hm ? am : 1;
+  const float ic = __builtin_amdgcn_rcpf((float)sac), im = __builtin_amdgcn_rcpf((float)sam);
+  const int32_t qc = zc + (int32_t)p.nz_c, qm = zm + (int32_t)p.nz_m;
+  int32_t xc, xm;
+  if (m.least) {
+    xc = qc > ac ? 0 : (ac - qc) * 100;
+    xm = qm > am ? 0 : (am - qm) * 100;
+  } else {
+    xc = (qc > ac ? ac : qc) * 100;
+    xm = (qm > am ? am : qm) * 100;
+  }
+  const int32_t sc = qdiv32(xc, sac, ic), sm = qdiv32(xm, sam, im);
+  const int32_t wc = (int32_t)m.wc, wm = (int32_t)m.wm;
+  int32_t num = (hc ? sc * wc : 0) + (hm ? sm * wm : 0);
+  int32_t ws = (hc ? wc : 0) + (hm ? wm : 0);
+  if (ex_on) {
+    const bool he = ae > 0;
+    const int32_t sae = he ? ae : 1, qe = re + qx;
+    const int32_t xe = m.least ? (qe > ae ? 0 : (ae - qe) * 100) : (qe > ae ? ae : qe) * 100;
+    const int32_t se = qdiv32(xe, sae, __builtin_amdgcn_rcpf((float)sae));
+    num += he ? se * w_ex : 0;
+    ws += he ? w_ex : 0;
+  }
+  fit = ws == 0 ? 0 : qdiv32(num, ws, __builtin_amdgcn_rcpf((float)ws));
+  double fc = ddiv_r((double)(rc + (int32_t)p.req_c), (double)sac, rcp.x);
+  double fm = ddiv_r((double)(rm + (int32_t)p.req_m), (double)sam, rcp.y);
+  fc = fc > 1 ? 1 : fc;
+  fm = fm > 1 ? 1 : fm;
+  const double sd = hc && hm ? fabs((fc - fm) / 2) : 0.0;
+  ba = (int32_t)((1 - sd) * (double)100);
+}
+
 struct OpMaxI32 { __device__ int32_t operator()(int32_t a, int32_t b) const { return a > b ? a : b; } };
 
 struct SweepPart {
@@ -321,6 +363,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
     const ksg_pod& p = a.pods[a.b0 + j];
     const SweepPod q = sweep_pod(sp, prof, p, R);
     const PodCM pc4 = pod_cm<NARROW>(p);
+    const int32_t qx32 = EX && NARROW ? (int32_t)p.req[a.nx] : 0;
     const uint64_t* srec = a.srec + (size_t)j * N;
     const int par = j & 1;
     SweepSlot* slots = a.slots + (size_t)par * gridDim.x;
@@ -334,7 +377,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       return ok;
     };
     auto eval_fast = [&](int n, uint64_t sr, int64_t ac, int64_t am, int64_t rc, int64_t rm, int64_t zc, int64_t zm,
-                         int32_t pc, int32_t al, int64_t ae, int64_t re) -> uint64_t {
+                         int32_t pc, int32_t al, int64_t ae, int64_t re, double2 rcp) -> uint64_t {
       bool ok = (sr & q.fmask) == 0;
       if (q.fit_on) {
         ok = ok && pc + 1 <= al;
@@ -349,8 +392,12 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
       }
       if (!ok) return 0;
       int64_t fs = 0, bs = 0;
-      sweep_cm_scores(sp.cm, pc4, ac, am, rc, rm, zc, zm, EX && q.ex_on, ae, re, EX ? p.req[EX ? sp.ex : 0] : 0,
-                      sp.w_ex, fs, bs);
+      if constexpr (NARROW)
+        sweep_cm_scores32(sp.cm, pc4, (int32_t)ac, (int32_t)am, (int32_t)rc, (int32_t)rm, (int32_t)zc, (int32_t)zm,
+                          rcp, EX && q.ex_on, (int32_t)ae, (int32_t)re, qx32, (int32_t)sp.w_ex, fs, bs);
+      else
+        sweep_cm_scores(sp.cm, pc4, ac, am, rc, rm, zc, zm, EX && q.ex_on, ae, re, EX ? p.req[EX ? sp.ex : 0] : 0,
+                        sp.w_ex, fs, bs);
       const int64_t rt = (sr >> 8) & 0xff, ra = (sr >> 16) & 0xffff, im = (sr >> 32) & 0xff;
       const int64_t part = im * q.w_img + ((q.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? fs * q.w_fit : 0) +
                            ((q.smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? bs * q.w_ba : 0);
@@ -382,6 +429,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
         uint64_t sr[U];
         int64_t ac[U], am[U], rc[U], rm[U], zc[U], zm[U], ae[U], re[U];
         int32_t pc[U], al[U];
+        double2 rcp[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const int n = tb + (k0 + u) * stride;
@@ -389,6 +437,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
           sr[u] = srec[nl];
           if constexpr (NARROW) {
             const int4 st4 = a.nstat[nl], mu = nmut[nl];
+            rcp[u] = a.nrcp[nl];
             ac[u] = st4.x;
             am[u] = st4.y;
             al[u] = st4.z;
@@ -408,6 +457,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
             zm[u] = nonzero[NN + nl];
             pc[u] = pod_count[nl];
             al[u] = c.allowed[nl];
+            rcp[u] = double2{0.0, 0.0};
           }
           if constexpr (!NARROW) {
             ae[u] = 0;
@@ -425,7 +475,7 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
           const int n = tb + (k0 + u) * stride;
           uint64_t x = 0;
           if (k0 + u < iters && n < N)
-            x = eval_fast(n, sr[u], ac[u], am[u], rc[u], rm[u], zc[u], zm[u], pc[u], al[u], ae[u], re[u]);
+            x = eval_fast(n, sr[u], ac[u], am[u], rc[u], rm[u], zc[u], zm[u], pc[u], al[u], ae[u], re[u], rcp[u]);
           account(n, x);
           if constexpr (KN > 0) {
             if (k0 + u < KN) recs[k0 + u < KR ? k0 + u : 0] = x;
@@ -527,13 +577,13 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
         if (!(x >> 63)) return;
         const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
         int64_t total = part;
-        if (q.smask & bit(KSG_PL_TAINT_TOLERATION)) {
-          const int64_t s = gmt != 0 ? 100 - qdiv(100 * rt, gmt, inv_t) : 100;
+        if (q.smask & bit(KSG_PL_TAINT_TOLERATION)) {   // 100 * rt < 2^15, 100 * ra < 2^23: qdiv32's range
+          const int64_t s = gmt != 0 ? 100 - (NARROW ? qdiv32(100 * (int32_t)rt, gmt, inv_t) : qdiv(100 * rt, gmt, inv_t)) : 100;
           err |= (s < 0 || s > 100);
           total += s * q.w_t;
         }
         if (q.smask & bit(KSG_PL_NODE_AFFINITY)) {
-          const int64_t s = gma != 0 ? qdiv(100 * ra, gma, inv_a) : ra;
+          const int64_t s = gma != 0 ? (NARROW ? qdiv32(100 * (int32_t)ra, gma, inv_a) : qdiv(100 * ra, gma, inv_a)) : ra;
           err |= (s < 0 || s > 100);
           total += s * q.w_a;
         }
@@ -631,8 +681,8 @@ struct NarrowBounds {
 // from the context's state): one static record per node, the mutable record
 // broadcast.  A node outside the ranges sets *bad; the host then runs the
 // int64 instances instead (nothing here writes the context's state).
-__global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st, int4* nstat, int4* nmut, int R,
-                                                       NarrowBounds b, unsigned* bad) {
+__global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st, int4* nstat, double2* nrcp,
+                                                       int4* nmut, int R, NarrowBounds b, unsigned* bad) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int N = c.N;
   if (n >= N) return;
@@ -653,13 +703,17 @@ __global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st
   ok = ok && (zm >> kNarrowMemShift) + (am >> kNarrowMemShift) + b.places * b.xm < k24;
   ok = ok && pc >= 0 && pc <= 255 && al >= 0 && al <= 255;              // pod count <= max(pc, al)
   ok = ok && ae <= 255 && re <= 255;
+  ok = ok && ac * 100 < (1 << 30) && (am >> kNarrowMemShift) * 100 < (1 << 30);   // sweep_cm_scores32's range
   if (!ok) {
     atomicOr(bad, 1u);
     return;
   }
   const int4 mu = make_int4((int32_t)(rc | (re << 24)), (int32_t)zc, (int32_t)(rm >> kNarrowMemShift),
                             (int32_t)((zm >> kNarrowMemShift) | ((int64_t)pc << 24)));
-  if (blockIdx.y == 0) nstat[n] = make_int4((int32_t)ac, (int32_t)(am >> kNarrowMemShift), al, (int32_t)ae);
+  if (blockIdx.y == 0) {
+    nstat[n] = make_int4((int32_t)ac, (int32_t)(am >> kNarrowMemShift), al, (int32_t)ae);
+    nrcp[n] = double2{ddiv_rcp((double)(ac > 0 ? ac : 1)), ddiv_rcp((double)(am > 0 ? am >> kNarrowMemShift : 1))};
+  }
   for (int r = blockIdx.y; r < R; r += gridDim.y) nmut[(size_t)r * N + n] = mu;
 }
 
