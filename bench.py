@@ -52,6 +52,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def usable_cores() -> int:
+    """Cores this process may actually run on: the affinity mask, capped by the
+    cgroup CPU quota and by the CPU share the GPU box exports (it shows the
+    whole machine in the mask but grants 16 cores; oversubscribing them
+    measures the OS scheduler, not the port)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    share = os.environ.get("OMP_NUM_THREADS", "")   # the GPU box exports its CPU share here
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return n
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -87,7 +105,7 @@ def cpu_baseline(enc, pf, n_threads: int, budget_s: float):
 def cpu_baselines(enc, pf, budget_s: float):
     """16 threads (upstream parallelism: 16) and every host core
     this process may run on (sched_getaffinity; nproc of the machine beside it)."""
-    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    usable = usable_cores()
     out = cpu_baseline(enc, pf, 16, budget_s)
     out["cpu_model"] = cpu_model()
     out["nproc"] = os.cpu_count()
