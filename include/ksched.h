@@ -269,12 +269,15 @@ int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out);
  * node state.  Candidate k is node cand_node[k]; its potential victims (the
  * pods on it with lower priority than `pod`, most important first:
  * util.MoreImportantPod order) are vic_pod[vic_off[k] .. vic_off[k+1]).
- * Per candidate: remove every potential victim, run NodeResourcesFit for
- * `pod` (fits[k] = 0: the node cannot help), then reprieve the victims in
- * order, each staying evicted (victim[i] = 1) only if `pod` no longer fits
- * with it back.  The caller (framework.DebuggableScheduler.preempt) limits
- * preemption to preemptors whose other filters do not depend on the pods of
- * the node, so NodeResourcesFit is the only filter the dry run re-runs. */
+ * Per candidate: remove every potential victim, re-run the filters that read
+ * the node's pods for `pod` (NodeResourcesFit; PodTopologySpread and
+ * InterPodAffinity with the PreFilter counts of the candidate's domains moved
+ * by the removals, as the RemovePod / AddPod extensions move them upstream)
+ * (fits[k] = 0: the node cannot help), then reprieve the victims in order,
+ * each staying evicted (victim[i] = 1) only if `pod` no longer fits with it
+ * back.  Node-static filters are not re-run: the caller
+ * (preemption.check_scope) requires them ordered before those three.
+ * KSG_E_UNSUPPORTED when the preemptor's terms exceed the dry run's limits. */
 int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int32_t n_cand,
                         const int32_t* vic_off, const int32_t* vic_pod, int32_t* fits, uint8_t* victim);
 /* A victim's deletion: the inverse of ksg_commit (NodeInfo.RemovePod and the

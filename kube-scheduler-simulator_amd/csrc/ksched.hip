@@ -2101,6 +2101,8 @@ __global__ __launch_bounds__(256) void ksg_preempt_kernel(DevCluster c, DevState
   }
 }
 
+#include "ksched_preempt.h"
+
 }  // namespace
 
 // ============================================================================
@@ -2156,6 +2158,8 @@ struct ksg_ctx {
   // DefaultPreemption dry-run scratch (grow-only)
   int32_t* d_pre = nullptr;
   size_t pre_words = 0;
+  PreemptTopo* d_pretopo = nullptr;    // topology dry run (ksched_preempt.h)
+  ksg_profile* d_preprof = nullptr;
   // chip-wide topology path buffers (lazily allocated)
   CoopAcc* d_coop_acc = nullptr;
   unsigned* d_coop_flags = nullptr;   // [0] barrier counter, [4] timeout
@@ -2230,6 +2234,8 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_prog = nullptr;
   ctx->pod_cap = ctx->prog_cap = 0;
   ctx->d_pre = nullptr;
+  ctx->d_pretopo = nullptr;
+  ctx->d_preprof = nullptr;
   ctx->pre_words = 0;
   ctx->d_rec = nullptr;
   ctx->d_img = nullptr;
@@ -3514,13 +3520,32 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
   HIPC(ctx, hipMemcpyAsync(d_cand, cand_node, sizeof(int32_t) * n_cand, hipMemcpyHostToDevice, ctx->stream));
   HIPC(ctx, hipMemcpyAsync(d_off, vic_off, sizeof(int32_t) * (n_cand + 1), hipMemcpyHostToDevice, ctx->stream));
   if (nv) HIPC(ctx, hipMemcpyAsync(d_vic, vic_pod, sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(ksg_preempt_kernel, dim3((n_cand + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
-                     ctx->d_pods, pod, ctx->prof.fit_ignored_res, fit_on ? 1 : 0, d_cand, n_cand, d_off, d_vic,
-                     d_fits, d_victim);
+  // a preemptor whose PodTopologySpread / InterPodAffinity filter reads the
+  // node's pods: the topology dry run (ksched_preempt.h), else Fit only
+  const bool topo = needs_topo(ctx, ctx->prof, pod, 1);
+  int32_t topo_ok = 1;
+  if (topo) {
+    if (!ctx->d_pretopo) {
+      if ((rc = dalloc(ctx, &ctx->d_pretopo, 1))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_preprof, 1))) return rc;
+    }
+    HIPC(ctx, hipMemcpyAsync(ctx->d_preprof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(ksg_preempt_prepass<1024>, dim3(1), dim3(1024), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
+                       ctx->d_prog, ctx->d_preprof, pod, ctx->d_pretopo);
+    hipLaunchKernelGGL(ksg_preempt_topo, dim3((n_cand + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
+                       ctx->d_pods, ctx->d_prog, ctx->d_preprof, pod, ctx->d_pretopo, d_cand, n_cand, d_off, d_vic,
+                       d_fits, d_victim);
+    HIPC(ctx, hipMemcpyAsync(&topo_ok, &ctx->d_pretopo->ok, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  } else {
+    hipLaunchKernelGGL(ksg_preempt_kernel, dim3((n_cand + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
+                       ctx->d_pods, pod, ctx->prof.fit_ignored_res, fit_on ? 1 : 0, d_cand, n_cand, d_off, d_vic,
+                       d_fits, d_victim);
+  }
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipMemcpyAsync(fits, d_fits, sizeof(int32_t) * n_cand, hipMemcpyDeviceToHost, ctx->stream));
   if (nv) HIPC(ctx, hipMemcpyAsync(victim, d_victim, nv, hipMemcpyDeviceToHost, ctx->stream));
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  if (!topo_ok) return fail(ctx, KSG_E_UNSUPPORTED, "preemption: topology terms exceed the dry run's limits");
   return KSG_OK;
 }
 

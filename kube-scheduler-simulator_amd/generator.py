@@ -278,3 +278,40 @@ def preemption_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, s
     queue.sort(key=lambda p: -p.priority)     # PrioritySort (stable: creation order within a priority)
     pods.extend(queue)
     return nodes, pods, bound, P.default_profile()
+
+
+def preemption_topo_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, seed: int = 21):
+    """preemption_case with topology: running pods of six apps (a fifth with
+    required hostname anti-affinity against another app), queued pods of
+    higher priority with DoNotSchedule spread constraints (hostname or zone,
+    on their own app), required anti-affinity (hostname) or required affinity
+    (zone) — preemptors whose PodTopologySpread / InterPodAffinity verdicts
+    change when victims leave the node.  Four zones, small nodes."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes, pods, bound, prof = preemption_case(n_nodes=n_nodes, n_bound=n_bound, n_queue=n_queue, seed=seed)
+    apps = [f"app-{k}" for k in range(6)]
+
+    def sel(a):
+        return m.LabelSelector(match_labels=(("app", a),))
+    nb = len(bound)
+    for p in pods[:nb]:
+        p.labels = {"app": apps[int(rng.integers(len(apps)))]}
+        if rng.random() < 0.20:
+            other = apps[int(rng.integers(len(apps)))]
+            p.pod_anti_affinity_required = [m.PodAffinityTerm(sel(other), m.LABEL_HOSTNAME)]
+    for p in pods[nb:]:
+        a = apps[int(rng.integers(len(apps)))]
+        p.labels = {"app": a}
+        u = rng.random()
+        if u < 0.35:
+            p.topology_spread_constraints = [m.TopologySpreadConstraint(1, m.LABEL_HOSTNAME, m.DO_NOT_SCHEDULE, sel(a))]
+        elif u < 0.55:
+            p.topology_spread_constraints = [m.TopologySpreadConstraint(int(rng.integers(1, 3)), m.LABEL_ZONE,
+                                                                        m.DO_NOT_SCHEDULE, sel(a))]
+        elif u < 0.75:
+            other = apps[int(rng.integers(len(apps)))]
+            p.pod_anti_affinity_required = [m.PodAffinityTerm(sel(other), m.LABEL_HOSTNAME)]
+        elif u < 0.85:
+            other = apps[int(rng.integers(len(apps)))]
+            p.pod_affinity_required = [m.PodAffinityTerm(sel(other), m.LABEL_ZONE)]
+    return nodes, pods, bound, prof

@@ -30,11 +30,15 @@ steps, and where each one runs here:
    `evaluateNominatedNode`): when it passes, it is the only feasible node and
    the pod binds there without scoring.
 
-Scope (refused with NotImplementedError, never computed wrongly): the dry
-run re-runs NodeResourcesFit only, so a preemptor whose PodTopologySpread or
-InterPodAffinity filter depends on the node's pods, and profiles that order a
-node-static filter after NodeResourcesFit, are outside it.  There are no
-PodDisruptionBudgets in a snapshot, so every victim is non-violating.
+The dry run re-runs the filters that read the node's pods: NodeResourcesFit
+and, for a preemptor with hard spread constraints or required inter-pod terms
+(or matched by existing pods' anti-affinity), PodTopologySpread and
+InterPodAffinity with the PreFilter counts of the candidate's domains moved by
+the removed / reprieved pods (ksched_preempt.h; the oracles recompute the
+PreFilter state instead).  Scope (refused with NotImplementedError, never
+computed wrongly): profiles that order a node-static filter after one of those
+three.  There are no PodDisruptionBudgets in a snapshot, so every victim is
+non-violating.
 """
 from __future__ import annotations
 
@@ -131,22 +135,19 @@ def pick_one_node(cands: Sequence[Tuple[int, Sequence[m.Pod], int]]) -> int:
     return pool[0][0]
 
 
+_POD_DEPENDENT = (P.NODE_RESOURCES_FIT, P.POD_TOPOLOGY_SPREAD, P.INTER_POD_AFFINITY)
+
+
 def check_scope(prof: P.Profile, pod: m.Pod, pods: Sequence[m.Pod]) -> None:
-    """Refuse preemption the Fit-only dry run cannot decide exactly."""
+    """Refuse preemption the dry run cannot decide exactly: it re-runs the
+    filters that read the node's pods (Fit, PodTopologySpread,
+    InterPodAffinity), so every node-static filter must come before them."""
     order = prof.filter_order()
-    if P.NODE_RESOURCES_FIT in order:
-        k = order.index(P.NODE_RESOURCES_FIT)
-        late = [P.PLUGIN_NAMES[p] for p in order[k + 1:] if p in _STATIC_FILTERS]
+    first = min((order.index(p) for p in _POD_DEPENDENT if p in order), default=None)
+    if first is not None:
+        late = [P.PLUGIN_NAMES[p] for p in order[first + 1:] if p in _STATIC_FILTERS]
         if late:
-            raise NotImplementedError(f"DefaultPreemption with {late} ordered after NodeResourcesFit")
-    if P.POD_TOPOLOGY_SPREAD in order and any(c.when_unsatisfiable == "DoNotSchedule"
-                                              for c in pod.topology_spread_constraints):
-        raise NotImplementedError("DefaultPreemption for a pod with DoNotSchedule topology spread constraints")
-    if P.INTER_POD_AFFINITY in order:
-        if pod.pod_affinity_required or pod.pod_anti_affinity_required:
-            raise NotImplementedError("DefaultPreemption for a pod with required inter-pod (anti-)affinity")
-        if any(q.pod_anti_affinity_required for q in pods):
-            raise NotImplementedError("DefaultPreemption with pods carrying required anti-affinity")
+            raise NotImplementedError(f"DefaultPreemption with {late} ordered after {P.PLUGIN_NAMES[order[first]]}")
 
 
 def potential_nodes(fstatus, req=None, alloc=None) -> List[int]:

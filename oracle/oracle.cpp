@@ -783,39 +783,47 @@ void uncommit(Ctx& c, int pi, int n) {
   v.erase(std::find(v.begin(), v.end(), pi));
 }
 
-// defaultpreemption.SelectVictimsOnNode (upstream v1.32) with NodeResourcesFit
-// as the only pod-dependent filter: on a copy of the node (here: the node's
-// own columns, restored afterwards), remove every lower-priority pod, run the
-// filter, reprieve the pods most important first.
+// defaultpreemption.SelectVictimsOnNode (upstream v1.32): on the node, remove
+// every lower-priority pod, run the filters, reprieve the pods most important
+// first.  Upstream keeps the cloned PreFilter state in step with each removal
+// and re-addition through the plugins' RemovePod / AddPod extensions; here the
+// PodTopologySpread and InterPodAffinity PreFilter states are recomputed from
+// scratch on the modified cluster (the same counts, by their definition), with
+// the PreFilter Skip decisions of the original cycle.  The node's pods are
+// restored afterwards.  Node-static filters are not re-run: the caller only
+// passes nodes whose first rejection came from Fit / PTS / IPA with every
+// static filter ordered before them (preemption.check_scope).
 void select_victims(Ctx& c, int pi, int n, const int32_t* vic, int nv, int32_t& fits, uint8_t* victim) {
   const ksg_pod& p = c.pods[pi];
-  bool fit_on = false;
-  for (int k = 0; k < c.prof.n_filter; k++) fit_on |= c.prof.filter_order[k] == KSG_PL_NODE_RESOURCES_FIT;
-  fit_on = fit_on && !((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u);
-  std::vector<int64_t> save_req(c.R);
-  for (int r = 0; r < c.R; r++) save_req[r] = c.requested[(size_t)r * c.N + n];
-  const int32_t save_pc = c.pod_count[n];
-  auto remove = [&](int q) {
-    for (int r = 0; r < c.R; r++) c.requested[(size_t)r * c.N + n] -= c.pods[q].req[r];
-    c.pod_count[n] -= 1;
+  const uint32_t fskip = p.filter_skip;
+  auto on = [&](int pl) { return in_filter(c, pl) && !((fskip >> pl) & 1u); };
+  const bool fit_on = on(KSG_PL_NODE_RESOURCES_FIT);
+  const PtsProg pg = pts_prog(c, p);
+  const bool pts_on = on(KSG_PL_POD_TOPOLOGY_SPREAD) && !pg.hard.empty();
+  const IpaProg ig = ipa_prog(c, p);
+  bool ipa_on = false;
+  if (p.ipa >= 0 && on(KSG_PL_INTER_POD_AFFINITY)) ipa_on = !ipa_prefilter(c, p, ig).skip;
+  auto passes = [&]() {
+    if (fit_on && fit_filter(c, p, n) != 0) return false;
+    if (pts_on && pts_filter(c, pg, pts_prefilter(c, p, pg), n) != 0) return false;
+    if (ipa_on && ipa_filter(c, ig, ipa_prefilter(c, p, ig), n) != 0) return false;
+    return true;
   };
-  auto add = [&](int q) {
-    for (int r = 0; r < c.R; r++) c.requested[(size_t)r * c.N + n] += c.pods[q].req[r];
-    c.pod_count[n] += 1;
-  };
-  for (int i = 0; i < nv; i++) remove(vic[i]);
-  fits = (!fit_on || fit_filter(c, p, n) == 0) ? 1 : 0;
+  std::vector<int> removed;
+  for (int i = 0; i < nv; i++) { uncommit(c, vic[i], n); removed.push_back(vic[i]); }
+  fits = passes() ? 1 : 0;
   for (int i = 0; i < nv; i++) {
     victim[i] = 0;
     if (!fits) continue;
-    add(vic[i]);                                   // reprievePod
-    if (fit_on && fit_filter(c, p, n) != 0) {
-      remove(vic[i]);
+    commit(c, vic[i], n);                          // reprievePod
+    removed.erase(std::find(removed.begin(), removed.end(), vic[i]));
+    if (!passes()) {
+      uncommit(c, vic[i], n);
+      removed.push_back(vic[i]);
       victim[i] = 1;
     }
   }
-  for (int r = 0; r < c.R; r++) c.requested[(size_t)r * c.N + n] = save_req[r];
-  c.pod_count[n] = save_pc;
+  for (int q : removed) commit(c, q, n);
 }
 
 }  // namespace

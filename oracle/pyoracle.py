@@ -995,21 +995,32 @@ def preempt(pod, infos, prof: P.Profile, rec):
         return -1, []
     want = min(max(len(potential) * prof.preemption_min_candidate_pct // 100, prof.preemption_min_candidate_abs),
                len(potential))
-    _, states, skip, _, _ = pod_prefilter(pod, infos, prof)
+    _, _, skip, _, _ = pod_prefilter(pod, infos, prof)
     cands = []
     for idx in potential:
         low = _more_important_first([q for q in infos[idx].pods if q.priority < pod.priority])
         if not low:
             continue      # "No preemption victims found for incoming pod"
         trial = infos[idx].snapshot()
+
+        def trial_fits():
+            # the PreFilter state as RemovePod / AddPod leave it = recomputed on
+            # the cluster with this node's trial copy; Skip decisions unchanged
+            view = list(infos)
+            view[idx] = trial
+            _, states, skip2, _, _ = pod_prefilter(pod, view, prof)
+            # a state the removals emptied into a PreFilter Skip (InterPodAffinity
+            # with no term left to check) filters nothing: pass it
+            return run_filters(pod, trial, prof, states, skip | skip2, len(infos))[1]
+
         for q in low:
             trial.remove_pod(q)
-        if not run_filters(pod, trial, prof, states, skip, len(infos))[1]:
+        if not trial_fits():
             continue
         victims = []
         for q in low:                              # reprievePod
             trial.add_pod(q)
-            if not run_filters(pod, trial, prof, states, skip, len(infos))[1]:
+            if not trial_fits():
                 trial.remove_pod(q)
                 victims.append(q)
         if victims:

@@ -12,7 +12,9 @@
 //  1. PodEligibleToPreemptOthers (preemptionPolicy Never);
 //  2. potential nodes = Unschedulable (not UnschedulableAndUnresolvable)
 //     filter statuses, from the device's status words;
-//  3. SelectVictimsOnNode for all of them in one ksg_preempt_victims call;
+//  3. SelectVictimsOnNode for all of them in one ksg_preempt_victims call
+//     (Fit, and PodTopologySpread / InterPodAffinity with the victims'
+//     domain counts moved, for preemptors with topology terms);
 //  4. the first calculateNumCandidates candidates in node order,
 //     pickOneNodeForPreemption's criteria, lowest column on a final tie;
 //  5. prepareCandidate: delete the victims through the API (their deletion

@@ -143,11 +143,38 @@ def test_framework_run_queue_matches_single_cycles():
 
 
 def test_scope_refusals():
+    """A node-static filter ordered after a pod-dependent one is refused."""
     nodes, pods, bound, prof = _kat(100)
-    pods[-1].topology_spread_constraints = [m.TopologySpreadConstraint(1, m.LABEL_HOSTNAME, "DoNotSchedule",
-                                                                       m.LabelSelector((("x", "y"),)))]
+    names = [n for n, _ in prof.plugins]
+    i, j = names.index("TaintToleration"), names.index("NodeResourcesFit")
+    prof.plugins[i], prof.plugins[j] = prof.plugins[j], prof.plugins[i]
     with pytest.raises(NotImplementedError):
         _run_framework(_oracle_engine(), nodes, pods, bound, prof)
+
+
+def _topo_preemptors(s, pods):
+    return [pi for pi, _, _ in s.preemptions
+            if pods[pi].topology_spread_constraints or pods[pi].pod_anti_affinity_required
+            or pods[pi].pod_affinity_required]
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_topology_preemption_framework_vs_pyoracle(seed):
+    """Preemptors with DoNotSchedule spread constraints / required inter-pod
+    terms, and victims carrying required anti-affinity: the C++ oracle's dry
+    run (PreFilter state recomputed) against pyoracle's, annotation bytes
+    included."""
+    nodes, pods, bound, prof = G.preemption_topo_case(seed=seed)
+    s, placed, ann = _run_framework(_oracle_engine(), nodes, pods, bound, prof)
+    nb = len(bound)
+    ora, recs = pyoracle_annotations(nodes, pods[nb:], prof, bound=[(pods[i], nodes[n].name) for i, n in bound])
+    assert _topo_preemptors(s, pods), "no preemption by a topology-constrained pod"
+    assert [r["selected_index"] for r in recs] == placed
+    pre = [(pi - nb, s.node_names[n], [(pods[v].namespace, pods[v].name) for v in vs]) for pi, n, vs in s.preemptions]
+    ref = [(k, r["first_attempt"]["nominated"], r["first_attempt"]["victims"])
+           for k, r in enumerate(recs) if "first_attempt" in r]
+    assert pre == ref
+    assert ann == ora
 
 
 # ---- GPU: the dry run and the deletions on the device ------------------------
@@ -181,3 +208,29 @@ def test_gpu_kat_and_run_queue(built):
     req_c = s_cpu.engine.read_state(3)
     for a, b in zip(req_g, req_c):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [21, 22, 23, 24])
+def test_gpu_topology_preemption_matches_pyoracle(built, seed):
+    """The device's topology dry run (ksg_preempt_prepass + ksg_preempt_topo:
+    incremental domain counts) against pyoracle's recomputed PreFilter state."""
+    nodes, pods, bound, prof = G.preemption_topo_case(seed=seed, n_nodes=60, n_bound=260, n_queue=160)
+    s, placed, ann = _run_framework(native.Engine(device=0), nodes, pods, bound, prof)
+    nb = len(bound)
+    ora, recs = pyoracle_annotations(nodes, pods[nb:], prof, bound=[(pods[i], nodes[n].name) for i, n in bound])
+    assert _topo_preemptors(s, pods)
+    assert [r["selected_index"] for r in recs] == placed
+    assert ann == ora
+
+
+@pytest.mark.gpu
+def test_gpu_topology_preemption_victims_match_cpp_oracle(built):
+    """Victim flags of every candidate of every preemption: device vs C++ oracle."""
+    nodes, pods, bound, prof = G.preemption_topo_case(seed=25, n_nodes=80, n_bound=400, n_queue=200)
+    nb = len(bound)
+    s_gpu = F.DebuggableScheduler(nodes, pods, prof, engine=native.Engine(device=0), bound=bound)
+    s_cpu = F.DebuggableScheduler(nodes, pods, prof, engine=_oracle_engine(), bound=bound)
+    for i in range(nb, len(pods)):
+        assert s_gpu.schedule_one(i) == s_cpu.schedule_one(i), i
+    assert s_gpu.preemptions == s_cpu.preemptions and _topo_preemptors(s_gpu, pods)
