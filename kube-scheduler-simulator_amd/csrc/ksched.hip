@@ -2733,16 +2733,26 @@ bool sweep_eligible(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first,
 // mode: 0 generic arithmetic, 1 fast (Fit/BA over {cpu, memory}), 2 fast with
 // one scalar Fit column (instantiated for the spill-free shapes only);
 // narrow: the 16-byte records (fast modes only)
-template <int BLOCK, int KN, bool MULTI>
-void launch_sweep(const SweepArgs& s, int grid, int mode, bool narrow, hipStream_t st) {
-  if (mode == 1 && narrow) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, false, true>), dim3(grid), dim3(BLOCK), 0, st, s);
-  else if (mode == 1) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
-  else hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, false, MULTI>), dim3(grid), dim3(BLOCK), 0, st, s);
+// MULTI (group barriers): a cooperative launch, so the runtime guarantees the
+// co-residency of every workgroup (or refuses the launch)
+template <int BLOCK, bool MULTI>
+hipError_t launch_one(const void* f, const SweepArgs& s, int grid, hipStream_t st) {
+  void* kargs[] = {const_cast<SweepArgs*>(&s)};
+  if (MULTI) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(BLOCK), kargs, 0, st);
+  return hipLaunchKernel(f, dim3(grid), dim3(BLOCK), kargs, 0, st);
 }
 template <int BLOCK, int KN, bool MULTI>
-void launch_sweep_ex(const SweepArgs& s, int grid, bool narrow, hipStream_t st) {
-  if (narrow) hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, true, true>), dim3(grid), dim3(BLOCK), 0, st, s);
-  else hipLaunchKernelGGL((ksg_sweep<BLOCK, KN, true, MULTI, true>), dim3(grid), dim3(BLOCK), 0, st, s);
+hipError_t launch_sweep(const SweepArgs& s, int grid, int mode, bool narrow, hipStream_t st) {
+  const void* f = mode == 1 && narrow ? (const void*)ksg_sweep<BLOCK, KN, true, MULTI, false, true>
+                  : mode == 1 ? (const void*)ksg_sweep<BLOCK, KN, true, MULTI>
+                              : (const void*)ksg_sweep<BLOCK, KN, false, MULTI>;
+  return launch_one<BLOCK, MULTI>(f, s, grid, st);
+}
+template <int BLOCK, int KN, bool MULTI>
+hipError_t launch_sweep_ex(const SweepArgs& s, int grid, bool narrow, hipStream_t st) {
+  const void* f = narrow ? (const void*)ksg_sweep<BLOCK, KN, true, MULTI, true, true>
+                         : (const void*)ksg_sweep<BLOCK, KN, true, MULTI, true>;
+  return launch_one<BLOCK, MULTI>(f, s, grid, st);
 }
 
 template <int BLOCK, int KN>
@@ -2926,38 +2936,40 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     s.b0 = first + off;
     s.nb = std::min(kBatch, count - off);
     s.out0 = off;
-    hipLaunchKernelGGL(ksg_sweep_static, dim3((N + 255) / 256, s.nb), dim3(256), 0, ctx->stream, s);
+    hipLaunchKernelGGL(ksg_sweep_static, dim3(static_blocks(N, s.nb)), dim3(256), 0, ctx->stream, s);
     if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)s.nb * N))) return rc;
     if (S > 1) HIPC(ctx, hipMemsetAsync(s.gbar, 0, sizeof(unsigned) * 16 * (size_t)R, ctx->stream));
     const int grid = R * S;
     const int key = block * 100 + kn;
+    hipError_t le;
     if (mode == 2) {
       if (S > 1) {
-        if (key == 25608) launch_sweep_ex<256, 8, true>(s, grid, narrow, ctx->stream);
-        else launch_sweep_ex<256, 0, true>(s, grid, narrow, ctx->stream);
+        if (key == 25608) le = launch_sweep_ex<256, 8, true>(s, grid, narrow, ctx->stream);
+        else le = launch_sweep_ex<256, 0, true>(s, grid, narrow, ctx->stream);
       } else {
-        if (key == 25608) launch_sweep_ex<256, 8, false>(s, grid, narrow, ctx->stream);
-        else if (key == 25600) launch_sweep_ex<256, 0, false>(s, grid, narrow, ctx->stream);
-        else launch_sweep_ex<1024, 0, false>(s, grid, narrow, ctx->stream);
+        if (key == 25608) le = launch_sweep_ex<256, 8, false>(s, grid, narrow, ctx->stream);
+        else if (key == 25600) le = launch_sweep_ex<256, 0, false>(s, grid, narrow, ctx->stream);
+        else le = launch_sweep_ex<1024, 0, false>(s, grid, narrow, ctx->stream);
       }
     } else if (S > 1) {
       switch (key) {
-        case 25608: launch_sweep<256, 8, true>(s, grid, mode, narrow, ctx->stream); break;
-        default: launch_sweep<256, 0, true>(s, grid, mode, narrow, ctx->stream); break;
+        case 25608: le = launch_sweep<256, 8, true>(s, grid, mode, narrow, ctx->stream); break;
+        default: le = launch_sweep<256, 0, true>(s, grid, mode, narrow, ctx->stream); break;
       }
     } else {
       switch (key) {
-        case 25608: launch_sweep<256, 8, false>(s, grid, mode, narrow, ctx->stream); break;
-        case 25616: launch_sweep<256, 16, false>(s, grid, mode, narrow, ctx->stream); break;
-        case 25620: launch_sweep<256, 20, false>(s, grid, mode, narrow, ctx->stream); break;
-        case 25624: launch_sweep<256, 24, false>(s, grid, mode, narrow, ctx->stream); break;
-        case 25632: launch_sweep<256, 32, false>(s, grid, mode, narrow, ctx->stream); break;
-        case 51232: launch_sweep<512, 32, false>(s, grid, mode, narrow, ctx->stream); break;
-        case 102432: launch_sweep<1024, 32, false>(s, grid, mode, narrow, ctx->stream); break;
-        case 25600: launch_sweep<256, 0, false>(s, grid, mode, narrow, ctx->stream); break;
-        default: launch_sweep<1024, 0, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25608: le = launch_sweep<256, 8, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25616: le = launch_sweep<256, 16, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25620: le = launch_sweep<256, 20, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25624: le = launch_sweep<256, 24, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25632: le = launch_sweep<256, 32, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 51232: le = launch_sweep<512, 32, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 102432: le = launch_sweep<1024, 32, false>(s, grid, mode, narrow, ctx->stream); break;
+        case 25600: le = launch_sweep<256, 0, false>(s, grid, mode, narrow, ctx->stream); break;
+        default: le = launch_sweep<1024, 0, false>(s, grid, mode, narrow, ctx->stream); break;
       }
     }
+    HIPC(ctx, le);
     if ((rc = tlaunched(ctx, narrow ? KSG_K_SWEEP_NARROW : KSG_K_SWEEP, (double)R * s.nb * N))) return rc;
   }
   ctx->sweep_timeout = S > 1 ? s.timeout : nullptr;
@@ -3043,21 +3055,20 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     const int nb = std::min(kCoopBatch, count - off);
     sa.b0 = first + off;
     sa.nb = nb;
-    hipLaunchKernelGGL(ksg_sweep_static, dim3((N + 255) / 256, nb), dim3(256), 0, ctx->stream, sa);
+    hipLaunchKernelGGL(ksg_sweep_static, dim3(static_blocks(N, nb)), dim3(256), 0, ctx->stream, sa);
     if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)nb * N))) return rc;
     a.first = first + off;
     a.count = nb;
     a.out0 = off;
     HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 16, ctx->stream));   // barrier counter (timeout kept)
     HIPC(ctx, hipMemsetAsync(ctx->d_coop_acc, 0, 2 * sizeof(CoopAcc), ctx->stream));
-    switch (kn) {
-      case 1: hipLaunchKernelGGL(ksg_topo_coop<1>, dim3(G), dim3(256), 0, ctx->stream, a); break;
-      case 2: hipLaunchKernelGGL(ksg_topo_coop<2>, dim3(G), dim3(256), 0, ctx->stream, a); break;
-      case 4: hipLaunchKernelGGL(ksg_topo_coop<4>, dim3(G), dim3(256), 0, ctx->stream, a); break;
-      case 8: hipLaunchKernelGGL(ksg_topo_coop<8>, dim3(G), dim3(256), 0, ctx->stream, a); break;
-      case 16: hipLaunchKernelGGL(ksg_topo_coop<16>, dim3(G), dim3(256), 0, ctx->stream, a); break;
-      default: hipLaunchKernelGGL(ksg_topo_coop<32>, dim3(G), dim3(256), 0, ctx->stream, a); break;
-    }
+    // cooperative launch: the runtime guarantees the G workgroups are
+    // co-resident (or refuses the launch), which the grid barrier needs
+    void* kargs[] = {&a};
+    const void* kf = kn == 1 ? (const void*)ksg_topo_coop<1> : kn == 2 ? (const void*)ksg_topo_coop<2>
+                   : kn == 4 ? (const void*)ksg_topo_coop<4> : kn == 8 ? (const void*)ksg_topo_coop<8>
+                   : kn == 16 ? (const void*)ksg_topo_coop<16> : (const void*)ksg_topo_coop<32>;
+    HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));
     if ((rc = tlaunched(ctx, KSG_K_TOPO_COOP, (double)nb * N))) return rc;
   }
   HIPC(ctx, hipGetLastError());

@@ -109,21 +109,32 @@ __device__ __forceinline__ bool arrive_and_wait(unsigned* bar, unsigned* timeout
   return s_timeout == 0;
 }
 
+// 1-D grid of static_blocks(N, nb) workgroups.  XCD-aware order (MI355X guide
+// T1, speed only): workgroups b and b + 8 share an XCD, so every pod of one
+// node tile lands in the same group of 8 and the tile's static columns are
+// read from HBM once per launch and from that XCD's L2 for the other pods
+// (config 5: 64 taints + 50 images per node, ~0.5 KB, re-read by 64 pods).
+__host__ __device__ inline int static_tiles8(int N) { return ((N + 255) / 256 + 7) / 8 * 8; }
+__host__ __device__ inline int static_blocks(int N, int nb) { return static_tiles8(N) * nb; }
+
 __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
   __shared__ ksg_profile s_prof;
   const int tid = threadIdx.x;
-  const int j = blockIdx.y;
   const DevCluster& c = a.c;
   const int N = c.N;
+  const int b = blockIdx.x, w = b >> 3;
+  const int j = w % a.nb;                       // pod of the batch
+  const int tile = (w / a.nb) * 8 + (b & 7);    // node tile: same b % 8 for all its pods
+  if (tile * 256 >= N) return;
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles)[tid];
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();
   const ksg_pod& p = s_pod;
   const PodView v = make_view(c, s_prof, p, s_blob, a.prog);
-  const int n = blockIdx.x * 256 + tid;
+  const int n = tile * 256 + tid;
   if (n >= N) return;
   const GNode nd{&c, n};
   uint32_t bits = 0;
@@ -328,7 +339,8 @@ template <int BLOCK, int KN, bool FAST, bool MULTI, bool EX = false, bool NARROW
 __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) {   // 16 waves per CU
   static_assert(!NARROW || FAST, "narrow state: the fast cpu/memory arithmetic");
   constexpr int NW = BLOCK / 64;
-  constexpr int U = !FAST ? (KN == 0 ? 2 : 1) : (KN >= 20 || EX ? 2 : 4);   // nodes whose loads are in flight together
+  // nodes whose loads are in flight together (narrow: 40 B per node, room for 4)
+  constexpr int U = !FAST ? (KN == 0 ? 2 : 1) : (NARROW && KN == 0 ? 4 : (KN >= 20 || EX ? 2 : 4));
   __shared__ ksg_profile s_prof;
   __shared__ SweepPart s_part[2][NW];
   __shared__ uint64_t s_best[2][NW];
