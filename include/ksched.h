@@ -289,6 +289,12 @@ int ksg_reset_state(ksg_ctx* ctx);
 /* Timing of the last ksg_run_queue / ksg_run_replicas kernel: milliseconds
  * between HIP events recorded on the stream the kernel was launched on. */
 int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
+/* Which path the last ksg_run_queue / ksg_run_replicas took: path 1 queue
+ * kernel, 2 batched, 3 replica sweep, 4 chip-wide topology; flags: the range-
+ * checked narrow forms that ran (exact either way; for tests and reports). */
+#define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
+#define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */
+int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event
  * record per launch).  With timing on, ksg_kernel_stats() returns, per kernel

@@ -1212,6 +1212,47 @@ __device__ __forceinline__ void cm_scores(const CmProf& m, const PodHot<RM>& h, 
   ba = (int32_t)((1 - sd) * (double)100);
 }
 
+// cm_scores in 32-bit integers with memory in MiB, for runs whose ranges the
+// host and ksg_range32 checked (the N32 instances): the same quotients as the
+// int64 form (memory quantities are whole MiB; every product stays below
+// 2^30).  The row's INVM / DAC / DAM words hold the N32 decode of
+// slot_word_value: 1 / (memory MiB) and ddiv_rcp of cpu and memory MiB.
+template <int RM>
+__device__ __forceinline__ void cm_scores32(const CmProf& m, const PodHot<RM>& h,
+                                            const int64_t (&w)[SlotLayout<RM>::W], int64_t& fit, int64_t& ba) {
+  using SL = SlotLayout<RM>;
+  const int32_t ac = (int32_t)w[2 * KSG_RES_CPU], am = (int32_t)(w[2 * KSG_RES_MEM] >> 20);
+  const bool hc = ac > 0, hm = am > 0;
+  const int32_t sac = hc ? ac : 1, sam = hm ? am : 1;
+  const float ic = __int_as_float((int32_t)w[SL::INVC]), im = __int_as_float((int32_t)w[SL::INVM]);
+  const int32_t qc = (int32_t)w[SL::NZC] + (int32_t)h.nz_cpu;
+  const int32_t qm = (int32_t)(w[SL::NZM] >> 20) + (int32_t)(h.nz_mem >> 20);
+  int32_t xc, xm;
+  if (m.least) {
+    xc = qc > ac ? 0 : (ac - qc) * 100;
+    xm = qm > am ? 0 : (am - qm) * 100;
+  } else {
+    xc = (qc > ac ? ac : qc) * 100;
+    xm = (qm > am ? am : qm) * 100;
+  }
+  const int32_t sc = qdiv32(xc, sac, ic), sm = qdiv32(xm, sam, im);
+  const int32_t wc = (int32_t)m.wc, wm = (int32_t)m.wm;
+  const int32_t num = (hc ? sc * wc : 0) + (hm ? sm * wm : 0);
+  const int32_t ws = (hc ? wc : 0) + (hm ? wm : 0);
+  float iws = __builtin_amdgcn_readfirstlane(0) ? 0.0f : m.inv_wm;
+  iws = hc ? m.inv_wc : iws;
+  iws = hc && hm ? m.inv_ws : iws;
+  fit = ws == 0 ? 0 : qdiv32(num, ws, iws);
+  const int32_t nc_ = (int32_t)w[2 * KSG_RES_CPU + 1] + (int32_t)h.req[KSG_RES_CPU];
+  const int32_t nm_ = (int32_t)(w[2 * KSG_RES_MEM + 1] >> 20) + (int32_t)(h.req[KSG_RES_MEM] >> 20);
+  double fc = ddiv_r((double)nc_, (double)sac, __longlong_as_double(w[SL::DAC]));
+  double fm = ddiv_r((double)nm_, (double)sam, __longlong_as_double(w[SL::DAM]));
+  fc = fc > 1 ? 1 : fc;
+  fm = fm > 1 ? 1 : fm;
+  const double sd = hc && hm ? fabs((fc - fm) / 2) : 0.0;
+  ba = (int32_t)((1 - sd) * (double)100);
+}
+
 template <int RM>
 __device__ __forceinline__ void slot_row_cols(const int64_t (&w)[SlotLayout<RM>::W], NodeCols& L) {
   using SL = SlotLayout<RM>;
@@ -1247,18 +1288,25 @@ __device__ __forceinline__ SlotFetch<RM> slot_word_fetch(const DevCluster& c, co
   const int32_t* p32 = lane == SL::PODS ? st.pod_count + n : c.allowed + n;
   return SlotFetch<RM>{*p64, *p32};
 }
-template <int RM>
+template <int RM, bool N32 = false>
 __device__ __forceinline__ int64_t slot_word_value(const SlotFetch<RM>& f, int lane, int R) {
   using SL = SlotLayout<RM>;
   if (lane == SL::PODS || lane == SL::ALLOWED) return (int64_t)f.v32;
   if (lane < 2 * RM) return (lane >> 1) < R ? f.v64 : 0;
+  if (N32) {   // cm_scores32's words: memory in MiB, ddiv_rcp reciprocals
+    const int64_t v = lane == SL::INVM || lane == SL::DAM ? (f.v64 >> 20) : f.v64;
+    if (lane == SL::INVC || lane == SL::INVM)
+      return (int64_t)(uint32_t)__float_as_int(v > 0 ? __builtin_amdgcn_rcpf((float)v) : 1.0f);
+    if (lane == SL::DAC || lane == SL::DAM) return __double_as_longlong(ddiv_rcp((double)(v > 0 ? v : 1)));
+  }
   if (lane == SL::INVC || lane == SL::INVM)   // qdiv's estimate: v_rcp_f32 (1 ulp) is within its correction
     return (int64_t)(uint32_t)__float_as_int(f.v64 > 0 ? __builtin_amdgcn_rcpf((float)f.v64) : 1.0f);
   if (lane == SL::DAC || lane == SL::DAM) return __double_as_longlong((double)f.v64);
   return lane < SL::W ? f.v64 : 0;
 }
 
-template <int RM, int BLOCK>
+// N32: the run's ranges were checked for cm_scores32 (ksg_range32)
+template <int RM, int BLOCK, bool N32 = false>
 __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   using SL = SlotLayout<RM>;
   constexpr int NW = BLOCK / 64, SW = SL::W;
@@ -1393,7 +1441,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
       } else {
         int64_t fs = 0, bs = 0;
         if (cm.fast) {
-          cm_scores<RM>(cm, h, sw, fs, bs);
+          if constexpr (N32) cm_scores32<RM>(cm, h, sw, fs, bs);
+          else cm_scores<RM>(cm, h, sw, fs, bs);
         } else {
           NodeCols L;
           slot_row_cols<RM>(sw, L);
@@ -1402,8 +1451,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
         }
         KSG_STAMP(11);
         const int64_t part = my_img + fs * h.w_fit + bs * h.w_ba;
-        const int64_t nt = mt1 != 0 ? 100 - qdiv(100 * rt, mt1, s1.inv_mt) : 100;
-        const int64_t na = ma1 != 0 ? qdiv(100 * ra, ma1, s1.inv_ma) : ra;
+        // 100 * rt < 2^15 and 100 * ra < 2^23: qdiv32's range
+        const int64_t nt = mt1 != 0 ? 100 - qdiv32(100 * (int32_t)rt, (int32_t)mt1, s1.inv_mt) : 100;
+        const int64_t na = ma1 != 0 ? qdiv32(100 * (int32_t)ra, (int32_t)ma1, s1.inv_ma) : ra;
         my_key = argmax_key(part + nt * h.w_t + na * h.w_a, my_node);
         cnt += 1u << 8;
         live = pack_rec(part, rt, ra);
@@ -1434,7 +1484,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
       }
     }
     KSG_STAMP(2);
-    __syncthreads();
+    lds_barrier();   // X2's loads stay in flight into Y (consumed at the assume)
 
     // ---- Y: decide (every wave, identically) -------------------------------
     uint64_t k0 = 0, bu = bu_key;
@@ -1561,7 +1611,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     }
     if (tid < K1) s_top[tid] = nx_top;
     KSG_STAMP(6);
-    const int64_t col_val = slot_word_value<RM>(col, lane, R);
+    const int64_t col_val = slot_word_value<RM, N32>(col, lane, R);
     KSG_STAMP(7);
     if (wv == 0 && selected >= 0) {
       const int slot = added ? nc : idx;
@@ -1598,7 +1648,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     }
     nc += added ? 1 : 0;
     KSG_STAMP(4);
-    __syncthreads();
+    lds_barrier();   // the count-table stores (wave 0, lane 0) need no drain: no lane reads them
     KSG_STAMP(5);
   }
   // No store is on the per-pod path: nothing in the walk reads a changed
@@ -2103,6 +2153,29 @@ __global__ __launch_bounds__(256) void ksg_preempt_kernel(DevCluster c, DevState
 
 #include "ksched_preempt.h"
 
+// Node half of the N32 check (range32_candidate): every value cm_scores32
+// will see for any pod of the run stays inside its 32-bit range; the requested
+// sums are bounded by max(current, allocatable) (the Fit filter) and the
+// non-zero sums by current + allocatable + (placeable pods + 1) x the pods'
+// non-zero excess.  Any failure sets *bad (the int64 instances run).
+__global__ __launch_bounds__(256) void ksg_range32(DevCluster c, DevState st, int64_t xc, int64_t xm, int32_t count,
+                                                   unsigned* bad) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int N = c.N;
+  if (n >= N) return;
+  const size_t NN = N;
+  constexpr int64_t kMiB = (int64_t)1 << 20, k30 = (int64_t)1 << 30, k31 = ((int64_t)1 << 31) - 1;
+  const int64_t ac = c.alloc[KSG_RES_CPU * NN + n], am = c.alloc[KSG_RES_MEM * NN + n];
+  const int64_t rc = st.requested[KSG_RES_CPU * NN + n], rm = st.requested[KSG_RES_MEM * NN + n];
+  const int64_t zc = st.nonzero[n], zm = st.nonzero[NN + n];
+  const int64_t places = (int64_t)max(0, min(count, c.allowed[n] - st.pod_count[n])) + 1;
+  bool ok = ac >= 0 && am >= 0 && rc >= 0 && rm >= 0 && zc >= 0 && zm >= 0;
+  ok = ok && ((am | rm | zm) & (kMiB - 1)) == 0;
+  ok = ok && ac * 100 < k30 && (am >> 20) * 100 < k30 && rc <= k31 && (rm >> 20) <= k31;
+  ok = ok && zc + ac + places * xc <= k31 && (zm >> 20) + (am >> 20) + places * xm <= k31;
+  if (!ok) atomicOr(bad, 1u);
+}
+
 }  // namespace
 
 // ============================================================================
@@ -2171,6 +2244,8 @@ struct ksg_ctx {
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched, 3 int64 sweep state
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
+  bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
+  unsigned* d_flag = nullptr; // range-check flag (ksg_range32)
   // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default), 3 "pipe"
   // (the pipelined phase 2 is exact but measured slower than slot:
   // profiles/r2/phase2_modes.log)
@@ -2235,6 +2310,7 @@ void free_all(ksg_ctx* ctx) {
   ctx->pod_cap = ctx->prog_cap = 0;
   ctx->d_pre = nullptr;
   ctx->d_pretopo = nullptr;
+  ctx->d_flag = nullptr;
   ctx->d_preprof = nullptr;
   ctx->pre_words = 0;
   ctx->d_rec = nullptr;
@@ -2452,12 +2528,42 @@ struct Tmp {
   } while (0)
 
 // ksg_batch_phase2s instances: (RM 4 | KSG_MAX_RES) x (64 | 128 | 256 lanes)
-static const std::array<const void*, 6>& slot_kernels() {
-  static const std::array<const void*, 6> k = {
+static const std::array<const void*, 9>& slot_kernels() {
+  static const std::array<const void*, 9> k = {
       (const void*)ksg_batch_phase2s<4, 64>,           (const void*)ksg_batch_phase2s<4, 128>,
       (const void*)ksg_batch_phase2s<4, 256>,          (const void*)ksg_batch_phase2s<KSG_MAX_RES, 64>,
-      (const void*)ksg_batch_phase2s<KSG_MAX_RES, 128>, (const void*)ksg_batch_phase2s<KSG_MAX_RES, 256>};
+      (const void*)ksg_batch_phase2s<KSG_MAX_RES, 128>, (const void*)ksg_batch_phase2s<KSG_MAX_RES, 256>,
+      (const void*)ksg_batch_phase2s<4, 64, true>,     (const void*)ksg_batch_phase2s<4, 128, true>,
+      (const void*)ksg_batch_phase2s<4, 256, true>};
   return k;
+}
+
+bool profile_cm_fast(const ksg_profile& prof);
+
+// Host half of the N32 check for a batched run of pods [first, first + count)
+// (the node half is ksg_range32): the profile scores Fit / BalancedAllocation
+// over exactly {cpu, memory} and filters with Fit for every pod (so the Fit
+// filter bounds every requested sum by the allocatable), the pods' memory
+// quantities are whole MiB and their cpu fits 30 bits, Fit's weights keep
+// the weighted numerator below 2^30.  Fills the pods' non-zero excess bounds.
+bool range32_candidate(ksg_ctx* ctx, int first, int count, int64_t* xc, int64_t* xm) {
+  const ksg_profile& prof = ctx->prof;
+  if (!profile_cm_fast(prof) || ctx->c.R > 4 || ctx->force_path == 3) return false;
+  bool fit = false;
+  for (int k = 0; k < prof.n_filter; k++) fit |= prof.filter_order[k] == KSG_PL_NODE_RESOURCES_FIT;
+  if (!fit || (prof.fit_w[0] + prof.fit_w[1]) * 100 >= (1 << 30)) return false;
+  constexpr int64_t kMiB = 1 << 20;
+  *xc = *xm = 0;
+  for (int i = first; i < first + count; i++) {
+    const ksg_pod& p = ctx->h_pods[i];
+    if ((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) return false;
+    const int64_t rc = p.req[KSG_RES_CPU], rm = p.req[KSG_RES_MEM];
+    if (rc < 0 || rm < 0 || p.nz_cpu < 0 || p.nz_mem < 0 || ((rm | p.nz_mem) & (kMiB - 1))) return false;
+    if (rc >= (1 << 30) || p.nz_cpu >= (1 << 30) || (rm >> 20) >= (1 << 30) || (p.nz_mem >> 20) >= (1 << 30)) return false;
+    *xc = std::max(*xc, p.nz_cpu - rc);
+    *xm = std::max(*xm, (p.nz_mem - rm) >> 20);
+  }
+  return true;
 }
 
 int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const CapArgs* cap,
@@ -2511,6 +2617,24 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
       HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
     attr_set = true;
   }
+  // 32-bit Fit / BalancedAllocation in the slot walk when the ranges allow (one
+  // small check launch + a 4-byte read per call)
+  bool n32 = false;
+  int64_t n32_xc = 0, n32_xm = 0;
+  if (ctx->batch_mode == 2 && slot_rm == 4 && range32_candidate(ctx, first, count, &n32_xc, &n32_xm)) {
+    if (!ctx->d_flag) {
+      int rc;
+      if ((rc = dalloc(ctx, &ctx->d_flag, 4))) return rc;
+    }
+    HIPC(ctx, hipMemsetAsync(ctx->d_flag, 0, 16, ctx->stream));
+    hipLaunchKernelGGL(ksg_range32, dim3((N + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st, n32_xc, n32_xm,
+                       count, ctx->d_flag);
+    unsigned bad = 0;
+    HIPC(ctx, hipMemcpyAsync(&bad, ctx->d_flag, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(ctx, hipStreamSynchronize(ctx->stream));
+    n32 = bad == 0;
+  }
+  ctx->last_n32 = n32;
   (void)hipGetLastError();
   treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
@@ -2547,7 +2671,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
       if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
       // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
       if (ctx->batch_mode == 2) {
-        const int si = (slot_rm == 4 ? 0 : 3) + (ctx->slot_block == 64 ? 0 : ctx->slot_block == 128 ? 1 : 2);
+        const int si = (n32 ? 6 : slot_rm == 4 ? 0 : 3) + (ctx->slot_block == 64 ? 0 : ctx->slot_block == 128 ? 1 : 2);
         hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(slot_kernels()[si])), dim3(1),
                            dim3(ctx->slot_block), bytes, ctx->stream, b);
         if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2S, 0.5 * b.nb * (b.nb + 1)))) return trc;
@@ -3758,6 +3882,13 @@ int ksg_kernel_stats(ksg_ctx* ctx, ksg_kernel_stat* out, int32_t max, int32_t* n
     k++;
   }
   *n = k;
+  return KSG_OK;
+}
+
+int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
+  if (!ctx || !path || !flags) return KSG_E_INVALID;
+  *path = ctx->last_path;
+  *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0);
   return KSG_OK;
 }
 

@@ -81,6 +81,12 @@ struct OpAdd32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { 
 struct OpMin32 { __device__ int32_t operator()(int32_t a, int32_t b) const { return a < b ? a : b; } };
 struct OpOr32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
 
+// Workgroup barrier for LDS-only handoffs: waits for this wave's LDS traffic
+// (lgkmcnt) but not for its global loads, which __syncthreads would drain
+// (vmcnt(0)); for walks that keep the next step's global loads in flight
+// across the barrier and read no global memory another wave wrote.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Per-pod values every lane needs, derived once from the LDS copy of the pod.
 struct PodView {
   const ksg_pod* p;

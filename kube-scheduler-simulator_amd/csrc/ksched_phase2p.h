@@ -43,7 +43,7 @@
 // global load (vmcnt(0)), which would expose the latency of the loads this
 // kernel keeps in flight across steps (records two pods ahead, the next top
 // set); nothing here reads global memory another wave of the workgroup wrote.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// lds_barrier(): ksched_kernels.h
 
 template <int RM>
 struct P2Cand {

@@ -149,6 +149,9 @@ def make_profile(fields: dict) -> KsgProfile:
     return p
 
 
+RUN_NARROW_SWEEP, RUN_SLOT32 = 1, 2   # ksg_last_run_info flags
+
+
 class CaptureBuffers:
     """Host buffers for `count` pods of capture output."""
 
@@ -222,6 +225,7 @@ class Engine:
         self._eval_pod = f("eval_pod", C.c_int, vp, vp, i32p, C.c_int64, C.POINTER(KsgResult),
                            C.POINTER(KsgCapture))
         self._last_ms = f("last_kernel_ms", C.c_int, vp, C.POINTER(C.c_double))
+        self._run_info = f("last_run_info", C.c_int, vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32))
         self._set_timing = f("set_timing", C.c_int, vp, C.c_int)
         self._kernel_stats = f("kernel_stats", C.c_int, vp, C.POINTER(KsgKernelStat), C.c_int32,
                                C.POINTER(C.c_int32))
@@ -341,6 +345,14 @@ class Engine:
             out.append({"name": k.name.decode(), "calls": k.calls, "total_ms": k.total_ms,
                         "avg_ms": k.total_ms / max(k.calls, 1), "units": k.units})
         return out
+
+    def last_run_info(self):
+        """(path, flags) of the last run (ksg_last_run_info): path 1 queue
+        kernel, 2 batched, 3 replica sweep, 4 chip-wide topology; flags
+        RUN_NARROW_SWEEP / RUN_SLOT32."""
+        p, fl = C.c_int32(), C.c_int32()
+        self._check(self._run_info(self.ctx, C.byref(p), C.byref(fl)))
+        return p.value, fl.value
 
     def last_kernel_ms(self) -> float:
         v = C.c_double()

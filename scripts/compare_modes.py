@@ -19,7 +19,9 @@ native = importlib.import_module("kube-scheduler-simulator_amd.native")
 
 MODES = [("pipe", {"KSG_BATCH_MODE": "pipe"}), ("pipe-nowindow", {"KSG_BATCH_MODE": "pipe", "KSG_PIPE_WINDOW": "0"}),
          ("pipe-nowindow-64", {"KSG_BATCH_MODE": "pipe", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"}),
-         ("pipe-64", {"KSG_BATCH_MODE": "pipe", "KSG_SLOT_BLOCK": "64"}), ("slot", {"KSG_BATCH_MODE": "slot"})]
+         ("pipe-64", {"KSG_BATCH_MODE": "pipe", "KSG_SLOT_BLOCK": "64"}), ("slot", {"KSG_BATCH_MODE": "slot"}),
+         ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
+         ("slot-256", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "256"})]
 
 
 def main():

@@ -77,3 +77,41 @@ def test_variant_placements_match_oracle(variant, oracle, name, make):
 
 def test_variant_full_config2(variant, oracle):
     _check(variant, oracle, *G.config2(), split=False)
+
+
+# ---- the 32-bit slot walk (KSG_RUN_SLOT32) ------------------------------------
+native = pkg("native")
+
+
+def test_slot32_runs_and_matches_int64(oracle):
+    """Config 2 takes the 32-bit Fit / BalancedAllocation instances (memory in
+    MiB, range-checked); the int64 instances (KSG_FORCE_PATH=3) and the oracle
+    agree with it bit for bit."""
+    nodes, pods, prof = G.config2(n_nodes=2000, n_pods=3000, seed=9)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = _engine_with_batch_mode("slot")
+    b = _engine_with_batch_mode("slot", KSG_FORCE_PATH=3)
+    out = []
+    for eng in (a, b, oracle):
+        eng.load(enc, pf)
+        out.append(eng.run_queue(0, len(pods)))
+    assert a.last_run_info() == (2, native.RUN_SLOT32)
+    assert b.last_run_info() == (2, 0)
+    for pl, res in out[1:]:
+        np.testing.assert_array_equal(out[0][0], pl)
+        for f in ("n_feasible", "status", "score_skip"):
+            np.testing.assert_array_equal(out[0][1][f], res[f], err_msg=f)
+
+
+def test_slot32_refused_on_sub_mib_memory(oracle):
+    nodes, pods, prof = G.config2(n_nodes=300, n_pods=400, seed=9)
+    nodes[3].allocatable["memory"] += 4096
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = _engine_with_batch_mode("slot")
+    a.load(enc, pf)
+    oracle.load(enc, pf)
+    pl, _ = a.run_queue(0, len(pods))
+    assert a.last_run_info() == (2, 0)
+    np.testing.assert_array_equal(pl, oracle.run_queue(0, len(pods))[0])
