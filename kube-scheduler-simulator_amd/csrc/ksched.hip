@@ -1274,18 +1274,22 @@ struct SlotFetch {
   int64_t v64;
   int32_t v32;
 };
-template <int RM>
+template <int RM, bool N32 = false>
 __device__ __forceinline__ SlotFetch<RM> slot_word_fetch(const DevCluster& c, const DevState& st, int lane, int R,
                                                           int n) {
   using SL = SlotLayout<RM>;
   const size_t N = c.N;
   const int r = lane >> 1;
   const int64_t* p64 = c.alloc + n;   // harmless default
+  const int32_t* p32 = lane == SL::PODS ? st.pod_count + n : c.allowed + n;
   if (lane < 2 * RM && r < R) p64 = ((lane & 1) ? st.requested : c.alloc) + (size_t)r * N + n;
   else if (lane == SL::NZC || lane == SL::NZM) p64 = st.nonzero + (size_t)(lane - SL::NZC) * N + n;
+  else if (N32 && (lane == SL::DAC || lane == SL::DAM))   // the per-node reciprocals, no decode
+    p64 = reinterpret_cast<const int64_t*>(c.rcp64) + 2 * (size_t)n + (lane == SL::DAM);
   else if (lane == SL::INVC || lane == SL::DAC) p64 = c.alloc + (size_t)KSG_RES_CPU * N + n;
   else if (lane == SL::INVM || lane == SL::DAM) p64 = c.alloc + (size_t)KSG_RES_MEM * N + n;
-  const int32_t* p32 = lane == SL::PODS ? st.pod_count + n : c.allowed + n;
+  if (N32 && (lane == SL::INVC || lane == SL::INVM))
+    p32 = reinterpret_cast<const int32_t*>(c.rcp32) + 2 * (size_t)n + (lane == SL::INVM);
   return SlotFetch<RM>{*p64, *p32};
 }
 template <int RM, bool N32 = false>
@@ -1293,11 +1297,9 @@ __device__ __forceinline__ int64_t slot_word_value(const SlotFetch<RM>& f, int l
   using SL = SlotLayout<RM>;
   if (lane == SL::PODS || lane == SL::ALLOWED) return (int64_t)f.v32;
   if (lane < 2 * RM) return (lane >> 1) < R ? f.v64 : 0;
-  if (N32) {   // cm_scores32's words: memory in MiB, ddiv_rcp reciprocals
-    const int64_t v = lane == SL::INVM || lane == SL::DAM ? (f.v64 >> 20) : f.v64;
-    if (lane == SL::INVC || lane == SL::INVM)
-      return (int64_t)(uint32_t)__float_as_int(v > 0 ? __builtin_amdgcn_rcpf((float)v) : 1.0f);
-    if (lane == SL::DAC || lane == SL::DAM) return __double_as_longlong(ddiv_rcp((double)(v > 0 ? v : 1)));
+  if (N32) {   // cm_scores32's words: DevCluster::rcp32 / rcp64 as fetched
+    if (lane == SL::INVC || lane == SL::INVM) return (int64_t)(uint32_t)f.v32;
+    if (lane == SL::DAC || lane == SL::DAM) return f.v64;
   }
   if (lane == SL::INVC || lane == SL::INVM)   // qdiv's estimate: v_rcp_f32 (1 ulp) is within its correction
     return (int64_t)(uint32_t)__float_as_int(f.v64 > 0 ? __builtin_amdgcn_rcpf((float)f.v64) : 1.0f);
@@ -1413,7 +1415,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     uint64_t nx_rec = a.rec[(size_t)jn * N + nn];
     int32_t nx_img = a.img[(size_t)jn * N + nn];
     uint64_t nx_top = a.top[(size_t)jn * KSG_BATCH_MAX + tid];
-    SlotFetch<RM> col = slot_word_fetch<RM>(c, a.st, lane, R, spec >= 0 ? spec : 0);
+    SlotFetch<RM> col = slot_word_fetch<RM, N32>(c, a.st, lane, R, spec >= 0 ? spec : 0);
     KSG_STAMP(1);
 
     // ---- X3: my changed node on its live slot ---------------------------------
@@ -1596,7 +1598,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     // ---- Y: assume ----------------------------------------------------------
     const bool added = selected >= 0 && idx < 0;
     if (added && selected != spec) {   // speculation missed: dependent loads
-      if (wv == 0) col = slot_word_fetch<RM>(c, a.st, lane, R, selected);
+      if (wv == 0) col = slot_word_fetch<RM, N32>(c, a.st, lane, R, selected);
       if (tid == nc) {
         nx_rec = a.rec[(size_t)jn * N + selected];
         nx_img = a.img[(size_t)jn * N + selected];
@@ -2152,6 +2154,16 @@ __global__ __launch_bounds__(256) void ksg_preempt_kernel(DevCluster c, DevState
 }
 
 #include "ksched_preempt.h"
+
+// DevCluster::rcp32 / rcp64 from the allocatable (static: once per load).
+__global__ __launch_bounds__(256) void ksg_node_rcp(DevCluster c, float2* r32, double2* r64) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= c.N) return;
+  const int64_t ac = c.alloc[(size_t)KSG_RES_CPU * c.N + n], am = c.alloc[(size_t)KSG_RES_MEM * c.N + n] >> 20;
+  const int64_t sc = ac > 0 ? ac : 1, sm = am > 0 ? am : 1;
+  r32[n] = float2{__builtin_amdgcn_rcpf((float)sc), __builtin_amdgcn_rcpf((float)sm)};
+  r64[n] = double2{ddiv_rcp((double)sc), ddiv_rcp((double)sm)};
+}
 
 // Node half of the N32 check (range32_candidate): every value cm_scores32
 // will see for any pod of the run stays inside its 32-bit range; the requested
@@ -3000,7 +3012,7 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   s.count = count;
   s.placements = d_pl;
   s.nstat = nstat;
-  s.nrcp = nrcp;
+  s.nrcp = nrcp;   // DevCluster::rcp64 on the narrow path
   s.nmut = nmut;
   s.nx = nx;
   TA(tmp, &s.srec, sizeof(uint64_t) * (size_t)kBatch * N);
@@ -3477,6 +3489,18 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
   UP(taints, nd->taints, (size_t)c.T * N);
   UP(taint_effect, nd->taint_effect, (size_t)std::max(c.V, 1));
   UP(images, nd->images, (size_t)c.I * N);
+  {
+    float2* r32;
+    double2* r64;
+    if ((rc = dalloc(ctx, &r32, N))) return rc;
+    if ((rc = dalloc(ctx, &r64, N))) return rc;
+    c.rcp32 = r32;
+    c.rcp64 = r64;
+    if (R > KSG_RES_MEM && N > 0) {
+      hipLaunchKernelGGL(ksg_node_rcp, dim3((N + 255) / 256), dim3(256), 0, ctx->stream, c, r32, r64);
+      HIPC(ctx, hipGetLastError());
+    }
+  }
   c.S = tp->n_selectors;
   c.n_tmpl = tp->n_templates;
   const int nt = std::max(tp->n_templates, 1);
@@ -3710,22 +3734,22 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   // ksg_narrow_init: nodes), else the int64 columns
   int4* nstat = nullptr;
   int4* nmut = nullptr;
-  double2* nrcp = nullptr;
+  const double2* nrcp = nullptr;
   NarrowBounds nb{};
   if (sweep && narrow_candidate(ctx, profiles, (int)RR, first, count, sweep_mode(profiles, (int)RR), &nb)) {
     unsigned* d_bad;
     TA(tmp, &nstat, sizeof(int4) * N);
-    TA(tmp, &nrcp, sizeof(double2) * N);
     TA(tmp, &nmut, sizeof(int4) * RR * N);
     TA(tmp, &d_bad, 16);
     HIPC(ctx, hipMemsetAsync(d_bad, 0, 16, ctx->stream));
     hipLaunchKernelGGL(ksg_narrow_init, dim3((unsigned)((N + 255) / 256), (unsigned)std::min<size_t>(RR, 64)), dim3(256),
-                       0, ctx->stream, ctx->c, ctx->st, nstat, nrcp, nmut, (int)RR, nb, d_bad);
+                       0, ctx->stream, ctx->c, ctx->st, nstat, nmut, (int)RR, nb, d_bad);
     HIPC(ctx, hipGetLastError());
     unsigned bad = 0;
     HIPC(ctx, hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
     HIPC(ctx, hipStreamSynchronize(ctx->stream));
     if (bad) nstat = nullptr, nmut = nullptr;
+    else nrcp = ctx->c.rcp64;
   }
   ctx->last_narrow = nstat != nullptr;
   // the sweep reads and writes only the Fit columns; the queue kernels also

@@ -33,6 +33,11 @@ struct DevCluster {
   const uint32_t* taints;          // [T][N]
   const uint8_t* taint_effect;     // [V]
   const uint32_t* images;          // [I][N]
+  // per-node reciprocals of the cpu and memory allocatable (memory in MiB; 1
+  // for a zero column), for the 32-bit Fit / BalancedAllocation forms:
+  // v_rcp_f32 estimates for qdiv32 and ddiv_rcp for float64 ddiv_r
+  const float2* rcp32;             // [N]
+  const double2* rcp64;            // [N]
   // topology
   int32_t S, n_tmpl;
   const int32_t* tmpl_col;

@@ -61,7 +61,7 @@ struct SweepArgs {
   // nx << 24), non-zero cpu milli, requested memory MiB, non-zero memory MiB
   // (24 bits) | pod count << 24}
   const int4* nstat;            // [N]
-  const double2* nrcp;          // [N] ddiv_rcp of the cpu / memory allocatable (1 when 0)
+  const double2* nrcp;          // [N] ddiv_rcp of the cpu / memory MiB allocatable (DevCluster::rcp64)
   int4* nmut;                   // [R][N]
   int32_t nx;                   // EX: the one scalar column any pod of the run requests
 };
@@ -693,8 +693,8 @@ struct NarrowBounds {
 // from the context's state): one static record per node, the mutable record
 // broadcast.  A node outside the ranges sets *bad; the host then runs the
 // int64 instances instead (nothing here writes the context's state).
-__global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st, int4* nstat, double2* nrcp,
-                                                       int4* nmut, int R, NarrowBounds b, unsigned* bad) {
+__global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st, int4* nstat, int4* nmut, int R,
+                                                       NarrowBounds b, unsigned* bad) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int N = c.N;
   if (n >= N) return;
@@ -722,10 +722,7 @@ __global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st
   }
   const int4 mu = make_int4((int32_t)(rc | (re << 24)), (int32_t)zc, (int32_t)(rm >> kNarrowMemShift),
                             (int32_t)((zm >> kNarrowMemShift) | ((int64_t)pc << 24)));
-  if (blockIdx.y == 0) {
-    nstat[n] = make_int4((int32_t)ac, (int32_t)(am >> kNarrowMemShift), al, (int32_t)ae);
-    nrcp[n] = double2{ddiv_rcp((double)(ac > 0 ? ac : 1)), ddiv_rcp((double)(am > 0 ? am >> kNarrowMemShift : 1))};
-  }
+  if (blockIdx.y == 0) nstat[n] = make_int4((int32_t)ac, (int32_t)(am >> kNarrowMemShift), al, (int32_t)ae);
   for (int r = blockIdx.y; r < R; r += gridDim.y) nmut[(size_t)r * N + n] = mu;
 }
 
