@@ -1274,6 +1274,39 @@ struct SlotFetch {
   int64_t v64;
   int32_t v32;
 };
+// The addresses slot_word_fetch selects, reduced once per walk to a lane
+// base plus a per-node step (1 or 2 words), so a fetch is one multiply-add
+// per pointer instead of the per-lane selects.
+struct SlotPlan {
+  const int64_t* b64;
+  const int32_t* b32;
+  int s64, s32;
+};
+template <int RM, bool N32 = false>
+__device__ __forceinline__ SlotPlan slot_plan(const DevCluster& c, const DevState& st, int lane, int R) {
+  using SL = SlotLayout<RM>;
+  const size_t N = c.N;
+  const int r = lane >> 1;
+  SlotPlan q{c.alloc, c.allowed, 1, 1};
+  if (lane == SL::PODS) q.b32 = st.pod_count;
+  if (lane < 2 * RM && r < R) q.b64 = ((lane & 1) ? st.requested : c.alloc) + (size_t)r * N;
+  else if (lane == SL::NZC || lane == SL::NZM) q.b64 = st.nonzero + (size_t)(lane - SL::NZC) * N;
+  else if (N32 && (lane == SL::DAC || lane == SL::DAM)) {
+    q.b64 = reinterpret_cast<const int64_t*>(c.rcp64) + (lane == SL::DAM);
+    q.s64 = 2;
+  } else if (lane == SL::INVC || lane == SL::DAC) q.b64 = c.alloc + (size_t)KSG_RES_CPU * N;
+  else if (lane == SL::INVM || lane == SL::DAM) q.b64 = c.alloc + (size_t)KSG_RES_MEM * N;
+  if (N32 && (lane == SL::INVC || lane == SL::INVM)) {
+    q.b32 = reinterpret_cast<const int32_t*>(c.rcp32) + (lane == SL::INVM);
+    q.s32 = 2;
+  }
+  return q;
+}
+template <int RM>
+__device__ __forceinline__ SlotFetch<RM> slot_plan_fetch(const SlotPlan& q, int n) {
+  return SlotFetch<RM>{q.b64[(size_t)n * q.s64], q.b32[(size_t)n * q.s32]};
+}
+
 template <int RM, bool N32 = false>
 __device__ __forceinline__ SlotFetch<RM> slot_word_fetch(const DevCluster& c, const DevState& st, int lane, int R,
                                                           int n) {
@@ -1348,6 +1381,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   const CmProf cm = cm_prof(s_prof);
   const bool ipa_filter = ipa_in_filter(s_prof);
   const bool ipa_score = ((s_prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) != 0;
+  const SlotPlan plan = slot_plan<RM, N32>(c, a.st, lane, R);
 
   auto changed = [&](int n) { return ((s_cmask[n >> 5] >> (n & 31)) & 1u) != 0; };
   int nc = 0;                  // |C|, block-uniform
@@ -1415,7 +1449,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     uint64_t nx_rec = a.rec[(size_t)jn * N + nn];
     int32_t nx_img = a.img[(size_t)jn * N + nn];
     uint64_t nx_top = a.top[(size_t)jn * KSG_BATCH_MAX + tid];
-    SlotFetch<RM> col = slot_word_fetch<RM, N32>(c, a.st, lane, R, spec >= 0 ? spec : 0);
+    SlotFetch<RM> col = slot_plan_fetch<RM>(plan, spec >= 0 ? spec : 0);
     KSG_STAMP(1);
 
     // ---- X3: my changed node on its live slot ---------------------------------
@@ -1598,7 +1632,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     // ---- Y: assume ----------------------------------------------------------
     const bool added = selected >= 0 && idx < 0;
     if (added && selected != spec) {   // speculation missed: dependent loads
-      if (wv == 0) col = slot_word_fetch<RM, N32>(c, a.st, lane, R, selected);
+      if (wv == 0) col = slot_plan_fetch<RM>(plan, selected);
       if (tid == nc) {
         nx_rec = a.rec[(size_t)jn * N + selected];
         nx_img = a.img[(size_t)jn * N + selected];
