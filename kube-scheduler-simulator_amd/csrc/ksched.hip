@@ -1355,6 +1355,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   __shared__ P2Part s_part[NW];
   __shared__ WRed s_w[NW];
   __shared__ ksg_result s_res[KSG_BATCH_MAX];  // per-pod results, stored after the walk
+  __shared__ uint8_t s_touched[KSG_BATCH_MAX];  // two-batch window: slot assumed onto in this batch
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const DevCluster& c = a.c;
@@ -1388,6 +1389,29 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   int my_node = 0;             // node of slot tid (tid < nc)
   uint64_t my_rec = 0;         // pod j's phase-1 record at my_node
   int32_t my_img = 0;
+  // Two-batch window (run_pipe with the slot walk): this batch's phase 1 saw
+  // the state before the previous batch's assumes, so the nodes the previous
+  // batch touched start as changed slots with their live rows.  Their phase-1
+  // records stay usable: an assume only ever removes capacity, so a record
+  // that says infeasible stays infeasible, and everything else about the node
+  // is re-evaluated on the row (the top sets hold k_extra = |carry| more keys).
+  if (a.carry) {
+    nc = *a.carry_n;
+    for (int t = tid; t < nc * SW; t += BLOCK) {
+      const int i = t / SW, w = t - i * SW;
+      const SlotFetch<RM> f = slot_word_fetch<RM, N32>(c, a.st, w, R, a.carry[i]);
+      s_slot[(size_t)i * SL::STRIDE + w] = slot_word_value<RM, N32>(f, w, R);
+    }
+    if (tid < nc) {
+      my_node = a.carry[tid];
+      s_clist[tid] = my_node;
+      atomicOr(&s_cmask[my_node >> 5], 1u << (my_node & 31));
+      my_rec = a.rec[my_node];
+      my_img = a.img[my_node];
+    }
+  }
+  if (tid < KSG_BATCH_MAX) s_touched[tid] = 0;
+  __syncthreads();
 #ifdef KSG_STAMPS
   unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -1672,6 +1696,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
         s_cmask[selected >> 5] |= 1u << (selected & 31);
         s_clist[nc] = selected;
       }
+      if (lane == 0 && a.carry_out) s_touched[slot] = 1;
     }
     if (tid == 0) {
       const bool sc = (status & KSG_ST_SCORED) != 0;
@@ -1702,6 +1727,20 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     if (a.results) a.results[a.out0 + i] = s_res[i];
   }
   for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
+  if (a.carry_out) {   // the nodes this batch touched, in slot order, for the next batch
+    const bool t = tid < nc && s_touched[tid];
+    const uint64_t m = __ballot(t);
+    if (lane == 0) s_part[wv].cnt = (uint32_t)__popcll(m);
+    __syncthreads();
+    int base = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      base += i < wv ? (int)s_part[i].cnt : 0;
+      total += (int)s_part[i].cnt;
+    }
+    if (t) a.carry_out[base + __popcll(m & ((1ull << lane) - 1))] = s_clist[tid];
+    if (tid == 0) *a.carry_out_n = total;
+  }
 #ifdef KSG_STAMPS
   if (tid == 0 && a.stamps)
     for (int i = 0; i < 16; i++) atomicAdd(&a.stamps[i], st_acc[i]);
@@ -2292,10 +2331,11 @@ struct ksg_ctx {
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   unsigned* d_flag = nullptr; // range-check flag (ksg_range32)
-  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot" (default), 3 "pipe"
-  // (the pipelined phase 2 is exact but measured slower than slot:
-  // profiles/r2/phase2_modes.log)
-  int batch_mode = 2;
+  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 3 "pipe", 4 "window"
+  // (default: the slot walk with the next batch's phase 1 + top-k overlapped
+  // through the two-batch window; the pipelined two-version walk is exact but
+  // measured slower: profiles/r2/phase2_modes.log)
+  int batch_mode = 4;
   int slot_block = 128;  // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (128: 1-2 % faster end to end than 256)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
@@ -2612,9 +2652,46 @@ bool range32_candidate(ksg_ctx* ctx, int first, int count, int64_t* xc, int64_t*
   return true;
 }
 
+// 32-bit Fit / BalancedAllocation in the slot walk when the ranges allow (one
+// small check launch + a 4-byte read per call).
+int decide_n32(ksg_ctx* ctx, int32_t first, int32_t count, bool* n32) {
+  *n32 = false;
+  int64_t xc = 0, xm = 0;
+  if (ctx->c.R <= 4 && range32_candidate(ctx, first, count, &xc, &xm)) {
+    if (!ctx->d_flag) {
+      int rc;
+      if ((rc = dalloc(ctx, &ctx->d_flag, 4))) return rc;
+    }
+    HIPC(ctx, hipMemsetAsync(ctx->d_flag, 0, 16, ctx->stream));
+    hipLaunchKernelGGL(ksg_range32, dim3((ctx->c.N + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st, xc, xm,
+                       count, ctx->d_flag);
+    unsigned bad = 0;
+    HIPC(ctx, hipMemcpyAsync(&bad, ctx->d_flag, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(ctx, hipStreamSynchronize(ctx->stream));
+    *n32 = bad == 0;
+  }
+  ctx->last_n32 = *n32;
+  return KSG_OK;
+}
+
+// LDS budget attribute of the phase-2 instances (once per process)
+int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
+  static bool attr_set = false;
+  if (attr_set) return KSG_OK;
+  HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
+  HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)budget));
+  for (const void* f : slot_kernels())
+    HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
+  attr_set = true;
+  return KSG_OK;
+}
+
 int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const CapArgs* cap,
                 const ksg_profile* d_prof) {
   const int N = ctx->c.N;
+  // the window mode (4) runs its slot walk here without the pipeline (capture runs)
+  const int bmode = ctx->batch_mode == 4 ? 2 : ctx->batch_mode;
   if (!ctx->d_rec) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rec, (size_t)KSG_BATCH_MAX * N))) return rc;
@@ -2651,43 +2728,24 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   constexpr size_t kLdsBudget = 120 * 1024;
   const size_t cm_words = (size_t)((((N + 31) / 32) + 3) & ~3);
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;   // ksg_batch_phase2s<RM> instance
-  const size_t slot_bytes = ctx->batch_mode == 2 ? 8 * (size_t)(2 * slot_rm + 10) : 8 * (size_t)(2 * ctx->c.R + 4);
-  const bool topset = ctx->batch_mode >= 1;   // top-set variants keep one slot per pod
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kLdsBudget));
-    HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
-    for (const void* f : slot_kernels())
-      HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
-    attr_set = true;
+  const size_t slot_bytes = bmode == 2 ? 8 * (size_t)(2 * slot_rm + 10) : 8 * (size_t)(2 * ctx->c.R + 4);
+  const bool topset = bmode >= 1;   // top-set variants keep one slot per pod
+  {
+    int rc;
+    if ((rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
   }
-  // 32-bit Fit / BalancedAllocation in the slot walk when the ranges allow (one
-  // small check launch + a 4-byte read per call)
   bool n32 = false;
-  int64_t n32_xc = 0, n32_xm = 0;
-  if (ctx->batch_mode == 2 && slot_rm == 4 && range32_candidate(ctx, first, count, &n32_xc, &n32_xm)) {
-    if (!ctx->d_flag) {
-      int rc;
-      if ((rc = dalloc(ctx, &ctx->d_flag, 4))) return rc;
-    }
-    HIPC(ctx, hipMemsetAsync(ctx->d_flag, 0, 16, ctx->stream));
-    hipLaunchKernelGGL(ksg_range32, dim3((N + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st, n32_xc, n32_xm,
-                       count, ctx->d_flag);
-    unsigned bad = 0;
-    HIPC(ctx, hipMemcpyAsync(&bad, ctx->d_flag, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
-    HIPC(ctx, hipStreamSynchronize(ctx->stream));
-    n32 = bad == 0;
+  if (bmode == 2) {
+    int rc;
+    if ((rc = decide_n32(ctx, first, count, &n32))) return rc;
   }
-  ctx->last_n32 = n32;
   (void)hipGetLastError();
   treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   int trc;
   if ((trc = tmark(ctx))) return trc;
   for (int off = 0; off < count;) {
-    int nb = std::min(ctx->batch_mode == 2 ? ctx->slot_block : KSG_BATCH_MAX, count - off);
+    int nb = std::min(bmode == 2 ? ctx->slot_block : KSG_BATCH_MAX, count - off);
     int64_t lo = 0, hi = 0;
     size_t bytes = 0;
     for (;;) {
@@ -2716,7 +2774,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
       hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
       if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
       // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
-      if (ctx->batch_mode == 2) {
+      if (bmode == 2) {
         const int si = (n32 ? 6 : slot_rm == 4 ? 0 : 3) + (ctx->slot_block == 64 ? 0 : ctx->slot_block == 128 ? 1 : 2);
         hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(slot_kernels()[si])), dim3(1),
                            dim3(ctx->slot_block), bytes, ctx->stream, b);
@@ -2791,14 +2849,26 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const int B = window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
   const int slots = window ? 2 * B : B;   // carried + this batch's slots
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
-  const void* kern = pipe_kernels()[(slot_rm == 4 ? 0 : 2) + (slots <= 128 ? 0 : 1)];
-  const int block = 2 * (slots <= 128 ? 128 : 256);
-  constexpr size_t kLdsBudget = 96 * 1024;
-  static bool attr_set = false;
-  if (!attr_set) {
-    for (const void* f : pipe_kernels())
-      HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
-    attr_set = true;
+  // mode 4: the slot walk (one lane per slot) inside this pipeline; mode 3:
+  // the pipelined two-version walk (ksched_phase2p.h)
+  const bool slotwalk = ctx->batch_mode == 4;
+  bool n32 = false;
+  if (slotwalk && (rc = decide_n32(ctx, first, count, &n32))) return rc;
+  const int sblock = slots <= 64 ? 64 : slots <= 128 ? 128 : 256;
+  const void* kern = slotwalk ? slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)]
+                              : pipe_kernels()[(slot_rm == 4 ? 0 : 2) + (slots <= 128 ? 0 : 1)];
+  const int block = slotwalk ? sblock : 2 * (slots <= 128 ? 128 : 256);
+  const size_t kLdsBudget = slotwalk ? 120 * 1024 : 96 * 1024;
+  const size_t slot_bytes = 8 * (size_t)(2 * slot_rm + 10);   // SlotLayout<RM>::STRIDE int64 words
+  if (slotwalk) {
+    if ((rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
+  } else {
+    static bool attr_set = false;
+    if (!attr_set) {
+      for (const void* f : pipe_kernels())
+        HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
+      attr_set = true;
+    }
   }
   BatchArgs b{};
   b.c = ctx->c;
@@ -2836,7 +2906,11 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
         lo = std::min<int64_t>(lo, q.blob);
         hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
       }
-      bytes = 4 * ((2 * cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3);
+      if (slotwalk)
+        bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
+                (size_t)sblock * slot_bytes;
+      else
+        bytes = 4 * ((2 * cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3);
       if (bytes <= kLdsBudget || nb == 1) break;
       nb = std::max(1, nb / 2);
     }
@@ -2869,7 +2943,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
     }
     hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(kern)), dim3(1), dim3(block), bytes, s2, b);
-    if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2P, 0.5 * nb * (nb + 1)))) return rc;
+    if ((rc = tlaunched(ctx, slotwalk ? KSG_K_BATCH_PHASE2S : KSG_K_BATCH_PHASE2P, 0.5 * nb * (nb + 1)))) return rc;
     if (overlap) HIPC(ctx, hipEventRecord(ctx->ev_p2[par], s2));
     prev_nb = nb;
     off += nb;
@@ -3297,7 +3371,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   }
   if (batched) {
     ctx->last_path = 2;
-    if (ctx->batch_mode == 3 && !want_cap) {
+    if ((ctx->batch_mode == 3 || ctx->batch_mode == 4) && !want_cap) {
       if ((rc = run_pipe(ctx, first, count, d_pl, d_res, d_prof))) return rc;
     } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, want_cap ? &ca : nullptr, d_prof))) {
       return rc;
@@ -3457,7 +3531,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
-    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : 2;
+    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : m == "slot" ? 2 : 4;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {

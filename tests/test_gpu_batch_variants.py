@@ -1,8 +1,9 @@
 """GPU parity of every phase-2 variant of the batched placement path
 (KSG_BATCH_MODE): "slot" (default) at each block size,
-"pipe" (with and without the two-batch window, at 64- and 128-pod batches,
-and with per-kernel timing on, which runs the same arithmetic without
-overlap), "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
+"window" (the slot walk inside the two-stream pipeline with the two-batch
+window; also without the window, at 64-pod batches and with per-kernel
+timing on, which runs the same arithmetic without overlap), "pipe" (the
+same variations), "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
 state bit-exact against the C++ oracle, including split calls."""
 import numpy as np
 import pytest
@@ -27,6 +28,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs
 # (mode, extra env): the slot variant at each of its block sizes (= batch sizes; 128 is the default)
 MODES = {"pipe": ("pipe", {}), "pipe64": ("pipe", {"KSG_SLOT_BLOCK": 64}),
          "pipe-nowindow": ("pipe", {"KSG_PIPE_WINDOW": 0}), "pipe-timed": ("pipe", {"_timing": 1}),
+         "window": ("window", {}), "window-timed": ("window", {"_timing": 1}),
+         "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "window64": ("window", {"KSG_SLOT_BLOCK": 64}),
          "slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
          "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
          "topset": ("topset", {}), "scan": ("scan", {})}
