@@ -33,7 +33,7 @@ if mode == "pipe":
     for i in range(1, 10):
         print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
     sys.exit(0)
-if mode == "slot":
+if mode in ("slot", "window"):
     names = ["(start)", "X: speculate + issue next-pod loads", "X: changed node + DPP reductions",
              "Y: barrier 1 + decide (+renorm)", "Y: row update + results", "barrier 2",
              "Y: next-pod records + top set (waits)", "Y: fetched column decode"]
@@ -41,7 +41,7 @@ else:
     names = ["(start)", "A: changed nodes + top sets", "barrier 1", "B: decide (+rescan)",
              "B: next-pod LDS writes", "barrier 2 (waits for the assume)"]
 print(f"[{mode}] {n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build)")
-if mode == "slot" and any(st[8:13]):   # the finer split of segments 1 and 2 (loop order)
+if mode in ("slot", "window") and any(st[8:13]):   # the finer split of segments 1 and 2 (loop order)
     names += [""] * 8
     names[8], names[9], names[1] = "X0: pod setup (LDS pod/P1 reads)", "X1: speculated node (top set, C)", "X2: issue next-pod loads"
     names[10], names[11], names[12] = "X3a: to slot evaluation", "X3b: slot read + Fit/BA scores", "X3c: normalise + key"
@@ -49,5 +49,5 @@ if mode == "slot" and any(st[8:13]):   # the finer split of segments 1 and 2 (lo
     for i in (8, 9, 1, 10, 11, 12, 2, 3, 6, 7, 4, 5):
         print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
     sys.exit(0)
-for i in range(1, 8 if mode == "slot" else 6):
+for i in range(1, 8 if mode in ("slot", "window") else 6):
     print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
