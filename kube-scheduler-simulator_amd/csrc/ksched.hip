@@ -1510,11 +1510,19 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
           bs = ba_score(prof, p, L);
         }
         KSG_STAMP(11);
-        const int64_t part = my_img + fs * h.w_fit + bs * h.w_ba;
         // 100 * rt < 2^15 and 100 * ra < 2^23: qdiv32's range
-        const int64_t nt = mt1 != 0 ? 100 - qdiv32(100 * (int32_t)rt, (int32_t)mt1, s1.inv_mt) : 100;
-        const int64_t na = ma1 != 0 ? qdiv32(100 * (int32_t)ra, (int32_t)ma1, s1.inv_ma) : ra;
-        my_key = argmax_key(part + nt * h.w_t + na * h.w_a, my_node);
+        const int32_t nt = mt1 != 0 ? 100 - qdiv32(100 * (int32_t)rt, (int32_t)mt1, s1.inv_mt) : 100;
+        const int32_t na = ma1 != 0 ? qdiv32(100 * (int32_t)ra, (int32_t)ma1, s1.inv_ma) : (int32_t)ra;
+        int64_t part, total;
+        if constexpr (N32) {   // range32_candidate: every weighted sum < 2^30
+          const int32_t p32 = my_img + (int32_t)fs * (int32_t)h.w_fit + (int32_t)bs * (int32_t)h.w_ba;
+          part = p32;
+          total = p32 + nt * (int32_t)h.w_t + na * (int32_t)h.w_a;
+        } else {
+          part = my_img + fs * h.w_fit + bs * h.w_ba;
+          total = part + nt * h.w_t + na * h.w_a;
+        }
+        my_key = argmax_key(total, my_node);
         cnt += 1u << 8;
         live = pack_rec(part, rt, ra);
       }
@@ -2638,6 +2646,13 @@ bool range32_candidate(ksg_ctx* ctx, int first, int count, int64_t* xc, int64_t*
   bool fit = false;
   for (int k = 0; k < prof.n_filter; k++) fit |= prof.filter_order[k] == KSG_PL_NODE_RESOURCES_FIT;
   if (!fit || (prof.fit_w[0] + prof.fit_w[1]) * 100 >= (1 << 30)) return false;
+  int64_t wsum = 0;   // the slot walk's weighted totals in 32 bits
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if ((prof.score_mask >> pl) & 1u) {
+      if (prof.weight[pl] < 0) return false;
+      wsum += prof.weight[pl];
+    }
+  if (wsum * 100 >= (1 << 30)) return false;
   constexpr int64_t kMiB = 1 << 20;
   *xc = *xm = 0;
   for (int i = first; i < first + count; i++) {
