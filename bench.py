@@ -290,6 +290,15 @@ def main():
     dev = f"cuda:{local_rank}"
     dist.init_process_group(backend="nccl", init_method="env://", world_size=world, rank=rank,
                             device_id=torch.device(dev))
+    # one collective before the library opens its streams: RCCL creates its
+    # own streams at the first collective, and with GPU_MAX_HW_QUEUES = 4 the
+    # order decides which streams share a hardware queue; opened after RCCL's,
+    # the library's two streams (phase 2 / phase 1 + top-k) keep separate
+    # queues and overlap (127 ms per step instead of 150 ms,
+    # scripts/wall_vs_device.py WITH_RCCL=1 / 2)
+    warm = torch.zeros(8, device=dev)
+    dist.all_reduce(warm)
+    torch.cuda.synchronize()
 
     G = importlib.import_module(PKG + ".generator")
     E = importlib.import_module(PKG + ".encoder")
@@ -322,8 +331,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        ts = time.perf_counter()
         pl = step()
         kernel_ms.append(eng.last_kernel_ms())
+        log(f"[rank {rank}] step wall {(time.perf_counter() - ts) * 1e3:.1f} ms, device {kernel_ms[-1]:.1f} ms")
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
