@@ -239,6 +239,9 @@ struct BatchArgs {
   unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
   uint64_t* rec;            // [KSG_BATCH_MAX][N] packed phase-1 records
   int32_t* img;             // [KSG_BATCH_MAX][N] weight x ImageLocality score of feasible nodes
+  int32_t* stat;            // [KSG_BATCH_MAX][N] the slot walk's N32 instances: img + the normalised
+                            // TaintToleration / NodeAffinity terms under the phase-1 maxima
+                            // (written by top-k), or null
   int32_t* pmax;            // [KSG_BATCH_MAX][2] phase-1 maxima (taint, node affinity)
   P1Stats* p1;              // [KSG_BATCH_MAX]
   uint64_t* top;            // [KSG_BATCH_MAX][KSG_BATCH_MAX] top-set argmax keys
@@ -550,6 +553,10 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
     return total_score(v, part, rt, ra, mt, ma, e, nullptr, nullptr);
   };
   int64_t tot[kTopQ];
+  // the slot walk's N32 instances add Fit + BalancedAllocation to this (the
+  // record's partial minus img is exactly those two weighted scores)
+  int32_t* stat = a.stat ? a.stat + (size_t)j * N : nullptr;
+  const int32_t* img = a.img + (size_t)j * N;
 #pragma unroll
   for (int q = 0; q < kTopQ; q++) {
     const int n = tid + q * BLOCK;
@@ -559,6 +566,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
     if (!(x >> 63)) continue;
     const int64_t t = total_of(x, err);
     tot[q] = t;
+    if (stat) stat[n] = (int32_t)(t - (int64_t)(uint32_t)x + img[n]);
   }
   auto stats = [&](uint64_t x, int n, int64_t t) {
     nfeas += 1;
@@ -575,7 +583,11 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
   }
   for (int n = tid + kTopQ * BLOCK; n < N; n += BLOCK) {
     const uint64_t x = rec[n];
-    if (x >> 63) stats(x, n, total_of(x, err));
+    if (x >> 63) {
+      const int64_t t = total_of(x, err);
+      stats(x, n, t);
+      if (stat) stat[n] = (int32_t)(t - (int64_t)(uint32_t)x + img[n]);
+    }
   }
   {
     const int64_t w0 = wave_min64(tmin), w1 = -wave_min64(-tmax);
@@ -1350,9 +1362,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   __shared__ ksg_profile s_prof;
   __shared__ P1Stats s_p1[KSG_BATCH_MAX];
   __shared__ int32_t s_clist[KSG_BATCH_MAX];
-  __shared__ uint64_t s_top[KSG_BATCH_MAX];    // T_j, sorted descending
   __shared__ uint64_t s_ce[KSG_BATCH_MAX];     // live record of changed slot i (renormalisation)
-  __shared__ P2Part s_part[NW];
+  __shared__ P2Part s_part[2][NW];             // by pod parity (one barrier per pod)
   __shared__ WRed s_w[NW];
   __shared__ ksg_result s_res[KSG_BATCH_MAX];  // per-pod results, stored after the walk
   __shared__ uint8_t s_touched[KSG_BATCH_MAX];  // two-batch window: slot assumed onto in this batch
@@ -1375,7 +1386,6 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     reinterpret_cast<int32_t*>(s_p1)[i] = reinterpret_cast<const int32_t*>(a.p1)[i];
   for (int i = tid; i < (int)(sizeof(ksg_profile) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(&s_prof)[i] = reinterpret_cast<const int32_t*>(a.prof)[i];
-  s_top[tid] = a.top[tid];
   bool fit_filter_on = false;
   for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
   __syncthreads();
@@ -1389,6 +1399,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   int my_node = 0;             // node of slot tid (tid < nc)
   uint64_t my_rec = 0;         // pod j's phase-1 record at my_node
   int32_t my_img = 0;
+  int32_t my_stat = 0;         // N32: pod j's static part of the total at my_node (a.stat)
   // Two-batch window (run_pipe with the slot walk): this batch's phase 1 saw
   // the state before the previous batch's assumes, so the nodes the previous
   // batch touched start as changed slots with their live rows.  Their phase-1
@@ -1408,10 +1419,22 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
       atomicOr(&s_cmask[my_node >> 5], 1u << (my_node & 31));
       my_rec = a.rec[my_node];
       my_img = a.img[my_node];
+      if constexpr (N32) my_stat = a.stat[my_node];
     }
   }
   if (tid < KSG_BATCH_MAX) s_touched[tid] = 0;
   __syncthreads();
+  // One barrier per pod.  Every wave keeps the first 64 entries of T_j in its
+  // lanes (t64) with their changed flags (t_chg, computed a pod ahead); a
+  // slot's row is written only by its owner wave (the wave of lanes that
+  // evaluate it), so its next read is in program order; the block-uniform rare
+  // paths read the LDS tables after barrier 1, which orders them after every
+  // earlier pod's writes.  A wave may still be in pod j - 1's assume while
+  // another evaluates pod j: the changed-set reads before barrier 1 add
+  // prev_sel, and the per-wave partials alternate by pod parity.
+  uint64_t t64 = a.top[lane];
+  bool t_chg = lane < s_p1[0].K ? changed(key_node(t64)) : true;
+  int prev_sel = -1;
 #ifdef KSG_STAMPS
   unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -1453,15 +1476,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     uint64_t bu_key = 0;
     bool bu_full = false;
     {
-      uint64_t key = 0;
-      bool ok = false;
-      if (lane < s1.K) {
-        key = s_top[lane];
-        ok = !changed(key_node(key));
-      }
-      const uint64_t m = __ballot(ok);
+      const uint64_t m = __ballot(lane < s1.K && !t_chg);
       if (m) {
-        bu_key = readlane64(key, __builtin_ctzll(m));
+        bu_key = readlane64(t64, __builtin_ctzll(m));
         spec = key_node(bu_key);
       }
       bu_full = m == 0 && s1.K > 64;
@@ -1472,7 +1489,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     const int nn = tid < nc ? my_node : (spec >= 0 ? spec : 0);
     uint64_t nx_rec = a.rec[(size_t)jn * N + nn];
     int32_t nx_img = a.img[(size_t)jn * N + nn];
-    uint64_t nx_top = a.top[(size_t)jn * KSG_BATCH_MAX + tid];
+    int32_t nx_stat = 0;
+    if constexpr (N32) nx_stat = a.stat[(size_t)jn * N + nn];
+    const uint64_t nx_t64 = a.top[(size_t)jn * KSG_BATCH_MAX + lane];
     SlotFetch<RM> col = slot_plan_fetch<RM>(plan, spec >= 0 ? spec : 0);
     KSG_STAMP(1);
 
@@ -1510,15 +1529,16 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
           bs = ba_score(prof, p, L);
         }
         KSG_STAMP(11);
-        // 100 * rt < 2^15 and 100 * ra < 2^23: qdiv32's range
-        const int32_t nt = mt1 != 0 ? 100 - qdiv32(100 * (int32_t)rt, (int32_t)mt1, s1.inv_mt) : 100;
-        const int32_t na = ma1 != 0 ? qdiv32(100 * (int32_t)ra, (int32_t)ma1, s1.inv_ma) : (int32_t)ra;
         int64_t part, total;
         if constexpr (N32) {   // range32_candidate: every weighted sum < 2^30
-          const int32_t p32 = my_img + (int32_t)fs * (int32_t)h.w_fit + (int32_t)bs * (int32_t)h.w_ba;
-          part = p32;
-          total = p32 + nt * (int32_t)h.w_t + na * (int32_t)h.w_a;
+          // the normalised TaintToleration / NodeAffinity terms come with my_stat (top-k)
+          const int32_t fb = (int32_t)fs * (int32_t)h.w_fit + (int32_t)bs * (int32_t)h.w_ba;
+          part = my_img + fb;
+          total = my_stat + fb;
         } else {
+          // 100 * rt < 2^15 and 100 * ra < 2^23: qdiv32's range
+          const int32_t nt = mt1 != 0 ? 100 - qdiv32(100 * (int32_t)rt, (int32_t)mt1, s1.inv_mt) : 100;
+          const int32_t na = ma1 != 0 ? qdiv32(100 * (int32_t)ra, (int32_t)ma1, s1.inv_ma) : (int32_t)ra;
           part = my_img + fs * h.w_fit + bs * h.w_ba;
           total = part + nt * h.w_t + na * h.w_a;
         }
@@ -1529,6 +1549,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     }
     KSG_STAMP(12);
     if (tid < nc) s_ce[tid] = live;
+    P2Part* part = s_part[j & 1];
     {
       const uint64_t k0 = wreduce(my_key, OpMaxU64{});
       const uint32_t wc = wreduce(cnt, OpAdd32{});
@@ -1536,9 +1557,10 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
       uint64_t bu = 0;
       if (bu_full) {   // best unchanged: this wave's slice of T_j (rare)
         uint64_t tk = 0;
-        if (tid < s1.K) {
-          const uint64_t key = s_top[tid];
-          if (!changed(key_node(key))) tk = key;
+        if (tid < s1.K) {   // (T_j from global memory; prev_sel: see above)
+          const uint64_t key = a.top[(size_t)j * KSG_BATCH_MAX + tid];
+          const int kn = key_node(key);
+          if (!changed(kn) && kn != prev_sel) tk = key;
         }
         bu = wreduce(tk, OpMaxU64{});
       }
@@ -1548,7 +1570,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
         o.bu = bu;
         o.cnt = wc;
         o.kidx = mk ? wv * 64 + __builtin_ctzll(mk) : -1;
-        s_part[wv] = o;
+        part[wv] = o;
       }
     }
     KSG_STAMP(2);
@@ -1560,7 +1582,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     int feas1 = 0, live_n = 0, lost_t = 0, lost_a = 0;
 #pragma unroll
     for (int i = 0; i < NW; i++) {
-      const P2Part o = s_part[i];
+      const P2Part o = part[i];
       if (o.k0 > k0) { k0 = o.k0; kidx = o.kidx; }
       if (bu_full) bu = o.bu > bu ? o.bu : bu;
       feas1 += o.cnt & 0xff;
@@ -1664,10 +1686,11 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     // ---- Y: assume ----------------------------------------------------------
     const bool added = selected >= 0 && idx < 0;
     if (added && selected != spec) {   // speculation missed: dependent loads
-      if (wv == 0) col = slot_plan_fetch<RM>(plan, selected);
+      col = slot_plan_fetch<RM>(plan, selected);
       if (tid == nc) {
         nx_rec = a.rec[(size_t)jn * N + selected];
         nx_img = a.img[(size_t)jn * N + selected];
+        if constexpr (N32) nx_stat = a.stat[(size_t)jn * N + selected];
       }
     }
     // pod j+1's state into place (waits for X2's loads, before this pod's
@@ -1676,16 +1699,24 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
     if (tid < nc + (added ? 1 : 0)) {
       my_rec = nx_rec;
       my_img = nx_img;
+      my_stat = nx_stat;
     }
-    if (tid < K1) s_top[tid] = nx_top;
+    // T_{j+1}'s changed flags: this pod's node may not be in the bitmap yet
+    t64 = nx_t64;
+    t_chg = lane < K1 ? (changed(key_node(t64)) || key_node(t64) == selected) : true;
     KSG_STAMP(6);
     const int64_t col_val = slot_word_value<RM, N32>(col, lane, R);
     KSG_STAMP(7);
-    if (wv == 0 && selected >= 0) {
-      const int slot = added ? nc : idx;
+    const int slot = added ? nc : idx;
+    if (selected >= 0 && wv == (slot >> 6)) {   // the slot's owner wave
       int64_t* row = s_slot + (size_t)slot * SL::STRIDE;
-      if (lane < SW)   // the live columns stay in the row; global memory gets them after the walk
-        row[lane] = (added ? col_val : row[lane]) + row_delta;
+      // the live columns stay in the row; global memory gets them after the walk
+      // (an existing row: an LDS add without return, nothing waits on it)
+      if (added) {
+        if (lane < SW) row[lane] = col_val + row_delta;
+      } else if (lane < SW && row_delta != 0) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(row + lane), (unsigned long long)row_delta);
+      }
       if (lane == 0 && has_commit) {   // PodTopologySpread / InterPodAffinity count tables
         const int32_t* cw = s_prog + (p.commit - a.prog_lo);
         const int ns = *cw++;
@@ -1716,10 +1747,10 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
       s_res[j] = res;
     }
     nc += added ? 1 : 0;
+    prev_sel = selected;
     KSG_STAMP(4);
-    lds_barrier();   // the count-table stores (wave 0, lane 0) need no drain: no lane reads them
-    KSG_STAMP(5);
   }
+  __syncthreads();
   // No store is on the per-pod path: nothing in the walk reads a changed
   // node's columns from global memory (they live in its LDS row), so the rows
   // and the results go out once, here.
@@ -1738,13 +1769,13 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   if (a.carry_out) {   // the nodes this batch touched, in slot order, for the next batch
     const bool t = tid < nc && s_touched[tid];
     const uint64_t m = __ballot(t);
-    if (lane == 0) s_part[wv].cnt = (uint32_t)__popcll(m);
+    if (lane == 0) s_part[0][wv].cnt = (uint32_t)__popcll(m);
     __syncthreads();
     int base = 0, total = 0;
 #pragma unroll
     for (int i = 0; i < NW; i++) {
-      base += i < wv ? (int)s_part[i].cnt : 0;
-      total += (int)s_part[i].cnt;
+      base += i < wv ? (int)s_part[0][i].cnt : 0;
+      total += (int)s_part[0][i].cnt;
     }
     if (t) a.carry_out[base + __popcll(m & ((1ull << lane) - 1))] = s_clist[tid];
     if (tid == 0) *a.carry_out_n = total;
@@ -2307,6 +2338,7 @@ struct ksg_ctx {
   // batched-path buffers (lazily allocated)
   uint64_t* d_rec = nullptr;
   int32_t* d_img = nullptr;
+  int32_t* d_stat = nullptr;
   int32_t* d_pmax = nullptr;
   P1Stats* d_p1 = nullptr;
   uint64_t* d_top = nullptr;
@@ -2314,6 +2346,7 @@ struct ksg_ctx {
   // phase 1 + top-k, the carried changed set)
   uint64_t* d_prec[2] = {nullptr, nullptr};
   int32_t* d_pimg[2] = {nullptr, nullptr};
+  int32_t* d_pstat[2] = {nullptr, nullptr};
   int32_t* d_ppmax[2] = {nullptr, nullptr};
   P1Stats* d_pp1[2] = {nullptr, nullptr};
   uint64_t* d_ptop[2] = {nullptr, nullptr};
@@ -2409,12 +2442,14 @@ void free_all(ksg_ctx* ctx) {
   ctx->pre_words = 0;
   ctx->d_rec = nullptr;
   ctx->d_img = nullptr;
+  ctx->d_stat = nullptr;
   ctx->d_pmax = nullptr;
   ctx->d_p1 = nullptr;
   ctx->d_top = nullptr;
   for (int q = 0; q < 2; q++) {
     ctx->d_prec[q] = nullptr;
     ctx->d_pimg[q] = nullptr;
+    ctx->d_pstat[q] = nullptr;
     ctx->d_ppmax[q] = nullptr;
     ctx->d_pp1[q] = nullptr;
     ctx->d_ptop[q] = nullptr;
@@ -2711,6 +2746,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rec, (size_t)KSG_BATCH_MAX * N))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_img, (size_t)KSG_BATCH_MAX * N))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_stat, (size_t)KSG_BATCH_MAX * N))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_pmax, (size_t)2 * KSG_BATCH_MAX))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_p1, (size_t)KSG_BATCH_MAX))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_top, (size_t)KSG_BATCH_MAX * KSG_BATCH_MAX))) return rc;
@@ -2754,6 +2790,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     int rc;
     if ((rc = decide_n32(ctx, first, count, &n32))) return rc;
   }
+  b.stat = n32 ? ctx->d_stat : nullptr;
   (void)hipGetLastError();
   treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
@@ -2843,6 +2880,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     for (int q = 0; q < 2; q++) {
       if ((rc = dalloc(ctx, &ctx->d_prec[q], (size_t)KSG_BATCH_MAX * N))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_pimg[q], (size_t)KSG_BATCH_MAX * N))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_pstat[q], (size_t)KSG_BATCH_MAX * N))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_ppmax[q], (size_t)2 * KSG_BATCH_MAX))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_pp1[q], (size_t)KSG_BATCH_MAX))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_ptop[q], (size_t)KSG_BATCH_MAX * KSG_BATCH_MAX))) return rc;
@@ -2937,6 +2975,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.prog_len = (int32_t)(hi - lo);
     b.rec = ctx->d_prec[par];
     b.img = ctx->d_pimg[par];
+    b.stat = slotwalk && n32 ? ctx->d_pstat[par] : nullptr;
     b.pmax = ctx->d_ppmax[par];
     b.p1 = ctx->d_pp1[par];
     b.top = ctx->d_ptop[par];
