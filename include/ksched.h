@@ -294,6 +294,7 @@ int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
  * checked narrow forms that ran (exact either way; for tests and reports). */
 #define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
 #define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */
+#define KSG_RUN_TCOL 4           /* phase 2 was the transposed walk (ksg_batch_phase2t) */
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event
@@ -319,7 +320,9 @@ enum {
   KSG_K_SWEEP_NARROW = 11,
   KSG_K_CAPTURE_EVAL = 12,
   KSG_K_CAPTURE_NORM = 13,
-  KSG_NKERNELS = 14
+  KSG_K_BATCH_PHASE2T = 14,
+  KSG_K_BATCH_TRANSPOSE = 15,
+  KSG_NKERNELS = 16
 };
 typedef struct ksg_kernel_stat {
   char name[48];

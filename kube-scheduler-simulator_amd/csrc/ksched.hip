@@ -253,6 +253,10 @@ struct BatchArgs {
   const int32_t* carry_n;   // their count (device), or null
   int32_t* carry_out;       // this batch's changed nodes, for the next batch
   int32_t* carry_out_n;
+  // transposed walk (ksched_phase2t.h): node-major copies [N][qs] of rec / stat
+  uint64_t* rect;
+  int32_t* statt;
+  int32_t qs;
 };
 
 // record: bit 63 feasible | rt (8 bits) << 48 | ra (16 bits) << 32 | partial (32 bits)
@@ -1787,6 +1791,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 }
 
 #include "ksched_phase2p.h"
+#include "ksched_phase2t.h"
 #include "ksched_capture.h"
 #include "ksched_sweep.h"
 
@@ -2371,8 +2376,12 @@ struct ksg_ctx {
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched, 3 int64 sweep state
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
+  bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
+  uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
+  int32_t* d_statt = nullptr;
   unsigned* d_flag = nullptr; // range-check flag (ksg_range32)
-  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 3 "pipe", 4 "window"
+  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 3 "pipe", 4 "window", 5 "tcol" (the transposed
+  // walk where the N32 check and tcol_candidate pass, else the slot walk)
   // (default: the slot walk with the next batch's phase 1 + top-k overlapped
   // through the two-batch window; the pipelined two-version walk is exact but
   // measured slower: profiles/r2/phase2_modes.log)
@@ -2443,6 +2452,8 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_rec = nullptr;
   ctx->d_img = nullptr;
   ctx->d_stat = nullptr;
+  ctx->d_rect = nullptr;
+  ctx->d_statt = nullptr;
   ctx->d_pmax = nullptr;
   ctx->d_p1 = nullptr;
   ctx->d_top = nullptr;
@@ -2468,7 +2479,8 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan",
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
                                           "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
-                                          "ksg_capture_eval", "ksg_capture_norm"};
+                                          "ksg_capture_eval", "ksg_capture_norm", "ksg_batch_phase2t",
+                                          "ksg_batch_transpose"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2737,11 +2749,28 @@ int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
   return KSG_OK;
 }
 
+// ksg_batch_phase2t instances: P = 1 (<= 64 pods per batch), 2 (<= 128)
+static const std::array<const void*, 2>& tcol_kernels() {
+  static const std::array<const void*, 2> k = {(const void*)ksg_batch_phase2t<1>, (const void*)ksg_batch_phase2t<2>};
+  return k;
+}
+constexpr size_t kTcolLds = 128 * 1024;   // dynamic LDS of the transposed walk (static part ~14 KB)
+
+// Host half of the transposed walk's scope (ksched_phase2t.h): on top of the
+// N32 check, every weighted total fits the column word's 14 bits.
+bool tcol_candidate(const ksg_ctx* ctx) {
+  int64_t wsum = 0;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if ((ctx->prof.score_mask >> pl) & 1u) wsum += ctx->prof.weight[pl];
+  return ctx->c.R <= 4 && wsum * 100 < (1 << 14);
+}
+
 int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const CapArgs* cap,
                 const ksg_profile* d_prof) {
   const int N = ctx->c.N;
-  // the window mode (4) runs its slot walk here without the pipeline (capture runs)
-  const int bmode = ctx->batch_mode == 4 ? 2 : ctx->batch_mode;
+  // the window mode (4) runs its slot walk here without the pipeline (capture
+  // runs); the transposed walk (5) falls back to the slot walk out of its scope
+  const int bmode = ctx->batch_mode >= 4 ? 2 : ctx->batch_mode;
   if (!ctx->d_rec) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rec, (size_t)KSG_BATCH_MAX * N))) return rc;
@@ -2791,15 +2820,34 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     if ((rc = decide_n32(ctx, first, count, &n32))) return rc;
   }
   b.stat = n32 ? ctx->d_stat : nullptr;
+  const bool tcol = ctx->batch_mode == 5 && n32 && tcol_candidate(ctx);
+  if (tcol) {
+    static bool tattr = false;
+    if (!tattr) {
+      for (const void* f : tcol_kernels())
+        HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTcolLds));
+      tattr = true;
+    }
+  }
+  ctx->last_tcol = tcol;
+  if (tcol && !ctx->d_rect) {
+    int rc;
+    if ((rc = dalloc(ctx, &ctx->d_rect, (size_t)128 * N))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_statt, (size_t)128 * N))) return rc;
+  }
+  b.rect = ctx->d_rect;
+  b.statt = ctx->d_statt;
   (void)hipGetLastError();
   treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   int trc;
   if ((trc = tmark(ctx))) return trc;
   for (int off = 0; off < count;) {
-    int nb = std::min(bmode == 2 ? ctx->slot_block : KSG_BATCH_MAX, count - off);
+    int nb = std::min(bmode == 2 ? (tcol ? std::min(ctx->slot_block, 128) : ctx->slot_block) : KSG_BATCH_MAX,
+                      count - off);
     int64_t lo = 0, hi = 0;
     size_t bytes = 0;
+    const size_t budget = tcol ? kTcolLds : kLdsBudget;
     for (;;) {
       lo = ctx->h_pods[first + off].blob;
       hi = lo;
@@ -2809,11 +2857,13 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
         hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
       }
       const size_t words = (cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3;
-      bytes = 4 * words + (topset ? (size_t)nb * slot_bytes : 0);
-      if (bytes <= kLdsBudget || nb == 1) break;
+      // the transposed walk: one slot row per pod + the [slot][pod] column store
+      bytes = 4 * words + (tcol ? (size_t)nb * slot_bytes + (size_t)nb * (nb > 64 ? 128 : 64) * 4
+                                : topset ? (size_t)nb * slot_bytes : 0);
+      if (bytes <= budget || nb == 1) break;
       nb = std::max(1, nb / 2);
     }
-    if (bytes > kLdsBudget) return fail(ctx, KSG_E_UNSUPPORTED, "batch does not fit the LDS budget");
+    if (bytes > budget) return fail(ctx, KSG_E_UNSUPPORTED, "batch does not fit the LDS budget");
     b.b0 = first + off;
     b.out0 = off;
     b.nb = nb;
@@ -2826,7 +2876,14 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
       hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
       if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
       // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
-      if (bmode == 2) {
+      if (tcol) {
+        b.qs = b.nb > 64 ? 128 : 64;
+        hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, ctx->stream, b);
+        if ((trc = tlaunched(ctx, KSG_K_BATCH_TRANSPOSE, units))) return trc;
+        hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(tcol_kernels()[b.nb > 64 ? 1 : 0])),
+                           dim3(1), dim3(64), bytes, ctx->stream, b);
+        if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2T, 0.5 * b.nb * (b.nb + 1)))) return trc;
+      } else if (bmode == 2) {
         const int si = (n32 ? 6 : slot_rm == 4 ? 0 : 3) + (ctx->slot_block == 64 ? 0 : ctx->slot_block == 128 ? 1 : 2);
         hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(slot_kernels()[si])), dim3(1),
                            dim3(ctx->slot_block), bytes, ctx->stream, b);
@@ -2876,6 +2933,7 @@ static const std::array<const void*, 4>& pipe_kernels() {
 int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const ksg_profile* d_prof) {
   const int N = ctx->c.N;
   int rc;
+  ctx->last_tcol = false;
   if (!ctx->d_prec[0]) {
     for (int q = 0; q < 2; q++) {
       if ((rc = dalloc(ctx, &ctx->d_prec[q], (size_t)KSG_BATCH_MAX * N))) return rc;
@@ -3585,7 +3643,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
-    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : m == "slot" ? 2 : 4;
+    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : m == "slot" ? 2 : m == "tcol" ? 5 : 4;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
@@ -4074,7 +4132,8 @@ int ksg_kernel_stats(ksg_ctx* ctx, ksg_kernel_stat* out, int32_t max, int32_t* n
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
   if (!ctx || !path || !flags) return KSG_E_INVALID;
   *path = ctx->last_path;
-  *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0);
+  *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0) |
+           (ctx->last_tcol ? KSG_RUN_TCOL : 0);
   return KSG_OK;
 }
 

@@ -149,7 +149,7 @@ def make_profile(fields: dict) -> KsgProfile:
     return p
 
 
-RUN_NARROW_SWEEP, RUN_SLOT32 = 1, 2   # ksg_last_run_info flags
+RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL = 1, 2, 4   # ksg_last_run_info flags
 
 
 class CaptureBuffers:

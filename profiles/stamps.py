@@ -33,6 +33,14 @@ if mode == "pipe":
     for i in range(1, 10):
         print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
     sys.exit(0)
+if mode == "tcol":
+    names = ["(loop top)", "rescan check + P1 reads", "decide", "assume + result", "next-pod candidate + loads",
+             "row read", "column eval + running maxima"]
+    print(f"[tcol] {n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build)")
+    tot = sum(st[0:7])
+    for i in range(0, 7):
+        print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
+    sys.exit(0)
 if mode in ("slot", "window"):
     names = ["(start)", "X: speculate + issue next-pod loads", "X: changed node + DPP reductions",
              "Y: barrier 1 + decide (+renorm)", "Y: row update + results", "barrier 2",

@@ -22,7 +22,8 @@ MODES = [("pipe", {"KSG_BATCH_MODE": "pipe"}), ("pipe-nowindow", {"KSG_BATCH_MOD
          ("pipe-64", {"KSG_BATCH_MODE": "pipe", "KSG_SLOT_BLOCK": "64"}), ("slot", {"KSG_BATCH_MODE": "slot"}),
          ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
          ("slot-256", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "256"}),
-         ("window", {"KSG_BATCH_MODE": "window"}), ("window-64", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "64"})]
+         ("window", {"KSG_BATCH_MODE": "window"}), ("window-64", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "64"}),
+         ("tcol", {"KSG_BATCH_MODE": "tcol"}), ("tcol-64", {"KSG_BATCH_MODE": "tcol", "KSG_SLOT_BLOCK": "64"})]
 
 
 def main():

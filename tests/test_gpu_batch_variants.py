@@ -1,6 +1,7 @@
 """GPU parity of every phase-2 variant of the batched placement path
 (KSG_BATCH_MODE): "slot" (default) at each block size,
-"window" (the slot walk inside the two-stream pipeline with the two-batch
+"tcol" (the transposed walk, ksched_phase2t.h, at 128- and 64-pod batches;
+the slot walk where its scope check fails), "window" (the slot walk inside the two-stream pipeline with the two-batch
 window; also without the window, at 64-pod batches and with per-kernel
 timing on, which runs the same arithmetic without overlap), "pipe" (the
 same variations), "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
@@ -32,7 +33,8 @@ MODES = {"pipe": ("pipe", {}), "pipe64": ("pipe", {"KSG_SLOT_BLOCK": 64}),
          "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "window64": ("window", {"KSG_SLOT_BLOCK": 64}),
          "slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
          "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
-         "topset": ("topset", {}), "scan": ("scan", {})}
+         "topset": ("topset", {}), "scan": ("scan", {}),
+         "tcol": ("tcol", {}), "tcol64": ("tcol", {"KSG_SLOT_BLOCK": 64})}
 
 
 @pytest.fixture(scope="module", params=list(MODES))
@@ -113,6 +115,46 @@ def test_slot32_refused_on_sub_mib_memory(oracle):
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
     a = _engine_with_batch_mode("slot")
+    a.load(enc, pf)
+    oracle.load(enc, pf)
+    pl, _ = a.run_queue(0, len(pods))
+    assert a.last_run_info() == (2, 0)
+    np.testing.assert_array_equal(pl, oracle.run_queue(0, len(pods))[0])
+
+
+# ---- the transposed walk (KSG_RUN_TCOL) -----------------------------------------
+@pytest.mark.parametrize("strategy", ["least", "most"])
+def test_tcol_runs_and_matches_oracle(oracle, strategy):
+    """Config 2 runs phase 2 as the transposed walk (one wave, lane = pod, a
+    column per changed node); MostAllocated re-chooses nodes within a batch, so
+    the column rewrites and the rescans of the running maxima run too."""
+    P = pkg("profile")
+    nodes, pods, prof = G.config2(n_nodes=1500, n_pods=2500, seed=21)
+    if strategy == "most":
+        prof = P.config2_profile(strategy=P.MOST_ALLOCATED)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = _engine_with_batch_mode("tcol")
+    a.load(enc, pf)
+    oracle.load(enc, pf)
+    pl, res = a.run_queue(0, len(pods))
+    assert a.last_run_info() == (2, native.RUN_SLOT32 | native.RUN_TCOL)
+    po, ro = oracle.run_queue(0, len(pods))
+    np.testing.assert_array_equal(pl, po)
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(res[f], ro[f], err_msg=f)
+    R = len(enc.cluster.res_names)
+    for x, y in zip(a.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_tcol_out_of_scope_falls_back(oracle):
+    """Sub-MiB memory fails the N32 check: the slot walk's int64 instances run."""
+    nodes, pods, prof = G.config2(n_nodes=300, n_pods=400, seed=9)
+    nodes[3].allocatable["memory"] += 4096
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = _engine_with_batch_mode("tcol")
     a.load(enc, pf)
     oracle.load(enc, pf)
     pl, _ = a.run_queue(0, len(pods))
