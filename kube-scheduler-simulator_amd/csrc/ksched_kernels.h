@@ -208,7 +208,9 @@ struct TopoCtx {
   bool has_rec;          // rec = the node's static record: inclusion() reads its verdict bits
   uint64_t rec;
   __device__ __forceinline__ int32_t tabv(int idx) const {
-    if (coherent) return __hip_atomic_load(const_cast<int32_t*>(tab) + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (coherent)   // agent-scope global (sc1) load: no stale L1 line, no acquire needed
+      return __hip_atomic_load((__attribute__((address_space(1))) int32_t*)(const_cast<int32_t*>(tab) + idx),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return tab[idx];
   }
 };

@@ -75,7 +75,7 @@ struct CoopAcc {    // atomics fallback for large histograms
   int32_t hist[KSG_HIST_MAX];
 };
 
-// ald(), arrive_and_wait(): ksched_sweep.h
+// (ksched_sweep.h: gld(), arrive_and_wait() of the replica sweep)
 
 #ifdef KSG_STAMPS
 #define KSG_CSTAMP(seg)                                                     \
@@ -108,8 +108,55 @@ struct CoopArgs {
   unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
 };
 
+// Hand-offs between the G workgroups without cache maintenance (MI355X guide,
+// Guideline 16, "Valid forms" table row 1): every byte another workgroup
+// reads is stored with an agent-scope (sc1, write-through) store or an
+// agent-scope atomic and read with an agent-scope global (sc1) load, every
+// storing wave drains its stores before the workgroup barrier in front of the
+// arrival, one lane per workgroup adds to the counter and polls it with sc1
+// loads, the other waves load after the workgroup barrier that lane joins.
+// No release (buffer_wbl2) and no acquire (buffer_inv): the round-1 barrier
+// paid both, ~8-9 k cycles each (profiles/r1/stamps_topo_coop.txt).
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {   // agent-scope (sc1) global load
+  return __hip_atomic_load((__attribute__((address_space(1))) T*)(const_cast<T*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T, class V>
+__device__ __forceinline__ void gst(T* p, V v) {   // agent-scope (sc1, write-through) global store
+  __hip_atomic_store((__attribute__((address_space(1))) T*)p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void gadd(int32_t* p, int32_t v) {   // agent-scope global atomic add
+  __hip_atomic_fetch_add((__attribute__((address_space(1))) int32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gor(int32_t* p, int32_t v) {    // agent-scope global atomic or
+  __hip_atomic_fetch_or((__attribute__((address_space(1))) int32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ bool coop_barrier(unsigned* bar, unsigned* timeout, int G, unsigned& target) {
-  return arrive_and_wait(bar, timeout, G, target);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 stores and atomics are done
+  __syncthreads();
+  target += (unsigned)G;
+  __shared__ int s_timeout;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)bar, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    int to = 0;
+    while (gld(bar) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26) || gld(timeout)) {
+        gst(timeout, 1u);
+        to = 1;
+        break;
+      }
+    }
+    s_timeout = to;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only: loads stay below the poll
+  __syncthreads();
+  return s_timeout == 0;
 }
 
 // PodTopologySpread with one soft constraint: the per-node count m of
@@ -220,9 +267,8 @@ __device__ __forceinline__ void coop_commit(const DevCluster& c, const DevState&
       const int t = w[2 * i];
       const uint32_t val = c.label_val[(size_t)c.tmpl_col[t] * N + n];
       if (!val) continue;
-      __hip_atomic_fetch_add(st.tab + c.tmpl_off[t] + val, c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(st.tmpl_total + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gadd(st.tab + c.tmpl_off[t] + val, c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1);
+      gadd(st.tmpl_total + t, 1);
     }
   }
 }
@@ -248,6 +294,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ int32_t s_i[NW][16];
   __shared__ int s_size[kMaxSoft];
   __shared__ long long s_tt[4];
+  __shared__ uint8_t s_wkind[kCoopPHist];   // partial-slot word: 1 histogram count (add), 0 presence bits (or), 2 mark (skip)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
@@ -282,13 +329,36 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         const int x = x0 + u * BLOCK;
         w[u] = x / G;
         const int qg = x - w[u] * G;
-        y[u] = x < total ? ald(a.phist + (size_t)qg * kCoopPHist + base + w[u]) : 0;
+        y[u] = x < total ? gld(a.phist + (size_t)qg * kCoopPHist + base + w[u]) : 0;
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         if (!y[u]) continue;
         if (bits) atomicOr((uint32_t*)&s_hist[base + w[u]], (uint32_t)y[u]);
         else atomicAdd(&s_hist[base + w[u]], y[u]);
+      }
+    }
+  };
+  // LDS words [0, nw) of the histogram slots += / |= every workgroup's partial
+  // slot, all at once: lanes walk (workgroup, word) with the word fastest, so a
+  // wave reads 64 consecutive words of one partial; 8 loads in flight per lane
+  auto fold_all = [&](int nw) {
+    const int total = nw * G;
+    for (int x0 = tid; x0 < total; x0 += 8 * BLOCK) {
+      int32_t y[8];
+      int w[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int x = x0 + u * BLOCK;
+        const int qg = x / nw;
+        w[u] = x - qg * nw;
+        y[u] = x < total && s_wkind[w[u]] != 2 ? gld(a.phist + (size_t)qg * kCoopPHist + w[u]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (!y[u]) continue;
+        if (s_wkind[w[u]]) atomicAdd(&s_hist[w[u]], y[u]);
+        else atomicOr((uint32_t*)&s_hist[w[u]], (uint32_t)y[u]);
       }
     }
   };
@@ -345,6 +415,22 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const int words = ok ? s_t.words : 0;
     const bool pmode = words <= kCoopPHist && words * G <= 32768;
     for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
+    if (pmode) {   // word kinds of the partial slot (fold_all)
+      for (int w = tid; w < words; w += BLOCK) {
+        int kind = 0;
+        auto in = [&](const Slot& sl) {
+          if (sl.unique) return;
+          if (w >= sl.hist && w < sl.hist + sl.V) kind = 1;
+          if (sl.mark >= 0 && w >= sl.mark && w < sl.mark + (sl.V + 31) / 32) kind = 2;
+        };
+        for (int i = 0; i < s_g.n_hard; i++) in(s_t.hard[i]);
+        for (int i = 0; i < s_g.n_soft; i++) in(s_t.soft[i]);
+        for (int i = 0; i < s_g.n_aff; i++) in(s_t.aff[i]);
+        for (int i = 0; i < s_g.n_anti; i++) in(s_t.anti[i]);
+        for (int i = 0; i < s_g.n_pref; i++) in(s_t.pref[i]);
+        s_wkind[w] = (uint8_t)kind;
+      }
+    }
     PodView v = make_view(c, prof, p, s_blob, a.prog, true);
     const TopoProg& g = s_g;
     const TopoCtx tc{&s_g, &s_t, s_hist, st.cnt, st.tab, true, false, 0};
@@ -460,15 +546,15 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       __syncthreads();
       // publish this workgroup's partial
       if (pmode) {
-        for (int i = tid; i < words; i += BLOCK) myhist[i] = s_hist[i];
+        for (int i = tid; i < words; i += BLOCK) gst(&myhist[i], s_hist[i]);
       } else {
         auto merge_slot = [&](const Slot& sl) {
           if (sl.unique) return;
           for (int i = tid; i < sl.V; i += BLOCK)
-            if (s_hist[sl.hist + i]) atomicAdd(&acc->hist[sl.hist + i], s_hist[sl.hist + i]);
+            if (s_hist[sl.hist + i]) gadd(&acc->hist[sl.hist + i], s_hist[sl.hist + i]);
           const int bw = (sl.V + 31) / 32;
           for (int i = tid; i < bw; i += BLOCK)
-            if (s_hist[sl.pres + i]) atomicOr((uint32_t*)&acc->hist[sl.pres + i], (uint32_t)s_hist[sl.pres + i]);
+            if (s_hist[sl.pres + i]) gor(&acc->hist[sl.pres + i], s_hist[sl.pres + i]);
         };
         for (int i = 0; i < g.n_hard; i++) merge_slot(s_t.hard[i]);
         for (int i = 0; i < g.n_soft; i++) merge_slot(s_t.soft[i]);
@@ -477,13 +563,13 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         for (int i = 0; i < g.n_pref; i++) merge_slot(s_t.pref[i]);
       }
       if (need_hmin && tid < g.n_hard) {
-        mine->hard_min[tid] = get_l(tid, OpMinL{});
-        mine->hard_dom[tid] = get_i(4 + tid, OpAddI{});
+        gst(&mine->hard_min[tid], get_l(tid, OpMinL{}));
+        gst(&mine->hard_dom[tid], get_i(4 + tid, OpAddI{}));
       } else if (need_se && tid >= 64 && tid < 64 + g.n_soft) {
-        mine->soft_empty[tid - 64] = get_l(8 + tid - 64, OpAddL{});
+        gst(&mine->soft_empty[tid - 64], get_l(8 + tid - 64, OpAddL{}));
       } else if (tid == 128) {
-        if (need_aff) mine->aff_total = get_l(12, OpAddL{});
-        if (need_pref) mine->pref_any = get_i(13, OpOrI{}) != 0;
+        if (need_aff) gst(&mine->aff_total, get_l(12, OpAddL{}));
+        if (need_pref) gst(&mine->pref_any, get_i(13, OpOrI{}) != 0);
       }
     }
     KSG_CSTAMP(1);
@@ -495,19 +581,9 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       if (pmode) {
         for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
         __syncthreads();
-        // (word, workgroup) pairs over the lanes: counts add, presence bitmaps or
-        auto fold_slot = [&](const Slot& sl) {
-          if (sl.unique) return;
-          fold_words(sl.hist, sl.V, false);
-          fold_words(sl.pres, (sl.V + 31) / 32, true);
-        };
-        for (int i = 0; i < g.n_hard; i++) fold_slot(s_t.hard[i]);
-        for (int i = 0; i < g.n_soft; i++) fold_slot(s_t.soft[i]);
-        for (int i = 0; i < g.n_aff; i++) fold_slot(s_t.aff[i]);
-        for (int i = 0; i < g.n_anti; i++) fold_slot(s_t.anti[i]);
-        for (int i = 0; i < g.n_pref; i++) fold_slot(s_t.pref[i]);
+        fold_all(words);   // counts add, presence bitmaps or, marks are left for phase 3
       } else {
-        for (int i = tid; i < words; i += BLOCK) s_hist[i] = ald(&acc->hist[i]);
+        for (int i = tid; i < words; i += BLOCK) s_hist[i] = gld(&acc->hist[i]);
       }
       // scalars: lane q folds workgroup q's slot
       if (need_hmin || need_se || need_aff || need_pref) {
@@ -521,12 +597,12 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           const CoopPart* q = a.parts + tid;
 #pragma unroll
           for (int i = 0; i < kMaxHard; i++)
-            if (need_hmin && i < g.n_hard) { hm[i] = ald(&q->hard_min[i]); hd[i] = ald(&q->hard_dom[i]); }
+            if (need_hmin && i < g.n_hard) { hm[i] = gld(&q->hard_min[i]); hd[i] = gld(&q->hard_dom[i]); }
 #pragma unroll
           for (int i = 0; i < kMaxSoft; i++)
-            if (need_se && i < g.n_soft) se[i] = ald(&q->soft_empty[i]);
-          if (need_aff) af = ald(&q->aff_total);
-          if (need_pref) pa = ald(&q->pref_any);
+            if (need_se && i < g.n_soft) se[i] = gld(&q->soft_empty[i]);
+          if (need_aff) af = gld(&q->aff_total);
+          if (need_pref) pa = gld(&q->pref_any);
         }
         __syncthreads();   // every wave is past its phase-1 get_*() reads
         if (need_hmin) {
@@ -577,14 +653,14 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     }
     KSG_CSTAMP(3);
     if (wg == 0 && prev_fallback_words)   // the set of pod kq - 1, read by everyone by now
-      for (int i = tid; i < prev_fallback_words; i += BLOCK) nxt->hist[i] = 0;
+      for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&nxt->hist[i], 0);
     prev_fallback_words = pmode ? 0 : words;
     {   // existing pods' terms matching this pod: totals, one template per lane
       const int n_t = g.ipa ? g.n_ma + g.n_mh + g.n_mp : 0;
       for (int i = tid; i < n_t; i += BLOCK) {
         const int which = i < g.n_ma ? 0 : (i < g.n_ma + g.n_mh ? 1 : 2);
         const int tm = which == 0 ? g.m_anti[i] : (which == 1 ? g.m_hard[i - g.n_ma] : g.m_pref[i - g.n_ma - g.n_mh]);
-        const int32_t x = ald(&st.tmpl_total[tm]);
+        const int32_t x = gld(&st.tmpl_total[tm]);
         if (x) atomicAdd((unsigned long long*)&s_tt[which], (unsigned long long)x);
       }
     }
@@ -694,25 +770,25 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     }
     __syncthreads();
     if (tid == 0) {
-      mine->nfeas = get_i(0, OpAddI{});
-      mine->minidx = get_i(1, OpMinI{});
-      mine->max_t = get_i(6, OpMaxI32{});
-      mine->max_a = get_i(7, OpMaxI32{});
-      if (need_ign) mine->n_ignored = get_i(2, OpAddI{});
+      gst(&mine->nfeas, get_i(0, OpAddI{}));
+      gst(&mine->minidx, get_i(1, OpMinI{}));
+      gst(&mine->max_t, get_i(6, OpMaxI32{}));
+      gst(&mine->max_a, get_i(7, OpMaxI32{}));
+      if (need_ign) gst(&mine->n_ignored, get_i(2, OpAddI{}));
       if (soft1) {
-        mine->has_val = get_i(3, OpOrI{});
-        mine->has_zero = get_i(4, OpOrI{});
-        mine->mmin = get_l(2, OpMinL{});
-        mine->mmax = get_l(3, OpMaxL{});
+        gst(&mine->has_val, get_i(3, OpOrI{}));
+        gst(&mine->has_zero, get_i(4, OpOrI{}));
+        gst(&mine->mmin, get_l(2, OpMinL{}));
+        gst(&mine->mmax, get_l(3, OpMaxL{}));
       }
       if (need_se)
         for (int i = 0; i < g.n_soft; i++) {
-          mine->soft_present[i] = get_i(8 + i, OpAddI{});
-          mine->soft_seen[i] = get_i(12 + i, OpOrI{});
+          gst(&mine->soft_present[i], get_i(8 + i, OpAddI{}));
+          gst(&mine->soft_seen[i], get_i(12 + i, OpOrI{}));
         }
       if (ipa_may_score) {
-        mine->imin = get_l(4, OpMinL{});
-        mine->imax = get_l(5, OpMaxL{});
+        gst(&mine->imin, get_l(4, OpMinL{}));
+        gst(&mine->imax, get_l(5, OpMaxL{}));
       }
     }
     if (g.pts_score && ok)   // domains seen among feasible nodes (non-unique soft slots)
@@ -720,8 +796,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         const Slot& sl = s_t.soft[i];
         if (g.soft[6 * i + 5] || sl.unique) continue;
         for (int wd = tid; wd < (sl.V + 31) / 32; wd += BLOCK) {
-          if (pmode) myhist[sl.mark + wd] = s_hist[sl.mark + wd];
-          else if (s_hist[sl.mark + wd]) atomicOr((uint32_t*)&acc->hist[sl.mark + wd], (uint32_t)s_hist[sl.mark + wd]);
+          if (pmode) gst(&myhist[sl.mark + wd], s_hist[sl.mark + wd]);
+          else if (s_hist[sl.mark + wd]) gor(&acc->hist[sl.mark + wd], s_hist[sl.mark + wd]);
         }
       }
     KSG_CSTAMP(6);
@@ -735,24 +811,24 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       long long f_mmin = BIG, f_mmax = -BIG - 1, f_imin = BIG, f_imax = -BIG - 1;
       if (tid < G) {
         const CoopPart* q = a.parts + tid;
-        f_n = ald(&q->nfeas);
-        f_min = ald(&q->minidx);
-        f_mt = (int32_t)ald(&q->max_t);
-        f_ma = (int32_t)ald(&q->max_a);
-        if (need_ign) f_ign = ald(&q->n_ignored);
+        f_n = gld(&q->nfeas);
+        f_min = gld(&q->minidx);
+        f_mt = (int32_t)gld(&q->max_t);
+        f_ma = (int32_t)gld(&q->max_a);
+        if (need_ign) f_ign = gld(&q->n_ignored);
         if (soft1) {
-          f_hv = ald(&q->has_val);
-          f_hz = ald(&q->has_zero);
-          f_mmin = ald(&q->mmin);
-          f_mmax = ald(&q->mmax);
+          f_hv = gld(&q->has_val);
+          f_hz = gld(&q->has_zero);
+          f_mmin = gld(&q->mmin);
+          f_mmax = gld(&q->mmax);
         }
         if (need_se)
 #pragma unroll
           for (int i = 0; i < kMaxSoft; i++)
-            if (i < g.n_soft) { f_pr[i] = ald(&q->soft_present[i]); f_se[i] = ald(&q->soft_seen[i]); }
+            if (i < g.n_soft) { f_pr[i] = gld(&q->soft_present[i]); f_se[i] = gld(&q->soft_seen[i]); }
         if (ipa_may_score) {
-          f_imin = ald(&q->imin);
-          f_imax = ald(&q->imax);
+          f_imin = gld(&q->imin);
+          f_imax = gld(&q->imax);
         }
       }
       bfold_i(f_n, OpAddI{}, 0);
@@ -796,7 +872,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         if (pmode) {   // or-ed into this workgroup's own marks
           fold_words(sl.mark, bw, true);
         } else {
-          for (int wd = tid; wd < bw; wd += BLOCK) s_hist[sl.mark + wd] = ald(&acc->hist[sl.mark + wd]);
+          for (int wd = tid; wd < bw; wd += BLOCK) s_hist[sl.mark + wd] = gld(&acc->hist[sl.mark + wd]);
         }
       }
       __syncthreads();
@@ -846,14 +922,14 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         bfold_l(hi, OpMaxL{}, 7);
         __syncthreads();
         if (tid == 0) {
-          mine->pmin = get_l(6, OpMinL{});
-          mine->pmax = get_l(7, OpMaxL{});
+          gst(&mine->pmin, get_l(6, OpMinL{}));
+          gst(&mine->pmax, get_l(7, OpMaxL{}));
         }
         if (!coop_barrier(a.bar, a.timeout, G, target)) return;
         long long l2 = BIG, h2 = -BIG - 1;
         if (tid < G) {
-          l2 = ald(&a.parts[tid].pmin);
-          h2 = ald(&a.parts[tid].pmax);
+          l2 = gld(&a.parts[tid].pmin);
+          h2 = gld(&a.parts[tid].pmax);
         }
         bfold_l(l2, OpMinL{}, 8);
         bfold_l(h2, OpMaxL{}, 9);
@@ -912,8 +988,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       unsigned long long b = 0;
       int32_t e = 0;
       for (int i = 0; i < NW; i++) { b = max(b, (unsigned long long)s_l[i][10]); e |= s_i[i][13]; }
-      mine->best = b;
-      mine->err = e;
+      gst(&mine->best, b);
+      gst(&mine->err, e);
     }
     KSG_CSTAMP(8);
     if (!coop_barrier(a.bar, a.timeout, G, target)) return;
@@ -924,8 +1000,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       unsigned long long b = 0;
       int32_t e = 0;
       if (tid < G) {
-        b = ald(&a.parts[tid].best);
-        e = ald(&a.parts[tid].err);
+        b = gld(&a.parts[tid].best);
+        e = gld(&a.parts[tid].err);
       }
       b = wreduce(b, OpMaxU64{});
       e = wreduce(e, OpOrI{});
