@@ -322,7 +322,8 @@ enum {
   KSG_K_CAPTURE_NORM = 13,
   KSG_K_BATCH_PHASE2T = 14,
   KSG_K_BATCH_TRANSPOSE = 15,
-  KSG_NKERNELS = 16
+  KSG_K_TCOL_CARRY = 16,
+  KSG_NKERNELS = 17
 };
 typedef struct ksg_kernel_stat {
   char name[48];

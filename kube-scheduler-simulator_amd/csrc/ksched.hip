@@ -257,6 +257,8 @@ struct BatchArgs {
   uint64_t* rect;
   int32_t* statt;
   int32_t qs;
+  uint32_t* tc_colinit;     // [carried slot][qs] column words of the carried nodes (ksg_tcol_carry)
+  void* tc_init;            // [qs] TcInit: per-pod maxima / counters over the carried columns
 };
 
 // record: bit 63 feasible | rt (8 bits) << 48 | ra (16 bits) << 32 | partial (32 bits)
@@ -2379,6 +2381,10 @@ struct ksg_ctx {
   bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
   uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
   int32_t* d_statt = nullptr;
+  uint64_t* d_prect[2] = {nullptr, nullptr};   // the same, per window parity
+  int32_t* d_pstatt[2] = {nullptr, nullptr};
+  uint32_t* d_tccol = nullptr;                 // carried columns [64][64]
+  uint64_t* d_tcinit = nullptr;                // TcInit [64] (4 words each)
   unsigned* d_flag = nullptr; // range-check flag (ksg_range32)
   // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 3 "pipe", 4 "window", 5 "tcol" (the transposed
   // walk where the N32 check and tcol_candidate pass, else the slot walk)
@@ -2454,6 +2460,10 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_stat = nullptr;
   ctx->d_rect = nullptr;
   ctx->d_statt = nullptr;
+  ctx->d_prect[0] = ctx->d_prect[1] = nullptr;
+  ctx->d_pstatt[0] = ctx->d_pstatt[1] = nullptr;
+  ctx->d_tccol = nullptr;
+  ctx->d_tcinit = nullptr;
   ctx->d_pmax = nullptr;
   ctx->d_p1 = nullptr;
   ctx->d_top = nullptr;
@@ -2480,7 +2490,7 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
                                           "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
                                           "ksg_capture_eval", "ksg_capture_norm", "ksg_batch_phase2t",
-                                          "ksg_batch_transpose"};
+                                          "ksg_batch_transpose", "ksg_tcol_carry"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2957,21 +2967,42 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   HIPC(ctx, hipMemsetAsync(carry_n, 0, 2 * sizeof(int32_t), ctx->stream));
   const bool window = ctx->pipe_window != 0;
   const bool overlap = window && !ctx->timing;
-  const int B = window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
-  const int slots = window ? 2 * B : B;   // carried + this batch's slots
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
   // mode 4: the slot walk (one lane per slot) inside this pipeline; mode 3:
-  // the pipelined two-version walk (ksched_phase2p.h)
-  const bool slotwalk = ctx->batch_mode == 4;
+  // the pipelined two-version walk (ksched_phase2p.h); mode 5: the transposed
+  // walk (ksched_phase2t.h) with the previous batch's nodes as carried columns,
+  // 64-pod batches, else the slot walk
   bool n32 = false;
-  if (slotwalk && (rc = decide_n32(ctx, first, count, &n32))) return rc;
+  if ((ctx->batch_mode == 4 || ctx->batch_mode == 5) && (rc = decide_n32(ctx, first, count, &n32))) return rc;
+  const bool tcolw = ctx->batch_mode == 5 && window && n32 && tcol_candidate(ctx);
+  const bool slotwalk = ctx->batch_mode == 4 || (ctx->batch_mode == 5 && !tcolw);
+  ctx->last_tcol = tcolw;
+  if (tcolw) {
+    if (!ctx->d_prect[0]) {
+      for (int q = 0; q < 2; q++) {
+        if ((rc = dalloc(ctx, &ctx->d_prect[q], (size_t)64 * N))) return rc;
+        if ((rc = dalloc(ctx, &ctx->d_pstatt[q], (size_t)64 * N))) return rc;
+      }
+      if ((rc = dalloc(ctx, &ctx->d_tccol, (size_t)64 * 64))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_tcinit, (size_t)4 * 64))) return rc;
+    }
+    static bool tattr = false;
+    if (!tattr) {
+      for (const void* f : tcol_kernels())
+        HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTcolLds));
+      tattr = true;
+    }
+  }
+  const int B = tcolw ? 64 : window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
+  const int slots = window ? 2 * B : B;   // carried + this batch's slots
   const int sblock = slots <= 64 ? 64 : slots <= 128 ? 128 : 256;
   const void* kern = slotwalk ? slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)]
                               : pipe_kernels()[(slot_rm == 4 ? 0 : 2) + (slots <= 128 ? 0 : 1)];
   const int block = slotwalk ? sblock : 2 * (slots <= 128 ? 128 : 256);
-  const size_t kLdsBudget = slotwalk ? 120 * 1024 : 96 * 1024;
+  const size_t kLdsBudget = tcolw ? kTcolLds : slotwalk ? 120 * 1024 : 96 * 1024;
   const size_t slot_bytes = 8 * (size_t)(2 * slot_rm + 10);   // SlotLayout<RM>::STRIDE int64 words
-  if (slotwalk) {
+  if (tcolw) {
+  } else if (slotwalk) {
     if ((rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
   } else {
     static bool attr_set = false;
@@ -3017,7 +3048,10 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
         lo = std::min<int64_t>(lo, q.blob);
         hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
       }
-      if (slotwalk)
+      if (tcolw)   // slot rows + the [slot][64] column store for this batch's and the carried slots
+        bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
+                (size_t)(nb + prev_nb) * (slot_bytes + 64 * 4);
+      else if (slotwalk)
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
                 (size_t)sblock * slot_bytes;
       else
@@ -3033,7 +3067,12 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.prog_len = (int32_t)(hi - lo);
     b.rec = ctx->d_prec[par];
     b.img = ctx->d_pimg[par];
-    b.stat = slotwalk && n32 ? ctx->d_pstat[par] : nullptr;
+    b.stat = (slotwalk || tcolw) && n32 ? ctx->d_pstat[par] : nullptr;
+    b.rect = tcolw ? ctx->d_prect[par] : nullptr;
+    b.statt = tcolw ? ctx->d_pstatt[par] : nullptr;
+    b.qs = 64;
+    b.tc_colinit = ctx->d_tccol;
+    b.tc_init = ctx->d_tcinit;
     b.pmax = ctx->d_ppmax[par];
     b.p1 = ctx->d_pp1[par];
     b.top = ctx->d_ptop[par];
@@ -3050,12 +3089,23 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return rc;
     hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(nb), dim3(512), 0, s1, b);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return rc;
+    if (tcolw) {
+      hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, s1, b);
+      if ((rc = tlaunched(ctx, KSG_K_BATCH_TRANSPOSE, units))) return rc;
+    }
     if (overlap) {
       HIPC(ctx, hipEventRecord(ctx->ev_tk[par], s1));
       HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
     }
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(kern)), dim3(1), dim3(block), bytes, s2, b);
-    if ((rc = tlaunched(ctx, slotwalk ? KSG_K_BATCH_PHASE2S : KSG_K_BATCH_PHASE2P, 0.5 * nb * (nb + 1)))) return rc;
+    if (tcolw) {   // the carried columns on the state after the previous walk, then the walk
+      hipLaunchKernelGGL(ksg_tcol_carry<1>, dim3(nb), dim3(64), 0, s2, b);
+      if ((rc = tlaunched(ctx, KSG_K_TCOL_CARRY, (double)nb * prev_nb))) return rc;
+      hipLaunchKernelGGL(ksg_batch_phase2t<1>, dim3(1), dim3(64), bytes, s2, b);
+      if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2T, 0.5 * nb * (nb + 1)))) return rc;
+    } else {
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(kern)), dim3(1), dim3(block), bytes, s2, b);
+      if ((rc = tlaunched(ctx, slotwalk ? KSG_K_BATCH_PHASE2S : KSG_K_BATCH_PHASE2P, 0.5 * nb * (nb + 1)))) return rc;
+    }
     if (overlap) HIPC(ctx, hipEventRecord(ctx->ev_p2[par], s2));
     prev_nb = nb;
     off += nb;
@@ -3483,7 +3533,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   }
   if (batched) {
     ctx->last_path = 2;
-    if ((ctx->batch_mode == 3 || ctx->batch_mode == 4) && !want_cap) {
+    if ((ctx->batch_mode == 3 || ctx->batch_mode == 4 || (ctx->batch_mode == 5 && ctx->pipe_window)) && !want_cap) {
       if ((rc = run_pipe(ctx, first, count, d_pl, d_res, d_prof))) return rc;
     } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, want_cap ? &ca : nullptr, d_prof))) {
       return rc;

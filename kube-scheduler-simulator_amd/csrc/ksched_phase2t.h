@@ -160,6 +160,107 @@ __device__ __forceinline__ bool tc_eval(const TcProf& m, const TcPod& h, const T
   return fits;
 }
 
+
+// the column evaluation's values of one pod
+__device__ __forceinline__ TcPod tc_pod(const ksg_pod& p, const ksg_profile& prof, const P1Stats& s1, bool fit_filter_on,
+                                        int R) {
+  TcPod h;
+  uint32_t mk = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    h.req[r] = r < R ? p.req[r] : 0;
+    const bool chk = r < R && h.req[r] > 0 && !(r >= 3 && ((prof.fit_ignored_res >> r) & 1u));
+    mk |= chk ? 1u << r : 0u;
+  }
+  if (fit_filter_on && !((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u)) mk |= 1u << 4;
+  h.mask = mk;
+  h.rc = (int32_t)p.req[KSG_RES_CPU];
+  h.rm = (int32_t)(p.req[KSG_RES_MEM] >> 20);
+  h.nzc = (int32_t)p.nz_cpu;
+  h.nzm = (int32_t)(p.nz_mem >> 20);
+  const uint32_t smask = prof.score_mask & ~p.score_skip;
+  h.wfit = (smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? (int32_t)prof.weight[KSG_PL_NODE_RESOURCES_FIT] : 0;
+  h.wba = (smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? (int32_t)prof.weight[KSG_PL_BALANCED_ALLOCATION] : 0;
+  h.mt = s1.mt;
+  h.ma = s1.ma;
+  return h;
+}
+
+// A pod's running maxima and counters over the columns carried in from the
+// previous batch (two-batch window), written by ksg_tcol_carry.
+struct TcInit {
+  uint64_t b1, b2;
+  int32_t s1, s2;
+  uint32_t cnt;
+  uint32_t pad;
+};
+
+// Two-batch window: the nodes the previous batch assumed onto (a.carry, its
+// slot order) start this batch as columns.  Block q = pod q of the batch, lane
+// t = carried node t (<= 64): pod q on node t's live row (global state after
+// the previous walk), the column word into tc_colinit[t][q], and the pod's
+// top-2 / counters over the carried columns into tc_init[q].  Same
+// arithmetic as the walk's column evaluation.
+template <int P>
+__global__ __launch_bounds__(64) void ksg_tcol_carry(BatchArgs a) {
+  constexpr int QS = 64 * P;
+  __shared__ ksg_profile s_prof;
+  const int q = blockIdx.x, lane = threadIdx.x;
+  const DevCluster& c = a.c;
+  const int N = c.N, R = c.R;
+  for (int i = lane; i < (int)(sizeof(ksg_profile) / 4); i += 64)
+    reinterpret_cast<int32_t*>(&s_prof)[i] = reinterpret_cast<const int32_t*>(a.prof)[i];
+  __syncthreads();
+  const ksg_profile& prof = s_prof;
+  bool fit_filter_on = false;
+  for (int kf = 0; kf < prof.n_filter; kf++) fit_filter_on |= prof.filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
+  const TcProf cm = tc_prof(cm_prof(prof));
+  const int nc0 = *a.carry_n;
+  const ksg_pod& p = a.pods[a.b0 + q];
+  const P1Stats s1 = a.p1[q];
+  const TcPod h = tc_pod(p, prof, s1, fit_filter_on, R);
+  uint64_t key = 0;
+  uint32_t dc = 0;
+  if (lane < nc0) {
+    const int d = a.carry[lane];
+    int64_t w[SlotLayout<4>::W];
+#pragma unroll
+    for (int x = 0; x < SlotLayout<4>::W; x++)
+      w[x] = slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, x, R, d), x, R);
+    const TcRow row = tc_row(cm, w);
+    const uint64_t x = a.rec[(size_t)q * N + d];
+    const bool p1f = (x >> 63) != 0;
+    const bool ft = p1f && (int32_t)((x >> 48) & 0xff) == h.mt;
+    const bool fa = p1f && (int32_t)((x >> 32) & 0xffff) == h.ma;
+    const int32_t stat = a.stat[(size_t)q * N + d];
+    int32_t fb = 0;
+    const bool live = tc_eval(cm, h, row, fb) && p1f;
+    const int32_t total = stat + fb;
+    a.tc_colinit[lane * QS + q] = tc_word(stat, total, ft, fa, p1f, live);
+    key = live ? argmax_key(total, d) : 0;
+    dc = (p1f ? 1u : 0u) + (live ? 1u << 8 : 0u) + (p1f && !live && ft ? 1u << 16 : 0u) +
+         (p1f && !live && fa ? 1u << 24 : 0u);
+  }
+  // keys of distinct nodes are distinct: the top two and their slots
+  const uint64_t b1 = wreduce(key, OpMaxU64{});
+  const uint64_t m1 = __ballot(b1 != 0 && key == b1);
+  const int s1i = m1 ? __builtin_ctzll(m1) : -1;
+  const uint64_t k2 = lane == s1i ? 0 : key;
+  const uint64_t b2 = wreduce(k2, OpMaxU64{});
+  const uint64_t m2 = __ballot(b2 != 0 && k2 == b2);
+  const uint32_t cn = wreduce(dc, OpAdd32{});
+  if (lane == 0) {
+    TcInit ti;
+    ti.b1 = b1;
+    ti.b2 = b2;
+    ti.s1 = s1i;
+    ti.s2 = m2 ? __builtin_ctzll(m2) : -1;
+    ti.cnt = cn;
+    ti.pad = 0;
+    reinterpret_cast<TcInit*>(a.tc_init)[q] = ti;
+  }
+}
+
 // Per-pod running maxima over the columns.
 struct TcTop {
   uint64_t b1, b2;
@@ -265,9 +366,10 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
   static_assert(QS <= KSG_BATCH_MAX, "pods per batch");
   extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
   __shared__ ksg_profile s_prof;
-  __shared__ int32_t s_clist[QS];
+  __shared__ int32_t s_clist[2 * QS];   // carried + this batch's slots
   __shared__ ksg_result s_res[QS];
   __shared__ __attribute__((aligned(16))) TcU s_u[QS];
+  __shared__ uint8_t s_touched[2 * QS];   // two-batch window: slot assumed onto in this batch
 
   const int lane = threadIdx.x, tid = lane;
   const DevCluster& c = a.c;
@@ -279,7 +381,8 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
   ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
   int32_t* s_prog = s_dyn + cm_words + nb * POD_WORDS;
   int64_t* s_slot = reinterpret_cast<int64_t*>(s_dyn + ((cm_words + nb * POD_WORDS + a.prog_len + 3) & ~3));
-  uint32_t* s_col = reinterpret_cast<uint32_t*>(s_slot + (size_t)nb * SL::STRIDE);
+  const int nslots = nb + (a.carry ? a.k_extra : 0);   // carried (<= the previous batch) + this batch's
+  uint32_t* s_col = reinterpret_cast<uint32_t*>(s_slot + (size_t)nslots * SL::STRIDE);
 
   for (int i = lane; i < cm_words; i += 64) s_cmask[i] = 0;
   for (int i = lane; i < nb * POD_WORDS; i += 64)
@@ -307,27 +410,18 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
     const int qq = q < nb ? q : 0;
     const ksg_pod& p = s_pods[qq];
     const P1Stats s1 = a.p1[qq];
-    TcPod& h = hp[i];
-    uint32_t mk = 0;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      h.req[r] = r < R ? p.req[r] : 0;
-      const bool chk = r < R && h.req[r] > 0 && !(r >= 3 && ((prof.fit_ignored_res >> r) & 1u));
-      mk |= chk ? 1u << r : 0u;
-    }
-    if (fit_filter_on && !((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u)) mk |= 1u << 4;
-    h.mask = mk;
-    h.rc = (int32_t)p.req[KSG_RES_CPU];
-    h.rm = (int32_t)(p.req[KSG_RES_MEM] >> 20);
-    h.nzc = (int32_t)p.nz_cpu;
-    h.nzm = (int32_t)(p.nz_mem >> 20);
+    hp[i] = tc_pod(p, prof, s1, fit_filter_on, R);
     const uint32_t smask = prof.score_mask & ~p.score_skip;
-    h.wfit = (smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? (int32_t)prof.weight[KSG_PL_NODE_RESOURCES_FIT] : 0;
-    h.wba = (smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? (int32_t)prof.weight[KSG_PL_BALANCED_ALLOCATION] : 0;
-    h.mt = s1.mt;
-    h.ma = s1.ma;
     tc_top_init(tp[i]);
     cnt[i] = 0;
+    if (a.carry && q < nb) {   // the previous batch's columns (ksg_tcol_carry)
+      const TcInit ti = reinterpret_cast<const TcInit*>(a.tc_init)[q];
+      tp[i].b1 = ti.b1;
+      tp[i].b2 = ti.b2;
+      tp[i].s1 = ti.s1;
+      tp[i].s2 = ti.s2;
+      cnt[i] = ti.cnt;
+    }
     if (q < nb) {
       TcU u;
 #pragma unroll
@@ -354,13 +448,35 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
   __syncthreads();
 
   int nc = 0;   // |D|, uniform
+  if (a.carry) {   // the previous batch's nodes: live rows, columns from ksg_tcol_carry
+    nc = *a.carry_n;
+    for (int t = lane; t < nc * SW; t += 64) {
+      const int i = t / SW, w = t - i * SW;
+      s_slot[(size_t)i * SL::STRIDE + w] = slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, w, R, a.carry[i]), w, R);
+    }
+    for (int t = lane; t < nc; t += 64) {
+      const int d = a.carry[t];
+      s_clist[t] = d;
+      atomicOr(&s_cmask[d >> 5], 1u << (d & 31));
+    }
+    for (int x = lane; x < nc * QS; x += 64) s_col[x] = a.tc_colinit[x];
+  }
+  for (int t = lane; t < 2 * QS; t += 64) s_touched[t] = 0;
+  __syncthreads();
   // Loop-carried loads are double-buffered (A/B by step parity, the loop
   // unrolled by two): a register copy of a load still in flight would wait
   // for it.  T_{k+1} is loaded a step ahead; T_0's first entry is pod 0's best node.
   uint64_t tA = nb > 1 ? a.top[(size_t)KSG_BATCH_MAX + lane] : 0;   // T_1
   uint64_t tB = 0;
-  uint64_t bu = s_u[0].K > 0 ? a.top[0] : 0;
+  uint64_t bu = 0;
   bool bu_full = false;
+  {
+    const uint64_t t0 = a.top[lane];
+    const int K0 = s_u[0].K;
+    const uint64_t m = __ballot(lane < K0 && !changed(key_node(t0)));
+    bu = m ? readlane64(t0, __builtin_ctzll(m)) : 0;
+    bu_full = m == 0 && K0 > 64;
+  }
   int spec = bu ? key_node(bu) : -1;
   TcFetch<P> fA = tc_fetch<P>(a, plan, lane, spec >= 0 ? spec : 0);
   TcFetch<P> fB = fA;
@@ -371,16 +487,21 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
   (void)tid;
   // one step: decide pod k, assume it, prefetch for pod k + 1 into (tnext, fnext),
   // evaluate the new column for the pods after k
-  auto step = [&](const int k, uint64_t& tcur, uint64_t& tnext, TcFetch<P>& fc, TcFetch<P>& fnext) {
+  // pod k's record is read a step ahead (double-buffered like the loads)
+  TcU uA = s_u[0], uB = uA;
+  auto step = [&](const int k, uint64_t& tcur, uint64_t& tnext, TcFetch<P>& fc, TcFetch<P>& fnext, const TcU& u,
+                  TcU& unext) {
     KSG_STAMP(0);
-    const TcU u = s_u[k];
     const int ki = k >> 6, kl = k & 63;
     const bool more = k + 1 < nb;
-    const int K1 = more ? s_u[k + 1].K : 0;
+    unext = s_u[more ? k + 1 : k];
+    const int K1 = more ? unext.K : 0;
     const uint64_t t64a = tcur;
     // T_{k+2}, consumed at the top of the next step (vmcnt counts in issue
     // order: node spec's values, issued at the end of this step, come after it)
-    tnext = k + 2 < nb ? a.top[(size_t)(k + 2) * KSG_BATCH_MAX + lane] : 0;
+    // (unconditional, clamped: a load issued on one path only makes the
+    // compiler's vmcnt path-dependent, i.e. vmcnt(0) at the next wait)
+    tnext = a.top[(size_t)min(k + 2, nb - 1) * KSG_BATCH_MAX + lane];
     // flags of T_{k+1} against D before this pod (LDS reads overlap the decision)
     const int tn = key_node(t64a);
     const bool pre_chg = lane < K1 ? changed(tn) : true;
@@ -523,6 +644,7 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
                               : lane == SL::PODS ? 1 : 0;
     if (added && selected != spec) fc = tc_fetch<P>(a, plan, lane, selected);   // dependent loads (rare)
     if (selected >= 0) {
+      if (lane == 0) s_touched[slot] = 1;
       int64_t* row = s_slot + (size_t)slot * SL::STRIDE;
       if (added) {
         const int64_t col_val = slot_word_value<4, true>(fc.col, lane, R);
@@ -563,11 +685,11 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
     KSG_STAMP(3);
 
     // ---- pod k + 1's best unchanged node and its loads; the next records -------
-    if (more) {
-      const bool tf = pre_chg || tn == selected;
+    {   // (issued on every step, see tnext)
+      const bool tf = !more || pre_chg || tn == selected;
       const uint64_t m = __ballot(!tf);
       bu = m ? readlane64(t64a, __builtin_ctzll(m)) : 0;
-      bu_full = m == 0 && K1 > 64;
+      bu_full = more && m == 0 && K1 > 64;
       spec = bu ? key_node(bu) : -1;
       fnext = tc_fetch<P>(a, plan, lane, spec >= 0 ? spec : 0);
     }
@@ -621,8 +743,8 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
 
   };
   for (int k = 0; k < nb; k += 2) {
-    step(k, tA, tB, fA, fB);
-    if (k + 1 < nb) step(k + 1, tB, tA, fB, fA);
+    step(k, tA, tB, fA, fB, uA, uB);
+    if (k + 1 < nb) step(k + 1, tB, tA, fB, fA, uB, uA);
   }
 #ifdef KSG_STAMPS
   if (lane == 0 && a.stamps)
@@ -642,4 +764,14 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
     if (a.results) a.results[a.out0 + i] = s_res[i];
   }
   for (int i = lane; i < 2 * nb; i += 64) a.pmax[i] = 0;   // ready for the next batch's phase 1
+  if (a.carry_out) {   // the nodes this batch touched, in slot order, for the next batch
+    int base = 0;
+    for (int b = 0; b < nc; b += 64) {
+      const bool t = b + lane < nc && s_touched[b + lane];
+      const uint64_t m = __ballot(t);
+      if (t) a.carry_out[base + __popcll(m & ((1ull << lane) - 1))] = s_clist[b + lane];
+      base += __popcll(m);
+    }
+    if (lane == 0) *a.carry_out_n = base;
+  }
 }

@@ -88,6 +88,8 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
         return bytes_per_eval + 12
     if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
         return 8
+    if name == "ksg_tcol_carry":
+        return 140   # live columns of a carried node (128 B) + record and static (12 B) per (pod, carried node)
     if name == "ksg_batch_transpose":
         return 24   # 12 B read + 12 B written per (pod, node)
     if name in ("ksg_batch_phase2", "ksg_batch_phase2s", "ksg_batch_phase2p", "ksg_batch_phase2t"):

@@ -23,7 +23,8 @@ MODES = [("pipe", {"KSG_BATCH_MODE": "pipe"}), ("pipe-nowindow", {"KSG_BATCH_MOD
          ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
          ("slot-256", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "256"}),
          ("window", {"KSG_BATCH_MODE": "window"}), ("window-64", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "64"}),
-         ("tcol", {"KSG_BATCH_MODE": "tcol"}), ("tcol-64", {"KSG_BATCH_MODE": "tcol", "KSG_SLOT_BLOCK": "64"})]
+         ("tcol", {"KSG_BATCH_MODE": "tcol"}), ("tcol-nowindow", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0"}),
+         ("tcol-nowindow-64", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"})]
 
 
 def main():

@@ -1,7 +1,9 @@
 """GPU parity of every phase-2 variant of the batched placement path
 (KSG_BATCH_MODE): "slot" (default) at each block size,
-"tcol" (the transposed walk, ksched_phase2t.h, at 128- and 64-pod batches;
-the slot walk where its scope check fails), "window" (the slot walk inside the two-stream pipeline with the two-batch
+"tcol" (the transposed walk, ksched_phase2t.h: in the two-stream
+pipeline with the previous batch's nodes as carried columns, serialised with
+timing on, and without the window at 128- and 64-pod batches; the slot walk
+where its scope check fails), "window" (the slot walk inside the two-stream pipeline with the two-batch
 window; also without the window, at 64-pod batches and with per-kernel
 timing on, which runs the same arithmetic without overlap), "pipe" (the
 same variations), "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
@@ -34,7 +36,9 @@ MODES = {"pipe": ("pipe", {}), "pipe64": ("pipe", {"KSG_SLOT_BLOCK": 64}),
          "slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
          "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
          "topset": ("topset", {}), "scan": ("scan", {}),
-         "tcol": ("tcol", {}), "tcol64": ("tcol", {"KSG_SLOT_BLOCK": 64})}
+         "tcol": ("tcol", {}), "tcol-timed": ("tcol", {"_timing": 1}),
+         "tcol-nowindow": ("tcol", {"KSG_PIPE_WINDOW": 0}),
+         "tcol-nowindow64": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 64})}
 
 
 @pytest.fixture(scope="module", params=list(MODES))
