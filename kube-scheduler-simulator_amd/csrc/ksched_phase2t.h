@@ -489,8 +489,15 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
   // evaluate the new column for the pods after k
   // pod k's record is read a step ahead (double-buffered like the loads)
   TcU uA = s_u[0], uB = uA;
+  // T_{k+1}'s changed flags, a step ahead (pA: T_1 against the carried nodes)
+  bool pA = false, pB = false;
+  {
+    const int t1 = key_node(tA);
+    pA = changed((unsigned)t1 < (unsigned)N ? t1 : 0);
+  }
+  int prev_sel = -1;
   auto step = [&](const int k, uint64_t& tcur, uint64_t& tnext, TcFetch<P>& fc, TcFetch<P>& fnext, const TcU& u,
-                  TcU& unext) {
+                  TcU& unext, const bool pcur, bool& pnext) {
     KSG_STAMP(0);
     const int ki = k >> 6, kl = k & 63;
     const bool more = k + 1 < nb;
@@ -504,7 +511,9 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
     tnext = a.top[(size_t)min(k + 2, nb - 1) * KSG_BATCH_MAX + lane];
     // flags of T_{k+1} against D before this pod (LDS reads overlap the decision)
     const int tn = key_node(t64a);
-    const bool pre_chg = lane < K1 ? changed(tn) : true;
+    // T_{k+1}'s changed flags against D before pod k - 1 were read at the end of
+    // the previous step (pcur); pods k - 1 and k are added below
+    const bool pre_chg = lane >= K1 || pcur || tn == prev_sel;
     // ---- decide pod k ---------------------------------------------------------
     // lazy rescan: pod k's best column is unknown (rare)
     {
@@ -739,12 +748,17 @@ __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {
         if (act) tp[i] = x;
       }
     }
+    {   // T_{k+2}'s changed flags against D up to this pod (LDS, used two steps on)
+      const int t2 = key_node(tnext);
+      pnext = changed((unsigned)t2 < (unsigned)N ? t2 : 0);
+    }
+    prev_sel = selected;
     KSG_STAMP(6);
 
   };
   for (int k = 0; k < nb; k += 2) {
-    step(k, tA, tB, fA, fB, uA, uB);
-    if (k + 1 < nb) step(k + 1, tB, tA, fB, fA, uB, uA);
+    step(k, tA, tB, fA, fB, uA, uB, pA, pB);
+    if (k + 1 < nb) step(k + 1, tB, tA, fB, fA, uB, uA, pB, pA);
   }
 #ifdef KSG_STAMPS
   if (lane == 0 && a.stamps)
