@@ -388,6 +388,20 @@ def main():
             roof = None
         if roof is None:   # no per-kernel timing: whole step as one launch
             roof = metrics.roofline(bpe, P * len(nodes), kms)
+        # Phase-2 kernels decide a batch of pods over every node: price a launch
+        # by SURVEY §8(d)'s bytes per node-eval x the node-evals it decides
+        # (batch pods x nodes), as the round-1 verdict recomputed it; the
+        # changed-slot figure the kernel stats count stays beside it.
+        if roof.get("kernel") in ("ksg_batch_phase2s", "ksg_batch_phase2t", "ksg_batch_phase2p", "ksg_batch_phase2"):
+            row = next((k for k in roof.get("kernels", []) if k["name"] == roof["kernel"]), None)
+            if row and row["calls"] and row["avg_ms"] > 0:
+                per_launch = bpe * P * len(nodes) / row["calls"]
+                roof["achieved_changed_slot_bytes"] = roof["achieved"]
+                roof["achieved"] = per_launch / (row["avg_ms"] * 1e-3) / 1e9
+                roof["frac"] = roof["achieved"] / roof["peak"]
+                roof["bytes_per_launch"] = per_launch
+                roof["unit_basis"] = ("SURVEY 8(d) bytes per node-eval x node-evals decided per launch "
+                                      "(batch pods x nodes)")
         roof["step"] = metrics.roofline(bpe, P * len(nodes), kms)
         roof["step"]["kernel_ms"] = kms
         # HBM bytes per launch of the dominant kernel from the committed PMC
@@ -395,7 +409,7 @@ def main():
         # + WRITE_SIZE per dispatch, gfx950-corrected), null when not collected
         roof["traffic"], roof["traffic_source"] = pmc_traffic(roof.get("kernel"), "pmc_config2.json")
         roof["bytes_per_node_eval"] = bpe
-        roof["node_evals_per_launch"] = P * len(nodes)
+        roof["node_evals_per_step"] = P * len(nodes)
         out = {
             "metric": "pods scheduled/sec @5k nodes, default plugins; node-evals/sec; % HBM peak",
             "value": pods_per_s, "unit": "pods/s", "n_gpus": world, "steps": args.steps,
