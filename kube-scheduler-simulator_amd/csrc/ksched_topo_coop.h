@@ -75,7 +75,7 @@ struct CoopAcc {    // atomics fallback for large histograms
   int32_t hist[KSG_HIST_MAX];
 };
 
-// (ksched_sweep.h: gld(), arrive_and_wait() of the replica sweep)
+// gld / gst / gadd / gor and arrive_and_wait_sc1: ksched_sweep.h
 
 #ifdef KSG_STAMPS
 #define KSG_CSTAMP(seg)                                                     \
@@ -117,46 +117,8 @@ struct CoopArgs {
 // loads, the other waves load after the workgroup barrier that lane joins.
 // No release (buffer_wbl2) and no acquire (buffer_inv): the round-1 barrier
 // paid both, ~8-9 k cycles each (profiles/r1/stamps_topo_coop.txt).
-template <class T>
-__device__ __forceinline__ T gld(const T* p) {   // agent-scope (sc1) global load
-  return __hip_atomic_load((__attribute__((address_space(1))) T*)(const_cast<T*>(p)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-template <class T, class V>
-__device__ __forceinline__ void gst(T* p, V v) {   // agent-scope (sc1, write-through) global store
-  __hip_atomic_store((__attribute__((address_space(1))) T*)p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void gadd(int32_t* p, int32_t v) {   // agent-scope global atomic add
-  __hip_atomic_fetch_add((__attribute__((address_space(1))) int32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gor(int32_t* p, int32_t v) {    // agent-scope global atomic or
-  __hip_atomic_fetch_or((__attribute__((address_space(1))) int32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __device__ __forceinline__ bool coop_barrier(unsigned* bar, unsigned* timeout, int G, unsigned& target) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 stores and atomics are done
-  __syncthreads();
-  target += (unsigned)G;
-  __shared__ int s_timeout;
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)bar, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    int to = 0;
-    while (gld(bar) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 26) || gld(timeout)) {
-        gst(timeout, 1u);
-        to = 1;
-        break;
-      }
-    }
-    s_timeout = to;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only: loads stay below the poll
-  __syncthreads();
-  return s_timeout == 0;
+  return arrive_and_wait_sc1(bar, timeout, G, target);
 }
 
 // PodTopologySpread with one soft constraint: the per-node count m of
