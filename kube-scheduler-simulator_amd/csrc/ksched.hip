@@ -2368,7 +2368,8 @@ struct ksg_ctx {
   ksg_profile* d_preprof = nullptr;
   // chip-wide topology path buffers (lazily allocated)
   CoopAcc* d_coop_acc = nullptr;
-  unsigned* d_coop_flags = nullptr;   // [0] barrier counter, [4] timeout
+  unsigned* d_coop_flags = nullptr;   // [4] timeout
+  unsigned* d_coop_wgflags = nullptr; // [256][32] per-workgroup barrier flags
   CoopPart* d_coop_parts = nullptr;   // [256] per-workgroup partials
   int32_t* d_coop_phist = nullptr;    // [256][kCoopPHist] per-workgroup partial histograms
   uint64_t* d_coop_srec = nullptr;    // [kCoopBatch][N] static records of the current batch
@@ -2479,6 +2480,7 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_stamps = nullptr;
   ctx->d_coop_acc = nullptr;
   ctx->d_coop_flags = nullptr;
+  ctx->d_coop_wgflags = nullptr;
   ctx->d_coop_parts = nullptr;
   ctx->d_coop_phist = nullptr;
   ctx->d_coop_srec = nullptr;
@@ -3419,7 +3421,8 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   if (G > occ * cus) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: grid exceeds co-resident workgroups");
   if (!ctx->d_coop_acc) {
     if ((rc = dalloc(ctx, &ctx->d_coop_acc, 2))) return rc;
-    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [0] barrier (own 16 B), [4] timeout
+    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [4] timeout
+    if ((rc = dalloc(ctx, &ctx->d_coop_wgflags, (size_t)256 * 32))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_parts, 256))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_phist, (size_t)256 * kCoopPHist))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_srec, (size_t)kCoopBatch * N))) return rc;
@@ -3437,7 +3440,7 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   a.parts = ctx->d_coop_parts;
   a.phist = ctx->d_coop_phist;
   a.acc = ctx->d_coop_acc;
-  a.bar = ctx->d_coop_flags;
+  a.bar = ctx->d_coop_wgflags;
   a.timeout = ctx->d_coop_flags + 4;
   SweepArgs sa{};
   sa.c = ctx->c;
@@ -3466,7 +3469,7 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     a.first = first + off;
     a.count = nb;
     a.out0 = off;
-    HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 16, ctx->stream));   // barrier counter (timeout kept)
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_wgflags, 0, sizeof(unsigned) * 32 * G, ctx->stream));   // barrier flags
     HIPC(ctx, hipMemsetAsync(ctx->d_coop_acc, 0, 2 * sizeof(CoopAcc), ctx->stream));
     // cooperative launch: the runtime guarantees the G workgroups are
     // co-resident (or refuses the launch), which the grid barrier needs

@@ -103,7 +103,7 @@ struct CoopArgs {
   CoopPart* parts;             // [G]
   int32_t* phist;              // [G][kCoopPHist]
   CoopAcc* acc;                // [2], zeroed before the launch
-  unsigned* bar;               // arrival counter, zeroed before the launch
+  unsigned* bar;               // per-workgroup barrier flags [G][32] (one 128-B line each), zeroed before the launch
   unsigned* timeout;           // set when a barrier poll gave up
   unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
 };
@@ -117,8 +117,37 @@ struct CoopArgs {
 // loads, the other waves load after the workgroup barrier that lane joins.
 // No release (buffer_wbl2) and no acquire (buffer_inv): the round-1 barrier
 // paid both, ~8-9 k cycles each (profiles/r1/stamps_topo_coop.txt).
-__device__ __forceinline__ bool coop_barrier(unsigned* bar, unsigned* timeout, int G, unsigned& target) {
-  return arrive_and_wait_sc1(bar, timeout, G, target);
+// Grid barrier on per-workgroup flags: each workgroup's lane 0 stores the
+// epoch into its own 128-byte line (sc1, after every wave's drain and the
+// workgroup barrier), and wave 0 polls all G flags with one sc1 load per lane
+// (G <= 256).  No atomic on a shared counter: 59 workgroups adding to one
+// word serialise at the memory side (the guide's "Valid forms" row 1, sharded).
+__device__ __forceinline__ bool coop_barrier(unsigned* flags, unsigned* timeout, int G, unsigned& epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 stores and atomics are done
+  __syncthreads();
+  epoch += 1;
+  __shared__ int s_to;
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    if (tid == 0) gst(&flags[(size_t)blockIdx.x * 32], epoch);
+    unsigned spins = 0;
+    int to = 0;
+    for (;;) {
+      bool ok = true;
+      for (int l = tid; l < G; l += 64) ok = ok && gld(&flags[(size_t)l * 32]) >= epoch;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26) || gld(timeout)) {
+        if (tid == 0) gst(timeout, 1u);
+        to = 1;
+        break;
+      }
+    }
+    if (tid == 0) s_to = to;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only: loads stay below the poll
+  __syncthreads();
+  return s_to == 0;
 }
 
 // PodTopologySpread with one soft constraint: the per-node count m of
