@@ -86,6 +86,10 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
         return bytes_per_eval
     if name == "ksg_batch_phase1":
         return bytes_per_eval + 12
+    if name == "ksg_capture_eval":   # node columns on the post-batch state + status word and record written
+        return bytes_per_eval + 12
+    if name == "ksg_capture_norm":   # record read, normalised row and total written (one scored row at least)
+        return 24
     if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
         return 8
     if name == "ksg_tcol_carry":
