@@ -2370,6 +2370,8 @@ struct ksg_ctx {
   CoopAcc* d_coop_acc = nullptr;
   unsigned* d_coop_flags = nullptr;   // [4] timeout
   unsigned* d_coop_wgflags = nullptr; // [256][32] per-workgroup barrier flags
+  int coop_pmode = 0;                 // env KSG_COOP_PMODE: 0 merge with atomics (33.3 k vs 32.1 k pods/s on
+                                      // config 3), 1 every workgroup folds every partial slot
   CoopPart* d_coop_parts = nullptr;   // [256] per-workgroup partials
   int32_t* d_coop_phist = nullptr;    // [256][kCoopPHist] per-workgroup partial histograms
   uint64_t* d_coop_srec = nullptr;    // [kCoopBatch][N] static records of the current batch
@@ -3441,6 +3443,7 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   a.phist = ctx->d_coop_phist;
   a.acc = ctx->d_coop_acc;
   a.bar = ctx->d_coop_wgflags;
+  a.pmode = ctx->coop_pmode;
   a.timeout = ctx->d_coop_flags + 4;
   SweepArgs sa{};
   sa.c = ctx->c;
@@ -3694,6 +3697,7 @@ int ksg_open(int device, ksg_ctx** out) {
   }
   if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
   if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
+  if (const char* f = getenv("KSG_COOP_PMODE")) ctx->coop_pmode = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : m == "slot" ? 2 : m == "tcol" ? 5 : 4;

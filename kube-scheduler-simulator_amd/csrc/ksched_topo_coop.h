@@ -105,6 +105,7 @@ struct CoopArgs {
   CoopAcc* acc;                // [2], zeroed before the launch
   unsigned* bar;               // per-workgroup barrier flags [G][32] (one 128-B line each), zeroed before the launch
   unsigned* timeout;           // set when a barrier poll gave up
+  int32_t pmode;               // 1: partial-slot histograms folded by every workgroup; 0: atomics into acc
   unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
 };
 
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     __syncthreads();
     const bool ok = s_t.ok;
     const int words = ok ? s_t.words : 0;
-    const bool pmode = words <= kCoopPHist && words * G <= 32768;
+    const bool pmode = a.pmode && words <= kCoopPHist && words * G <= 32768;
     for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
     if (pmode) {   // word kinds of the partial slot (fold_all)
       for (int w = tid; w < words; w += BLOCK) {

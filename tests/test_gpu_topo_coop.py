@@ -17,9 +17,21 @@ native = pkg("native")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def gpu(built):
-    return native.Engine(device=0)
+@pytest.fixture(scope="module", params=[0, 1], ids=["atomic-merge", "partial-slots"])
+def gpu(built, request):
+    """Both histogram hand-offs (KSG_COOP_PMODE, read at ksg_open): 0 (default)
+    merges each workgroup's partial histograms into an accumulator with
+    agent-scope atomics, 1 folds every workgroup's partial slot."""
+    import os
+    old = os.environ.get("KSG_COOP_PMODE")
+    os.environ["KSG_COOP_PMODE"] = str(request.param)
+    try:
+        return native.Engine(device=0)
+    finally:
+        if old is None:
+            del os.environ["KSG_COOP_PMODE"]
+        else:
+            os.environ["KSG_COOP_PMODE"] = old
 
 
 @pytest.fixture(scope="module")
