@@ -2395,7 +2395,7 @@ struct ksg_ctx {
   // through the two-batch window; the pipelined two-version walk is exact but
   // measured slower: profiles/r2/phase2_modes.log)
   int batch_mode = 4;
-  int slot_block = 128;  // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (128: 1-2 % faster end to end than 256)
+  int slot_block = 64;   // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (64: the window walk at 64-pod batches, 2 waves, 416 k vs 408 k pods/s at 128, profiles/r2/phase2_window_blocks.log)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
   bool timing = false;

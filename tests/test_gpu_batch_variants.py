@@ -1,5 +1,5 @@
 """GPU parity of every phase-2 variant of the batched placement path
-(KSG_BATCH_MODE): "slot" (default) at each block size,
+(KSG_BATCH_MODE): "slot" at each block size,
 "tcol" (the transposed walk, ksched_phase2t.h: in the two-stream
 pipeline with the previous batch's nodes as carried columns, serialised with
 timing on, and without the window at 128- and 64-pod batches; the slot walk
@@ -32,12 +32,12 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs
 MODES = {"pipe": ("pipe", {}), "pipe64": ("pipe", {"KSG_SLOT_BLOCK": 64}),
          "pipe-nowindow": ("pipe", {"KSG_PIPE_WINDOW": 0}), "pipe-timed": ("pipe", {"_timing": 1}),
          "window": ("window", {}), "window-timed": ("window", {"_timing": 1}),
-         "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "window64": ("window", {"KSG_SLOT_BLOCK": 64}),
-         "slot": ("slot", {}), "slot64": ("slot", {"KSG_SLOT_BLOCK": 64}),
+         "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "window128": ("window", {"KSG_SLOT_BLOCK": 128}),
+         "slot": ("slot", {}), "slot128": ("slot", {"KSG_SLOT_BLOCK": 128}),
          "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
          "topset": ("topset", {}), "scan": ("scan", {}),
          "tcol": ("tcol", {}), "tcol-timed": ("tcol", {"_timing": 1}),
-         "tcol-nowindow": ("tcol", {"KSG_PIPE_WINDOW": 0}),
+         "tcol-nowindow": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 128}),
          "tcol-nowindow64": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 64})}
 
 
