@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KSG_ABI_VERSION 2
+#define KSG_ABI_VERSION 3
 
 #define KSG_OK 0
 #define KSG_E_INVALID (-1)     /* bad argument / inconsistent sizes            */

@@ -184,10 +184,31 @@ typedef struct ksg_pod_view {
 
 typedef struct ksg_plugin_view { const char* name; int32_t weight; } ksg_plugin_view;
 
+/* Extension points whose per-point plugin sets the evaluator models. */
+#define KSG_POINT_PREFILTER 0
+#define KSG_POINT_FILTER 1
+#define KSG_POINT_PRESCORE 2
+#define KSG_POINT_SCORE 3
+#define KSG_NPOINTS 4
+
+/* One extension point's configv1.PluginSet as ConvertForSimulator keeps it
+ * (plugins.go:177-186 applyPluginSet: enabled plugins renamed to XWrapped with
+ * their weights, disabled ones renamed except "*"; either spelling is
+ * accepted).  n_enabled = n_disabled = 0: the point is not configured and
+ * takes the MultiPoint expansion alone. */
+typedef struct ksg_plugin_set_view {
+  int32_t n_enabled;
+  const ksg_plugin_view* enabled;
+  int32_t n_disabled;
+  const char* const* disabled;
+} ksg_plugin_set_view;
+
 /* Profile 0 after ConvertForSimulator (plugins.go:174-197): MultiPoint plugins
  * in order (names with or without the "Wrapped" suffix), weights as written
- * (getScorePluginWeight maps 0 to 1, plugins.go:289-304), and the plugin args
- * the evaluator models (defaults: plugins_test.go:876-1000). */
+ * (getScorePluginWeight maps 0 to 1, plugins.go:289-304), the per-point sets
+ * (PreFilter / Filter / PreScore / Score), and the plugin args the evaluator
+ * models, as the plugin factories receive them decoded (defaults:
+ * plugins_test.go:876-1000). */
 typedef struct ksg_profile_view {
   int32_t n_plugins;
   const ksg_plugin_view* plugins;
@@ -204,7 +225,34 @@ typedef struct ksg_profile_view {
   int32_t ignore_preferred_terms_of_existing_pods;
   int32_t pts_system_defaulted;              /* PodTopologySpreadArgs.defaultingType == System */
   int32_t ba_skip_best_effort;
+  ksg_plugin_set_view points[KSG_NPOINTS];   /* indexed by KSG_POINT_* */
 } ksg_profile_view;
+
+/* The profile as the framework and the simulator's Store see it (derived by
+ * ksg_snapshot_new from ksg_profile_view):
+ *   order[KSG_POINT_*]  plugin ids each extension point runs, in order: the
+ *                       framework's expansion of MultiPoint into the point
+ *                       [upstream v1.32 expandMultiPointPlugins, TO VERIFY:
+ *                       DESIGN.md §9]: the point's own plugins that
+ *                       MultiPoint also lists, then the other MultiPoint
+ *                       plugins implementing the point and not disabled
+ *                       there, then the point's remaining plugins;
+ *   store_weight        getScorePluginWeight (plugins.go:289-304): Score
+ *                       enabled then MultiPoint enabled, a later entry
+ *                       replaces an earlier one, 0 -> 1; 0 = not in the map
+ *                       (the Store then records final = raw x 0).  This is
+ *                       the weight array ksg_annotate takes;
+ *   selection_weight    the framework's weight of each Score plugin in the
+ *                       weighted total (the point's own weight first);
+ *   normalize_mask      plugins with ScoreExtensions. */
+typedef struct ksg_profile_info {
+  int32_t n_order[KSG_NPOINTS];
+  int32_t order[KSG_NPOINTS][KSG_NPLUGINS];
+  int64_t store_weight[KSG_NPLUGINS];
+  int32_t selection_weight[KSG_NPLUGINS];
+  uint32_t normalize_mask;
+  int32_t pad;
+} ksg_profile_info;
 
 typedef struct ksg_snapshot ksg_snapshot;
 
@@ -215,6 +263,8 @@ typedef struct ksg_snapshot ksg_snapshot;
 #define KSG_CODE_SKIP 5
 
 int ksg_snapshot_new(const ksg_profile_view* profile, ksg_snapshot** out);
+/* The derived extension-point orders and the two weight maps (no device). */
+int ksg_snapshot_profile_info(ksg_snapshot* s, ksg_profile_info* out);
 int ksg_snapshot_free(ksg_snapshot* s);
 const char* ksg_snapshot_error(ksg_snapshot* s);
 

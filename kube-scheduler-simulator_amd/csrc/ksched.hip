@@ -2587,7 +2587,17 @@ int check_ready(ksg_ctx* ctx) {
   if (!ctx) return KSG_E_INVALID;
   if (!ctx->have_nodes || !ctx->have_wl || !ctx->have_prof)
     return fail(ctx, KSG_E_STATE, "profile, nodes and workload must be loaded first");
-  if (ctx->max_blob > KSG_BLOB_MAX) return fail(ctx, KSG_E_UNSUPPORTED, "pod program blob exceeds LDS budget");
+  return KSG_OK;
+}
+
+// Pods [first, first + count) are staged into LDS by the evaluating kernels:
+// each one's program blob must fit.  Checked per evaluated range, so one
+// oversized pod refuses only its own evaluations (commits read programs from
+// global memory and need no LDS).
+int check_blobs(ksg_ctx* ctx, int first, int count) {
+  for (int i = first; i < first + count; i++)
+    if (ctx->h_pods[i].blob_len > KSG_BLOB_MAX)
+      return fail(ctx, KSG_E_UNSUPPORTED, "pod " + std::to_string(i) + ": program blob exceeds the LDS budget");
   return KSG_OK;
 }
 
@@ -3493,6 +3503,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (first < 0 || count < 0 || first + count > ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod range");
+  if ((rc = check_blobs(ctx, first, count))) return rc;
   if ((rc = check_supported(ctx, ctx->prof, first, count))) return rc;
   if (count == 0) return KSG_OK;
   HIPC(ctx, hipSetDevice(ctx->device));
@@ -3660,6 +3671,28 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
   ctx->prog_used = used;
   ctx->max_blob = max_blob;
   return KSG_OK;
+}
+
+// Existing pods' required anti-affinity templates matching the preemptor
+// (the m_anti list of its InterPodAffinity program, parse_topo's layout);
+// bounds-checked against the host pool, INT32_MAX when malformed.
+int32_t preempt_n_ma(const ksg_ctx* ctx, const ksg_pod& p) {
+  if (p.ipa < 0) return 0;
+  const std::vector<int32_t>& P = ctx->h_prog;
+  const int64_t end = std::min<int64_t>((int64_t)p.blob + p.blob_len, (int64_t)P.size());
+  int64_t w = p.ipa;
+  auto at = [&](int64_t i) -> int64_t { return i >= 0 && i < end ? P[i] : -1; };
+  const int64_t na = at(w);
+  if (na < 0) return 0x7fffffff;
+  w += 3 + na;
+  const int64_t nn = at(w++);
+  if (nn < 0) return 0x7fffffff;
+  w += 2 * nn;
+  const int64_t np = at(w++);
+  if (np < 0) return 0x7fffffff;
+  w += 3 * np;
+  const int64_t nm = at(w);
+  return nm < 0 ? 0x7fffffff : (int32_t)nm;
 }
 
 int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, int off) {
@@ -3926,6 +3959,7 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
   if (rc) return rc;
   if (pod < 0 || pod >= ctx->n_pods || n_cand < 0 || (n_cand > 0 && (!cand_node || !vic_off || !fits)))
     return fail(ctx, KSG_E_INVALID, "preempt arguments");
+  if ((rc = check_blobs(ctx, pod, 1))) return rc;
   if (n_cand == 0) return KSG_OK;
   const int32_t nv = vic_off[n_cand];
   if (vic_off[0] != 0 || nv < 0 || (nv > 0 && (!vic_pod || !victim)))
@@ -3961,6 +3995,11 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
   const bool topo = needs_topo(ctx, ctx->prof, pod, 1);
   int32_t topo_ok = 1;
   if (topo) {
+    // refuse on the host what the dry run cannot hold, before any launch
+    if ((rc = check_supported(ctx, ctx->prof, pod, 1))) return rc;
+    if (preempt_n_ma(ctx, p) > kPreMaxMAnti)
+      return fail(ctx, KSG_E_UNSUPPORTED, "preemption: more than " + std::to_string(kPreMaxMAnti) +
+                                              " existing anti-affinity templates match the preemptor");
     if (!ctx->d_pretopo) {
       if ((rc = dalloc(ctx, &ctx->d_pretopo, 1))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_preprof, 1))) return rc;
@@ -3991,6 +4030,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   if (rc) return rc;
   if (!profiles || n_replicas <= 0 || first < 0 || count < 0 || first + count > ctx->n_pods || !placements)
     return fail(ctx, KSG_E_INVALID, "replica arguments");
+  if ((rc = check_blobs(ctx, first, count))) return rc;
   for (int r = 0; r < n_replicas; r++)
     if ((rc = check_supported(ctx, profiles[r], first, count))) return rc;
   HIPC(ctx, hipSetDevice(ctx->device));

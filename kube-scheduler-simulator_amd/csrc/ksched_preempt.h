@@ -72,13 +72,17 @@ __global__ __launch_bounds__(BLOCK) void ksg_preempt_prepass(DevCluster c, DevSt
     s_t.ipa_skip_filter = !s_g.ipa || (ma == 0 && s_g.n_aff == 0 && s_g.n_anti == 0);
     for (int i = 0; i < kMaxHard; i++) { s_t.hard_min[i] = BIG; s_t.hard_dom[i] = 0; s_m2[i] = BIG; s_c1[i] = 0; }
     s_t.aff_total = 0;
+    // over the limits: nothing below touches the histograms (s_t.words may
+    // exceed KSG_HIST_MAX then) and the host reports UNSUPPORTED
+    s_t.ok = s_t.ok && s_g.n_ma <= kPreMaxMAnti;
+    if (!s_t.ok) s_t.words = 0;
   }
   __syncthreads();
   for (int i = tid; i < s_t.words; i += BLOCK) s_hist[i] = 0;
   const PodView v = make_view(c, s_prof, p, s_blob, prog, true);
   const TopoProg& g = s_g;
   const int32_t* cnt = st.cnt;
-  const bool ok = s_t.ok && g.n_ma <= kPreMaxMAnti;
+  const bool ok = s_t.ok;
   __syncthreads();
   if (ok) {
     long long lmin[kMaxHard], laff = 0;
@@ -254,6 +258,11 @@ __global__ __launch_bounds__(256) void ksg_preempt_topo(DevCluster c, DevState s
   __syncthreads();
   const int k = blockIdx.x * 256 + tid;
   if (k >= n_cand) return;
+  if (!topo->ok) {   // the prepass refused the preemptor: PreDelta's arrays cannot hold its terms
+    fits[k] = 0;
+    for (int i = off[k]; i < off[k + 1]; i++) victim[i] = 0;
+    return;
+  }
   const PodView v = make_view(c, prof, p, s_blob, prog, true);
   const TopoProg& g = s_g;
   const TopoShared& t = s_t;

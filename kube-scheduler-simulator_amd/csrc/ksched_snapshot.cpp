@@ -434,6 +434,10 @@ struct Profile {
   int32_t hard_weight;
   bool ignore_pref, pts_system, ba_skip_be;
   std::vector<int> enabled;   // plugin ids in MultiPoint order
+  // derived (profile.py Profile._expand / weights / selection_weights)
+  std::vector<int> order[KSG_NPOINTS];   // per extension point, run order
+  int64_t store_w[KSG_NPLUGINS] = {};    // getScorePluginWeight, 0 = absent
+  int32_t sel_w[KSG_NPLUGINS] = {};      // the framework's Score weights, 0 = absent
 };
 
 }  // namespace
@@ -1254,25 +1258,105 @@ void encode_all(ksg_snapshot* s) {
 }
 
 // ---- profile ---------------------------------------------------------------------
+std::string plain_name(std::string n) {
+  if (n.size() > 7 && n.compare(n.size() - 7, 7, "Wrapped") == 0) n.resize(n.size() - 7);
+  return n;
+}
+int plugin_id(const std::string& plain) {
+  for (int k = 0; k < KSG_NPLUGINS; k++)
+    if (plain == kPluginNames[k]) return k;
+  return -1;
+}
+bool non_eval(const std::string& plain) {
+  for (const char* n : kNonEval)
+    if (plain == n) return true;
+  return false;
+}
+
+// The framework's plugin list of extension point `pt` (extension index ext):
+// profile.py Profile._expand [upstream v1.32 expandMultiPointPlugins, TO
+// VERIFY, DESIGN.md §9].  Returns false with a message for a configuration
+// the framework (or the simulator's registry, plugins.go:39-60) refuses.
+bool expand_point(const ksg_plugin_set_view& ps, const std::vector<int>& enabled, int ext, std::vector<int>& out,
+                  std::string& err) {
+  std::vector<int> multi;
+  for (int pid : enabled)
+    if (kExt[pid][ext]) multi.push_back(pid);
+  if (ps.n_enabled <= 0 && ps.n_disabled <= 0) {
+    out = multi;
+    return true;
+  }
+  std::vector<int> own;
+  for (int32_t i = 0; i < ps.n_enabled; i++) {
+    const std::string n = plain_name(S(ps.enabled[i].name));
+    const int pid = plugin_id(n);
+    if (pid < 0) {
+      err = "plugin " + n + " is not an in-tree Filter/Score plugin";
+      return false;
+    }
+    if (!kExt[pid][ext]) {
+      err = "plugin " + n + " does not extend this point";
+      return false;
+    }
+    if (std::find(own.begin(), own.end(), pid) != own.end()) {
+      err = "plugin " + n + " listed twice";
+      return false;
+    }
+    own.push_back(pid);
+  }
+  bool all = false;
+  std::set<int> off;
+  for (int32_t i = 0; i < ps.n_disabled; i++) {
+    const std::string n = S(ps.disabled[i]);
+    if (n == "*") all = true;
+    const int pid = plugin_id(plain_name(n));
+    if (pid >= 0) off.insert(pid);
+  }
+  out.clear();
+  if (all) {
+    out = own;
+    return true;
+  }
+  auto in = [](const std::vector<int>& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); };
+  for (int pid : own)
+    if (in(multi, pid)) out.push_back(pid);
+  for (int pid : multi)
+    if (!off.count(pid) && !in(own, pid)) out.push_back(pid);
+  for (int pid : own)
+    if (!in(multi, pid)) out.push_back(pid);
+  return true;
+}
+
+// Orders of the four modelled points and the two weight maps.
+bool derive_profile(Profile& p, const ksg_profile_view* pv, std::string& err) {
+  static const int kExtOf[KSG_NPOINTS] = {0, 1, 2, 3};   // prefilter, filter, prescore, score
+  for (int pt = 0; pt < KSG_NPOINTS; pt++)
+    if (!expand_point(pv->points[pt], p.enabled, kExtOf[pt], p.order[pt], err)) return false;
+  // Score.Enabled then MultiPoint.Enabled (plugins.go:291-292)
+  std::vector<std::pair<std::string, int32_t>> seq;
+  const ksg_plugin_set_view& sc = pv->points[KSG_POINT_SCORE];
+  for (int32_t i = 0; i < sc.n_enabled; i++) seq.emplace_back(S(sc.enabled[i].name), sc.enabled[i].weight);
+  seq.insert(seq.end(), p.plugins.begin(), p.plugins.end());
+  for (auto& kv : seq) {
+    const int pid = plugin_id(plain_name(kv.first));
+    if (pid < 0) continue;
+    const int32_t w = kv.second != 0 ? kv.second : 1;
+    p.store_w[pid] = w;                   // the store map: a later entry replaces (plugins.go:293-301)
+    if (p.sel_w[pid] == 0) p.sel_w[pid] = w;   // the framework: the point's own weight first
+  }
+  return true;
+}
+
 int encode_profile(ksg_snapshot* s) {
   const Profile& pr = s->prof;
   Encoded& e = s->e;
   ksg_profile& p = e.prof;
   std::memset(&p, 0, sizeof(p));
-  std::map<std::string, int32_t> weights;
-  for (auto& pl : pr.plugins) {
-    std::string key = pl.first;
-    if (key.size() > 7 && key.compare(key.size() - 7, 7, "Wrapped") == 0) key.resize(key.size() - 7);
-    weights[key] = pl.second != 0 ? pl.second : 1;
+  for (int pid : pr.order[KSG_POINT_FILTER]) p.filter_order[p.n_filter++] = pid;
+  for (int pid : pr.order[KSG_POINT_SCORE]) {
+    p.score_mask |= 1u << pid;
+    p.weight[pid] = pr.sel_w[pid] != 0 ? pr.sel_w[pid] : 1;
   }
-  for (int pid : pr.enabled)
-    if (kExt[pid][1]) p.filter_order[p.n_filter++] = pid;
-  for (int pid : pr.enabled)
-    if (kExt[pid][3]) {
-      p.score_mask |= 1u << pid;
-      auto it = weights.find(kPluginNames[pid]);
-      p.weight[pid] = it == weights.end() ? 1 : it->second;
-    }
   p.fit_strategy = pr.fit_strategy == "MostAllocated" ? KSG_MOST_ALLOCATED : KSG_LEAST_ALLOCATED;
   for (auto& r : pr.fit_res) {
     auto it = e.res_col.find(r.first);
@@ -1440,21 +1524,19 @@ int ksg_snapshot_new(const ksg_profile_view* pv, ksg_snapshot** out) {
   for (int32_t i = 0; i < pv->n_plugins; i++) {
     std::string name = S(pv->plugins[i].name);
     p.plugins.emplace_back(name, pv->plugins[i].weight);
-    std::string key = name;
-    if (key.size() > 7 && key.compare(key.size() - 7, 7, "Wrapped") == 0) key.resize(key.size() - 7);
-    int pid = -1;
-    for (int k = 0; k < KSG_NPLUGINS; k++)
-      if (key == kPluginNames[k]) pid = k;
+    const std::string key = plain_name(name);
+    const int pid = plugin_id(key);
     if (pid >= 0) {
       p.enabled.push_back(pid);
-    } else {
-      bool known = false;
-      for (const char* n : kNonEval) known = known || key == n;
-      if (!known) {
-        delete s;
-        return KSG_E_UNSUPPORTED;   // not an in-tree Filter/Score plugin
-      }
+    } else if (!non_eval(key)) {
+      delete s;
+      return KSG_E_UNSUPPORTED;   // not an in-tree Filter/Score plugin
     }
+  }
+  std::string perr;
+  if (!derive_profile(p, pv, perr)) {
+    delete s;
+    return KSG_E_UNSUPPORTED;   // a per-point set the registry / framework refuses
   }
   p.fit_strategy = pv->fit_strategy ? S(pv->fit_strategy) : "LeastAllocated";
   if (p.fit_strategy != "LeastAllocated" && p.fit_strategy != "MostAllocated") {
@@ -1472,6 +1554,22 @@ int ksg_snapshot_new(const ksg_profile_view* pv, ksg_snapshot** out) {
   p.pts_system = pv->pts_system_defaulted != 0;
   p.ba_skip_be = pv->ba_skip_best_effort != 0;
   *out = s;
+  return KSG_OK;
+}
+
+int ksg_snapshot_profile_info(ksg_snapshot* s, ksg_profile_info* out) {
+  if (!s || !out) return KSG_E_INVALID;
+  std::memset(out, 0, sizeof(*out));
+  const Profile& p = s->prof;
+  for (int pt = 0; pt < KSG_NPOINTS; pt++) {
+    out->n_order[pt] = (int32_t)p.order[pt].size();
+    for (size_t k = 0; k < p.order[pt].size(); k++) out->order[pt][k] = p.order[pt][k];
+  }
+  for (int pid = 0; pid < KSG_NPLUGINS; pid++) {
+    out->store_weight[pid] = p.store_w[pid];
+    out->selection_weight[pid] = p.sel_w[pid];
+    if (kExt[pid][4]) out->normalize_mask |= 1u << pid;
+  }
   return KSG_OK;
 }
 

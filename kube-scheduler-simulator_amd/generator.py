@@ -226,6 +226,21 @@ def readme_kat() -> Tuple[List[m.Node], List[m.Pod], P.Profile]:
     return nodes, [pod], P.default_profile()
 
 
+def readme_kat2() -> Tuple[List[m.Node], List[m.Pod], P.Profile]:
+    """The second reference-held vector (simulator/docs/plugin-extender.md:
+    85-107): the README cluster after one 100m / 16Gi pod went to node-282x7;
+    the next identical pod sees node-282x7 at NodeResourcesFit 47 /
+    BalancedAllocation 52 (assume: NonZeroRequested feeds Fit, Requested
+    feeds BalancedAllocation, whose memory fraction is capped at exactly 1),
+    node-gp9t4 at 73 / 76, and is placed on node-gp9t4.  As a queue: the
+    first pod lands on node-282x7 (lowest-index tie-break of two equal
+    nodes), the second is the documented one."""
+    nodes, pods, prof = readme_kat()
+    second = m.Pod(name="pod-8ldq5", containers=[m.Container(
+        image="registry.k8s.io/pause:3.5", requests={m.CPU: 100, m.MEMORY: 16 * GI})])
+    return nodes, pods + [second], prof
+
+
 def preemption_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, seed: int = 7):
     """A cluster filled with lower-priority running pods and a queue of
     higher-priority pods that only fit by preemption (DefaultPreemption

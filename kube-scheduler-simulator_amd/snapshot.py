@@ -115,6 +115,16 @@ class PluginView(C.Structure):
     _fields_ = [("name", cp), ("weight", i32)]
 
 
+class PluginSetView(C.Structure):
+    _fields_ = [("n_enabled", i32), ("enabled", C.POINTER(PluginView)), ("n_disabled", i32),
+                ("disabled", C.POINTER(cp))]
+
+
+# ksg_profile_view.points index (KSG_POINT_*) of profile.Profile.points keys
+POINTS = ("preFilter", "filter", "preScore", "score")
+NPOINTS = len(POINTS)
+
+
 class ProfileView(C.Structure):
     _fields_ = [("n_plugins", i32), ("plugins", C.POINTER(PluginView)), ("fit_strategy", cp),
                 ("n_fit_resources", i32), ("fit_resources", C.POINTER(Quantity)),
@@ -122,7 +132,15 @@ class ProfileView(C.Structure):
                 ("n_fit_ignored_resources", i32), ("fit_ignored_resources", C.POINTER(cp)),
                 ("n_fit_ignored_groups", i32), ("fit_ignored_groups", C.POINTER(cp)),
                 ("hard_pod_affinity_weight", i32), ("ignore_preferred_terms_of_existing_pods", i32),
-                ("pts_system_defaulted", i32), ("ba_skip_best_effort", i32)]
+                ("pts_system_defaulted", i32), ("ba_skip_best_effort", i32),
+                ("points", PluginSetView * NPOINTS)]
+
+
+class ProfileInfo(C.Structure):
+    """ksg_profile_info: per-point run orders and the two weight maps."""
+    _fields_ = [("n_order", i32 * NPOINTS), ("order", (i32 * native.NPLUGINS) * NPOINTS),
+                ("store_weight", i64 * native.NPLUGINS), ("selection_weight", i32 * native.NPLUGINS),
+                ("normalize_mask", C.c_uint32), ("pad", i32)]
 
 
 class _Keep:
@@ -239,9 +257,17 @@ def profile_view(prof: P.Profile, k: _Keep) -> ProfileView:
     ni, ig = k.strs(list(prof.fit_ignored_resources))
     ng, gr = k.strs(list(prof.fit_ignored_resource_groups))
     strat = {P.LEAST_ALLOCATED: "LeastAllocated", P.MOST_ALLOCATED: "MostAllocated"}[prof.fit_strategy]
-    return ProfileView(n, pl, _b(strat), nf, fr, nb, br, ni, ig, ng, gr, int(prof.hard_pod_affinity_weight),
-                       1 if prof.ignore_preferred_terms_of_existing_pods else 0,
-                       1 if prof.pts_system_defaulted else 0, 1 if prof.ba_skip_best_effort else 0)
+    v = ProfileView(n, pl, _b(strat), nf, fr, nb, br, ni, ig, ng, gr, int(prof.hard_pod_affinity_weight),
+                    1 if prof.ignore_preferred_terms_of_existing_pods else 0,
+                    1 if prof.pts_system_defaulted else 0, 1 if prof.ba_skip_best_effort else 0)
+    for idx, point in enumerate(POINTS):
+        if point not in prof.points:
+            continue
+        enabled, disabled = prof.points[point]
+        ne, en = k.arr(PluginView, [PluginView(_b(nm), int(w)) for nm, w in enabled])
+        nd, dis = k.strs(list(disabled))
+        v.points[idx] = PluginSetView(ne, en, nd, dis)
+    return v
 
 
 CODE_SUCCESS, CODE_UNSCHEDULABLE, CODE_UNRESOLVABLE, CODE_SKIP = 0, 2, 3, 5   # framework.Code
@@ -281,6 +307,7 @@ class Snapshot:
                          C.POINTER(i32))
         self._prefilter = f("prefilter", C.c_int, vp, i32, i32, C.c_uint32, C.POINTER(i32), C.POINTER(i32),
                             C.POINTER(cp), i32, C.POINTER(i32))
+        self._profile_info = f("profile_info", C.c_int, vp, C.POINTER(ProfileInfo))
         self.h = vp()
         k = _Keep()
         rc = self._new(C.byref(profile_view(prof, k)), C.byref(self.h))
@@ -394,6 +421,19 @@ class Snapshot:
 
     def forget(self, engine: native.Engine, pod: int, node: int):
         self._check(self._forget(self.h, engine.ctx, pod, node), "forget")
+
+    def profile_info(self) -> dict:
+        """ksg_snapshot_profile_info: {point: [plugin ids]}, store / selection
+        weights by plugin name (0 entries dropped), normalize mask."""
+        pi = ProfileInfo()
+        self._check(self._profile_info(self.h, C.byref(pi)), "profile_info")
+        out = {pt: [pi.order[k][i] for i in range(pi.n_order[k])] for k, pt in enumerate(POINTS)}
+        out["store_weight"] = {P.PLUGIN_NAMES[i]: int(pi.store_weight[i]) for i in range(native.NPLUGINS)
+                               if pi.store_weight[i]}
+        out["selection_weight"] = {P.PLUGIN_NAMES[i]: int(pi.selection_weight[i]) for i in range(native.NPLUGINS)
+                                   if pi.selection_weight[i]}
+        out["normalize_mask"] = int(pi.normalize_mask)
+        return out
 
     # -- framework.Status --------------------------------------------------
     def status(self, pod: int, word: int, node: int) -> Tuple[int, str]:

@@ -32,7 +32,7 @@ def test_library_exports_every_symbol(built):
     missing = [s for s in declared_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     lib.ksg_abi_version.restype = ctypes.c_int
-    assert lib.ksg_abi_version() == 2
+    assert lib.ksg_abi_version() == 3
 
 
 def test_struct_layouts_match(tmp_path):
@@ -73,7 +73,8 @@ def test_snapshot_view_layouts(tmp_path):
              "ksg_label_selector_view": S.LabelSelectorView, "ksg_affinity_term_view": S.AffinityTermView,
              "ksg_spread_view": S.SpreadView, "ksg_container_view": S.ContainerView, "ksg_image_view": S.ImageView,
              "ksg_node_view": S.NodeView, "ksg_pod_view": S.PodView, "ksg_plugin_view": S.PluginView,
-             "ksg_profile_view": S.ProfileView}
+             "ksg_plugin_set_view": S.PluginSetView, "ksg_profile_view": S.ProfileView,
+             "ksg_profile_info": S.ProfileInfo}
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "ksched_snapshot.h"\nint main(void){' +
                    "".join(f'printf("%zu\\n", sizeof({n}));' for n in pairs) + "return 0;}")

@@ -55,7 +55,7 @@ def oracle():
 
 
 CASES = [
-    ("c1-100x300", lambda: G.config1(n_nodes=100, n_pods=300)),
+    ("c1-100x1000", lambda: G.config1(n_nodes=100, n_pods=1000)),   # configs[0] at full size
     ("c2-60x200", lambda: G.config2(n_nodes=60, n_pods=200)),
     ("c2-tight", lambda: G.config2(n_nodes=7, n_pods=120, seed=11)),
     ("c2-1000x1500", lambda: G.config2(n_nodes=1000, n_pods=1500)),
@@ -64,6 +64,7 @@ CASES = [
     ("c5-small", lambda: G.config5(n_nodes=400, n_pods=300, n_images=200, taint_vocab=128,
                                    taints_per_node=16, images_per_node=20)),
     ("readme-kat", G.readme_kat),
+    ("readme-kat2", G.readme_kat2),
     ("c3-60x400", lambda: G.config3(n_nodes=60, n_pods=400, apps=12, zones=4)),
     ("c3-600x3000", lambda: G.config3(n_nodes=600, n_pods=3000, apps=40, zones=8)),
 ] + [(f"zoo-{s}", (lambda s=s: __import__("zoo").zoo(s))) for s in range(8)]
@@ -104,6 +105,36 @@ def test_placement_queue_matches_oracle(gpu_batched, oracle, name, make):
     p1, _ = gpu.run_queue(0, half)
     p2, _ = gpu.run_queue(half, len(pods) - half)
     np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
+
+
+def test_readme_kat2_gpu(gpu, gpu_batched):
+    """The second reference-held vector (plugin-extender.md:85-107, tests/
+    test_kat.py): the per-cycle path (ksg_eval + ksg_commit, as the cgo shim
+    drives it) and the batched captured queue both give node-282x7 Fit 47 /
+    BalancedAllocation 52, node-gp9t4 73 / 76, and select node-gp9t4."""
+    from test_kat import KAT2, KAT2_SELECTED
+    nodes, pods, prof = G.readme_kat2()
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    names = enc.cluster.node_names
+    gpu.load(enc, pf)
+    r0 = gpu.eval(0)
+    assert names[r0.selected] == "node-282x7"
+    gpu.commit(0, r0.selected)
+    cap = native.CaptureBuffers(2, 1)
+    r1 = gpu.eval(1, cap)
+    assert r1.n_feasible == 2 and names[r1.selected] == KAT2_SELECTED
+    for n, node in enumerate(names):
+        assert cap.raw[0, P.NODE_RESOURCES_FIT, n] == KAT2[node]["NodeResourcesFit"]
+        assert cap.raw[0, P.BALANCED_ALLOCATION, n] == KAT2[node]["NodeResourcesBalancedAllocation"]
+    for eng in (gpu, gpu_batched):
+        eng.load(enc, pf)
+        capq = native.CaptureBuffers(2, 2)
+        pl, _ = eng.run_queue(0, 2, capture=capq)
+        assert [names[x] for x in pl] == ["node-282x7", KAT2_SELECTED]
+        for n, node in enumerate(names):
+            assert capq.raw[1, P.NODE_RESOURCES_FIT, n] == KAT2[node]["NodeResourcesFit"]
+            assert capq.raw[1, P.BALANCED_ALLOCATION, n] == KAT2[node]["NodeResourcesBalancedAllocation"]
 
 
 @pytest.mark.parametrize("seed", [0, 3, 5])

@@ -42,6 +42,52 @@ def test_readme_kat_oracle_cpp():
     assert list(cap.norm[0, P.TAINT_TOLERATION]) == [100, 100]
 
 
+# The second reference-held vector (simulator/docs/plugin-extender.md:85-107):
+# the same README cluster after one 100m / 16Gi pod went to node-282x7.  Only
+# the per-plugin values and the selection are asserted: the plugin set there
+# is an older upstream's (AzureDiskLimits, EBSLimits, ...) plus the sample's
+# out-of-tree NodeNumber plugin.
+KAT2 = {"node-282x7": {"NodeResourcesFit": 47, "NodeResourcesBalancedAllocation": 52},
+        "node-gp9t4": {"NodeResourcesFit": 73, "NodeResourcesBalancedAllocation": 76}}
+KAT2_SELECTED = "node-gp9t4"
+
+
+def test_readme_kat2_pyoracle():
+    import pyoracle
+    nodes, pods, prof = G.readme_kat2()
+    first, second = pyoracle.run_queue(nodes, [], pods, prof)[:2]
+    assert first["selected"] == "node-282x7"
+    for node, want in KAT2.items():
+        for pl, v in want.items():
+            assert second["score"][node][pl] == str(v)
+            assert second["finalscore"][node][pl] == str(v)   # weight 1, no ScoreExtensions
+        assert second["finalscore"][node]["TaintToleration"] == "300"
+    assert second["selected"] == KAT2_SELECTED
+
+
+def test_readme_kat2_oracle_cpp():
+    import binding
+    E = pkg("encoder")
+    native = pkg("native")
+    nodes, pods, prof = G.readme_kat2()
+    enc = E.Encoder(nodes, pods, prof)
+    o = binding.Oracle(1)
+    o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    r0 = o.eval(0)
+    assert r0.selected == 0
+    o.commit(0, r0.selected)
+    cap = native.CaptureBuffers(2, 1)
+    r = o.eval(1, cap)
+    assert r.n_feasible == 2 and enc.cluster.node_names[r.selected] == KAT2_SELECTED
+    for n, node in enumerate(enc.cluster.node_names):
+        assert cap.raw[0, P.NODE_RESOURCES_FIT, n] == KAT2[node]["NodeResourcesFit"]
+        assert cap.raw[0, P.BALANCED_ALLOCATION, n] == KAT2[node]["NodeResourcesBalancedAllocation"]
+    # the batched queue of the oracle agrees
+    o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    pl, _ = o.run_queue(0, 2)
+    assert [enc.cluster.node_names[x] for x in pl] == ["node-282x7", KAT2_SELECTED]
+
+
 def test_store_weight_application():
     # store_test.go:284-333: raw "10" with weight 2 -> final "20"
     s = A.ResultStore({"plugin1": 2})

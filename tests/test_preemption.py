@@ -234,3 +234,55 @@ def test_gpu_topology_preemption_victims_match_cpp_oracle(built):
     for i in range(nb, len(pods)):
         assert s_gpu.schedule_one(i) == s_cpu.schedule_one(i), i
     assert s_gpu.preemptions == s_cpu.preemptions and _topo_preemptors(s_gpu, pods)
+
+
+def _many_anti_templates(n_templates: int):
+    """Four nodes, one low-priority running pod per existing anti-affinity
+    template (selector k<i>=x, hostname), and a high-priority preemptor whose
+    labels match every template: its InterPodAffinity program lists
+    n_templates existing-pod anti-affinity templates."""
+    nodes = [m.Node(name=f"node-{i}", labels={m.LABEL_HOSTNAME: f"node-{i}"},
+                    allocatable={m.CPU: 4000, m.MEMORY: 16 * GI, m.PODS: 110}) for i in range(4)]
+    pods, bound = [], []
+    for i in range(n_templates):
+        p = m.Pod(name=f"run-{i}", containers=[m.Container(image="pause", requests={m.CPU: 200, m.MEMORY: GI})])
+        p.priority, p.node_name = 1, f"node-{i % 4}"
+        p.pod_anti_affinity_required = [m.PodAffinityTerm(m.LabelSelector(match_labels=((f"k{i}", "x"),)),
+                                                          m.LABEL_HOSTNAME)]
+        pods.append(p)
+        bound.append((i, i % 4))
+    pre = m.Pod(name="preemptor", labels={f"k{i}": "x" for i in range(n_templates)},
+                containers=[m.Container(image="pause", requests={m.CPU: 3000, m.MEMORY: GI})])
+    pre.priority = 10
+    pods.append(pre)
+    return nodes, pods, bound, P.default_profile()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_templates", [16, 17])
+def test_gpu_preemption_refuses_too_many_anti_templates(built, n_templates):
+    """The topology dry run holds 16 existing anti-affinity templates per
+    preemptor; 17 are refused on the host before any launch, 16
+    run and agree with the C++ oracle."""
+    E = pkg("encoder")
+    nodes, pods, bound, prof = _many_anti_templates(n_templates)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu, cpu = native.Engine(device=0), _oracle_engine()
+    for eng in (gpu, cpu):
+        eng.load(enc, pf)
+        for pi, ni in bound:
+            eng.commit(pi, ni)
+    pre = len(pods) - 1
+    cand = [0, 1, 2, 3]
+    lists = [[q for q, n in bound if n == c] for c in cand]
+    off = np.concatenate([[0], np.cumsum([len(v) for v in lists])]).astype(np.int32)
+    vic = np.array([q for v in lists for q in v], np.int32)
+    if n_templates > 16:
+        with pytest.raises(native.KschedError, match="anti-affinity templates"):
+            gpu.preempt_victims(pre, cand, off, vic)
+        return
+    fg, vg = gpu.preempt_victims(pre, cand, off, vic)
+    fc, vc = cpu.preempt_victims(pre, cand, off, vic)
+    np.testing.assert_array_equal(fg, fc)
+    np.testing.assert_array_equal(vg, vc)

@@ -212,3 +212,66 @@ def test_prefilter_statuses(built):
                 assert names == enc.prefilter_node_names[pi]
             else:
                 assert names is None
+
+
+def _native_info(prof):
+    return S.Snapshot(prof).profile_info()
+
+
+def _python_info(prof):
+    out = {"preFilter": prof.prefilter_order(), "filter": prof.filter_order(), "preScore": prof.prescore_order(),
+           "score": prof.score_order()}
+    out["store_weight"] = {k: v for k, v in prof.weights().items() if k in P.PLUGIN_ID}
+    sel = prof.selection_weights()
+    out["selection_weight"] = {k: v for k, v in sel.items() if k in P.PLUGIN_ID}
+    return out
+
+
+def _per_point_profiles():
+    I = pkg("ingest")
+    from test_ingest import export_config_loadable
+    yield I.profile_from_config(export_config_loadable())[0]
+    yield P.default_profile()
+    yield P.config2_profile()
+    for cfg in (
+        {"filter": {"disabled": [{"name": "NodeAffinity"}]}},
+        {"score": {"enabled": [{"name": "ImageLocality", "weight": 7}], "disabled": [{"name": "*"}]}},
+        {"score": {"enabled": [{"name": "TaintTolerationWrapped", "weight": 9}, {"name": "ImageLocality"}]},
+         "preScore": {"disabled": [{"name": "TaintToleration"}]}},
+        {"preFilter": {"enabled": [{"name": "InterPodAffinity"}, {"name": "NodeResourcesFit"}],
+                       "disabled": [{"name": "NodePorts"}]},
+         "filter": {"enabled": [{"name": "NodeResourcesFit"}], "disabled": [{"name": "*"}]}},
+    ):
+        yield I.profile_from_config({"profiles": [{"plugins": cfg}]})[0]
+
+
+def test_profile_info_matches_python(built):
+    """ksg_profile_view's per-point sets (ConvertForSimulator keeps them,
+    plugins.go:174-197) expand natively exactly as profile.py does, and the
+    native store / selection weight maps equal profile.weights() /
+    selection_weights() (getScorePluginWeight, plugins.go:289-304), on the
+    reference's export sample and on disable / "*" / weight-override cases."""
+    for prof in _per_point_profiles():
+        got, want = _native_info(prof), _python_info(prof)
+        for k, v in want.items():
+            assert got[k] == v, (k, prof.points)
+
+
+def test_export_sample_profile_encodes_identically(built):
+    """The export sample's profile through the native encoder: same encoded
+    ksg_profile (filter order from the Filter point, score mask from the Score
+    point, selection weights) as encoder.encode_profile."""
+    I = pkg("ingest")
+    from test_ingest import export_config_loadable
+    prof = I.profile_from_config(export_config_loadable())[0]
+    nodes, pods, _ = G.config3(n_nodes=30, n_pods=60, apps=6, zones=3)
+    _assert_same(nodes, pods, prof)
+
+
+def test_per_point_refusals(built):
+    for cfg in ({"filter": {"enabled": [{"name": "ImageLocality"}]}},      # does not extend Filter
+                {"score": {"enabled": [{"name": "NoSuchPlugin"}]}}):
+        prof = P.Profile(points={k: ([(e["name"], e.get("weight", 0)) for e in v.get("enabled", [])],
+                                     tuple(d["name"] for d in v.get("disabled", []))) for k, v in cfg.items()})
+        with pytest.raises(S.SnapshotError):
+            S.Snapshot(prof)
