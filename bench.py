@@ -233,6 +233,72 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
             "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(), "threads": threads}
 
 
+def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
+    """The drop-in's per-cycle path, the calls the Go
+    shim makes per scheduling cycle, through the C ABI of libksched.so:
+    ksg_snapshot_add_pod -> ksg_snapshot_sync (append to the device
+    workload) -> ksg_eval with capture (status words + the score rows) ->
+    ksg_snapshot_statuses (every rejected node's framework.Status, once per
+    pod) -> ksg_snapshot_assume.  configs[1]'s cluster, starting empty; the
+    first `warm` pods fill the encoding universe (a pod that adds a label
+    value forces a full re-encode, counted), then `n_pods` cycles are timed
+    call by call (pod views built beforehand; ctypes call overhead included).
+    The placements must equal one ksg_run_queue over the same pods."""
+    import numpy as np
+    nodes, pods, prof = G.config2(n_nodes=n_nodes, n_pods=warm + n_pods)
+    snap = S.Snapshot(prof, nodes)
+    eng = native.Engine(device=0)
+    snap.load(eng)
+    N = len(nodes)
+    cap = native.CaptureBuffers(N, 1)
+    keep = []
+    views = []
+    for p in pods:
+        k = S._Keep()
+        views.append(S.pod_view(p, k))
+        keep.append(k)
+    phases = np.zeros((n_pods, 5))
+    placed = np.full(warm + n_pods, -1, np.int32)
+    appended = reloads = 0
+    clock = time.perf_counter_ns
+    for i, v in enumerate(views):
+        t0 = clock()
+        idx = snap.add_pod_view(v)
+        t1 = clock()
+        ap = snap.sync(eng)
+        t2 = clock()
+        r = eng.eval(idx, cap)
+        t3 = clock()
+        snap.statuses(idx, cap.fstatus[0])
+        t4 = clock()
+        if r.selected >= 0:
+            snap.assume(eng, idx, r.selected)
+        t5 = clock()
+        placed[i] = r.selected
+        if i >= warm:
+            phases[i - warm] = (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4)
+            appended += ap
+            reloads += not ap
+    # the same pods as one device-resident queue
+    import importlib
+    E = importlib.import_module(PKG + ".encoder")
+    enc = E.Encoder(nodes, pods, prof)
+    q = native.Engine(device=0)
+    q.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    want, _ = q.run_queue(0, len(pods), results=False)
+    us = phases / 1e3
+    per = us.sum(axis=1)
+    names = ["add_pod", "sync", "eval_capture", "statuses", "assume"]
+    return {"workload": f"configs[1] cluster ({N} nodes), per-cycle C-ABI path, {n_pods} cycles timed after {warm}",
+            "us_per_cycle_mean": float(per.mean()), "us_per_cycle_p50": float(np.percentile(per, 50)),
+            "us_per_cycle_p99": float(np.percentile(per, 99)), "pods_per_s": float(1e6 / per.mean()),
+            "breakdown_us_mean": {k: float(us[:, j].mean()) for j, k in enumerate(names)},
+            "breakdown_us_p50": {k: float(np.percentile(us[:, j], 50)) for j, k in enumerate(names)},
+            "appended": int(appended), "full_reloads": int(reloads),
+            "placements_equal_run_queue": bool(np.array_equal(placed, want)),
+            "eval_path": eng.last_run_info()[0]}
+
+
 def default_profile_line(native, G, E, n_nodes: int, n_pods: int, steps: int):
     """The in-tree default profile at n_nodes (generator.config1): pods/s of
     reset + one ksg_run_queue over n_pods, best of `steps`."""
@@ -271,6 +337,8 @@ def main():
     ap.add_argument("--annotate-pods", type=int, default=2000, help="annotation sidecar; 0 disables")
     ap.add_argument("--annotate-threads", type=int, default=16)
     ap.add_argument("--default-pods", type=int, default=20000, help="default-profile line; 0 disables")
+    ap.add_argument("--cycle-pods", type=int, default=2000, help="per-cycle sidecar; 0 disables")
+    ap.add_argument("--cycle-warm", type=int, default=500)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -368,6 +436,13 @@ def main():
                                      args.annotate_threads)
         except Exception as e:
             log(f"[rank {rank}] annotation sidecar unavailable: {e}")
+    cyc = None
+    if world == 1 and args.cycle_pods > 0:
+        try:
+            S = importlib.import_module(PKG + ".snapshot")
+            cyc = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods)
+        except Exception as e:
+            log(f"[rank {rank}] per-cycle sidecar unavailable: {e}")
     if world == 1 and args.default_pods > 0:
         try:
             dflt = default_profile_line(native, G, E, args.nodes, args.default_pods, 2)
@@ -428,6 +503,8 @@ def main():
             out["annotations"] = ann
         if dflt is not None:
             out["default_profile"] = dflt
+        if cyc is not None:
+            out["per_cycle"] = cyc
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baselines(enc, pf, args.cpu_budget)
         print(json.dumps(out), flush=True)

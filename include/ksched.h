@@ -240,14 +240,20 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl);
  * uses.  The new pods get indices n_pods, n_pods + 1, ... */
 int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base);
 /* Evaluate pod `pod` (index into the loaded workload) against the current
- * node state; no state change.  `cap` may be NULL. */
+ * node state; no state change.  `cap` may be NULL.  The per-cycle call of the
+ * Go shim: a pod whose plugins are all node-local takes the chip-wide path
+ * (two launches over N / 256 workgroups, persistent device and pinned host
+ * buffers, one device -> host copy); topology pods take the single-workgroup
+ * queue kernel. */
 int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap);
 /* Evaluate an encoded pod that is not part of the workload: `pod`'s program
  * offsets index `prog[0 .. prog_len)`.  Same outputs as ksg_eval; the pod
  * is not retained (ksg_append_pods it first to commit it). */
 int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t prog_len, ksg_result* res,
                  ksg_capture* cap);
-/* Assume pod `pod` onto node `node` (NodeInfo.AddPod + count tables). */
+/* Assume pod `pod` onto node `node` (NodeInfo.AddPod + count tables).
+ * Stream-ordered: returns once the update is enqueued; every later
+ * evaluation and read-back of the context sees it. */
 int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node);
 /* Schedule pods [first, first+count) in order on the device.  placements
  * [count]; results [count] may be NULL; cap may be NULL (else per-pod arrays
@@ -289,8 +295,9 @@ int ksg_reset_state(ksg_ctx* ctx);
 /* Timing of the last ksg_run_queue / ksg_run_replicas kernel: milliseconds
  * between HIP events recorded on the stream the kernel was launched on. */
 int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
-/* Which path the last ksg_run_queue / ksg_run_replicas took: path 1 queue
- * kernel, 2 batched, 3 replica sweep, 4 chip-wide topology; flags: the range-
+/* Which path the last ksg_run_queue / ksg_run_replicas / ksg_eval took: path
+ * 1 queue kernel, 2 batched, 3 replica sweep, 4 chip-wide topology, 5 the
+ * per-cycle chip-wide evaluation of ksg_eval; flags: the range-
  * checked narrow forms that ran (exact either way; for tests and reports). */
 #define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
 #define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */

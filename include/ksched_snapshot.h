@@ -303,6 +303,15 @@ int ksg_snapshot_forget(ksg_snapshot* s, ksg_ctx* ctx, int32_t pod, int32_t node
  * length.  Word 0 = Success (empty message). */
 int ksg_snapshot_status(ksg_snapshot* s, int32_t pod, uint32_t word, int32_t node, int32_t* code, char* msg,
                         int32_t cap, int32_t* len);
+/* Every node's Filter status at once (the Go shim decodes a pod's statuses
+ * once per cycle, in evalPod, instead of once per Filter call under a lock):
+ * code[n] = KSG_CODE_*, msg[n] = index of the node's Status.Message() among
+ * the pod's distinct messages (-1: success or not evaluated).  The distinct
+ * messages go to buf NUL-separated in index order when cap >= *len; *n_msgs
+ * and *len (bytes, NULs included) are always set, so a caller can size buf
+ * and call again. */
+int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
+                          int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len);
 /* PreFilter of plugin `plugin` for `pod` (given the device result's status
  * bits): *code = KSG_CODE_SUCCESS / SKIP / UNSCHEDULABLE_AND_UNRESOLVABLE
  * (NodeAffinity "pod affinity terms conflict"); NodeAffinity's

@@ -2406,6 +2406,17 @@ struct ksg_ctx {
   double kstat_units[KSG_NKERNELS] = {};
   int32_t kstat_calls[KSG_NKERNELS] = {};
   unsigned long long* d_stamps = nullptr;   // KSG_STAMPS diagnostic build only
+  // per-cycle evaluation (eval_fast): one grow-only device block and its
+  // pinned host mirror, reused by every ksg_eval / ksg_eval_pod call
+  char* d_ev = nullptr;
+  size_t ev_bytes = 0;
+  char* h_ev = nullptr;                     // hipHostMalloc'd, freed by ksg_close
+  size_t h_ev_bytes = 0;
+  int ev_parity = 0;                        // which of the two stats slots this call uses
+  bool ev_clean = false;                    // both slots zeroed
+  ksg_profile* d_ev_prof = nullptr;
+  bool ev_prof_dirty = true;
+  bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
 };
 
 namespace {
@@ -2486,6 +2497,11 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_coop_parts = nullptr;
   ctx->d_coop_phist = nullptr;
   ctx->d_coop_srec = nullptr;
+  ctx->d_ev = nullptr;
+  ctx->ev_bytes = 0;
+  ctx->ev_clean = false;
+  ctx->d_ev_prof = nullptr;
+  ctx->ev_prof_dirty = true;
 }
 
 // ---- per-kernel timing -------------------------------------------------------
@@ -3607,6 +3623,163 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   return KSG_OK;
 }
 
+// ---- the per-cycle path ---------------------------------------------------------
+// ksg_eval of one pod whose plugins are all node-local (the batched path's
+// eligibility): the framework's PreFilter .. NormalizeScore for one pod, as the
+// Go shim calls it once per scheduling cycle.  No allocation per call: one
+// grow-only device block (two parity slots of per-call statistics, the
+// capture rows, the record scratch) and its pinned host mirror.  Two chip-wide
+// launches (ksg_capture_eval and ksg_capture_norm, N / 256 workgroups each,
+// nothing assumed: the pod sees the live state) and one device -> host copy of
+// the slot plus every row the caller asked for; the host then fills the
+// caller's arrays and decodes the result.  The other parity's slot is zeroed
+// by the second launch, so no memset runs per call.
+struct EvSlot {
+  int32_t stats[4];              // feasible count, max taint, max node affinity, max (N - n) over feasible n
+  unsigned long long best;       // selectHost key
+  uint32_t err;
+  uint32_t pad;
+};
+static_assert(sizeof(EvSlot) == 32, "EvSlot layout");
+
+bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
+  return ctx->eval_fast && ctx->force_path != 1 && batch_eligible(ctx, pod, 1);
+}
+
+int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
+  const size_t N = ctx->c.N;
+  const ksg_profile& prof = ctx->prof;
+  int rows[KSG_NPLUGINS], n_rows = 0;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if ((prof.score_mask >> pl) & 1u) rows[n_rows++] = pl;
+  const bool want_fs = cap && cap->fstatus, want_raw = cap && cap->raw, want_norm = cap && cap->norm,
+             want_tot = cap && cap->total;
+  // block: slot[2] | -1 | fstatus[N] | raw[n_rows][N] | norm[n_rows][N] | total[N] | rec[N]
+  const size_t o_neg = 2 * sizeof(EvSlot), o_fs = o_neg + 8, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
+  const size_t o_norm = o_raw + 8 * N * n_rows, o_tot = o_norm + 8 * N * n_rows, o_rec = o_tot + 8 * N;
+  const size_t need = o_rec + 8 * N;
+  int rc;
+  HIPC(ctx, hipSetDevice(ctx->device));
+  if (need > ctx->ev_bytes) {
+    if (ctx->d_ev) {
+      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_ev);
+      if (it != ctx->allocs.end()) ctx->allocs.erase(it);
+      HIPC(ctx, hipStreamSynchronize(ctx->stream));
+      (void)hipFree(ctx->d_ev);
+      ctx->d_ev = nullptr;
+    }
+    if ((rc = dalloc(ctx, &ctx->d_ev, need))) return rc;
+    ctx->ev_bytes = need;
+    ctx->ev_clean = false;
+  }
+  if (!ctx->d_ev_prof && (rc = dalloc(ctx, &ctx->d_ev_prof, 1))) return rc;
+  if (o_rec > ctx->h_ev_bytes) {   // the host mirror holds everything but the record scratch
+    if (ctx->h_ev) {
+      HIPC(ctx, hipStreamSynchronize(ctx->stream));
+      (void)hipHostFree(ctx->h_ev);
+      ctx->h_ev = nullptr;
+      ctx->h_ev_bytes = 0;
+    }
+    HIPC(ctx, hipHostMalloc((void**)&ctx->h_ev, o_rec, hipHostMallocDefault));
+    ctx->h_ev_bytes = o_rec;
+  }
+  if (!ctx->ev_clean) {
+    static const int32_t init[2] = {-1, 0};
+    HIPC(ctx, hipMemsetAsync(ctx->d_ev, 0, o_neg, ctx->stream));
+    HIPC(ctx, hipMemcpyAsync(ctx->d_ev + o_neg, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
+    ctx->ev_parity = 0;
+    ctx->ev_clean = true;
+  }
+  if (ctx->ev_prof_dirty) {
+    HIPC(ctx, hipMemcpyAsync(ctx->d_ev_prof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream));
+    ctx->ev_prof_dirty = false;
+  }
+  const int par = ctx->ev_parity;
+  EvSlot* slot = reinterpret_cast<EvSlot*>(ctx->d_ev) + par;
+  CapArgs ca{};
+  ca.c = ctx->c;
+  ca.st = ctx->st;
+  ca.pods = ctx->d_pods;
+  ca.prog = ctx->d_prog;
+  ca.prof = ctx->d_ev_prof;
+  ca.b0 = pod;
+  ca.nb = 1;
+  ca.out0 = 0;
+  ca.placements = reinterpret_cast<const int32_t*>(ctx->d_ev + o_neg);
+  ca.rec = reinterpret_cast<uint64_t*>(ctx->d_ev + o_rec);
+  ca.stats = slot->stats;
+  ca.n_rows = n_rows;
+  for (int q = 0; q < n_rows; q++) ca.rows[q] = rows[q];
+  ca.fstatus = reinterpret_cast<uint32_t*>(ctx->d_ev + o_fs);
+  ca.raw = reinterpret_cast<int64_t*>(ctx->d_ev + o_raw);
+  ca.norm = reinterpret_cast<int64_t*>(ctx->d_ev + o_norm);
+  ca.total = want_tot ? reinterpret_cast<int64_t*>(ctx->d_ev + o_tot) : nullptr;
+  ca.best = &slot->best;
+  ca.err = &slot->err;
+  ca.next = reinterpret_cast<int32_t*>(reinterpret_cast<EvSlot*>(ctx->d_ev) + (1 - par));
+  const dim3 grid((unsigned)((N + 255) / 256), 1);
+  ctx->ev_clean = false;   // until the second launch is in: it zeroes the other slot
+  hipLaunchKernelGGL(ksg_capture_eval, grid, dim3(256), 0, ctx->stream, ca);
+  hipLaunchKernelGGL(ksg_capture_norm, grid, dim3(256), 0, ctx->stream, ca);
+  HIPC(ctx, hipGetLastError());
+  ctx->ev_parity = 1 - par;
+  ctx->ev_clean = true;
+  // one copy back: both slots, the -1 word and the rows the caller asked for
+  size_t back = o_fs;
+  if (want_fs) back = o_raw;
+  if (want_raw || want_norm) back = o_tot;
+  if (want_tot) back = o_rec;
+  HIPC(ctx, hipMemcpyAsync(ctx->h_ev, ctx->d_ev, back, hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  const EvSlot& h = reinterpret_cast<const EvSlot*>(ctx->h_ev)[par];
+  const int32_t nfeas = h.stats[0];
+  uint32_t status = 0;
+  int32_t selected = -1;
+  if (nfeas == 1) {
+    selected = (int32_t)N - h.stats[3];
+  } else if (nfeas >= 2) {
+    status |= KSG_ST_SCORED;
+    if (h.err) status |= KSG_ST_SCORE_ERROR;
+    else selected = (int32_t)(0xffffffffu - (uint32_t)(h.best & 0xffffffffu));
+  }
+  // ipa_skip_bits (ksched_kernels.h) on the host: the pod carries no
+  // InterPodAffinity program on this path
+  const ksg_pod& p = ctx->h_pods[pod];
+  uint32_t score_skip = p.score_skip;
+  bool ipa_filter = false;
+  for (int kf = 0; kf < prof.n_filter; kf++) ipa_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
+  if (p.ipa < 0) {
+    if (ipa_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
+    if ((status & KSG_ST_SCORED) && ((prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) &&
+        !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u)) {
+      status |= KSG_ST_IPA_PRESCORE_SKIP;
+      score_skip |= 1u << KSG_PL_INTER_POD_AFFINITY;
+    }
+  }
+  res->selected = selected;
+  res->n_feasible = nfeas;
+  res->status = status;
+  res->score_skip = score_skip;
+  if (want_fs) std::memcpy(cap->fstatus, ctx->h_ev + o_fs, 4 * N);
+  for (int q = 0; q < n_rows; q++) {
+    if (want_raw) std::memcpy(cap->raw + (size_t)rows[q] * N, ctx->h_ev + o_raw + 8 * N * q, 8 * N);
+    if (want_norm) std::memcpy(cap->norm + (size_t)rows[q] * N, ctx->h_ev + o_norm + 8 * N * q, 8 * N);
+  }
+  if (want_tot) std::memcpy(cap->total, ctx->h_ev + o_tot, 8 * N);
+  ctx->last_path = 5;
+  return KSG_OK;
+}
+
+int eval_internal(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
+  if ((rc = check_blobs(ctx, pod, 1))) return rc;
+  if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, cap);
+  int32_t pl;
+  return run_internal(ctx, pod, 1, 0, &pl, res, cap);
+}
+
 // Grow a device array to `need` elements, keeping its first `used` ones.
 template <typename T>
 int dgrow(ksg_ctx* ctx, T** p, size_t* cap, size_t used, size_t need) {
@@ -3736,6 +3909,7 @@ int ksg_open(int device, ksg_ctx** out) {
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : m == "slot" ? 2 : m == "tcol" ? 5 : 4;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
+  if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);
     ctx->slot_block = v <= 64 ? 64 : v <= 128 ? 128 : KSG_BATCH_MAX;
@@ -3756,6 +3930,7 @@ int ksg_close(ksg_ctx* ctx) {
     if (ctx->ev_p2[q]) (void)hipEventDestroy(ctx->ev_p2[q]);
   }
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->h_ev) (void)hipHostFree(ctx->h_ev);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -3772,6 +3947,7 @@ int ksg_set_profile(ksg_ctx* ctx, const ksg_profile* prof) {
     return fail(ctx, KSG_E_INVALID, "profile field out of range");
   ctx->prof = *prof;
   ctx->have_prof = true;
+  ctx->ev_prof_dirty = true;
   return KSG_OK;
 }
 
@@ -3895,8 +4071,7 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
 
 int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   if (!res) return fail(ctx, KSG_E_INVALID, "null result");
-  int32_t pl;
-  return run_internal(ctx, pod, 1, 0, &pl, res, cap);
+  return eval_internal(ctx, pod, res, cap);
 }
 
 int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base) {
@@ -3917,10 +4092,7 @@ int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t 
   const int32_t n0 = ctx->n_pods, blob0 = ctx->max_blob;
   const int64_t used0 = ctx->prog_used;
   int rc = append_internal(ctx, &p, 1, prog, prog_len, base);
-  if (!rc) {
-    int32_t pl;
-    rc = run_internal(ctx, n0, 1, 0, &pl, res, cap);
-  }
+  if (!rc) rc = eval_internal(ctx, n0, res, cap);
   if (ctx->n_pods > n0) {
     ctx->n_pods = n0;
     ctx->h_pods.resize(n0);
@@ -3944,8 +4116,9 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
   HIPC(ctx, hipSetDevice(ctx->device));
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
                      ctx->d_prog, pod, node, sign);
+  // stream-ordered: the next evaluation on ctx->stream sees the update, and
+  // every read-back synchronises the stream; no host wait per assume
   HIPC(ctx, hipGetLastError());
-  HIPC(ctx, hipStreamSynchronize(ctx->stream));
   return KSG_OK;
 }
 

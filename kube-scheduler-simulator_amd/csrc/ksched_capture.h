@@ -41,6 +41,14 @@ struct CapArgs {
   int64_t* raw;                  // [count][n_rows][N]
   int64_t* norm;                 // [count][n_rows][N]
   int64_t* total;                // [count][N]
+  // per-cycle evaluation (ksg_eval's fast path, nb = 1, nothing assumed):
+  // stats[3] = max over feasible nodes of N - n (lowest feasible index),
+  // *best = selectHost's packed argmax key, *err = a normalised score left
+  // [0, 100]; *next is the other call parity's slot, zeroed by block 0 of
+  // ksg_capture_norm for the next call (no memset launch).  Null otherwise.
+  unsigned long long* best;
+  uint32_t* err;
+  int32_t* next;                 // 8 words: the next call's stats[4], best, err
 };
 
 __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
@@ -48,7 +56,7 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
   __shared__ ksg_pod s_pod;
   __shared__ ksg_profile s_prof;
   __shared__ int32_t s_pl[KSG_BATCH_MAX];
-  __shared__ int32_t s_st[3][4];
+  __shared__ int32_t s_st[4][4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int j = blockIdx.y;
   const DevCluster& c = a.c;
@@ -62,7 +70,7 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
   const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog);
   const int n = blockIdx.x * 256 + tid;
   const size_t o = (size_t)(a.out0 + j);
-  int32_t feas = 0, mt = 0, ma = 0;
+  int32_t feas = 0, mt = 0, ma = 0, lo = 0;
   if (n < N) {
     NodeCols L;
     load_cols(c, a.st.requested, a.st.nonzero, a.st.pod_count, n, L);
@@ -102,19 +110,27 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
       feas = 1;
       mt = (int32_t)e.rt;
       ma = (int32_t)e.ra;
+      lo = N - n;
     }
   }
   feas = wave_sum32(feas);
   mt = (int32_t)wave_max64(mt);
   ma = (int32_t)wave_max64(ma);
-  if (lane == 0) { s_st[0][wv] = feas; s_st[1][wv] = mt; s_st[2][wv] = ma; }
+  if (a.best) lo = (int32_t)wave_max64(lo);
+  if (lane == 0) { s_st[0][wv] = feas; s_st[1][wv] = mt; s_st[2][wv] = ma; s_st[3][wv] = lo; }
   __syncthreads();
   if (tid == 0) {
-    int32_t f = 0, t = 0, m = 0;
-    for (int i = 0; i < 4; i++) { f += s_st[0][i]; t = max(t, s_st[1][i]); m = max(m, s_st[2][i]); }
+    int32_t f = 0, t = 0, m = 0, l = 0;
+    for (int i = 0; i < 4; i++) {
+      f += s_st[0][i];
+      t = max(t, s_st[1][i]);
+      m = max(m, s_st[2][i]);
+      l = max(l, s_st[3][i]);
+    }
     if (f) atomicAdd(&a.stats[4 * j], f);
     if (t) atomicMax(&a.stats[4 * j + 1], t);
     if (m) atomicMax(&a.stats[4 * j + 2], m);
+    if (a.best && l) atomicMax(&a.stats[4 * j + 3], l);
   }
 }
 
@@ -122,27 +138,51 @@ __global__ __launch_bounds__(256) void ksg_capture_norm(CapArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
   __shared__ ksg_profile s_prof;
-  const int tid = threadIdx.x;
+  __shared__ unsigned long long s_key[4];
+  __shared__ uint32_t s_err[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int j = blockIdx.y;
   const DevCluster& c = a.c;
   const int N = c.N;
   const size_t NN = N;
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  if (a.next && blockIdx.x == 0 && tid < 8) a.next[tid] = 0;   // the next call's slot
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();
   const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog);
   const int n = blockIdx.x * 256 + tid;
+  const int32_t nfeas = a.stats[4 * j], max_t = a.stats[4 * j + 1], max_a = a.stats[4 * j + 2];
+  if (a.best) {   // selectHost over this block's nodes, merged by one atomic per block
+    uint64_t key = 0;
+    uint32_t err = 0;
+    if (n < N && nfeas >= 2) {
+      const uint64_t x = a.rec[(size_t)j * NN + n];
+      if (x >> 63)
+        key = argmax_key(total_score(v, (uint32_t)x, (x >> 48) & 0xff, (x >> 32) & 0xffff, max_t, max_a, err,
+                                     nullptr, nullptr), n);
+    }
+    key = wave_max_u64(key);
+    err = wave_or32(err);
+    if (lane == 0) { s_key[wv] = key; s_err[wv] = err; }
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t k = 0;
+      uint32_t e = 0;
+      for (int i = 0; i < 4; i++) { k = s_key[i] > k ? s_key[i] : k; e |= s_err[i]; }
+      if (k) atomicMax(a.best, (unsigned long long)k);
+      if (e) atomicOr(a.err, e);
+    }
+  }
   if (n >= N) return;
   const size_t o = (size_t)(a.out0 + j);
-  const int32_t nfeas = a.stats[4 * j], max_t = a.stats[4 * j + 1], max_a = a.stats[4 * j + 2];
   const uint64_t x = a.rec[(size_t)j * NN + n];
   int64_t total = 0, nt = 0, na = 0;
   if (nfeas >= 2 && (x >> 63)) {
     uint32_t err = 0;
     total = total_score(v, (uint32_t)x, (x >> 48) & 0xff, (x >> 32) & 0xffff, max_t, max_a, err, &nt, &na);
   }
-  a.total[o * NN + n] = total;
+  if (a.total) a.total[o * NN + n] = total;
   for (int q = 0; q < a.n_rows; q++) {
     const int pl = a.rows[q];
     if (nfeas < 2) {   // fewer than two feasible nodes: no Score runs, nothing recorded

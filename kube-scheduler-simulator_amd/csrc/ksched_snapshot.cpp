@@ -1511,6 +1511,86 @@ int full_load(ksg_snapshot* s, ksg_ctx* ctx) {
   return rc ? rc : upload_all(s, ctx);
 }
 
+// framework.Status (code, Message()) of a Filter status word at `node` for
+// `pod`; msg may be null when only the code is wanted.
+bool status_of(const Encoded& e, int32_t pod, uint32_t word, int32_t node, int* code, std::string* msg,
+               std::string* err) {
+  std::string m;
+  int c = KSG_CODE_SUCCESS;
+  const int pl = (int)(word & 0xffu) - 1;
+  const uint32_t reason = word >> 8;
+  if (word == KSG_FS_NOT_EVALUATED) {
+    *err = "node not evaluated";
+    return false;
+  }
+  switch (pl) {
+    case -1:
+      break;
+    case KSG_PL_NODE_UNSCHEDULABLE:
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      m = "node(s) were unschedulable";
+      break;
+    case KSG_PL_NODE_NAME:
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      m = "node(s) didn't match the requested node name";
+      break;
+    case KSG_PL_TAINT_TOLERATION: {
+      if ((int)reason >= e.max_taints) {
+        *err = "taint slot";
+        return false;
+      }
+      const uint32_t t = e.taints[(size_t)reason * e.N + node];
+      if (t == 0) {
+        *err = "empty taint slot";
+        return false;
+      }
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      if (msg) m = "node(s) had untolerated taint " + e.taint_strings[t - 1];
+      break;
+    }
+    case KSG_PL_NODE_AFFINITY:
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      m = "node(s) didn't match Pod's node affinity/selector";
+      break;
+    case KSG_PL_NODE_PORTS:
+      c = KSG_CODE_UNSCHEDULABLE;
+      m = "node(s) didn't have free ports for the requested pod ports";
+      break;
+    case KSG_PL_NODE_RESOURCES_FIT: {
+      // fitsRequest reason order: pods, cpu, memory, ephemeral, scalars;
+      // Unresolvable when the request exceeds the allocatable outright.
+      c = KSG_CODE_UNSCHEDULABLE;
+      const ksg_pod& p = e.pods[pod];
+      std::vector<std::string> rs;
+      if (reason & 1u) rs.push_back("Too many pods");
+      for (size_t r = 0; r < e.res_names.size(); r++)
+        if (reason & (1u << (r + 1))) {
+          rs.push_back("Insufficient " + e.res_names[r]);
+          if (p.req[r] > e.alloc[r * e.N + node]) c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+        }
+      for (size_t k = 0; k < rs.size(); k++) m += (k ? ", " : "") + rs[k];
+      break;
+    }
+    case KSG_PL_POD_TOPOLOGY_SPREAD:
+      c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
+      m = reason == 1 ? "node(s) didn't match pod topology spread constraints (missing required label)"
+                      : "node(s) didn't match pod topology spread constraints";
+      break;
+    case KSG_PL_INTER_POD_AFFINITY:
+      c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
+      m = reason == 1   ? "node(s) didn't match pod affinity rules"
+          : reason == 2 ? "node(s) didn't match pod anti-affinity rules"
+                        : "node(s) didn't satisfy existing pods anti-affinity rules";
+      break;
+    default:
+      *err = "unexpected word";
+      return false;
+  }
+  *code = c;
+  if (msg) *msg = std::move(m);
+  return true;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1745,70 +1825,64 @@ int ksg_snapshot_status(ksg_snapshot* s, int32_t pod, uint32_t word, int32_t nod
   if (!s || !code) return KSG_E_INVALID;
   if (!s->encoded || pod < 0 || pod >= (int32_t)s->e.pods.size() || node < 0 || node >= s->e.N)
     return fail(s, KSG_E_INVALID, "status: index out of range");
-  const Encoded& e = s->e;
-  std::string m;
-  int c = KSG_CODE_SUCCESS;
-  const int pl = (int)(word & 0xffu) - 1;
-  const uint32_t reason = word >> 8;
-  if (word == KSG_FS_NOT_EVALUATED) return fail(s, KSG_E_INVALID, "status: node not evaluated");
-  switch (pl) {
-    case -1:
-      break;
-    case KSG_PL_NODE_UNSCHEDULABLE:
-      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      m = "node(s) were unschedulable";
-      break;
-    case KSG_PL_NODE_NAME:
-      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      m = "node(s) didn't match the requested node name";
-      break;
-    case KSG_PL_TAINT_TOLERATION: {
-      if ((int)reason >= e.max_taints) return fail(s, KSG_E_INVALID, "status: taint slot");
-      const uint32_t t = e.taints[(size_t)reason * e.N + node];
-      if (t == 0) return fail(s, KSG_E_INVALID, "status: empty taint slot");
-      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      m = "node(s) had untolerated taint " + e.taint_strings[t - 1];
-      break;
-    }
-    case KSG_PL_NODE_AFFINITY:
-      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      m = "node(s) didn't match Pod's node affinity/selector";
-      break;
-    case KSG_PL_NODE_RESOURCES_FIT: {
-      // fitsRequest reason order: pods, cpu, memory, ephemeral, scalars;
-      // Unresolvable when the request exceeds the allocatable outright.
-      c = KSG_CODE_UNSCHEDULABLE;
-      const ksg_pod& p = e.pods[pod];
-      std::vector<std::string> rs;
-      if (reason & 1u) rs.push_back("Too many pods");
-      for (size_t r = 0; r < e.res_names.size(); r++)
-        if (reason & (1u << (r + 1))) {
-          rs.push_back("Insufficient " + e.res_names[r]);
-          if (p.req[r] > e.alloc[r * e.N + node]) c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-        }
-      for (size_t k = 0; k < rs.size(); k++) m += (k ? ", " : "") + rs[k];
-      break;
-    }
-    case KSG_PL_POD_TOPOLOGY_SPREAD:
-      c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
-      m = reason == 1 ? "node(s) didn't match pod topology spread constraints (missing required label)"
-                      : "node(s) didn't match pod topology spread constraints";
-      break;
-    case KSG_PL_INTER_POD_AFFINITY:
-      c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
-      m = reason == 1   ? "node(s) didn't match pod affinity rules"
-          : reason == 2 ? "node(s) didn't match pod anti-affinity rules"
-                        : "node(s) didn't satisfy existing pods anti-affinity rules";
-      break;
-    default:
-      return fail(s, KSG_E_INVALID, "status: unexpected word");
-  }
+  std::string m, err;
+  int c;
+  if (!status_of(s->e, pod, word, node, &c, &m, &err)) return fail(s, KSG_E_INVALID, "status: " + err);
   *code = c;
   if (len) *len = (int32_t)m.size();
   if (msg && cap > 0) {
     const size_t n = std::min<size_t>(m.size(), (size_t)cap - 1);
     std::memcpy(msg, m.data(), n);
     msg[n] = 0;
+  }
+  return KSG_OK;
+}
+
+int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
+                          int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len) {
+  if (!s || !words || !code || !msg) return KSG_E_INVALID;
+  if (!s->encoded || pod < 0 || pod >= (int32_t)s->e.pods.size() || n_nodes != s->e.N)
+    return fail(s, KSG_E_INVALID, "statuses: index out of range");
+  const Encoded& e = s->e;
+  // distinct messages: keyed by the word, plus the taint id for TaintToleration
+  std::map<uint64_t, int32_t> seen;
+  std::vector<std::string> msgs;
+  for (int32_t n = 0; n < n_nodes; n++) {
+    const uint32_t w = words[n];
+    if (w == 0 || w == KSG_FS_NOT_EVALUATED) {
+      code[n] = KSG_CODE_SUCCESS;
+      msg[n] = -1;
+      continue;
+    }
+    const int pl = (int)(w & 0xffu) - 1;
+    uint64_t key = w;
+    if (pl == KSG_PL_TAINT_TOLERATION && (int)(w >> 8) < e.max_taints)
+      key |= (uint64_t)e.taints[(size_t)(w >> 8) * e.N + n] << 32;
+    auto it = seen.find(key);
+    int c;
+    std::string err;
+    if (it == seen.end()) {
+      std::string m;
+      if (!status_of(e, pod, w, n, &c, &m, &err)) return fail(s, KSG_E_INVALID, "statuses: " + err);
+      it = seen.emplace(key, (int32_t)msgs.size()).first;
+      msgs.push_back(std::move(m));
+    } else if (!status_of(e, pod, w, n, &c, nullptr, &err)) {   // the code may depend on the node
+      return fail(s, KSG_E_INVALID, "statuses: " + err);
+    }
+    code[n] = c;
+    msg[n] = it->second;
+  }
+  int64_t total = 0;
+  for (auto& m : msgs) total += (int64_t)m.size() + 1;
+  if (n_msgs) *n_msgs = (int32_t)msgs.size();
+  if (len) *len = total;
+  if (buf && cap >= total) {
+    char* o = buf;
+    for (auto& m : msgs) {
+      std::memcpy(o, m.data(), m.size());
+      o += m.size();
+      *o++ = 0;
+    }
   }
   return KSG_OK;
 }

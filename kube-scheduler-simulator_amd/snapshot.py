@@ -308,6 +308,8 @@ class Snapshot:
         self._prefilter = f("prefilter", C.c_int, vp, i32, i32, C.c_uint32, C.POINTER(i32), C.POINTER(i32),
                             C.POINTER(cp), i32, C.POINTER(i32))
         self._profile_info = f("profile_info", C.c_int, vp, C.POINTER(ProfileInfo))
+        self._statuses = f("statuses", C.c_int, vp, i32, C.POINTER(C.c_uint32), i32, C.POINTER(i32),
+                           C.POINTER(i32), C.c_char_p, i64, C.POINTER(i32), C.POINTER(i64))
         self.h = vp()
         k = _Keep()
         rc = self._new(C.byref(profile_view(prof, k)), C.byref(self.h))
@@ -348,6 +350,14 @@ class Snapshot:
         k = _Keep()
         idx = i32()
         self._check(self._add_pod(self.h, C.byref(pod_view(p, k)), C.byref(idx)), "add_pod")
+        self.n_pods = idx.value + 1
+        return idx.value
+
+    def add_pod_view(self, view: "PodView") -> int:
+        """ksg_snapshot_add_pod of a view built beforehand (pod_view; its
+        buffers kept alive by the caller): the per-cycle call alone."""
+        idx = i32()
+        self._check(self._add_pod(self.h, C.byref(view), C.byref(idx)), "add_pod")
         self.n_pods = idx.value + 1
         return idx.value
 
@@ -445,6 +455,23 @@ class Snapshot:
             self._check(self._status(self.h, pod, word, node, C.byref(code), buf, ln.value + 1, C.byref(ln)),
                         "status")
         return code.value, buf.value.decode("utf-8")
+
+    def statuses(self, pod: int, words) -> Tuple[np.ndarray, np.ndarray, List[str]]:
+        """ksg_snapshot_statuses: (codes[N], message index[N] (-1 = none),
+        distinct messages) of every node's Filter status word at once."""
+        w = np.ascontiguousarray(words, np.uint32)
+        n = len(w)
+        code = np.zeros(n, np.int32)
+        msg = np.zeros(n, np.int32)
+        nm, ln = i32(), i64()
+        u32p = C.POINTER(C.c_uint32)
+        args = (self.h, pod, w.ctypes.data_as(u32p), n, code.ctypes.data_as(C.POINTER(i32)),
+                msg.ctypes.data_as(C.POINTER(i32)))
+        self._check(self._statuses(*args, None, 0, C.byref(nm), C.byref(ln)), "statuses")
+        buf = C.create_string_buffer(max(ln.value, 1))
+        self._check(self._statuses(*args, buf, ln.value, C.byref(nm), C.byref(ln)), "statuses")
+        texts = buf.raw[:ln.value].split(b"\0")[:nm.value]
+        return code, msg, [t.decode("utf-8") for t in texts]
 
     def prefilter(self, pod: int, plugin: int, result_status: int = 0):
         """(code, node names or None) of plugin's PreFilter for the pod."""

@@ -301,6 +301,62 @@ static scenario scenario_kat(void) {
   return s;
 }
 
+/* ---- the reference's export sample profile (tests/golden/export_profile.txt,
+ * written by tests/golden/make_export_profile.py from export.md:32): the view a
+ * Go caller builds after ConvertForSimulator, per-point sets included ---- */
+static const char* g_export_path = NULL;
+
+static int load_export_profile(const char* path, ksg_profile_view* pv) {
+  static const char* pts[KSG_NPOINTS] = {"preFilter", "filter", "preScore", "score"};
+  FILE* f = fopen(path, "r");
+  if (!f) return -1;
+  memset(pv, 0, sizeof *pv);
+  ksg_plugin_view* mp = A(64, sizeof *mp);
+  ksg_plugin_view* en[KSG_NPOINTS];
+  const char** dis[KSG_NPOINTS];
+  for (int k = 0; k < KSG_NPOINTS; k++) { en[k] = A(32, sizeof **en); dis[k] = A(32, sizeof **dis); }
+  ksg_quantity* fr = A(8, sizeof *fr);
+  ksg_quantity* br = A(8, sizeof *br);
+  char line[512], a[128], b[128], c[128];
+  while (fgets(line, sizeof line, f)) {
+    if (line[0] == '#' || line[0] == '\n') continue;
+    int w = 0, k;
+    if (sscanf(line, "multipoint %127s %d", a, &w) == 2) {
+      mp[pv->n_plugins++] = (ksg_plugin_view){strdup(a), w};
+    } else if (sscanf(line, "enabled %127s %127s %d", a, b, &w) == 3) {
+      for (k = 0; k < KSG_NPOINTS && strcmp(a, pts[k]); k++) {}
+      if (k == KSG_NPOINTS) return -1;
+      en[k][pv->points[k].n_enabled++] = (ksg_plugin_view){strdup(b), w};
+      pv->points[k].enabled = en[k];
+    } else if (sscanf(line, "disabled %127s %127s", a, b) == 2) {
+      for (k = 0; k < KSG_NPOINTS && strcmp(a, pts[k]); k++) {}
+      if (k == KSG_NPOINTS) return -1;
+      dis[k][pv->points[k].n_disabled++] = strdup(b);
+      pv->points[k].disabled = dis[k];
+    } else if (sscanf(line, "fit_strategy %127s", a) == 1) {
+      pv->fit_strategy = strdup(a);
+    } else if (sscanf(line, "fit_resource %127s %d", a, &w) == 2) {
+      fr[pv->n_fit_resources++] = (ksg_quantity){strdup(a), w};
+      pv->fit_resources = fr;
+    } else if (sscanf(line, "ba_resource %127s %d", a, &w) == 2) {
+      br[pv->n_ba_resources++] = (ksg_quantity){strdup(a), w};
+      pv->ba_resources = br;
+    } else if (sscanf(line, "hard_pod_affinity_weight %d", &w) == 1) {
+      pv->hard_pod_affinity_weight = w;
+    } else if (sscanf(line, "ignore_preferred_terms_of_existing_pods %d", &w) == 1) {
+      pv->ignore_preferred_terms_of_existing_pods = w;
+    } else if (sscanf(line, "pts_system_defaulted %d", &w) == 1) {
+      pv->pts_system_defaulted = w;
+    } else if (sscanf(line, "%127s %127s %127s", a, b, c) >= 1) {
+      fclose(f);
+      return -1;
+    }
+  }
+  fclose(f);
+  pv->plugins = mp;
+  return pv->n_plugins > 0 ? 0 : -1;
+}
+
 static ksg_snapshot* build(const scenario* s, int n_pods) {
   ksg_snapshot* snap;
   OK(ksg_snapshot_new(&s->prof, &snap));
@@ -484,9 +540,220 @@ static int run_gpu(void) {
   return g_fail;
 }
 
+/* ---- annotations of one cycle through ksg_annotate, with the profile's
+ * derived orders and the Store's weight map (ksg_snapshot_profile_info) ---- */
+typedef struct {
+  const char* s[3];
+  int64_t len[3];
+} ann3;
+
+static ksg_annotator* annotator_of(ksg_snapshot* snap) {
+  static const char* plugin_names[KSG_NPLUGINS] = {
+      "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts", "NodeResourcesFit",
+      "VolumeRestrictions", "NodeVolumeLimits", "VolumeBinding", "VolumeZone", "PodTopologySpread",
+      "InterPodAffinity", "NodeResourcesBalancedAllocation", "ImageLocality"};
+  int32_t N, P, R, T;
+  OK(ksg_snapshot_counts(snap, &N, &P, &R, &T));
+  const char** node = A(N, sizeof *node);
+  const char** res = A(R, sizeof *res);
+  const char** taint = A(T ? T : 1, sizeof *taint);
+  OK(ksg_snapshot_names(snap, node, res, taint));
+  ksg_nodes nd;
+  OK(ksg_snapshot_view(snap, &nd, NULL, NULL, NULL));
+  ksg_names nm = {N, node, plugin_names, R, res, T, taint, nd.max_taints, nd.taints};
+  ksg_annotator* an;
+  OK(ksg_annotator_new(&nm, &an));
+  return an;
+}
+
+/* filter-result / score-result / finalscore-result of one cycle; the strings
+ * are copied (the annotator owns its buffers until the next call) */
+static ann3 annotate(ksg_annotator* an, const ksg_profile_info* info, const ksg_pod* pod, const ksg_result* r,
+                     const ksg_capture* cap) {
+  int32_t fo[KSG_NPLUGINS], so[KSG_NPLUGINS], nf = 0, ns = 0;
+  uint32_t fskip = pod->filter_skip;
+  if (r->status & KSG_ST_IPA_PREFILTER_SKIP) fskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
+  for (int k = 0; k < info->n_order[KSG_POINT_FILTER]; k++) {
+    const int pl = info->order[KSG_POINT_FILTER][k];
+    if (!((fskip >> pl) & 1u)) fo[nf++] = pl;
+  }
+  if (r->n_feasible >= 2)
+    for (int k = 0; k < info->n_order[KSG_POINT_SCORE]; k++) {
+      const int pl = info->order[KSG_POINT_SCORE][k];
+      if (!((r->score_skip >> pl) & 1u)) so[ns++] = pl;
+    }
+  ksg_annotate_in in = {nf, fo, ns, so, info->normalize_mask, info->store_weight, r->n_feasible,
+                        cap->fstatus, cap->raw, cap->norm};
+  const char* js[3];
+  int64_t ln[3];
+  OK(ksg_annotate(an, &in, js, ln));
+  ann3 out;
+  for (int i = 0; i < 3; i++) {
+    char* c = malloc(ln[i] + 1);
+    memcpy(c, js[i], ln[i]);
+    c[ln[i]] = 0;
+    out.s[i] = c;
+    out.len[i] = ln[i];
+  }
+  return out;
+}
+
+static void free_ann(ann3* a) {
+  for (int i = 0; i < 3; i++) free((void*)a->s[i]);
+}
+
+/* Orders and weights the sample's profile must derive (the Python model pins
+ * the same lists: tests/test_ingest.py test_export_sample_per_point_expansion). */
+static void check_export_info(ksg_snapshot* snap, ksg_profile_info* info) {
+  OK(ksg_snapshot_profile_info(snap, info));
+  static const int filter[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+  static const int prefilter[] = {5, 4, 6, 10, 11, 8, 3, 7, 9};
+  static const int prescore[] = {11, 10, 2, 3, 5, 8, 12};
+  static const int score[] = {12, 13, 11, 5, 3, 10, 2, 8};
+  const int* want[KSG_NPOINTS] = {prefilter, filter, prescore, score};
+  const int nwant[KSG_NPOINTS] = {9, 12, 7, 8};
+  for (int pt = 0; pt < KSG_NPOINTS; pt++) {
+    int same = info->n_order[pt] == nwant[pt];
+    for (int k = 0; same && k < nwant[pt]; k++) same = info->order[pt][k] == want[pt][k];
+    CHECK(same, "export profile: point %d order differs", pt);
+  }
+  /* the Store keeps MultiPoint's weight, the framework the Score point's */
+  CHECK(info->store_weight[KSG_PL_TAINT_TOLERATION] == 3 && info->selection_weight[KSG_PL_TAINT_TOLERATION] == 1,
+        "export profile: TaintToleration weights %lld / %d", (long long)info->store_weight[KSG_PL_TAINT_TOLERATION],
+        info->selection_weight[KSG_PL_TAINT_TOLERATION]);
+  CHECK(info->store_weight[KSG_PL_POD_TOPOLOGY_SPREAD] == 2 && info->selection_weight[KSG_PL_POD_TOPOLOGY_SPREAD] == 2,
+        "export profile: PodTopologySpread weights");
+  CHECK(info->store_weight[KSG_PL_NODE_AFFINITY] == 2 && info->selection_weight[KSG_PL_NODE_AFFINITY] == 1,
+        "export profile: NodeAffinity weights");
+}
+
+/* The sample's profile over a config-2 cluster (node-local pods: the
+ * per-cycle chip-wide path) and a config-3 cluster (topology pods). */
+static scenario scenario_export(int k, const ksg_profile_view* pv) {
+  scenario s = k == 0 ? scenario_c2(96, 300, 24) : scenario_c3(64, 240, 16, 8);
+  s.name = k == 0 ? "export-c2" : "export-c3";
+  s.prof = *pv;
+  return s;
+}
+
+static int run_export(int gpu) {
+  ksg_profile_view pv;
+  if (!g_export_path || load_export_profile(g_export_path, &pv)) {
+    fprintf(stderr, "cannot read the export profile fixture %s\n", g_export_path ? g_export_path : "(none)");
+    return 2;
+  }
+  for (int k = 0; k < 2; k++) {
+    const scenario sc = scenario_export(k, &pv);
+    const scenario* s = &sc;
+    const int N = s->n_nodes, Q = s->n_pods - s->n_bound;
+    ksg_snapshot* full = build(s, s->n_pods);
+    ksg_profile_info info;
+    check_export_info(full, &info);
+    OK(ksg_snapshot_encode(full));
+    kso_ctx* o = oracle_of(full, s);
+    int32_t* want = A(Q, 4);
+    ksg_result* wres = A(Q, sizeof *wres);
+    oracle_queue(o, s, want, wres);
+    kso_close(o);
+    if (!gpu) {
+      int placed = 0;
+      for (int i = 0; i < Q; i++) placed += want[i] >= 0;
+      CHECK(placed > 0, "%s: nothing placed", s->name);
+      printf("ok %s profile info (per-point orders, store vs selection weights), oracle queue %d of %d placed\n",
+             s->name, placed, Q);
+      ksg_snapshot_free(full);
+      continue;
+    }
+    /* (1) whole queue on the device */
+    ksg_ctx* ctx;
+    OK(ksg_open(0, &ctx));
+    if (ksg_snapshot_load(full, ctx)) {
+      fprintf(stderr, "load: %s\n", ksg_snapshot_error(full));
+      return 2;
+    }
+    int32_t* pl = A(Q, 4);
+    ksg_result* res = A(Q, sizeof *res);
+    OK(ksg_run_queue(ctx, s->n_bound, Q, pl, res, NULL));
+    int bad = 0;
+    for (int i = 0; i < Q; i++)
+      bad += pl[i] != want[i] || res[i].n_feasible != wres[i].n_feasible || res[i].status != wres[i].status ||
+             res[i].score_skip != wres[i].score_skip;
+    CHECK(bad == 0, "%s: %d of %d pods differ from the oracle (ksg_run_queue)", s->name, bad, Q);
+    ksg_close(ctx);
+    /* (2) the per-cycle path with capture, statuses and annotation bytes */
+    ksg_snapshot* cyc = build(s, s->n_bound);
+    OK(ksg_open(0, &ctx));
+    if (ksg_snapshot_load(cyc, ctx)) {
+      fprintf(stderr, "load: %s\n", ksg_snapshot_error(cyc));
+      return 2;
+    }
+    o = oracle_of(full, s);
+    uint32_t *fs = A(N, 4), *wfs = A(N, 4);
+    int64_t *raw = A((size_t)KSG_NPLUGINS * N, 8), *norm = A((size_t)KSG_NPLUGINS * N, 8), *tot = A(N, 8);
+    int64_t *wraw = A((size_t)KSG_NPLUGINS * N, 8), *wnorm = A((size_t)KSG_NPLUGINS * N, 8), *wtot = A(N, 8);
+    ksg_capture cap = {fs, raw, norm, tot}, wcap = {wfs, wraw, wnorm, wtot};
+    int32_t* codes = A(N, 4);
+    int32_t* msgi = A(N, 4);
+    char* msgs = A(1 << 16, 1);
+    ksg_annotator* an = annotator_of(full);
+    int mismatch = 0, ann_bad = 0, scored = 0, fast = 0;
+    int64_t ann_bytes = 0;
+    for (int j = s->n_bound; j < s->n_pods; j++) {
+      int32_t idx, ap, path, flags, nm;
+      int64_t ml;
+      OK(ksg_snapshot_add_pod(cyc, &s->pods[j], &idx));
+      if (ksg_snapshot_sync(cyc, ctx, &ap)) {
+        fprintf(stderr, "sync: %s\n", ksg_snapshot_error(cyc));
+        return 2;
+      }
+      memset(raw, 0, 8 * (size_t)KSG_NPLUGINS * N);
+      memset(norm, 0, 8 * (size_t)KSG_NPLUGINS * N);
+      memset(wraw, 0, 8 * (size_t)KSG_NPLUGINS * N);
+      memset(wnorm, 0, 8 * (size_t)KSG_NPLUGINS * N);
+      ksg_result r, wr;
+      OK(ksg_eval(ctx, idx, &r, &cap));
+      OK(ksg_last_run_info(ctx, &path, &flags));
+      fast += path == 5;
+      OK(kso_eval(o, j, &wr, &wcap));
+      if (r.selected != wr.selected || r.n_feasible != wr.n_feasible || r.status != wr.status ||
+          memcmp(fs, wfs, 4 * N) != 0)
+        mismatch++;
+      OK(ksg_snapshot_statuses(cyc, idx, fs, N, codes, msgi, msgs, 1 << 16, &nm, &ml));
+      ksg_workload wl;
+      OK(ksg_snapshot_view(cyc, NULL, NULL, &wl, NULL));
+      ann3 a = annotate(an, &info, &wl.pods[idx], &r, &cap);
+      ann3 b = annotate(an, &info, &wl.pods[idx], &wr, &wcap);
+      for (int i = 0; i < 3; i++) {
+        ann_bad += a.len[i] != b.len[i] || memcmp(a.s[i], b.s[i], a.len[i]) != 0;
+        ann_bytes += a.len[i];
+      }
+      free_ann(&a);
+      free_ann(&b);
+      scored += r.n_feasible >= 2;
+      if (r.selected >= 0) {
+        OK(ksg_snapshot_assume(cyc, ctx, idx, r.selected));
+        OK(kso_commit(o, j, r.selected));
+      }
+    }
+    CHECK(mismatch == 0, "%s: %d of %d cycles differ from the oracle", s->name, mismatch, Q);
+    CHECK(ann_bad == 0, "%s: %d annotation values differ from the oracle's", s->name, ann_bad);
+    CHECK(k != 0 || fast == Q, "%s: %d of %d cycles on the per-cycle chip-wide path", s->name, fast, Q);
+    printf("ok %s: ksg_run_queue identical; per-cycle path %d cycles (%d chip-wide, %d scored), status words and "
+           "%lld annotation bytes identical to the oracle\n", s->name, Q, fast, scored, (long long)ann_bytes);
+    ksg_annotator_free(an);
+    kso_close(o);
+    ksg_close(ctx);
+    ksg_snapshot_free(cyc);
+    ksg_snapshot_free(full);
+  }
+  return g_fail;
+}
+
 int main(int argc, char** argv) {
   const int gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
-  const int rc = gpu ? run_gpu() : run_cpu();
+  if (argc > 2) g_export_path = argv[2];
+  int rc = gpu ? run_gpu() : run_cpu();
+  if (rc == 0 && g_export_path) rc = run_export(gpu);
   printf(rc ? "FAILED (%d checks)\n" : "PASSED\n", rc);
   return rc ? 1 : 0;
 }

@@ -1,0 +1,138 @@
+"""The per-cycle path (ksg_eval): one pod's PreFilter ..
+NormalizeScore on the chip-wide kernels with persistent buffers, as the Go
+shim calls it once per scheduling cycle, against the C++ oracle's ksg_eval
+(kso_eval) pod by pod: result, every node's status word, the score plugins'
+raw / normalised rows and the totals; each pod is then assumed on both (the
+host-driven eval -> commit loop).  Topology pods take the queue kernel."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import pkg
+
+G = pkg("generator")
+E = pkg("encoder")
+P = pkg("profile")
+native = pkg("native")
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "c2-1000x120": lambda: G.config2(n_nodes=1000, n_pods=120, seed=3),
+    "c2-tight": lambda: G.config2(n_nodes=7, n_pods=60, seed=11),
+    "c2-most": lambda: (lambda n, p, _: (n, p, P.config2_profile(strategy=P.MOST_ALLOCATED)))(
+        *G.config2(n_nodes=300, n_pods=80, seed=12)),
+    "c1-100x150": lambda: G.config1(n_nodes=100, n_pods=150),
+    "c5-small": lambda: G.config5(n_nodes=400, n_pods=60, n_images=200, taint_vocab=128, taints_per_node=16,
+                                  images_per_node=20),
+    "c3-60x80": lambda: G.config3(n_nodes=60, n_pods=80, apps=12, zones=4),
+    "readme-kat2": G.readme_kat2,
+}
+CASES.update({f"zoo-{s}": (lambda s=s: __import__("zoo").zoo(s, n_pods=60)) for s in range(4)})
+
+
+@pytest.fixture(scope="module")
+def gpu(built):
+    return native.Engine(device=0)
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import binding
+    return binding.Oracle(8)
+
+
+def _score_rows(pf):
+    return [p for p in range(native.NPLUGINS) if (pf["score_mask"] >> p) & 1]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_eval_cycle_matches_oracle(gpu, oracle, name):
+    nodes, pods, prof = CASES[name]()
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    oracle.load(enc, pf)
+    N = len(nodes)
+    rows = _score_rows(pf)
+    fast = 0
+    for i in range(len(pods)):
+        cg, co = native.CaptureBuffers(N, 1), native.CaptureBuffers(N, 1)
+        rg, ro = gpu.eval(i, cg), oracle.eval(i, co)
+        fast += gpu.last_run_info()[0] == 5
+        assert (rg.selected, rg.n_feasible, rg.status, rg.score_skip) == \
+            (ro.selected, ro.n_feasible, ro.status, ro.score_skip), (name, i)
+        np.testing.assert_array_equal(cg.fstatus, co.fstatus, err_msg=f"{name} pod {i} status words")
+        if ro.status & native.ST_SCORED:
+            feas = co.fstatus[0] == 0
+            for pid in rows:
+                if (ro.score_skip >> pid) & 1:
+                    continue
+                np.testing.assert_array_equal(cg.raw[0, pid][feas], co.raw[0, pid][feas], err_msg=f"{name} {i} raw")
+                np.testing.assert_array_equal(cg.norm[0, pid][feas], co.norm[0, pid][feas], err_msg=f"{name} {i}")
+            np.testing.assert_array_equal(cg.total[0][feas], co.total[0][feas], err_msg=f"{name} pod {i} total")
+        if rg.selected >= 0:
+            gpu.commit(i, rg.selected)
+            oracle.commit(i, ro.selected)
+    R = len(enc.cluster.res_names)
+    for a, b in zip(gpu.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(a, b)
+    if name.startswith(("c2", "c1", "c5", "readme")):
+        assert fast == len(pods), f"{name}: {fast} of {len(pods)} cycles on the per-cycle path"
+
+
+def test_eval_fast_equals_queue_kernel_capture(gpu, built):
+    """The chip-wide per-cycle capture equals the single-workgroup queue
+    kernel's (KSG_EVAL_FAST=0) on every row the profile scores, infeasible
+    nodes included."""
+    old = os.environ.get("KSG_EVAL_FAST")
+    os.environ["KSG_EVAL_FAST"] = "0"
+    try:
+        slow = native.Engine(device=0)
+    finally:
+        if old is None:
+            del os.environ["KSG_EVAL_FAST"]
+        else:
+            os.environ["KSG_EVAL_FAST"] = old
+    nodes, pods, prof = G.config2(n_nodes=2000, n_pods=40, seed=8)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    slow.load(enc, pf)
+    rows = _score_rows(pf)
+    for i in range(len(pods)):
+        a, b = native.CaptureBuffers(len(nodes), 1), native.CaptureBuffers(len(nodes), 1)
+        ra, rb = gpu.eval(i, a), slow.eval(i, b)
+        assert gpu.last_run_info()[0] == 5 and slow.last_run_info()[0] == 1
+        assert (ra.selected, ra.n_feasible, ra.status, ra.score_skip) == (rb.selected, rb.n_feasible, rb.status,
+                                                                           rb.score_skip)
+        np.testing.assert_array_equal(a.fstatus, b.fstatus)
+        np.testing.assert_array_equal(a.raw[:, rows], b.raw[:, rows])
+        np.testing.assert_array_equal(a.norm[:, rows], b.norm[:, rows])
+        if ra.selected >= 0:
+            gpu.commit(i, ra.selected)
+            slow.commit(i, rb.selected)
+
+
+def test_eval_without_capture_and_eval_pod(gpu, oracle):
+    """No capture buffers (placement only), and ksg_eval_pod of an encoded pod
+    outside the workload, on the per-cycle path."""
+    nodes, pods, prof = G.config2(n_nodes=500, n_pods=30, seed=4)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    oracle.load(enc, pf)
+    for i in range(len(pods)):
+        rg, ro = gpu.eval(i), oracle.eval(i)
+        assert (rg.selected, rg.n_feasible, rg.status) == (ro.selected, ro.n_feasible, ro.status)
+        rec = enc.workload.pods[i].copy()
+        lo, hi = int(rec["blob"]), int(rec["blob"]) + int(rec["blob_len"])
+        for f in ("tol", "na_req", "na_pref", "img", "node_set", "pts", "ipa", "commit", "blob"):
+            if int(rec[f]) >= 0:
+                rec[f] = int(rec[f]) - lo
+        rp = gpu.eval_pod(rec, enc.workload.prog[lo:hi])
+        assert (rp.selected, rp.n_feasible, rp.status) == (ro.selected, ro.n_feasible, ro.status)
+        if rg.selected >= 0:
+            gpu.commit(i, rg.selected)
+            oracle.commit(i, ro.selected)

@@ -1,17 +1,24 @@
 """The drop-in boundary from C only (tests/c/snapshot_c_test.c): clusters
 built from strings through include/ksched_snapshot.h, encoded by
 libksched.so, scheduled on the oracle (CPU) and on the MI355X (GPU, whole
-queue and the Go shim's per-cycle path), compared with the oracle."""
+queue and the Go shim's per-cycle path), compared with the oracle; and the
+reference's export sample profile (per-point plugin sets, Store vs selection
+weights) through the C ABI only: placements, status words and annotation
+bytes against the oracle's."""
 import os
 import subprocess
 
 import pytest
 
-BIN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "snapshot_c_test")
+HERE = os.path.dirname(os.path.abspath(__file__))
+BIN = os.path.join(HERE, "c", "snapshot_c_test")
+# the reference's export sample profile as a cgo caller passes it
+# (tests/golden/make_export_profile.py)
+EXPORT_PROFILE = os.path.join(HERE, "golden", "export_profile.txt")
 
 
 def _run(flag):
-    r = subprocess.run([BIN, flag], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([BIN, flag, EXPORT_PROFILE], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr

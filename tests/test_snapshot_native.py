@@ -190,6 +190,15 @@ def test_status_codes_and_messages(built):
             assert msg == dec.message(w, n)
             assert code == F.status_code(w, enc, pi, n)
             seen.add((w & 0xFF) - 1)
+        # the bulk decode (once per pod, as the Go shim's evalPod) agrees node by node
+        codes, idx, texts = snap.statuses(pi, cap.fstatus[0])
+        for n, w in enumerate(cap.fstatus[0]):
+            w = int(w)
+            if w in (0, E.FS_NOT_EVALUATED):
+                assert codes[n] == 0 and idx[n] == -1
+            else:
+                assert (int(codes[n]), texts[idx[n]]) == snap.status(pi, w, n)
+        assert len(texts) == len(set(texts))
         o.commit(pi, max(0, int(np.argmin(cap.fstatus[0]))))
     assert {P.TAINT_TOLERATION, P.NODE_RESOURCES_FIT} <= seen
 
