@@ -2417,6 +2417,10 @@ struct ksg_ctx {
   ksg_profile* d_ev_prof = nullptr;
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
+  // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
+  char* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
+  hipEvent_t ev_stage = nullptr;            // the last staged copy is done when this fires
 };
 
 namespace {
@@ -3649,14 +3653,27 @@ bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
 int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   const size_t N = ctx->c.N;
   const ksg_profile& prof = ctx->prof;
-  int rows[KSG_NPLUGINS], n_rows = 0;
-  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+  // score rows, the normalising plugins first (only their norm rows differ
+  // from the raw ones, so only those come back)
+  int rows[KSG_NPLUGINS], n_rows = 0, n_normrows = 0;
+  for (int pl : {KSG_PL_TAINT_TOLERATION, KSG_PL_NODE_AFFINITY})
     if ((prof.score_mask >> pl) & 1u) rows[n_rows++] = pl;
+  n_normrows = n_rows;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if (((prof.score_mask >> pl) & 1u) && pl != KSG_PL_TAINT_TOLERATION && pl != KSG_PL_NODE_AFFINITY)
+      rows[n_rows++] = pl;
+  // int32 rows when every total fits (raw values are bounded by batch_eligible)
+  int64_t wabs = 0;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if ((prof.score_mask >> pl) & 1u) wabs += prof.weight[pl] < 0 ? -(int64_t)prof.weight[pl] : prof.weight[pl];
+  const bool narrow = wabs * 100 < (1ll << 31);
+  const size_t es = narrow ? 4 : 8;
   const bool want_fs = cap && cap->fstatus, want_raw = cap && cap->raw, want_norm = cap && cap->norm,
              want_tot = cap && cap->total;
-  // block: slot[2] | -1 | fstatus[N] | raw[n_rows][N] | norm[n_rows][N] | total[N] | rec[N]
+  // block: slot[2] | -1 | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_rows][N] | rec[N] (u64)
   const size_t o_neg = 2 * sizeof(EvSlot), o_fs = o_neg + 8, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
-  const size_t o_norm = o_raw + 8 * N * n_rows, o_tot = o_norm + 8 * N * n_rows, o_rec = o_tot + 8 * N;
+  const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
+  const size_t o_rec = o_norm + ((es * N * n_rows + 7) & ~(size_t)7);
   const size_t need = o_rec + 8 * N;
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
@@ -3714,6 +3731,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   ca.raw = reinterpret_cast<int64_t*>(ctx->d_ev + o_raw);
   ca.norm = reinterpret_cast<int64_t*>(ctx->d_ev + o_norm);
   ca.total = want_tot ? reinterpret_cast<int64_t*>(ctx->d_ev + o_tot) : nullptr;
+  ca.narrow = narrow ? 1 : 0;
   ca.best = &slot->best;
   ca.err = &slot->err;
   ca.next = reinterpret_cast<int32_t*>(reinterpret_cast<EvSlot*>(ctx->d_ev) + (1 - par));
@@ -3727,8 +3745,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   // one copy back: both slots, the -1 word and the rows the caller asked for
   size_t back = o_fs;
   if (want_fs) back = o_raw;
-  if (want_raw || want_norm) back = o_tot;
-  if (want_tot) back = o_rec;
+  if (want_raw || want_norm) back = o_raw + es * N * n_rows;
+  if (want_tot) back = o_tot + es * N;
+  if (want_norm && n_normrows) back = o_norm + es * N * n_normrows;
   HIPC(ctx, hipMemcpyAsync(ctx->h_ev, ctx->d_ev, back, hipMemcpyDeviceToHost, ctx->stream));
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
   const EvSlot& h = reinterpret_cast<const EvSlot*>(ctx->h_ev)[par];
@@ -3760,12 +3779,21 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   res->n_feasible = nfeas;
   res->status = status;
   res->score_skip = score_skip;
+  auto put_row = [&](int64_t* dst, size_t off) {   // one row into the caller's int64 array
+    if (narrow) {
+      const int32_t* src = reinterpret_cast<const int32_t*>(ctx->h_ev + off);
+      for (size_t n = 0; n < N; n++) dst[n] = src[n];
+    } else {
+      std::memcpy(dst, ctx->h_ev + off, 8 * N);
+    }
+  };
   if (want_fs) std::memcpy(cap->fstatus, ctx->h_ev + o_fs, 4 * N);
   for (int q = 0; q < n_rows; q++) {
-    if (want_raw) std::memcpy(cap->raw + (size_t)rows[q] * N, ctx->h_ev + o_raw + 8 * N * q, 8 * N);
-    if (want_norm) std::memcpy(cap->norm + (size_t)rows[q] * N, ctx->h_ev + o_norm + 8 * N * q, 8 * N);
+    if (want_raw) put_row(cap->raw + (size_t)rows[q] * N, o_raw + es * N * q);
+    // plugins without ScoreExtensions record the raw score as the final one
+    if (want_norm) put_row(cap->norm + (size_t)rows[q] * N, q < n_normrows ? o_norm + es * N * q : o_raw + es * N * q);
   }
-  if (want_tot) std::memcpy(cap->total, ctx->h_ev + o_tot, 8 * N);
+  if (want_tot) put_row(cap->total, o_tot);
   ctx->last_path = 5;
   return KSG_OK;
 }
@@ -3830,10 +3858,31 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
   int rc;
   if ((rc = dgrow(ctx, &ctx->d_pods, &ctx->pod_cap, (size_t)ctx->n_pods, (size_t)ctx->n_pods + n))) return rc;
   if ((rc = dgrow(ctx, &ctx->d_prog, &ctx->prog_cap, (size_t)prog_base, (size_t)std::max<int64_t>(new_len, 1)))) return rc;
-  if (n) HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->n_pods, pods, sizeof(ksg_pod) * n, hipMemcpyHostToDevice, ctx->stream));
-  if (prog_len)
-    HIPC(ctx, hipMemcpyAsync(ctx->d_prog + prog_base, prog, sizeof(int32_t) * prog_len, hipMemcpyHostToDevice, ctx->stream));
-  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  const size_t pb = sizeof(ksg_pod) * n, gb = sizeof(int32_t) * prog_len;
+  if (pb + gb <= (1u << 20)) {
+    // the per-cycle append: through a pinned staging buffer, stream-ordered
+    // before the next evaluation, no host wait (the caller's buffers are free
+    // once this returns)
+    if (!ctx->ev_stage) HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_stage, hipEventDisableTiming));
+    else HIPC(ctx, hipEventSynchronize(ctx->ev_stage));   // the previous staged copy has left the buffer
+    if (pb + gb > ctx->h_stage_bytes) {
+      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+      ctx->h_stage = nullptr;
+      ctx->h_stage_bytes = 0;
+      HIPC(ctx, hipHostMalloc((void**)&ctx->h_stage, 1u << 20, hipHostMallocDefault));
+      ctx->h_stage_bytes = 1u << 20;
+    }
+    if (pb) std::memcpy(ctx->h_stage, pods, pb);
+    if (gb) std::memcpy(ctx->h_stage + pb, prog, gb);
+    if (pb) HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->n_pods, ctx->h_stage, pb, hipMemcpyHostToDevice, ctx->stream));
+    if (gb)
+      HIPC(ctx, hipMemcpyAsync(ctx->d_prog + prog_base, ctx->h_stage + pb, gb, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(ctx, hipEventRecord(ctx->ev_stage, ctx->stream));
+  } else {
+    if (n) HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->n_pods, pods, pb, hipMemcpyHostToDevice, ctx->stream));
+    if (prog_len) HIPC(ctx, hipMemcpyAsync(ctx->d_prog + prog_base, prog, gb, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  }
   ctx->h_prog.resize(new_len);
   if (prog_len) std::copy(prog, prog + prog_len, ctx->h_prog.begin() + prog_base);
   for (int i = 0; i < n; i++) {
@@ -3931,6 +3980,8 @@ int ksg_close(ksg_ctx* ctx) {
   }
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->h_ev) (void)hipHostFree(ctx->h_ev);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->ev_stage) (void)hipEventDestroy(ctx->ev_stage);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -4030,7 +4081,9 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
 }
 
 int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
-  if (!ctx || !wl || !wl->pods || wl->n_pods < 0 || wl->prog_len < 0) return KSG_E_INVALID;
+  if (!ctx || !wl || (!wl->pods && wl->n_pods > 0) || wl->n_pods < 0 || wl->prog_len < 0 ||
+      (!wl->prog && wl->prog_len > 0))
+    return KSG_E_INVALID;
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "load nodes before the workload");
   HIPC(ctx, hipSetDevice(ctx->device));
   ctx->h_pods.assign(wl->pods, wl->pods + wl->n_pods);
@@ -4059,8 +4112,11 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
     ctx->d_pods = nullptr;
     ctx->d_prog = nullptr;
   }
-  if ((rc = upload(ctx, &ctx->d_pods, wl->pods, std::max(wl->n_pods, 1)))) return rc;
-  if ((rc = upload(ctx, &ctx->d_prog, wl->prog, (size_t)std::max<int64_t>(wl->prog_len, 1)))) return rc;
+  // an empty workload (pods arrive later through ksg_append_pods) still gets
+  // one-element buffers
+  if ((rc = wl->n_pods ? upload(ctx, &ctx->d_pods, wl->pods, wl->n_pods) : dalloc(ctx, &ctx->d_pods, 1))) return rc;
+  if ((rc = wl->prog_len ? upload(ctx, &ctx->d_prog, wl->prog, (size_t)wl->prog_len) : dalloc(ctx, &ctx->d_prog, 1)))
+    return rc;
   ctx->pod_cap = std::max(wl->n_pods, 1);
   ctx->prog_cap = (size_t)std::max<int64_t>(wl->prog_len, 1);
   HIPC(ctx, hipStreamSynchronize(ctx->stream));

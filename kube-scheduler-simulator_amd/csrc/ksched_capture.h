@@ -49,7 +49,15 @@ struct CapArgs {
   unsigned long long* best;
   uint32_t* err;
   int32_t* next;                 // 8 words: the next call's stats[4], best, err
+  int32_t narrow;                // raw / norm / total rows are int32 (the per-cycle path's copy-back; the
+                                 // host checked every value fits) instead of int64
 };
+
+// Row element idx of a capture array: int64, or int32 in the narrow form.
+__device__ __forceinline__ void cap_put(int64_t* base, size_t idx, int64_t v, bool narrow) {
+  if (narrow) reinterpret_cast<int32_t*>(base)[idx] = (int32_t)v;
+  else base[idx] = v;
+}
 
 __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
@@ -101,10 +109,11 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
         default: break;
       }
       x = ok && ((v.smask >> pl) & 1u) ? x : 0;
-      a.raw[(o * a.n_rows + q) * NN + n] = x;
+      cap_put(a.raw, (o * a.n_rows + q) * NN + n, x, a.narrow);
       // plugins without ScoreExtensions record the raw score again; the two
       // normalised ones are overwritten by ksg_capture_norm
-      a.norm[(o * a.n_rows + q) * NN + n] = (pl == KSG_PL_TAINT_TOLERATION || pl == KSG_PL_NODE_AFFINITY) ? 0 : x;
+      cap_put(a.norm, (o * a.n_rows + q) * NN + n,
+              (pl == KSG_PL_TAINT_TOLERATION || pl == KSG_PL_NODE_AFFINITY) ? 0 : x, a.narrow);
     }
     if (ok) {
       feas = 1;
@@ -182,16 +191,16 @@ __global__ __launch_bounds__(256) void ksg_capture_norm(CapArgs a) {
     uint32_t err = 0;
     total = total_score(v, (uint32_t)x, (x >> 48) & 0xff, (x >> 32) & 0xffff, max_t, max_a, err, &nt, &na);
   }
-  if (a.total) a.total[o * NN + n] = total;
+  if (a.total) cap_put(a.total, o * NN + n, total, a.narrow);
   for (int q = 0; q < a.n_rows; q++) {
     const int pl = a.rows[q];
     if (nfeas < 2) {   // fewer than two feasible nodes: no Score runs, nothing recorded
-      a.raw[(o * a.n_rows + q) * NN + n] = 0;
-      a.norm[(o * a.n_rows + q) * NN + n] = 0;
+      cap_put(a.raw, (o * a.n_rows + q) * NN + n, 0, a.narrow);
+      cap_put(a.norm, (o * a.n_rows + q) * NN + n, 0, a.narrow);
     } else if (pl == KSG_PL_TAINT_TOLERATION) {
-      a.norm[(o * a.n_rows + q) * NN + n] = nt;
+      cap_put(a.norm, (o * a.n_rows + q) * NN + n, nt, a.narrow);
     } else if (pl == KSG_PL_NODE_AFFINITY) {
-      a.norm[(o * a.n_rows + q) * NN + n] = na;
+      cap_put(a.norm, (o * a.n_rows + q) * NN + n, na, a.narrow);
     }
   }
 }

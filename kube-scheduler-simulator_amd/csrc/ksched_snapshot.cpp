@@ -29,6 +29,7 @@
 #include <set>
 #include <string>
 #include <tuple>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -1528,11 +1529,11 @@ bool status_of(const Encoded& e, int32_t pod, uint32_t word, int32_t node, int* 
       break;
     case KSG_PL_NODE_UNSCHEDULABLE:
       c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      m = "node(s) were unschedulable";
+      if (msg) m = "node(s) were unschedulable";
       break;
     case KSG_PL_NODE_NAME:
       c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      m = "node(s) didn't match the requested node name";
+      if (msg) m = "node(s) didn't match the requested node name";
       break;
     case KSG_PL_TAINT_TOLERATION: {
       if ((int)reason >= e.max_taints) {
@@ -1550,37 +1551,37 @@ bool status_of(const Encoded& e, int32_t pod, uint32_t word, int32_t node, int* 
     }
     case KSG_PL_NODE_AFFINITY:
       c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      m = "node(s) didn't match Pod's node affinity/selector";
+      if (msg) m = "node(s) didn't match Pod's node affinity/selector";
       break;
     case KSG_PL_NODE_PORTS:
       c = KSG_CODE_UNSCHEDULABLE;
-      m = "node(s) didn't have free ports for the requested pod ports";
+      if (msg) m = "node(s) didn't have free ports for the requested pod ports";
       break;
     case KSG_PL_NODE_RESOURCES_FIT: {
       // fitsRequest reason order: pods, cpu, memory, ephemeral, scalars;
       // Unresolvable when the request exceeds the allocatable outright.
       c = KSG_CODE_UNSCHEDULABLE;
       const ksg_pod& p = e.pods[pod];
-      std::vector<std::string> rs;
-      if (reason & 1u) rs.push_back("Too many pods");
+      if (msg && (reason & 1u)) m = "Too many pods";
       for (size_t r = 0; r < e.res_names.size(); r++)
         if (reason & (1u << (r + 1))) {
-          rs.push_back("Insufficient " + e.res_names[r]);
+          if (msg) m += (m.empty() ? "Insufficient " : ", Insufficient ") + e.res_names[r];
           if (p.req[r] > e.alloc[r * e.N + node]) c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
         }
-      for (size_t k = 0; k < rs.size(); k++) m += (k ? ", " : "") + rs[k];
       break;
     }
     case KSG_PL_POD_TOPOLOGY_SPREAD:
       c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
-      m = reason == 1 ? "node(s) didn't match pod topology spread constraints (missing required label)"
-                      : "node(s) didn't match pod topology spread constraints";
+      if (msg)
+        m = reason == 1 ? "node(s) didn't match pod topology spread constraints (missing required label)"
+                        : "node(s) didn't match pod topology spread constraints";
       break;
     case KSG_PL_INTER_POD_AFFINITY:
       c = reason == 1 ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE;
-      m = reason == 1   ? "node(s) didn't match pod affinity rules"
-          : reason == 2 ? "node(s) didn't match pod anti-affinity rules"
-                        : "node(s) didn't satisfy existing pods anti-affinity rules";
+      if (msg)
+        m = reason == 1   ? "node(s) didn't match pod affinity rules"
+            : reason == 2 ? "node(s) didn't match pod anti-affinity rules"
+                          : "node(s) didn't satisfy existing pods anti-affinity rules";
       break;
     default:
       *err = "unexpected word";
@@ -1845,7 +1846,8 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     return fail(s, KSG_E_INVALID, "statuses: index out of range");
   const Encoded& e = s->e;
   // distinct messages: keyed by the word, plus the taint id for TaintToleration
-  std::map<uint64_t, int32_t> seen;
+  std::unordered_map<uint64_t, int32_t> seen;
+  seen.reserve(64);
   std::vector<std::string> msgs;
   for (int32_t n = 0; n < n_nodes; n++) {
     const uint32_t w = words[n];

@@ -467,9 +467,13 @@ class Snapshot:
         u32p = C.POINTER(C.c_uint32)
         args = (self.h, pod, w.ctypes.data_as(u32p), n, code.ctypes.data_as(C.POINTER(i32)),
                 msg.ctypes.data_as(C.POINTER(i32)))
-        self._check(self._statuses(*args, None, 0, C.byref(nm), C.byref(ln)), "statuses")
-        buf = C.create_string_buffer(max(ln.value, 1))
-        self._check(self._statuses(*args, buf, ln.value, C.byref(nm), C.byref(ln)), "statuses")
+        buf = getattr(self, "_status_buf", None)
+        if buf is None:
+            buf = self._status_buf = C.create_string_buffer(1 << 16)
+        self._check(self._statuses(*args, buf, len(buf), C.byref(nm), C.byref(ln)), "statuses")
+        if ln.value > len(buf):   # one more call with a buffer that fits
+            buf = self._status_buf = C.create_string_buffer(ln.value)
+            self._check(self._statuses(*args, buf, len(buf), C.byref(nm), C.byref(ln)), "statuses")
         texts = buf.raw[:ln.value].split(b"\0")[:nm.value]
         return code, msg, [t.decode("utf-8") for t in texts]
 

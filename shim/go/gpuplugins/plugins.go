@@ -37,11 +37,23 @@ const stateKey framework.StateKey = "ksched/eval"
 
 const fsNotEvaluated = 0xFF // KSG_FS_NOT_EVALUATED
 
-// podState is the per-pod SoA result, computed once per scheduling cycle.
+// podState is the per-pod SoA result, computed once per scheduling cycle,
+// with every node's framework.Status and every plugin's PreFilter status
+// decoded up front, so the framework's 16 Filter / Score goroutines read it
+// without taking Evaluator.mu.
 type podState struct {
 	pod   int // snapshot pod index
 	ev    *ksched.PodEval
 	index map[string]int // node name -> column
+	codes []int32        // per node: framework.Code of the rejection (ksched.Code*)
+	msgID []int32        // per node: index into msgs, -1 = passed / not evaluated
+	msgs  []string
+	pre   [ksched.NPlugins]preFilterResult
+}
+
+type preFilterResult struct {
+	code  int
+	names []string // NodeAffinity's PreFilterResult, nil = none
 }
 
 func (s *podState) Clone() framework.StateData { return s }
@@ -221,10 +233,22 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 	for i, n := range e.nodes {
 		st.index[n] = i
 	}
+	// every rejected node's Status, once per pod (ksg_snapshot_statuses)
+	if st.codes, st.msgID, st.msgs, err = e.snap.Statuses(idx, ev.FStatus); err != nil {
+		return nil, err
+	}
+	for id := 0; id < ksched.NPlugins; id++ {
+		code, names, err := e.snap.PreFilter(idx, id, ev.Status)
+		if err != nil {
+			return nil, err
+		}
+		st.pre[id] = preFilterResult{code: code, names: names}
+	}
 	cs.Write(stateKey, st)
 	return st, nil
 }
 
+// status answers one Filter call from the pod's decoded statuses (no lock).
 func (e *Evaluator) status(st *podState, id int, node string) *framework.Status {
 	col, ok := st.index[node]
 	if !ok {
@@ -234,13 +258,23 @@ func (e *Evaluator) status(st *podState, id int, node string) *framework.Status 
 	if w == 0 || w == fsNotEvaluated || int(w&0xff)-1 != id {
 		return nil // passed this plugin (the framework stops at the first rejection, as the device does)
 	}
+	return framework.NewStatus(frameworkCode(int(st.codes[col])), st.msgs[st.msgID[col]])
+}
+
+// applyArgs records a factory's decoded args; a change after the snapshot
+// was built re-encodes it at the next cycle.
+func (e *Evaluator) applyArgs(name string, obj runtime.Object) error {
 	e.mu.Lock()
-	code, msg, err := e.snap.Status(st.pod, w, col)
-	e.mu.Unlock()
-	if err != nil {
-		return framework.AsStatus(err)
+	defer e.mu.Unlock()
+	if err := e.prof.ApplyPluginArgs(name, obj); err != nil {
+		return err
 	}
-	return framework.NewStatus(frameworkCode(code), msg)
+	if e.snap != nil {
+		e.snap.Free()
+		e.snap = nil
+		e.nodes = nil
+	}
+	return nil
 }
 
 func frameworkCode(c int) framework.Code {
@@ -298,12 +332,7 @@ func (b *base) preFilter(cs *framework.CycleState, pod *v1.Pod) (*framework.PreF
 	if s != nil {
 		return nil, s
 	}
-	b.ev.mu.Lock()
-	code, names, err := b.ev.snap.PreFilter(st.pod, b.id, st.ev.Status)
-	b.ev.mu.Unlock()
-	if err != nil {
-		return nil, framework.AsStatus(err)
-	}
+	code, names := st.pre[b.id].code, st.pre[b.id].names
 	switch code {
 	case ksched.CodeSkip:
 		return nil, framework.NewStatus(framework.Skip) // recorded as "" (store.go:522)
@@ -462,7 +491,14 @@ func Factories(ev *Evaluator) map[string]func(context.Context, runtime.Object, f
 	out := map[string]func(context.Context, runtime.Object, framework.Handle) (framework.Plugin, error){}
 	for _, t := range table {
 		t := t
-		out[t.name] = func(_ context.Context, _ runtime.Object, h framework.Handle) (framework.Plugin, error) {
+		out[t.name] = func(_ context.Context, obj runtime.Object, h framework.Handle) (framework.Plugin, error) {
+			// the plugin's args as the framework decoded them (NodeResourcesFitArgs,
+			// NodeResourcesBalancedAllocationArgs, InterPodAffinityArgs,
+			// PodTopologySpreadArgs, NodeAffinityArgs): into the profile the
+			// snapshot is encoded with
+			if err := ev.applyArgs(t.name, obj); err != nil {
+				return nil, err
+			}
 			return t.make(base{name: t.name, id: t.id, ev: ev, h: h}), nil
 		}
 	}

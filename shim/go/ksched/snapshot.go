@@ -289,17 +289,43 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 	return v
 }
 
+// Plugin is one configv1.Plugin (name, weight).
+type Plugin struct {
+	Name   string
+	Weight int32
+}
+
+// PluginSet is one extension point's configv1.PluginSet after
+// ConvertForSimulator (plugins.go:177-186): names may carry the Wrapped
+// suffix; "*" in Disabled disables every MultiPoint default for the point.
+type PluginSet struct {
+	Enabled  []Plugin
+	Disabled []string
+}
+
+// Extension points of ProfileArgs.Points (KSG_POINT_*).
+const (
+	PointPreFilter = int(C.KSG_POINT_PREFILTER)
+	PointFilter    = int(C.KSG_POINT_FILTER)
+	PointPreScore  = int(C.KSG_POINT_PRESCORE)
+	PointScore     = int(C.KSG_POINT_SCORE)
+	NPoints        = int(C.KSG_NPOINTS)
+)
+
 // ProfileArgs is profile 0 of the KubeSchedulerConfiguration as the
-// evaluator models it (plugins in MultiPoint order with weights, plugin args).
+// evaluator models it: MultiPoint plugins in order with weights, the
+// per-point sets, and the plugin args (filled by ApplyPluginArgs from the
+// decoded runtime.Object each plugin factory receives).
 type ProfileArgs struct {
-	Plugins                            []struct{ Name string; Weight int32 }
-	FitStrategy                        string            // LeastAllocated / MostAllocated
-	FitResources, BAResources          map[string]int64 // name -> weight (Go map: order is irrelevant)
-	FitResourceOrder, BAResourceOrder  []string          // the args' list order
+	Plugins                               []Plugin
+	Points                                [NPoints]PluginSet
+	FitStrategy                           string           // LeastAllocated / MostAllocated
+	FitResources, BAResources             map[string]int64 // name -> weight
+	FitResourceOrder, BAResourceOrder     []string         // the args' list order
 	FitIgnoredResources, FitIgnoredGroups []string
-	HardPodAffinityWeight              int32
-	IgnorePreferredTermsOfExistingPods bool
-	PTSSystemDefaulted                 bool
+	HardPodAffinityWeight                 int32
+	IgnorePreferredTermsOfExistingPods    bool
+	PTSSystemDefaulted                    bool
 }
 
 // Snapshot is one ksg_snapshot (not thread-safe; the caller serialises).
@@ -342,6 +368,15 @@ func NewSnapshot(p *ProfileArgs) (*Snapshot, error) {
 	}
 	if p.PTSSystemDefaulted {
 		pv.pts_system_defaulted = 1
+	}
+	for k := 0; k < NPoints; k++ {
+		ps := p.Points[k]
+		en := unsafe.Slice((*C.ksg_plugin_view)(a.alloc(len(ps.Enabled), C.sizeof_ksg_plugin_view)), len(ps.Enabled)+1)
+		for i, pl := range ps.Enabled {
+			en[i].name, en[i].weight = a.str(pl.Name), C.int32_t(pl.Weight)
+		}
+		pv.points[k].n_enabled, pv.points[k].enabled = C.int32_t(len(ps.Enabled)), &en[0]
+		pv.points[k].n_disabled, pv.points[k].disabled = a.strs(ps.Disabled)
 	}
 	x := &Snapshot{}
 	if rc := C.ksg_snapshot_new(&pv, &x.s); rc != 0 {
@@ -432,6 +467,69 @@ func (x *Snapshot) Status(pod int, word uint32, node int) (int, string, error) {
 		return int(code), C.GoString(big), nil
 	}
 	return int(code), C.GoString(buf), nil
+}
+
+// Statuses decodes every node's Filter status word of a pod at once
+// (ksg_snapshot_statuses): codes[n] (Code*), msg[n] = index into msgs, -1
+// for success / not evaluated.
+func (x *Snapshot) Statuses(pod int, words []uint32) (codes, msg []int32, msgs []string, err error) {
+	n := len(words)
+	cw := (*C.uint32_t)(C.malloc(C.size_t(4 * (n + 1))))
+	defer C.free(unsafe.Pointer(cw))
+	copy(unsafe.Slice((*uint32)(unsafe.Pointer(cw)), n), words)
+	cc := (*C.int32_t)(C.malloc(C.size_t(4 * (n + 1))))
+	defer C.free(unsafe.Pointer(cc))
+	cm := (*C.int32_t)(C.malloc(C.size_t(4 * (n + 1))))
+	defer C.free(unsafe.Pointer(cm))
+	var nm C.int32_t
+	var ln C.int64_t
+	if err = x.check(C.ksg_snapshot_statuses(x.s, C.int32_t(pod), cw, C.int32_t(n), cc, cm, nil, 0, &nm, &ln)); err != nil {
+		return
+	}
+	buf := (*C.char)(C.malloc(C.size_t(ln) + 1))
+	defer C.free(unsafe.Pointer(buf))
+	if err = x.check(C.ksg_snapshot_statuses(x.s, C.int32_t(pod), cw, C.int32_t(n), cc, cm, buf, ln+1, &nm, &ln)); err != nil {
+		return
+	}
+	codes = append([]int32(nil), unsafe.Slice((*int32)(unsafe.Pointer(cc)), n)...)
+	msg = append([]int32(nil), unsafe.Slice((*int32)(unsafe.Pointer(cm)), n)...)
+	raw := C.GoBytes(unsafe.Pointer(buf), C.int(ln))
+	start := 0
+	for i := 0; i < len(raw) && len(msgs) < int(nm); i++ {
+		if raw[i] == 0 {
+			msgs = append(msgs, string(raw[start:i]))
+			start = i + 1
+		}
+	}
+	return
+}
+
+// ProfileInfo is the profile as the framework and the Store see it
+// (ksg_snapshot_profile_info): per-point run orders and the two weight maps.
+type ProfileInfo struct {
+	Order           [NPoints][]int
+	StoreWeight     [NPlugins]int64 // getScorePluginWeight (plugins.go:289-304), 0 = absent
+	SelectionWeight [NPlugins]int32
+	NormalizeMask   uint32
+}
+
+// ProfileInfo returns the derived orders and weights.
+func (x *Snapshot) ProfileInfo() (*ProfileInfo, error) {
+	var ci C.ksg_profile_info
+	if err := x.check(C.ksg_snapshot_profile_info(x.s, &ci)); err != nil {
+		return nil, err
+	}
+	out := &ProfileInfo{NormalizeMask: uint32(ci.normalize_mask)}
+	for k := 0; k < NPoints; k++ {
+		for i := 0; i < int(ci.n_order[k]); i++ {
+			out.Order[k] = append(out.Order[k], int(ci.order[k][i]))
+		}
+	}
+	for i := 0; i < NPlugins; i++ {
+		out.StoreWeight[i] = int64(ci.store_weight[i])
+		out.SelectionWeight[i] = int32(ci.selection_weight[i])
+	}
+	return out, nil
 }
 
 // PreFilter is plugin's PreFilter code for the pod and, for NodeAffinity,

@@ -136,3 +136,30 @@ def test_eval_without_capture_and_eval_pod(gpu, oracle):
         if rg.selected >= 0:
             gpu.commit(i, rg.selected)
             oracle.commit(i, ro.selected)
+
+
+def test_cycles_from_an_empty_snapshot(built):
+    """The Go shim's life cycle from an empty pod set (bench.py per_cycle):
+    nodes only at load, then add_pod -> sync -> eval -> statuses -> assume per
+    pod; placements equal one device queue over the same pods."""
+    S = pkg("snapshot")
+    nodes, pods, prof = G.config2(n_nodes=400, n_pods=150, seed=6)
+    snap = S.Snapshot(prof, nodes)
+    eng = native.Engine(device=0)
+    snap.load(eng)
+    cap = native.CaptureBuffers(len(nodes), 1)
+    placed = []
+    for p in pods:
+        idx = snap.add_pod(p)
+        snap.sync(eng)
+        r = eng.eval(idx, cap)
+        codes, msg, texts = snap.statuses(idx, cap.fstatus[0])
+        assert ((codes != 0) == (msg >= 0)).all()
+        if r.selected >= 0:
+            snap.assume(eng, idx, r.selected)
+        placed.append(r.selected)
+    enc = E.Encoder(nodes, pods, prof)
+    q = native.Engine(device=0)
+    q.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    want, _ = q.run_queue(0, len(pods), results=False)
+    np.testing.assert_array_equal(np.array(placed, np.int32), want)
