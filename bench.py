@@ -10,11 +10,15 @@ score, normalise, select, assume for every pod, in queue order) with every
 input already resident in HBM.
 
 Multi-GPU: the per-pod decision does not shard (every binding changes the
-state the next pod reads), so N GPUs run N independent what-if replicas of the
-same queue (weak scaling, no data-path collective); value = pods scheduled by
-all ranks / max-over-ranks time.  The process group is RCCL ("nccl") at every
-N, N = 1 included (a one-rank group on 127.0.0.1), so the collectives run on
-the box.
+state the next pod reads), so N GPUs run N DISTINCT what-if replicas of the
+queue (north star (3)): rank 0 the configs[1] profile, rank
+r >= 1 what-if profile r of generator.replica_profiles (per-plugin weights in
+[1, 5], LeastAllocated or MostAllocated), each over the full 50,000-pod queue
+on its own copy of the cluster (weak scaling: per-GPU work fixed; no data-path
+collective).  value = pods scheduled by all ranks / max-over-ranks time; one
+RCCL all_gather of every replica's placements per step.  The process group is
+RCCL ("nccl") at every N, N = 1 included (a one-rank group on 127.0.0.1), so
+the collective runs on the box.
 
 Prints ONE JSON line (rank 0).  The line also carries:
 * `replica_sweep`: BASELINE configs[3], 1,024 what-if replicas (weights and
@@ -299,13 +303,17 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
             "eval_path": eng.last_run_info()[0]}
 
 
-def default_profile_line(native, G, E, n_nodes: int, n_pods: int, steps: int):
-    """The in-tree default profile at n_nodes (generator.config1): pods/s of
-    reset + one ksg_run_queue over n_pods, best of `steps`."""
+def default_profile_line(native, G, E, metrics, n_nodes: int, n_pods: int, steps: int, cpu_budget: float):
+    """The in-tree default profile (generator.config1: every Filter / Score
+    plugin, pods without topology terms) at n_nodes: pods/s of reset + one
+    ksg_run_queue over n_pods (best of `steps`), the dominant kernel's
+    roofline (per-kernel HIP events, priced like the headline), and the C++
+    oracle on a bounded prefix of the same queue (16 threads)."""
     nodes, pods, prof = G.config1(n_nodes=n_nodes, n_pods=n_pods)
     enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
     eng = native.Engine(device=0)
-    eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    eng.load(enc, pf)
     best, kms = None, None
     for _ in range(steps + 1):
         eng.reset_state()
@@ -317,10 +325,16 @@ def default_profile_line(native, G, E, n_nodes: int, n_pods: int, steps: int):
     eng.set_timing(True)
     eng.reset_state()
     eng.run_queue(0, n_pods, results=False)
-    names = sorted({k["name"] for k in eng.kernel_stats()})
-    return {"workload": f"default profile (every in-tree Filter/Score plugin), generator.config1: {n_nodes} nodes x "
-                        f"{n_pods} pods", "pods_per_s": n_pods / best, "device_pods_per_s": n_pods / (kms * 1e-3),
-            "scheduled": int((pl >= 0).sum()), "kernels": names}
+    ks = eng.kernel_stats()
+    eng.set_timing(False)
+    bpe = sum(metrics.bytes_per_node_eval(enc, prof).values())
+    roof = metrics.price_decided_node_evals(metrics.dominant_kernel_roofline(ks, bpe), bpe, n_pods * n_nodes)
+    out = {"workload": f"default profile (every in-tree Filter/Score plugin), generator.config1: {n_nodes} nodes x "
+                       f"{n_pods} pods", "pods_per_s": n_pods / best, "device_pods_per_s": n_pods / (kms * 1e-3),
+           "scheduled": int((pl >= 0).sum()), "roofline": roof, "bytes_per_node_eval": bpe}
+    if cpu_budget > 0:
+        out["cpu_baseline"] = cpu_baseline(enc, pf, 16, cpu_budget)
+    return out
 
 
 def main():
@@ -336,7 +350,7 @@ def main():
     ap.add_argument("--sweep-pods", type=int, default=1000)
     ap.add_argument("--annotate-pods", type=int, default=2000, help="annotation sidecar; 0 disables")
     ap.add_argument("--annotate-threads", type=int, default=16)
-    ap.add_argument("--default-pods", type=int, default=20000, help="default-profile line; 0 disables")
+    ap.add_argument("--default-pods", type=int, default=50000, help="default-profile line; 0 disables")
     ap.add_argument("--cycle-pods", type=int, default=2000, help="per-cycle sidecar; 0 disables")
     ap.add_argument("--cycle-warm", type=int, default=500)
     args = ap.parse_args()
@@ -378,9 +392,13 @@ def main():
     nodes, pods, prof = G.config2(n_nodes=args.nodes, n_pods=args.pods)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
+    # this rank's what-if replica: rank 0 the configs[1] profile, rank r >= 1
+    # replica profile r (distinct weights / strategy: no duplicated work)
+    prof_r = prof if rank == 0 else G.replica_profiles(world)[rank]
+    pf_r = pf if rank == 0 else E.encode_profile(prof_r, enc.cluster.res_names)
     log(f"[rank {rank}] encoded {len(nodes)} nodes x {len(pods)} pods in {time.perf_counter() - t:.1f}s")
     eng = native.Engine(device=local_rank)
-    eng.load(enc, pf)   # inputs resident in HBM from here on
+    eng.load(enc, pf_r)   # inputs resident in HBM from here on
     P = len(pods)
 
     gather_out = [torch.empty(P, dtype=torch.int32, device=dev) for _ in range(world)]
@@ -410,6 +428,11 @@ def main():
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
     scheduled = int((pl >= 0).sum())
+    # every replica's placements, gathered by RCCL in the last step: distinct
+    # what-ifs at N > 1 (rank 0's is the configs[1] placement)
+    import hashlib
+    replica_digest = hashlib.sha256(b"".join(g.cpu().numpy().tobytes() for g in gather_out)).hexdigest()
+    distinct = len({hashlib.sha256(g.cpu().numpy().tobytes()).hexdigest() for g in gather_out})
     # one extra, untimed step with per-kernel HIP-event timing (ksg_set_timing)
     kstats = []
     try:
@@ -445,7 +468,8 @@ def main():
             log(f"[rank {rank}] per-cycle sidecar unavailable: {e}")
     if world == 1 and args.default_pods > 0:
         try:
-            dflt = default_profile_line(native, G, E, args.nodes, args.default_pods, 2)
+            dflt = default_profile_line(native, G, E, metrics, args.nodes, args.default_pods, 2,
+                                        0.0 if args.no_cpu_baseline else 8.0)
         except Exception as e:
             log(f"[rank {rank}] default-profile line unavailable: {e}")
 
@@ -463,20 +487,8 @@ def main():
             roof = None
         if roof is None:   # no per-kernel timing: whole step as one launch
             roof = metrics.roofline(bpe, P * len(nodes), kms)
-        # Phase-2 kernels decide a batch of pods over every node: price a launch
-        # by SURVEY §8(d)'s bytes per node-eval x the node-evals it decides
-        # (batch pods x nodes), as the round-1 verdict recomputed it; the
-        # changed-slot figure the kernel stats count stays beside it.
-        if roof.get("kernel") in ("ksg_batch_phase2s", "ksg_batch_phase2t", "ksg_batch_phase2p", "ksg_batch_phase2"):
-            row = next((k for k in roof.get("kernels", []) if k["name"] == roof["kernel"]), None)
-            if row and row["calls"] and row["avg_ms"] > 0:
-                per_launch = bpe * P * len(nodes) / row["calls"]
-                roof["achieved_changed_slot_bytes"] = roof["achieved"]
-                roof["achieved"] = per_launch / (row["avg_ms"] * 1e-3) / 1e9
-                roof["frac"] = roof["achieved"] / roof["peak"]
-                roof["bytes_per_launch"] = per_launch
-                roof["unit_basis"] = ("SURVEY 8(d) bytes per node-eval x node-evals decided per launch "
-                                      "(batch pods x nodes)")
+        # Phase-2 kernels decide a batch of pods over every node (metrics.price_decided_node_evals)
+        roof = metrics.price_decided_node_evals(roof, bpe, P * len(nodes))
         roof["step"] = metrics.roofline(bpe, P * len(nodes), kms)
         roof["step"]["kernel_ms"] = kms
         # HBM bytes per launch of the dominant kernel from the committed PMC
@@ -491,9 +503,12 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int64", "data": "synthetic",
             "config": {"workload": f"configs[1]: {len(nodes)} nodes x {P} pods, NodeResourcesFit(LeastAllocated)"
-                                   f"+BalancedAllocation+TaintToleration+NodeAffinity, generator.config2 seed 2",
+                                   f"+BalancedAllocation+TaintToleration+NodeAffinity, generator.config2 seed 2"
+                                   + (f"; ranks 1..{world - 1}: distinct what-if profiles (replica_profiles)"
+                                      if world > 1 else ""),
                        "nodes": len(nodes), "pods": P, "parallelism": f"replicas{world}",
-                       "pods_scheduled_per_step": scheduled},
+                       "pods_scheduled_per_step": scheduled, "distinct_replica_placements": distinct,
+                       "replica_placements_sha256": replica_digest},
             "node_evals_per_sec": node_evals,
             "roofline": roof,
         }

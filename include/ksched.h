@@ -73,6 +73,8 @@ enum {
 #define KSG_EFFECT_NO_EXECUTE 3
 
 /* ---- per-node filter status word --------------------------------------
+ * (NodePorts: no payload; "node(s) didn't have free ports for the requested
+ * pod ports", Unschedulable)
  * bits 0..7  : 0 = passed every filter that ran; else failing plugin id + 1
  * bits 8..31 : reason payload
  *   NodeResourcesFit : bit0 "Too many pods", bit1 cpu, bit2 memory, bit3
@@ -106,6 +108,9 @@ typedef struct ksg_nodes {
   int32_t max_images;
   const uint32_t* images;        /* [max_images][n_nodes] ascending image id + 1, 0 = end */
   int32_t n_images;              /* image vocabulary size                          */
+  int32_t n_port_vocab;          /* host-port vocabulary size (NodePorts): every (hostIP,
+                                    protocol, hostPort) a pod uses; each node's UsedPorts is
+                                    a bitmap over it, empty at load (bound pods are assumed) */
 } ksg_nodes;
 
 /* ---- topology tables for PodTopologySpread / InterPodAffinity ----------- */
@@ -149,9 +154,9 @@ typedef struct ksg_pod {
   int32_t pts;               /* PodTopologySpread program                      */
   int32_t ipa;               /* InterPodAffinity program                       */
   int32_t commit;            /* selectors matched + templates owned (assume)   */
-  int32_t blob;              /* tol..commit programs are contiguous:           */
+  int32_t blob;              /* tol..ports programs are contiguous:            */
   int32_t blob_len;          /*   prog[blob, blob + blob_len) (staged into LDS) */
-  int32_t pad;
+  int32_t ports;             /* NodePorts program: conflicting host-port ids, own ids */
 } ksg_pod;
 
 typedef struct ksg_workload {
@@ -302,6 +307,7 @@ int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
 #define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
 #define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */
 #define KSG_RUN_TCOL 4           /* phase 2 was the transposed walk (ksg_batch_phase2t) */
+#define KSG_RUN_WAVE 8           /* phase 2 was the one-wave slot walk (ksg_batch_phase2w) */
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event
@@ -330,7 +336,9 @@ enum {
   KSG_K_BATCH_PHASE2T = 14,
   KSG_K_BATCH_TRANSPOSE = 15,
   KSG_K_TCOL_CARRY = 16,
-  KSG_NKERNELS = 17
+  KSG_K_EVAL_FUSED = 17,
+  KSG_K_BATCH_PHASE2W = 18,
+  KSG_NKERNELS = 19
 };
 typedef struct ksg_kernel_stat {
   char name[48];

@@ -114,12 +114,24 @@ typedef struct ksg_spread_view {
   const char* const* match_label_keys;
 } ksg_spread_view;
 
+/* One containers[].ports[] entry with a hostPort (v1.ContainerPort): the
+ * NodePorts plugin's input (schedutil.GetHostPorts).  host_ip / protocol may
+ * be "" or NULL (sanitised to 0.0.0.0 / TCP as HostPortInfo does); entries
+ * with host_port <= 0 are ignored. */
+typedef struct ksg_host_port_view {
+  const char* host_ip;
+  const char* protocol;
+  int32_t host_port;
+  int32_t pad;
+} ksg_host_port_view;
+
 typedef struct ksg_container_view {
   const char* image;
   int32_t n_requests;
   const ksg_quantity* requests;
   int32_t restartable;      /* init container with restartPolicy Always (sidecar) */
-  int32_t n_host_ports;     /* > 0: NodePorts with ports (refused: KSG_E_UNSUPPORTED) */
+  int32_t n_host_ports;
+  const ksg_host_port_view* host_ports;
 } ksg_container_view;
 
 typedef struct ksg_image_view {

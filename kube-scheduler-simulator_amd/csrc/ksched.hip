@@ -93,6 +93,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
   int32_t* tmpl_total = a.st.tmpl_total + rep * a.st.stride_tt;
   int64_t* partial = a.st.partial + rep * a.st.stride_part;
   int64_t* sraw = a.st.sraw + rep * a.st.stride_sraw;
+  uint32_t* ports = a.st.ports ? a.st.ports + rep * a.st.stride_ports : nullptr;
   const bool cap = a.cap_fstatus != nullptr && rep == 0;
 
   if (tid < (int)(sizeof(ksg_profile) / 4))
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
     __syncthreads();
     const ksg_pod& p = s_pod;
     const ksg_profile& prof = s_prof;
-    const PodView v = make_view(c, prof, p, s_blob, a.prog);
+    const PodView v = make_view(c, prof, p, s_blob, a.prog, false, ports);
     uint32_t* cfs = cap ? a.cap_fstatus + (size_t)k * N : nullptr;
     int64_t* craw = cap ? a.cap_raw + (size_t)k * KSG_NPLUGINS * N : nullptr;
     int64_t* cnorm = cap ? a.cap_norm + (size_t)k * KSG_NPLUGINS * N : nullptr;
@@ -190,7 +191,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
     if (tid == 0) {
       if (a.do_commit && selected >= 0)
         commit_node(c, requested, nonzero, pod_count, cnt, tab, tmpl_total, p,
-                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected);
+                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected, 1, ports,
+                    v.ports >= 0 ? s_blob + v.ports : nullptr);
       a.placements[(size_t)rep * a.count + k] = selected;
       if (a.results) {
         ksg_result res;
@@ -247,7 +249,7 @@ struct BatchArgs {
   uint64_t* top;            // [KSG_BATCH_MAX][KSG_BATCH_MAX] top-set argmax keys
   int32_t* placements;
   ksg_result* results;      // or null
-  // pipelined phase 2 (ksched_phase2p.h): the two-batch window
+  // pipelined phase 2 (run_pipe): the two-batch window
   int32_t k_extra;          // top sets hold min(j + 1 + k_extra, nfeas) keys
   const int32_t* carry;     // nodes the previous batch changed (slot order), or null
   const int32_t* carry_n;   // their count (device), or null
@@ -1792,10 +1794,11 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 #endif
 }
 
-#include "ksched_phase2p.h"
+#include "ksched_phase2w.h"
 #include "ksched_phase2t.h"
 #include "ksched_capture.h"
 #include "ksched_sweep.h"
+#include "ksched_eval.h"
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
 template <int BLOCK>
@@ -1825,6 +1828,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
   int32_t* tab = a.st.tab + rep * a.st.stride_tab;
   int32_t* tmpl_total = a.st.tmpl_total + rep * a.st.stride_tt;
   int64_t* partial = a.st.partial + rep * a.st.stride_part;
+  uint32_t* ports = a.st.ports ? a.st.ports + rep * a.st.stride_ports : nullptr;
   int64_t* sraw = a.st.sraw + rep * a.st.stride_sraw;
   const bool cap = a.cap_fstatus != nullptr && rep == 0;
 
@@ -1864,7 +1868,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
     __syncthreads();
     const bool ok = s_t.ok;
     for (int i = tid; i < s_t.words; i += BLOCK) s_hist[i] = 0;
-    PodView v = make_view(c, prof, p, s_blob, a.prog, true);
+    PodView v = make_view(c, prof, p, s_blob, a.prog, true, ports);
     if (s_t.ipa_skip_filter) v.fskip |= bit(KSG_PL_INTER_POD_AFFINITY);
     const TopoProg& g = s_g;
     const TopoCtx tc{&s_g, &s_t, s_hist, cnt, tab};
@@ -2176,7 +2180,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
     if (tid == 0) {
       if (a.do_commit && selected >= 0)
         commit_node(c, requested, nonzero, pod_count, cnt, tab, tmpl_total, p,
-                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected);
+                    v.commit >= 0 ? s_blob + v.commit : nullptr, selected, 1, ports,
+                    v.ports >= 0 ? s_blob + v.ports : nullptr);
       a.placements[(size_t)rep * a.count + k] = selected;
       if (a.results) {
         ksg_result res;
@@ -2227,7 +2232,8 @@ __global__ void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const ksg_pod& p = pods[pod];
   commit_node(c, st.requested, st.nonzero, st.pod_count, st.cnt, st.tab, st.tmpl_total, p,
-              p.commit >= 0 ? prog + p.commit : nullptr, node, sign);
+              p.commit >= 0 ? prog + p.commit : nullptr, node, sign, st.ports,
+              p.ports >= 0 ? prog + p.ports : nullptr);
 }
 
 // DefaultPreemption dry run (SelectVictimsOnNode), one lane per candidate
@@ -2382,6 +2388,8 @@ struct ksg_ctx {
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
+  bool wave_walk = true;      // env KSG_WAVE_WALK=0: the slot walk with one lane per slot (2 waves at 64-pod batches)
+  bool last_wave = false;     // the last batched run's phase 2 was the one-wave walk
   uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
   int32_t* d_statt = nullptr;
   uint64_t* d_prect[2] = {nullptr, nullptr};   // the same, per window parity
@@ -2389,11 +2397,10 @@ struct ksg_ctx {
   uint32_t* d_tccol = nullptr;                 // carried columns [64][64]
   uint64_t* d_tcinit = nullptr;                // TcInit [64] (4 words each)
   unsigned* d_flag = nullptr; // range-check flag (ksg_range32)
-  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 3 "pipe", 4 "window", 5 "tcol" (the transposed
+  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 4 "window", 5 "tcol" (the transposed
   // walk where the N32 check and tcol_candidate pass, else the slot walk)
   // (default: the slot walk with the next batch's phase 1 + top-k overlapped
-  // through the two-batch window; the pipelined two-version walk is exact but
-  // measured slower: profiles/r2/phase2_modes.log)
+  // through the two-batch window)
   int batch_mode = 4;
   int slot_block = 64;   // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (64: the window walk at 64-pod batches, 2 waves, 416 k vs 408 k pods/s at 128, profiles/r2/phase2_window_blocks.log)
   // per-kernel timing (ksg_set_timing): one event before the first and after
@@ -2417,6 +2424,9 @@ struct ksg_ctx {
   ksg_profile* d_ev_prof = nullptr;
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
+  bool ev_fused = true;                     // env KSG_EVAL_FUSED=0: two launches instead of the cooperative one
+  int ev_fused_max = 0;                     // co-resident workgroups of ksg_eval_fused (occupancy x CUs)
+  unsigned ev_bar = 0;                      // the per-cycle grid barrier's arrival count so far
   // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
   char* h_stage = nullptr;
   size_t h_stage_bytes = 0;
@@ -2514,7 +2524,8 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
                                           "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
                                           "ksg_capture_eval", "ksg_capture_norm", "ksg_batch_phase2t",
-                                          "ksg_batch_transpose", "ksg_tcol_carry"};
+                                          "ksg_batch_transpose", "ksg_tcol_carry", "ksg_eval_fused",
+                                          "ksg_batch_phase2w"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2670,9 +2681,19 @@ int check_supported(ksg_ctx* ctx, const ksg_profile& prof, int first, int count)
 
 // The batched path covers node-local plugins only and packs raw scores into
 // 8-byte records; use it only when the values provably fit.
+// Any pod of [first, first + count) with host ports (NodePorts reads and its
+// assume writes the node's UsedPorts: the queue kernels and the per-cycle
+// path model that; the batched, sweep and chip-wide topology paths do not).
+bool range_has_ports(const ksg_ctx* ctx, int first, int count) {
+  for (int i = first; i < first + count; i++)
+    if (ctx->h_pods[i].ports >= 0) return true;
+  return false;
+}
+
 bool batch_eligible(ksg_ctx* ctx, int first, int count) {
   const ksg_profile& prof = ctx->prof;
   if (needs_topo(ctx, prof, first, count)) return false;
+  if (range_has_ports(ctx, first, count)) return false;
   if (ctx->c.T > 255) return false;
   if (ctx->c.N > (1 << 19)) return false;   // changed-node bitmap must fit LDS
   int64_t wsum = 0;
@@ -2781,6 +2802,14 @@ int decide_n32(ksg_ctx* ctx, int32_t first, int32_t count, bool* n32) {
 }
 
 // LDS budget attribute of the phase-2 instances (once per process)
+// ksg_batch_phase2w instances (the one-wave walk, <= 128 slots): RM 4, RM 4 N32, KSG_MAX_RES
+static const std::array<const void*, 3>& wave_kernels() {
+  static const std::array<const void*, 3> k = {(const void*)ksg_batch_phase2w<4, false>,
+                                               (const void*)ksg_batch_phase2w<4, true>,
+                                               (const void*)ksg_batch_phase2w<KSG_MAX_RES, false>};
+  return k;
+}
+
 int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
   static bool attr_set = false;
   if (attr_set) return KSG_OK;
@@ -2788,6 +2817,8 @@ int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
   HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)budget));
   for (const void* f : slot_kernels())
+    HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
+  for (const void* f : wave_kernels())
     HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
   attr_set = true;
   return KSG_OK;
@@ -2874,6 +2905,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     }
   }
   ctx->last_tcol = tcol;
+  ctx->last_wave = false;
   if (tcol && !ctx->d_rect) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rect, (size_t)128 * N))) return rc;
@@ -2959,15 +2991,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   return KSG_OK;
 }
 
-// ksg_batch_phase2p instances: (RM 4 | KSG_MAX_RES) x (SLOTS 128 | 256)
-static const std::array<const void*, 4>& pipe_kernels() {
-  static const std::array<const void*, 4> k = {
-      (const void*)ksg_batch_phase2p<4, 128>, (const void*)ksg_batch_phase2p<4, 256>,
-      (const void*)ksg_batch_phase2p<KSG_MAX_RES, 128>, (const void*)ksg_batch_phase2p<KSG_MAX_RES, 256>};
-  return k;
-}
-
-// Pipelined batched path (ksched_phase2p.h).  Batch b's phase 1 + top-k run on
+// Pipelined batched path (the two-batch window).  Batch b's phase 1 + top-k run on
 // a second stream while batch b - 1's phase 2 runs: phase 1 of batch b reads
 // the state at least as of the end of batch b - 2 (it waits for that phase 2),
 // and phase 2 of batch b carries batch b - 1's changed nodes as changed slots
@@ -3002,14 +3026,15 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const bool window = ctx->pipe_window != 0;
   const bool overlap = window && !ctx->timing;
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
-  // mode 4: the slot walk (one lane per slot) inside this pipeline; mode 3:
-  // the pipelined two-version walk (ksched_phase2p.h); mode 5: the transposed
-  // walk (ksched_phase2t.h) with the previous batch's nodes as carried columns,
-  // 64-pod batches, else the slot walk
+  // mode 4: the slot walk inside this pipeline (one wave, two slots per lane,
+  // ksched_phase2w.h, when the slots fit; else one lane per slot); mode 5:
+  // the transposed walk (ksched_phase2t.h) with the previous batch's nodes as
+  // carried columns, 64-pod batches, else the slot walk.  (The round-2
+  // two-version walk, measured slower, was removed in round 3.)
   bool n32 = false;
   if ((ctx->batch_mode == 4 || ctx->batch_mode == 5) && (rc = decide_n32(ctx, first, count, &n32))) return rc;
   const bool tcolw = ctx->batch_mode == 5 && window && n32 && tcol_candidate(ctx);
-  const bool slotwalk = ctx->batch_mode == 4 || (ctx->batch_mode == 5 && !tcolw);
+  const bool slotwalk = !tcolw;
   ctx->last_tcol = tcolw;
   if (tcolw) {
     if (!ctx->d_prect[0]) {
@@ -3030,22 +3055,15 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const int B = tcolw ? 64 : window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
   const int slots = window ? 2 * B : B;   // carried + this batch's slots
   const int sblock = slots <= 64 ? 64 : slots <= 128 ? 128 : 256;
-  const void* kern = slotwalk ? slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)]
-                              : pipe_kernels()[(slot_rm == 4 ? 0 : 2) + (slots <= 128 ? 0 : 1)];
-  const int block = slotwalk ? sblock : 2 * (slots <= 128 ? 128 : 256);
-  const size_t kLdsBudget = tcolw ? kTcolLds : slotwalk ? 120 * 1024 : 96 * 1024;
+  // the one-wave walk (ksched_phase2w.h) whenever the slots fit two per lane
+  const bool wave1 = slotwalk && ctx->wave_walk && slots <= 128;
+  ctx->last_wave = wave1;
+  const void* kern = wave1 ? wave_kernels()[n32 ? 1 : slot_rm == 4 ? 0 : 2]
+                          : slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)];
+  const int block = wave1 ? 64 : sblock;
+  const size_t kLdsBudget = tcolw ? kTcolLds : 120 * 1024;
   const size_t slot_bytes = 8 * (size_t)(2 * slot_rm + 10);   // SlotLayout<RM>::STRIDE int64 words
-  if (tcolw) {
-  } else if (slotwalk) {
-    if ((rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
-  } else {
-    static bool attr_set = false;
-    if (!attr_set) {
-      for (const void* f : pipe_kernels())
-        HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
-      attr_set = true;
-    }
-  }
+  if (!tcolw && (rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
   BatchArgs b{};
   b.c = ctx->c;
   b.st = ctx->st;
@@ -3085,11 +3103,9 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       if (tcolw)   // slot rows + the [slot][64] column store for this batch's and the carried slots
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
                 (size_t)(nb + prev_nb) * (slot_bytes + 64 * 4);
-      else if (slotwalk)
+      else
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
                 (size_t)sblock * slot_bytes;
-      else
-        bytes = 4 * ((2 * cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3);
       if (bytes <= kLdsBudget || nb == 1) break;
       nb = std::max(1, nb / 2);
     }
@@ -3138,7 +3154,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2T, 0.5 * nb * (nb + 1)))) return rc;
     } else {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(kern)), dim3(1), dim3(block), bytes, s2, b);
-      if ((rc = tlaunched(ctx, slotwalk ? KSG_K_BATCH_PHASE2S : KSG_K_BATCH_PHASE2P, 0.5 * nb * (nb + 1)))) return rc;
+      if ((rc = tlaunched(ctx, wave1 ? KSG_K_BATCH_PHASE2W : KSG_K_BATCH_PHASE2S, 0.5 * nb * (nb + 1)))) return rc;
     }
     if (overlap) HIPC(ctx, hipEventRecord(ctx->ev_p2[par], s2));
     prev_nb = nb;
@@ -3154,6 +3170,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
 // every replica profile is node-local and the values provably fit.
 bool sweep_eligible(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first, int count) {
   if (ctx->c.T > 255) return false;
+  if (range_has_ports(ctx, first, count)) return false;
   for (int r = 0; r < R; r++) {
     const ksg_profile& prof = profiles[r];
     if (needs_topo(ctx, prof, first, count)) return false;
@@ -3570,7 +3587,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   }
   if (batched) {
     ctx->last_path = 2;
-    if ((ctx->batch_mode == 3 || ctx->batch_mode == 4 || (ctx->batch_mode == 5 && ctx->pipe_window)) && !want_cap) {
+    if ((ctx->batch_mode == 4 || (ctx->batch_mode == 5 && ctx->pipe_window)) && !want_cap) {
       if ((rc = run_pipe(ctx, first, count, d_pl, d_res, d_prof))) return rc;
     } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, want_cap ? &ca : nullptr, d_prof))) {
       return rc;
@@ -3587,7 +3604,8 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     const bool topo = needs_topo(ctx, ctx->prof, first, count);
     // the chip-wide path always assumes its pods: ksg_eval (do_commit = 0)
     // takes the single-workgroup kernel
-    if (topo && !want_cap && do_commit && ctx->topo_coop && ctx->force_path != 1) {
+    if (topo && !want_cap && do_commit && ctx->topo_coop && ctx->force_path != 1 &&
+        !range_has_ports(ctx, first, count)) {
       ctx->last_path = 4;
       if ((rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof))) return rc;
     } else if ((rc = launch_queue(ctx, a, 1, block, topo))) {
@@ -3670,8 +3688,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   const size_t es = narrow ? 4 : 8;
   const bool want_fs = cap && cap->fstatus, want_raw = cap && cap->raw, want_norm = cap && cap->norm,
              want_tot = cap && cap->total;
-  // block: slot[2] | -1 | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_rows][N] | rec[N] (u64)
-  const size_t o_neg = 2 * sizeof(EvSlot), o_fs = o_neg + 8, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
+  // block: slot[2] | bar, timeout | -1 | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_rows][N] | rec[N] (u64)
+  const size_t o_bar = 2 * sizeof(EvSlot), o_neg = o_bar + 8, o_fs = o_neg + 8,
+               o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
   const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
   const size_t o_rec = o_norm + ((es * N * n_rows + 7) & ~(size_t)7);
   const size_t need = o_rec + 8 * N;
@@ -3700,11 +3719,12 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
     HIPC(ctx, hipHostMalloc((void**)&ctx->h_ev, o_rec, hipHostMallocDefault));
     ctx->h_ev_bytes = o_rec;
   }
-  if (!ctx->ev_clean) {
+  if (!ctx->ev_clean) {   // both slots, the barrier counter and the timeout word
     static const int32_t init[2] = {-1, 0};
     HIPC(ctx, hipMemsetAsync(ctx->d_ev, 0, o_neg, ctx->stream));
     HIPC(ctx, hipMemcpyAsync(ctx->d_ev + o_neg, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
     ctx->ev_parity = 0;
+    ctx->ev_bar = 0;
     ctx->ev_clean = true;
   }
   if (ctx->ev_prof_dirty) {
@@ -3735,10 +3755,26 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   ca.best = &slot->best;
   ca.err = &slot->err;
   ca.next = reinterpret_cast<int32_t*>(reinterpret_cast<EvSlot*>(ctx->d_ev) + (1 - par));
-  const dim3 grid((unsigned)((N + 255) / 256), 1);
-  ctx->ev_clean = false;   // until the second launch is in: it zeroes the other slot
-  hipLaunchKernelGGL(ksg_capture_eval, grid, dim3(256), 0, ctx->stream, ca);
-  hipLaunchKernelGGL(ksg_capture_norm, grid, dim3(256), 0, ctx->stream, ca);
+  const unsigned G = (unsigned)((N + 255) / 256);
+  ctx->ev_clean = false;   // until the launch is in: it zeroes the other slot
+  treset(ctx);
+  if ((rc = tmark(ctx))) return rc;
+  if (ctx->ev_fused && G <= (unsigned)ctx->ev_fused_max) {
+    // one cooperative launch: the eval half, a grid barrier, the norm half
+    unsigned* bar = reinterpret_cast<unsigned*>(ctx->d_ev + o_bar);
+    unsigned* tmo = bar + 1;
+    unsigned target = ctx->ev_bar + G;
+    void* args[] = {&ca, &bar, &tmo, &target};
+    HIPC(ctx, hipLaunchCooperativeKernel((const void*)ksg_eval_fused, dim3(G), dim3(256), args, 0, ctx->stream));
+    ctx->ev_bar = target;
+    if ((rc = tlaunched(ctx, KSG_K_EVAL_FUSED, (double)N))) return rc;
+  } else {
+    ca.rec = reinterpret_cast<uint64_t*>(ctx->d_ev + o_rec);
+    hipLaunchKernelGGL(ksg_capture_eval, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
+    if ((rc = tlaunched(ctx, KSG_K_CAPTURE_EVAL, (double)N))) return rc;
+    hipLaunchKernelGGL(ksg_capture_norm, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
+    if ((rc = tlaunched(ctx, KSG_K_CAPTURE_NORM, (double)N))) return rc;
+  }
   HIPC(ctx, hipGetLastError());
   ctx->ev_parity = 1 - par;
   ctx->ev_clean = true;
@@ -3750,6 +3786,11 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   if (want_norm && n_normrows) back = o_norm + es * N * n_normrows;
   HIPC(ctx, hipMemcpyAsync(ctx->h_ev, ctx->d_ev, back, hipMemcpyDeviceToHost, ctx->stream));
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  if ((rc = tcollect(ctx))) return rc;
+  if (reinterpret_cast<const unsigned*>(ctx->h_ev + o_bar)[1]) {
+    ctx->ev_clean = false;
+    return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: grid barrier timed out");
+  }
   const EvSlot& h = reinterpret_cast<const EvSlot*>(ctx->h_ev)[par];
   const int32_t nfeas = h.stats[0];
   uint32_t status = 0;
@@ -3828,6 +3869,35 @@ int dgrow(ksg_ctx* ctx, T** p, size_t* cap, size_t used, size_t need) {
   return KSG_OK;
 }
 
+// Every program offset of a pod lies inside its blob (the kernels index them
+// relative to the staged blob), the blob inside the pool of `len` words.
+bool pod_offsets_ok(const ksg_pod& p, int64_t len) {
+  if (p.blob < 0 || p.blob_len < 0 || (int64_t)p.blob + p.blob_len > len) return false;
+  for (int32_t off : {p.tol, p.na_req, p.na_pref, p.img, p.pts, p.ipa, p.commit, p.ports})
+    if (off >= 0 && (off < p.blob || off >= p.blob + p.blob_len)) return false;
+  return true;
+}
+
+// The pod's ports program (n_conf conf[] n_own own[]) lies inside its blob
+// and names only UsedPorts bits that exist (< 32 * PW): the kernels index the
+// per-node bitmap with these ids.  `at` reads a program word.
+template <class At>
+bool ports_prog_ok(const ksg_pod& p, int PW, At at) {
+  if (p.ports < 0) return true;
+  const int64_t end = (int64_t)p.blob + p.blob_len;
+  int64_t w = p.ports;
+  for (int part = 0; part < 2; part++) {
+    if (w >= end) return false;
+    const int64_t n = at(w++);
+    if (n < 0 || w + n > end) return false;
+    for (int64_t i = 0; i < n; i++) {
+      const int64_t id = at(w++);
+      if (id < 0 || id >= 32 * (int64_t)PW) return false;
+    }
+  }
+  return true;
+}
+
 // Extent of the program words a pod uses (blob and node set).
 int64_t pod_prog_end(const ksg_pod& p, int N) {
   int64_t e = (int64_t)p.blob + p.blob_len;
@@ -3835,7 +3905,7 @@ int64_t pod_prog_end(const ksg_pod& p, int N) {
   return e;
 }
 
-int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, int off);
+int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, const ksg_pod& p);
 
 int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t* prog, int64_t prog_len,
                     int64_t prog_base) {
@@ -3849,8 +3919,12 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
   int32_t max_blob = ctx->max_blob;
   for (int i = 0; i < n; i++) {
     const ksg_pod& p = pods[i];
-    if (p.blob < 0 || p.blob_len < 0 || pod_prog_end(p, N) > new_len)
+    if (p.blob < 0 || p.blob_len < 0 || pod_prog_end(p, N) > new_len || !pod_offsets_ok(p, new_len))
       return fail(ctx, KSG_E_INVALID, "appended pod program outside the pool");
+    if (!ports_prog_ok(p, ctx->c.PW, [&](int64_t k) -> int64_t {
+          return k >= prog_base ? prog[k - prog_base] : ctx->h_prog[k];
+        }))
+      return fail(ctx, KSG_E_INVALID, "appended pod: host-port ids outside the vocabulary");
     used = std::max(used, pod_prog_end(p, N));
     max_blob = std::max(max_blob, p.blob_len);
   }
@@ -3887,7 +3961,7 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
   if (prog_len) std::copy(prog, prog + prog_len, ctx->h_prog.begin() + prog_base);
   for (int i = 0; i < n; i++) {
     ctx->h_pods.push_back(pods[i]);
-    ctx->h_na_pref_sum.push_back(na_pref_weight_sum(ctx->h_prog, pods[i].na_pref));
+    ctx->h_na_pref_sum.push_back(na_pref_weight_sum(ctx->h_prog, pods[i]));
   }
   ctx->n_pods += n;
   ctx->prog_used = used;
@@ -3917,17 +3991,31 @@ int32_t preempt_n_ma(const ksg_ctx* ctx, const ksg_pod& p) {
   return nm < 0 ? 0x7fffffff : (int32_t)nm;
 }
 
-int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, int off) {
-  // na_pref := n_terms { weight n_reqs requirement[n_reqs] }
+int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, const ksg_pod& p) {
+  // na_pref := n_terms { weight n_reqs requirement[n_reqs] }; every word read
+  // is bounds-checked against the pod's blob (a malformed program yields
+  // INT32_MAX, which keeps the pod off the batched path)
+  const int64_t off = p.na_pref;
   if (off < 0) return 0;
-  size_t w = off;
-  const int nt = prog[w++];
+  const int64_t end = std::min<int64_t>((int64_t)p.blob + p.blob_len, (int64_t)prog.size());
+  int64_t w = off;
+  auto at = [&](int64_t i, bool& ok) -> int64_t {
+    if (i < 0 || i >= end) { ok = false; return 0; }
+    return prog[i];
+  };
+  bool ok = true;
+  const int64_t nt = at(w++, ok);
   int64_t s = 0;
-  for (int t = 0; t < nt; t++) {
-    s += prog[w++];
-    const int nr = prog[w++];
-    for (int r = 0; r < nr; r++) w += 3 + prog[w + 2];
+  for (int64_t t = 0; ok && t < nt; t++) {
+    s += at(w++, ok);
+    const int64_t nr = at(w++, ok);
+    for (int64_t r = 0; ok && r < nr; r++) {
+      const int64_t nv = at(w + 2, ok);
+      if (nv < 0) ok = false;
+      w += 3 + nv;
+    }
   }
+  if (!ok || s < 0) return 0x7fffffff;
   return s > 0x7fffffff ? 0x7fffffff : (int32_t)s;
 }
 
@@ -3955,10 +4043,18 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_COOP_PMODE")) ctx->coop_pmode = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
-    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "pipe" ? 3 : m == "slot" ? 2 : m == "tcol" ? 5 : 4;
+    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : 4;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
+  if (const char* f = getenv("KSG_WAVE_WALK")) ctx->wave_walk = atoi(f) != 0;
+  if (const char* f = getenv("KSG_EVAL_FUSED")) ctx->ev_fused = atoi(f) != 0;
+  {
+    int occ = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)ksg_eval_fused, 256, 0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
+      ctx->ev_fused_max = occ * cus;
+  }
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);
     ctx->slot_block = v <= 64 ? 64 : v <= 128 ? 128 : KSG_BATCH_MAX;
@@ -4015,6 +4111,8 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
   c = DevCluster{};
   c.N = N; c.R = R; c.L = nd->n_label_cols; c.T = nd->max_taints; c.I = nd->max_images;
   c.V = nd->n_taint_vocab; c.W = std::max(1, (nd->n_taint_vocab + 31) / 32);
+  if (nd->n_port_vocab < 0) return fail(ctx, KSG_E_INVALID, "bad host-port vocabulary size");
+  c.PW = std::max(1, (nd->n_port_vocab + 31) / 32);
   int rc = 0;
 #define UP(field, src, cnt) if ((rc = upc(ctx, c.field, src, cnt))) return rc
   UP(alloc, nd->alloc, (size_t)R * N);
@@ -4069,6 +4167,8 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
   if ((rc = dalloc(ctx, &st.tmpl_total, nt))) return rc;
   if ((rc = dalloc(ctx, &st.partial, N))) return rc;
   if ((rc = dalloc(ctx, &st.sraw, (size_t)4 * N))) return rc;
+  if ((rc = dalloc(ctx, &st.ports, (size_t)c.PW * N))) return rc;   // UsedPorts: empty at load
+  HIPC(ctx, hipMemsetAsync(st.ports, 0, sizeof(uint32_t) * c.PW * (size_t)N, ctx->stream));
   HIPC(ctx, hipMemsetAsync(st.cnt, 0, sizeof(int32_t) * std::max(c.S, 1) * (size_t)N, ctx->stream));
   HIPC(ctx, hipMemsetAsync(st.tab, 0, sizeof(int32_t) * ctx->tab_words, ctx->stream));
   HIPC(ctx, hipMemsetAsync(st.tmpl_total, 0, sizeof(int32_t) * nt, ctx->stream));
@@ -4093,11 +4193,12 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
   for (int i = 0; i < wl->n_pods; i++) {
     const ksg_pod& p = ctx->h_pods[i];
     ctx->max_blob = std::max(ctx->max_blob, p.blob_len);
-    if (p.blob < 0 || (int64_t)p.blob + p.blob_len > wl->prog_len)
-      return fail(ctx, KSG_E_INVALID, "pod blob outside the program pool");
+    if (!pod_offsets_ok(p, wl->prog_len)) return fail(ctx, KSG_E_INVALID, "pod program outside its blob / the pool");
+    if (!ports_prog_ok(p, ctx->c.PW, [&](int64_t k) -> int64_t { return prog[k]; }))
+      return fail(ctx, KSG_E_INVALID, "pod " + std::to_string(i) + ": host-port ids outside the vocabulary");
     if (p.node_set >= 0 && (int64_t)p.node_set + (ctx->c.N + 31) / 32 > wl->prog_len)
       return fail(ctx, KSG_E_INVALID, "node set outside the program pool");
-    ctx->h_na_pref_sum[i] = na_pref_weight_sum(prog, p.na_pref);
+    ctx->h_na_pref_sum[i] = na_pref_weight_sum(prog, p);
   }
   ctx->h_prog = std::move(prog);
   ctx->prog_used = 0;
@@ -4143,7 +4244,8 @@ int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t 
   // then drop it again: the device buffers keep the capacity.
   const int64_t base = (int64_t)ctx->h_prog.size();
   ksg_pod p = *pod;
-  for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob})
+  for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob,
+                     &p.ports})
     if (*f >= 0) *f = (int32_t)(*f + base);
   const int32_t n0 = ctx->n_pods, blob0 = ctx->max_blob;
   const int64_t used0 = ctx->prog_used;
@@ -4189,6 +4291,8 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
   if (pod < 0 || pod >= ctx->n_pods || n_cand < 0 || (n_cand > 0 && (!cand_node || !vic_off || !fits)))
     return fail(ctx, KSG_E_INVALID, "preempt arguments");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
+  if (ctx->h_pods[pod].ports >= 0)   // the dry run re-runs Fit / PTS / IPA only
+    return fail(ctx, KSG_E_UNSUPPORTED, "preemption: a preemptor with host ports (NodePorts) is not modelled");
   if (n_cand == 0) return KSG_OK;
   const int32_t nv = vic_off[n_cand];
   if (vic_off[0] != 0 || nv < 0 || (nv > 0 && (!vic_pod || !victim)))
@@ -4305,6 +4409,11 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     TA(tmp, &s.nonzero, 8 * RR * s.stride_nz);
     TA(tmp, &s.pod_count, 4 * RR * s.stride_pc);
   }
+  s.ports = nullptr;   // replicas never share the context's UsedPorts
+  if (!sweep && range_has_ports(ctx, first, count)) {
+    s.stride_ports = (size_t)ctx->c.PW * N;
+    TA(tmp, &s.ports, 4 * RR * s.stride_ports);
+  }
   if (!sweep) {
     TA(tmp, &s.cnt, 4 * RR * s.stride_cnt);
     TA(tmp, &s.tab, 4 * RR * s.stride_tab);
@@ -4335,6 +4444,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     bcast(ctx->st.tab, s.tab, s.stride_tab, s.stride_tab);
     bcast(ctx->st.tmpl_total, s.tmpl_total, s.stride_tt, s.stride_tt);
   }
+  if (s.ports) bcast(ctx->st.ports, s.ports, s.stride_ports, s.stride_ports);
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipMemcpyAsync(d_prof, profiles, sizeof(ksg_profile) * RR, hipMemcpyHostToDevice, ctx->stream));
   a.profiles = d_prof;
@@ -4415,6 +4525,7 @@ int ksg_reset_state(ksg_ctx* ctx) {
   HIPC(ctx, hipMemsetAsync(ctx->st.cnt, 0, 4 * std::max(ctx->c.S, 1) * N, ctx->stream));
   HIPC(ctx, hipMemsetAsync(ctx->st.tab, 0, 4 * ctx->tab_words, ctx->stream));
   HIPC(ctx, hipMemsetAsync(ctx->st.tmpl_total, 0, 4 * std::max(ctx->c.n_tmpl, 1), ctx->stream));
+  HIPC(ctx, hipMemsetAsync(ctx->st.ports, 0, 4 * (size_t)ctx->c.PW * N, ctx->stream));
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
   return KSG_OK;
 }
@@ -4459,7 +4570,7 @@ int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
   if (!ctx || !path || !flags) return KSG_E_INVALID;
   *path = ctx->last_path;
   *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0) |
-           (ctx->last_tcol ? KSG_RUN_TCOL : 0);
+           (ctx->last_tcol ? KSG_RUN_TCOL : 0) | (ctx->last_wave ? KSG_RUN_WAVE : 0);
   return KSG_OK;
 }
 

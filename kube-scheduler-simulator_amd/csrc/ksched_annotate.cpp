@@ -155,6 +155,7 @@ bool filter_message(const ksg_annotator* a, uint32_t st, int n, std::string& msg
       return true;
     }
     case KSG_PL_NODE_AFFINITY: msg = "node(s) didn't match Pod's node affinity/selector"; return true;
+    case KSG_PL_NODE_PORTS: msg = "node(s) didn't have free ports for the requested pod ports"; return true;
     case KSG_PL_NODE_RESOURCES_FIT: {
       // noderesources.fitsRequest order: pods, cpu, memory, ephemeral, scalars by column
       bool first = true;

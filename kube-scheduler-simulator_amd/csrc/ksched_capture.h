@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
   for (int k = tid; k < a.nb; k += 256) s_pl[k] = a.placements[a.out0 + k];
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();
-  const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog);
+  const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog, false, a.st.ports);
   const int n = blockIdx.x * 256 + tid;
   const size_t o = (size_t)(a.out0 + j);
   int32_t feas = 0, mt = 0, ma = 0, lo = 0;
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void ksg_capture_norm(CapArgs a) {
   if (a.next && blockIdx.x == 0 && tid < 8) a.next[tid] = 0;   // the next call's slot
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();
-  const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog);
+  const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog, false, a.st.ports);
   const int n = blockIdx.x * 256 + tid;
   const int32_t nfeas = a.stats[4 * j], max_t = a.stats[4 * j + 1], max_a = a.stats[4 * j + 2];
   if (a.best) {   // selectHost over this block's nodes, merged by one atomic per block
@@ -204,3 +204,4 @@ __global__ __launch_bounds__(256) void ksg_capture_norm(CapArgs a) {
     }
   }
 }
+

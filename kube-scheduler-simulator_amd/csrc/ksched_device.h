@@ -48,6 +48,7 @@ struct DevCluster {
   const uint8_t* col_unique;       // [L]
   const double* log_table;
   int32_t log_n;
+  int32_t PW;                      // NodePorts: words of a node's UsedPorts bitmap (host-port vocabulary / 32)
 };
 
 // Mutable per-replica state.  Replica r's arrays start at base + r * stride.
@@ -61,8 +62,36 @@ struct DevState {
   // scratch (per replica)
   int64_t* partial;     // [N] Σ weight × score of un-normalised plugins, -1 = infeasible
   int64_t* sraw;        // [4][N] raw scores of normalised plugins (taint, NA, PTS, IPA)
-  size_t stride_req, stride_nz, stride_pc, stride_cnt, stride_tab, stride_tt, stride_part, stride_sraw;
+  uint32_t* ports;      // [PW][N]  NodeInfo.UsedPorts as a bitmap over the host-port vocabulary
+  size_t stride_req, stride_nz, stride_pc, stride_cnt, stride_tab, stride_tt, stride_part, stride_sraw,
+      stride_ports;
 };
+
+// nodeports.fitsPorts: does any id of the pod's conflict list sit in the
+// node's UsedPorts?  (HostPortInfo.CheckConflict, resolved on the host into
+// vocabulary ids: ksched.h ksg_pod.ports.)
+__device__ __forceinline__ bool ports_conflict(const uint32_t* used, int N, int n, const int32_t* w) {
+  const int nconf = w[0];
+  bool hit = false;
+  for (int i = 0; i < nconf; i++) {
+    const uint32_t id = (uint32_t)w[1 + i];
+    hit = hit || ((used[(size_t)(id >> 5) * N + n] >> (id & 31)) & 1u);
+  }
+  return hit;
+}
+// NodeInfo.updateUsedPorts: Add (sign > 0) / Remove (sign < 0) the pod's own
+// ids.  A set, as HostPortInfo is: Remove drops the entry even if another pod
+// on the node uses the same (IP, protocol, port).
+__device__ __forceinline__ void ports_commit(uint32_t* used, int N, int n, const int32_t* w, int sign) {
+  const int32_t* own = w + 1 + w[0];
+  const int nown = own[0];
+  for (int i = 0; i < nown; i++) {
+    const uint32_t id = (uint32_t)own[1 + i];
+    uint32_t& word = used[(size_t)(id >> 5) * N + n];
+    if (sign > 0) word |= 1u << (id & 31);
+    else word &= ~(1u << (id & 31));
+  }
+}
 
 __device__ __forceinline__ int64_t ld64(const int32_t* w) {
   return (int64_t)(((uint64_t)(uint32_t)w[1] << 32) | (uint32_t)w[0]);

@@ -99,13 +99,16 @@ struct PodView {
   uint32_t fskip;            // filter plugins not run (PreFilter Skip)
   uint32_t smask;            // score plugins run (enabled and not PreScore Skip)
   int64_t w_fit, w_ba, w_img, w_t, w_a;
+  int ports;                 // NodePorts program (blob-relative), -1 = none
+  const uint32_t* used_ports;   // the replica's UsedPorts bitmaps (set by kernels that evaluate NodePorts)
 };
 
 // topo = false: PodTopologySpread / InterPodAffinity reach this evaluator only
 // for pods without terms (host check), i.e. they Skip.  topo = true: the
 // topology kernel evaluates them (IPA Skip decided on the device).
 __device__ __forceinline__ PodView make_view(const DevCluster& c, const ksg_profile& prof, const ksg_pod& p,
-                                             const int32_t* P, const int32_t* gprog, bool topo = false) {
+                                             const int32_t* P, const int32_t* gprog, bool topo = false,
+                                             const uint32_t* used_ports = nullptr) {
   PodView v;
   const int boff = p.blob;
   auto rb = [boff](int off) { return off < 0 ? -1 : off - boff; };
@@ -115,6 +118,8 @@ __device__ __forceinline__ PodView make_view(const DevCluster& c, const ksg_prof
   v.na_pref = rb(p.na_pref);
   v.img = rb(p.img);
   v.commit = rb(p.commit);
+  v.ports = rb(p.ports);
+  v.used_ports = used_ports;
   v.tolf = P + rb(p.tol);
   v.tolp = v.tolf + c.W;
   v.node_set = p.node_set >= 0 ? gprog + p.node_set : nullptr;
@@ -459,6 +464,9 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
         case KSG_PL_NODE_AFFINITY:
           if (!na_required_match(nd, v.P, v.na_req)) st = (uint32_t)(pl + 1) | (1u << 8);
           break;
+        case KSG_PL_NODE_PORTS:   // reached only by pods with host ports (PreFilter Skip otherwise)
+          if (v.ports >= 0 && v.used_ports && ports_conflict(v.used_ports, N, n, v.P + v.ports)) st = pl + 1;
+          break;
         case KSG_PL_NODE_RESOURCES_FIT: {
           const uint32_t b = fit_filter(c, p, L, prof.fit_ignored_res);
           if (b) st = (uint32_t)(pl + 1) | (b << 8);
@@ -582,8 +590,10 @@ __device__ __forceinline__ void ipa_skip_bits(const ksg_profile& prof, const ksg
 // deletion (NodeInfo.RemovePod), the exact inverse.
 __device__ void commit_node(const DevCluster& c, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
                             int32_t* cnt, int32_t* tab, int32_t* tmpl_total, const ksg_pod& p,
-                            const int32_t* commit_prog, int n, int sign = 1) {
+                            const int32_t* commit_prog, int n, int sign = 1, uint32_t* ports = nullptr,
+                            const int32_t* ports_prog = nullptr) {
   const int N = c.N;
+  if (ports && ports_prog) ports_commit(ports, N, n, ports_prog, sign);
   for (int r = 0; r < c.R; r++) requested[(size_t)r * N + n] += sign * p.req[r];
   nonzero[n] += sign * p.nz_cpu;
   nonzero[(size_t)N + n] += sign * p.nz_mem;

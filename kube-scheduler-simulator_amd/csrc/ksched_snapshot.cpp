@@ -53,6 +53,7 @@ const char* const kNonEval[] = {"SchedulingGates", "PrioritySort", "DefaultPreem
 const std::string kCPU = "cpu", kMemory = "memory", kEphemeral = "ephemeral-storage", kPods = "pods";
 const std::string kHostname = "kubernetes.io/hostname", kZone = "topology.kubernetes.io/zone";
 const std::string kObjectName = "metadata.name";
+const std::string kBindAllHostIP = "0.0.0.0";   // framework.DefaultBindAllHostIP
 const std::string kUnschedTaint = "node.kubernetes.io/unschedulable";
 constexpr int64_t kDefaultMilliCPU = 100, kDefaultMemory = 200ll * 1024 * 1024;
 
@@ -164,11 +165,13 @@ struct Spread {
   Sel sel;
   std::vector<std::string> mlk;
 };
+// sanitised (hostIP, protocol, hostPort): framework.HostPortInfo's key
+using HostPort = std::tuple<std::string, std::string, int32_t>;
 struct Container {
   std::string image;
   ResMap req;
   bool restartable;
-  int32_t host_ports;
+  std::vector<HostPort> host_ports;   // hostPort > 0 only
 };
 struct Taint {
   std::string key, value, effect;
@@ -259,9 +262,25 @@ std::vector<AffTerm> copy_aff(int32_t n, const ksg_affinity_term_view* v) {
 }
 std::vector<Container> copy_containers(int32_t n, const ksg_container_view* v) {
   std::vector<Container> out;
-  for (int32_t i = 0; i < n; i++)
-    out.push_back(Container{S(v[i].image), copy_res(v[i].n_requests, v[i].requests), v[i].restartable != 0,
-                            v[i].n_host_ports});
+  for (int32_t i = 0; i < n; i++) {
+    Container c{S(v[i].image), copy_res(v[i].n_requests, v[i].requests), v[i].restartable != 0, {}};
+    for (int32_t k = 0; k < v[i].n_host_ports; k++) {
+      const ksg_host_port_view& hp = v[i].host_ports[k];
+      if (hp.host_port <= 0) continue;   // GetHostPorts: only ports with a hostPort
+      std::string ip = S(hp.host_ip), proto = S(hp.protocol);
+      c.host_ports.emplace_back(ip.empty() ? kBindAllHostIP : ip, proto.empty() ? "TCP" : proto, hp.host_port);
+    }
+    out.push_back(std::move(c));
+  }
+  return out;
+}
+
+// schedutil.GetHostPorts: restartable init containers, then the containers
+std::vector<HostPort> pod_host_ports(const Pod& p) {
+  std::vector<HostPort> out;
+  for (auto& c : p.init)
+    if (c.restartable) out.insert(out.end(), c.host_ports.begin(), c.host_ports.end());
+  for (auto& c : p.containers) out.insert(out.end(), c.host_ports.begin(), c.host_ports.end());
   return out;
 }
 
@@ -402,6 +421,8 @@ struct Encoded {
   std::map<Taint, int> taint_id;
   std::vector<std::string> image_vocab;
   std::map<std::string, int> image_id;
+  std::vector<HostPort> port_vocab;    // every host port a pod uses, sorted
+  std::map<HostPort, int> port_id;
   std::map<std::string, std::pair<int64_t, int64_t>> image_state;   // name -> (size, numNodes)
   int max_taints = 1, max_images = 1, tol_words = 1;
   // topology universe
@@ -466,6 +487,9 @@ struct ksg_snapshot {
   std::vector<std::pair<ResMap, ResMap>> req_cache;
   // views handed out
   std::vector<const char*> v_nodes, v_res, v_taints;
+  // scalar resource names of the nodes, pods and profile so far (add_pod
+  // refuses a pod that would push the resource columns past KSG_MAX_RES)
+  std::set<std::string> scalars;
 };
 
 namespace {
@@ -682,6 +706,17 @@ void build_taints(ksg_snapshot* s) {
   e.tol_words = std::max<int>(1, ((int)e.taint_vocab.size() + 31) / 32);
   e.taint_strings.clear();
   for (auto& t : e.taint_vocab) e.taint_strings.push_back("{" + t.key + ": " + t.value + "}");
+}
+
+// The host-port vocabulary (encoder._build_ports): NodeInfo.UsedPorts only
+// ever holds the ports of the snapshot's pods.
+void build_ports(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  std::set<HostPort> all;
+  for (auto& p : s->pods)
+    for (auto& hp : pod_host_ports(p)) all.insert(hp);
+  e.port_vocab.assign(all.begin(), all.end());
+  for (size_t v = 0; v < e.port_vocab.size(); v++) e.port_id[e.port_vocab[v]] = (int)v;
 }
 
 void build_images(ksg_snapshot* s) {
@@ -921,6 +956,8 @@ void prepare_frozen(ksg_snapshot* s, int i, Pass& ps) {
     }
     owned.emplace_back(it->second, wt);
   };
+  for (auto& hp : pod_host_ports(p))
+    if (!e.port_id.count(hp)) ps.miss = true;
   for (auto& t : p.anti_req) own(TMPL_REQ_ANTI, t, 1);
   for (auto& t : p.aff_req) own(TMPL_REQ_AFF, t, 1);
   for (auto& t : p.aff_pref) own(TMPL_PREF, t, t.weight);
@@ -949,8 +986,6 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
   const Pod& p = s->pods[i];
   const Profile& prof = s->prof;
   std::vector<int32_t>& prog = e.prog;
-  for (auto& c : p.containers)
-    if (c.host_ports > 0) throw EncodeError{KSG_E_UNSUPPORTED, "hostPorts (NodePorts) are not encoded yet"};
   const ResMap& r = s->req_cache[i].first;
   const ResMap& nz = s->req_cache[i].second;
   ksg_pod rec;
@@ -980,7 +1015,8 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
   if (best_effort) flags |= KSG_POD_BEST_EFFORT;
   uint32_t fskip = 0, sskip = 0;
   if (!na_required) fskip |= 1u << KSG_PL_NODE_AFFINITY;
-  fskip |= 1u << KSG_PL_NODE_PORTS;
+  const std::vector<HostPort> hports = pod_host_ports(p);
+  if (hports.empty()) fskip |= 1u << KSG_PL_NODE_PORTS;   // nodeports PreFilter: Skip without ports
   for (int v : {KSG_PL_VOLUME_RESTRICTIONS, KSG_PL_NODE_VOLUME_LIMITS, KSG_PL_VOLUME_BINDING, KSG_PL_VOLUME_ZONE})
     fskip |= 1u << v;
   const auto& hard = s->pts_cache[i].first;
@@ -1192,6 +1228,32 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
       for (auto& pr : tmo) prog.insert(prog.end(), {pr.first, pr.second});
     }
   }
+  // ports := n_conf conf[n_conf] n_own own[n_own] (HostPortInfo.CheckConflict
+  // over the vocabulary; own = what the pod's assume adds to UsedPorts)
+  rec.ports = -1;
+  if (!hports.empty()) {
+    std::set<int32_t> conf, own;
+    for (auto& hp : hports) {
+      auto it = e.port_id.find(hp);
+      if (it == e.port_id.end()) {   // frozen pass: the vocabulary would grow
+        ps.miss = true;
+        break;
+      }
+      own.insert(it->second);
+      const std::string& ip = std::get<0>(hp);
+      for (size_t v = 0; v < e.port_vocab.size(); v++) {
+        const HostPort& q = e.port_vocab[v];
+        if (std::get<1>(q) == std::get<1>(hp) && std::get<2>(q) == std::get<2>(hp) &&
+            (ip == kBindAllHostIP || std::get<0>(q) == kBindAllHostIP || std::get<0>(q) == ip))
+          conf.insert((int32_t)v);
+      }
+    }
+    rec.ports = (int32_t)prog.size();
+    prog.push_back((int32_t)conf.size());
+    prog.insert(prog.end(), conf.begin(), conf.end());
+    prog.push_back((int32_t)own.size());
+    prog.insert(prog.end(), own.begin(), own.end());
+  }
   rec.blob = blob;
   rec.blob_len = (int32_t)prog.size() - blob;
   if ((int)e.pods.size() <= i) e.pods.resize(i + 1);
@@ -1216,6 +1278,7 @@ void encode_all(ksg_snapshot* s) {
   build_label_columns(s);
   build_taints(s);
   build_images(s);
+  build_ports(s);
   build_topology_universe(s);
   // node columns
   const size_t R = e.res_names.size();
@@ -1418,6 +1481,7 @@ void fill_views(ksg_snapshot* s, ksg_nodes* nd, ksg_topology* tp, ksg_workload* 
     nd->max_images = e.max_images;
     nd->images = e.images.data();
     nd->n_images = (int32_t)e.image_vocab.size();
+    nd->n_port_vocab = (int32_t)e.port_vocab.size();
   }
   if (tp) {
     *tp = ksg_topology{};
@@ -1510,6 +1574,21 @@ int upload_all(ksg_snapshot* s, ksg_ctx* ctx) {
 int full_load(ksg_snapshot* s, ksg_ctx* ctx) {
   const int rc = do_encode(s);
   return rc ? rc : upload_all(s, ctx);
+}
+
+// Everything encode_pod would refuse for this pod alone, checked before the
+// pod joins the snapshot: one unsupported pod must not make every later
+// sync / encode of the snapshot fail.  Throws EncodeError.
+void validate_pod(const ksg_snapshot* s, const Pod& p) {
+  for (auto& c : p.spread) (void)canon_selector(c.sel);
+  (void)canon_selector(p.default_sel);
+  for (auto* v : {&p.aff_req, &p.aff_pref, &p.anti_req, &p.anti_pref})
+    for (auto& t : *v) (void)term_scope(t, p);
+  std::set<std::string> scal = s->scalars;
+  for (auto& kv : pod_requests(p, false))
+    if (is_scalar(kv.first)) scal.insert(kv.first);
+  if (3 + scal.size() > (size_t)KSG_MAX_RES)
+    throw EncodeError{KSG_E_UNSUPPORTED, "more than " + std::to_string(KSG_MAX_RES) + " resource columns"};
 }
 
 // framework.Status (code, Message()) of a Filter status word at `node` for
@@ -1630,6 +1709,10 @@ int ksg_snapshot_new(const ksg_profile_view* pv, ksg_snapshot** out) {
     p.ba_res.emplace_back(S(pv->ba_resources[i].name), pv->ba_resources[i].value);
   for (int32_t i = 0; i < pv->n_fit_ignored_resources; i++) p.ignored.insert(S(pv->fit_ignored_resources[i]));
   for (int32_t i = 0; i < pv->n_fit_ignored_groups; i++) p.ignored_groups.insert(S(pv->fit_ignored_groups[i]));
+  for (auto& r : p.fit_res)
+    if (is_scalar(r.first)) s->scalars.insert(r.first);
+  for (auto& r : p.ba_res)
+    if (is_scalar(r.first)) s->scalars.insert(r.first);
   p.hard_weight = pv->hard_pod_affinity_weight;
   p.ignore_pref = pv->ignore_preferred_terms_of_existing_pods != 0;
   p.pts_system = pv->pts_system_defaulted != 0;
@@ -1671,6 +1754,13 @@ int ksg_snapshot_add_node(ksg_snapshot* s, const ksg_node_view* v, int32_t* inde
     n.taints.push_back(Taint{S(v->taints[i].key), S(v->taints[i].value), S(v->taints[i].effect)});
   n.alloc = copy_res(v->n_alloc, v->allocatable);
   n.unsched = v->unschedulable != 0;
+  std::set<std::string> scal = s->scalars;
+  for (auto& kv : n.alloc)
+    if (is_scalar(kv.first)) scal.insert(kv.first);
+  if (3 + scal.size() > (size_t)KSG_MAX_RES)
+    return fail(s, KSG_E_UNSUPPORTED, "node " + n.name + ": more than " + std::to_string(KSG_MAX_RES) +
+                                          " resource columns");
+  s->scalars = std::move(scal);
   for (int32_t i = 0; i < v->n_images; i++) {
     Image im;
     for (int32_t k = 0; k < v->images[i].n_names; k++) im.names.push_back(S(v->images[i].names[k]));
@@ -1727,6 +1817,13 @@ int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index)
   p.default_sel = copy_sel(v->default_spread_selector);
   p.terminating = v->terminating != 0;
   p.priority = v->priority;
+  try {
+    validate_pod(s, p);
+  } catch (const EncodeError& x) {
+    return fail(s, x.code, "pod " + p.ns + "/" + p.name + ": " + x.msg);
+  }
+  for (auto& kv : pod_requests(p, false))
+    if (is_scalar(kv.first)) s->scalars.insert(kv.first);
   const int32_t idx = (int32_t)s->pods.size();
   s->pods.push_back(std::move(p));
   if (index) *index = idx;

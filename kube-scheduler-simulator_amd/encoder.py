@@ -40,8 +40,12 @@ Program grammar (int32 words; offsets are word indices, -1 = absent):
                   n_m_anti tmpl[n_m_anti]  n_m_hard tmpl[n_m_hard]  n_m_pref tmpl[n_m_pref]
   commit       := n_sel sel[n_sel] n_tmpl {tmpl weight}[n_tmpl]   (weight: the term's signed
                   preferred weight, 1 for required terms)
+  ports        := n_conf conf[n_conf] n_own own[n_own]   (NodePorts: ids into the host-port
+                  vocabulary of every (hostIP, protocol, hostPort) any pod uses, sanitised and
+                  sorted; conf = the ids HostPortInfo.CheckConflict reports for the pod's ports,
+                  own = the pod's ports, which its assume adds to the node's UsedPorts)
 
-A pod's tol..commit programs are contiguous: [blob, blob + blob_len).
+A pod's tol..ports programs are contiguous: [blob, blob + blob_len).
 """
 from __future__ import annotations
 
@@ -76,7 +80,7 @@ POD_DTYPE = np.dtype([
     ("flags", "<u4"), ("filter_skip", "<u4"), ("score_skip", "<u4"),
     ("node_name", "<i4"), ("n_containers", "<i4"), ("tol", "<i4"), ("na_req", "<i4"),
     ("na_pref", "<i4"), ("img", "<i4"), ("node_set", "<i4"), ("pts", "<i4"), ("ipa", "<i4"),
-    ("commit", "<i4"), ("blob", "<i4"), ("blob_len", "<i4"), ("pad", "<i4"),
+    ("commit", "<i4"), ("blob", "<i4"), ("blob_len", "<i4"), ("ports", "<i4"),
 ])
 assert POD_DTYPE.itemsize == 144
 
@@ -250,6 +254,7 @@ class Encoder:
         self._build_taints()
         self._build_images()
         self._build_topology_universe()
+        self._build_ports()
         self.cluster = self._encode_cluster()
         self.workload = self._encode_pods()
         # requirement values may extend a column's vocabulary after the node
@@ -275,6 +280,31 @@ class Encoder:
         if len(self.res_names) > MAX_RES:
             raise NotImplementedError(f"more than {MAX_RES} resource columns")
         self.res_col = {r: i for i, r in enumerate(self.res_names)}
+
+    # -------------------------------------------------------------- host ports
+    def _build_ports(self):
+        """The host-port vocabulary: every sanitised (hostIP, protocol,
+        hostPort) a pod of the workload uses, sorted (NodeInfo.UsedPorts only
+        ever holds those)."""
+        vocab = set()
+        for p in self.pods:
+            for ip, proto, port in p.host_ports():
+                vocab.add((*m.sanitize_host_port(ip, proto), int(port)))
+        self.port_vocab = sorted(vocab)
+        self.port_id = {t: i for i, t in enumerate(self.port_vocab)}
+
+    def _ports(self, p: m.Pod) -> int:
+        want = [(*m.sanitize_host_port(ip, proto), int(port)) for ip, proto, port in p.host_ports()]
+        if not want:
+            return -1
+        conf = set()
+        for ip, proto, port in want:   # HostPortInfo.CheckConflict over the vocabulary
+            for i, (vip, vproto, vport) in enumerate(self.port_vocab):
+                if vproto == proto and vport == port and (
+                        ip == m.DEFAULT_BIND_ALL_HOST_IP or vip in (m.DEFAULT_BIND_ALL_HOST_IP, ip)):
+                    conf.add(i)
+        own = sorted({self.port_id[t] for t in want})
+        return self._emit([len(conf)] + sorted(conf) + [len(own)] + own)
 
     # -------------------------------------------------------------- labels
     def _pts_constraints(self, pod: m.Pod):
@@ -672,6 +702,7 @@ class Encoder:
         ec.max_taints = self.max_taints
         ec.max_images = self.max_images
         ec.n_images = len(self.image_vocab)
+        ec.n_port_vocab = len(self.port_vocab)
         return ec
 
     def _encode_pods(self) -> EncodedWorkload:
@@ -681,8 +712,6 @@ class Encoder:
         ba_cols = [self.res_col[r] for r, _ in prof.ba_resources if r in self.res_col]
         for i, p in enumerate(self.pods):
             names.append(f"{p.namespace}/{p.name}")
-            if p.host_ports():
-                raise NotImplementedError("hostPorts (NodePorts) are not encoded yet")
             r, nz = self._req_cache[i]
             e = rec[i]
             for k, v in r.items():
@@ -702,7 +731,8 @@ class Encoder:
             sskip = 0
             if not na_required:
                 fskip |= 1 << P.NODE_AFFINITY
-            fskip |= 1 << P.NODE_PORTS     # no hostPorts (checked above)
+            if not p.host_ports():
+                fskip |= 1 << P.NODE_PORTS     # nodeports PreFilter: Skip without host ports
             for v in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE):
                 fskip |= 1 << v
             hard, soft = self._pts_cache[i]
@@ -755,6 +785,7 @@ class Encoder:
             e["pts"] = self._pts(i, p)
             e["ipa"] = self._ipa(i, p)
             e["commit"] = self._commit(i)
+            e["ports"] = self._ports(p)
             e["blob"] = blob
             e["blob_len"] = len(self.prog) - blob
             self.max_blob = max(self.max_blob, len(self.prog) - blob)

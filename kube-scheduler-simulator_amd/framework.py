@@ -38,6 +38,7 @@ FS_NOT_EVALUATED = E.FS_NOT_EVALUATED
 MSG_UNSCHEDULABLE = "node(s) were unschedulable"
 MSG_NODE_NAME = "node(s) didn't match the requested node name"
 MSG_NODE_AFFINITY = "node(s) didn't match Pod's node affinity/selector"
+MSG_NODE_PORTS = "node(s) didn't have free ports for the requested pod ports"
 MSG_NA_CONFLICT = "pod affinity terms conflict"
 MSG_PTS = "node(s) didn't match pod topology spread constraints"
 MSG_PTS_LABEL = MSG_PTS + " (missing required label)"
@@ -79,6 +80,8 @@ class Decoder:
             return f"node(s) had untolerated taint {{{t.key}: {t.value}}}"
         if pl == P.NODE_AFFINITY:
             return MSG_NODE_AFFINITY
+        if pl == P.NODE_PORTS:
+            return MSG_NODE_PORTS
         if pl == P.NODE_RESOURCES_FIT:
             return ", ".join(fit_reasons(reason, self.cl.res_names))
         if pl == P.POD_TOPOLOGY_SPREAD:

@@ -330,3 +330,66 @@ def preemption_topo_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 1
             other = apps[int(rng.integers(len(apps)))]
             p.pod_affinity_required = [m.PodAffinityTerm(sel(other), m.LABEL_ZONE)]
     return nodes, pods, bound, prof
+
+
+def host_ports_case(n_nodes: int = 40, n_queue: int = 240, seed: int = 9, daemonset: bool = True):
+    """NodePorts parity case.  Every node runs a DaemonSet-style pod already
+    bound to it (hostPort 9100/TCP, as a node exporter; `daemonset`), ingested
+    like any running pod.  The queue mixes: ingress pods on 80 + 443 (one per
+    node at most), pods pinned to a host IP (127.0.0.1:8080 conflicts with a
+    0.0.0.0:8080 pod and vice versa, 10.0.0.1:8080 does not conflict with
+    127.0.0.1:8080), UDP/53 next to TCP/53 (different protocol: no
+    conflict), a restartable init container (sidecar) holding 15000 (its
+    ports count), a plain init container holding 15000 (its ports don't),
+    a pod repeating its own port in two containers, DaemonSet-style pods
+    for new ports with a matchFields node pin, and port-less pods.  Returns
+    (nodes, pods, bound [(pod, node)], profile)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = [_node(i, rng, 4) for i in range(n_nodes)]
+    pods, bound = [], []
+
+    def pod(name, ports=(), init=None, req=None):
+        c = m.Container(image="registry.k8s.io/pause:3.10", host_ports=tuple(ports),
+                        requests=req if req is not None else {m.CPU: 100, m.MEMORY: 128 * MI})
+        return m.Pod(name=name, containers=[c], init_containers=[init] if init else [])
+    if daemonset:
+        for i in range(n_nodes):
+            p = pod(f"node-exporter-{i:04d}", [("", "", 9100)])
+            p.node_name = nodes[i].name
+            bound.append((len(pods), i))
+            pods.append(p)
+    kinds = ["ingress", "lo8080", "any8080", "ip8080", "dns-udp", "dns-tcp", "sidecar", "init", "dup",
+             "exporter", "ds-new", "plain", "plain"]
+    for j in range(n_queue):
+        k = kinds[int(rng.integers(len(kinds)))]
+        name = f"{k}-{j:05d}"
+        if k == "ingress":
+            p = pod(name, [("", "TCP", 80), ("", "TCP", 443)])
+        elif k == "lo8080":
+            p = pod(name, [("127.0.0.1", "TCP", 8080)])
+        elif k == "any8080":
+            p = pod(name, [("0.0.0.0", "", 8080)])
+        elif k == "ip8080":
+            p = pod(name, [("10.0.0.1", "TCP", 8080)])
+        elif k == "dns-udp":
+            p = pod(name, [("", "UDP", 53)])
+        elif k == "dns-tcp":
+            p = pod(name, [("", "TCP", 53), ("", "TCP", 0)])   # hostPort 0: not a host port
+        elif k == "sidecar":
+            p = pod(name, init=m.Container(image="envoy", restartable=True, host_ports=(("", "TCP", 15000),)))
+        elif k == "init":
+            p = pod(name, init=m.Container(image="busybox", host_ports=(("", "TCP", 15000),)))
+        elif k == "dup":
+            p = pod(name, [("", "TCP", 7000)])
+            p.containers.append(m.Container(image="registry.k8s.io/pause:3.10", host_ports=(("", "TCP", 7000),)))
+        elif k == "exporter":   # a second exporter asks for the DaemonSet's port
+            p = pod(name, [("", "TCP", 9100)])
+        elif k == "ds-new":     # DaemonSet controller: required matchFields metadata.name In [node]
+            p = pod(name, [("", "TCP", 9200)])
+            p.node_affinity_required = [m.NodeSelectorTerm(match_fields=(m.Requirement(
+                m.OBJECT_NAME_FIELD, m.IN, (nodes[int(rng.integers(n_nodes))].name,)),))]
+            p.tolerations.append(m.Toleration("", m.OP_EXISTS))
+        else:
+            p = pod(name)
+        pods.append(p)
+    return nodes, pods, bound, P.default_profile()

@@ -90,13 +90,15 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
         return bytes_per_eval + 12
     if name == "ksg_capture_norm":   # record read, normalised row and total written (one scored row at least)
         return 24
+    if name == "ksg_eval_fused":     # ksg_capture_eval + ksg_capture_norm in one cooperative launch
+        return bytes_per_eval + 12 + 24
     if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
         return 8
     if name == "ksg_tcol_carry":
         return 140   # live columns of a carried node (128 B) + record and static (12 B) per (pod, carried node)
     if name == "ksg_batch_transpose":
         return 24   # 12 B read + 12 B written per (pod, node)
-    if name in ("ksg_batch_phase2", "ksg_batch_phase2s", "ksg_batch_phase2p", "ksg_batch_phase2t"):
+    if name in ("ksg_batch_phase2", "ksg_batch_phase2s", "ksg_batch_phase2p", "ksg_batch_phase2t", "ksg_batch_phase2w"):
         return 20
     if name in ("ksg_sweep_static", "ksg_sweep"):
         if not isinstance(cols, dict):
@@ -127,3 +129,26 @@ def dominant_kernel_roofline(kstats, bytes_per_eval):
     return {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": dom["frac"], "kernel": dom["name"], "avg_launch_ms": dom["avg_ms"],
             "bytes_per_launch": dom["bytes_per_launch"], "kernels": rows}
+
+
+PHASE2_KERNELS = ("ksg_batch_phase2w", "ksg_batch_phase2s", "ksg_batch_phase2t", "ksg_batch_phase2p",
+                  "ksg_batch_phase2")
+
+
+def price_decided_node_evals(roof, bytes_per_eval: int, node_evals: int):
+    """A phase-2 walk decides a batch of pods over every node: price a launch
+    by SURVEY §8(d)'s bytes per node-eval x the node-evals it decides (batch
+    pods x nodes, i.e. node_evals of the run / launches), as the round-1
+    verdict recomputed it; the changed-slot figure the kernel stats count is
+    kept as achieved_changed_slot_bytes."""
+    if not roof or roof.get("kernel") not in PHASE2_KERNELS:
+        return roof
+    row = next((k for k in roof.get("kernels", []) if k["name"] == roof["kernel"]), None)
+    if row and row["calls"] and row["avg_ms"] > 0:
+        per_launch = bytes_per_eval * node_evals / row["calls"]
+        roof["achieved_changed_slot_bytes"] = roof["achieved"]
+        roof["achieved"] = per_launch / (row["avg_ms"] * 1e-3) / 1e9
+        roof["frac"] = roof["achieved"] / roof["peak"]
+        roof["bytes_per_launch"] = per_launch
+        roof["unit_basis"] = "SURVEY 8(d) bytes per node-eval x node-evals decided per launch (batch pods x nodes)"
+    return roof

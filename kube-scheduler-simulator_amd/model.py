@@ -201,10 +201,25 @@ class Pod:
                     or self.pod_anti_affinity_required or self.pod_anti_affinity_preferred)
 
     def host_ports(self):
+        """schedutil.GetHostPorts [upstream v1.32 pkg/scheduler/util, TO
+        VERIFY: DESIGN.md §9]: the ports with a hostPort of the init
+        containers that keep running (restartPolicy Always, sidecars), then of
+        the regular containers, as (hostIP, protocol, hostPort) unsanitised."""
         out = []
+        for c in self.init_containers:
+            if c.restartable:
+                out.extend(x for x in c.host_ports if x[2] > 0)
         for c in self.containers:
-            out.extend(c.host_ports)
+            out.extend(x for x in c.host_ports if x[2] > 0)
         return out
+
+
+DEFAULT_BIND_ALL_HOST_IP = "0.0.0.0"
+
+
+def sanitize_host_port(ip: str, protocol: str):
+    """framework.HostPortInfo.sanitize: "" -> 0.0.0.0 / TCP."""
+    return (ip or DEFAULT_BIND_ALL_HOST_IP), (protocol or "TCP")
 
 
 @dataclass

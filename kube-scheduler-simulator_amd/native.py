@@ -32,7 +32,8 @@ class KsgNodes(C.Structure):
                 ("nonzero", i64p), ("allowed_pods", i32p), ("pod_count", i32p), ("unschedulable", u8p),
                 ("n_label_cols", C.c_int32), ("label_val", u32p), ("label_num", i64p), ("label_num_ok", u8p),
                 ("max_taints", C.c_int32), ("taints", u32p), ("n_taint_vocab", C.c_int32), ("taint_effect", u8p),
-                ("max_images", C.c_int32), ("images", u32p), ("n_images", C.c_int32)]
+                ("max_images", C.c_int32), ("images", u32p), ("n_images", C.c_int32),
+                ("n_port_vocab", C.c_int32)]
 
 
 class KsgTopology(C.Structure):
@@ -119,7 +120,7 @@ class Marshalled:
             n_taint_vocab=len(ec.taint_vocab),
             taint_effect=_ptr(keep("taint_effect", a["taint_effect"], np.uint8), u8p),
             max_images=ec.max_images, images=_ptr(keep("images", a["images"], np.uint32), u32p),
-            n_images=ec.n_images)
+            n_images=ec.n_images, n_port_vocab=getattr(ec, "n_port_vocab", 0))
         self.topo = KsgTopology(
             n_selectors=ec.n_selectors, n_templates=ec.n_templates,
             tmpl_col=_ptr(keep("tmpl_col", a["tmpl_col"], np.int32), i32p),
@@ -149,7 +150,7 @@ def make_profile(fields: dict) -> KsgProfile:
     return p
 
 
-RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL = 1, 2, 4   # ksg_last_run_info flags
+RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL, RUN_WAVE = 1, 2, 4, 8   # ksg_last_run_info flags
 
 
 class CaptureBuffers:

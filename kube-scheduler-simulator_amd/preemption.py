@@ -142,6 +142,9 @@ def check_scope(prof: P.Profile, pod: m.Pod, pods: Sequence[m.Pod]) -> None:
     """Refuse preemption the dry run cannot decide exactly: it re-runs the
     filters that read the node's pods (Fit, PodTopologySpread,
     InterPodAffinity), so every node-static filter must come before them."""
+    if pod.host_ports() and P.NODE_PORTS in prof.filter_order():
+        # the device dry run re-runs Fit / PTS / IPA only (ksg_preempt)
+        raise NotImplementedError("DefaultPreemption for a preemptor with host ports (NodePorts)")
     order = prof.filter_order()
     first = min((order.index(p) for p in _POD_DEPENDENT if p in order), default=None)
     if first is not None:

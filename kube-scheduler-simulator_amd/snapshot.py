@@ -76,9 +76,13 @@ class SpreadView(C.Structure):
                 ("n_match_label_keys", i32), ("match_label_keys", C.POINTER(cp))]
 
 
+class HostPortView(C.Structure):
+    _fields_ = [("host_ip", cp), ("protocol", cp), ("host_port", i32), ("pad", i32)]
+
+
 class ContainerView(C.Structure):
     _fields_ = [("image", cp), ("n_requests", i32), ("requests", C.POINTER(Quantity)), ("restartable", i32),
-                ("n_host_ports", i32)]
+                ("n_host_ports", i32), ("host_ports", C.POINTER(HostPortView))]
 
 
 class ImageView(C.Structure):
@@ -195,7 +199,9 @@ class _Keep:
         out = []
         for c in cs:
             n, rq = self.res(c.requests)
-            out.append(ContainerView(_b(c.image), n, rq, 1 if c.restartable else 0, len(c.host_ports)))
+            nh, hp = self.arr(HostPortView, [HostPortView(_b(ip), _b(proto), int(port), 0)
+                                             for ip, proto, port in c.host_ports])
+            out.append(ContainerView(_b(c.image), n, rq, 1 if c.restartable else 0, nh, hp))
         return self.arr(ContainerView, out)
 
 
@@ -411,6 +417,7 @@ class Snapshot:
         out["profile"] = {f: (list(getattr(pf, f)) if isinstance(getattr(pf, f), C.Array) else getattr(pf, f))
                           for f, _ in native.KsgProfile._fields_}
         out["meta"] = {"n_label_cols": nd.n_label_cols, "n_taint_vocab": nd.n_taint_vocab, "n_images": nd.n_images,
+                       "n_port_vocab": nd.n_port_vocab,
                        "n_selectors": tp.n_selectors, "n_templates": tp.n_templates, "n_res": R}
         return out
 

@@ -42,6 +42,7 @@
 #include <map>
 #include <string>
 #include <unordered_map>
+#include <set>
 #include <vector>
 
 #include <omp.h>
@@ -83,6 +84,9 @@ struct Ctx {
   std::vector<int32_t> prog;
   // per-node pod lists (NodeInfo.Pods)
   std::vector<std::vector<int32_t>> pods_on;
+  // NodeInfo.UsedPorts per node: host-port vocabulary ids (a set, as
+  // HostPortInfo is: a pod's removal drops its entries whoever else uses them)
+  std::vector<std::set<int32_t>> used_ports;
 };
 
 inline uint32_t lv(const Ctx& c, int col, int n) { return c.label_val[(size_t)col * c.N + n]; }
@@ -627,6 +631,12 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
           case KSG_PL_NODE_AFFINITY:
             if (!na_required_match(c, p, n)) { fail = true; reason = 1; }
             break;
+          case KSG_PL_NODE_PORTS:   // nodeports.fitsPorts over the conflict ids (encoder.py ports grammar)
+            if (p.ports >= 0) {
+              const int32_t* w = c.prog.data() + p.ports;
+              for (int i = 0; i < w[0] && !fail; i++) fail = c.used_ports[n].count(w[1 + i]) != 0;
+            }
+            break;
           case KSG_PL_NODE_RESOURCES_FIT: {
             uint32_t b = fit_filter(c, p, n);
             if (b) { fail = true; reason = b; }
@@ -643,7 +653,7 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
             break;
           }
           default:
-            break;  // NodePorts / volume plugins: pass (Skip for encodable pods)
+            break;  // volume plugins: pass (Skip for volume-less pods)
         }
         if (fail) st = (uint32_t)(pl + 1) | (reason << 8);
       }
@@ -770,6 +780,10 @@ void commit(Ctx& c, int pi, int n) {
   c.nonzero[(size_t)c.N + n] += p.nz_mem;
   c.pod_count[n] += 1;
   c.pods_on[n].push_back(pi);
+  if (p.ports >= 0) {   // UsedPorts.Add of the pod's own ids
+    const int32_t* own = c.prog.data() + p.ports + 1 + c.prog[p.ports];
+    for (int i = 0; i < own[0]; i++) c.used_ports[n].insert(own[1 + i]);
+  }
 }
 
 // NodeInfo.RemovePod for a preemption victim (the inverse of commit).
@@ -781,6 +795,10 @@ void uncommit(Ctx& c, int pi, int n) {
   c.pod_count[n] -= 1;
   auto& v = c.pods_on[n];
   v.erase(std::find(v.begin(), v.end(), pi));
+  if (p.ports >= 0) {   // UsedPorts.Remove
+    const int32_t* own = c.prog.data() + p.ports + 1 + c.prog[p.ports];
+    for (int i = 0; i < own[0]; i++) c.used_ports[n].erase(own[1 + i]);
+  }
 }
 
 // defaultpreemption.SelectVictimsOnNode (upstream v1.32): on the node, remove
@@ -877,6 +895,7 @@ int kso_load_nodes(kso_ctx* c, const ksg_nodes* nd, const ksg_topology* tp) {
   cp(c->log_table, tp->log_table, tp->log_n);
   c->requested0 = c->requested; c->nonzero0 = c->nonzero; c->pod_count0 = c->pod_count;
   c->pods_on.assign(N, {});
+  c->used_ports.assign(N, {});
   c->have_nodes = true;
   return KSG_OK;
 }
@@ -902,7 +921,8 @@ int kso_eval_pod(kso_ctx* c, const ksg_pod* pod, const int32_t* prog, int64_t pr
   if (!c || !pod || !res || !c->have_nodes || !c->have_wl || !c->have_prof) return KSG_E_STATE;
   const int64_t base = (int64_t)c->prog.size();
   ksg_pod p = *pod;
-  for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob})
+  for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob,
+                     &p.ports})
     if (*f >= 0) *f = (int32_t)(*f + base);
   c->prog.insert(c->prog.end(), prog, prog + prog_len);
   c->pods.push_back(p);
@@ -915,6 +935,7 @@ int kso_eval_pod(kso_ctx* c, const ksg_pod* pod, const int32_t* prog, int64_t pr
 int kso_reset_state(kso_ctx* c) {
   c->requested = c->requested0; c->nonzero = c->nonzero0; c->pod_count = c->pod_count0;
   c->pods_on.assign(c->N, {});
+  c->used_ports.assign(c->N, {});
   return KSG_OK;
 }
 

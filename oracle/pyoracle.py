@@ -161,6 +161,7 @@ class NodeInfo:
         self.nz_cpu = 0
         self.nz_mem = 0
         self.image_states = {}  # normalized name -> (size, num_nodes)
+        self.used = {}          # NodeInfo.UsedPorts: HostPortInfo ip -> {(protocol, port)}
 
     def add_pod(self, pod: m.Pod):
         """NodeInfo.AddPod / update(sign=+1) [upstream framework/types.go]."""
@@ -172,6 +173,9 @@ class NodeInfo:
         self.nz_cpu += nz.get(m.CPU, 0)
         self.nz_mem += nz.get(m.MEMORY, 0)
         self.pods.append(pod)
+        for ip, proto, port in pod.host_ports():   # NodeInfo.updateUsedPorts: UsedPorts.Add
+            ip, proto = m.sanitize_host_port(ip, proto)
+            self.used.setdefault(ip, set()).add((proto, port))
 
     def remove_pod(self, pod: m.Pod):
         """NodeInfo.RemovePod (update with sign -1)."""
@@ -183,6 +187,13 @@ class NodeInfo:
         self.nz_cpu -= nz.get(m.CPU, 0)
         self.nz_mem -= nz.get(m.MEMORY, 0)
         self.pods = [p for p in self.pods if p is not pod]
+        for ip, proto, port in pod.host_ports():   # UsedPorts.Remove: the entry goes, whoever else uses it
+            ip, proto = m.sanitize_host_port(ip, proto)
+            s = self.used.get(ip)
+            if s is not None:
+                s.discard((proto, port))
+                if not s:
+                    del self.used[ip]
 
     def snapshot(self) -> "NodeInfo":
         """NodeInfo.Snapshot: an independent copy."""
@@ -191,13 +202,18 @@ class NodeInfo:
         c.nz_cpu, c.nz_mem = self.nz_cpu, self.nz_mem
         c.image_states = self.image_states
         c.pods = list(self.pods)
+        c.used = {ip: set(v) for ip, v in self.used.items()}
         return c
 
-    def used_ports(self):
-        out = []
-        for p in self.pods:
-            out.extend(p.host_ports())
-        return out
+    def port_conflict(self, ip: str, proto: str, port: int) -> bool:
+        """HostPortInfo.CheckConflict: 0.0.0.0 conflicts with the (protocol,
+        port) pair on any IP; another IP with itself and 0.0.0.0."""
+        if port <= 0:
+            return False
+        ip, proto = m.sanitize_host_port(ip, proto)
+        if ip == m.DEFAULT_BIND_ALL_HOST_IP:
+            return any((proto, port) in v for v in self.used.values())
+        return any((proto, port) in self.used.get(k, ()) for k in (m.DEFAULT_BIND_ALL_HOST_IP, ip))
 
 
 def build_snapshot(nodes: List[m.Node], bound):
@@ -767,12 +783,9 @@ def run_filters(pod, ni, prof, states, skip, total_nodes):
         elif pid == P.NODE_AFFINITY:
             if not required_node_affinity_match(pod, node):
                 msg = "node(s) didn't match Pod's node affinity/selector"
-        elif pid == P.NODE_PORTS:
-            used = ni.used_ports()
-            for (ip, proto, port) in pod.host_ports():
-                for (uip, uproto, uport) in used:
-                    if uport == port and uproto == proto and (uip == ip or uip == "0.0.0.0" or ip == "0.0.0.0"):
-                        msg = "node(s) didn't have free ports for the requested pod ports"
+        elif pid == P.NODE_PORTS:   # nodeports.fitsPorts
+            if any(ni.port_conflict(ip, proto, port) for ip, proto, port in pod.host_ports()):
+                msg = "node(s) didn't have free ports for the requested pod ports"
         elif pid == P.NODE_RESOURCES_FIT:
             r = fits_request(pod, ni, prof)
             if r:

@@ -17,13 +17,11 @@ G = importlib.import_module("kube-scheduler-simulator_amd.generator")
 E = importlib.import_module("kube-scheduler-simulator_amd.encoder")
 native = importlib.import_module("kube-scheduler-simulator_amd.native")
 
-MODES = [("pipe", {"KSG_BATCH_MODE": "pipe"}), ("pipe-nowindow", {"KSG_BATCH_MODE": "pipe", "KSG_PIPE_WINDOW": "0"}),
-         ("pipe-nowindow-64", {"KSG_BATCH_MODE": "pipe", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"}),
-         ("pipe-64", {"KSG_BATCH_MODE": "pipe", "KSG_SLOT_BLOCK": "64"}), ("slot", {"KSG_BATCH_MODE": "slot"}),
-         ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
-         ("slot-256", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "256"}),
-         ("window", {"KSG_BATCH_MODE": "window"}), ("window-64", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "64"}),
-         ("tcol", {"KSG_BATCH_MODE": "tcol"}), ("tcol-nowindow", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0"}),
+MODES = [("window", {"KSG_BATCH_MODE": "window"}),
+         ("window-2wave", {"KSG_BATCH_MODE": "window", "KSG_WAVE_WALK": "0"}),
+         ("window-128", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "128"}),
+         ("slot", {"KSG_BATCH_MODE": "slot"}), ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
+         ("tcol", {"KSG_BATCH_MODE": "tcol"}),
          ("tcol-nowindow-64", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"})]
 
 
@@ -36,7 +34,7 @@ def main():
     nodes, pods, prof = G.config2(n_nodes=a.nodes, n_pods=a.pods)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
-    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK")
+    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK", "KSG_WAVE_WALK")
     want = set(a.modes.split(","))
     ref = None
     for name, env in MODES:

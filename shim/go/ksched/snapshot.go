@@ -178,11 +178,16 @@ func (a *arena) containers(cs []v1.Container, init bool) (C.int32_t, *C.ksg_cont
 		if init && c.RestartPolicy != nil && *c.RestartPolicy == v1.ContainerRestartPolicyAlways {
 			arr[i].restartable = 1
 		}
+		hp := unsafe.Slice((*C.ksg_host_port_view)(a.alloc(len(c.Ports), C.sizeof_ksg_host_port_view)), len(c.Ports)+1)
+		n := 0
 		for _, p := range c.Ports {
-			if p.HostPort > 0 {
-				arr[i].n_host_ports++
+			if p.HostPort > 0 { // schedutil.GetHostPorts; "" ip / protocol sanitised natively
+				hp[n].host_ip, hp[n].protocol = a.str(p.HostIP), a.str(string(p.Protocol))
+				hp[n].host_port = C.int32_t(p.HostPort)
+				n++
 			}
 		}
+		arr[i].n_host_ports, arr[i].host_ports = C.int32_t(n), &hp[0]
 	}
 	return C.int32_t(len(cs)), &arr[0]
 }

@@ -71,7 +71,7 @@ def test_snapshot_view_layouts(tmp_path):
              "ksg_toleration_view": S.TolerationView, "ksg_requirement_view": S.RequirementView,
              "ksg_node_selector_term_view": S.NodeSelectorTermView, "ksg_preferred_term_view": S.PreferredTermView,
              "ksg_label_selector_view": S.LabelSelectorView, "ksg_affinity_term_view": S.AffinityTermView,
-             "ksg_spread_view": S.SpreadView, "ksg_container_view": S.ContainerView, "ksg_image_view": S.ImageView,
+             "ksg_spread_view": S.SpreadView, "ksg_host_port_view": S.HostPortView, "ksg_container_view": S.ContainerView, "ksg_image_view": S.ImageView,
              "ksg_node_view": S.NodeView, "ksg_pod_view": S.PodView, "ksg_plugin_view": S.PluginView,
              "ksg_plugin_set_view": S.PluginSetView, "ksg_profile_view": S.ProfileView,
              "ksg_profile_info": S.ProfileInfo}

@@ -58,6 +58,7 @@ def _assert_same(nodes, pods, prof, bound=()):
     assert meta["n_label_cols"] == len(enc.cluster.label_cols)
     assert meta["n_taint_vocab"] == len(enc.cluster.taint_vocab)
     assert meta["n_images"] == enc.cluster.n_images
+    assert meta["n_port_vocab"] == len(enc.port_vocab)
     assert meta["n_selectors"] == enc.cluster.n_selectors
     assert meta["n_templates"] == enc.cluster.n_templates
     pf = E.encode_profile(prof, enc.cluster.res_names)
@@ -110,12 +111,23 @@ def test_profiles_and_args(built):
 
 
 def test_unsupported_inputs_refused(built):
+    """A pod the encoder cannot model is refused when it is added, and the
+    snapshot stays usable: later pods encode and sync as before (ADVICE r2:
+    one unsupported pod must not break every later cycle)."""
+    import copy
     nodes, pods, prof = zoo.zoo(1)
     pods = list(pods)
-    pods[3].containers[0].host_ports = (("", "TCP", 8080),)
-    snap = S.Snapshot(prof, nodes, pods)
-    with pytest.raises(S.SnapshotError, match="hostPorts"):
-        snap.encode()
+    bad = copy.deepcopy(pods[3])
+    bad.containers[0].requests = {f"example.com/r{k}": 1 for k in range(12)}
+    snap = S.Snapshot(prof, nodes, pods[:3])
+    with pytest.raises(S.SnapshotError, match="resource columns"):
+        snap.add_pod(bad)
+    for p in pods[3:]:
+        snap.add_pod(p)
+    snap.encode()
+    want = S.Snapshot(prof, nodes, pods)
+    want.encode()
+    assert snap.arrays()["pods"].tobytes() == want.arrays()["pods"].tobytes()
     with pytest.raises(S.SnapshotError):
         S.Snapshot(P.Profile(plugins=[("NoSuchPlugin", 1)]))
 

@@ -4,7 +4,9 @@ nodeAffinityPolicy / nodeTaintsPolicy, matchLabelKeys, system-default
 spreading, InterPodAffinity required / preferred terms both ways, namespaces
 and namespace selectors, node selectors with Gt/Lt/NotIn/DoesNotExist,
 matchFields, nodes without labels, unschedulable nodes, NoExecute taints,
-nodeName, init containers and sidecars, scalar resources, images."""
+nodeName, init containers and sidecars, scalar resources, images; with
+`ports`, host ports (NodePorts: bind-all vs specific host IPs, protocols,
+sidecar ports) drawn from a separate stream so the other draws stay put."""
 import numpy as np
 
 from conftest import pkg
@@ -29,8 +31,13 @@ def _sel(rng, apps):
     return m.LabelSelector(match_expressions=(m.Requirement("app", m.NOT_IN, (f"a{int(rng.integers(apps))}",)),))
 
 
-def zoo(seed: int, n_nodes: int = 24, n_pods: int = 160, apps: int = 5, zones: int = 3):
+PORTS = [("", "TCP", 80), ("", "TCP", 443), ("127.0.0.1", "TCP", 8080), ("0.0.0.0", "TCP", 8080),
+         ("10.0.0.1", "", 8080), ("", "UDP", 53), ("", "TCP", 53), ("", "SCTP", 9000)]
+
+
+def zoo(seed: int, n_nodes: int = 24, n_pods: int = 160, apps: int = 5, zones: int = 3, ports: bool = False):
     rng = np.random.Generator(np.random.PCG64(seed))
+    prng = np.random.Generator(np.random.PCG64(seed + 7919))
     nodes = []
     for i in range(n_nodes):
         labels = {m.LABEL_HOSTNAME: f"n{i}", "rank": str(int(rng.integers(0, 20)))}
@@ -141,6 +148,13 @@ def zoo(seed: int, n_nodes: int = 24, n_pods: int = 160, apps: int = 5, zones: i
         if rng.random() < 0.2:
             p.pod_anti_affinity_preferred = [m.WeightedPodAffinityTerm(int(rng.integers(1, 100)), m.PodAffinityTerm(
                 m.LabelSelector(match_labels=(("app", app),)), str(rng.choice([m.LABEL_ZONE, m.LABEL_HOSTNAME]))))]
+        if ports and prng.random() < 0.3:
+            hp = tuple(PORTS[int(k)] for k in prng.choice(len(PORTS), size=int(prng.integers(1, 3)), replace=False))
+            if prng.random() < 0.2:
+                p.init_containers.append(m.Container(image="envoy", restartable=bool(prng.random() < 0.7),
+                                                     host_ports=hp))
+            else:
+                p.containers[0].host_ports = hp
         pods.append(p)
     prof = P.default_profile()
     if seed % 3 == 1:
