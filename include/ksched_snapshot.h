@@ -282,6 +282,16 @@ const char* ksg_snapshot_error(ksg_snapshot* s);
 
 int ksg_snapshot_add_node(ksg_snapshot* s, const ksg_node_view* node, int32_t* index);
 int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* pod, int32_t* index);
+/* Namespace `name` with its labels (v1.Namespace; the exported snapshot's
+ * namespaces).  Pod (anti-)affinity terms whose namespaceSelector has
+ * requirements resolve against the namespaces added so far, as the
+ * InterPodAffinity PreFilter's namespace lister would
+ * (mergeAffinityTermNamespacesIfNotEmpty): namespaces ∪ {matching names}.
+ * A pod with such a term is refused (KSG_E_UNSUPPORTED) until at least one
+ * namespace was added; adding or relabelling a namespace re-resolves every
+ * pod's terms (the next sync re-encodes when any changed).  Replaces the
+ * reference's namespace informer feed (snapshot.go namespaces). */
+int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labels, const ksg_str_pair* labels);
 /* Pod `pod` runs on `node` (NodeInfo.Pods): replayed as an assume at load. */
 int ksg_snapshot_bind(ksg_snapshot* s, int32_t pod, int32_t node);
 int ksg_snapshot_node_index(ksg_snapshot* s, const char* name, int32_t* index);

@@ -158,7 +158,15 @@ struct AffTerm {
   std::string key;
   std::vector<std::string> ns;
   Sel ns_sel;
+  // a namespaceSelector with requirements, as given: resolved into `ns`
+  // against the snapshot's namespaces (ns_given ∪ matching namespaces)
+  bool resolved = false;
+  std::vector<std::string> ns_given;
+  Sel ns_req;
 };
+// A namespace no pod can have: a resolved namespaceSelector that matched
+// nothing (ingest.py NO_NAMESPACE).
+const std::string kNoNamespace = std::string("\0none", 5);
 struct Spread {
   int32_t skew, min_domains;
   std::string key, when, nap, ntp;
@@ -392,8 +400,8 @@ struct Scope {
 };
 
 Scope term_scope(const AffTerm& t, const Pod& owner) {
-  if (t.ns_sel.set && !t.ns_sel.empty())
-    throw EncodeError{KSG_E_UNSUPPORTED, "namespaceSelector with requirements is not modelled"};
+  if (t.ns_sel.set && !t.ns_sel.empty())   // add_pod resolves these (resolve_namespaces)
+    throw EncodeError{KSG_E_UNSUPPORTED, "namespaceSelector with requirements needs the snapshot's namespaces"};
   Scope s;
   s.canon = canon_selector(t.sel);
   s.ns_all = t.ns_sel.set;
@@ -490,6 +498,10 @@ struct ksg_snapshot {
   // scalar resource names of the nodes, pods and profile so far (add_pod
   // refuses a pod that would push the resource columns past KSG_MAX_RES)
   std::set<std::string> scalars;
+  // namespaces and their labels (ksg_snapshot_add_namespace): namespaceSelector
+  // terms resolve against these
+  bool have_namespaces = false;
+  std::map<std::string, StrMap> namespaces;
 };
 
 namespace {
@@ -1776,6 +1788,61 @@ int ksg_snapshot_add_node(ksg_snapshot* s, const ksg_node_view* v, int32_t* inde
   return KSG_OK;
 }
 
+namespace {
+// framework.AffinityTerm matches Namespaces ∪ {ns : namespaceSelector matches
+// its labels} [upstream interpodaffinity mergeAffinityTermNamespacesIfNotEmpty,
+// v1.32]: the selector becomes the list of the snapshot's namespaces it
+// matches (ingest.py _affinity_term).  Returns whether `t.ns` changed.
+bool resolve_term(const ksg_snapshot* s, AffTerm& t) {
+  if (!t.resolved) {
+    if (!t.ns_sel.set || t.ns_sel.empty()) return false;
+    t.resolved = true;
+    t.ns_given = t.ns;
+    t.ns_req = t.ns_sel;
+    t.ns_sel = Sel{};
+  }
+  const Canon c = canon_selector(t.ns_req);
+  std::set<std::string> ns(t.ns_given.begin(), t.ns_given.end());
+  for (auto& kv : s->namespaces)
+    if (selector_matches(c, kv.second)) ns.insert(kv.first);
+  std::vector<std::string> out(ns.begin(), ns.end());
+  if (out.empty()) out = {kNoNamespace};
+  if (out == t.ns) return false;
+  t.ns = std::move(out);
+  return true;
+}
+
+bool resolve_namespaces(const ksg_snapshot* s, Pod& p) {
+  bool changed = false;
+  for (auto* v : {&p.aff_req, &p.aff_pref, &p.anti_req, &p.anti_pref})
+    for (auto& t : *v)
+      if (t.resolved || (t.ns_sel.set && !t.ns_sel.empty())) {
+        if (!s->have_namespaces)
+          throw EncodeError{KSG_E_UNSUPPORTED,
+                            "namespaceSelector with requirements needs the snapshot's namespaces "
+                            "(ksg_snapshot_add_namespace)"};
+        changed = resolve_term(s, t) || changed;
+      }
+  return changed;
+}
+}  // namespace
+
+int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labels, const ksg_str_pair* labels) {
+  if (!s || !name || n_labels < 0 || (n_labels > 0 && !labels)) return KSG_E_INVALID;
+  s->namespaces[S(name)] = copy_pairs(n_labels, labels);
+  s->have_namespaces = true;
+  // re-resolve the selectors already taken in; a change invalidates the
+  // encoding (next sync re-encodes in full)
+  bool changed = false;
+  try {
+    for (auto& p : s->pods) changed = resolve_namespaces(s, p) || changed;
+  } catch (const EncodeError& x) {
+    return fail(s, x.code, x.msg);
+  }
+  if (changed) s->encoded = false;
+  return KSG_OK;
+}
+
 int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index) {
   if (!s || !v || !v->name) return KSG_E_INVALID;
   Pod p;
@@ -1818,6 +1885,7 @@ int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index)
   p.terminating = v->terminating != 0;
   p.priority = v->priority;
   try {
+    resolve_namespaces(s, p);
     validate_pod(s, p);
   } catch (const EncodeError& x) {
     return fail(s, x.code, "pod " + p.ns + "/" + p.name + ": " + x.msg);

@@ -13,7 +13,7 @@ messages the Go shim returns from Filter / PreFilter.
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -287,7 +287,8 @@ class Snapshot:
     """ksg_snapshot: the native encoder over the cluster objects."""
 
     def __init__(self, prof: P.Profile, nodes: Sequence[m.Node] = (), pods: Sequence[m.Pod] = (),
-                 bound: Sequence[Tuple[int, int]] = (), lib_path: Optional[str] = None):
+                 bound: Sequence[Tuple[int, int]] = (), lib_path: Optional[str] = None,
+                 namespaces: Sequence[Tuple[str, Dict[str, str]]] = ()):
         import os
         path = lib_path or native.LIB_PATH
         if not os.path.exists(path):
@@ -300,6 +301,7 @@ class Snapshot:
         self._err = f("error", cp, vp)
         self._add_node = f("add_node", C.c_int, vp, C.POINTER(NodeView), C.POINTER(i32))
         self._add_pod = f("add_pod", C.c_int, vp, C.POINTER(PodView), C.POINTER(i32))
+        self._add_ns = f("add_namespace", C.c_int, vp, cp, i32, C.POINTER(StrPair))
         self._bind_ = f("bind", C.c_int, vp, i32, i32)
         self._encode = f("encode", C.c_int, vp)
         self._encode_inc = f("encode_incremental", C.c_int, vp, C.POINTER(i32))
@@ -323,6 +325,8 @@ class Snapshot:
             raise SnapshotError(f"ksg_snapshot_new rc={rc}")
         self.prof = prof
         self.n_pods = 0
+        for name, labels in namespaces:
+            self.add_namespace(name, labels)
         for n in nodes:
             self.add_node(n)
         for p in pods:
@@ -351,6 +355,11 @@ class Snapshot:
         idx = i32()
         self._check(self._add_node(self.h, C.byref(node_view(n, k)), C.byref(idx)), "add_node")
         return idx.value
+
+    def add_namespace(self, name: str, labels: Dict[str, str]) -> None:
+        k = _Keep()
+        n, arr = k.pairs(labels)
+        self._check(self._add_ns(self.h, _b(name), n, arr), "add_namespace")
 
     def add_pod(self, p: m.Pod) -> int:
         k = _Keep()

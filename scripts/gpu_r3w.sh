@@ -4,7 +4,7 @@ set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/$1
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_batch_variants.py tests/test_gpu_eval.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests/test_node_ports.py tests/test_gpu_eval.py tests/test_gpu_batch_variants.py tests/test_snapshot_c.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 echo "tests rc=$rc"; tail -3 $O/tests.log
 [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" $O/tests.log | head -30; exit 1; }
 timeout -k 10 300 python -u scripts/compare_modes.py --modes window,window-2wave,tcol > $O/modes.log 2>&1; rc=$?

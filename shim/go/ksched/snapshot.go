@@ -411,6 +411,15 @@ func (x *Snapshot) AddPod(p *v1.Pod, defaultSel labels.Selector) (int, error) {
 	return int(idx), err
 }
 
+// AddNamespace registers a namespace and its labels: namespaceSelector
+// terms resolve against the namespaces added so far (re-resolved on change).
+func (x *Snapshot) AddNamespace(ns *v1.Namespace) error {
+	var a arena
+	defer a.free()
+	n, l := a.pairs(ns.Labels)
+	return x.check(C.ksg_snapshot_add_namespace(x.s, a.str(ns.Name), n, l))
+}
+
 // Bind records a pod already running on a node (replayed at load).
 func (x *Snapshot) Bind(pod, node int) error {
 	return x.check(C.ksg_snapshot_bind(x.s, C.int32_t(pod), C.int32_t(node)))

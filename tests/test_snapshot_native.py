@@ -296,3 +296,69 @@ def test_per_point_refusals(built):
                                      tuple(d["name"] for d in v.get("disabled", []))) for k, v in cfg.items()})
         with pytest.raises(S.SnapshotError):
             S.Snapshot(prof)
+
+
+def _resolve(pods, ns_labels):
+    """ingest.py's namespaceSelector resolution applied to model pods."""
+    import copy
+    I = pkg("ingest")
+    out = []
+    for p in pods:
+        q = copy.deepcopy(p)
+        for attr in ("pod_affinity_required", "pod_anti_affinity_required"):
+            setattr(q, attr, [_resolve_term(t, ns_labels, I) for t in getattr(q, attr)])
+        for attr in ("pod_affinity_preferred", "pod_anti_affinity_preferred"):
+            setattr(q, attr, [m.WeightedPodAffinityTerm(w.weight, _resolve_term(w.term, ns_labels, I))
+                              for w in getattr(q, attr)])
+        out.append(q)
+    return out
+
+
+def _resolve_term(t, ns_labels, I):
+    sel = t.namespace_selector
+    if sel is None or sel.empty():
+        return t
+    hit = {n for n, lb in ns_labels.items() if I._selector_matches(sel, lb)}
+    ns = tuple(sorted(set(t.namespaces) | hit)) or (I.NO_NAMESPACE,)
+    return m.PodAffinityTerm(t.label_selector, t.topology_key, namespaces=ns, namespace_selector=None)
+
+
+def _ns_selector_pods():
+    nodes, pods, prof = zoo.zoo(4, n_pods=80)
+    pods = list(pods)
+    team = m.LabelSelector(match_labels=(("team", "y"),))
+    notx = m.LabelSelector(match_expressions=(m.Requirement("team", m.NOT_IN, ("x",)),))
+    app = m.LabelSelector(match_labels=(("app", "a1"),))
+    for k, p in enumerate(pods):
+        if k % 7 == 3:
+            p.pod_anti_affinity_required = [m.PodAffinityTerm(app, m.LABEL_HOSTNAME, namespace_selector=team)]
+        elif k % 7 == 5:
+            p.pod_affinity_preferred = [m.WeightedPodAffinityTerm(30, m.PodAffinityTerm(
+                app, m.LABEL_ZONE, namespaces=("default",), namespace_selector=notx))]
+    return nodes, pods, prof
+
+
+def test_namespace_selector_resolution(built):
+    """namespaceSelector with requirements: resolved natively against the
+    namespaces added (ksg_snapshot_add_namespace) exactly as ingest.py
+    resolves it; relabelling a namespace later re-resolves and re-encodes."""
+    nodes, pods, prof = _ns_selector_pods()
+    ns0 = {"default": {"team": "x"}, "other": {"team": "y"}}
+    with pytest.raises(S.SnapshotError, match="namespaces"):
+        S.Snapshot(prof, nodes, pods)
+    snap = S.Snapshot(prof, nodes, pods, namespaces=list(ns0.items()))
+    snap.encode()
+    enc = E.Encoder(nodes, _resolve(pods, ns0), prof)
+    got = snap.arrays()
+    assert got["pods"].tobytes() == enc.workload.pods.tobytes()
+    np.testing.assert_array_equal(got["prog"], enc.workload.prog)
+    # relabel: "default" now matches team=y too; "other" matches nothing for NotIn x? (it does: y)
+    ns1 = {"default": {"team": "y"}, "other": {"team": "x"}}
+    for name, lb in ns1.items():
+        snap.add_namespace(name, lb)
+    assert snap.encode_incremental() is False   # a full re-encode
+    enc1 = E.Encoder(nodes, _resolve(pods, ns1), prof)
+    got1 = snap.arrays()
+    assert got1["pods"].tobytes() == enc1.workload.pods.tobytes()
+    np.testing.assert_array_equal(got1["prog"], enc1.workload.prog)
+    assert not np.array_equal(got1["prog"], got["prog"]) or got1["pods"].tobytes() != got["pods"].tobytes()
