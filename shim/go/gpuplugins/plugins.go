@@ -49,6 +49,17 @@ type podState struct {
 	msgID []int32        // per node: index into msgs, -1 = passed / not evaluated
 	msgs  []string
 	pre   [ksched.NPlugins]preFilterResult
+	// nodes with nominated pods of priority >= the pod's: the node's Filter
+	// verdict with those pods assumed (RunFilterPluginsWithNominatedPods' first
+	// pass), and the nominated UIDs that identify that pass's NodeInfo
+	nom map[int]*nominatedVerdict
+}
+
+type nominatedVerdict struct {
+	word uint32
+	code int32
+	msg  string
+	uids map[types.UID]bool
 }
 
 type preFilterResult struct {
@@ -79,7 +90,15 @@ type Evaluator struct {
 	podIdx  map[types.UID]int // pod -> snapshot index
 	podRV   map[types.UID]string
 	podNode map[types.UID]int // pods bound / assumed on the device -> column
+	// snapshot pods no longer current (a pod re-encoded after an update, or
+	// deleted while pending): the snapshot only appends, so past a threshold
+	// the next sync rebuilds it from the NodeInfos (bound pods only)
+	stale int
 }
+
+// staleLimit: rebuild once this many superseded snapshot pods accumulated
+// (and they outnumber the live ones).
+const staleLimit = 4096
 
 // NewEvaluator opens device dev for profile 0.
 func NewEvaluator(dev int, prof *ksched.ProfileArgs, ds DefaultSelectorFunc) (*Evaluator, error) {
@@ -111,6 +130,7 @@ func (e *Evaluator) rebuild(infos []*framework.NodeInfo) error {
 	e.nodes = e.nodes[:0]
 	e.nodeRV, e.nodeGen = map[string]string{}, map[string]int64{}
 	e.podIdx, e.podRV, e.podNode = map[types.UID]int{}, map[types.UID]string{}, map[types.UID]int{}
+	e.stale = 0
 	for _, ni := range infos {
 		n := ni.Node()
 		if _, err := snap.AddNode(n); err != nil {
@@ -140,7 +160,8 @@ func (e *Evaluator) rebuild(infos []*framework.NodeInfo) error {
 // that appeared on / left a node since the last cycle (the previous cycle's
 // assume among them) are assumed / forgotten one by one.
 func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
-	same := e.snap != nil && len(infos) == len(e.nodes)
+	same := e.snap != nil && len(infos) == len(e.nodes) &&
+		!(e.stale > staleLimit && e.stale > len(e.podIdx))
 	for i := 0; same && i < len(infos); i++ {
 		n := infos[i].Node()
 		same = n.Name == e.nodes[i] && n.ResourceVersion == e.nodeRV[n.Name]
@@ -199,7 +220,8 @@ func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
 
 // evalPod runs the whole sweep for the pod once per cycle (the first of the
 // shim's plugins to be called pays) and stashes it in CycleState.
-func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*framework.NodeInfo) (*podState, error) {
+func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*framework.NodeInfo,
+	nom framework.PodNominator) (*podState, error) {
 	if d, err := cs.Read(stateKey); err == nil {
 		return d.(*podState), nil
 	}
@@ -211,6 +233,7 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 	idx, known := e.podIdx[pod.UID]
 	if known && e.podRV[pod.UID] != pod.ResourceVersion {
 		known = false // the pod object changed since it was encoded: encode it again
+		e.stale++
 	}
 	if !known {
 		var err error
@@ -244,15 +267,122 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 		}
 		st.pre[id] = preFilterResult{code: code, names: names}
 	}
+	if nom != nil {
+		if err := e.nominatedPass(st, pod, nom); err != nil {
+			return nil, err
+		}
+	}
 	cs.Write(stateKey, st)
 	return st, nil
 }
 
+// nominatedPass restates addGENominatedPods + RunFilterPluginsWithNominatedPods
+// [framework/runtime/framework.go, v1.32]: for each node holding nominated
+// pods of priority >= the pod's (other than the pod itself), evaluate once
+// more with only that node's nominated pods assumed on it (PreFilter state
+// and NodeInfo both see them, as AddPod extensions would), then forget them.
+// Filter answers the framework's first pass from this verdict and its second
+// pass from the plain evaluation.  Nominated nodes are few (preemptors
+// waiting for their victims to leave), so this costs an evaluation each.
+func (e *Evaluator) nominatedPass(st *podState, pod *v1.Pod, nom framework.PodNominator) error {
+	prio := podPriority(pod)
+	for col, name := range e.nodes {
+		var add []*v1.Pod
+		for _, pi := range nom.NominatedPodsForNode(name) {
+			if pi.Pod.UID != pod.UID && podPriority(pi.Pod) >= prio {
+				add = append(add, pi.Pod)
+			}
+		}
+		if len(add) == 0 {
+			continue
+		}
+		v := &nominatedVerdict{uids: map[types.UID]bool{}}
+		var assumed []int
+		forget := func() error {
+			for _, q := range assumed {
+				if err := e.snap.Forget(e.ctx, q, col); err != nil {
+					return err
+				}
+			}
+			return nil
+		}
+		for _, q := range add {
+			idx, known := e.podIdx[q.UID]
+			if !known || e.podRV[q.UID] != q.ResourceVersion {
+				if known {
+					e.stale++
+				}
+				var err error
+				if idx, err = e.snap.AddPod(q, e.selectorOf(q)); err != nil {
+					_ = forget()
+					return err
+				}
+				if _, err := e.snap.Sync(e.ctx); err != nil {
+					_ = forget()
+					return err
+				}
+				e.podIdx[q.UID], e.podRV[q.UID] = idx, q.ResourceVersion
+				if _, ok := e.podNode[q.UID]; !ok {
+					e.podNode[q.UID] = -1
+				}
+			}
+			if err := e.snap.Assume(e.ctx, idx, col); err != nil {
+				_ = forget()
+				return err
+			}
+			assumed = append(assumed, idx)
+			v.uids[q.UID] = true
+		}
+		ev, err := e.ctx.Eval(st.pod)
+		if ferr := forget(); err == nil {
+			err = ferr
+		}
+		if err != nil {
+			return err
+		}
+		v.word = ev.FStatus[col]
+		if v.word != 0 && v.word != fsNotEvaluated {
+			code, msg, err := e.snap.Status(st.pod, v.word, col)
+			if err != nil {
+				return err
+			}
+			v.code, v.msg = int32(code), msg
+		}
+		if st.nom == nil {
+			st.nom = map[int]*nominatedVerdict{}
+		}
+		st.nom[col] = v
+	}
+	return nil
+}
+
+// podPriority is corev1helpers.PodPriority.
+func podPriority(p *v1.Pod) int32 {
+	if p.Spec.Priority != nil {
+		return *p.Spec.Priority
+	}
+	return 0
+}
+
 // status answers one Filter call from the pod's decoded statuses (no lock).
-func (e *Evaluator) status(st *podState, id int, node string) *framework.Status {
+// ni is the NodeInfo the framework filters against: on a node with
+// nominated pods, the first pass's NodeInfo holds them and is answered from
+// the nominated verdict.
+func (e *Evaluator) status(st *podState, id int, ni *framework.NodeInfo) *framework.Status {
+	node := ni.Node().Name
 	col, ok := st.index[node]
 	if !ok {
 		return framework.AsStatus(fmt.Errorf("node %q not in the evaluated snapshot", node))
+	}
+	if v := st.nom[col]; v != nil {
+		for _, pi := range ni.Pods {
+			if v.uids[pi.Pod.UID] {
+				if v.word == 0 || v.word == fsNotEvaluated || int(v.word&0xff)-1 != id {
+					return nil
+				}
+				return framework.NewStatus(frameworkCode(int(v.code)), v.msg)
+			}
+		}
 	}
 	w := st.ev.FStatus[col]
 	if w == 0 || w == fsNotEvaluated || int(w&0xff)-1 != id {
@@ -320,7 +450,7 @@ func (b *base) run(cs *framework.CycleState, pod *v1.Pod) (*podState, *framework
 	if err != nil {
 		return nil, framework.AsStatus(err)
 	}
-	st, err := b.ev.evalPod(cs, pod, infos)
+	st, err := b.ev.evalPod(cs, pod, infos, b.h)
 	if err != nil {
 		return nil, framework.AsStatus(err)
 	}
@@ -350,7 +480,7 @@ func (b *base) filter(cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeI
 	if s != nil {
 		return s
 	}
-	return b.ev.status(st, b.id, ni.Node().Name)
+	return b.ev.status(st, b.id, ni)
 }
 
 func (b *base) preScore(cs *framework.CycleState, pod *v1.Pod) *framework.Status {
