@@ -4113,6 +4113,8 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
   c.V = nd->n_taint_vocab; c.W = std::max(1, (nd->n_taint_vocab + 31) / 32);
   if (nd->n_port_vocab < 0) return fail(ctx, KSG_E_INVALID, "bad host-port vocabulary size");
   c.PW = std::max(1, (nd->n_port_vocab + 31) / 32);
+  c.lab_stride = N;
+  c.lab_base = 0;
   int rc = 0;
 #define UP(field, src, cnt) if ((rc = upc(ctx, c.field, src, cnt))) return rc
   UP(alloc, nd->alloc, (size_t)R * N);

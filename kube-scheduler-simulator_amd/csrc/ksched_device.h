@@ -49,6 +49,10 @@ struct DevCluster {
   const double* log_table;
   int32_t log_n;
   int32_t PW;                      // NodePorts: words of a node's UsedPorts bitmap (host-port vocabulary / 32)
+  // label_val addressing: value of (col, n) at label_val[col * lab_stride + n -
+  // lab_base] (N / 0; ksg_topo_coop points a private copy at the lane nodes'
+  // labels staged in LDS)
+  int32_t lab_stride, lab_base;
 };
 
 // Mutable per-replica state.  Replica r's arrays start at base + r * stride.
@@ -166,7 +170,9 @@ __device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
 struct GNode {
   const DevCluster* c;
   int n;
-  __device__ __forceinline__ uint32_t label(int col) const { return c->label_val[(size_t)col * c->N + n]; }
+  __device__ __forceinline__ uint32_t label(int col) const {
+    return c->label_val[(size_t)col * c->lab_stride + (n - c->lab_base)];
+  }
   __device__ __forceinline__ bool num(int col, int64_t& x) const {
     const size_t k = (size_t)col * c->N + n;
     if (!c->label_num_ok[k]) return false;

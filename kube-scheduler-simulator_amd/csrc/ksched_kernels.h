@@ -296,7 +296,7 @@ __device__ __forceinline__ int32_t cnt_at(const int32_t* cnt, int N, int sel, in
   return sel < 0 ? 0 : cnt[(size_t)sel * N + n];
 }
 __device__ __forceinline__ uint32_t lab(const DevCluster& c, int col, int n) {
-  return c.label_val[(size_t)col * c.N + n];
+  return c.label_val[(size_t)col * c.lab_stride + (n - c.lab_base)];
 }
 __device__ __forceinline__ bool has_all(const DevCluster& c, const int32_t* cons, int ncons, int stride, int n) {
   for (int i = 0; i < ncons; i++)

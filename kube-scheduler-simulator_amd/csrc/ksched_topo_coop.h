@@ -52,6 +52,8 @@
 
 constexpr int kCoopBatch = 64;      // pods per launch (static records [kCoopBatch][N])
 constexpr int kCoopPHist = 512;     // partial-histogram words per workgroup slot
+constexpr int kCoopLabCols = 16;    // KN == 1: label columns of the lane's node staged in LDS
+constexpr int kCoopTmpl = 2048;     // term templates whose column / table offset are staged in LDS
 
 struct CoopPart {   // one workgroup's partial results of the current pod
   // phase 1
@@ -287,15 +289,39 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ int s_size[kMaxSoft];
   __shared__ long long s_tt[4];
   __shared__ uint8_t s_wkind[kCoopPHist];   // partial-slot word: 1 histogram count (add), 0 presence bits (or), 2 mark (skip)
+  // read-only node / template tables staged once per launch: every label,
+  // column and template lookup of the per-pod critical path is an LDS read
+  __shared__ uint32_t s_lab[kCoopLabCols * BLOCK];
+  __shared__ int32_t s_cv[kCoopLabCols];
+  __shared__ uint8_t s_cu[kCoopLabCols];
+  __shared__ int32_t s_tcol[kCoopTmpl], s_toff[kCoopTmpl];
+  __shared__ ksg_pod s_pods[kCoopBatch];   // the batch's pod records
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
-  const DevCluster& c = a.c;
-  const int N = c.N;
+  const DevCluster& cg = a.c;   // global tables (assume writes; other nodes' labels)
+  const int N = cg.N;
   const DevState& st = a.st;
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profile)[tid];
+  for (int i = tid; i < a.count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
+    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
+  const bool lab_lds = KN == 1 && cg.L <= kCoopLabCols;
+  const bool col_lds = cg.L <= kCoopLabCols;
+  const bool tmpl_lds = cg.n_tmpl <= kCoopTmpl;
+  if (lab_lds) {
+    const int n = wg * BLOCK + tid;
+    for (int col = 0; col < cg.L; col++) s_lab[col * BLOCK + tid] = n < N ? cg.label_val[(size_t)col * N + n] : 0u;
+  }
+  if (col_lds && tid < cg.L) { s_cv[tid] = cg.col_vocab[tid]; s_cu[tid] = cg.col_unique[tid]; }
+  if (tmpl_lds)
+    for (int i = tid; i < cg.n_tmpl; i += BLOCK) { s_tcol[i] = cg.tmpl_col[i]; s_toff[i] = cg.tmpl_off[i]; }
   __syncthreads();
+  DevCluster cl = cg;   // the evaluators' view: the staged copies where they fit
+  if (lab_lds) { cl.label_val = s_lab; cl.lab_stride = BLOCK; cl.lab_base = wg * BLOCK; }
+  if (col_lds) { cl.col_vocab = s_cv; cl.col_unique = s_cu; }
+  if (tmpl_lds) { cl.tmpl_col = s_tcol; cl.tmpl_off = s_toff; }
+  const DevCluster& c = cl;
   const ksg_profile& prof = s_prof;
   bool ipa_in_filter = false;
   for (int kf = 0; kf < prof.n_filter; kf++) ipa_in_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
@@ -374,13 +400,24 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     return x;
   };
 
+  constexpr int kCoopPrefetch = 4;   // program words per lane prefetched for the next pod
+  int32_t nb[kCoopPrefetch] = {0, 0, 0, 0};
+  int nb_len = 0;
   for (int kq = 0; kq < a.count; kq++) {
-    const int pi = a.first + kq;
     CoopAcc* acc = a.acc + (kq & 1);
     CoopAcc* nxt = a.acc + ((kq + 1) & 1);
     const uint64_t* srow = a.srec + (size_t)kq * N;
     __syncthreads();
-    stage_pod<BLOCK>(a.pods, a.prog, pi, &s_pod, s_blob);
+    if (tid < (int)(sizeof(ksg_pod) / 4))
+      reinterpret_cast<int32_t*>(&s_pod)[tid] = reinterpret_cast<const int32_t*>(&s_pods[kq])[tid];
+    if (kq == 0 || nb_len > kCoopPrefetch * BLOCK) {
+      const int boff = s_pods[kq].blob, blen = s_pods[kq].blob_len;
+      for (int i = tid; i < blen; i += BLOCK) s_blob[i] = a.prog[boff + i];
+    } else {   // prefetched during the previous pod's last barrier
+#pragma unroll
+      for (int u = 0; u < kCoopPrefetch; u++)
+        if (tid + u * BLOCK < nb_len) s_blob[tid + u * BLOCK] = nb[u];
+    }
     __syncthreads();
     const ksg_pod& p = s_pod;
     if (tid == 0) {
@@ -983,6 +1020,14 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       gst(&mine->best, b);
       gst(&mine->err, e);
     }
+    // the next pod's program words, loaded while this pod's last barrier waits
+    nb_len = kq + 1 < a.count ? s_pods[kq + 1].blob_len : 0;
+    if (nb_len <= kCoopPrefetch * BLOCK) {
+      const int boff = kq + 1 < a.count ? s_pods[kq + 1].blob : 0;
+#pragma unroll
+      for (int u = 0; u < kCoopPrefetch; u++)
+        nb[u] = tid + u * BLOCK < nb_len ? a.prog[boff + tid + u * BLOCK] : 0;
+    }
     KSG_CSTAMP(8);
     if (!coop_barrier(a.bar, a.timeout, G, target)) return;
     KSG_CSTAMP(9);
@@ -1015,7 +1060,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       else selected = key_node(b);
     }
     if (selected >= 0 && ((selected / BLOCK) % G) == wg && (selected % BLOCK) == tid)
-      coop_commit(c, st, p, p.commit >= 0 ? s_blob + (p.commit - p.blob) : nullptr, selected);
+      coop_commit(cg, st, p, p.commit >= 0 ? s_blob + (p.commit - p.blob) : nullptr, selected);
     if (wg == 0 && tid == 0) {
       uint32_t score_skip = p.score_skip;
       if (ipa_in_filter && s_t.ipa_skip_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
