@@ -246,8 +246,10 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
     pod) -> ksg_snapshot_assume.  configs[1]'s cluster, starting empty; the
     first `warm` pods fill the encoding universe (a pod that adds a label
     value forces a full re-encode, counted), then `n_pods` cycles are timed
-    call by call (pod views built beforehand; ctypes call overhead included).
-    The placements must equal one ksg_run_queue over the same pods."""
+    call by call in C (tests/c/cycle_driver.c: no Python in the loop; pod
+    views built beforehand).  The placements must equal one ksg_run_queue
+    over the same pods."""
+    import ctypes as C
     import numpy as np
     nodes, pods, prof = G.config2(n_nodes=n_nodes, n_pods=warm + n_pods)
     snap = S.Snapshot(prof, nodes)
@@ -261,28 +263,20 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
         k = S._Keep()
         views.append(S.pod_view(p, k))
         keep.append(k)
-    phases = np.zeros((n_pods, 5))
+    arr = (S.PodView * len(views))(*views)
+    drv = C.CDLL(os.path.join(ROOT, "tests", "c", "libcycle.so"))
+    i32p = C.POINTER(C.c_int32)
+    drv.cycle_run.restype = C.c_int
+    drv.cycle_run.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(S.PodView), C.c_int32, C.c_int32, C.c_void_p,
+                              C.c_int32, i32p, C.POINTER(C.c_int64), i32p, i32p, i32p]
     placed = np.full(warm + n_pods, -1, np.int32)
-    appended = reloads = 0
-    clock = time.perf_counter_ns
-    for i, v in enumerate(views):
-        t0 = clock()
-        idx = snap.add_pod_view(v)
-        t1 = clock()
-        ap = snap.sync(eng)
-        t2 = clock()
-        r = eng.eval(idx, cap)
-        t3 = clock()
-        snap.statuses(idx, cap.fstatus[0])
-        t4 = clock()
-        if r.selected >= 0:
-            snap.assume(eng, idx, r.selected)
-        t5 = clock()
-        placed[i] = r.selected
-        if i >= warm:
-            phases[i - warm] = (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4)
-            appended += ap
-            reloads += not ap
+    phases = np.zeros((n_pods, 5), np.int64)
+    ap, rl, where = C.c_int32(), C.c_int32(), C.c_int32(-1)
+    rc = drv.cycle_run(snap.h, eng.ctx, arr, len(views), warm, C.addressof(cap.struct), N,
+                       placed.ctypes.data_as(i32p), phases.ctypes.data_as(C.POINTER(C.c_int64)),
+                       C.byref(ap), C.byref(rl), C.byref(where))
+    if rc != 0:
+        raise RuntimeError(f"cycle driver: rc={rc} in phase {where.value}: {snap._err(snap.h).decode()}")
     # the same pods as one device-resident queue
     import importlib
     E = importlib.import_module(PKG + ".encoder")
@@ -294,11 +288,12 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
     per = us.sum(axis=1)
     names = ["add_pod", "sync", "eval_capture", "statuses", "assume"]
     return {"workload": f"configs[1] cluster ({N} nodes), per-cycle C-ABI path, {n_pods} cycles timed after {warm}",
+            "driver": "C (tests/c/cycle_driver.c), CLOCK_MONOTONIC per call",
             "us_per_cycle_mean": float(per.mean()), "us_per_cycle_p50": float(np.percentile(per, 50)),
             "us_per_cycle_p99": float(np.percentile(per, 99)), "pods_per_s": float(1e6 / per.mean()),
             "breakdown_us_mean": {k: float(us[:, j].mean()) for j, k in enumerate(names)},
             "breakdown_us_p50": {k: float(np.percentile(us[:, j], 50)) for j, k in enumerate(names)},
-            "appended": int(appended), "full_reloads": int(reloads),
+            "appended": int(ap.value), "full_reloads": int(rl.value),
             "placements_equal_run_queue": bool(np.array_equal(placed, want)),
             "eval_path": eng.last_run_info()[0]}
 

@@ -106,7 +106,7 @@ typedef struct ksg_nodes {
   int32_t n_taint_vocab;
   const uint8_t* taint_effect;   /* [n_taint_vocab] KSG_EFFECT_*                   */
   int32_t max_images;
-  const uint32_t* images;        /* [max_images][n_nodes] ascending image id + 1, 0 = end */
+  const uint32_t* images;        /* [max_images][n_nodes] strictly ascending image id + 1, 0 = end */
   int32_t n_images;              /* image vocabulary size                          */
   int32_t n_port_vocab;          /* host-port vocabulary size (NodePorts): every (hostIP,
                                     protocol, hostPort) a pod uses; each node's UsedPorts is
@@ -307,7 +307,6 @@ int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
 #define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
 #define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */
 #define KSG_RUN_TCOL 4           /* phase 2 was the transposed walk (ksg_batch_phase2t) */
-#define KSG_RUN_WAVE 8           /* phase 2 was the one-wave slot walk (ksg_batch_phase2w) */
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event
@@ -336,9 +335,7 @@ enum {
   KSG_K_BATCH_PHASE2T = 14,
   KSG_K_BATCH_TRANSPOSE = 15,
   KSG_K_TCOL_CARRY = 16,
-  KSG_K_EVAL_FUSED = 17,
-  KSG_K_BATCH_PHASE2W = 18,
-  KSG_NKERNELS = 19
+  KSG_NKERNELS = 17
 };
 typedef struct ksg_kernel_stat {
   char name[48];

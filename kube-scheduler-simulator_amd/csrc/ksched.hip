@@ -1794,11 +1794,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 #endif
 }
 
-#include "ksched_phase2w.h"
 #include "ksched_phase2t.h"
 #include "ksched_capture.h"
 #include "ksched_sweep.h"
-#include "ksched_eval.h"
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
 template <int BLOCK>
@@ -2388,8 +2386,6 @@ struct ksg_ctx {
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
-  bool wave_walk = true;      // env KSG_WAVE_WALK=0: the slot walk with one lane per slot (2 waves at 64-pod batches)
-  bool last_wave = false;     // the last batched run's phase 2 was the one-wave walk
   uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
   int32_t* d_statt = nullptr;
   uint64_t* d_prect[2] = {nullptr, nullptr};   // the same, per window parity
@@ -2424,8 +2420,6 @@ struct ksg_ctx {
   ksg_profile* d_ev_prof = nullptr;
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
-  bool ev_fused = true;                     // env KSG_EVAL_FUSED=0: two launches instead of the cooperative one
-  int ev_fused_max = 0;                     // co-resident workgroups of ksg_eval_fused (occupancy x CUs)
   unsigned ev_bar = 0;                      // the per-cycle grid barrier's arrival count so far
   // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
   char* h_stage = nullptr;
@@ -2524,8 +2518,7 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
                                           "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
                                           "ksg_capture_eval", "ksg_capture_norm", "ksg_batch_phase2t",
-                                          "ksg_batch_transpose", "ksg_tcol_carry", "ksg_eval_fused",
-                                          "ksg_batch_phase2w"};
+                                          "ksg_batch_transpose", "ksg_tcol_carry"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2802,14 +2795,6 @@ int decide_n32(ksg_ctx* ctx, int32_t first, int32_t count, bool* n32) {
 }
 
 // LDS budget attribute of the phase-2 instances (once per process)
-// ksg_batch_phase2w instances (the one-wave walk, <= 128 slots): RM 4, RM 4 N32, KSG_MAX_RES
-static const std::array<const void*, 3>& wave_kernels() {
-  static const std::array<const void*, 3> k = {(const void*)ksg_batch_phase2w<4, false>,
-                                               (const void*)ksg_batch_phase2w<4, true>,
-                                               (const void*)ksg_batch_phase2w<KSG_MAX_RES, false>};
-  return k;
-}
-
 int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
   static bool attr_set = false;
   if (attr_set) return KSG_OK;
@@ -2817,8 +2802,6 @@ int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
   HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)budget));
   for (const void* f : slot_kernels())
-    HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
-  for (const void* f : wave_kernels())
     HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
   attr_set = true;
   return KSG_OK;
@@ -2905,7 +2888,6 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     }
   }
   ctx->last_tcol = tcol;
-  ctx->last_wave = false;
   if (tcol && !ctx->d_rect) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rect, (size_t)128 * N))) return rc;
@@ -3026,11 +3008,11 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const bool window = ctx->pipe_window != 0;
   const bool overlap = window && !ctx->timing;
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
-  // mode 4: the slot walk inside this pipeline (one wave, two slots per lane,
-  // ksched_phase2w.h, when the slots fit; else one lane per slot); mode 5:
+  // mode 4: the slot walk inside this pipeline (one lane per slot); mode 5:
   // the transposed walk (ksched_phase2t.h) with the previous batch's nodes as
   // carried columns, 64-pod batches, else the slot walk.  (The round-2
-  // two-version walk, measured slower, was removed in round 3.)
+  // two-version walk and a round-3 one-wave walk with two slots per lane, both
+  // measured slower, were removed.)
   bool n32 = false;
   if ((ctx->batch_mode == 4 || ctx->batch_mode == 5) && (rc = decide_n32(ctx, first, count, &n32))) return rc;
   const bool tcolw = ctx->batch_mode == 5 && window && n32 && tcol_candidate(ctx);
@@ -3055,12 +3037,8 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const int B = tcolw ? 64 : window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
   const int slots = window ? 2 * B : B;   // carried + this batch's slots
   const int sblock = slots <= 64 ? 64 : slots <= 128 ? 128 : 256;
-  // the one-wave walk (ksched_phase2w.h) whenever the slots fit two per lane
-  const bool wave1 = slotwalk && ctx->wave_walk && slots <= 128;
-  ctx->last_wave = wave1;
-  const void* kern = wave1 ? wave_kernels()[n32 ? 1 : slot_rm == 4 ? 0 : 2]
-                          : slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)];
-  const int block = wave1 ? 64 : sblock;
+  const void* kern = slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)];
+  const int block = sblock;
   const size_t kLdsBudget = tcolw ? kTcolLds : 120 * 1024;
   const size_t slot_bytes = 8 * (size_t)(2 * slot_rm + 10);   // SlotLayout<RM>::STRIDE int64 words
   if (!tcolw && (rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
@@ -3154,7 +3132,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2T, 0.5 * nb * (nb + 1)))) return rc;
     } else {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(kern)), dim3(1), dim3(block), bytes, s2, b);
-      if ((rc = tlaunched(ctx, wave1 ? KSG_K_BATCH_PHASE2W : KSG_K_BATCH_PHASE2S, 0.5 * nb * (nb + 1)))) return rc;
+      if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2S, 0.5 * nb * (nb + 1)))) return rc;
     }
     if (overlap) HIPC(ctx, hipEventRecord(ctx->ev_p2[par], s2));
     prev_nb = nb;
@@ -3759,22 +3737,10 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   ctx->ev_clean = false;   // until the launch is in: it zeroes the other slot
   treset(ctx);
   if ((rc = tmark(ctx))) return rc;
-  if (ctx->ev_fused && G <= (unsigned)ctx->ev_fused_max) {
-    // one cooperative launch: the eval half, a grid barrier, the norm half
-    unsigned* bar = reinterpret_cast<unsigned*>(ctx->d_ev + o_bar);
-    unsigned* tmo = bar + 1;
-    unsigned target = ctx->ev_bar + G;
-    void* args[] = {&ca, &bar, &tmo, &target};
-    HIPC(ctx, hipLaunchCooperativeKernel((const void*)ksg_eval_fused, dim3(G), dim3(256), args, 0, ctx->stream));
-    ctx->ev_bar = target;
-    if ((rc = tlaunched(ctx, KSG_K_EVAL_FUSED, (double)N))) return rc;
-  } else {
-    ca.rec = reinterpret_cast<uint64_t*>(ctx->d_ev + o_rec);
-    hipLaunchKernelGGL(ksg_capture_eval, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
-    if ((rc = tlaunched(ctx, KSG_K_CAPTURE_EVAL, (double)N))) return rc;
-    hipLaunchKernelGGL(ksg_capture_norm, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
-    if ((rc = tlaunched(ctx, KSG_K_CAPTURE_NORM, (double)N))) return rc;
-  }
+  hipLaunchKernelGGL(ksg_capture_eval, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
+  if ((rc = tlaunched(ctx, KSG_K_CAPTURE_EVAL, (double)N))) return rc;
+  hipLaunchKernelGGL(ksg_capture_norm, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
+  if ((rc = tlaunched(ctx, KSG_K_CAPTURE_NORM, (double)N))) return rc;
   HIPC(ctx, hipGetLastError());
   ctx->ev_parity = 1 - par;
   ctx->ev_clean = true;
@@ -4047,14 +4013,6 @@ int ksg_open(int device, ksg_ctx** out) {
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
-  if (const char* f = getenv("KSG_WAVE_WALK")) ctx->wave_walk = atoi(f) != 0;
-  if (const char* f = getenv("KSG_EVAL_FUSED")) ctx->ev_fused = atoi(f) != 0;
-  {
-    int occ = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)ksg_eval_fused, 256, 0) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
-      ctx->ev_fused_max = occ * cus;
-  }
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);
     ctx->slot_block = v <= 64 ? 64 : v <= 128 ? 128 : KSG_BATCH_MAX;
@@ -4572,7 +4530,7 @@ int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
   if (!ctx || !path || !flags) return KSG_E_INVALID;
   *path = ctx->last_path;
   *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0) |
-           (ctx->last_tcol ? KSG_RUN_TCOL : 0) | (ctx->last_wave ? KSG_RUN_WAVE : 0);
+           (ctx->last_tcol ? KSG_RUN_TCOL : 0);
   return KSG_OK;
 }
 

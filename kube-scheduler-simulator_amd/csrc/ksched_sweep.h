@@ -133,10 +133,73 @@ __device__ __forceinline__ bool arrive_and_wait_sc1(unsigned* bar, unsigned* tim
 __host__ __device__ inline int static_tiles8(int N) { return ((N + 255) / 256 + 7) / 8 * 8; }
 __host__ __device__ inline int static_blocks(int N, int nb) { return static_tiles8(N) * nb; }
 
+// The node's taint slots in chunks of kStaticChunk independent loads (the
+// slot loops of untolerated_slot / taint_score end at the first empty slot and
+// chain every load behind the previous compare): TaintToleration's Filter
+// verdict (an untolerated NoSchedule / NoExecute taint) and its Score count
+// (untolerated PreferNoSchedule taints) in one pass; effects from LDS.
+constexpr int kStaticChunk = 8;
+constexpr int kStaticEff = 4096;   // taint vocabulary staged in LDS up to this size
+
+__device__ __forceinline__ void static_taints(const DevCluster& c, int n, const int32_t* tolf, const int32_t* tolp,
+                                              const uint8_t* eff, bool& reject, int64_t& score) {
+  reject = false;
+  score = 0;
+  for (int s0 = 0; s0 < c.T; s0 += kStaticChunk) {
+    uint32_t id[kStaticChunk];
+#pragma unroll
+    for (int k = 0; k < kStaticChunk; k++) id[k] = s0 + k < c.T ? c.taints[(size_t)(s0 + k) * c.N + n] : 0u;
+    bool end = false;
+#pragma unroll
+    for (int k = 0; k < kStaticChunk; k++) {
+      end |= id[k] == 0;
+      if (end) continue;
+      const uint32_t vid = id[k] - 1;
+      const uint8_t e = eff[vid];
+      if (e == KSG_EFFECT_NO_SCHEDULE || e == KSG_EFFECT_NO_EXECUTE) reject |= !tol_bit(tolf, vid);
+      else if (e == KSG_EFFECT_PREFER_NO_SCHEDULE) score += !tol_bit(tolp, vid);
+    }
+    if (end) break;
+  }
+}
+
+// ImageLocality's sum over the pod's image entries, the node's sorted image
+// ids read in chunks of independent loads (image_score's arithmetic after it).
+__device__ __forceinline__ int64_t static_images(const DevCluster& c, int n, const int32_t* P, int img,
+                                                 int n_containers) {
+  int64_t sum = 0;
+  if (img >= 0) {
+    const int32_t* w0 = P + img;
+    const int cnt = *w0++;
+    uint32_t top = 0;   // largest image id the pod asks for
+    for (int i = 0; i < cnt; i++) top = max(top, (uint32_t)w0[3 * i]);
+    for (int s0 = 0; cnt > 0 && s0 < c.I; s0 += kStaticChunk) {
+      uint32_t x[kStaticChunk];
+#pragma unroll
+      for (int k = 0; k < kStaticChunk; k++) x[k] = s0 + k < c.I ? c.images[(size_t)(s0 + k) * c.N + n] : 0u;
+      bool end = false;
+#pragma unroll
+      for (int k = 0; k < kStaticChunk; k++) {
+        end |= x[k] == 0 || x[k] > top;
+        if (end) continue;
+        for (int i = 0; i < cnt; i++)
+          if ((uint32_t)w0[3 * i] == x[k]) sum += ld64(w0 + 3 * i + 1);
+      }
+      if (end) break;
+    }
+  }
+  const int64_t mb = 1024 * 1024, minT = 23 * mb;
+  const int64_t mx = 1000 * mb * (int64_t)n_containers;
+  if (sum < minT) sum = minT;
+  else if (sum > mx) sum = mx;
+  return div_small(100 * (sum - minT), mx - minT);
+}
+
 __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
   __shared__ ksg_profile s_prof;
+  __shared__ uint8_t s_eff[kStaticEff];
   const int tid = threadIdx.x;
   const DevCluster& c = a.c;
   const int N = c.N;
@@ -146,6 +209,9 @@ __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   if (tile * 256 >= N) return;
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles)[tid];
+  const bool eff_lds = c.V <= kStaticEff;
+  if (eff_lds)
+    for (int i = tid; i < c.V; i += 256) s_eff[i] = c.taint_effect[i];
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();
   const ksg_pod& p = s_pod;
@@ -157,11 +223,14 @@ __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) bits |= kSrNotEval;
   if (nd.unsched() && !(p.flags & KSG_POD_TOL_UNSCHED)) bits |= kSrUnsched;
   if (p.node_name != -1 && p.node_name != n) bits |= kSrNodeName;
-  if (untolerated_slot(c, nd, v.tolf) >= 0) bits |= kSrTaint;
+  bool treject;
+  int64_t tscore;
+  static_taints(c, n, v.tolf, v.tolp, eff_lds ? s_eff : c.taint_effect, treject, tscore);
+  if (treject) bits |= kSrTaint;
   if (!na_required_match(nd, v.P, v.na_req)) bits |= kSrNodeAff;
-  const uint64_t rt = (uint64_t)taint_score(c, nd, v.tolp);
+  const uint64_t rt = (uint64_t)tscore;
   const uint64_t ra = v.na_pref >= 0 ? (uint64_t)na_pref_score(nd, v.P, v.na_pref) : 0;
-  const uint64_t im = (uint64_t)image_score(c, nd, v.P, v.img, p.n_containers);
+  const uint64_t im = (uint64_t)static_images(c, n, v.P, v.img, p.n_containers);
   a.srec[(size_t)j * N + n] = bits | ((rt & 0xff) << 8) | ((ra & 0xffff) << 16) | ((im & 0xff) << 32);
 }
 

@@ -18,7 +18,6 @@ E = importlib.import_module("kube-scheduler-simulator_amd.encoder")
 native = importlib.import_module("kube-scheduler-simulator_amd.native")
 
 MODES = [("window", {"KSG_BATCH_MODE": "window"}),
-         ("window-2wave", {"KSG_BATCH_MODE": "window", "KSG_WAVE_WALK": "0"}),
          ("window-128", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "128"}),
          ("slot", {"KSG_BATCH_MODE": "slot"}), ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
          ("tcol", {"KSG_BATCH_MODE": "tcol"}),
@@ -34,7 +33,7 @@ def main():
     nodes, pods, prof = G.config2(n_nodes=a.nodes, n_pods=a.pods)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
-    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK", "KSG_WAVE_WALK")
+    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK")
     want = set(a.modes.split(","))
     ref = None
     for name, env in MODES:

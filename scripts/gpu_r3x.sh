@@ -11,7 +11,7 @@ echo "tests rc=$rc"; tail -3 $O/tests.log
 timeout -k 10 300 python -u scripts/bench_configs.py --config 3 --pods 5000 --no-cpu-baseline > $O/config3.json 2> $O/config3.err; rc=$?
 echo "config3 rc=$rc"; tail -c 1500 $O/config3.json; echo
 [ $rc -eq 0 ] || exit 1
-timeout -k 10 300 python -u scripts/compare_modes.py --modes window,window-2wave,tcol > $O/modes.log 2>&1; rc=$?
+timeout -k 10 300 python -u scripts/compare_modes.py --modes window,tcol > $O/modes.log 2>&1; rc=$?
 echo "modes rc=$rc"; tail -12 $O/modes.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 600 python -u bench.py --steps 3 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0 --no-cpu-baseline > $O/bench.json 2> $O/bench.err; rc=$?

@@ -3,10 +3,9 @@
 "tcol" (the transposed walk, ksched_phase2t.h: in the two-stream
 pipeline with the previous batch's nodes as carried columns, serialised with
 timing on, and without the window at 128- and 64-pod batches; the slot walk
-where its scope check fails), "window" (the default: the one-wave slot walk inside the two-stream pipeline
-with the two-batch window; also the two-wave form, without the window, at
-128-pod batches and with per-kernel timing on, which runs the same arithmetic
-without overlap), and (opt-in) "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
+where its scope check fails), "window" (the default: the slot walk inside the two-stream pipeline with
+the two-batch window; also without the window, at 128-pod batches and with
+per-kernel timing on, which runs the same arithmetic without overlap), and (opt-in) "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
 state bit-exact against the C++ oracle, including split calls."""
 import numpy as np
 import pytest
@@ -28,14 +27,13 @@ def _have_gpu():
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
 
-# (mode, extra env).  "window" is the default (the one-wave walk at 64-pod
-# batches); "window-2wave" the one-lane-per-slot walk in the same pipeline.
+# (mode, extra env).  "window" is the default (the slot walk, one lane per
+# slot, at 64-pod batches).
 # "topset" and "scan" (the round-1 forms, 7.5 and 13 us per pod) and the
 # extra slot block sizes run only with KSG_TEST_ALL_VARIANTS=1: they are not
 # on any default path and cost GPU minutes.
 import os
 MODES = {"window": ("window", {}), "window-timed": ("window", {"_timing": 1}),
-         "window-2wave": ("window", {"KSG_WAVE_WALK": 0}),
          "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "window128": ("window", {"KSG_SLOT_BLOCK": 128}),
          "slot": ("slot", {}),
          "tcol": ("tcol", {}), "tcol-nowindow64": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 64})}
@@ -127,7 +125,7 @@ def test_slot32_refused_on_sub_mib_memory(oracle):
     oracle.load(enc, pf)
     pl, _ = a.run_queue(0, len(pods))
     path, flags = a.last_run_info()
-    assert path == 2 and not flags & (native.RUN_TCOL | native.RUN_SLOT32)   # int64 walk (wave or slot)
+    assert path == 2 and not flags & (native.RUN_TCOL | native.RUN_SLOT32)   # the int64 slot walk
     np.testing.assert_array_equal(pl, oracle.run_queue(0, len(pods))[0])
 
 
@@ -168,5 +166,5 @@ def test_tcol_out_of_scope_falls_back(oracle):
     oracle.load(enc, pf)
     pl, _ = a.run_queue(0, len(pods))
     path, flags = a.last_run_info()
-    assert path == 2 and not flags & (native.RUN_TCOL | native.RUN_SLOT32)   # int64 walk (wave or slot)
+    assert path == 2 and not flags & (native.RUN_TCOL | native.RUN_SLOT32)   # the int64 slot walk
     np.testing.assert_array_equal(pl, oracle.run_queue(0, len(pods))[0])
