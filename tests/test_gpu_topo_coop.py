@@ -43,29 +43,44 @@ def oracle():
 CASES = [
     ("c3-4000x1200", lambda: G.config3(n_nodes=4000, n_pods=1200, apps=60, zones=8)),
     ("c3-15000x300", lambda: G.config3(n_nodes=15000, n_pods=300)),
+    # configs[2]'s full cluster with a queue long enough for domains to fill
+    # (every zone holds pods of the big apps, hostname spreads bind)
+    ("c3-15000x3000", lambda: G.config3(n_nodes=15000, n_pods=3000)),
     ("c1-2000x800", lambda: G.config1(n_nodes=2000, n_pods=800)),
 ] + [(f"zoo-big-{s}", (lambda s=s: __import__("zoo").zoo(s, n_nodes=700, n_pods=400, apps=7, zones=5)))
      for s in range(4)]
 
 
+_ORACLE = {}   # case -> (workload, oracle placements, results, final state): both hand-offs compare to one run
+
+
+def _case(oracle, name, make):
+    if name not in _ORACLE:
+        nodes, pods, prof = make()
+        enc = E.Encoder(nodes, pods, prof)
+        pf = E.encode_profile(prof, enc.cluster.res_names)
+        oracle.load(enc, pf)
+        po, ro = oracle.run_queue(0, len(pods))
+        R = len(enc.cluster.res_names)
+        ro = {f: np.array(ro[f]) for f in ("n_feasible", "status", "score_skip")}
+        _ORACLE[name] = (enc, pf, len(pods), np.array(po), ro, [np.array(x) for x in oracle.read_state(R)])
+    return _ORACLE[name]
+
+
 @pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
 def test_topo_coop_matches_oracle(gpu, oracle, name, make):
-    nodes, pods, prof = make()
-    enc = E.Encoder(nodes, pods, prof)
-    pf = E.encode_profile(prof, enc.cluster.res_names)
+    enc, pf, P, po, ro, ostate = _case(oracle, name, make)
     gpu.load(enc, pf)
-    oracle.load(enc, pf)
-    pg, rg = gpu.run_queue(0, len(pods))
-    po, ro = oracle.run_queue(0, len(pods))
+    pg, rg = gpu.run_queue(0, P)
     bad = np.nonzero(pg != po)[0]
     assert bad.size == 0, f"{name}: first mismatches at pods {bad[:5]}: gpu {pg[bad[:5]]} oracle {po[bad[:5]]}"
     for f in ("n_feasible", "status", "score_skip"):
         np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
     R = len(enc.cluster.res_names)
-    for a, b in zip(gpu.read_state(R), oracle.read_state(R)):
+    for a, b in zip(gpu.read_state(R), ostate):
         np.testing.assert_array_equal(a, b)
     gpu.reset_state()
-    third = len(pods) // 3
+    third = P // 3
     p1, _ = gpu.run_queue(0, third)
-    p2, _ = gpu.run_queue(third, len(pods) - third)
+    p2, _ = gpu.run_queue(third, P - third)
     np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
