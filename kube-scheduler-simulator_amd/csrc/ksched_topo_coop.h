@@ -331,7 +331,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   CoopPart* const mine = a.parts + wg;
   int32_t* const myhist = a.phist + (size_t)wg * kCoopPHist;
 #ifdef KSG_STAMPS
-  unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+  unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                     st_last = __builtin_amdgcn_s_memtime();
 #endif
 
   auto node_of = [&](int k) { return (k * G + wg) * BLOCK + tid; };
@@ -555,6 +556,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           }
         }
       }
+      KSG_CSTAMP(15);
       if (need_hmin) {
 #pragma unroll
         for (int i = 0; i < kMaxHard; i++) {
@@ -733,6 +735,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       NodeCols L;
       load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
       ev[k] = eval_node_rec(c, prof, v, L, n, tn);
+      KSG_CSTAMP(11);
       if (ev[k].st != 0) continue;
       nfeas += 1;
       minidx = min(minidx, n);
@@ -766,6 +769,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           else if (r == 1) has_zero = 1;
         }
       }
+      KSG_CSTAMP(12);
       if (ipa_may_score) {
         yv[k] = ipa_score_node(c, prof, tn, n);
         imin = min(imin, (long long)yv[k]);
@@ -885,6 +889,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     __syncthreads();
+    KSG_CSTAMP(13);
     const int gnfeas = get_i(0, OpAddI{});
     const int gminidx = get_i(1, OpMinI{});
     const bool scored = ok && gnfeas >= 2;
@@ -969,6 +974,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         pmax = l2 <= h2 ? h2 : 0;
       }
     }
+    KSG_CSTAMP(14);
     uint64_t best = 0;
     uint32_t err = 0;
     if (scored) {
@@ -1082,6 +1088,6 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   }
 #ifdef KSG_STAMPS
   if (tid == 0 && wg == 0 && a.stamps)
-    for (int i = 0; i < 11; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+    for (int i = 0; i < 16; i++) atomicAdd(&a.stamps[i], st_acc[i]);
 #endif
 }

@@ -24,9 +24,11 @@ fn = eng.lib.ksg_debug_stamps
 fn.argtypes = [C.c_void_p, C.c_void_p]
 assert fn(eng.ctx, st) == 0
 tot = sum(st)
-names = ["setup (stage pod, layout)", "phase 1 (pre-pass + merge)", "barrier 1", "2a: merged counts to LDS",
-         "2b: reset next set, IPA skips", "2c: sweep A", "2d: reductions, marks", "barrier 2",
-         "phase 3 (normalise, argmax)", "barrier 3", "phase 4 (select, assume)"]
+names = ["setup (stage pod, layout)", "phase 1: merge / publish", "barrier 1", "2a: merged counts to LDS",
+         "2b: reset next set, IPA skips", "2c3: sweep A, IPA score", "2d: reductions, marks", "barrier 2",
+         "3c: normalise, argmax", "barrier 3", "phase 4 (select, assume)", "2c1: sweep A, load + filters",
+         "2c2: sweep A, PTS soft", "3a: fold phase-2 partials", "3b: marks, sizes, weights", "phase 1: node loop"]
+order = [0, 15, 1, 2, 3, 4, 11, 12, 5, 6, 7, 13, 14, 8, 9, 10]
 print(f"[topo coop] {n_pods} pods x {len(nodes)} nodes, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped)")
-for i in range(11):
-    print(f"  {names[i]:30s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / max(tot, 1):5.1f} %")
+for i in order:
+    print(f"  {names[i]:34s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / max(tot, 1):5.1f} %")
