@@ -2424,6 +2424,13 @@ struct ksg_ctx {
   // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
   char* h_stage = nullptr;
   size_t h_stage_bytes = 0;
+  const char* d_stage = nullptr;            // h_stage's device address (fine-grained: no stale GPU cache lines)
+  // a staged append not yet copied to d_pods / d_prog: the next ksg_eval of
+  // that pod reads it from the staging buffer and copies it on the device
+  // (no copy launches in the cycle); any other call copies it first
+  bool stage_pending = false;
+  int32_t stage_first = 0, stage_n = 0;
+  int64_t stage_base = 0, stage_len = 0;
   hipEvent_t ev_stage = nullptr;            // the last staged copy is done when this fires
   hipEvent_t ev_spin = nullptr;             // per-cycle completion, polled (spin_sync)
 };
@@ -2470,6 +2477,7 @@ int upc(ksg_ctx* ctx, const T*& field, const T* src, size_t count) {
 void free_all(ksg_ctx* ctx) {
   for (void* p : ctx->allocs) (void)hipFree(p);
   ctx->allocs.clear();
+  ctx->stage_pending = false;   // its destination arrays are gone
   ctx->d_pods = nullptr;
   ctx->d_prog = nullptr;
   ctx->pod_cap = ctx->prog_cap = 0;
@@ -3514,6 +3522,8 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   return KSG_OK;
 }
 
+int flush_stage(ksg_ctx* ctx);
+
 int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int32_t* placements,
                  ksg_result* results, ksg_capture* cap) {
   int rc = check_ready(ctx);
@@ -3523,6 +3533,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   if ((rc = check_supported(ctx, ctx->prof, first, count))) return rc;
   if (count == 0) return KSG_OK;
   HIPC(ctx, hipSetDevice(ctx->device));
+  if ((rc = flush_stage(ctx))) return rc;
   const size_t N = ctx->c.N;
   Tmp tmp;
   ksg_profile* d_prof = nullptr;
@@ -3726,6 +3737,14 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
     HIPC(ctx, hipMemcpyAsync(ctx->d_ev_prof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream));
     ctx->ev_prof_dirty = false;
   }
+  // the pod's append still staged: read from the staging buffer by the
+  // first kernel (its programs must all lie in the staged words)
+  const ksg_pod& hp = ctx->h_pods[pod];
+  const bool staged = ctx->stage_pending && ctx->stage_n == 1 && ctx->stage_first == pod && ctx->d_stage &&
+                      hp.blob >= ctx->stage_base && (int64_t)hp.blob + hp.blob_len <= ctx->stage_base + ctx->stage_len &&
+                      (hp.node_set < 0 || (hp.node_set >= ctx->stage_base &&
+                                           (int64_t)hp.node_set + ((int64_t)N + 31) / 32 <= ctx->stage_base + ctx->stage_len));
+  if (!staged && (rc = flush_stage(ctx))) return rc;
   const int par = ctx->ev_parity;
   EvSlot* slot = reinterpret_cast<EvSlot*>(ctx->d_ev) + par;
   CapArgs ca{};
@@ -3750,15 +3769,28 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   ca.best = &slot->best;
   ca.err = &slot->err;
   ca.next = reinterpret_cast<int32_t*>(reinterpret_cast<EvSlot*>(ctx->d_ev) + (1 - par));
+  if (staged) {
+    ca.spod = reinterpret_cast<const ksg_pod*>(ctx->d_stage);
+    ca.sprog = reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod));
+    ca.sbase = ctx->stage_base;
+    ca.slen = ctx->stage_len;
+    ca.wpods = ctx->d_pods + pod;
+    ca.wprog = ctx->d_prog + ctx->stage_base;
+  }
   const unsigned G = (unsigned)((N + 255) / 256);
   ctx->ev_clean = false;   // until the launch is in: it zeroes the other slot
   treset(ctx);
   if ((rc = tmark(ctx))) return rc;
   hipLaunchKernelGGL(ksg_capture_eval, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
   if ((rc = tlaunched(ctx, KSG_K_CAPTURE_EVAL, (double)N))) return rc;
+  ca.spod = nullptr;   // the second kernel reads the device copy the first one made
   hipLaunchKernelGGL(ksg_capture_norm, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
   if ((rc = tlaunched(ctx, KSG_K_CAPTURE_NORM, (double)N))) return rc;
   HIPC(ctx, hipGetLastError());
+  if (staged) {   // consumed; the staging buffer is free once the stream passes this point
+    ctx->stage_pending = false;
+    HIPC(ctx, hipEventRecord(ctx->ev_stage, ctx->stream));
+  }
   ctx->ev_parity = 1 - par;
   ctx->ev_clean = true;
   // one copy back: both slots, the -1 word and the rows the caller asked for
@@ -3827,7 +3859,7 @@ int eval_internal(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) 
   if (rc) return rc;
   if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
-  if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, cap);
+  if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, cap);   // consumes or flushes a staged append
   int32_t pl;
   return run_internal(ctx, pod, 1, 0, &pl, res, cap);
 }
@@ -3890,6 +3922,21 @@ int64_t pod_prog_end(const ksg_pod& p, int N) {
 
 int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, const ksg_pod& p);
 
+// Issue a pending staged append (append_internal) as two stream-ordered
+// copies.  Every entry point that launches kernels reading d_pods / d_prog
+// calls this first, except the per-cycle evaluation of the staged pod.
+int flush_stage(ksg_ctx* ctx) {
+  if (!ctx->stage_pending) return KSG_OK;
+  const size_t pb = sizeof(ksg_pod) * ctx->stage_n, gb = sizeof(int32_t) * ctx->stage_len;
+  if (pb)
+    HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->stage_first, ctx->h_stage, pb, hipMemcpyHostToDevice, ctx->stream));
+  if (gb)
+    HIPC(ctx, hipMemcpyAsync(ctx->d_prog + ctx->stage_base, ctx->h_stage + pb, gb, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(ctx, hipEventRecord(ctx->ev_stage, ctx->stream));
+  ctx->stage_pending = false;
+  return KSG_OK;
+}
+
 int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t* prog, int64_t prog_len,
                     int64_t prog_base) {
   if (!ctx->have_wl) return fail(ctx, KSG_E_STATE, "load a workload before appending");
@@ -3913,28 +3960,37 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
   }
   HIPC(ctx, hipSetDevice(ctx->device));
   int rc;
+  if ((rc = flush_stage(ctx))) return rc;
   if ((rc = dgrow(ctx, &ctx->d_pods, &ctx->pod_cap, (size_t)ctx->n_pods, (size_t)ctx->n_pods + n))) return rc;
   if ((rc = dgrow(ctx, &ctx->d_prog, &ctx->prog_cap, (size_t)prog_base, (size_t)std::max<int64_t>(new_len, 1)))) return rc;
   const size_t pb = sizeof(ksg_pod) * n, gb = sizeof(int32_t) * prog_len;
   if (pb + gb <= (1u << 20)) {
-    // the per-cycle append: through a pinned staging buffer, stream-ordered
-    // before the next evaluation, no host wait (the caller's buffers are free
-    // once this returns)
+    // the per-cycle append: into a pinned, fine-grained staging buffer, no
+    // host wait and no copy launch (the caller's buffers are free once this
+    // returns).  The copy to the device arrays is pending: the next ksg_eval
+    // of the pod consumes it (ksg_capture_eval reads the staged words and its
+    // first workgroup writes them to d_pods / d_prog), any other call issues
+    // it first (flush_stage).
     if (!ctx->ev_stage) HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_stage, hipEventDisableTiming));
-    else HIPC(ctx, hipEventSynchronize(ctx->ev_stage));   // the previous staged copy has left the buffer
+    else HIPC(ctx, hipEventSynchronize(ctx->ev_stage));   // a flushed copy has left the buffer
     if (pb + gb > ctx->h_stage_bytes) {
       if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
       ctx->h_stage = nullptr;
+      ctx->d_stage = nullptr;
       ctx->h_stage_bytes = 0;
-      HIPC(ctx, hipHostMalloc((void**)&ctx->h_stage, 1u << 20, hipHostMallocDefault));
+      HIPC(ctx, hipHostMalloc((void**)&ctx->h_stage, 1u << 20, hipHostMallocMapped | hipHostMallocCoherent));
       ctx->h_stage_bytes = 1u << 20;
+      void* dp = nullptr;
+      HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_stage, 0));
+      ctx->d_stage = static_cast<const char*>(dp);
     }
     if (pb) std::memcpy(ctx->h_stage, pods, pb);
     if (gb) std::memcpy(ctx->h_stage + pb, prog, gb);
-    if (pb) HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->n_pods, ctx->h_stage, pb, hipMemcpyHostToDevice, ctx->stream));
-    if (gb)
-      HIPC(ctx, hipMemcpyAsync(ctx->d_prog + prog_base, ctx->h_stage + pb, gb, hipMemcpyHostToDevice, ctx->stream));
-    HIPC(ctx, hipEventRecord(ctx->ev_stage, ctx->stream));
+    ctx->stage_pending = true;
+    ctx->stage_first = ctx->n_pods;
+    ctx->stage_n = n;
+    ctx->stage_base = prog_base;
+    ctx->stage_len = prog_len;
   } else {
     if (n) HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->n_pods, pods, pb, hipMemcpyHostToDevice, ctx->stream));
     if (prog_len) HIPC(ctx, hipMemcpyAsync(ctx->d_prog + prog_base, prog, gb, hipMemcpyHostToDevice, ctx->stream));
@@ -4164,6 +4220,7 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
     return KSG_E_INVALID;
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "load nodes before the workload");
   HIPC(ctx, hipSetDevice(ctx->device));
+  ctx->stage_pending = false;   // a staged append of the replaced workload
   ctx->h_pods.assign(wl->pods, wl->pods + wl->n_pods);
   std::vector<int32_t> prog(wl->prog, wl->prog + wl->prog_len);
   ctx->max_blob = 0;
@@ -4229,6 +4286,7 @@ int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t 
   const int64_t used0 = ctx->prog_used;
   int rc = append_internal(ctx, &p, 1, prog, prog_len, base);
   if (!rc) rc = eval_internal(ctx, n0, res, cap);
+  if (ctx->stage_pending && ctx->stage_first >= n0) ctx->stage_pending = false;   // the staged pod is dropped
   if (ctx->n_pods > n0) {
     ctx->n_pods = n0;
     ctx->h_pods.resize(n0);
@@ -4250,6 +4308,7 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
   if (rc) return rc;
   if (pod < 0 || pod >= ctx->n_pods || node < 0 || node >= ctx->c.N) return fail(ctx, KSG_E_INVALID, "commit range");
   HIPC(ctx, hipSetDevice(ctx->device));
+  if ((rc = flush_stage(ctx))) return rc;
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
                      ctx->d_prog, pod, node, sign);
   // stream-ordered: the next evaluation on ctx->stream sees the update, and
@@ -4269,6 +4328,7 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
   if (pod < 0 || pod >= ctx->n_pods || n_cand < 0 || (n_cand > 0 && (!cand_node || !vic_off || !fits)))
     return fail(ctx, KSG_E_INVALID, "preempt arguments");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
+  if ((rc = flush_stage(ctx))) return rc;
   if (ctx->h_pods[pod].ports >= 0)   // the dry run re-runs Fit / PTS / IPA only
     return fail(ctx, KSG_E_UNSUPPORTED, "preemption: a preemptor with host ports (NodePorts) is not modelled");
   if (n_cand == 0) return KSG_OK;
@@ -4342,6 +4402,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   if (!profiles || n_replicas <= 0 || first < 0 || count < 0 || first + count > ctx->n_pods || !placements)
     return fail(ctx, KSG_E_INVALID, "replica arguments");
   if ((rc = check_blobs(ctx, first, count))) return rc;
+  if ((rc = flush_stage(ctx))) return rc;
   for (int r = 0; r < n_replicas; r++)
     if ((rc = check_supported(ctx, profiles[r], first, count))) return rc;
   HIPC(ctx, hipSetDevice(ctx->device));

@@ -51,6 +51,16 @@ struct CapArgs {
   int32_t* next;                 // 8 words: the next call's stats[4], best, err
   int32_t narrow;                // raw / norm / total rows are int32 (the per-cycle path's copy-back; the
                                  // host checked every value fits) instead of int64
+  // per-cycle evaluation of a pod whose append is still staged (ksched.hip
+  // flush_stage): its record and program words [sbase, sbase + slen) are read
+  // from the fine-grained host staging buffer, and workgroup (0, 0) writes them
+  // to the device arrays (wpods = &pods[b0], wprog = &prog[sbase]) for the
+  // kernels after this one.  Null otherwise.
+  const ksg_pod* spod;
+  const int32_t* sprog;
+  int64_t sbase, slen;
+  ksg_pod* wpods;
+  int32_t* wprog;
 };
 
 // Row element idx of a capture array: int64, or int32 in the narrow form.
@@ -73,9 +83,24 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
   for (int k = tid; k < a.nb; k += 256) s_pl[k] = a.placements[a.out0 + k];
-  stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
+  const int32_t* gprog = a.prog;
+  if (a.spod) {   // the staged append (nb = 1)
+    if (tid < (int)(sizeof(ksg_pod) / 4))
+      reinterpret_cast<int32_t*>(&s_pod)[tid] = reinterpret_cast<const int32_t*>(a.spod)[tid];
+    __syncthreads();
+    const int64_t boff = s_pod.blob - a.sbase;
+    for (int i = tid; i < s_pod.blob_len; i += 256) s_blob[i] = a.sprog[boff + i];
+    gprog = a.sprog - a.sbase;   // the node set (outside the blob) is staged too (host-checked)
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      if (tid < (int)(sizeof(ksg_pod) / 4))
+        reinterpret_cast<int32_t*>(a.wpods)[tid] = reinterpret_cast<const int32_t*>(&s_pod)[tid];
+      for (int64_t i = tid; i < a.slen; i += 256) a.wprog[i] = a.sprog[i];
+    }
+  } else {
+    stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
+  }
   __syncthreads();
-  const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog, false, a.st.ports);
+  const PodView v = make_view(c, s_prof, s_pod, s_blob, gprog, false, a.st.ports);
   const int n = blockIdx.x * 256 + tid;
   const size_t o = (size_t)(a.out0 + j);
   int32_t feas = 0, mt = 0, ma = 0, lo = 0;
