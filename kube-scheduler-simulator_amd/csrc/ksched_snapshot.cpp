@@ -502,6 +502,7 @@ struct ksg_snapshot {
   // terms resolve against these
   bool have_namespaces = false;
   std::map<std::string, StrMap> namespaces;
+  std::unordered_map<uint64_t, int32_t> status_seen;   // ksg_snapshot_statuses scratch
 };
 
 namespace {
@@ -2010,10 +2011,18 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
   if (!s->encoded || pod < 0 || pod >= (int32_t)s->e.pods.size() || n_nodes != s->e.N)
     return fail(s, KSG_E_INVALID, "statuses: index out of range");
   const Encoded& e = s->e;
-  // distinct messages: keyed by the word, plus the taint id for TaintToleration
-  std::unordered_map<uint64_t, int32_t> seen;
-  seen.reserve(64);
+  // distinct messages: keyed by the word, plus the taint id for TaintToleration.
+  // The code depends on the node only for NodeResourcesFit (a request above
+  // the node's allocatable is unresolvable); every other code is cached with
+  // its message.  Neighbouring nodes mostly repeat a word: last-key shortcut.
+  auto& seen = s->status_seen;   // reused across calls (no rehash per pod)
+  seen.clear();
   std::vector<std::string> msgs;
+  std::vector<int32_t> codes;
+  const ksg_pod& p = e.pods[pod];
+  uint64_t last_key = ~0ull;
+  int32_t last_idx = -1;
+  std::string err;
   for (int32_t n = 0; n < n_nodes; n++) {
     const uint32_t w = words[n];
     if (w == 0 || w == KSG_FS_NOT_EVALUATED) {
@@ -2025,19 +2034,32 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     uint64_t key = w;
     if (pl == KSG_PL_TAINT_TOLERATION && (int)(w >> 8) < e.max_taints)
       key |= (uint64_t)e.taints[(size_t)(w >> 8) * e.N + n] << 32;
-    auto it = seen.find(key);
-    int c;
-    std::string err;
-    if (it == seen.end()) {
-      std::string m;
-      if (!status_of(e, pod, w, n, &c, &m, &err)) return fail(s, KSG_E_INVALID, "statuses: " + err);
-      it = seen.emplace(key, (int32_t)msgs.size()).first;
-      msgs.push_back(std::move(m));
-    } else if (!status_of(e, pod, w, n, &c, nullptr, &err)) {   // the code may depend on the node
-      return fail(s, KSG_E_INVALID, "statuses: " + err);
+    int32_t idx;
+    if (key == last_key) {
+      idx = last_idx;
+    } else {
+      auto it = seen.find(key);
+      if (it == seen.end()) {
+        std::string m;
+        int c;
+        if (!status_of(e, pod, w, n, &c, &m, &err)) return fail(s, KSG_E_INVALID, "statuses: " + err);
+        it = seen.emplace(key, (int32_t)msgs.size()).first;
+        msgs.push_back(std::move(m));
+        codes.push_back(c);
+      }
+      idx = it->second;
+      last_key = key;
+      last_idx = idx;
+    }
+    int c = codes[idx];
+    if (pl == KSG_PL_NODE_RESOURCES_FIT) {   // status_of's Fit code, per node
+      const uint32_t reason = w >> 8;
+      c = KSG_CODE_UNSCHEDULABLE;
+      for (size_t r = 0; r < e.res_names.size(); r++)
+        if ((reason & (1u << (r + 1))) && p.req[r] > e.alloc[r * e.N + n]) c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     }
     code[n] = c;
-    msg[n] = it->second;
+    msg[n] = idx;
   }
   int64_t total = 0;
   for (auto& m : msgs) total += (int64_t)m.size() + 1;
