@@ -335,7 +335,8 @@ enum {
   KSG_K_BATCH_PHASE2T = 14,
   KSG_K_BATCH_TRANSPOSE = 15,
   KSG_K_TCOL_CARRY = 16,
-  KSG_NKERNELS = 17
+  KSG_K_EVAL_CYCLE = 17,
+  KSG_NKERNELS = 18
 };
 typedef struct ksg_kernel_stat {
   char name[48];

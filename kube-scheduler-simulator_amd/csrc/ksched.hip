@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <cstdio>
 #include <cstring>
@@ -1797,6 +1798,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 #include "ksched_phase2t.h"
 #include "ksched_capture.h"
 #include "ksched_sweep.h"
+#include "ksched_cycle.h"
 
 // ---- queue kernel with PodTopologySpread / InterPodAffinity -------------------
 template <int BLOCK>
@@ -2415,12 +2417,12 @@ struct ksg_ctx {
   size_t ev_bytes = 0;
   char* h_ev = nullptr;                     // hipHostMalloc'd, freed by ksg_close
   size_t h_ev_bytes = 0;
-  int ev_parity = 0;                        // which of the two stats slots this call uses
-  bool ev_clean = false;                    // both slots zeroed
+  char* d_hev = nullptr;                    // h_ev's device address (the kernel writes the results there)
+  unsigned ev_seq = 0;                      // the per-cycle completion flag's last value
+  bool ev_clean = false;                    // the arrival counter is zero
   ksg_profile* d_ev_prof = nullptr;
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
-  unsigned ev_bar = 0;                      // the per-cycle grid barrier's arrival count so far
   // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
   char* h_stage = nullptr;
   size_t h_stage_bytes = 0;
@@ -2432,7 +2434,6 @@ struct ksg_ctx {
   int32_t stage_first = 0, stage_n = 0;
   int64_t stage_base = 0, stage_len = 0;
   hipEvent_t ev_stage = nullptr;            // the last staged copy is done when this fires
-  hipEvent_t ev_spin = nullptr;             // per-cycle completion, polled (spin_sync)
 };
 
 namespace {
@@ -2527,7 +2528,7 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
                                           "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
                                           "ksg_capture_eval", "ksg_capture_norm", "ksg_batch_phase2t",
-                                          "ksg_batch_transpose", "ksg_tcol_carry"};
+                                          "ksg_batch_transpose", "ksg_tcol_carry", "ksg_eval_cycle"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -3638,38 +3639,12 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
 // ---- the per-cycle path ---------------------------------------------------------
 // ksg_eval of one pod whose plugins are all node-local (the batched path's
 // eligibility): the framework's PreFilter .. NormalizeScore for one pod, as the
-// Go shim calls it once per scheduling cycle.  No allocation per call: one
-// grow-only device block (two parity slots of per-call statistics, the
-// capture rows, the record scratch) and its pinned host mirror.  Two chip-wide
-// launches (ksg_capture_eval and ksg_capture_norm, N / 256 workgroups each,
-// nothing assumed: the pod sees the live state) and one device -> host copy of
-// the slot plus every row the caller asked for; the host then fills the
-// caller's arrays and decodes the result.  The other parity's slot is zeroed
-// by the second launch, so no memset runs per call.
-// Wait for the stream by polling an event: the per-cycle path waits for
-// ~20-40 us of device work per call, where a blocking wait's wake-up costs
-// as much again (measured: 113 us per ksg_eval with hipStreamSynchronize,
-// 65 us with the wait spinning).  The calling thread spins; the scheduler's
-// cycle is blocked on the result anyway.
-int spin_sync(ksg_ctx* ctx) {
-  if (!ctx->ev_spin) HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_spin, hipEventDisableTiming));
-  HIPC(ctx, hipEventRecord(ctx->ev_spin, ctx->stream));
-  for (;;) {
-    const hipError_t e = hipEventQuery(ctx->ev_spin);
-    if (e == hipSuccess) return KSG_OK;
-    if (e != hipErrorNotReady) return fail(ctx, KSG_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
-    __builtin_ia32_pause();
-  }
-}
-
-struct EvSlot {
-  int32_t stats[4];              // feasible count, max taint, max node affinity, max (N - n) over feasible n
-  unsigned long long best;       // selectHost key
-  uint32_t err;
-  uint32_t pad;
-};
-static_assert(sizeof(EvSlot) == 32, "EvSlot layout");
-
+// Go shim calls it once per scheduling cycle.  No allocation per call, one
+// launch (ksg_eval_cycle, ksched_cycle.h: N / 256 workgroups, the last to
+// arrive normalises and selects), results written by the kernel into a
+// pinned, fine-grained host block, completion read from a flag in that block
+// (no copy, no event, no stream synchronisation); the host then fills the
+// caller's arrays and decodes the result.
 bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
   return ctx->eval_fast && ctx->force_path != 1 && batch_eligible(ctx, pod, 1);
 }
@@ -3678,7 +3653,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   const size_t N = ctx->c.N;
   const ksg_profile& prof = ctx->prof;
   // score rows, the normalising plugins first (only their norm rows differ
-  // from the raw ones, so only those come back)
+  // from the raw ones, so only those are written)
   int rows[KSG_NPLUGINS], n_rows = 0, n_normrows = 0;
   for (int pl : {KSG_PL_TAINT_TOLERATION, KSG_PL_NODE_AFFINITY})
     if ((prof.score_mask >> pl) & 1u) rows[n_rows++] = pl;
@@ -3692,17 +3667,16 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
     if ((prof.score_mask >> pl) & 1u) wabs += prof.weight[pl] < 0 ? -(int64_t)prof.weight[pl] : prof.weight[pl];
   const bool narrow = wabs * 100 < (1ll << 31);
   const size_t es = narrow ? 4 : 8;
-  const bool want_fs = cap && cap->fstatus, want_raw = cap && cap->raw, want_norm = cap && cap->norm,
-             want_tot = cap && cap->total;
-  // block: slot[2] | bar, timeout | -1 | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_rows][N] | rec[N] (u64)
-  const size_t o_bar = 2 * sizeof(EvSlot), o_neg = o_bar + 8, o_fs = o_neg + 8,
-               o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
-  const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
-  const size_t o_rec = o_norm + ((es * N * n_rows + 7) & ~(size_t)7);
-  const size_t need = o_rec + 8 * N;
+  const unsigned G = (unsigned)((N + 255) / 256);
+  // host block: stats[4] best err flag | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_normrows][N]
+  const size_t o_fs = 32, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
+  const size_t o_tot = o_raw + es * N * n_rows, o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
+  const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
+  // device block: rec[N] | parts[G] | done
+  const size_t d_parts = 8 * N, d_done = d_parts + sizeof(CycPart) * G, d_need = d_done + 8;
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
-  if (need > ctx->ev_bytes) {
+  if (d_need > ctx->ev_bytes) {
     if (ctx->d_ev) {
       auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_ev);
       if (it != ctx->allocs.end()) ctx->allocs.erase(it);
@@ -3710,27 +3684,26 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
       (void)hipFree(ctx->d_ev);
       ctx->d_ev = nullptr;
     }
-    if ((rc = dalloc(ctx, &ctx->d_ev, need))) return rc;
-    ctx->ev_bytes = need;
+    if ((rc = dalloc(ctx, &ctx->d_ev, d_need))) return rc;
+    ctx->ev_bytes = d_need;
     ctx->ev_clean = false;
   }
   if (!ctx->d_ev_prof && (rc = dalloc(ctx, &ctx->d_ev_prof, 1))) return rc;
-  if (o_rec > ctx->h_ev_bytes) {   // the host mirror holds everything but the record scratch
+  if (h_need > ctx->h_ev_bytes) {
     if (ctx->h_ev) {
       HIPC(ctx, hipStreamSynchronize(ctx->stream));
       (void)hipHostFree(ctx->h_ev);
       ctx->h_ev = nullptr;
       ctx->h_ev_bytes = 0;
     }
-    HIPC(ctx, hipHostMalloc((void**)&ctx->h_ev, o_rec, hipHostMallocDefault));
-    ctx->h_ev_bytes = o_rec;
+    HIPC(ctx, hipHostMalloc((void**)&ctx->h_ev, h_need, hipHostMallocMapped | hipHostMallocCoherent));
+    ctx->h_ev_bytes = h_need;
+    void* dp = nullptr;
+    HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_ev, 0));
+    ctx->d_hev = static_cast<char*>(dp);
   }
-  if (!ctx->ev_clean) {   // both slots, the barrier counter and the timeout word
-    static const int32_t init[2] = {-1, 0};
-    HIPC(ctx, hipMemsetAsync(ctx->d_ev, 0, o_neg, ctx->stream));
-    HIPC(ctx, hipMemcpyAsync(ctx->d_ev + o_neg, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
-    ctx->ev_parity = 0;
-    ctx->ev_bar = 0;
+  if (!ctx->ev_clean) {   // the arrival counter
+    HIPC(ctx, hipMemsetAsync(ctx->d_ev + d_done, 0, 8, ctx->stream));
     ctx->ev_clean = true;
   }
   if (ctx->ev_prof_dirty) {
@@ -3738,37 +3711,40 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
     ctx->ev_prof_dirty = false;
   }
   // the pod's append still staged: read from the staging buffer by the
-  // first kernel (its programs must all lie in the staged words)
+  // kernel (its programs must all lie in the staged words)
   const ksg_pod& hp = ctx->h_pods[pod];
   const bool staged = ctx->stage_pending && ctx->stage_n == 1 && ctx->stage_first == pod && ctx->d_stage &&
                       hp.blob >= ctx->stage_base && (int64_t)hp.blob + hp.blob_len <= ctx->stage_base + ctx->stage_len &&
                       (hp.node_set < 0 || (hp.node_set >= ctx->stage_base &&
                                            (int64_t)hp.node_set + ((int64_t)N + 31) / 32 <= ctx->stage_base + ctx->stage_len));
   if (!staged && (rc = flush_stage(ctx))) return rc;
-  const int par = ctx->ev_parity;
-  EvSlot* slot = reinterpret_cast<EvSlot*>(ctx->d_ev) + par;
-  CapArgs ca{};
+  char* hb = ctx->h_ev;
+  char* db = ctx->d_hev;
+  volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(hb + 28);
+  const unsigned seq = ++ctx->ev_seq == 0 ? ++ctx->ev_seq : ctx->ev_seq;   // never 0 (a fresh block)
+  CycArgs ca{};
   ca.c = ctx->c;
   ca.st = ctx->st;
   ca.pods = ctx->d_pods;
   ca.prog = ctx->d_prog;
   ca.prof = ctx->d_ev_prof;
-  ca.b0 = pod;
-  ca.nb = 1;
-  ca.out0 = 0;
-  ca.placements = reinterpret_cast<const int32_t*>(ctx->d_ev + o_neg);
-  ca.rec = reinterpret_cast<uint64_t*>(ctx->d_ev + o_rec);
-  ca.stats = slot->stats;
+  ca.pod = pod;
   ca.n_rows = n_rows;
+  ca.n_normrows = n_normrows;
   for (int q = 0; q < n_rows; q++) ca.rows[q] = rows[q];
-  ca.fstatus = reinterpret_cast<uint32_t*>(ctx->d_ev + o_fs);
-  ca.raw = reinterpret_cast<int64_t*>(ctx->d_ev + o_raw);
-  ca.norm = reinterpret_cast<int64_t*>(ctx->d_ev + o_norm);
-  ca.total = want_tot ? reinterpret_cast<int64_t*>(ctx->d_ev + o_tot) : nullptr;
   ca.narrow = narrow ? 1 : 0;
-  ca.best = &slot->best;
-  ca.err = &slot->err;
-  ca.next = reinterpret_cast<int32_t*>(reinterpret_cast<EvSlot*>(ctx->d_ev) + (1 - par));
+  ca.h_fs = reinterpret_cast<uint32_t*>(db + o_fs);
+  ca.h_raw = db + o_raw;
+  ca.h_tot = db + o_tot;
+  ca.h_norm = db + o_norm;
+  ca.h_stats = reinterpret_cast<int32_t*>(db);
+  ca.h_best = reinterpret_cast<unsigned long long*>(db + 16);
+  ca.h_err = reinterpret_cast<uint32_t*>(db + 24);
+  ca.h_flag = reinterpret_cast<unsigned*>(db + 28);
+  ca.seq = seq;
+  ca.rec = reinterpret_cast<uint64_t*>(ctx->d_ev);
+  ca.parts = reinterpret_cast<CycPart*>(ctx->d_ev + d_parts);
+  ca.done = reinterpret_cast<unsigned*>(ctx->d_ev + d_done);
   if (staged) {
     ca.spod = reinterpret_cast<const ksg_pod*>(ctx->d_stage);
     ca.sprog = reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod));
@@ -3777,56 +3753,53 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
     ca.wpods = ctx->d_pods + pod;
     ca.wprog = ctx->d_prog + ctx->stage_base;
   }
-  const unsigned G = (unsigned)((N + 255) / 256);
-  ctx->ev_clean = false;   // until the launch is in: it zeroes the other slot
   treset(ctx);
   if ((rc = tmark(ctx))) return rc;
-  hipLaunchKernelGGL(ksg_capture_eval, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
-  if ((rc = tlaunched(ctx, KSG_K_CAPTURE_EVAL, (double)N))) return rc;
-  ca.spod = nullptr;   // the second kernel reads the device copy the first one made
-  hipLaunchKernelGGL(ksg_capture_norm, dim3(G, 1), dim3(256), 0, ctx->stream, ca);
-  if ((rc = tlaunched(ctx, KSG_K_CAPTURE_NORM, (double)N))) return rc;
+  hipLaunchKernelGGL(ksg_eval_cycle, dim3(G), dim3(256), 0, ctx->stream, ca);
+  if ((rc = tlaunched(ctx, KSG_K_EVAL_CYCLE, (double)N))) return rc;
   HIPC(ctx, hipGetLastError());
   if (staged) {   // consumed; the staging buffer is free once the stream passes this point
     ctx->stage_pending = false;
     HIPC(ctx, hipEventRecord(ctx->ev_stage, ctx->stream));
   }
-  ctx->ev_parity = 1 - par;
-  ctx->ev_clean = true;
-  // one copy back: both slots, the -1 word and the rows the caller asked for
-  size_t back = o_fs;
-  if (want_fs) back = o_raw;
-  if (want_raw || want_norm) back = o_raw + es * N * n_rows;
-  if (want_tot) back = o_tot + es * N;
-  if (want_norm && n_normrows) back = o_norm + es * N * n_normrows;
-  HIPC(ctx, hipMemcpyAsync(ctx->h_ev, ctx->d_ev, back, hipMemcpyDeviceToHost, ctx->stream));
-  if ((rc = spin_sync(ctx))) return rc;
-  if ((rc = tcollect(ctx))) return rc;
-  if (reinterpret_cast<const unsigned*>(ctx->h_ev + o_bar)[1]) {
-    ctx->ev_clean = false;
-    return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: grid barrier timed out");
+  // the kernel's last workgroup stores seq after every result: spin on it,
+  // checking the stream now and then (a failed launch never stores it)
+  for (unsigned spins = 0; *flag != seq; spins++) {
+    __builtin_ia32_pause();
+    if ((spins & 1023) == 1023) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipSuccess && *flag != seq) {
+        ctx->ev_clean = false;
+        return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: kernel finished without its completion flag");
+      }
+      if (e != hipSuccess && e != hipErrorNotReady)
+        return fail(ctx, KSG_E_DEVICE, std::string("per-cycle evaluation: ") + hipGetErrorString(e));
+    }
   }
-  const EvSlot& h = reinterpret_cast<const EvSlot*>(ctx->h_ev)[par];
-  const int32_t nfeas = h.stats[0];
+  std::atomic_thread_fence(std::memory_order_acquire);
+  if ((rc = tcollect(ctx))) return rc;
+  const int32_t* st = reinterpret_cast<const int32_t*>(hb);
+  const int32_t nfeas = st[0];
+  const unsigned long long best = *reinterpret_cast<const unsigned long long*>(hb + 16);
+  const uint32_t herr = *reinterpret_cast<const uint32_t*>(hb + 24);
   uint32_t status = 0;
   int32_t selected = -1;
   if (nfeas == 1) {
-    selected = (int32_t)N - h.stats[3];
+    selected = (int32_t)N - st[3];
   } else if (nfeas >= 2) {
     status |= KSG_ST_SCORED;
-    if (h.err) status |= KSG_ST_SCORE_ERROR;
-    else selected = (int32_t)(0xffffffffu - (uint32_t)(h.best & 0xffffffffu));
+    if (herr) status |= KSG_ST_SCORE_ERROR;
+    else selected = (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffu));
   }
   // ipa_skip_bits (ksched_kernels.h) on the host: the pod carries no
   // InterPodAffinity program on this path
-  const ksg_pod& p = ctx->h_pods[pod];
-  uint32_t score_skip = p.score_skip;
+  uint32_t score_skip = hp.score_skip;
   bool ipa_filter = false;
   for (int kf = 0; kf < prof.n_filter; kf++) ipa_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
-  if (p.ipa < 0) {
+  if (hp.ipa < 0) {
     if (ipa_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
     if ((status & KSG_ST_SCORED) && ((prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) &&
-        !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u)) {
+        !((hp.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u)) {
       status |= KSG_ST_IPA_PRESCORE_SKIP;
       score_skip |= 1u << KSG_PL_INTER_POD_AFFINITY;
     }
@@ -3837,13 +3810,15 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   res->score_skip = score_skip;
   auto put_row = [&](int64_t* dst, size_t off) {   // one row into the caller's int64 array
     if (narrow) {
-      const int32_t* src = reinterpret_cast<const int32_t*>(ctx->h_ev + off);
+      const int32_t* src = reinterpret_cast<const int32_t*>(hb + off);
       for (size_t n = 0; n < N; n++) dst[n] = src[n];
     } else {
-      std::memcpy(dst, ctx->h_ev + off, 8 * N);
+      std::memcpy(dst, hb + off, 8 * N);
     }
   };
-  if (want_fs) std::memcpy(cap->fstatus, ctx->h_ev + o_fs, 4 * N);
+  const bool want_fs = cap && cap->fstatus, want_raw = cap && cap->raw, want_norm = cap && cap->norm,
+             want_tot = cap && cap->total;
+  if (want_fs) std::memcpy(cap->fstatus, hb + o_fs, 4 * N);
   for (int q = 0; q < n_rows; q++) {
     if (want_raw) put_row(cap->raw + (size_t)rows[q] * N, o_raw + es * N * q);
     // plugins without ScoreExtensions record the raw score as the final one
@@ -4109,7 +4084,6 @@ int ksg_close(ksg_ctx* ctx) {
   if (ctx->h_ev) (void)hipHostFree(ctx->h_ev);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->ev_stage) (void)hipEventDestroy(ctx->ev_stage);
-  if (ctx->ev_spin) (void)hipEventDestroy(ctx->ev_spin);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

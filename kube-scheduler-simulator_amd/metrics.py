@@ -90,6 +90,8 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
         return bytes_per_eval + 12
     if name == "ksg_capture_norm":   # record read, normalised row and total written (one scored row at least)
         return 24
+    if name == "ksg_eval_cycle":     # ksg_capture_eval + ksg_capture_norm in one launch (per-cycle path)
+        return bytes_per_eval + 12 + 24
     if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
         return 8
     if name == "ksg_tcol_carry":
