@@ -54,6 +54,7 @@ constexpr int kCoopBatch = 64;      // pods per launch (static records [kCoopBat
 constexpr int kCoopPHist = 512;     // partial-histogram words per workgroup slot
 constexpr int kCoopLabCols = 16;    // KN == 1: label columns of the lane's node staged in LDS
 constexpr int kCoopTmpl = 2048;     // term templates whose column / table offset are staged in LDS
+constexpr int kCoopLog = 512;       // log_table entries staged in LDS
 
 struct CoopPart {   // one workgroup's partial results of the current pod
   // phase 1
@@ -296,6 +297,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ uint8_t s_cu[kCoopLabCols];
   __shared__ int32_t s_tcol[kCoopTmpl], s_toff[kCoopTmpl];
   __shared__ ksg_pod s_pods[kCoopBatch];   // the batch's pod records
+  __shared__ double s_log[kCoopLog];       // log_table[0 .. kCoopLog): topologyNormalizingWeight of small domains
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
@@ -316,6 +318,14 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   if (col_lds && tid < cg.L) { s_cv[tid] = cg.col_vocab[tid]; s_cu[tid] = cg.col_unique[tid]; }
   if (tmpl_lds)
     for (int i = tid; i < cg.n_tmpl; i += BLOCK) { s_tcol[i] = cg.tmpl_col[i]; s_toff[i] = cg.tmpl_off[i]; }
+  for (int i = tid; i < kCoopLog && i < cg.log_n; i += BLOCK) s_log[i] = cg.log_table[i];
+  // KN == 1: the lane's node's Fit / BalancedAllocation columns stay in
+  // registers for the launch (only this lane reads or assumes onto the node)
+  NodeCols Lreg;
+  if (KN == 1) {
+    const int n = wg * BLOCK + tid;
+    if (n < N) load_cols(cg, st.requested, st.nonzero, st.pod_count, n, Lreg);
+  }
   __syncthreads();
   DevCluster cl = cg;   // the evaluators' view: the staged copies where they fit
   if (lab_lds) { cl.label_val = s_lab; cl.lab_stride = BLOCK; cl.lab_base = wg * BLOCK; }
@@ -733,7 +743,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       tn.has_rec = true;
       tn.rec = srk[k];
       NodeCols L;
-      load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
+      if (KN == 1) L = Lreg;
+      else load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
       ev[k] = eval_node_rec(c, prof, v, L, n, tn);
       KSG_CSTAMP(11);
       if (ev[k].st != 0) continue;
@@ -927,7 +938,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           if (g.soft[6 * i + 5]) sz = gnfeas - n_ign;
           else if (sl.unique) sz = get_i(8 + i, OpAddI{}) + get_i(12 + i, OpOrI{});
           else sz = s_size[i];
-          s_t.soft_w[i] = c.log_table[sz + 2];   // topologyNormalizingWeight = math.Log(size + 2)
+          s_t.soft_w[i] = sz + 2 < kCoopLog ? s_log[sz + 2] : c.log_table[sz + 2];   // math.Log(size + 2)
         }
       }
       __syncthreads();
@@ -1066,7 +1077,17 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       else selected = key_node(b);
     }
     if (selected >= 0 && ((selected / BLOCK) % G) == wg && (selected % BLOCK) == tid)
+    {
       coop_commit(cg, st, p, p.commit >= 0 ? s_blob + (p.commit - p.blob) : nullptr, selected);
+      if (KN == 1) {   // the register copy
+#pragma unroll
+        for (int r = 0; r < KSG_MAX_RES; r++)
+          if (r < cg.R) Lreg.req[r] += p.req[r];
+        Lreg.nz_cpu += p.nz_cpu;
+        Lreg.nz_mem += p.nz_mem;
+        Lreg.pod_count += 1;
+      }
+    }
     if (wg == 0 && tid == 0) {
       uint32_t score_skip = p.score_skip;
       if (ipa_in_filter && s_t.ipa_skip_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
