@@ -241,7 +241,8 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
     """The drop-in's per-cycle path, the calls the Go
     shim makes per scheduling cycle, through the C ABI of libksched.so:
     ksg_snapshot_add_pod -> ksg_snapshot_sync (append to the device
-    workload) -> ksg_eval with capture (status words + the score rows) ->
+    workload) -> ksg_eval_view (status words + the score rows, left in the
+    library's pinned block) ->
     ksg_snapshot_statuses (every rejected node's framework.Status, once per
     pod) -> ksg_snapshot_assume.  configs[1]'s cluster, starting empty; the
     first `warm` pods fill the encoding universe (a pod that adds a label
@@ -256,7 +257,7 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
     eng = native.Engine(device=0)
     snap.load(eng)
     N = len(nodes)
-    cap = native.CaptureBuffers(N, 1)
+    rows = native.KsgEvalRows()
     keep = []
     views = []
     for p in pods:
@@ -272,7 +273,7 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
     placed = np.full(warm + n_pods, -1, np.int32)
     phases = np.zeros((n_pods, 5), np.int64)
     ap, rl, where = C.c_int32(), C.c_int32(), C.c_int32(-1)
-    rc = drv.cycle_run(snap.h, eng.ctx, arr, len(views), warm, C.addressof(cap.struct), N,
+    rc = drv.cycle_run(snap.h, eng.ctx, arr, len(views), warm, C.addressof(rows), N,
                        placed.ctypes.data_as(i32p), phases.ctypes.data_as(C.POINTER(C.c_int64)),
                        C.byref(ap), C.byref(rl), C.byref(where))
     if rc != 0:

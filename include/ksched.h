@@ -245,12 +245,33 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl);
  * uses.  The new pods get indices n_pods, n_pods + 1, ... */
 int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base);
 /* Evaluate pod `pod` (index into the loaded workload) against the current
- * node state; no state change.  `cap` may be NULL.  The per-cycle call of the
- * Go shim: a pod whose plugins are all node-local takes the chip-wide path
- * (two launches over N / 256 workgroups, persistent device and pinned host
- * buffers, one device -> host copy); topology pods take the single-workgroup
- * queue kernel. */
+ * node state; no state change.  `cap` may be NULL.  A pod whose plugins are
+ * all node-local takes the chip-wide per-cycle path (one launch over N / 256
+ * workgroups writing into a pinned host block, completion polled from a flag
+ * there, persistent buffers); topology pods take the single-workgroup queue
+ * kernel. */
 int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap);
+
+/* The per-cycle results of ksg_eval_view, in library memory (no copy into
+ * caller arrays): valid until the next ksg_eval / ksg_eval_view / ksg_eval_pod
+ * on the context.  Rows hold elem_bytes-wide signed integers (4 when every
+ * weighted total fits 32 bits, else 8), one per node; raw[pl] / norm[pl] are
+ * NULL for a plugin the profile does not score (norm[pl] == raw[pl] for the
+ * plugins without ScoreExtensions).  A pod with fewer than two feasible nodes
+ * has all-zero rows (no Score runs).  The Go shim's Score / NormalizeScore
+ * answers read these rows directly (wrappedplugin.go:420-445 / 388-415). */
+typedef struct ksg_eval_rows {
+  int32_t n_nodes;
+  int32_t elem_bytes;
+  const uint32_t* fstatus;                /* [n_nodes] Filter status words */
+  const void* raw[KSG_NPLUGINS];
+  const void* norm[KSG_NPLUGINS];
+  const void* total;                      /* [n_nodes] weighted totals (0: not scored) */
+} ksg_eval_rows;
+/* ksg_eval with the rows left in library memory (the per-cycle call of the Go
+ * shim; replaces the framework's per-(pod, node, plugin) Filter / Score /
+ * NormalizeScore calls, wrappedplugin.go:388-548). */
+int ksg_eval_view(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_eval_rows* rows);
 /* Evaluate an encoded pod that is not part of the workload: `pod`'s program
  * offsets index `prog[0 .. prog_len)`.  Same outputs as ksg_eval; the pod
  * is not retained (ksg_append_pods it first to commit it). */

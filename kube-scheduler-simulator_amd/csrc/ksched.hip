@@ -2418,6 +2418,8 @@ struct ksg_ctx {
   char* h_ev = nullptr;                     // hipHostMalloc'd, freed by ksg_close
   size_t h_ev_bytes = 0;
   char* d_hev = nullptr;                    // h_ev's device address (the kernel writes the results there)
+  std::vector<uint32_t> view_fs;            // ksg_eval_view of a pod off the per-cycle path: library-owned rows
+  std::vector<int64_t> view_rows;
   unsigned ev_seq = 0;                      // the per-cycle completion flag's last value
   bool ev_clean = false;                    // the arrival counter is zero
   ksg_profile* d_ev_prof = nullptr;
@@ -3649,7 +3651,7 @@ bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
   return ctx->eval_fast && ctx->force_path != 1 && batch_eligible(ctx, pod, 1);
 }
 
-int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
+int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_eval_rows* view = nullptr) {
   const size_t N = ctx->c.N;
   const ksg_profile& prof = ctx->prof;
   // score rows, the normalising plugins first (only their norm rows differ
@@ -3816,6 +3818,17 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
       std::memcpy(dst, hb + off, 8 * N);
     }
   };
+  if (view) {   // the rows where the kernel wrote them
+    *view = ksg_eval_rows{};
+    view->n_nodes = (int32_t)N;
+    view->elem_bytes = (int32_t)es;
+    view->fstatus = reinterpret_cast<const uint32_t*>(hb + o_fs);
+    for (int q = 0; q < n_rows; q++) {
+      view->raw[rows[q]] = hb + o_raw + es * N * q;
+      view->norm[rows[q]] = q < n_normrows ? hb + o_norm + es * N * q : view->raw[rows[q]];
+    }
+    view->total = hb + o_tot;
+  }
   const bool want_fs = cap && cap->fstatus, want_raw = cap && cap->raw, want_norm = cap && cap->norm,
              want_tot = cap && cap->total;
   if (want_fs) std::memcpy(cap->fstatus, hb + o_fs, 4 * N);
@@ -4238,6 +4251,34 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
 int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   if (!res) return fail(ctx, KSG_E_INVALID, "null result");
   return eval_internal(ctx, pod, res, cap);
+}
+
+int ksg_eval_view(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_eval_rows* rows) {
+  if (!ctx || !res || !rows) return ctx ? fail(ctx, KSG_E_INVALID, "null result") : KSG_E_INVALID;
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
+  if ((rc = check_blobs(ctx, pod, 1))) return rc;
+  if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, nullptr, rows);
+  // topology pods: the queue kernel into library-owned int64 rows
+  const size_t N = ctx->c.N;
+  ctx->view_fs.resize(N);
+  ctx->view_rows.resize((2 * (size_t)KSG_NPLUGINS + 1) * N);
+  ksg_capture cap{ctx->view_fs.data(), ctx->view_rows.data(), ctx->view_rows.data() + KSG_NPLUGINS * N,
+                  ctx->view_rows.data() + 2 * KSG_NPLUGINS * N};
+  int32_t pl;
+  if ((rc = run_internal(ctx, pod, 1, 0, &pl, res, &cap))) return rc;
+  *rows = ksg_eval_rows{};
+  rows->n_nodes = (int32_t)N;
+  rows->elem_bytes = 8;
+  rows->fstatus = cap.fstatus;
+  for (int p = 0; p < KSG_NPLUGINS; p++)
+    if ((ctx->prof.score_mask >> p) & 1u) {
+      rows->raw[p] = cap.raw + (size_t)p * N;
+      rows->norm[p] = cap.norm + (size_t)p * N;
+    }
+  rows->total = cap.total;
+  return KSG_OK;
 }
 
 int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base) {

@@ -66,6 +66,12 @@ class KsgCapture(C.Structure):
     _fields_ = [("fstatus", u32p), ("raw", i64p), ("norm", i64p), ("total", i64p)]
 
 
+class KsgEvalRows(C.Structure):
+    """ksg_eval_rows: the per-cycle rows in library memory."""
+    _fields_ = [("n_nodes", C.c_int32), ("elem_bytes", C.c_int32), ("fstatus", u32p),
+                ("raw", C.c_void_p * NPLUGINS), ("norm", C.c_void_p * NPLUGINS), ("total", C.c_void_p)]
+
+
 class KsgNodeState(C.Structure):
     _fields_ = [("requested", i64p), ("nonzero", i64p), ("pod_count", i32p)]
 
@@ -209,6 +215,9 @@ class Engine:
         self._load_nodes = f("load_nodes", C.c_int, vp, C.POINTER(KsgNodes), C.POINTER(KsgTopology))
         self._load_workload = f("load_workload", C.c_int, vp, C.POINTER(KsgWorkload))
         self._eval = f("eval", C.c_int, vp, C.c_int32, C.POINTER(KsgResult), C.POINTER(KsgCapture))
+        # the product library's zero-copy per-cycle call (the CPU oracle has none)
+        self._eval_view = (f("eval_view", C.c_int, vp, C.c_int32, C.POINTER(KsgResult), C.POINTER(KsgEvalRows))
+                           if hasattr(self.lib, self.PREFIX + "eval_view") else None)
         self._commit = f("commit", C.c_int, vp, C.c_int32, C.c_int32)
         self._run_queue = f("run_queue", C.c_int, vp, C.c_int32, C.c_int32, i32p, vp, C.POINTER(KsgCapture))
         self._read_state = f("read_state", C.c_int, vp, C.POINTER(KsgNodeState))
@@ -275,6 +284,23 @@ class Engine:
         r = KsgResult()
         self._check(self._eval(self.ctx, pod, C.byref(r), C.byref(capture.struct) if capture else None))
         return r
+
+    def eval_view(self, pod: int):
+        """ksg_eval_view: (result, {"fstatus": u32[N], "raw"/"norm": {plugin: int64[N]}, "total": int64[N]}),
+        copied out of the library's rows (valid there until the next evaluation)."""
+        r, v = KsgResult(), KsgEvalRows()
+        self._check(self._eval_view(self.ctx, pod, C.byref(r), C.byref(v)))
+        n = v.n_nodes
+        dt = np.int32 if v.elem_bytes == 4 else np.int64
+
+        def row(ptr):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int32 if dt is np.int32 else C.c_int64)),
+                                         (n,)).astype(np.int64)
+        out = {"fstatus": np.ctypeslib.as_array(v.fstatus, (n,)).copy(), "elem_bytes": v.elem_bytes,
+               "raw": {p: row(v.raw[p]) for p in range(NPLUGINS) if v.raw[p]},
+               "norm": {p: row(v.norm[p]) for p in range(NPLUGINS) if v.norm[p]},
+               "total": row(v.total)}
+        return r, out
 
     def append_pods(self, pods: np.ndarray, prog: np.ndarray, prog_base: int):
         """ksg_append_pods: pods (POD_DTYPE, absolute program offsets) whose

@@ -248,11 +248,19 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 	if _, err := e.snap.Sync(e.ctx); err != nil {
 		return nil, err
 	}
-	ev, err := e.ctx.Eval(idx)
+	st := &podState{pod: idx, index: make(map[string]int, len(e.nodes))}
+	// nominated pods first: their evaluations reuse the library's result
+	// block, which the pod's own evaluation below then keeps for the cycle
+	if nom != nil {
+		if err := e.nominatedPass(st, pod, nom); err != nil {
+			return nil, err
+		}
+	}
+	ev, err := e.ctx.EvalView(idx)
 	if err != nil {
 		return nil, err
 	}
-	st := &podState{pod: idx, ev: ev, index: make(map[string]int, len(e.nodes))}
+	st.ev = ev
 	for i, n := range e.nodes {
 		st.index[n] = i
 	}
@@ -266,11 +274,6 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 			return nil, err
 		}
 		st.pre[id] = preFilterResult{code: code, names: names}
-	}
-	if nom != nil {
-		if err := e.nominatedPass(st, pod, nom); err != nil {
-			return nil, err
-		}
 	}
 	cs.Write(stateKey, st)
 	return st, nil
@@ -499,8 +502,7 @@ func (b *base) score(cs *framework.CycleState, pod *v1.Pod, node string) (int64,
 	if s != nil {
 		return 0, s
 	}
-	n := len(st.ev.Total)
-	return st.ev.Raw[b.id*n+st.index[node]], nil
+	return st.ev.Raw(b.id, st.index[node]), nil
 }
 
 func (b *base) normalize(cs *framework.CycleState, scores framework.NodeScoreList) *framework.Status {
@@ -508,9 +510,8 @@ func (b *base) normalize(cs *framework.CycleState, scores framework.NodeScoreLis
 	if s != nil {
 		return s
 	}
-	n := len(st.ev.Total)
 	for k := range scores {
-		scores[k].Score = st.ev.Norm[b.id*n+st.index[scores[k].Name]]
+		scores[k].Score = st.ev.Norm(b.id, st.index[scores[k].Name])
 	}
 	return nil
 }

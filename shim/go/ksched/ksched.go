@@ -158,30 +158,81 @@ func (x *Ctx) LoadWorkload(pods []C.ksg_pod, prog []int32) error {
 }
 
 // PodEval is everything the wrapped plugins record for one pod, in SoA form.
+// From EvalView the rows stay in the library's pinned block (ksg_eval_view):
+// valid until the next evaluation on the context; from Eval they are copied
+// into Go memory.
 type PodEval struct {
 	Selected, NFeasible int
 	Status, ScoreSkip   uint32
 	FStatus             []uint32 // [n_nodes]
-	Raw, Norm           []int64  // [NPlugins][n_nodes]
-	Total               []int64  // [n_nodes]
+	n, elem             int
+	raw, norm           [NPlugins]unsafe.Pointer
+	total               unsafe.Pointer
+	keep                [][]int64 // Eval: the Go rows the pointers above refer to
 }
 
-// Eval runs the full per-pod sweep (filters in profile order with
+func (e *PodEval) at(p unsafe.Pointer, node int) int64 {
+	if p == nil {
+		return 0
+	}
+	if e.elem == 4 {
+		return int64(*(*int32)(unsafe.Add(p, 4*node)))
+	}
+	return *(*int64)(unsafe.Add(p, 8*node))
+}
+
+// Raw is plugin's Score() value at node (0 for a plugin the profile does not score).
+func (e *PodEval) Raw(plugin, node int) int64 { return e.at(e.raw[plugin], node) }
+
+// Norm is plugin's value after NormalizeScore at node.
+func (e *PodEval) Norm(plugin, node int) int64 { return e.at(e.norm[plugin], node) }
+
+// Total is the weighted sum at node (0: not scored).
+func (e *PodEval) Total(node int) int64 { return e.at(e.total, node) }
+
+// NumNodes is the number of node columns.
+func (e *PodEval) NumNodes() int { return e.n }
+
+// EvalView runs the full per-pod sweep (filters in profile order with
 // first-rejection exit, raw scores, normalisation, weighted totals, selectHost)
-// without changing node state.  One call per pod, at PreFilter time.
+// without changing node state, leaving the rows in library memory (no copy).
+// One call per pod, at PreFilter time.
+func (x *Ctx) EvalView(pod int) (*PodEval, error) {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	var res C.ksg_result
+	var rows C.ksg_eval_rows
+	if err := x.check(C.ksg_eval_view(x.c, C.int32_t(pod), &res, &rows)); err != nil {
+		return nil, err
+	}
+	e := &PodEval{n: int(rows.n_nodes), elem: int(rows.elem_bytes)}
+	e.FStatus = unsafe.Slice((*uint32)(unsafe.Pointer(rows.fstatus)), e.n)
+	for p := 0; p < NPlugins; p++ {
+		e.raw[p], e.norm[p] = unsafe.Pointer(rows.raw[p]), unsafe.Pointer(rows.norm[p])
+	}
+	e.total = unsafe.Pointer(rows.total)
+	e.Selected, e.NFeasible = int(res.selected), int(res.n_feasible)
+	e.Status, e.ScoreSkip = uint32(res.status), uint32(res.score_skip)
+	return e, nil
+}
+
+// Eval is EvalView with the rows copied into Go memory (they survive later
+// evaluations).
 func (x *Ctx) Eval(pod int) (*PodEval, error) {
 	x.mu.Lock()
 	defer x.mu.Unlock()
 	n := x.nN
-	e := &PodEval{
-		FStatus: make([]uint32, n), Raw: make([]int64, NPlugins*n),
-		Norm: make([]int64, NPlugins*n), Total: make([]int64, n),
-	}
+	fs, raw, norm, total := make([]uint32, n), make([]int64, NPlugins*n), make([]int64, NPlugins*n), make([]int64, n)
 	var res C.ksg_result
-	cap := C.ksg_capture{fstatus: pu32(e.FStatus), raw: p64(e.Raw), norm: p64(e.Norm), total: p64(e.Total)}
+	cap := C.ksg_capture{fstatus: pu32(fs), raw: p64(raw), norm: p64(norm), total: p64(total)}
 	if err := x.check(C.ksg_eval(x.c, C.int32_t(pod), &res, &cap)); err != nil {
 		return nil, err
 	}
+	e := &PodEval{FStatus: fs, n: n, elem: 8, keep: [][]int64{raw, norm, total}}
+	for p := 0; p < NPlugins; p++ {
+		e.raw[p], e.norm[p] = unsafe.Pointer(&raw[p*n]), unsafe.Pointer(&norm[p*n])
+	}
+	e.total = unsafe.Pointer(&total[0])
 	e.Selected, e.NFeasible = int(res.selected), int(res.n_feasible)
 	e.Status, e.ScoreSkip = uint32(res.status), uint32(res.score_skip)
 	return e, nil

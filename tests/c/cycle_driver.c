@@ -2,8 +2,8 @@
  * makes per scheduling cycle, in C, timed call by call with CLOCK_MONOTONIC,
  * so the measured cost is the C ABI's alone (no Python / ctypes in the loop):
  *
- *   ksg_snapshot_add_pod -> ksg_snapshot_sync -> ksg_eval (with capture)
- *   -> ksg_snapshot_statuses -> ksg_snapshot_assume
+ *   ksg_snapshot_add_pod -> ksg_snapshot_sync -> ksg_eval_view (the rows
+ *   in library memory) -> ksg_snapshot_statuses -> ksg_snapshot_assume
  *
  * Bench infrastructure, not product: links libksched.so only. */
 #include <stdint.h>
@@ -25,7 +25,7 @@ static int64_t now_ns(void) {
  * re-encoded.  Returns 0 or the failing call's code (negative), with *where
  * naming the phase. */
 int cycle_run(ksg_snapshot* s, ksg_ctx* ctx, const ksg_pod_view* views, int32_t n, int32_t warm,
-              ksg_capture* cap, int32_t n_nodes, int32_t* placed, int64_t* phase_ns, int32_t* appended,
+              ksg_eval_rows* rows, int32_t n_nodes, int32_t* placed, int64_t* phase_ns, int32_t* appended,
               int32_t* reloads, int32_t* where) {
   int32_t* code = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_nodes);
   int32_t* msg = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_nodes);
@@ -42,9 +42,9 @@ int cycle_run(ksg_snapshot* s, ksg_ctx* ctx, const ksg_pod_view* views, int32_t 
     const int64_t t1 = now_ns();
     if ((rc = ksg_snapshot_sync(s, ctx, &ap))) { *where = 1; break; }
     const int64_t t2 = now_ns();
-    if ((rc = ksg_eval(ctx, idx, &r, cap))) { *where = 2; break; }
+    if ((rc = ksg_eval_view(ctx, idx, &r, rows))) { *where = 2; break; }
     const int64_t t3 = now_ns();
-    if ((rc = ksg_snapshot_statuses(s, idx, cap->fstatus, n_nodes, code, msg, buf, cap_bytes, &n_msgs, &len))) {
+    if ((rc = ksg_snapshot_statuses(s, idx, rows->fstatus, n_nodes, code, msg, buf, cap_bytes, &n_msgs, &len))) {
       *where = 3;
       break;
     }

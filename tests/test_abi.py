@@ -43,7 +43,7 @@ def test_struct_layouts_match(tmp_path):
     src = tmp_path / "sz.c"
     names = ["ksg_nodes", "ksg_topology", "ksg_pod", "ksg_workload", "ksg_profile", "ksg_result",
              "ksg_capture", "ksg_node_state", "ksg_replica_summary", "ksg_kernel_stat", "ksg_names",
-             "ksg_annotate_in"]
+             "ksg_annotate_in", "ksg_eval_rows"]
     src.write_text('#include <stdio.h>\n#include "ksched.h"\nint main(void){' +
                    "".join(f'printf("%zu\\n", sizeof({n}));' for n in names) + "return 0;}")
     exe = tmp_path / "sz"
@@ -61,6 +61,7 @@ def test_struct_layouts_match(tmp_path):
     assert sizes["ksg_kernel_stat"] == ctypes.sizeof(native.KsgKernelStat)
     assert sizes["ksg_names"] == ctypes.sizeof(native.KsgNames)
     assert sizes["ksg_annotate_in"] == ctypes.sizeof(native.KsgAnnotateIn)
+    assert sizes["ksg_eval_rows"] == ctypes.sizeof(native.KsgEvalRows)
 
 
 def test_snapshot_view_layouts(tmp_path):

@@ -163,3 +163,29 @@ def test_cycles_from_an_empty_snapshot(built):
     q.load(enc, E.encode_profile(prof, enc.cluster.res_names))
     want, _ = q.run_queue(0, len(pods), results=False)
     np.testing.assert_array_equal(np.array(placed, np.int32), want)
+
+
+def test_eval_view_equals_eval_with_capture(gpu, built):
+    """ksg_eval_view leaves the rows in library memory: the same status words,
+    raw / normalised rows and totals as ksg_eval with capture buffers, on the
+    per-cycle path and (a topology pod) the queue kernel."""
+    import zoo
+    for nodes, pods, prof in (G.config2(n_nodes=1500, n_pods=30, seed=3), zoo.zoo(2, n_pods=40)):
+        enc = E.Encoder(nodes, pods, prof)
+        pf = E.encode_profile(prof, enc.cluster.res_names)
+        gpu.load(enc, pf)
+        rows = _score_rows(pf)
+        for i in range(len(pods)):
+            cap = native.CaptureBuffers(len(nodes), 1)
+            ra = gpu.eval(i, cap)
+            rv, v = gpu.eval_view(i)
+            assert (ra.selected, ra.n_feasible, ra.status, ra.score_skip) == (rv.selected, rv.n_feasible, rv.status,
+                                                                               rv.score_skip)
+            np.testing.assert_array_equal(cap.fstatus[0], v["fstatus"])
+            assert sorted(v["raw"]) == sorted(rows)
+            for p in rows:
+                np.testing.assert_array_equal(cap.raw[0, p], v["raw"][p])
+                np.testing.assert_array_equal(cap.norm[0, p], v["norm"][p])
+            np.testing.assert_array_equal(cap.total[0], v["total"])
+            if ra.selected >= 0:
+                gpu.commit(i, ra.selected)
