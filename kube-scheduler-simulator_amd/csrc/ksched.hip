@@ -262,6 +262,13 @@ struct BatchArgs {
   int32_t qs;
   uint32_t* tc_colinit;     // [carried slot][qs] column words of the carried nodes (ksg_tcol_carry)
   void* tc_init;            // [qs] TcInit: per-pod maxima / counters over the carried columns
+  // the window pipeline's top-k -> walk hand-off without a cross-stream event
+  // (run_pipe): the last top-k workgroup of batch b stores tk_seq = b + 1 into
+  // *tk_done; the walk of batch b polls it, then acquires.  Null: stream order.
+  unsigned* tk_arrive;      // top-k workgroups of this batch that finished (reset by the last)
+  unsigned* tk_done;
+  unsigned tk_seq;
+  unsigned* tk_timeout;     // set when the walk's poll gave up
 };
 
 // record: bit 63 feasible | rt (8 bits) << 48 | ra (16 bits) << 32 | partial (32 bits)
@@ -532,7 +539,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2_scan(BatchArgs a) {
 constexpr int kTopQ = 16;   // keys held in registers per lane (N <= 8192 at 512 lanes)
 
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
+__device__ __forceinline__ void batch_topk_body(const BatchArgs& a) {
   constexpr int NW = BLOCK / 64;
   constexpr long long BIG = 0x7fffffffffffffffll;
   __shared__ ksg_profile s_prof;
@@ -705,6 +712,23 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
   }
   uint64_t* out = a.top + (size_t)j * KSG_BATCH_MAX;
   for (int i = tid; i < K; i += BLOCK) out[i] = s_keys[i];
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
+  batch_topk_body<BLOCK>(a);
+  if (a.tk_done) {   // hand-off to the walk: every workgroup releases its outputs, the last one signals
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      using G1 = __attribute__((address_space(1))) unsigned;
+      const unsigned old = __hip_atomic_fetch_add((G1*)a.tk_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x - 1) {
+        __hip_atomic_store((G1*)a.tk_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((G1*)a.tk_done, a.tk_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // Phase 2: one workgroup walks the batch in queue order and keeps every node
@@ -1387,6 +1411,21 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
   int32_t* s_prog = s_dyn + cm_words + a.nb * POD_WORDS;
   int64_t* s_slot = reinterpret_cast<int64_t*>(s_dyn + ((cm_words + a.nb * POD_WORDS + a.prog_len + 3) & ~3));
 
+  if (a.tk_done) {   // this batch's top-k (second stream) is done: poll, then acquire
+    if (tid == 0) {
+      using G1 = __attribute__((address_space(1))) unsigned;
+      unsigned spins = 0;
+      while (__hip_atomic_load((G1*)a.tk_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.tk_seq) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {
+          __hip_atomic_store((G1*)a.tk_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
   for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
   for (int i = tid; i < a.nb * POD_WORDS; i += BLOCK)
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
@@ -2418,6 +2457,7 @@ struct ksg_ctx {
   char* h_ev = nullptr;                     // hipHostMalloc'd, freed by ksg_close
   size_t h_ev_bytes = 0;
   char* d_hev = nullptr;                    // h_ev's device address (the kernel writes the results there)
+  unsigned* pipe_tk = nullptr;              // the last run_pipe's top-k hand-off words (checked after the run)
   std::vector<uint32_t> view_fs;            // ksg_eval_view of a pod off the per-cycle path: library-owned rows
   std::vector<int64_t> view_rows;
   unsigned ev_seq = 0;                      // the per-cycle completion flag's last value
@@ -3006,7 +3046,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       if ((rc = dalloc(ctx, &ctx->d_ptop[q], (size_t)KSG_BATCH_MAX * KSG_BATCH_MAX))) return rc;
       HIPC(ctx, hipMemsetAsync(ctx->d_ppmax[q], 0, sizeof(int32_t) * 2 * KSG_BATCH_MAX, ctx->stream));
     }
-    if ((rc = dalloc(ctx, &ctx->d_carry, (size_t)2 * KSG_BATCH_MAX + 2))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_carry, (size_t)2 * KSG_BATCH_MAX + 6))) return rc;   // + carry_n[2], tk[4]
   }
   if (!ctx->stream2) {
     HIPC(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
@@ -3016,7 +3056,9 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     }
   }
   int32_t* carry_n = ctx->d_carry + 2 * KSG_BATCH_MAX;   // [2]
-  HIPC(ctx, hipMemsetAsync(carry_n, 0, 2 * sizeof(int32_t), ctx->stream));
+  unsigned* tk = reinterpret_cast<unsigned*>(carry_n + 2);   // top-k hand-off: arrive, done, timeout
+  ctx->pipe_tk = tk;
+  HIPC(ctx, hipMemsetAsync(carry_n, 0, 6 * sizeof(int32_t), ctx->stream));
   const bool window = ctx->pipe_window != 0;
   const bool overlap = window && !ctx->timing;
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
@@ -3122,6 +3164,14 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.carry_out = window ? ctx->d_carry + par * KSG_BATCH_MAX : nullptr;
     b.carry_out_n = window ? carry_n + par : nullptr;
     const double units = (double)nb * N;
+    // the walk waits for this batch's top-k: the slot walk polls a flag the
+    // last top-k workgroup stores (no cross-stream event in front of it on the
+    // critical stream); the transposed walk's kernels wait on an event
+    const bool tk_flag = overlap && !tcolw;
+    b.tk_arrive = tk_flag ? tk : nullptr;
+    b.tk_done = tk_flag ? tk + 1 : nullptr;
+    b.tk_timeout = tk_flag ? tk + 2 : nullptr;
+    b.tk_seq = (unsigned)bi + 1;
     // phase 1 of batch b reads the state as of the end of batch b - 2 at least,
     // and reuses the buffers phase 2 of batch b - 2 read
     if (overlap && bi >= 2) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev_p2[par], 0));
@@ -3133,7 +3183,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, s1, b);
       if ((rc = tlaunched(ctx, KSG_K_BATCH_TRANSPOSE, units))) return rc;
     }
-    if (overlap) {
+    if (overlap && !tk_flag) {
       HIPC(ctx, hipEventRecord(ctx->ev_tk[par], s1));
       HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
     }
@@ -3630,6 +3680,12 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
   if ((rc = tcollect(ctx))) return rc;
+  if (ctx->pipe_tk) {   // the window pipeline's top-k hand-off (run_pipe)
+    unsigned tkf[3] = {0, 0, 0};
+    HIPC(ctx, hipMemcpy(tkf, ctx->pipe_tk, sizeof(tkf), hipMemcpyDeviceToHost));
+    ctx->pipe_tk = nullptr;
+    if (tkf[2]) return fail(ctx, KSG_E_DEVICE, "batched path: top-k hand-off poll timed out");
+  }
   if (ctx->last_path == 4) {
     unsigned flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPC(ctx, hipMemcpy(flags, ctx->d_coop_flags, sizeof(flags), hipMemcpyDeviceToHost));
