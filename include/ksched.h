@@ -328,6 +328,7 @@ int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
 #define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
 #define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */
 #define KSG_RUN_TCOL 4           /* phase 2 was the transposed walk (ksg_batch_phase2t) */
+#define KSG_RUN_SPEC 8           /* phase 2 was the speculate-and-verify walk (ksg_batch_phase2v) */
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event
@@ -357,7 +358,8 @@ enum {
   KSG_K_BATCH_TRANSPOSE = 15,
   KSG_K_TCOL_CARRY = 16,
   KSG_K_EVAL_CYCLE = 17,
-  KSG_NKERNELS = 18
+  KSG_K_BATCH_PHASE2V = 18,
+  KSG_NKERNELS = 19
 };
 typedef struct ksg_kernel_stat {
   char name[48];

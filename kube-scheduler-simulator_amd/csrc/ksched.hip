@@ -1835,6 +1835,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 }
 
 #include "ksched_phase2t.h"
+#include "ksched_phase2v.h"
 #include "ksched_capture.h"
 #include "ksched_sweep.h"
 #include "ksched_cycle.h"
@@ -2427,6 +2428,7 @@ struct ksg_ctx {
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
+  bool last_spec = false;     // ... the speculate-and-verify walk
   uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
   int32_t* d_statt = nullptr;
   uint64_t* d_prect[2] = {nullptr, nullptr};   // the same, per window parity
@@ -2570,7 +2572,8 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
                                           "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
                                           "ksg_capture_eval", "ksg_capture_norm", "ksg_batch_phase2t",
-                                          "ksg_batch_transpose", "ksg_tcol_carry", "ksg_eval_cycle"};
+                                          "ksg_batch_transpose", "ksg_tcol_carry", "ksg_eval_cycle",
+                                          "ksg_batch_phase2v"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -2865,6 +2868,7 @@ static const std::array<const void*, 2>& tcol_kernels() {
   return k;
 }
 constexpr size_t kTcolLds = 128 * 1024;   // dynamic LDS of the transposed walk (static part ~14 KB)
+constexpr size_t kSpecLds = 120 * 1024;   // ... of the speculate-and-verify walk (static part ~16 KB)
 
 // Host half of the transposed walk's scope (ksched_phase2t.h): on top of the
 // N32 check, every weighted total fits the column word's 14 bits.
@@ -2940,6 +2944,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     }
   }
   ctx->last_tcol = tcol;
+  ctx->last_spec = false;
   if (tcol && !ctx->d_rect) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rect, (size_t)128 * N))) return rc;
@@ -3036,6 +3041,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const int N = ctx->c.N;
   int rc;
   ctx->last_tcol = false;
+  ctx->last_spec = false;
   if (!ctx->d_prec[0]) {
     for (int q = 0; q < 2; q++) {
       if ((rc = dalloc(ctx, &ctx->d_prec[q], (size_t)KSG_BATCH_MAX * N))) return rc;
@@ -3068,16 +3074,28 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   // two-version walk and a round-3 one-wave walk with two slots per lane, both
   // measured slower, were removed.)
   bool n32 = false;
-  if ((ctx->batch_mode == 4 || ctx->batch_mode == 5) && (rc = decide_n32(ctx, first, count, &n32))) return rc;
+  if (ctx->batch_mode >= 4 && (rc = decide_n32(ctx, first, count, &n32))) return rc;
   const bool tcolw = ctx->batch_mode == 5 && window && n32 && tcol_candidate(ctx);
-  const bool slotwalk = !tcolw;
+  // mode 6: the speculate-and-verify walk (ksched_phase2v.h), N32 scope, 64-pod batches
+  const bool specw = ctx->batch_mode == 6 && window && n32;
   ctx->last_tcol = tcolw;
+  ctx->last_spec = specw;
+  if ((tcolw || specw) && !ctx->d_prect[0]) {
+    for (int q = 0; q < 2; q++) {
+      if ((rc = dalloc(ctx, &ctx->d_prect[q], (size_t)64 * N))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_pstatt[q], (size_t)64 * N))) return rc;
+    }
+  }
+  if (specw) {
+    static bool sattr = false;
+    if (!sattr) {
+      HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2v<64 * kSvWaves>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSpecLds));
+      sattr = true;
+    }
+  }
   if (tcolw) {
-    if (!ctx->d_prect[0]) {
-      for (int q = 0; q < 2; q++) {
-        if ((rc = dalloc(ctx, &ctx->d_prect[q], (size_t)64 * N))) return rc;
-        if ((rc = dalloc(ctx, &ctx->d_pstatt[q], (size_t)64 * N))) return rc;
-      }
+    if (!ctx->d_tccol) {
       if ((rc = dalloc(ctx, &ctx->d_tccol, (size_t)64 * 64))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_tcinit, (size_t)4 * 64))) return rc;
     }
@@ -3088,12 +3106,12 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       tattr = true;
     }
   }
-  const int B = tcolw ? 64 : window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
+  const int B = tcolw || specw ? 64 : window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
   const int slots = window ? 2 * B : B;   // carried + this batch's slots
   const int sblock = slots <= 64 ? 64 : slots <= 128 ? 128 : 256;
   const void* kern = slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)];
   const int block = sblock;
-  const size_t kLdsBudget = tcolw ? kTcolLds : 120 * 1024;
+  const size_t kLdsBudget = tcolw ? kTcolLds : specw ? kSpecLds : 120 * 1024;
   const size_t slot_bytes = 8 * (size_t)(2 * slot_rm + 10);   // SlotLayout<RM>::STRIDE int64 words
   if (!tcolw && (rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
   BatchArgs b{};
@@ -3132,7 +3150,10 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
         lo = std::min<int64_t>(lo, q.blob);
         hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
       }
-      if (tcolw)   // slot rows + the [slot][64] column store for this batch's and the carried slots
+      if (specw)   // row versions + T as node indices ([pod][nb + carried])
+        bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
+                (size_t)kSvSlots * kSvRow * 8 + (size_t)64 * (nb + prev_nb) * 4;
+      else if (tcolw)   // slot rows + the [slot][64] column store for this batch's and the carried slots
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
                 (size_t)(nb + prev_nb) * (slot_bytes + 64 * 4);
       else
@@ -3149,9 +3170,9 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.prog_len = (int32_t)(hi - lo);
     b.rec = ctx->d_prec[par];
     b.img = ctx->d_pimg[par];
-    b.stat = (slotwalk || tcolw) && n32 ? ctx->d_pstat[par] : nullptr;
-    b.rect = tcolw ? ctx->d_prect[par] : nullptr;
-    b.statt = tcolw ? ctx->d_pstatt[par] : nullptr;
+    b.stat = n32 ? ctx->d_pstat[par] : nullptr;
+    b.rect = tcolw || specw ? ctx->d_prect[par] : nullptr;
+    b.statt = tcolw || specw ? ctx->d_pstatt[par] : nullptr;
     b.qs = 64;
     b.tc_colinit = ctx->d_tccol;
     b.tc_init = ctx->d_tcinit;
@@ -3167,27 +3188,35 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     // the walk waits for this batch's top-k: the slot walk polls a flag the
     // last top-k workgroup stores (no cross-stream event in front of it on the
     // critical stream); the transposed walk's kernels wait on an event
+    // (the speculate-and-verify walk also reads the transpose: the transpose signals)
     const bool tk_flag = overlap && !tcolw;
     b.tk_arrive = tk_flag ? tk : nullptr;
     b.tk_done = tk_flag ? tk + 1 : nullptr;
     b.tk_timeout = tk_flag ? tk + 2 : nullptr;
     b.tk_seq = (unsigned)bi + 1;
+    BatchArgs bt = b;   // the top-k launch: signals unless a transpose follows it
+    if (specw) bt.tk_done = nullptr;
     // phase 1 of batch b reads the state as of the end of batch b - 2 at least,
     // and reuses the buffers phase 2 of batch b - 2 read
     if (overlap && bi >= 2) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev_p2[par], 0));
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, nb), dim3(256), 0, s1, b);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return rc;
-    hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(nb), dim3(512), 0, s1, b);
+    hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(nb), dim3(512), 0, s1, bt);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return rc;
-    if (tcolw) {
-      hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, s1, b);
+    if (tcolw || specw) {
+      BatchArgs bx = b;
+      if (!specw) bx.tk_done = nullptr;
+      hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, s1, bx);
       if ((rc = tlaunched(ctx, KSG_K_BATCH_TRANSPOSE, units))) return rc;
     }
     if (overlap && !tk_flag) {
       HIPC(ctx, hipEventRecord(ctx->ev_tk[par], s1));
       HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
     }
-    if (tcolw) {   // the carried columns on the state after the previous walk, then the walk
+    if (specw) {
+      hipLaunchKernelGGL(ksg_batch_phase2v<64 * kSvWaves>, dim3(1), dim3(64 * kSvWaves), bytes, s2, b);
+      if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2V, 0.5 * nb * (nb + 1)))) return rc;
+    } else if (tcolw) {   // the carried columns on the state after the previous walk, then the walk
       hipLaunchKernelGGL(ksg_tcol_carry<1>, dim3(nb), dim3(64), 0, s2, b);
       if ((rc = tlaunched(ctx, KSG_K_TCOL_CARRY, (double)nb * prev_nb))) return rc;
       hipLaunchKernelGGL(ksg_batch_phase2t<1>, dim3(1), dim3(64), bytes, s2, b);
@@ -3630,7 +3659,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   }
   if (batched) {
     ctx->last_path = 2;
-    if ((ctx->batch_mode == 4 || (ctx->batch_mode == 5 && ctx->pipe_window)) && !want_cap) {
+    if ((ctx->batch_mode == 4 || (ctx->batch_mode >= 5 && ctx->pipe_window)) && !want_cap) {
       if ((rc = run_pipe(ctx, first, count, d_pl, d_res, d_prof))) return rc;
     } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, want_cap ? &ca : nullptr, d_prof))) {
       return rc;
@@ -4126,7 +4155,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_COOP_PMODE")) ctx->coop_pmode = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
-    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : 4;
+    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : m == "spec" ? 6 : 4;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
@@ -4680,7 +4709,7 @@ int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
   if (!ctx || !path || !flags) return KSG_E_INVALID;
   *path = ctx->last_path;
   *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0) |
-           (ctx->last_tcol ? KSG_RUN_TCOL : 0);
+           (ctx->last_tcol ? KSG_RUN_TCOL : 0) | (ctx->last_spec ? KSG_RUN_SPEC : 0);
   return KSG_OK;
 }
 

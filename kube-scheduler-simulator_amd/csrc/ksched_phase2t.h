@@ -356,6 +356,18 @@ __global__ __launch_bounds__(256) void ksg_batch_transpose(BatchArgs a) {
       a.statt[(size_t)n * qs + j] = s_s[j][nn];
     }
   }
+  if (a.tk_done) {   // the window's hand-off to the speculate-and-verify walk (as ksg_batch_topk's)
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      using G1 = __attribute__((address_space(1))) unsigned;
+      const unsigned old = __hip_atomic_fetch_add((G1*)a.tk_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x - 1) {
+        __hip_atomic_store((G1*)a.tk_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((G1*)a.tk_done, a.tk_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 template <int P>

@@ -98,7 +98,7 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
         return 140   # live columns of a carried node (128 B) + record and static (12 B) per (pod, carried node)
     if name == "ksg_batch_transpose":
         return 24   # 12 B read + 12 B written per (pod, node)
-    if name in ("ksg_batch_phase2", "ksg_batch_phase2s", "ksg_batch_phase2p", "ksg_batch_phase2t"):
+    if name in ("ksg_batch_phase2", "ksg_batch_phase2s", "ksg_batch_phase2p", "ksg_batch_phase2t", "ksg_batch_phase2v"):
         return 20
     if name in ("ksg_sweep_static", "ksg_sweep"):
         if not isinstance(cols, dict):
@@ -131,7 +131,7 @@ def dominant_kernel_roofline(kstats, bytes_per_eval):
             "bytes_per_launch": dom["bytes_per_launch"], "kernels": rows}
 
 
-PHASE2_KERNELS = ("ksg_batch_phase2s", "ksg_batch_phase2t", "ksg_batch_phase2p",
+PHASE2_KERNELS = ("ksg_batch_phase2s", "ksg_batch_phase2t", "ksg_batch_phase2v", "ksg_batch_phase2p",
                   "ksg_batch_phase2")
 
 

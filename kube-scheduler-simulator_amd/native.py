@@ -156,7 +156,7 @@ def make_profile(fields: dict) -> KsgProfile:
     return p
 
 
-RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL = 1, 2, 4   # ksg_last_run_info flags
+RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL, RUN_SPEC = 1, 2, 4, 8   # ksg_last_run_info flags
 
 
 class CaptureBuffers:

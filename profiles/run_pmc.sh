@@ -8,6 +8,10 @@ set -uo pipefail
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# a PMC pass prints nothing until it ends: keep a heartbeat under gpurun_out/
+( while sleep 45; do date >> "$OUT/heartbeat.txt"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0"
 S="python3 scripts/bench_configs.py --config 4 --replicas 1024 --pods 256 --reps 1 --no-cpu-baseline"
 SP="$S --no-timing"

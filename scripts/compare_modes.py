@@ -21,7 +21,8 @@ MODES = [("window", {"KSG_BATCH_MODE": "window"}),
          ("window-128", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "128"}),
          ("slot", {"KSG_BATCH_MODE": "slot"}), ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
          ("tcol", {"KSG_BATCH_MODE": "tcol"}),
-         ("tcol-nowindow-64", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"})]
+         ("tcol-nowindow-64", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"}),
+         ("spec", {"KSG_BATCH_MODE": "spec"})]
 
 
 def main():

@@ -36,7 +36,8 @@ import os
 MODES = {"window": ("window", {}), "window-timed": ("window", {"_timing": 1}),
          "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "window128": ("window", {"KSG_SLOT_BLOCK": 128}),
          "slot": ("slot", {}),
-         "tcol": ("tcol", {}), "tcol-nowindow64": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 64})}
+         "tcol": ("tcol", {}), "tcol-nowindow64": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 64}),
+         "spec": ("spec", {}), "spec-timed": ("spec", {"_timing": 1})}
 if os.environ.get("KSG_TEST_ALL_VARIANTS") == "1":
     MODES.update({"slot128": ("slot", {"KSG_SLOT_BLOCK": 128}), "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
                   "topset": ("topset", {}), "scan": ("scan", {}), "tcol-timed": ("tcol", {"_timing": 1}),
@@ -168,3 +169,31 @@ def test_tcol_out_of_scope_falls_back(oracle):
     path, flags = a.last_run_info()
     assert path == 2 and not flags & (native.RUN_TCOL | native.RUN_SLOT32)   # the int64 slot walk
     np.testing.assert_array_equal(pl, oracle.run_queue(0, len(pods))[0])
+
+
+# ---- the speculate-and-verify walk (KSG_RUN_SPEC) ---------------------------------
+@pytest.mark.parametrize("strategy,seed", [("least", 21), ("most", 21), ("least", 5)])
+def test_spec_runs_and_matches_oracle(oracle, strategy, seed):
+    """Config 2 runs phase 2 as the speculate-and-verify walk (ksched_phase2v.h).
+    LeastAllocated mostly speculates right; MostAllocated re-chooses the node
+    it packs, so nearly every pod is a mis-speculation corrected in its own
+    round: both exercise the rollback, the re-choice versions and the pointer
+    snapshots."""
+    P = pkg("profile")
+    nodes, pods, prof = G.config2(n_nodes=1500, n_pods=2500, seed=seed)
+    if strategy == "most":
+        prof = P.config2_profile(strategy=P.MOST_ALLOCATED)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = _engine_with_batch_mode("spec")
+    a.load(enc, pf)
+    oracle.load(enc, pf)
+    pl, res = a.run_queue(0, len(pods))
+    assert a.last_run_info() == (2, native.RUN_SLOT32 | native.RUN_SPEC)
+    po, ro = oracle.run_queue(0, len(pods))
+    np.testing.assert_array_equal(pl, po)
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(res[f], ro[f], err_msg=f)
+    R = len(enc.cluster.res_names)
+    for x, y in zip(a.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(x, y)
