@@ -536,16 +536,15 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2_scan(BatchArgs a) {
 // nodes change before pod j, so T_j always contains the best unchanged node.
 // The K-th largest key is found by a binary search over a dense key
 // ((total - tmin) * N + N - 1 - n), one block count per step.
-constexpr int kTopQ = 16;   // keys held in registers per lane (N <= 8192 at 512 lanes)
 
 template <int BLOCK>
 __device__ __forceinline__ void batch_topk_body(const BatchArgs& a) {
   constexpr int NW = BLOCK / 64;
+  constexpr int kTopQ = 8192 / BLOCK;   // totals held in registers per lane (N <= 8192)
   constexpr long long BIG = 0x7fffffffffffffffll;
   __shared__ ksg_profile s_prof;
   __shared__ long long s_r[NW][4];
   __shared__ int32_t s_i[NW][6];
-  __shared__ int32_t s_cnt[3];
   __shared__ int32_t s_pos;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int j = blockIdx.x;
@@ -553,7 +552,6 @@ __device__ __forceinline__ void batch_topk_body(const BatchArgs& a) {
   const int N = c.N;
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
-  if (tid < 3) s_cnt[tid] = 0;
   if (tid == 0) s_pos = 0;
   __syncthreads();
   const ksg_pod& p = a.pods[a.b0 + j];
@@ -649,69 +647,91 @@ __device__ __forceinline__ void batch_topk_body(const BatchArgs& a) {
     a.p1[j] = s;
   }
   if (K == 0) return;
-  // dense key: larger = better (higher total, then lower node index)
+  // dense key: larger = better (higher total, then lower node index); distinct per node
   auto dkey = [&](int64_t t, int n) -> int64_t { return (t - gmin) * (int64_t)N + (N - 1 - n); };
-  auto count_ge = [&](int64_t th) -> int32_t {
-    int32_t k = 0;
+  auto each_key = [&](auto&& f) {   // f(dense key, total, node) for every feasible node
 #pragma unroll
     for (int q = 0; q < kTopQ; q++) {
       const int n = tid + q * BLOCK;
-      k += (tot[q] != BIG && dkey(tot[q], n) >= th);
+      if (tot[q] != BIG) f(dkey(tot[q], n), tot[q], n);
     }
     for (int n = tid + kTopQ * BLOCK; n < N; n += BLOCK) {
       const uint64_t x = rec[n];
       uint32_t e = 0;
-      if (x >> 63) k += dkey(total_of(x, e), n) >= th;
+      if (x >> 63) {
+        const int64_t t = total_of(x, e);
+        f(dkey(t, n), t, n);
+      }
     }
-    return k;
   };
-  int64_t lo = 0, hi = dkey(gmax, 0);
-  for (int it = 0; lo < hi; it++) {
-    const int64_t mid = lo + (hi - lo + 1) / 2;
-    const int32_t k = wave_sum32(count_ge(mid));
-    if (lane == 0) atomicAdd(&s_cnt[it % 3], k);
+  // Radix select of the K-th largest dense key: 11-bit digits from the top
+  // (two levels at configs[1]'s ranges), one LDS histogram per level, the bin
+  // holding the K-th key found by one wave's suffix sums.
+  constexpr int RB = 11, NB = 1 << RB, PL = NB / 64;
+  __shared__ int32_t s_hist[NB];
+  __shared__ int32_t s_sel[2];   // selected bin, keys in higher bins
+  const int64_t dmax = dkey(gmax, 0);
+  const int top_bit = 64 - __builtin_clzll((unsigned long long)dmax | 1ull);
+  int64_t prefix = 0;   // the digits fixed so far (dkey >> (shift + RB))
+  int need = K;         // keys still to take at or below the prefix
+  for (int shift = ((top_bit - 1) / RB) * RB; shift >= 0; shift -= RB) {
+    for (int i = tid; i < NB; i += BLOCK) s_hist[i] = 0;
     __syncthreads();
-    const int32_t tot_k = s_cnt[it % 3];
-    if (tid == 0) s_cnt[(it + 2) % 3] = 0;
-    if (tot_k >= K) lo = mid;
-    else hi = mid - 1;
+    each_key([&](int64_t d, int64_t, int) {
+      if (shift + RB >= 63 || (d >> (shift + RB)) == prefix) atomicAdd(&s_hist[(d >> shift) & (NB - 1)], 1);
+    });
+    __syncthreads();
+    if (wv == 0) {
+      int32_t h[PL];
+      int32_t sum = 0;
+#pragma unroll
+      for (int i = 0; i < PL; i++) {
+        h[i] = s_hist[lane * PL + i];
+        sum += h[i];
+      }
+      int32_t suf = sum;   // keys in this lane's bins and every higher lane's
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t v = __shfl_down(suf, o, 64);
+        if (lane + o < 64) suf += v;
+      }
+      const int32_t above = suf - sum;
+      if (above < need && suf >= need) {
+        int32_t acc = above, b = lane * PL;
+#pragma unroll
+        for (int i = PL - 1; i >= 0; i--) {
+          if (acc + h[i] >= need) {
+            b = lane * PL + i;
+            break;
+          }
+          acc += h[i];
+        }
+        s_sel[0] = b;
+        s_sel[1] = acc;
+      }
+    }
+    __syncthreads();
+    prefix = (prefix << RB) | s_sel[0];
+    need -= s_sel[1];
   }
-  // collect the K keys (dense keys are distinct, so exactly K pass) and sort
-  // them descending in LDS: phase 2 takes the first entry outside C.
+  const int64_t thr = prefix;   // the K-th largest dense key: exactly K keys are >= it
+  // collect the K keys, then sort them descending by rank (phase 2 takes the
+  // first entry outside C): a key's position is the number of larger keys
   __shared__ uint64_t s_keys[KSG_BATCH_MAX];
-  for (int i = tid; i < KSG_BATCH_MAX; i += BLOCK) s_keys[i] = 0;
-  __syncthreads();
-  auto emit = [&](int64_t t, int n) {
-    if (dkey(t, n) >= lo) {
+  each_key([&](int64_t d, int64_t t, int n) {
+    if (d >= thr) {
       const int pos = atomicAdd(&s_pos, 1);
       if (pos < KSG_BATCH_MAX) s_keys[pos] = argmax_key(t, n);
     }
-  };
-#pragma unroll
-  for (int q = 0; q < kTopQ; q++) {
-    const int n = tid + q * BLOCK;
-    if (tot[q] != BIG) emit(tot[q], n);
-  }
-  for (int n = tid + kTopQ * BLOCK; n < N; n += BLOCK) {
-    const uint64_t x = rec[n];
-    uint32_t e = 0;
-    if (x >> 63) emit(total_of(x, e), n);
-  }
+  });
   __syncthreads();
-  static_assert(BLOCK >= KSG_BATCH_MAX / 2, "one compare-exchange per lane per step");
-  for (int k = 2; k <= KSG_BATCH_MAX; k <<= 1) {     // bitonic sort, descending
-    for (int m = k >> 1; m > 0; m >>= 1) {
-      if (tid < KSG_BATCH_MAX / 2) {
-        const int i = 2 * tid - (tid & (m - 1)), l = i + m;   // i has bit m clear
-        const uint64_t x = s_keys[i], y = s_keys[l];
-        const bool desc = (i & k) == 0;
-        if (desc ? x < y : x > y) { s_keys[i] = y; s_keys[l] = x; }
-      }
-      __syncthreads();
-    }
-  }
   uint64_t* out = a.top + (size_t)j * KSG_BATCH_MAX;
-  for (int i = tid; i < K; i += BLOCK) out[i] = s_keys[i];
+  for (int i = tid; i < K; i += BLOCK) {
+    const uint64_t x = s_keys[i];
+    int r = 0;
+    for (int m = 0; m < K; m++) r += s_keys[m] > x ? 1 : 0;
+    out[r] = x;
+  }
 }
 
 template <int BLOCK>
@@ -2429,6 +2449,7 @@ struct ksg_ctx {
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
   bool last_spec = false;     // ... the speculate-and-verify walk
+  bool spec_transpose = true;   // env KSG_SPEC_TRANSPOSE: the spec walk reads node-major copies of the records (70 vs 83 us per walk without)
   uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
   int32_t* d_statt = nullptr;
   uint64_t* d_prect[2] = {nullptr, nullptr};   // the same, per window parity
@@ -2868,7 +2889,7 @@ static const std::array<const void*, 2>& tcol_kernels() {
   return k;
 }
 constexpr size_t kTcolLds = 128 * 1024;   // dynamic LDS of the transposed walk (static part ~14 KB)
-constexpr size_t kSpecLds = 120 * 1024;   // ... of the speculate-and-verify walk (static part ~16 KB)
+constexpr size_t kSpecLds = 128 * 1024;   // ... of the speculate-and-verify walk (static part ~14 KB)
 
 // Host half of the transposed walk's scope (ksched_phase2t.h): on top of the
 // N32 check, every weighted total fits the column word's 14 bits.
@@ -2877,6 +2898,15 @@ bool tcol_candidate(const ksg_ctx* ctx) {
   for (int pl = 0; pl < KSG_NPLUGINS; pl++)
     if ((ctx->prof.score_mask >> pl) & 1u) wsum += ctx->prof.weight[pl];
   return ctx->c.R <= 4 && wsum * 100 < (1 << 14);
+}
+
+// Host half of the speculate-and-verify walk's scope (ksched_phase2v.h): on top
+// of the N32 check, every weighted total fits the column word's 27 bits.
+bool spec_candidate(const ksg_ctx* ctx) {
+  int64_t wsum = 0;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if ((ctx->prof.score_mask >> pl) & 1u) wsum += ctx->prof.weight[pl];
+  return ctx->c.R <= 4 && wsum * 100 < (1 << kSvTotalBits);
 }
 
 int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const CapArgs* cap,
@@ -2988,7 +3018,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, b);
     if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return trc;
     if (topset) {
-      hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(b.nb), dim3(512), 0, ctx->stream, b);
+      hipLaunchKernelGGL(ksg_batch_topk<1024>, dim3(b.nb), dim3(1024), 0, ctx->stream, b);
       if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
       // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
       if (tcol) {
@@ -3077,7 +3107,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   if (ctx->batch_mode >= 4 && (rc = decide_n32(ctx, first, count, &n32))) return rc;
   const bool tcolw = ctx->batch_mode == 5 && window && n32 && tcol_candidate(ctx);
   // mode 6: the speculate-and-verify walk (ksched_phase2v.h), N32 scope, 64-pod batches
-  const bool specw = ctx->batch_mode == 6 && window && n32;
+  const bool specw = ctx->batch_mode == 6 && window && n32 && spec_candidate(ctx);
   ctx->last_tcol = tcolw;
   ctx->last_spec = specw;
   if ((tcolw || specw) && !ctx->d_prect[0]) {
@@ -3152,7 +3182,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       }
       if (specw)   // row versions + T as node indices ([pod][nb + carried])
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
-                (size_t)kSvSlots * kSvRow * 8 + (size_t)64 * (nb + prev_nb) * 4;
+                (size_t)kSvSlots * kSvRow * 8 + (size_t)kSvSlots * 64 * 4 + (size_t)64 * (nb + prev_nb) * 4;
       else if (tcolw)   // slot rows + the [slot][64] column store for this batch's and the carried slots
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
                 (size_t)(nb + prev_nb) * (slot_bytes + 64 * 4);
@@ -3171,8 +3201,9 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.rec = ctx->d_prec[par];
     b.img = ctx->d_pimg[par];
     b.stat = n32 ? ctx->d_pstat[par] : nullptr;
-    b.rect = tcolw || specw ? ctx->d_prect[par] : nullptr;
-    b.statt = tcolw || specw ? ctx->d_pstatt[par] : nullptr;
+    const bool xpose = tcolw || (specw && ctx->spec_transpose);
+    b.rect = xpose ? ctx->d_prect[par] : nullptr;
+    b.statt = xpose ? ctx->d_pstatt[par] : nullptr;
     b.qs = 64;
     b.tc_colinit = ctx->d_tccol;
     b.tc_init = ctx->d_tcinit;
@@ -3195,15 +3226,15 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.tk_timeout = tk_flag ? tk + 2 : nullptr;
     b.tk_seq = (unsigned)bi + 1;
     BatchArgs bt = b;   // the top-k launch: signals unless a transpose follows it
-    if (specw) bt.tk_done = nullptr;
+    if (specw && xpose) bt.tk_done = nullptr;
     // phase 1 of batch b reads the state as of the end of batch b - 2 at least,
     // and reuses the buffers phase 2 of batch b - 2 read
     if (overlap && bi >= 2) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev_p2[par], 0));
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, nb), dim3(256), 0, s1, b);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return rc;
-    hipLaunchKernelGGL(ksg_batch_topk<512>, dim3(nb), dim3(512), 0, s1, bt);
+    hipLaunchKernelGGL(ksg_batch_topk<1024>, dim3(nb), dim3(1024), 0, s1, bt);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return rc;
-    if (tcolw || specw) {
+    if (xpose) {
       BatchArgs bx = b;
       if (!specw) bx.tk_done = nullptr;
       hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, s1, bx);
@@ -4158,6 +4189,7 @@ int ksg_open(int device, ksg_ctx** out) {
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : m == "spec" ? 6 : 4;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
+  if (const char* f = getenv("KSG_SPEC_TRANSPOSE")) ctx->spec_transpose = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);

@@ -1,74 +1,91 @@
-// Phase 2, speculate-and-verify walk (KSG_BATCH_MODE=spec), included by
-// ksched.hip after ksched_phase2t.h (it reuses the transposed walk's N32
-// column evaluation: TcPod / TcRow / tc_eval).
+// Phase 2, speculate-and-verify walk (KSG_BATCH_MODE=spec, the default for
+// runs in its scope), included by ksched.hip after ksched_phase2t.h (it reuses
+// the transposed walk's N32 column evaluation: TcPod / TcRow / tc_eval).
 //
 // The slot walk and the transposed walk both put one exact evaluation of a
 // changed node on every pod's critical path.  On configs[1] about 97 % of the
 // pods take their best UNCHANGED node (the first entry of the top set T_j
 // outside the changed set D_j), which needs no evaluation at all: it follows
-// from the top sets and from which nodes earlier pods took.  So each round:
+// from the top sets and from which nodes earlier pods took.  So the batch runs
+// in rounds, each round from `start` (the first undecided pod):
 //
-//   1. speculate (wave 0, lane q = pod q): from `start` on, every pod takes its
-//      best unchanged node.  Lane q keeps a pointer into T_q (staged in LDS)
-//      past every entry already in D; per pod k one v_readlane gives d_k, the
-//      lanes whose candidate is d_k step their pointer on (LDS reads of T and
-//      of the changed bitmap).  No evaluation on this chain.  Every lane's
-//      pointer is snapshotted per step (a rollback restores it).
-//   2. versions (all waves): pod k's assume onto d_k creates a new slot with
-//      one row version, node d_k's live columns + pod k's deltas (one global
-//      fetch per word, one thread per (pod, word)).
-//   3. verify (all waves, lane = pod): every row version v of every changed
-//      slot (carried slots' live rows, earlier rounds' committed versions,
-//      this round's speculated ones) is visible to the pods in (t_v, t_next];
-//      each wave evaluates its versions for all 64 pods at once (the N32
-//      Fit / BalancedAllocation of tc_eval, phase-1 records from the
-//      node-major copies) and folds them into per-pod LDS maxima and counters
-//      (ds_max_u64 / ds_add_u32).
-//   4. check (wave 0): each pod's exact decision from its counters, best column
+//   S  speculate (wave 0, lane q = pod q): every pod takes its best unchanged
+//      node.  Lane q keeps a pointer into T_q (staged in LDS) past every entry
+//      already in D; per pod k one v_readlane gives d_k, the lanes whose
+//      candidate is d_k step their pointer on (the next entry is read ahead;
+//      one LDS read of the changed bitmap per step-on).  No evaluation on this
+//      chain.  Every decision is published through an LDS progress counter, and
+//      every lane's pointer is snapshotted per step (a rollback restores it).
+//   V  verify, pipelined behind S (waves 1..7, lane = pod): each published
+//      decision is a new row version of a node (its live columns + the pod's
+//      deltas); a consumer wave fetches the row and evaluates the version for
+//      all 64 pods at once (tc_eval's N32 Fit / BalancedAllocation, phase-1
+//      records from the node-major copies) into a per-(slot, pod) column word.
+//      Round 1 also evaluates the carried slots (the previous batch's nodes).
+//      Column words of versions committed in earlier rounds stay valid, so a
+//      round evaluates only its new versions.
+//   A  aggregate (all waves): per pod, over every slot present at its turn, the
+//      best live column key and the counters (phase-1 feasible, live, lost
+//      TaintToleration / NodeAffinity maximum holders).
+//   C  check (wave 0): each pod's exact decision from its counters, best column
 //      and best unchanged key, exactly as the slot walk decides it.  The first
 //      pod k* whose decision differs from the speculated one (or that needs the
 //      renormalisation rescan) ends the round: pods before it are committed,
 //      k*'s exact decision is applied (a new version of an existing slot, or a
-//      new slot), the speculated slots after it are dropped, and the next
-//      round speculates from k* + 1 with the pointers restored from k*'s
-//      snapshot.
+//      new slot, evaluated as the next round's first item), the speculated
+//      slots after it are dropped, and the next round speculates from k* + 1
+//      with the pointers restored from k*'s snapshot.
 //
 // Every decision equals the sequential one: a pod's decision is committed only
 // after verification against the state every earlier committed decision left,
 // and k*'s decision is computed from that same verified state.  Results equal
 // the slot walk's and the oracle's bit for bit.
 //
-// Scope (host: run_pipe, mode 6): the transposed walk's (N32 ranges, compact
-// Fit / BalancedAllocation profile, <= 64-pod batches in the two-batch window).
+// Scope (host: spec_candidate): N32 ranges, the compact Fit /
+// BalancedAllocation profile, weighted totals < 2^27 (column words), <= 64-pod
+// batches in the two-batch window.
 
-constexpr int kSvWaves = 16;                  // 1024 lanes
+constexpr int kSvWaves = 12;                  // wave 0 speculates (then verifies), 1..11 verify
 constexpr int kSvSlots = 2 * 64;              // carried (<= previous batch) + this batch's
 constexpr int kSvRow = SlotLayout<4>::STRIDE; // int64 words per LDS row
+constexpr int kSvTotalBits = 27;
 
 __device__ __forceinline__ bool sv_changed(const uint32_t* cm, int n) { return ((cm[n >> 5] >> (n & 31)) & 1u) != 0; }
+
+// column word: total (27 bits) | live << 27 | phase-1 feasible << 28 | held the
+// phase-1 TaintToleration maximum << 29 | ... NodeAffinity << 30 | present << 31
+__device__ __forceinline__ uint32_t sv_word(int32_t total, bool live, bool p1f, bool ft, bool fa) {
+  return ((uint32_t)total & ((1u << kSvTotalBits) - 1)) | (live ? 1u << 27 : 0u) | (p1f ? 1u << 28 : 0u) |
+         (ft ? 1u << 29 : 0u) | (fa ? 1u << 30 : 0u) | (1u << 31);
+}
+
+// A queue entry of the verification: a row version to evaluate.
+struct SvItem {
+  int32_t node, slot, v;   // node, its slot, the version index (row stored at s_vrow[v])
+  int32_t src;             // row source: a version index, or -1 (the node's live columns in global memory)
+  int32_t t;               // the pod whose assume made the version (-1: none, the carried live row)
+};
 
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   using SL = SlotLayout<4>;
   constexpr int NW = BLOCK / 64;
   constexpr int SW = SL::W;
-  static_assert(BLOCK == 64 * kSvWaves && SW == 16 && 64 * SW == BLOCK, "one thread per (pod, row word)");
+  static_assert(BLOCK == 64 * kSvWaves && SW == 16, "spec walk layout");
   extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
   __shared__ ksg_profile s_prof;
   __shared__ __attribute__((aligned(16))) TcU s_u[64];
   __shared__ ksg_result s_res[64];
   __shared__ int32_t s_clist[kSvSlots];   // node of slot (-1: a hole, pod without a node)
   __shared__ int32_t s_lastv[kSvSlots];   // newest version of slot
-  __shared__ int32_t s_vslot[kSvSlots];   // slot of version (-1: hole)
   __shared__ int32_t s_vt[kSvSlots];      // pod whose assume made the version (-1: carried live row)
-  __shared__ int32_t s_vnext[kSvSlots];   // next version of the same slot, -1 if newest
   __shared__ int32_t s_dec[64];           // pod's node (speculated, then committed)
-  __shared__ int32_t s_dslot[64];         // slot of s_dec, -1 if none
   __shared__ uint64_t s_bu[64];           // pod's best unchanged key (0: none)
-  __shared__ uint64_t s_best[64];         // verification: best live column key
-  __shared__ uint32_t s_cnt[64];          // verification: p1 feasible | live << 8 | lost taint << 16 | lost aff << 24
+  __shared__ uint64_t s_best[64];         // aggregate: best live column key
+  __shared__ uint32_t s_cnt[64];          // aggregate: p1 feasible | live << 8 | lost taint << 16 | lost aff << 24
   __shared__ uint8_t s_snap[64 * 64];     // [step][pod] T pointer before the step's conflicts
-  __shared__ int32_t s_ctl[4];            // round control: next start, k*
+  __shared__ SvItem s_item[64 + 1];       // a round's special items: carried slots / the correction
+  __shared__ int32_t s_ctl[8];            // round: start, nv_c, ns_c, n_special; progress; next item
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const DevCluster& c = a.c;
@@ -81,8 +98,12 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
   int32_t* s_prog = s_dyn + cm_words + nb * POD_WORDS;
   int64_t* s_vrow = reinterpret_cast<int64_t*>(s_dyn + ((cm_words + nb * POD_WORDS + a.prog_len + 3) & ~3));
-  int32_t* s_top = reinterpret_cast<int32_t*>(s_vrow + (size_t)kSvSlots * kSvRow);   // [64][KT] nodes
+  uint32_t* s_col = reinterpret_cast<uint32_t*>(s_vrow + (size_t)kSvSlots * kSvRow);   // [slot][64]
+  int32_t* s_top = reinterpret_cast<int32_t*>(s_col + (size_t)kSvSlots * 64);         // [64][KT] nodes
 
+#ifdef KSG_STAMPS
+  unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
+#endif
   if (a.tk_done) {   // this batch's phase 1 / top-k / transpose (second stream) are done: poll, then acquire
     if (tid == 0) {
       using G1 = __attribute__((address_space(1))) unsigned;
@@ -99,43 +120,73 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
-  for (int i = tid; i < nb * POD_WORDS; i += BLOCK)
-    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
-  for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
+  {   // every staging load issued before the first LDS store
+    constexpr int PI = (64 * POD_WORDS + BLOCK - 1) / BLOCK;
+    int32_t pw[PI];
+#pragma unroll
+    for (int it = 0; it < PI; it++) {
+      const int i = tid + it * BLOCK;
+      pw[it] = i < nb * POD_WORDS ? reinterpret_cast<const int32_t*>(a.pods + a.b0)[i] : 0;
+    }
+#pragma unroll
+    for (int it = 0; it < PI; it++) {
+      const int i = tid + it * BLOCK;
+      if (i < nb * POD_WORDS) reinterpret_cast<int32_t*>(s_pods)[i] = pw[it];
+    }
+  }
+  for (int i0 = 0; i0 < a.prog_len; i0 += 4 * BLOCK) {
+    int32_t g[4];
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+      const int i = i0 + tid + it * BLOCK;
+      g[it] = i < a.prog_len ? a.prog[a.prog_lo + i] : 0;
+    }
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+      const int i = i0 + tid + it * BLOCK;
+      if (i < a.prog_len) s_prog[i] = g[it];
+    }
+  }
   for (int i = tid; i < (int)(sizeof(ksg_profile) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(&s_prof)[i] = reinterpret_cast<const int32_t*>(a.prof)[i];
   bool fit_filter_on = false;
   for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
-  // T as node indices, [pod][KT]
-  for (int x = tid; x < nb * KT; x += BLOCK) {
-    const int q = x / KT, i = x - q * KT;
-    const int K = a.p1[q].K;
-    s_top[x] = i < K ? key_node(a.top[(size_t)q * KSG_BATCH_MAX + i]) : -1;
+  {   // T as node indices, [pod][KT] (every key and K load issued before the first store)
+    constexpr int TI = (64 * kSvSlots + BLOCK - 1) / BLOCK;
+    uint64_t key[TI];
+    int32_t kk[TI];
+#pragma unroll
+    for (int it = 0; it < TI; it++) {
+      const int x = tid + it * BLOCK, q = x / KT, i = x - q * KT;
+      const bool ok = x < nb * KT;
+      key[it] = ok ? a.top[(size_t)q * KSG_BATCH_MAX + i] : 0;
+      kk[it] = ok ? a.p1[q].K : 0;
+    }
+#pragma unroll
+    for (int it = 0; it < TI; it++) {
+      const int x = tid + it * BLOCK, q = x / KT, i = x - q * KT;
+      if (x < nb * KT) s_top[x] = i < kk[it] ? key_node(key[it]) : -1;
+    }
   }
+  // carried slots: slot t = version t = carried node t, evaluated as round 1's
+  // special items (their rows come from global memory)
   const int nc0 = a.carry ? *a.carry_n : 0;
-  // carried slots: version t = slot t = the live row of carried node t
-  for (int x = tid; x < nc0 * SW; x += BLOCK) {
-    const int t = x / SW, w = x - t * SW;
-    const int d = a.carry[t];
-    s_vrow[(size_t)t * kSvRow + w] = slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, w, R, d), w, R);
-    if (w == 0) {
-      s_clist[t] = d;
-      s_lastv[t] = t;
-      s_vslot[t] = t;
-      s_vt[t] = -1;
-      s_vnext[t] = -1;
+  if (tid < 64) {
+    const int d = a.carry && tid < nc0 ? a.carry[tid] : 0;
+    if (tid < nc0) {
+      s_clist[tid] = d;
+      s_lastv[tid] = tid;
+      s_vt[tid] = -1;
+      s_item[tid] = SvItem{d, tid, tid, -1, -1};
     }
   }
   __syncthreads();
   const ksg_profile& prof = s_prof;
   const TcProf cm = tc_prof(cm_prof(prof));
-  const bool ipa_filter = ipa_in_filter(prof);
-  const bool ipa_score = ((prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) != 0;
-  for (int t = tid; t < nc0; t += BLOCK) atomicOr(&s_cmask[a.carry[t] >> 5], 1u << (a.carry[t] & 31));
-  // lane q's pod (every wave: the verification evaluates for every pod)
-  const int qq = lane < nb ? lane : 0;
-  const TcPod hp = tc_pod(s_pods[qq], prof, a.p1[qq], fit_filter_on, R);
+  if (tid < nc0) atomicOr(&s_cmask[s_clist[tid] >> 5], 1u << (s_clist[tid] & 31));
   if (wv == 0 && lane < nb) {
+    const bool ipa_filter = ipa_in_filter(prof);
+    const bool ipa_score = ((prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) != 0;
     const ksg_pod& p = s_pods[lane];
     const P1Stats s1 = a.p1[lane];
     const uint32_t smask = prof.score_mask & ~p.score_skip;
@@ -160,10 +211,18 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     u.pad[0] = u.pad[1] = u.pad[2] = 0;
     s_u[lane] = u;
   }
+  if (tid == 0) {
+    s_ctl[0] = 0;     // start
+    s_ctl[1] = nc0;   // committed versions
+    s_ctl[2] = nc0;   // committed slots
+    s_ctl[3] = nc0;   // special items of round 1: the carried slots
+    s_ctl[4] = 0;     // progress: speculation steps published
+    s_ctl[6] = 0;     // next verification item to take
+  }
   __syncthreads();
   // initial pointers: T_q's first entry outside the carried nodes (wave w: pods w, w + NW, ...)
   for (int q = wv; q < nb; q += NW) {
-    const int K = a.p1[q].K;
+    const int K = s_u[q].K;
     int ptr = K;
     for (int b = 0; b < K && ptr == K; b += 64) {
       const int i = b + lane;
@@ -175,103 +234,208 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   }
   __syncthreads();
 
-  // This lane's pod's row delta word `w` (the assume: requested += req, nonzero, pod count)
+  // pod t's row delta word `w` (the assume: requested += req, nonzero, pod count)
   auto delta_word = [&](const TcU& u, int w) -> int64_t {
     const int rl = (w >> 1) & 3;
     const int64_t req_l = rl == 0 ? u.req[0] : rl == 1 ? u.req[1] : rl == 2 ? u.req[2] : u.req[3];
     return w < 8 ? ((w & 1) ? req_l : 0) : w == SL::NZC ? u.nzc : w == SL::NZM ? u.nzm : w == SL::PODS ? 1 : 0;
   };
+  // lane q's pod (consumer waves evaluate every version for every pod)
+  const int qq = lane < nb ? lane : 0;
+  const TcPod hp = tc_pod(s_pods[qq], prof, a.p1[qq], fit_filter_on, R);
+  // Evaluate one row version for every pod into its slot's column words (a
+  // consumer wave).  Pods after t see it; a new slot is absent for the pods up
+  // to t; a re-choice leaves the earlier pods their previous version's words.
+  // Split in two so that the next item's loads are in flight while this one
+  // is evaluated: issue() starts the loads, finish() evaluates.
+  struct Pending {
+    SvItem it;
+    uint64_t x;    // pod lane's phase-1 record at the node
+    int32_t st;    // pod lane's static part of the total at the node
+    int64_t wd;    // row word `lane` (lanes < SW) before the pod's delta
+  };
+  auto issue = [&](const SvItem& it) -> Pending {
+    Pending p{it, 0, 0, 0};
+    if (it.node < 0) return p;
+    // the node-major copies (ksg_batch_transpose), else the pod-major arrays (KSG_SPEC_TRANSPOSE=0)
+    p.x = a.rect ? a.rect[(size_t)it.node * 64 + lane] : a.rec[(size_t)lane * N + it.node];
+    p.st = a.statt ? a.statt[(size_t)it.node * 64 + lane] : a.stat[(size_t)lane * N + it.node];
+    const int wl = lane < SW ? lane : 0;
+    p.wd = it.src >= 0 ? s_vrow[(size_t)it.src * kSvRow + wl]
+                       : slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, wl, R, it.node), wl, R);
+    return p;
+  };
+  auto finish = [&](const Pending& p) {
+    const SvItem& it = p.it;
+    if (it.node < 0) return;
+    if (lane < SW) s_vrow[(size_t)it.v * kSvRow + lane] = p.wd + (it.t >= 0 ? delta_word(s_u[it.t], lane) : 0);
+    int64_t w[SW];
+    {
+      const int4* src = reinterpret_cast<const int4*>(s_vrow + (size_t)it.v * kSvRow);
+#pragma unroll
+      for (int k = 0; k < SW / 2; k++) reinterpret_cast<int4*>(w)[k] = src[k];
+    }
+    const TcRow row = tc_row(cm, w);
+    const bool p1f = (p.x >> 63) != 0;
+    const bool ft = p1f && (int32_t)((p.x >> 48) & 0xff) == hp.mt;
+    const bool fa = p1f && (int32_t)((p.x >> 32) & 0xffff) == hp.ma;
+    int32_t fb = 0;
+    const bool live = tc_eval(cm, hp, row, fb) && p1f;
+    if (lane > it.t) s_col[it.slot * 64 + lane] = sv_word(p.st + fb, live, p1f, ft, fa);
+    else if (it.src < 0) s_col[it.slot * 64 + lane] = 0u;
+  };
 
-  int start = 0;
-  int nv_c = nc0, ns_c = nc0;   // committed versions / slots (uniform)
-  // wave 0's speculation state: lane q's pointer into T_q and its node (-1: none)
-  int ptr = 0, cnode = -1;
+  // wave 0's speculation state: lane q's pointer into T_q, its node (-1: none)
+  // and the entry after it (read ahead: a step-on costs one LDS round trip)
+  int ptr = 0, cnode = -1, nnode = -1;
   if (wv == 0 && lane < nb) {
     ptr = s_snap[lane];
-    cnode = ptr < s_u[lane].K ? s_top[lane * KT + ptr] : -1;
+    const int K = s_u[lane].K;
+    cnode = ptr < K ? s_top[lane * KT + ptr] : -1;
+    nnode = ptr + 1 < K ? s_top[lane * KT + ptr + 1] : -1;
   }
+  int start = 0, nv_c = nc0, ns_c = nc0, nspecial = nc0;
   int guard = 0;
+  KSG_STAMP(0);
   while (start < nb && guard++ <= nb) {
-    // ---- 1. speculate (wave 0) ---------------------------------------------------
+#ifdef KSG_STAMPS
+    if (tid == 0) st_acc[15] += 1;   // rounds
+#endif
     if (wv == 0) {
+      // ---- S: speculate, publishing each step ---------------------------------------
+      // (the chain's wave issues first where it shares a SIMD with a consumer)
+      __builtin_amdgcn_s_setprio(3);
+      if (lane >= start && lane < nb) {
+        s_best[lane] = 0;
+        s_cnt[lane] = 0;
+      }
       const int Kq = lane < nb ? s_u[lane].K : 0;
+      const uint64_t lanes_lt_nb = nb >= 64 ? ~0ull : (1ull << nb) - 1;
       for (int k = start; k < nb; k++) {
         s_snap[k * 64 + lane] = (uint8_t)ptr;
         const int d = __builtin_amdgcn_readlane(cnode, k);
+#ifdef KSG_STAMPS
+        if (tid == 0) st_acc[14] += 1;   // speculation steps
+#endif
+        if (lane == 0) {   // publish: LDS executes a wave's DS instructions in order, so a
+                           // consumer that sees the progress sees s_dec / s_snap (no wait here)
+          // (relaxed workgroup-scope atomics on the __shared__ words: plain ds_write_b32;
+          // a volatile cast would lose the address space and become a flat store + vmcnt wait)
+          __hip_atomic_store(&s_dec[k], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (d >= 0) atomicOr(&s_cmask[d >> 5], 1u << (d & 31));
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          __hip_atomic_store(&s_ctl[4], k - start + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         if (d < 0) continue;
-        if (lane == 0) s_cmask[d >> 5] |= 1u << (d & 31);
-        bool conflict = lane > k && lane < nb && cnode == d;
-        while (__ballot(conflict)) {
+        // lanes after k holding d (a wave-uniform mask: no divergent branch when it is empty)
+        uint64_t m = __ballot(cnode == d) & lanes_lt_nb & (~1ull << k);
+        bool conflict = (m >> lane) & 1ull;
+        while (m) {
+#ifdef KSG_STAMPS
+          if (tid == 0) st_acc[13] += 1;   // step-on iterations
+#endif
           if (conflict) {
             ptr++;
-            cnode = ptr < Kq ? s_top[lane * KT + ptr] : -1;
+            cnode = nnode;
+            nnode = ptr + 1 < Kq ? s_top[lane * KT + ptr + 1] : -1;
             conflict = cnode >= 0 && sv_changed(s_cmask, cnode);
           }
+          m = __ballot(conflict);
         }
       }
+      __builtin_amdgcn_s_setprio(0);
+      KSG_STAMP(1);
     }
-    __syncthreads();
-    // ---- 2. this round's versions: thread (pod k, word w) ------------------------
     {
-      const int k = tid >> 4, w = tid & 15;
-      if (k >= start && k < nb) {
+      // ---- V: verify behind the speculation (waves 1.., and wave 0 once S is done) ------
+      // items are taken in order from an LDS counter (load balance across the
+      // waves); items [0, nspecial): s_item (carried slots / the correction); then
+      // pod k = start + (i - nspecial) once the speculation published it (a
+      // hole, node -1, when the pod took no node).  take(): 1 taken, 0 not
+      // published yet (only when !wait), -1 past the end.
+      auto take = [&](int i, bool wait, SvItem& it) -> int {
+        if (i < nspecial) {
+          it = s_item[i];
+          return 1;
+        }
+        const int k = start + (i - nspecial);
+        if (k >= nb) return -1;
+        // (bounded: every step is published, the bound only keeps a fault from hanging the launch)
+        for (unsigned spins = 0;
+             __hip_atomic_load(&s_ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k - start; spins++) {
+          if (!wait) return 0;
+          if (spins >= (1u << 24)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int d = s_dec[k];
+        const int sl = ns_c + (k - start), v = nv_c + (k - start);
         const int pk = s_snap[k * 64 + k];
-        const int d = pk < s_u[k].K ? s_top[k * KT + pk] : -1;
-        const int v = nv_c + (k - start), s = ns_c + (k - start);
-        if (d >= 0) {
-          const int64_t base = slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, w, R, d), w, R);
-          s_vrow[(size_t)v * kSvRow + w] = base + delta_word(s_u[k], w);
-        }
-        if (w == 0) {
-          s_dec[k] = d;
-          s_dslot[k] = d >= 0 ? s : -1;
-          s_bu[k] = d >= 0 ? a.top[(size_t)k * KSG_BATCH_MAX + pk] : 0;
-          s_clist[s] = d;
-          s_lastv[s] = v;
-          s_vslot[v] = d >= 0 ? s : -1;
+        if (lane == 0) {
+          s_clist[sl] = d;
+          s_lastv[sl] = v;
           s_vt[v] = k;
-          s_vnext[v] = -1;
-          s_best[k] = 0;
-          s_cnt[k] = 0;
+          s_bu[k] = d >= 0 ? a.top[(size_t)k * KSG_BATCH_MAX + pk] : 0;
+        }
+        it = SvItem{d, sl, v, -1, k};
+        return 1;
+      };
+      auto grab = [&]() -> int {
+        int i = 0;
+        if (lane == 0) i = atomicAdd(&s_ctl[6], 1);
+        return __builtin_amdgcn_readfirstlane(i);
+      };
+      SvItem ia, ib;
+      int xa = grab();
+      int ra = take(xa, true, ia);
+      Pending pa = issue(ia), pb;
+      while (ra > 0) {
+        const int xb = grab();
+        int rb = take(xb, false, ib);
+        if (rb > 0) pb = issue(ib);
+        finish(pa);
+        if (rb == 0) {
+          rb = take(xb, true, ib);
+          if (rb > 0) pb = issue(ib);
+        }
+        if (rb < 0) break;
+        xa = grab();
+        ra = take(xa, false, ia);
+        if (ra > 0) pa = issue(ia);
+        finish(pb);
+        if (ra == 0) {
+          ra = take(xa, true, ia);
+          if (ra > 0) pa = issue(ia);
         }
       }
+      KSG_STAMP(2);
     }
     __syncthreads();
-    const int nv = nv_c + (nb - start);
-    // ---- 3. verify: wave w evaluates versions w, w + NW, ... for every pod --------
+    KSG_STAMP(3);
+    // ---- A: aggregate every slot present at each pod's turn (wave w: slots w, w + NW, ...)
     {
-      const bool mine = lane < nb && lane >= start;
-      for (int v = wv; v < nv; v += NW) {
-        const int s = s_vslot[v];
-        if (s < 0) continue;
-        const int t_lo = s_vt[v], vn = s_vnext[v];
-        const int t_hi = vn >= 0 ? s_vt[vn] : nb - 1;
-        if (t_hi < start) continue;
+      const int ns = ns_c + (nb - start);
+      const bool mine = lane >= start && lane < nb;
+      uint32_t dc = 0;   // this wave's slots, in registers; one LDS atomic per pod at the end
+      uint64_t bk = 0;
+      for (int s = wv; s < ns; s += NW) {
         const int node = s_clist[s];
-        const uint64_t x = a.rect[(size_t)node * 64 + lane];
-        const int32_t stat = a.statt[(size_t)node * 64 + lane];
-        int64_t w[SW];
-        {
-          const int4* src = reinterpret_cast<const int4*>(s_vrow + (size_t)v * kSvRow);
-#pragma unroll
-          for (int i = 0; i < SW / 2; i++) reinterpret_cast<int4*>(w)[i] = src[i];
-        }
-        const TcRow row = tc_row(cm, w);
-        const bool act = mine && lane > t_lo && lane <= t_hi;
-        const bool p1f = (x >> 63) != 0;
-        const bool ft = p1f && (int32_t)((x >> 48) & 0xff) == hp.mt;
-        const bool fa = p1f && (int32_t)((x >> 32) & 0xffff) == hp.ma;
-        int32_t fb = 0;
-        const bool live = tc_eval(cm, hp, row, fb) && p1f;
-        const uint32_t dc = (p1f ? 1u : 0u) + (live ? 1u << 8 : 0u) + (p1f && !live && ft ? 1u << 16 : 0u) +
-                            (p1f && !live && fa ? 1u << 24 : 0u);
-        if (act && dc) atomicAdd(&s_cnt[lane], dc);
-        if (act && live) atomicMax(reinterpret_cast<unsigned long long*>(&s_best[lane]),
-                                   (unsigned long long)argmax_key(stat + fb, node));
+        if (node < 0) continue;
+        const uint32_t e = s_col[s * 64 + lane];
+        const bool pres = (e >> 31) != 0;
+        const bool live = pres && ((e >> 27) & 1u), p1f = pres && ((e >> 28) & 1u);
+        const bool ft = (e >> 29) & 1u, fa = (e >> 30) & 1u;
+        dc += (p1f ? 1u : 0u) + (live ? 1u << 8 : 0u) + (p1f && !live && ft ? 1u << 16 : 0u) +
+              (p1f && !live && fa ? 1u << 24 : 0u);
+        const uint64_t key = live ? argmax_key((int64_t)(e & ((1u << kSvTotalBits) - 1)), node) : 0;
+        bk = key > bk ? key : bk;
       }
+      if (mine && dc) atomicAdd(&s_cnt[lane], dc);
+      if (mine && bk) atomicMax(reinterpret_cast<unsigned long long*>(&s_best[lane]), (unsigned long long)bk);
     }
     __syncthreads();
-    // ---- 4. check + commit (wave 0) ------------------------------------------------
+    KSG_STAMP(4);
+    // ---- C: check + commit (wave 0) ------------------------------------------------
     if (wv == 0) {
       const bool mine = lane < nb && lane >= start;
       const TcU u = s_u[lane < nb ? lane : 0];
@@ -301,6 +465,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
       if (mine && lane >= ks && spec >= 0) atomicAnd(&s_cmask[spec >> 5], ~(1u << (spec & 31)));
       nv_c += ks - start;
       ns_c += ks - start;
+      nspecial = 0;
       if (ks < nb) {
         const int k = ks;
         const TcU uk = s_u[k];
@@ -371,35 +536,23 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
             const uint64_t mk = __ballot(b + lane < ns_c && s_clist[b + lane] == selected);
             if (mk) idx = b + __builtin_ctzll(mk);
           }
-        const int v = nv_c;
-        if (selected >= 0) {
-          const int s = idx >= 0 ? idx : ns_c;
-          if (lane < SW) {
-            const int64_t base = idx >= 0 ? s_vrow[(size_t)s_lastv[idx] * kSvRow + lane]
-                                          : slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, lane, R, selected),
-                                                                     lane, R);
-            s_vrow[(size_t)v * kSvRow + lane] = base + delta_word(uk, lane);
-          }
+        if (selected >= 0) {   // the corrected version: the next round's first item
+          const int s = idx >= 0 ? idx : ns_c, v = nv_c;
           if (lane == 0) {
-            if (idx >= 0) s_vnext[s_lastv[idx]] = v;
-            else {
+            s_item[0] = SvItem{selected, s, v, idx >= 0 ? s_lastv[idx] : -1, k};
+            if (idx < 0) {
               s_clist[s] = selected;
               s_cmask[selected >> 5] |= 1u << (selected & 31);
             }
             s_lastv[s] = v;
-            s_vslot[v] = s;
             s_vt[v] = k;
-            s_vnext[v] = -1;
-            s_dec[k] = selected;
-            s_dslot[k] = s;
           }
+          nspecial = 1;
           nv_c += 1;
           if (idx < 0) ns_c += 1;
-        } else if (lane == 0) {
-          s_dec[k] = -1;
-          s_dslot[k] = -1;
         }
         if (lane == 0) {
+          s_dec[k] = selected;
           const bool sc = (status & KSG_ST_SCORED) != 0;
           ksg_result res;
           res.selected = selected;
@@ -412,29 +565,50 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
         if (lane > k && lane < nb) {
           ptr = s_snap[k * 64 + lane];
           cnode = ptr < u.K ? s_top[lane * KT + ptr] : -1;
+          nnode = ptr + 1 < u.K ? s_top[lane * KT + ptr + 1] : -1;
           // a new node taken by pod k (the rescan's choice): lanes holding it step on
           bool conflict = selected >= 0 && idx < 0 && cnode == selected;
           while (conflict) {
             ptr++;
-            cnode = ptr < u.K ? s_top[lane * KT + ptr] : -1;
+            cnode = nnode;
+            nnode = ptr + 1 < u.K ? s_top[lane * KT + ptr + 1] : -1;
             conflict = cnode >= 0 && sv_changed(s_cmask, cnode);
           }
         }
       }
-      if (lane == 0) s_ctl[0] = ks < nb ? ks + 1 : nb;
-      if (lane == 0) s_ctl[1] = nv_c;
-      if (lane == 0) s_ctl[2] = ns_c;
+      if (lane == 0) {
+        s_ctl[0] = ks < nb ? ks + 1 : nb;
+        s_ctl[1] = nv_c;
+        s_ctl[2] = ns_c;
+        s_ctl[3] = nspecial;
+        s_ctl[4] = 0;
+        s_ctl[6] = 0;
+      }
     }
+    KSG_STAMP(5);
     __syncthreads();
+    KSG_STAMP(6);
     start = s_ctl[0];
     nv_c = s_ctl[1];
     ns_c = s_ctl[2];
+    nspecial = s_ctl[3];
   }
   if (tid == 0 && start < nb && a.tk_timeout) {   // cannot happen: each round commits >= 1 pod
     using G1 = __attribute__((address_space(1))) unsigned;
     __hip_atomic_store((G1*)a.tk_timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // ---- epilogue: rows, results, count tables, carry-out -----------------------------
+  // (a correction left as the last round's item has its row written here)
+  if (nspecial && wv == 0) {
+    const SvItem it = s_item[0];
+    if (lane < SW) {
+      int64_t wd = it.src >= 0 ? s_vrow[(size_t)it.src * kSvRow + lane]
+                               : slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, lane, R, it.node), lane, R);
+      wd += delta_word(s_u[it.t], lane);
+      s_vrow[(size_t)it.v * kSvRow + lane] = wd;
+    }
+  }
+  __syncthreads();
   for (int x = tid; x < ns_c * SW; x += BLOCK) {
     const int s = x / SW, w = x - s * SW, node = s_clist[s];
     if (node < 0) continue;
@@ -448,10 +622,12 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     if (a.results) a.results[a.out0 + i] = s_res[i];
   }
   for (int i = tid; i < 2 * nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
-  if (tid == 0) {   // PodTopologySpread / InterPodAffinity count tables of the committed pods
+  uint64_t cmt = 0;   // pods with count-table updates (PodTopologySpread / InterPodAffinity selectors)
+  if (wv == 0) cmt = __ballot(lane < nb && s_res[lane].selected >= 0 && (s_u[lane].flags & 8u));
+  if (tid == 0 && cmt) {
     for (int k = 0; k < nb; k++) {
+      if (!((cmt >> k) & 1ull)) continue;
       const int sel = s_res[k].selected;
-      if (sel < 0 || !(s_u[k].flags & 8u)) continue;
       const ksg_pod& p = s_pods[k];
       const int32_t* cw = s_prog + (p.commit - a.prog_lo);
       const int ns = *cw++;
@@ -478,4 +654,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     }
     if (lane == 0) *a.carry_out_n = base;
   }
+  KSG_STAMP(7);
+#ifdef KSG_STAMPS
+  if (tid == 0 && a.stamps)
+    for (int i = 0; i < 16; i++) atomicAdd(&a.stamps[i], st_acc[i]);
+#endif
 }

@@ -41,6 +41,17 @@ if mode == "tcol":
     for i in range(0, 7):
         print(f"  {names[i]:36s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
     sys.exit(0)
+if mode == "spec":
+    names = ["setup (LDS staging, initial pointers)", "S: speculate + publish (wave 0)", "V: wave 0 verifying after S",
+             "barrier (other waves still verifying)", "A: aggregate + barrier", "C: check + commit (wave 0)",
+             "barrier", "epilogue"]
+    print(f"[spec] {n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build); "
+          f"rounds per batch {st[15] / max(1, (n_pods + 63) // 64):.2f}, speculation steps per batch "
+          f"{st[14] / max(1, (n_pods + 63) // 64):.1f}, step-on iterations per batch {st[13] / max(1, (n_pods + 63) // 64):.1f}")
+    tot = sum(st[0:8])
+    for i in range(0, 8):
+        print(f"  {names[i]:40s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
+    sys.exit(0)
 if mode in ("slot", "window"):
     names = ["(start)", "X: speculate + issue next-pod loads", "X: changed node + DPP reductions",
              "Y: barrier 1 + decide (+renorm)", "Y: row update + results", "barrier 2",

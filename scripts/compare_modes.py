@@ -22,7 +22,8 @@ MODES = [("window", {"KSG_BATCH_MODE": "window"}),
          ("slot", {"KSG_BATCH_MODE": "slot"}), ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
          ("tcol", {"KSG_BATCH_MODE": "tcol"}),
          ("tcol-nowindow-64", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"}),
-         ("spec", {"KSG_BATCH_MODE": "spec"})]
+         ("spec", {"KSG_BATCH_MODE": "spec"}),
+         ("spec-xpose", {"KSG_BATCH_MODE": "spec", "KSG_SPEC_TRANSPOSE": "1"})]
 
 
 def main():
@@ -34,7 +35,7 @@ def main():
     nodes, pods, prof = G.config2(n_nodes=a.nodes, n_pods=a.pods)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
-    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK")
+    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK", "KSG_SPEC_TRANSPOSE")
     want = set(a.modes.split(","))
     ref = None
     for name, env in MODES:
