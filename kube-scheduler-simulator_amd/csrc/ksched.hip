@@ -2458,10 +2458,11 @@ struct ksg_ctx {
   uint64_t* d_tcinit = nullptr;                // TcInit [64] (4 words each)
   unsigned* d_flag = nullptr; // range-check flag (ksg_range32)
   // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 4 "window", 5 "tcol" (the transposed
-  // walk where the N32 check and tcol_candidate pass, else the slot walk)
-  // (default: the slot walk with the next batch's phase 1 + top-k overlapped
+  // walk where the N32 check and tcol_candidate pass, else the slot walk), 6 "spec"
+  // (default: the speculate-and-verify walk where the N32 check and spec_candidate pass,
+  // else the window slot walk; both with the next batch's phase 1 + top-k overlapped
   // through the two-batch window)
-  int batch_mode = 4;
+  int batch_mode = 6;
   int slot_block = 64;   // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (64: the window walk at 64-pod batches, 2 waves, 416 k vs 408 k pods/s at 128, profiles/r2/phase2_window_blocks.log)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
@@ -3744,7 +3745,8 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     unsigned tkf[3] = {0, 0, 0};
     HIPC(ctx, hipMemcpy(tkf, ctx->pipe_tk, sizeof(tkf), hipMemcpyDeviceToHost));
     ctx->pipe_tk = nullptr;
-    if (tkf[2]) return fail(ctx, KSG_E_DEVICE, "batched path: top-k hand-off poll timed out");
+    if (tkf[2] == 1) return fail(ctx, KSG_E_DEVICE, "batched path: top-k hand-off poll timed out");
+    if (tkf[2]) return fail(ctx, KSG_E_DEVICE, "batched path: speculate-and-verify walk invariant broken");
   }
   if (ctx->last_path == 4) {
     unsigned flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};

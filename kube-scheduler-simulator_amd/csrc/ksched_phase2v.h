@@ -257,6 +257,14 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   auto issue = [&](const SvItem& it) -> Pending {
     Pending p{it, 0, 0, 0};
     if (it.node < 0) return p;
+    if (it.node >= N) {   // cannot happen; never load through it (reported as code 3)
+      p.it.node = -1;
+      if (lane == 0 && a.tk_timeout) {
+        using G1 = __attribute__((address_space(1))) unsigned;
+        __hip_atomic_store((G1*)a.tk_timeout, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return p;
+    }
     // the node-major copies (ksg_batch_transpose), else the pod-major arrays (KSG_SPEC_TRANSPOSE=0)
     p.x = a.rect ? a.rect[(size_t)it.node * 64 + lane] : a.rec[(size_t)lane * N + it.node];
     p.st = a.statt ? a.statt[(size_t)it.node * 64 + lane] : a.stat[(size_t)lane * N + it.node];
@@ -354,6 +362,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
       // hole, node -1, when the pod took no node).  take(): 1 taken, 0 not
       // published yet (only when !wait), -1 past the end.
       auto take = [&](int i, bool wait, SvItem& it) -> int {
+        it = SvItem{-1, 0, 0, -1, -1};   // (a hole unless filled below: never issue() an unset item)
         if (i < nspecial) {
           it = s_item[i];
           return 1;
@@ -388,7 +397,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
       SvItem ia, ib;
       int xa = grab();
       int ra = take(xa, true, ia);
-      Pending pa = issue(ia), pb;
+      Pending pa = issue(ia), pb = issue(SvItem{-1, 0, 0, -1, -1});
       while (ra > 0) {
         const int xb = grab();
         int rb = take(xb, false, ib);
