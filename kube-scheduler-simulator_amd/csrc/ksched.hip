@@ -260,6 +260,12 @@ struct BatchArgs {
   uint64_t* rect;
   int32_t* statt;
   int32_t qs;
+  // speculate-and-verify walk (ksched_phase2v.h): phase 1 itself writes the
+  // node-major copies rect and imgt ([N][64], weight x ImageLocality) from a
+  // 1-D XCD-ordered grid (every pod of a node tile on one XCD, so the partial
+  // lines of a node's row merge in that XCD's L2); no transpose launch
+  int32_t* imgt;
+  int32_t xcd_grid;
   uint32_t* tc_colinit;     // [carried slot][qs] column words of the carried nodes (ksg_tcol_carry)
   void* tc_init;            // [qs] TcInit: per-pod maxima / counters over the carried columns
   // the window pipeline's top-k -> walk hand-off without a cross-stream event
@@ -285,20 +291,32 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
   __shared__ ksg_profile s_prof;
   __shared__ int32_t s_mt[4], s_ma[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int j = blockIdx.y;
   const DevCluster& c = a.c;
   const int N = c.N;
+  int j = blockIdx.y, tile = blockIdx.x;
+  if (a.xcd_grid) {   // block b: XCD b % 8; all nb pods of tile t run on XCD t % 8
+    const int b = blockIdx.x, w = b >> 3;
+    j = w % a.nb;
+    tile = (w / a.nb) * 8 + (b & 7);
+    if (tile * 256 >= N) return;
+  }
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();
   const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog);
-  const int n = blockIdx.x * 256 + tid;
+  const int n = tile * 256 + tid;
   int32_t mt = 0, ma = 0;
   if (n < N) {
     const NodeEval e = eval_node(c, s_prof, v, a.st.requested, a.st.nonzero, a.st.pod_count, n, nullptr, nullptr);
-    a.rec[(size_t)j * N + n] = pack_rec(e);
-    a.img[(size_t)j * N + n] = e.st == 0 ? (int32_t)e.img : 0;
+    const uint64_t r = pack_rec(e);
+    const int32_t im = e.st == 0 ? (int32_t)e.img : 0;
+    a.rec[(size_t)j * N + n] = r;
+    a.img[(size_t)j * N + n] = im;
+    if (a.imgt) {
+      a.rect[(size_t)n * 64 + j] = r;
+      a.imgt[(size_t)n * 64 + j] = im;
+    }
     if (e.st == 0) { mt = (int32_t)e.rt; ma = (int32_t)e.ra; }
   }
   mt = (int32_t)wave_max64(mt);
@@ -2449,7 +2467,9 @@ struct ksg_ctx {
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
   bool last_spec = false;     // ... the speculate-and-verify walk
-  bool spec_transpose = true;   // env KSG_SPEC_TRANSPOSE: the spec walk reads node-major copies of the records (70 vs 83 us per walk without)
+  bool pipe_overlap = true;   // env KSG_PIPE_OVERLAP=0: the window pipeline on one stream (same arithmetic;
+                              // for counter passes, which serialise kernels: a walk polling for the
+                              // other stream's top-k would wait out its poll bound)
   uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
   int32_t* d_statt = nullptr;
   uint64_t* d_prect[2] = {nullptr, nullptr};   // the same, per window parity
@@ -3097,7 +3117,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   ctx->pipe_tk = tk;
   HIPC(ctx, hipMemsetAsync(carry_n, 0, 6 * sizeof(int32_t), ctx->stream));
   const bool window = ctx->pipe_window != 0;
-  const bool overlap = window && !ctx->timing;
+  const bool overlap = window && !ctx->timing && ctx->pipe_overlap;
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
   // mode 4: the slot walk inside this pipeline (one lane per slot); mode 5:
   // the transposed walk (ksched_phase2t.h) with the previous batch's nodes as
@@ -3201,10 +3221,12 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.prog_len = (int32_t)(hi - lo);
     b.rec = ctx->d_prec[par];
     b.img = ctx->d_pimg[par];
-    b.stat = n32 ? ctx->d_pstat[par] : nullptr;
-    const bool xpose = tcolw || (specw && ctx->spec_transpose);
-    b.rect = xpose ? ctx->d_prect[par] : nullptr;
+    b.stat = n32 && !specw ? ctx->d_pstat[par] : nullptr;   // (the spec walk computes its statics)
+    const bool xpose = tcolw;   // the transpose launch (the spec walk's copies come from phase 1)
+    b.rect = xpose || specw ? ctx->d_prect[par] : nullptr;
     b.statt = xpose ? ctx->d_pstatt[par] : nullptr;
+    b.imgt = specw ? ctx->d_pstatt[par] : nullptr;
+    b.xcd_grid = specw ? 1 : 0;
     b.qs = 64;
     b.tc_colinit = ctx->d_tccol;
     b.tc_init = ctx->d_tcinit;
@@ -3226,18 +3248,20 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.tk_done = tk_flag ? tk + 1 : nullptr;
     b.tk_timeout = tk_flag ? tk + 2 : nullptr;
     b.tk_seq = (unsigned)bi + 1;
-    BatchArgs bt = b;   // the top-k launch: signals unless a transpose follows it
-    if (specw && xpose) bt.tk_done = nullptr;
+    BatchArgs bt = b;   // the top-k launch: signals (no transpose follows it in the spec walk)
     // phase 1 of batch b reads the state as of the end of batch b - 2 at least,
     // and reuses the buffers phase 2 of batch b - 2 read
     if (overlap && bi >= 2) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev_p2[par], 0));
-    hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, nb), dim3(256), 0, s1, b);
+    if (specw)
+      hipLaunchKernelGGL(ksg_batch_phase1, dim3(((((N + 255) / 256) + 7) & ~7) * nb), dim3(256), 0, s1, b);
+    else
+      hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, nb), dim3(256), 0, s1, b);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return rc;
     hipLaunchKernelGGL(ksg_batch_topk<1024>, dim3(nb), dim3(1024), 0, s1, bt);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return rc;
     if (xpose) {
       BatchArgs bx = b;
-      if (!specw) bx.tk_done = nullptr;
+      bx.tk_done = nullptr;
       hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, s1, bx);
       if ((rc = tlaunched(ctx, KSG_K_BATCH_TRANSPOSE, units))) return rc;
     }
@@ -4191,7 +4215,7 @@ int ksg_open(int device, ksg_ctx** out) {
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : m == "spec" ? 6 : 4;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
-  if (const char* f = getenv("KSG_SPEC_TRANSPOSE")) ctx->spec_transpose = atoi(f) != 0;
+  if (const char* f = getenv("KSG_PIPE_OVERLAP")) ctx->pipe_overlap = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);

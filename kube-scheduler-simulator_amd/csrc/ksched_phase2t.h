@@ -75,6 +75,8 @@ struct TcPod {
   int32_t wfit, wba;       // weights if the plugin scores this pod, else 0
   int32_t mt, ma;          // phase-1 maxima of the raw TaintToleration / NodeAffinity scores
   uint32_t mask;           // bits 0-3: Fit filter checks column r; bit 4: Fit filter on
+  int32_t wt, wa;          // TaintToleration / NodeAffinity weights if scored, else 0 (spec walk)
+  float inv_mt, inv_ma;    // qdiv32 estimates of 1 / mt, 1 / ma
 };
 
 // Pod k's batch-uniform values for the decision, the assume and its result:
@@ -183,6 +185,10 @@ __device__ __forceinline__ TcPod tc_pod(const ksg_pod& p, const ksg_profile& pro
   h.wba = (smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? (int32_t)prof.weight[KSG_PL_BALANCED_ALLOCATION] : 0;
   h.mt = s1.mt;
   h.ma = s1.ma;
+  h.wt = (smask & bit(KSG_PL_TAINT_TOLERATION)) ? (int32_t)prof.weight[KSG_PL_TAINT_TOLERATION] : 0;
+  h.wa = (smask & bit(KSG_PL_NODE_AFFINITY)) ? (int32_t)prof.weight[KSG_PL_NODE_AFFINITY] : 0;
+  h.inv_mt = s1.inv_mt;
+  h.inv_ma = s1.inv_ma;
   return h;
 }
 

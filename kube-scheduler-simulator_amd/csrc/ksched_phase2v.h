@@ -251,7 +251,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   struct Pending {
     SvItem it;
     uint64_t x;    // pod lane's phase-1 record at the node
-    int32_t st;    // pod lane's static part of the total at the node
+    int32_t st;    // pod lane's weight x ImageLocality at the node (the static part after finish's terms)
     int64_t wd;    // row word `lane` (lanes < SW) before the pod's delta
   };
   auto issue = [&](const SvItem& it) -> Pending {
@@ -265,9 +265,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
       }
       return p;
     }
-    // the node-major copies (ksg_batch_transpose), else the pod-major arrays (KSG_SPEC_TRANSPOSE=0)
-    p.x = a.rect ? a.rect[(size_t)it.node * 64 + lane] : a.rec[(size_t)lane * N + it.node];
-    p.st = a.statt ? a.statt[(size_t)it.node * 64 + lane] : a.stat[(size_t)lane * N + it.node];
+    // the node-major copies phase 1 wrote: record and weight x ImageLocality
+    p.x = a.rect[(size_t)it.node * 64 + lane];
+    p.st = a.imgt[(size_t)it.node * 64 + lane];
     const int wl = lane < SW ? lane : 0;
     p.wd = it.src >= 0 ? s_vrow[(size_t)it.src * kSvRow + wl]
                        : slot_word_value<4, true>(slot_word_fetch<4, true>(c, a.st, wl, R, it.node), wl, R);
@@ -287,9 +287,16 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     const bool p1f = (p.x >> 63) != 0;
     const bool ft = p1f && (int32_t)((p.x >> 48) & 0xff) == hp.mt;
     const bool fa = p1f && (int32_t)((p.x >> 32) & 0xffff) == hp.ma;
+    // the static part of the total: top-k's total_score terms under the phase-1
+    // maxima (TaintToleration 100 - 100 rt / mt, NodeAffinity 100 ra / ma, floor
+    // divisions; the same qdiv32 as the transposed walk)
+    const int32_t rt = (int32_t)((p.x >> 48) & 0xff), ra = (int32_t)((p.x >> 32) & 0xffff);
+    const int32_t nt = hp.mt != 0 ? 100 - qdiv32(100 * rt, hp.mt, hp.inv_mt) : 100;
+    const int32_t na = hp.ma != 0 ? qdiv32(100 * ra, hp.ma, hp.inv_ma) : ra;
+    const int32_t stat = p.st + hp.wt * nt + hp.wa * na;
     int32_t fb = 0;
     const bool live = tc_eval(cm, hp, row, fb) && p1f;
-    if (lane > it.t) s_col[it.slot * 64 + lane] = sv_word(p.st + fb, live, p1f, ft, fa);
+    if (lane > it.t) s_col[it.slot * 64 + lane] = sv_word(stat + fb, live, p1f, ft, fa);
     else if (it.src < 0) s_col[it.slot * 64 + lane] = 0u;
   };
 

@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 ( while sleep 45; do date >> "$OUT/heartbeat.txt"; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0"
+B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0 --cycle-pods 0"
 S="python3 scripts/bench_configs.py --config 4 --replicas 1024 --pods 256 --reps 1 --no-cpu-baseline"
 SP="$S --no-timing"
 run() {  # name, rocprof args..., -- command
@@ -24,8 +24,12 @@ run() {  # name, rocprof args..., -- command
 }
 if [ -z "${SKIP_BENCH:-}" ]; then
 run bench_kt --kernel-trace --stats --output-format csv -d "$OUT/bench_kt" -o run -- $B
+# counter passes serialise kernels: the window pipeline on one stream (same
+# arithmetic), else each walk would wait out its poll for the other stream
+export KSG_PIPE_OVERLAP=0
 run bench_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/bench_fetch" -o run -- $B
 run bench_write --pmc WRITE_SIZE --output-format csv -d "$OUT/bench_write" -o run -- $B
+unset KSG_PIPE_OVERLAP
 fi
 run sweep_kt --kernel-trace --stats --output-format csv -d "$OUT/sweep_kt" -o run -- $S
 run sweep_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/sweep_fetch" -o run -- $SP

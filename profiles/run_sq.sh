@@ -6,7 +6,8 @@ set -uo pipefail
 OUT=${1:-gpurun_out/sq}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0"
+export KSG_PIPE_OVERLAP=0   # counter passes serialise kernels (see run_pmc.sh)
+B="python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0 --cycle-pods 0"
 timeout -s KILL 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 pass() {  # name, counters...
   local name=$1; shift
