@@ -2910,7 +2910,9 @@ static const std::array<const void*, 2>& tcol_kernels() {
   return k;
 }
 constexpr size_t kTcolLds = 128 * 1024;   // dynamic LDS of the transposed walk (static part ~14 KB)
-constexpr size_t kSpecLds = 128 * 1024;   // ... of the speculate-and-verify walk (static part ~14 KB)
+constexpr size_t kSpecLds = 140 * 1024;   // ... of the speculate-and-verify walk (static part ~16 KB): the
+                                          // launch always asks for all of it, so that no other kernel's
+                                          // workgroup shares the walk's CU
 
 // Host half of the transposed walk's scope (ksched_phase2t.h): on top of the
 // N32 check, every weighted total fits the column word's 14 bits.
@@ -3164,7 +3166,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const int block = sblock;
   const size_t kLdsBudget = tcolw ? kTcolLds : specw ? kSpecLds : 120 * 1024;
   const size_t slot_bytes = 8 * (size_t)(2 * slot_rm + 10);   // SlotLayout<RM>::STRIDE int64 words
-  if (!tcolw && (rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
+  if (!tcolw && (rc = set_phase2_attrs(ctx, 120 * 1024))) return rc;   // the slot-walk instances (fallback)
   BatchArgs b{};
   b.c = ctx->c;
   b.st = ctx->st;
@@ -3270,7 +3272,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
     }
     if (specw) {
-      hipLaunchKernelGGL(ksg_batch_phase2v<64 * kSvWaves>, dim3(1), dim3(64 * kSvWaves), bytes, s2, b);
+      hipLaunchKernelGGL(ksg_batch_phase2v<64 * kSvWaves>, dim3(1), dim3(64 * kSvWaves), kSpecLds, s2, b);
       if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2V, 0.5 * nb * (nb + 1)))) return rc;
     } else if (tcolw) {   // the carried columns on the state after the previous walk, then the walk
       hipLaunchKernelGGL(ksg_tcol_carry<1>, dim3(nb), dim3(64), 0, s2, b);

@@ -119,6 +119,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  KSG_STAMP(8);   // the wait for this batch's phase 1 / top-k
   for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
   {   // every staging load issued before the first LDS store
     constexpr int PI = (64 * POD_WORDS + BLOCK - 1) / BLOCK;
@@ -168,6 +169,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
       if (x < nb * KT) s_top[x] = i < kk[it] ? key_node(key[it]) : -1;
     }
   }
+  KSG_STAMP(9);   // staging loads issued and stored
   // carried slots: slot t = version t = carried node t, evaluated as round 1's
   // special items (their rows come from global memory)
   const int nc0 = a.carry ? *a.carry_n : 0;

@@ -48,8 +48,10 @@ if mode == "spec":
     print(f"[spec] {n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build); "
           f"rounds per batch {st[15] / max(1, (n_pods + 63) // 64):.2f}, speculation steps per batch "
           f"{st[14] / max(1, (n_pods + 63) // 64):.1f}, step-on iterations per batch {st[13] / max(1, (n_pods + 63) // 64):.1f}")
-    tot = sum(st[0:8])
-    for i in range(0, 8):
+    names += ["setup: wait for phase 1 / top-k", "setup: staging (pods, programs, T)"]
+    names[0] = "setup: carried slots, pod records, initial pointers"
+    tot = sum(st[0:10])
+    for i in (8, 9, 0, 1, 2, 3, 4, 5, 6, 7):
         print(f"  {names[i]:40s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / tot:5.1f} %")
     sys.exit(0)
 if mode in ("slot", "window"):
