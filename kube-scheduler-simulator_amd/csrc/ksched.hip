@@ -275,7 +275,26 @@ struct BatchArgs {
   unsigned* tk_done;
   unsigned tk_seq;
   unsigned* tk_timeout;     // set when the walk's poll gave up
+  // the spec walk's hand-off without a release fence (MI355X guide, "valid
+  // forms"): top-k stores T and P1Stats with sc0 sc1 stores, every storing
+  // wave drains vmcnt(0) before the workgroup barrier in front of the one-lane
+  // agent add; the walk loads those bytes with sc0 sc1 loads.  (An agent
+  // release per workgroup, buffer_wbl2, made top-k 31 instead of 19 us.)
+  int32_t tk_sc;
 };
+
+// sc0 sc1 (system-scope relaxed) stores / loads of the spec walk's hand-off bytes
+// (global address space explicitly: global_store / global_load, never flat_)
+template <typename T>
+__device__ __forceinline__ void st_sc(T* p, T v) {
+  using GT = __attribute__((address_space(1))) T;
+  __hip_atomic_store((GT*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T ld_sc(const T* p) {
+  using GT = __attribute__((address_space(1))) T;
+  return __hip_atomic_load((GT*)const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // record: bit 63 feasible | rt (8 bits) << 48 | ra (16 bits) << 32 | partial (32 bits)
 __device__ __forceinline__ uint64_t pack_rec(int64_t part, int64_t rt, int64_t ra) {
@@ -662,7 +681,13 @@ __device__ __forceinline__ void batch_topk_body(const BatchArgs& a) {
     s.inv_mt = mt ? 1.0f / (float)mt : 1.0f;
     s.inv_ma = ma ? 1.0f / (float)ma : 1.0f;
     s.pad = 0;
-    a.p1[j] = s;
+    if (a.tk_sc) {
+#pragma unroll
+      for (int w = 0; w < (int)(sizeof(P1Stats) / 4); w++)
+        st_sc(reinterpret_cast<int32_t*>(&a.p1[j]) + w, reinterpret_cast<const int32_t*>(&s)[w]);
+    } else {
+      a.p1[j] = s;
+    }
   }
   if (K == 0) return;
   // dense key: larger = better (higher total, then lower node index); distinct per node
@@ -748,7 +773,8 @@ __device__ __forceinline__ void batch_topk_body(const BatchArgs& a) {
     const uint64_t x = s_keys[i];
     int r = 0;
     for (int m = 0; m < K; m++) r += s_keys[m] > x ? 1 : 0;
-    out[r] = x;
+    if (a.tk_sc) st_sc(out + r, x);
+    else out[r] = x;
   }
 }
 
@@ -756,14 +782,20 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
   batch_topk_body<BLOCK>(a);
   if (a.tk_done) {   // hand-off to the walk: every workgroup releases its outputs, the last one signals
-    __threadfence();
-    __syncthreads();
+    if (a.tk_sc) {   // sc0 sc1 stores: every wave drains them, no release fence
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
+      __threadfence();
+      __syncthreads();
+    }
     if (threadIdx.x == 0) {
       using G1 = __attribute__((address_space(1))) unsigned;
       const unsigned old = __hip_atomic_fetch_add((G1*)a.tk_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old == gridDim.x - 1) {
         __hip_atomic_store((G1*)a.tk_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((G1*)a.tk_done, a.tk_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.tk_sc) __hip_atomic_store((G1*)a.tk_done, a.tk_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_store((G1*)a.tk_done, a.tk_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -3251,6 +3283,8 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.tk_timeout = tk_flag ? tk + 2 : nullptr;
     b.tk_seq = (unsigned)bi + 1;
     BatchArgs bt = b;   // the top-k launch: signals (no transpose follows it in the spec walk)
+    bt.tk_sc = specw && tk_flag ? 1 : 0;
+    b.tk_sc = bt.tk_sc;
     // phase 1 of batch b reads the state as of the end of batch b - 2 at least,
     // and reuses the buffers phase 2 of batch b - 2 read
     if (overlap && bi >= 2) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev_p2[par], 0));

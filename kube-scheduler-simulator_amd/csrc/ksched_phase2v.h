@@ -86,6 +86,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   __shared__ uint8_t s_snap[64 * 64];     // [step][pod] T pointer before the step's conflicts
   __shared__ SvItem s_item[64 + 1];       // a round's special items: carried slots / the correction
   __shared__ int32_t s_ctl[8];            // round: start, nv_c, ns_c, n_special; progress; next item
+  __shared__ P1Stats s_p1[64];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const DevCluster& c = a.c;
@@ -152,22 +153,32 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     reinterpret_cast<int32_t*>(&s_prof)[i] = reinterpret_cast<const int32_t*>(a.prof)[i];
   bool fit_filter_on = false;
   for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
-  {   // T as node indices, [pod][KT] (every key and K load issued before the first store)
-    constexpr int TI = (64 * kSvSlots + BLOCK - 1) / BLOCK;
-    uint64_t key[TI];
-    int32_t kk[TI];
+  {   // T as node indices, [pod][KT]: two keys per 16-byte load, every load issued
+      // before the first store; entries past a pod's K are never read (every
+      // reader bounds its pointer by K), so they are converted unchecked
+    const int KP = (KT + 1) >> 1;   // key pairs per row
+    constexpr int TI = (64 * kSvSlots / 2 + BLOCK - 1) / BLOCK;
+    ulonglong2 kp[TI];
 #pragma unroll
     for (int it = 0; it < TI; it++) {
-      const int x = tid + it * BLOCK, q = x / KT, i = x - q * KT;
-      const bool ok = x < nb * KT;
-      key[it] = ok ? a.top[(size_t)q * KSG_BATCH_MAX + i] : 0;
-      kk[it] = ok ? a.p1[q].K : 0;
+      const int x = tid + it * BLOCK, q = x / KP, i = 2 * (x - q * KP);
+      const uint64_t* tp = a.top + (size_t)q * KSG_BATCH_MAX + i;
+      if (x >= nb * KP) kp[it] = ulonglong2{0, 0};
+      else if (a.tk_sc) kp[it] = ulonglong2{ld_sc(tp), ld_sc(tp + 1)};   // top-k's sc0 sc1 hand-off
+      else kp[it] = *reinterpret_cast<const ulonglong2*>(tp);
     }
 #pragma unroll
     for (int it = 0; it < TI; it++) {
-      const int x = tid + it * BLOCK, q = x / KT, i = x - q * KT;
-      if (x < nb * KT) s_top[x] = i < kk[it] ? key_node(key[it]) : -1;
+      const int x = tid + it * BLOCK, q = x / KP, i = 2 * (x - q * KP);
+      if (x < nb * KP) {
+        s_top[q * KT + i] = key_node(kp[it].x);
+        if (i + 1 < KT) s_top[q * KT + i + 1] = key_node(kp[it].y);
+      }
     }
+  }
+  if (tid < nb * (int)(sizeof(P1Stats) / 4)) {   // the pods' phase-1 statistics, read once
+    const int32_t* src = reinterpret_cast<const int32_t*>(a.p1) + tid;
+    reinterpret_cast<int32_t*>(s_p1)[tid] = a.tk_sc ? ld_sc(src) : *src;
   }
   KSG_STAMP(9);   // staging loads issued and stored
   // carried slots: slot t = version t = carried node t, evaluated as round 1's
@@ -190,7 +201,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     const bool ipa_filter = ipa_in_filter(prof);
     const bool ipa_score = ((prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) != 0;
     const ksg_pod& p = s_pods[lane];
-    const P1Stats s1 = a.p1[lane];
+    const P1Stats s1 = s_p1[lane];
     const uint32_t smask = prof.score_mask & ~p.score_skip;
     TcU u;
 #pragma unroll
@@ -244,7 +255,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   };
   // lane q's pod (consumer waves evaluate every version for every pod)
   const int qq = lane < nb ? lane : 0;
-  const TcPod hp = tc_pod(s_pods[qq], prof, a.p1[qq], fit_filter_on, R);
+  const TcPod hp = tc_pod(s_pods[qq], prof, s_p1[qq], fit_filter_on, R);
   // Evaluate one row version for every pod into its slot's column words (a
   // consumer wave).  Pods after t see it; a new slot is absent for the pods up
   // to t; a re-choice leaves the earlier pods their previous version's words.
@@ -393,7 +404,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
           s_clist[sl] = d;
           s_lastv[sl] = v;
           s_vt[v] = k;
-          s_bu[k] = d >= 0 ? a.top[(size_t)k * KSG_BATCH_MAX + pk] : 0;
+          const uint64_t* tp = a.top + (size_t)k * KSG_BATCH_MAX + pk;
+          s_bu[k] = d < 0 ? 0 : a.tk_sc ? ld_sc(tp) : *tp;
         }
         it = SvItem{d, sl, v, -1, k};
         return 1;
@@ -494,7 +506,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
         if (renorm_k) {   // the renormalisation rescan: pod k over its phase-1 records and the live columns
           const ksg_pod& p = s_pods[k];
           const PodView pv = make_view(c, prof, p, s_prog + (p.blob - a.prog_lo), a.prog);
-          const TcPod hk = tc_pod(p, prof, a.p1[k], fit_filter_on, R);
+          const TcPod hk = tc_pod(p, prof, s_p1[k], fit_filter_on, R);
           const uint64_t* rec = a.rec + (size_t)k * N;
           const int32_t* img = a.img + (size_t)k * N;
           auto live_rec = [&](int s) -> uint64_t {   // pod k on slot s's newest committed version
