@@ -346,10 +346,10 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
         if (tid == 0) st_acc[14] += 1;   // speculation steps
 #endif
         if (lane == 0) {   // publish: LDS executes a wave's DS instructions in order, so a
-                           // consumer that sees the progress sees s_dec / s_snap (no wait here)
-          // (relaxed workgroup-scope atomics on the __shared__ words: plain ds_write_b32;
+                           // consumer that sees the progress sees s_snap (no wait here); the
+                           // consumer derives d_k from the snapshot row and T
+          // (a relaxed workgroup-scope atomic on the __shared__ word: plain ds_write_b32;
           // a volatile cast would lose the address space and become a flat store + vmcnt wait)
-          __hip_atomic_store(&s_dec[k], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (d >= 0) atomicOr(&s_cmask[d >> 5], 1u << (d & 31));
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
           __hip_atomic_store(&s_ctl[4], k - start + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -397,10 +397,11 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
           __builtin_amdgcn_s_sleep(1);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const int d = s_dec[k];
         const int sl = ns_c + (k - start), v = nv_c + (k - start);
         const int pk = s_snap[k * 64 + k];
+        const int d = pk < s_u[k].K ? s_top[k * KT + pk] : -1;   // pod k's speculated node
         if (lane == 0) {
+          s_dec[k] = d;
           s_clist[sl] = d;
           s_lastv[sl] = v;
           s_vt[v] = k;
