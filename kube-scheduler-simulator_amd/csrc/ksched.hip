@@ -2942,7 +2942,7 @@ static const std::array<const void*, 2>& tcol_kernels() {
   return k;
 }
 constexpr size_t kTcolLds = 128 * 1024;   // dynamic LDS of the transposed walk (static part ~14 KB)
-constexpr size_t kSpecLds = 140 * 1024;   // ... of the speculate-and-verify walk (static part ~16 KB): the
+constexpr size_t kSpecLds = 130 * 1024;   // ... of the speculate-and-verify walk (static part ~16 KB): the
                                           // launch always asks for all of it, so that no other kernel's
                                           // workgroup shares the walk's CU
 

@@ -49,6 +49,7 @@ constexpr int kSvWaves = 12;                  // wave 0 speculates (then verifie
 constexpr int kSvSlots = 2 * 64;              // carried (<= previous batch) + this batch's
 constexpr int kSvRow = SlotLayout<4>::STRIDE; // int64 words per LDS row
 constexpr int kSvTotalBits = 27;
+constexpr int kSvOwner = 2048;                // hashed owner table of the speculation's macro-steps
 
 __device__ __forceinline__ bool sv_changed(const uint32_t* cm, int n) { return ((cm[n >> 5] >> (n & 31)) & 1u) != 0; }
 
@@ -83,7 +84,10 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   __shared__ uint64_t s_bu[64];           // pod's best unchanged key (0: none)
   __shared__ uint64_t s_best[64];         // aggregate: best live column key
   __shared__ uint32_t s_cnt[64];          // aggregate: p1 feasible | live << 8 | lost taint << 16 | lost aff << 24
-  __shared__ uint8_t s_snap[64 * 64];     // [step][pod] T pointer before the step's conflicts
+  __shared__ uint8_t s_snap[64 * 64];     // [macro-step][pod] T pointers at the macro-step's start
+  __shared__ uint8_t s_mstep[64];         // pod's macro-step in the current round
+  __shared__ uint8_t s_dptr[64];          // pod's T pointer when it was decided
+  __shared__ uint32_t s_owner[kSvOwner];  // lowest lane holding a node (hashed), 0xffffffff = none
   __shared__ SvItem s_item[64 + 1];       // a round's special items: carried slots / the correction
   __shared__ int32_t s_ctl[8];            // round: start, nv_c, ns_c, n_special; progress; next item
   __shared__ P1Stats s_p1[64];
@@ -122,6 +126,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   }
   KSG_STAMP(8);   // the wait for this batch's phase 1 / top-k
   for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
+  for (int i = tid; i < kSvOwner; i += BLOCK) s_owner[i] = 0xffffffffu;
   {   // every staging load issued before the first LDS store
     constexpr int PI = (64 * POD_WORDS + BLOCK - 1) / BLOCK;
     int32_t pw[PI];
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
       const uint64_t m = __ballot(i < K && !sv_changed(s_cmask, n));
       if (m) ptr = b + __builtin_ctzll(m);
     }
-    if (lane == 0) s_snap[q] = (uint8_t)ptr;   // step 0's row of the snapshot = the round-1 pointers
+    if (lane == 0) s_dptr[q] = (uint8_t)ptr;   // the round-1 pointers
   }
   __syncthreads();
 
@@ -317,7 +322,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   // and the entry after it (read ahead: a step-on costs one LDS round trip)
   int ptr = 0, cnode = -1, nnode = -1;
   if (wv == 0 && lane < nb) {
-    ptr = s_snap[lane];
+    ptr = s_dptr[lane];
     const int K = s_u[lane].K;
     cnode = ptr < K ? s_top[lane * KT + ptr] : -1;
     nnode = ptr + 1 < K ? s_top[lane * KT + ptr + 1] : -1;
@@ -338,27 +343,40 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
         s_cnt[lane] = 0;
       }
       const int Kq = lane < nb ? s_u[lane].K : 0;
-      const uint64_t lanes_lt_nb = nb >= 64 ? ~0ull : (1ull << nb) - 1;
-      for (int k = start; k < nb; k++) {
-        s_snap[k * 64 + lane] = (uint8_t)ptr;
-        const int d = __builtin_amdgcn_readlane(cnode, k);
+      // Macro-steps: every undecided pod from `cur` on holds a free candidate;
+      // the pods up to the first one whose candidate an earlier one also holds
+      // (found through a hashed table of the lowest lane per node: ds_min) take
+      // their candidates at once, exactly as the one-pod steps would (none of
+      // them conflicts with an earlier one); then the later pods whose
+      // candidate was taken step on.  Pointer snapshots per macro-step; a
+      // rollback restores the one of k*'s macro-step and re-validates.
+      int mi = 0;
+      for (int cur = start; cur < nb; mi++) {
+        s_snap[mi * 64 + lane] = (uint8_t)ptr;
+        const bool act = lane >= cur && lane < nb && cnode >= 0;
+        const int hsh = cnode & (kSvOwner - 1);
+        if (act) atomicMin(&s_owner[hsh], (unsigned)lane);
+        // (one wave: the LDS executes its DS instructions in order, so this read sees every lane's min)
+        const unsigned o = act ? s_owner[hsh] : (unsigned)lane;
+        const uint64_t dup = __ballot(act && o != (unsigned)lane);
+        const int f = dup ? __builtin_ctzll(dup) : nb;
 #ifdef KSG_STAMPS
-        if (tid == 0) st_acc[14] += 1;   // speculation steps
+        if (tid == 0) { st_acc[14] += f - cur; st_acc[12] += 1; }   // steps, macro-steps
 #endif
-        if (lane == 0) {   // publish: LDS executes a wave's DS instructions in order, so a
-                           // consumer that sees the progress sees s_snap (no wait here); the
-                           // consumer derives d_k from the snapshot row and T
-          // (a relaxed workgroup-scope atomic on the __shared__ word: plain ds_write_b32;
-          // a volatile cast would lose the address space and become a flat store + vmcnt wait)
-          if (d >= 0) atomicOr(&s_cmask[d >> 5], 1u << (d & 31));
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          __hip_atomic_store(&s_ctl[4], k - start + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane >= cur && lane < f) {   // the run: decided
+          s_dptr[lane] = (uint8_t)ptr;
+          s_mstep[lane] = (uint8_t)mi;
+          if (cnode >= 0) atomicOr(&s_cmask[cnode >> 5], 1u << (cnode & 31));
         }
-        if (d < 0) continue;
-        // lanes after k holding d (a wave-uniform mask: no divergent branch when it is empty)
-        uint64_t m = __ballot(cnode == d) & lanes_lt_nb & (~1ull << k);
-        bool conflict = (m >> lane) & 1ull;
-        while (m) {
+        if (act) s_owner[hsh] = 0xffffffffu;
+        if (lane == 0) {   // publish (in-order DS: a consumer that sees it sees s_dptr / s_mstep)
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          __hip_atomic_store(&s_ctl[4], f - start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // later pods whose candidate the run took (the owner prefilter has no
+        // false negatives; the bitmap decides, hashing collisions included)
+        bool conflict = lane >= f && lane < nb && cnode >= 0 && o < (unsigned)f && sv_changed(s_cmask, cnode);
+        while (__ballot(conflict)) {
 #ifdef KSG_STAMPS
           if (tid == 0) st_acc[13] += 1;   // step-on iterations
 #endif
@@ -368,8 +386,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
             nnode = ptr + 1 < Kq ? s_top[lane * KT + ptr + 1] : -1;
             conflict = cnode >= 0 && sv_changed(s_cmask, cnode);
           }
-          m = __ballot(conflict);
         }
+        cur = f;
       }
       __builtin_amdgcn_s_setprio(0);
       KSG_STAMP(1);
@@ -398,7 +416,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int sl = ns_c + (k - start), v = nv_c + (k - start);
-        const int pk = s_snap[k * 64 + k];
+        const int pk = s_dptr[k];
         const int d = pk < s_u[k].K ? s_top[k * KT + pk] : -1;   // pod k's speculated node
         if (lane == 0) {
           s_dec[k] = d;
@@ -594,11 +612,12 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
         }
         // the next round's speculation: pointers as they were before pod k's step
         if (lane > k && lane < nb) {
-          ptr = s_snap[k * 64 + lane];
+          ptr = s_snap[s_mstep[k] * 64 + lane];   // at the start of k's macro-step
           cnode = ptr < u.K ? s_top[lane * KT + ptr] : -1;
           nnode = ptr + 1 < u.K ? s_top[lane * KT + ptr + 1] : -1;
-          // a new node taken by pod k (the rescan's choice): lanes holding it step on
-          bool conflict = selected >= 0 && idx < 0 && cnode == selected;
+          // re-validate: nodes the committed pods of that macro-step took, and a
+          // new node taken by pod k (the rescan's choice), are stepped over
+          bool conflict = cnode >= 0 && sv_changed(s_cmask, cnode);
           while (conflict) {
             ptr++;
             cnode = nnode;

@@ -47,7 +47,8 @@ if mode == "spec":
              "barrier", "epilogue"]
     print(f"[spec] {n_pods} pods, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped build); "
           f"rounds per batch {st[15] / max(1, (n_pods + 63) // 64):.2f}, speculation steps per batch "
-          f"{st[14] / max(1, (n_pods + 63) // 64):.1f}, step-on iterations per batch {st[13] / max(1, (n_pods + 63) // 64):.1f}")
+          f"{st[14] / max(1, (n_pods + 63) // 64):.1f} in {st[12] / max(1, (n_pods + 63) // 64):.1f} macro-steps, "
+          f"step-on iterations per batch {st[13] / max(1, (n_pods + 63) // 64):.1f}")
     names += ["setup: wait for phase 1 / top-k", "setup: staging (pods, programs, T)"]
     names[0] = "setup: carried slots, pod records, initial pointers"
     tot = sum(st[0:10])
