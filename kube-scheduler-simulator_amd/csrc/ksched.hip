@@ -3599,9 +3599,9 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
 // Single replica, PodTopologySpread / InterPodAffinity, no capture: the queue
 // on G co-resident workgroups (ksched_topo_coop.h), in batches of kCoopBatch
 // pods, each preceded by its static records (ksg_sweep_static).
-template <int KN>
+template <int KN, bool LL = false>
 int coop_occupancy(ksg_ctx* ctx, int* occ) {
-  HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ksg_topo_coop<KN>, 256, 0));
+  HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ksg_topo_coop<KN, LL>, 256, 0));
   return KSG_OK;
 }
 
@@ -3618,9 +3618,11 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   while ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N && kn < 32) kn *= 2;
   if ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: too many nodes");
   const int G = (int)((N + 256 * kn - 1) / (256 * kn));
+  // the variant whose label / vocabulary / template tables are LDS at compile time
+  const bool ll = kn == 1 && ctx->c.L <= kCoopLabCols && ctx->c.n_tmpl <= kCoopTmpl && !getenv("KSG_COOP_NO_LL");
   int occ = 0;
   switch (kn) {
-    case 1: rc = coop_occupancy<1>(ctx, &occ); break;
+    case 1: rc = ll ? coop_occupancy<1, true>(ctx, &occ) : coop_occupancy<1>(ctx, &occ); break;
     case 2: rc = coop_occupancy<2>(ctx, &occ); break;
     case 4: rc = coop_occupancy<4>(ctx, &occ); break;
     case 8: rc = coop_occupancy<8>(ctx, &occ); break;
@@ -3685,7 +3687,7 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     // cooperative launch: the runtime guarantees the G workgroups are
     // co-resident (or refuses the launch), which the grid barrier needs
     void* kargs[] = {&a};
-    const void* kf = kn == 1 ? (const void*)ksg_topo_coop<1> : kn == 2 ? (const void*)ksg_topo_coop<2>
+    const void* kf = ll ? (const void*)ksg_topo_coop<1, true> : kn == 1 ? (const void*)ksg_topo_coop<1> : kn == 2 ? (const void*)ksg_topo_coop<2>
                    : kn == 4 ? (const void*)ksg_topo_coop<4> : kn == 8 ? (const void*)ksg_topo_coop<8>
                    : kn == 16 ? (const void*)ksg_topo_coop<16> : (const void*)ksg_topo_coop<32>;
     HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));

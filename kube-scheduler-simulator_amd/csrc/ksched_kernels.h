@@ -160,18 +160,29 @@ __device__ __forceinline__ PodView make_view(const DevCluster& c, const ksg_prof
 // ============================================================================
 constexpr int kMaxHard = 4, kMaxSoft = 4, kMaxAff = 4, kMaxAnti = 4, kMaxPref = 8;
 
+// A pointer into LDS.  Every parse_topo caller passes its LDS copy of the
+// pod's programs, so the program pointers of TopoProg carry the LDS address
+// space: a generic pointer read back from LDS would compile every program
+// lookup on the per-node paths to a flat load (vmcnt + lgkmcnt wait each).
+// (The host pass only sees the struct's declaration: a plain pointer there.)
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(3))) int32_t* lds_i32p;
+#else
+typedef const int32_t* lds_i32p;
+#endif
+
 struct TopoProg {
   int n_hard, n_soft, require_all;
-  const int32_t* hard;   // {col sel max_skew min_domains self_match na nt} x n_hard
-  const int32_t* soft;   // {col sel max_skew na nt is_hostname} x n_soft
+  lds_i32p hard;   // {col sel max_skew min_domains self_match na nt} x n_hard
+  lds_i32p soft;   // {col sel max_skew na nt is_hostname} x n_soft
   int n_aff, sel_all, self_all;
-  const int32_t* aff_cols;
+  lds_i32p aff_cols;
   int n_anti;
-  const int32_t* anti;   // {col sel}
+  lds_i32p anti;   // {col sel}
   int n_pref;
-  const int32_t* pref;   // {col sel weight}
+  lds_i32p pref;   // {col sel weight}
   int n_ma, n_mh, n_mp;
-  const int32_t *m_anti, *m_hard, *m_pref;
+  lds_i32p m_anti, m_hard, m_pref;
   bool pts_filter, pts_score, ipa;
 };
 
@@ -225,7 +236,7 @@ __device__ __forceinline__ void parse_topo(const ksg_pod& p, const int32_t* P, u
   g = TopoProg{};
   const int boff = p.blob;
   if (p.pts >= 0) {
-    const int32_t* w = P + (p.pts - boff);
+    lds_i32p w = (lds_i32p)(P + (p.pts - boff));
     g.n_hard = w[0];
     g.n_soft = w[1];
     g.require_all = w[2];
@@ -235,7 +246,7 @@ __device__ __forceinline__ void parse_topo(const ksg_pod& p, const int32_t* P, u
   g.pts_filter = g.n_hard > 0 && !((fskip >> KSG_PL_POD_TOPOLOGY_SPREAD) & 1u);
   g.pts_score = g.n_soft > 0 && ((smask >> KSG_PL_POD_TOPOLOGY_SPREAD) & 1u);
   if (p.ipa >= 0) {
-    const int32_t* w = P + (p.ipa - boff);
+    lds_i32p w = (lds_i32p)(P + (p.ipa - boff));
     g.n_aff = w[0];
     g.sel_all = w[1];
     g.self_all = w[2];

@@ -275,7 +275,10 @@ struct OpAddI { __device__ int32_t operator()(int32_t a, int32_t b) const { retu
 struct OpMinI { __device__ int32_t operator()(int32_t a, int32_t b) const { return a < b ? a : b; } };
 struct OpOrI { __device__ int32_t operator()(int32_t a, int32_t b) const { return a | b; } };
 
-template <int KN>
+// LL: the host guarantees KN == 1, every label column, the column vocabulary
+// and every term template fit their LDS copies; the evaluators' tables are then
+// LDS pointers at compile time (ds_read, not flat loads on the node paths).
+template <int KN, bool LL = false>
 __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   constexpr int BLOCK = 256, NW = BLOCK / 64;
   constexpr long long BIG = 0x7fffffffffffffffll;
@@ -308,9 +311,9 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profile)[tid];
   for (int i = tid; i < a.count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
-  const bool lab_lds = KN == 1 && cg.L <= kCoopLabCols;
-  const bool col_lds = cg.L <= kCoopLabCols;
-  const bool tmpl_lds = cg.n_tmpl <= kCoopTmpl;
+  const bool lab_lds = LL || (KN == 1 && cg.L <= kCoopLabCols);
+  const bool col_lds = LL || cg.L <= kCoopLabCols;
+  const bool tmpl_lds = LL || cg.n_tmpl <= kCoopTmpl;
   if (lab_lds) {
     const int n = wg * BLOCK + tid;
     for (int col = 0; col < cg.L; col++) s_lab[col * BLOCK + tid] = n < N ? cg.label_val[(size_t)col * N + n] : 0u;
@@ -328,9 +331,15 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   }
   __syncthreads();
   DevCluster cl = cg;   // the evaluators' view: the staged copies where they fit
-  if (lab_lds) { cl.label_val = s_lab; cl.lab_stride = BLOCK; cl.lab_base = wg * BLOCK; }
-  if (col_lds) { cl.col_vocab = s_cv; cl.col_unique = s_cu; }
-  if (tmpl_lds) { cl.tmpl_col = s_tcol; cl.tmpl_off = s_toff; }
+  if (LL) {
+    cl.label_val = s_lab; cl.lab_stride = BLOCK; cl.lab_base = wg * BLOCK;
+    cl.col_vocab = s_cv; cl.col_unique = s_cu;
+    cl.tmpl_col = s_tcol; cl.tmpl_off = s_toff;
+  } else {
+    if (lab_lds) { cl.label_val = s_lab; cl.lab_stride = BLOCK; cl.lab_base = wg * BLOCK; }
+    if (col_lds) { cl.col_vocab = s_cv; cl.col_unique = s_cu; }
+    if (tmpl_lds) { cl.tmpl_col = s_tcol; cl.tmpl_off = s_toff; }
+  }
   const DevCluster& c = cl;
   const ksg_profile& prof = s_prof;
   bool ipa_in_filter = false;
