@@ -366,9 +366,23 @@ def main():
     ap.add_argument("--default-pods", type=int, default=50000, help="default-profile line; 0 disables")
     ap.add_argument("--cycle-pods", type=int, default=2000, help="per-cycle sidecar; 0 disables")
     ap.add_argument("--cycle-warm", type=int, default=500)
+    ap.add_argument("--no-build-check", action="store_true",
+                    help="skip the check that libksched.so embeds the tree's source hash")
     args = ap.parse_args()
 
+    # Before anything touches the GPU: the library must be built from this
+    # tree's source (a mismatch rebuilds it), and `--gpus N` without a
+    # launcher starts N ranks here (launcher.py; the parent stays off the GPU).
+    launcher = importlib.import_module(PKG + ".launcher")
+    if not launcher.launched():
+        if not args.no_build_check:
+            src_hash = importlib.import_module("__graft_entry__").ensure_current()
+            log(f"libksched.so built from source {src_hash[:12]}")
+        if args.gpus > 1:
+            sys.exit(launcher.launch(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:] + ["--no-build-check"]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
@@ -525,6 +539,9 @@ def main():
             "node_evals_per_sec": node_evals,
             "roofline": roof,
         }
+        ge = importlib.import_module("__graft_entry__")
+        out["source_hash"] = {"library": ge.library_hash(), "tree": ge.source_hash()}
+        out["source_hash"]["matches"] = out["source_hash"]["library"] == out["source_hash"]["tree"]
         if sweep is not None:
             out["replica_sweep"] = sweep
         if ann is not None:

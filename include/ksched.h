@@ -11,9 +11,12 @@
  *   NormalizeScore  simulator/scheduler/plugin/wrappedplugin.go:388 (-> :400)
  *   Reserve/assume  simulator/scheduler/plugin/wrappedplugin.go:622 (AddSelectedNode)
  * and each call lands in Store (resultstore/store.go:423,461,481,522,537,562).
- * A cgo shim calls ksg_eval() ONCE per pod at PreFilter time,
- * stashes the returned SoA in CycleState, and answers every Filter / Score /
- * NormalizeScore call from it; Reserve calls ksg_commit().  ksg_run_queue()
+ * A cgo shim calls ksg_eval_view() ONCE per pod at PreFilter
+ * time, stashes the returned SoA in CycleState, and answers every Filter /
+ * Score / NormalizeScore call from it.  The shim has no Reserve plugin (it
+ * would add an annotation entry upstream never writes): the assumed pod
+ * reaches the device at the next cycle's snapshot diff, through
+ * ksg_snapshot_assume -> ksg_commit().  ksg_run_queue()
  * runs a whole pod queue on the device (filter -> score -> normalise ->
  * weighted sum -> selectHost -> assume) without returning to the host.
  *
@@ -229,6 +232,9 @@ typedef struct ksg_replica_summary {
 typedef struct ksg_ctx ksg_ctx;
 
 int ksg_abi_version(void);
+/* sha256 (hex) of the sources the library was built from (csrc/, include/),
+ * embedded at build time; bench.py and the tests compare it with the tree. */
+const char* ksg_source_hash(void);
 int ksg_open(int device, ksg_ctx** out);
 int ksg_close(ksg_ctx* ctx);
 const char* ksg_last_error(ksg_ctx* ctx);

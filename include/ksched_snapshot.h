@@ -153,6 +153,21 @@ typedef struct ksg_node_view {
   const ksg_image_view* images;      /* status.images */
 } ksg_node_view;
 
+/* One spec.volumes[] entry (v1.Volume): kind = the JSON key of the
+ * VolumeSource field that is set ("persistentVolumeClaim", "emptyDir",
+ * "configMap", ...), claim_name = persistentVolumeClaim.claimName.  A pod with
+ * a claim, a generic ephemeral volume or an in-tree disk volume
+ * (gcePersistentDisk, awsElasticBlockStore, azureDisk, azureFile, cinder,
+ * vsphereVolume, portworxVolume, rbd, iscsi) makes VolumeBinding /
+ * NodeVolumeLimits / VolumeRestrictions / VolumeZone PreFilter run: while one
+ * of those plugins is enabled, ksg_snapshot_add_pod refuses it
+ * (KSG_E_UNSUPPORTED); every other source is their Skip, as upstream. */
+typedef struct ksg_volume_view {
+  const char* name;
+  const char* kind;
+  const char* claim_name;
+} ksg_volume_view;
+
 typedef struct ksg_pod_view {
   const char* namespace_;
   const char* name;
@@ -192,6 +207,8 @@ typedef struct ksg_pod_view {
   ksg_label_selector_view default_spread_selector;
   int32_t terminating;                       /* metadata.deletionTimestamp != nil */
   int32_t priority;                          /* corev1helpers.PodPriority */
+  int32_t n_volumes;
+  const ksg_volume_view* volumes;            /* spec.volumes */
 } ksg_pod_view;
 
 typedef struct ksg_plugin_view { const char* name; int32_t weight; } ksg_plugin_view;

@@ -275,6 +275,8 @@ struct BatchArgs {
   unsigned* tk_done;
   unsigned tk_seq;
   unsigned* tk_timeout;     // set when the walk's poll gave up
+  unsigned* walk_err;       // the speculate-and-verify walk's broken-invariant code (armed in every mode)
+  int32_t inject_walk_err;  // tests only (env KSG_TEST_INJECT_WALK_ERR): the walk's first item reports code 3
   // the spec walk's hand-off without a release fence (MI355X guide, "valid
   // forms"): top-k stores T and P1Stats with sc0 sc1 stores, every storing
   // wave drains vmcnt(0) before the workgroup barrier in front of the one-lane
@@ -2541,6 +2543,10 @@ struct ksg_ctx {
   ksg_profile* d_ev_prof = nullptr;
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
+  int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
+  int cycle_block = 128;                    // env KSG_CYCLE_BLOCK: nodes per workgroup of ksg_eval_cycle (64/128/256)
+  bool cycle_sys = true;                    // env KSG_CYCLE_SYS=0: plain host stores + __threadfence_system
+  int cycle_cap[3] = {0, 0, 0};             // co-resident ksg_eval_cycle workgroups per block size (0 = not queried)
   // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
   char* h_stage = nullptr;
   size_t h_stage_bytes = 0;
@@ -3149,7 +3155,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   int32_t* carry_n = ctx->d_carry + 2 * KSG_BATCH_MAX;   // [2]
   unsigned* tk = reinterpret_cast<unsigned*>(carry_n + 2);   // top-k hand-off: arrive, done, timeout
   ctx->pipe_tk = tk;
-  HIPC(ctx, hipMemsetAsync(carry_n, 0, 6 * sizeof(int32_t), ctx->stream));
+  HIPC(ctx, hipMemsetAsync(carry_n, 0, 6 * sizeof(int32_t), ctx->stream));   // carry_n, tk[0..3]
   const bool window = ctx->pipe_window != 0;
   const bool overlap = window && !ctx->timing && ctx->pipe_overlap;
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
@@ -3281,6 +3287,8 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.tk_arrive = tk_flag ? tk : nullptr;
     b.tk_done = tk_flag ? tk + 1 : nullptr;
     b.tk_timeout = tk_flag ? tk + 2 : nullptr;
+    b.walk_err = tk + 3;
+    b.inject_walk_err = ctx->inject_walk_err;
     b.tk_seq = (unsigned)bi + 1;
     BatchArgs bt = b;   // the top-k launch: signals (no transpose follows it in the spec walk)
     bt.tk_sc = specw && tk_flag ? 1 : 0;
@@ -3803,12 +3811,14 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   HIPC(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
   if ((rc = tcollect(ctx))) return rc;
-  if (ctx->pipe_tk) {   // the window pipeline's top-k hand-off (run_pipe)
-    unsigned tkf[3] = {0, 0, 0};
+  if (ctx->pipe_tk) {   // the window pipeline's top-k hand-off and the walk's invariant word (run_pipe)
+    unsigned tkf[4] = {0, 0, 0, 0};
     HIPC(ctx, hipMemcpy(tkf, ctx->pipe_tk, sizeof(tkf), hipMemcpyDeviceToHost));
     ctx->pipe_tk = nullptr;
     if (tkf[2] == 1) return fail(ctx, KSG_E_DEVICE, "batched path: top-k hand-off poll timed out");
-    if (tkf[2]) return fail(ctx, KSG_E_DEVICE, "batched path: speculate-and-verify walk invariant broken");
+    if (tkf[2] || tkf[3])
+      return fail(ctx, KSG_E_DEVICE, "batched path: speculate-and-verify walk invariant broken (code " +
+                                         std::to_string(tkf[3] ? tkf[3] : tkf[2]) + ")");
   }
   if (ctx->last_path == 4) {
     unsigned flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -3822,11 +3832,12 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
 // ksg_eval of one pod whose plugins are all node-local (the batched path's
 // eligibility): the framework's PreFilter .. NormalizeScore for one pod, as the
 // Go shim calls it once per scheduling cycle.  No allocation per call, one
-// launch (ksg_eval_cycle, ksched_cycle.h: N / 256 workgroups, the last to
-// arrive normalises and selects), results written by the kernel into a
-// pinned, fine-grained host block, completion read from a flag in that block
-// (no copy, no event, no stream synchronisation); the host then fills the
-// caller's arrays and decodes the result.
+// cooperative launch (ksg_eval_cycle, ksched_cycle.h: N / BLOCK co-resident
+// workgroups, one exchange of the pod-wide maxima, every workgroup normalises
+// its own nodes, the last to arrive folds the selectHost keys), results
+// written by the kernel into a pinned, fine-grained host block, completion
+// read from a flag in that block (no copy, no event, no stream
+// synchronisation); the host then decodes the result.
 bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
   return ctx->eval_fast && ctx->force_path != 1 && batch_eligible(ctx, pod, 1);
 }
@@ -3849,15 +3860,39 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     if ((prof.score_mask >> pl) & 1u) wabs += prof.weight[pl] < 0 ? -(int64_t)prof.weight[pl] : prof.weight[pl];
   const bool narrow = wabs * 100 < (1ll << 31);
   const size_t es = narrow ? 4 : 8;
-  const unsigned G = (unsigned)((N + 255) / 256);
+  int rc;
+  HIPC(ctx, hipSetDevice(ctx->device));
+  // workgroup size: the configured one, or a larger one when the grid would
+  // not be co-resident (the exchange needs every workgroup resident; the
+  // cooperative launch refuses otherwise)
+  auto kernel_of = [&](int b) -> const void* {
+    if (b == 64) return ctx->cycle_sys ? (const void*)ksg_eval_cycle<64, true> : (const void*)ksg_eval_cycle<64, false>;
+    if (b == 128) return ctx->cycle_sys ? (const void*)ksg_eval_cycle<128, true> : (const void*)ksg_eval_cycle<128, false>;
+    return ctx->cycle_sys ? (const void*)ksg_eval_cycle<256, true> : (const void*)ksg_eval_cycle<256, false>;
+  };
+  int block = ctx->cycle_block;
+  for (;; block *= 2) {
+    const int bi = block == 64 ? 0 : block == 128 ? 1 : 2;
+    if (!ctx->cycle_cap[bi]) {
+      int per_cu = 0;
+      HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_of(block), block, 0));
+      hipDeviceProp_t dp;
+      HIPC(ctx, hipGetDeviceProperties(&dp, ctx->device));
+      ctx->cycle_cap[bi] = std::max(1, per_cu) * dp.multiProcessorCount;
+    }
+    if ((N + block - 1) / block <= (size_t)ctx->cycle_cap[bi]) break;
+    if (block == 256) return fail(ctx, KSG_E_UNSUPPORTED, "per-cycle evaluation: grid not co-resident");
+  }
+  const unsigned G = (unsigned)((N + block - 1) / block);
   // host block: stats[4] best err flag | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_normrows][N]
   const size_t o_fs = 32, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
   const size_t o_tot = o_raw + es * N * n_rows, o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
   const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
-  // device block: rec[N] | parts[G] | done
-  const size_t d_parts = 8 * N, d_done = d_parts + sizeof(CycPart) * G, d_need = d_done + 8;
-  int rc;
-  HIPC(ctx, hipSetDevice(ctx->device));
+  // device block: parts[Gmax] | keys[Gmax] | flags[Gmax][32] | done | timeout, sized for the
+  // largest grid (64-lane workgroups) so a block-size change needs no reallocation
+  const size_t Gm = (N + 63) / 64;
+  const size_t d_keys = sizeof(CycPart) * Gm, d_flags = d_keys + sizeof(CycKey) * Gm,
+               d_done = d_flags + 128 * Gm, d_need = d_done + 128;
   if (d_need > ctx->ev_bytes) {
     if (ctx->d_ev) {
       auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_ev);
@@ -3884,8 +3919,8 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_ev, 0));
     ctx->d_hev = static_cast<char*>(dp);
   }
-  if (!ctx->ev_clean) {   // the arrival counter
-    HIPC(ctx, hipMemsetAsync(ctx->d_ev + d_done, 0, 8, ctx->stream));
+  if (!ctx->ev_clean) {   // flags (no call's sequence number is 0), the arrival counter, the timeout word
+    HIPC(ctx, hipMemsetAsync(ctx->d_ev + d_flags, 0, d_need - d_flags, ctx->stream));
     ctx->ev_clean = true;
   }
   if (ctx->ev_prof_dirty) {
@@ -3924,9 +3959,11 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   ca.h_err = reinterpret_cast<uint32_t*>(db + 24);
   ca.h_flag = reinterpret_cast<unsigned*>(db + 28);
   ca.seq = seq;
-  ca.rec = reinterpret_cast<uint64_t*>(ctx->d_ev);
-  ca.parts = reinterpret_cast<CycPart*>(ctx->d_ev + d_parts);
+  ca.parts = reinterpret_cast<CycPart*>(ctx->d_ev);
+  ca.keys = reinterpret_cast<CycKey*>(ctx->d_ev + d_keys);
+  ca.flags = reinterpret_cast<unsigned*>(ctx->d_ev + d_flags);
   ca.done = reinterpret_cast<unsigned*>(ctx->d_ev + d_done);
+  ca.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_done + 64);
   if (staged) {
     ca.spod = reinterpret_cast<const ksg_pod*>(ctx->d_stage);
     ca.sprog = reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod));
@@ -3937,7 +3974,8 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   }
   treset(ctx);
   if ((rc = tmark(ctx))) return rc;
-  hipLaunchKernelGGL(ksg_eval_cycle, dim3(G), dim3(256), 0, ctx->stream, ca);
+  void* kargs[] = {&ca};
+  HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
   if ((rc = tlaunched(ctx, KSG_K_EVAL_CYCLE, (double)N))) return rc;
   HIPC(ctx, hipGetLastError());
   if (staged) {   // consumed; the staging buffer is free once the stream passes this point
@@ -3964,13 +4002,17 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   const int32_t nfeas = st[0];
   const unsigned long long best = *reinterpret_cast<const unsigned long long*>(hb + 16);
   const uint32_t herr = *reinterpret_cast<const uint32_t*>(hb + 24);
+  if (herr & 2u) {
+    ctx->ev_clean = false;   // clears the sticky timeout word before the next call
+    return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: workgroup exchange timed out");
+  }
   uint32_t status = 0;
   int32_t selected = -1;
   if (nfeas == 1) {
     selected = (int32_t)N - st[3];
   } else if (nfeas >= 2) {
     status |= KSG_ST_SCORED;
-    if (herr) status |= KSG_ST_SCORE_ERROR;
+    if (herr & 1u) status |= KSG_ST_SCORE_ERROR;
     else selected = (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffu));
   }
   // ipa_skip_bits (ksched_kernels.h) on the host: the pod carries no
@@ -4255,6 +4297,12 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_PIPE_OVERLAP")) ctx->pipe_overlap = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_BLOCK")) {
+    const int v = atoi(f);
+    ctx->cycle_block = v <= 64 ? 64 : v <= 128 ? 128 : 256;
+  }
+  if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
+  if (const char* f = getenv("KSG_TEST_INJECT_WALK_ERR")) ctx->inject_walk_err = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);
     ctx->slot_block = v <= 64 ? 64 : v <= 128 ? 128 : KSG_BATCH_MAX;

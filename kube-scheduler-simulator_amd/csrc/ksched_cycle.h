@@ -1,30 +1,45 @@
 // The per-cycle evaluation (ksg_eval's fast path, the Go shim's one call per
-// scheduling cycle), included by ksched.hip inside its anonymous namespace.
+// scheduling cycle, wrappedplugin.go:388-548), included by ksched.hip inside
+// its anonymous namespace.
 //
-// One launch, results written straight into pinned host memory, completion
-// signalled by a flag the host polls: no copy launch, no event, no second
-// kernel.  N / 256 workgroups:
+// One launch of G = ceil(N / BLOCK) co-resident workgroups (cooperative
+// launch), one node per lane, results written straight into the pinned,
+// fine-grained host block the caller reads in place (ksg_eval_view):
 //
-//   every workgroup   its nodes' Filter status words and raw score rows (host
-//                     memory), a packed record per node (device memory,
-//                     agent-scope stores) and its partial feasible count /
-//                     TaintToleration and NodeAffinity maxima / lowest
-//                     feasible index (its own slot, agent-scope stores); then
-//                     one arrival on a device counter
-//   the last arrival  folds the slots, normalises TaintToleration and
-//                     NodeAffinity over every node from the records, writes
-//                     the normalised rows and totals, the selectHost argmax,
-//                     the statistics slot, resets the counter and stores the
-//                     call's sequence number into the host flag
+//   phase 1 (every workgroup)  stage the pod into LDS; evaluate its nodes
+//                              (filters in profile order, raw scores); store
+//                              each node's status word and raw score rows to
+//                              the host block at once (coalesced, in flight
+//                              during the exchange); keep the packed record in
+//                              registers; publish the workgroup's feasible
+//                              count, TaintToleration / NodeAffinity maxima and
+//                              lowest feasible index in its own slot
+//   exchange                   grid barrier on per-workgroup flags (one
+//                              128-byte line each, tagged with the call's
+//                              sequence number, so nothing is reset per call)
+//   phase 2 (every workgroup)  fold the G slots (every workgroup computes the
+//                              same pod-wide values), normalise its own nodes
+//                              (DefaultNormalizeScore), store the normalised
+//                              rows and weighted totals, its selectHost key;
+//                              a pod with < 2 feasible nodes ran no Score, so
+//                              its raw rows are zeroed instead
+//   the last arrival           folds the G keys (G words, not N nodes), writes
+//                              the statistics and sets the host flag
 //
-// Hand-offs between workgroups follow ksched_sweep.h (gst / gld: agent-scope
-// stores and loads, no cache maintenance); what the host reads is ordered by a
-// system-scope fence in every workgroup before its arrival (its host stores)
+// No workgroup walks all N nodes, and no row is written twice except in the
+// < 2 feasible case.  Hand-offs between workgroups follow ksched_sweep.h
+// (gst / gld: agent-scope stores and loads, every wave drained before the
+// workgroup barrier in front of the arrival); the host-visible bytes are
+// ordered by a system-scope release in every workgroup before its arrival
 // and in the last one before the flag.  Same arithmetic as ksg_capture_eval +
 // ksg_capture_norm (nb = 1, nothing assumed), bit for bit.
 
-struct CycPart {   // one workgroup's partial statistics
+struct CycPart {   // one workgroup's phase-1 statistics
   int32_t nfeas, max_t, max_a, lo;   // lo = max over its feasible nodes of N - n
+};
+struct CycKey {    // one workgroup's phase-2 result
+  unsigned long long key;
+  uint32_t err, pad;
 };
 
 struct CycArgs {
@@ -44,13 +59,15 @@ struct CycArgs {
   char* h_norm;                      // [n_normrows][N]
   int32_t* h_stats;                  // [4] nfeas, max taint, max node affinity, max (N - n)
   unsigned long long* h_best;        // selectHost key
-  uint32_t* h_err;                   // a normalised score left [0, 100]
+  uint32_t* h_err;                   // bit 0: a normalised score left [0, 100]; bit 1: exchange timed out
   unsigned* h_flag;                  // = seq once everything above is written
   unsigned seq;
   // device scratch
-  uint64_t* rec;                     // [N]
   CycPart* parts;                    // [G]
-  unsigned* done;                    // arrivals of this call (reset to 0 by the last one)
+  CycKey* keys;                      // [G]
+  unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
+  unsigned* done;                    // phase-2 arrivals of this call (reset to 0 by the last one)
+  unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
   // a staged append of this pod (ksg_capture_eval's spod fields)
   const ksg_pod* spod;
   const int32_t* sprog;
@@ -59,20 +76,71 @@ struct CycArgs {
   int32_t* wprog;
 };
 
+// Stores into the host block.  SYS: system-scope relaxed stores (global_store
+// sc0 sc1: written through to the fine-grained host memory, nothing left in
+// L2), so a vmcnt(0) wait orders them before the flag and no L2 write-back
+// (buffer_wbl2) is needed; else plain stores + __threadfence_system.
+template <bool SYS, class T>
+__device__ __forceinline__ void hst(T* p, T v) {
+  if constexpr (SYS) __hip_atomic_store((__attribute__((address_space(1))) T*)p, v, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_SYSTEM);
+  else *p = v;
+}
+template <bool SYS>
 __device__ __forceinline__ void cyc_put(char* base, size_t idx, int64_t v, bool narrow) {
-  if (narrow) reinterpret_cast<int32_t*>(base)[idx] = (int32_t)v;
-  else reinterpret_cast<int64_t*>(base)[idx] = v;
+  if (narrow) hst<SYS>(reinterpret_cast<int32_t*>(base) + idx, (int32_t)v);
+  else hst<SYS>(reinterpret_cast<int64_t*>(base) + idx, v);
+}
+// Every host store of this wave performed before what follows (the arrival,
+// the flag).
+template <bool SYS>
+__device__ __forceinline__ void host_release() {
+  if constexpr (SYS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else __threadfence_system();
 }
 
-__global__ __launch_bounds__(256) void ksg_eval_cycle(CycArgs a) {
+// Grid exchange: workgroup g stores `seq` into its own flag line, wave 0 polls
+// every flag until all hold `seq` (bounded; a timeout is sticky and reported).
+template <int BLOCK>
+__device__ __forceinline__ bool cyc_exchange(const CycArgs& a, int G) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its agent-scope stores are done
+  __syncthreads();
+  __shared__ int s_to;
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    if (tid == 0) gst(&a.flags[(size_t)blockIdx.x * 32], a.seq);
+    unsigned spins = 0;
+    int to = 0;
+    for (;;) {
+      bool ok = true;
+      for (int l = tid; l < G; l += 64) ok = ok && gld(&a.flags[(size_t)l * 32]) == a.seq;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22) || gld(a.timeout)) {
+        if (tid == 0) gst(a.timeout, 1u);
+        to = 1;
+        break;
+      }
+    }
+    if (tid == 0) s_to = to;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only: loads stay below the poll
+  __syncthreads();
+  return s_to == 0;
+}
+
+template <int BLOCK, bool SYS>
+__global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
+  constexpr int NW = BLOCK / 64;
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
   __shared__ ksg_profile s_prof;
-  __shared__ int32_t s_st[4][4];
-  __shared__ unsigned long long s_key[4];
-  __shared__ uint32_t s_err[4];
+  __shared__ int32_t s_st[4][NW];
+  __shared__ unsigned long long s_key[NW];
+  __shared__ uint32_t s_err[NW];
   __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int G = (int)gridDim.x;
   const DevCluster& c = a.c;
   const int N = c.N;
   const size_t NN = N;
@@ -85,143 +153,175 @@ __global__ __launch_bounds__(256) void ksg_eval_cycle(CycArgs a) {
       reinterpret_cast<int32_t*>(&s_pod)[tid] = reinterpret_cast<const int32_t*>(a.spod)[tid];
     __syncthreads();
     const int64_t boff = s_pod.blob - a.sbase;
-    for (int i = tid; i < s_pod.blob_len; i += 256) s_blob[i] = a.sprog[boff + i];
+    for (int i = tid; i < s_pod.blob_len; i += BLOCK) s_blob[i] = a.sprog[boff + i];
     gprog = a.sprog - a.sbase;
     if (blockIdx.x == 0) {
       if (tid < (int)(sizeof(ksg_pod) / 4))
         reinterpret_cast<int32_t*>(a.wpods)[tid] = reinterpret_cast<const int32_t*>(&s_pod)[tid];
-      for (int64_t i = tid; i < a.slen; i += 256) a.wprog[i] = a.sprog[i];
+      for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
     }
   } else {
-    stage_pod<256>(a.pods, a.prog, a.pod, &s_pod, s_blob);
+    stage_pod<BLOCK>(a.pods, a.prog, a.pod, &s_pod, s_blob);
   }
   __syncthreads();
   const PodView v = make_view(c, s_prof, s_pod, s_blob, gprog, false, a.st.ports);
 
-  // ---- every workgroup: its nodes ------------------------------------------------
-  const int n = blockIdx.x * 256 + tid;
-  int32_t feas = 0, mt = 0, ma = 0, lo = 0;
-  if (n < N) {
+  // ---- phase 1: this workgroup's nodes ------------------------------------------------
+  const int n = blockIdx.x * BLOCK + tid;
+  const bool own = n < N;
+  NodeEval e{KSG_FS_NOT_EVALUATED, 0, 0, 0, 0};
+  int64_t lraw[KSG_NPLUGINS] = {};
+  if (own) {
     NodeCols L;
     load_cols(c, a.st.requested, a.st.nonzero, a.st.pod_count, n, L);
-    int64_t lraw[KSG_NPLUGINS] = {};
-    const NodeEval e = eval_node_src(c, s_prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw);
-    a.h_fs[n] = e.st;
-    gst(&a.rec[n], pack_rec(e));
-    const bool ok = e.st == 0;
-    for (int q = 0; q < a.n_rows; q++) {
-      const int pl = a.rows[q];
-      int64_t x = 0;
-      switch (pl) {   // the node-local plugins; the others are not on this path
-        case KSG_PL_NODE_RESOURCES_FIT: x = lraw[KSG_PL_NODE_RESOURCES_FIT]; break;
-        case KSG_PL_BALANCED_ALLOCATION: x = lraw[KSG_PL_BALANCED_ALLOCATION]; break;
-        case KSG_PL_IMAGE_LOCALITY: x = lraw[KSG_PL_IMAGE_LOCALITY]; break;
-        case KSG_PL_TAINT_TOLERATION: x = lraw[KSG_PL_TAINT_TOLERATION]; break;
-        case KSG_PL_NODE_AFFINITY: x = lraw[KSG_PL_NODE_AFFINITY]; break;
-        default: break;
-      }
-      x = ok && ((v.smask >> pl) & 1u) ? x : 0;
-      cyc_put(a.h_raw, (size_t)q * NN + n, x, narrow);   // a pod with < 2 feasible nodes: zeroed below
-    }
-    if (ok) {
-      feas = 1;
-      mt = (int32_t)e.rt;
-      ma = (int32_t)e.ra;
-      lo = N - n;
-    }
+    e = eval_node_src(c, s_prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw);
   }
+  const bool ok = own && e.st == 0;
+  // the row value of score row q (node-local plugins only on this path)
+  auto raw_of = [&](int q) -> int64_t {
+    const int pl = a.rows[q];
+    int64_t x = 0;
+    switch (pl) {
+      case KSG_PL_NODE_RESOURCES_FIT: x = lraw[KSG_PL_NODE_RESOURCES_FIT]; break;
+      case KSG_PL_BALANCED_ALLOCATION: x = lraw[KSG_PL_BALANCED_ALLOCATION]; break;
+      case KSG_PL_IMAGE_LOCALITY: x = lraw[KSG_PL_IMAGE_LOCALITY]; break;
+      case KSG_PL_TAINT_TOLERATION: x = lraw[KSG_PL_TAINT_TOLERATION]; break;
+      case KSG_PL_NODE_AFFINITY: x = lraw[KSG_PL_NODE_AFFINITY]; break;
+      default: break;
+    }
+    return ok && ((v.smask >> pl) & 1u) ? x : 0;
+  };
+  if (own) {
+    hst<SYS>(a.h_fs + n, e.st);
+    for (int q = 0; q < a.n_rows; q++) cyc_put<SYS>(a.h_raw, (size_t)q * NN + n, raw_of(q), narrow);
+  }
+  int32_t feas = ok ? 1 : 0, mt = ok ? (int32_t)e.rt : 0, ma = ok ? (int32_t)e.ra : 0, lo = ok ? N - n : 0;
   feas = wave_sum32(feas);
   mt = (int32_t)wave_max64(mt);
   ma = (int32_t)wave_max64(ma);
   lo = (int32_t)wave_max64(lo);
-  if (lane == 0) { s_st[0][wv] = feas; s_st[1][wv] = mt; s_st[2][wv] = ma; s_st[3][wv] = lo; }
-  __syncthreads();
+  if (NW > 1) {
+    if (lane == 0) { s_st[0][wv] = feas; s_st[1][wv] = mt; s_st[2][wv] = ma; s_st[3][wv] = lo; }
+    __syncthreads();
+    if (tid == 0)
+      for (int i = 1; i < NW; i++) {
+        feas += s_st[0][i];
+        mt = max(mt, s_st[1][i]);
+        ma = max(ma, s_st[2][i]);
+        lo = max(lo, s_st[3][i]);
+      }
+  }
   if (tid == 0) {
-    int32_t f = 0, t = 0, m = 0, l = 0;
-    for (int i = 0; i < 4; i++) {
-      f += s_st[0][i];
-      t = max(t, s_st[1][i]);
-      m = max(m, s_st[2][i]);
-      l = max(l, s_st[3][i]);
-    }
     CycPart* pp = a.parts + blockIdx.x;
-    gst(&pp->nfeas, f);
-    gst(&pp->max_t, t);
-    gst(&pp->max_a, m);
-    gst(&pp->lo, l);
+    gst(&pp->nfeas, feas);
+    gst(&pp->max_t, mt);
+    gst(&pp->max_a, ma);
+    gst(&pp->lo, lo);
   }
-  // every wave's host and hand-off stores performed before the arrival
-  __threadfence_system();
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)a.done, 1u,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
 
-  // ---- the last arrival: fold, normalise, select ------------------------------------
-  int32_t f = 0, t = 0, m = 0, l = 0;
-  for (int b = tid; b < (int)gridDim.x; b += 256) {
-    const CycPart* pp = a.parts + b;
-    f += gld(&pp->nfeas);
-    t = max(t, gld(&pp->max_t));
-    m = max(m, gld(&pp->max_a));
-    l = max(l, gld(&pp->lo));
-  }
-  f = wave_sum32(f);
-  t = (int32_t)wave_max64(t);
-  m = (int32_t)wave_max64(m);
-  l = (int32_t)wave_max64(l);
-  __syncthreads();   // s_st reuse
-  if (lane == 0) { s_st[0][wv] = f; s_st[1][wv] = t; s_st[2][wv] = m; s_st[3][wv] = l; }
-  __syncthreads();
+  // ---- exchange -------------------------------------------------------------------------
+  const bool xok = cyc_exchange<BLOCK>(a, G);
+
+  // ---- phase 2: fold the slots, normalise this workgroup's nodes ------------------------
   int32_t nfeas = 0, max_t = 0, max_a = 0, low = 0;
-  for (int i = 0; i < 4; i++) {
-    nfeas += s_st[0][i];
-    max_t = max(max_t, s_st[1][i]);
-    max_a = max(max_a, s_st[2][i]);
-    low = max(low, s_st[3][i]);
+  for (int b = tid; b < G; b += BLOCK) {
+    const CycPart* pp = a.parts + b;
+    nfeas += gld(&pp->nfeas);
+    max_t = max(max_t, gld(&pp->max_t));
+    max_a = max(max_a, gld(&pp->max_a));
+    low = max(low, gld(&pp->lo));
+  }
+  nfeas = wave_sum32(nfeas);
+  max_t = (int32_t)wave_max64(max_t);
+  max_a = (int32_t)wave_max64(max_a);
+  low = (int32_t)wave_max64(low);
+  if (NW > 1) {
+    __syncthreads();   // s_st reuse
+    if (lane == 0) { s_st[0][wv] = nfeas; s_st[1][wv] = max_t; s_st[2][wv] = max_a; s_st[3][wv] = low; }
+    __syncthreads();
+    nfeas = 0; max_t = 0; max_a = 0; low = 0;
+    for (int i = 0; i < NW; i++) {
+      nfeas += s_st[0][i];
+      max_t = max(max_t, s_st[1][i]);
+      max_a = max(max_a, s_st[2][i]);
+      low = max(low, s_st[3][i]);
+    }
   }
   uint64_t key = 0;
   uint32_t err = 0;
-  for (int k = tid; k < N; k += 256) {
-    const uint64_t x = gld(&a.rec[k]);
+  if (own) {
     int64_t total = 0, nt = 0, na = 0;
-    if (nfeas >= 2 && (x >> 63)) {
-      total = total_score(v, (uint32_t)x, (x >> 48) & 0xff, (x >> 32) & 0xffff, max_t, max_a, err, &nt, &na);
-      const uint64_t kk = argmax_key(total, k);
-      key = kk > key ? kk : key;
+    if (nfeas >= 2 && ok) {
+      total = total_score(v, e.part, e.rt, e.ra, max_t, max_a, err, &nt, &na);
+      key = argmax_key(total, n);
     }
-    cyc_put(a.h_tot, k, total, narrow);
-    for (int q = 0; q < a.n_rows; q++) {
-      const int pl = a.rows[q];
-      if (nfeas < 2) {   // fewer than two feasible nodes: no Score runs, nothing recorded
-        cyc_put(a.h_raw, (size_t)q * NN + k, 0, narrow);
-        if (q < a.n_normrows) cyc_put(a.h_norm, (size_t)q * NN + k, 0, narrow);
-      } else if (q < a.n_normrows) {
-        cyc_put(a.h_norm, (size_t)q * NN + k, pl == KSG_PL_TAINT_TOLERATION ? nt : na, narrow);
+    cyc_put<SYS>(a.h_tot, n, total, narrow);
+    if (nfeas >= 2) {
+      for (int q = 0; q < a.n_normrows; q++)
+        cyc_put<SYS>(a.h_norm, (size_t)q * NN + n, a.rows[q] == KSG_PL_TAINT_TOLERATION ? nt : na, narrow);
+    } else {   // fewer than two feasible nodes: no Score ran, nothing recorded
+      for (int q = 0; q < a.n_rows; q++) {
+        cyc_put<SYS>(a.h_raw, (size_t)q * NN + n, 0, narrow);
+        if (q < a.n_normrows) cyc_put<SYS>(a.h_norm, (size_t)q * NN + n, 0, narrow);
       }
     }
   }
   key = wave_max_u64(key);
   err = wave_or32(err);
-  if (lane == 0) { s_key[wv] = key; s_err[wv] = err; }
+  if (NW > 1) {
+    if (lane == 0) { s_key[wv] = key; s_err[wv] = err; }
+    __syncthreads();
+    if (tid == 0)
+      for (int i = 1; i < NW; i++) { key = s_key[i] > key ? s_key[i] : key; err |= s_err[i]; }
+  }
+  if (tid == 0) {
+    gst(&a.keys[blockIdx.x].key, key);
+    gst(&a.keys[blockIdx.x].err, err | (xok ? 0u : 2u));
+  }
+  // every wave's host stores performed (system scope) and its keys store
+  // drained before the arrival
+  host_release<SYS>();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    uint64_t k = 0;
-    uint32_t e = 0;
-    for (int i = 0; i < 4; i++) { k = s_key[i] > k ? s_key[i] : k; e |= s_err[i]; }
-    a.h_stats[0] = nfeas;
-    a.h_stats[1] = max_t;
-    a.h_stats[2] = max_a;
-    a.h_stats[3] = low;
-    *a.h_best = k;
-    *a.h_err = e;
-    gst(a.done, 0u);   // the next call's arrivals
+    const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)a.done, 1u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == (unsigned)G - 1;
   }
-  __threadfence_system();
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(a.h_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // The last adder reads the G keys with sc1 loads only (gld), every one
+  // stored sc1 and drained before its workgroup's add: the MI355X guide's
+  // "Valid forms" row 1 (one unsharded counter, the workgroup whose add came
+  // last), so no acquire fence.
+  if (!s_last) return;
+
+  // ---- the last arrival: fold G keys, publish -------------------------------------------
+  uint64_t best = 0;
+  uint32_t berr = 0;
+  for (int b = tid; b < G; b += BLOCK) {
+    const uint64_t k = gld(&a.keys[b].key);
+    best = k > best ? k : best;
+    berr |= gld(&a.keys[b].err);
+  }
+  best = wave_max_u64(best);
+  berr = wave_or32(berr);
+  if (NW > 1) {
+    __syncthreads();   // s_key reuse
+    if (lane == 0) { s_key[wv] = best; s_err[wv] = berr; }
+    __syncthreads();
+    if (tid == 0)
+      for (int i = 1; i < NW; i++) { best = s_key[i] > best ? s_key[i] : best; berr |= s_err[i]; }
+  }
+  if (tid == 0) {
+    hst<SYS>(a.h_stats + 0, nfeas);
+    hst<SYS>(a.h_stats + 1, max_t);
+    hst<SYS>(a.h_stats + 2, max_a);
+    hst<SYS>(a.h_stats + 3, low);
+    hst<SYS>(a.h_best, (unsigned long long)best);
+    hst<SYS>(a.h_err, berr);
+    gst(a.done, 0u);   // the next call's arrivals
+    host_release<SYS>();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.h_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }

@@ -275,11 +275,15 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   auto issue = [&](const SvItem& it) -> Pending {
     Pending p{it, 0, 0, 0};
     if (it.node < 0) return p;
+    if (a.inject_walk_err && lane == 0 && it.node >= 0) {   // tests: the report path below, without a bad load
+      using G1 = __attribute__((address_space(1))) unsigned;
+      __hip_atomic_store((G1*)a.walk_err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (it.node >= N) {   // cannot happen; never load through it (reported as code 3)
       p.it.node = -1;
-      if (lane == 0 && a.tk_timeout) {
+      if (lane == 0) {
         using G1 = __attribute__((address_space(1))) unsigned;
-        __hip_atomic_store((G1*)a.tk_timeout, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((G1*)a.walk_err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return p;
     }
@@ -643,9 +647,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     ns_c = s_ctl[2];
     nspecial = s_ctl[3];
   }
-  if (tid == 0 && start < nb && a.tk_timeout) {   // cannot happen: each round commits >= 1 pod
+  if (tid == 0 && start < nb) {   // cannot happen: each round commits >= 1 pod
     using G1 = __attribute__((address_space(1))) unsigned;
-    __hip_atomic_store((G1*)a.tk_timeout, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((G1*)a.walk_err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // ---- epilogue: rows, results, count tables, carry-out -----------------------------
   // (a correction left as the last round's item has its row written here)

@@ -1885,6 +1885,27 @@ int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index)
   p.default_sel = copy_sel(v->default_spread_selector);
   p.terminating = v->terminating != 0;
   p.priority = v->priority;
+  // volumes whose source makes a volume plugin's PreFilter run (include/
+  // ksched_snapshot.h ksg_volume_view; model.Pod.volumes_needing_plugins):
+  // refused while any volume plugin runs at PreFilter or Filter
+  if (v->n_volumes < 0 || (v->n_volumes > 0 && !v->volumes)) return KSG_E_INVALID;
+  bool vol_run = false;
+  for (int pt : {KSG_POINT_PREFILTER, KSG_POINT_FILTER})
+    for (int pid : s->prof.order[pt])
+      vol_run = vol_run || pid == KSG_PL_VOLUME_RESTRICTIONS || pid == KSG_PL_NODE_VOLUME_LIMITS ||
+                pid == KSG_PL_VOLUME_BINDING || pid == KSG_PL_VOLUME_ZONE;
+  for (int32_t i = 0; vol_run && i < v->n_volumes; i++) {
+    static const char* const kRefused[] = {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk",
+                                           "awsElasticBlockStore", "azureDisk", "azureFile", "cinder",
+                                           "vsphereVolume", "portworxVolume", "rbd", "iscsi"};
+    const std::string kind = S(v->volumes[i].kind);
+    for (const char* k : kRefused)
+      if (kind == k)
+        return fail(s, KSG_E_UNSUPPORTED,
+                    "pod " + p.ns + "/" + p.name + ": volume '" + S(v->volumes[i].name) + "' (" + kind +
+                        ") makes the volume plugins' PreFilter run; VolumeBinding / VolumeZone / NodeVolumeLimits / "
+                        "VolumeRestrictions are modelled only as their Skip");
+  }
   try {
     resolve_namespaces(s, p);
     validate_pod(s, p);

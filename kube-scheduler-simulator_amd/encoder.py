@@ -707,6 +707,16 @@ class Encoder:
 
     def _encode_pods(self) -> EncodedWorkload:
         prof = self.prof
+        vol = {P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE}
+        vol_run = vol & (set(prof.prefilter_order()) | set(prof.filter_order()))
+        if vol_run:
+            for p in self.pods:
+                bad = p.volumes_needing_plugins()
+                if bad:
+                    raise NotImplementedError(
+                        f"pod {p.namespace}/{p.name}: volume {bad[0][0]!r} ({bad[0][1]}) makes the volume plugins' "
+                        f"PreFilter run; VolumeBinding / VolumeZone / NodeVolumeLimits / VolumeRestrictions are "
+                        f"modelled only as their Skip")
         rec = np.zeros(len(self.pods), POD_DTYPE)
         names = []
         ba_cols = [self.res_col[r] for r, _ in prof.ba_resources if r in self.res_col]
@@ -734,7 +744,7 @@ class Encoder:
             if not p.host_ports():
                 fskip |= 1 << P.NODE_PORTS     # nodeports PreFilter: Skip without host ports
             for v in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE):
-                fskip |= 1 << v
+                fskip |= 1 << v   # no claim / ephemeral / in-tree disk volume (checked above): PreFilter Skip
             hard, soft = self._pts_cache[i]
             if not hard:
                 fskip |= 1 << P.POD_TOPOLOGY_SPREAD

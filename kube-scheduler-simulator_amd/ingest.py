@@ -173,6 +173,16 @@ def _container(c: dict, init: bool) -> m.Container:
                        restartable=init and c.get("restartPolicy") == "Always", host_ports=ports)
 
 
+def _volume(v: dict) -> Tuple[str, str, str]:
+    """v1.Volume -> (name, the VolumeSource field set (its JSON key), claimName)."""
+    kinds = [k for k in v if k != "name" and v[k] is not None]
+    if len(kinds) != 1:
+        raise ValueError(f"volume {v.get('name')!r}: expected exactly one volume source, got {kinds}")
+    kind = kinds[0]
+    claim = (v[kind] or {}).get("claimName", "") if kind == "persistentVolumeClaim" else ""
+    return v.get("name", ""), kind, claim
+
+
 def pod_from_k8s(obj: dict, ns_labels: Optional[Dict[str, Dict[str, str]]] = None) -> m.Pod:
     """v1.Pod JSON -> model.Pod, after the simulator's mutatePods (owners and
     service account dropped: they do not enter the Filter/Score path except
@@ -205,6 +215,7 @@ def pod_from_k8s(obj: dict, ns_labels: Optional[Dict[str, Dict[str, str]]] = Non
                                for t in a.get("preferredDuringSchedulingIgnoredDuringExecution") or ()])
     p.tolerations = [m.Toleration(t.get("key", ""), t.get("operator", ""), str(t.get("value", "")), t.get("effect", ""))
                      for t in spec.get("tolerations") or ()]
+    p.volumes = [_volume(v) for v in spec.get("volumes") or ()]
     p.topology_spread_constraints = [
         m.TopologySpreadConstraint(int(c["maxSkew"]), c["topologyKey"], c["whenUnsatisfiable"],
                                    label_selector(c.get("labelSelector")),

@@ -195,6 +195,20 @@ class Pod:
     priority: int = 0
     preemption_policy: str = "PreemptLowerPriority"
     start_time: Optional[int] = None
+    # spec.volumes: (name, the v1.VolumeSource field that is set, its JSON key,
+    # persistentVolumeClaim.claimName or "")
+    volumes: List[Tuple[str, str, str]] = field(default_factory=list)
+
+    def volumes_needing_plugins(self):
+        """The volumes whose source makes a volume plugin's PreFilter run
+        instead of returning Skip [upstream v1.32 plugins/volumebinding
+        (podHasPVCs: claims and generic ephemeral volumes),
+        nodevolumelimits/csi.go PreFilter (claims, ephemeral, in-tree volumes
+        CSI migration translates), volumerestrictions (GCE PD, AWS EBS, RBD,
+        iSCSI, ReadWriteOncePod claims), volumezone (claims)]: the evaluator
+        models every other source as those plugins' Skip, and refuses these
+        (NotImplementedError) rather than record a Skip upstream would not."""
+        return [(n, k) for n, k, _ in self.volumes if k in VOLUME_SOURCES_REFUSED]
 
     def has_pod_affinity(self) -> bool:
         return bool(self.pod_affinity_required or self.pod_affinity_preferred
@@ -213,6 +227,10 @@ class Pod:
             out.extend(x for x in c.host_ports if x[2] > 0)
         return out
 
+
+VOLUME_SOURCES_REFUSED = frozenset((
+    "persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "azureFile",
+    "cinder", "vsphereVolume", "portworxVolume", "rbd", "iscsi"))
 
 DEFAULT_BIND_ALL_HOST_IP = "0.0.0.0"
 

@@ -95,6 +95,10 @@ class NodeView(C.Structure):
                 ("unschedulable", i32), ("n_images", i32), ("images", C.POINTER(ImageView))]
 
 
+class VolumeView(C.Structure):
+    _fields_ = [("name", cp), ("kind", cp), ("claim_name", cp)]
+
+
 class PodView(C.Structure):
     _fields_ = [
         ("namespace_", cp), ("name", cp), ("n_labels", i32), ("labels", C.POINTER(StrPair)),
@@ -112,7 +116,7 @@ class PodView(C.Structure):
         ("n_tolerations", i32), ("tolerations", C.POINTER(TolerationView)),
         ("n_spread", i32), ("spread", C.POINTER(SpreadView)),
         ("default_spread_selector", LabelSelectorView),
-        ("terminating", i32), ("priority", i32)]
+        ("terminating", i32), ("priority", i32), ("n_volumes", i32), ("volumes", C.POINTER(VolumeView))]
 
 
 class PluginView(C.Structure):
@@ -253,6 +257,7 @@ def pod_view(p: m.Pod, k: _Keep) -> PodView:
     v.default_spread_selector = k.sel(p.default_spread_selector)
     v.terminating = 1 if p.terminating else 0
     v.priority = int(p.priority)
+    v.n_volumes, v.volumes = k.arr(VolumeView, [VolumeView(_b(n), _b(kind), _b(claim)) for n, kind, claim in p.volumes])
     return v
 
 

@@ -28,6 +28,7 @@ import (
 	"k8s.io/apimachinery/pkg/runtime"
 	"k8s.io/apimachinery/pkg/types"
 	"k8s.io/apimachinery/pkg/util/sets"
+	"k8s.io/client-go/tools/cache"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
 
 	"example.invalid/ksched-mi355x/shim/go/ksched"
@@ -44,7 +45,7 @@ const fsNotEvaluated = 0xFF // KSG_FS_NOT_EVALUATED
 type podState struct {
 	pod   int // snapshot pod index
 	ev    *ksched.PodEval
-	index map[string]int // node name -> column
+	index map[string]int // node name -> column (the Evaluator's, built once per snapshot load)
 	codes []int32        // per node: framework.Code of the rejection (ksched.Code*)
 	msgID []int32        // per node: index into msgs, -1 = passed / not evaluated
 	msgs  []string
@@ -85,15 +86,25 @@ type Evaluator struct {
 	defaultSel DefaultSelectorFunc
 
 	nodes   []string          // column order of the loaded snapshot
+	index   map[string]int    // node name -> column; replaced (never mutated) by rebuild
 	nodeRV  map[string]string // node ResourceVersion at load
 	nodeGen map[string]int64  // NodeInfo.Generation at the last diff
 	podIdx  map[types.UID]int // pod -> snapshot index
 	podRV   map[types.UID]string
 	podNode map[types.UID]int // pods bound / assumed on the device -> column
-	// snapshot pods no longer current (a pod re-encoded after an update, or
-	// deleted while pending): the snapshot only appends, so past a threshold
+	// snapshot pods no longer current (a pod re-encoded after an update, a
+	// pod that left its node, a pending pod deleted): the snapshot only
+	// appends, so once they outnumber the live pods (podIdx) past a threshold
 	// the next sync rebuilds it from the NodeInfos (bound pods only)
 	stale int
+
+	// fed by informer handlers (attach), drained under mu:
+	side      sync.Mutex
+	nominated map[string]struct{} // nodes that may hold nominated pods
+	gone      []types.UID         // pods deleted since the last sync
+	nsDirty   bool                // a namespace was added or its labels changed
+	attached  sync.Once
+	nsList    func() ([]*v1.Namespace, error) // the handle's namespace lister, nil before attach
 }
 
 // staleLimit: rebuild once this many superseded snapshot pods accumulated
@@ -106,7 +117,112 @@ func NewEvaluator(dev int, prof *ksched.ProfileArgs, ds DefaultSelectorFunc) (*E
 	if err != nil {
 		return nil, err
 	}
-	return &Evaluator{ctx: ctx, prof: prof, defaultSel: ds}, nil
+	return &Evaluator{ctx: ctx, prof: prof, defaultSel: ds, nominated: map[string]struct{}{}}, nil
+}
+
+// attach subscribes to the handle's informers once: namespaces (their labels
+// resolve namespaceSelector terms: the snapshot must hold them before any pod
+// that uses one is encoded) and pods (nominations, so the nominated pass
+// visits only nodes that may hold nominated pods, and deletions of pending
+// pods, which make their snapshot entries stale).
+func (e *Evaluator) attach(h framework.Handle) {
+	e.attached.Do(func() {
+		f := h.SharedInformerFactory()
+		if f == nil {
+			return
+		}
+		nsInf := f.Core().V1().Namespaces()
+		lister := nsInf.Lister()
+		e.side.Lock()
+		e.nsList = func() ([]*v1.Namespace, error) { return lister.List(labels.Everything()) }
+		e.nsDirty = true
+		e.side.Unlock()
+		_, _ = nsInf.Informer().AddEventHandler(cache.ResourceEventHandlerFuncs{
+			AddFunc:    func(interface{}) { e.markNamespaces() },
+			UpdateFunc: func(o, n interface{}) { e.markNamespaces() },
+		})
+		_, _ = f.Core().V1().Pods().Informer().AddEventHandler(cache.ResourceEventHandlerFuncs{
+			AddFunc:    func(o interface{}) { e.notePod(o) },
+			UpdateFunc: func(_, n interface{}) { e.notePod(n) },
+			DeleteFunc: func(o interface{}) {
+				if t, ok := o.(cache.DeletedFinalStateUnknown); ok {
+					o = t.Obj
+				}
+				if p, ok := o.(*v1.Pod); ok {
+					e.side.Lock()
+					e.gone = append(e.gone, p.UID)
+					e.side.Unlock()
+				}
+			},
+		})
+	})
+}
+
+func (e *Evaluator) markNamespaces() {
+	e.side.Lock()
+	e.nsDirty = true
+	e.side.Unlock()
+}
+
+func (e *Evaluator) notePod(o interface{}) {
+	if p, ok := o.(*v1.Pod); ok && p.Status.NominatedNodeName != "" {
+		e.noteNominated(p.Status.NominatedNodeName)
+	}
+}
+
+// noteNominated records a node that may hold nominated pods (the informer,
+// and this shim's own PostFilter when it nominates).
+func (e *Evaluator) noteNominated(node string) {
+	e.side.Lock()
+	e.nominated[node] = struct{}{}
+	e.side.Unlock()
+}
+
+// syncNamespaces (under mu) registers every namespace with the snapshot when
+// one was added or relabelled since the last sync; the native encoder
+// re-resolves namespaceSelector terms when a namespace's labels change.
+func (e *Evaluator) syncNamespaces(force bool) error {
+	e.side.Lock()
+	dirty, list := e.nsDirty || force, e.nsList
+	e.nsDirty = false
+	e.side.Unlock()
+	if !dirty || list == nil || e.snap == nil {
+		return nil
+	}
+	nss, err := list()
+	if err != nil {
+		return err
+	}
+	for _, ns := range nss {
+		if err := e.snap.AddNamespace(ns); err != nil {
+			return err
+		}
+	}
+	return nil
+}
+
+// pruneGone (under mu) drops pods deleted while pending from the maps and
+// counts their snapshot entries as stale.
+func (e *Evaluator) pruneGone() {
+	e.side.Lock()
+	gone := e.gone
+	e.gone = nil
+	e.side.Unlock()
+	for _, uid := range gone {
+		if c, ok := e.podNode[uid]; ok && c >= 0 {
+			continue // still on the device: syncCluster forgets it when it leaves its node
+		}
+		if _, ok := e.podIdx[uid]; ok {
+			e.forgetUID(uid)
+		}
+	}
+}
+
+func (e *Evaluator) forgetUID(uid types.UID) {
+	delete(e.podIdx, uid)
+	delete(e.podRV, uid)
+	delete(e.podNode, uid)
+	e.stale++
 }
 
 func (e *Evaluator) selectorOf(p *v1.Pod) labels.Selector {
@@ -128,17 +244,24 @@ func (e *Evaluator) rebuild(infos []*framework.NodeInfo) error {
 	}
 	e.snap = snap
 	e.nodes = e.nodes[:0]
+	e.index = make(map[string]int, len(infos))
 	e.nodeRV, e.nodeGen = map[string]string{}, map[string]int64{}
 	e.podIdx, e.podRV, e.podNode = map[types.UID]int{}, map[types.UID]string{}, map[types.UID]int{}
 	e.stale = 0
-	for _, ni := range infos {
+	for col, ni := range infos {
 		n := ni.Node()
 		if _, err := snap.AddNode(n); err != nil {
 			return err
 		}
 		e.nodes = append(e.nodes, n.Name)
+		e.index[n.Name] = col
 		e.nodeRV[n.Name] = n.ResourceVersion
 		e.nodeGen[n.Name] = ni.Generation
+	}
+	// every namespace before the first pod: a bound pod's namespaceSelector
+	// term needs them to encode
+	if err := e.syncNamespaces(true); err != nil {
+		return err
 	}
 	for col, ni := range infos {
 		for _, pi := range ni.Pods {
@@ -160,6 +283,7 @@ func (e *Evaluator) rebuild(infos []*framework.NodeInfo) error {
 // that appeared on / left a node since the last cycle (the previous cycle's
 // assume among them) are assumed / forgotten one by one.
 func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
+	e.pruneGone()
 	same := e.snap != nil && len(infos) == len(e.nodes) &&
 		!(e.stale > staleLimit && e.stale > len(e.podIdx))
 	for i := 0; same && i < len(infos); i++ {
@@ -168,6 +292,9 @@ func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
 	}
 	if !same {
 		return e.rebuild(infos)
+	}
+	if err := e.syncNamespaces(false); err != nil {
+		return err
 	}
 	for col, ni := range infos {
 		name := e.nodes[col]
@@ -210,7 +337,9 @@ func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
 				if err := e.snap.Forget(e.ctx, e.podIdx[uid], col); err != nil {
 					return err
 				}
-				e.podNode[uid] = -1
+				// deleted (or moved: a node visited later finds it unknown and
+				// encodes it afresh); its snapshot entry is stale either way
+				e.forgetUID(uid)
 			}
 		}
 		e.nodeGen[name] = ni.Generation
@@ -248,7 +377,10 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 	if _, err := e.snap.Sync(e.ctx); err != nil {
 		return nil, err
 	}
-	st := &podState{pod: idx, index: make(map[string]int, len(e.nodes))}
+	if pod.Status.NominatedNodeName != "" {
+		e.noteNominated(pod.Status.NominatedNodeName)
+	}
+	st := &podState{pod: idx, index: e.index}
 	// nominated pods first: their evaluations reuse the library's result
 	// block, which the pod's own evaluation below then keeps for the cycle
 	if nom != nil {
@@ -261,9 +393,6 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 		return nil, err
 	}
 	st.ev = ev
-	for i, n := range e.nodes {
-		st.index[n] = i
-	}
 	// every rejected node's Status, once per pod (ksg_snapshot_statuses)
 	if st.codes, st.msgID, st.msgs, err = e.snap.Statuses(idx, ev.FStatus); err != nil {
 		return nil, err
@@ -287,11 +416,29 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 // Filter answers the framework's first pass from this verdict and its second
 // pass from the plain evaluation.  Nominated nodes are few (preemptors
 // waiting for their victims to leave), so this costs an evaluation each.
+// Only nodes that may hold nominated pods are visited (attach, PostFilter);
+// a node found without any is dropped from that set.
 func (e *Evaluator) nominatedPass(st *podState, pod *v1.Pod, nom framework.PodNominator) error {
 	prio := podPriority(pod)
-	for col, name := range e.nodes {
+	e.side.Lock()
+	names := make([]string, 0, len(e.nominated))
+	for name := range e.nominated {
+		names = append(names, name)
+	}
+	e.side.Unlock()
+	for _, name := range names {
+		col, ok := e.index[name]
+		nominated := nom.NominatedPodsForNode(name)
+		if len(nominated) == 0 {
+			e.side.Lock()
+			delete(e.nominated, name)
+			e.side.Unlock()
+		}
+		if !ok {
+			continue
+		}
 		var add []*v1.Pod
-		for _, pi := range nom.NominatedPodsForNode(name) {
+		for _, pi := range nominated {
 			if pi.Pod.UID != pod.UID && podPriority(pi.Pod) >= prio {
 				add = append(add, pi.Pod)
 			}
@@ -630,6 +777,7 @@ func Factories(ev *Evaluator) map[string]func(context.Context, runtime.Object, f
 			if err := ev.applyArgs(t.name, obj); err != nil {
 				return nil, err
 			}
+			ev.attach(h)
 			return t.make(base{name: t.name, id: t.id, ev: ev, h: h}), nil
 		}
 	}

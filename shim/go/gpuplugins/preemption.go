@@ -218,6 +218,7 @@ func (p *preemption) PostFilter(ctx context.Context, cs *framework.CycleState, p
 		return nil, framework.NewStatus(framework.Unschedulable, "preemption: no candidate node")
 	}
 	best := pickOne(cands)
+	e.noteNominated(best.node) // the next cycles' nominated pass visits it
 	for _, v := range best.victims { // prepareCandidate
 		if err := p.h.ClientSet().CoreV1().Pods(v.Namespace).Delete(ctx, v.Name, metav1.DeleteOptions{}); err != nil {
 			return nil, framework.AsStatus(err)

@@ -291,7 +291,46 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 	if p.Spec.Priority != nil {
 		v.priority = C.int32_t(*p.Spec.Priority)
 	}
+	vols := unsafe.Slice((*C.ksg_volume_view)(a.alloc(len(p.Spec.Volumes), C.sizeof_ksg_volume_view)), len(p.Spec.Volumes)+1)
+	for i, vol := range p.Spec.Volumes {
+		vols[i].name, vols[i].kind = a.str(vol.Name), a.str(volumeKind(&vol.VolumeSource))
+		if vol.PersistentVolumeClaim != nil {
+			vols[i].claim_name = a.str(vol.PersistentVolumeClaim.ClaimName)
+		}
+	}
+	v.n_volumes, v.volumes = C.int32_t(len(p.Spec.Volumes)), &vols[0]
 	return v
+}
+
+// volumeKind is the JSON key of the VolumeSource field that is set (the
+// sources the volume plugins' PreFilter reacts to are named; any other one is
+// "other", which they Skip).
+func volumeKind(s *v1.VolumeSource) string {
+	switch {
+	case s.PersistentVolumeClaim != nil:
+		return "persistentVolumeClaim"
+	case s.Ephemeral != nil:
+		return "ephemeral"
+	case s.GCEPersistentDisk != nil:
+		return "gcePersistentDisk"
+	case s.AWSElasticBlockStore != nil:
+		return "awsElasticBlockStore"
+	case s.AzureDisk != nil:
+		return "azureDisk"
+	case s.AzureFile != nil:
+		return "azureFile"
+	case s.Cinder != nil:
+		return "cinder"
+	case s.VsphereVolume != nil:
+		return "vsphereVolume"
+	case s.PortworxVolume != nil:
+		return "portworxVolume"
+	case s.RBD != nil:
+		return "rbd"
+	case s.ISCSI != nil:
+		return "iscsi"
+	}
+	return "other"
 }
 
 // Plugin is one configv1.Plugin (name, weight).

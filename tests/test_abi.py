@@ -73,7 +73,7 @@ def test_snapshot_view_layouts(tmp_path):
              "ksg_node_selector_term_view": S.NodeSelectorTermView, "ksg_preferred_term_view": S.PreferredTermView,
              "ksg_label_selector_view": S.LabelSelectorView, "ksg_affinity_term_view": S.AffinityTermView,
              "ksg_spread_view": S.SpreadView, "ksg_host_port_view": S.HostPortView, "ksg_container_view": S.ContainerView, "ksg_image_view": S.ImageView,
-             "ksg_node_view": S.NodeView, "ksg_pod_view": S.PodView, "ksg_plugin_view": S.PluginView,
+             "ksg_node_view": S.NodeView, "ksg_volume_view": S.VolumeView, "ksg_pod_view": S.PodView, "ksg_plugin_view": S.PluginView,
              "ksg_plugin_set_view": S.PluginSetView, "ksg_profile_view": S.ProfileView,
              "ksg_profile_info": S.ProfileInfo}
     src = tmp_path / "sz.c"
@@ -91,3 +91,16 @@ def test_product_path_fails_loudly_without_library(tmp_path):
     import pytest
     with pytest.raises(native.KschedError):
         native.Engine(lib_path=str(tmp_path / "missing.so"))
+
+
+def test_library_embeds_the_tree_source_hash(built):
+    """bench.py measures the committed source: the built library carries the
+    sha256 of csrc/ + include/ (ksg_source_hash), equal to the tree's."""
+    import importlib
+    ge = importlib.import_module("__graft_entry__")
+    native = pkg("native")
+    lib = ctypes.CDLL(native.LIB_PATH)
+    lib.ksg_source_hash.restype = ctypes.c_char_p
+    want = ge.source_hash()
+    assert lib.ksg_source_hash().decode() == want
+    assert ge.library_hash(native.LIB_PATH) == want

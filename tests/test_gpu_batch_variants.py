@@ -197,3 +197,17 @@ def test_spec_runs_and_matches_oracle(oracle, strategy, seed):
     R = len(enc.cluster.res_names)
     for x, y in zip(a.read_state(R), oracle.read_state(R)):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_spec_walk_guard_reaches_the_host(overlap):
+    """The walk's broken-invariant word (a node index outside the cluster,
+    or a round that committed nothing) is armed in every mode, the PMC passes'
+    KSG_PIPE_OVERLAP=0 included: an injected report fails the call loudly."""
+    nodes, pods, prof = G.config2(n_nodes=600, n_pods=400, seed=3)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = _engine_with_batch_mode("spec", KSG_PIPE_OVERLAP=overlap, KSG_TEST_INJECT_WALK_ERR=1)
+    a.load(enc, pf)
+    with pytest.raises(native.KschedError, match="invariant broken"):
+        a.run_queue(0, len(pods))

@@ -296,3 +296,73 @@ def test_export_profile_cpp_oracle_vs_pyoracle():
     assert want == got
     # the two weight maps really differ here, so the test separates them
     assert snap.profile.weights()["TaintToleration"] != snap.profile.selection_weights()["TaintToleration"]
+
+
+# ---- volumes: export.md case 2 holds 2 PVs and 1 PVC ----
+
+def _volume_doc(disable_volume_plugins: bool = False):
+    """export.md case 2 (its PVs, PVC and priority classes) plus one node, a
+    pod claiming the sample's pvc1 and a pod with only an emptyDir."""
+    import copy
+    doc = copy.deepcopy(_export("case2"))
+    cfg = export_config_loadable()
+    if disable_volume_plugins:
+        for point in ("multiPoint", "preFilter", "filter"):
+            ps = cfg["profiles"][0]["plugins"].setdefault(point, {})
+            ps["enabled"] = [e for e in ps.get("enabled") or () if e["name"] not in
+                             ("VolumeBinding", "VolumeZone", "NodeVolumeLimits", "VolumeRestrictions")]
+            ps["disabled"] = list(ps.get("disabled") or ()) + [
+                {"name": n} for n in ("VolumeBinding", "VolumeZone", "NodeVolumeLimits", "VolumeRestrictions")]
+    doc["schedulerConfig"] = cfg
+    node = I.node_to_k8s(m.Node(name="n1", labels={"kubernetes.io/hostname": "n1"},
+                                allocatable={m.CPU: 4000, m.MEMORY: 8 << 30, "pods": 110}))
+    def pod(name, volumes):
+        d = I.pod_to_k8s(m.Pod(name=name, containers=[m.Container(requests={m.CPU: 100})]))
+        d["spec"]["volumes"] = volumes
+        return d
+    doc["nodes"] = [node]
+    doc["pods"] = [pod("scratch", [{"name": "tmp", "emptyDir": {}}]),
+                   pod("claims", [{"name": "data", "persistentVolumeClaim": {"claimName": "pvc1"}}])]
+    return doc
+
+
+def test_volumes_parsed_from_the_export_sample():
+    doc = _volume_doc()
+    assert len(doc["pvs"]) == 2 and len(doc["pvcs"]) == 1 and doc["pvcs"][0]["metadata"]["name"] == "pvc1"
+    snap = I.load_snapshot(doc)
+    byname = {p.name: p for p in snap.pods}
+    assert byname["claims"].volumes == [("data", "persistentVolumeClaim", "pvc1")]
+    assert byname["claims"].volumes_needing_plugins() == [("data", "persistentVolumeClaim")]
+    assert byname["scratch"].volumes == [("tmp", "emptyDir", "")]
+    assert byname["scratch"].volumes_needing_plugins() == []
+
+
+def test_claim_volume_refused_by_both_encoders():
+    """A PVC makes VolumeBinding / NodeVolumeLimits / VolumeZone PreFilter run
+    upstream: refused, never recorded as their Skip."""
+    S = pkg("snapshot")
+    snap = I.load_snapshot(_volume_doc())
+    with pytest.raises(NotImplementedError, match="pvc|persistentVolumeClaim"):
+        E.Encoder(snap.nodes, snap.pods, snap.profile)
+    s = S.Snapshot(snap.profile, snap.nodes)
+    ok = [p for p in snap.pods if p.name == "scratch"][0]
+    s.add_pod(ok)
+    with pytest.raises(S.SnapshotError, match="persistentVolumeClaim"):
+        s.add_pod([p for p in snap.pods if p.name == "claims"][0])
+
+
+def test_volume_sources_the_plugins_skip_encode():
+    """emptyDir (and every source outside the refused set) is the volume
+    plugins' Skip; with the volume plugins disabled a claim is irrelevant."""
+    snap = I.load_snapshot(_volume_doc())
+    pods = [p for p in snap.pods if p.name == "scratch"]
+    enc = E.Encoder(snap.nodes, pods, snap.profile)
+    fskip = int(enc.workload.pods[0]["filter_skip"])
+    for v in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE):
+        assert fskip >> v & 1
+    snap2 = I.load_snapshot(_volume_doc(disable_volume_plugins=True))
+    E.Encoder(snap2.nodes, snap2.pods, snap2.profile)   # no refusal
+    S = pkg("snapshot")
+    s = S.Snapshot(snap2.profile, snap2.nodes)
+    for p in snap2.pods:
+        s.add_pod(p)
