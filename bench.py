@@ -202,7 +202,7 @@ def replica_sweep(eng, enc, prof, G, E, metrics, replicas, R: int, P: int, rank:
             "roofline": roof}
 
 
-def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threads: int):
+def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threads: int, label: str = "configs[1]"):
     """Annotation bytes for the first n_pods of the queue (bulk.annotate_queue):
     end-to-end wall (device capture + D2H + ksg_annotate on `threads` workers),
     the capture alone, and an xxh3 digest over every pod's three values."""
@@ -245,8 +245,8 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
     eng.set_timing(False)
     h = xxhash.xxh3_64()
     h.update(digests.tobytes())
-    return {"workload": f"configs[1] cluster, first {n_pods} pods, {chunk}-pod chunks, capture on the batched "
-                        f"path + ksg_annotate on {threads} threads",
+    return {"workload": f"{label} cluster, first {n_pods} pods, {chunk}-pod chunks, device capture "
+                        f"+ ksg_annotate on {threads} threads",
             "pods_per_s": n_pods / wall, "wall_s": wall, "annotation_bytes": int(sizes.sum()),
             "annotation_MB_per_s": sizes.sum() / wall / 1e6,
             "capture_only_pods_per_s": n_pods / cap_wall, "capture_device_ms": dev_ms,
@@ -254,7 +254,7 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
             "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(), "threads": threads}
 
 
-def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
+def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=None, label: str = "configs[1]"):
     """The drop-in's per-cycle path, the calls the Go
     shim makes per scheduling cycle, through the C ABI of libksched.so:
     ksg_snapshot_add_pod -> ksg_snapshot_sync (append to the device
@@ -269,7 +269,7 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
     over the same pods."""
     import ctypes as C
     import numpy as np
-    nodes, pods, prof = G.config2(n_nodes=n_nodes, n_pods=warm + n_pods)
+    nodes, pods, prof = (make or G.config2)(n_nodes=n_nodes, n_pods=warm + n_pods)
     snap = S.Snapshot(prof, nodes)
     eng = native.Engine(device=0)
     snap.load(eng)
@@ -305,7 +305,7 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
     us = phases / 1e3
     per = us.sum(axis=1)
     names = ["add_pod", "sync", "eval_capture", "statuses", "assume"]
-    return {"workload": f"configs[1] cluster ({N} nodes), per-cycle C-ABI path, {n_pods} cycles timed after {warm}",
+    return {"workload": f"{label} cluster ({N} nodes), per-cycle C-ABI path, {n_pods} cycles timed after {warm}",
             "driver": "C (tests/c/cycle_driver.c), CLOCK_MONOTONIC per call",
             "us_per_cycle_mean": float(per.mean()), "us_per_cycle_p50": float(np.percentile(per, 50)),
             "us_per_cycle_p99": float(np.percentile(per, 99)), "pods_per_s": float(1e6 / per.mean()),
@@ -313,7 +313,7 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int):
             "breakdown_us_p50": {k: float(np.percentile(us[:, j], 50)) for j, k in enumerate(names)},
             "appended": int(ap.value), "full_reloads": int(rl.value),
             "placements_equal_run_queue": bool(np.array_equal(placed, want)),
-            "eval_path": eng.last_run_info()[0]}
+            "eval_path": eng.last_run_info()[0], "eval_path_legend": "5 per-cycle kernel, 6 its topology form"}
 
 
 def default_profile_line(native, G, E, metrics, n_nodes: int, n_pods: int, steps: int, cpu_budget: float):
@@ -350,6 +350,32 @@ def default_profile_line(native, G, E, metrics, n_nodes: int, n_pods: int, steps
     return out
 
 
+def kubelet_memory_line(native, G, E, n_nodes: int, n_pods: int, steps: int, headline_pods_per_s: float):
+    """configs[1] with kubelet-style memory (generator.config2_kubelet:
+    allocatable a whole number of Ki, not of Mi; 30 % of the pods request
+    decimal quantities): the N32 forms do not apply, the speculate-and-verify
+    walk runs its wide-memory instance (KSG_RUN_WIDE_MEM).  pods/s of reset +
+    one ksg_run_queue (best of `steps`), beside the headline."""
+    nodes, pods, prof = G.config2_kubelet(n_nodes=n_nodes, n_pods=n_pods)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    eng = native.Engine(device=0)
+    eng.load(enc, pf)
+    best = None
+    for _ in range(steps + 1):
+        eng.reset_state()
+        t = time.perf_counter()
+        pl, _ = eng.run_queue(0, n_pods, results=False)
+        dt = time.perf_counter() - t
+        best = dt if best is None or dt < best else best
+    path, flags = eng.last_run_info()
+    v = n_pods / best
+    return {"workload": f"configs[1] with kubelet-style memory (generator.config2_kubelet): {n_nodes} nodes x "
+                        f"{n_pods} pods", "pods_per_s": v, "headline_over_this": headline_pods_per_s / v,
+            "wide_memory_walk": bool(flags & native.RUN_WIDE_MEM), "run_flags": flags,
+            "scheduled": int((pl >= 0).sum())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -366,6 +392,10 @@ def main():
     ap.add_argument("--default-pods", type=int, default=50000, help="default-profile line; 0 disables")
     ap.add_argument("--cycle-pods", type=int, default=2000, help="per-cycle sidecar; 0 disables")
     ap.add_argument("--cycle-warm", type=int, default=500)
+    ap.add_argument("--kubelet-pods", type=int, default=50000, help="kubelet-memory line; 0 disables")
+    ap.add_argument("--topo-nodes", type=int, default=15000, help="configs[2] cluster of the topology legs")
+    ap.add_argument("--topo-cycle-pods", type=int, default=400, help="configs[2] per-cycle leg; 0 disables")
+    ap.add_argument("--topo-annotate-pods", type=int, default=256, help="configs[2] annotation leg; 0 disables")
     ap.add_argument("--no-build-check", action="store_true",
                     help="skip the check that libksched.so embeds the tree's source hash")
     args = ap.parse_args()
@@ -500,6 +530,34 @@ def main():
         except Exception as e:
             log(f"[rank {rank}] default-profile line unavailable: {e}")
 
+    cyc3 = ann3 = None
+    if world == 1 and args.topo_cycle_pods > 0:
+        try:
+            S = importlib.import_module(PKG + ".snapshot")
+            cyc3 = per_cycle_sidecar(native, G, S, args.topo_nodes, 300, args.topo_cycle_pods, make=G.config3,
+                                     label="configs[2]")
+        except Exception as e:
+            log(f"[rank {rank}] configs[2] per-cycle sidecar unavailable: {e}")
+    if world == 1 and args.topo_annotate_pods > 0:
+        try:
+            B = importlib.import_module(PKG + ".bulk")
+            n3, p3, prof3 = G.config3(n_nodes=args.topo_nodes, n_pods=args.topo_annotate_pods)
+            enc3 = E.Encoder(n3, p3, prof3)
+            eng3 = native.Engine(device=local_rank)
+            eng3.load(enc3, E.encode_profile(prof3, enc3.cluster.res_names))
+            ann3 = annotation_sidecar(eng3, enc3, prof3, native, B, len(p3), 64, args.annotate_threads,
+                                      label="configs[2]")
+            del eng3
+        except Exception as e:
+            log(f"[rank {rank}] configs[2] annotation sidecar unavailable: {e}")
+    kub = None
+    if world == 1 and args.kubelet_pods > 0:
+        try:
+            kub = kubelet_memory_line(native, G, E, args.nodes, min(args.kubelet_pods, args.pods), 2,
+                                      P * args.steps / elapsed)
+        except Exception as e:
+            log(f"[rank {rank}] kubelet-memory line unavailable: {e}")
+
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
         pods_per_s = world * P * args.steps / elapsed
@@ -550,6 +608,12 @@ def main():
             out["default_profile"] = dflt
         if cyc is not None:
             out["per_cycle"] = cyc
+        if kub is not None:
+            out["kubelet_memory"] = kub
+        if cyc3 is not None:
+            out["per_cycle_configs2"] = cyc3
+        if ann3 is not None:
+            out["annotations_configs2"] = ann3
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baselines(enc, pf, args.cpu_budget)
         print(json.dumps(out), flush=True)

@@ -252,16 +252,18 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl);
 int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base);
 /* Evaluate pod `pod` (index into the loaded workload) against the current
  * node state; no state change.  `cap` may be NULL.  A pod whose plugins are
- * all node-local takes the chip-wide per-cycle path (one launch over N / 256
- * workgroups writing into a pinned host block, completion polled from a flag
- * there, persistent buffers); topology pods take the single-workgroup queue
- * kernel. */
+ * all node-local takes the chip-wide per-cycle path (one cooperative launch
+ * writing into a pinned host block, completion polled from a flag there,
+ * persistent buffers); a PodTopologySpread / InterPodAffinity pod takes the
+ * chip-wide topology kernel in its evaluate-only capture form, also writing
+ * into the pinned block. */
 int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap);
 
 /* The per-cycle results of ksg_eval_view, in library memory (no copy into
  * caller arrays): valid until the next ksg_eval / ksg_eval_view / ksg_eval_pod
- * on the context.  Rows hold elem_bytes-wide signed integers (4 when every
- * weighted total fits 32 bits, else 8), one per node; raw[pl] / norm[pl] are
+ * on the context.  Rows hold elem_bytes-wide signed integers (2 when every
+ * raw score, normalised score and weighted total fits 16 bits, 4 when they fit
+ * 32 bits, else 8), one per node; raw[pl] / norm[pl] are
  * NULL for a plugin the profile does not score (norm[pl] == raw[pl] for the
  * plugins without ScoreExtensions).  A pod with fewer than two feasible nodes
  * has all-zero rows (no Score runs).  The Go shim's Score / NormalizeScore
@@ -329,12 +331,15 @@ int ksg_reset_state(ksg_ctx* ctx);
 int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
 /* Which path the last ksg_run_queue / ksg_run_replicas / ksg_eval took: path
  * 1 queue kernel, 2 batched, 3 replica sweep, 4 chip-wide topology, 5 the
- * per-cycle chip-wide evaluation of ksg_eval; flags: the range-
+ * per-cycle chip-wide evaluation of ksg_eval, 6 its topology form (a
+ * PodTopologySpread / InterPodAffinity pod on the chip-wide topology kernel,
+ * no assume); flags: the range-
  * checked narrow forms that ran (exact either way; for tests and reports). */
 #define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
 #define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */
 #define KSG_RUN_TCOL 4           /* phase 2 was the transposed walk (ksg_batch_phase2t) */
 #define KSG_RUN_SPEC 8           /* phase 2 was the speculate-and-verify walk (ksg_batch_phase2v) */
+#define KSG_RUN_WIDE_MEM 16      /* ... in its wide-memory instance (memory not whole MiB: int64 bytes) */
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event

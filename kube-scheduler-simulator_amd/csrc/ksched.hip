@@ -37,7 +37,10 @@
 #include <array>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <set>
 #include <string>
+#include <tuple>
 #include <type_traits>
 #include <vector>
 
@@ -2407,21 +2410,30 @@ __global__ __launch_bounds__(256) void ksg_node_rcp(DevCluster c, float2* r32, d
 // sums are bounded by max(current, allocatable) (the Fit filter) and the
 // non-zero sums by current + allocatable + (placeable pods + 1) x the pods'
 // non-zero excess.  Any failure sets *bad (the int64 instances run).
+//
+// mw = 1: the wide-memory instance (memory in int64 bytes): the cpu half as
+// above; memory needs no alignment, only every quantity and reachable sum
+// below 2^46, so x 100 stays exact in float64 and below qdiv's 2^53.
 __global__ __launch_bounds__(256) void ksg_range32(DevCluster c, DevState st, int64_t xc, int64_t xm, int32_t count,
-                                                   unsigned* bad) {
+                                                   int32_t mw, unsigned* bad) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int N = c.N;
   if (n >= N) return;
   const size_t NN = N;
-  constexpr int64_t kMiB = (int64_t)1 << 20, k30 = (int64_t)1 << 30, k31 = ((int64_t)1 << 31) - 1;
+  constexpr int64_t kMiB = (int64_t)1 << 20, k30 = (int64_t)1 << 30, k31 = ((int64_t)1 << 31) - 1,
+                    k46 = (int64_t)1 << 46;
   const int64_t ac = c.alloc[KSG_RES_CPU * NN + n], am = c.alloc[KSG_RES_MEM * NN + n];
   const int64_t rc = st.requested[KSG_RES_CPU * NN + n], rm = st.requested[KSG_RES_MEM * NN + n];
   const int64_t zc = st.nonzero[n], zm = st.nonzero[NN + n];
   const int64_t places = (int64_t)max(0, min(count, c.allowed[n] - st.pod_count[n])) + 1;
   bool ok = ac >= 0 && am >= 0 && rc >= 0 && rm >= 0 && zc >= 0 && zm >= 0;
-  ok = ok && ((am | rm | zm) & (kMiB - 1)) == 0;
-  ok = ok && ac * 100 < k30 && (am >> 20) * 100 < k30 && rc <= k31 && (rm >> 20) <= k31;
-  ok = ok && zc + ac + places * xc <= k31 && (zm >> 20) + (am >> 20) + places * xm <= k31;
+  ok = ok && ac * 100 < k30 && rc <= k31 && zc + ac + places * xc <= k31;
+  if (mw) {
+    ok = ok && am < k46 && rm < k46 && zm < k46 && (double)zm + (double)am + (double)places * (double)xm < (double)k46;
+  } else {
+    ok = ok && ((am | rm | zm) & (kMiB - 1)) == 0;
+    ok = ok && (am >> 20) * 100 < k30 && (rm >> 20) <= k31 && (zm >> 20) + (am >> 20) + places * xm <= k31;
+  }
   if (!ok) atomicOr(bad, 1u);
 }
 
@@ -2501,6 +2513,7 @@ struct ksg_ctx {
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
   bool last_spec = false;     // ... the speculate-and-verify walk
+  bool last_mw = false;       // ... in its wide-memory instance
   bool pipe_overlap = true;   // env KSG_PIPE_OVERLAP=0: the window pipeline on one stream (same arithmetic;
                               // for counter passes, which serialise kernels: a walk polling for the
                               // other stream's top-k would wait out its poll bound)
@@ -2541,11 +2554,18 @@ struct ksg_ctx {
   unsigned ev_seq = 0;                      // the per-cycle completion flag's last value
   bool ev_clean = false;                    // the arrival counter is zero
   ksg_profile* d_ev_prof = nullptr;
+  int32_t* d_ev_pl = nullptr;               // eval_topo_fast's placement word
+  char* h_evt = nullptr;                    // eval_topo_fast's pinned block (its own: eval_fast polls words
+  size_t h_evt_bytes = 0;                   // that topology rows would otherwise overwrite)
+  char* d_hevt = nullptr;
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
   int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
   int cycle_block = 128;                    // env KSG_CYCLE_BLOCK: nodes per workgroup of ksg_eval_cycle (64/128/256)
   bool cycle_sys = true;                    // env KSG_CYCLE_SYS=0: plain host stores + __threadfence_system
+  bool cycle_coop = false;                  // per-cycle launch: plain (G within the occupancy API's residency,
+                                            // ~7 us less host time); cooperative after an exchange timeout,
+                                            // or always with env KSG_CYCLE_COOP=1
   int cycle_cap[3] = {0, 0, 0};             // co-resident ksg_eval_cycle workgroups per block size (0 = not queried)
   // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
   char* h_stage = nullptr;
@@ -2573,6 +2593,20 @@ int fail(ksg_ctx* ctx, int code, const std::string& msg) {
     if (_e != hipSuccess)                                                                   \
       return fail(ctx, KSG_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));    \
   } while (0)
+
+// A kernel's dynamic-LDS budget attribute, set once per (device, kernel,
+// budget): the attribute is per device, and contexts on several devices (or
+// threads) may open in one process.
+int func_lds_attr(ksg_ctx* ctx, const void* f, size_t bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<int, const void*, size_t>> done;
+  std::lock_guard<std::mutex> g(mu);
+  const auto key = std::make_tuple(ctx->device, f, bytes);
+  if (done.count(key)) return KSG_OK;
+  HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  done.insert(key);
+  return KSG_OK;
+}
 
 template <typename T>
 int dalloc(ksg_ctx* ctx, T** p, size_t count) {
@@ -2880,7 +2914,7 @@ bool profile_cm_fast(const ksg_profile& prof);
 // filter bounds every requested sum by the allocatable), the pods' memory
 // quantities are whole MiB and their cpu fits 30 bits, Fit's weights keep
 // the weighted numerator below 2^30.  Fills the pods' non-zero excess bounds.
-bool range32_candidate(ksg_ctx* ctx, int first, int count, int64_t* xc, int64_t* xm) {
+bool range32_candidate(ksg_ctx* ctx, int first, int count, int64_t* xc, int64_t* xm, bool mw = false) {
   const ksg_profile& prof = ctx->prof;
   if (!profile_cm_fast(prof) || ctx->c.R > 4 || ctx->force_path == 3) return false;
   bool fit = false;
@@ -2893,16 +2927,22 @@ bool range32_candidate(ksg_ctx* ctx, int first, int count, int64_t* xc, int64_t*
       wsum += prof.weight[pl];
     }
   if (wsum * 100 >= (1 << 30)) return false;
-  constexpr int64_t kMiB = 1 << 20;
+  constexpr int64_t kMiB = 1 << 20, k46 = (int64_t)1 << 46;
   *xc = *xm = 0;
   for (int i = first; i < first + count; i++) {
     const ksg_pod& p = ctx->h_pods[i];
     if ((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) return false;
     const int64_t rc = p.req[KSG_RES_CPU], rm = p.req[KSG_RES_MEM];
-    if (rc < 0 || rm < 0 || p.nz_cpu < 0 || p.nz_mem < 0 || ((rm | p.nz_mem) & (kMiB - 1))) return false;
-    if (rc >= (1 << 30) || p.nz_cpu >= (1 << 30) || (rm >> 20) >= (1 << 30) || (p.nz_mem >> 20) >= (1 << 30)) return false;
+    if (rc < 0 || rm < 0 || p.nz_cpu < 0 || p.nz_mem < 0) return false;
+    if (rc >= (1 << 30) || p.nz_cpu >= (1 << 30)) return false;
+    if (mw) {   // the wide-memory instance: bytes, below 2^46
+      if (rm >= k46 || p.nz_mem >= k46) return false;
+      *xm = std::max(*xm, p.nz_mem - rm);
+    } else {
+      if (((rm | p.nz_mem) & (kMiB - 1)) || (rm >> 20) >= (1 << 30) || (p.nz_mem >> 20) >= (1 << 30)) return false;
+      *xm = std::max(*xm, (p.nz_mem - rm) >> 20);
+    }
     *xc = std::max(*xc, p.nz_cpu - rc);
-    *xm = std::max(*xm, (p.nz_mem - rm) >> 20);
   }
   return true;
 }
@@ -2919,7 +2959,7 @@ int decide_n32(ksg_ctx* ctx, int32_t first, int32_t count, bool* n32) {
     }
     HIPC(ctx, hipMemsetAsync(ctx->d_flag, 0, 16, ctx->stream));
     hipLaunchKernelGGL(ksg_range32, dim3((ctx->c.N + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st, xc, xm,
-                       count, ctx->d_flag);
+                       count, 0, ctx->d_flag);
     unsigned bad = 0;
     HIPC(ctx, hipMemcpyAsync(&bad, ctx->d_flag, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
     HIPC(ctx, hipStreamSynchronize(ctx->stream));
@@ -2929,16 +2969,34 @@ int decide_n32(ksg_ctx* ctx, int32_t first, int32_t count, bool* n32) {
   return KSG_OK;
 }
 
+// The wide-memory scope of the speculate-and-verify walk: the N32 check's cpu
+// half, memory in bytes (ksg_range32 mw = 1).
+int decide_mw(ksg_ctx* ctx, int32_t first, int32_t count, bool* mw) {
+  *mw = false;
+  int64_t xc = 0, xm = 0;
+  if (ctx->c.R <= 4 && ctx->force_path != 3 && range32_candidate(ctx, first, count, &xc, &xm, true)) {
+    if (!ctx->d_flag) {
+      int rc;
+      if ((rc = dalloc(ctx, &ctx->d_flag, 4))) return rc;
+    }
+    HIPC(ctx, hipMemsetAsync(ctx->d_flag, 0, 16, ctx->stream));
+    hipLaunchKernelGGL(ksg_range32, dim3((ctx->c.N + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st, xc, xm,
+                       count, 1, ctx->d_flag);
+    unsigned bad = 0;
+    HIPC(ctx, hipMemcpyAsync(&bad, ctx->d_flag, sizeof(bad), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(ctx, hipStreamSynchronize(ctx->stream));
+    *mw = bad == 0;
+  }
+  return KSG_OK;
+}
+
 // LDS budget attribute of the phase-2 instances (once per process)
 int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
-  static bool attr_set = false;
-  if (attr_set) return KSG_OK;
-  HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
-  HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2_scan<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)budget));
+  int rc;
+  if ((rc = func_lds_attr(ctx, (const void*)ksg_batch_phase2, budget))) return rc;
+  if ((rc = func_lds_attr(ctx, (const void*)ksg_batch_phase2_scan<512>, budget))) return rc;
   for (const void* f : slot_kernels())
-    HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget));
-  attr_set = true;
+    if ((rc = func_lds_attr(ctx, f, budget))) return rc;
   return KSG_OK;
 }
 
@@ -3026,16 +3084,14 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   }
   b.stat = n32 ? ctx->d_stat : nullptr;
   const bool tcol = ctx->batch_mode == 5 && n32 && tcol_candidate(ctx);
-  if (tcol) {
-    static bool tattr = false;
-    if (!tattr) {
-      for (const void* f : tcol_kernels())
-        HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTcolLds));
-      tattr = true;
+  if (tcol)
+    for (const void* f : tcol_kernels()) {
+      int rc;
+      if ((rc = func_lds_attr(ctx, f, kTcolLds))) return rc;
     }
-  }
   ctx->last_tcol = tcol;
   ctx->last_spec = false;
+  ctx->last_mw = false;
   if (tcol && !ctx->d_rect) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rect, (size_t)128 * N))) return rc;
@@ -3133,6 +3189,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   int rc;
   ctx->last_tcol = false;
   ctx->last_spec = false;
+  ctx->last_mw = false;
   if (!ctx->d_prec[0]) {
     for (int q = 0; q < 2; q++) {
       if ((rc = dalloc(ctx, &ctx->d_prec[q], (size_t)KSG_BATCH_MAX * N))) return rc;
@@ -3164,38 +3221,35 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   // carried columns, 64-pod batches, else the slot walk.  (The round-2
   // two-version walk and a round-3 one-wave walk with two slots per lane, both
   // measured slower, were removed.)
-  bool n32 = false;
+  bool n32 = false, mw = false;
   if (ctx->batch_mode >= 4 && (rc = decide_n32(ctx, first, count, &n32))) return rc;
   const bool tcolw = ctx->batch_mode == 5 && window && n32 && tcol_candidate(ctx);
-  // mode 6: the speculate-and-verify walk (ksched_phase2v.h), N32 scope, 64-pod batches
-  const bool specw = ctx->batch_mode == 6 && window && n32 && spec_candidate(ctx);
+  // mode 6: the speculate-and-verify walk (ksched_phase2v.h), N32 scope, 64-pod
+  // batches; memory outside the N32 ranges (not whole MiB, as kubelets report
+  // it, or too large) takes its wide-memory instance (MW: memory in int64
+  // bytes, the same quotients)
+  if (ctx->batch_mode == 6 && window && !n32 && spec_candidate(ctx) && (rc = decide_mw(ctx, first, count, &mw)))
+    return rc;
+  const bool specw = ctx->batch_mode == 6 && window && (n32 || mw) && spec_candidate(ctx);
   ctx->last_tcol = tcolw;
   ctx->last_spec = specw;
+  ctx->last_mw = specw && mw;
+  const void* spec_kern = mw ? (const void*)ksg_batch_phase2v<64 * kSvWaves, true>
+                             : (const void*)ksg_batch_phase2v<64 * kSvWaves, false>;
   if ((tcolw || specw) && !ctx->d_prect[0]) {
     for (int q = 0; q < 2; q++) {
       if ((rc = dalloc(ctx, &ctx->d_prect[q], (size_t)64 * N))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_pstatt[q], (size_t)64 * N))) return rc;
     }
   }
-  if (specw) {
-    static bool sattr = false;
-    if (!sattr) {
-      HIPC(ctx, hipFuncSetAttribute((const void*)ksg_batch_phase2v<64 * kSvWaves>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSpecLds));
-      sattr = true;
-    }
-  }
+  if (specw && (rc = func_lds_attr(ctx, spec_kern, kSpecLds))) return rc;
   if (tcolw) {
     if (!ctx->d_tccol) {
       if ((rc = dalloc(ctx, &ctx->d_tccol, (size_t)64 * 64))) return rc;
       if ((rc = dalloc(ctx, &ctx->d_tcinit, (size_t)4 * 64))) return rc;
     }
-    static bool tattr = false;
-    if (!tattr) {
-      for (const void* f : tcol_kernels())
-        HIPC(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTcolLds));
-      tattr = true;
-    }
+    for (const void* f : tcol_kernels())
+      if ((rc = func_lds_attr(ctx, f, kTcolLds))) return rc;
   }
   const int B = tcolw || specw ? 64 : window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
   const int slots = window ? 2 * B : B;   // carried + this batch's slots
@@ -3314,7 +3368,8 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
     }
     if (specw) {
-      hipLaunchKernelGGL(ksg_batch_phase2v<64 * kSvWaves>, dim3(1), dim3(64 * kSvWaves), kSpecLds, s2, b);
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(spec_kern)), dim3(1),
+                         dim3(64 * kSvWaves), kSpecLds, s2, b);
       if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2V, 0.5 * nb * (nb + 1)))) return rc;
     } else if (tcolw) {   // the carried columns on the state after the previous walk, then the walk
       hipLaunchKernelGGL(ksg_tcol_carry<1>, dim3(nb), dim3(64), 0, s2, b);
@@ -3613,8 +3668,36 @@ int coop_occupancy(ksg_ctx* ctx, int* occ) {
   return KSG_OK;
 }
 
+// The capture outputs of a chip-wide topology run (CoopArgs cap_*; mode 1
+// device rows of a captured queue, mode 2 the per-cycle host block).
+struct CoopCap {
+  int mode = 0;
+  uint32_t* fs = nullptr;
+  char *raw = nullptr, *norm = nullptr, *tot = nullptr;
+  int32_t rows[KSG_NPLUGINS] = {};
+  int32_t n_rows = 0, n_normrows = 0, narrow = 0;
+  ksg_result* h_res = nullptr;
+  unsigned* h_flag = nullptr;
+  unsigned seq = 0;
+};
+
+// ksg_topo_coop<KN, LL, CAP>: capture instances exist for KN <= 4 (up to
+// 262,144 nodes); nullptr where there is none.
+const void* coop_kernel(int kn, bool ll, int cap) {
+  if (cap == 0)
+    return ll ? (const void*)ksg_topo_coop<1, true> : kn == 1 ? (const void*)ksg_topo_coop<1> : kn == 2 ? (const void*)ksg_topo_coop<2>
+         : kn == 4 ? (const void*)ksg_topo_coop<4> : kn == 8 ? (const void*)ksg_topo_coop<8>
+         : kn == 16 ? (const void*)ksg_topo_coop<16> : (const void*)ksg_topo_coop<32>;
+  if (cap == 1)
+    return ll ? (const void*)ksg_topo_coop<1, true, 1> : kn == 1 ? (const void*)ksg_topo_coop<1, false, 1>
+         : kn == 2 ? (const void*)ksg_topo_coop<2, false, 1> : kn == 4 ? (const void*)ksg_topo_coop<4, false, 1> : nullptr;
+  return ll ? (const void*)ksg_topo_coop<1, true, 2> : kn == 1 ? (const void*)ksg_topo_coop<1, false, 2>
+       : kn == 2 ? (const void*)ksg_topo_coop<2, false, 2> : kn == 4 ? (const void*)ksg_topo_coop<4, false, 2> : nullptr;
+}
+
 int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
-                  const ksg_profile* d_prof) {
+                  const ksg_profile* d_prof, int do_commit = 1, const CoopCap* cap = nullptr,
+                  bool timed = true) {
   const int N = ctx->c.N;
   int rc;
   int cus = 0;
@@ -3663,6 +3746,23 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   a.bar = ctx->d_coop_wgflags;
   a.pmode = ctx->coop_pmode;
   a.timeout = ctx->d_coop_flags + 4;
+  a.commit = do_commit;
+  const int cmode = cap ? cap->mode : 0;
+  const void* kf = coop_kernel(kn, ll, cmode);
+  if (!kf) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: no capture instance for this many nodes");
+  if (cap) {
+    a.cap_fs = cap->fs;
+    a.cap_raw = cap->raw;
+    a.cap_norm = cap->norm;
+    a.cap_tot = cap->tot;
+    for (int q = 0; q < KSG_NPLUGINS; q++) a.cap_rows[q] = cap->rows[q];
+    a.cap_n_rows = cap->n_rows;
+    a.cap_n_normrows = cap->n_normrows;
+    a.cap_narrow = cap->narrow;
+    a.h_res = cap->h_res;
+    a.h_flag = cap->h_flag;
+    a.seq = cap->seq;
+  }
   SweepArgs sa{};
   sa.c = ctx->c;
   sa.pods = ctx->d_pods;
@@ -3679,12 +3779,19 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
 #endif
   (void)hipGetLastError();
   treset(ctx);
-  HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  if (timed) HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   if ((rc = tmark(ctx))) return rc;
   for (int off = 0; off < count; off += kCoopBatch) {
     const int nb = std::min(kCoopBatch, count - off);
     sa.b0 = first + off;
     sa.nb = nb;
+    if (cap && cap->mode == 1) {   // this launch's pods start at row `off` of the capture arrays
+      const size_t es = cap->narrow ? 4 : 8, NN = N;
+      a.cap_fs = cap->fs + (size_t)off * NN;
+      a.cap_raw = cap->raw + (size_t)off * cap->n_rows * NN * es;
+      a.cap_norm = cap->norm + (size_t)off * cap->n_normrows * NN * es;
+      a.cap_tot = cap->tot + (size_t)off * NN * es;
+    }
     hipLaunchKernelGGL(ksg_sweep_static, dim3(static_blocks(N, nb)), dim3(256), 0, ctx->stream, sa);
     if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)nb * N))) return rc;
     a.first = first + off;
@@ -3695,18 +3802,19 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     // cooperative launch: the runtime guarantees the G workgroups are
     // co-resident (or refuses the launch), which the grid barrier needs
     void* kargs[] = {&a};
-    const void* kf = ll ? (const void*)ksg_topo_coop<1, true> : kn == 1 ? (const void*)ksg_topo_coop<1> : kn == 2 ? (const void*)ksg_topo_coop<2>
-                   : kn == 4 ? (const void*)ksg_topo_coop<4> : kn == 8 ? (const void*)ksg_topo_coop<8>
-                   : kn == 16 ? (const void*)ksg_topo_coop<16> : (const void*)ksg_topo_coop<32>;
     HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));
     if ((rc = tlaunched(ctx, KSG_K_TOPO_COOP, (double)nb * N))) return rc;
   }
   HIPC(ctx, hipGetLastError());
-  HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  if (timed) HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   return KSG_OK;
 }
 
 int flush_stage(ksg_ctx* ctx);
+
+// The capture instances of ksg_topo_coop cover up to 4 nodes per lane
+// (coop_kernel): 262,144 nodes on 256 workgroups.
+bool coop_capture_fits(const ksg_ctx* ctx) { return ctx->c.N <= 4 * 256 * 256; }
 
 int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int32_t* placements,
                  ksg_result* results, ksg_capture* cap) {
@@ -3731,10 +3839,16 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   QueueArgs a = base_args(ctx);
   bool batched = do_commit && batch_eligible(ctx, first, count);
   if (ctx->force_path == 1) batched = false;
+  // topology pods: the chip-wide path (ksched_topo_coop.h) for placements,
+  // ksg_eval (no assume) and captured queues alike
+  const bool topo = !batched && needs_topo(ctx, ctx->prof, first, count);
+  const bool coop = topo && ctx->topo_coop && ctx->force_path != 1 && !range_has_ports(ctx, first, count) &&
+                    (!want_cap || coop_capture_fits(ctx));
   // captured queues take the batched path too (ksched_capture.h): the capture
-  // kernels write the profile's score rows only, in a compact layout
+  // kernels write the profile's score rows only, in a compact layout (the
+  // chip-wide topology path writes the same layout)
   CapArgs ca{};
-  if (want_cap && batched) {
+  if (want_cap && (batched || coop)) {
     ca.c = ctx->c;
     ca.st = ctx->st;
     ca.pods = ctx->d_pods;
@@ -3775,20 +3889,26 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     a.placements = d_pl;
     a.results = d_res;
     const int block = N >= 512 ? 512 : 256;   // 512 lanes: <= 256 VGPRs per lane, no spills
-    const bool topo = needs_topo(ctx, ctx->prof, first, count);
-    // the chip-wide path always assumes its pods: ksg_eval (do_commit = 0)
-    // takes the single-workgroup kernel
-    if (topo && !want_cap && do_commit && ctx->topo_coop && ctx->force_path != 1 &&
-        !range_has_ports(ctx, first, count)) {
+    if (coop) {
       ctx->last_path = 4;
-      if ((rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof))) return rc;
+      CoopCap cc;
+      if (want_cap) {
+        cc.mode = 1;
+        cc.fs = ca.fstatus;
+        cc.raw = reinterpret_cast<char*>(ca.raw);
+        cc.norm = reinterpret_cast<char*>(ca.norm);
+        cc.tot = reinterpret_cast<char*>(ca.total);
+        for (int q = 0; q < ca.n_rows; q++) cc.rows[q] = ca.rows[q];
+        cc.n_rows = cc.n_normrows = ca.n_rows;
+      }
+      if ((rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof, do_commit, want_cap ? &cc : nullptr))) return rc;
     } else if ((rc = launch_queue(ctx, a, 1, block, topo))) {
       return rc;
     }
   }
   if (placements) HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * count, hipMemcpyDeviceToHost, ctx->stream));
   if (results) HIPC(ctx, hipMemcpyAsync(results, d_res, sizeof(ksg_result) * count, hipMemcpyDeviceToHost, ctx->stream));
-  if (want_cap && batched) {
+  if (want_cap && (batched || coop)) {
     if (cap->fstatus) HIPC(ctx, hipMemcpyAsync(cap->fstatus, ca.fstatus, sizeof(uint32_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
     if (cap->total) HIPC(ctx, hipMemcpyAsync(cap->total, ca.total, sizeof(int64_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
     for (int q = 0; q < ca.n_rows; q++) {   // compact row q -> the caller's plugin row, every pod
@@ -3838,6 +3958,24 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
 // written by the kernel into a pinned, fine-grained host block, completion
 // read from a flag in that block (no copy, no event, no stream
 // synchronisation); the host then decodes the result.
+// The largest raw NodeAffinity score a pod can get: its preferred terms'
+// summed |weight| (program: nterms, then per term weight, nr, nr x {col, op,
+// nv, values[nv]}).
+int64_t na_pref_bound(const ksg_ctx* ctx, const ksg_pod& p) {
+  if (p.na_pref < 0) return 0;
+  const int32_t* w = ctx->h_prog.data() + p.na_pref;
+  const int32_t* end = ctx->h_prog.data() + p.blob + p.blob_len;
+  int64_t s = 0;
+  const int nt = *w++;
+  for (int t = 0; t < nt && w < end; t++) {
+    const int32_t weight = *w++;
+    s += weight < 0 ? -(int64_t)weight : weight;
+    const int nr = *w++;
+    for (int r = 0; r < nr && w + 2 < end; r++) w += 3 + w[2];
+  }
+  return w <= end ? s : INT64_MAX / 2;   // a malformed program: the widest rows
+}
+
 bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
   return ctx->eval_fast && ctx->force_path != 1 && batch_eligible(ctx, pod, 1);
 }
@@ -3854,12 +3992,16 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   for (int pl = 0; pl < KSG_NPLUGINS; pl++)
     if (((prof.score_mask >> pl) & 1u) && pl != KSG_PL_TAINT_TOLERATION && pl != KSG_PL_NODE_AFFINITY)
       rows[n_rows++] = pl;
-  // int32 rows when every total fits (raw values are bounded by batch_eligible)
+  // Row width: the narrowest exact one.  Raw Fit / BalancedAllocation /
+  // ImageLocality and every normalised score are in [0, 100]; raw
+  // TaintToleration is at most the node's taint count, raw NodeAffinity at
+  // most the pod's summed preferred weights; totals at most Σ|weight| x 100.
+  const ksg_pod& hp = ctx->h_pods[pod];
   int64_t wabs = 0;
   for (int pl = 0; pl < KSG_NPLUGINS; pl++)
     if ((prof.score_mask >> pl) & 1u) wabs += prof.weight[pl] < 0 ? -(int64_t)prof.weight[pl] : prof.weight[pl];
-  const bool narrow = wabs * 100 < (1ll << 31);
-  const size_t es = narrow ? 4 : 8;
+  int64_t bound = std::max<int64_t>({wabs * 100, 100, ctx->c.T, na_pref_bound(ctx, hp)});
+  const size_t es = bound < (1 << 15) ? 2 : bound < (1ll << 31) ? 4 : 8;
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
   // workgroup size: the configured one, or a larger one when the grid would
@@ -3878,21 +4020,21 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_of(block), block, 0));
       hipDeviceProp_t dp;
       HIPC(ctx, hipGetDeviceProperties(&dp, ctx->device));
-      ctx->cycle_cap[bi] = std::max(1, per_cu) * dp.multiProcessorCount;
+      // one fewer than the API's answer per CU (MI355X guide: the hardware may admit one fewer)
+      ctx->cycle_cap[bi] = std::max(1, per_cu - 1) * dp.multiProcessorCount;
     }
     if ((N + block - 1) / block <= (size_t)ctx->cycle_cap[bi]) break;
     if (block == 256) return fail(ctx, KSG_E_UNSUPPORTED, "per-cycle evaluation: grid not co-resident");
   }
   const unsigned G = (unsigned)((N + block - 1) / block);
-  // host block: stats[4] best err flag | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_normrows][N]
-  const size_t o_fs = 32, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
-  const size_t o_tot = o_raw + es * N * n_rows, o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
+  const size_t Gm = (N + 63) / 64;   // the largest grid (64-lane workgroups): no reallocation on a block change
+  // host block: stats[4] | pad | per-workgroup {key, err, done}[Gm] | fstatus[N] | raw[n_rows][N] | total[N] |
+  // norm[n_normrows][N]
+  const size_t o_wg = 32, o_fs = o_wg + sizeof(CycWg) * Gm, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
+  const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
   const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
-  // device block: parts[Gmax] | keys[Gmax] | flags[Gmax][32] | done | timeout, sized for the
-  // largest grid (64-lane workgroups) so a block-size change needs no reallocation
-  const size_t Gm = (N + 63) / 64;
-  const size_t d_keys = sizeof(CycPart) * Gm, d_flags = d_keys + sizeof(CycKey) * Gm,
-               d_done = d_flags + 128 * Gm, d_need = d_done + 128;
+  // device block: parts[Gm] | flags[Gm][32] | timeout
+  const size_t d_flags = sizeof(CycPart) * Gm, d_to = d_flags + 128 * Gm, d_need = d_to + 128;
   if (d_need > ctx->ev_bytes) {
     if (ctx->d_ev) {
       auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_ev);
@@ -3914,12 +4056,13 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       ctx->h_ev_bytes = 0;
     }
     HIPC(ctx, hipHostMalloc((void**)&ctx->h_ev, h_need, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(ctx->h_ev, 0, h_need);   // done words: no call's sequence number is 0
     ctx->h_ev_bytes = h_need;
     void* dp = nullptr;
     HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_ev, 0));
     ctx->d_hev = static_cast<char*>(dp);
   }
-  if (!ctx->ev_clean) {   // flags (no call's sequence number is 0), the arrival counter, the timeout word
+  if (!ctx->ev_clean) {   // exchange flags (no call's sequence number is 0) and the timeout word
     HIPC(ctx, hipMemsetAsync(ctx->d_ev + d_flags, 0, d_need - d_flags, ctx->stream));
     ctx->ev_clean = true;
   }
@@ -3929,7 +4072,6 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   }
   // the pod's append still staged: read from the staging buffer by the
   // kernel (its programs must all lie in the staged words)
-  const ksg_pod& hp = ctx->h_pods[pod];
   const bool staged = ctx->stage_pending && ctx->stage_n == 1 && ctx->stage_first == pod && ctx->d_stage &&
                       hp.blob >= ctx->stage_base && (int64_t)hp.blob + hp.blob_len <= ctx->stage_base + ctx->stage_len &&
                       (hp.node_set < 0 || (hp.node_set >= ctx->stage_base &&
@@ -3937,7 +4079,6 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   if (!staged && (rc = flush_stage(ctx))) return rc;
   char* hb = ctx->h_ev;
   char* db = ctx->d_hev;
-  volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(hb + 28);
   const unsigned seq = ++ctx->ev_seq == 0 ? ++ctx->ev_seq : ctx->ev_seq;   // never 0 (a fresh block)
   CycArgs ca{};
   ca.c = ctx->c;
@@ -3946,24 +4087,29 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   ca.prog = ctx->d_prog;
   ca.prof = ctx->d_ev_prof;
   ca.pod = pod;
+  ca.blob = hp.blob;   // the same pool index in the staging buffer (sprog - sbase) and in d_prog
+  ca.blob_len = hp.blob_len;
   ca.n_rows = n_rows;
   ca.n_normrows = n_normrows;
   for (int q = 0; q < n_rows; q++) ca.rows[q] = rows[q];
-  ca.narrow = narrow ? 1 : 0;
+  ca.es = (int32_t)es;
   ca.h_fs = reinterpret_cast<uint32_t*>(db + o_fs);
   ca.h_raw = db + o_raw;
   ca.h_tot = db + o_tot;
   ca.h_norm = db + o_norm;
   ca.h_stats = reinterpret_cast<int32_t*>(db);
-  ca.h_best = reinterpret_cast<unsigned long long*>(db + 16);
-  ca.h_err = reinterpret_cast<uint32_t*>(db + 24);
-  ca.h_flag = reinterpret_cast<unsigned*>(db + 28);
+  ca.h_wg = reinterpret_cast<CycWg*>(db + o_wg);
   ca.seq = seq;
   ca.parts = reinterpret_cast<CycPart*>(ctx->d_ev);
-  ca.keys = reinterpret_cast<CycKey*>(ctx->d_ev + d_keys);
   ca.flags = reinterpret_cast<unsigned*>(ctx->d_ev + d_flags);
-  ca.done = reinterpret_cast<unsigned*>(ctx->d_ev + d_done);
-  ca.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_done + 64);
+  ca.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_to);
+#ifdef KSG_STAMPS
+  if (!ctx->d_stamps) {
+    if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 128, ctx->stream));
+  }
+  ca.stamps = ctx->d_stamps;
+#endif
   if (staged) {
     ca.spod = reinterpret_cast<const ksg_pod*>(ctx->d_stage);
     ca.sprog = reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod));
@@ -3975,22 +4121,30 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   treset(ctx);
   if ((rc = tmark(ctx))) return rc;
   void* kargs[] = {&ca};
-  HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
+  if (ctx->cycle_coop)
+    HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
+  else   // G is within the occupancy API's co-resident count less one per CU (the exchange's poll is bounded)
+    HIPC(ctx, hipLaunchKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
   if ((rc = tlaunched(ctx, KSG_K_EVAL_CYCLE, (double)N))) return rc;
   HIPC(ctx, hipGetLastError());
   if (staged) {   // consumed; the staging buffer is free once the stream passes this point
     ctx->stage_pending = false;
     HIPC(ctx, hipEventRecord(ctx->ev_stage, ctx->stream));
   }
-  // the kernel's last workgroup stores seq after every result: spin on it,
-  // checking the stream now and then (a failed launch never stores it)
-  for (unsigned spins = 0; *flag != seq; spins++) {
+  // every workgroup stores seq into its record after its rows: spin on them,
+  // checking the stream now and then (a failed launch never stores them)
+  const CycWg* wgr = reinterpret_cast<const CycWg*>(hb + o_wg);
+  for (unsigned g = 0, spins = 0; g < G; spins++) {
+    if (reinterpret_cast<const volatile CycWg*>(wgr)[g].done == seq) {
+      g++;
+      continue;
+    }
     __builtin_ia32_pause();
     if ((spins & 1023) == 1023) {
       const hipError_t e = hipStreamQuery(ctx->stream);
-      if (e == hipSuccess && *flag != seq) {
+      if (e == hipSuccess && reinterpret_cast<const volatile CycWg*>(wgr)[g].done != seq) {
         ctx->ev_clean = false;
-        return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: kernel finished without its completion flag");
+        return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: kernel finished without its completion words");
       }
       if (e != hipSuccess && e != hipErrorNotReady)
         return fail(ctx, KSG_E_DEVICE, std::string("per-cycle evaluation: ") + hipGetErrorString(e));
@@ -4000,10 +4154,18 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   if ((rc = tcollect(ctx))) return rc;
   const int32_t* st = reinterpret_cast<const int32_t*>(hb);
   const int32_t nfeas = st[0];
-  const unsigned long long best = *reinterpret_cast<const unsigned long long*>(hb + 16);
-  const uint32_t herr = *reinterpret_cast<const uint32_t*>(hb + 24);
+  unsigned long long best = 0;
+  uint32_t herr = 0;
+  for (unsigned g = 0; g < G; g++) {   // selectHost over the workgroups' keys
+    best = wgr[g].key > best ? wgr[g].key : best;
+    herr |= wgr[g].err;
+  }
   if (herr & 2u) {
     ctx->ev_clean = false;   // clears the sticky timeout word before the next call
+    if (!ctx->cycle_coop) {   // not every workgroup was resident: the cooperative launch from now on
+      ctx->cycle_coop = true;
+      return eval_fast(ctx, pod, res, cap, view);
+    }
     return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: workgroup exchange timed out");
   }
   uint32_t status = 0;
@@ -4033,7 +4195,10 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   res->status = status;
   res->score_skip = score_skip;
   auto put_row = [&](int64_t* dst, size_t off) {   // one row into the caller's int64 array
-    if (narrow) {
+    if (es == 2) {
+      const int16_t* src = reinterpret_cast<const int16_t*>(hb + off);
+      for (size_t n = 0; n < N; n++) dst[n] = src[n];
+    } else if (es == 4) {
       const int32_t* src = reinterpret_cast<const int32_t*>(hb + off);
       for (size_t n = 0; n < N; n++) dst[n] = src[n];
     } else {
@@ -4064,12 +4229,120 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   return KSG_OK;
 }
 
+// ---- the per-cycle path of a topology pod ------------------------------------------
+// ksg_eval of one PodTopologySpread / InterPodAffinity pod: the chip-wide
+// topology kernel (ksched_topo_coop.h, its per-cycle capture instance CAP = 2)
+// evaluates the pod without assuming it and writes the status words, the
+// profile's score rows (int64) and the result into the pinned host block the
+// caller reads in place, then sets the flag; no copy, no event.
+bool eval_topo_eligible(ksg_ctx* ctx, int32_t pod) {
+  return ctx->eval_fast && ctx->topo_coop && ctx->force_path != 1 && needs_topo(ctx, ctx->prof, pod, 1) &&
+         !range_has_ports(ctx, pod, 1) && coop_capture_fits(ctx) && check_supported(ctx, ctx->prof, pod, 1) == KSG_OK;
+}
+
+int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_eval_rows* view = nullptr) {
+  const size_t N = ctx->c.N;
+  const ksg_profile& prof = ctx->prof;
+  int rows[KSG_NPLUGINS], n_rows = 0, n_normrows = 0;
+  for (int pl : {KSG_PL_TAINT_TOLERATION, KSG_PL_NODE_AFFINITY, KSG_PL_POD_TOPOLOGY_SPREAD, KSG_PL_INTER_POD_AFFINITY})
+    if ((prof.score_mask >> pl) & 1u) rows[n_rows++] = pl;
+  n_normrows = n_rows;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    if (((prof.score_mask >> pl) & 1u) && pl != KSG_PL_TAINT_TOLERATION && pl != KSG_PL_NODE_AFFINITY &&
+        pl != KSG_PL_POD_TOPOLOGY_SPREAD && pl != KSG_PL_INTER_POD_AFFINITY)
+      rows[n_rows++] = pl;
+  constexpr size_t es = 8;   // raw PodTopologySpread / InterPodAffinity scores are not range-checked: int64 rows
+  // host block: result (16 B) .. flag at 28 | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_normrows][N]
+  const size_t o_fs = 32, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
+  const size_t o_tot = o_raw + es * N * n_rows, o_norm = o_tot + es * N;
+  const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
+  int rc;
+  HIPC(ctx, hipSetDevice(ctx->device));
+  if ((rc = flush_stage(ctx))) return rc;   // the topology kernel reads the pod from the device pool
+  if (!ctx->d_ev_prof && (rc = dalloc(ctx, &ctx->d_ev_prof, 1))) return rc;
+  if (!ctx->d_ev_pl && (rc = dalloc(ctx, &ctx->d_ev_pl, 4))) return rc;
+  if (h_need > ctx->h_evt_bytes) {
+    if (ctx->h_evt) {
+      HIPC(ctx, hipStreamSynchronize(ctx->stream));
+      (void)hipHostFree(ctx->h_evt);
+      ctx->h_evt = nullptr;
+      ctx->h_evt_bytes = 0;
+    }
+    HIPC(ctx, hipHostMalloc((void**)&ctx->h_evt, h_need, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(ctx->h_evt, 0, h_need);
+    ctx->h_evt_bytes = h_need;
+    void* dp = nullptr;
+    HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_evt, 0));
+    ctx->d_hevt = static_cast<char*>(dp);
+  }
+  if (ctx->ev_prof_dirty) {
+    HIPC(ctx, hipMemcpyAsync(ctx->d_ev_prof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream));
+    ctx->ev_prof_dirty = false;
+  }
+  char* hb = ctx->h_evt;
+  char* db = ctx->d_hevt;
+  volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(hb + 28);
+  const unsigned seq = ++ctx->ev_seq == 0 ? ++ctx->ev_seq : ctx->ev_seq;
+  CoopCap cc;
+  cc.mode = 2;
+  cc.fs = reinterpret_cast<uint32_t*>(db + o_fs);
+  cc.raw = db + o_raw;
+  cc.norm = db + o_norm;
+  cc.tot = db + o_tot;
+  for (int q = 0; q < n_rows; q++) cc.rows[q] = rows[q];
+  cc.n_rows = n_rows;
+  cc.n_normrows = n_normrows;
+  cc.narrow = 0;
+  cc.h_res = reinterpret_cast<ksg_result*>(db);
+  cc.h_flag = reinterpret_cast<unsigned*>(db + 28);
+  cc.seq = seq;
+  if ((rc = run_topo_coop(ctx, pod, 1, ctx->d_ev_pl, nullptr, ctx->d_ev_prof, 0, &cc, false))) return rc;
+  for (unsigned spins = 0; *flag != seq; spins++) {
+    __builtin_ia32_pause();
+    if ((spins & 1023) == 1023) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipSuccess && *flag != seq)
+        return fail(ctx, KSG_E_DEVICE, "per-cycle topology evaluation: kernel finished without its completion flag "
+                                       "(grid barrier timed out?)");
+      if (e != hipSuccess && e != hipErrorNotReady)
+        return fail(ctx, KSG_E_DEVICE, std::string("per-cycle topology evaluation: ") + hipGetErrorString(e));
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  if ((rc = tcollect(ctx))) return rc;
+  *res = *reinterpret_cast<const ksg_result*>(hb);
+  if (view) {
+    *view = ksg_eval_rows{};
+    view->n_nodes = (int32_t)N;
+    view->elem_bytes = (int32_t)es;
+    view->fstatus = reinterpret_cast<const uint32_t*>(hb + o_fs);
+    for (int q = 0; q < n_rows; q++) {
+      view->raw[rows[q]] = hb + o_raw + es * N * q;
+      view->norm[rows[q]] = q < n_normrows ? hb + o_norm + es * N * q : view->raw[rows[q]];
+    }
+    view->total = hb + o_tot;
+  }
+  if (cap) {
+    if (cap->fstatus) std::memcpy(cap->fstatus, hb + o_fs, 4 * N);
+    for (int q = 0; q < n_rows; q++) {
+      if (cap->raw) std::memcpy(cap->raw + (size_t)rows[q] * N, hb + o_raw + es * N * q, es * N);
+      if (cap->norm)
+        std::memcpy(cap->norm + (size_t)rows[q] * N, hb + (q < n_normrows ? o_norm + es * N * q : o_raw + es * N * q),
+                    es * N);
+    }
+    if (cap->total) std::memcpy(cap->total, hb + o_tot, es * N);
+  }
+  ctx->last_path = 6;
+  return KSG_OK;
+}
+
 int eval_internal(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) {
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
   if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, cap);   // consumes or flushes a staged append
+  if (eval_topo_eligible(ctx, pod)) return eval_topo_fast(ctx, pod, res, cap);
   int32_t pl;
   return run_internal(ctx, pod, 1, 0, &pl, res, cap);
 }
@@ -4302,6 +4575,7 @@ int ksg_open(int device, ksg_ctx** out) {
     ctx->cycle_block = v <= 64 ? 64 : v <= 128 ? 128 : 256;
   }
   if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_TEST_INJECT_WALK_ERR")) ctx->inject_walk_err = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);
@@ -4324,6 +4598,7 @@ int ksg_close(ksg_ctx* ctx) {
   }
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->h_ev) (void)hipHostFree(ctx->h_ev);
+  if (ctx->h_evt) (void)hipHostFree(ctx->h_evt);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->ev_stage) (void)hipEventDestroy(ctx->ev_stage);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -4489,7 +4764,8 @@ int ksg_eval_view(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_eval_rows* row
   if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
   if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, nullptr, rows);
-  // topology pods: the queue kernel into library-owned int64 rows
+  if (eval_topo_eligible(ctx, pod)) return eval_topo_fast(ctx, pod, res, nullptr, rows);
+  // otherwise: run_internal into library-owned int64 rows
   const size_t N = ctx->c.N;
   ctx->view_fs.resize(N);
   ctx->view_rows.resize((2 * (size_t)KSG_NPLUGINS + 1) * N);
@@ -4853,7 +5129,8 @@ int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
   if (!ctx || !path || !flags) return KSG_E_INVALID;
   *path = ctx->last_path;
   *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0) |
-           (ctx->last_tcol ? KSG_RUN_TCOL : 0) | (ctx->last_spec ? KSG_RUN_SPEC : 0);
+           (ctx->last_tcol ? KSG_RUN_TCOL : 0) | (ctx->last_spec ? KSG_RUN_SPEC : 0) |
+           (ctx->last_mw ? KSG_RUN_WIDE_MEM : 0);
   return KSG_OK;
 }
 

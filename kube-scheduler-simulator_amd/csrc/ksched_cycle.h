@@ -23,23 +23,27 @@
 //                              rows and weighted totals, its selectHost key;
 //                              a pod with < 2 feasible nodes ran no Score, so
 //                              its raw rows are zeroed instead
-//   the last arrival           folds the G keys (G words, not N nodes), writes
-//                              the statistics and sets the host flag
+//   completion                 every workgroup writes its selectHost key and
+//                              error bits into its own record of the host
+//                              block, then (after its rows) its done word =
+//                              the call's sequence number; the host folds the
+//                              G keys (no arrival counter, no last workgroup)
 //
-// No workgroup walks all N nodes, and no row is written twice except in the
-// < 2 feasible case.  Hand-offs between workgroups follow ksched_sweep.h
-// (gst / gld: agent-scope stores and loads, every wave drained before the
-// workgroup barrier in front of the arrival); the host-visible bytes are
-// ordered by a system-scope release in every workgroup before its arrival
-// and in the last one before the flag.  Same arithmetic as ksg_capture_eval +
+// No workgroup walks all N nodes and every row is written once.  The
+// exchange follows ksched_sweep.h (gst / gld: agent-scope stores and loads,
+// every wave drained before the workgroup barrier in front of the flag); the
+// host-visible bytes are system-scope stores drained (vmcnt(0)) before the
+// workgroup's done word.  Rows are 2, 4 or 8 bytes per value (the narrowest
+// exact width, chosen by the host).  Same arithmetic as ksg_capture_eval +
 // ksg_capture_norm (nb = 1, nothing assumed), bit for bit.
 
 struct CycPart {   // one workgroup's phase-1 statistics
   int32_t nfeas, max_t, max_a, lo;   // lo = max over its feasible nodes of N - n
 };
-struct CycKey {    // one workgroup's phase-2 result
-  unsigned long long key;
-  uint32_t err, pad;
+struct CycWg {     // one workgroup's record in the host block
+  unsigned long long key;   // its selectHost key (0: no feasible node)
+  uint32_t err;             // bit 0: a normalised score left [0, 100]; bit 1: the exchange timed out
+  uint32_t done;            // = seq once every row of the workgroup and the two words above are written
 };
 
 struct CycArgs {
@@ -49,25 +53,23 @@ struct CycArgs {
   const int32_t* prog;
   const ksg_profile* prof;
   int32_t pod;
+  int32_t blob, blob_len;            // the pod's program blob (host copy of pods[pod].blob / blob_len)
   int32_t n_rows, n_normrows;        // score rows (the normalising ones first)
   int32_t rows[KSG_NPLUGINS];
-  int32_t narrow;                    // rows are int32 (host-checked) instead of int64
+  int32_t es;                        // bytes per row value: 2, 4 or 8 (host range-checked)
   // host outputs (fine-grained pinned memory, device addresses)
   uint32_t* h_fs;                    // [N]
   char* h_raw;                       // [n_rows][N]
   char* h_tot;                       // [N]
   char* h_norm;                      // [n_normrows][N]
-  int32_t* h_stats;                  // [4] nfeas, max taint, max node affinity, max (N - n)
-  unsigned long long* h_best;        // selectHost key
-  uint32_t* h_err;                   // bit 0: a normalised score left [0, 100]; bit 1: exchange timed out
-  unsigned* h_flag;                  // = seq once everything above is written
+  int32_t* h_stats;                  // [4] nfeas, max taint, max node affinity, max (N - n) (workgroup 0)
+  CycWg* h_wg;                       // [G]
   unsigned seq;
   // device scratch
   CycPart* parts;                    // [G]
-  CycKey* keys;                      // [G]
   unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
-  unsigned* done;                    // phase-2 arrivals of this call (reset to 0 by the last one)
   unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
+  unsigned long long* stamps;        // KSG_STAMPS builds: per-segment cycle sums of workgroup 0
   // a staged append of this pod (ksg_capture_eval's spod fields)
   const ksg_pod* spod;
   const int32_t* sprog;
@@ -91,6 +93,23 @@ __device__ __forceinline__ void cyc_put(char* base, size_t idx, int64_t v, bool 
   if (narrow) hst<SYS>(reinterpret_cast<int32_t*>(base) + idx, (int32_t)v);
   else hst<SYS>(reinterpret_cast<int64_t*>(base) + idx, v);
 }
+template <bool SYS>
+__device__ __forceinline__ void cyc_put_es(char* base, size_t idx, int64_t v, int es) {
+  if (es == 2) hst<SYS>(reinterpret_cast<int16_t*>(base) + idx, (int16_t)v);
+  else cyc_put<SYS>(base, idx, v, es == 4);
+}
+
+#ifdef KSG_STAMPS
+#define KSG_YSTAMP(seg)                                                       \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();               \
+    if (tid == 0 && blockIdx.x == 0) { y_acc[seg] += _t - y_last; y_last = _t; } \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+  } while (0)
+#else
+#define KSG_YSTAMP(seg) do {} while (0)
+#endif
 // Every host store of this wave performed before what follows (the arrival,
 // the flag).
 template <bool SYS>
@@ -132,50 +151,62 @@ __device__ __forceinline__ bool cyc_exchange(const CycArgs& a, int G) {
 template <int BLOCK, bool SYS>
 __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
   constexpr int NW = BLOCK / 64;
+  constexpr int PW = (int)(sizeof(ksg_pod) / 4), FW = (int)(sizeof(ksg_profile) / 4);
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
   __shared__ ksg_profile s_prof;
   __shared__ int32_t s_st[4][NW];
   __shared__ unsigned long long s_key[NW];
   __shared__ uint32_t s_err[NW];
-  __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int G = (int)gridDim.x;
   const DevCluster& c = a.c;
   const int N = c.N;
   const size_t NN = N;
-  const bool narrow = a.narrow != 0;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
-  const int32_t* gprog = a.prog;
-  if (a.spod) {   // the staged append: read it from the host buffer; workgroup 0 copies it to the device
-    if (tid < (int)(sizeof(ksg_pod) / 4))
-      reinterpret_cast<int32_t*>(&s_pod)[tid] = reinterpret_cast<const int32_t*>(a.spod)[tid];
-    __syncthreads();
-    const int64_t boff = s_pod.blob - a.sbase;
-    for (int i = tid; i < s_pod.blob_len; i += BLOCK) s_blob[i] = a.sprog[boff + i];
-    gprog = a.sprog - a.sbase;
-    if (blockIdx.x == 0) {
-      if (tid < (int)(sizeof(ksg_pod) / 4))
-        reinterpret_cast<int32_t*>(a.wpods)[tid] = reinterpret_cast<const int32_t*>(&s_pod)[tid];
-      for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
-    }
-  } else {
-    stage_pod<BLOCK>(a.pods, a.prog, a.pod, &s_pod, s_blob);
+  const int es = a.es;
+#ifdef KSG_STAMPS
+  unsigned long long y_acc[10] = {}, y_last = __builtin_amdgcn_s_memtime();
+#endif
+  // Every load of the prologue is issued before the first wait: the profile,
+  // the pod record and its program blob (offset and length come with the
+  // launch, so the blob loads do not wait for the record) and this lane's
+  // node columns, so the chain costs one memory latency instead of three.
+  const int32_t* gprog = a.spod ? a.sprog - a.sbase : a.prog;
+  const int32_t* prec = a.spod ? reinterpret_cast<const int32_t*>(a.spod)
+                               : reinterpret_cast<const int32_t*>(a.pods + a.pod);
+  const int32_t fw = tid < FW ? reinterpret_cast<const int32_t*>(a.prof)[tid] : 0;
+  const int32_t pw = tid < PW ? prec[tid] : 0;
+  constexpr int BI = (KSG_BLOB_MAX + BLOCK - 1) / BLOCK;
+  int32_t bw[BI];
+#pragma unroll
+  for (int u = 0; u < BI; u++) {
+    const int i = tid + u * BLOCK;
+    bw[u] = i < a.blob_len ? gprog[a.blob + i] : 0;
   }
-  __syncthreads();
+  const int n = blockIdx.x * BLOCK + tid;
+  const bool own = n < N;
+  NodeCols L;
+  if (own) load_cols(c, a.st.requested, a.st.nonzero, a.st.pod_count, n, L);
+  if (tid < FW) reinterpret_cast<int32_t*>(&s_prof)[tid] = fw;
+  if (tid < PW) reinterpret_cast<int32_t*>(&s_pod)[tid] = pw;
+#pragma unroll
+  for (int u = 0; u < BI; u++) {
+    const int i = tid + u * BLOCK;
+    if (i < a.blob_len) s_blob[i] = bw[u];
+  }
+  if (a.spod && blockIdx.x == 0) {   // the staged append: workgroup 0 copies it to the device
+    if (tid < PW) reinterpret_cast<int32_t*>(a.wpods)[tid] = pw;
+    for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
+  }
+  lds_barrier();   // LDS only: the node-column loads stay in flight
+  KSG_YSTAMP(0);
   const PodView v = make_view(c, s_prof, s_pod, s_blob, gprog, false, a.st.ports);
 
   // ---- phase 1: this workgroup's nodes ------------------------------------------------
-  const int n = blockIdx.x * BLOCK + tid;
-  const bool own = n < N;
   NodeEval e{KSG_FS_NOT_EVALUATED, 0, 0, 0, 0};
   int64_t lraw[KSG_NPLUGINS] = {};
-  if (own) {
-    NodeCols L;
-    load_cols(c, a.st.requested, a.st.nonzero, a.st.pod_count, n, L);
-    e = eval_node_src(c, s_prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw);
-  }
+  if (own) e = eval_node_src(c, s_prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw);
+  KSG_YSTAMP(1);
   const bool ok = own && e.st == 0;
   // the row value of score row q (node-local plugins only on this path)
   auto raw_of = [&](int q) -> int64_t {
@@ -191,10 +222,6 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
     }
     return ok && ((v.smask >> pl) & 1u) ? x : 0;
   };
-  if (own) {
-    hst<SYS>(a.h_fs + n, e.st);
-    for (int q = 0; q < a.n_rows; q++) cyc_put<SYS>(a.h_raw, (size_t)q * NN + n, raw_of(q), narrow);
-  }
   int32_t feas = ok ? 1 : 0, mt = ok ? (int32_t)e.rt : 0, ma = ok ? (int32_t)e.ra : 0, lo = ok ? N - n : 0;
   feas = wave_sum32(feas);
   mt = (int32_t)wave_max64(mt);
@@ -219,8 +246,10 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
     gst(&pp->lo, lo);
   }
 
+  KSG_YSTAMP(2);
   // ---- exchange -------------------------------------------------------------------------
   const bool xok = cyc_exchange<BLOCK>(a, G);
+  KSG_YSTAMP(3);
 
   // ---- phase 2: fold the slots, normalise this workgroup's nodes ------------------------
   int32_t nfeas = 0, max_t = 0, max_a = 0, low = 0;
@@ -247,24 +276,23 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
       low = max(low, s_st[3][i]);
     }
   }
+  KSG_YSTAMP(4);
+  // every row of this workgroup's nodes, written once (the exchange above
+  // waited for nothing on the host link)
   uint64_t key = 0;
   uint32_t err = 0;
   if (own) {
+    const bool scored = nfeas >= 2;   // fewer than two feasible nodes: no Score ran, nothing recorded
     int64_t total = 0, nt = 0, na = 0;
-    if (nfeas >= 2 && ok) {
+    if (scored && ok) {
       total = total_score(v, e.part, e.rt, e.ra, max_t, max_a, err, &nt, &na);
       key = argmax_key(total, n);
     }
-    cyc_put<SYS>(a.h_tot, n, total, narrow);
-    if (nfeas >= 2) {
-      for (int q = 0; q < a.n_normrows; q++)
-        cyc_put<SYS>(a.h_norm, (size_t)q * NN + n, a.rows[q] == KSG_PL_TAINT_TOLERATION ? nt : na, narrow);
-    } else {   // fewer than two feasible nodes: no Score ran, nothing recorded
-      for (int q = 0; q < a.n_rows; q++) {
-        cyc_put<SYS>(a.h_raw, (size_t)q * NN + n, 0, narrow);
-        if (q < a.n_normrows) cyc_put<SYS>(a.h_norm, (size_t)q * NN + n, 0, narrow);
-      }
-    }
+    hst<SYS>(a.h_fs + n, e.st);
+    for (int q = 0; q < a.n_rows; q++) cyc_put_es<SYS>(a.h_raw, (size_t)q * NN + n, scored ? raw_of(q) : 0, es);
+    for (int q = 0; q < a.n_normrows; q++)
+      cyc_put_es<SYS>(a.h_norm, (size_t)q * NN + n, a.rows[q] == KSG_PL_TAINT_TOLERATION ? nt : na, es);
+    cyc_put_es<SYS>(a.h_tot, n, total, es);
   }
   key = wave_max_u64(key);
   err = wave_or32(err);
@@ -274,54 +302,26 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
     if (tid == 0)
       for (int i = 1; i < NW; i++) { key = s_key[i] > key ? s_key[i] : key; err |= s_err[i]; }
   }
+  host_release<SYS>();   // this wave's rows are written
+  KSG_YSTAMP(5);
+  __syncthreads();       // ... and every other wave's
   if (tid == 0) {
-    gst(&a.keys[blockIdx.x].key, key);
-    gst(&a.keys[blockIdx.x].err, err | (xok ? 0u : 2u));
-  }
-  // every wave's host stores performed (system scope) and its keys store
-  // drained before the arrival
-  host_release<SYS>();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)a.done, 1u,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == (unsigned)G - 1;
-  }
-  __syncthreads();
-  // The last adder reads the G keys with sc1 loads only (gld), every one
-  // stored sc1 and drained before its workgroup's add: the MI355X guide's
-  // "Valid forms" row 1 (one unsharded counter, the workgroup whose add came
-  // last), so no acquire fence.
-  if (!s_last) return;
-
-  // ---- the last arrival: fold G keys, publish -------------------------------------------
-  uint64_t best = 0;
-  uint32_t berr = 0;
-  for (int b = tid; b < G; b += BLOCK) {
-    const uint64_t k = gld(&a.keys[b].key);
-    best = k > best ? k : best;
-    berr |= gld(&a.keys[b].err);
-  }
-  best = wave_max_u64(best);
-  berr = wave_or32(berr);
-  if (NW > 1) {
-    __syncthreads();   // s_key reuse
-    if (lane == 0) { s_key[wv] = best; s_err[wv] = berr; }
-    __syncthreads();
-    if (tid == 0)
-      for (int i = 1; i < NW; i++) { best = s_key[i] > best ? s_key[i] : best; berr |= s_err[i]; }
-  }
-  if (tid == 0) {
-    hst<SYS>(a.h_stats + 0, nfeas);
-    hst<SYS>(a.h_stats + 1, max_t);
-    hst<SYS>(a.h_stats + 2, max_a);
-    hst<SYS>(a.h_stats + 3, low);
-    hst<SYS>(a.h_best, (unsigned long long)best);
-    hst<SYS>(a.h_err, berr);
-    gst(a.done, 0u);   // the next call's arrivals
+    CycWg* w = a.h_wg + blockIdx.x;
+    hst<SYS>(&w->key, (unsigned long long)key);
+    hst<SYS>(&w->err, err | (xok ? 0u : 2u));
+    if (blockIdx.x == 0) {   // the pod-wide statistics (every workgroup folded the same values)
+      hst<SYS>(a.h_stats + 0, nfeas);
+      hst<SYS>(a.h_stats + 1, max_t);
+      hst<SYS>(a.h_stats + 2, max_a);
+      hst<SYS>(a.h_stats + 3, low);
+    }
     host_release<SYS>();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(a.h_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&w->done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  KSG_YSTAMP(6);
+#ifdef KSG_STAMPS
+  if (tid == 0 && blockIdx.x == 0 && a.stamps)
+    for (int i = 0; i < 7; i++) atomicAdd(&a.stamps[i], y_acc[i]);
+#endif
 }

@@ -210,8 +210,10 @@ struct TopoShared {
 
 // Static record of a (pod, node) (ksg_sweep_static): bits 0-4 filter verdicts
 // (1 = rejects), 8-15 raw TaintToleration, 16-31 raw NodeAffinity, 32-39 raw
-// ImageLocality.
+// ImageLocality, 40-55 the node's first untolerated NoSchedule / NoExecute
+// taint slot (TaintToleration's status payload).
 constexpr uint32_t kSrUnsched = 1u, kSrNodeName = 2u, kSrTaint = 4u, kSrNodeAff = 8u, kSrNotEval = 16u;
+constexpr int kSrTaintSlotShift = 40;
 
 struct TopoCtx {
   const TopoProg* g;

@@ -67,7 +67,7 @@ struct SvItem {
   int32_t t;               // the pod whose assume made the version (-1: none, the carried live row)
 };
 
-template <int BLOCK>
+template <int BLOCK, bool MW = false>
 __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   using SL = SlotLayout<4>;
   constexpr int NW = BLOCK / 64;
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
 #pragma unroll
       for (int k = 0; k < SW / 2; k++) reinterpret_cast<int4*>(w)[k] = src[k];
     }
-    const TcRow row = tc_row(cm, w);
+    const TcRow row = tc_row<MW>(cm, w);
     const bool p1f = (p.x >> 63) != 0;
     const bool ft = p1f && (int32_t)((p.x >> 48) & 0xff) == hp.mt;
     const bool fa = p1f && (int32_t)((p.x >> 32) & 0xffff) == hp.ma;
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
     const int32_t na = hp.ma != 0 ? qdiv32(100 * ra, hp.ma, hp.inv_ma) : ra;
     const int32_t stat = p.st + hp.wt * nt + hp.wa * na;
     int32_t fb = 0;
-    const bool live = tc_eval(cm, hp, row, fb) && p1f;
+    const bool live = tc_eval<MW>(cm, hp, row, fb) && p1f;
     if (lane > it.t) s_col[it.slot * 64 + lane] = sv_word(stat + fb, live, p1f, ft, fa);
     else if (it.src < 0) s_col[it.slot * 64 + lane] = 0u;
   };
@@ -542,7 +542,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
 #pragma unroll
             for (int i = 0; i < SW; i++) w[i] = src[i];
             int32_t fb = 0;
-            if (!tc_eval(cm, hk, tc_row(cm, w), fb)) return 0;
+            if (!tc_eval<MW>(cm, hk, tc_row<MW>(cm, w), fb)) return 0;
             return pack_rec((int64_t)img[nd] + fb, (x >> 48) & 0xff, (x >> 32) & 0xffff);
           };
           Red r{0, 0, 0, 0x7fffffff};

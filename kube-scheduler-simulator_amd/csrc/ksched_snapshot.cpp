@@ -2044,13 +2044,24 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
   uint64_t last_key = ~0ull;
   int32_t last_idx = -1;
   std::string err;
-  for (int32_t n = 0; n < n_nodes; n++) {
-    const uint32_t w = words[n];
-    if (w == 0 || w == KSG_FS_NOT_EVALUATED) {
-      code[n] = KSG_CODE_SUCCESS;
-      msg[n] = -1;
-      continue;
+  // Most nodes pass: the passed defaults are written in straight vector loops
+  // over blocks of 64 nodes, whose rejected nodes (a 64-bit mask) are then
+  // decoded one by one.
+  constexpr int32_t kB = 64;
+  for (int32_t b = 0; b < n_nodes; b += kB) {
+    const int32_t m = std::min(kB, n_nodes - b);
+    uint8_t rj[kB];
+    for (int32_t i = 0; i < m; i++) {
+      const uint32_t w = words[b + i];
+      rj[i] = (uint8_t)(w != 0 && w != KSG_FS_NOT_EVALUATED);
     }
+    for (int32_t i = 0; i < m; i++) code[b + i] = KSG_CODE_SUCCESS;
+    for (int32_t i = 0; i < m; i++) msg[b + i] = -1;
+    uint64_t mask = 0;
+    for (int32_t i = 0; i < m; i++) mask |= (uint64_t)rj[i] << i;
+    for (; mask; mask &= mask - 1) {
+    const int32_t n = b + __builtin_ctzll(mask);
+    const uint32_t w = words[n];
     const int pl = (int)(w & 0xffu) - 1;
     uint64_t key = w;
     if (pl == KSG_PL_TAINT_TOLERATION && (int)(w >> 8) < e.max_taints)
@@ -2081,6 +2092,7 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     }
     code[n] = c;
     msg[n] = idx;
+    }
   }
   int64_t total = 0;
   for (auto& m : msgs) total += (int64_t)m.size() + 1;

@@ -142,9 +142,10 @@ constexpr int kStaticChunk = 8;
 constexpr int kStaticEff = 4096;   // taint vocabulary staged in LDS up to this size
 
 __device__ __forceinline__ void static_taints(const DevCluster& c, int n, const int32_t* tolf, const int32_t* tolp,
-                                              const uint8_t* eff, bool& reject, int64_t& score) {
+                                              const uint8_t* eff, bool& reject, int64_t& score, int* slot = nullptr) {
   reject = false;
   score = 0;
+  int first = -1;   // untolerated_slot: the first rejecting slot
   for (int s0 = 0; s0 < c.T; s0 += kStaticChunk) {
     uint32_t id[kStaticChunk];
 #pragma unroll
@@ -156,11 +157,17 @@ __device__ __forceinline__ void static_taints(const DevCluster& c, int n, const 
       if (end) continue;
       const uint32_t vid = id[k] - 1;
       const uint8_t e = eff[vid];
-      if (e == KSG_EFFECT_NO_SCHEDULE || e == KSG_EFFECT_NO_EXECUTE) reject |= !tol_bit(tolf, vid);
-      else if (e == KSG_EFFECT_PREFER_NO_SCHEDULE) score += !tol_bit(tolp, vid);
+      if (e == KSG_EFFECT_NO_SCHEDULE || e == KSG_EFFECT_NO_EXECUTE) {
+        const bool r = !tol_bit(tolf, vid);
+        if (r && first < 0) first = s0 + k;
+        reject |= r;
+      } else if (e == KSG_EFFECT_PREFER_NO_SCHEDULE) {
+        score += !tol_bit(tolp, vid);
+      }
     }
     if (end) break;
   }
+  if (slot) *slot = first;
 }
 
 // ImageLocality's sum over the pod's image entries, the node's sorted image
@@ -225,13 +232,15 @@ __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   if (p.node_name != -1 && p.node_name != n) bits |= kSrNodeName;
   bool treject;
   int64_t tscore;
-  static_taints(c, n, v.tolf, v.tolp, eff_lds ? s_eff : c.taint_effect, treject, tscore);
+  int tslot = -1;
+  static_taints(c, n, v.tolf, v.tolp, eff_lds ? s_eff : c.taint_effect, treject, tscore, &tslot);
   if (treject) bits |= kSrTaint;
   if (!na_required_match(nd, v.P, v.na_req)) bits |= kSrNodeAff;
   const uint64_t rt = (uint64_t)tscore;
   const uint64_t ra = v.na_pref >= 0 ? (uint64_t)na_pref_score(nd, v.P, v.na_pref) : 0;
   const uint64_t im = (uint64_t)static_images(c, n, v.P, v.img, p.n_containers);
-  a.srec[(size_t)j * N + n] = bits | ((rt & 0xff) << 8) | ((ra & 0xffff) << 16) | ((im & 0xff) << 32);
+  a.srec[(size_t)j * N + n] = bits | ((rt & 0xff) << 8) | ((ra & 0xffff) << 16) | ((im & 0xff) << 32) |
+                              ((uint64_t)(tslot < 0 ? 0 : tslot & 0xffff) << kSrTaintSlotShift);
 }
 
 // Replica-uniform facts of a profile for the sweep.

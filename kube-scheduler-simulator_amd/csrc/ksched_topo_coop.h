@@ -110,6 +110,20 @@ struct CoopArgs {
   unsigned* timeout;           // set when a barrier poll gave up
   int32_t pmode;               // 1: partial-slot histograms folded by every workgroup; 0: atomics into acc
   unsigned long long* stamps;  // diagnostic build only (KSG_STAMPS): per-segment cycle sums
+  int32_t commit;              // 0: evaluate only (ksg_eval / ksg_eval_view): no assume
+  // capture (CAP instances): every pod's status words and the profile's score
+  // rows, compact (row q = plugin cap_rows[q], the normalising ones first),
+  // every node written (no memset): [count][N] / [count][rows][N]
+  uint32_t* cap_fs;
+  char* cap_raw;
+  char* cap_norm;              // rows q < cap_n_normrows
+  char* cap_tot;
+  int32_t cap_rows[KSG_NPLUGINS];
+  int32_t cap_n_rows, cap_n_normrows, cap_narrow;
+  // CAP == 2, the per-cycle host block (one pod): the result, then the flag
+  ksg_result* h_res;
+  unsigned* h_flag;
+  unsigned seq;
 };
 
 // Hand-offs between the G workgroups without cache maintenance (MI355X guide,
@@ -202,8 +216,8 @@ __device__ __forceinline__ NodeEval eval_node_rec(const DevCluster& c, const ksg
         case KSG_PL_NODE_NAME:
           if (sr & kSrNodeName) st = pl + 1;
           break;
-        case KSG_PL_TAINT_TOLERATION:
-          if (sr & kSrTaint) st = pl + 1;
+        case KSG_PL_TAINT_TOLERATION:   // payload: the node's first untolerated taint slot (static record)
+          if (sr & kSrTaint) st = (uint32_t)(pl + 1) | ((uint32_t)((sr >> kSrTaintSlotShift) & 0xffff) << 8);
           break;
         case KSG_PL_NODE_AFFINITY:
           if (sr & kSrNodeAff) st = (uint32_t)(pl + 1) | (1u << 8);
@@ -278,7 +292,10 @@ struct OpOrI { __device__ int32_t operator()(int32_t a, int32_t b) const { retur
 // LL: the host guarantees KN == 1, every label column, the column vocabulary
 // and every term template fit their LDS copies; the evaluators' tables are then
 // LDS pointers at compile time (ds_read, not flat loads on the node paths).
-template <int KN, bool LL = false>
+// CAP: 0 placement only; 1 capture into device rows (captured queues);
+// 2 capture into the pinned host block + completion flag (the per-cycle
+// evaluation of a topology pod: one pod, a.commit = 0).
+template <int KN, bool LL = false, int CAP = 0>
 __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   constexpr int BLOCK = 256, NW = BLOCK / 64;
   constexpr long long BIG = 0x7fffffffffffffffll;
@@ -733,6 +750,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const bool soft1 = g.pts_score && g.n_soft == 1;
 
     NodeEval ev[KN];
+    int32_t fitr[KN], bar[KN];   // CAP: the raw NodeResourcesFit / BalancedAllocation scores
     int64_t yv[KN];
     int64_t pm[KN];   // one soft PTS constraint: the node's count m ...
     int32_t pr[KN];   // ... and pts_soft1_m's case (0 m valid, 1 no key, 2 ignored)
@@ -757,6 +775,10 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       ev[k] = eval_node_rec(c, prof, v, L, n, tn);
       KSG_CSTAMP(11);
       if (ev[k].st != 0) continue;
+      if constexpr (CAP != 0) {
+        fitr[k] = (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? (int32_t)fit_score(prof, p, L) : 0;
+        bar[k] = (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? (int32_t)ba_score(prof, p, L) : 0;
+      }
       nfeas += 1;
       minidx = min(minidx, n);
       max_t = max(max_t, (long long)ev[k].rt);
@@ -997,13 +1019,20 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     KSG_CSTAMP(14);
     uint64_t best = 0;
     uint32_t err = 0;
+    // CAP: per node the weighted total, the normalised TaintToleration /
+    // NodeAffinity / PodTopologySpread / InterPodAffinity scores and the raw
+    // PodTopologySpread (negative: ignored node, recorded 0)
+    int64_t ctot[KN], cnt_[KN], cna[KN], cps[KN], cis[KN], cpr[KN];
+#pragma unroll
+    for (int k = 0; k < KN; k++) ctot[k] = cnt_[k] = cna[k] = cps[k] = cis[k] = cpr[k] = 0;
     if (scored) {
       const int64_t w_pts = prof.weight[KSG_PL_POD_TOPOLOGY_SPREAD], w_ipa = prof.weight[KSG_PL_INTER_POD_AFFINITY];
 #pragma unroll
       for (int k = 0; k < KN; k++) {
         const int n = node_of(k);
         if (n >= N || ev[k].st != 0) continue;
-        int64_t total = total_score(v, ev[k].part, ev[k].rt, ev[k].ra, gmax_t, gmax_a, err, nullptr, nullptr);
+        int64_t total = total_score(v, ev[k].part, ev[k].rt, ev[k].ra, gmax_t, gmax_a, err,
+                                    CAP ? &cnt_[k] : nullptr, CAP ? &cna[k] : nullptr);
         if (do_pts) {   // PodTopologySpread.NormalizeScore
           int64_t x;
           if (soft1) {   // from the count kept since sweep A: no loads
@@ -1020,6 +1049,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           else s = div_small(100 * (pmax + pmin - x), pmax);
           err |= (s < 0 || s > 100);
           total += s * w_pts;
+          if constexpr (CAP != 0) { cps[k] = s; cpr[k] = x < 0 ? 0 : x; }
         }
         if (do_ipa) {   // InterPodAffinity.NormalizeScore (float64 min-max)
           const int64_t y = yv[k];
@@ -1029,9 +1059,42 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           const int64_t s = (int64_t)f;
           err |= (s < 0 || s > 100);
           total += s * w_ipa;
+          if constexpr (CAP != 0) cis[k] = s;
         }
         const uint64_t key = argmax_key(total, n);
         best = key > best ? key : best;
+        if constexpr (CAP != 0) ctot[k] = total;
+      }
+    }
+    if constexpr (CAP != 0) {   // every row of this lane's nodes (ksg_capture semantics: < 2 feasible nodes record no scores)
+      constexpr bool SYS = CAP == 2;
+      const size_t NN = N;
+      const bool nar = a.cap_narrow != 0;
+      for (int k = 0; k < KN; k++) {
+        const int n = node_of(k);
+        if (n >= N) break;
+        const bool feas = scored && ev[k].st == 0;
+        hst<SYS>(a.cap_fs + (size_t)kq * NN + n, ok ? ev[k].st : (uint32_t)KSG_FS_NOT_EVALUATED);
+        for (int q = 0; q < a.cap_n_rows; q++) {
+          const int pl = a.cap_rows[q];
+          int64_t raw = 0, nrm = 0;
+          if (feas && ((v.smask >> pl) & 1u)) {
+            switch (pl) {
+              case KSG_PL_NODE_RESOURCES_FIT: raw = fitr[k]; nrm = raw; break;
+              case KSG_PL_BALANCED_ALLOCATION: raw = bar[k]; nrm = raw; break;
+              case KSG_PL_IMAGE_LOCALITY: raw = (int64_t)((srk[k] >> 32) & 0xff); nrm = raw; break;
+              case KSG_PL_TAINT_TOLERATION: raw = ev[k].rt; nrm = cnt_[k]; break;
+              case KSG_PL_NODE_AFFINITY: raw = ev[k].ra; nrm = cna[k]; break;
+              case KSG_PL_POD_TOPOLOGY_SPREAD: if (do_pts) { raw = cpr[k]; nrm = cps[k]; } break;
+              case KSG_PL_INTER_POD_AFFINITY: if (do_ipa) { raw = yv[k]; nrm = cis[k]; } break;
+              default: break;
+            }
+          }
+          const size_t row = ((size_t)kq * a.cap_n_rows + q) * NN + n;
+          cyc_put<SYS>(a.cap_raw, row, raw, nar);
+          if (q < a.cap_n_normrows) cyc_put<SYS>(a.cap_norm, ((size_t)kq * a.cap_n_normrows + q) * NN + n, nrm, nar);
+        }
+        cyc_put<SYS>(a.cap_tot, (size_t)kq * NN + n, feas ? ctot[k] : 0, nar);
       }
     }
     best = wreduce(best, OpMaxU64{});
@@ -1085,7 +1148,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       if (e) status |= KSG_ST_SCORE_ERROR;
       else selected = key_node(b);
     }
-    if (selected >= 0 && ((selected / BLOCK) % G) == wg && (selected % BLOCK) == tid)
+    if (a.commit && selected >= 0 && ((selected / BLOCK) % G) == wg && (selected % BLOCK) == tid)
     {
       coop_commit(cg, st, p, p.commit >= 0 ? s_blob + (p.commit - p.blob) : nullptr, selected);
       if (KN == 1) {   // the register copy
@@ -1105,13 +1168,19 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         score_skip |= bit(KSG_PL_INTER_POD_AFFINITY);
       }
       a.placements[a.out0 + kq] = selected;
-      if (a.results) {
-        ksg_result res;
-        res.selected = selected;
-        res.n_feasible = ok ? gnfeas : 0;
-        res.status = status;
-        res.score_skip = score_skip;
-        a.results[a.out0 + kq] = res;
+      ksg_result res;
+      res.selected = selected;
+      res.n_feasible = ok ? gnfeas : 0;
+      res.status = status;
+      res.score_skip = score_skip;
+      if (a.results) a.results[a.out0 + kq] = res;
+      if constexpr (CAP == 2) {   // every workgroup's host rows are done (barrier 3 drained them)
+        hst<true>(&a.h_res->selected, res.selected);
+        hst<true>(&a.h_res->n_feasible, res.n_feasible);
+        hst<true>(&a.h_res->status, res.status);
+        hst<true>(&a.h_res->score_skip, res.score_skip);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.h_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     KSG_CSTAMP(10);

@@ -112,6 +112,32 @@ def config2(n_nodes: int = 5000, n_pods: int = 50000, seed: int = 2, zones: int 
     return nodes, pods, P.config2_profile()
 
 
+def kubelet_memory(nodes, pods, seed: int = 12, pod_frac: float = 0.3):
+    """Memory as real clusters report it: node allocatable = capacity minus
+    kube-reserved / system-reserved / the eviction threshold, a whole number of
+    Ki but not of Mi (kubelet's status.allocatable, e.g. "65544720Ki"), and a
+    share of the pods requesting decimal quantities ("300M", "1500M": 10^6-byte
+    multiples).  Outside the 32-bit MiB forms; the wide-memory instance of the
+    speculate-and-verify walk covers it."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    for n in nodes:
+        reserved_ki = int(rng.integers(256 * 1024, 2 * 1024 * 1024)) | 1   # odd Ki: never whole MiB
+        n.allocatable[m.MEMORY] = n.allocatable[m.MEMORY] - reserved_ki * 1024
+    for p in pods:
+        if rng.random() < pod_frac:
+            for c in p.containers:
+                if c.requests.get(m.MEMORY):
+                    c.requests[m.MEMORY] = int(rng.integers(1, 80)) * 100 * 1000 * 1000   # 100M .. 7900M
+    return nodes, pods
+
+
+def config2_kubelet(n_nodes: int = 5000, n_pods: int = 50000, seed: int = 2):
+    """configs[1] with kubelet-style memory (kubelet_memory)."""
+    nodes, pods, prof = config2(n_nodes, n_pods, seed)
+    kubelet_memory(nodes, pods)
+    return nodes, pods, prof
+
+
 @functools.lru_cache(maxsize=None)
 def _zipf_cdf(n: int, a: float) -> np.ndarray:
     w = 1.0 / np.arange(1, n + 1) ** a

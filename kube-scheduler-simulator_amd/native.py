@@ -156,7 +156,7 @@ def make_profile(fields: dict) -> KsgProfile:
     return p
 
 
-RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL, RUN_SPEC = 1, 2, 4, 8   # ksg_last_run_info flags
+RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL, RUN_SPEC, RUN_WIDE_MEM = 1, 2, 4, 8, 16   # ksg_last_run_info flags
 
 
 class CaptureBuffers:
@@ -291,11 +291,10 @@ class Engine:
         r, v = KsgResult(), KsgEvalRows()
         self._check(self._eval_view(self.ctx, pod, C.byref(r), C.byref(v)))
         n = v.n_nodes
-        dt = np.int32 if v.elem_bytes == 4 else np.int64
+        ct = {2: C.c_int16, 4: C.c_int32, 8: C.c_int64}[v.elem_bytes]
 
         def row(ptr):
-            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int32 if dt is np.int32 else C.c_int64)),
-                                         (n,)).astype(np.int64)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), (n,)).astype(np.int64)
         out = {"fstatus": np.ctypeslib.as_array(v.fstatus, (n,)).copy(), "elem_bytes": v.elem_bytes,
                "raw": {p: row(v.raw[p]) for p in range(NPLUGINS) if v.raw[p]},
                "norm": {p: row(v.norm[p]) for p in range(NPLUGINS) if v.norm[p]},

@@ -175,7 +175,10 @@ func (e *PodEval) at(p unsafe.Pointer, node int) int64 {
 	if p == nil {
 		return 0
 	}
-	if e.elem == 4 {
+	switch e.elem {
+	case 2:
+		return int64(*(*int16)(unsafe.Add(p, 2*node)))
+	case 4:
 		return int64(*(*int32)(unsafe.Add(p, 4*node)))
 	}
 	return *(*int64)(unsafe.Add(p, 8*node))

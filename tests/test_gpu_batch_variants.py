@@ -211,3 +211,30 @@ def test_spec_walk_guard_reaches_the_host(overlap):
     a.load(enc, pf)
     with pytest.raises(native.KschedError, match="invariant broken"):
         a.run_queue(0, len(pods))
+
+
+# ---- the wide-memory instance of the spec walk (KSG_RUN_WIDE_MEM) ----------------
+@pytest.mark.parametrize("strategy,n_nodes,n_pods", [("least", 1500, 2500), ("most", 1500, 2500),
+                                                     ("least", 5000, 50000)])
+def test_spec_wide_memory_matches_oracle(oracle, strategy, n_nodes, n_pods):
+    """Kubelet-style memory (allocatable a whole number of Ki, not of Mi;
+    decimal pod requests): outside the N32 forms, so the spec walk runs its
+    wide-memory instance (memory in int64 bytes) and stays bit-exact."""
+    P = pkg("profile")
+    nodes, pods, prof = G.config2_kubelet(n_nodes=n_nodes, n_pods=n_pods)
+    if strategy == "most":
+        prof = P.config2_profile(strategy=P.MOST_ALLOCATED)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = _engine_with_batch_mode("spec")
+    a.load(enc, pf)
+    oracle.load(enc, pf)
+    pl, res = a.run_queue(0, len(pods))
+    assert a.last_run_info() == (2, native.RUN_SPEC | native.RUN_WIDE_MEM)
+    po, ro = oracle.run_queue(0, len(pods))
+    np.testing.assert_array_equal(pl, po)
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(res[f], ro[f], err_msg=f)
+    R = len(enc.cluster.res_names)
+    for x, y in zip(a.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(x, y)

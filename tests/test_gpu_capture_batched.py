@@ -110,3 +110,39 @@ def test_batched_capture_split_calls(timed, oracle):
         np.testing.assert_array_equal(a.total, b.total)
         np.testing.assert_array_equal(a.raw, b.raw)
         np.testing.assert_array_equal(a.norm, b.norm)
+
+
+# ---- captured topology queues on the chip-wide kernel ----
+TOPO_CASES = [
+    ("c3-400x300", lambda: G.config3(n_nodes=400, n_pods=300, apps=20, zones=4)),
+    ("c3-3000x200", lambda: G.config3(n_nodes=3000, n_pods=200, apps=40, zones=8)),
+    ("zoo-1", lambda: __import__("zoo").zoo(1, n_pods=120)),
+    ("zoo-3", lambda: __import__("zoo").zoo(3, n_pods=120)),
+]
+
+
+@pytest.mark.parametrize("name,make", TOPO_CASES, ids=[c[0] for c in TOPO_CASES])
+def test_topology_capture_on_the_chip_wide_kernel(timed, queue_kernel, oracle, name, make):
+    """PodTopologySpread / InterPodAffinity pods captured by ksg_topo_coop's
+    capture instance (compact rows, every node written) equal the oracle and
+    the single-workgroup queue kernel on every array, every node."""
+    nodes, pods, prof = make()
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    n, N = len(pods), len(nodes)
+    pg, rg, cg = _run(timed, enc, pf, n, N)
+    names = {k["name"] for k in timed.kernel_stats()}
+    assert any("ksg_topo_coop" in k for k in names), names
+    po, ro, co = _run(oracle, enc, pf, n, N)
+    pq, rq, cq = _run(queue_kernel, enc, pf, n, N)
+    for other, label in ((co, "oracle"), (cq, "queue kernel")):
+        np.testing.assert_array_equal(cg.fstatus, other.fstatus, err_msg=f"{label}: fstatus")
+        np.testing.assert_array_equal(cg.total, other.total, err_msg=f"{label}: total")
+        for pid in range(native.NPLUGINS):
+            if (pf["score_mask"] >> pid) & 1:
+                np.testing.assert_array_equal(cg.raw[:, pid], other.raw[:, pid], err_msg=f"{label}: raw {pid}")
+                np.testing.assert_array_equal(cg.norm[:, pid], other.norm[:, pid], err_msg=f"{label}: norm {pid}")
+    for p in (po, pq):
+        np.testing.assert_array_equal(pg, p)
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
