@@ -2310,6 +2310,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
   }
 }
 
+#include "ksched_topo_tables.h"
 #include "ksched_topo_coop.h"
 
 // dst[r * stride + i] = src[i] for every replica r = blockIdx.y (replica state
@@ -2507,6 +2508,10 @@ struct ksg_ctx {
   uint64_t* d_coop_srec = nullptr;    // [kCoopBatch][N] static records of the current batch
   int coop_gmax = 0;                  // co-resident workgroups of ksg_topo_coop
   bool topo_coop = true;              // env KSG_TOPO_COOP=0 disables
+  bool coop_tables = true;            // env KSG_COOP_TABLES=0: every pod runs phase 1 (no maintained tables)
+  int32_t* d_coop_notables = nullptr; // a zeroed word set standing for "no tables"
+  int32_t* d_tables = nullptr;        // the maintained domain tables and their index (ksched_topo_tables.h)
+  size_t tables_words = 0;
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched, 3 int64 sweep state
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
@@ -2673,10 +2678,14 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_coop_parts = nullptr;
   ctx->d_coop_phist = nullptr;
   ctx->d_coop_srec = nullptr;
+  ctx->d_tables = nullptr;
+  ctx->tables_words = 0;
+  ctx->d_coop_notables = nullptr;
   ctx->d_ev = nullptr;
   ctx->ev_bytes = 0;
   ctx->ev_clean = false;
   ctx->d_ev_prof = nullptr;
+  ctx->d_ev_pl = nullptr;
   ctx->ev_prof_dirty = true;
 }
 
@@ -3695,6 +3704,133 @@ const void* coop_kernel(int kn, bool ll, int cap) {
        : kn == 2 ? (const void*)ksg_topo_coop<2, false, 2> : kn == 4 ? (const void*)ksg_topo_coop<4, false, 2> : nullptr;
 }
 
+// The maintained domain tables for a topology run of pods [first, first +
+// count): the (selector, non-unique column) pairs, the unique-key hard
+// selectors and the totals their programs read (the same program layout as
+// parse_topo), laid out in one device block and rebuilt from cnt and the
+// labels by ksg_topo_tables_init.  Returns false (tables unused) when the
+// layout would not fit its limits.
+bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* out, int* rc) {
+  *rc = KSG_OK;
+  const int S = ctx->c.S, L = ctx->c.L, N = ctx->c.N;
+  if (S <= 0 || L <= 0 || (size_t)S * L > (1u << 24)) return false;
+  constexpr int kKc = 256;   // count-of-counts bins: a node's matching pods stay below 255
+  std::vector<int32_t> pair_off((size_t)S * L, -1), cc_off(S, -1), pres_off(L, -1);
+  std::vector<uint8_t> want_tot(S, 0);
+  std::vector<TopoTableTask> tasks;
+  size_t dom_words = 0, cc_words = 0, pres_words = 0;
+  bool fits = true;
+  auto pair = [&](int sel, int col) {
+    if (sel < 0 || col < 0 || col >= L || ctx->h_col_unique[col] || sel >= S) return;
+    const int V = ctx->h_col_vocab[col];
+    if (V > kTableLds) { fits = false; return; }
+    int32_t& o = pair_off[(size_t)sel * L + col];
+    if (o >= 0) return;
+    o = (int32_t)dom_words;
+    int po = -1;
+    if (pres_off[col] < 0) {
+      pres_off[col] = (int32_t)pres_words;
+      po = pres_off[col];
+      pres_words += (V + 31) / 32;
+    }
+    tasks.push_back(TopoTableTask{0, sel, col, o, po});
+    dom_words += V;
+  };
+  auto cc = [&](int sel) {
+    if (sel < 0 || sel >= S || cc_off[sel] >= 0) return;
+    cc_off[sel] = (int32_t)cc_words;
+    cc_words += kKc;
+    want_tot[sel] = 1;
+  };
+  const int32_t* P = ctx->h_prog.data();
+  for (int i = first; i < first + count; i++) {
+    const ksg_pod& p = ctx->h_pods[i];
+    if (p.pts >= 0) {
+      const int32_t* w = P + p.pts;
+      const int nh = w[0], ns = w[1];
+      const int32_t* hard = w + 3;
+      for (int k = 0; k < nh; k++) {
+        const int col = hard[7 * k], sel = hard[7 * k + 1];
+        if (col >= 0 && col < L && ctx->h_col_unique[col]) cc(sel);
+        else pair(sel, col);
+      }
+      const int32_t* soft = hard + 7 * nh;
+      for (int k = 0; k < ns; k++)
+        if (!soft[6 * k + 5]) pair(soft[6 * k + 1], soft[6 * k]);
+    }
+    if (p.ipa >= 0) {
+      const int32_t* w = P + p.ipa;
+      const int na = w[0], sel_all = w[1];
+      for (int k = 0; k < na; k++) {
+        const int col = w[3 + k];
+        if (col >= 0 && col < L && ctx->h_col_unique[col]) { if (sel_all >= 0 && sel_all < S) want_tot[sel_all] = 1; }
+        else pair(sel_all, col);
+      }
+      w += 3 + na;
+      const int nanti = *w++;
+      for (int k = 0; k < nanti; k++) pair(w[2 * k + 1], w[2 * k]);
+      w += 2 * nanti;
+      const int npref = *w++;
+      for (int k = 0; k < npref; k++) {
+        const int col = w[3 * k], sel = w[3 * k + 1];
+        if (col >= 0 && col < L && ctx->h_col_unique[col]) { if (sel >= 0 && sel < S) want_tot[sel] = 1; }
+        else pair(sel, col);
+      }
+    }
+  }
+  if (!fits || dom_words > (64u << 20)) return false;
+  for (int s = 0; s < S; s++)
+    if (want_tot[s]) tasks.push_back(TopoTableTask{1, s, 0, cc_off[s], -1});
+  for (int col = 0; col < L; col++) tasks.push_back(TopoTableTask{2, 0, col, 0, -1});
+  // block: dom | tot[S] | cc | pres | col_missing[L] | col_empty[L] | invalid | pair_off[S*L] | cc_off[S] |
+  // pres_off[L] | tasks
+  const size_t o_tot = dom_words, o_cc = o_tot + S, o_pres = o_cc + cc_words, o_miss = o_pres + pres_words,
+               o_empty = o_miss + L, o_inv = o_empty + L, o_pair = o_inv + 1, o_ccoff = o_pair + (size_t)S * L,
+               o_preso = o_ccoff + S, o_tasks = (o_preso + L + 3) & ~(size_t)3,
+               words = o_tasks + tasks.size() * (sizeof(TopoTableTask) / 4);
+  if (words > ctx->tables_words) {
+    if (ctx->d_tables) {
+      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_tables);
+      if (it != ctx->allocs.end()) ctx->allocs.erase(it);
+      if (hipStreamSynchronize(ctx->stream) != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: sync"); return false; }
+      (void)hipFree(ctx->d_tables);
+      ctx->d_tables = nullptr;
+      ctx->tables_words = 0;
+    }
+    if ((*rc = dalloc(ctx, &ctx->d_tables, words))) return false;
+    ctx->tables_words = words;
+  }
+  int32_t* b = ctx->d_tables;
+  auto up = [&](size_t off, const void* src, size_t bytes) {
+    return hipMemcpyAsync(b + off, src, bytes, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
+  };
+  bool ok = hipMemsetAsync(b, 0, sizeof(int32_t) * o_pair, ctx->stream) == hipSuccess &&
+            up(o_pair, pair_off.data(), sizeof(int32_t) * pair_off.size()) &&
+            up(o_ccoff, cc_off.data(), sizeof(int32_t) * S) && up(o_preso, pres_off.data(), sizeof(int32_t) * L) &&
+            up(o_tasks, tasks.data(), sizeof(TopoTableTask) * tasks.size());
+  if (!ok) { *rc = fail(ctx, KSG_E_DEVICE, "tables: upload"); return false; }
+  TopoTables t{};
+  t.dom = b;
+  t.tot = b + o_tot;
+  t.cc = b + o_cc;
+  t.pair_off = b + o_pair;
+  t.cc_off = b + o_ccoff;
+  t.pres = reinterpret_cast<uint32_t*>(b + o_pres);
+  t.pres_off = b + o_preso;
+  t.col_missing = b + o_miss;
+  t.col_empty = b + o_empty;
+  t.invalid = reinterpret_cast<unsigned*>(b + o_inv);
+  t.S = S;
+  t.L = L;
+  t.Kc = kKc;
+  hipLaunchKernelGGL(ksg_topo_tables_init, dim3((unsigned)tasks.size()), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
+                     t, reinterpret_cast<const TopoTableTask*>(b + o_tasks));
+  if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: init launch"); return false; }
+  (void)N;
+  *out = t;
+  return true;
+}
+
 int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
                   const ksg_profile* d_prof, int do_commit = 1, const CoopCap* cap = nullptr,
                   bool timed = true) {
@@ -3747,6 +3883,24 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   a.pmode = ctx->coop_pmode;
   a.timeout = ctx->d_coop_flags + 4;
   a.commit = do_commit;
+  // the maintained tables: placement runs (they are rebuilt per run from the
+  // state; a single-pod evaluation runs phase 1 instead of paying the rebuild)
+  if (ctx->coop_tables && do_commit && count > 1) {
+    TopoTables t{};
+    if (build_topo_tables(ctx, first, count, &t, &rc)) {
+      a.tt = t;
+      a.use_tables = 1;
+    } else if (rc) {
+      return rc;
+    }
+  }
+  if (!a.use_tables) {   // the kernel reads tt.invalid and the index arrays at setup: a valid empty set
+    if (!ctx->d_coop_notables && (rc = dalloc(ctx, &ctx->d_coop_notables, 64))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_notables, 0, 64 * sizeof(int32_t), ctx->stream));
+    TopoTables t{};
+    t.invalid = reinterpret_cast<unsigned*>(ctx->d_coop_notables);
+    a.tt = t;
+  }
   const int cmode = cap ? cap->mode : 0;
   const void* kf = coop_kernel(kn, ll, cmode);
   if (!kf) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: no capture instance for this many nodes");
@@ -4563,6 +4717,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
   if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_COOP_PMODE")) ctx->coop_pmode = atoi(f) != 0;
+  if (const char* f = getenv("KSG_COOP_TABLES")) ctx->coop_tables = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : m == "spec" ? 6 : 4;

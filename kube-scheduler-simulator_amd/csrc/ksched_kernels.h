@@ -225,11 +225,20 @@ struct TopoCtx {
                          // read it with agent-scope atomic loads, never from a cache line
   bool has_rec;          // rec = the node's static record: inclusion() reads its verdict bits
   uint64_t rec;
+  // ksg_topo_coop: the previous pod's assume reaches tab one pod late; these
+  // entries (index, added weight) are added by the reader meanwhile
+  const int32_t* lag_idx = nullptr;
+  const int32_t* lag_w = nullptr;
+  int lag_n = 0;
   __device__ __forceinline__ int32_t tabv(int idx) const {
+    int32_t v;
     if (coherent)   // agent-scope global (sc1) load: no stale L1 line, no acquire needed
-      return __hip_atomic_load((__attribute__((address_space(1))) int32_t*)(const_cast<int32_t*>(tab) + idx),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return tab[idx];
+      v = __hip_atomic_load((__attribute__((address_space(1))) int32_t*)(const_cast<int32_t*>(tab) + idx),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      v = tab[idx];
+    for (int i = 0; i < lag_n; i++) v += lag_idx[i] == idx ? lag_w[i] : 0;
+    return v;
   }
 };
 

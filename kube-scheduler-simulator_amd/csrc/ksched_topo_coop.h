@@ -72,6 +72,9 @@ struct CoopPart {   // one workgroup's partial results of the current pod
   // phase 3
   unsigned long long best;
   int32_t err;
+  // the pod's lag selectors' counts at this workgroup's best-key node and at
+  // its lowest feasible node (the winner's become the lag delta's old counts)
+  int32_t best_cnt[kLagSel], min_cnt[kLagSel];
 };
 
 struct CoopAcc {    // atomics fallback for large histograms
@@ -124,6 +127,9 @@ struct CoopArgs {
   ksg_result* h_res;
   unsigned* h_flag;
   unsigned seq;
+  // the maintained domain tables (ksched_topo_tables.h)
+  TopoTables tt;
+  int32_t use_tables;          // 1: pods within their scope skip phase 1 and barrier 1
 };
 
 // Hand-offs between the G workgroups without cache maintenance (MI355X guide,
@@ -259,8 +265,10 @@ __device__ __forceinline__ NodeEval eval_node_rec(const DevCluster& c, const ksg
 
 // NodeInfo.AddPod for node n by the lane that owns it: node columns and
 // selector counts with plain stores, domain tables with atomics.
+// tab_now = false: the template tables reach tab one pod late (the lag buffer,
+// applied by workgroup 0; readers add it meanwhile).
 __device__ __forceinline__ void coop_commit(const DevCluster& c, const DevState& st, const ksg_pod& p,
-                                            const int32_t* commit_prog, int n) {
+                                            const int32_t* commit_prog, int n, bool tab_now = true) {
   const int N = c.N;
   for (int r = 0; r < c.R; r++) st.requested[(size_t)r * N + n] += p.req[r];
   st.nonzero[n] += p.nz_cpu;
@@ -272,12 +280,49 @@ __device__ __forceinline__ void coop_commit(const DevCluster& c, const DevState&
     for (int i = 0; i < ns; i++) st.cnt[(size_t)w[i] * N + n] += 1;
     w += ns;
     const int nt = *w++;
-    for (int i = 0; i < nt; i++) {
+    for (int i = 0; tab_now && i < nt; i++) {
       const int t = w[2 * i];
       const uint32_t val = c.label_val[(size_t)c.tmpl_col[t] * N + n];
       if (!val) continue;
       gadd(st.tab + c.tmpl_off[t] + val, c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1);
       gadd(st.tmpl_total + t, 1);
+    }
+  }
+}
+
+// Workgroup 0 applies a pending assume to the tables (dom, tot, cc) and, when
+// they were lagged, to the template tables.  Called between the barrier after
+// every reader of the tables of this pod and the next barrier.
+__device__ __forceinline__ void lag_apply(const DevCluster& cg, const DevState& st, const TopoTables& t,
+                                          const LagDelta& d, bool tables, bool tab) {
+  const int tid = threadIdx.x, N = cg.N;
+  if (d.node < 0) return;
+  if (tables && tid < d.n_sel) {   // lane i: selector i
+    const int s = d.sel[tid];
+    gadd(t.tot + s, 1);
+    for (int col = 0; col < t.L; col++) {
+      const int off = t.pair_off[(size_t)s * t.L + col];
+      if (off < 0) continue;
+      const uint32_t v = cg.label_val[(size_t)col * N + d.node];
+      if (v) gadd(t.dom + off + v, 1);
+    }
+    const int co = t.cc_off[s];
+    if (co >= 0) {
+      const int k = d.old_cnt[tid];
+      if (k + 1 >= t.Kc - 1) {
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned*)t.invalid, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        gadd(t.cc + co + k, -1);
+        gadd(t.cc + co + k + 1, 1);
+      }
+    }
+  }
+  if (tab && tid >= 64 && tid < 64 + d.n_tmpl) {   // wave 1: the template-table entries
+    const int i = tid - 64;
+    if (d.tidx[i] >= 0) {
+      gadd(st.tab + d.tidx[i], d.tw[i]);
+      gadd(st.tmpl_total + d.tt[i], 1);
     }
   }
 }
@@ -318,12 +363,31 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ int32_t s_tcol[kCoopTmpl], s_toff[kCoopTmpl];
   __shared__ ksg_pod s_pods[kCoopBatch];   // the batch's pod records
   __shared__ double s_log[kCoopLog];       // log_table[0 .. kCoopLog): topologyNormalizingWeight of small domains
+  // the one-pod lag (ksched_topo_tables.h): the previous pod's assume, not yet
+  // in the tables / template tables; identical in every workgroup
+  __shared__ LagDelta s_lag;
+  __shared__ int s_lag_tab;      // 1: s_lag's template-table entries are pending (readers add them)
+  __shared__ int s_prev_imm;     // the previous pod wrote its template tables at once: barrier 1 orders them
+  __shared__ int s_tables_ok;    // the tables are exact for this launch
+  __shared__ int s_skip;         // this pod: no phase 1, no barrier 1 (tables, or nothing to count)
+  __shared__ int s_lsel[kLagSel];   // this pod's matched selectors (commit program) ...
+  __shared__ int s_nlsel;           // ... and their number (may exceed kLagSel)
+  __shared__ int s_wmin;            // this workgroup's lowest feasible node (phase 2)
+  __shared__ unsigned long long s_wbest;   // this workgroup's best key (phase 3)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
   const DevCluster& cg = a.c;   // global tables (assume writes; other nodes' labels)
   const int N = cg.N;
   const DevState& st = a.st;
+  const TopoTables& tt = a.tt;
+  if (tid == 0) {
+    s_lag.node = -1;
+    s_lag.n_sel = s_lag.n_tmpl = 0;
+    s_lag_tab = 0;
+    s_prev_imm = 0;
+    s_tables_ok = a.use_tables && !gld(tt.invalid);
+  }
   if (tid < (int)(sizeof(ksg_profile) / 4))
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profile)[tid];
   for (int i = tid; i < a.count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
@@ -461,6 +525,46 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       const PodView v0 = make_view(c, prof, p, s_blob, a.prog, true);
       parse_topo(p, s_blob, v0.fskip, v0.smask, s_g);
       layout_slots(c, s_g, s_t);
+      // this pod's matched selectors (its commit program): the lag delta of its assume
+      s_nlsel = 0;
+      if (p.commit >= 0) {
+        const int32_t* cw = s_blob + (p.commit - p.blob);
+        s_nlsel = cw[0];
+        for (int i = 0; i < kLagSel && i < cw[0]; i++) s_lsel[i] = cw[1 + i];
+      }
+      // Tables scope: every constraint counts over every node (default
+      // inclusion, every node has the key), and each histogram has its table.
+      const TopoProg& g0 = s_g;
+      // (a count-of-counts overflow in the previous pod's lag_apply sets invalid)
+      bool e = s_tables_ok != 0 && s_t.ok && !gld(tt.invalid);
+      auto pair = [&](int sel, int col) { return sel >= 0 ? tt.pair_off[(size_t)sel * tt.L + col] : -1; };
+      auto all = [&](int col) { return tt.col_missing[col] == 0; };
+      for (int i = 0; e && i < g0.n_hard; i++) {
+        const int32_t* h = g0.hard + 7 * i;
+        e = all(h[0]) && (!h[5] || p.na_req < 0) && !h[6] &&
+            (c.col_unique[h[0]] ? h[1] >= 0 && tt.cc_off[h[1]] >= 0 : pair(h[1], h[0]) >= 0 && tt.pres_off[h[0]] >= 0);
+      }
+      for (int i = 0; e && i < g0.n_soft; i++) {
+        const int32_t* sc = g0.soft + 6 * i;
+        e = all(sc[0]) && (!sc[3] || p.na_req < 0) && !sc[4] &&
+            (sc[5] || (c.col_unique[sc[0]] ? tt.col_empty[sc[0]] == 0 : pair(sc[1], sc[0]) >= 0));
+      }
+      if (g0.ipa) {
+        for (int i = 0; e && i < g0.n_aff; i++) {
+          const int col = g0.aff_cols[i];
+          e = c.col_unique[col] ? all(col) : pair(g0.sel_all, col) >= 0 && tt.pres_off[col] >= 0;
+        }
+        for (int i = 0; e && i < g0.n_anti; i++) {
+          const int col = g0.anti[2 * i];
+          e = c.col_unique[col] || (pair(g0.anti[2 * i + 1], col) >= 0 && tt.pres_off[col] >= 0);
+        }
+        for (int i = 0; e && i < g0.n_pref; i++) {
+          const int col = g0.pref[3 * i];
+          e = c.col_unique[col] ? all(col) : pair(g0.pref[3 * i + 1], col) >= 0 && tt.pres_off[col] >= 0;
+        }
+      }
+      const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
+      s_skip = !s_prev_imm && (!has_pre || e);
       for (int i = 0; i < kMaxHard; i++) { s_t.hard_min[i] = BIG; s_t.hard_dom[i] = 0; }
       for (int i = 0; i < kMaxSoft; i++) {
         s_t.soft_empty[i] = 0; s_t.soft_present[i] = 0; s_t.soft_empty_seen[i] = 0; s_size[i] = 0;
@@ -499,7 +603,12 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     }
     PodView v = make_view(c, prof, p, s_blob, a.prog, true);
     const TopoProg& g = s_g;
-    const TopoCtx tc{&s_g, &s_t, s_hist, st.cnt, st.tab, true, false, 0};
+    TopoCtx tc{&s_g, &s_t, s_hist, st.cnt, st.tab, true, false, 0};
+    if (s_lag_tab && s_lag.node >= 0) {   // tab lags the previous pod's assume: readers add its entries
+      tc.lag_idx = s_lag.tidx;
+      tc.lag_w = s_lag.tw;
+      tc.lag_n = s_lag.n_tmpl;
+    }
     __syncthreads();
     // which partial values this pod needs at all (pod-uniform): folds of the
     // others are skipped
@@ -510,8 +619,12 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     KSG_CSTAMP(0);
 
     // ---- phase 1: pre-pass over this lane's nodes -------------------------
+    // (skipped with the tables: the domain counts come from them in phase 2,
+    // and barrier 1 is not needed either, every cross-workgroup write of the
+    // previous pod being lagged)
     const bool pre = ok && (g.pts_filter || g.pts_score || g.ipa);
-    if (pre) {
+    const bool skip = s_skip != 0;
+    if (pre && !skip) {
       long long lmin[kMaxHard], ldom[kMaxHard], lempty[kMaxSoft], laff = 0, lany = 0;
 #pragma unroll
       for (int i = 0; i < kMaxHard; i++) { lmin[i] = BIG; ldom[i] = 0; }
@@ -640,11 +753,90 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     KSG_CSTAMP(1);
-    if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+    if (!skip && !coop_barrier(a.bar, a.timeout, G, target)) return;
     KSG_CSTAMP(2);
 
     // ---- phase 2: fold the partials into LDS; sweep A --------------------------
-    if (pre) {
+    if (pre && skip) {
+      // the domain counts from the tables, plus the pending assume of the
+      // previous pod (s_lag: +1 on its node's domain for the selectors it matched)
+      const LagDelta& d = s_lag;
+      auto in_lag = [&](int sel) {
+        int hit = -1;
+        for (int i = 0; i < d.n_sel; i++) hit = d.sel[i] == sel ? i : hit;
+        return d.node >= 0 ? hit : -1;
+      };
+      auto fill = [&](const Slot& sl, bool pres) {   // hist (+ presence bits) of a non-unique slot
+        const int off = tt.pair_off[(size_t)sl.sel * tt.L + sl.col];
+        const uint32_t lv = in_lag(sl.sel) >= 0 ? cg.label_val[(size_t)sl.col * N + d.node] : 0u;   // 0: none
+        for (int v = tid; v < sl.V; v += BLOCK) s_hist[sl.hist + v] = gld(tt.dom + off + v) + (lv && (uint32_t)v == lv ? 1 : 0);
+        if (pres) {
+          const int po = tt.pres_off[sl.col];
+          for (int w = tid; w < (sl.V + 31) / 32; w += BLOCK) s_hist[sl.pres + w] = (int32_t)tt.pres[po + w];
+        }
+      };
+      auto total = [&](int sel) { return (long long)gld(tt.tot + sel) + (in_lag(sel) >= 0 ? 1 : 0); };
+      for (int i = 0; i < g.n_hard; i++)
+        if (!s_t.hard[i].unique) fill(s_t.hard[i], true);
+      for (int i = 0; i < g.n_soft; i++)
+        if (!g.soft[6 * i + 5] && !s_t.soft[i].unique) fill(s_t.soft[i], false);
+      if (g.ipa) {
+        for (int i = 0; i < g.n_aff; i++)
+          if (!s_t.aff[i].unique) fill(s_t.aff[i], true);
+        for (int i = 0; i < g.n_anti; i++)
+          if (!s_t.anti[i].unique) fill(s_t.anti[i], true);
+        for (int i = 0; i < g.n_pref; i++)
+          if (!s_t.pref[i].unique) fill(s_t.pref[i], true);
+      }
+      // unique hard keys: the minimum count over the nodes from the
+      // count-of-counts table (wave w < n_hard: constraint w)
+      if (wv < g.n_hard && s_t.hard[wv].unique) {
+        const int sel = s_t.hard[wv].sel, co = tt.cc_off[sel], li = in_lag(sel);
+        const int old = li >= 0 ? d.old_cnt[li] : -2;
+        int first = 0x7fffffff;
+        for (int k0 = 0; k0 < tt.Kc && first == 0x7fffffff; k0 += 64) {
+          const int k = k0 + lane;
+          const int x = k < tt.Kc ? gld(tt.cc + co + k) - (k == old ? 1 : 0) + (k == old + 1 ? 1 : 0) : 0;
+          const unsigned long long b = __ballot(x > 0);
+          if (b) first = k0 + __builtin_ctzll(b);
+        }
+        if (lane == 0) { s_t.hard_min[wv] = first; s_t.hard_dom[wv] = N; }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        for (int i = 0; i < g.n_soft; i++) s_t.soft_empty[i] = 0;   // no node lacks the key or has ""
+        if (g.ipa) {
+          long long af = 0;
+          for (int i = 0; i < g.n_aff; i++) {
+            const Slot& sl = s_t.aff[i];
+            if (sl.unique) af += total(g.sel_all);
+            else for (int v = 1; v < sl.V; v++) af += s_hist[sl.hist + v];
+          }
+          s_t.aff_total = af;
+          int any = 0;
+          for (int i = 0; i < g.n_pref; i++) {
+            const Slot& sl = s_t.pref[i];
+            if (sl.unique) any |= total(sl.sel) > 0;
+            else for (int v = 1; v < sl.V; v++) any |= s_hist[sl.hist + v] > 0;
+          }
+          s_t.pref_any = any;
+        }
+      }
+      __syncthreads();
+      for (int i = 0; i < g.n_hard; i++) {   // minimum over present domains of the non-unique hard slots
+        const Slot& sl = s_t.hard[i];
+        if (sl.unique) continue;
+        long long m = BIG, dd = 0;
+        for (int val = tid; val < sl.V; val += BLOCK)
+          if (bit_get(s_hist, sl.pres, val)) { m = min(m, (long long)s_hist[sl.hist + val]); dd += 1; }
+        m = wave_min64(m);
+        dd = wave_sum64(dd);
+        if (lane == 0) {
+          atomicMin((unsigned long long*)&s_t.hard_min[i], (unsigned long long)m);
+          atomicAdd(&s_t.hard_dom[i], (int)dd);
+        }
+      }
+    } else if (pre) {
       if (pmode) {
         for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
         __syncthreads();
@@ -721,13 +913,15 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     KSG_CSTAMP(3);
     if (wg == 0 && prev_fallback_words)   // the set of pod kq - 1, read by everyone by now
       for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&nxt->hist[i], 0);
-    prev_fallback_words = pmode ? 0 : words;
+    prev_fallback_words = pmode ? 0 : words;   // (a skipping pod still merges its soft marks into acc)
     {   // existing pods' terms matching this pod: totals, one template per lane
       const int n_t = g.ipa ? g.n_ma + g.n_mh + g.n_mp : 0;
       for (int i = tid; i < n_t; i += BLOCK) {
         const int which = i < g.n_ma ? 0 : (i < g.n_ma + g.n_mh ? 1 : 2);
         const int tm = which == 0 ? g.m_anti[i] : (which == 1 ? g.m_hard[i - g.n_ma] : g.m_pref[i - g.n_ma - g.n_mh]);
-        const int32_t x = gld(&st.tmpl_total[tm]);
+        int32_t x = gld(&st.tmpl_total[tm]);
+        if (s_lag_tab && s_lag.node >= 0)   // the previous pod's pending template entries
+          for (int j = 0; j < s_lag.n_tmpl; j++) x += s_lag.tt[j] == tm && s_lag.tidx[j] >= 0 ? 1 : 0;
         if (x) atomicAdd((unsigned long long*)&s_tt[which], (unsigned long long)x);
       }
     }
@@ -845,8 +1039,9 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     }
     __syncthreads();
     if (tid == 0) {
+      s_wmin = get_i(1, OpMinI{});
       gst(&mine->nfeas, get_i(0, OpAddI{}));
-      gst(&mine->minidx, get_i(1, OpMinI{}));
+      gst(&mine->minidx, s_wmin);
       gst(&mine->max_t, get_i(6, OpMaxI32{}));
       gst(&mine->max_a, get_i(7, OpMaxI32{}));
       if (need_ign) gst(&mine->n_ignored, get_i(2, OpAddI{}));
@@ -880,6 +1075,10 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     KSG_CSTAMP(7);
 
     // ---- phase 3: fold phase 2; sizes, normalisation, argmax --------------------
+    // every reader of the tables and template tables for this pod is past
+    // barrier 2: workgroup 0 applies the previous pod's assume to them now (the
+    // next pod reads after barrier 3)
+    if (wg == 0) lag_apply(cg, st, tt, s_lag, s_tables_ok != 0, s_lag_tab != 0);
     {
       int32_t f_n = 0, f_min = 0x7fffffff, f_ign = 0, f_hv = 0, f_hz = 0, f_mt = 0, f_ma = 0;
       int32_t f_pr[kMaxSoft] = {0, 0, 0, 0}, f_se[kMaxSoft] = {0, 0, 0, 0};
@@ -1108,6 +1307,21 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       for (int i = 0; i < NW; i++) { b = max(b, (unsigned long long)s_l[i][10]); e |= s_i[i][13]; }
       gst(&mine->best, b);
       gst(&mine->err, e);
+      s_wbest = b;
+    }
+    if (a.commit && s_nlsel > 0) {   // the counts the assume will change (the winner's become the lag's)
+      __syncthreads();
+      const int nl = min(s_nlsel, kLagSel);
+      const int bn = s_wbest ? key_node(s_wbest) : -1, mn = s_wmin;
+#pragma unroll
+      for (int k = 0; k < KN; k++) {
+        const int n = node_of(k);
+        if (n >= N) break;
+        if (n == bn)
+          for (int i = 0; i < nl; i++) gst(&mine->best_cnt[i], cnt_at(st.cnt, N, s_lsel[i], n));
+        if (n == mn)
+          for (int i = 0; i < nl; i++) gst(&mine->min_cnt[i], cnt_at(st.cnt, N, s_lsel[i], n));
+      }
     }
     // the next pod's program words, loaded while this pod's last barrier waits
     nb_len = kq + 1 < a.count ? s_pods[kq + 1].blob_len : 0;
@@ -1148,9 +1362,14 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       if (e) status |= KSG_ST_SCORE_ERROR;
       else selected = key_node(b);
     }
+    // the template tables reach tab one pod late unless the pod owns more
+    // templates than the lag buffer holds
+    const int32_t* cprog = p.commit >= 0 ? s_blob + (p.commit - p.blob) : nullptr;
+    const int n_own_tmpl = cprog ? cprog[1 + cprog[0]] : 0;
+    const bool tab_now = n_own_tmpl > kLagTmpl;
     if (a.commit && selected >= 0 && ((selected / BLOCK) % G) == wg && (selected % BLOCK) == tid)
     {
-      coop_commit(cg, st, p, p.commit >= 0 ? s_blob + (p.commit - p.blob) : nullptr, selected);
+      coop_commit(cg, st, p, cprog, selected, tab_now);
       if (KN == 1) {   // the register copy
 #pragma unroll
         for (int r = 0; r < KSG_MAX_RES; r++)
@@ -1158,6 +1377,41 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         Lreg.nz_cpu += p.nz_cpu;
         Lreg.nz_mem += p.nz_mem;
         Lreg.pod_count += 1;
+      }
+    }
+    __syncthreads();   // every wave is past this pod's reads of s_lag (applied by workgroup 0 in phase 3)
+    if (tid == 0) {   // this pod's assume becomes the pending lag, in every workgroup alike
+      LagDelta& d = s_lag;
+      d.node = a.commit && selected >= 0 ? selected : -1;
+      d.n_sel = d.n_tmpl = 0;
+      s_lag_tab = 0;
+      s_prev_imm = 0;
+      if (d.node >= 0 && cprog) {
+        if (s_nlsel > kLagSel) {   // more matched selectors than the lag holds: the tables go unused
+          s_tables_ok = 0;
+          if (wg == 0) gst(tt.invalid, 1u);
+        }
+        d.n_sel = min(s_nlsel, kLagSel);
+        const int owner = (selected / BLOCK) % G;
+        const int32_t* cnts = scored ? a.parts[owner].best_cnt : a.parts[owner].min_cnt;
+        for (int i = 0; i < d.n_sel; i++) {
+          d.sel[i] = s_lsel[i];
+          d.old_cnt[i] = gld(cnts + i);
+        }
+        if (tab_now) {
+          s_prev_imm = 1;   // written at once by the owner lane: the next pod runs barrier 1
+        } else {
+          const int32_t* w = cprog + 2 + cprog[0];
+          d.n_tmpl = n_own_tmpl;
+          for (int i = 0; i < n_own_tmpl; i++) {
+            const int t = w[2 * i];
+            const uint32_t val = cg.label_val[(size_t)cg.tmpl_col[t] * N + selected];
+            d.tidx[i] = val ? cg.tmpl_off[t] + (int)val : -1;
+            d.tw[i] = cg.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1;
+            d.tt[i] = t;
+          }
+          s_lag_tab = 1;
+        }
       }
     }
     if (wg == 0 && tid == 0) {
@@ -1185,6 +1439,9 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     }
     KSG_CSTAMP(10);
   }
+  // the last pod's assume: no reader follows in this launch
+  __syncthreads();
+  if (wg == 0) lag_apply(cg, st, tt, s_lag, s_tables_ok != 0, s_lag_tab != 0);
 #ifdef KSG_STAMPS
   if (tid == 0 && wg == 0 && a.stamps)
     for (int i = 0; i < 16; i++) atomicAdd(&a.stamps[i], st_acc[i]);

@@ -1,0 +1,115 @@
+// Domain tables maintained at assume time for the chip-wide topology path
+// (ksched_topo_coop.h), included by ksched.hip inside its anonymous namespace.
+//
+// Upstream PodTopologySpread / InterPodAffinity PreFilter and PreScore count
+// matching pods per topology domain by walking every pod of every node
+// [upstream podtopologyspread/filtering.go calPreFilterState, scoring.go
+// PreScore; interpodaffinity/filtering.go PreFilter].  The topology kernel's
+// phase 1 folded the per-node selector counts cnt[s][n] into per-domain
+// histograms for every pod (a node loop, a merge of G partial histograms and a
+// grid barrier).  Here the domain counts are kept as state instead, updated
+// O(1) per assume:
+//
+//   dom[(s, c)][v]  Σ cnt[s][n] over the nodes whose label column c (a
+//                   non-unique topology key) has value v
+//   tot[s]          Σ cnt[s][n] over every node
+//   cc[s][k]        how many nodes have cnt[s][n] == k, for the selectors of
+//                   hard constraints on a unique key (hostname): its minimum
+//                   over the nodes is the smallest k with cc[s][k] > 0
+//   pres[c]         the values of column c that some node has (static)
+//
+// They are exact for a pod whose constraints count over every node (default
+// inclusion policies, every node carries the keys: col_missing),
+// which then skips phase 1 and its barrier.  Assumes reach the tables one pod
+// late (the lag lets the kernel run two grid barriers per pod; see
+// ksched_topo_coop.h) and every reader adds the pending delta itself.
+
+struct TopoTables {
+  int32_t* dom;                // dom words
+  int32_t* tot;                // [S]
+  int32_t* cc;                 // cc words: [Kc] per registered selector
+  const int32_t* pair_off;     // [S][L]: offset of (s, c)'s table in dom, -1 none
+  const int32_t* cc_off;       // [S]: offset of s's count-of-counts in cc, -1 none
+  uint32_t* pres;              // presence bitmaps
+  const int32_t* pres_off;     // [L]: offset of c's bitmap in pres (words), -1 none
+  int32_t* col_missing;        // [L]: 0 iff every node has label column c
+  int32_t* col_empty;          // [L]: some node has the value "" (id 1)
+  unsigned* invalid;           // set when a count or an assume did not fit: the tables go unused
+  int32_t S, L, Kc;
+};
+
+// One table-building task per workgroup (ksg_topo_tables_init).
+struct TopoTableTask {
+  int32_t kind;                // 0: dom[(s, c)] (+ pres[c] when first for c), 1: tot[s] + cc[s], 2: col_all /
+                               // col_empty of column col
+  int32_t sel, col, off, pres_off;
+};
+
+// Rebuild the tables from cnt and the labels: one workgroup per task, an LDS
+// histogram over the task's values, one pass over the nodes.
+constexpr int kTableLds = 8192;   // LDS words of a task's histogram (vocab / Kc bins)
+
+__global__ __launch_bounds__(256) void ksg_topo_tables_init(DevCluster c, DevState st, TopoTables t,
+                                                             const TopoTableTask* tasks) {
+  __shared__ int32_t s_h[kTableLds];
+  __shared__ int32_t s_tot;
+  const TopoTableTask k = tasks[blockIdx.x];
+  const int tid = threadIdx.x, N = c.N;
+  if (k.kind == 2) {
+    int missing = 0, empty = 0;
+    for (int n = tid; n < N; n += 256) {
+      const uint32_t v = lab(c, k.col, n);
+      missing += v == 0;
+      empty += v == 1;
+    }
+    missing = wave_sum32(missing);
+    empty = wave_sum32(empty);
+    if ((tid & 63) == 0) {
+      if (missing) atomicAdd(&t.col_missing[k.col], 1);   // counts the waves that saw a missing label
+      if (empty) atomicAdd(&t.col_empty[k.col], 1);
+    }
+    return;
+  }
+  const int bins = k.kind == 0 ? c.col_vocab[k.col] : t.Kc;
+  for (int i = tid; i < bins && i < kTableLds; i += 256) s_h[i] = 0;
+  if (tid == 0) s_tot = 0;
+  __syncthreads();
+  int32_t tot = 0;
+  for (int n = tid; n < N; n += 256) {
+    const int32_t x = st.cnt[(size_t)k.sel * N + n];
+    if (k.kind == 0) {
+      const uint32_t v = lab(c, k.col, n);
+      if (v && x) atomicAdd(&s_h[v], x);
+      if (k.pres_off >= 0 && v) atomicOr(&t.pres[k.pres_off + (v >> 5)], 1u << (v & 31));
+    } else {
+      tot += x;
+      if (k.off >= 0) atomicAdd(&s_h[x < t.Kc - 1 ? x : t.Kc - 1], 1);
+      if (k.off >= 0 && x >= t.Kc - 1) atomicOr(t.invalid, 1u);   // a count past the table
+    }
+  }
+  tot = wave_sum32(tot);
+  if ((tid & 63) == 0 && tot) atomicAdd(&s_tot, tot);
+  __syncthreads();
+  if (k.kind == 0) {
+    for (int i = tid; i < bins; i += 256) t.dom[k.off + i] = s_h[i];
+  } else {
+    if (tid == 0) t.tot[k.sel] = s_tot;
+    if (k.off >= 0)
+      for (int i = tid; i < t.Kc; i += 256) t.cc[k.off + i] = s_h[i];
+  }
+}
+
+// The pending effect of one assume on the tables and template tables, as every
+// workgroup of the topology kernel knows it one pod late (the lag buffers).
+constexpr int kLagSel = 8;    // matched selectors of the assumed pod that carry tables
+constexpr int kLagTmpl = 8;   // templates the assumed pod owns
+
+struct LagDelta {
+  int node;                    // the assumed node (-1: nothing pending)
+  int n_sel, n_tmpl;
+  int sel[kLagSel];            // matched selectors (all of them when <= kLagSel)
+  int old_cnt[kLagSel];        // cnt[sel][node] before the assume (the winner's published counts)
+  int tidx[kLagTmpl];          // tab index tmpl_off[t] + label value (-1: the node lacks the key)
+  int tw[kLagTmpl];            // the added weight (PREF: the term weight; else 1)
+  int tt[kLagTmpl];            // the template
+};

@@ -121,6 +121,7 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event run (PMC passes)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save-placements", default=None, help="write the last run's placements (.npy)")
     args = ap.parse_args()
 
     t0 = time.time()
@@ -187,6 +188,9 @@ def main():
     }
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baselines(enc, pf, profiles, P, args.cpu_budget)
+    if args.save_placements:
+        import numpy as np
+        np.save(args.save_placements, np.asarray(pl))
     print(json.dumps(out), flush=True)
 
 
