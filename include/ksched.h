@@ -289,6 +289,11 @@ int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t 
  * Stream-ordered: returns once the update is enqueued; every later
  * evaluation and read-back of the context sees it. */
 int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node);
+/* NodeInfo.AddPod of n pods at once: pods[i] onto nodes[i] (the pods already
+ * running when a snapshot is loaded, NodeInfo.Pods; the snapshot's replay of
+ * its bindings).  One launch, one lane per pod, every update an atomic
+ * addition (the result does not depend on the order of the AddPod calls). */
+int ksg_commit_batch(ksg_ctx* ctx, const int32_t* pods, const int32_t* nodes, int32_t n);
 /* Schedule pods [first, first+count) in order on the device.  placements
  * [count]; results [count] may be NULL; cap may be NULL (else per-pod arrays
  * of count * n_nodes entries). */

@@ -309,6 +309,15 @@ int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* pod, int32_t* inde
  * pod's terms (the next sync re-encodes when any changed).  Replaces the
  * reference's namespace informer feed (snapshot.go namespaces). */
 int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labels, const ksg_str_pair* labels);
+/* A pod the caller will add later (a pending pod of the scheduling queue, as
+ * the pod informer delivers it: upstream eventhandlers.go addPodToSchedulingQueue
+ * feeding the simulator's scheduler).  Its selectors, term templates, label
+ * keys, scalar resources and host ports join the encoding universe at the
+ * next encode / sync (one full re-encode per batch of hints); the pod itself
+ * is not a workload pod until ksg_snapshot_add_pod.  Adding it then appends in
+ * place (ksg_snapshot_sync *appended = 1) instead of re-encoding.  Hints never
+ * change a result: a selector or template nobody evaluates is only data. */
+int ksg_snapshot_hint_pod(ksg_snapshot* s, const ksg_pod_view* pod);
 /* Pod `pod` runs on `node` (NodeInfo.Pods): replayed as an assume at load. */
 int ksg_snapshot_bind(ksg_snapshot* s, int32_t pod, int32_t node);
 int ksg_snapshot_node_index(ksg_snapshot* s, const char* name, int32_t* index);

@@ -2352,6 +2352,47 @@ __global__ void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods
               p.ports >= 0 ? prog + p.ports : nullptr);
 }
 
+// ksg_commit_batch: commit_node of many (pod, node) pairs, one lane each;
+// every column update is an atomic add (or, for the UsedPorts bitmap, an
+// atomic or), so lanes sharing a node need no order.
+__global__ __launch_bounds__(256) void ksg_commit_batch_kernel(DevCluster c, DevState st, const ksg_pod* pods,
+                                                               const int32_t* prog, const int32_t* bp,
+                                                               const int32_t* bn, int n_binds) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_binds) return;
+  const ksg_pod& p = pods[bp[k]];
+  const int n = bn[k], N = c.N;
+  auto add64 = [](int64_t* a, int64_t v) {
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
+  };
+  for (int r = 0; r < c.R; r++) add64(st.requested + (size_t)r * N + n, p.req[r]);
+  add64(st.nonzero + n, p.nz_cpu);
+  add64(st.nonzero + (size_t)N + n, p.nz_mem);
+  atomicAdd(st.pod_count + n, 1);
+  if (p.ports >= 0 && st.ports) {
+    const int32_t* w = prog + p.ports;
+    const int32_t* own = w + 1 + w[0];
+    for (int i = 0; i < own[0]; i++) {
+      const uint32_t id = (uint32_t)own[1 + i];
+      atomicOr(st.ports + (size_t)(id >> 5) * N + n, 1u << (id & 31));
+    }
+  }
+  if (p.commit >= 0) {
+    const int32_t* w = prog + p.commit;
+    const int ns = *w++;
+    for (int i = 0; i < ns; i++) atomicAdd(st.cnt + (size_t)w[i] * N + n, 1);
+    w += ns;
+    const int nt = *w++;
+    for (int i = 0; i < nt; i++) {
+      const int t = w[2 * i];
+      const uint32_t val = c.label_val[(size_t)c.tmpl_col[t] * N + n];
+      if (!val) continue;
+      atomicAdd(st.tab + c.tmpl_off[t] + val, c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1);
+      atomicAdd(st.tmpl_total + t, 1);
+    }
+  }
+}
+
 // DefaultPreemption dry run (SelectVictimsOnNode), one lane per candidate
 // node: the lane takes the node's live columns, removes every potential
 // victim, checks NodeResourcesFit for the preemptor, then reprieves the
@@ -2509,6 +2550,10 @@ struct ksg_ctx {
   int coop_gmax = 0;                  // co-resident workgroups of ksg_topo_coop
   bool topo_coop = true;              // env KSG_TOPO_COOP=0 disables
   bool coop_tables = true;            // env KSG_COOP_TABLES=0: every pod runs phase 1 (no maintained tables)
+  // a deferred assume (ksg_commit): applied by the next per-cycle kernel, or
+  // launched by flush_commit before anything else reads the node state
+  bool defer_commit = true;           // env KSG_DEFER_COMMIT=0 disables
+  int32_t pc_pod = -1, pc_node = -1;
   int32_t* d_coop_notables = nullptr; // a zeroed word set standing for "no tables"
   int32_t* d_tables = nullptr;        // the maintained domain tables and their index (ksched_topo_tables.h)
   size_t tables_words = 0;
@@ -2680,6 +2725,7 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_coop_srec = nullptr;
   ctx->d_tables = nullptr;
   ctx->tables_words = 0;
+  ctx->pc_node = -1;   // a deferred assume onto the freed state
   ctx->d_coop_notables = nullptr;
   ctx->d_ev = nullptr;
   ctx->ev_bytes = 0;
@@ -3782,11 +3828,22 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
   for (int s = 0; s < S; s++)
     if (want_tot[s]) tasks.push_back(TopoTableTask{1, s, 0, cc_off[s], -1});
   for (int col = 0; col < L; col++) tasks.push_back(TopoTableTask{2, 0, col, 0, -1});
+  // each selector's (column, table offset) pairs (lag_apply)
+  std::vector<int32_t> sp_off(S + 1, 0), sp;
+  for (int s = 0; s < S; s++) {
+    sp_off[s] = (int32_t)(sp.size() / 2);
+    for (int col = 0; col < L; col++) {
+      const int32_t o = pair_off[(size_t)s * L + col];
+      if (o >= 0) { sp.push_back(col); sp.push_back(o); }
+    }
+  }
+  sp_off[S] = (int32_t)(sp.size() / 2);
   // block: dom | tot[S] | cc | pres | col_missing[L] | col_empty[L] | invalid | pair_off[S*L] | cc_off[S] |
-  // pres_off[L] | tasks
+  // pres_off[L] | sp_off[S+1] | sp | elig[count] (bytes) | tasks
   const size_t o_tot = dom_words, o_cc = o_tot + S, o_pres = o_cc + cc_words, o_miss = o_pres + pres_words,
                o_empty = o_miss + L, o_inv = o_empty + L, o_pair = o_inv + 1, o_ccoff = o_pair + (size_t)S * L,
-               o_preso = o_ccoff + S, o_tasks = (o_preso + L + 3) & ~(size_t)3,
+               o_preso = o_ccoff + S, o_spoff = o_preso + L, o_sp = o_spoff + S + 1, o_elig = o_sp + sp.size(),
+               o_tasks = (o_elig + ((size_t)count + 3) / 4 + 3) & ~(size_t)3,
                words = o_tasks + tasks.size() * (sizeof(TopoTableTask) / 4);
   if (words > ctx->tables_words) {
     if (ctx->d_tables) {
@@ -3807,6 +3864,8 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
   bool ok = hipMemsetAsync(b, 0, sizeof(int32_t) * o_pair, ctx->stream) == hipSuccess &&
             up(o_pair, pair_off.data(), sizeof(int32_t) * pair_off.size()) &&
             up(o_ccoff, cc_off.data(), sizeof(int32_t) * S) && up(o_preso, pres_off.data(), sizeof(int32_t) * L) &&
+            up(o_spoff, sp_off.data(), sizeof(int32_t) * (S + 1)) &&
+            (sp.empty() || up(o_sp, sp.data(), sizeof(int32_t) * sp.size())) &&
             up(o_tasks, tasks.data(), sizeof(TopoTableTask) * tasks.size());
   if (!ok) { *rc = fail(ctx, KSG_E_DEVICE, "tables: upload"); return false; }
   TopoTables t{};
@@ -3820,12 +3879,19 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
   t.col_missing = b + o_miss;
   t.col_empty = b + o_empty;
   t.invalid = reinterpret_cast<unsigned*>(b + o_inv);
+  t.sp_off = b + o_spoff;
+  t.sp = b + o_sp;
+  t.elig = reinterpret_cast<const uint8_t*>(b + o_elig);
+  t.first = first;
   t.S = S;
   t.L = L;
   t.Kc = kKc;
   hipLaunchKernelGGL(ksg_topo_tables_init, dim3((unsigned)tasks.size()), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
                      t, reinterpret_cast<const TopoTableTask*>(b + o_tasks));
   if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: init launch"); return false; }
+  hipLaunchKernelGGL(ksg_topo_tables_elig, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, ctx->stream, ctx->c, t,
+                     ctx->d_pods, ctx->d_prog, count, reinterpret_cast<uint8_t*>(b + o_elig));
+  if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: scope launch"); return false; }
   (void)N;
   *out = t;
   return true;
@@ -3965,6 +4031,7 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
 }
 
 int flush_stage(ksg_ctx* ctx);
+int flush_commit(ksg_ctx* ctx);
 
 // The capture instances of ksg_topo_coop cover up to 4 nodes per lane
 // (coop_kernel): 262,144 nodes on 256 workgroups.
@@ -3980,6 +4047,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   if (count == 0) return KSG_OK;
   HIPC(ctx, hipSetDevice(ctx->device));
   if ((rc = flush_stage(ctx))) return rc;
+  if ((rc = flush_commit(ctx))) return rc;
   const size_t N = ctx->c.N;
   Tmp tmp;
   ksg_profile* d_prof = nullptr;
@@ -4237,10 +4305,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   CycArgs ca{};
   ca.c = ctx->c;
   ca.st = ctx->st;
-  ca.pods = ctx->d_pods;
-  ca.prog = ctx->d_prog;
   ca.prof = ctx->d_ev_prof;
-  ca.pod = pod;
   ca.blob = hp.blob;   // the same pool index in the staging buffer (sprog - sbase) and in d_prog
   ca.blob_len = hp.blob_len;
   ca.n_rows = n_rows;
@@ -4264,13 +4329,25 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   }
   ca.stamps = ctx->d_stamps;
 #endif
+  // the pod's record and programs: the staged append (read over the host
+  // link, then written to the device pool by workgroup 0) or the device pool
+  const int32_t* sprog = staged ? reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod)) : nullptr;
+  ca.gprog = staged ? sprog - ctx->stage_base : ctx->d_prog;
+  ca.psrc = staged ? reinterpret_cast<const int32_t*>(ctx->d_stage) : reinterpret_cast<const int32_t*>(ctx->d_pods + pod);
+  ca.bsrc = ca.gprog + hp.blob;
   if (staged) {
-    ca.spod = reinterpret_cast<const ksg_pod*>(ctx->d_stage);
-    ca.sprog = reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod));
-    ca.sbase = ctx->stage_base;
-    ca.slen = ctx->stage_len;
     ca.wpods = ctx->d_pods + pod;
     ca.wprog = ctx->d_prog + ctx->stage_base;
+    ca.sprog = sprog;
+    ca.slen = ctx->stage_len;
+  }
+  ca.cm_node = -1;
+  if (ctx->pc_node >= 0) {   // the deferred assume: the node's owner lane adds it before evaluating
+    const ksg_pod& q = ctx->h_pods[ctx->pc_pod];
+    ca.cm_node = ctx->pc_node;
+    for (int r = 0; r < KSG_MAX_RES; r++) ca.cm_req[r] = q.req[r];
+    ca.cm_nz_cpu = q.nz_cpu;
+    ca.cm_nz_mem = q.nz_mem;
   }
   treset(ctx);
   if ((rc = tmark(ctx))) return rc;
@@ -4279,12 +4356,13 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
   else   // G is within the occupancy API's co-resident count less one per CU (the exchange's poll is bounded)
     HIPC(ctx, hipLaunchKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
+  ctx->pc_node = -1;   // applied by this launch (a retry below must not add it again)
   if ((rc = tlaunched(ctx, KSG_K_EVAL_CYCLE, (double)N))) return rc;
   HIPC(ctx, hipGetLastError());
-  if (staged) {   // consumed; the staging buffer is free once the stream passes this point
-    ctx->stage_pending = false;
-    HIPC(ctx, hipEventRecord(ctx->ev_stage, ctx->stream));
-  }
+  // the staged append is consumed: the kernel read it (or had it with the
+  // launch) before its workgroups stored their done words, which this call
+  // waits for, so the staging buffer is free when it returns (no event)
+  if (staged) ctx->stage_pending = false;
   // every workgroup stores seq into its record after its rows: spin on them,
   // checking the stream now and then (a failed launch never stores them)
   const CycWg* wgr = reinterpret_cast<const CycWg*>(hb + o_wg);
@@ -4413,6 +4491,7 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
   if ((rc = flush_stage(ctx))) return rc;   // the topology kernel reads the pod from the device pool
+  if ((rc = flush_commit(ctx))) return rc;
   if (!ctx->d_ev_prof && (rc = dalloc(ctx, &ctx->d_ev_prof, 1))) return rc;
   if (!ctx->d_ev_pl && (rc = dalloc(ctx, &ctx->d_ev_pl, 4))) return rc;
   if (h_need > ctx->h_evt_bytes) {
@@ -4574,6 +4653,29 @@ int flush_stage(ksg_ctx* ctx) {
   return KSG_OK;
 }
 
+// Launch a deferred assume (ksg_commit): every entry point that reads or
+// replaces the node state calls this first, except the per-cycle evaluation,
+// whose kernel applies the assume itself (ksched_cycle.h, cm_*).
+int flush_commit(ksg_ctx* ctx) {
+  if (ctx->pc_node < 0) return KSG_OK;
+  const int pod = ctx->pc_pod, node = ctx->pc_node;
+  ctx->pc_node = -1;
+  hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
+                     ctx->d_prog, pod, node, 1);
+  HIPC(ctx, hipGetLastError());
+  return KSG_OK;
+}
+
+// An assume the per-cycle kernel can apply: node columns only (no selector
+// counts, template tables or host ports).
+bool commit_deferrable(const ksg_ctx* ctx, int32_t pod) {
+  const ksg_pod& p = ctx->h_pods[pod];
+  if (p.ports >= 0) return false;
+  if (p.commit < 0) return true;
+  const int32_t* w = ctx->h_prog.data() + p.commit;
+  return w[0] == 0 && w[1] == 0;
+}
+
 int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t* prog, int64_t prog_len,
                     int64_t prog_base) {
   if (!ctx->have_wl) return fail(ctx, KSG_E_STATE, "load a workload before appending");
@@ -4718,6 +4820,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_COOP_PMODE")) ctx->coop_pmode = atoi(f) != 0;
   if (const char* f = getenv("KSG_COOP_TABLES")) ctx->coop_tables = atoi(f) != 0;
+  if (const char* f = getenv("KSG_DEFER_COMMIT")) ctx->defer_commit = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
     ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : m == "spec" ? 6 : 4;
@@ -4866,6 +4969,10 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
     return KSG_E_INVALID;
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "load nodes before the workload");
   HIPC(ctx, hipSetDevice(ctx->device));
+  {   // a deferred assume reads its pod from the pool about to be replaced
+    const int rc = flush_commit(ctx);
+    if (rc) return rc;
+  }
   ctx->stage_pending = false;   // a staged append of the replaced workload
   ctx->h_pods.assign(wl->pods, wl->pods + wl->n_pods);
   std::vector<int32_t> prog(wl->prog, wl->prog + wl->prog_len);
@@ -4984,6 +5091,12 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
   if (pod < 0 || pod >= ctx->n_pods || node < 0 || node >= ctx->c.N) return fail(ctx, KSG_E_INVALID, "commit range");
   HIPC(ctx, hipSetDevice(ctx->device));
   if ((rc = flush_stage(ctx))) return rc;
+  if ((rc = flush_commit(ctx))) return rc;   // one deferred assume at a time, in call order
+  if (sign > 0 && ctx->defer_commit && ctx->eval_fast && commit_deferrable(ctx, pod)) {
+    ctx->pc_pod = pod;   // the next per-cycle kernel applies it (or flush_commit launches it)
+    ctx->pc_node = node;
+    return KSG_OK;
+  }
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
                      ctx->d_prog, pod, node, sign);
   // stream-ordered: the next evaluation on ctx->stream sees the update, and
@@ -4993,6 +5106,30 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
 }
 
 int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node) { return commit_signed(ctx, pod, node, 1); }
+
+int ksg_commit_batch(ksg_ctx* ctx, const int32_t* pods, const int32_t* nodes, int32_t n) {
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && (!pods || !nodes))) return fail(ctx, KSG_E_INVALID, "commit batch arguments");
+  for (int32_t i = 0; i < n; i++)
+    if (pods[i] < 0 || pods[i] >= ctx->n_pods || nodes[i] < 0 || nodes[i] >= ctx->c.N)
+      return fail(ctx, KSG_E_INVALID, "commit batch: pod or node out of range");
+  if (n == 0) return KSG_OK;
+  HIPC(ctx, hipSetDevice(ctx->device));
+  if ((rc = flush_stage(ctx))) return rc;
+  if ((rc = flush_commit(ctx))) return rc;
+  Tmp tmp;
+  int32_t *dp = nullptr, *dn = nullptr;
+  TA(tmp, &dp, sizeof(int32_t) * (size_t)n);
+  TA(tmp, &dn, sizeof(int32_t) * (size_t)n);
+  HIPC(ctx, hipMemcpyAsync(dp, pods, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(ctx, hipMemcpyAsync(dn, nodes, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(ksg_commit_batch_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->c,
+                     ctx->st, ctx->d_pods, ctx->d_prog, dp, dn, n);
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));   // the temporaries are freed on return
+  return KSG_OK;
+}
 
 int ksg_uncommit(ksg_ctx* ctx, int32_t pod, int32_t node) { return commit_signed(ctx, pod, node, -1); }
 
@@ -5004,6 +5141,7 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
     return fail(ctx, KSG_E_INVALID, "preempt arguments");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
   if ((rc = flush_stage(ctx))) return rc;
+  if ((rc = flush_commit(ctx))) return rc;
   if (ctx->h_pods[pod].ports >= 0)   // the dry run re-runs Fit / PTS / IPA only
     return fail(ctx, KSG_E_UNSUPPORTED, "preemption: a preemptor with host ports (NodePorts) is not modelled");
   if (n_cand == 0) return KSG_OK;
@@ -5078,6 +5216,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     return fail(ctx, KSG_E_INVALID, "replica arguments");
   if ((rc = check_blobs(ctx, first, count))) return rc;
   if ((rc = flush_stage(ctx))) return rc;
+  if ((rc = flush_commit(ctx))) return rc;
   for (int r = 0; r < n_replicas; r++)
     if ((rc = check_supported(ctx, profiles[r], first, count))) return rc;
   HIPC(ctx, hipSetDevice(ctx->device));
@@ -5220,6 +5359,8 @@ int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out) {
   if (!ctx || !out) return KSG_E_INVALID;
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "no nodes loaded");
   HIPC(ctx, hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = flush_commit(ctx))) return rc;
   const size_t N = ctx->c.N, R = ctx->c.R;
   if (out->requested) HIPC(ctx, hipMemcpyAsync(out->requested, ctx->st.requested, 8 * R * N, hipMemcpyDeviceToHost, ctx->stream));
   if (out->nonzero) HIPC(ctx, hipMemcpyAsync(out->nonzero, ctx->st.nonzero, 16 * N, hipMemcpyDeviceToHost, ctx->stream));
@@ -5232,6 +5373,7 @@ int ksg_reset_state(ksg_ctx* ctx) {
   if (!ctx) return KSG_E_INVALID;
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "no nodes loaded");
   HIPC(ctx, hipSetDevice(ctx->device));
+  ctx->pc_node = -1;   // a deferred assume is reset with the rest
   const size_t N = ctx->c.N, R = ctx->c.R;
   HIPC(ctx, hipMemcpyAsync(ctx->st.requested, ctx->d_req0, 8 * R * N, hipMemcpyDeviceToDevice, ctx->stream));
   HIPC(ctx, hipMemcpyAsync(ctx->st.nonzero, ctx->d_nz0, 16 * N, hipMemcpyDeviceToDevice, ctx->stream));

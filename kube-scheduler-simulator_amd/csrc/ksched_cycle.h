@@ -46,14 +46,28 @@ struct CycWg {     // one workgroup's record in the host block
   uint32_t done;            // = seq once every row of the workgroup and the two words above are written
 };
 
+// The launch arguments.  The prologue's fields come first and together: the
+// kernel-argument segment is read with scalar loads, and fields the compiler
+// reaches through separate branches cost one round trip each.
 struct CycArgs {
+  // ---- prologue ----
+  const int32_t* psrc;               // the pod record: device pool or staged append
+  const int32_t* bsrc;               // its program blob
+  const int32_t* gprog;              // the program pool as the kernel sees it (node_set)
+  const ksg_profile* prof;
+  int32_t blob, blob_len;            // the pod's program blob (host copy of pods[pod].blob / blob_len)
+  int32_t cm_node;                   // a deferred assume (ksg_commit of a pod without selectors, templates or
+                                     // host ports) onto node cm_node, -1 none: its owner lane adds it first
+  int64_t cm_req[KSG_MAX_RES];
+  int64_t cm_nz_cpu, cm_nz_mem;
+  // a staged append of this pod: workgroup 0 writes it to the device pool
+  ksg_pod* wpods;                    // null: nothing staged
+  int32_t* wprog;
+  const int32_t* sprog;              // the staged words
+  int64_t slen;
+  // ---- evaluation ----
   DevCluster c;
   DevState st;
-  const ksg_pod* pods;
-  const int32_t* prog;
-  const ksg_profile* prof;
-  int32_t pod;
-  int32_t blob, blob_len;            // the pod's program blob (host copy of pods[pod].blob / blob_len)
   int32_t n_rows, n_normrows;        // score rows (the normalising ones first)
   int32_t rows[KSG_NPLUGINS];
   int32_t es;                        // bytes per row value: 2, 4 or 8 (host range-checked)
@@ -70,12 +84,6 @@ struct CycArgs {
   unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
   unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
   unsigned long long* stamps;        // KSG_STAMPS builds: per-segment cycle sums of workgroup 0
-  // a staged append of this pod (ksg_capture_eval's spod fields)
-  const ksg_pod* spod;
-  const int32_t* sprog;
-  int64_t sbase, slen;
-  ksg_pod* wpods;
-  int32_t* wprog;
 };
 
 // Stores into the host block.  SYS: system-scope relaxed stores (global_store
@@ -151,10 +159,9 @@ __device__ __forceinline__ bool cyc_exchange(const CycArgs& a, int G) {
 template <int BLOCK, bool SYS>
 __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
   constexpr int NW = BLOCK / 64;
-  constexpr int PW = (int)(sizeof(ksg_pod) / 4), FW = (int)(sizeof(ksg_profile) / 4);
+  constexpr int PW = (int)(sizeof(ksg_pod) / 4);
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
-  __shared__ ksg_profile s_prof;
   __shared__ int32_t s_st[4][NW];
   __shared__ unsigned long long s_key[NW];
   __shared__ uint32_t s_err[NW];
@@ -167,45 +174,60 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
 #ifdef KSG_STAMPS
   unsigned long long y_acc[10] = {}, y_last = __builtin_amdgcn_s_memtime();
 #endif
-  // Every load of the prologue is issued before the first wait: the profile,
-  // the pod record and its program blob (offset and length come with the
-  // launch, so the blob loads do not wait for the record) and this lane's
-  // node columns, so the chain costs one memory latency instead of three.
-  const int32_t* gprog = a.spod ? a.sprog - a.sbase : a.prog;
-  const int32_t* prec = a.spod ? reinterpret_cast<const int32_t*>(a.spod)
-                               : reinterpret_cast<const int32_t*>(a.pods + a.pod);
-  const int32_t fw = tid < FW ? reinterpret_cast<const int32_t*>(a.prof)[tid] : 0;
+  // Every load of the prologue is issued before the first wait: the pod
+  // record and its program blob (offset and length come with the launch, so
+  // the blob loads do not wait for the record) and this lane's node columns,
+  // so the chain costs one memory latency.  The sources are host-resolved
+  // pointers (no branch on the arguments: their scalar loads go out together).
+  // The profile is read through the constant address space: every plugin
+  // loop over it is a wave-uniform scalar load, not an LDS round trip per step.
+  const ksg_profile& prof = *(const ksg_profile*)(const __attribute__((address_space(4))) ksg_profile*)a.prof;
+  const int32_t* prec = a.psrc;
+  const int32_t* bsrc = a.bsrc;
   const int32_t pw = tid < PW ? prec[tid] : 0;
   constexpr int BI = (KSG_BLOB_MAX + BLOCK - 1) / BLOCK;
   int32_t bw[BI];
 #pragma unroll
   for (int u = 0; u < BI; u++) {
     const int i = tid + u * BLOCK;
-    bw[u] = i < a.blob_len ? gprog[a.blob + i] : 0;
+    bw[u] = i < a.blob_len ? bsrc[i] : 0;
   }
   const int n = blockIdx.x * BLOCK + tid;
   const bool own = n < N;
   NodeCols L;
   if (own) load_cols(c, a.st.requested, a.st.nonzero, a.st.pod_count, n, L);
-  if (tid < FW) reinterpret_cast<int32_t*>(&s_prof)[tid] = fw;
   if (tid < PW) reinterpret_cast<int32_t*>(&s_pod)[tid] = pw;
 #pragma unroll
   for (int u = 0; u < BI; u++) {
     const int i = tid + u * BLOCK;
     if (i < a.blob_len) s_blob[i] = bw[u];
   }
-  if (a.spod && blockIdx.x == 0) {   // the staged append: workgroup 0 copies it to the device
+  if (a.wpods && blockIdx.x == 0) {   // the staged append: workgroup 0 copies it to the device
     if (tid < PW) reinterpret_cast<int32_t*>(a.wpods)[tid] = pw;
     for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
   }
+  if (own && n == a.cm_node) {   // the deferred assume: NodeInfo.AddPod on the lane's own node
+#pragma unroll
+    for (int r = 0; r < KSG_MAX_RES; r++)
+      if (r < c.R) {
+        L.req[r] += a.cm_req[r];
+        a.st.requested[(size_t)r * NN + n] = L.req[r];
+      }
+    L.nz_cpu += a.cm_nz_cpu;
+    L.nz_mem += a.cm_nz_mem;
+    L.pod_count += 1;
+    a.st.nonzero[n] = L.nz_cpu;
+    a.st.nonzero[NN + n] = L.nz_mem;
+    a.st.pod_count[n] = L.pod_count;
+  }
   lds_barrier();   // LDS only: the node-column loads stay in flight
   KSG_YSTAMP(0);
-  const PodView v = make_view(c, s_prof, s_pod, s_blob, gprog, false, a.st.ports);
+  const PodView v = make_view(c, prof, s_pod, s_blob, a.gprog, false, a.st.ports);
 
   // ---- phase 1: this workgroup's nodes ------------------------------------------------
   NodeEval e{KSG_FS_NOT_EVALUATED, 0, 0, 0, 0};
   int64_t lraw[KSG_NPLUGINS] = {};
-  if (own) e = eval_node_src(c, s_prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw);
+  if (own) e = eval_node_src(c, prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw);
   KSG_YSTAMP(1);
   const bool ok = own && e.st == 0;
   // the row value of score row q (node-local plugins only on this path)

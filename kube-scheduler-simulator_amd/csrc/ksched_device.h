@@ -180,6 +180,7 @@ struct GNode {
     return true;
   }
   __device__ __forceinline__ uint32_t taint(int s) const { return c->taints[(size_t)s * c->N + n]; }
+  __device__ __forceinline__ uint8_t effect(uint32_t vid) const { return c->taint_effect[vid]; }
   __device__ __forceinline__ uint32_t image(int s) const { return c->images[(size_t)s * c->N + n]; }
   __device__ __forceinline__ bool unsched() const { return c->unsched[n] != 0; }
 };
@@ -253,7 +254,7 @@ __device__ __forceinline__ int untolerated_slot(const DevCluster& c, const Src& 
     const uint32_t id = nd.taint(s);
     if (!id) break;
     const uint32_t vid = id - 1;
-    const uint8_t e = c.taint_effect[vid];
+    const uint8_t e = nd.effect(vid);
     if (e != KSG_EFFECT_NO_SCHEDULE && e != KSG_EFFECT_NO_EXECUTE) continue;
     if (!tol_bit(tolf, vid)) return s;
   }
@@ -267,7 +268,7 @@ __device__ __forceinline__ int64_t taint_score(const DevCluster& c, const Src& n
     const uint32_t id = nd.taint(s);
     if (!id) break;
     const uint32_t vid = id - 1;
-    if (c.taint_effect[vid] != KSG_EFFECT_PREFER_NO_SCHEDULE) continue;
+    if (nd.effect(vid) != KSG_EFFECT_PREFER_NO_SCHEDULE) continue;
     k += !tol_bit(tolp, vid);
   }
   return k;

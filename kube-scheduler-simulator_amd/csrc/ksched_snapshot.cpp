@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <emmintrin.h>   // SSE2 (x86-64 baseline): ksg_snapshot_statuses
 #include <iterator>
 #include <map>
 #include <optional>
@@ -478,6 +479,13 @@ struct ksg_snapshot {
   std::vector<Node> nodes;
   std::map<std::string, int> node_index;
   std::vector<Pod> pods;
+  // pods the caller expects to add later (pending in the scheduling queue):
+  // their selectors, term templates, label keys, scalar resources and host
+  // ports join the encoding universe now, so adding them later appends in
+  // place instead of re-encoding (ksg_snapshot_hint_pod).  No program, no
+  // binding: they are not pods of the workload.
+  std::vector<Pod> hints;
+  bool hints_new = false;           // hints added since the last full encode
   std::vector<std::pair<int32_t, int32_t>> binds;   // (pod, node) in order: bound, then assumed
   Encoded e;
   bool encoded = false;     // e reflects nodes and pods [0, n_encoded)
@@ -513,7 +521,8 @@ int fail(ksg_snapshot* s, int code, const std::string& m) {
 }
 
 // PodTopologySpread constraints of a pod (encoder._pts_constraints)
-std::pair<std::vector<Constraint>, std::vector<Constraint>> pts_constraints(const Pod& p, const Profile& prof) {
+using PtsPair = std::pair<std::vector<Constraint>, std::vector<Constraint>>;   // (hard, soft)
+PtsPair pts_constraints(const Pod& p, const Profile& prof) {
   std::vector<Constraint> hard, soft;
   if (!p.spread.empty()) {
     for (auto& c : p.spread) {
@@ -619,6 +628,9 @@ void build_resources(ksg_snapshot* s) {
     for (auto& kv : s->req_cache.back().first)
       if (is_scalar(kv.first)) scal.insert(kv.first);
   }
+  for (auto& h : s->hints)
+    for (auto& kv : pod_requests(h, false))
+      if (is_scalar(kv.first)) scal.insert(kv.first);
   for (auto& r : s->prof.fit_res)
     if (is_scalar(r.first)) scal.insert(r.first);
   for (auto& r : s->prof.ba_res)
@@ -636,7 +648,7 @@ void build_label_columns(ksg_snapshot* s) {
   std::set<std::string> keys;
   bool name_field = false;
   s->pts_cache.clear();
-  for (auto& p : s->pods) {
+  auto pod_keys = [&](const Pod& p, const PtsPair& pts) {
     if (p.has_node_selector)
       for (auto& kv : p.node_selector) keys.insert(kv.first);
     if (p.has_na_req)
@@ -649,12 +661,16 @@ void build_label_columns(ksg_snapshot* s) {
         for (auto& r : pt.pref.expr) keys.insert(r.key);
         name_field |= !pt.pref.fields.empty();
       }
-    s->pts_cache.push_back(pts_constraints(p, s->prof));
-    for (auto& c : s->pts_cache.back().first) keys.insert(c.key);
-    for (auto& c : s->pts_cache.back().second) keys.insert(c.key);
+    for (auto& c : pts.first) keys.insert(c.key);
+    for (auto& c : pts.second) keys.insert(c.key);
     for (auto* v : {&p.aff_req, &p.anti_req, &p.aff_pref, &p.anti_pref})
       for (auto& t : *v) keys.insert(t.key);
+  };
+  for (auto& p : s->pods) {
+    s->pts_cache.push_back(pts_constraints(p, s->prof));
+    pod_keys(p, s->pts_cache.back());
   }
+  for (auto& h : s->hints) pod_keys(h, pts_constraints(h, s->prof));
   e.label_cols.assign(keys.begin(), keys.end());
   if (name_field) e.label_cols.push_back(kObjectName);
   e.col_index.clear();
@@ -726,8 +742,9 @@ void build_taints(ksg_snapshot* s) {
 void build_ports(ksg_snapshot* s) {
   Encoded& e = s->e;
   std::set<HostPort> all;
-  for (auto& p : s->pods)
-    for (auto& hp : pod_host_ports(p)) all.insert(hp);
+  for (auto* lst : {&s->pods, &s->hints})
+    for (auto& p : *lst)
+      for (auto& hp : pod_host_ports(p)) all.insert(hp);
   e.port_vocab.assign(all.begin(), all.end());
   for (size_t v = 0; v < e.port_vocab.size(); v++) e.port_id[e.port_vocab[v]] = (int)v;
 }
@@ -816,9 +833,11 @@ void build_topology_universe(ksg_snapshot* s) {
   e.templates.clear();
   e.tmpl_order.clear();
   s->owned_templates.assign(P, {});
-  for (size_t i = 0; i < P; i++) {
-    const Pod& p = s->pods[i];
-    auto& hs = s->pts_cache[i];
+  for (size_t i = 0; i < P + s->hints.size(); i++) {
+    const bool hint = i >= P;
+    const Pod& p = hint ? s->hints[i - P] : s->pods[i];
+    const PtsPair hint_pts = hint ? pts_constraints(p, s->prof) : PtsPair{};
+    const auto& hs = hint ? hint_pts : s->pts_cache[i];
     for (auto* lst : {&hs.first, &hs.second})
       for (auto& c : *lst)
         if (c.canon && !c.canon->empty()) {
@@ -853,7 +872,7 @@ void build_topology_universe(ksg_snapshot* s) {
       } else {
         tid = it->second;
       }
-      s->owned_templates[i].emplace_back(tid, wt);
+      if (!hint) s->owned_templates[i].emplace_back(tid, wt);
     };
     for (auto& t : p.anti_req) own(TMPL_REQ_ANTI, t, 1);
     for (auto& t : p.aff_req) own(TMPL_REQ_AFF, t, 1);
@@ -1331,6 +1350,7 @@ void encode_all(ksg_snapshot* s) {
   finish_arrays(s);
   s->encoded = true;
   s->n_encoded = (int)P;
+  s->hints_new = false;
   s->epoch++;
 }
 
@@ -1526,7 +1546,7 @@ void fill_views(ksg_snapshot* s, ksg_nodes* nd, ksg_topology* tp, ksg_workload* 
 // otherwise (*appended = 0).
 int encode_incremental(ksg_snapshot* s, int32_t* appended) {
   if (appended) *appended = 0;
-  if (!s->encoded) return do_encode(s);
+  if (!s->encoded || s->hints_new) return do_encode(s);   // hints extend the universe: once per batch
   const int P = (int)s->pods.size();
   if (s->n_encoded == P) {
     if (appended) *appended = 1;
@@ -1575,8 +1595,15 @@ int upload_all(ksg_snapshot* s, ksg_ctx* ctx) {
   if ((rc = ksg_set_profile(ctx, &pf))) return dev(rc, "ksg_set_profile");
   if ((rc = ksg_load_nodes(ctx, &nd, &tp))) return dev(rc, "ksg_load_nodes");
   if ((rc = ksg_load_workload(ctx, &wl))) return dev(rc, "ksg_load_workload");
-  for (auto& b : s->binds)
-    if ((rc = ksg_commit(ctx, b.first, b.second))) return dev(rc, "ksg_commit (replayed binding)");
+  if (!s->binds.empty()) {   // the bindings replayed in one launch
+    std::vector<int32_t> bp, bn;
+    for (auto& b : s->binds) {
+      bp.push_back(b.first);
+      bn.push_back(b.second);
+    }
+    if ((rc = ksg_commit_batch(ctx, bp.data(), bn.data(), (int32_t)bp.size())))
+      return dev(rc, "ksg_commit_batch (replayed bindings)");
+  }
   s->loaded_ctx = ctx;
   s->loaded_epoch = s->epoch;
   s->n_loaded = s->n_encoded;
@@ -1837,6 +1864,7 @@ int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labe
   bool changed = false;
   try {
     for (auto& p : s->pods) changed = resolve_namespaces(s, p) || changed;
+    for (auto& h : s->hints) changed = resolve_namespaces(s, h) || changed;
   } catch (const EncodeError& x) {
     return fail(s, x.code, x.msg);
   }
@@ -1844,9 +1872,10 @@ int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labe
   return KSG_OK;
 }
 
-int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index) {
-  if (!s || !v || !v->name) return KSG_E_INVALID;
-  Pod p;
+namespace {
+// A pod view into the snapshot's Pod, validated (ksg_snapshot_add_pod /
+// ksg_snapshot_hint_pod).  Returns 0 or the failing code (message set).
+int pod_from_view(ksg_snapshot* s, const ksg_pod_view* v, Pod& p) {
   p.ns = v->namespace_ ? S(v->namespace_) : "default";
   p.name = S(v->name);
   p.labels = copy_pairs(v->n_labels, v->labels);
@@ -1912,11 +1941,32 @@ int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index)
   } catch (const EncodeError& x) {
     return fail(s, x.code, "pod " + p.ns + "/" + p.name + ": " + x.msg);
   }
+  return KSG_OK;
+}
+}  // namespace
+
+int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index) {
+  if (!s || !v || !v->name) return KSG_E_INVALID;
+  Pod p;
+  const int rc = pod_from_view(s, v, p);
+  if (rc) return rc;
   for (auto& kv : pod_requests(p, false))
     if (is_scalar(kv.first)) s->scalars.insert(kv.first);
   const int32_t idx = (int32_t)s->pods.size();
   s->pods.push_back(std::move(p));
   if (index) *index = idx;
+  return KSG_OK;
+}
+
+int ksg_snapshot_hint_pod(ksg_snapshot* s, const ksg_pod_view* v) {
+  if (!s || !v || !v->name) return KSG_E_INVALID;
+  Pod p;
+  const int rc = pod_from_view(s, v, p);
+  if (rc) return rc;
+  for (auto& kv : pod_requests(p, false))
+    if (is_scalar(kv.first)) s->scalars.insert(kv.first);
+  s->hints.push_back(std::move(p));
+  s->hints_new = true;
   return KSG_OK;
 }
 
@@ -2043,22 +2093,35 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
   const ksg_pod& p = e.pods[pod];
   uint64_t last_key = ~0ull;
   int32_t last_idx = -1;
+  // a direct-mapped cache in front of the map: the distinct keys of one pod
+  // are few (a plugin, a reason set, a taint), the rejected nodes many
+  constexpr int kDm = 256;
+  uint64_t dm_key[kDm];
+  int32_t dm_idx[kDm];
+  for (int i = 0; i < kDm; i++) dm_key[i] = ~0ull;
   std::string err;
-  // Most nodes pass: the passed defaults are written in straight vector loops
-  // over blocks of 64 nodes, whose rejected nodes (a 64-bit mask) are then
-  // decoded one by one.
+  // Most nodes pass: the passed defaults are filled first, then each block of
+  // 64 nodes yields its rejected nodes as a 64-bit mask (SSE2 compares), which
+  // are decoded one by one.
+  std::fill(code, code + n_nodes, (int32_t)KSG_CODE_SUCCESS);
+  std::fill(msg, msg + n_nodes, (int32_t)-1);
   constexpr int32_t kB = 64;
+  const __m128i v_pass = _mm_setzero_si128(), v_ne = _mm_set1_epi32((int)KSG_FS_NOT_EVALUATED);
   for (int32_t b = 0; b < n_nodes; b += kB) {
     const int32_t m = std::min(kB, n_nodes - b);
-    uint8_t rj[kB];
-    for (int32_t i = 0; i < m; i++) {
-      const uint32_t w = words[b + i];
-      rj[i] = (uint8_t)(w != 0 && w != KSG_FS_NOT_EVALUATED);
+    uint64_t mask = 0;   // the block's rejected nodes: four words per compare
+    if (m == kB) {
+      for (int32_t i = 0; i < kB; i += 4) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(words + b + i));
+        const __m128i ok = _mm_or_si128(_mm_cmpeq_epi32(v, v_pass), _mm_cmpeq_epi32(v, v_ne));
+        mask |= (uint64_t)(~_mm_movemask_ps(_mm_castsi128_ps(ok)) & 0xf) << i;
+      }
+    } else {
+      for (int32_t i = 0; i < m; i++) {
+        const uint32_t w = words[b + i];
+        mask |= (uint64_t)(w != 0 && w != KSG_FS_NOT_EVALUATED) << i;
+      }
     }
-    for (int32_t i = 0; i < m; i++) code[b + i] = KSG_CODE_SUCCESS;
-    for (int32_t i = 0; i < m; i++) msg[b + i] = -1;
-    uint64_t mask = 0;
-    for (int32_t i = 0; i < m; i++) mask |= (uint64_t)rj[i] << i;
     for (; mask; mask &= mask - 1) {
     const int32_t n = b + __builtin_ctzll(mask);
     const uint32_t w = words[n];
@@ -2067,8 +2130,13 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     if (pl == KSG_PL_TAINT_TOLERATION && (int)(w >> 8) < e.max_taints)
       key |= (uint64_t)e.taints[(size_t)(w >> 8) * e.N + n] << 32;
     int32_t idx;
+    const int slot = (int)((key * 0x9E3779B97F4A7C15ull) >> 56);
     if (key == last_key) {
       idx = last_idx;
+    } else if (dm_key[slot] == key) {
+      idx = dm_idx[slot];
+      last_key = key;
+      last_idx = idx;
     } else {
       auto it = seen.find(key);
       if (it == seen.end()) {
@@ -2080,6 +2148,8 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
         codes.push_back(c);
       }
       idx = it->second;
+      dm_key[slot] = key;
+      dm_idx[slot] = idx;
       last_key = key;
       last_idx = idx;
     }

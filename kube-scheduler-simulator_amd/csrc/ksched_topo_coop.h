@@ -292,23 +292,28 @@ __device__ __forceinline__ void coop_commit(const DevCluster& c, const DevState&
 
 // Workgroup 0 applies a pending assume to the tables (dom, tot, cc) and, when
 // they were lagged, to the template tables.  Called between the barrier after
-// every reader of the tables of this pod and the next barrier.
+// every reader of the tables of this pod and the next barrier.  Every update
+// is an independent no-return atomic: wave 0 lane i takes selector i's
+// (column, table) pairs, wave 1 the template entries, wave 2 tot and cc.
 __device__ __forceinline__ void lag_apply(const DevCluster& cg, const DevState& st, const TopoTables& t,
                                           const LagDelta& d, bool tables, bool tab) {
   const int tid = threadIdx.x, N = cg.N;
   if (d.node < 0) return;
-  if (tables && tid < d.n_sel) {   // lane i: selector i
+  if (tables && tid < d.n_sel) {   // wave 0: the domain tables of selector tid
     const int s = d.sel[tid];
-    gadd(t.tot + s, 1);
-    for (int col = 0; col < t.L; col++) {
-      const int off = t.pair_off[(size_t)s * t.L + col];
-      if (off < 0) continue;
+    const int b = t.sp_off[s], e = t.sp_off[s + 1];
+    for (int k = b; k < e; k++) {
+      const int col = t.sp[2 * k], off = t.sp[2 * k + 1];
       const uint32_t v = cg.label_val[(size_t)col * N + d.node];
       if (v) gadd(t.dom + off + v, 1);
     }
+  }
+  if (tables && tid >= 128 && tid < 128 + d.n_sel) {   // wave 2: totals and count-of-counts
+    const int i = tid - 128, s = d.sel[i];
+    gadd(t.tot + s, 1);
     const int co = t.cc_off[s];
     if (co >= 0) {
-      const int k = d.old_cnt[tid];
+      const int k = d.old_cnt[i];
       if (k + 1 >= t.Kc - 1) {
         __hip_atomic_store((__attribute__((address_space(1))) unsigned*)t.invalid, 1u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -374,6 +379,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ int s_nlsel;           // ... and their number (may exceed kLagSel)
   __shared__ int s_wmin;            // this workgroup's lowest feasible node (phase 2)
   __shared__ unsigned long long s_wbest;   // this workgroup's best key (phase 3)
+  __shared__ uint8_t s_elig[kCoopBatch];    // tables_scope of the batch's pods
+  __shared__ int s_inv;                     // the tables were invalidated (read per pod)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
@@ -392,6 +399,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profile)[tid];
   for (int i = tid; i < a.count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
+  for (int i = tid; i < a.count; i += BLOCK) s_elig[i] = a.use_tables ? tt.elig[a.first - tt.first + i] : 0;
   const bool lab_lds = LL || (KN == 1 && cg.L <= kCoopLabCols);
   const bool col_lds = LL || cg.L <= kCoopLabCols;
   const bool tmpl_lds = LL || cg.n_tmpl <= kCoopTmpl;
@@ -511,6 +519,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     __syncthreads();
     if (tid < (int)(sizeof(ksg_pod) / 4))
       reinterpret_cast<int32_t*>(&s_pod)[tid] = reinterpret_cast<const int32_t*>(&s_pods[kq])[tid];
+    if (tid == BLOCK - 1) s_inv = s_tables_ok ? gld(tt.invalid) != 0 : 1;   // read beside the pod's staging
     if (kq == 0 || nb_len > kCoopPrefetch * BLOCK) {
       const int boff = s_pods[kq].blob, blen = s_pods[kq].blob_len;
       for (int i = tid; i < blen; i += BLOCK) s_blob[i] = a.prog[boff + i];
@@ -532,37 +541,11 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         s_nlsel = cw[0];
         for (int i = 0; i < kLagSel && i < cw[0]; i++) s_lsel[i] = cw[1 + i];
       }
-      // Tables scope: every constraint counts over every node (default
-      // inclusion, every node has the key), and each histogram has its table.
+      // Tables scope (tables_scope, one flag per pod computed at the run's
+      // start), the tables exact (no count-of-counts overflow in the previous
+      // pod's lag_apply: s_inv) and the histograms within their limits.
       const TopoProg& g0 = s_g;
-      // (a count-of-counts overflow in the previous pod's lag_apply sets invalid)
-      bool e = s_tables_ok != 0 && s_t.ok && !gld(tt.invalid);
-      auto pair = [&](int sel, int col) { return sel >= 0 ? tt.pair_off[(size_t)sel * tt.L + col] : -1; };
-      auto all = [&](int col) { return tt.col_missing[col] == 0; };
-      for (int i = 0; e && i < g0.n_hard; i++) {
-        const int32_t* h = g0.hard + 7 * i;
-        e = all(h[0]) && (!h[5] || p.na_req < 0) && !h[6] &&
-            (c.col_unique[h[0]] ? h[1] >= 0 && tt.cc_off[h[1]] >= 0 : pair(h[1], h[0]) >= 0 && tt.pres_off[h[0]] >= 0);
-      }
-      for (int i = 0; e && i < g0.n_soft; i++) {
-        const int32_t* sc = g0.soft + 6 * i;
-        e = all(sc[0]) && (!sc[3] || p.na_req < 0) && !sc[4] &&
-            (sc[5] || (c.col_unique[sc[0]] ? tt.col_empty[sc[0]] == 0 : pair(sc[1], sc[0]) >= 0));
-      }
-      if (g0.ipa) {
-        for (int i = 0; e && i < g0.n_aff; i++) {
-          const int col = g0.aff_cols[i];
-          e = c.col_unique[col] ? all(col) : pair(g0.sel_all, col) >= 0 && tt.pres_off[col] >= 0;
-        }
-        for (int i = 0; e && i < g0.n_anti; i++) {
-          const int col = g0.anti[2 * i];
-          e = c.col_unique[col] || (pair(g0.anti[2 * i + 1], col) >= 0 && tt.pres_off[col] >= 0);
-        }
-        for (int i = 0; e && i < g0.n_pref; i++) {
-          const int col = g0.pref[3 * i];
-          e = c.col_unique[col] ? all(col) : pair(g0.pref[3 * i + 1], col) >= 0 && tt.pres_off[col] >= 0;
-        }
-      }
+      const bool e = s_tables_ok != 0 && s_t.ok && s_elig[kq] && !s_inv;
       const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
       s_skip = !s_prev_imm && (!has_pre || e);
       for (int i = 0; i < kMaxHard; i++) { s_t.hard_min[i] = BIG; s_t.hard_dom[i] = 0; }
@@ -1380,37 +1363,37 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     __syncthreads();   // every wave is past this pod's reads of s_lag (applied by workgroup 0 in phase 3)
-    if (tid == 0) {   // this pod's assume becomes the pending lag, in every workgroup alike
+    {   // this pod's assume becomes the pending lag, in every workgroup alike
+        // (lanes 0 .. n_sel - 1: the selectors' old counts; wave 1: the templates)
       LagDelta& d = s_lag;
-      d.node = a.commit && selected >= 0 ? selected : -1;
-      d.n_sel = d.n_tmpl = 0;
-      s_lag_tab = 0;
-      s_prev_imm = 0;
-      if (d.node >= 0 && cprog) {
-        if (s_nlsel > kLagSel) {   // more matched selectors than the lag holds: the tables go unused
-          s_tables_ok = 0;
-          if (wg == 0) gst(tt.invalid, 1u);
-        }
-        d.n_sel = min(s_nlsel, kLagSel);
+      const int node = a.commit && selected >= 0 ? selected : -1;
+      const bool any = node >= 0 && cprog;
+      const int n_sel = any ? min(s_nlsel, kLagSel) : 0;
+      const int n_tm = any && !tab_now ? n_own_tmpl : 0;
+      if (tid < n_sel) {
         const int owner = (selected / BLOCK) % G;
         const int32_t* cnts = scored ? a.parts[owner].best_cnt : a.parts[owner].min_cnt;
-        for (int i = 0; i < d.n_sel; i++) {
-          d.sel[i] = s_lsel[i];
-          d.old_cnt[i] = gld(cnts + i);
-        }
-        if (tab_now) {
-          s_prev_imm = 1;   // written at once by the owner lane: the next pod runs barrier 1
-        } else {
-          const int32_t* w = cprog + 2 + cprog[0];
-          d.n_tmpl = n_own_tmpl;
-          for (int i = 0; i < n_own_tmpl; i++) {
-            const int t = w[2 * i];
-            const uint32_t val = cg.label_val[(size_t)cg.tmpl_col[t] * N + selected];
-            d.tidx[i] = val ? cg.tmpl_off[t] + (int)val : -1;
-            d.tw[i] = cg.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1;
-            d.tt[i] = t;
-          }
-          s_lag_tab = 1;
+        d.sel[tid] = s_lsel[tid];
+        d.old_cnt[tid] = gld(cnts + tid);
+      }
+      if (tid >= 64 && tid < 64 + n_tm) {
+        const int i = tid - 64;
+        const int32_t* w = cprog + 2 + cprog[0];
+        const int t = w[2 * i];
+        const uint32_t val = cg.label_val[(size_t)cg.tmpl_col[t] * N + selected];
+        d.tidx[i] = val ? cg.tmpl_off[t] + (int)val : -1;
+        d.tw[i] = cg.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1;
+        d.tt[i] = t;
+      }
+      if (tid == 0) {
+        d.node = node;
+        d.n_sel = n_sel;
+        d.n_tmpl = n_tm;
+        s_lag_tab = n_tm > 0 || (any && !tab_now) ? 1 : 0;
+        s_prev_imm = any && tab_now ? 1 : 0;   // written at once by the owner lane: the next pod runs barrier 1
+        if (any && s_nlsel > kLagSel) {   // more matched selectors than the lag holds: the tables go unused
+          s_tables_ok = 0;
+          if (wg == 0) gst(tt.invalid, 1u);
         }
       }
     }

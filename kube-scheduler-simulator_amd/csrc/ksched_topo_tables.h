@@ -35,8 +35,70 @@ struct TopoTables {
   int32_t* col_missing;        // [L]: 0 iff every node has label column c
   int32_t* col_empty;          // [L]: some node has the value "" (id 1)
   unsigned* invalid;           // set when a count or an assume did not fit: the tables go unused
+  const int32_t* sp_off;       // [S + 1]: selector s's (column, dom offset) pairs are sp[2 * sp_off[s] ..]
+  const int32_t* sp;
+  const uint8_t* elig;         // [pods of the run]: the pod's constraints are all within the tables' scope
+  int32_t first;               // the run's first pod (elig index 0)
   int32_t S, L, Kc;
 };
+
+// Whether every topology constraint of pod p counts over every node and has
+// its table (the scope in which a pod reads the tables instead of running the
+// pre-pass): default inclusion policies, every node carries the key (no node
+// has "" for a unique soft key), each non-unique key's (selector, column)
+// table and presence bitmap, each unique hard key's count-of-counts.  P: the
+// program pool (absolute offsets).  Same program layout as parse_topo.
+__device__ __forceinline__ bool tables_scope(const DevCluster& c, const TopoTables& tt, const ksg_pod& p,
+                                             const int32_t* P) {
+  auto pair = [&](int sel, int col) { return sel >= 0 ? tt.pair_off[(size_t)sel * tt.L + col] : -1; };
+  auto all = [&](int col) { return tt.col_missing[col] == 0; };
+  bool e = true;
+  if (p.pts >= 0) {
+    const int32_t* w = P + p.pts;
+    const int nh = w[0], ns = w[1];
+    const int32_t* hard = w + 3;
+    for (int i = 0; e && i < nh; i++) {
+      const int32_t* h = hard + 7 * i;
+      e = all(h[0]) && (!h[5] || p.na_req < 0) && !h[6] &&
+          (c.col_unique[h[0]] ? h[1] >= 0 && tt.cc_off[h[1]] >= 0 : pair(h[1], h[0]) >= 0 && tt.pres_off[h[0]] >= 0);
+    }
+    const int32_t* soft = hard + 7 * nh;
+    for (int i = 0; e && i < ns; i++) {
+      const int32_t* sc = soft + 6 * i;
+      e = all(sc[0]) && (!sc[3] || p.na_req < 0) && !sc[4] &&
+          (sc[5] || (c.col_unique[sc[0]] ? tt.col_empty[sc[0]] == 0 : pair(sc[1], sc[0]) >= 0));
+    }
+  }
+  if (p.ipa >= 0) {
+    const int32_t* w = P + p.ipa;
+    const int na = w[0], sel_all = w[1];
+    for (int i = 0; e && i < na; i++) {
+      const int col = w[3 + i];
+      e = c.col_unique[col] ? all(col) : pair(sel_all, col) >= 0 && tt.pres_off[col] >= 0;
+    }
+    w += 3 + na;
+    const int nanti = *w++;
+    for (int i = 0; e && i < nanti; i++) {
+      const int col = w[2 * i];
+      e = c.col_unique[col] || (pair(w[2 * i + 1], col) >= 0 && tt.pres_off[col] >= 0);
+    }
+    w += 2 * nanti;
+    const int npref = *w++;
+    for (int i = 0; e && i < npref; i++) {
+      const int col = w[3 * i];
+      e = c.col_unique[col] ? all(col) : pair(w[3 * i + 1], col) >= 0 && tt.pres_off[col] >= 0;
+    }
+  }
+  return e;
+}
+
+// One lane per pod of the run: tables_scope into elig (after ksg_topo_tables_init).
+__global__ __launch_bounds__(64) void ksg_topo_tables_elig(DevCluster c, TopoTables t, const ksg_pod* pods,
+                                                           const int32_t* prog, int count, uint8_t* elig) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= count) return;
+  elig[i] = tables_scope(c, t, pods[t.first + i], prog) ? 1 : 0;
+}
 
 // One table-building task per workgroup (ksg_topo_tables_init).
 struct TopoTableTask {

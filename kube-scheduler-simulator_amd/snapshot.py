@@ -307,6 +307,7 @@ class Snapshot:
         self._add_node = f("add_node", C.c_int, vp, C.POINTER(NodeView), C.POINTER(i32))
         self._add_pod = f("add_pod", C.c_int, vp, C.POINTER(PodView), C.POINTER(i32))
         self._add_ns = f("add_namespace", C.c_int, vp, cp, i32, C.POINTER(StrPair))
+        self._hint_pod = f("hint_pod", C.c_int, vp, C.POINTER(PodView))
         self._bind_ = f("bind", C.c_int, vp, i32, i32)
         self._encode = f("encode", C.c_int, vp)
         self._encode_inc = f("encode_incremental", C.c_int, vp, C.POINTER(i32))
@@ -380,6 +381,12 @@ class Snapshot:
         self._check(self._add_pod(self.h, C.byref(view), C.byref(idx)), "add_pod")
         self.n_pods = idx.value + 1
         return idx.value
+
+    def hint_pod(self, p: m.Pod) -> None:
+        """ksg_snapshot_hint_pod: a pending pod's selectors / templates join the
+        encoding universe now, so its later add_pod appends in place."""
+        k = _Keep()
+        self._check(self._hint_pod(self.h, C.byref(pod_view(p, k))), "hint_pod")
 
     def bind(self, pod: int, node: int):
         self._check(self._bind_(self.h, pod, node), "bind")

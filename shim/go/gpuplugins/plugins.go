@@ -92,6 +92,7 @@ type Evaluator struct {
 	podIdx  map[types.UID]int // pod -> snapshot index
 	podRV   map[types.UID]string
 	podNode map[types.UID]int // pods bound / assumed on the device -> column
+	hinted  map[types.UID]struct{} // pending pods announced to this snapshot (hintPending)
 	// snapshot pods no longer current (a pod re-encoded after an update, a
 	// pod that left its node, a pending pod deleted): the snapshot only
 	// appends, so once they outnumber the live pods (podIdx) past a threshold
@@ -102,6 +103,7 @@ type Evaluator struct {
 	side      sync.Mutex
 	nominated map[string]struct{} // nodes that may hold nominated pods
 	gone      []types.UID         // pods deleted since the last sync
+	pending   []*v1.Pod           // pending pods created since the last sync (hinted to the snapshot)
 	nsDirty   bool                // a namespace was added or its labels changed
 	attached  sync.Once
 	nsList    func() ([]*v1.Namespace, error) // the handle's namespace lister, nil before attach
@@ -165,8 +167,44 @@ func (e *Evaluator) markNamespaces() {
 }
 
 func (e *Evaluator) notePod(o interface{}) {
-	if p, ok := o.(*v1.Pod); ok && p.Status.NominatedNodeName != "" {
+	p, ok := o.(*v1.Pod)
+	if !ok {
+		return
+	}
+	if p.Status.NominatedNodeName != "" {
 		e.noteNominated(p.Status.NominatedNodeName)
+	}
+	if p.Spec.NodeName == "" && p.DeletionTimestamp == nil {
+		e.side.Lock()
+		e.pending = append(e.pending, p)
+		e.side.Unlock()
+	}
+}
+
+// hintPending (under mu) announces the pending pods the informer delivered
+// since the last sync to the snapshot (ksg_snapshot_hint_pod): a burst of new
+// workloads costs one re-encode at the next sync instead of one per pod.  A
+// pod the encoder refuses is left to its own cycle, which reports it.
+func (e *Evaluator) hintPending() {
+	e.side.Lock()
+	pend := e.pending
+	e.pending = nil
+	e.side.Unlock()
+	if e.snap == nil {
+		return
+	}
+	if e.hinted == nil {
+		e.hinted = map[types.UID]struct{}{}
+	}
+	for _, p := range pend {
+		if _, known := e.podIdx[p.UID]; known {
+			continue
+		}
+		if _, done := e.hinted[p.UID]; done {
+			continue
+		}
+		e.hinted[p.UID] = struct{}{}
+		_ = e.snap.HintPod(p, e.selectorOf(p))
 	}
 }
 
@@ -248,6 +286,7 @@ func (e *Evaluator) rebuild(infos []*framework.NodeInfo) error {
 	e.nodeRV, e.nodeGen = map[string]string{}, map[string]int64{}
 	e.podIdx, e.podRV, e.podNode = map[types.UID]int{}, map[types.UID]string{}, map[types.UID]int{}
 	e.stale = 0
+	e.hinted = nil // a new snapshot: pending pods are announced again as they arrive
 	for col, ni := range infos {
 		n := ni.Node()
 		if _, err := snap.AddNode(n); err != nil {
@@ -296,6 +335,7 @@ func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
 	if err := e.syncNamespaces(false); err != nil {
 		return err
 	}
+	e.hintPending()
 	for col, ni := range infos {
 		name := e.nodes[col]
 		if ni.Generation == e.nodeGen[name] {

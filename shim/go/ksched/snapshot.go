@@ -450,6 +450,15 @@ func (x *Snapshot) AddPod(p *v1.Pod, defaultSel labels.Selector) (int, error) {
 	return int(idx), err
 }
 
+// HintPod announces a pending pod (ksg_snapshot_hint_pod): its selectors and
+// term templates join the encoding universe at the next Sync, so adding it
+// when its cycle comes appends in place instead of re-encoding.
+func (x *Snapshot) HintPod(p *v1.Pod, defaultSel labels.Selector) error {
+	var a arena
+	defer a.free()
+	return x.check(C.ksg_snapshot_hint_pod(x.s, a.pod(p, defaultSel)))
+}
+
 // AddNamespace registers a namespace and its labels: namespaceSelector
 // terms resolve against the namespaces added so far (re-resolved on change).
 func (x *Snapshot) AddNamespace(ns *v1.Namespace) error {

@@ -191,3 +191,62 @@ def test_eval_view_equals_eval_with_capture(gpu, built):
             np.testing.assert_array_equal(cap.total[0], v["total"])
             if ra.selected >= 0:
                 gpu.commit(i, ra.selected)
+
+
+def _engine_with(env):
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return native.Engine(device=0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def test_deferred_assume_reaches_every_reader(built):
+    """ksg_commit after a per-cycle evaluation is applied by the next
+    per-cycle kernel (or launched first by any other reader of the node
+    state): evaluations, read_state, run_queue, uncommit and reset_state see
+    the same state as with every assume launched at once (KSG_DEFER_COMMIT=0)."""
+    nodes, pods, prof = G.config2(n_nodes=600, n_pods=60, seed=9)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = native.Engine(device=0)
+    b = _engine_with({"KSG_DEFER_COMMIT": "0"})
+    a.load(enc, pf)
+    b.load(enc, pf)
+    R = len(enc.cluster.res_names)
+
+    def same_state():
+        for x, y in zip(a.read_state(R), b.read_state(R)):
+            np.testing.assert_array_equal(x, y)
+
+    for i in range(40):
+        ra, rb = a.eval(i), b.eval(i)
+        assert a.last_run_info()[0] == 5
+        assert (ra.selected, ra.n_feasible, ra.status) == (rb.selected, rb.n_feasible, rb.status), i
+        if ra.selected < 0:
+            continue
+        a.commit(i, ra.selected)
+        b.commit(i, rb.selected)
+        k = i % 6
+        if k == 1:
+            same_state()
+        elif k == 2:   # the queue kernels read the state after the pending assume
+            pa, _ = a.run_queue(50, 2, results=False)
+            pb, _ = b.run_queue(50, 2, results=False)
+            np.testing.assert_array_equal(pa, pb)
+        elif k == 3:   # forget the pod just assumed (pending on a)
+            a.uncommit(i, ra.selected)
+            b.uncommit(i, rb.selected)
+            same_state()
+        elif k == 4:   # two assumes in a row: the first is launched, the second deferred
+            a.commit(i, ra.selected)
+            b.commit(i, rb.selected)
+    same_state()
+    a.reset_state()   # a pending assume is dropped with the rest
+    b.reset_state()
+    same_state()

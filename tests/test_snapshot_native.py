@@ -362,3 +362,46 @@ def test_namespace_selector_resolution(built):
     assert got1["pods"].tobytes() == enc1.workload.pods.tobytes()
     np.testing.assert_array_equal(got1["prog"], enc1.workload.prog)
     assert not np.array_equal(got1["prog"], got["prog"]) or got1["pods"].tobytes() != got["pods"].tobytes()
+
+
+def _oracle_on_views(snap, n_pods):
+    """The C++ oracle loaded straight from the snapshot's encoded views."""
+    import ctypes as C
+    import binding
+    native = pkg("native")
+    nd, tp, wl, pf = native.KsgNodes(), native.KsgTopology(), native.KsgWorkload(), native.KsgProfile()
+    assert snap._view(snap.h, C.byref(nd), C.byref(tp), C.byref(wl), C.byref(pf)) == 0
+    o = binding.Oracle(4)
+    o._check(o._set_profile(o.ctx, C.byref(pf)))
+    o._check(o._load_nodes(o.ctx, C.byref(nd), C.byref(tp)))
+    o._check(o._load_workload(o.ctx, C.byref(wl)))
+    pl, _ = o.run_queue(0, n_pods, results=False)
+    return pl
+
+
+def test_hinted_pods_append_in_place(built):
+    """ksg_snapshot_hint_pod: pending pods announced up front extend the
+    universe once; adding them one by one then appends every pod in place (no
+    re-encode), where the same sequence without hints re-encodes; and the
+    hinted encoding schedules exactly as the Python encoder's (oracle)."""
+    import binding
+    nodes, pods, prof = G.config3(n_nodes=150, n_pods=400, apps=120)
+    snap = S.Snapshot(prof, nodes, pods[:50])
+    for p in pods[50:]:
+        snap.hint_pod(p)
+    snap.encode()
+    for p in pods[50:]:
+        snap.add_pod(p)
+        assert snap.encode_incremental()
+    plain = S.Snapshot(prof, nodes, pods[:50])
+    plain.encode()
+    misses = 0
+    for p in pods[50:]:
+        plain.add_pod(p)
+        misses += not plain.encode_incremental()
+    assert misses > 0
+    enc = E.Encoder(nodes, pods, prof)
+    o = binding.Oracle(4)
+    o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    want, _ = o.run_queue(0, len(pods), results=False)
+    np.testing.assert_array_equal(_oracle_on_views(snap, len(pods)), want)
