@@ -186,10 +186,10 @@ __device__ __forceinline__ int pts_soft1_m(const DevCluster& c, const PodView& v
   const uint32_t val = lab(c, sc[0], n);
   if (!val) return 1;
   const Slot& sl = s.soft[0];
-  if (sc[5]) m = cnt_at(t.cnt, c.N, sl.sel, n);
+  if (sc[5]) m = t.cntv(c.N, sl.sel, n);
   else if (!sl.unique) m = t.hist[sl.hist + val];
   else if (val == 1) m = s.soft_empty[0];
-  else m = inclusion(c, v, t, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
+  else m = inclusion(c, v, t, sc[3], sc[4], n) ? t.cntv(c.N, sl.sel, n) : 0;
   return 0;
 }
 
@@ -381,6 +381,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ unsigned long long s_wbest;   // this workgroup's best key (phase 3)
   __shared__ uint8_t s_elig[kCoopBatch];    // tables_scope of the batch's pods
   __shared__ int s_inv;                     // the tables were invalidated (read per pod)
+  __shared__ int s_csel[kTopoCache], s_ctm[kTopoCache], s_nc, s_nt;   // the TopoCtx cache's keys
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
@@ -548,6 +549,38 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       const bool e = s_tables_ok != 0 && s_t.ok && s_elig[kq] && !s_inv;
       const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
       s_skip = !s_prev_imm && (!has_pre || e);
+      // the selector counts / template entries the evaluators read per node
+      // (TopoCtx cache, KN == 1): unique-key slots' selectors; the templates
+      // only when every template write of the previous pod is lagged (skip)
+      int nc = 0, nt = 0;
+      if (KN == 1 && s_t.ok) {
+        auto addc = [&](int sel) {
+          if (sel < 0) return;
+          for (int k = 0; k < nc; k++)
+            if (s_csel[k] == sel) return;
+          if (nc < kTopoCache) s_csel[nc++] = sel;
+        };
+        for (int i = 0; i < g0.n_hard; i++)
+          if (s_t.hard[i].unique) addc(s_t.hard[i].sel);
+        for (int i = 0; i < g0.n_soft; i++)
+          if (g0.soft[6 * i + 5] || s_t.soft[i].unique) addc(s_t.soft[i].sel);
+        if (g0.ipa) {
+          for (int i = 0; i < g0.n_aff; i++)
+            if (s_t.aff[i].unique) addc(g0.sel_all);
+          for (int i = 0; i < g0.n_anti; i++)
+            if (s_t.anti[i].unique) addc(s_t.anti[i].sel);
+          for (int i = 0; i < g0.n_pref; i++)
+            if (s_t.pref[i].unique) addc(s_t.pref[i].sel);
+          if (s_skip) {
+            for (int i = 0; i < g0.n_ma && nt < kTopoCache; i++) s_ctm[nt++] = g0.m_anti[i];
+            if (prof.hard_pod_affinity_weight > 0)
+              for (int i = 0; i < g0.n_mh && nt < kTopoCache; i++) s_ctm[nt++] = g0.m_hard[i];
+            for (int i = 0; i < g0.n_mp && nt < kTopoCache; i++) s_ctm[nt++] = g0.m_pref[i];
+          }
+        }
+      }
+      s_nc = nc;
+      s_nt = nt;
       for (int i = 0; i < kMaxHard; i++) { s_t.hard_min[i] = BIG; s_t.hard_dom[i] = 0; }
       for (int i = 0; i < kMaxSoft; i++) {
         s_t.soft_empty[i] = 0; s_t.soft_present[i] = 0; s_t.soft_empty_seen[i] = 0; s_size[i] = 0;
@@ -568,7 +601,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const int words = ok ? s_t.words : 0;
     const bool pmode = a.pmode && words <= kCoopPHist && words * G <= 32768;
     for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
-    if (pmode) {   // word kinds of the partial slot (fold_all)
+    if (pmode && !s_skip) {   // word kinds of the partial slot (fold_all, phase 1's hand-off)
       for (int w = tid; w < words; w += BLOCK) {
         int kind = 0;
         auto in = [&](const Slot& sl) {
@@ -591,6 +624,32 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       tc.lag_idx = s_lag.tidx;
       tc.lag_w = s_lag.tw;
       tc.lag_n = s_lag.n_tmpl;
+    }
+    if (KN == 1) {   // the cache's loads, in flight through the tables fill
+      const int n0 = node_of(0);
+      const bool own0 = n0 < N;
+      tc.nc = own0 ? s_nc : 0;
+      tc.nt = own0 ? s_nt : 0;
+#pragma unroll
+      for (int k = 0; k < kTopoCache; k++) {
+        tc.csel[k] = k < tc.nc ? s_csel[k] : -1;
+        tc.cval[k] = k < tc.nc ? st.cnt[(size_t)tc.csel[k] * N + n0] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kTopoCache; k++) {
+        int idx = -2;
+        int32_t x = 0;
+        if (k < tc.nt) {
+          const int tm = s_ctm[k];
+          const uint32_t val = lab(c, c.tmpl_col[tm], n0);
+          if (val) {
+            idx = c.tmpl_off[tm] + (int)val;
+            x = gld(st.tab + idx);
+          }
+        }
+        tc.tidx[k] = idx;   // -2: no entry (the evaluators skip a node without the key)
+        tc.tval[k] = x;
+      }
     }
     __syncthreads();
     // which partial values this pod needs at all (pod-uniform): folds of the

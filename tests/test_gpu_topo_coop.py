@@ -84,3 +84,33 @@ def test_topo_coop_matches_oracle(gpu, oracle, name, make):
     p1, _ = gpu.run_queue(0, third)
     p2, _ = gpu.run_queue(third, P - third)
     np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
+
+
+@pytest.mark.parametrize("tables", ["1", "0"], ids=["tables", "pre-pass"])
+def test_configs2_30000_pods_golden(built, tables):
+    """configs[2]'s full 15,000-node cluster with a 30,000-pod queue against the
+    C++ oracle's placements, per-pod results and final pod counts
+    (tests/golden/c3_15000x30000.npz, tests/golden/make_c3_large.py: the oracle
+    takes minutes at this size): the maintained domain tables and their
+    one-pod lag over a long queue, and the pre-pass path (KSG_COOP_TABLES=0)."""
+    import os
+    gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c3_15000x30000.npz"))
+    nodes, pods, prof = G.config3(n_nodes=15000, n_pods=30000)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    old = os.environ.get("KSG_COOP_TABLES")
+    os.environ["KSG_COOP_TABLES"] = tables
+    try:
+        eng = native.Engine(device=0)
+    finally:
+        if old is None:
+            del os.environ["KSG_COOP_TABLES"]
+        else:
+            os.environ["KSG_COOP_TABLES"] = old
+    eng.load(enc, pf)
+    pg, rg = eng.run_queue(0, len(pods))
+    bad = np.nonzero(pg != gold["placements"])[0]
+    assert bad.size == 0, f"first mismatches at pods {bad[:5]}: gpu {pg[bad[:5]]} oracle {gold['placements'][bad[:5]]}"
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(np.asarray(rg[f]).astype(gold[f].dtype), gold[f], err_msg=f)
+    np.testing.assert_array_equal(eng.read_state(len(enc.cluster.res_names))[2], gold["pod_count"])
