@@ -2555,6 +2555,16 @@ struct ksg_ctx {
   bool defer_commit = true;           // env KSG_DEFER_COMMIT=0 disables
   int32_t pc_pod = -1, pc_node = -1;
   int32_t* d_coop_notables = nullptr; // a zeroed word set standing for "no tables"
+  // the chip-wide topology path's launch setup, kept across calls: the group
+  // shape for cfg_N nodes, the barrier flag generation (no flag reset per
+  // launch) and whether the flags / atomics sets / timeout word need a reset
+  // (after an allocation or a failed launch; a completed launch leaves them clean)
+  int coop_cfg_N = -1, coop_kn = 1, coop_G = 1;
+  bool coop_ll = false;
+  unsigned coop_gen = 0;
+  bool coop_dirty = true;
+  bool topo_eval_coop = false;        // the one-pod evaluation launches cooperatively (after a plain launch's
+                                      // workgroups were not all resident)
   int32_t* d_tables = nullptr;        // the maintained domain tables and their index (ksched_topo_tables.h)
   size_t tables_words = 0;
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
@@ -2727,6 +2737,9 @@ void free_all(ksg_ctx* ctx) {
   ctx->tables_words = 0;
   ctx->pc_node = -1;   // a deferred assume onto the freed state
   ctx->d_coop_notables = nullptr;
+  ctx->coop_cfg_N = -1;
+  ctx->coop_gen = 0;
+  ctx->coop_dirty = true;
   ctx->d_ev = nullptr;
   ctx->ev_bytes = 0;
   ctx->ev_clean = false;
@@ -3731,8 +3744,10 @@ struct CoopCap {
   char *raw = nullptr, *norm = nullptr, *tot = nullptr;
   int32_t rows[KSG_NPLUGINS] = {};
   int32_t n_rows = 0, n_normrows = 0, narrow = 0;
+  int32_t es = 8;                     // mode 2: bytes per row value
   ksg_result* h_res = nullptr;
   unsigned* h_flag = nullptr;
+  unsigned* h_ovf = nullptr;
   unsigned seq = 0;
 };
 
@@ -3902,28 +3917,36 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
                   bool timed = true) {
   const int N = ctx->c.N;
   int rc;
-  int cus = 0;
-  HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  if (!ctx->coop_gmax) ctx->coop_gmax = std::min(cus, 256);   // one workgroup per CU: lanes wait on memory
-  // Measurement knob: cap on the group size (fewer workgroups, more nodes per lane).
-  if (const char* f = getenv("KSG_COOP_GMAX")) ctx->coop_gmax = std::max(1, std::min(atoi(f), std::min(cus, 256)));
-  int kn = 1;
-  while ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N && kn < 32) kn *= 2;
-  if ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: too many nodes");
-  const int G = (int)((N + 256 * kn - 1) / (256 * kn));
-  // the variant whose label / vocabulary / template tables are LDS at compile time
-  const bool ll = kn == 1 && ctx->c.L <= kCoopLabCols && ctx->c.n_tmpl <= kCoopTmpl && !getenv("KSG_COOP_NO_LL");
-  int occ = 0;
-  switch (kn) {
-    case 1: rc = ll ? coop_occupancy<1, true>(ctx, &occ) : coop_occupancy<1>(ctx, &occ); break;
-    case 2: rc = coop_occupancy<2>(ctx, &occ); break;
-    case 4: rc = coop_occupancy<4>(ctx, &occ); break;
-    case 8: rc = coop_occupancy<8>(ctx, &occ); break;
-    case 16: rc = coop_occupancy<16>(ctx, &occ); break;
-    default: rc = coop_occupancy<32>(ctx, &occ); break;
+  if (ctx->coop_cfg_N != N) {   // the group shape, once per node set
+    int cus = 0;
+    HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    if (!ctx->coop_gmax) ctx->coop_gmax = std::min(cus, 256);   // one workgroup per CU: lanes wait on memory
+    // Measurement knob: cap on the group size (fewer workgroups, more nodes per lane).
+    if (const char* f = getenv("KSG_COOP_GMAX")) ctx->coop_gmax = std::max(1, std::min(atoi(f), std::min(cus, 256)));
+    int kn = 1;
+    while ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N && kn < 32) kn *= 2;
+    if ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: too many nodes");
+    const int G = (int)((N + 256 * kn - 1) / (256 * kn));
+    // the variant whose label / vocabulary / template tables are LDS at compile time
+    const bool ll = kn == 1 && ctx->c.L <= kCoopLabCols && ctx->c.n_tmpl <= kCoopTmpl && !getenv("KSG_COOP_NO_LL");
+    int occ = 0;
+    switch (kn) {
+      case 1: rc = ll ? coop_occupancy<1, true>(ctx, &occ) : coop_occupancy<1>(ctx, &occ); break;
+      case 2: rc = coop_occupancy<2>(ctx, &occ); break;
+      case 4: rc = coop_occupancy<4>(ctx, &occ); break;
+      case 8: rc = coop_occupancy<8>(ctx, &occ); break;
+      case 16: rc = coop_occupancy<16>(ctx, &occ); break;
+      default: rc = coop_occupancy<32>(ctx, &occ); break;
+    }
+    if (rc) return rc;
+    if (G > occ * cus) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: grid exceeds co-resident workgroups");
+    ctx->coop_kn = kn;
+    ctx->coop_G = G;
+    ctx->coop_ll = ll;
+    ctx->coop_cfg_N = N;
   }
-  if (rc) return rc;
-  if (G > occ * cus) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: grid exceeds co-resident workgroups");
+  const int kn = ctx->coop_kn, G = ctx->coop_G;
+  const bool ll = ctx->coop_ll;
   if (!ctx->d_coop_acc) {
     if ((rc = dalloc(ctx, &ctx->d_coop_acc, 2))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [4] timeout
@@ -3931,6 +3954,18 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     if ((rc = dalloc(ctx, &ctx->d_coop_parts, 256))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_phist, (size_t)256 * kCoopPHist))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_srec, (size_t)kCoopBatch * N))) return rc;
+    ctx->coop_dirty = true;
+  }
+  // the barrier flags are monotonic across launches ((gen << 16) + epoch, a
+  // launch runs < 2^16 barriers); reset with the atomics sets and the timeout
+  // word after a failed launch or when the generation wraps
+  const int n_launch = (count + kCoopBatch - 1) / kCoopBatch;
+  if (ctx->coop_dirty || ctx->coop_gen + (unsigned)n_launch >= 0xffffu) {
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_wgflags, 0, sizeof(unsigned) * 32 * 256, ctx->stream));
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_acc, 0, 2 * sizeof(CoopAcc), ctx->stream));
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 32, ctx->stream));
+    ctx->coop_gen = 0;
+    ctx->coop_dirty = false;
   }
   CoopArgs a{};
   a.c = ctx->c;
@@ -3961,8 +3996,10 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     }
   }
   if (!a.use_tables) {   // the kernel reads tt.invalid and the index arrays at setup: a valid empty set
-    if (!ctx->d_coop_notables && (rc = dalloc(ctx, &ctx->d_coop_notables, 64))) return rc;
-    HIPC(ctx, hipMemsetAsync(ctx->d_coop_notables, 0, 64 * sizeof(int32_t), ctx->stream));
+    if (!ctx->d_coop_notables) {
+      if ((rc = dalloc(ctx, &ctx->d_coop_notables, 64))) return rc;
+      HIPC(ctx, hipMemsetAsync(ctx->d_coop_notables, 0, 64 * sizeof(int32_t), ctx->stream));
+    }
     TopoTables t{};
     t.invalid = reinterpret_cast<unsigned*>(ctx->d_coop_notables);
     a.tt = t;
@@ -3979,17 +4016,23 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     a.cap_n_rows = cap->n_rows;
     a.cap_n_normrows = cap->n_normrows;
     a.cap_narrow = cap->narrow;
+    a.cap_es = cap->es;
     a.h_res = cap->h_res;
     a.h_flag = cap->h_flag;
+    a.h_ovf = cap->h_ovf;
     a.seq = cap->seq;
   }
+  // one pod evaluated (the per-cycle path): the static records in place, a
+  // plain launch (every workgroup one per CU, the barrier's poll is bounded;
+  // the caller relaunches cooperatively if they were not all resident)
+  const bool one = count == 1 && cmode == 2;
+  a.fused_static = one ? 1 : 0;
   SweepArgs sa{};
   sa.c = ctx->c;
   sa.pods = ctx->d_pods;
   sa.prog = ctx->d_prog;
   sa.profiles = d_prof;
   sa.srec = ctx->d_coop_srec;
-  HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 32, ctx->stream));
 #ifdef KSG_STAMPS
   if (!ctx->d_stamps) {
     if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
@@ -4012,17 +4055,21 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
       a.cap_norm = cap->norm + (size_t)off * cap->n_normrows * NN * es;
       a.cap_tot = cap->tot + (size_t)off * NN * es;
     }
-    hipLaunchKernelGGL(ksg_sweep_static, dim3(static_blocks(N, nb)), dim3(256), 0, ctx->stream, sa);
-    if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)nb * N))) return rc;
+    if (!one) {
+      hipLaunchKernelGGL(ksg_sweep_static, dim3(static_blocks(N, nb)), dim3(256), 0, ctx->stream, sa);
+      if ((rc = tlaunched(ctx, KSG_K_SWEEP_STATIC, (double)nb * N))) return rc;
+    }
     a.first = first + off;
     a.count = nb;
     a.out0 = off;
-    HIPC(ctx, hipMemsetAsync(ctx->d_coop_wgflags, 0, sizeof(unsigned) * 32 * G, ctx->stream));   // barrier flags
-    HIPC(ctx, hipMemsetAsync(ctx->d_coop_acc, 0, 2 * sizeof(CoopAcc), ctx->stream));
+    a.gen = ++ctx->coop_gen;
     // cooperative launch: the runtime guarantees the G workgroups are
     // co-resident (or refuses the launch), which the grid barrier needs
     void* kargs[] = {&a};
-    HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));
+    if (one && !ctx->topo_eval_coop)
+      HIPC(ctx, hipLaunchKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));
+    else
+      HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));
     if ((rc = tlaunched(ctx, KSG_K_TOPO_COOP, (double)nb * N))) return rc;
   }
   HIPC(ctx, hipGetLastError());
@@ -4165,7 +4212,10 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   if (ctx->last_path == 4) {
     unsigned flags[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPC(ctx, hipMemcpy(flags, ctx->d_coop_flags, sizeof(flags), hipMemcpyDeviceToHost));
-    if (flags[4]) return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
+    if (flags[4]) {
+      ctx->coop_dirty = true;
+      return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
+    }
   }
   return KSG_OK;
 }
@@ -4472,7 +4522,8 @@ bool eval_topo_eligible(ksg_ctx* ctx, int32_t pod) {
          !range_has_ports(ctx, pod, 1) && coop_capture_fits(ctx) && check_supported(ctx, ctx->prof, pod, 1) == KSG_OK;
 }
 
-int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_eval_rows* view = nullptr) {
+int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_eval_rows* view = nullptr,
+                   int es = 2) {
   const size_t N = ctx->c.N;
   const ksg_profile& prof = ctx->prof;
   int rows[KSG_NPLUGINS], n_rows = 0, n_normrows = 0;
@@ -4483,11 +4534,15 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
     if (((prof.score_mask >> pl) & 1u) && pl != KSG_PL_TAINT_TOLERATION && pl != KSG_PL_NODE_AFFINITY &&
         pl != KSG_PL_POD_TOPOLOGY_SPREAD && pl != KSG_PL_INTER_POD_AFFINITY)
       rows[n_rows++] = pl;
-  constexpr size_t es = 8;   // raw PodTopologySpread / InterPodAffinity scores are not range-checked: int64 rows
-  // host block: result (16 B) .. flag at 28 | fstatus[N] | raw[n_rows][N] | total[N] | norm[n_normrows][N]
+  // Row width es: 2 bytes first (every score of the default weights fits);
+  // the kernel flags a value that does not fit (raw PodTopologySpread /
+  // InterPodAffinity scores have no fixed range) and the pod is evaluated
+  // again at 4, then 8 bytes.  The block is sized for 8.
+  // host block: result (16 B) .. overflow word at 24, flag at 28 | fstatus[N] | raw[n_rows][N] | total[N] |
+  // norm[n_normrows][N]
   const size_t o_fs = 32, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
-  const size_t o_tot = o_raw + es * N * n_rows, o_norm = o_tot + es * N;
-  const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
+  const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
+  const size_t h_need = o_raw + 8 * N * (n_rows + 1 + std::max(n_normrows, 1)) + 64;
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
   if ((rc = flush_stage(ctx))) return rc;   // the topology kernel reads the pod from the device pool
@@ -4526,24 +4581,50 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
   cc.n_rows = n_rows;
   cc.n_normrows = n_normrows;
   cc.narrow = 0;
+  cc.es = es;
   cc.h_res = reinterpret_cast<ksg_result*>(db);
+  cc.h_ovf = reinterpret_cast<unsigned*>(db + 24);
   cc.h_flag = reinterpret_cast<unsigned*>(db + 28);
   cc.seq = seq;
-  if ((rc = run_topo_coop(ctx, pod, 1, ctx->d_ev_pl, nullptr, ctx->d_ev_prof, 0, &cc, false))) return rc;
+  if ((rc = run_topo_coop(ctx, pod, 1, ctx->d_ev_pl, nullptr, ctx->d_ev_prof, 0, &cc, false))) {
+    ctx->coop_dirty = true;
+    return rc;
+  }
   for (unsigned spins = 0; *flag != seq; spins++) {
     __builtin_ia32_pause();
     if ((spins & 1023) == 1023) {
       const hipError_t e = hipStreamQuery(ctx->stream);
-      if (e == hipSuccess && *flag != seq)
+      if (e == hipSuccess && *flag != seq) {
+        ctx->coop_dirty = true;   // a grid barrier timed out: the flags and atomics sets are reset next time
+        if (!ctx->topo_eval_coop) {   // not every workgroup was resident: cooperative launches from now on
+          ctx->topo_eval_coop = true;
+          return eval_topo_fast(ctx, pod, res, cap, view, es);
+        }
         return fail(ctx, KSG_E_DEVICE, "per-cycle topology evaluation: kernel finished without its completion flag "
-                                       "(grid barrier timed out?)");
-      if (e != hipSuccess && e != hipErrorNotReady)
+                                       "(grid barrier timed out)");
+      }
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        ctx->coop_dirty = true;
         return fail(ctx, KSG_E_DEVICE, std::string("per-cycle topology evaluation: ") + hipGetErrorString(e));
+      }
     }
   }
   std::atomic_thread_fence(std::memory_order_acquire);
   if ((rc = tcollect(ctx))) return rc;
+  if (*reinterpret_cast<const volatile unsigned*>(hb + 24) && es < 8)   // a value wider than the rows
+    return eval_topo_fast(ctx, pod, res, cap, view, es * 2);
   *res = *reinterpret_cast<const ksg_result*>(hb);
+  auto put_row = [&](int64_t* dst, size_t off) {   // one row into the caller's int64 array
+    if (es == 2) {
+      const int16_t* src = reinterpret_cast<const int16_t*>(hb + off);
+      for (size_t n = 0; n < N; n++) dst[n] = src[n];
+    } else if (es == 4) {
+      const int32_t* src = reinterpret_cast<const int32_t*>(hb + off);
+      for (size_t n = 0; n < N; n++) dst[n] = src[n];
+    } else {
+      std::memcpy(dst, hb + off, 8 * N);
+    }
+  };
   if (view) {
     *view = ksg_eval_rows{};
     view->n_nodes = (int32_t)N;
@@ -4558,12 +4639,10 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
   if (cap) {
     if (cap->fstatus) std::memcpy(cap->fstatus, hb + o_fs, 4 * N);
     for (int q = 0; q < n_rows; q++) {
-      if (cap->raw) std::memcpy(cap->raw + (size_t)rows[q] * N, hb + o_raw + es * N * q, es * N);
-      if (cap->norm)
-        std::memcpy(cap->norm + (size_t)rows[q] * N, hb + (q < n_normrows ? o_norm + es * N * q : o_raw + es * N * q),
-                    es * N);
+      if (cap->raw) put_row(cap->raw + (size_t)rows[q] * N, o_raw + es * N * q);
+      if (cap->norm) put_row(cap->norm + (size_t)rows[q] * N, q < n_normrows ? o_norm + es * N * q : o_raw + es * N * q);
     }
-    if (cap->total) std::memcpy(cap->total, hb + o_tot, es * N);
+    if (cap->total) put_row(cap->total, o_tot);
   }
   ctx->last_path = 6;
   return KSG_OK;

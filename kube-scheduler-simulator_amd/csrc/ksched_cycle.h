@@ -206,6 +206,9 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
     if (tid < PW) reinterpret_cast<int32_t*>(a.wpods)[tid] = pw;
     for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
   }
+  lds_barrier();   // LDS only: the node-column loads stay in flight
+  // (after the barrier: only the owner lane's wave waits for its columns, where
+  // its evaluation would wait for them anyway)
   if (own && n == a.cm_node) {   // the deferred assume: NodeInfo.AddPod on the lane's own node
 #pragma unroll
     for (int r = 0; r < KSG_MAX_RES; r++)
@@ -220,7 +223,6 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
     a.st.nonzero[NN + n] = L.nz_mem;
     a.st.pod_count[n] = L.pod_count;
   }
-  lds_barrier();   // LDS only: the node-column loads stay in flight
   KSG_YSTAMP(0);
   const PodView v = make_view(c, prof, s_pod, s_blob, a.gprog, false, a.st.ports);
 

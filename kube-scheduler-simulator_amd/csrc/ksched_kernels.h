@@ -215,8 +215,6 @@ struct TopoShared {
 constexpr uint32_t kSrUnsched = 1u, kSrNodeName = 2u, kSrTaint = 4u, kSrNodeAff = 8u, kSrNotEval = 16u;
 constexpr int kSrTaintSlotShift = 40;
 
-constexpr int kTopoCache = 8;   // TopoCtx: cached selector counts / template entries per lane
-
 struct TopoCtx {
   const TopoProg* g;
   const TopoShared* s;
@@ -232,34 +230,13 @@ struct TopoCtx {
   const int32_t* lag_idx = nullptr;
   const int32_t* lag_w = nullptr;
   int lag_n = 0;
-  // ksg_topo_coop (one node per lane): the lane's node's selector counts and
-  // template-table entries the pod reads, loaded at the pod's setup so the
-  // evaluators' reads are register hits, not dependent global loads
-  int nc = 0, nt = 0;
-  int csel[kTopoCache];
-  int32_t cval[kTopoCache];
-  int tidx[kTopoCache];
-  int32_t tval[kTopoCache];
-  __device__ __forceinline__ int32_t cntv(int N, int sel, int n) const {
-    if (sel < 0) return 0;
-#pragma unroll
-    for (int k = 0; k < kTopoCache; k++)
-      if (k < nc && csel[k] == sel) return cval[k];
-    return cnt[(size_t)sel * N + n];
-  }
   __device__ __forceinline__ int32_t tabv(int idx) const {
     int32_t v;
-    bool hit = false;
-#pragma unroll
-    for (int k = 0; k < kTopoCache; k++)
-      if (!hit && k < nt && tidx[k] == idx) { v = tval[k]; hit = true; }
-    if (!hit) {
-      if (coherent)   // agent-scope global (sc1) load: no stale L1 line, no acquire needed
-        v = __hip_atomic_load((__attribute__((address_space(1))) int32_t*)(const_cast<int32_t*>(tab) + idx),
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        v = tab[idx];
-    }
+    if (coherent)   // agent-scope global (sc1) load: no stale L1 line, no acquire needed
+      v = __hip_atomic_load((__attribute__((address_space(1))) int32_t*)(const_cast<int32_t*>(tab) + idx),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      v = tab[idx];
     for (int i = 0; i < lag_n; i++) v += lag_idx[i] == idx ? lag_w[i] : 0;
     return v;
   }
@@ -381,7 +358,7 @@ __device__ __forceinline__ uint32_t pts_filter_node(const DevCluster& c, const P
     if (!val) return 1;
     const Slot& sl = s.hard[i];
     int64_t m;
-    if (sl.unique) m = (all && inclusion(c, v, t, h[5], h[6], n)) ? t.cntv(c.N, sl.sel, n) : 0;
+    if (sl.unique) m = (all && inclusion(c, v, t, h[5], h[6], n)) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
     else m = hist_at(t.hist, sl, val);
     if (m + h[4] - s.hard_min[i] > h[2]) return 2;
   }
@@ -397,7 +374,7 @@ __device__ __forceinline__ uint32_t ipa_filter_node(const DevCluster& c, const T
     const Slot& sl = s.aff[i];
     const uint32_t val = lab(c, sl.col, n);
     if (!val) return 1;
-    const int64_t m = sl.unique ? t.cntv(c.N, g.sel_all, n) : hist_at(t.hist, sl, val);
+    const int64_t m = sl.unique ? cnt_at(t.cnt, c.N, g.sel_all, n) : hist_at(t.hist, sl, val);
     if (m <= 0) pods_exist = false;
   }
   if (!pods_exist && !(s.aff_total == 0 && g.n_aff > 0 && g.self_all)) return 1;
@@ -405,7 +382,7 @@ __device__ __forceinline__ uint32_t ipa_filter_node(const DevCluster& c, const T
     const Slot& sl = s.anti[i];
     const uint32_t val = lab(c, sl.col, n);
     if (!val) continue;
-    const int64_t m = sl.unique ? t.cntv(c.N, sl.sel, n) : hist_at(t.hist, sl, val);
+    const int64_t m = sl.unique ? cnt_at(t.cnt, c.N, sl.sel, n) : hist_at(t.hist, sl, val);
     if (m > 0) return 2;
   }
   for (int i = 0; i < g.n_ma; i++) {
@@ -428,10 +405,10 @@ __device__ __forceinline__ int64_t pts_score_node(const DevCluster& c, const Pod
     if (!val) continue;
     const Slot& sl = s.soft[i];
     int64_t m;
-    if (sc[5]) m = t.cntv(c.N, sl.sel, n);                    // hostname: this node's pods
+    if (sc[5]) m = cnt_at(t.cnt, c.N, sl.sel, n);                    // hostname: this node's pods
     else if (!sl.unique) m = t.hist[sl.hist + val];
     else if (val == 1) m = s.soft_empty[i];
-    else m = inclusion(c, v, t, sc[3], sc[4], n) ? t.cntv(c.N, sl.sel, n) : 0;
+    else m = inclusion(c, v, t, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
     const double x = (double)m * s.soft_w[i];
     score += x + (double)(sc[2] - 1);
   }
@@ -448,7 +425,7 @@ __device__ __forceinline__ int64_t ipa_score_node(const DevCluster& c, const ksg
     const Slot& sl = s.pref[i];
     const uint32_t val = lab(c, sl.col, n);
     if (!val) continue;
-    const int64_t m = sl.unique ? t.cntv(c.N, sl.sel, n) : hist_at(t.hist, sl, val);
+    const int64_t m = sl.unique ? cnt_at(t.cnt, c.N, sl.sel, n) : hist_at(t.hist, sl, val);
     sc += (int64_t)g.pref[3 * i + 2] * m;
   }
   if (prof.hard_pod_affinity_weight > 0)

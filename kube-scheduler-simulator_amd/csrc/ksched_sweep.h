@@ -202,6 +202,28 @@ __device__ __forceinline__ int64_t static_images(const DevCluster& c, int n, con
   return div_small(100 * (sum - minT), mx - minT);
 }
 
+// The static record of (pod, node n): the replica-independent verdicts and raw
+// scores (also computed in place by ksg_topo_coop's one-pod evaluation).
+__device__ __forceinline__ uint64_t static_record(const DevCluster& c, const ksg_pod& p, const PodView& v, int n,
+                                                  const uint8_t* eff) {
+  const GNode nd{&c, n};
+  uint32_t bits = 0;
+  if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) bits |= kSrNotEval;
+  if (nd.unsched() && !(p.flags & KSG_POD_TOL_UNSCHED)) bits |= kSrUnsched;
+  if (p.node_name != -1 && p.node_name != n) bits |= kSrNodeName;
+  bool treject;
+  int64_t tscore;
+  int tslot = -1;
+  static_taints(c, n, v.tolf, v.tolp, eff, treject, tscore, &tslot);
+  if (treject) bits |= kSrTaint;
+  if (!na_required_match(nd, v.P, v.na_req)) bits |= kSrNodeAff;
+  const uint64_t rt = (uint64_t)tscore;
+  const uint64_t ra = v.na_pref >= 0 ? (uint64_t)na_pref_score(nd, v.P, v.na_pref) : 0;
+  const uint64_t im = (uint64_t)static_images(c, n, v.P, v.img, p.n_containers);
+  return bits | ((rt & 0xff) << 8) | ((ra & 0xffff) << 16) | ((im & 0xff) << 32) |
+         ((uint64_t)(tslot < 0 ? 0 : tslot & 0xffff) << kSrTaintSlotShift);
+}
+
 __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
@@ -225,22 +247,7 @@ __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   const PodView v = make_view(c, s_prof, p, s_blob, a.prog);
   const int n = tile * 256 + tid;
   if (n >= N) return;
-  const GNode nd{&c, n};
-  uint32_t bits = 0;
-  if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) bits |= kSrNotEval;
-  if (nd.unsched() && !(p.flags & KSG_POD_TOL_UNSCHED)) bits |= kSrUnsched;
-  if (p.node_name != -1 && p.node_name != n) bits |= kSrNodeName;
-  bool treject;
-  int64_t tscore;
-  int tslot = -1;
-  static_taints(c, n, v.tolf, v.tolp, eff_lds ? s_eff : c.taint_effect, treject, tscore, &tslot);
-  if (treject) bits |= kSrTaint;
-  if (!na_required_match(nd, v.P, v.na_req)) bits |= kSrNodeAff;
-  const uint64_t rt = (uint64_t)tscore;
-  const uint64_t ra = v.na_pref >= 0 ? (uint64_t)na_pref_score(nd, v.P, v.na_pref) : 0;
-  const uint64_t im = (uint64_t)static_images(c, n, v.P, v.img, p.n_containers);
-  a.srec[(size_t)j * N + n] = bits | ((rt & 0xff) << 8) | ((ra & 0xffff) << 16) | ((im & 0xff) << 32) |
-                              ((uint64_t)(tslot < 0 ? 0 : tslot & 0xffff) << kSrTaintSlotShift);
+  a.srec[(size_t)j * N + n] = static_record(c, p, v, n, eff_lds ? s_eff : c.taint_effect);
 }
 
 // Replica-uniform facts of a profile for the sweep.

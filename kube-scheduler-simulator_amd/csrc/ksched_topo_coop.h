@@ -130,6 +130,13 @@ struct CoopArgs {
   // the maintained domain tables (ksched_topo_tables.h)
   TopoTables tt;
   int32_t use_tables;          // 1: pods within their scope skip phase 1 and barrier 1
+  unsigned gen;                // barrier flag generation: flags are (gen << 16) + epoch, monotonic across
+                               // launches, so nothing is reset per launch
+  int32_t fused_static;        // 1 (one pod): every lane computes its node's static record itself
+                               // (no ksg_sweep_static launch)
+  int32_t cap_es;              // CAP == 2: bytes per row value (2, 4, 8); a value that does not fit
+                               // sets *h_ovf and the host evaluates again wider
+  unsigned* h_ovf;
 };
 
 // Hand-offs between the G workgroups without cache maintenance (MI355X guide,
@@ -186,10 +193,10 @@ __device__ __forceinline__ int pts_soft1_m(const DevCluster& c, const PodView& v
   const uint32_t val = lab(c, sc[0], n);
   if (!val) return 1;
   const Slot& sl = s.soft[0];
-  if (sc[5]) m = t.cntv(c.N, sl.sel, n);
+  if (sc[5]) m = cnt_at(t.cnt, c.N, sl.sel, n);
   else if (!sl.unique) m = t.hist[sl.hist + val];
   else if (val == 1) m = s.soft_empty[0];
-  else m = inclusion(c, v, t, sc[3], sc[4], n) ? t.cntv(c.N, sl.sel, n) : 0;
+  else m = inclusion(c, v, t, sc[3], sc[4], n) ? cnt_at(t.cnt, c.N, sl.sel, n) : 0;
   return 0;
 }
 
@@ -381,7 +388,6 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ unsigned long long s_wbest;   // this workgroup's best key (phase 3)
   __shared__ uint8_t s_elig[kCoopBatch];    // tables_scope of the batch's pods
   __shared__ int s_inv;                     // the tables were invalidated (read per pod)
-  __shared__ int s_csel[kTopoCache], s_ctm[kTopoCache], s_nc, s_nt;   // the TopoCtx cache's keys
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
@@ -435,7 +441,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   bool ipa_in_filter = false;
   for (int kf = 0; kf < prof.n_filter; kf++) ipa_in_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
   const bool ipa_in_score = (prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u;
-  unsigned target = 0;
+  unsigned target = a.gen << 16;   // this launch's barrier epochs
   int prev_fallback_words = 0;   // words of the previous pod's atomics-merged histograms (0: partial slots)
   CoopPart* const mine = a.parts + wg;
   int32_t* const myhist = a.phist + (size_t)wg * kCoopPHist;
@@ -549,38 +555,6 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       const bool e = s_tables_ok != 0 && s_t.ok && s_elig[kq] && !s_inv;
       const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
       s_skip = !s_prev_imm && (!has_pre || e);
-      // the selector counts / template entries the evaluators read per node
-      // (TopoCtx cache, KN == 1): unique-key slots' selectors; the templates
-      // only when every template write of the previous pod is lagged (skip)
-      int nc = 0, nt = 0;
-      if (KN == 1 && s_t.ok) {
-        auto addc = [&](int sel) {
-          if (sel < 0) return;
-          for (int k = 0; k < nc; k++)
-            if (s_csel[k] == sel) return;
-          if (nc < kTopoCache) s_csel[nc++] = sel;
-        };
-        for (int i = 0; i < g0.n_hard; i++)
-          if (s_t.hard[i].unique) addc(s_t.hard[i].sel);
-        for (int i = 0; i < g0.n_soft; i++)
-          if (g0.soft[6 * i + 5] || s_t.soft[i].unique) addc(s_t.soft[i].sel);
-        if (g0.ipa) {
-          for (int i = 0; i < g0.n_aff; i++)
-            if (s_t.aff[i].unique) addc(g0.sel_all);
-          for (int i = 0; i < g0.n_anti; i++)
-            if (s_t.anti[i].unique) addc(s_t.anti[i].sel);
-          for (int i = 0; i < g0.n_pref; i++)
-            if (s_t.pref[i].unique) addc(s_t.pref[i].sel);
-          if (s_skip) {
-            for (int i = 0; i < g0.n_ma && nt < kTopoCache; i++) s_ctm[nt++] = g0.m_anti[i];
-            if (prof.hard_pod_affinity_weight > 0)
-              for (int i = 0; i < g0.n_mh && nt < kTopoCache; i++) s_ctm[nt++] = g0.m_hard[i];
-            for (int i = 0; i < g0.n_mp && nt < kTopoCache; i++) s_ctm[nt++] = g0.m_pref[i];
-          }
-        }
-      }
-      s_nc = nc;
-      s_nt = nt;
       for (int i = 0; i < kMaxHard; i++) { s_t.hard_min[i] = BIG; s_t.hard_dom[i] = 0; }
       for (int i = 0; i < kMaxSoft; i++) {
         s_t.soft_empty[i] = 0; s_t.soft_present[i] = 0; s_t.soft_empty_seen[i] = 0; s_size[i] = 0;
@@ -591,10 +565,19 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       s_tt[0] = s_tt[1] = s_tt[2] = 0;
     }
     uint64_t srk[KN];
+    if (a.fused_static) {   // one pod: the record of ksg_sweep_static, computed in place
+      const PodView vs = make_view(c, prof, s_pod, s_blob, a.prog);
 #pragma unroll
-    for (int k = 0; k < KN; k++) {
-      const int n = node_of(k);
-      srk[k] = srow[n < N ? n : 0];
+      for (int k = 0; k < KN; k++) {
+        const int n = node_of(k);
+        srk[k] = n < N ? static_record(cg, s_pod, vs, n, cg.taint_effect) : 0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KN; k++) {
+        const int n = node_of(k);
+        srk[k] = srow[n < N ? n : 0];
+      }
     }
     __syncthreads();
     const bool ok = s_t.ok;
@@ -624,32 +607,6 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       tc.lag_idx = s_lag.tidx;
       tc.lag_w = s_lag.tw;
       tc.lag_n = s_lag.n_tmpl;
-    }
-    if (KN == 1) {   // the cache's loads, in flight through the tables fill
-      const int n0 = node_of(0);
-      const bool own0 = n0 < N;
-      tc.nc = own0 ? s_nc : 0;
-      tc.nt = own0 ? s_nt : 0;
-#pragma unroll
-      for (int k = 0; k < kTopoCache; k++) {
-        tc.csel[k] = k < tc.nc ? s_csel[k] : -1;
-        tc.cval[k] = k < tc.nc ? st.cnt[(size_t)tc.csel[k] * N + n0] : 0;
-      }
-#pragma unroll
-      for (int k = 0; k < kTopoCache; k++) {
-        int idx = -2;
-        int32_t x = 0;
-        if (k < tc.nt) {
-          const int tm = s_ctm[k];
-          const uint32_t val = lab(c, c.tmpl_col[tm], n0);
-          if (val) {
-            idx = c.tmpl_off[tm] + (int)val;
-            x = gld(st.tab + idx);
-          }
-        }
-        tc.tidx[k] = idx;   // -2: no entry (the evaluators skip a node without the key)
-        tc.tval[k] = x;
-      }
     }
     __syncthreads();
     // which partial values this pod needs at all (pod-uniform): folds of the
@@ -1310,7 +1267,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     if constexpr (CAP != 0) {   // every row of this lane's nodes (ksg_capture semantics: < 2 feasible nodes record no scores)
       constexpr bool SYS = CAP == 2;
       const size_t NN = N;
-      const bool nar = a.cap_narrow != 0;
+      const int es = CAP == 2 ? a.cap_es : (a.cap_narrow ? 4 : 8);
+      auto fits = [&](int64_t x) { return es == 8 || (es == 4 ? x == (int64_t)(int32_t)x : x == (int64_t)(int16_t)x); };
       for (int k = 0; k < KN; k++) {
         const int n = node_of(k);
         if (n >= N) break;
@@ -1332,10 +1290,16 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
             }
           }
           const size_t row = ((size_t)kq * a.cap_n_rows + q) * NN + n;
-          cyc_put<SYS>(a.cap_raw, row, raw, nar);
-          if (q < a.cap_n_normrows) cyc_put<SYS>(a.cap_norm, ((size_t)kq * a.cap_n_normrows + q) * NN + n, nrm, nar);
+          cyc_put_es<SYS>(a.cap_raw, row, raw, es);
+          err |= fits(raw) ? 0u : 2u;
+          if (q < a.cap_n_normrows) {
+            cyc_put_es<SYS>(a.cap_norm, ((size_t)kq * a.cap_n_normrows + q) * NN + n, nrm, es);
+            err |= fits(nrm) ? 0u : 2u;
+          }
         }
-        cyc_put<SYS>(a.cap_tot, (size_t)kq * NN + n, feas ? ctot[k] : 0, nar);
+        const int64_t tv = feas ? ctot[k] : 0;
+        cyc_put_es<SYS>(a.cap_tot, (size_t)kq * NN + n, tv, es);
+        err |= fits(tv) ? 0u : 2u;
       }
     }
     best = wreduce(best, OpMaxU64{});
@@ -1401,7 +1365,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       unsigned long long b = 0;
       int32_t e = 0;
       for (int i = 0; i < NW; i++) { b = max(b, (unsigned long long)s_l[i][11]); e |= s_i[i][14]; }
-      if (e) status |= KSG_ST_SCORE_ERROR;
+      if (e & 1) status |= KSG_ST_SCORE_ERROR;   // (bit 1: a capture value wider than the rows, CAP == 2)
       else selected = key_node(b);
     }
     // the template tables reach tab one pod late unless the pod owns more
@@ -1456,6 +1420,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         }
       }
     }
+    if (wg == 0 && kq == a.count - 1)   // the last pod's atomics set, read by everyone before barrier 3:
+      for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&acc->hist[i], 0);   // clean for the next launch
     if (wg == 0 && tid == 0) {
       uint32_t score_skip = p.score_skip;
       if (ipa_in_filter && s_t.ipa_skip_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
@@ -1471,6 +1437,9 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       res.score_skip = score_skip;
       if (a.results) a.results[a.out0 + kq] = res;
       if constexpr (CAP == 2) {   // every workgroup's host rows are done (barrier 3 drained them)
+        int32_t ovf = 0;
+        for (int i = 0; i < NW; i++) ovf |= s_i[i][14];
+        hst<true>(a.h_ovf, (unsigned)((ovf >> 1) & 1));
         hst<true>(&a.h_res->selected, res.selected);
         hst<true>(&a.h_res->n_feasible, res.n_feasible);
         hst<true>(&a.h_res->status, res.status);
