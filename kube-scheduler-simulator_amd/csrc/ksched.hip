@@ -5472,6 +5472,14 @@ int ksg_debug_stamps(ksg_ctx* ctx, unsigned long long* out8) {   // 16 segment s
   HIPC(ctx, hipMemcpy(out8, ctx->d_stamps, 128, hipMemcpyDeviceToHost));
   return KSG_OK;
 }
+// eval_node_src's 16 segment sums (g_eval_stamp)
+int ksg_debug_eval_stamps(ksg_ctx* ctx, unsigned long long* out16) {
+  if (!ctx || !out16) return KSG_E_INVALID;
+  HIPC(ctx, hipSetDevice(ctx->device));
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  HIPC(ctx, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_eval_stamp), 128, 0, hipMemcpyDeviceToHost));
+  return KSG_OK;
+}
 #endif
 
 int ksg_set_timing(ksg_ctx* ctx, int on) {

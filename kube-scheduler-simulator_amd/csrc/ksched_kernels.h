@@ -456,6 +456,23 @@ struct NodeEval {
 // constant indices: registers).
 // Src: GNode (columns in global memory) or LNode (a node cached in LDS); L:
 // the node's resource columns, already gathered by the caller.
+#ifdef KSG_STAMPS
+// Diagnostic build only: per-segment cycles of eval_node_src, lane 0 of
+// workgroup 0 (slot 0 the node-set check, 1 + p filter plugin p, 13 the Fit /
+// BalancedAllocation scores, 14 ImageLocality + TaintToleration, 15 NodeAffinity).
+__device__ unsigned long long g_eval_stamp[16];
+#define KSG_ESTAMP(k)                                                          \
+  do {                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                \
+    if (threadIdx.x == 0 && blockIdx.x == 0) { g_eval_stamp[k] += _t - _es_last; } \
+    _es_last = _t;                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+  } while (0)
+#else
+#define KSG_ESTAMP(k) do {} while (0)
+#endif
+
 template <class Src>
 __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg_profile& prof, const PodView& v,
                                                   const Src& nd, const NodeCols& L, int n, int64_t* craw,
@@ -465,12 +482,29 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
   const int N = c.N;
   NodeEval e{0, 0, 0, 0, 0};
   uint32_t st = 0;
+#ifdef KSG_STAMPS
+  unsigned long long _es_last = __builtin_amdgcn_s_memtime();
+#endif
   if (v.reject || (v.node_set && !((((uint32_t)v.node_set[n >> 5]) >> (n & 31)) & 1u))) {
     st = KSG_FS_NOT_EVALUATED;
   } else {
+    KSG_ESTAMP(0);
     for (int kf = 0; kf < prof.n_filter && !st; kf++) {
       const int pl = prof.filter_order[kf];
       if ((v.fskip >> pl) & 1u) continue;
+#ifdef KSG_STAMPS
+      struct EStampOnExit {   // the plugin's slot, stamped when its case ends
+        unsigned long long& last;
+        int k;
+        __device__ ~EStampOnExit() {
+          __builtin_amdgcn_sched_barrier(0);
+          const unsigned long long t = __builtin_amdgcn_s_memtime();
+          if (threadIdx.x == 0 && blockIdx.x == 0) g_eval_stamp[k] += t - last;
+          last = t;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } _es_guard{_es_last, 1 + (pl < 12 ? pl : 11)};
+#endif
       switch (pl) {
         case KSG_PL_NODE_UNSCHEDULABLE:
           if (nd.unsched() && !(p.flags & KSG_POD_TOL_UNSCHED)) st = pl + 1;
@@ -513,6 +547,7 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
   }
   e.st = st;
   if (st != 0) return e;
+  KSG_ESTAMP(0);
   if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) {
     const int64_t s = fit_score(prof, p, L);
     e.part += s * v.w_fit;
@@ -525,6 +560,7 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
     if (lraw) lraw[KSG_PL_BALANCED_ALLOCATION] = s;
     if (craw) { craw[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; cnorm[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; }
   }
+  KSG_ESTAMP(13);
   if (v.smask & bit(KSG_PL_IMAGE_LOCALITY)) {
     const int64_t s = image_score(c, nd, v.P, v.img, p.n_containers);
     e.img = s * v.w_img;
@@ -537,11 +573,13 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
     if (lraw) lraw[KSG_PL_TAINT_TOLERATION] = e.rt;
     if (craw) craw[(size_t)KSG_PL_TAINT_TOLERATION * N + n] = e.rt;
   }
+  KSG_ESTAMP(14);
   if (v.smask & bit(KSG_PL_NODE_AFFINITY)) {
     e.ra = na_pref_score(nd, v.P, v.na_pref);
     if (lraw) lraw[KSG_PL_NODE_AFFINITY] = e.ra;
     if (craw) craw[(size_t)KSG_PL_NODE_AFFINITY * N + n] = e.ra;
   }
+  KSG_ESTAMP(15);
   return e;
 }
 

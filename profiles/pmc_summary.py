@@ -2,8 +2,10 @@
 
   python profiles/pmc_summary.py <run_pmc out dir> <dest dir>
 
-Writes <dest>/{bench,sweep}_kernel_stats.csv (the --stats summaries, copied)
-and <dest>/pmc_{config2,config4}.json: per kernel, dispatches, average
+Writes <dest>/{bench,sweep,topo,cycle}_kernel_stats.csv (the --stats
+summaries, copied), <dest>/pmc_{config2,config4,config3,per_cycle}.json and,
+where an SQ pass ran, <dest>/sq_<config>.json (average counter values per
+dispatch).  pmc_*.json: per kernel, dispatches, average
 FETCH_SIZE and WRITE_SIZE per dispatch (KB as rocprofv3 reports them) and HBM
 bytes per dispatch = 2 x FETCH_SIZE + WRITE_SIZE (x 1024): the gfx950
 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE counts half the bytes of
@@ -45,10 +47,27 @@ def counters(path):
     return out
 
 
+def counters_by_name(path):
+    """{kernel: {counter: average per dispatch}} from a multi-counter pass."""
+    acc, n = defaultdict(lambda: defaultdict(float)), defaultdict(int)
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = kernel_key(row.get("Kernel_Name") or row.get("Kernel-Name") or "")
+                acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
+                n[(k, row["Counter_Name"])] += 1
+    return {k: {c: v / n[(k, c)] for c, v in sorted(d.items())} for k, d in acc.items()}
+
+
 def main():
     src, dest = sys.argv[1], sys.argv[2]
     os.makedirs(dest, exist_ok=True)
-    for tag, cfg in (("bench", "config2"), ("sweep", "config4")):
+    for tag, cfg in (("bench", "config2"), ("sweep", "config4"), ("topo", "config3"), ("cycle", "per_cycle")):
+        if not glob.glob(os.path.join(src, f"{tag}_*")):
+            continue
+        sq = counters_by_name(os.path.join(src, f"{tag}_sq"))
+        if sq:
+            json.dump(sq, open(os.path.join(dest, f"sq_{cfg}.json"), "w"), indent=1)
         for f in glob.glob(os.path.join(src, f"{tag}_kt", "**", "*kernel_stats.csv"), recursive=True):
             shutil.copy(f, os.path.join(dest, f"{tag}_kernel_stats.csv"))
         fetch, write = counters(os.path.join(src, f"{tag}_fetch")), counters(os.path.join(src, f"{tag}_write"))

@@ -3,6 +3,9 @@
 #   1. rocprofv3 --kernel-trace --stats of the default bench (config 2)
 #   2. PMC passes FETCH_SIZE and WRITE_SIZE (separate runs) of the same bench
 #   3. the same three for the config-4 replica sweep (scripts/bench_configs.py)
+#   4. TOPO=1: configs[2]'s topology kernel (kernel trace, FETCH / WRITE, SQ mix)
+#   5. CYCLE=1: the per-cycle path (scripts/percycle.py)
+# SKIP_BENCH / SKIP_SWEEP drop parts 1-2 / 3.
 # Summaries are folded by profiles/pmc_summary.py into profiles/rNN/.
 set -uo pipefail
 OUT=${1:-gpurun_out/pmc}
@@ -31,7 +34,25 @@ run bench_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/bench_fetch" -o ru
 run bench_write --pmc WRITE_SIZE --output-format csv -d "$OUT/bench_write" -o run -- $B
 unset KSG_PIPE_OVERLAP
 fi
+if [ -z "${SKIP_SWEEP:-}" ]; then
 run sweep_kt --kernel-trace --stats --output-format csv -d "$OUT/sweep_kt" -o run -- $S
 run sweep_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/sweep_fetch" -o run -- $SP
 run sweep_write --pmc WRITE_SIZE --output-format csv -d "$OUT/sweep_write" -o run -- $SP
+fi
+# 4. configs[2] (TOPO=1): the chip-wide topology kernel, 3,000 pods at
+#    15,000 nodes: kernel trace, FETCH_SIZE, WRITE_SIZE and the SQ issue / wait mix
+if [ -n "${TOPO:-}" ]; then
+T="python3 scripts/bench_configs.py --config 3 --pods 3000 --reps 1 --no-cpu-baseline"
+run topo_kt --kernel-trace --stats --output-format csv -d "$OUT/topo_kt" -o run -- $T
+run topo_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/topo_fetch" -o run -- $T --no-timing
+run topo_write --pmc WRITE_SIZE --output-format csv -d "$OUT/topo_write" -o run -- $T --no-timing
+run topo_sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/topo_sq" -o run -- $T --no-timing
+fi
+# 5. the per-cycle path (CYCLE=1): 2,000 cycles at 5,000 nodes through the C driver
+if [ -n "${CYCLE:-}" ]; then
+C="python3 scripts/percycle.py 5000 500 2000"
+run cycle_kt --kernel-trace --stats --output-format csv -d "$OUT/cycle_kt" -o run -- $C
+run cycle_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/cycle_fetch" -o run -- $C
+run cycle_write --pmc WRITE_SIZE --output-format csv -d "$OUT/cycle_write" -o run -- $C
+fi
 find "$OUT" -name "*.csv" | sort
