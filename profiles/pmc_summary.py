@@ -62,7 +62,8 @@ def counters_by_name(path):
 def main():
     src, dest = sys.argv[1], sys.argv[2]
     os.makedirs(dest, exist_ok=True)
-    for tag, cfg in (("bench", "config2"), ("sweep", "config4"), ("topo", "config3"), ("cycle", "per_cycle")):
+    for tag, cfg in (("bench", "config2"), ("sweep", "config4"), ("topo", "config3"), ("cycle", "per_cycle"),
+                     ("c5", "config5")):
         if not glob.glob(os.path.join(src, f"{tag}_*")):
             continue
         sq = counters_by_name(os.path.join(src, f"{tag}_sq"))
