@@ -1233,34 +1233,7 @@ struct P2Part {
 
 // qdiv(), ddiv(): ksched_device.h
 
-// Batch-uniform profile facts for the compact evaluator.
-struct CmProf {
-  bool fast;        // Fit and BalancedAllocation both score exactly {cpu, memory}
-  bool least;
-  int64_t wc, wm;   // Fit resource weights of cpu / memory
-  float inv_ws, inv_wc, inv_wm;   // 1 / (wc + wm), 1 / wc, 1 / wm
-};
-
-__device__ __forceinline__ CmProf cm_prof(const ksg_profile& prof) {
-  CmProf m{false, prof.fit_strategy == KSG_LEAST_ALLOCATED, 0, 0, 1.0f, 1.0f, 1.0f};
-  bool ok = prof.fit_n == 2 && prof.ba_n == 2;
-  if (ok) {
-    const int r0 = prof.fit_res[0], r1 = prof.fit_res[1];
-    ok = (r0 == KSG_RES_CPU && r1 == KSG_RES_MEM) || (r0 == KSG_RES_MEM && r1 == KSG_RES_CPU);
-    m.wc = r0 == KSG_RES_CPU ? prof.fit_w[0] : prof.fit_w[1];
-    m.wm = r0 == KSG_RES_CPU ? prof.fit_w[1] : prof.fit_w[0];
-    const int b0 = prof.ba_res[0], b1 = prof.ba_res[1];
-    ok = ok && ((b0 == KSG_RES_CPU && b1 == KSG_RES_MEM) || (b0 == KSG_RES_MEM && b1 == KSG_RES_CPU));
-    ok = ok && m.wc > 0 && m.wm > 0;
-  }
-  m.fast = ok;
-  if (ok) {
-    m.inv_ws = 1.0f / (float)(m.wc + m.wm);
-    m.inv_wc = 1.0f / (float)m.wc;
-    m.inv_wm = 1.0f / (float)m.wm;
-  }
-  return m;
-}
+// CmProf / cm_prof: ksched_device.h
 
 // Per-pod values of the changed-node evaluation, read from LDS in one batch.
 template <int RM>

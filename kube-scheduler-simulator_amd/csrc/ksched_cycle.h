@@ -229,7 +229,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
   // ---- phase 1: this workgroup's nodes ------------------------------------------------
   NodeEval e{KSG_FS_NOT_EVALUATED, 0, 0, 0, 0};
   int64_t lraw[KSG_NPLUGINS] = {};
-  if (own) e = eval_node_src(c, prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw);
+  const CmProf cm = cm_prof(prof);
+  if (own) e = eval_node_src(c, prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw, &cm);
   KSG_YSTAMP(1);
   const bool ok = own && e.st == 0;
   // the row value of score row q (node-local plugins only on this path)

@@ -396,6 +396,66 @@ __device__ __forceinline__ int64_t ba_score(const ksg_profile& prof, const ksg_p
   return (int64_t)((1 - sd) * (double)100);
 }
 
+// Batch-uniform profile facts for the compact evaluator.
+struct CmProf {
+  bool fast;        // Fit and BalancedAllocation both score exactly {cpu, memory}
+  bool least;
+  int64_t wc, wm;   // Fit resource weights of cpu / memory
+  float inv_ws, inv_wc, inv_wm;   // 1 / (wc + wm), 1 / wc, 1 / wm
+};
+
+__device__ __forceinline__ CmProf cm_prof(const ksg_profile& prof) {
+  CmProf m{false, prof.fit_strategy == KSG_LEAST_ALLOCATED, 0, 0, 1.0f, 1.0f, 1.0f};
+  bool ok = prof.fit_n == 2 && prof.ba_n == 2;
+  if (ok) {
+    const int r0 = prof.fit_res[0], r1 = prof.fit_res[1];
+    ok = (r0 == KSG_RES_CPU && r1 == KSG_RES_MEM) || (r0 == KSG_RES_MEM && r1 == KSG_RES_CPU);
+    m.wc = r0 == KSG_RES_CPU ? prof.fit_w[0] : prof.fit_w[1];
+    m.wm = r0 == KSG_RES_CPU ? prof.fit_w[1] : prof.fit_w[0];
+    const int b0 = prof.ba_res[0], b1 = prof.ba_res[1];
+    ok = ok && ((b0 == KSG_RES_CPU && b1 == KSG_RES_MEM) || (b0 == KSG_RES_MEM && b1 == KSG_RES_CPU));
+    ok = ok && m.wc > 0 && m.wm > 0;
+  }
+  m.fast = ok;
+  if (ok) {
+    m.inv_ws = 1.0f / (float)(m.wc + m.wm);
+    m.inv_wc = 1.0f / (float)m.wc;
+    m.inv_wm = 1.0f / (float)m.wm;
+  }
+  return m;
+}
+
+// fit_score + ba_score for a CmProf::fast profile (both over exactly {cpu,
+// memory}): the same arithmetic without branches or loops over the profile's
+// resource lists, so the two chains interleave (sweep_cm_scores' restatement
+// on a node's gathered columns).  Equal to fit_score / ba_score bit for bit.
+__device__ __forceinline__ void fit_ba_cm(const CmProf& m, const ksg_pod& p, const NodeCols& L, int64_t& fit,
+                                          int64_t& ba) {
+  const int64_t ac = L.alloc[KSG_RES_CPU], am = L.alloc[KSG_RES_MEM];
+  const bool hc = ac > 0, hm = am > 0;
+  const int64_t sac = hc ? ac : 1, sam = hm ? am : 1;
+  const float ic = __builtin_amdgcn_rcpf((float)sac), im = __builtin_amdgcn_rcpf((float)sam);
+  const int64_t qc = L.nz_cpu + p.nz_cpu, qm = L.nz_mem + p.nz_mem;
+  int64_t xc, xm;
+  if (m.least) {
+    xc = qc > ac ? 0 : (ac - qc) * 100;
+    xm = qm > am ? 0 : (am - qm) * 100;
+  } else {
+    xc = (qc > ac ? ac : qc) * 100;
+    xm = (qm > am ? am : qm) * 100;
+  }
+  const int64_t sc = qdiv(xc, sac, ic), sm = qdiv(xm, sam, im);
+  const int64_t num = (hc ? sc * m.wc : 0) + (hm ? sm * m.wm : 0);
+  const int64_t ws = (hc ? m.wc : 0) + (hm ? m.wm : 0);
+  fit = ws == 0 ? 0 : qdiv(num, ws, __builtin_amdgcn_rcpf((float)ws));
+  double fc = ddiv((double)(L.req[KSG_RES_CPU] + p.req[KSG_RES_CPU]), (double)sac);
+  double fm = ddiv((double)(L.req[KSG_RES_MEM] + p.req[KSG_RES_MEM]), (double)sam);
+  fc = fc > 1 ? 1 : fc;
+  fm = fm > 1 ? 1 : fm;
+  const double sd = hc && hm ? fabs((fc - fm) / 2) : 0.0;
+  ba = (int64_t)((1 - sd) * (double)100);
+}
+
 template <class Src>
 __device__ __forceinline__ int64_t image_score(const DevCluster& c, const Src& nd, const int32_t* P, int img,
                                                int n_containers) {

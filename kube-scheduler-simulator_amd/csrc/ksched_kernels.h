@@ -473,11 +473,13 @@ __device__ unsigned long long g_eval_stamp[16];
 #define KSG_ESTAMP(k) do {} while (0)
 #endif
 
+// cm: the profile's CmProf when the caller computed it (Fit + BalancedAllocation
+// then take fit_ba_cm when cm->fast).
 template <class Src>
 __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg_profile& prof, const PodView& v,
                                                   const Src& nd, const NodeCols& L, int n, int64_t* craw,
                                                   int64_t* cnorm, const TopoCtx* tc = nullptr,
-                                                  int64_t* lraw = nullptr) {
+                                                  int64_t* lraw = nullptr, const CmProf* cm = nullptr) {
   const ksg_pod& p = *v.p;
   const int N = c.N;
   NodeEval e{0, 0, 0, 0, 0};
@@ -548,6 +550,20 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
   e.st = st;
   if (st != 0) return e;
   KSG_ESTAMP(0);
+  if (cm && cm->fast && (v.smask & (bit(KSG_PL_NODE_RESOURCES_FIT) | bit(KSG_PL_BALANCED_ALLOCATION)))) {
+    int64_t sf, sb;
+    fit_ba_cm(*cm, p, L, sf, sb);
+    if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) {
+      e.part += sf * v.w_fit;
+      if (lraw) lraw[KSG_PL_NODE_RESOURCES_FIT] = sf;
+      if (craw) { craw[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = sf; cnorm[(size_t)KSG_PL_NODE_RESOURCES_FIT * N + n] = sf; }
+    }
+    if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) {
+      e.part += sb * v.w_ba;
+      if (lraw) lraw[KSG_PL_BALANCED_ALLOCATION] = sb;
+      if (craw) { craw[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = sb; cnorm[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = sb; }
+    }
+  } else {
   if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) {
     const int64_t s = fit_score(prof, p, L);
     e.part += s * v.w_fit;
@@ -559,6 +575,7 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
     e.part += s * v.w_ba;
     if (lraw) lraw[KSG_PL_BALANCED_ALLOCATION] = s;
     if (craw) { craw[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; cnorm[(size_t)KSG_PL_BALANCED_ALLOCATION * N + n] = s; }
+  }
   }
   KSG_ESTAMP(13);
   if (v.smask & bit(KSG_PL_IMAGE_LOCALITY)) {

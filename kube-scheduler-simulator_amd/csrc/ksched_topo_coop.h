@@ -211,7 +211,7 @@ __device__ __forceinline__ int64_t pts_soft1_score(const TopoProg& g, const Topo
 // static record (t.rec): RunFilterPlugins (feasibility; the coop path records
 // no per-node status word) + the raw scores.
 __device__ __forceinline__ NodeEval eval_node_rec(const DevCluster& c, const ksg_profile& prof, const PodView& v,
-                                                  const NodeCols& L, int n, const TopoCtx& t) {
+                                                  const NodeCols& L, int n, const TopoCtx& t, const CmProf& cm) {
   const ksg_pod& p = *v.p;
   const uint64_t sr = t.rec;
   NodeEval e{0, 0, 0, 0, 0};
@@ -259,8 +259,15 @@ __device__ __forceinline__ NodeEval eval_node_rec(const DevCluster& c, const ksg
   }
   e.st = st;
   if (st != 0) return e;
-  if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) e.part += fit_score(prof, p, L) * v.w_fit;
-  if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) e.part += ba_score(prof, p, L) * v.w_ba;
+  if (cm.fast && (v.smask & (bit(KSG_PL_NODE_RESOURCES_FIT) | bit(KSG_PL_BALANCED_ALLOCATION)))) {
+    int64_t sf, sb;   // both chains at once (fit_ba_cm: the same bits)
+    fit_ba_cm(cm, p, L, sf, sb);
+    if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) e.part += sf * v.w_fit;
+    if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) e.part += sb * v.w_ba;
+  } else {
+    if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) e.part += fit_score(prof, p, L) * v.w_fit;
+    if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) e.part += ba_score(prof, p, L) * v.w_ba;
+  }
   if (v.smask & bit(KSG_PL_IMAGE_LOCALITY)) {
     e.img = (int64_t)((sr >> 32) & 0xff) * v.w_img;
     e.part += e.img;
@@ -438,6 +445,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   }
   const DevCluster& c = cl;
   const ksg_profile& prof = s_prof;
+  const CmProf cmp = cm_prof(prof);   // Fit + BalancedAllocation over exactly {cpu, memory}: fit_ba_cm
   bool ipa_in_filter = false;
   for (int kf = 0; kf < prof.n_filter; kf++) ipa_in_filter |= prof.filter_order[kf] == KSG_PL_INTER_POD_AFFINITY;
   const bool ipa_in_score = (prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u;
@@ -965,7 +973,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       NodeCols L;
       if (KN == 1) L = Lreg;
       else load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
-      ev[k] = eval_node_rec(c, prof, v, L, n, tn);
+      ev[k] = eval_node_rec(c, prof, v, L, n, tn, cmp);
       KSG_CSTAMP(11);
       if (ev[k].st != 0) continue;
       if constexpr (CAP != 0) {
