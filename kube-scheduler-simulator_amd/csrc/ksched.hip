@@ -3827,11 +3827,12 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
   }
   sp_off[S] = (int32_t)(sp.size() / 2);
   // block: dom | tot[S] | cc | pres | col_missing[L] | col_empty[L] | invalid | pair_off[S*L] | cc_off[S] |
-  // pres_off[L] | sp_off[S+1] | sp | elig[count] (bytes) | tasks
+  // pres_off[L] | sp_off[S+1] | sp | elig[count] (bytes) | fill tasks [count][kTopoFill] int4 | tasks
   const size_t o_tot = dom_words, o_cc = o_tot + S, o_pres = o_cc + cc_words, o_miss = o_pres + pres_words,
                o_empty = o_miss + L, o_inv = o_empty + L, o_pair = o_inv + 1, o_ccoff = o_pair + (size_t)S * L,
                o_preso = o_ccoff + S, o_spoff = o_preso + L, o_sp = o_spoff + S + 1, o_elig = o_sp + sp.size(),
-               o_tasks = (o_elig + ((size_t)count + 3) / 4 + 3) & ~(size_t)3,
+               o_fo = (o_elig + ((size_t)count + 3) / 4 + 3) & ~(size_t)3,
+               o_tasks = o_fo + (size_t)count * kTopoFill * 4,
                words = o_tasks + tasks.size() * (sizeof(TopoTableTask) / 4);
   if (words > ctx->tables_words) {
     if (ctx->d_tables) {
@@ -3870,6 +3871,7 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
   t.sp_off = b + o_spoff;
   t.sp = b + o_sp;
   t.elig = reinterpret_cast<const uint8_t*>(b + o_elig);
+  t.fo = reinterpret_cast<const int4*>(b + o_fo);
   t.first = first;
   t.S = S;
   t.L = L;
@@ -3878,7 +3880,8 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
                      t, reinterpret_cast<const TopoTableTask*>(b + o_tasks));
   if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: init launch"); return false; }
   hipLaunchKernelGGL(ksg_topo_tables_elig, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, ctx->stream, ctx->c, t,
-                     ctx->d_pods, ctx->d_prog, count, reinterpret_cast<uint8_t*>(b + o_elig));
+                     ctx->d_pods, ctx->d_prog, count, reinterpret_cast<uint8_t*>(b + o_elig),
+                     reinterpret_cast<int4*>(b + o_fo));
   if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: scope launch"); return false; }
   (void)N;
   *out = t;

@@ -395,6 +395,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ unsigned long long s_wbest;   // this workgroup's best key (phase 3)
   __shared__ uint8_t s_elig[kCoopBatch];    // tables_scope of the batch's pods
   __shared__ int s_inv;                     // the tables were invalidated (read per pod)
+  __shared__ int4 s_fo[kTopoFill];          // the pod's fill tasks (tables' fo), loaded at setup
+  __shared__ long long s_totv[1 + kMaxPref];   // tot[sel_all], tot[pref selectors], loaded at setup
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = blockIdx.x, G = a.G;
@@ -544,25 +546,18 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         if (tid + u * BLOCK < nb_len) s_blob[tid + u * BLOCK] = nb[u];
     }
     __syncthreads();
+    KSG_CSTAMP(15);   // (stamps build: the pod staged; segment 15 is phase 1's node loop otherwise)
     const ksg_pod& p = s_pod;
-    if (tid == 0) {
-      const PodView v0 = make_view(c, prof, p, s_blob, a.prog, true);
-      parse_topo(p, s_blob, v0.fskip, v0.smask, s_g);
-      layout_slots(c, s_g, s_t);
-      // this pod's matched selectors (its commit program): the lag delta of its assume
-      s_nlsel = 0;
+    if (tid == 64) {   // this pod's matched selectors (its commit program): the lag delta of its assume
+      int nl = 0;
       if (p.commit >= 0) {
         const int32_t* cw = s_blob + (p.commit - p.blob);
-        s_nlsel = cw[0];
+        nl = cw[0];
         for (int i = 0; i < kLagSel && i < cw[0]; i++) s_lsel[i] = cw[1 + i];
       }
-      // Tables scope (tables_scope, one flag per pod computed at the run's
-      // start), the tables exact (no count-of-counts overflow in the previous
-      // pod's lag_apply: s_inv) and the histograms within their limits.
-      const TopoProg& g0 = s_g;
-      const bool e = s_tables_ok != 0 && s_t.ok && s_elig[kq] && !s_inv;
-      const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
-      s_skip = !s_prev_imm && (!has_pre || e);
+      s_nlsel = nl;
+    }
+    if (tid == 128) {   // the per-pod accumulators (beside tid 0's parse: other fields of s_t)
       for (int i = 0; i < kMaxHard; i++) { s_t.hard_min[i] = BIG; s_t.hard_dom[i] = 0; }
       for (int i = 0; i < kMaxSoft; i++) {
         s_t.soft_empty[i] = 0; s_t.soft_present[i] = 0; s_t.soft_empty_seen[i] = 0; s_size[i] = 0;
@@ -571,6 +566,18 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       s_t.aff_total = 0;
       s_t.pref_any = 0;
       s_tt[0] = s_tt[1] = s_tt[2] = 0;
+    }
+    if (tid == 0) {
+      const PodView v0 = make_view(c, prof, p, s_blob, a.prog, true);
+      parse_topo(p, s_blob, v0.fskip, v0.smask, s_g);
+      layout_slots(c, s_g, s_t);
+      // Tables scope (tables_scope, one flag per pod computed at the run's
+      // start), the tables exact (no count-of-counts overflow in the previous
+      // pod's lag_apply: s_inv) and the histograms within their limits.
+      const TopoProg& g0 = s_g;
+      const bool e = s_tables_ok != 0 && s_t.ok && s_elig[kq] && !s_inv;
+      const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
+      s_skip = !s_prev_imm && (!has_pre || e);
     }
     uint64_t srk[KN];
     if (a.fused_static) {   // one pod: the record of ksg_sweep_static, computed in place
@@ -588,8 +595,31 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     __syncthreads();
+    KSG_CSTAMP(2);    // (stamps build: tid 0's parse and layout; segment 2 is barrier 1 otherwise)
     const bool ok = s_t.ok;
     const int words = ok ? s_t.words : 0;
+    // a pod reading the tables: its fill tasks, the totals its affinity /
+    // preferred terms read and the existing pods' template totals, loaded now
+    // (every write they see is lagged or was applied before barrier 3 of the
+    // previous pod), in flight through the rest of the setup
+    const bool tab_read = s_skip && s_tables_ok && ok;
+    if (tab_read) {
+      const TopoProg& g1 = s_g;
+      if (tid < kTopoFill) s_fo[tid] = tt.fo[(size_t)(a.first - tt.first + kq) * kTopoFill + tid];
+      if (g1.ipa && tid >= 64 && tid < 64 + 1 + g1.n_pref) {
+        const int sel = tid == 64 ? g1.sel_all : g1.pref[3 * (tid - 65) + 1];
+        s_totv[tid - 64] = sel >= 0 ? (long long)gld(tt.tot + sel) : 0;
+      }
+      const int n_t = g1.ipa ? g1.n_ma + g1.n_mh + g1.n_mp : 0;
+      for (int i = tid - 128; i >= 0 && i < n_t; i += BLOCK - 128) {
+        const int which = i < g1.n_ma ? 0 : (i < g1.n_ma + g1.n_mh ? 1 : 2);
+        const int tm = which == 0 ? g1.m_anti[i] : (which == 1 ? g1.m_hard[i - g1.n_ma] : g1.m_pref[i - g1.n_ma - g1.n_mh]);
+        int32_t x = gld(&st.tmpl_total[tm]);
+        if (s_lag_tab && s_lag.node >= 0)   // the previous pod's pending template entries
+          for (int j = 0; j < s_lag.n_tmpl; j++) x += s_lag.tt[j] == tm && s_lag.tidx[j] >= 0 ? 1 : 0;
+        if (x) atomicAdd((unsigned long long*)&s_tt[which], (unsigned long long)x);
+      }
+    }
     const bool pmode = a.pmode && words <= kCoopPHist && words * G <= 32768;
     for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
     if (pmode && !s_skip) {   // word kinds of the partial slot (fold_all, phase 1's hand-off)
@@ -773,16 +803,18 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         for (int i = 0; i < d.n_sel; i++) hit = d.sel[i] == sel ? i : hit;
         return d.node >= 0 ? hit : -1;
       };
+      // the non-unique slots' histograms, task k = the k-th such slot in
+      // layout order (s_fo: dom offset, presence offset, column, selector);
+      // every load of a task (the table words, the lag node's label) in flight
+      // at once
+      int k_task = 0;
       auto fill = [&](const Slot& sl, bool pres) {   // hist (+ presence bits) of a non-unique slot
-        const int off = tt.pair_off[(size_t)sl.sel * tt.L + sl.col];
+        const int4 f = s_fo[k_task++];
         const uint32_t lv = in_lag(sl.sel) >= 0 ? cg.label_val[(size_t)sl.col * N + d.node] : 0u;   // 0: none
-        for (int v = tid; v < sl.V; v += BLOCK) s_hist[sl.hist + v] = gld(tt.dom + off + v) + (lv && (uint32_t)v == lv ? 1 : 0);
-        if (pres) {
-          const int po = tt.pres_off[sl.col];
-          for (int w = tid; w < (sl.V + 31) / 32; w += BLOCK) s_hist[sl.pres + w] = (int32_t)tt.pres[po + w];
-        }
+        for (int v = tid; v < sl.V; v += BLOCK) s_hist[sl.hist + v] = gld(tt.dom + f.x + v) + (lv && (uint32_t)v == lv ? 1 : 0);
+        if (pres)
+          for (int w = tid; w < (sl.V + 31) / 32; w += BLOCK) s_hist[sl.pres + w] = (int32_t)tt.pres[f.y + w];
       };
-      auto total = [&](int sel) { return (long long)gld(tt.tot + sel) + (in_lag(sel) >= 0 ? 1 : 0); };
       for (int i = 0; i < g.n_hard; i++)
         if (!s_t.hard[i].unique) fill(s_t.hard[i], true);
       for (int i = 0; i < g.n_soft; i++)
@@ -796,9 +828,10 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           if (!s_t.pref[i].unique) fill(s_t.pref[i], true);
       }
       // unique hard keys: the minimum count over the nodes from the
-      // count-of-counts table (wave w < n_hard: constraint w)
-      if (wv < g.n_hard && s_t.hard[wv].unique) {
-        const int sel = s_t.hard[wv].sel, co = tt.cc_off[sel], li = in_lag(sel);
+      // count-of-counts table (constraint i on wave NW - 1 - i, off wave 0's fill loads)
+      const int hw = NW - 1 - wv;
+      if (hw < g.n_hard && s_t.hard[hw].unique) {
+        const int sel = s_t.hard[hw].sel, co = tt.cc_off[sel], li = in_lag(sel);
         const int old = li >= 0 ? d.old_cnt[li] : -2;
         int first = 0x7fffffff;
         for (int k0 = 0; k0 < tt.Kc && first == 0x7fffffff; k0 += 64) {
@@ -807,23 +840,25 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           const unsigned long long b = __ballot(x > 0);
           if (b) first = k0 + __builtin_ctzll(b);
         }
-        if (lane == 0) { s_t.hard_min[wv] = first; s_t.hard_dom[wv] = N; }
+        if (lane == 0) { s_t.hard_min[hw] = first; s_t.hard_dom[hw] = N; }
       }
       __syncthreads();
       if (tid == 0) {
+        // the totals came with the setup (s_totv: tot[sel_all], tot[pref selector i])
+        auto total = [&](int sel, long long t) { return t + (in_lag(sel) >= 0 ? 1 : 0); };
         for (int i = 0; i < g.n_soft; i++) s_t.soft_empty[i] = 0;   // no node lacks the key or has ""
         if (g.ipa) {
           long long af = 0;
           for (int i = 0; i < g.n_aff; i++) {
             const Slot& sl = s_t.aff[i];
-            if (sl.unique) af += total(g.sel_all);
+            if (sl.unique) af += total(g.sel_all, s_totv[0]);
             else for (int v = 1; v < sl.V; v++) af += s_hist[sl.hist + v];
           }
           s_t.aff_total = af;
           int any = 0;
           for (int i = 0; i < g.n_pref; i++) {
             const Slot& sl = s_t.pref[i];
-            if (sl.unique) any |= total(sl.sel) > 0;
+            if (sl.unique) any |= total(sl.sel, s_totv[1 + i]) > 0;
             else for (int v = 1; v < sl.V; v++) any |= s_hist[sl.hist + v] > 0;
           }
           s_t.pref_any = any;
@@ -921,7 +956,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     if (wg == 0 && prev_fallback_words)   // the set of pod kq - 1, read by everyone by now
       for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&nxt->hist[i], 0);
     prev_fallback_words = pmode ? 0 : words;   // (a skipping pod still merges its soft marks into acc)
-    {   // existing pods' terms matching this pod: totals, one template per lane
+    if (!tab_read) {   // existing pods' terms matching this pod: totals, one template per lane (tab_read: setup)
       const int n_t = g.ipa ? g.n_ma + g.n_mh + g.n_mp : 0;
       for (int i = tid; i < n_t; i += BLOCK) {
         const int which = i < g.n_ma ? 0 : (i < g.n_ma + g.n_mh ? 1 : 2);
@@ -1086,6 +1121,20 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     // barrier 2: workgroup 0 applies the previous pod's assume to them now (the
     // next pod reads after barrier 3)
     if (wg == 0) lag_apply(cg, st, tt, s_lag, s_tables_ok != 0, s_lag_tab != 0);
+    // the soft constraints' domain marks of every workgroup, loaded beside the
+    // partial scalars below (one memory round trip for both; unused when the
+    // pod turns out to have < 2 feasible nodes)
+    if (g.pts_score && ok)
+      for (int i = 0; i < g.n_soft; i++) {
+        const Slot& sl = s_t.soft[i];
+        if (g.soft[6 * i + 5] || sl.unique) continue;
+        const int bw = (sl.V + 31) / 32;
+        if (pmode) {   // or-ed into this workgroup's own marks
+          fold_words(sl.mark, bw, true);
+        } else {
+          for (int wd = tid; wd < bw; wd += BLOCK) s_hist[sl.mark + wd] = gld(&acc->hist[sl.mark + wd]);
+        }
+      }
     {
       int32_t f_n = 0, f_min = 0x7fffffff, f_ign = 0, f_hv = 0, f_hz = 0, f_mt = 0, f_ma = 0;
       int32_t f_pr[kMaxSoft] = {0, 0, 0, 0}, f_se[kMaxSoft] = {0, 0, 0, 0};
@@ -1146,18 +1195,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const int64_t gmax_t = get_i(6, OpMaxI32{}), gmax_a = get_i(7, OpMaxI32{});
     const long long gimin = do_ipa ? get_l(4, OpMinL{}) : 0, gimax = do_ipa ? get_l(5, OpMaxL{}) : 0;
     long long pmin = BIG, pmax = 0;
-    if (do_pts) {
-      for (int i = 0; i < g.n_soft; i++) {
-        const Slot& sl = s_t.soft[i];
-        if (g.soft[6 * i + 5] || sl.unique) continue;
-        const int bw = (sl.V + 31) / 32;
-        if (pmode) {   // or-ed into this workgroup's own marks
-          fold_words(sl.mark, bw, true);
-        } else {
-          for (int wd = tid; wd < bw; wd += BLOCK) s_hist[sl.mark + wd] = gld(&acc->hist[sl.mark + wd]);
-        }
-      }
-      __syncthreads();
+    if (do_pts) {   // (the marks were folded at the start of phase 3; the fold's barrier ordered them)
       for (int i = 0; i < g.n_soft; i++) {
         const Slot& sl = s_t.soft[i];
         if (g.soft[6 * i + 5] || sl.unique) continue;

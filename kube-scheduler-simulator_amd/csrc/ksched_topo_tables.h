@@ -38,6 +38,8 @@ struct TopoTables {
   const int32_t* sp_off;       // [S + 1]: selector s's (column, dom offset) pairs are sp[2 * sp_off[s] ..]
   const int32_t* sp;
   const uint8_t* elig;         // [pods of the run]: the pod's constraints are all within the tables' scope
+  const int4* fo;              // [pods of the run][kTopoFill]: per fill task (dom offset, presence offset,
+                               // column, selector), in ksg_topo_coop's slot order
   int32_t first;               // the run's first pod (elig index 0)
   int32_t S, L, Kc;
 };
@@ -92,12 +94,49 @@ __device__ __forceinline__ bool tables_scope(const DevCluster& c, const TopoTabl
   return e;
 }
 
-// One lane per pod of the run: tables_scope into elig (after ksg_topo_tables_init).
+constexpr int kTopoFill = 24;   // fill tasks per pod: kMaxHard + kMaxSoft + kMaxAff + kMaxAnti + kMaxPref
+
+// One lane per pod of the run: tables_scope into elig (after ksg_topo_tables_init)
+// and the pod's fill tasks: every non-unique slot's table offsets in the order
+// the topology kernel lays its histograms out (hard, soft without a hostname
+// key, affinity, anti-affinity, preferred), so the kernel's fill needs no
+// dependent index load.
 __global__ __launch_bounds__(64) void ksg_topo_tables_elig(DevCluster c, TopoTables t, const ksg_pod* pods,
-                                                           const int32_t* prog, int count, uint8_t* elig) {
+                                                           const int32_t* prog, int count, uint8_t* elig,
+                                                           int4* fo) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= count) return;
-  elig[i] = tables_scope(c, t, pods[t.first + i], prog) ? 1 : 0;
+  const ksg_pod& p = pods[t.first + i];
+  const bool e = tables_scope(c, t, p, prog);
+  elig[i] = e ? 1 : 0;
+  int4* out = fo + (size_t)i * kTopoFill;
+  int k = 0;
+  auto task = [&](int sel, int col, bool pres) {
+    if (k >= kTopoFill || col < 0 || col >= t.L || c.col_unique[col]) return;
+    const int off = sel >= 0 && sel < t.S ? t.pair_off[(size_t)sel * t.L + col] : -1;
+    out[k++] = make_int4(off, pres ? t.pres_off[col] : -1, col, sel);
+  };
+  if (e && p.pts >= 0) {
+    const int32_t* w = prog + p.pts;
+    const int nh = w[0], ns = w[1];
+    const int32_t* hard = w + 3;
+    for (int j = 0; j < nh && j < kMaxHard; j++) task(hard[7 * j + 1], hard[7 * j], true);
+    const int32_t* soft = hard + 7 * nh;
+    for (int j = 0; j < ns && j < kMaxSoft; j++)
+      if (!soft[6 * j + 5]) task(soft[6 * j + 1], soft[6 * j], false);
+  }
+  if (e && p.ipa >= 0) {
+    const int32_t* w = prog + p.ipa;
+    const int na = w[0], sel_all = w[1];
+    for (int j = 0; j < na && j < kMaxAff; j++) task(sel_all, w[3 + j], true);
+    w += 3 + na;
+    const int nanti = *w++;
+    for (int j = 0; j < nanti && j < kMaxAnti; j++) task(w[2 * j + 1], w[2 * j], true);
+    w += 2 * nanti;
+    const int npref = *w++;
+    for (int j = 0; j < npref && j < kMaxPref; j++) task(w[3 * j + 1], w[3 * j], true);
+  }
+  for (; k < kTopoFill; k++) out[k] = make_int4(-1, -1, -1, -1);
 }
 
 // One table-building task per workgroup (ksg_topo_tables_init).
