@@ -321,6 +321,16 @@ class Engine:
     def commit(self, pod: int, node: int):
         self._check(self._commit(self.ctx, pod, node))
 
+    def commit_batch(self, pods, nodes):
+        """ksg_commit_batch: NodeInfo.AddPod of pods[i] onto nodes[i], one launch
+        (the snapshot's replay of its bindings)."""
+        pods = np.ascontiguousarray(pods, np.int32)
+        nodes = np.ascontiguousarray(nodes, np.int32)
+        fn = getattr(self.lib, self.PREFIX + "commit_batch")
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, i32p, i32p, C.c_int32]
+        self._check(fn(self.ctx, _ptr(pods, i32p), _ptr(nodes, i32p), len(pods)))
+
     def uncommit(self, pod: int, node: int):
         """A preemption victim's deletion (ksg_uncommit: NodeInfo.RemovePod)."""
         self._check(self._uncommit(self.ctx, pod, node))

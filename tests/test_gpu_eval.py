@@ -250,3 +250,34 @@ def test_deferred_assume_reaches_every_reader(built):
     a.reset_state()   # a pending assume is dropped with the rest
     b.reset_state()
     same_state()
+
+
+def test_commit_batch_equals_sequential_commits(built):
+    """ksg_commit_batch (one launch, atomic additions; the snapshot's replay of
+    its bindings) leaves the node state, selector counts and template tables
+    exactly as one ksg_commit per pod does: later evaluations agree, topology
+    pods included."""
+    import zoo
+    nodes, pods, prof = zoo.zoo(1, n_nodes=300, n_pods=120)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    a = native.Engine(device=0)
+    b = _engine_with({"KSG_DEFER_COMMIT": "0"})
+    a.load(enc, pf)
+    b.load(enc, pf)
+    rng = np.random.default_rng(5)
+    bp = np.arange(0, 80, dtype=np.int32)
+    bn = rng.integers(0, len(nodes), size=len(bp)).astype(np.int32)
+    bn[:10] = 7   # several pods on one node: lanes sharing a node
+    a.commit_batch(bp, bn)
+    for q, n in zip(bp, bn):
+        b.commit(int(q), int(n))
+    R = len(enc.cluster.res_names)
+    for x, y in zip(a.read_state(R), b.read_state(R)):
+        np.testing.assert_array_equal(x, y)
+    for i in range(80, len(pods)):   # selector counts and template tables: later pods see the same state
+        ca, cb = native.CaptureBuffers(len(nodes), 1), native.CaptureBuffers(len(nodes), 1)
+        ra, rb = a.eval(i, ca), b.eval(i, cb)
+        assert (ra.selected, ra.n_feasible, ra.status) == (rb.selected, rb.n_feasible, rb.status), i
+        np.testing.assert_array_equal(ca.fstatus, cb.fstatus)
+        np.testing.assert_array_equal(ca.total, cb.total)
