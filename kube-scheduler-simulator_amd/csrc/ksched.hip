@@ -2595,7 +2595,7 @@ struct ksg_ctx {
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
   int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
   int cycle_block = 128;                    // env KSG_CYCLE_BLOCK: nodes per workgroup of ksg_eval_cycle (64/128/256)
-  bool cycle_sys = true;                    // env KSG_CYCLE_SYS=0: plain host stores + __threadfence_system
+  bool cycle_sys = false;                    // plain host stores + __threadfence_system (measured faster); env KSG_CYCLE_SYS=1: system-scope stores
   bool cycle_coop = false;                  // per-cycle launch: plain (G within the occupancy API's residency,
                                             // ~7 us less host time); cooperative after an exchange timeout,
                                             // or always with env KSG_CYCLE_COOP=1
