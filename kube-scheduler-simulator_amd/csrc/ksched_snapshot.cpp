@@ -510,7 +510,22 @@ struct ksg_snapshot {
   // terms resolve against these
   bool have_namespaces = false;
   std::map<std::string, StrMap> namespaces;
-  std::unordered_map<uint64_t, int32_t> status_seen;   // ksg_snapshot_statuses scratch
+  // ksg_snapshot_statuses: a status key's (code, message) is kept across
+  // pods until the next full encode (status_epoch); per call, stamp/local
+  // number the keys a pod meets in first-seen order
+  struct StatusCache {
+    int epoch = -1;
+    std::unordered_map<uint64_t, int32_t> ids;   // key -> id
+    std::vector<std::string> msgs;
+    std::vector<int32_t> codes;
+    std::vector<uint32_t> stamp;
+    std::vector<int32_t> local;
+    std::vector<int32_t> order;   // this call's ids, first-seen order
+    uint32_t gen = 0;
+    static constexpr int kDm = 256;   // direct-mapped front of `ids`
+    uint64_t dm_key[kDm];
+    int32_t dm_id[kDm];
+  } status;
 };
 
 namespace {
@@ -1631,6 +1646,24 @@ void validate_pod(const ksg_snapshot* s, const Pod& p) {
     throw EncodeError{KSG_E_UNSUPPORTED, "more than " + std::to_string(KSG_MAX_RES) + " resource columns"};
 }
 
+// ksg_snapshot_statuses' scan of one block of 64 nodes: stores the passed
+// defaults (code Success, no message) and returns the rejected nodes as a
+// bit mask (a word other than 0 / KSG_FS_NOT_EVALUATED).  (An AVX2 form was
+// no faster: the pass is bound by its stores.)
+uint64_t scan_block_sse2(const uint32_t* w, int32_t* code, int32_t* msg) {
+  const __m128i v_pass = _mm_setzero_si128(), v_ne = _mm_set1_epi32((int)KSG_FS_NOT_EVALUATED);
+  const __m128i v_ok = _mm_set1_epi32((int)KSG_CODE_SUCCESS), v_none = _mm_set1_epi32(-1);
+  uint64_t mask = 0;
+  for (int i = 0; i < 64; i += 4) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(w + i));
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(code + i), v_ok);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(msg + i), v_none);
+    const __m128i ok = _mm_or_si128(_mm_cmpeq_epi32(v, v_pass), _mm_cmpeq_epi32(v, v_ne));
+    mask |= (uint64_t)(~_mm_movemask_ps(_mm_castsi128_ps(ok)) & 0xf) << i;
+  }
+  return mask;
+}
+
 // framework.Status (code, Message()) of a Filter status word at `node` for
 // `pod`; msg may be null when only the code is wanted.
 bool status_of(const Encoded& e, int32_t pod, uint32_t word, int32_t node, int* code, std::string* msg,
@@ -2083,42 +2116,50 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     return fail(s, KSG_E_INVALID, "statuses: index out of range");
   const Encoded& e = s->e;
   // distinct messages: keyed by the word, plus the taint id for TaintToleration.
-  // The code depends on the node only for NodeResourcesFit (a request above
-  // the node's allocatable is unresolvable); every other code is cached with
-  // its message.  Neighbouring nodes mostly repeat a word: last-key shortcut.
-  auto& seen = s->status_seen;   // reused across calls (no rehash per pod)
-  seen.clear();
-  std::vector<std::string> msgs;
-  std::vector<int32_t> codes;
+  // A key's message and code depend on nothing else (the taint strings and
+  // resource names change only with a full encode), except NodeResourcesFit's
+  // code, recomputed per node below (a request above the node's allocatable
+  // is unresolvable).  So keys are formatted once per encoding, not per pod;
+  // a call numbers the keys it meets in first-seen order.  Neighbouring nodes
+  // mostly repeat a word: last-key shortcut, then a direct-mapped cache.
+  auto& sc = s->status;
+  if (sc.epoch != s->epoch) {
+    sc.ids.clear();
+    sc.msgs.clear();
+    sc.codes.clear();
+    sc.stamp.clear();
+    sc.local.clear();
+    for (int i = 0; i < sc.kDm; i++) sc.dm_key[i] = ~0ull;
+    sc.epoch = s->epoch;
+  }
+  if (++sc.gen == 0) {   // stamp wrap: forget every call's stamp
+    std::fill(sc.stamp.begin(), sc.stamp.end(), 0u);
+    sc.gen = 1;
+  }
+  const uint32_t gen = sc.gen;
+  sc.order.clear();
   const ksg_pod& p = e.pods[pod];
   uint64_t last_key = ~0ull;
   int32_t last_idx = -1;
-  // a direct-mapped cache in front of the map: the distinct keys of one pod
-  // are few (a plugin, a reason set, a taint), the rejected nodes many
-  constexpr int kDm = 256;
-  uint64_t dm_key[kDm];
-  int32_t dm_idx[kDm];
-  for (int i = 0; i < kDm; i++) dm_key[i] = ~0ull;
   std::string err;
-  // Most nodes pass: the passed defaults are filled first, then each block of
-  // 64 nodes yields its rejected nodes as a 64-bit mask (SSE2 compares), which
-  // are decoded one by one.
-  std::fill(code, code + n_nodes, (int32_t)KSG_CODE_SUCCESS);
-  std::fill(msg, msg + n_nodes, (int32_t)-1);
+  // Most nodes pass: each block of 64 nodes stores the passed defaults and
+  // yields its rejected nodes as a 64-bit mask in the same pass; the rejected
+  // nodes are then decoded one by one.
   constexpr int32_t kB = 64;
-  const __m128i v_pass = _mm_setzero_si128(), v_ne = _mm_set1_epi32((int)KSG_FS_NOT_EVALUATED);
+  const uint32_t* taints = e.taints.data();
+  const size_t N = (size_t)e.N;
+  const uint32_t max_taints = (uint32_t)std::max(e.max_taints, 0);
+  int32_t last_code = 0;
   for (int32_t b = 0; b < n_nodes; b += kB) {
     const int32_t m = std::min(kB, n_nodes - b);
     uint64_t mask = 0;   // the block's rejected nodes: four words per compare
     if (m == kB) {
-      for (int32_t i = 0; i < kB; i += 4) {
-        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(words + b + i));
-        const __m128i ok = _mm_or_si128(_mm_cmpeq_epi32(v, v_pass), _mm_cmpeq_epi32(v, v_ne));
-        mask |= (uint64_t)(~_mm_movemask_ps(_mm_castsi128_ps(ok)) & 0xf) << i;
-      }
+      mask = scan_block_sse2(words + b, code + b, msg + b);
     } else {
       for (int32_t i = 0; i < m; i++) {
         const uint32_t w = words[b + i];
+        code[b + i] = KSG_CODE_SUCCESS;
+        msg[b + i] = -1;
         mask |= (uint64_t)(w != 0 && w != KSG_FS_NOT_EVALUATED) << i;
       }
     }
@@ -2127,50 +2168,56 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     const uint32_t w = words[n];
     const int pl = (int)(w & 0xffu) - 1;
     uint64_t key = w;
-    if (pl == KSG_PL_TAINT_TOLERATION && (int)(w >> 8) < e.max_taints)
-      key |= (uint64_t)e.taints[(size_t)(w >> 8) * e.N + n] << 32;
-    int32_t idx;
-    const int slot = (int)((key * 0x9E3779B97F4A7C15ull) >> 56);
-    if (key == last_key) {
-      idx = last_idx;
-    } else if (dm_key[slot] == key) {
-      idx = dm_idx[slot];
-      last_key = key;
-      last_idx = idx;
-    } else {
-      auto it = seen.find(key);
-      if (it == seen.end()) {
-        std::string m;
-        int c;
-        if (!status_of(e, pod, w, n, &c, &m, &err)) return fail(s, KSG_E_INVALID, "statuses: " + err);
-        it = seen.emplace(key, (int32_t)msgs.size()).first;
-        msgs.push_back(std::move(m));
-        codes.push_back(c);
+    if (pl == KSG_PL_TAINT_TOLERATION && (w >> 8) < max_taints) key |= (uint64_t)taints[(w >> 8) * N + n] << 32;
+    if (key != last_key) {
+      int32_t id;
+      const int slot = (int)((key * 0x9E3779B97F4A7C15ull) >> 56);
+      if (sc.dm_key[slot] == key) {
+        id = sc.dm_id[slot];
+      } else {
+        auto it = sc.ids.find(key);
+        if (it == sc.ids.end()) {
+          std::string m;
+          int c;
+          if (!status_of(e, pod, w, n, &c, &m, &err)) return fail(s, KSG_E_INVALID, "statuses: " + err);
+          it = sc.ids.emplace(key, (int32_t)sc.msgs.size()).first;
+          sc.msgs.push_back(std::move(m));
+          sc.codes.push_back(c);
+          sc.stamp.push_back(0u);
+          sc.local.push_back(-1);
+        }
+        id = it->second;
+        sc.dm_key[slot] = key;
+        sc.dm_id[slot] = id;
       }
-      idx = it->second;
-      dm_key[slot] = key;
-      dm_idx[slot] = idx;
+      if (sc.stamp[id] != gen) {
+        sc.stamp[id] = gen;
+        sc.local[id] = (int32_t)sc.order.size();
+        sc.order.push_back(id);
+      }
       last_key = key;
-      last_idx = idx;
+      last_idx = sc.local[id];
+      last_code = sc.codes[id];
     }
-    int c = codes[idx];
+    int c = last_code;
     if (pl == KSG_PL_NODE_RESOURCES_FIT) {   // status_of's Fit code, per node
       const uint32_t reason = w >> 8;
       c = KSG_CODE_UNSCHEDULABLE;
       for (size_t r = 0; r < e.res_names.size(); r++)
-        if ((reason & (1u << (r + 1))) && p.req[r] > e.alloc[r * e.N + n]) c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+        if ((reason & (1u << (r + 1))) && p.req[r] > e.alloc[r * N + n]) c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     }
     code[n] = c;
-    msg[n] = idx;
+    msg[n] = last_idx;
     }
   }
   int64_t total = 0;
-  for (auto& m : msgs) total += (int64_t)m.size() + 1;
-  if (n_msgs) *n_msgs = (int32_t)msgs.size();
+  for (int32_t id : sc.order) total += (int64_t)sc.msgs[id].size() + 1;
+  if (n_msgs) *n_msgs = (int32_t)sc.order.size();
   if (len) *len = total;
   if (buf && cap >= total) {
     char* o = buf;
-    for (auto& m : msgs) {
+    for (int32_t id : sc.order) {
+      const std::string& m = sc.msgs[id];
       std::memcpy(o, m.data(), m.size());
       o += m.size();
       *o++ = 0;

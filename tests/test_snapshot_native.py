@@ -215,6 +215,36 @@ def test_status_codes_and_messages(built):
     assert {P.TAINT_TOLERATION, P.NODE_RESOURCES_FIT} <= seen
 
 
+def test_statuses_cache_follows_reencode(built):
+    """ksg_snapshot_statuses keeps each key's message across pods until the
+    next full encode.  A node with a scalar resource that sorts first
+    renumbers the resource columns, so the same Fit word names another
+    resource after the re-encode; every decode must agree with the per-node
+    call (words made up, every node rejected by the one word)."""
+    import dataclasses
+    nodes, pods, prof = zoo.zoo(2)
+    snap = S.Snapshot(prof, nodes, pods)
+    snap.encode()
+    fit4 = (P.NODE_RESOURCES_FIT + 1) | ((1 << 4) << 8)   # resource column 3
+
+    def texts_of(n_nodes):
+        out = set()
+        for pi in (0, 1, 0):
+            w = np.full(n_nodes, fit4, np.uint32)
+            codes, idx, texts = snap.statuses(pi, w)
+            for n in range(n_nodes):
+                assert (int(codes[n]), texts[idx[n]]) == snap.status(pi, fit4, n)
+            out |= set(texts)
+        return out
+
+    before = texts_of(len(nodes))
+    extra = dataclasses.replace(nodes[0], name="aaa-extra", allocatable={**nodes[0].allocatable, "aaa.com/first": 1})
+    snap.add_node(extra)
+    snap.encode()
+    after = texts_of(len(nodes) + 1)
+    assert before == {"Insufficient example.com/fpga"} and after == {"Insufficient aaa.com/first"}
+
+
 def test_prefilter_statuses(built):
     nodes, pods, prof = zoo.zoo(4)
     enc = E.Encoder(nodes, pods, prof)
