@@ -374,7 +374,8 @@ type ProfileArgs struct {
 
 // Snapshot is one ksg_snapshot (not thread-safe; the caller serialises).
 type Snapshot struct {
-	s *C.ksg_snapshot
+	s      *C.ksg_snapshot
+	msgBuf []byte // Statuses' message texts, kept across calls (callers serialise, as the C snapshot requires)
 }
 
 func (x *Snapshot) check(rc C.int) error {
@@ -533,29 +534,38 @@ func (x *Snapshot) Status(pod int, word uint32, node int) (int, string, error) {
 
 // Statuses decodes every node's Filter status word of a pod at once
 // (ksg_snapshot_statuses): codes[n] (Code*), msg[n] = index into msgs, -1
-// for success / not evaluated.
+// for success / not evaluated.  One C call writes straight into the result
+// slices (plain int32 / uint32 memory, valid to pass for the call) and into
+// the Snapshot's message buffer; a second call only when the texts outgrow it.
 func (x *Snapshot) Statuses(pod int, words []uint32) (codes, msg []int32, msgs []string, err error) {
 	n := len(words)
-	cw := (*C.uint32_t)(C.malloc(C.size_t(4 * (n + 1))))
-	defer C.free(unsafe.Pointer(cw))
-	copy(unsafe.Slice((*uint32)(unsafe.Pointer(cw)), n), words)
-	cc := (*C.int32_t)(C.malloc(C.size_t(4 * (n + 1))))
-	defer C.free(unsafe.Pointer(cc))
-	cm := (*C.int32_t)(C.malloc(C.size_t(4 * (n + 1))))
-	defer C.free(unsafe.Pointer(cm))
+	codes = make([]int32, n, n+1) // capacity n+1: a valid first element even for n == 0
+	msg = make([]int32, n, n+1)
+	wp := words
+	if n == 0 {
+		wp = make([]uint32, 1)
+	}
+	if len(x.msgBuf) == 0 {
+		x.msgBuf = make([]byte, 1<<16)
+	}
 	var nm C.int32_t
 	var ln C.int64_t
-	if err = x.check(C.ksg_snapshot_statuses(x.s, C.int32_t(pod), cw, C.int32_t(n), cc, cm, nil, 0, &nm, &ln)); err != nil {
-		return
+	call := func() error {
+		return x.check(C.ksg_snapshot_statuses(x.s, C.int32_t(pod), (*C.uint32_t)(unsafe.Pointer(&wp[0])), C.int32_t(n),
+			(*C.int32_t)(unsafe.Pointer(&codes[:1][0])), (*C.int32_t)(unsafe.Pointer(&msg[:1][0])),
+			(*C.char)(unsafe.Pointer(&x.msgBuf[0])), C.int64_t(len(x.msgBuf)), &nm, &ln))
 	}
-	buf := (*C.char)(C.malloc(C.size_t(ln) + 1))
-	defer C.free(unsafe.Pointer(buf))
-	if err = x.check(C.ksg_snapshot_statuses(x.s, C.int32_t(pod), cw, C.int32_t(n), cc, cm, buf, ln+1, &nm, &ln)); err != nil {
-		return
+	if err = call(); err != nil {
+		return nil, nil, nil, err
 	}
-	codes = append([]int32(nil), unsafe.Slice((*int32)(unsafe.Pointer(cc)), n)...)
-	msg = append([]int32(nil), unsafe.Slice((*int32)(unsafe.Pointer(cm)), n)...)
-	raw := C.GoBytes(unsafe.Pointer(buf), C.int(ln))
+	if int64(ln) > int64(len(x.msgBuf)) { // the texts did not fit: once more with a buffer that does
+		x.msgBuf = make([]byte, int64(ln)+1)
+		if err = call(); err != nil {
+			return nil, nil, nil, err
+		}
+	}
+	raw := x.msgBuf[:ln]
+	msgs = make([]string, 0, int(nm))
 	start := 0
 	for i := 0; i < len(raw) && len(msgs) < int(nm); i++ {
 		if raw[i] == 0 {
