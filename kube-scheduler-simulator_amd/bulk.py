@@ -55,13 +55,15 @@ class BulkAnnotator:
         nf = int(res["n_feasible"][k])
         sskip = int(res["score_skip"][k])
         sorder = [p for p in self.score_order if not (sskip >> p) & 1] if nf >= 2 else []
-        return ann.annotate_bytes(order, sorder, self.norm_mask, self.weights, nf, cap.fstatus[k], cap.raw[k],
+        return ann.annotate_views(order, sorder, self.norm_mask, self.weights, nf, cap.fstatus[k], cap.raw[k],
                                   cap.norm[k])
 
     def serialise(self, first: int, res, cap: native.CaptureBuffers, count: int,
                   sink: Callable[[int, tuple], None]):
         """ksg_annotate for pods first .. first + count of a captured chunk;
-        sink(pod index, (filter, score, finalscore) bytes) in pod order per worker."""
+        sink(pod index, (filter, score, finalscore)) in pod order per worker; the
+        values are read-only memoryviews valid for the sink call only (bytes(v)
+        keeps one; hash.update(v) reads it in place)."""
         T = len(self.annotators)
 
         def work(t):

@@ -9,8 +9,14 @@
 // encoding/json output: map keys sorted bytewise, HTML-safe escaping of < > &,
 // U+2028/U+2029 escaped, invalid UTF-8 replaced by U+FFFD, \b \f \n \r \t
 // short escapes, other control characters as \u00XX.
+//
+// Output side: each value goes into a raw append buffer kept by the annotator
+// (reserved once per node for that node's worst case, then plain stores);
+// node keys are escaped once per annotator, a passing node's filter entries
+// are one fragment per call, integers are written right to left.
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -75,32 +81,69 @@ void go_string(std::string& o, const char* s) {
   o.push_back('"');
 }
 
-void go_int(std::string& o, int64_t v) {
-  char b[24];
-  int n = 0;
-  uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
-  do { b[n++] = (char)('0' + u % 10); u /= 10; } while (u);
-  o.push_back('"');
-  if (v < 0) o.push_back('-');
-  while (n) o.push_back(b[--n]);
-  o.push_back('"');
-}
-
 const char* kFitRes[3] = {"cpu", "memory", "ephemeral-storage"};
+
+// A growable byte buffer without initialisation on growth: reserve() for the
+// worst case of what follows, then put() / ch() store without checks.
+struct Buf {
+  char* d = nullptr;
+  size_t n = 0, cap = 0;
+  Buf() = default;
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  ~Buf() { std::free(d); }
+  bool reserve(size_t k) {   // room for k more bytes and a terminating NUL
+    if (n + k + 1 <= cap) return true;
+    const size_t c = std::max(cap * 2, n + k + 1 + ((size_t)1 << 16));
+    char* x = static_cast<char*>(std::realloc(d, c));
+    if (!x) return false;
+    d = x;
+    cap = c;
+    return true;
+  }
+  void put(const char* s, size_t k) {
+    std::memcpy(d + n, s, k);
+    n += k;
+  }
+  void put(const std::string& s) { put(s.data(), s.size()); }
+  void ch(char c) { d[n++] = c; }
+  void qint(int64_t v) {   // "<decimal>" (go_int's bytes); at most 22 bytes
+    char t[24];
+    char* e = t + sizeof t;
+    char* q = e;
+    uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    do {
+      *--q = (char)('0' + u % 10);
+      u /= 10;
+    } while (u);
+    if (v < 0) *--q = '-';
+    d[n++] = '"';
+    put(q, (size_t)(e - q));
+    d[n++] = '"';
+  }
+};
+constexpr size_t kQint = 22;
 
 }  // namespace
 
 struct ksg_annotator {
   int32_t N = 0;
-  std::vector<std::string> node_json;     // escaped, quoted node names
+  std::vector<std::string> node_json;     // escaped, quoted node names, then ':'
+  size_t node_json_max = 0;
   std::vector<int32_t> node_order;        // node indices sorted bytewise by name
-  std::string plugin[KSG_NPLUGINS];       // escaped, quoted plugin names
+  std::string plugin[KSG_NPLUGINS];       // escaped, quoted plugin names, then ':'
   std::string plugin_raw[KSG_NPLUGINS];
   std::vector<std::string> res;           // resource names
   std::vector<std::string> taint;         // "{key: value}" per taint-vocab id
   int32_t max_taints = 0;
   std::vector<uint32_t> taints;           // [max_taints][N]
-  std::string out[3];
+  Buf out[3];
+  std::string pass_all, msg;   // per-call scratch
+  // a rejected node's message, JSON-escaped, by status key (the word, plus the
+  // taint id for TaintToleration): direct-mapped, valid for one call
+  static constexpr int kMsgSlots = 64;
+  uint64_t msg_key[kMsgSlots];
+  std::string msg_json[kMsgSlots];
 };
 
 extern "C" int ksg_annotator_new(const ksg_names* names, ksg_annotator** out) {
@@ -113,6 +156,8 @@ extern "C" int ksg_annotator_new(const ksg_names* names, ksg_annotator** out) {
   a->node_order.resize(a->N);
   for (int i = 0; i < a->N; i++) {
     go_string(a->node_json[i], names->node[i] ? names->node[i] : "");
+    a->node_json[i].push_back(':');
+    a->node_json_max = std::max(a->node_json_max, a->node_json[i].size());
     a->node_order[i] = i;
   }
   std::stable_sort(a->node_order.begin(), a->node_order.end(), [&](int x, int y) {
@@ -122,6 +167,7 @@ extern "C" int ksg_annotator_new(const ksg_names* names, ksg_annotator** out) {
     const char* s = names->plugin[p] ? names->plugin[p] : "";
     a->plugin_raw[p] = s;
     go_string(a->plugin[p], s);
+    a->plugin[p].push_back(':');
   }
   for (int r = 0; r < names->n_res; r++) a->res.emplace_back(names->res[r] ? names->res[r] : "");
   for (int t = 0; t < names->n_taint_vocab; t++) a->taint.emplace_back(names->taint[t] ? names->taint[t] : "");
@@ -201,10 +247,11 @@ extern "C" int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const c
   for (int i = 0; i < in->n_score; i++)
     if (in->score_order[i] < 0 || in->score_order[i] >= KSG_NPLUGINS) return KSG_E_INVALID;
   const int N = a->N;
+  for (auto& b : a->out) b.n = 0;
   // ---- filter-result (store.go:423; nodes outside PreFilterResult absent)
-  std::string& f = a->out[0];
-  f.clear();
-  f.push_back('{');
+  Buf& f = a->out[0];
+  if (!f.reserve(2)) return KSG_E_NOMEM;
+  f.ch('{');
   if (in->n_filter > 0) {
     // position of each plugin in run order; a node's entries are the plugins
     // up to and including the first rejecting one
@@ -212,77 +259,108 @@ extern "C" int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const c
     for (int p = 0; p < KSG_NPLUGINS; p++) pos[p] = -1;
     for (int i = 0; i < in->n_filter; i++) pos[in->filter_order[i]] = i;
     const std::vector<int> by_name = sorted_plugins(a, in->filter_order, in->n_filter);
-    std::string msg;
+    for (auto& k : a->msg_key) k = ~0ull;
+    // a passing node's entries: every plugin that ran, "passed"
+    std::string& pass_all = a->pass_all;
+    pass_all.assign(1, '{');
+    size_t keys = 0;
+    for (int p : by_name) {
+      if (pass_all.size() > 1) pass_all.push_back(',');
+      pass_all += a->plugin[p];
+      pass_all += "\"passed\"";
+      keys += a->plugin[p].size() + 1;
+    }
+    pass_all.push_back('}');
+    const size_t pass_bound = a->node_json_max + 1 + pass_all.size();
     bool first_node = true;
     for (int k = 0; k < N; k++) {
       const int n = a->node_order[k];
       const uint32_t st = in->fstatus[n];
       if (st == KSG_FS_NOT_EVALUATED) continue;
-      const int fail = st == 0 ? -1 : (int)(st & 0xFF) - 1;
-      const int last = fail < 0 ? in->n_filter : (fail < KSG_NPLUGINS ? pos[fail] : -1);
+      if (st == 0) {
+        if (!f.reserve(pass_bound)) return KSG_E_NOMEM;
+        if (!first_node) f.ch(',');
+        first_node = false;
+        f.put(a->node_json[n]);
+        f.put(pass_all);
+        continue;
+      }
+      const int fail = (int)(st & 0xFF) - 1;
+      const int last = fail < KSG_NPLUGINS ? pos[fail] : -1;
       if (last < 0) return KSG_E_INVALID;   // rejected by a plugin that did not run
-      if (fail >= 0 && !filter_message(a, st, n, msg)) return KSG_E_INVALID;
-      if (!first_node) f.push_back(',');
+      uint64_t key = st;
+      if (fail == KSG_PL_TAINT_TOLERATION && (int)(st >> 8) < a->max_taints)
+        key |= (uint64_t)a->taints[(size_t)(st >> 8) * N + n] << 32;
+      const int slot = (int)((key * 0x9E3779B97F4A7C15ull) >> 58);
+      std::string& mj = a->msg_json[slot];
+      if (a->msg_key[slot] != key) {
+        if (!filter_message(a, st, n, a->msg)) return KSG_E_INVALID;
+        mj.clear();
+        go_string(mj, a->msg.c_str());
+        a->msg_key[slot] = key;
+      }
+      if (!f.reserve(a->node_json_max + 3 + keys + by_name.size() * 8 + mj.size())) return KSG_E_NOMEM;
+      if (!first_node) f.ch(',');
       first_node = false;
-      f += a->node_json[n];
-      f += ":{";
+      f.put(a->node_json[n]);
+      f.ch('{');
       bool first = true;
       for (int p : by_name) {
         if (pos[p] > last) continue;
-        if (!first) f.push_back(',');
+        if (!first) f.ch(',');
         first = false;
-        f += a->plugin[p];
-        f.push_back(':');
-        if (p == fail) go_string(f, msg.c_str());
-        else f += "\"passed\"";
+        f.put(a->plugin[p]);
+        if (p == fail) f.put(mj);
+        else f.put("\"passed\"", 8);
       }
-      f.push_back('}');
+      f.ch('}');
     }
   }
-  f.push_back('}');
+  f.ch('}');
   // ---- score-result / finalscore-result (store.go:461, :481, :504-507)
-  std::string& s = a->out[1];
-  std::string& t = a->out[2];
-  s.clear();
-  t.clear();
-  s.push_back('{');
-  t.push_back('{');
+  Buf& s = a->out[1];
+  Buf& t = a->out[2];
+  if (!s.reserve(2) || !t.reserve(2)) return KSG_E_NOMEM;
+  s.ch('{');
+  t.ch('{');
   if (in->n_feasible >= 2 && in->n_score > 0) {
     if (!in->raw || !in->weight) return KSG_E_INVALID;
     const std::vector<int> by_name = sorted_plugins(a, in->score_order, in->n_score);
+    size_t bound = a->node_json_max + 3;
+    for (int p : by_name) bound += a->plugin[p].size() + 1 + kQint;
     bool first_node = true;
     for (int k = 0; k < N; k++) {
       const int n = a->node_order[k];
       if (in->fstatus[n] != 0) continue;
-      if (!first_node) { s.push_back(','); t.push_back(','); }
+      if (!s.reserve(bound) || !t.reserve(bound)) return KSG_E_NOMEM;
+      if (!first_node) { s.ch(','); t.ch(','); }
       first_node = false;
-      s += a->node_json[n];
-      s += ":{";
-      t += a->node_json[n];
-      t += ":{";
+      s.put(a->node_json[n]);
+      s.ch('{');
+      t.put(a->node_json[n]);
+      t.ch('{');
       bool first = true;
       for (int p : by_name) {
-        if (!first) { s.push_back(','); t.push_back(','); }
+        if (!first) { s.ch(','); t.ch(','); }
         first = false;
-        s += a->plugin[p];
-        s.push_back(':');
-        t += a->plugin[p];
-        t.push_back(':');
+        s.put(a->plugin[p]);
+        t.put(a->plugin[p]);
         const int64_t raw = in->raw[(size_t)p * N + n];
-        go_int(s, raw);
+        s.qint(raw);
         const bool normed = ((in->normalize_mask >> p) & 1u) && in->norm;
         const uint64_t v = (uint64_t)(normed ? in->norm[(size_t)p * N + n] : raw) * (uint64_t)in->weight[p];
-        go_int(t, (int64_t)v);   // Go int64 multiplication wraps
+        t.qint((int64_t)v);   // Go int64 multiplication wraps
       }
-      s.push_back('}');
-      t.push_back('}');
+      s.ch('}');
+      t.ch('}');
     }
   }
-  s.push_back('}');
-  t.push_back('}');
+  s.ch('}');
+  t.ch('}');
   for (int i = 0; i < 3; i++) {
-    json[i] = a->out[i].c_str();
-    len[i] = (int64_t)a->out[i].size();
+    a->out[i].d[a->out[i].n] = 0;
+    json[i] = a->out[i].d;
+    len[i] = (int64_t)a->out[i].n;
   }
   return KSG_OK;
 }

@@ -443,11 +443,15 @@ class Annotator:
         self._free = f("annotator_free", C.c_int, C.c_void_p)
         self._annotate = f("annotate", C.c_int, C.c_void_p, C.POINTER(KsgAnnotateIn),
                            C.POINTER(C.c_char_p), C.POINTER(C.c_int64))
+        # the same entry point, its strings taken as plain addresses (annotate_views)
+        self._annotate_v = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(KsgAnnotateIn), C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_int64))(("ksg_annotate", self.lib))
         self._keep = [_cstrs(node_names), _cstrs(plugin_names), _cstrs(res_names), _cstrs(taint_strings),
                       np.ascontiguousarray(taints, np.uint32)]
         names = KsgNames(len(node_names), self._keep[0], self._keep[1], len(res_names), self._keep[2],
                          len(taint_strings), self._keep[3], int(self._keep[4].shape[0]),
                          _ptr(self._keep[4], u32p))
+        self._view_bufs = [np.empty(0, np.uint8) for _ in range(3)]
         self.h = C.c_void_p()
         rc = self._new(C.byref(names), C.byref(self.h))
         if rc != 0:
@@ -475,6 +479,35 @@ class Annotator:
         if rc != 0:
             raise KschedError(f"ksg_annotate rc={rc}")
         return tuple(C.string_at(out[i], ln[i]) for i in range(3))
+
+    def annotate_views(self, filter_order, score_order, normalize_mask: int, weight, n_feasible: int,
+                       fstatus: np.ndarray, raw: np.ndarray, norm: np.ndarray):
+        """annotate_bytes' values as read-only memoryviews, valid until this
+        annotator's next call (as the C strings are).  They are copied out by
+        ctypes.memmove into buffers the annotator keeps: every byte moves with
+        the GIL released and no page is faulted in again per call, so worker
+        threads serialise in parallel (string_at copies under the GIL)."""
+        fo = np.ascontiguousarray(filter_order, np.int32)
+        so = np.ascontiguousarray(score_order, np.int32)
+        w = np.ascontiguousarray(weight, np.int64)
+        fs = np.ascontiguousarray(fstatus, np.uint32)
+        rw = np.ascontiguousarray(raw, np.int64)
+        nm = np.ascontiguousarray(norm, np.int64)
+        inp = KsgAnnotateIn(len(fo), _ptr(fo, i32p), len(so), _ptr(so, i32p), normalize_mask, _ptr(w, i64p),
+                            n_feasible, _ptr(fs, u32p), _ptr(rw, i64p), _ptr(nm, i64p))
+        out = (C.c_void_p * 3)()
+        ln = (C.c_int64 * 3)()
+        rc = self._annotate_v(self.h, C.byref(inp), out, ln)
+        if rc != 0:
+            raise KschedError(f"ksg_annotate rc={rc}")
+        bufs = self._view_bufs
+        views = []
+        for i in range(3):
+            if len(bufs[i]) < ln[i]:
+                bufs[i] = np.empty(max(ln[i], 2 * len(bufs[i])), np.uint8)
+            C.memmove(bufs[i].ctypes.data, out[i], ln[i])
+            views.append(memoryview(bufs[i])[:ln[i]].toreadonly())
+        return tuple(views)
 
     def close(self):
         if self.h:

@@ -36,7 +36,7 @@ def _bulk(nodes, pods, prof, engine, threads, chunk):
 
     def sink(i, vals):
         with lock:
-            got[i] = tuple(v.decode("utf-8") for v in vals)
+            got[i] = tuple(bytes(v).decode("utf-8") for v in vals)
 
     try:
         pl = B.annotate_queue(engine, bulk, 0, len(pods), sink, chunk=chunk)
