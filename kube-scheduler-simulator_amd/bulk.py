@@ -35,9 +35,12 @@ class BulkAnnotator:
                            for _ in range(max(1, threads))]
         store_w = prof.weights()
         self.weights = np.array([store_w.get(n, 0) for n in P.PLUGIN_NAMES], np.int64)
+        self._w_addr = self.weights.ctypes.data
         self.norm_mask = sum(1 << pid for pid in range(len(P.PLUGIN_NAMES)) if P.EXT[pid][4])
         self.filter_order = prof.filter_order()
         self.score_order = prof.score_order()
+        self.fskip = enc.workload.pods["filter_skip"].astype(np.int64).tolist()
+        self._orders = {}   # (filter skips, score skips or -1) -> (arrays, lengths, addresses)
         self.pool = ThreadPoolExecutor(max_workers=len(self.annotators)) if len(self.annotators) > 1 else None
 
     def close(self):
@@ -46,17 +49,32 @@ class BulkAnnotator:
         for a in self.annotators:
             a.close()
 
+    def _order(self, fskip: int, sskip: int):
+        """The plugins that ran, per (filter skips, score skips), as int32 arrays
+        kept alive here with their addresses (a few distinct keys per queue)."""
+        key = (fskip, sskip)
+        v = self._orders.get(key)
+        if v is None:
+            fo = np.array([p for p in self.filter_order if not (fskip >> p) & 1], np.int32)
+            so = np.array([p for p in self.score_order if not (sskip >> p) & 1] if sskip >= 0 else [], np.int32)
+            v = (fo, so, len(fo), fo.ctypes.data, len(so), so.ctypes.data)
+            self._orders[key] = v
+        return v
+
     def _pod(self, ann: native.Annotator, k: int, pi: int, res, cap: native.CaptureBuffers):
-        rec = self.enc.workload.pods[pi]
-        fskip = int(rec["filter_skip"])
-        if int(res["status"][k]) & native.ST_IPA_PREFILTER_SKIP:
+        st, nf, sskip = int(res["status"][k]), int(res["n_feasible"][k]), int(res["score_skip"][k])
+        return self._pod_at(ann, k, pi, st, nf, sskip, cap)
+
+    def _pod_at(self, ann: native.Annotator, k: int, pi: int, status: int, nf: int, sskip: int,
+                cap: native.CaptureBuffers):
+        fskip = self.fskip[pi]
+        if status & native.ST_IPA_PREFILTER_SKIP:
             fskip |= 1 << P.INTER_POD_AFFINITY
-        order = [p for p in self.filter_order if not (fskip >> p) & 1]
-        nf = int(res["n_feasible"][k])
-        sskip = int(res["score_skip"][k])
-        sorder = [p for p in self.score_order if not (sskip >> p) & 1] if nf >= 2 else []
-        return ann.annotate_views(order, sorder, self.norm_mask, self.weights, nf, cap.fstatus[k], cap.raw[k],
-                                  cap.norm[k])
+        _, _, nfo, fo, nso, so = self._order(fskip, sskip if nf >= 2 else -1)
+        N = self.n_nodes
+        return ann.annotate_at(nfo, fo, nso, so, self.norm_mask, self._w_addr, nf,
+                               cap.fstatus.ctypes.data + 4 * N * k, cap.raw.ctypes.data + 8 * native.NPLUGINS * N * k,
+                               cap.norm.ctypes.data + 8 * native.NPLUGINS * N * k)
 
     def serialise(self, first: int, res, cap: native.CaptureBuffers, count: int,
                   sink: Callable[[int, tuple], None]):
@@ -65,10 +83,13 @@ class BulkAnnotator:
         values are read-only memoryviews valid for the sink call only (bytes(v)
         keeps one; hash.update(v) reads it in place)."""
         T = len(self.annotators)
+        status, nfeas, sskip = (res[f][:count].tolist() for f in ("status", "n_feasible", "score_skip"))
+        assert cap.fstatus.shape == (cap.fstatus.shape[0], self.n_nodes) and count <= cap.fstatus.shape[0]
 
         def work(t):
+            ann = self.annotators[t]
             for k in range(t, count, T):
-                sink(first + k, self._pod(self.annotators[t], k, first + k, res, cap))
+                sink(first + k, self._pod_at(ann, k, first + k, status[k], nfeas[k], sskip[k], cap))
 
         if self.pool is None:
             work(0)

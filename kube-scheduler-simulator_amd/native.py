@@ -421,6 +421,13 @@ class KsgAnnotateIn(C.Structure):
                 ("fstatus", u32p), ("raw", i64p), ("norm", i64p)]
 
 
+class KsgAnnotateInAt(C.Structure):
+    """ksg_annotate_in with its pointers as plain addresses (Annotator.annotate_at)."""
+    _fields_ = [("n_filter", C.c_int32), ("filter_order", C.c_void_p), ("n_score", C.c_int32),
+                ("score_order", C.c_void_p), ("normalize_mask", C.c_uint32), ("weight", C.c_void_p),
+                ("n_feasible", C.c_int32), ("fstatus", C.c_void_p), ("raw", C.c_void_p), ("norm", C.c_void_p)]
+
+
 def _cstrs(items):
     arr = (C.c_char_p * max(len(items), 1))()
     for i, s in enumerate(items):
@@ -446,6 +453,11 @@ class Annotator:
         # the same entry point, its strings taken as plain addresses (annotate_views)
         self._annotate_v = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(KsgAnnotateIn), C.POINTER(C.c_void_p),
                                        C.POINTER(C.c_int64))(("ksg_annotate", self.lib))
+        self._annotate_at = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_int64))(("ksg_annotate", self.lib))
+        self._in_at = KsgAnnotateInAt()
+        self._in_at_ref = C.addressof(self._in_at)
+        self._out_at = ((C.c_void_p * 3)(), (C.c_int64 * 3)())
         self._keep = [_cstrs(node_names), _cstrs(plugin_names), _cstrs(res_names), _cstrs(taint_strings),
                       np.ascontiguousarray(taints, np.uint32)]
         names = KsgNames(len(node_names), self._keep[0], self._keep[1], len(res_names), self._keep[2],
@@ -500,6 +512,24 @@ class Annotator:
         rc = self._annotate_v(self.h, C.byref(inp), out, ln)
         if rc != 0:
             raise KschedError(f"ksg_annotate rc={rc}")
+        return self._views(out, ln)
+
+    def annotate_at(self, n_filter: int, filter_order: int, n_score: int, score_order: int, normalize_mask: int,
+                    weight: int, n_feasible: int, fstatus: int, raw: int, norm: int):
+        """annotate_views with every array given as an address the caller keeps
+        valid (the bulk path's per-pod call: no conversions, one reused
+        argument struct)."""
+        a = self._in_at
+        a.n_filter, a.filter_order, a.n_score, a.score_order = n_filter, filter_order, n_score, score_order
+        a.normalize_mask, a.weight, a.n_feasible = normalize_mask, weight, n_feasible
+        a.fstatus, a.raw, a.norm = fstatus, raw, norm
+        out, ln = self._out_at
+        rc = self._annotate_at(self.h, self._in_at_ref, out, ln)
+        if rc != 0:
+            raise KschedError(f"ksg_annotate rc={rc}")
+        return self._views(out, ln)
+
+    def _views(self, out, ln):
         bufs = self._view_bufs
         views = []
         for i in range(3):
