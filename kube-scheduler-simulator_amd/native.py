@@ -421,6 +421,16 @@ class KsgAnnotateIn(C.Structure):
                 ("fstatus", u32p), ("raw", i64p), ("norm", i64p)]
 
 
+# a read-only memoryview of `n` bytes at address `p` (PyMemoryView_FromMemory, PyBUF_READ)
+_memview = C.pythonapi.PyMemoryView_FromMemory
+_memview.restype = C.py_object
+_memview.argtypes = [C.c_void_p, C.c_ssize_t, C.c_int]
+
+
+def _view_at(p, n):
+    return _memview(p, n, 0x100) if n else memoryview(b"")
+
+
 class KsgAnnotateInAt(C.Structure):
     """ksg_annotate_in with its pointers as plain addresses (Annotator.annotate_at)."""
     _fields_ = [("n_filter", C.c_int32), ("filter_order", C.c_void_p), ("n_score", C.c_int32),
@@ -463,7 +473,6 @@ class Annotator:
         names = KsgNames(len(node_names), self._keep[0], self._keep[1], len(res_names), self._keep[2],
                          len(taint_strings), self._keep[3], int(self._keep[4].shape[0]),
                          _ptr(self._keep[4], u32p))
-        self._view_bufs = [np.empty(0, np.uint8) for _ in range(3)]
         self.h = C.c_void_p()
         rc = self._new(C.byref(names), C.byref(self.h))
         if rc != 0:
@@ -494,11 +503,10 @@ class Annotator:
 
     def annotate_views(self, filter_order, score_order, normalize_mask: int, weight, n_feasible: int,
                        fstatus: np.ndarray, raw: np.ndarray, norm: np.ndarray):
-        """annotate_bytes' values as read-only memoryviews, valid until this
-        annotator's next call (as the C strings are).  They are copied out by
-        ctypes.memmove into buffers the annotator keeps: every byte moves with
-        the GIL released and no page is faulted in again per call, so worker
-        threads serialise in parallel (string_at copies under the GIL)."""
+        """annotate_bytes' values as read-only memoryviews of the annotator's
+        own buffers, valid until its next call (as the C strings are): nothing
+        is copied, so worker threads serialise in parallel (string_at copied
+        every value under the GIL)."""
         fo = np.ascontiguousarray(filter_order, np.int32)
         so = np.ascontiguousarray(score_order, np.int32)
         w = np.ascontiguousarray(weight, np.int64)
@@ -530,14 +538,8 @@ class Annotator:
         return self._views(out, ln)
 
     def _views(self, out, ln):
-        bufs = self._view_bufs
-        views = []
-        for i in range(3):
-            if len(bufs[i]) < ln[i]:
-                bufs[i] = np.empty(max(ln[i], 2 * len(bufs[i])), np.uint8)
-            C.memmove(bufs[i].ctypes.data, out[i], ln[i])
-            views.append(memoryview(bufs[i])[:ln[i]].toreadonly())
-        return tuple(views)
+        # read-only views straight onto the annotator's buffers: no copy at all
+        return tuple(_view_at(out[i], ln[i]) for i in range(3))
 
     def close(self):
         if self.h:
