@@ -83,6 +83,18 @@ void go_string(std::string& o, const char* s) {
 
 const char* kFitRes[3] = {"cpu", "memory", "ephemeral-storage"};
 
+// Fixed-width pieces for the score maps' inner loop: a plugin's key (with the
+// separator before it) in a 48-byte slot, and "0" .. "999" quoted in 8-byte
+// slots; each is stored whole and the buffer advances by its length (the
+// reserve covers the slack).
+struct Frag {
+  char b[48];
+  uint32_t n;
+};
+struct SmallInt {
+  char b[8];
+  uint32_t n;
+};
 // A growable byte buffer without initialisation on growth: reserve() for the
 // worst case of what follows, then put() / ch() store without checks.
 struct Buf {
@@ -107,6 +119,18 @@ struct Buf {
   }
   void put(const std::string& s) { put(s.data(), s.size()); }
   void ch(char c) { d[n++] = c; }
+  void frag(const Frag& f) {   // 48 bytes stored, f.n kept
+    std::memcpy(d + n, f.b, sizeof f.b);
+    n += f.n;
+  }
+  void qint_small(int64_t v, const SmallInt* t) {
+    if ((uint64_t)v < 1000) {
+      std::memcpy(d + n, t[v].b, sizeof t[v].b);
+      n += t[v].n;
+    } else {
+      qint(v);
+    }
+  }
   void qint(int64_t v) {   // "<decimal>" (go_int's bytes); at most 22 bytes
     char t[24];
     char* e = t + sizeof t;
@@ -123,6 +147,20 @@ struct Buf {
   }
 };
 constexpr size_t kQint = 22;
+
+const SmallInt* small_ints() {
+  static const std::vector<SmallInt> t = [] {
+    std::vector<SmallInt> v(1000);
+    for (int i = 0; i < 1000; i++) {
+      const std::string q = "\"" + std::to_string(i) + "\"";
+      std::memset(v[i].b, 0, sizeof v[i].b);
+      std::memcpy(v[i].b, q.data(), q.size());
+      v[i].n = (uint32_t)q.size();
+    }
+    return v;
+  }();
+  return t.data();
+}
 
 }  // namespace
 
@@ -326,8 +364,27 @@ extern "C" int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const c
   if (in->n_feasible >= 2 && in->n_score > 0) {
     if (!in->raw || !in->weight) return KSG_E_INVALID;
     const std::vector<int> by_name = sorted_plugins(a, in->score_order, in->n_score);
+    // per plugin in key order: its key fragment ("{" or "," before it), its
+    // rows and weight
+    const int S = (int)by_name.size();
+    std::vector<Frag> frag(S);
+    std::vector<const int64_t*> raw_row(S), fin_row(S);
+    std::vector<uint64_t> wt(S);
+    bool fixed = true;
+    for (int i = 0; i < S; i++) {
+      const int p = by_name[i];
+      const std::string key = (i ? "," : "{") + a->plugin[p];
+      fixed = fixed && key.size() <= sizeof frag[i].b;
+      std::memset(frag[i].b, 0, sizeof frag[i].b);
+      std::memcpy(frag[i].b, key.data(), std::min(key.size(), sizeof frag[i].b));
+      frag[i].n = (uint32_t)key.size();
+      raw_row[i] = in->raw + (size_t)p * N;
+      fin_row[i] = ((in->normalize_mask >> p) & 1u) && in->norm ? in->norm + (size_t)p * N : raw_row[i];
+      wt[i] = (uint64_t)in->weight[p];
+    }
+    const SmallInt* small = small_ints();
     size_t bound = a->node_json_max + 3;
-    for (int p : by_name) bound += a->plugin[p].size() + 1 + kQint;
+    for (int p : by_name) bound += a->plugin[p].size() + 1 + sizeof(Frag{}.b) + kQint + 8;
     bool first_node = true;
     for (int k = 0; k < N; k++) {
       const int n = a->node_order[k];
@@ -336,21 +393,22 @@ extern "C" int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const c
       if (!first_node) { s.ch(','); t.ch(','); }
       first_node = false;
       s.put(a->node_json[n]);
-      s.ch('{');
       t.put(a->node_json[n]);
-      t.ch('{');
-      bool first = true;
-      for (int p : by_name) {
-        if (!first) { s.ch(','); t.ch(','); }
-        first = false;
-        s.put(a->plugin[p]);
-        t.put(a->plugin[p]);
-        const int64_t raw = in->raw[(size_t)p * N + n];
-        s.qint(raw);
-        const bool normed = ((in->normalize_mask >> p) & 1u) && in->norm;
-        const uint64_t v = (uint64_t)(normed ? in->norm[(size_t)p * N + n] : raw) * (uint64_t)in->weight[p];
-        t.qint((int64_t)v);   // Go int64 multiplication wraps
+      for (int i = 0; i < S; i++) {
+        if (fixed) {
+          s.frag(frag[i]);
+          t.frag(frag[i]);
+        } else {
+          const std::string key = (i ? "," : "{") + a->plugin[by_name[i]];
+          s.put(key);
+          t.put(key);
+        }
+        const int64_t raw = raw_row[i][n];
+        s.qint_small(raw, small);
+        const uint64_t v = (uint64_t)fin_row[i][n] * wt[i];
+        t.qint_small((int64_t)v, small);   // Go int64 multiplication wraps
       }
+      if (S == 0) { s.ch('{'); t.ch('{'); }
       s.ch('}');
       t.ch('}');
     }

@@ -79,3 +79,34 @@ def test_native_serialiser_faster_than_store(built):
             s.annotations(c.pod)
         times[nat] = time.perf_counter() - t0
     assert times[True] < times[False]
+
+
+@pytest.mark.parametrize("width", [3, 60])
+def test_score_maps_fixed_and_long_keys(built, width):
+    """score-result / finalscore-result: plugin keys within and beyond the
+    serialiser's fixed-width key slot, values inside and outside its small-
+    integer table (negative, 999 / 1000, int64 wrap-around of raw x weight)."""
+    import numpy as np
+    names = ["n%d" % i for i in range(5)]
+    plugins = [("P%d" % i).ljust(width, "x") for i in range(native.NPLUGINS)]
+    ann = native.Annotator(names, plugins, ["cpu", "memory"], [], np.zeros((0, len(names)), "uint32"))
+    raw = np.zeros((native.NPLUGINS, len(names)), np.int64)
+    norm = np.zeros_like(raw)
+    raw[0] = [0, 999, 1000, -5, 2 ** 62]
+    raw[1] = [7, 100, 12345, 1, 3]
+    norm[1] = [100, 0, 55, 999, 1000]
+    weight = np.zeros(native.NPLUGINS, np.int64)
+    weight[0], weight[1] = 3, 2
+    fs = np.zeros(len(names), np.uint32)
+    fs[2] = 0x1   # rejected: no score entries
+    f, s, t = ann.annotate([0], [1, 0], 1 << 1, weight, 4, fs, raw, norm)
+
+    def wrap(x):
+        x &= (1 << 64) - 1
+        return x - (1 << 64) if x >> 63 else x
+    keep = [i for i in range(len(names)) if fs[i] == 0]
+    want_s = {names[i]: {plugins[0]: str(int(raw[0][i])), plugins[1]: str(int(raw[1][i]))} for i in keep}
+    want_t = {names[i]: {plugins[0]: str(wrap(int(raw[0][i]) * 3)), plugins[1]: str(wrap(int(norm[1][i]) * 2))}
+              for i in keep}
+    assert s == A.go_marshal(want_s)
+    assert t == A.go_marshal(want_t)
