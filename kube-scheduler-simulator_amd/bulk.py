@@ -13,6 +13,7 @@ per-pod path's, which tests/test_gpu_bulk_annotations.py checks.
 """
 from __future__ import annotations
 
+import itertools
 from concurrent.futures import ThreadPoolExecutor
 from typing import Callable, List, Optional
 
@@ -79,16 +80,20 @@ class BulkAnnotator:
     def serialise(self, first: int, res, cap: native.CaptureBuffers, count: int,
                   sink: Callable[[int, tuple], None]):
         """ksg_annotate for pods first .. first + count of a captured chunk;
-        sink(pod index, (filter, score, finalscore)) in pod order per worker; the
+        sink(pod index, (filter, score, finalscore)), increasing per worker; the
         values are read-only memoryviews valid for the sink call only (bytes(v)
         keeps one; hash.update(v) reads it in place)."""
         T = len(self.annotators)
         status, nfeas, sskip = (res[f][:count].tolist() for f in ("status", "n_feasible", "score_skip"))
         assert cap.fstatus.shape == (cap.fstatus.shape[0], self.n_nodes) and count <= cap.fstatus.shape[0]
 
+        nxt = itertools.count()   # pods handed out one at a time (their sizes differ)
+
         def work(t):
             ann = self.annotators[t]
-            for k in range(t, count, T):
+            for k in iter(nxt.__next__, None):
+                if k >= count:
+                    return
                 sink(first + k, self._pod_at(ann, k, first + k, status[k], nfeas[k], sskip[k], cap))
 
         if self.pool is None:
