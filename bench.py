@@ -1,42 +1,49 @@
 #!/usr/bin/env python3
 """Headline benchmark: the debuggable scheduler's Filter/Score hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): 5,000 nodes x 50,000 pods, NodeResourcesFit
-(LeastAllocated) + BalancedAllocation + TaintToleration + NodeAffinity (+ the
-always-on NodeUnschedulable / NodeName filters), synthetic cluster from
-generator.config2 (seed 2).  One step = schedule the whole 50,000-pod queue
-onto the fresh cluster (reset node state + one ksg_run_queue launch: filter,
-score, normalise, select, assume for every pod, in queue order) with every
-input already resident in HBM.
+Workload (BASELINE.json `metric`: "pods scheduled/sec @5k nodes, default
+plugins"): the in-tree default KubeSchedulerConfiguration profile (every
+Filter / Score plugin: NodeUnschedulable, NodeName, TaintToleration,
+NodeAffinity, NodePorts, NodeResourcesFit, the volume plugins,
+PodTopologySpread, InterPodAffinity, BalancedAllocation, ImageLocality) on
+5,000 nodes x 50,000 pods, synthetic cluster from generator.config1 (seed 1,
+the configs[0] generator at 5,000 nodes: 4 zones, 20 % of the pods with a
+zone nodeSelector).  One step = schedule the whole 50,000-pod queue onto the
+fresh cluster (reset node state + one ksg_run_queue: filter, score,
+normalise, select, assume for every pod, in queue order) with every input
+already resident in HBM.
 
 Multi-GPU: the per-pod decision does not shard (every binding changes the
 state the next pod reads), so N GPUs run N DISTINCT what-if replicas of the
-queue (north star (3)): rank 0 the configs[1] profile, rank
-r >= 1 what-if profile r of generator.replica_profiles (per-plugin weights in
-[1, 5], LeastAllocated or MostAllocated), each over the full 50,000-pod queue
-on its own copy of the cluster (weak scaling: per-GPU work fixed; no data-path
+queue (north star (3)): rank 0 the default profile, rank r >= 1
+what-if profile r of generator.default_replica_profiles (every Score weight
+in [1, 5], LeastAllocated or MostAllocated), each over the full queue on its
+own copy of the cluster (weak scaling: per-GPU work fixed; no data-path
 collective).  value = pods scheduled by all ranks / max-over-ranks time; one
 RCCL all_gather of every replica's placements per step.  The process group is
 RCCL ("nccl") at every N, N = 1 included (a one-rank group on 127.0.0.1), so
 the collective runs on the box.
 
 Prints ONE JSON line (rank 0).  The line also carries:
+* `configs1`: BASELINE configs[1] (5,000 x 50,000, NodeResourcesFit +
+  BalancedAllocation + TaintToleration + NodeAffinity, generator.config2) with
+  its own roofline, PMC traffic and CPU baseline (the rounds 1-4 headline);
 * `replica_sweep`: BASELINE configs[3], 1,024 what-if replicas (weights and
-  strategy per replica) of the first 1,000 pods on the same cluster, sharded
-  over the N ranks by replicas.run_sweep (contiguous replica blocks, one
-  RCCL all_gather of placements + summaries at the end): aggregate
+  strategy per replica) of the first 1,000 pods of configs[1], sharded over
+  the N ranks by replicas.run_sweep (contiguous replica blocks, one RCCL
+  all_gather of placements + summaries at the end): aggregate
   replica-pods/s over max-over-ranks time, the roofline of its dominant
   kernel, and a digest of all 1,024 replicas' placements (identical at every
   N);
 * `cpu_baseline` (rank 0, N = 1): the C++ restatement (oracle/) on a bounded
-  prefix of the same queue, at 16 threads (upstream parallelism) and at every
-  host core this process may use, with the CPU model;
+  prefix of the headline queue, at 16 threads (upstream parallelism) and at
+  every host core this process may use, with the CPU model and the limit
+  that capped the core count;
 * `annotations` (N = 1): the simulator's product for the first 2,000 pods of
-  the same queue: captured batched run + filter-result / score-result /
-  finalscore-result bytes from ksg_annotate (bulk.annotate_queue, device
-  capture of the next chunk overlapping the serialisation of this one);
-* `default_profile` (N = 1): the in-tree default profile (every Filter/Score
-  plugin, generator.config1) at the same 5,000 nodes.
+  configs[1]: captured batched run + filter-result / score-result /
+  finalscore-result bytes (bulk.annotate_queue);
+* `per_cycle` / `per_cycle_configs2` (N = 1): the drop-in's per-cycle C-ABI
+  path, call by call from C.
 """
 from __future__ import annotations
 
@@ -56,22 +63,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def usable_cores() -> int:
-    """Cores this process may actually run on: the affinity mask, capped by the
-    cgroup CPU quota and by the CPU share the GPU box exports (it shows the
-    whole machine in the mask but grants 16 cores; oversubscribing them
-    measures the OS scheduler, not the port)."""
+def usable_cores():
+    """(cores, limit): the cores this process may actually run on and what
+    capped them -- the affinity mask, the cgroup CPU quota, or the CPU share
+    the GPU box exports in OMP_NUM_THREADS (the box shows the whole machine in
+    the mask but grants 16 cores)."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    limit = "affinity"
     try:
         quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if quota != "max":
-            n = min(n, max(1, int(quota) // int(period)))
+        if quota != "max" and int(quota) // int(period) < n:
+            n, limit = max(1, int(quota) // int(period)), "cgroup cpu.max"
     except (OSError, ValueError):
         pass
-    share = os.environ.get("OMP_NUM_THREADS", "")   # the GPU box exports its CPU share here
-    if share.isdigit() and int(share) > 0:
-        n = min(n, int(share))
-    return n
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and 0 < int(share) < n:
+        n, limit = int(share), "OMP_NUM_THREADS"
+    return n, limit
 
 
 def cpu_model() -> str:
@@ -107,16 +115,29 @@ def cpu_baseline(enc, pf, n_threads: int, budget_s: float):
 
 
 def cpu_baselines(enc, pf, budget_s: float):
-    """16 threads (upstream parallelism: 16) and every host core
-    this process may run on (sched_getaffinity; nproc of the machine beside it)."""
-    usable = usable_cores()
+    """BASELINE.md / SURVEY §8(d): 16 threads (upstream parallelism: 16) and
+    every host core this process may use (the limit that applied is named);
+    when the affinity mask holds more cores than that limit grants, the port
+    also runs at min(affinity, 64) threads, labelled as possibly
+    oversubscribed (north star: "then all host cores")."""
+    usable, limit = usable_cores()
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     out = cpu_baseline(enc, pf, 16, budget_s)
     out["cpu_model"] = cpu_model()
     out["nproc"] = os.cpu_count()
+    out["affinity_cores"] = affinity
     out["usable_cores"] = usable
+    out["usable_cores_limit"] = limit
     if usable != 16:
         allc = cpu_baseline(enc, pf, usable, budget_s)
         out["all_cores"] = {k: allc[k] for k in ("value", "cores", "sample", "node_evals_per_sec")}
+        out["all_cores"]["limit"] = limit
+    wide = min(affinity, 64)
+    if affinity > usable and wide > 16:
+        w = cpu_baseline(enc, pf, wide, budget_s)
+        out["affinity_cores_leg"] = {k: w[k] for k in ("value", "cores", "sample", "node_evals_per_sec")}
+        out["affinity_cores_leg"]["note"] = (f"{wide} threads over the {affinity}-core affinity mask; the box "
+                                             f"grants {usable} ({limit}): possibly oversubscribed")
     return out
 
 
@@ -127,7 +148,7 @@ def pmc_traffic(kernel, name):
     """HBM bytes per dispatch of `kernel` from a committed PMC summary
     (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE +
     WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
-    for rnd in ("r4", "r3", "r2"):   # the newest round's passes first
+    for rnd in ("r5", "r4", "r3", "r2"):   # the newest round's passes first
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             row = json.load(open(path)).get(kernel) if kernel else None
@@ -322,16 +343,42 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=N
             "eval_path": eng.last_run_info()[0], "eval_path_legend": "5 per-cycle kernel, 6 its topology form"}
 
 
-def default_profile_line(native, G, E, metrics, n_nodes: int, n_pods: int, steps: int, cpu_budget: float):
-    """The in-tree default profile (generator.config1: every Filter / Score
-    plugin, pods without topology terms) at n_nodes: pods/s of reset + one
-    ksg_run_queue over n_pods (best of `steps`), the dominant kernel's
-    roofline (per-kernel HIP events, priced like the headline), and the C++
-    oracle on a bounded prefix of the same queue (16 threads)."""
-    nodes, pods, prof = G.config1(n_nodes=n_nodes, n_pods=n_pods)
+def queue_roofline(metrics, kstats, bpe: int, node_evals: int, kms: float, pmc_file: str):
+    """The dominant kernel's roofline (algorithmic bytes per launch / its
+    average HIP-event duration, SURVEY §8(d) pricing of the node-evals a
+    phase-2 launch decides), the whole step beside it, PMC traffic per launch
+    from the committed passes and the memory-side rate that traffic implies."""
+    roof = metrics.dominant_kernel_roofline(kstats, bpe) if kstats else None
+    if roof is None:   # no per-kernel timing: whole step as one launch
+        roof = metrics.roofline(bpe, node_evals, kms)
+    roof = metrics.price_decided_node_evals(roof, bpe, node_evals)
+    roof["step"] = metrics.roofline(bpe, node_evals, kms)
+    roof["step"]["kernel_ms"] = kms
+    # HBM bytes per launch of the dominant kernel from the committed PMC passes
+    # (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE +
+    # WRITE_SIZE per dispatch, gfx950-corrected), null when not collected
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(roof.get("kernel"), pmc_file)
+    if roof.get("traffic") and roof.get("avg_launch_ms"):
+        ms = roof["traffic"] / (roof["avg_launch_ms"] * 1e-3) / 1e9
+        roof["memory_side_GBps"] = ms
+        roof["memory_side_frac_of_hbm"] = ms / roof["peak"]
+        roof["traffic_over_algorithmic"] = roof["traffic"] / roof["bytes_per_launch"]
+    roof["bytes_per_node_eval"] = bpe
+    roof["node_evals_per_step"] = node_evals
+    return roof
+
+
+def configs1_line(native, G, E, metrics, n_nodes: int, n_pods: int, steps: int, cpu_budget: float, local_rank: int):
+    """BASELINE configs[1] (generator.config2: NodeResourcesFit LeastAllocated +
+    BalancedAllocation + TaintToleration + NodeAffinity) beside the headline:
+    pods/s of reset + one ksg_run_queue (best of `steps`), the dominant
+    kernel's roofline with its PMC traffic (pmc_config2.json), and the C++
+    oracle on a bounded prefix (16 threads).  Returns the line and the loaded
+    engine, which the configs[3] / annotation / kubelet legs reuse."""
+    nodes, pods, prof = G.config2(n_nodes=n_nodes, n_pods=n_pods)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
-    eng = native.Engine(device=0)
+    eng = native.Engine(device=local_rank)
     eng.load(enc, pf)
     best, kms = None, None
     for _ in range(steps + 1):
@@ -347,16 +394,18 @@ def default_profile_line(native, G, E, metrics, n_nodes: int, n_pods: int, steps
     ks = eng.kernel_stats()
     eng.set_timing(False)
     bpe = sum(metrics.bytes_per_node_eval(enc, prof).values())
-    roof = metrics.price_decided_node_evals(metrics.dominant_kernel_roofline(ks, bpe), bpe, n_pods * n_nodes)
-    out = {"workload": f"default profile (every in-tree Filter/Score plugin), generator.config1: {n_nodes} nodes x "
-                       f"{n_pods} pods", "pods_per_s": n_pods / best, "device_pods_per_s": n_pods / (kms * 1e-3),
-           "scheduled": int((pl >= 0).sum()), "roofline": roof, "bytes_per_node_eval": bpe}
+    out = {"workload": f"configs[1]: {n_nodes} nodes x {n_pods} pods, NodeResourcesFit(LeastAllocated)"
+                       f"+BalancedAllocation+TaintToleration+NodeAffinity, generator.config2 seed 2",
+           "pods_per_s": n_pods / best, "device_pods_per_s": n_pods / (kms * 1e-3),
+           "scheduled": int((pl >= 0).sum()),
+           "placements_sha256": __import__("hashlib").sha256(pl.tobytes()).hexdigest(),
+           "roofline": queue_roofline(metrics, ks, bpe, n_pods * n_nodes, kms, "pmc_config2.json")}
     if cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline(enc, pf, 16, cpu_budget)
-    return out
+    return out, eng, enc, prof
 
 
-def kubelet_memory_line(native, G, E, n_nodes: int, n_pods: int, steps: int, headline_pods_per_s: float):
+def kubelet_memory_line(native, G, E, n_nodes: int, n_pods: int, steps: int, configs1_pods_per_s: float):
     """configs[1] with kubelet-style memory (generator.config2_kubelet:
     allocatable a whole number of Ki, not of Mi; 30 % of the pods request
     decimal quantities): the N32 forms do not apply, the speculate-and-verify
@@ -377,7 +426,7 @@ def kubelet_memory_line(native, G, E, n_nodes: int, n_pods: int, steps: int, hea
     path, flags = eng.last_run_info()
     v = n_pods / best
     return {"workload": f"configs[1] with kubelet-style memory (generator.config2_kubelet): {n_nodes} nodes x "
-                        f"{n_pods} pods", "pods_per_s": v, "headline_over_this": headline_pods_per_s / v,
+                        f"{n_pods} pods", "pods_per_s": v, "configs1_over_this": configs1_pods_per_s / v,
             "wide_memory_walk": bool(flags & native.RUN_WIDE_MEM), "run_flags": flags,
             "scheduled": int((pl >= 0).sum())}
 
@@ -391,11 +440,14 @@ def main():
     ap.add_argument("--pods", type=int, default=50000)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=("default", "configs1"), default="default",
+                    help="the timed queue: the metric's default profile (headline) or configs[1] (profiling passes)")
+    ap.add_argument("--configs1-pods", type=int, default=50000,
+                    help="configs[1] line (and the legs on its cluster); 0 disables")
     ap.add_argument("--sweep-replicas", type=int, default=1024, help="configs[3] sidecar; 0 disables")
     ap.add_argument("--sweep-pods", type=int, default=1000)
     ap.add_argument("--annotate-pods", type=int, default=2000, help="annotation sidecar; 0 disables")
     ap.add_argument("--annotate-threads", type=int, default=16)
-    ap.add_argument("--default-pods", type=int, default=50000, help="default-profile line; 0 disables")
     ap.add_argument("--cycle-pods", type=int, default=2000, help="per-cycle sidecar; 0 disables")
     ap.add_argument("--cycle-warm", type=int, default=500)
     ap.add_argument("--kubelet-pods", type=int, default=50000, help="kubelet-memory line; 0 disables")
@@ -407,18 +459,24 @@ def main():
     args = ap.parse_args()
 
     # Before anything touches the GPU: the library must be built from this
-    # tree's source (a mismatch rebuilds it), and `--gpus N` without a
-    # launcher starts N ranks here (launcher.py; the parent stays off the GPU).
+    # tree's source, and `--gpus N` without a launcher starts N ranks here
+    # (launcher.py; the parent stays off the GPU).  Under an outside launcher
+    # (torchrun) WORLD_SIZE decides the world and the library is only checked:
+    # ranks must not race to rebuild it.
     launcher = importlib.import_module(PKG + ".launcher")
+    ge = importlib.import_module("__graft_entry__")
     if not launcher.launched():
         if not args.no_build_check:
-            src_hash = importlib.import_module("__graft_entry__").ensure_current()
+            src_hash = ge.ensure_current()
             log(f"libksched.so built from source {src_hash[:12]}")
         if args.gpus > 1:
             sys.exit(launcher.launch(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:] + ["--no-build-check"]))
+    elif not args.no_build_check and ge.library_hash() != ge.source_hash():
+        raise SystemExit("bench.py: libksched.so does not embed this tree's source hash; run "
+                         "__graft_entry__.build() before launching the ranks")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+        log(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s); using {world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
@@ -451,13 +509,24 @@ def main():
     metrics = importlib.import_module(PKG + ".metrics")
     replicas = importlib.import_module(PKG + ".replicas")
 
+    # ---- the headline: default profile, 5,000 nodes x 50,000 pods ----------------------
     t = time.perf_counter()
-    nodes, pods, prof = G.config2(n_nodes=args.nodes, n_pods=args.pods)
+    if args.workload == "default":
+        nodes, pods, prof = G.config1(n_nodes=args.nodes, n_pods=args.pods)
+        whatifs, pmc_file = G.default_replica_profiles, "pmc_default.json"
+        label = (f"default profile (every in-tree Filter/Score plugin, weights TaintToleration 3, NodeAffinity 2, "
+                 f"PodTopologySpread 2, InterPodAffinity 2, NodeResourcesFit 1 LeastAllocated, BalancedAllocation 1, "
+                 f"ImageLocality 1): {len(nodes)} nodes x {len(pods)} pods, generator.config1 seed 1")
+    else:   # configs[1] as the timed queue (its PMC passes, profiles/run_pmc.sh)
+        nodes, pods, prof = G.config2(n_nodes=args.nodes, n_pods=args.pods)
+        whatifs, pmc_file = G.replica_profiles, "pmc_config2.json"
+        label = (f"configs[1]: {len(nodes)} nodes x {len(pods)} pods, NodeResourcesFit(LeastAllocated)"
+                 f"+BalancedAllocation+TaintToleration+NodeAffinity, generator.config2 seed 2")
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
-    # this rank's what-if replica: rank 0 the configs[1] profile, rank r >= 1
-    # replica profile r (distinct weights / strategy: no duplicated work)
-    prof_r = prof if rank == 0 else G.replica_profiles(world)[rank]
+    # this rank's what-if replica: rank 0 the workload's profile, rank r >= 1
+    # what-if r of it (distinct weights / strategy)
+    prof_r = prof if rank == 0 else whatifs(world)[rank]
     pf_r = pf if rank == 0 else E.encode_profile(prof_r, enc.cluster.res_names)
     log(f"[rank {rank}] encoded {len(nodes)} nodes x {len(pods)} pods in {time.perf_counter() - t:.1f}s")
     eng = native.Engine(device=local_rank)
@@ -492,7 +561,7 @@ def main():
     elapsed = float(tt.item())
     scheduled = int((pl >= 0).sum())
     # every replica's placements, gathered by RCCL in the last step: distinct
-    # what-ifs at N > 1 (rank 0's is the configs[1] placement)
+    # what-ifs at N > 1 (rank 0's is the default profile's placement)
     import hashlib
     replica_digest = hashlib.sha256(b"".join(g.cpu().numpy().tobytes() for g in gather_out)).hexdigest()
     distinct = len({hashlib.sha256(g.cpu().numpy().tobytes()).hexdigest() for g in gather_out})
@@ -506,22 +575,31 @@ def main():
     except Exception as e:   # timing is diagnostic; never lose the bench line over it
         log(f"[rank {rank}] per-kernel timing unavailable: {e}")
 
-    sweep = None
-    if args.sweep_replicas > 0:
+    # ---- configs[1] and the legs on its cluster ----------------------------------------
+    c1 = eng1 = enc1 = prof1 = None
+    if args.configs1_pods > 0:
         try:
-            sweep = replica_sweep(eng, enc, prof, G, E, metrics, replicas, args.sweep_replicas,
-                                  min(args.sweep_pods, P), rank, world, dist, dev)
+            c1, eng1, enc1, prof1 = configs1_line(native, G, E, metrics, args.nodes, args.configs1_pods, 2,
+                                                  0.0 if args.no_cpu_baseline or world > 1 else 8.0, local_rank)
+        except Exception as e:
+            log(f"[rank {rank}] configs[1] line unavailable: {e}")
+    sweep = None
+    if args.sweep_replicas > 0 and eng1 is not None:
+        try:
+            sweep = replica_sweep(eng1, enc1, prof1, G, E, metrics, replicas, args.sweep_replicas,
+                                  min(args.sweep_pods, args.configs1_pods), rank, world, dist, dev)
         except Exception as e:   # a sidecar; never lose the headline line over it
             log(f"[rank {rank}] replica sweep unavailable: {e}")
-
-    ann = dflt = None
-    if world == 1 and args.annotate_pods > 0:
+    ann = None
+    if world == 1 and args.annotate_pods > 0 and eng1 is not None:
         try:
             B = importlib.import_module(PKG + ".bulk")
-            ann = annotation_sidecar(eng, enc, prof, native, B, min(args.annotate_pods, P), 256,
+            ann = annotation_sidecar(eng1, enc1, prof1, native, B, min(args.annotate_pods, args.configs1_pods), 256,
                                      args.annotate_threads)
         except Exception as e:
             log(f"[rank {rank}] annotation sidecar unavailable: {e}")
+    if eng1 is not None:
+        eng1.close()
     cyc = None
     if world == 1 and args.cycle_pods > 0:
         try:
@@ -529,13 +607,6 @@ def main():
             cyc = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods)
         except Exception as e:
             log(f"[rank {rank}] per-cycle sidecar unavailable: {e}")
-    if world == 1 and args.default_pods > 0:
-        try:
-            dflt = default_profile_line(native, G, E, metrics, args.nodes, args.default_pods, 2,
-                                        0.0 if args.no_cpu_baseline else 8.0)
-        except Exception as e:
-            log(f"[rank {rank}] default-profile line unavailable: {e}")
-
     cyc3 = ann3 = None
     if world == 1 and args.topo_cycle_pods > 0:
         try:
@@ -553,14 +624,14 @@ def main():
             eng3.load(enc3, E.encode_profile(prof3, enc3.cluster.res_names))
             ann3 = annotation_sidecar(eng3, enc3, prof3, native, B, len(p3), 64, args.annotate_threads,
                                       label="configs[2]")
-            del eng3
+            eng3.close()
         except Exception as e:
             log(f"[rank {rank}] configs[2] annotation sidecar unavailable: {e}")
     kub = None
-    if world == 1 and args.kubelet_pods > 0:
+    if world == 1 and args.kubelet_pods > 0 and c1 is not None:
         try:
             kub = kubelet_memory_line(native, G, E, args.nodes, min(args.kubelet_pods, args.pods), 2,
-                                      P * args.steps / elapsed)
+                                      c1["pods_per_s"])
         except Exception as e:
             log(f"[rank {rank}] kubelet-memory line unavailable: {e}")
 
@@ -568,61 +639,36 @@ def main():
         ms_step = elapsed * 1e3 / args.steps
         pods_per_s = world * P * args.steps / elapsed
         node_evals = world * P * len(nodes) * args.steps / elapsed
-        per_eval = metrics.bytes_per_node_eval(enc, prof)
-        bpe = sum(per_eval.values())
+        bpe = sum(metrics.bytes_per_node_eval(enc, prof).values())
         kms = float(np.mean(kernel_ms))
         try:
-            roof = metrics.dominant_kernel_roofline(kstats, bpe)
+            roof = queue_roofline(metrics, kstats, bpe, P * len(nodes), kms, pmc_file)
         except Exception as e:
             log(f"per-kernel roofline unavailable: {e}")
-            roof = None
-        if roof is None:   # no per-kernel timing: whole step as one launch
             roof = metrics.roofline(bpe, P * len(nodes), kms)
-        # Phase-2 kernels decide a batch of pods over every node (metrics.price_decided_node_evals)
-        roof = metrics.price_decided_node_evals(roof, bpe, P * len(nodes))
-        roof["step"] = metrics.roofline(bpe, P * len(nodes), kms)
-        roof["step"]["kernel_ms"] = kms
-        # HBM bytes per launch of the dominant kernel from the committed PMC
-        # passes (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE
-        # + WRITE_SIZE per dispatch, gfx950-corrected), null when not collected
-        roof["traffic"], roof["traffic_source"] = pmc_traffic(roof.get("kernel"), "pmc_config2.json")
-        roof["bytes_per_node_eval"] = bpe
-        roof["node_evals_per_step"] = P * len(nodes)
         out = {
             "metric": "pods scheduled/sec @5k nodes, default plugins; node-evals/sec; % HBM peak",
             "value": pods_per_s, "unit": "pods/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": f"configs[1]: {len(nodes)} nodes x {P} pods, NodeResourcesFit(LeastAllocated)"
-                                   f"+BalancedAllocation+TaintToleration+NodeAffinity, generator.config2 seed 2"
-                                   + (f"; ranks 1..{world - 1}: distinct what-if profiles (replica_profiles)"
-                                      if world > 1 else ""),
+            "config": {"workload": label + (f"; ranks 1..{world - 1}: distinct what-if profiles"
+                                            if world > 1 else ""),
                        "nodes": len(nodes), "pods": P, "parallelism": f"replicas{world}",
                        "pods_scheduled_per_step": scheduled, "distinct_replica_placements": distinct,
                        "replica_placements_sha256": replica_digest},
             "node_evals_per_sec": node_evals,
             "roofline": roof,
         }
-        ge = importlib.import_module("__graft_entry__")
         out["source_hash"] = {"library": ge.library_hash(), "tree": ge.source_hash()}
         out["source_hash"]["matches"] = out["source_hash"]["library"] == out["source_hash"]["tree"]
-        if sweep is not None:
-            out["replica_sweep"] = sweep
-        if ann is not None:
-            out["annotations"] = ann
-        if dflt is not None:
-            out["default_profile"] = dflt
-        if cyc is not None:
-            out["per_cycle"] = cyc
-        if kub is not None:
-            out["kubelet_memory"] = kub
-        if cyc3 is not None:
-            out["per_cycle_configs2"] = cyc3
-        if ann3 is not None:
-            out["annotations_configs2"] = ann3
+        for key, val in (("configs1", c1), ("replica_sweep", sweep), ("annotations", ann), ("per_cycle", cyc),
+                         ("kubelet_memory", kub), ("per_cycle_configs2", cyc3), ("annotations_configs2", ann3)):
+            if val is not None:
+                out[key] = val
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baselines(enc, pf, args.cpu_budget)
         print(json.dumps(out), flush=True)
+    eng.close()
     dist.barrier()
     dist.destroy_process_group()
 

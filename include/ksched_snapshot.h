@@ -313,11 +313,18 @@ int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labe
  * the pod informer delivers it: upstream eventhandlers.go addPodToSchedulingQueue
  * feeding the simulator's scheduler).  Its selectors, term templates, label
  * keys, scalar resources and host ports join the encoding universe at the
- * next encode / sync (one full re-encode per batch of hints); the pod itself
- * is not a workload pod until ksg_snapshot_add_pod.  Adding it then appends in
+ * next encode / sync: that sync re-encodes only when a hint brings in
+ * something the current encoding lacks (each new hint is encoded against the
+ * frozen universe first, as an append would be), once per batch of such hints;
+ * the pod itself is not a workload pod until ksg_snapshot_add_pod, which also
+ * drops its hint (matched by namespace and name).  Adding it then appends in
  * place (ksg_snapshot_sync *appended = 1) instead of re-encoding.  Hints never
  * change a result: a selector or template nobody evaluates is only data. */
 int ksg_snapshot_hint_pod(ksg_snapshot* s, const ksg_pod_view* pod);
+/* A hinted pod was deleted before it was added (the informer's delete of a
+ * pending pod, upstream eventhandlers.go deletePodFromSchedulingQueue): its
+ * hint is dropped.  Namespace null = "default".  Unknown pods are ignored. */
+int ksg_snapshot_unhint_pod(ksg_snapshot* s, const char* namespace_, const char* name);
 /* Pod `pod` runs on `node` (NodeInfo.Pods): replayed as an assume at load. */
 int ksg_snapshot_bind(ksg_snapshot* s, int32_t pod, int32_t node);
 int ksg_snapshot_node_index(ksg_snapshot* s, const char* name, int32_t* index);

@@ -485,7 +485,7 @@ struct ksg_snapshot {
   // place instead of re-encoding (ksg_snapshot_hint_pod).  No program, no
   // binding: they are not pods of the workload.
   std::vector<Pod> hints;
-  bool hints_new = false;           // hints added since the last full encode
+  size_t hints_seen = 0;            // hints[0, hints_seen) are inside the current encoding universe
   std::vector<std::pair<int32_t, int32_t>> binds;   // (pod, node) in order: bound, then assumed
   Encoded e;
   bool encoded = false;     // e reflects nodes and pods [0, n_encoded)
@@ -1365,7 +1365,7 @@ void encode_all(ksg_snapshot* s) {
   finish_arrays(s);
   s->encoded = true;
   s->n_encoded = (int)P;
-  s->hints_new = false;
+  s->hints_seen = s->hints.size();
   s->epoch++;
 }
 
@@ -1559,13 +1559,53 @@ void fill_views(ksg_snapshot* s, ksg_nodes* nd, ksg_topology* tp, ksg_workload* 
 // selectors, term templates) they are encoded against it and appended
 // (*appended = 1): byte-identical to a full re-encode, which is what runs
 // otherwise (*appended = 0).
+// Whether pod p (a hint) would extend the encoding universe: it is encoded
+// against the frozen universe at index P, exactly as an append would, and
+// everything that touched is undone.  Needs every pod encoded (caches sized P).
+bool extends_universe(ksg_snapshot* s, const Pod& p) {
+  Encoded& e = s->e;
+  const int P = (int)s->pods.size();
+  const size_t prog0 = e.prog.size(), pods0 = e.pods.size(), caches0 = s->req_cache.size();
+  s->pods.push_back(p);
+  bool miss = false;
+  try {
+    Pass ps{s, true};
+    prepare_frozen(s, P, ps);
+    if (!ps.miss) encode_pod(s, P, ps);
+    miss = ps.miss;
+  } catch (const EncodeError&) {
+    miss = true;
+  }
+  e.prog.resize(prog0);
+  e.pods.resize(pods0);
+  s->req_cache.resize(caches0);
+  s->pts_cache.resize(caches0);
+  s->owned_templates.resize(caches0);
+  s->pod_selectors.resize(caches0);
+  s->tmpl_match.resize(caches0);
+  e.prefilter_names.erase(P);
+  s->pods.pop_back();
+  return miss;
+}
+
+// The hints announced since the last check: a full re-encode only when one of
+// them extends the universe (a hint alone no longer forces one).
+int check_hints(ksg_snapshot* s, int32_t* appended) {
+  for (; s->hints_seen < s->hints.size(); s->hints_seen++)
+    if (extends_universe(s, s->hints[s->hints_seen])) {
+      if (appended) *appended = 0;
+      return do_encode(s);
+    }
+  return KSG_OK;
+}
+
 int encode_incremental(ksg_snapshot* s, int32_t* appended) {
   if (appended) *appended = 0;
-  if (!s->encoded || s->hints_new) return do_encode(s);   // hints extend the universe: once per batch
+  if (!s->encoded) return do_encode(s);
   const int P = (int)s->pods.size();
   if (s->n_encoded == P) {
     if (appended) *appended = 1;
-    return KSG_OK;
+    return check_hints(s, appended);
   }
   Encoded& e = s->e;
   const size_t prog0 = e.prog.size(), pods0 = e.pods.size(), caches0 = s->req_cache.size();
@@ -1593,7 +1633,7 @@ int encode_incremental(ksg_snapshot* s, int32_t* appended) {
   finish_arrays(s);
   s->n_encoded = P;
   if (appended) *appended = 1;
-  return KSG_OK;
+  return check_hints(s, appended);
 }
 
 // Upload the current encoding and replay the bindings.
@@ -1978,6 +2018,17 @@ int pod_from_view(ksg_snapshot* s, const ksg_pod_view* v, Pod& p) {
 }
 }  // namespace
 
+// Forget the hint of pod ns/name, if any (the pod was added or deleted).  The
+// current encoding keeps what the hint brought in until the next full encode.
+void drop_hint(ksg_snapshot* s, const std::string& ns, const std::string& name) {
+  for (size_t k = 0; k < s->hints.size(); k++)
+    if (s->hints[k].ns == ns && s->hints[k].name == name) {
+      s->hints.erase(s->hints.begin() + (std::ptrdiff_t)k);
+      if (k < s->hints_seen) s->hints_seen--;
+      return;
+    }
+}
+
 int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index) {
   if (!s || !v || !v->name) return KSG_E_INVALID;
   Pod p;
@@ -1985,6 +2036,7 @@ int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index)
   if (rc) return rc;
   for (auto& kv : pod_requests(p, false))
     if (is_scalar(kv.first)) s->scalars.insert(kv.first);
+  drop_hint(s, p.ns, p.name);   // the pod itself now keeps its terms in the universe
   const int32_t idx = (int32_t)s->pods.size();
   s->pods.push_back(std::move(p));
   if (index) *index = idx;
@@ -1998,8 +2050,14 @@ int ksg_snapshot_hint_pod(ksg_snapshot* s, const ksg_pod_view* v) {
   if (rc) return rc;
   for (auto& kv : pod_requests(p, false))
     if (is_scalar(kv.first)) s->scalars.insert(kv.first);
+  drop_hint(s, p.ns, p.name);   // announced again: the newer spec replaces the older
   s->hints.push_back(std::move(p));
-  s->hints_new = true;
+  return KSG_OK;
+}
+
+int ksg_snapshot_unhint_pod(ksg_snapshot* s, const char* ns, const char* name) {
+  if (!s || !name) return KSG_E_INVALID;
+  drop_hint(s, ns ? ns : "default", name);   // pod_from_view's defaulting
   return KSG_OK;
 }
 

@@ -194,6 +194,20 @@ def replica_profiles(n_replicas: int, seed: int = 4) -> List[P.Profile]:
     return out
 
 
+def default_replica_profiles(n_replicas: int, seed: int = 6) -> List[P.Profile]:
+    """What-if replicas of the in-tree default profile (the headline's
+    multi-GPU ranks): every Score plugin's weight in [1, 5] and the Fit
+    strategy drawn per replica; replica 0 is the default profile itself."""
+    out = [P.default_profile()]
+    for r in range(1, n_replicas):
+        rng = np.random.Generator(np.random.PCG64(seed + r))
+        prof = P.default_profile()
+        prof.plugins = [(n, int(rng.integers(1, 6)) if w else 0) for n, w in prof.plugins]
+        prof.fit_strategy = P.LEAST_ALLOCATED if rng.random() < 0.5 else P.MOST_ALLOCATED
+        out.append(prof)
+    return out
+
+
 def config4(n_replicas: int = 1024, n_nodes: int = 5000, n_pods: int = 50000):
     nodes, pods, base = config2(n_nodes, n_pods, seed=2)
     return nodes, pods, base, replica_profiles(n_replicas)

@@ -6,8 +6,11 @@ the import of `Lib` fails loudly, so no GPU test can pass on a CPU path.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
+import shutil
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -19,6 +22,47 @@ LIB_PATH = os.path.join(HERE, "libksched.so")
 
 NPLUGINS = 14
 MAX_RES = 8
+
+# Every live native handle (Engine, Snapshot, Annotator) is closed by an
+# atexit hook before the interpreter tears down, most recently opened first,
+# so no context is freed from __del__ during finalisation or left for the HIP
+# runtime's own exit handlers (under rocprofv3 the process used to end in
+# SIGSEGV inside exit()).  KSG_EXIT_MAPS=<path> also copies
+# /proc/self/maps there at that point, to map a crash in a later exit handler
+# to its library.
+_LIVE: "weakref.WeakValueDictionary[int, object]" = weakref.WeakValueDictionary()
+_SEQ = [0]
+_HOOKED = [False]
+
+
+def _close_all():
+    path = os.environ.get("KSG_EXIT_MAPS")
+    if path:
+        try:
+            shutil.copyfile("/proc/self/maps", path)
+        except OSError:
+            pass
+    if os.environ.get("KSG_NO_EXIT_CLOSE") == "1":   # diagnostic: leave the handles to finalisation
+        return
+    for k in sorted(_LIVE.keys(), reverse=True):
+        obj = _LIVE.get(k)
+        if obj is not None:
+            try:
+                obj.close()
+            except Exception:
+                pass
+
+
+def track(obj) -> None:
+    """Register a native handle for the exit hook (registered on the first
+    handle, i.e. after the process has initialised the GPU: atexit runs the
+    newest hooks first, so this one runs before torch's)."""
+    _SEQ[0] += 1
+    _LIVE[_SEQ[0]] = obj
+    if not _HOOKED[0]:
+        atexit.register(_close_all)
+        _HOOKED[0] = True
+
 
 i32p = C.POINTER(C.c_int32)
 u32p = C.POINTER(C.c_uint32)
@@ -204,6 +248,7 @@ class Engine:
         self._check(self._open(device, C.byref(self.ctx)))
         self._m: Optional[Marshalled] = None
         self._nn = 0
+        track(self)
 
     def _declare(self):
         f = _bind(self.lib, self.PREFIX)
@@ -478,6 +523,7 @@ class Annotator:
         if rc != 0:
             raise KschedError(f"ksg_annotator_new rc={rc}")
         self.n_nodes = len(node_names)
+        track(self)
 
     def annotate(self, filter_order, score_order, normalize_mask: int, weight, n_feasible: int,
                  fstatus: np.ndarray, raw: np.ndarray, norm: np.ndarray):

@@ -308,6 +308,7 @@ class Snapshot:
         self._add_pod = f("add_pod", C.c_int, vp, C.POINTER(PodView), C.POINTER(i32))
         self._add_ns = f("add_namespace", C.c_int, vp, cp, i32, C.POINTER(StrPair))
         self._hint_pod = f("hint_pod", C.c_int, vp, C.POINTER(PodView))
+        self._unhint_pod = f("unhint_pod", C.c_int, vp, cp, cp)
         self._bind_ = f("bind", C.c_int, vp, i32, i32)
         self._encode = f("encode", C.c_int, vp)
         self._encode_inc = f("encode_incremental", C.c_int, vp, C.POINTER(i32))
@@ -329,6 +330,7 @@ class Snapshot:
         rc = self._new(C.byref(profile_view(prof, k)), C.byref(self.h))
         if rc != 0:
             raise SnapshotError(f"ksg_snapshot_new rc={rc}")
+        native.track(self)
         self.prof = prof
         self.n_pods = 0
         for name, labels in namespaces:
@@ -387,6 +389,10 @@ class Snapshot:
         encoding universe now, so its later add_pod appends in place."""
         k = _Keep()
         self._check(self._hint_pod(self.h, C.byref(pod_view(p, k))), "hint_pod")
+
+    def unhint_pod(self, namespace: str, name: str) -> None:
+        """ksg_snapshot_unhint_pod: a hinted pending pod was deleted."""
+        self._check(self._unhint_pod(self.h, _b(namespace), _b(name)), "unhint_pod")
 
     def bind(self, pod: int, node: int):
         self._check(self._bind_(self.h, pod, node), "bind")

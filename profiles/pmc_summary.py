@@ -2,8 +2,8 @@
 
   python profiles/pmc_summary.py <run_pmc out dir> <dest dir>
 
-Writes <dest>/{bench,sweep,topo,cycle}_kernel_stats.csv (the --stats
-summaries, copied), <dest>/pmc_{config2,config4,config3,per_cycle}.json and,
+Writes <dest>/{bench,c1,sweep,topo,cycle,c5}_kernel_stats.csv (the --stats
+summaries, copied), <dest>/pmc_{default,config2,config4,config3,per_cycle,config5}.json and,
 where an SQ pass ran, <dest>/sq_<config>.json (average counter values per
 dispatch).  pmc_*.json: per kernel, dispatches, average
 FETCH_SIZE and WRITE_SIZE per dispatch (KB as rocprofv3 reports them) and HBM
@@ -62,7 +62,7 @@ def counters_by_name(path):
 def main():
     src, dest = sys.argv[1], sys.argv[2]
     os.makedirs(dest, exist_ok=True)
-    for tag, cfg in (("bench", "config2"), ("sweep", "config4"), ("topo", "config3"), ("cycle", "per_cycle"),
+    for tag, cfg in (("bench", "default"), ("c1", "config2"), ("sweep", "config4"), ("topo", "config3"), ("cycle", "per_cycle"),
                      ("c5", "config5")):
         if not glob.glob(os.path.join(src, f"{tag}_*")):
             continue

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Profiles on one MI355X (run from the repo root on the GPU box):
-#   1. rocprofv3 --kernel-trace --stats of the default bench (config 2)
-#   2. PMC passes FETCH_SIZE and WRITE_SIZE (separate runs) of the same bench
+#   1. rocprofv3 --kernel-trace --stats of the headline bench (default profile
+#      at 5,000 x 50,000) and of configs[1] (bench.py --workload configs1)
+#   2. PMC passes FETCH_SIZE and WRITE_SIZE (separate runs) of the same two
 #   3. the same three for the config-4 replica sweep (scripts/bench_configs.py)
 #   4. TOPO=1: configs[2]'s topology kernel (kernel trace, FETCH / WRITE, SQ mix)
 #   5. CYCLE=1: the per-cycle path (scripts/percycle.py)
@@ -15,20 +16,17 @@ export TMPDIR=/tmp
 ( while sleep 45; do date >> "$OUT/heartbeat.txt"; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --sweep-replicas 0 --annotate-pods 0 --default-pods 0 --cycle-pods 0"
+B="python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --configs1-pods 0 --sweep-replicas 0 --annotate-pods 0 --cycle-pods 0 --kubelet-pods 0 --topo-cycle-pods 0 --topo-annotate-pods 0"
+B1="$B --workload configs1"
 S="python3 scripts/bench_configs.py --config 4 --replicas 1024 --pods 256 --reps 1 --no-cpu-baseline"
 SP="$S --no-timing"
 run() {  # name, rocprof args..., -- command
   local name=$1; shift
-  timeout -k 10 240 rocprofv3 "$@" > "$OUT/$name.log" 2>&1
+  # every profiled process must exit 0: native handles are closed by an
+  # atexit hook (native.track), and a crash at exit is a failure, not noise
+  KSG_EXIT_MAPS="$OUT/$name.maps" timeout -k 10 240 rocprofv3 "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
-  # rocprofv3 7.2 can crash in its own exit handler (SIGSEGV, rc 139) after
-  # writing every file: accept that when the CSVs are there, nothing else
-  if [ $rc -eq 139 ] && ls "$OUT/$name"/*.csv > /dev/null 2>&1 && grep -q "Profiling.*done\|Opened result file\|kernel_stats\|counter_collection" "$OUT/$name.log" 2>/dev/null; then
-    echo "$name: profiler crashed at exit after writing its output (kept)"
-    return 0
-  fi
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit 1; }
 }
 if [ -z "${SKIP_BENCH:-}" ]; then
@@ -38,6 +36,11 @@ run bench_kt --kernel-trace --stats --output-format csv -d "$OUT/bench_kt" -o ru
 export KSG_PIPE_OVERLAP=0
 run bench_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/bench_fetch" -o run -- $B
 run bench_write --pmc WRITE_SIZE --output-format csv -d "$OUT/bench_write" -o run -- $B
+unset KSG_PIPE_OVERLAP
+run c1_kt --kernel-trace --stats --output-format csv -d "$OUT/c1_kt" -o run -- $B1
+export KSG_PIPE_OVERLAP=0
+run c1_fetch --pmc FETCH_SIZE --output-format csv -d "$OUT/c1_fetch" -o run -- $B1
+run c1_write --pmc WRITE_SIZE --output-format csv -d "$OUT/c1_write" -o run -- $B1
 unset KSG_PIPE_OVERLAP
 fi
 if [ -z "${SKIP_SWEEP:-}" ]; then

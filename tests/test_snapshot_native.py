@@ -435,3 +435,38 @@ def test_hinted_pods_append_in_place(built):
     o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
     want, _ = o.run_queue(0, len(pods), results=False)
     np.testing.assert_array_equal(_oracle_on_views(snap, len(pods)), want)
+
+
+def test_hint_without_new_terms_keeps_appending(built):
+    """a hint re-encodes only when it brings something new into the
+    universe.  A hinted pending pod like the ones already encoded keeps the
+    next sync on the append path; a hint with a label key nobody references
+    yet re-encodes once; hints are dropped when their pod is added or
+    deleted; and the result still schedules exactly as the Python encoder's."""
+    import copy
+    nodes, pods, prof = G.config2(n_nodes=120, n_pods=300)
+    snap = S.Snapshot(prof, nodes, pods[:100])
+    snap.encode()
+    for k in range(100, 200):   # pending pods announced one per cycle, as the Go shim does
+        snap.hint_pod(pods[k])
+        snap.add_pod(pods[k])
+        assert snap.encode_incremental(), f"pod {k}: a hint of known terms forced a re-encode"
+    novel = copy.deepcopy(pods[200])
+    novel.node_selector = {"example.com/brand-new-key": "x"}
+    snap.hint_pod(novel)
+    snap.add_pod(pods[201])
+    assert not snap.encode_incremental()   # the new key joins the universe: one full encode
+    snap.add_pod(pods[202])
+    assert snap.encode_incremental()
+    snap.unhint_pod(novel.namespace, novel.name)
+    for k in range(203, 300):
+        snap.add_pod(pods[k])
+        assert snap.encode_incremental()
+    snap.unhint_pod("default", "no-such-pod")   # unknown: ignored
+    order = pods[:200] + pods[201:300]
+    enc = E.Encoder(nodes, order, prof)
+    import binding
+    o = binding.Oracle(4)
+    o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    want, _ = o.run_queue(0, len(order), results=False)
+    np.testing.assert_array_equal(_oracle_on_views(snap, len(order)), want)
