@@ -69,6 +69,7 @@ __device__ __forceinline__ void cap_put(int64_t* base, size_t idx, int64_t v, bo
   else base[idx] = v;
 }
 
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
@@ -167,7 +168,9 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
     if (a.best && l) atomicMax(&a.stats[4 * j + 3], l);
   }
 }
+#endif  // KSG_PART
 
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_capture_norm(CapArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
@@ -229,4 +232,5 @@ __global__ __launch_bounds__(256) void ksg_capture_norm(CapArgs a) {
     }
   }
 }
+#endif  // KSG_PART
 

@@ -86,27 +86,6 @@ struct CycArgs {
   unsigned long long* stamps;        // KSG_STAMPS builds: per-segment cycle sums of workgroup 0
 };
 
-// Stores into the host block.  SYS: system-scope relaxed stores (global_store
-// sc0 sc1: written through to the fine-grained host memory, nothing left in
-// L2), so a vmcnt(0) wait orders them before the flag and no L2 write-back
-// (buffer_wbl2) is needed; else plain stores + __threadfence_system.
-template <bool SYS, class T>
-__device__ __forceinline__ void hst(T* p, T v) {
-  if constexpr (SYS) __hip_atomic_store((__attribute__((address_space(1))) T*)p, v, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_SYSTEM);
-  else *p = v;
-}
-template <bool SYS>
-__device__ __forceinline__ void cyc_put(char* base, size_t idx, int64_t v, bool narrow) {
-  if (narrow) hst<SYS>(reinterpret_cast<int32_t*>(base) + idx, (int32_t)v);
-  else hst<SYS>(reinterpret_cast<int64_t*>(base) + idx, v);
-}
-template <bool SYS>
-__device__ __forceinline__ void cyc_put_es(char* base, size_t idx, int64_t v, int es) {
-  if (es == 2) hst<SYS>(reinterpret_cast<int16_t*>(base) + idx, (int16_t)v);
-  else cyc_put<SYS>(base, idx, v, es == 4);
-}
-
 #ifdef KSG_STAMPS
 #define KSG_YSTAMP(seg)                                                       \
   do {                                                                        \
@@ -118,14 +97,6 @@ __device__ __forceinline__ void cyc_put_es(char* base, size_t idx, int64_t v, in
 #else
 #define KSG_YSTAMP(seg) do {} while (0)
 #endif
-// Every host store of this wave performed before what follows (the arrival,
-// the flag).
-template <bool SYS>
-__device__ __forceinline__ void host_release() {
-  if constexpr (SYS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else __threadfence_system();
-}
-
 // Grid exchange: workgroup g stores `seq` into its own flag line, wave 0 polls
 // every flag until all hold `seq` (bounded; a timeout is sticky and reported).
 template <int BLOCK>

@@ -460,6 +460,9 @@ struct NodeEval {
 // Diagnostic build only: per-segment cycles of eval_node_src, lane 0 of
 // workgroup 0 (slot 0 the node-set check, 1 + p filter plugin p, 13 the Fit /
 // BalancedAllocation scores, 14 ImageLocality + TaintToleration, 15 NodeAffinity).
+#ifdef KSG_PART
+static   // a part's own copy (diagnostic stamps are read from the host TU's)
+#endif
 __device__ unsigned long long g_eval_stamp[16];
 #define KSG_ESTAMP(k)                                                          \
   do {                                                                         \

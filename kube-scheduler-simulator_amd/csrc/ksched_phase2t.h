@@ -376,6 +376,7 @@ __device__ __forceinline__ TcFetch<P> tc_fetch(const BatchArgs& a, const SlotPla
 // [nb][N] -> [N][qs] copies of the phase-1 records and the N32 statics (rows
 // beyond nb are left as they are: the walk never reads them for a live pod).
 // Tiles of 32 nodes through LDS: reads and writes are both contiguous.
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_batch_transpose(BatchArgs a) {
   __shared__ uint64_t s_r[128][33];
   __shared__ int32_t s_s[128][33];
@@ -410,6 +411,7 @@ __global__ __launch_bounds__(256) void ksg_batch_transpose(BatchArgs a) {
     }
   }
 }
+#endif  // KSG_PART
 
 template <int P>
 __global__ __launch_bounds__(64) void ksg_batch_phase2t(BatchArgs a) {

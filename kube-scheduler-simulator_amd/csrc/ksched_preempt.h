@@ -232,6 +232,7 @@ __device__ __forceinline__ void pre_delta(const TopoProg& g, const TopoShared& t
   }
 }
 
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_preempt_topo(DevCluster c, DevState st, const ksg_pod* pods,
                                                         const int32_t* prog, const ksg_profile* profp, int pod,
                                                         const PreemptTopo* topo, const int32_t* cand, int n_cand,
@@ -353,3 +354,4 @@ __global__ __launch_bounds__(256) void ksg_preempt_topo(DevCluster c, DevState s
     victim[i] = out;
   }
 }
+#endif  // KSG_PART

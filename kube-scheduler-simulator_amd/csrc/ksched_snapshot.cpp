@@ -486,6 +486,7 @@ struct ksg_snapshot {
   // binding: they are not pods of the workload.
   std::vector<Pod> hints;
   size_t hints_seen = 0;            // hints[0, hints_seen) are inside the current encoding universe
+  std::unordered_map<std::string, size_t> hint_index;   // "ns/name" -> index in hints
   std::vector<std::pair<int32_t, int32_t>> binds;   // (pod, node) in order: bound, then assumed
   Encoded e;
   bool encoded = false;     // e reflects nodes and pods [0, n_encoded)
@@ -2018,15 +2019,32 @@ int pod_from_view(ksg_snapshot* s, const ksg_pod_view* v, Pod& p) {
 }
 }  // namespace
 
-// Forget the hint of pod ns/name, if any (the pod was added or deleted).  The
-// current encoding keeps what the hint brought in until the next full encode.
+std::string hint_key(const std::string& ns, const std::string& name) { return ns + '/' + name; }
+
+void hint_swap(ksg_snapshot* s, size_t i, size_t j) {
+  if (i == j) return;
+  std::swap(s->hints[i], s->hints[j]);
+  s->hint_index[hint_key(s->hints[i].ns, s->hints[i].name)] = i;
+  s->hint_index[hint_key(s->hints[j].ns, s->hints[j].name)] = j;
+}
+
+// Forget the hint of pod ns/name, if any (the pod was added or deleted), in
+// O(1): swapped to the end and popped.  A hint inside the probed prefix
+// [0, hints_seen) first trades places with the prefix's last entry, so the
+// entry that lands at the prefix boundary is re-probed (a seen hint probes
+// clean, so that costs one probe, never a result).  The current encoding
+// keeps what the hint brought in until the next full encode.
 void drop_hint(ksg_snapshot* s, const std::string& ns, const std::string& name) {
-  for (size_t k = 0; k < s->hints.size(); k++)
-    if (s->hints[k].ns == ns && s->hints[k].name == name) {
-      s->hints.erase(s->hints.begin() + (std::ptrdiff_t)k);
-      if (k < s->hints_seen) s->hints_seen--;
-      return;
-    }
+  auto it = s->hint_index.find(hint_key(ns, name));
+  if (it == s->hint_index.end()) return;
+  size_t k = it->second;
+  if (k < s->hints_seen) {
+    hint_swap(s, k, s->hints_seen - 1);
+    k = --s->hints_seen;
+  }
+  hint_swap(s, k, s->hints.size() - 1);
+  s->hint_index.erase(hint_key(ns, name));
+  s->hints.pop_back();
 }
 
 int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* v, int32_t* index) {
@@ -2051,6 +2069,7 @@ int ksg_snapshot_hint_pod(ksg_snapshot* s, const ksg_pod_view* v) {
   for (auto& kv : pod_requests(p, false))
     if (is_scalar(kv.first)) s->scalars.insert(kv.first);
   drop_hint(s, p.ns, p.name);   // announced again: the newer spec replaces the older
+  s->hint_index[hint_key(p.ns, p.name)] = s->hints.size();
   s->hints.push_back(std::move(p));
   return KSG_OK;
 }

@@ -224,6 +224,7 @@ __device__ __forceinline__ uint64_t static_record(const DevCluster& c, const ksg
          ((uint64_t)(tslot < 0 ? 0 : tslot & 0xffff) << kSrTaintSlotShift);
 }
 
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
@@ -249,6 +250,7 @@ __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   if (n >= N) return;
   a.srec[(size_t)j * N + n] = static_record(c, p, v, n, eff_lds ? s_eff : c.taint_effect);
 }
+#endif  // KSG_PART
 
 // Replica-uniform facts of a profile for the sweep.
 struct SweepProf {
@@ -794,6 +796,7 @@ struct NarrowBounds {
 // from the context's state): one static record per node, the mutable record
 // broadcast.  A node outside the ranges sets *bad; the host then runs the
 // int64 instances instead (nothing here writes the context's state).
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st, int4* nstat, int4* nmut, int R,
                                                        NarrowBounds b, unsigned* bad) {
   const int n = blockIdx.x * 256 + threadIdx.x;
@@ -826,8 +829,10 @@ __global__ __launch_bounds__(256) void ksg_narrow_init(DevCluster c, DevState st
   if (blockIdx.y == 0) nstat[n] = make_int4((int32_t)ac, (int32_t)(am >> kNarrowMemShift), al, (int32_t)ae);
   for (int r = blockIdx.y; r < R; r += gridDim.y) nmut[(size_t)r * N + n] = mu;
 }
+#endif  // KSG_PART
 
 // Σ requested cpu / memory per replica from the narrow state (the summaries).
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_narrow_sums(const int4* nmut, int N, uint32_t cpu_mask, int64_t* out) {
   __shared__ int64_t s_p[2][4];
   const int4* q = nmut + (size_t)blockIdx.x * N;
@@ -847,3 +852,4 @@ __global__ __launch_bounds__(256) void ksg_narrow_sums(const int4* nmut, int N, 
     out[2 * blockIdx.x + 1] = s_p[1][0] + s_p[1][1] + s_p[1][2] + s_p[1][3];
   }
 }
+#endif  // KSG_PART

@@ -101,6 +101,7 @@ constexpr int kTopoFill = 24;   // fill tasks per pod: kMaxHard + kMaxSoft + kMa
 // the topology kernel lays its histograms out (hard, soft without a hostname
 // key, affinity, anti-affinity, preferred), so the kernel's fill needs no
 // dependent index load.
+#ifndef KSG_PART
 __global__ __launch_bounds__(64) void ksg_topo_tables_elig(DevCluster c, TopoTables t, const ksg_pod* pods,
                                                            const int32_t* prog, int count, uint8_t* elig,
                                                            int4* fo) {
@@ -138,6 +139,7 @@ __global__ __launch_bounds__(64) void ksg_topo_tables_elig(DevCluster c, TopoTab
   }
   for (; k < kTopoFill; k++) out[k] = make_int4(-1, -1, -1, -1);
 }
+#endif  // KSG_PART
 
 // One table-building task per workgroup (ksg_topo_tables_init).
 struct TopoTableTask {
@@ -150,6 +152,7 @@ struct TopoTableTask {
 // histogram over the task's values, one pass over the nodes.
 constexpr int kTableLds = 8192;   // LDS words of a task's histogram (vocab / Kc bins)
 
+#ifndef KSG_PART
 __global__ __launch_bounds__(256) void ksg_topo_tables_init(DevCluster c, DevState st, TopoTables t,
                                                              const TopoTableTask* tasks) {
   __shared__ int32_t s_h[kTableLds];
@@ -199,6 +202,7 @@ __global__ __launch_bounds__(256) void ksg_topo_tables_init(DevCluster c, DevSta
       for (int i = tid; i < t.Kc; i += 256) t.cc[k.off + i] = s_h[i];
   }
 }
+#endif  // KSG_PART
 
 // The pending effect of one assume on the tables and template tables, as every
 // workgroup of the topology kernel knows it one pod late (the lag buffers).
