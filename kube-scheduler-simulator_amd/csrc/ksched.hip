@@ -192,12 +192,12 @@ struct ksg_ctx {
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
   int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
-  int cycle_block = 128;                    // env KSG_CYCLE_BLOCK: nodes per workgroup of ksg_eval_cycle (64/128/256)
-  bool cycle_sys = false;                    // plain host stores + __threadfence_system (measured faster); env KSG_CYCLE_SYS=1: system-scope stores
+  CycArgs cyc_args{};                       // ksg_eval_cycle's launch arguments, rebuilt in place per call
+  int cycle_kn = 1;                         // env KSG_CYCLE_KN (1/2/4): the smallest nodes-per-lane tried (tests)
   bool cycle_coop = false;                  // per-cycle launch: plain (G within the occupancy API's residency,
                                             // ~7 us less host time); cooperative after an exchange timeout,
                                             // or always with env KSG_CYCLE_COOP=1
-  int cycle_cap[3] = {0, 0, 0};             // co-resident ksg_eval_cycle workgroups per block size (0 = not queried)
+  int cycle_cap[3] = {0, 0, 0};             // co-resident ksg_eval_cycle workgroups per KN = 1, 2, 4 (0 = not queried)
   // pinned staging of ksg_append_pods (the per-cycle append needs no host wait)
   char* h_stage = nullptr;
   size_t h_stage_bytes = 0;
@@ -1850,30 +1850,29 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   const size_t es = bound < (1 << 15) ? 2 : bound < (1ll << 31) ? 4 : 8;
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
-  // workgroup size: the configured one, or a larger one when the grid would
-  // not be co-resident (the exchange needs every workgroup resident; the
-  // cooperative launch refuses otherwise)
-  auto kernel_of = [&](int b) -> const void* {
-    if (b == 64) return ctx->cycle_sys ? (const void*)ksg_eval_cycle<64, true> : (const void*)ksg_eval_cycle<64, false>;
-    if (b == 128) return ctx->cycle_sys ? (const void*)ksg_eval_cycle<128, true> : (const void*)ksg_eval_cycle<128, false>;
-    return ctx->cycle_sys ? (const void*)ksg_eval_cycle<256, true> : (const void*)ksg_eval_cycle<256, false>;
+  // one-wave workgroups, KN nodes per lane: the smallest KN whose grid is
+  // co-resident (the exchange needs every workgroup resident)
+  auto kernel_of = [&](int kn) -> const void* {
+    if (kn == 1) return (const void*)ksg_eval_cycle<1>;
+    if (kn == 2) return (const void*)ksg_eval_cycle<2>;
+    return (const void*)ksg_eval_cycle<4>;
   };
-  int block = ctx->cycle_block;
-  for (;; block *= 2) {
-    const int bi = block == 64 ? 0 : block == 128 ? 1 : 2;
+  int kn = ctx->cycle_kn;
+  for (;; kn *= 2) {
+    const int bi = kn == 1 ? 0 : kn == 2 ? 1 : 2;
     if (!ctx->cycle_cap[bi]) {
       int per_cu = 0;
-      HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_of(block), block, 0));
+      HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_of(kn), 64, 0));
       hipDeviceProp_t dp;
       HIPC(ctx, hipGetDeviceProperties(&dp, ctx->device));
       // one fewer than the API's answer per CU (MI355X guide: the hardware may admit one fewer)
       ctx->cycle_cap[bi] = std::max(1, per_cu - 1) * dp.multiProcessorCount;
     }
-    if ((N + block - 1) / block <= (size_t)ctx->cycle_cap[bi]) break;
-    if (block == 256) return fail(ctx, KSG_E_UNSUPPORTED, "per-cycle evaluation: grid not co-resident");
+    if ((N + 64 * kn - 1) / (64 * kn) <= (size_t)ctx->cycle_cap[bi]) break;
+    if (kn == kCycMaxKN) return fail(ctx, KSG_E_UNSUPPORTED, "per-cycle evaluation: grid not co-resident");
   }
-  const unsigned G = (unsigned)((N + block - 1) / block);
-  const size_t Gm = (N + 63) / 64;   // the largest grid (64-lane workgroups): no reallocation on a block change
+  const unsigned G = (unsigned)((N + 64 * kn - 1) / (64 * kn));
+  const size_t Gm = (N + 63) / 64;   // the largest grid (KN = 1): no reallocation on a KN change
   // host block: stats[4] | pad | per-workgroup {key, err, done}[Gm] | fstatus[N] | raw[n_rows][N] | total[N] |
   // norm[n_normrows][N]
   const size_t o_wg = 32, o_fs = o_wg + sizeof(CycWg) * Gm, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
@@ -1926,16 +1925,60 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   char* hb = ctx->h_ev;
   char* db = ctx->d_hev;
   const unsigned seq = ++ctx->ev_seq == 0 ? ++ctx->ev_seq : ctx->ev_seq;   // never 0 (a fresh block)
-  CycArgs ca{};
+  // The launch arguments, rebuilt in place (the scalar part changes only with
+  // the context; the pod, its programs and the deferred assume per call)
+  CycArgs& ca = ctx->cyc_args;
   ca.c = ctx->c;
-  ca.st = ctx->st;
-  ca.prof = ctx->d_ev_prof;
-  ca.blob = hp.blob;   // the same pool index in the staging buffer (sprog - sbase) and in d_prog
-  ca.blob_len = hp.blob_len;
+  ca.requested = ctx->st.requested;
+  ca.nonzero = ctx->st.nonzero;
+  ca.pod_count = ctx->st.pod_count;
+  ca.used_ports = ctx->st.ports;
+  ca.pod = hp;
+  // the profile facts of this pod (make_view(topo = false) + cm_prof, on the host)
+  {
+    uint32_t fskip = hp.filter_skip | (1u << KSG_PL_INTER_POD_AFFINITY) | (1u << KSG_PL_POD_TOPOLOGY_SPREAD);
+    ca.forder = 0;
+    ca.fmask = 0;
+    ca.n_filter = prof.n_filter;
+    for (int kf = 0; kf < prof.n_filter; kf++) {
+      const int pl = prof.filter_order[kf];
+      ca.forder |= (uint64_t)(pl & 15) << (4 * kf);
+      if (!((fskip >> pl) & 1u)) ca.fmask |= 1u << pl;
+    }
+    ca.smask = prof.score_mask & ~hp.score_skip &
+               ~((1u << KSG_PL_INTER_POD_AFFINITY) | (1u << KSG_PL_POD_TOPOLOGY_SPREAD));
+    ca.w_fit = prof.weight[KSG_PL_NODE_RESOURCES_FIT];
+    ca.w_ba = prof.weight[KSG_PL_BALANCED_ALLOCATION];
+    ca.w_img = prof.weight[KSG_PL_IMAGE_LOCALITY];
+    ca.w_t = prof.weight[KSG_PL_TAINT_TOLERATION];
+    ca.w_a = prof.weight[KSG_PL_NODE_AFFINITY];
+    ca.fit_ignored = prof.fit_ignored_res;
+    bool ok = prof.fit_n == 2 && prof.ba_n == 2;   // cm_prof (ksched_device.h)
+    int64_t wc = 0, wm = 0;
+    if (ok) {
+      const int r0 = prof.fit_res[0], r1 = prof.fit_res[1];
+      ok = (r0 == KSG_RES_CPU && r1 == KSG_RES_MEM) || (r0 == KSG_RES_MEM && r1 == KSG_RES_CPU);
+      wc = r0 == KSG_RES_CPU ? prof.fit_w[0] : prof.fit_w[1];
+      wm = r0 == KSG_RES_CPU ? prof.fit_w[1] : prof.fit_w[0];
+      const int b0 = prof.ba_res[0], b1 = prof.ba_res[1];
+      ok = ok && ((b0 == KSG_RES_CPU && b1 == KSG_RES_MEM) || (b0 == KSG_RES_MEM && b1 == KSG_RES_CPU));
+      ok = ok && wc > 0 && wm > 0;
+    }
+    ca.cm_fast = ok;
+    ca.cm_least = prof.fit_strategy == KSG_LEAST_ALLOCATED;
+    ca.cm_wc = ok ? wc : 0;
+    ca.cm_wm = ok ? wm : 0;
+    ca.cm_inv_ws = ok ? 1.0f / (float)(wc + wm) : 1.0f;
+    ca.cm_inv_wc = ok ? 1.0f / (float)wc : 1.0f;
+    ca.cm_inv_wm = ok ? 1.0f / (float)wm : 1.0f;
+  }
+  ca.gprof = ctx->d_ev_prof;
   ca.n_rows = n_rows;
   ca.n_normrows = n_normrows;
-  for (int q = 0; q < n_rows; q++) ca.rows[q] = rows[q];
   ca.es = (int32_t)es;
+  ca.kn = kn;
+  ca.rows = 0;
+  for (int q = 0; q < n_rows; q++) ca.rows |= (uint64_t)(rows[q] & 15) << (4 * q);
   ca.h_fs = reinterpret_cast<uint32_t*>(db + o_fs);
   ca.h_raw = db + o_raw;
   ca.h_tot = db + o_tot;
@@ -1946,6 +1989,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   ca.parts = reinterpret_cast<CycPart*>(ctx->d_ev);
   ca.flags = reinterpret_cast<unsigned*>(ctx->d_ev + d_flags);
   ca.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_to);
+  ca.stamps = nullptr;
 #ifdef KSG_STAMPS
   if (!ctx->d_stamps) {
     if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
@@ -1953,12 +1997,17 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   }
   ca.stamps = ctx->d_stamps;
 #endif
-  // the pod's record and programs: the staged append (read over the host
-  // link, then written to the device pool by workgroup 0) or the device pool
+  // the pod's programs: inline in the arguments (from the host copy) when they
+  // fit, else read by the kernel from the staged append or the device pool
   const int32_t* sprog = staged ? reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod)) : nullptr;
   ca.gprog = staged ? sprog - ctx->stage_base : ctx->d_prog;
-  ca.psrc = staged ? reinterpret_cast<const int32_t*>(ctx->d_stage) : reinterpret_cast<const int32_t*>(ctx->d_pods + pod);
+  ca.blob_len = hp.blob_len;
   ca.bsrc = ca.gprog + hp.blob;
+  if (hp.blob_len <= kCycBlob && hp.blob >= 0 && (size_t)hp.blob + hp.blob_len <= ctx->h_prog.size())
+    std::memcpy(ca.blob, ctx->h_prog.data() + hp.blob, sizeof(int32_t) * hp.blob_len);
+  else if (hp.blob_len <= kCycBlob)
+    return fail(ctx, KSG_E_STATE, "per-cycle evaluation: pod programs outside the host program copy");
+  ca.wpods = nullptr;
   if (staged) {
     ca.wpods = ctx->d_pods + pod;
     ca.wprog = ctx->d_prog + ctx->stage_base;
@@ -1977,9 +2026,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   if ((rc = tmark(ctx))) return rc;
   void* kargs[] = {&ca};
   if (ctx->cycle_coop)
-    HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
+    HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(kn), dim3(G), dim3(64), kargs, 0, ctx->stream));
   else   // G is within the occupancy API's co-resident count less one per CU (the exchange's poll is bounded)
-    HIPC(ctx, hipLaunchKernel(kernel_of(block), dim3(G), dim3(block), kargs, 0, ctx->stream));
+    HIPC(ctx, hipLaunchKernel(kernel_of(kn), dim3(G), dim3(64), kargs, 0, ctx->stream));
   ctx->pc_node = -1;   // applied by this launch (a retry below must not add it again)
   if ((rc = tlaunched(ctx, KSG_K_EVAL_CYCLE, (double)N))) return rc;
   HIPC(ctx, hipGetLastError());
@@ -2481,12 +2530,11 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_PIPE_OVERLAP")) ctx->pipe_overlap = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
-  if (const char* f = getenv("KSG_CYCLE_BLOCK")) {
-    const int v = atoi(f);
-    ctx->cycle_block = v <= 64 ? 64 : v <= 128 ? 128 : 256;
-  }
-  if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_KN")) {
+    const int v = atoi(f);
+    ctx->cycle_kn = v >= 4 ? 4 : v >= 2 ? 2 : 1;
+  }
   if (const char* f = getenv("KSG_TEST_INJECT_WALK_ERR")) ctx->inject_walk_err = atoi(f) != 0;
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);

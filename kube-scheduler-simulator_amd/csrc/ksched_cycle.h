@@ -1,41 +1,56 @@
 // The per-cycle evaluation (ksg_eval's fast path, the Go shim's one call per
-// scheduling cycle, wrappedplugin.go:388-548), included by ksched.hip inside
-// its anonymous namespace.
+// scheduling cycle, wrappedplugin.go:388-548), included by ksched_dev.h inside
+// namespace ksk.
 //
-// One launch of G = ceil(N / BLOCK) co-resident workgroups (cooperative
-// launch), one node per lane, results written straight into the pinned,
-// fine-grained host block the caller reads in place (ksg_eval_view):
+// One launch of G = ceil(N / (64 KN)) one-wave workgroups, all co-resident,
+// KN nodes per lane (lane l of workgroup g owns nodes (k G + g) 64 + l),
+// results written straight into the pinned, fine-grained host block the
+// caller reads in place (ksg_eval_view).  The round-5 form is built around
+// the latency chain of one wave, not around throughput:
 //
-//   phase 1 (every workgroup)  stage the pod into LDS; evaluate its nodes
-//                              (filters in profile order, raw scores); store
-//                              each node's status word and raw score rows to
-//                              the host block at once (coalesced, in flight
-//                              during the exchange); keep the packed record in
-//                              registers; publish the workgroup's feasible
-//                              count, TaintToleration / NodeAffinity maxima and
-//                              lowest feasible index in its own slot
-//   exchange                   grid barrier on per-workgroup flags (one
-//                              128-byte line each, tagged with the call's
-//                              sequence number, so nothing is reset per call)
-//   phase 2 (every workgroup)  fold the G slots (every workgroup computes the
-//                              same pod-wide values), normalise its own nodes
-//                              (DefaultNormalizeScore), store the normalised
-//                              rows and weighted totals, its selectHost key;
-//                              a pod with < 2 feasible nodes ran no Score, so
-//                              its raw rows are zeroed instead
-//   completion                 every workgroup writes its selectHost key and
-//                              error bits into its own record of the host
-//                              block, then (after its rows) its done word =
-//                              the call's sequence number; the host folds the
-//                              G keys (no arrival counter, no last workgroup)
+//   entry      the kernel arguments carry everything the wave needs: the node
+//              column pointers, the pod record, the profile facts the host
+//              derived for this pod (filter order as nibbles, the filters and
+//              scores that run, weights, the compact Fit / BalancedAllocation
+//              form) and up to kCycBlob words of the pod's programs.  Every
+//              64-byte line of the scalar part is touched by one s_load at
+//              entry (one miss latency for all of them, instead of one per
+//              use site deep in the evaluation: round 4's kernel waited on
+//              ~60 scattered kernel-argument loads); the programs are copied
+//              to LDS by vector loads issued beside them.
+//   prefetch   every node column the evaluation can touch is loaded at once:
+//              the resource columns, the unschedulable byte, the first
+//              kCycLab label columns, kCycTnt taint slots and (scoring
+//              ImageLocality) kCycImg image slots into registers, the taint
+//              effect table into LDS; a deeper column falls back to a global
+//              load.
+//   evaluate   every filter the pod runs is evaluated independently (no
+//              first-rejection chain of dependent loads), then the status word
+//              is the first rejection in profile order; raw scores of a
+//              feasible node.
+//   exchange   the wave's feasible count, TaintToleration / NodeAffinity
+//              maxima and lowest feasible index (DPP reductions) go to its
+//              own slot; grid exchange on per-workgroup flags tagged with the
+//              call's sequence number (agent-scope stores and loads, no reset
+//              between calls); every workgroup folds the G slots.
+//   rows       status words, raw, normalised and total rows (2, 4 or 8 bytes)
+//              with plain stores to the host block, one system-scope release,
+//              then the workgroup's selectHost key, error bits and done word.
 //
-// No workgroup walks all N nodes and every row is written once.  The
-// exchange follows ksched_sweep.h (gst / gld: agent-scope stores and loads,
-// every wave drained before the workgroup barrier in front of the flag); the
-// host-visible bytes are system-scope stores drained (vmcnt(0)) before the
-// workgroup's done word.  Rows are 2, 4 or 8 bytes per value (the narrowest
-// exact width, chosen by the host).  Same arithmetic as ksg_capture_eval +
-// ksg_capture_norm (nb = 1, nothing assumed), bit for bit.
+// The evaluation is eval_node_src's arithmetic (same helpers: untolerated_slot,
+// na_required_match, fit_filter, fit_ba_cm / fit_score / ba_score,
+// image_score, taint_score, na_pref_score) on a prefetched node source, and
+// the normalisation is total_score's (untolerated_slot / taint_score /
+// image_score restated on the prefetched registers: pnode_taints,
+// pnode_image_score): results equal ksg_capture_eval +
+// ksg_capture_norm (nb = 1, nothing assumed) bit for bit.
+
+constexpr int kCycBlob = 256;    // program words carried in the kernel arguments
+constexpr int kCycLab = 8;       // label columns prefetched into registers
+constexpr int kCycTnt = 8;       // taint slots prefetched into registers
+constexpr int kCycImg = 8;       // image slots prefetched into registers (ImageLocality pods)
+constexpr int kCycEff = 4096;    // taint-effect bytes staged in LDS
+constexpr int kCycMaxKN = 4;     // nodes per lane
 
 struct CycPart {   // one workgroup's phase-1 statistics
   int32_t nfeas, max_t, max_a, lo;   // lo = max over its feasible nodes of N - n
@@ -46,32 +61,40 @@ struct CycWg {     // one workgroup's record in the host block
   uint32_t done;            // = seq once every row of the workgroup and the two words above are written
 };
 
-// The launch arguments.  The prologue's fields come first and together: the
-// kernel-argument segment is read with scalar loads, and fields the compiler
-// reaches through separate branches cost one round trip each.
+// The launch arguments.  Scalar part first (warmed line by line at entry),
+// the program words last (copied to LDS by vector loads).
 struct CycArgs {
-  // ---- prologue ----
-  const int32_t* psrc;               // the pod record: device pool or staged append
-  const int32_t* bsrc;               // its program blob
-  const int32_t* gprog;              // the program pool as the kernel sees it (node_set)
-  const ksg_profile* prof;
-  int32_t blob, blob_len;            // the pod's program blob (host copy of pods[pod].blob / blob_len)
-  int32_t cm_node;                   // a deferred assume (ksg_commit of a pod without selectors, templates or
-                                     // host ports) onto node cm_node, -1 none: its owner lane adds it first
+  // ---- node columns and state --------------------------------------------------------
+  DevCluster c;
+  int64_t* requested;
+  int64_t* nonzero;
+  int32_t* pod_count;
+  const uint32_t* used_ports;
+  const int32_t* gprog;              // the program pool as the kernel sees it (node_set; programs not inline)
+  // ---- the pod and its profile facts (host-derived) ----------------------------------
+  ksg_pod pod;
+  uint64_t forder;                   // filter plugins in profile order, 4 bits each
+  int32_t n_filter;
+  uint32_t fmask;                    // plugins of the order that run their Filter for this pod
+  uint32_t smask;                    // plugins whose Score runs for this pod (PodView::smask)
+  int32_t w_fit, w_ba, w_img, w_t, w_a;
+  uint32_t fit_ignored;
+  int32_t cm_fast, cm_least;
+  int64_t cm_wc, cm_wm;
+  float cm_inv_ws, cm_inv_wc, cm_inv_wm;
+  const ksg_profile* gprof;          // device copy (the generic Fit / BalancedAllocation forms)
+  // ---- the deferred assume of the previous pod ---------------------------------------
+  int32_t cm_node;                   // -1: none; else its owner lane adds it first (NodeInfo.AddPod)
   int64_t cm_req[KSG_MAX_RES];
   int64_t cm_nz_cpu, cm_nz_mem;
-  // a staged append of this pod: workgroup 0 writes it to the device pool
+  // ---- a staged append of this pod: workgroup 0 writes it to the device pool ----------
   ksg_pod* wpods;                    // null: nothing staged
   int32_t* wprog;
-  const int32_t* sprog;              // the staged words
+  const int32_t* sprog;
   int64_t slen;
-  // ---- evaluation ----
-  DevCluster c;
-  DevState st;
-  int32_t n_rows, n_normrows;        // score rows (the normalising ones first)
-  int32_t rows[KSG_NPLUGINS];
-  int32_t es;                        // bytes per row value: 2, 4 or 8 (host range-checked)
-  // host outputs (fine-grained pinned memory, device addresses)
+  // ---- outputs (fine-grained pinned host memory, device addresses) -------------------
+  int32_t n_rows, n_normrows, es, kn;
+  uint64_t rows;                     // score row q's plugin in bits 4q..4q+3 (the normalising ones first)
   uint32_t* h_fs;                    // [N]
   char* h_raw;                       // [n_rows][N]
   char* h_tot;                       // [N]
@@ -79,245 +102,470 @@ struct CycArgs {
   int32_t* h_stats;                  // [4] nfeas, max taint, max node affinity, max (N - n) (workgroup 0)
   CycWg* h_wg;                       // [G]
   unsigned seq;
-  // device scratch
   CycPart* parts;                    // [G]
   unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
   unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
   unsigned long long* stamps;        // KSG_STAMPS builds: per-segment cycle sums of workgroup 0
+  const int32_t* bsrc;               // the programs when blob_len > kCycBlob
+  int32_t blob_len;
+  int32_t pad_;
+  // ---- program words (vector-loaded into LDS) ----------------------------------------
+  int32_t blob[kCycBlob];
 };
+
+// The node a lane evaluates, its columns prefetched: the first kCycLab label
+// columns in an LDS row of the lane (labels are looked up by a column the
+// pod's programs name at run time: an indexed register array would live in
+// scratch), the first kCycTnt taint and kCycImg image slots in registers
+// (read only with constant indices, by pnode_taints / pnode_image_score),
+// global memory beyond them; taint effects from the LDS copy when the
+// vocabulary fits.
+#define KSG_G1 __attribute__((address_space(1)))
+#define KSG_L3 __attribute__((address_space(3)))
+struct PNode {
+  // the columns beyond the prefetched ones (values, not a pointer to the
+  // launch arguments: taking the arguments' address copies them to scratch)
+  const KSG_G1 uint32_t* label_val;
+  const KSG_G1 int64_t* label_num;
+  const KSG_G1 uint8_t* label_num_ok;
+  const KSG_G1 uint32_t* taints;
+  const KSG_G1 uint8_t* taint_effect;
+  const KSG_G1 uint32_t* images;
+  size_t N;
+  int n;
+  const KSG_L3 uint32_t* lab;   // this lane's prefetched labels: lab[q * 64]
+  uint32_t tnt[kCycTnt], img[kCycImg];
+  bool uns;
+  bool eff_lds;
+  const KSG_L3 uint8_t* eff;
+  __device__ __forceinline__ uint32_t label(int col) const {
+    return col < kCycLab ? lab[col * 64] : label_val[(size_t)col * N + n];
+  }
+  __device__ __forceinline__ bool num(int col, int64_t& x) const {
+    const size_t k = (size_t)col * N + n;
+    if (!label_num_ok[k]) return false;
+    x = label_num[k];
+    return true;
+  }
+  __device__ __forceinline__ uint8_t effect(uint32_t vid) const { return eff_lds ? eff[vid] : taint_effect[vid]; }
+  __device__ __forceinline__ bool unsched() const { return uns; }
+};
+
+// untolerated_slot + taint_score on a prefetched node (the same walks: slots in
+// order until the 0 terminator), the register slots with constant indices.
+__device__ __forceinline__ void pnode_taints(const PNode& x, int T, const int32_t* tolf, const int32_t* tolp,
+                                             bool want_slot, bool want_score, int& slot, int64_t& score) {
+  slot = -1;
+  score = 0;
+  bool end = false;
+  auto one = [&](int s, uint32_t id) {
+    if (end || s >= T || !id) {
+      end = true;
+      return;
+    }
+    const uint32_t vid = id - 1;
+    const uint8_t e = x.effect(vid);
+    if (want_slot && slot < 0 && (e == KSG_EFFECT_NO_SCHEDULE || e == KSG_EFFECT_NO_EXECUTE) && !tol_bit(tolf, vid))
+      slot = s;
+    if (want_score && e == KSG_EFFECT_PREFER_NO_SCHEDULE) score += !tol_bit(tolp, vid);
+  };
+#pragma unroll
+  for (int s = 0; s < kCycTnt; s++) one(s, x.tnt[s]);
+  for (int s = kCycTnt; s < T && !end; s++) one(s, x.taints[(size_t)s * x.N + x.n]);
+}
+
+// image_score on a prefetched node: per container of the pod, the node's
+// ascending image slots until the id is reached or passed.
+__device__ __forceinline__ int64_t pnode_image_score(const PNode& x, int I, const int32_t* P, int img,
+                                                     int n_containers) {
+  int64_t sum = 0;
+  if (img >= 0) {
+    const int32_t* w = P + img;
+    const int cnt = *w++;
+    for (int i = 0; i < cnt; i++, w += 3) {
+      const uint32_t id = (uint32_t)w[0];
+      const int64_t contrib = ld64(w + 1);
+      bool done = false;
+#pragma unroll
+      for (int s = 0; s < kCycImg; s++) {
+        const uint32_t v = x.img[s];
+        if (!done && s < I) {
+          if (!v || v > id) done = true;
+          else if (v == id) { sum += contrib; done = true; }
+        } else {
+          done = true;
+        }
+      }
+      if (!done)
+        for (int s = kCycImg; s < I; s++) {
+          const uint32_t v = x.images[(size_t)s * x.N + x.n];
+          if (!v || v > id) break;
+          if (v == id) { sum += contrib; break; }
+        }
+    }
+  }
+  const int64_t mb = 1024 * 1024, minT = 23 * mb;
+  const int64_t mx = 1000 * mb * (int64_t)n_containers;
+  if (sum < minT) sum = minT;
+  else if (sum > mx) sum = mx;
+  return div_small(100 * (sum - minT), mx - minT);
+}
 
 #ifdef KSG_STAMPS
 #define KSG_YSTAMP(seg)                                                       \
   do {                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                        \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();               \
-    if (tid == 0 && blockIdx.x == 0) { y_acc[seg] += _t - y_last; y_last = _t; } \
+    if (blockIdx.x == 0) { y_acc[seg] += _t - y_last; y_last = _t; }          \
     __builtin_amdgcn_sched_barrier(0);                                        \
   } while (0)
 #else
 #define KSG_YSTAMP(seg) do {} while (0)
 #endif
-// Grid exchange: workgroup g stores `seq` into its own flag line, wave 0 polls
-// every flag until all hold `seq` (bounded; a timeout is sticky and reported).
-template <int BLOCK>
-__device__ __forceinline__ bool cyc_exchange(const CycArgs& a, int G) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its agent-scope stores are done
-  __syncthreads();
-  __shared__ int s_to;
-  const int tid = threadIdx.x;
-  if (tid < 64) {
-    if (tid == 0) gst(&a.flags[(size_t)blockIdx.x * 32], a.seq);
-    unsigned spins = 0;
-    int to = 0;
-    for (;;) {
-      bool ok = true;
-      for (int l = tid; l < G; l += 64) ok = ok && gld(&a.flags[(size_t)l * 32]) == a.seq;
-      if (__all(ok)) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22) || gld(a.timeout)) {
-        if (tid == 0) gst(a.timeout, 1u);
-        to = 1;
-        break;
-      }
-    }
-    if (tid == 0) s_to = to;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only: loads stay below the poll
-  __syncthreads();
-  return s_to == 0;
+
+// One scalar load per 64-byte line of CycArgs' scalar part (the first 768
+// bytes of the argument segment), all in flight together and drained by one
+// wait inside the same statement (a load may not be left pending into a
+// register the compiler reuses): every later scalar read of an argument hits
+// the scalar cache.  Loads only.
+__device__ __forceinline__ void cyc_warm_args() {
+  auto k = __builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t d0, d1, d2, d3, d4, d5, d6, d7, d8, d9, d10, d11;
+  asm volatile(
+      "s_load_dword %0, %12, 0x0\n\t"
+      "s_load_dword %1, %12, 0x40\n\t"
+      "s_load_dword %2, %12, 0x80\n\t"
+      "s_load_dword %3, %12, 0xc0\n\t"
+      "s_load_dword %4, %12, 0x100\n\t"
+      "s_load_dword %5, %12, 0x140\n\t"
+      "s_load_dword %6, %12, 0x180\n\t"
+      "s_load_dword %7, %12, 0x1c0\n\t"
+      "s_load_dword %8, %12, 0x200\n\t"
+      "s_load_dword %9, %12, 0x240\n\t"
+      "s_load_dword %10, %12, 0x280\n\t"
+      "s_load_dword %11, %12, 0x2c0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(d0), "=&s"(d1), "=&s"(d2), "=&s"(d3), "=&s"(d4), "=&s"(d5), "=&s"(d6), "=&s"(d7), "=&s"(d8),
+        "=&s"(d9), "=&s"(d10), "=&s"(d11)
+      : "s"(k)
+      : "memory");
 }
 
-template <int BLOCK, bool SYS>
-__global__ __launch_bounds__(BLOCK) void ksg_eval_cycle(CycArgs a) {
-  constexpr int NW = BLOCK / 64;
-  constexpr int PW = (int)(sizeof(ksg_pod) / 4);
+// Grid exchange of a one-wave workgroup: its flag line gets `seq`, then the
+// wave polls every flag until all hold `seq` (bounded; a timeout is sticky and
+// reported).
+__device__ __forceinline__ bool cyc_exchange(const CycArgs& a, int G) {
+  const int lane = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its agent-scope slot stores are done
+  if (lane == 0) gst(&a.flags[(size_t)blockIdx.x * 32], a.seq);
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+    for (int l = lane; l < G; l += 64) ok = ok && gld(&a.flags[(size_t)l * 32]) == a.seq;
+    if (__all(ok)) return true;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 22) || gld(a.timeout)) {
+      if (lane == 0) gst(a.timeout, 1u);
+      return false;
+    }
+  }
+}
+
+
+template <int KN>
+__global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
-  __shared__ ksg_pod s_pod;
-  __shared__ int32_t s_st[4][NW];
-  __shared__ unsigned long long s_key[NW];
-  __shared__ uint32_t s_err[NW];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ uint8_t s_eff[kCycEff];
+  __shared__ uint32_t s_lab[KN][kCycLab][64];
+  const int lane = threadIdx.x;
   const int G = (int)gridDim.x;
+#ifdef KSG_STAMPS
+  unsigned long long y_acc[8] = {}, y_last = __builtin_amdgcn_s_memtime();
+#endif
+  // ---- entry: argument lines, programs, node columns, all in flight together ----------
+  static_assert(offsetof(CycArgs, blob) <= 768 && sizeof(CycArgs) >= 768, "cyc_warm_args covers 12 lines");
+  cyc_warm_args();
   const DevCluster& c = a.c;
   const int N = c.N;
   const size_t NN = N;
-  const int es = a.es;
-#ifdef KSG_STAMPS
-  unsigned long long y_acc[10] = {}, y_last = __builtin_amdgcn_s_memtime();
-#endif
-  // Every load of the prologue is issued before the first wait: the pod
-  // record and its program blob (offset and length come with the launch, so
-  // the blob loads do not wait for the record) and this lane's node columns,
-  // so the chain costs one memory latency.  The sources are host-resolved
-  // pointers (no branch on the arguments: their scalar loads go out together).
-  // The profile is read through the constant address space: every plugin
-  // loop over it is a wave-uniform scalar load, not an LDS round trip per step.
-  const ksg_profile& prof = *(const ksg_profile*)(const __attribute__((address_space(4))) ksg_profile*)a.prof;
-  const int32_t* prec = a.psrc;
-  const int32_t* bsrc = a.bsrc;
-  const int32_t pw = tid < PW ? prec[tid] : 0;
-  constexpr int BI = (KSG_BLOB_MAX + BLOCK - 1) / BLOCK;
-  int32_t bw[BI];
+  const ksg_pod& p = a.pod;
+  const int blen = a.blob_len;
+  // the node columns of this lane's nodes: every load unconditional and
+  // unmasked (clamped indices; a column past the allocated ones reads a valid
+  // word that the evaluation never uses), so the loads of the whole prologue
+  // are in flight together and the first wait below covers them all
+  int nk[KN];
+  NodeCols L[KN];
+  PNode nd[KN];
+  uint32_t nsw[KN];
+  uint32_t lv[KN][kCycLab];
+  const bool want_img = (a.smask >> KSG_PL_IMAGE_LOCALITY) & 1u;
+  const int R = c.R, Lc = c.L, T = c.T, I = c.I;
+  const uint32_t* tcol = T > 0 ? c.taints : (const uint32_t*)c.allowed;
+  const uint32_t* icol = want_img && I > 0 ? c.images : (const uint32_t*)c.allowed;
+  const int Tm = T > 0 ? T : 1, Im = want_img && I > 0 ? I : 1;
+  const int32_t* nset = p.node_set >= 0 ? a.gprog + p.node_set : nullptr;
+  const int32_t* nsrc = nset ? nset : c.allowed;
 #pragma unroll
-  for (int u = 0; u < BI; u++) {
-    const int i = tid + u * BLOCK;
-    bw[u] = i < a.blob_len ? bsrc[i] : 0;
-  }
-  const int n = blockIdx.x * BLOCK + tid;
-  const bool own = n < N;
-  NodeCols L;
-  if (own) load_cols(c, a.st.requested, a.st.nonzero, a.st.pod_count, n, L);
-  if (tid < PW) reinterpret_cast<int32_t*>(&s_pod)[tid] = pw;
+  for (int k = 0; k < KN; k++) {
+    const int n = (k * G + (int)blockIdx.x) * 64 + lane;
+    nk[k] = n;
+    const int m = n < N ? n : N - 1;
 #pragma unroll
-  for (int u = 0; u < BI; u++) {
-    const int i = tid + u * BLOCK;
-    if (i < a.blob_len) s_blob[i] = bw[u];
-  }
-  if (a.wpods && blockIdx.x == 0) {   // the staged append: workgroup 0 copies it to the device
-    if (tid < PW) reinterpret_cast<int32_t*>(a.wpods)[tid] = pw;
-    for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
-  }
-  lds_barrier();   // LDS only: the node-column loads stay in flight
-  // (after the barrier: only the owner lane's wave waits for its columns, where
-  // its evaluation would wait for them anyway)
-  if (own && n == a.cm_node) {   // the deferred assume: NodeInfo.AddPod on the lane's own node
-#pragma unroll
-    for (int r = 0; r < KSG_MAX_RES; r++)
-      if (r < c.R) {
-        L.req[r] += a.cm_req[r];
-        a.st.requested[(size_t)r * NN + n] = L.req[r];
-      }
-    L.nz_cpu += a.cm_nz_cpu;
-    L.nz_mem += a.cm_nz_mem;
-    L.pod_count += 1;
-    a.st.nonzero[n] = L.nz_cpu;
-    a.st.nonzero[NN + n] = L.nz_mem;
-    a.st.pod_count[n] = L.pod_count;
-  }
-  KSG_YSTAMP(0);
-  const PodView v = make_view(c, prof, s_pod, s_blob, a.gprog, false, a.st.ports);
-
-  // ---- phase 1: this workgroup's nodes ------------------------------------------------
-  NodeEval e{KSG_FS_NOT_EVALUATED, 0, 0, 0, 0};
-  int64_t lraw[KSG_NPLUGINS] = {};
-  const CmProf cm = cm_prof(prof);
-  if (own) e = eval_node_src(c, prof, v, GNode{&c, n}, L, n, nullptr, nullptr, nullptr, lraw, &cm);
-  KSG_YSTAMP(1);
-  const bool ok = own && e.st == 0;
-  // the row value of score row q (node-local plugins only on this path)
-  auto raw_of = [&](int q) -> int64_t {
-    const int pl = a.rows[q];
-    int64_t x = 0;
-    switch (pl) {
-      case KSG_PL_NODE_RESOURCES_FIT: x = lraw[KSG_PL_NODE_RESOURCES_FIT]; break;
-      case KSG_PL_BALANCED_ALLOCATION: x = lraw[KSG_PL_BALANCED_ALLOCATION]; break;
-      case KSG_PL_IMAGE_LOCALITY: x = lraw[KSG_PL_IMAGE_LOCALITY]; break;
-      case KSG_PL_TAINT_TOLERATION: x = lraw[KSG_PL_TAINT_TOLERATION]; break;
-      case KSG_PL_NODE_AFFINITY: x = lraw[KSG_PL_NODE_AFFINITY]; break;
-      default: break;
+    for (int r = 0; r < KSG_MAX_RES; r++) {
+      const size_t o = (size_t)(r < R ? r : 0) * NN + m;
+      L[k].alloc[r] = c.alloc[o];
+      L[k].req[r] = a.requested[o];
     }
-    return ok && ((v.smask >> pl) & 1u) ? x : 0;
-  };
-  int32_t feas = ok ? 1 : 0, mt = ok ? (int32_t)e.rt : 0, ma = ok ? (int32_t)e.ra : 0, lo = ok ? N - n : 0;
-  feas = wave_sum32(feas);
-  mt = (int32_t)wave_max64(mt);
-  ma = (int32_t)wave_max64(ma);
-  lo = (int32_t)wave_max64(lo);
-  if (NW > 1) {
-    if (lane == 0) { s_st[0][wv] = feas; s_st[1][wv] = mt; s_st[2][wv] = ma; s_st[3][wv] = lo; }
-    __syncthreads();
-    if (tid == 0)
-      for (int i = 1; i < NW; i++) {
-        feas += s_st[0][i];
-        mt = max(mt, s_st[1][i]);
-        ma = max(ma, s_st[2][i]);
-        lo = max(lo, s_st[3][i]);
-      }
+    L[k].nz_cpu = a.nonzero[m];
+    L[k].nz_mem = a.nonzero[NN + m];
+    L[k].pod_count = a.pod_count[m];
+    L[k].allowed = c.allowed[m];
+    nd[k].uns = c.unsched[m] != 0;
+#pragma unroll
+    for (int q = 0; q < kCycLab; q++) lv[k][q] = c.label_val[(size_t)(q < Lc ? q : 0) * NN + m];
+#pragma unroll
+    for (int q = 0; q < kCycTnt; q++) nd[k].tnt[q] = tcol[(size_t)(q < Tm ? q : 0) * NN + m];
+#pragma unroll
+    for (int q = 0; q < kCycImg; q++) nd[k].img[q] = icol[(size_t)(q < Im ? q : 0) * NN + m];
+    nsw[k] = (uint32_t)nsrc[m >> 5];
+    nd[k].label_val = (const KSG_G1 uint32_t*)c.label_val;
+    nd[k].label_num = (const KSG_G1 int64_t*)c.label_num;
+    nd[k].label_num_ok = (const KSG_G1 uint8_t*)c.label_num_ok;
+    nd[k].taints = (const KSG_G1 uint32_t*)c.taints;
+    nd[k].taint_effect = (const KSG_G1 uint8_t*)c.taint_effect;
+    nd[k].images = (const KSG_G1 uint32_t*)c.images;
+    nd[k].N = NN;
+    nd[k].n = m;
+    nd[k].lab = (const KSG_L3 uint32_t*)&s_lab[k][0][lane];
   }
-  if (tid == 0) {
+  // the pod's programs and the taint effects into LDS (issued behind the columns)
+  if (blen <= kCycBlob) {
+    const __attribute__((address_space(4))) int32_t* kb =
+        (const __attribute__((address_space(4))) int32_t*)((const __attribute__((address_space(4))) char*)
+                                                               __builtin_amdgcn_kernarg_segment_ptr() +
+                                                           offsetof(CycArgs, blob));
+    int32_t w[kCycBlob / 64];
+#pragma unroll
+    for (int u = 0; u < kCycBlob / 64; u++) w[u] = kb[lane + 64 * u];   // inside the arguments: unconditional
+#pragma unroll
+    for (int u = 0; u < kCycBlob / 64; u++)
+      if (lane + 64 * u < blen) s_blob[lane + 64 * u] = w[u];
+  } else {
+    for (int i = lane; i < blen; i += 64) s_blob[i] = a.bsrc[i];
+  }
+  const bool eff_lds = c.V <= kCycEff;
+  if (eff_lds)
+    for (int i = lane; i < c.V; i += 64) s_eff[i] = c.taint_effect[i];
+  // masks and the label rows, once the loads are in
+#pragma unroll
+  for (int k = 0; k < KN; k++) {
+#pragma unroll
+    for (int r = 0; r < KSG_MAX_RES; r++) {
+      L[k].alloc[r] = r < R ? L[k].alloc[r] : 0;
+      L[k].req[r] = r < R ? L[k].req[r] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < kCycLab; q++) s_lab[k][q][lane] = q < Lc ? lv[k][q] : 0;
+    nd[k].eff_lds = eff_lds;
+    nd[k].eff = (const KSG_L3 uint8_t*)s_eff;
+  }
+  if (a.wpods && blockIdx.x == 0) {   // the staged append: workgroup 0 copies it to the device pool
+    constexpr int PW = (int)(sizeof(ksg_pod) / 4);
+    const __attribute__((address_space(4))) int32_t* kp =
+        (const __attribute__((address_space(4))) int32_t*)((const __attribute__((address_space(4))) char*)
+                                                               __builtin_amdgcn_kernarg_segment_ptr() +
+                                                           offsetof(CycArgs, pod));
+    if (lane < PW) reinterpret_cast<int32_t*>(a.wpods)[lane] = kp[lane];
+    for (int64_t i = lane; i < a.slen; i += 64) a.wprog[i] = a.sprog[i];
+  }
+  // the deferred assume: NodeInfo.AddPod on the owner lane's node
+#pragma unroll
+  for (int k = 0; k < KN; k++)
+    if (nk[k] == a.cm_node) {
+      const int n = nk[k];
+#pragma unroll
+      for (int r = 0; r < KSG_MAX_RES; r++)
+        if (r < c.R) {
+          L[k].req[r] += a.cm_req[r];
+          a.requested[(size_t)r * NN + n] = L[k].req[r];
+        }
+      L[k].nz_cpu += a.cm_nz_cpu;
+      L[k].nz_mem += a.cm_nz_mem;
+      L[k].pod_count += 1;
+      a.nonzero[n] = L[k].nz_cpu;
+      a.nonzero[NN + n] = L[k].nz_mem;
+      a.pod_count[n] = L[k].pod_count;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS copies visible to the (single) wave
+  KSG_YSTAMP(0);
+
+  // ---- evaluate: every filter independently, then the first rejection in order ---------
+  const int32_t* P = s_blob;
+  const int boff = p.blob;
+  auto rb = [boff](int off) { return off < 0 ? -1 : off - boff; };
+  const int32_t* tolf = P + rb(p.tol);
+  const int32_t* tolp = tolf + c.W;
+  const int na_req = rb(p.na_req), na_pref = rb(p.na_pref), img = rb(p.img), ports = rb(p.ports);
+  const bool reject = (p.flags & KSG_POD_PREFILTER_REJECT) != 0;
+  const CmProf cm{a.cm_fast != 0, a.cm_least != 0, a.cm_wc, a.cm_wm, a.cm_inv_ws, a.cm_inv_wc, a.cm_inv_wm};
+  const uint32_t fm = a.fmask, sm = a.smask;
+  uint32_t st[KN];
+  int64_t part[KN], rt[KN], ra[KN], rf[KN], rbal[KN], rimg[KN];
+#pragma unroll
+  for (int k = 0; k < KN; k++) {
+    const int n = nk[k];
+    const PNode& x = nd[k];
+    uint32_t w[KSG_NPLUGINS] = {};   // per-plugin status word (0: passes or not run)
+    if (fm & bit(KSG_PL_NODE_UNSCHEDULABLE))
+      w[KSG_PL_NODE_UNSCHEDULABLE] =
+          (x.unsched() && !(p.flags & KSG_POD_TOL_UNSCHED)) ? KSG_PL_NODE_UNSCHEDULABLE + 1 : 0;
+    if (fm & bit(KSG_PL_NODE_NAME))
+      w[KSG_PL_NODE_NAME] = (p.node_name != -1 && p.node_name != n) ? KSG_PL_NODE_NAME + 1 : 0;
+    int tslot;
+    int64_t tscore;
+    pnode_taints(x, c.T, tolf, tolp, (fm & bit(KSG_PL_TAINT_TOLERATION)) != 0,
+                 (sm & bit(KSG_PL_TAINT_TOLERATION)) != 0, tslot, tscore);
+    if (fm & bit(KSG_PL_TAINT_TOLERATION))
+      w[KSG_PL_TAINT_TOLERATION] = tslot >= 0 ? (uint32_t)(KSG_PL_TAINT_TOLERATION + 1) | ((uint32_t)tslot << 8) : 0;
+    if (fm & bit(KSG_PL_NODE_AFFINITY))
+      w[KSG_PL_NODE_AFFINITY] =
+          na_required_match(x, P, na_req) ? 0 : (uint32_t)(KSG_PL_NODE_AFFINITY + 1) | (1u << 8);
+    if ((fm & bit(KSG_PL_NODE_PORTS)) && ports >= 0 && a.used_ports)
+      w[KSG_PL_NODE_PORTS] =
+          ports_conflict(a.used_ports, N, n < N ? n : N - 1, P + ports) ? KSG_PL_NODE_PORTS + 1 : 0;
+    if (fm & bit(KSG_PL_NODE_RESOURCES_FIT)) {
+      const uint32_t b = fit_filter(c, p, L[k], a.fit_ignored);
+      w[KSG_PL_NODE_RESOURCES_FIT] = b ? (uint32_t)(KSG_PL_NODE_RESOURCES_FIT + 1) | (b << 8) : 0;
+    }
+    uint32_t s = 0;
+    for (int kf = 0; kf < a.n_filter && !s; kf++) {
+      const int pl = (int)((a.forder >> (4 * kf)) & 15u);
+      uint32_t v = 0;
+#pragma unroll
+      for (int q = 0; q < KSG_NPLUGINS; q++) v = pl == q ? w[q] : v;
+      s = v;
+    }
+    if (reject || (nset && !((nsw[k] >> (n & 31)) & 1u))) s = KSG_FS_NOT_EVALUATED;
+    st[k] = n < N ? s : (uint32_t)KSG_FS_NOT_EVALUATED;
+    // raw scores of a feasible node
+    part[k] = rt[k] = ra[k] = rf[k] = rbal[k] = rimg[k] = 0;
+    if (st[k] == 0) {
+      if (sm & (bit(KSG_PL_NODE_RESOURCES_FIT) | bit(KSG_PL_BALANCED_ALLOCATION))) {
+        if (cm.fast) {
+          fit_ba_cm(cm, p, L[k], rf[k], rbal[k]);
+        } else {
+          rf[k] = fit_score(*a.gprof, p, L[k]);
+          rbal[k] = ba_score(*a.gprof, p, L[k]);
+        }
+        if (!(sm & bit(KSG_PL_NODE_RESOURCES_FIT))) rf[k] = 0;
+        if (!(sm & bit(KSG_PL_BALANCED_ALLOCATION))) rbal[k] = 0;
+      }
+      if (sm & bit(KSG_PL_IMAGE_LOCALITY)) rimg[k] = pnode_image_score(x, c.I, P, img, p.n_containers);
+      if (sm & bit(KSG_PL_TAINT_TOLERATION)) rt[k] = tscore;
+      if (sm & bit(KSG_PL_NODE_AFFINITY)) ra[k] = na_pref_score(x, P, na_pref);
+      part[k] = rf[k] * a.w_fit + rbal[k] * a.w_ba + rimg[k] * a.w_img;
+    }
+  }
+  KSG_YSTAMP(1);
+
+  // ---- this workgroup's statistics, the exchange ---------------------------------------
+  int32_t feas = 0, mt = 0, ma = 0, lo = 0;
+#pragma unroll
+  for (int k = 0; k < KN; k++)
+    if (st[k] == 0) {
+      feas += 1;
+      mt = max(mt, (int32_t)rt[k]);
+      ma = max(ma, (int32_t)ra[k]);
+      lo = max(lo, N - nk[k]);
+    }
+  feas = (int32_t)wreduce((uint32_t)feas, OpAdd32{});
+  mt = wreduce(mt, OpMaxI32{});
+  ma = wreduce(ma, OpMaxI32{});
+  lo = wreduce(lo, OpMaxI32{});
+  if (lane == 0) {
     CycPart* pp = a.parts + blockIdx.x;
     gst(&pp->nfeas, feas);
     gst(&pp->max_t, mt);
     gst(&pp->max_a, ma);
     gst(&pp->lo, lo);
   }
-
   KSG_YSTAMP(2);
-  // ---- exchange -------------------------------------------------------------------------
-  const bool xok = cyc_exchange<BLOCK>(a, G);
+  const bool xok = cyc_exchange(a, G);
   KSG_YSTAMP(3);
-
-  // ---- phase 2: fold the slots, normalise this workgroup's nodes ------------------------
   int32_t nfeas = 0, max_t = 0, max_a = 0, low = 0;
-  for (int b = tid; b < G; b += BLOCK) {
+  for (int b = lane; b < G; b += 64) {
     const CycPart* pp = a.parts + b;
     nfeas += gld(&pp->nfeas);
     max_t = max(max_t, gld(&pp->max_t));
     max_a = max(max_a, gld(&pp->max_a));
     low = max(low, gld(&pp->lo));
   }
-  nfeas = wave_sum32(nfeas);
-  max_t = (int32_t)wave_max64(max_t);
-  max_a = (int32_t)wave_max64(max_a);
-  low = (int32_t)wave_max64(low);
-  if (NW > 1) {
-    __syncthreads();   // s_st reuse
-    if (lane == 0) { s_st[0][wv] = nfeas; s_st[1][wv] = max_t; s_st[2][wv] = max_a; s_st[3][wv] = low; }
-    __syncthreads();
-    nfeas = 0; max_t = 0; max_a = 0; low = 0;
-    for (int i = 0; i < NW; i++) {
-      nfeas += s_st[0][i];
-      max_t = max(max_t, s_st[1][i]);
-      max_a = max(max_a, s_st[2][i]);
-      low = max(low, s_st[3][i]);
-    }
-  }
+  nfeas = (int32_t)wreduce((uint32_t)nfeas, OpAdd32{});
+  max_t = wreduce(max_t, OpMaxI32{});
+  max_a = wreduce(max_a, OpMaxI32{});
+  low = wreduce(low, OpMaxI32{});
   KSG_YSTAMP(4);
-  // every row of this workgroup's nodes, written once (the exchange above
-  // waited for nothing on the host link)
+
+  // ---- rows: every node of this workgroup, written once --------------------------------
+  const int es = a.es;
+  const bool scored = nfeas >= 2;   // fewer than two feasible nodes: no Score ran, nothing recorded
+  PodView v{};                       // total_score's inputs
+  v.smask = sm;
+  v.w_t = a.w_t;
+  v.w_a = a.w_a;
   uint64_t key = 0;
   uint32_t err = 0;
-  if (own) {
-    const bool scored = nfeas >= 2;   // fewer than two feasible nodes: no Score ran, nothing recorded
+#pragma unroll
+  for (int k = 0; k < KN; k++) {
+    const int n = nk[k];
+    if (n >= N) continue;
+    const bool ok = st[k] == 0;
     int64_t total = 0, nt = 0, na = 0;
     if (scored && ok) {
-      total = total_score(v, e.part, e.rt, e.ra, max_t, max_a, err, &nt, &na);
-      key = argmax_key(total, n);
+      total = total_score(v, part[k], rt[k], ra[k], max_t, max_a, err, &nt, &na);
+      const uint64_t kk = argmax_key(total, n);
+      key = kk > key ? kk : key;
     }
-    hst<SYS>(a.h_fs + n, e.st);
-    for (int q = 0; q < a.n_rows; q++) cyc_put_es<SYS>(a.h_raw, (size_t)q * NN + n, scored ? raw_of(q) : 0, es);
-    for (int q = 0; q < a.n_normrows; q++)
-      cyc_put_es<SYS>(a.h_norm, (size_t)q * NN + n, a.rows[q] == KSG_PL_TAINT_TOLERATION ? nt : na, es);
-    cyc_put_es<SYS>(a.h_tot, n, total, es);
+    a.h_fs[n] = st[k];
+    for (int q = 0; q < a.n_rows; q++) {
+      const int pl = (int)((a.rows >> (4 * q)) & 15u);
+      int64_t x = 0;
+      if (scored && ok && ((sm >> pl) & 1u))
+        x = pl == KSG_PL_NODE_RESOURCES_FIT     ? rf[k]
+            : pl == KSG_PL_BALANCED_ALLOCATION ? rbal[k]
+            : pl == KSG_PL_IMAGE_LOCALITY      ? rimg[k]
+            : pl == KSG_PL_TAINT_TOLERATION    ? rt[k]
+            : pl == KSG_PL_NODE_AFFINITY       ? ra[k]
+                                               : 0;
+      cyc_put_es<false>(a.h_raw, (size_t)q * NN + n, x, es);
+    }
+    for (int q = 0; q < a.n_normrows; q++) {
+      const int pl = (int)((a.rows >> (4 * q)) & 15u);
+      cyc_put_es<false>(a.h_norm, (size_t)q * NN + n, pl == KSG_PL_TAINT_TOLERATION ? nt : na, es);
+    }
+    cyc_put_es<false>(a.h_tot, n, total, es);
   }
-  key = wave_max_u64(key);
-  err = wave_or32(err);
-  if (NW > 1) {
-    if (lane == 0) { s_key[wv] = key; s_err[wv] = err; }
-    __syncthreads();
-    if (tid == 0)
-      for (int i = 1; i < NW; i++) { key = s_key[i] > key ? s_key[i] : key; err |= s_err[i]; }
-  }
-  host_release<SYS>();   // this wave's rows are written
+  key = wreduce(key, OpMaxU64{});
+  err = wreduce(err, OpOr32{});
+  host_release<false>();   // this wave's rows are written
   KSG_YSTAMP(5);
-  __syncthreads();       // ... and every other wave's
-  if (tid == 0) {
+  if (lane == 0) {
     CycWg* w = a.h_wg + blockIdx.x;
-    hst<SYS>(&w->key, (unsigned long long)key);
-    hst<SYS>(&w->err, err | (xok ? 0u : 2u));
+    w->key = key;
+    w->err = err | (xok ? 0u : 2u);
     if (blockIdx.x == 0) {   // the pod-wide statistics (every workgroup folded the same values)
-      hst<SYS>(a.h_stats + 0, nfeas);
-      hst<SYS>(a.h_stats + 1, max_t);
-      hst<SYS>(a.h_stats + 2, max_a);
-      hst<SYS>(a.h_stats + 3, low);
+      a.h_stats[0] = nfeas;
+      a.h_stats[1] = max_t;
+      a.h_stats[2] = max_a;
+      a.h_stats[3] = low;
     }
-    host_release<SYS>();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    host_release<false>();
     __hip_atomic_store(&w->done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   KSG_YSTAMP(6);
 #ifdef KSG_STAMPS
-  if (tid == 0 && blockIdx.x == 0 && a.stamps)
+  if (lane == 0 && blockIdx.x == 0 && a.stamps)
     for (int i = 0; i < 7; i++) atomicAdd(&a.stamps[i], y_acc[i]);
 #endif
 }

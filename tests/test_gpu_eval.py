@@ -30,6 +30,11 @@ CASES = {
     "c3-60x80": lambda: G.config3(n_nodes=60, n_pods=80, apps=12, zones=4),
     "c3-15000x40": lambda: G.config3(n_nodes=15000, n_pods=40, apps=30, zones=16),
     "readme-kat2": G.readme_kat2,
+    # taint vocabulary of 8,192: toleration bitmaps of 512 words (programs too
+    # long for the kernel arguments) and effects too many for the LDS copy
+    "c5-vocab8k": lambda: G.config5(n_nodes=300, n_pods=40, n_images=100, taint_vocab=8192, taints_per_node=12,
+                                    images_per_node=10),
+    "c1-images": lambda: G.config1(n_nodes=700, n_pods=60, seed=5),
 }
 CASES.update({f"zoo-{s}": (lambda s=s: __import__("zoo").zoo(s, n_pods=60)) for s in range(4)})
 
@@ -51,7 +56,23 @@ def _score_rows(pf):
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_eval_cycle_matches_oracle(gpu, oracle, name):
-    nodes, pods, prof = CASES[name]()
+    _check_cycles(gpu, oracle, name, *CASES[name]())
+
+
+@pytest.mark.parametrize("kn", [2, 4])
+@pytest.mark.parametrize("name", ["c2-1000x120", "c5-small", "zoo-1"])
+def test_eval_cycle_nodes_per_lane(oracle, monkeypatch, kn, name):
+    """KN = 2 and 4 nodes per lane (the per-cycle kernel's form above ~98 k
+    nodes, forced here by KSG_CYCLE_KN) equal the oracle as KN = 1 does."""
+    monkeypatch.setenv("KSG_CYCLE_KN", str(kn))
+    eng = native.Engine(device=0)
+    try:
+        _check_cycles(eng, oracle, name, *CASES[name]())
+    finally:
+        eng.close()
+
+
+def _check_cycles(gpu, oracle, name, nodes, pods, prof):
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
     gpu.load(enc, pf)
