@@ -176,6 +176,8 @@ def _container(c: dict, init: bool) -> m.Container:
 def _volume(v: dict) -> Tuple[str, str, str]:
     """v1.Volume -> (name, the VolumeSource field set (its JSON key), claimName)."""
     kinds = [k for k in v if k != "name" and v[k] is not None]
+    if not kinds:   # API defaulting (SetDefaults_Volume): no source set means emptyDir
+        return v.get("name", ""), "emptyDir", ""
     if len(kinds) != 1:
         raise ValueError(f"volume {v.get('name')!r}: expected exactly one volume source, got {kinds}")
     kind = kinds[0]
@@ -407,8 +409,12 @@ def load_snapshot(doc, n_nodes_check: bool = True) -> Snapshot:
     queue = list(range(len(bound_objs), len(pods)))
     prof, pct = profile_from_config(doc.get("schedulerConfig"))
     if n_nodes_check and pct not in (None, 100) and len(nodes) > 100:
-        raise NotImplementedError(f"percentageOfNodesToScore={pct} with {len(nodes)} nodes: "
-                                  "the evaluator scores every feasible node (set it to 100)")
+        raise NotImplementedError(
+            f"percentageOfNodesToScore={pct} with {len(nodes)} nodes: the evaluator scores every feasible node, "
+            "as north_star fixes (set it to 100). Upstream's early stop (findNodesThatPassFilters stops after "
+            "numFeasibleNodesToFind nodes, starting at nextStartNodeIndex) depends on which of the 16 parallel "
+            "filter goroutines finishes first, so its placements are not reproducible and there is no exact "
+            "result to match; at or below 100 nodes every node is scored anyway and the setting is accepted")
     for i in queue:
         pods[i].node_name = ""
     return Snapshot(nodes, pods, bound, queue, prof, skipped)

@@ -102,7 +102,8 @@ type Evaluator struct {
 	// fed by informer handlers (attach), drained under mu:
 	side      sync.Mutex
 	nominated map[string]struct{} // nodes that may hold nominated pods
-	gone      []types.UID         // pods deleted since the last sync
+	subscribed bool               // attach() registered the pod informer: nominated is maintained
+	gone      []*v1.Pod           // pods deleted since the last sync
 	pending   []*v1.Pod           // pending pods created since the last sync (hinted to the snapshot)
 	nsDirty   bool                // a namespace was added or its labels changed
 	attached  sync.Once
@@ -131,7 +132,7 @@ func (e *Evaluator) attach(h framework.Handle) {
 	e.attached.Do(func() {
 		f := h.SharedInformerFactory()
 		if f == nil {
-			return
+			return // no informers: nominatedPass visits every node (subscribed stays false)
 		}
 		nsInf := f.Core().V1().Namespaces()
 		lister := nsInf.Lister()
@@ -152,11 +153,14 @@ func (e *Evaluator) attach(h framework.Handle) {
 				}
 				if p, ok := o.(*v1.Pod); ok {
 					e.side.Lock()
-					e.gone = append(e.gone, p.UID)
+					e.gone = append(e.gone, p)
 					e.side.Unlock()
 				}
 			},
 		})
+		e.side.Lock()
+		e.subscribed = true
+		e.side.Unlock()
 	})
 }
 
@@ -246,7 +250,14 @@ func (e *Evaluator) pruneGone() {
 	gone := e.gone
 	e.gone = nil
 	e.side.Unlock()
-	for _, uid := range gone {
+	for _, p := range gone {
+		uid := p.UID
+		if _, ok := e.hinted[uid]; ok { // a pending pod deleted before its cycle: its hint goes too
+			delete(e.hinted, uid)
+			if e.snap != nil {
+				_ = e.snap.UnhintPod(p.Namespace, p.Name)
+			}
+		}
 		if c, ok := e.podNode[uid]; ok && c >= 0 {
 			continue // still on the device: syncCluster forgets it when it leaves its node
 		}
@@ -462,8 +473,14 @@ func (e *Evaluator) nominatedPass(st *podState, pod *v1.Pod, nom framework.PodNo
 	prio := podPriority(pod)
 	e.side.Lock()
 	names := make([]string, 0, len(e.nominated))
-	for name := range e.nominated {
-		names = append(names, name)
+	if e.subscribed {
+		for name := range e.nominated {
+			names = append(names, name)
+		}
+	} else { // nobody reports nominations to this evaluator: every node may hold some
+		for name := range e.index {
+			names = append(names, name)
+		}
 	}
 	e.side.Unlock()
 	for _, name := range names {

@@ -291,7 +291,12 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 	if p.Spec.Priority != nil {
 		v.priority = C.int32_t(*p.Spec.Priority)
 	}
-	vols := unsafe.Slice((*C.ksg_volume_view)(a.alloc(len(p.Spec.Volumes), C.sizeof_ksg_volume_view)), len(p.Spec.Volumes)+1)
+	// the arena allocates max(len, 1) views: the slice covers exactly that
+	nv := len(p.Spec.Volumes)
+	if nv < 1 {
+		nv = 1
+	}
+	vols := unsafe.Slice((*C.ksg_volume_view)(a.alloc(len(p.Spec.Volumes), C.sizeof_ksg_volume_view)), nv)
 	for i, vol := range p.Spec.Volumes {
 		vols[i].name, vols[i].kind = a.str(vol.Name), a.str(volumeKind(&vol.VolumeSource))
 		if vol.PersistentVolumeClaim != nil {
@@ -458,6 +463,14 @@ func (x *Snapshot) HintPod(p *v1.Pod, defaultSel labels.Selector) error {
 	var a arena
 	defer a.free()
 	return x.check(C.ksg_snapshot_hint_pod(x.s, a.pod(p, defaultSel)))
+}
+
+// UnhintPod drops the hint of a pending pod deleted before it was added
+// (ksg_snapshot_unhint_pod); adding a pod drops its hint by itself.
+func (x *Snapshot) UnhintPod(namespace, name string) error {
+	var a arena
+	defer a.free()
+	return x.check(C.ksg_snapshot_unhint_pod(x.s, a.str(namespace), a.str(name)))
 }
 
 // AddNamespace registers a namespace and its labels: namespaceSelector

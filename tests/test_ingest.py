@@ -366,3 +366,14 @@ def test_volume_sources_the_plugins_skip_encode():
     s = S.Snapshot(snap2.profile, snap2.nodes)
     for p in snap2.pods:
         s.add_pod(p)
+
+
+def test_volume_without_a_source_is_empty_dir():
+    """a volume with only a name is an emptyDir after API defaulting
+    (SetDefaults_Volume), not an error."""
+    doc = _volume_doc()
+    doc["pods"][0]["spec"]["volumes"] = [{"name": "bare"}]
+    snap = I.load_snapshot(doc)
+    byname = {p.name: p for p in snap.pods}
+    assert byname["scratch"].volumes == [("bare", "emptyDir", "")]
+    assert byname["scratch"].volumes_needing_plugins() == []
