@@ -194,6 +194,8 @@ struct ksg_ctx {
   int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
   CycArgs cyc_args{};                       // ksg_eval_cycle's launch arguments, rebuilt in place per call
   int cycle_kn = 1;                         // env KSG_CYCLE_KN (1/2/4): the smallest nodes-per-lane tried (tests)
+  bool cycle_sys = false;                   // env KSG_CYCLE_SYS=1: system-scope host stores (no L2 write-back)
+  int cycle_es = 0;                         // env KSG_CYCLE_ES=2/4/8: force the row width (measurements)
   bool cycle_coop = false;                  // per-cycle launch: plain (G within the occupancy API's residency,
                                             // ~7 us less host time); cooperative after an exchange timeout,
                                             // or always with env KSG_CYCLE_COOP=1
@@ -1847,15 +1849,21 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   for (int pl = 0; pl < KSG_NPLUGINS; pl++)
     if ((prof.score_mask >> pl) & 1u) wabs += prof.weight[pl] < 0 ? -(int64_t)prof.weight[pl] : prof.weight[pl];
   int64_t bound = std::max<int64_t>({wabs * 100, 100, ctx->c.T, na_pref_bound(ctx, hp)});
-  const size_t es = bound < (1 << 15) ? 2 : bound < (1ll << 31) ? 4 : 8;
+  size_t es = bound < (1 << 15) ? 2 : bound < (1ll << 31) ? 4 : 8;
+  if (ctx->cycle_es == 4 || ctx->cycle_es == 8) es = std::max<size_t>(es, ctx->cycle_es);
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
   // one-wave workgroups, KN nodes per lane: the smallest KN whose grid is
   // co-resident (the exchange needs every workgroup resident)
   auto kernel_of = [&](int kn) -> const void* {
-    if (kn == 1) return (const void*)ksg_eval_cycle<1>;
-    if (kn == 2) return (const void*)ksg_eval_cycle<2>;
-    return (const void*)ksg_eval_cycle<4>;
+    if (ctx->cycle_sys) {
+      if (kn == 1) return (const void*)ksg_eval_cycle<1, true>;
+      if (kn == 2) return (const void*)ksg_eval_cycle<2, true>;
+      return (const void*)ksg_eval_cycle<4, true>;
+    }
+    if (kn == 1) return (const void*)ksg_eval_cycle<1, false>;
+    if (kn == 2) return (const void*)ksg_eval_cycle<2, false>;
+    return (const void*)ksg_eval_cycle<4, false>;
   };
   int kn = ctx->cycle_kn;
   for (;; kn *= 2) {
@@ -2531,6 +2539,8 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_PIPE_OVERLAP")) ctx->pipe_overlap = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_ES")) ctx->cycle_es = atoi(f);
   if (const char* f = getenv("KSG_CYCLE_KN")) {
     const int v = atoi(f);
     ctx->cycle_kn = v >= 4 ? 4 : v >= 2 ? 2 : 1;

@@ -34,8 +34,9 @@
 //              call's sequence number (agent-scope stores and loads, no reset
 //              between calls); every workgroup folds the G slots.
 //   rows       status words, raw, normalised and total rows (2, 4 or 8 bytes)
-//              with plain stores to the host block, one system-scope release,
-//              then the workgroup's selectHost key, error bits and done word.
+//              and the workgroup's selectHost key and error bits with plain
+//              stores to the host block (SYS: system-scope stores), one
+//              system-scope release, then the done word.
 //
 // The evaluation is eval_node_src's arithmetic (same helpers: untolerated_slot,
 // na_required_match, fit_filter, fit_ba_cm / fit_score / ba_score,
@@ -272,7 +273,7 @@ __device__ __forceinline__ bool cyc_exchange(const CycArgs& a, int G) {
 }
 
 
-template <int KN>
+template <int KN, bool SYS>
 __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ uint8_t s_eff[kCycEff];
@@ -527,7 +528,7 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
       const uint64_t kk = argmax_key(total, n);
       key = kk > key ? kk : key;
     }
-    a.h_fs[n] = st[k];
+    hst<SYS>(a.h_fs + n, st[k]);
     for (int q = 0; q < a.n_rows; q++) {
       const int pl = (int)((a.rows >> (4 * q)) & 15u);
       int64_t x = 0;
@@ -538,31 +539,32 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
             : pl == KSG_PL_TAINT_TOLERATION    ? rt[k]
             : pl == KSG_PL_NODE_AFFINITY       ? ra[k]
                                                : 0;
-      cyc_put_es<false>(a.h_raw, (size_t)q * NN + n, x, es);
+      cyc_put_es<SYS>(a.h_raw, (size_t)q * NN + n, x, es);
     }
     for (int q = 0; q < a.n_normrows; q++) {
       const int pl = (int)((a.rows >> (4 * q)) & 15u);
-      cyc_put_es<false>(a.h_norm, (size_t)q * NN + n, pl == KSG_PL_TAINT_TOLERATION ? nt : na, es);
+      cyc_put_es<SYS>(a.h_norm, (size_t)q * NN + n, pl == KSG_PL_TAINT_TOLERATION ? nt : na, es);
     }
-    cyc_put_es<false>(a.h_tot, n, total, es);
+    cyc_put_es<SYS>(a.h_tot, n, total, es);
   }
   key = wreduce(key, OpMaxU64{});
   err = wreduce(err, OpOr32{});
-  host_release<false>();   // this wave's rows are written
-  KSG_YSTAMP(5);
+  // the workgroup's record beside its rows, then ONE release for all of them
+  // and the done word behind it (round 4 released twice)
+  CycWg* w = a.h_wg + blockIdx.x;
   if (lane == 0) {
-    CycWg* w = a.h_wg + blockIdx.x;
-    w->key = key;
-    w->err = err | (xok ? 0u : 2u);
+    hst<SYS>(&w->key, (unsigned long long)key);
+    hst<SYS>(&w->err, err | (xok ? 0u : 2u));
     if (blockIdx.x == 0) {   // the pod-wide statistics (every workgroup folded the same values)
-      a.h_stats[0] = nfeas;
-      a.h_stats[1] = max_t;
-      a.h_stats[2] = max_a;
-      a.h_stats[3] = low;
+      hst<SYS>(a.h_stats + 0, nfeas);
+      hst<SYS>(a.h_stats + 1, max_t);
+      hst<SYS>(a.h_stats + 2, max_a);
+      hst<SYS>(a.h_stats + 3, low);
     }
-    host_release<false>();
-    __hip_atomic_store(&w->done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  host_release<SYS>();
+  KSG_YSTAMP(5);
+  if (lane == 0) __hip_atomic_store(&w->done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   KSG_YSTAMP(6);
 #ifdef KSG_STAMPS
   if (lane == 0 && blockIdx.x == 0 && a.stamps)
