@@ -275,7 +275,8 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
             "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(), "threads": threads}
 
 
-def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=None, label: str = "configs[1]"):
+def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=None, label: str = "configs[1]",
+                      server: bool = False):
     """The drop-in's per-cycle path, the calls the Go
     shim makes per scheduling cycle, through the C ABI of libksched.so:
     ksg_snapshot_add_pod -> ksg_snapshot_sync (append to the device
@@ -297,7 +298,15 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=N
     # in the encoding universe before their cycles, so adding them appends
     for p in pods:
         snap.hint_pod(p)
-    eng = native.Engine(device=0)
+    prev = os.environ.get("KSG_CYCLE_SERVER")
+    os.environ["KSG_CYCLE_SERVER"] = "1" if server else "0"   # read once, when the context opens
+    try:
+        eng = native.Engine(device=0)
+    finally:
+        if prev is None:
+            os.environ.pop("KSG_CYCLE_SERVER")
+        else:
+            os.environ["KSG_CYCLE_SERVER"] = prev
     snap.load(eng)
     N = len(nodes)
     rows = native.KsgEvalRows()
@@ -331,8 +340,11 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=N
     us = phases / 1e3
     per = us.sum(axis=1)
     names = ["add_pod", "sync", "eval_capture", "statuses", "assume"]
+    eval_path = eng.last_run_info()[0]
+    eng.close()
     return {"workload": f"{label} cluster ({N} nodes), per-cycle C-ABI path, {n_pods} cycles timed after {warm}",
             "driver": "C (tests/c/cycle_driver.c), CLOCK_MONOTONIC per call",
+            "mode": "persistent server (KSG_CYCLE_SERVER=1)" if server else "one launch per cycle",
             "pending_pods_hinted": True,
             "us_per_cycle_mean": float(per.mean()), "us_per_cycle_p50": float(np.percentile(per, 50)),
             "us_per_cycle_p99": float(np.percentile(per, 99)), "pods_per_s": float(1e6 / per.mean()),
@@ -340,7 +352,7 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=N
             "breakdown_us_p50": {k: float(np.percentile(us[:, j], 50)) for j, k in enumerate(names)},
             "appended": int(ap.value), "full_reloads": int(rl.value),
             "placements_equal_run_queue": bool(np.array_equal(placed, want)),
-            "eval_path": eng.last_run_info()[0], "eval_path_legend": "5 per-cycle kernel, 6 its topology form"}
+            "eval_path": eval_path, "eval_path_legend": "5 per-cycle kernel, 6 its topology form"}
 
 
 def queue_roofline(metrics, kstats, bpe: int, node_evals: int, kms: float, pmc_file: str):
@@ -600,11 +612,12 @@ def main():
             log(f"[rank {rank}] annotation sidecar unavailable: {e}")
     if eng1 is not None:
         eng1.close()
-    cyc = None
+    cyc = cyc_srv = None
     if world == 1 and args.cycle_pods > 0:
         try:
             S = importlib.import_module(PKG + ".snapshot")
             cyc = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods)
+            cyc_srv = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods, server=True)
         except Exception as e:
             log(f"[rank {rank}] per-cycle sidecar unavailable: {e}")
     cyc3 = ann3 = None
@@ -662,6 +675,7 @@ def main():
         out["source_hash"] = {"library": ge.library_hash(), "tree": ge.source_hash()}
         out["source_hash"]["matches"] = out["source_hash"]["library"] == out["source_hash"]["tree"]
         for key, val in (("configs1", c1), ("replica_sweep", sweep), ("annotations", ann), ("per_cycle", cyc),
+                         ("per_cycle_server", cyc_srv),
                          ("kubelet_memory", kub), ("per_cycle_configs2", cyc3), ("annotations_configs2", ann3)):
             if val is not None:
                 out[key] = val

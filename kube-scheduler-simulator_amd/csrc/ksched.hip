@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <array>
 #include <cstdio>
 #include <cstring>
@@ -193,6 +194,16 @@ struct ksg_ctx {
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
   int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
   CycArgs cyc_args{};                       // ksg_eval_cycle's launch arguments, rebuilt in place per call
+  // the persistent per-cycle server (env KSG_CYCLE_SERVER=1, ksched_cycle.h ksg_cycle_server)
+  bool srv_mode = false;
+  bool srv_running = false;
+  int srv_kn = 0;
+  unsigned srv_G = 0;
+  bool srv_img = false, srv_sys = false;
+  CycStatic srv_static{};
+  SrvMailbox* h_mb = nullptr;               // pinned host mailbox
+  const SrvMailbox* d_mb = nullptr;
+  std::chrono::steady_clock::time_point srv_last{};
   int cycle_kn = 1;                         // env KSG_CYCLE_KN (1/2/4): the smallest nodes-per-lane tried (tests)
   bool cycle_sys = false;                   // env KSG_CYCLE_SYS=1: system-scope host stores (no L2 write-back)
   int cycle_es = 0;                         // env KSG_CYCLE_ES=2/4/8: force the row width (measurements)
@@ -414,6 +425,21 @@ int launch_queue(ksg_ctx* ctx, QueueArgs& a, int n_replicas, int block, bool top
   HIPC(ctx, hipGetLastError());
   if ((rc = tlaunched(ctx, topo ? KSG_K_QUEUE_TOPO : KSG_K_QUEUE, (double)n_replicas * a.count * a.c.N))) return rc;
   HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  return KSG_OK;
+}
+
+// Stop the persistent per-cycle server, if one runs: a stop call through the
+// mailbox, then the stream drains.  Everything that puts work on the
+// context's stream or reads / replaces node state calls this first (the
+// server holds the node columns in registers while it runs).
+int srv_stop(ksg_ctx* ctx) {
+  if (!ctx || !ctx->srv_running) return KSG_OK;
+  ctx->srv_running = false;
+  SrvMailbox* mb = ctx->h_mb;
+  mb->k.op = 1;
+  const unsigned seq = ++ctx->ev_seq == 0 ? ++ctx->ev_seq : ctx->ev_seq;
+  __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
   return KSG_OK;
 }
 
@@ -1664,6 +1690,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
                  ksg_result* results, ksg_capture* cap) {
   int rc = check_ready(ctx);
   if (rc) return rc;
+  if ((rc = srv_stop(ctx))) return rc;
   if (first < 0 || count < 0 || first + count > ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod range");
   if ((rc = check_blobs(ctx, first, count))) return rc;
   if ((rc = check_supported(ctx, ctx->prof, first, count))) return rc;
@@ -1888,6 +1915,8 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
   // device block: parts[Gm] | flags[Gm][32] | timeout
   const size_t d_flags = sizeof(CycPart) * Gm, d_to = d_flags + 128 * Gm, d_need = d_to + 128;
+  if (d_need > ctx->ev_bytes || h_need > ctx->h_ev_bytes || !ctx->ev_clean || ctx->ev_prof_dirty || !ctx->d_ev_prof)
+    if ((rc = srv_stop(ctx))) return rc;   // stream work ahead: a running server leaves first
   if (d_need > ctx->ev_bytes) {
     if (ctx->d_ev) {
       auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_ev);
@@ -1932,35 +1961,89 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   if (!staged && (rc = flush_stage(ctx))) return rc;
   char* hb = ctx->h_ev;
   char* db = ctx->d_hev;
-  const unsigned seq = ++ctx->ev_seq == 0 ? ++ctx->ev_seq : ctx->ev_seq;   // never 0 (a fresh block)
-  // The launch arguments, rebuilt in place (the scalar part changes only with
-  // the context; the pod, its programs and the deferred assume per call)
+  // The arguments: the static part (what the persistent server keeps) and this
+  // call (the pod, its profile facts, the deferred assume, the outputs)
   CycArgs& ca = ctx->cyc_args;
-  ca.c = ctx->c;
-  ca.requested = ctx->st.requested;
-  ca.nonzero = ctx->st.nonzero;
-  ca.pod_count = ctx->st.pod_count;
-  ca.used_ports = ctx->st.ports;
-  ca.pod = hp;
+  CycStatic& cs = ca.s;
+  cs.c = ctx->c;
+  cs.requested = ctx->st.requested;
+  cs.nonzero = ctx->st.nonzero;
+  cs.pod_count = ctx->st.pod_count;
+  cs.used_ports = ctx->st.ports;
+  cs.parts = reinterpret_cast<CycPart*>(ctx->d_ev);
+  cs.flags = reinterpret_cast<unsigned*>(ctx->d_ev + d_flags);
+  cs.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_to);
+  cs.stamps = nullptr;
+#ifdef KSG_STAMPS
+  if (!ctx->d_stamps) {
+    if ((rc = srv_stop(ctx))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 128, ctx->stream));
+  }
+  cs.stamps = ctx->d_stamps;
+#endif
+  const bool want_img = ((prof.score_mask >> KSG_PL_IMAGE_LOCALITY) & 1u) && ctx->c.I > 0;
+  const bool server = ctx->srv_mode;
+  if (ctx->srv_running) {   // a server launched for other arguments, or idle long enough to be near its own exit
+    const double idle = std::chrono::duration<double>(std::chrono::steady_clock::now() - ctx->srv_last).count();
+    if (!server || ctx->srv_kn != kn || ctx->srv_G != G || ctx->srv_img != want_img || ctx->srv_sys != ctx->cycle_sys ||
+        idle > 0.25 || std::memcmp(&ctx->srv_static, &cs, sizeof(CycStatic)) != 0)
+      if ((rc = srv_stop(ctx))) return rc;
+  }
+  if (server && !ctx->srv_running) {   // the persistent form: started once, fed through the mailbox
+    if (!ctx->h_mb) {
+      HIPC(ctx, hipHostMalloc((void**)&ctx->h_mb, sizeof(SrvMailbox), hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(ctx->h_mb, 0, sizeof(SrvMailbox));
+      void* dp = nullptr;
+      HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_mb, 0));
+      ctx->d_mb = static_cast<const SrvMailbox*>(dp);
+    }
+    SrvArgs sa{};
+    sa.s = cs;
+    sa.mb = ctx->d_mb;
+    sa.last = __atomic_load_n(&ctx->h_mb->seq, __ATOMIC_ACQUIRE);
+    sa.want_img = want_img;
+    void* sargs[] = {&sa};
+    const void* kf = ctx->cycle_sys ? (kn == 1 ? (const void*)ksg_cycle_server<1, true>
+                                      : kn == 2 ? (const void*)ksg_cycle_server<2, true>
+                                                : (const void*)ksg_cycle_server<4, true>)
+                                    : (kn == 1 ? (const void*)ksg_cycle_server<1, false>
+                                      : kn == 2 ? (const void*)ksg_cycle_server<2, false>
+                                                : (const void*)ksg_cycle_server<4, false>);
+    // cooperative: every workgroup resident (or the launch is refused), as the
+    // exchanges need for the server's whole life
+    HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(64), sargs, 0, ctx->stream));
+    HIPC(ctx, hipGetLastError());
+    ctx->srv_running = true;
+    ctx->srv_last = std::chrono::steady_clock::now();
+    ctx->srv_kn = kn;
+    ctx->srv_G = G;
+    ctx->srv_img = want_img;
+    ctx->srv_sys = ctx->cycle_sys;
+    ctx->srv_static = cs;
+  }
+  const unsigned seq = ++ctx->ev_seq == 0 ? ++ctx->ev_seq : ctx->ev_seq;   // never 0 (a fresh block)
+  CycCall& ck = ca.k;
+  ck.pod = hp;
   // the profile facts of this pod (make_view(topo = false) + cm_prof, on the host)
   {
     uint32_t fskip = hp.filter_skip | (1u << KSG_PL_INTER_POD_AFFINITY) | (1u << KSG_PL_POD_TOPOLOGY_SPREAD);
-    ca.forder = 0;
-    ca.fmask = 0;
-    ca.n_filter = prof.n_filter;
+    ck.forder = 0;
+    ck.fmask = 0;
+    ck.n_filter = prof.n_filter;
     for (int kf = 0; kf < prof.n_filter; kf++) {
       const int pl = prof.filter_order[kf];
-      ca.forder |= (uint64_t)(pl & 15) << (4 * kf);
-      if (!((fskip >> pl) & 1u)) ca.fmask |= 1u << pl;
+      ck.forder |= (uint64_t)(pl & 15) << (4 * kf);
+      if (!((fskip >> pl) & 1u)) ck.fmask |= 1u << pl;
     }
-    ca.smask = prof.score_mask & ~hp.score_skip &
+    ck.smask = prof.score_mask & ~hp.score_skip &
                ~((1u << KSG_PL_INTER_POD_AFFINITY) | (1u << KSG_PL_POD_TOPOLOGY_SPREAD));
-    ca.w_fit = prof.weight[KSG_PL_NODE_RESOURCES_FIT];
-    ca.w_ba = prof.weight[KSG_PL_BALANCED_ALLOCATION];
-    ca.w_img = prof.weight[KSG_PL_IMAGE_LOCALITY];
-    ca.w_t = prof.weight[KSG_PL_TAINT_TOLERATION];
-    ca.w_a = prof.weight[KSG_PL_NODE_AFFINITY];
-    ca.fit_ignored = prof.fit_ignored_res;
+    ck.w_fit = prof.weight[KSG_PL_NODE_RESOURCES_FIT];
+    ck.w_ba = prof.weight[KSG_PL_BALANCED_ALLOCATION];
+    ck.w_img = prof.weight[KSG_PL_IMAGE_LOCALITY];
+    ck.w_t = prof.weight[KSG_PL_TAINT_TOLERATION];
+    ck.w_a = prof.weight[KSG_PL_NODE_AFFINITY];
+    ck.fit_ignored = prof.fit_ignored_res;
     bool ok = prof.fit_n == 2 && prof.ba_n == 2;   // cm_prof (ksched_device.h)
     int64_t wc = 0, wm = 0;
     if (ok) {
@@ -1972,74 +2055,74 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       ok = ok && ((b0 == KSG_RES_CPU && b1 == KSG_RES_MEM) || (b0 == KSG_RES_MEM && b1 == KSG_RES_CPU));
       ok = ok && wc > 0 && wm > 0;
     }
-    ca.cm_fast = ok;
-    ca.cm_least = prof.fit_strategy == KSG_LEAST_ALLOCATED;
-    ca.cm_wc = ok ? wc : 0;
-    ca.cm_wm = ok ? wm : 0;
-    ca.cm_inv_ws = ok ? 1.0f / (float)(wc + wm) : 1.0f;
-    ca.cm_inv_wc = ok ? 1.0f / (float)wc : 1.0f;
-    ca.cm_inv_wm = ok ? 1.0f / (float)wm : 1.0f;
+    ck.cm_fast = ok;
+    ck.cm_least = prof.fit_strategy == KSG_LEAST_ALLOCATED;
+    ck.cm_wc = ok ? wc : 0;
+    ck.cm_wm = ok ? wm : 0;
+    ck.cm_inv_ws = ok ? 1.0f / (float)(wc + wm) : 1.0f;
+    ck.cm_inv_wc = ok ? 1.0f / (float)wc : 1.0f;
+    ck.cm_inv_wm = ok ? 1.0f / (float)wm : 1.0f;
   }
-  ca.gprof = ctx->d_ev_prof;
-  ca.n_rows = n_rows;
-  ca.n_normrows = n_normrows;
-  ca.es = (int32_t)es;
-  ca.kn = kn;
-  ca.rows = 0;
-  for (int q = 0; q < n_rows; q++) ca.rows |= (uint64_t)(rows[q] & 15) << (4 * q);
-  ca.h_fs = reinterpret_cast<uint32_t*>(db + o_fs);
-  ca.h_raw = db + o_raw;
-  ca.h_tot = db + o_tot;
-  ca.h_norm = db + o_norm;
-  ca.h_stats = reinterpret_cast<int32_t*>(db);
-  ca.h_wg = reinterpret_cast<CycWg*>(db + o_wg);
-  ca.seq = seq;
-  ca.parts = reinterpret_cast<CycPart*>(ctx->d_ev);
-  ca.flags = reinterpret_cast<unsigned*>(ctx->d_ev + d_flags);
-  ca.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_to);
-  ca.stamps = nullptr;
-#ifdef KSG_STAMPS
-  if (!ctx->d_stamps) {
-    if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
-    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 128, ctx->stream));
-  }
-  ca.stamps = ctx->d_stamps;
-#endif
-  // the pod's programs: inline in the arguments (from the host copy) when they
-  // fit, else read by the kernel from the staged append or the device pool
+  ck.gprof = ctx->d_ev_prof;
+  ck.n_rows = n_rows;
+  ck.n_normrows = n_normrows;
+  ck.es = (int32_t)es;
+  ck.kn = kn;
+  ck.rows = 0;
+  for (int q = 0; q < n_rows; q++) ck.rows |= (uint64_t)(rows[q] & 15) << (4 * q);
+  ck.h_fs = reinterpret_cast<uint32_t*>(db + o_fs);
+  ck.h_raw = db + o_raw;
+  ck.h_tot = db + o_tot;
+  ck.h_norm = db + o_norm;
+  ck.h_stats = reinterpret_cast<int32_t*>(db);
+  ck.h_wg = reinterpret_cast<CycWg*>(db + o_wg);
+  ck.seq = seq;
+  ck.op = 0;
+  // the pod's programs: inline (kernel arguments or mailbox, from the host
+  // copy) when they fit, else read by the kernel from the staged append or
+  // the device pool
   const int32_t* sprog = staged ? reinterpret_cast<const int32_t*>(ctx->d_stage + sizeof(ksg_pod)) : nullptr;
-  ca.gprog = staged ? sprog - ctx->stage_base : ctx->d_prog;
-  ca.blob_len = hp.blob_len;
-  ca.bsrc = ca.gprog + hp.blob;
-  if (hp.blob_len <= kCycBlob && hp.blob >= 0 && (size_t)hp.blob + hp.blob_len <= ctx->h_prog.size())
-    std::memcpy(ca.blob, ctx->h_prog.data() + hp.blob, sizeof(int32_t) * hp.blob_len);
-  else if (hp.blob_len <= kCycBlob)
+  ck.gprog = staged ? sprog - ctx->stage_base : ctx->d_prog;
+  ck.blob_len = hp.blob_len;
+  ck.bsrc = ck.gprog + hp.blob;
+  if (hp.blob < 0 || (size_t)hp.blob + hp.blob_len > ctx->h_prog.size())
     return fail(ctx, KSG_E_STATE, "per-cycle evaluation: pod programs outside the host program copy");
-  ca.wpods = nullptr;
+  ck.wpods = nullptr;
   if (staged) {
-    ca.wpods = ctx->d_pods + pod;
-    ca.wprog = ctx->d_prog + ctx->stage_base;
-    ca.sprog = sprog;
-    ca.slen = ctx->stage_len;
+    ck.wpods = ctx->d_pods + pod;
+    ck.wprog = ctx->d_prog + ctx->stage_base;
+    ck.sprog = sprog;
+    ck.slen = ctx->stage_len;
   }
-  ca.cm_node = -1;
+  ck.cm_node = -1;
   if (ctx->pc_node >= 0) {   // the deferred assume: the node's owner lane adds it before evaluating
     const ksg_pod& q = ctx->h_pods[ctx->pc_pod];
-    ca.cm_node = ctx->pc_node;
-    for (int r = 0; r < KSG_MAX_RES; r++) ca.cm_req[r] = q.req[r];
-    ca.cm_nz_cpu = q.nz_cpu;
-    ca.cm_nz_mem = q.nz_mem;
+    ck.cm_node = ctx->pc_node;
+    for (int r = 0; r < KSG_MAX_RES; r++) ck.cm_req[r] = q.req[r];
+    ck.cm_nz_cpu = q.nz_cpu;
+    ck.cm_nz_mem = q.nz_mem;
   }
-  treset(ctx);
-  if ((rc = tmark(ctx))) return rc;
-  void* kargs[] = {&ca};
-  if (ctx->cycle_coop)
-    HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(kn), dim3(G), dim3(64), kargs, 0, ctx->stream));
-  else   // G is within the occupancy API's co-resident count less one per CU (the exchange's poll is bounded)
-    HIPC(ctx, hipLaunchKernel(kernel_of(kn), dim3(G), dim3(64), kargs, 0, ctx->stream));
-  ctx->pc_node = -1;   // applied by this launch (a retry below must not add it again)
-  if ((rc = tlaunched(ctx, KSG_K_EVAL_CYCLE, (double)N))) return rc;
-  HIPC(ctx, hipGetLastError());
+  if (server) {
+    // the call, then its sequence number (x86 stores are ordered; the server
+    // reads seq, then the rest)
+    SrvMailbox* mb = ctx->h_mb;
+    std::memcpy(&mb->k, &ck, sizeof(CycCall));
+    std::memcpy(mb->blob, ctx->h_prog.data() + hp.blob, sizeof(int32_t) * hp.blob_len);
+    __builtin_ia32_sfence();   // (in case a copy used streaming stores)
+    __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
+  } else {
+    if (hp.blob_len <= kCycBlob) std::memcpy(ca.blob, ctx->h_prog.data() + hp.blob, sizeof(int32_t) * hp.blob_len);
+    treset(ctx);
+    if ((rc = tmark(ctx))) return rc;
+    void* kargs[] = {&ca};
+    if (ctx->cycle_coop)
+      HIPC(ctx, hipLaunchCooperativeKernel(kernel_of(kn), dim3(G), dim3(64), kargs, 0, ctx->stream));
+    else   // G is within the occupancy API's co-resident count less one per CU (the exchange's poll is bounded)
+      HIPC(ctx, hipLaunchKernel(kernel_of(kn), dim3(G), dim3(64), kargs, 0, ctx->stream));
+    if ((rc = tlaunched(ctx, KSG_K_EVAL_CYCLE, (double)N))) return rc;
+    HIPC(ctx, hipGetLastError());
+  }
+  ctx->pc_node = -1;   // applied by this call (a retry below must not add it again)
   // the staged append is consumed: the kernel read it (or had it with the
   // launch) before its workgroups stored their done words, which this call
   // waits for, so the staging buffer is free when it returns (no event)
@@ -2057,7 +2140,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       const hipError_t e = hipStreamQuery(ctx->stream);
       if (e == hipSuccess && reinterpret_cast<const volatile CycWg*>(wgr)[g].done != seq) {
         ctx->ev_clean = false;
-        return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: kernel finished without its completion words");
+        ctx->srv_running = false;
+        return fail(ctx, KSG_E_DEVICE, server ? "per-cycle server: left without serving the call"
+                                              : "per-cycle evaluation: kernel finished without its completion words");
       }
       if (e != hipSuccess && e != hipErrorNotReady)
         return fail(ctx, KSG_E_DEVICE, std::string("per-cycle evaluation: ") + hipGetErrorString(e));
@@ -2073,8 +2158,14 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     best = wgr[g].key > best ? wgr[g].key : best;
     herr |= wgr[g].err;
   }
+  if (server) ctx->srv_last = std::chrono::steady_clock::now();
   if (herr & 2u) {
     ctx->ev_clean = false;   // clears the sticky timeout word before the next call
+    if (server) {            // every workgroup of the server leaves on a timed-out exchange
+      (void)hipStreamSynchronize(ctx->stream);
+      ctx->srv_running = false;
+      return fail(ctx, KSG_E_DEVICE, "per-cycle server: workgroup exchange timed out");
+    }
     if (!ctx->cycle_coop) {   // not every workgroup was resident: the cooperative launch from now on
       ctx->cycle_coop = true;
       return eval_fast(ctx, pod, res, cap, view);
@@ -2285,6 +2376,7 @@ int eval_internal(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) 
   if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
   if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, cap);   // consumes or flushes a staged append
+  if ((rc = srv_stop(ctx))) return rc;   // the other paths put work on the stream
   if (eval_topo_eligible(ctx, pod)) return eval_topo_fast(ctx, pod, res, cap);
   int32_t pl;
   return run_internal(ctx, pod, 1, 0, &pl, res, cap);
@@ -2294,6 +2386,7 @@ int eval_internal(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap) 
 template <typename T>
 int dgrow(ksg_ctx* ctx, T** p, size_t* cap, size_t used, size_t need) {
   if (need <= *cap && *p) return KSG_OK;
+  if (int rc = srv_stop(ctx)) return rc;
   const size_t ncap = std::max(need, 2 * *cap);
   T* np = nullptr;
   int rc = dalloc(ctx, &np, ncap);
@@ -2353,6 +2446,7 @@ int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, const ksg_pod& p);
 // calls this first, except the per-cycle evaluation of the staged pod.
 int flush_stage(ksg_ctx* ctx) {
   if (!ctx->stage_pending) return KSG_OK;
+  if (int rc = srv_stop(ctx)) return rc;
   const size_t pb = sizeof(ksg_pod) * ctx->stage_n, gb = sizeof(int32_t) * ctx->stage_len;
   if (pb)
     HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->stage_first, ctx->h_stage, pb, hipMemcpyHostToDevice, ctx->stream));
@@ -2368,6 +2462,7 @@ int flush_stage(ksg_ctx* ctx) {
 // whose kernel applies the assume itself (ksched_cycle.h, cm_*).
 int flush_commit(ksg_ctx* ctx) {
   if (ctx->pc_node < 0) return KSG_OK;
+  if (int rc = srv_stop(ctx)) return rc;
   const int pod = ctx->pc_pod, node = ctx->pc_node;
   ctx->pc_node = -1;
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
@@ -2424,6 +2519,7 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
     else HIPC(ctx, hipEventSynchronize(ctx->ev_stage));   // a flushed copy has left the buffer
     if (pb + gb > ctx->h_stage_bytes) {
       if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_mb) (void)hipHostFree(ctx->h_mb);
       ctx->h_stage = nullptr;
       ctx->d_stage = nullptr;
       ctx->h_stage_bytes = 0;
@@ -2441,6 +2537,7 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
     ctx->stage_base = prog_base;
     ctx->stage_len = prog_len;
   } else {
+    if ((rc = srv_stop(ctx))) return rc;
     if (n) HIPC(ctx, hipMemcpyAsync(ctx->d_pods + ctx->n_pods, pods, pb, hipMemcpyHostToDevice, ctx->stream));
     if (prog_len) HIPC(ctx, hipMemcpyAsync(ctx->d_prog + prog_base, prog, gb, hipMemcpyHostToDevice, ctx->stream));
     HIPC(ctx, hipStreamSynchronize(ctx->stream));
@@ -2540,6 +2637,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_SERVER")) ctx->srv_mode = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_ES")) ctx->cycle_es = atoi(f);
   if (const char* f = getenv("KSG_CYCLE_KN")) {
     const int v = atoi(f);
@@ -2555,6 +2653,7 @@ int ksg_open(int device, ksg_ctx** out) {
 }
 
 int ksg_close(ksg_ctx* ctx) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx) return KSG_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -2580,6 +2679,7 @@ int ksg_close(ksg_ctx* ctx) {
 const char* ksg_last_error(ksg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 int ksg_set_profile(ksg_ctx* ctx, const ksg_profile* prof) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !prof) return KSG_E_INVALID;
   if (prof->n_filter < 0 || prof->n_filter > KSG_NPLUGINS || prof->fit_n < 0 || prof->fit_n > KSG_MAX_RES ||
       prof->ba_n < 0 || prof->ba_n > KSG_MAX_RES)
@@ -2591,6 +2691,7 @@ int ksg_set_profile(ksg_ctx* ctx, const ksg_profile* prof) {
 }
 
 int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !nd || !tp) return KSG_E_INVALID;
   HIPC(ctx, hipSetDevice(ctx->device));
   if (nd->n_nodes <= 0 || nd->n_res < 3 || nd->n_res > KSG_MAX_RES)
@@ -2675,6 +2776,7 @@ int ksg_load_nodes(ksg_ctx* ctx, const ksg_nodes* nd, const ksg_topology* tp) {
 }
 
 int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !wl || (!wl->pods && wl->n_pods > 0) || wl->n_pods < 0 || wl->prog_len < 0 ||
       (!wl->prog && wl->prog_len > 0))
     return KSG_E_INVALID;
@@ -2737,6 +2839,7 @@ int ksg_eval_view(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_eval_rows* row
   if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
   if (eval_fast_eligible(ctx, pod)) return eval_fast(ctx, pod, res, nullptr, rows);
+  if ((rc = srv_stop(ctx))) return rc;   // the other paths put work on the stream
   if (eval_topo_eligible(ctx, pod)) return eval_topo_fast(ctx, pod, res, nullptr, rows);
   // otherwise: run_internal into library-owned int64 rows
   const size_t N = ctx->c.N;
@@ -2766,6 +2869,7 @@ int ksg_append_pods(ksg_ctx* ctx, const ksg_workload* tail, int64_t prog_base) {
 
 int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t prog_len, ksg_result* res,
                  ksg_capture* cap) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !pod || !res) return KSG_E_INVALID;
   if (!ctx->have_wl) return fail(ctx, KSG_E_STATE, "load a workload first");
   // Stage the pod behind the loaded workload (offsets rebased), evaluate it,
@@ -2808,6 +2912,7 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
     ctx->pc_node = node;
     return KSG_OK;
   }
+  if ((rc = srv_stop(ctx))) return rc;
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
                      ctx->d_prog, pod, node, sign);
   // stream-ordered: the next evaluation on ctx->stream sees the update, and
@@ -2819,6 +2924,7 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
 int ksg_commit(ksg_ctx* ctx, int32_t pod, int32_t node) { return commit_signed(ctx, pod, node, 1); }
 
 int ksg_commit_batch(ksg_ctx* ctx, const int32_t* pods, const int32_t* nodes, int32_t n) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (n < 0 || (n > 0 && (!pods || !nodes))) return fail(ctx, KSG_E_INVALID, "commit batch arguments");
@@ -2846,6 +2952,7 @@ int ksg_uncommit(ksg_ctx* ctx, int32_t pod, int32_t node) { return commit_signed
 
 int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int32_t n_cand, const int32_t* vic_off,
                         const int32_t* vic_pod, int32_t* fits, uint8_t* victim) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (pod < 0 || pod >= ctx->n_pods || n_cand < 0 || (n_cand > 0 && (!cand_node || !vic_off || !fits)))
@@ -2921,6 +3028,7 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
 
 int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replicas, int32_t first, int32_t count,
                      int32_t* placements, ksg_replica_summary* summaries) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   int rc = check_ready(ctx);
   if (rc) return rc;
   if (!profiles || n_replicas <= 0 || first < 0 || count < 0 || first + count > ctx->n_pods || !placements)
@@ -3067,6 +3175,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
 }
 
 int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !out) return KSG_E_INVALID;
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "no nodes loaded");
   HIPC(ctx, hipSetDevice(ctx->device));
@@ -3081,6 +3190,7 @@ int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out) {
 }
 
 int ksg_reset_state(ksg_ctx* ctx) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx) return KSG_E_INVALID;
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "no nodes loaded");
   HIPC(ctx, hipSetDevice(ctx->device));
@@ -3099,13 +3209,15 @@ int ksg_reset_state(ksg_ctx* ctx) {
 
 #ifdef KSG_STAMPS
 // Diagnostic build only: cycle sums per phase-2 segment since load.
-int ksg_debug_stamps(ksg_ctx* ctx, unsigned long long* out8) {   // 16 segment sums
+int ksg_debug_stamps(ksg_ctx* ctx, unsigned long long* out8) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first   // 16 segment sums
   if (!ctx || !out8 || !ctx->d_stamps) return KSG_E_STATE;
   HIPC(ctx, hipMemcpy(out8, ctx->d_stamps, 128, hipMemcpyDeviceToHost));
   return KSG_OK;
 }
 // eval_node_src's 16 segment sums (g_eval_stamp)
 int ksg_debug_eval_stamps(ksg_ctx* ctx, unsigned long long* out16) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !out16) return KSG_E_INVALID;
   HIPC(ctx, hipSetDevice(ctx->device));
   HIPC(ctx, hipStreamSynchronize(ctx->stream));
@@ -3115,6 +3227,7 @@ int ksg_debug_eval_stamps(ksg_ctx* ctx, unsigned long long* out16) {
 #endif
 
 int ksg_set_timing(ksg_ctx* ctx, int on) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx) return KSG_E_INVALID;
   ctx->timing = on != 0;
   treset(ctx);
@@ -3122,6 +3235,7 @@ int ksg_set_timing(ksg_ctx* ctx, int on) {
 }
 
 int ksg_kernel_stats(ksg_ctx* ctx, ksg_kernel_stat* out, int32_t max, int32_t* n) {
+  if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !n || (max > 0 && !out)) return KSG_E_INVALID;
   int k = 0;
   for (int i = 0; i < KSG_NKERNELS; i++) {

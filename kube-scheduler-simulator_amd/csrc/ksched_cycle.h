@@ -38,6 +38,15 @@
 //              stores to the host block (SYS: system-scope stores), one
 //              system-scope release, then the done word.
 //
+// ksg_cycle_server<KN, SYS> is the same evaluation as a persistent kernel
+// (KSG_CYCLE_SERVER=1): the node columns are loaded once and stay in
+// registers / LDS, and each cycle's call (CycCall + programs) arrives in a
+// pinned host mailbox the workgroups poll, so a cycle pays neither a launch
+// nor the entry latencies.  It leaves on a stop request, after kSrvIdle of
+// idleness (the host never calls a server idle for more than 0.25 s: it
+// restarts it instead, so a call never races the idle exit), or when an
+// exchange times out, so every wave always ends.
+//
 // The evaluation is eval_node_src's arithmetic (same helpers: untolerated_slot,
 // na_required_match, fit_filter, fit_ba_cm / fit_score / ba_score,
 // image_score, taint_score, na_pref_score) on a prefetched node source, and
@@ -47,11 +56,13 @@
 // ksg_capture_norm (nb = 1, nothing assumed) bit for bit.
 
 constexpr int kCycBlob = 256;    // program words carried in the kernel arguments
-constexpr int kCycLab = 8;       // label columns prefetched into registers
+constexpr int kCycLab = 8;       // label columns prefetched into LDS rows
 constexpr int kCycTnt = 8;       // taint slots prefetched into registers
 constexpr int kCycImg = 8;       // image slots prefetched into registers (ImageLocality pods)
 constexpr int kCycEff = 4096;    // taint-effect bytes staged in LDS
 constexpr int kCycMaxKN = 4;     // nodes per lane
+constexpr unsigned long long kSrvIdle = 1000000000ull;   // server: 10 s of the 100 MHz real-time clock
+                                                        // (the host restarts a server idle for 0.25 s)
 
 struct CycPart {   // one workgroup's phase-1 statistics
   int32_t nfeas, max_t, max_a, lo;   // lo = max over its feasible nodes of N - n
@@ -62,17 +73,23 @@ struct CycWg {     // one workgroup's record in the host block
   uint32_t done;            // = seq once every row of the workgroup and the two words above are written
 };
 
-// The launch arguments.  Scalar part first (warmed line by line at entry),
-// the program words last (copied to LDS by vector loads).
-struct CycArgs {
-  // ---- node columns and state --------------------------------------------------------
+// What does not change between calls on a loaded context.
+struct CycStatic {
   DevCluster c;
   int64_t* requested;
   int64_t* nonzero;
   int32_t* pod_count;
   const uint32_t* used_ports;
+  CycPart* parts;                    // [G]
+  unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
+  unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
+  unsigned long long* stamps;        // KSG_STAMPS builds: per-segment cycle sums of workgroup 0
+};
+
+// One call: the pod, the profile facts the host derived for it, the deferred
+// assume of the previous pod, a staged append, where the rows go.
+struct CycCall {
   const int32_t* gprog;              // the program pool as the kernel sees it (node_set; programs not inline)
-  // ---- the pod and its profile facts (host-derived) ----------------------------------
   ksg_pod pod;
   uint64_t forder;                   // filter plugins in profile order, 4 bits each
   int32_t n_filter;
@@ -84,34 +101,50 @@ struct CycArgs {
   int64_t cm_wc, cm_wm;
   float cm_inv_ws, cm_inv_wc, cm_inv_wm;
   const ksg_profile* gprof;          // device copy (the generic Fit / BalancedAllocation forms)
-  // ---- the deferred assume of the previous pod ---------------------------------------
-  int32_t cm_node;                   // -1: none; else its owner lane adds it first (NodeInfo.AddPod)
+  int32_t cm_node;                   // the deferred assume: -1 none; else its owner lane adds it first
   int64_t cm_req[KSG_MAX_RES];
   int64_t cm_nz_cpu, cm_nz_mem;
-  // ---- a staged append of this pod: workgroup 0 writes it to the device pool ----------
-  ksg_pod* wpods;                    // null: nothing staged
+  ksg_pod* wpods;                    // a staged append of this pod (workgroup 0 writes it); null: none
   int32_t* wprog;
   const int32_t* sprog;
   int64_t slen;
-  // ---- outputs (fine-grained pinned host memory, device addresses) -------------------
   int32_t n_rows, n_normrows, es, kn;
   uint64_t rows;                     // score row q's plugin in bits 4q..4q+3 (the normalising ones first)
-  uint32_t* h_fs;                    // [N]
+  uint32_t* h_fs;                    // [N]          (fine-grained pinned host memory, device addresses)
   char* h_raw;                       // [n_rows][N]
   char* h_tot;                       // [N]
   char* h_norm;                      // [n_normrows][N]
   int32_t* h_stats;                  // [4] nfeas, max taint, max node affinity, max (N - n) (workgroup 0)
   CycWg* h_wg;                       // [G]
   unsigned seq;
-  CycPart* parts;                    // [G]
-  unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
-  unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
-  unsigned long long* stamps;        // KSG_STAMPS builds: per-segment cycle sums of workgroup 0
-  const int32_t* bsrc;               // the programs when blob_len > kCycBlob
+  int32_t op;                        // server mailbox: 0 evaluate, 1 stop
+  const int32_t* bsrc;               // the programs when they are not inline
   int32_t blob_len;
   int32_t pad_;
-  // ---- program words (vector-loaded into LDS) ----------------------------------------
+};
+
+// The launch arguments of ksg_eval_cycle: scalar part first (warmed line by
+// line at entry), the program words last (copied to LDS by vector loads).
+struct CycArgs {
+  CycStatic s;
+  CycCall k;
   int32_t blob[kCycBlob];
+};
+
+// The persistent server's mailbox (pinned host memory): the host writes the
+// call and its programs, then `seq` (x86 stores are ordered; the server reads
+// seq, then the rest, with system-scope loads).
+struct SrvMailbox {
+  unsigned seq;
+  unsigned pad_[15];
+  CycCall k;
+  int32_t blob[KSG_BLOB_MAX];
+};
+struct SrvArgs {
+  CycStatic s;
+  const SrvMailbox* mb;              // device address of the mailbox
+  unsigned last;                     // the last sequence number served before this launch
+  int32_t want_img;                  // the profile scores ImageLocality: keep the image slots
 };
 
 // The node a lane evaluates, its columns prefetched: the first kCycLab label
@@ -255,58 +288,39 @@ __device__ __forceinline__ void cyc_warm_args() {
 // Grid exchange of a one-wave workgroup: its flag line gets `seq`, then the
 // wave polls every flag until all hold `seq` (bounded; a timeout is sticky and
 // reported).
-__device__ __forceinline__ bool cyc_exchange(const CycArgs& a, int G) {
+__device__ __forceinline__ bool cyc_exchange(const CycStatic& S, unsigned seq, int G) {
   const int lane = threadIdx.x;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its agent-scope slot stores are done
-  if (lane == 0) gst(&a.flags[(size_t)blockIdx.x * 32], a.seq);
+  if (lane == 0) gst(&S.flags[(size_t)blockIdx.x * 32], seq);
   unsigned spins = 0;
   for (;;) {
     bool ok = true;
-    for (int l = lane; l < G; l += 64) ok = ok && gld(&a.flags[(size_t)l * 32]) == a.seq;
+    for (int l = lane; l < G; l += 64) ok = ok && gld(&S.flags[(size_t)l * 32]) == seq;
     if (__all(ok)) return true;
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 22) || gld(a.timeout)) {
-      if (lane == 0) gst(a.timeout, 1u);
+    if (++spins > (1u << 22) || gld(S.timeout)) {
+      if (lane == 0) gst(S.timeout, 1u);
       return false;
     }
   }
 }
 
-
-template <int KN, bool SYS>
-__global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
-  __shared__ int32_t s_blob[KSG_BLOB_MAX];
-  __shared__ uint8_t s_eff[kCycEff];
-  __shared__ uint32_t s_lab[KN][kCycLab][64];
+// A lane's nodes: indices, resource columns, the prefetched static columns.
+// Every load unconditional and unmasked (clamped indices; a column past the
+// allocated ones reads a valid word the evaluation never uses), so they are
+// all in flight together; cyc_stage_nodes finishes them once they are in.
+template <int KN>
+__device__ __forceinline__ void cyc_load_nodes(const CycStatic& S, bool want_img, int G, int (&nk)[KN],
+                                               NodeCols (&L)[KN], PNode (&nd)[KN], uint32_t (&lv)[KN][kCycLab],
+                                               uint32_t (*s_lab)[kCycLab][64]) {
+  const DevCluster& c = S.c;
   const int lane = threadIdx.x;
-  const int G = (int)gridDim.x;
-#ifdef KSG_STAMPS
-  unsigned long long y_acc[8] = {}, y_last = __builtin_amdgcn_s_memtime();
-#endif
-  // ---- entry: argument lines, programs, node columns, all in flight together ----------
-  static_assert(offsetof(CycArgs, blob) <= 768 && sizeof(CycArgs) >= 768, "cyc_warm_args covers 12 lines");
-  cyc_warm_args();
-  const DevCluster& c = a.c;
   const int N = c.N;
   const size_t NN = N;
-  const ksg_pod& p = a.pod;
-  const int blen = a.blob_len;
-  // the node columns of this lane's nodes: every load unconditional and
-  // unmasked (clamped indices; a column past the allocated ones reads a valid
-  // word that the evaluation never uses), so the loads of the whole prologue
-  // are in flight together and the first wait below covers them all
-  int nk[KN];
-  NodeCols L[KN];
-  PNode nd[KN];
-  uint32_t nsw[KN];
-  uint32_t lv[KN][kCycLab];
-  const bool want_img = (a.smask >> KSG_PL_IMAGE_LOCALITY) & 1u;
   const int R = c.R, Lc = c.L, T = c.T, I = c.I;
   const uint32_t* tcol = T > 0 ? c.taints : (const uint32_t*)c.allowed;
   const uint32_t* icol = want_img && I > 0 ? c.images : (const uint32_t*)c.allowed;
   const int Tm = T > 0 ? T : 1, Im = want_img && I > 0 ? I : 1;
-  const int32_t* nset = p.node_set >= 0 ? a.gprog + p.node_set : nullptr;
-  const int32_t* nsrc = nset ? nset : c.allowed;
 #pragma unroll
   for (int k = 0; k < KN; k++) {
     const int n = (k * G + (int)blockIdx.x) * 64 + lane;
@@ -316,11 +330,11 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
     for (int r = 0; r < KSG_MAX_RES; r++) {
       const size_t o = (size_t)(r < R ? r : 0) * NN + m;
       L[k].alloc[r] = c.alloc[o];
-      L[k].req[r] = a.requested[o];
+      L[k].req[r] = S.requested[o];
     }
-    L[k].nz_cpu = a.nonzero[m];
-    L[k].nz_mem = a.nonzero[NN + m];
-    L[k].pod_count = a.pod_count[m];
+    L[k].nz_cpu = S.nonzero[m];
+    L[k].nz_mem = S.nonzero[NN + m];
+    L[k].pod_count = S.pod_count[m];
     L[k].allowed = c.allowed[m];
     nd[k].uns = c.unsched[m] != 0;
 #pragma unroll
@@ -329,7 +343,6 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
     for (int q = 0; q < kCycTnt; q++) nd[k].tnt[q] = tcol[(size_t)(q < Tm ? q : 0) * NN + m];
 #pragma unroll
     for (int q = 0; q < kCycImg; q++) nd[k].img[q] = icol[(size_t)(q < Im ? q : 0) * NN + m];
-    nsw[k] = (uint32_t)nsrc[m >> 5];
     nd[k].label_val = (const KSG_G1 uint32_t*)c.label_val;
     nd[k].label_num = (const KSG_G1 int64_t*)c.label_num;
     nd[k].label_num_ok = (const KSG_G1 uint8_t*)c.label_num_ok;
@@ -340,25 +353,20 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
     nd[k].n = m;
     nd[k].lab = (const KSG_L3 uint32_t*)&s_lab[k][0][lane];
   }
-  // the pod's programs and the taint effects into LDS (issued behind the columns)
-  if (blen <= kCycBlob) {
-    const __attribute__((address_space(4))) int32_t* kb =
-        (const __attribute__((address_space(4))) int32_t*)((const __attribute__((address_space(4))) char*)
-                                                               __builtin_amdgcn_kernarg_segment_ptr() +
-                                                           offsetof(CycArgs, blob));
-    int32_t w[kCycBlob / 64];
-#pragma unroll
-    for (int u = 0; u < kCycBlob / 64; u++) w[u] = kb[lane + 64 * u];   // inside the arguments: unconditional
-#pragma unroll
-    for (int u = 0; u < kCycBlob / 64; u++)
-      if (lane + 64 * u < blen) s_blob[lane + 64 * u] = w[u];
-  } else {
-    for (int i = lane; i < blen; i += 64) s_blob[i] = a.bsrc[i];
-  }
+}
+
+// The taint effects into LDS (issued behind the columns), then the masks and
+// the label rows once the loads are in.
+template <int KN>
+__device__ __forceinline__ void cyc_stage_nodes(const CycStatic& S, NodeCols (&L)[KN], PNode (&nd)[KN],
+                                                const uint32_t (&lv)[KN][kCycLab], uint32_t (*s_lab)[kCycLab][64],
+                                                uint8_t* s_eff) {
+  const DevCluster& c = S.c;
+  const int lane = threadIdx.x;
+  const int R = c.R, Lc = c.L;
   const bool eff_lds = c.V <= kCycEff;
   if (eff_lds)
     for (int i = lane; i < c.V; i += 64) s_eff[i] = c.taint_effect[i];
-  // masks and the label rows, once the loads are in
 #pragma unroll
   for (int k = 0; k < KN; k++) {
 #pragma unroll
@@ -371,46 +379,60 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
     nd[k].eff_lds = eff_lds;
     nd[k].eff = (const KSG_L3 uint8_t*)s_eff;
   }
-  if (a.wpods && blockIdx.x == 0) {   // the staged append: workgroup 0 copies it to the device pool
+}
+
+// One call on a wave whose nodes are loaded (L, nd) and whose pod programs are
+// in LDS (P): the deferred assume, the staged append, the evaluation, the
+// exchange, the rows.  K is the kernel arguments' copy (ksg_eval_cycle) or
+// the LDS copy of the mailbox (ksg_cycle_server); podw its pod record as words.
+template <int KN, bool SYS>
+__device__ __forceinline__ void cyc_serve(const CycStatic& S, const CycCall& K, const int32_t* P,
+                                          const int32_t* podw, const int (&nk)[KN], NodeCols (&L)[KN],
+                                          const PNode (&nd)[KN], const uint32_t (&nsw)[KN], int G
+#ifdef KSG_STAMPS
+                                          , unsigned long long* y_acc, unsigned long long& y_last
+#endif
+) {
+  const int lane = threadIdx.x;
+  const DevCluster& c = S.c;
+  const int N = c.N;
+  const size_t NN = N;
+  const ksg_pod& p = K.pod;
+  if (K.wpods && blockIdx.x == 0) {   // the staged append: workgroup 0 copies it to the device pool
     constexpr int PW = (int)(sizeof(ksg_pod) / 4);
-    const __attribute__((address_space(4))) int32_t* kp =
-        (const __attribute__((address_space(4))) int32_t*)((const __attribute__((address_space(4))) char*)
-                                                               __builtin_amdgcn_kernarg_segment_ptr() +
-                                                           offsetof(CycArgs, pod));
-    if (lane < PW) reinterpret_cast<int32_t*>(a.wpods)[lane] = kp[lane];
-    for (int64_t i = lane; i < a.slen; i += 64) a.wprog[i] = a.sprog[i];
+    if (lane < PW) reinterpret_cast<int32_t*>(K.wpods)[lane] = podw[lane];
+    for (int64_t i = lane; i < K.slen; i += 64) K.wprog[i] = K.sprog[i];
   }
   // the deferred assume: NodeInfo.AddPod on the owner lane's node
 #pragma unroll
   for (int k = 0; k < KN; k++)
-    if (nk[k] == a.cm_node) {
+    if (nk[k] == K.cm_node) {
       const int n = nk[k];
 #pragma unroll
       for (int r = 0; r < KSG_MAX_RES; r++)
         if (r < c.R) {
-          L[k].req[r] += a.cm_req[r];
-          a.requested[(size_t)r * NN + n] = L[k].req[r];
+          L[k].req[r] += K.cm_req[r];
+          S.requested[(size_t)r * NN + n] = L[k].req[r];
         }
-      L[k].nz_cpu += a.cm_nz_cpu;
-      L[k].nz_mem += a.cm_nz_mem;
+      L[k].nz_cpu += K.cm_nz_cpu;
+      L[k].nz_mem += K.cm_nz_mem;
       L[k].pod_count += 1;
-      a.nonzero[n] = L[k].nz_cpu;
-      a.nonzero[NN + n] = L[k].nz_mem;
-      a.pod_count[n] = L[k].pod_count;
+      S.nonzero[n] = L[k].nz_cpu;
+      S.nonzero[NN + n] = L[k].nz_mem;
+      S.pod_count[n] = L[k].pod_count;
     }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS copies visible to the (single) wave
   KSG_YSTAMP(0);
 
   // ---- evaluate: every filter independently, then the first rejection in order ---------
-  const int32_t* P = s_blob;
   const int boff = p.blob;
   auto rb = [boff](int off) { return off < 0 ? -1 : off - boff; };
   const int32_t* tolf = P + rb(p.tol);
   const int32_t* tolp = tolf + c.W;
   const int na_req = rb(p.na_req), na_pref = rb(p.na_pref), img = rb(p.img), ports = rb(p.ports);
   const bool reject = (p.flags & KSG_POD_PREFILTER_REJECT) != 0;
-  const CmProf cm{a.cm_fast != 0, a.cm_least != 0, a.cm_wc, a.cm_wm, a.cm_inv_ws, a.cm_inv_wc, a.cm_inv_wm};
-  const uint32_t fm = a.fmask, sm = a.smask;
+  const bool has_nset = p.node_set >= 0;
+  const CmProf cm{K.cm_fast != 0, K.cm_least != 0, K.cm_wc, K.cm_wm, K.cm_inv_ws, K.cm_inv_wc, K.cm_inv_wm};
+  const uint32_t fm = K.fmask, sm = K.smask;
   uint32_t st[KN];
   int64_t part[KN], rt[KN], ra[KN], rf[KN], rbal[KN], rimg[KN];
 #pragma unroll
@@ -432,22 +454,22 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
     if (fm & bit(KSG_PL_NODE_AFFINITY))
       w[KSG_PL_NODE_AFFINITY] =
           na_required_match(x, P, na_req) ? 0 : (uint32_t)(KSG_PL_NODE_AFFINITY + 1) | (1u << 8);
-    if ((fm & bit(KSG_PL_NODE_PORTS)) && ports >= 0 && a.used_ports)
+    if ((fm & bit(KSG_PL_NODE_PORTS)) && ports >= 0 && S.used_ports)
       w[KSG_PL_NODE_PORTS] =
-          ports_conflict(a.used_ports, N, n < N ? n : N - 1, P + ports) ? KSG_PL_NODE_PORTS + 1 : 0;
+          ports_conflict(S.used_ports, N, n < N ? n : N - 1, P + ports) ? KSG_PL_NODE_PORTS + 1 : 0;
     if (fm & bit(KSG_PL_NODE_RESOURCES_FIT)) {
-      const uint32_t b = fit_filter(c, p, L[k], a.fit_ignored);
+      const uint32_t b = fit_filter(c, p, L[k], K.fit_ignored);
       w[KSG_PL_NODE_RESOURCES_FIT] = b ? (uint32_t)(KSG_PL_NODE_RESOURCES_FIT + 1) | (b << 8) : 0;
     }
     uint32_t s = 0;
-    for (int kf = 0; kf < a.n_filter && !s; kf++) {
-      const int pl = (int)((a.forder >> (4 * kf)) & 15u);
+    for (int kf = 0; kf < K.n_filter && !s; kf++) {
+      const int pl = (int)((K.forder >> (4 * kf)) & 15u);
       uint32_t v = 0;
 #pragma unroll
       for (int q = 0; q < KSG_NPLUGINS; q++) v = pl == q ? w[q] : v;
       s = v;
     }
-    if (reject || (nset && !((nsw[k] >> (n & 31)) & 1u))) s = KSG_FS_NOT_EVALUATED;
+    if (reject || (has_nset && !((nsw[k] >> (n & 31)) & 1u))) s = KSG_FS_NOT_EVALUATED;
     st[k] = n < N ? s : (uint32_t)KSG_FS_NOT_EVALUATED;
     // raw scores of a feasible node
     part[k] = rt[k] = ra[k] = rf[k] = rbal[k] = rimg[k] = 0;
@@ -456,8 +478,8 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
         if (cm.fast) {
           fit_ba_cm(cm, p, L[k], rf[k], rbal[k]);
         } else {
-          rf[k] = fit_score(*a.gprof, p, L[k]);
-          rbal[k] = ba_score(*a.gprof, p, L[k]);
+          rf[k] = fit_score(*K.gprof, p, L[k]);
+          rbal[k] = ba_score(*K.gprof, p, L[k]);
         }
         if (!(sm & bit(KSG_PL_NODE_RESOURCES_FIT))) rf[k] = 0;
         if (!(sm & bit(KSG_PL_BALANCED_ALLOCATION))) rbal[k] = 0;
@@ -465,7 +487,7 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
       if (sm & bit(KSG_PL_IMAGE_LOCALITY)) rimg[k] = pnode_image_score(x, c.I, P, img, p.n_containers);
       if (sm & bit(KSG_PL_TAINT_TOLERATION)) rt[k] = tscore;
       if (sm & bit(KSG_PL_NODE_AFFINITY)) ra[k] = na_pref_score(x, P, na_pref);
-      part[k] = rf[k] * a.w_fit + rbal[k] * a.w_ba + rimg[k] * a.w_img;
+      part[k] = rf[k] * K.w_fit + rbal[k] * K.w_ba + rimg[k] * K.w_img;
     }
   }
   KSG_YSTAMP(1);
@@ -485,18 +507,19 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
   ma = wreduce(ma, OpMaxI32{});
   lo = wreduce(lo, OpMaxI32{});
   if (lane == 0) {
-    CycPart* pp = a.parts + blockIdx.x;
+    CycPart* pp = S.parts + blockIdx.x;
     gst(&pp->nfeas, feas);
     gst(&pp->max_t, mt);
     gst(&pp->max_a, ma);
     gst(&pp->lo, lo);
   }
   KSG_YSTAMP(2);
-  const bool xok = cyc_exchange(a, G);
+  const unsigned seq = K.seq;
+  const bool xok = cyc_exchange(S, seq, G);
   KSG_YSTAMP(3);
   int32_t nfeas = 0, max_t = 0, max_a = 0, low = 0;
   for (int b = lane; b < G; b += 64) {
-    const CycPart* pp = a.parts + b;
+    const CycPart* pp = S.parts + b;
     nfeas += gld(&pp->nfeas);
     max_t = max(max_t, gld(&pp->max_t));
     max_a = max(max_a, gld(&pp->max_a));
@@ -509,12 +532,12 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
   KSG_YSTAMP(4);
 
   // ---- rows: every node of this workgroup, written once --------------------------------
-  const int es = a.es;
+  const int es = K.es;
   const bool scored = nfeas >= 2;   // fewer than two feasible nodes: no Score ran, nothing recorded
   PodView v{};                       // total_score's inputs
   v.smask = sm;
-  v.w_t = a.w_t;
-  v.w_a = a.w_a;
+  v.w_t = K.w_t;
+  v.w_a = K.w_a;
   uint64_t key = 0;
   uint32_t err = 0;
 #pragma unroll
@@ -528,9 +551,9 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
       const uint64_t kk = argmax_key(total, n);
       key = kk > key ? kk : key;
     }
-    hst<SYS>(a.h_fs + n, st[k]);
-    for (int q = 0; q < a.n_rows; q++) {
-      const int pl = (int)((a.rows >> (4 * q)) & 15u);
+    hst<SYS>(K.h_fs + n, st[k]);
+    for (int q = 0; q < K.n_rows; q++) {
+      const int pl = (int)((K.rows >> (4 * q)) & 15u);
       int64_t x = 0;
       if (scored && ok && ((sm >> pl) & 1u))
         x = pl == KSG_PL_NODE_RESOURCES_FIT     ? rf[k]
@@ -539,35 +562,165 @@ __global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
             : pl == KSG_PL_TAINT_TOLERATION    ? rt[k]
             : pl == KSG_PL_NODE_AFFINITY       ? ra[k]
                                                : 0;
-      cyc_put_es<SYS>(a.h_raw, (size_t)q * NN + n, x, es);
+      cyc_put_es<SYS>(K.h_raw, (size_t)q * NN + n, x, es);
     }
-    for (int q = 0; q < a.n_normrows; q++) {
-      const int pl = (int)((a.rows >> (4 * q)) & 15u);
-      cyc_put_es<SYS>(a.h_norm, (size_t)q * NN + n, pl == KSG_PL_TAINT_TOLERATION ? nt : na, es);
+    for (int q = 0; q < K.n_normrows; q++) {
+      const int pl = (int)((K.rows >> (4 * q)) & 15u);
+      cyc_put_es<SYS>(K.h_norm, (size_t)q * NN + n, pl == KSG_PL_TAINT_TOLERATION ? nt : na, es);
     }
-    cyc_put_es<SYS>(a.h_tot, n, total, es);
+    cyc_put_es<SYS>(K.h_tot, n, total, es);
   }
   key = wreduce(key, OpMaxU64{});
   err = wreduce(err, OpOr32{});
   // the workgroup's record beside its rows, then ONE release for all of them
   // and the done word behind it (round 4 released twice)
-  CycWg* w = a.h_wg + blockIdx.x;
+  CycWg* wr = K.h_wg + blockIdx.x;
   if (lane == 0) {
-    hst<SYS>(&w->key, (unsigned long long)key);
-    hst<SYS>(&w->err, err | (xok ? 0u : 2u));
+    hst<SYS>(&wr->key, (unsigned long long)key);
+    hst<SYS>(&wr->err, err | (xok ? 0u : 2u));
     if (blockIdx.x == 0) {   // the pod-wide statistics (every workgroup folded the same values)
-      hst<SYS>(a.h_stats + 0, nfeas);
-      hst<SYS>(a.h_stats + 1, max_t);
-      hst<SYS>(a.h_stats + 2, max_a);
-      hst<SYS>(a.h_stats + 3, low);
+      hst<SYS>(K.h_stats + 0, nfeas);
+      hst<SYS>(K.h_stats + 1, max_t);
+      hst<SYS>(K.h_stats + 2, max_a);
+      hst<SYS>(K.h_stats + 3, low);
     }
   }
   host_release<SYS>();
   KSG_YSTAMP(5);
-  if (lane == 0) __hip_atomic_store(&w->done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) __hip_atomic_store(&wr->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   KSG_YSTAMP(6);
+}
+
 #ifdef KSG_STAMPS
-  if (lane == 0 && blockIdx.x == 0 && a.stamps)
-    for (int i = 0; i < 7; i++) atomicAdd(&a.stamps[i], y_acc[i]);
+#define KSG_YSTAMP_ARGS , y_acc, y_last
+#else
+#define KSG_YSTAMP_ARGS
+#endif
+
+template <int KN, bool SYS>
+__global__ __launch_bounds__(64) void ksg_eval_cycle(CycArgs a) {
+  __shared__ int32_t s_blob[KSG_BLOB_MAX];
+  __shared__ uint8_t s_eff[kCycEff];
+  __shared__ uint32_t s_lab[KN][kCycLab][64];
+  const int lane = threadIdx.x;
+  const int G = (int)gridDim.x;
+#ifdef KSG_STAMPS
+  unsigned long long y_acc[8] = {}, y_last = __builtin_amdgcn_s_memtime();
+#endif
+  // ---- entry: argument lines, node columns, programs, all in flight together ----------
+  static_assert(offsetof(CycArgs, blob) <= 768 && sizeof(CycArgs) >= 768, "cyc_warm_args covers 12 lines");
+  cyc_warm_args();
+  const CycStatic& S = a.s;
+  const CycCall& K = a.k;
+  const int N = S.c.N;
+  const int blen = K.blob_len;
+  int nk[KN];
+  NodeCols L[KN];
+  PNode nd[KN];
+  uint32_t lv[KN][kCycLab];
+  uint32_t nsw[KN];
+  cyc_load_nodes<KN>(S, (K.smask >> KSG_PL_IMAGE_LOCALITY) & 1u, G, nk, L, nd, lv, s_lab);
+  const int32_t* nsrc = K.pod.node_set >= 0 ? K.gprog + K.pod.node_set : S.c.allowed;
+#pragma unroll
+  for (int k = 0; k < KN; k++) nsw[k] = (uint32_t)nsrc[(nk[k] < N ? nk[k] : N - 1) >> 5];
+  // the pod's programs into LDS (issued behind the columns)
+  const __attribute__((address_space(4))) char* kbase =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  if (blen <= kCycBlob) {
+    const __attribute__((address_space(4))) int32_t* kb =
+        (const __attribute__((address_space(4))) int32_t*)(kbase + offsetof(CycArgs, blob));
+    int32_t w[kCycBlob / 64];
+#pragma unroll
+    for (int u = 0; u < kCycBlob / 64; u++) w[u] = kb[lane + 64 * u];   // inside the arguments: unconditional
+#pragma unroll
+    for (int u = 0; u < kCycBlob / 64; u++)
+      if (lane + 64 * u < blen) s_blob[lane + 64 * u] = w[u];
+  } else {
+    for (int i = lane; i < blen; i += 64) s_blob[i] = K.bsrc[i];
+  }
+  cyc_stage_nodes<KN>(S, L, nd, lv, s_lab, s_eff);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS copies visible to the (single) wave
+  const int32_t* podw =
+      (const int32_t*)(const __attribute__((address_space(4))) int32_t*)(kbase + offsetof(CycArgs, k) +
+                                                                         offsetof(CycCall, pod));
+  cyc_serve<KN, SYS>(S, K, s_blob, podw, nk, L, nd, nsw, G KSG_YSTAMP_ARGS);
+#ifdef KSG_STAMPS
+  if (lane == 0 && blockIdx.x == 0 && S.stamps)
+    for (int i = 0; i < 7; i++) atomicAdd(&S.stamps[i], y_acc[i]);
+#endif
+}
+
+// System-scope load of host memory (the mailbox): around the GPU caches.
+template <class T>
+__device__ __forceinline__ T sys_ld(const T* p) {
+  return __hip_atomic_load((__attribute__((address_space(1))) T*)(const_cast<T*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The persistent form.  Every workgroup polls the mailbox's seq (lane 0, with
+// s_sleep), copies the call and the programs into LDS, serves it, and loops;
+// it leaves on op = 1 (stop), after kSrvIdle without a new call, or when an
+// exchange timed out (the host then finds the launch finished without its
+// done words and fails loudly).  Node columns stay in registers / LDS: only
+// this kernel changes them while it runs (the deferred assumes, written back).
+template <int KN, bool SYS>
+__global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
+  __shared__ int32_t s_blob[KSG_BLOB_MAX];
+  __shared__ uint8_t s_eff[kCycEff];
+  __shared__ uint32_t s_lab[KN][kCycLab][64];
+  __shared__ __attribute__((aligned(16))) CycCall s_k;
+  const int lane = threadIdx.x;
+  const int G = (int)gridDim.x;
+  const CycStatic& S = a.s;
+  const int N = S.c.N;
+  int nk[KN];
+  NodeCols L[KN];
+  PNode nd[KN];
+  uint32_t lv[KN][kCycLab];
+  uint32_t nsw[KN];
+  cyc_load_nodes<KN>(S, a.want_img != 0, G, nk, L, nd, lv, s_lab);
+  cyc_stage_nodes<KN>(S, L, nd, lv, s_lab, s_eff);
+  const SrvMailbox* mb = a.mb;
+  unsigned last = a.last;
+#ifdef KSG_STAMPS
+  unsigned long long y_acc[8] = {}, y_last = __builtin_amdgcn_s_memtime();
+#endif
+  for (;;) {
+    // ---- wait for the next call ----------------------------------------------------------
+    unsigned seq = last;
+    if (lane == 0) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        seq = sys_ld(&mb->seq);
+        if (seq != last) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kSrvIdle || gld(S.timeout)) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    seq = (unsigned)__builtin_amdgcn_readfirstlane((int)seq);
+    if (seq == last) break;   // idle or a timed-out exchange elsewhere: leave
+    // ---- the call and its programs into LDS ----------------------------------------------
+    constexpr int KW = (int)(sizeof(CycCall) / 4);
+    const int32_t* src = reinterpret_cast<const int32_t*>(&mb->k);
+    for (int i = lane; i < KW; i += 64) reinterpret_cast<int32_t*>(&s_k)[i] = sys_ld(src + i);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (s_k.op != 0) break;   // stop
+    const int blen = s_k.blob_len;
+    for (int i = lane; i < blen; i += 64) s_blob[i] = sys_ld(mb->blob + i);
+    const int32_t* nsrc = s_k.pod.node_set >= 0 ? s_k.gprog + s_k.pod.node_set : S.c.allowed;
+#pragma unroll
+    for (int k = 0; k < KN; k++) nsw[k] = (uint32_t)nsrc[(nk[k] < N ? nk[k] : N - 1) >> 5];
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#ifdef KSG_STAMPS
+    y_last = __builtin_amdgcn_s_memtime();
+#endif
+    cyc_serve<KN, SYS>(S, s_k, s_blob, reinterpret_cast<const int32_t*>(&s_k.pod), nk, L, nd, nsw,
+                       G KSG_YSTAMP_ARGS);
+    last = seq;
+    if (gld(S.timeout)) break;   // an exchange gave up: every workgroup leaves
+  }
+#ifdef KSG_STAMPS
+  if (lane == 0 && blockIdx.x == 0 && S.stamps)
+    for (int i = 0; i < 7; i++) atomicAdd(&S.stamps[i], y_acc[i]);
 #endif
 }

@@ -72,6 +72,52 @@ def test_eval_cycle_nodes_per_lane(oracle, monkeypatch, kn, name):
         eng.close()
 
 
+@pytest.mark.parametrize("name", ["c2-1000x120", "c1-100x150", "c5-small", "c5-vocab8k", "zoo-0", "zoo-3",
+                                  "readme-kat2"])
+def test_eval_cycle_server_matches_oracle(oracle, monkeypatch, name):
+    """The persistent per-cycle server (KSG_CYCLE_SERVER=1: node columns held
+    in registers across cycles, calls through the pinned mailbox) equals the
+    oracle pod by pod, deferred assumes included; read_state at the end stops
+    it, so the state it wrote back is what the oracle holds."""
+    monkeypatch.setenv("KSG_CYCLE_SERVER", "1")
+    eng = native.Engine(device=0)
+    try:
+        _check_cycles(eng, oracle, name, *CASES[name]())
+    finally:
+        eng.close()
+
+
+def test_eval_cycle_server_interleaved_with_queue_runs(oracle, monkeypatch):
+    """Calls that need the stream (a queue run, a non-deferrable assume, a
+    reload) stop the server and the next evaluation starts it again, reading
+    the node state those calls left."""
+    monkeypatch.setenv("KSG_CYCLE_SERVER", "1")
+    nodes, pods, prof = G.config2(n_nodes=700, n_pods=90, seed=21)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    eng = native.Engine(device=0)
+    try:
+        eng.load(enc, pf)
+        oracle.load(enc, pf)
+        for lo, hi, how in ((0, 30, "eval"), (30, 50, "queue"), (50, 70, "eval"), (70, 75, "queue"), (75, 90, "eval")):
+            if how == "queue":
+                pg, _ = eng.run_queue(lo, hi - lo, results=False)
+                po, _ = oracle.run_queue(lo, hi - lo, results=False)
+                np.testing.assert_array_equal(pg, po)
+                continue
+            for i in range(lo, hi):
+                rg, ro = eng.eval(i), oracle.eval(i)
+                assert (rg.selected, rg.n_feasible, rg.status) == (ro.selected, ro.n_feasible, ro.status), i
+                if rg.selected >= 0:
+                    eng.commit(i, rg.selected)
+                    oracle.commit(i, ro.selected)
+        R = len(enc.cluster.res_names)
+        for a, b in zip(eng.read_state(R), oracle.read_state(R)):
+            np.testing.assert_array_equal(a, b)
+    finally:
+        eng.close()
+
+
 def _check_cycles(gpu, oracle, name, nodes, pods, prof):
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)

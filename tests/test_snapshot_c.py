@@ -17,8 +17,9 @@ BIN = os.path.join(HERE, "c", "snapshot_c_test")
 EXPORT_PROFILE = os.path.join(HERE, "golden", "export_profile.txt")
 
 
-def _run(flag):
-    r = subprocess.run([BIN, flag, EXPORT_PROFILE], capture_output=True, text=True, timeout=300)
+def _run(flag, env=None):
+    r = subprocess.run([BIN, flag, EXPORT_PROFILE], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, **(env or {})))
     print(r.stdout)
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -32,3 +33,9 @@ def test_c_boundary_cpu(built):
 @pytest.mark.gpu
 def test_c_boundary_gpu(built):
     _run("--gpu")
+
+
+@pytest.mark.gpu
+def test_c_boundary_gpu_cycle_server(built):
+    """The same C-only cycles with the persistent per-cycle server."""
+    _run("--gpu", {"KSG_CYCLE_SERVER": "1"})
