@@ -202,10 +202,12 @@ struct ksg_ctx {
   bool srv_img = false, srv_sys = false;
   CycStatic srv_static{};
   SrvMailbox* h_mb = nullptr;               // pinned host mailbox
+  char* d_srv = nullptr;                    // the server's device relay of the call (dalloc: freed with the context)
   const SrvMailbox* d_mb = nullptr;
   std::chrono::steady_clock::time_point srv_last{};
   int cycle_kn = 1;                         // env KSG_CYCLE_KN (1/2/4): the smallest nodes-per-lane tried (tests)
-  bool cycle_sys = false;                   // env KSG_CYCLE_SYS=1: system-scope host stores (no L2 write-back)
+  bool cycle_sys = true;                    // system-scope host stores + a vmcnt wait (no L2 write-back); env
+                                            // KSG_CYCLE_SYS=0: plain stores + __threadfence_system (round 4)
   int cycle_es = 0;                         // env KSG_CYCLE_ES=2/4/8: force the row width (measurements)
   bool cycle_coop = false;                  // per-cycle launch: plain (G within the occupancy API's residency,
                                             // ~7 us less host time); cooperative after an exchange timeout,
@@ -330,6 +332,7 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_ev_prof = nullptr;
   ctx->d_ev_pl = nullptr;
   ctx->ev_prof_dirty = true;
+  ctx->d_srv = nullptr;   // (the server was stopped before anything freed)
 }
 
 // ---- per-kernel timing -------------------------------------------------------
@@ -1998,9 +2001,16 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_mb, 0));
       ctx->d_mb = static_cast<const SrvMailbox*>(dp);
     }
+    if (!ctx->d_srv) {   // the relay: call | programs | go word (zeroed: no sequence number is 0)
+      if ((rc = dalloc(ctx, &ctx->d_srv, sizeof(CycCall) + sizeof(int32_t) * KSG_BLOB_MAX + 128))) return rc;
+      HIPC(ctx, hipMemsetAsync(ctx->d_srv, 0, sizeof(CycCall) + sizeof(int32_t) * KSG_BLOB_MAX + 128, ctx->stream));
+    }
     SrvArgs sa{};
     sa.s = cs;
     sa.mb = ctx->d_mb;
+    sa.d_call = reinterpret_cast<CycCall*>(ctx->d_srv);
+    sa.d_blob = reinterpret_cast<int32_t*>(ctx->d_srv + sizeof(CycCall));
+    sa.d_go = reinterpret_cast<unsigned*>(ctx->d_srv + sizeof(CycCall) + sizeof(int32_t) * KSG_BLOB_MAX);
     sa.last = __atomic_load_n(&ctx->h_mb->seq, __ATOMIC_ACQUIRE);
     sa.want_img = want_img;
     void* sargs[] = {&sa};

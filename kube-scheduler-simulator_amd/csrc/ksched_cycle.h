@@ -143,6 +143,9 @@ struct SrvMailbox {
 struct SrvArgs {
   CycStatic s;
   const SrvMailbox* mb;              // device address of the mailbox
+  CycCall* d_call;                   // device copy of the current call (workgroup 0 relays it) ...
+  int32_t* d_blob;                   // ... and of its programs
+  unsigned* d_go;                    // 128-byte line: the relayed call's sequence number
   unsigned last;                     // the last sequence number served before this launch
   int32_t want_img;                  // the profile scores ImageLocality: keep the image slots
 };
@@ -657,10 +660,14 @@ __device__ __forceinline__ T sys_ld(const T* p) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The persistent form.  Every workgroup polls the mailbox's seq (lane 0, with
-// s_sleep), copies the call and the programs into LDS, serves it, and loops;
-// it leaves on op = 1 (stop), after kSrvIdle without a new call, or when an
-// exchange timed out (the host then finds the launch finished without its
+// The persistent form.  Workgroup 0 alone polls the host mailbox (lane 0,
+// one PCIe read in flight at a time), reads the call and its programs, and
+// relays them into device memory behind a go word (agent-scope stores); the
+// other workgroups poll the go word and read the relayed copy, so PCIe carries
+// one poll and one call per cycle (every workgroup polling the host line
+// measured 59 us per call: the host side of the cycle slowed down too).  A
+// workgroup leaves on op = 1 (stop), after kSrvIdle without a new call, or when
+// an exchange timed out (the host then finds the launch finished without its
 // done words and fails loudly).  Node columns stay in registers / LDS: only
 // this kernel changes them while it runs (the deferred assumes, written back).
 template <int KN, bool SYS>
@@ -673,6 +680,7 @@ __global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
   const int G = (int)gridDim.x;
   const CycStatic& S = a.s;
   const int N = S.c.N;
+  const bool relay = blockIdx.x == 0;
   int nk[KN];
   NodeCols L[KN];
   PNode nd[KN];
@@ -685,28 +693,48 @@ __global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
 #ifdef KSG_STAMPS
   unsigned long long y_acc[8] = {}, y_last = __builtin_amdgcn_s_memtime();
 #endif
+  constexpr int KW = (int)(sizeof(CycCall) / 4);
   for (;;) {
-    // ---- wait for the next call ----------------------------------------------------------
+    // ---- wait for the next call: the host line (workgroup 0) or the go word -------------
     unsigned seq = last;
     if (lane == 0) {
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
-        seq = sys_ld(&mb->seq);
+        seq = relay ? sys_ld(&mb->seq) : gld(a.d_go);
         if (seq != last) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kSrvIdle || gld(S.timeout)) break;
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       }
     }
     seq = (unsigned)__builtin_amdgcn_readfirstlane((int)seq);
     if (seq == last) break;   // idle or a timed-out exchange elsewhere: leave
-    // ---- the call and its programs into LDS ----------------------------------------------
-    constexpr int KW = (int)(sizeof(CycCall) / 4);
-    const int32_t* src = reinterpret_cast<const int32_t*>(&mb->k);
-    for (int i = lane; i < KW; i += 64) reinterpret_cast<int32_t*>(&s_k)[i] = sys_ld(src + i);
+    // ---- the call and its programs into LDS (workgroup 0: from the host, relayed) -------
+    if (relay) {
+      const int32_t* src = reinterpret_cast<const int32_t*>(&mb->k);
+      int32_t* dst = reinterpret_cast<int32_t*>(a.d_call);
+      for (int i = lane; i < KW; i += 64) {
+        const int32_t x = sys_ld(src + i);
+        reinterpret_cast<int32_t*>(&s_k)[i] = x;
+        gst(dst + i, x);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const int blen = s_k.op != 0 ? 0 : s_k.blob_len;
+      for (int i = lane; i < blen; i += 64) {
+        const int32_t x = sys_ld(mb->blob + i);
+        s_blob[i] = x;
+        gst(a.d_blob + i, x);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the relayed words are stored ...
+      if (lane == 0) gst(a.d_go, seq);                     // ... before the go word
+    } else {
+      const int32_t* src = reinterpret_cast<const int32_t*>(a.d_call);
+      for (int i = lane; i < KW; i += 64) reinterpret_cast<int32_t*>(&s_k)[i] = gld(src + i);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const int blen = s_k.op != 0 ? 0 : s_k.blob_len;
+      for (int i = lane; i < blen; i += 64) s_blob[i] = gld(a.d_blob + i);
+    }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if (s_k.op != 0) break;   // stop
-    const int blen = s_k.blob_len;
-    for (int i = lane; i < blen; i += 64) s_blob[i] = sys_ld(mb->blob + i);
     const int32_t* nsrc = s_k.pod.node_set >= 0 ? s_k.gprog + s_k.pod.node_set : S.c.allowed;
 #pragma unroll
     for (int k = 0; k < KN; k++) nsw[k] = (uint32_t)nsrc[(nk[k] < N ? nk[k] : N - 1) >> 5];

@@ -1,8 +1,10 @@
-"""Golden vector for the ≥30,000-pod configs[2] parity case (VERDICT r3 item
-4): the C++ oracle's placements and per-pod results for generator.config3 at
-15,000 nodes x 30,000 pods (seed 3), saved as tests/golden/c3_15000x30000.npz.
-The oracle takes minutes at this size, so the GPU test compares against this
-file instead of re-running it.  Regenerate: python tests/golden/make_c3_large.py [threads]"""
+"""Golden vectors for the large configs[2] parity cases (VERDICT r3 item 4,
+r4 item 4): the C++ oracle's placements and per-pod results for
+generator.config3 at 15,000 nodes x P pods (seed 3), saved as
+tests/golden/c3_15000x<P>.npz (P = 30,000, and the full 150,000-pod queue).
+The oracle takes minutes to hours at these sizes, so the GPU tests compare
+against these files instead of re-running it.
+Regenerate: python tests/golden/make_c3_large.py [threads] [pods]"""
 import os
 import sys
 import time
@@ -19,19 +21,25 @@ G = importlib.import_module("kube-scheduler-simulator_amd.generator")
 E = importlib.import_module("kube-scheduler-simulator_amd.encoder")
 import binding  # noqa: E402
 
-N_NODES, N_PODS = 15000, 30000
+N_NODES = 15000
 
 
 def main():
     threads = int(sys.argv[1]) if len(sys.argv) > 1 else os.cpu_count()
+    N_PODS = int(sys.argv[2]) if len(sys.argv) > 2 else 30000
     t = time.time()
     nodes, pods, prof = G.config3(n_nodes=N_NODES, n_pods=N_PODS)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
     o = binding.Oracle(threads)
     o.load(enc, pf)
-    pl, res = o.run_queue(0, N_PODS)
-    np.savez_compressed(os.path.join(HERE, "c3_15000x30000.npz"), placements=np.asarray(pl, np.int32),
+    chunks, step = [], 2000
+    for lo in range(0, N_PODS, step):   # in chunks, with progress (the full queue runs for a long time)
+        chunks.append(o.run_queue(lo, min(step, N_PODS - lo)))
+        print(f"  {lo + len(chunks[-1][0])} pods, {time.time() - t:.0f} s", flush=True)
+    pl = np.concatenate([c[0] for c in chunks])
+    res = {k: np.concatenate([np.asarray(c[1][k]) for c in chunks]) for k in ("n_feasible", "status", "score_skip")}
+    np.savez_compressed(os.path.join(HERE, f"c3_15000x{N_PODS}.npz"), placements=np.asarray(pl, np.int32),
                         n_feasible=np.asarray(res["n_feasible"], np.int32),
                         status=np.asarray(res["status"], np.uint32),
                         score_skip=np.asarray(res["score_skip"], np.uint32),
