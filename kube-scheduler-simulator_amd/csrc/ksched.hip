@@ -194,6 +194,7 @@ struct ksg_ctx {
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
   int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
   CycArgs cyc_args{};                       // ksg_eval_cycle's launch arguments, rebuilt in place per call
+  unsigned cyc_last_G = 0;                  // the grid of the last per-cycle call (its counter counts multiples of it)
   // the persistent per-cycle server (env KSG_CYCLE_SERVER=1, ksched_cycle.h ksg_cycle_server)
   bool srv_mode = false;
   bool srv_running = false;
@@ -1911,13 +1912,16 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   }
   const unsigned G = (unsigned)((N + 64 * kn - 1) / (64 * kn));
   const size_t Gm = (N + 63) / 64;   // the largest grid (KN = 1): no reallocation on a KN change
-  // host block: stats[4] | pad | per-workgroup {key, err, done}[Gm] | fstatus[N] | raw[n_rows][N] | total[N] |
+  // host block: result line (stats[4], best key, error bits, done) | pad | fstatus[N] | raw[n_rows][N] | total[N] |
   // norm[n_normrows][N]
-  const size_t o_wg = 32, o_fs = o_wg + sizeof(CycWg) * Gm, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
+  const size_t o_fs = 64, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
   const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
   const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
-  // device block: parts[Gm] | flags[Gm][32] | timeout
-  const size_t d_flags = sizeof(CycPart) * Gm, d_to = d_flags + 128 * Gm, d_need = d_to + 128;
+  // device block: parts[Gm] | flags[Gm][32] | timeout | completion counter | key slot, error slot
+  const size_t d_flags = sizeof(CycPart) * Gm, d_to = d_flags + 128 * Gm, d_arr = d_to + 128, d_key = d_arr + 128;
+  const size_t d_need = d_key + 128;
+  if (G != ctx->cyc_last_G) ctx->ev_clean = false;   // the counter counts in multiples of G
+  ctx->cyc_last_G = G;
   if (d_need > ctx->ev_bytes || h_need > ctx->h_ev_bytes || !ctx->ev_clean || ctx->ev_prof_dirty || !ctx->d_ev_prof)
     if ((rc = srv_stop(ctx))) return rc;   // stream work ahead: a running server leaves first
   if (d_need > ctx->ev_bytes) {
@@ -1976,6 +1980,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   cs.parts = reinterpret_cast<CycPart*>(ctx->d_ev);
   cs.flags = reinterpret_cast<unsigned*>(ctx->d_ev + d_flags);
   cs.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_to);
+  cs.arrive = reinterpret_cast<unsigned*>(ctx->d_ev + d_arr);
+  cs.key = reinterpret_cast<unsigned long long*>(ctx->d_ev + d_key);
+  cs.errw = reinterpret_cast<unsigned*>(ctx->d_ev + d_key + 16);
   cs.stamps = nullptr;
 #ifdef KSG_STAMPS
   if (!ctx->d_stamps) {
@@ -2085,7 +2092,6 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   ck.h_tot = db + o_tot;
   ck.h_norm = db + o_norm;
   ck.h_stats = reinterpret_cast<int32_t*>(db);
-  ck.h_wg = reinterpret_cast<CycWg*>(db + o_wg);
   ck.seq = seq;
   ck.op = 0;
   // the pod's programs: inline (kernel arguments or mailbox, from the host
@@ -2137,22 +2143,19 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   // launch) before its workgroups stored their done words, which this call
   // waits for, so the staging buffer is free when it returns (no event)
   if (staged) ctx->stage_pending = false;
-  // every workgroup stores seq into its record after its rows: spin on them,
-  // checking the stream now and then (a failed launch never stores them)
-  const CycWg* wgr = reinterpret_cast<const CycWg*>(hb + o_wg);
-  for (unsigned g = 0, spins = 0; g < G; spins++) {
-    if (reinterpret_cast<const volatile CycWg*>(wgr)[g].done == seq) {
-      g++;
-      continue;
-    }
+  // the last workgroup stores the result line and then seq into its done word
+  // (after every workgroup's rows): spin on it, checking the stream now and
+  // then (a failed launch never stores it)
+  const volatile int32_t* line = reinterpret_cast<const volatile int32_t*>(hb);
+  for (unsigned spins = 0; (unsigned)line[7] != seq; spins++) {
     __builtin_ia32_pause();
     if ((spins & 1023) == 1023) {
       const hipError_t e = hipStreamQuery(ctx->stream);
-      if (e == hipSuccess && reinterpret_cast<const volatile CycWg*>(wgr)[g].done != seq) {
+      if (e == hipSuccess && (unsigned)line[7] != seq) {
         ctx->ev_clean = false;
         ctx->srv_running = false;
         return fail(ctx, KSG_E_DEVICE, server ? "per-cycle server: left without serving the call"
-                                              : "per-cycle evaluation: kernel finished without its completion words");
+                                              : "per-cycle evaluation: kernel finished without its completion word");
       }
       if (e != hipSuccess && e != hipErrorNotReady)
         return fail(ctx, KSG_E_DEVICE, std::string("per-cycle evaluation: ") + hipGetErrorString(e));
@@ -2162,12 +2165,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   if ((rc = tcollect(ctx))) return rc;
   const int32_t* st = reinterpret_cast<const int32_t*>(hb);
   const int32_t nfeas = st[0];
-  unsigned long long best = 0;
-  uint32_t herr = 0;
-  for (unsigned g = 0; g < G; g++) {   // selectHost over the workgroups' keys
-    best = wgr[g].key > best ? wgr[g].key : best;
-    herr |= wgr[g].err;
-  }
+  unsigned long long best;
+  std::memcpy(&best, st + 4, 8);
+  const uint32_t herr = (uint32_t)st[6];
   if (server) ctx->srv_last = std::chrono::steady_clock::now();
   if (herr & 2u) {
     ctx->ev_clean = false;   // clears the sticky timeout word before the next call

@@ -34,9 +34,11 @@
 //              call's sequence number (agent-scope stores and loads, no reset
 //              between calls); every workgroup folds the G slots.
 //   rows       status words, raw, normalised and total rows (2, 4 or 8 bytes)
-//              and the workgroup's selectHost key and error bits with plain
-//              stores to the host block (SYS: system-scope stores), one
-//              system-scope release, then the done word.
+//              to the host block (SYS, the default: system-scope stores and a
+//              vmcnt wait; else plain stores and __threadfence_system); the
+//              selectHost keys and error bits fold into device slots by
+//              atomics, and the last workgroup to arrive stores the result
+//              line and its done word: the host polls one word.
 //
 // ksg_cycle_server<KN, SYS> is the same evaluation as a persistent kernel
 // (KSG_CYCLE_SERVER=1): the node columns are loaded once and stay in
@@ -67,11 +69,6 @@ constexpr unsigned long long kSrvIdle = 1000000000ull;   // server: 10 s of the 
 struct CycPart {   // one workgroup's phase-1 statistics
   int32_t nfeas, max_t, max_a, lo;   // lo = max over its feasible nodes of N - n
 };
-struct CycWg {     // one workgroup's record in the host block
-  unsigned long long key;   // its selectHost key (0: no feasible node)
-  uint32_t err;             // bit 0: a normalised score left [0, 100]; bit 1: the exchange timed out
-  uint32_t done;            // = seq once every row of the workgroup and the two words above are written
-};
 
 // What does not change between calls on a loaded context.
 struct CycStatic {
@@ -83,6 +80,9 @@ struct CycStatic {
   CycPart* parts;                    // [G]
   unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
   unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
+  unsigned* arrive;                  // completion counter (monotonic; a multiple of G between calls)
+  unsigned long long* key;           // the running call's best selectHost key (zero between calls)
+  unsigned* errw;                    // its error bits (zero between calls)
   unsigned long long* stamps;        // KSG_STAMPS builds: per-segment cycle sums of workgroup 0
 };
 
@@ -114,8 +114,8 @@ struct CycCall {
   char* h_raw;                       // [n_rows][N]
   char* h_tot;                       // [N]
   char* h_norm;                      // [n_normrows][N]
-  int32_t* h_stats;                  // [4] nfeas, max taint, max node affinity, max (N - n) (workgroup 0)
-  CycWg* h_wg;                       // [G]
+  int32_t* h_stats;                  // [8] nfeas, max taint, max node affinity, max (N - n), best key (2 words),
+                                     // error bits, done (= seq; stored last, by the last workgroup)
   unsigned seq;
   int32_t op;                        // server mailbox: 0 evaluate, 1 stop
   const int32_t* bsrc;               // the programs when they are not inline
@@ -575,22 +575,44 @@ __device__ __forceinline__ void cyc_serve(const CycStatic& S, const CycCall& K, 
   }
   key = wreduce(key, OpMaxU64{});
   err = wreduce(err, OpOr32{});
-  // the workgroup's record beside its rows, then ONE release for all of them
-  // and the done word behind it (round 4 released twice)
-  CycWg* wr = K.h_wg + blockIdx.x;
+  // Completion: one word for the host.  Every workgroup folds its selectHost
+  // key and error bits into this call's slot with agent-scope atomics, waits
+  // for its host rows (system-scope stores: vmcnt(0) means performed), and
+  // arrives on a counter; the last to arrive reads the slots and stores the
+  // result line (statistics, best key, error bits) and then its done word,
+  // taking the slots' values with exchanges that leave them zero for the next
+  // call (which starts only after the host has seen this one's done word, so
+  // the sequence numbers need not be consecutive).
+  // (Round 4: one record per workgroup, which the host polled one by one.)
+  unsigned long long* kslot = S.key;
   if (lane == 0) {
-    hst<SYS>(&wr->key, (unsigned long long)key);
-    hst<SYS>(&wr->err, err | (xok ? 0u : 2u));
-    if (blockIdx.x == 0) {   // the pod-wide statistics (every workgroup folded the same values)
-      hst<SYS>(K.h_stats + 0, nfeas);
-      hst<SYS>(K.h_stats + 1, max_t);
-      hst<SYS>(K.h_stats + 2, max_a);
-      hst<SYS>(K.h_stats + 3, low);
+    __hip_atomic_fetch_max((__attribute__((address_space(1))) unsigned long long*)kslot, (unsigned long long)key,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (err | (xok ? 0u : 2u))
+      __hip_atomic_fetch_or((__attribute__((address_space(1))) unsigned*)(S.errw), err | (xok ? 0u : 2u),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  host_release<SYS>();   // this wave's rows and atomics are performed
+  KSG_YSTAMP(5);
+  if (lane == 0) {
+    const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)S.arrive, 1u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((old + 1) % (unsigned)G == 0) {   // the last workgroup of this call
+      const unsigned long long best = __hip_atomic_exchange(
+          (__attribute__((address_space(1))) unsigned long long*)kslot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned e = __hip_atomic_exchange((__attribute__((address_space(1))) unsigned*)S.errw, 0u,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int32_t* h = K.h_stats;
+      hst<SYS>(h + 0, nfeas);
+      hst<SYS>(h + 1, max_t);
+      hst<SYS>(h + 2, max_a);
+      hst<SYS>(h + 3, low);
+      hst<SYS>(reinterpret_cast<unsigned long long*>(h + 4), best);
+      hst<SYS>(reinterpret_cast<uint32_t*>(h + 6), e);
+      host_release<SYS>();
+      __hip_atomic_store(reinterpret_cast<unsigned*>(h + 7), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-  host_release<SYS>();
-  KSG_YSTAMP(5);
-  if (lane == 0) __hip_atomic_store(&wr->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   KSG_YSTAMP(6);
 }
 
