@@ -1917,8 +1917,8 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   const size_t o_fs = 64, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
   const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
   const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
-  // device block: parts[Gm] | flags[Gm][32] | timeout | completion counter | key slot, error slot
-  const size_t d_flags = sizeof(CycPart) * Gm, d_to = d_flags + 128 * Gm, d_arr = d_to + 128, d_key = d_arr + 128;
+  // device block: exchange lines [Gm][32] | timeout | completion counter | key slot, error slot
+  const size_t d_flags = 0, d_to = d_flags + 128 * Gm, d_arr = d_to + 128, d_key = d_arr + 128;
   const size_t d_need = d_key + 128;
   if (G != ctx->cyc_last_G) ctx->ev_clean = false;   // the counter counts in multiples of G
   ctx->cyc_last_G = G;
@@ -1977,7 +1977,6 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   cs.nonzero = ctx->st.nonzero;
   cs.pod_count = ctx->st.pod_count;
   cs.used_ports = ctx->st.ports;
-  cs.parts = reinterpret_cast<CycPart*>(ctx->d_ev);
   cs.flags = reinterpret_cast<unsigned*>(ctx->d_ev + d_flags);
   cs.timeout = reinterpret_cast<unsigned*>(ctx->d_ev + d_to);
   cs.arrive = reinterpret_cast<unsigned*>(ctx->d_ev + d_arr);

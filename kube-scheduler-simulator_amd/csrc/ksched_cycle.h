@@ -66,10 +66,6 @@ constexpr int kCycMaxKN = 4;     // nodes per lane
 constexpr unsigned long long kSrvIdle = 1000000000ull;   // server: 10 s of the 100 MHz real-time clock
                                                         // (the host restarts a server idle for 0.25 s)
 
-struct CycPart {   // one workgroup's phase-1 statistics
-  int32_t nfeas, max_t, max_a, lo;   // lo = max over its feasible nodes of N - n
-};
-
 // What does not change between calls on a loaded context.
 struct CycStatic {
   DevCluster c;
@@ -77,8 +73,7 @@ struct CycStatic {
   int64_t* nonzero;
   int32_t* pod_count;
   const uint32_t* used_ports;
-  CycPart* parts;                    // [G]
-  unsigned* flags;                   // [G][32]: workgroup g's exchange flag at [g * 32]
+  unsigned* flags;                   // [G][32]: workgroup g's exchange line (cyc_arrive) at [g * 32]
   unsigned* timeout;                 // sticky: an exchange poll gave up (reported to the host)
   unsigned* arrive;                  // completion counter (monotonic; a multiple of G between calls)
   unsigned long long* key;           // the running call's best selectHost key (zero between calls)
@@ -288,22 +283,53 @@ __device__ __forceinline__ void cyc_warm_args() {
       : "memory");
 }
 
-// Grid exchange of a one-wave workgroup: its flag line gets `seq`, then the
-// wave polls every flag until all hold `seq` (bounded; a timeout is sticky and
-// reported).
-__device__ __forceinline__ bool cyc_exchange(const CycStatic& S, unsigned seq, int G) {
+// Grid exchange of a one-wave workgroup, in two halves.  cyc_arrive stores
+// its statistics (feasible count, the taint / affinity raw maxima, lo) into
+// its flag line as four words each tagged with `seq` in the high half (an
+// aligned 8-byte store is single-copy atomic, so a word holding `seq` holds
+// this call's value); cyc_await polls every line until all words hold `seq`
+// (bounded; a timeout is sticky and reported) and folds them as it reads.
+// Work issued between the two (the host rows) overlaps the wait.
+// (Until round 5 the statistics went to a slot array read after the flags:
+// one more dependent load round trip.)
+__device__ __forceinline__ void cyc_arrive(const CycStatic& S, unsigned seq, const int32_t (&v)[4]) {
   const int lane = threadIdx.x;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // its agent-scope slot stores are done
-  if (lane == 0) gst(&S.flags[(size_t)blockIdx.x * 32], seq);
+  const uint32_t x = lane == 0 ? (uint32_t)v[0] : lane == 1 ? (uint32_t)v[1] : lane == 2 ? (uint32_t)v[2] : (uint32_t)v[3];
+  if (lane < 4)
+    gst(reinterpret_cast<unsigned long long*>(S.flags + (size_t)blockIdx.x * 32) + lane,
+        ((unsigned long long)seq << 32) | x);
+}
+
+// v: [0] summed, [1..3] max (all non-negative), over every workgroup
+__device__ __forceinline__ bool cyc_await(const CycStatic& S, unsigned seq, int G, int32_t (&v)[4]) {
+  const int lane = threadIdx.x;
   unsigned spins = 0;
   for (;;) {
     bool ok = true;
-    for (int l = lane; l < G; l += 64) ok = ok && gld(&S.flags[(size_t)l * 32]) == seq;
-    if (__all(ok)) return true;
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 22) || gld(S.timeout)) {
-      if (lane == 0) gst(S.timeout, 1u);
-      return false;
+    int32_t a = 0, b = 0, c = 0, d = 0;
+    for (int l = lane; l < G; l += 64) {
+      const unsigned long long* f = reinterpret_cast<const unsigned long long*>(S.flags + (size_t)l * 32);
+      const unsigned long long w0 = gld(f), w1 = gld(f + 1), w2 = gld(f + 2), w3 = gld(f + 3);
+      ok = ok && (unsigned)(w0 >> 32) == seq && (unsigned)(w1 >> 32) == seq && (unsigned)(w2 >> 32) == seq &&
+           (unsigned)(w3 >> 32) == seq;
+      a += (int32_t)(uint32_t)w0;
+      b = max(b, (int32_t)(uint32_t)w1);
+      c = max(c, (int32_t)(uint32_t)w2);
+      d = max(d, (int32_t)(uint32_t)w3);
+    }
+    const bool done = __all(ok);
+    bool give_up = false;
+    if (!done) {
+      __builtin_amdgcn_s_sleep(1);
+      give_up = ++spins > (1u << 22) || gld(S.timeout);
+      if (give_up && lane == 0) gst(S.timeout, 1u);
+    }
+    if (done || give_up) {
+      v[0] = (int32_t)wreduce((uint32_t)a, OpAdd32{});
+      v[1] = wreduce(b, OpMaxI32{});
+      v[2] = wreduce(c, OpMaxI32{});
+      v[3] = wreduce(d, OpMaxI32{});
+      return done;
     }
   }
 }
@@ -505,37 +531,44 @@ __device__ __forceinline__ void cyc_serve(const CycStatic& S, const CycCall& K, 
       ma = max(ma, (int32_t)ra[k]);
       lo = max(lo, N - nk[k]);
     }
-  feas = (int32_t)wreduce((uint32_t)feas, OpAdd32{});
-  mt = wreduce(mt, OpMaxI32{});
-  ma = wreduce(ma, OpMaxI32{});
-  lo = wreduce(lo, OpMaxI32{});
-  if (lane == 0) {
-    CycPart* pp = S.parts + blockIdx.x;
-    gst(&pp->nfeas, feas);
-    gst(&pp->max_t, mt);
-    gst(&pp->max_a, ma);
-    gst(&pp->lo, lo);
+  {
+    const int32_t mine[4] = {(int32_t)wreduce((uint32_t)feas, OpAdd32{}), wreduce(mt, OpMaxI32{}),
+                             wreduce(ma, OpMaxI32{}), wreduce(lo, OpMaxI32{})};
+    cyc_arrive(S, K.seq, mine);
+  }
+  const unsigned seq = K.seq;
+  // ---- the rows that need no global fact, while the other workgroups arrive:
+  // filter statuses and raw scores (as if Score runs; a call with fewer than
+  // two feasible nodes, where it does not, zeroes its one feasible node's raw
+  // values after the exchange)
+  const int es = K.es;
+#pragma unroll
+  for (int k = 0; k < KN; k++) {
+    const int n = nk[k];
+    if (n >= N) continue;
+    const bool ok = st[k] == 0;
+    hst<SYS>(K.h_fs + n, st[k]);
+    for (int q = 0; q < K.n_rows; q++) {
+      const int pl = (int)((K.rows >> (4 * q)) & 15u);
+      int64_t x = 0;
+      if (ok && ((sm >> pl) & 1u))
+        x = pl == KSG_PL_NODE_RESOURCES_FIT     ? rf[k]
+            : pl == KSG_PL_BALANCED_ALLOCATION ? rbal[k]
+            : pl == KSG_PL_IMAGE_LOCALITY      ? rimg[k]
+            : pl == KSG_PL_TAINT_TOLERATION    ? rt[k]
+            : pl == KSG_PL_NODE_AFFINITY       ? ra[k]
+                                               : 0;
+      cyc_put_es<SYS>(K.h_raw, (size_t)q * NN + n, x, es);
+    }
   }
   KSG_YSTAMP(2);
-  const unsigned seq = K.seq;
-  const bool xok = cyc_exchange(S, seq, G);
+  int32_t gs[4];
+  const bool xok = cyc_await(S, seq, G, gs);
   KSG_YSTAMP(3);
-  int32_t nfeas = 0, max_t = 0, max_a = 0, low = 0;
-  for (int b = lane; b < G; b += 64) {
-    const CycPart* pp = S.parts + b;
-    nfeas += gld(&pp->nfeas);
-    max_t = max(max_t, gld(&pp->max_t));
-    max_a = max(max_a, gld(&pp->max_a));
-    low = max(low, gld(&pp->lo));
-  }
-  nfeas = (int32_t)wreduce((uint32_t)nfeas, OpAdd32{});
-  max_t = wreduce(max_t, OpMaxI32{});
-  max_a = wreduce(max_a, OpMaxI32{});
-  low = wreduce(low, OpMaxI32{});
+  const int32_t nfeas = gs[0], max_t = gs[1], max_a = gs[2], low = gs[3];
   KSG_YSTAMP(4);
 
-  // ---- rows: every node of this workgroup, written once --------------------------------
-  const int es = K.es;
+  // ---- the rows that need the fold: normalized and total scores ------------------------
   const bool scored = nfeas >= 2;   // fewer than two feasible nodes: no Score ran, nothing recorded
   PodView v{};                       // total_score's inputs
   v.smask = sm;
@@ -554,19 +587,8 @@ __device__ __forceinline__ void cyc_serve(const CycStatic& S, const CycCall& K, 
       const uint64_t kk = argmax_key(total, n);
       key = kk > key ? kk : key;
     }
-    hst<SYS>(K.h_fs + n, st[k]);
-    for (int q = 0; q < K.n_rows; q++) {
-      const int pl = (int)((K.rows >> (4 * q)) & 15u);
-      int64_t x = 0;
-      if (scored && ok && ((sm >> pl) & 1u))
-        x = pl == KSG_PL_NODE_RESOURCES_FIT     ? rf[k]
-            : pl == KSG_PL_BALANCED_ALLOCATION ? rbal[k]
-            : pl == KSG_PL_IMAGE_LOCALITY      ? rimg[k]
-            : pl == KSG_PL_TAINT_TOLERATION    ? rt[k]
-            : pl == KSG_PL_NODE_AFFINITY       ? ra[k]
-                                               : 0;
-      cyc_put_es<SYS>(K.h_raw, (size_t)q * NN + n, x, es);
-    }
+    if (!scored && ok)   // no Score ran: nothing recorded for it
+      for (int q = 0; q < K.n_rows; q++) cyc_put_es<SYS>(K.h_raw, (size_t)q * NN + n, 0, es);
     for (int q = 0; q < K.n_normrows; q++) {
       const int pl = (int)((K.rows >> (4 * q)) & 15u);
       cyc_put_es<SYS>(K.h_norm, (size_t)q * NN + n, pl == KSG_PL_TAINT_TOLERATION ? nt : na, es);

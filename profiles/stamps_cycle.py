@@ -27,8 +27,8 @@ for i in range(50, P):
         eng.commit(i, r.selected)
 dt = (time.perf_counter() - t) / (P - 50)
 st = (C.c_ulonglong * 16)(); fn(eng.ctx, st)
-names = ["entry (arguments, columns, programs)", "evaluate (filters, scores)", "reductions + slot stores",
-         "exchange wait", "fold", "host rows + release", "record + done word"]
+names = ["entry (arguments, columns, programs)", "evaluate (filters, scores)", "reductions, slots, status+raw rows",
+         "exchange wait (folding the lines)", "(fold: empty since r5)", "norm+total rows + release", "record + done word"]
 d = [st[i] - st0[i] for i in range(7)]
 tot = sum(d)
 print(f"[cycle] {N} nodes, {P-50} evals, {dt*1e6:.1f} us per eval+commit (python loop)")

@@ -3,7 +3,7 @@
 # relayed persistent server: parity, stamps, C-driver timing.
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r5f
+O=gpurun_out/r5g
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 500 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_eval.py tests/test_snapshot_c.py > $O/tests.log 2>&1 || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
