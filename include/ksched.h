@@ -172,6 +172,8 @@ typedef struct ksg_workload {
 /* ---- profile ------------------------------------------------------------ */
 #define KSG_LEAST_ALLOCATED 0
 #define KSG_MOST_ALLOCATED 1
+#define KSG_REQUESTED_TO_CAPACITY_RATIO 2
+#define KSG_MAX_SHAPE 16                 /* RequestedToCapacityRatio shape points  */
 #define KSG_PROF_BA_SKIP_BEST_EFFORT (1u << 0)
 #define KSG_PROF_IPA_IGNORE_EXISTING_PREF (1u << 1)
 typedef struct ksg_profile {
@@ -179,7 +181,7 @@ typedef struct ksg_profile {
   int32_t filter_order[KSG_NPLUGINS];  /* Filter plugins in MultiPoint order      */
   uint32_t score_mask;                 /* bit p: plugin p runs at Score           */
   int32_t weight[KSG_NPLUGINS];        /* getScorePluginWeight (0 -> 1)           */
-  int32_t fit_strategy;                /* KSG_LEAST_ALLOCATED / KSG_MOST_ALLOCATED */
+  int32_t fit_strategy;                /* KSG_LEAST_ALLOCATED / _MOST_ALLOCATED / _REQUESTED_TO_CAPACITY_RATIO */
   int32_t fit_n;
   int32_t fit_res[KSG_MAX_RES];        /* resource columns scored by Fit          */
   int64_t fit_w[KSG_MAX_RES];
@@ -188,6 +190,9 @@ typedef struct ksg_profile {
   int32_t hard_pod_affinity_weight;
   uint32_t flags;                      /* KSG_PROF_*                              */
   uint32_t fit_ignored_res;            /* bit r: scalar column r ignored by the Fit filter */
+  int32_t shape_n;                     /* RequestedToCapacityRatio: shape points,   */
+  int32_t shape_util[KSG_MAX_SHAPE];   /*   utilization 0..100 increasing, and the  */
+  int32_t shape_score[KSG_MAX_SHAPE];  /*   score scaled to 0..100 (written x 10)   */
   int32_t pad;
 } ksg_profile;
 

@@ -241,7 +241,8 @@ typedef struct ksg_plugin_set_view {
 typedef struct ksg_profile_view {
   int32_t n_plugins;
   const ksg_plugin_view* plugins;
-  const char* fit_strategy;                  /* "LeastAllocated" / "MostAllocated" */
+  const char* fit_strategy;                  /* "LeastAllocated" / "MostAllocated" /
+                                                "RequestedToCapacityRatio" (shape below) */
   int32_t n_fit_resources;
   const ksg_quantity* fit_resources;         /* (name, weight) */
   int32_t n_ba_resources;
@@ -255,6 +256,16 @@ typedef struct ksg_profile_view {
   int32_t pts_system_defaulted;              /* PodTopologySpreadArgs.defaultingType == System */
   int32_t ba_skip_best_effort;
   ksg_plugin_set_view points[KSG_NPOINTS];   /* indexed by KSG_POINT_* */
+  /* NodeResourcesFitArgs.scoringStrategy.requestedToCapacityRatio.shape as
+   * written (utilization 0..100 increasing, score 0..10; at most
+   * KSG_MAX_SHAPE points), read when fit_strategy is RequestedToCapacityRatio */
+  int32_t n_shape;
+  const int32_t* shape_utilization;
+  const int32_t* shape_score;
+  /* PodTopologySpreadArgs.defaultConstraints (defaultingType List, i.e.
+   * pts_system_defaulted = 0): selector unset, the owners' selector is used */
+  int32_t n_default_constraints;
+  const ksg_spread_view* default_constraints;
 } ksg_profile_view;
 
 /* The profile as the framework and the simulator's Store see it (derived by

@@ -1124,7 +1124,7 @@ int sweep_occupancy(ksg_ctx* ctx, int mode, bool narrow, int* occ) {   // the MU
 // {cpu, memory, one scalar column}, BalancedAllocation over {cpu, memory},
 // positive weights.
 bool profile_ex_fast(const ksg_profile& prof) {
-  if (prof.fit_n != 3 || prof.ba_n != 2) return false;
+  if (prof.fit_n != 3 || prof.ba_n != 2 || prof.fit_strategy == KSG_REQUESTED_TO_CAPACITY_RATIO) return false;
   int nc = 0, nm = 0, nx = 0;
   for (int i = 0; i < 3; i++) {
     const int r = prof.fit_res[i];
@@ -1139,7 +1139,7 @@ bool profile_ex_fast(const ksg_profile& prof) {
 }
 
 bool profile_cm_fast(const ksg_profile& prof) {
-  if (prof.fit_n != 2 || prof.ba_n != 2) return false;
+  if (prof.fit_n != 2 || prof.ba_n != 2 || prof.fit_strategy == KSG_REQUESTED_TO_CAPACITY_RATIO) return false;
   auto cpumem = [](int a, int b) {
     return (a == KSG_RES_CPU && b == KSG_RES_MEM) || (a == KSG_RES_MEM && b == KSG_RES_CPU);
   };
@@ -2069,7 +2069,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       wm = r0 == KSG_RES_CPU ? prof.fit_w[1] : prof.fit_w[0];
       const int b0 = prof.ba_res[0], b1 = prof.ba_res[1];
       ok = ok && ((b0 == KSG_RES_CPU && b1 == KSG_RES_MEM) || (b0 == KSG_RES_MEM && b1 == KSG_RES_CPU));
-      ok = ok && wc > 0 && wm > 0;
+      ok = ok && wc > 0 && wm > 0 && prof.fit_strategy != KSG_REQUESTED_TO_CAPACITY_RATIO;
     }
     ck.cm_fast = ok;
     ck.cm_least = prof.fit_strategy == KSG_LEAST_ALLOCATED;
@@ -2691,8 +2691,14 @@ int ksg_set_profile(ksg_ctx* ctx, const ksg_profile* prof) {
   if (int rc_ = srv_stop(ctx)) return rc_;   // the persistent per-cycle server leaves first
   if (!ctx || !prof) return KSG_E_INVALID;
   if (prof->n_filter < 0 || prof->n_filter > KSG_NPLUGINS || prof->fit_n < 0 || prof->fit_n > KSG_MAX_RES ||
-      prof->ba_n < 0 || prof->ba_n > KSG_MAX_RES)
+      prof->ba_n < 0 || prof->ba_n > KSG_MAX_RES || prof->fit_strategy < KSG_LEAST_ALLOCATED ||
+      prof->fit_strategy > KSG_REQUESTED_TO_CAPACITY_RATIO || prof->shape_n < 0 || prof->shape_n > KSG_MAX_SHAPE ||
+      (prof->fit_strategy == KSG_REQUESTED_TO_CAPACITY_RATIO && prof->shape_n == 0))
     return fail(ctx, KSG_E_INVALID, "profile field out of range");
+  for (int i = 0; i < prof->shape_n; i++)   // ValidateNodeResourcesFitArgs' shape rules (scores already x 10)
+    if (prof->shape_util[i] < 0 || prof->shape_util[i] > 100 || prof->shape_score[i] < 0 ||
+        prof->shape_score[i] > 100 || (i > 0 && prof->shape_util[i] <= prof->shape_util[i - 1]))
+      return fail(ctx, KSG_E_INVALID, "RequestedToCapacityRatio shape out of range or not increasing");
   ctx->prof = *prof;
   ctx->have_prof = true;
   ctx->ev_prof_dirty = true;

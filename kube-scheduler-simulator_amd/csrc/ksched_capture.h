@@ -81,8 +81,8 @@ __global__ __launch_bounds__(256) void ksg_capture_eval(CapArgs a) {
   const DevCluster& c = a.c;
   const int N = c.N;
   const size_t NN = N;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
   for (int k = tid; k < a.nb; k += 256) s_pl[k] = a.placements[a.out0 + k];
   const int32_t* gprog = a.prog;
   if (a.spod) {   // the staged append (nb = 1)
@@ -182,8 +182,8 @@ __global__ __launch_bounds__(256) void ksg_capture_norm(CapArgs a) {
   const DevCluster& c = a.c;
   const int N = c.N;
   const size_t NN = N;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
   if (a.next && blockIdx.x == 0 && tid < 8) a.next[tid] = 0;   // the next call's slot
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();

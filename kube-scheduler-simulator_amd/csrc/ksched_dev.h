@@ -64,8 +64,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_kernel(QueueArgs a) {
   uint32_t* ports = a.st.ports ? a.st.ports + rep * a.st.stride_ports : nullptr;
   const bool cap = a.cap_fstatus != nullptr && rep == 0;
 
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles + rep)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.profiles + rep)[i_];
 
   for (int k = 0; k < a.count; k++) {
     const int pi = a.first + k;
@@ -289,8 +289,8 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
     tile = (w / a.nb) * 8 + (b & 7);
     if (tile * 256 >= N) return;
   }
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
   stage_pod<256>(a.pods, a.prog, a.b0 + j, &s_pod, s_blob);
   __syncthreads();
   const PodView v = make_view(c, s_prof, s_pod, s_blob, a.prog);
@@ -374,8 +374,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2_scan(BatchArgs a) {
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
   for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
   for (int i = tid; i < 2 * a.nb; i += BLOCK) s_pmax[i] = a.pmax[i];
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
   if (tid == 0) s_nc = 0;
 
   uint64_t rr[kRPT];
@@ -558,8 +558,8 @@ __device__ __forceinline__ void batch_topk_body(const BatchArgs& a) {
   const int j = blockIdx.x;
   const DevCluster& c = a.c;
   const int N = c.N;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
   if (tid == 0) s_pos = 0;
   __syncthreads();
   const ksg_pod& p = a.pods[a.b0 + j];
@@ -846,8 +846,8 @@ __global__ __launch_bounds__(kP2Block) void ksg_batch_phase2(BatchArgs a) {
   for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
   for (int i = tid; i < a.nb * (int)(sizeof(P1Stats) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(s_p1)[i] = reinterpret_cast<const int32_t*>(a.p1)[i];
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.prof)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
   if (tid < KSG_BATCH_MAX) {
     s_top[0][tid] = a.top[tid];
     if (a.nb > 1) s_top[1][tid] = a.top[KSG_BATCH_MAX + tid];
@@ -1898,8 +1898,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
   int64_t* sraw = a.st.sraw + rep * a.st.stride_sraw;
   const bool cap = a.cap_fstatus != nullptr && rep == 0;
 
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles + rep)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.profiles + rep)[i_];
   __syncthreads();
   const ksg_profile& prof = s_prof;
   bool ipa_in_filter = false;

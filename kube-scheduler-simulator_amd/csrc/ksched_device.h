@@ -346,19 +346,48 @@ __device__ __forceinline__ void alloc_req(const ksg_pod& p, const NodeCols& L, i
   q = base + pr;
 }
 
+// helper.BuildBrokenLinearFunction over the profile's shape (scores already
+// x 10): the first point at or above p, interpolated from the one before
+// [upstream v1.32 pkg/scheduler/framework/plugins/helper/shape_score.go]
+__device__ __forceinline__ int64_t rtcr_shape(const ksg_profile& prof, int64_t p) {
+  for (int i = 0; i < prof.shape_n; i++) {
+    const int64_t u = prof.shape_util[i];
+    if (p <= u) {
+      if (i == 0) return prof.shape_score[0];
+      const int64_t u0 = prof.shape_util[i - 1], s0 = prof.shape_score[i - 1];
+      return s0 + (prof.shape_score[i] - s0) * (p - u0) / (u - u0);   // Go's truncating division
+    }
+  }
+  return prof.shape_n > 0 ? prof.shape_score[prof.shape_n - 1] : 0;
+}
+
+// NodeResourcesFit's score: LeastAllocated / MostAllocated (integer means),
+// RequestedToCapacityRatio (the shape at each resource's utilization, only
+// positive scores weighted, the mean rounded half away from zero)
+// [upstream v1.32 noderesources/least_allocated.go, most_allocated.go,
+// requested_to_capacity_ratio.go]
 __device__ __forceinline__ int64_t fit_score(const ksg_profile& prof, const ksg_pod& p, const NodeCols& L) {
   int64_t num = 0, wsum = 0;
+  const bool rtcr = prof.fit_strategy == KSG_REQUESTED_TO_CAPACITY_RATIO;
   for (int i = 0; i < prof.fit_n; i++) {
     int64_t a, q;
     alloc_req(p, L, prof.fit_res[i], false, a, q);
     if (a == 0) continue;
     int64_t s;
-    if (prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : div_small((a - q) * 100, a);
-    else s = div_small((q > a ? a : q) * 100, a);
+    if (rtcr) {
+      s = rtcr_shape(prof, q > a ? 100 : q * 100 / a);
+      if (s <= 0) continue;
+    } else if (prof.fit_strategy == KSG_LEAST_ALLOCATED) {
+      s = q > a ? 0 : div_small((a - q) * 100, a);
+    } else {
+      s = div_small((q > a ? a : q) * 100, a);
+    }
     num += s * prof.fit_w[i];
     wsum += prof.fit_w[i];
   }
-  return wsum == 0 ? 0 : div_small(num, wsum);
+  if (wsum == 0) return 0;
+  if (rtcr) return (int64_t)round((double)num / (double)wsum);
+  return div_small(num, wsum);
 }
 
 // balancedResourceScorer, in Go's float64 operation order.  Fractions are
@@ -406,7 +435,7 @@ struct CmProf {
 
 __device__ __forceinline__ CmProf cm_prof(const ksg_profile& prof) {
   CmProf m{false, prof.fit_strategy == KSG_LEAST_ALLOCATED, 0, 0, 1.0f, 1.0f, 1.0f};
-  bool ok = prof.fit_n == 2 && prof.ba_n == 2;
+  bool ok = prof.fit_n == 2 && prof.ba_n == 2 && prof.fit_strategy != KSG_REQUESTED_TO_CAPACITY_RATIO;
   if (ok) {
     const int r0 = prof.fit_res[0], r1 = prof.fit_res[1];
     ok = (r0 == KSG_RES_CPU && r1 == KSG_RES_MEM) || (r0 == KSG_RES_MEM && r1 == KSG_RES_CPU);

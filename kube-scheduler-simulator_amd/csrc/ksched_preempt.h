@@ -58,8 +58,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_preempt_prepass(DevCluster c, DevSt
   __shared__ int32_t s_c1[kMaxHard];
   const int tid = threadIdx.x, lane = tid & 63;
   const int N = c.N;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(profp)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(profp)[i_];
   stage_pod<BLOCK>(pods, prog, pod, &s_pod, s_blob);
   __syncthreads();
   const ksg_pod& p = s_pod;
@@ -245,8 +245,8 @@ __global__ __launch_bounds__(256) void ksg_preempt_topo(DevCluster c, DevState s
   __shared__ TopoShared s_t;
   const int tid = threadIdx.x;
   const int N = c.N;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(profp)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(profp)[i_];
   stage_pod<256>(pods, prog, pod, &s_pod, s_blob);
   __syncthreads();
   const ksg_pod& p = s_pod;

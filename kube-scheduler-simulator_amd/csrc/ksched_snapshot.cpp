@@ -464,6 +464,8 @@ struct Profile {
   std::set<std::string> ignored, ignored_groups;
   int32_t hard_weight;
   bool ignore_pref, pts_system, ba_skip_be;
+  std::vector<std::pair<int32_t, int32_t>> shape;   // RequestedToCapacityRatio (utilization, score 0..10)
+  std::vector<Spread> pts_defaults;                 // defaultConstraints (defaultingType List)
   std::vector<int> enabled;   // plugin ids in MultiPoint order
   // derived (profile.py Profile._expand / weights / selection_weights)
   std::vector<int> order[KSG_NPOINTS];   // per extension point, run order
@@ -553,11 +555,19 @@ PtsPair pts_constraints(const Pod& p, const Profile& prof) {
       if (c.when == "DoNotSchedule") hard.push_back(ent);
       else if (c.when == "ScheduleAnyway") soft.push_back(ent);
     }
-  } else if (prof.pts_system && p.default_sel.set) {
+  } else if (p.default_sel.set) {   // buildDefaultConstraints with the owners' selector
     Canon canon = canon_selector(p.default_sel);
     if (canon && !canon->empty()) {
-      soft.push_back(Constraint{3, kHostname, canon, 1, true, false});
-      soft.push_back(Constraint{5, kZone, canon, 1, true, false});
+      if (prof.pts_system) {
+        soft.push_back(Constraint{3, kHostname, canon, 1, true, false});
+        soft.push_back(Constraint{5, kZone, canon, 1, true, false});
+      } else {
+        for (auto& c : prof.pts_defaults) {
+          Constraint ent{c.skew, c.key, canon, c.min_domains > 0 ? c.min_domains : 1,
+                         c.nap.empty() || c.nap == "Honor", !c.ntp.empty() && c.ntp == "Honor"};
+          (c.when == "DoNotSchedule" ? hard : soft).push_back(ent);
+        }
+      }
     }
   }
   return {hard, soft};
@@ -1470,7 +1480,14 @@ int encode_profile(ksg_snapshot* s) {
     p.score_mask |= 1u << pid;
     p.weight[pid] = pr.sel_w[pid] != 0 ? pr.sel_w[pid] : 1;
   }
-  p.fit_strategy = pr.fit_strategy == "MostAllocated" ? KSG_MOST_ALLOCATED : KSG_LEAST_ALLOCATED;
+  p.fit_strategy = pr.fit_strategy == "MostAllocated"              ? KSG_MOST_ALLOCATED
+                   : pr.fit_strategy == "RequestedToCapacityRatio" ? KSG_REQUESTED_TO_CAPACITY_RATIO
+                                                                   : KSG_LEAST_ALLOCATED;
+  if (p.fit_strategy == KSG_REQUESTED_TO_CAPACITY_RATIO)
+    for (auto& pt : pr.shape) {   // scores scaled by MaxNodeScore / MaxCustomPriorityScore
+      p.shape_util[p.shape_n] = pt.first;
+      p.shape_score[p.shape_n++] = pt.second * 10;
+    }
   for (auto& r : pr.fit_res) {
     auto it = e.res_col.find(r.first);
     if (it == e.res_col.end()) continue;
@@ -1813,9 +1830,47 @@ int ksg_snapshot_new(const ksg_profile_view* pv, ksg_snapshot** out) {
     return KSG_E_UNSUPPORTED;   // a per-point set the registry / framework refuses
   }
   p.fit_strategy = pv->fit_strategy ? S(pv->fit_strategy) : "LeastAllocated";
-  if (p.fit_strategy != "LeastAllocated" && p.fit_strategy != "MostAllocated") {
+  if (p.fit_strategy != "LeastAllocated" && p.fit_strategy != "MostAllocated" &&
+      p.fit_strategy != "RequestedToCapacityRatio") {
     delete s;
-    return KSG_E_UNSUPPORTED;   // RequestedToCapacityRatio is not modelled
+    return KSG_E_INVALID;   // not a scoring strategy
+  }
+  // the plugin-args validation of the scheduler (profile.py Profile.validate_args)
+  if (p.fit_strategy == "RequestedToCapacityRatio") {
+    if (pv->n_shape <= 0 || pv->n_shape > KSG_MAX_SHAPE || !pv->shape_utilization || !pv->shape_score) {
+      delete s;
+      return pv->n_shape > KSG_MAX_SHAPE ? KSG_E_UNSUPPORTED : KSG_E_INVALID;
+    }
+    for (int32_t i = 0; i < pv->n_shape; i++) {
+      const int32_t u = pv->shape_utilization[i], sc = pv->shape_score[i];
+      if (u < 0 || u > 100 || sc < 0 || sc > 10 || (i > 0 && u <= pv->shape_utilization[i - 1])) {
+        delete s;
+        return KSG_E_INVALID;
+      }
+      p.shape.emplace_back(u, sc);
+    }
+  }
+  if (pv->n_default_constraints < 0 || (pv->n_default_constraints > 0 && !pv->default_constraints) ||
+      (pv->n_default_constraints > 0 && pv->pts_system_defaulted)) {
+    delete s;
+    return KSG_E_INVALID;
+  }
+  std::set<std::pair<std::string, std::string>> seen;
+  for (int32_t i = 0; i < pv->n_default_constraints; i++) {
+    const ksg_spread_view& c = pv->default_constraints[i];
+    Spread sp;
+    sp.skew = c.max_skew;
+    sp.key = S(c.topology_key);
+    sp.when = S(c.when_unsatisfiable);
+    sp.min_domains = c.min_domains;
+    sp.nap = S(c.node_affinity_policy);
+    sp.ntp = S(c.node_taints_policy);
+    if (sp.skew <= 0 || sp.key.empty() || (sp.when != "DoNotSchedule" && sp.when != "ScheduleAnyway") ||
+        c.selector.is_set || !seen.insert({sp.key, sp.when}).second) {
+      delete s;
+      return KSG_E_INVALID;
+    }
+    p.pts_defaults.push_back(std::move(sp));
   }
   for (int32_t i = 0; i < pv->n_fit_resources; i++)
     p.fit_res.emplace_back(S(pv->fit_resources[i].name), pv->fit_resources[i].value);

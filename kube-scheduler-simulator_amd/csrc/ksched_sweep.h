@@ -237,8 +237,8 @@ __global__ __launch_bounds__(256) void ksg_sweep_static(SweepArgs a) {
   const int j = w % a.nb;                       // pod of the batch
   const int tile = (w / a.nb) * 8 + (b & 7);    // node tile: same b % 8 for all its pods
   if (tile * 256 >= N) return;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.profiles)[i_];
   const bool eff_lds = c.V <= kStaticEff;
   if (eff_lds)
     for (int i = tid; i < c.V; i += 256) s_eff[i] = c.taint_effect[i];
@@ -277,7 +277,7 @@ __device__ __forceinline__ SweepProf sweep_prof(const ksg_profile& prof) {
   s.cm = cm_prof(prof);
   s.ex = -1;
   s.w_ex = 0;
-  if (!s.cm.fast && prof.fit_n == 3) {
+  if (!s.cm.fast && prof.fit_n == 3 && prof.fit_strategy != KSG_REQUESTED_TO_CAPACITY_RATIO) {
     for (int i = 0; i < 3; i++) {
       const int r = prof.fit_res[i];
       if (r == KSG_RES_CPU) s.cm.wc = prof.fit_w[i];
@@ -464,8 +464,8 @@ __global__ __launch_bounds__(BLOCK, 1024 / BLOCK) void ksg_sweep(SweepArgs a) { 
   int32_t* pod_count = a.st.pod_count + rep * a.st.stride_pc;
   int4* nmut = NARROW ? a.nmut + (size_t)rep * N : nullptr;
   uint64_t* scratch = KN == 0 ? a.scratch + (size_t)rep * N : nullptr;
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profiles + rep)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.profiles + rep)[i_];
   __syncthreads();
   const ksg_profile& prof = s_prof;
   const SweepProf sp = sweep_prof(prof);

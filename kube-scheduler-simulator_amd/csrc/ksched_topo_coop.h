@@ -411,8 +411,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     s_prev_imm = 0;
     s_tables_ok = a.use_tables && !gld(tt.invalid);
   }
-  if (tid < (int)(sizeof(ksg_profile) / 4))
-    reinterpret_cast<int32_t*>(&s_prof)[tid] = reinterpret_cast<const int32_t*>(a.profile)[tid];
+  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
+    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.profile)[i_];
   for (int i = tid; i < a.count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
   for (int i = tid; i < a.count; i += BLOCK) s_elig[i] = a.use_tables ? tt.elig[a.first - tt.first + i] : 0;

@@ -326,11 +326,19 @@ class Encoder:
                     hard.append(ent)
                 elif c.when_unsatisfiable == m.SCHEDULE_ANYWAY:
                     soft.append(ent)
-        elif self.prof.pts_system_defaulted and pod.default_spread_selector is not None:
+        elif pod.default_spread_selector is not None:
+            # buildDefaultConstraints: the profile's defaults (System: the
+            # two ScheduleAnyway constraints; List: defaultConstraints as
+            # written), each with the owners' selector
             canon = canon_selector(pod.default_spread_selector)
             if canon:   # selector.Empty() -> no default constraints
-                for skew, key in SYSTEM_DEFAULT_SPREAD:
-                    soft.append((skew, key, canon, 1, m.POLICY_HONOR, m.POLICY_IGNORE))
+                if self.prof.pts_system_defaulted:
+                    for skew, key in SYSTEM_DEFAULT_SPREAD:
+                        soft.append((skew, key, canon, 1, m.POLICY_HONOR, m.POLICY_IGNORE))
+                for c in () if self.prof.pts_system_defaulted else self.prof.pts_default_constraints:
+                    ent = (c.max_skew, c.topology_key, canon, c.min_domains if c.min_domains is not None else 1,
+                           c.node_affinity_policy or m.POLICY_HONOR, c.node_taints_policy or m.POLICY_IGNORE)
+                    (hard if c.when_unsatisfiable == m.DO_NOT_SCHEDULE else soft).append(ent)
         return hard, soft
 
     def _build_label_columns(self):
@@ -825,10 +833,14 @@ def encode_profile(prof: P.Profile, res_names: Sequence[str]) -> dict:
         if "/" in r and (r in prof.fit_ignored_resources or r.split("/")[0] in prof.fit_ignored_resource_groups):
             ign |= 1 << res_col[r]
     flags = (1 if prof.ba_skip_best_effort else 0) | (2 if prof.ignore_preferred_terms_of_existing_pods else 0)
+    prof.validate_args()
+    shape = list(prof.fit_shape) if prof.fit_strategy == P.REQUESTED_TO_CAPACITY_RATIO else []
+    pad = [0] * (P.MAX_SHAPE - len(shape))
     return dict(n_filter=len(order), filter_order=order + [0] * (NPLUGINS - len(order)),
                 score_mask=score_mask, weight=w, fit_strategy=prof.fit_strategy,
                 fit_n=len(fit), fit_res=[c for c, _ in fit] + [0] * (MAX_RES - len(fit)),
                 fit_w=[wt for _, wt in fit] + [0] * (MAX_RES - len(fit)),
                 ba_n=len(ba), ba_res=ba + [0] * (MAX_RES - len(ba)),
                 hard_pod_affinity_weight=prof.hard_pod_affinity_weight, flags=flags,
-                fit_ignored_res=ign)
+                fit_ignored_res=ign, shape_n=len(shape), shape_util=[u for u, _ in shape] + pad,
+                shape_score=[sc * (100 // P.MAX_CUSTOM_PRIORITY_SCORE) for _, sc in shape] + pad)

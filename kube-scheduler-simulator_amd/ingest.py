@@ -218,15 +218,33 @@ def pod_from_k8s(obj: dict, ns_labels: Optional[Dict[str, Dict[str, str]]] = Non
     p.tolerations = [m.Toleration(t.get("key", ""), t.get("operator", ""), str(t.get("value", "")), t.get("effect", ""))
                      for t in spec.get("tolerations") or ()]
     p.volumes = [_volume(v) for v in spec.get("volumes") or ()]
-    p.topology_spread_constraints = [
-        m.TopologySpreadConstraint(int(c["maxSkew"]), c["topologyKey"], c["whenUnsatisfiable"],
-                                   label_selector(c.get("labelSelector")),
-                                   min_domains=int(c["minDomains"]) if c.get("minDomains") is not None else None,
-                                   node_affinity_policy=c.get("nodeAffinityPolicy"),
-                                   node_taints_policy=c.get("nodeTaintsPolicy"),
-                                   match_label_keys=tuple(c.get("matchLabelKeys") or ()))
-        for c in spec.get("topologySpreadConstraints") or ()]
+    p.topology_spread_constraints = [_spread(c) for c in spec.get("topologySpreadConstraints") or ()]
     return p
+
+
+def _spread(c: dict) -> m.TopologySpreadConstraint:
+    """v1.TopologySpreadConstraint (a pod's, or a PodTopologySpreadArgs default)."""
+    return m.TopologySpreadConstraint(int(c["maxSkew"]), c["topologyKey"], c["whenUnsatisfiable"],
+                                      label_selector(c.get("labelSelector")),
+                                      min_domains=int(c["minDomains"]) if c.get("minDomains") is not None else None,
+                                      node_affinity_policy=c.get("nodeAffinityPolicy"),
+                                      node_taints_policy=c.get("nodeTaintsPolicy"),
+                                      match_label_keys=tuple(c.get("matchLabelKeys") or ()))
+
+
+def _spread_json(c: m.TopologySpreadConstraint) -> dict:
+    d = {"maxSkew": c.max_skew, "topologyKey": c.topology_key, "whenUnsatisfiable": c.when_unsatisfiable}
+    if c.label_selector is not None:
+        d["labelSelector"] = _sel_json(c.label_selector)
+    if c.min_domains is not None:
+        d["minDomains"] = c.min_domains
+    if c.node_affinity_policy is not None:
+        d["nodeAffinityPolicy"] = c.node_affinity_policy
+    if c.node_taints_policy is not None:
+        d["nodeTaintsPolicy"] = c.node_taints_policy
+    if c.match_label_keys:
+        d["matchLabelKeys"] = list(c.match_label_keys)
+    return d
 
 
 def pod_priority(obj: dict, classes: Dict[str, int], global_default: int) -> int:
@@ -329,8 +347,10 @@ def profile_from_config(cfg: Optional[dict]) -> Tuple[P.Profile, Optional[int]]:
             ss = args.get("scoringStrategy") or {}
             t = ss.get("type", "LeastAllocated")
             if t not in P.STRATEGY_NAMES:
-                raise NotImplementedError(f"NodeResourcesFit scoringStrategy {t!r}")
+                raise ValueError(f"NodeResourcesFit scoringStrategy {t!r}")
             prof.fit_strategy = P.STRATEGY_NAMES[t]
+            rtcr = ss.get("requestedToCapacityRatio") or {}
+            prof.fit_shape = [(int(pt.get("utilization", 0)), int(pt.get("score", 0))) for pt in rtcr.get("shape") or ()]
             if ss.get("resources"):
                 prof.fit_resources = [(r["name"], int(r.get("weight", 1) or 1)) for r in ss["resources"]]
             prof.fit_ignored_resources = tuple(args.get("ignoredResources") or ())
@@ -347,12 +367,11 @@ def profile_from_config(cfg: Optional[dict]) -> Tuple[P.Profile, Optional[int]]:
             prof.preemption_min_candidate_abs = int(args.get("minCandidateNodesAbsolute", 100))
         elif name == "PodTopologySpread":
             dt = args.get("defaultingType", "System")
-            if dt == "System":
-                prof.pts_system_defaulted = True
-            elif dt == "List" and not args.get("defaultConstraints"):
-                prof.pts_system_defaulted = False
-            else:
-                raise NotImplementedError("PodTopologySpread defaultConstraints (defaultingType List)")
+            if dt not in ("System", "List"):
+                raise ValueError(f"PodTopologySpread defaultingType {dt!r}")
+            prof.pts_system_defaulted = dt == "System"
+            prof.pts_default_constraints = [_spread(c) for c in args.get("defaultConstraints") or ()]
+    prof.validate_args()   # what the scheduler's config validation refuses
     return prof, pct
 
 
@@ -548,21 +567,7 @@ def pod_to_k8s(p: m.Pod) -> dict:
         spec["tolerations"] = [{k: v for k, v in (("key", t.key), ("operator", t.operator), ("value", t.value),
                                                   ("effect", t.effect)) if v} for t in p.tolerations]
     if p.topology_spread_constraints:
-        cs = []
-        for c in p.topology_spread_constraints:
-            d = {"maxSkew": c.max_skew, "topologyKey": c.topology_key, "whenUnsatisfiable": c.when_unsatisfiable}
-            if c.label_selector is not None:
-                d["labelSelector"] = _sel_json(c.label_selector)
-            if c.min_domains is not None:
-                d["minDomains"] = c.min_domains
-            if c.node_affinity_policy is not None:
-                d["nodeAffinityPolicy"] = c.node_affinity_policy
-            if c.node_taints_policy is not None:
-                d["nodeTaintsPolicy"] = c.node_taints_policy
-            if c.match_label_keys:
-                d["matchLabelKeys"] = list(c.match_label_keys)
-            cs.append(d)
-        spec["topologySpreadConstraints"] = cs
+        spec["topologySpreadConstraints"] = [_spread_json(c) for c in p.topology_spread_constraints]
     if p.priority:
         spec["priority"] = p.priority
     if p.preemption_policy != "PreemptLowerPriority":
@@ -596,8 +601,13 @@ def profile_to_config(prof: P.Profile) -> dict:
         {"name": "InterPodAffinity", "args": {"hardPodAffinityWeight": prof.hard_pod_affinity_weight,
                                               "ignorePreferredTermsOfExistingPods":
                                                   prof.ignore_preferred_terms_of_existing_pods}},
-        {"name": "PodTopologySpread", "args": {"defaultingType": "System" if prof.pts_system_defaulted else "List"}},
+        {"name": "PodTopologySpread", "args": {"defaultingType": "System" if prof.pts_system_defaulted else "List",
+                                               "defaultConstraints": [_spread_json(c)
+                                                                      for c in prof.pts_default_constraints]}},
     ]
+    if prof.fit_strategy == P.REQUESTED_TO_CAPACITY_RATIO:
+        pcs[0]["args"]["scoringStrategy"]["requestedToCapacityRatio"] = {
+            "shape": [{"utilization": u, "score": sc} for u, sc in prof.fit_shape]}
     return {"apiVersion": "kubescheduler.config.k8s.io/v1", "kind": "KubeSchedulerConfiguration",
             "percentageOfNodesToScore": 100,
             "profiles": [{"schedulerName": "default-scheduler",

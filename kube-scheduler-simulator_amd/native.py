@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(HERE, "libksched.so")
 
 NPLUGINS = 14
 MAX_RES = 8
+MAX_SHAPE = 16     # KSG_MAX_SHAPE
 
 # Every live native handle (Engine, Snapshot, Annotator) is closed by an
 # atexit hook before the interpreter tears down, most recently opened first,
@@ -95,7 +96,8 @@ class KsgProfile(C.Structure):
                 ("weight", C.c_int32 * NPLUGINS), ("fit_strategy", C.c_int32), ("fit_n", C.c_int32),
                 ("fit_res", C.c_int32 * MAX_RES), ("fit_w", C.c_int64 * MAX_RES), ("ba_n", C.c_int32),
                 ("ba_res", C.c_int32 * MAX_RES), ("hard_pod_affinity_weight", C.c_int32),
-                ("flags", C.c_uint32), ("fit_ignored_res", C.c_uint32), ("pad", C.c_int32)]
+                ("flags", C.c_uint32), ("fit_ignored_res", C.c_uint32), ("shape_n", C.c_int32),
+                ("shape_util", C.c_int32 * MAX_SHAPE), ("shape_score", C.c_int32 * MAX_SHAPE), ("pad", C.c_int32)]
 
 
 class KsgResult(C.Structure):

@@ -81,7 +81,11 @@ EXT = {
 
 LEAST_ALLOCATED = 0
 MOST_ALLOCATED = 1
-STRATEGY_NAMES = {"LeastAllocated": LEAST_ALLOCATED, "MostAllocated": MOST_ALLOCATED}
+REQUESTED_TO_CAPACITY_RATIO = 2
+STRATEGY_NAMES = {"LeastAllocated": LEAST_ALLOCATED, "MostAllocated": MOST_ALLOCATED,
+                  "RequestedToCapacityRatio": REQUESTED_TO_CAPACITY_RATIO}
+MAX_SHAPE = 16            # KSG_MAX_SHAPE: shape points the evaluator carries
+MAX_CUSTOM_PRIORITY_SCORE = 10   # a shape point's score range (config.MaxCustomPriorityScore)
 
 DEFAULT_MULTIPOINT: List[Tuple[str, int]] = [
     ("SchedulingGates", 0), ("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0),
@@ -103,8 +107,15 @@ class Profile:
     fit_ignored_resource_groups: Tuple[str, ...] = ()
     hard_pod_affinity_weight: int = 1
     ignore_preferred_terms_of_existing_pods: bool = False
+    # NodeResourcesFitArgs.scoringStrategy.requestedToCapacityRatio.shape:
+    # (utilization 0..100 increasing, score 0..10) points as written
+    fit_shape: List[Tuple[int, int]] = field(default_factory=list)
     # PodTopologySpreadArgs.defaultingType == System (no explicit defaultConstraints)
     pts_system_defaulted: bool = True
+    # PodTopologySpreadArgs.defaultConstraints (defaultingType List): the
+    # constraints a pod without its own gets, with the selector of its owning
+    # services / controllers (buildDefaultConstraints); label_selector unset
+    pts_default_constraints: List[m.TopologySpreadConstraint] = field(default_factory=list)
     # BalancedAllocation PreScore Skip for best-effort pods [upstream; believed
     # to land after v1.32 — TO VERIFY, SURVEY.md Appendix A.2]
     ba_skip_best_effort: bool = False
@@ -115,6 +126,40 @@ class Profile:
     # per-extension-point sets: point ("preFilter", "filter", "preScore",
     # "score") -> (enabled [(name, weight)], disabled names)
     points: Dict[str, Tuple[List[Tuple[str, int]], Tuple[str, ...]]] = field(default_factory=dict)
+
+    def validate_args(self) -> None:
+        """The plugin-args rules the scheduler's config validation applies to
+        the args modelled here [upstream v1.32 apis/config/validation/
+        validation_pluginargs.go: ValidateNodeResourcesFitArgs' shape rules,
+        ValidatePodTopologySpreadArgs]; ValueError on a configuration the
+        reference's scheduler would refuse to start with."""
+        if self.fit_strategy == REQUESTED_TO_CAPACITY_RATIO:
+            if not self.fit_shape:
+                raise ValueError("requestedToCapacityRatio.shape: at least one point must be specified")
+            if len(self.fit_shape) > MAX_SHAPE:
+                raise NotImplementedError(f"requestedToCapacityRatio.shape: more than {MAX_SHAPE} points")
+            for i, (u, sc) in enumerate(self.fit_shape):
+                if not 0 <= u <= 100:
+                    raise ValueError(f"shape[{i}].utilization {u} not in [0, 100]")
+                if i and u <= self.fit_shape[i - 1][0]:
+                    raise ValueError("shape utilization values must be sorted in increasing order")
+                if not 0 <= sc <= MAX_CUSTOM_PRIORITY_SCORE:
+                    raise ValueError(f"shape[{i}].score {sc} not in [0, {MAX_CUSTOM_PRIORITY_SCORE}]")
+        if self.pts_system_defaulted and self.pts_default_constraints:
+            raise ValueError("defaultConstraints must be empty when defaultingType is System")
+        seen = set()
+        for i, c in enumerate(self.pts_default_constraints):
+            if c.max_skew <= 0:
+                raise ValueError(f"defaultConstraints[{i}].maxSkew must be greater than zero")
+            if not c.topology_key:
+                raise ValueError(f"defaultConstraints[{i}].topologyKey can not be empty")
+            if c.when_unsatisfiable not in (m.DO_NOT_SCHEDULE, m.SCHEDULE_ANYWAY):
+                raise ValueError(f"defaultConstraints[{i}].whenUnsatisfiable {c.when_unsatisfiable!r}")
+            if (c.topology_key, c.when_unsatisfiable) in seen:
+                raise ValueError(f"defaultConstraints[{i}]: duplicate (topologyKey, whenUnsatisfiable)")
+            seen.add((c.topology_key, c.when_unsatisfiable))
+            if c.label_selector is not None:
+                raise ValueError(f"defaultConstraints[{i}]: constraint must not define a selector")
 
     # -- derived views ---------------------------------------------------
     def enabled_ids(self) -> List[int]:

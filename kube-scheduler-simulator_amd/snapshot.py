@@ -141,7 +141,9 @@ class ProfileView(C.Structure):
                 ("n_fit_ignored_groups", i32), ("fit_ignored_groups", C.POINTER(cp)),
                 ("hard_pod_affinity_weight", i32), ("ignore_preferred_terms_of_existing_pods", i32),
                 ("pts_system_defaulted", i32), ("ba_skip_best_effort", i32),
-                ("points", PluginSetView * NPOINTS)]
+                ("points", PluginSetView * NPOINTS), ("n_shape", i32), ("shape_utilization", C.POINTER(i32)),
+                ("shape_score", C.POINTER(i32)), ("n_default_constraints", i32),
+                ("default_constraints", C.POINTER(SpreadView))]
 
 
 class ProfileInfo(C.Structure):
@@ -247,18 +249,19 @@ def pod_view(p: m.Pod, k: _Keep) -> PodView:
     v.n_pod_anti_affinity_preferred, v.pod_anti_affinity_preferred = k.aff(p.pod_anti_affinity_preferred, True)
     v.n_tolerations, v.tolerations = k.arr(
         TolerationView, [TolerationView(_b(t.key), _b(t.operator), _b(t.value), _b(t.effect)) for t in p.tolerations])
-    spreads = []
-    for c in p.topology_spread_constraints:
-        nk, keys = k.strs(list(c.match_label_keys))
-        spreads.append(SpreadView(c.max_skew, _b(c.topology_key), _b(c.when_unsatisfiable), k.sel(c.label_selector),
-                                  c.min_domains if c.min_domains is not None else 0,
-                                  _b(c.node_affinity_policy or ""), _b(c.node_taints_policy or ""), nk, keys))
-    v.n_spread, v.spread = k.arr(SpreadView, spreads)
+    v.n_spread, v.spread = k.arr(SpreadView, [_spread_view(c, k) for c in p.topology_spread_constraints])
     v.default_spread_selector = k.sel(p.default_spread_selector)
     v.terminating = 1 if p.terminating else 0
     v.priority = int(p.priority)
     v.n_volumes, v.volumes = k.arr(VolumeView, [VolumeView(_b(n), _b(kind), _b(claim)) for n, kind, claim in p.volumes])
     return v
+
+
+def _spread_view(c: m.TopologySpreadConstraint, k: _Keep) -> SpreadView:
+    nk, keys = k.strs(list(c.match_label_keys))
+    return SpreadView(c.max_skew, _b(c.topology_key), _b(c.when_unsatisfiable), k.sel(c.label_selector),
+                      c.min_domains if c.min_domains is not None else 0,
+                      _b(c.node_affinity_policy or ""), _b(c.node_taints_policy or ""), nk, keys)
 
 
 def profile_view(prof: P.Profile, k: _Keep) -> ProfileView:
@@ -267,7 +270,7 @@ def profile_view(prof: P.Profile, k: _Keep) -> ProfileView:
     nb, br = k.arr(Quantity, [Quantity(_b(r), int(w)) for r, w in prof.ba_resources])
     ni, ig = k.strs(list(prof.fit_ignored_resources))
     ng, gr = k.strs(list(prof.fit_ignored_resource_groups))
-    strat = {P.LEAST_ALLOCATED: "LeastAllocated", P.MOST_ALLOCATED: "MostAllocated"}[prof.fit_strategy]
+    strat = {v: n for n, v in P.STRATEGY_NAMES.items()}[prof.fit_strategy]
     v = ProfileView(n, pl, _b(strat), nf, fr, nb, br, ni, ig, ng, gr, int(prof.hard_pod_affinity_weight),
                     1 if prof.ignore_preferred_terms_of_existing_pods else 0,
                     1 if prof.pts_system_defaulted else 0, 1 if prof.ba_skip_best_effort else 0)
@@ -278,6 +281,10 @@ def profile_view(prof: P.Profile, k: _Keep) -> ProfileView:
         ne, en = k.arr(PluginView, [PluginView(_b(nm), int(w)) for nm, w in enabled])
         nd, dis = k.strs(list(disabled))
         v.points[idx] = PluginSetView(ne, en, nd, dis)
+    v.n_shape, v.shape_utilization = k.arr(i32, [int(u) for u, _ in prof.fit_shape])
+    _, v.shape_score = k.arr(i32, [int(sc) for _, sc in prof.fit_shape])
+    v.n_default_constraints, v.default_constraints = k.arr(
+        SpreadView, [_spread_view(c, k) for c in prof.pts_default_constraints])
     return v
 
 

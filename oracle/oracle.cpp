@@ -220,6 +220,20 @@ void alloc_req(const Ctx& c, const ksg_pod& p, int r, int n, bool use_requested,
   q = base + pr;
 }
 
+// RequestedToCapacityRatio's broken-line function of utilization u in
+// [0, 100] [upstream v1.32 helper/shape_score.go BuildBrokenLinearFunction;
+// not vendored, parity unpinned]: left of the first point its score, right of
+// the last point the last score, else linear between the two points around u
+// (Go int64 division); shape scores arrive already scaled by 100 / 10.
+int64_t broken_line(const ksg_profile& pf, int64_t u) {
+  int k = 0;
+  while (k < pf.shape_n && u > pf.shape_util[k]) k++;
+  if (k == pf.shape_n) return pf.shape_score[pf.shape_n - 1];
+  if (k == 0) return pf.shape_score[0];
+  const int64_t du = pf.shape_util[k] - pf.shape_util[k - 1], ds = pf.shape_score[k] - pf.shape_score[k - 1];
+  return pf.shape_score[k - 1] + ds * (u - pf.shape_util[k - 1]) / du;
+}
+
 int64_t fit_score(const Ctx& c, const ksg_pod& p, int n) {
   int64_t num = 0, wsum = 0;
   for (int i = 0; i < c.prof.fit_n; i++) {
@@ -228,12 +242,23 @@ int64_t fit_score(const Ctx& c, const ksg_pod& p, int n) {
     alloc_req(c, p, r, n, false, a, q);
     if (a == 0) continue;
     int64_t s;
-    if (c.prof.fit_strategy == KSG_LEAST_ALLOCATED) s = q > a ? 0 : ((a - q) * kMaxNodeScore) / a;
-    else s = ((q > a ? a : q) * kMaxNodeScore) / a;
+    if (c.prof.fit_strategy == KSG_REQUESTED_TO_CAPACITY_RATIO) {
+      // requested_to_capacity_ratio.go: over capacity scores as full; only
+      // resources scoring above zero enter the weighted mean
+      s = broken_line(c.prof, q > a ? kMaxNodeScore : q * kMaxNodeScore / a);
+      if (s <= 0) continue;
+    } else if (c.prof.fit_strategy == KSG_LEAST_ALLOCATED) {
+      s = q > a ? 0 : ((a - q) * kMaxNodeScore) / a;
+    } else {
+      s = ((q > a ? a : q) * kMaxNodeScore) / a;
+    }
     num += s * c.prof.fit_w[i];
     wsum += c.prof.fit_w[i];
   }
-  return wsum == 0 ? 0 : num / wsum;
+  if (wsum == 0) return 0;
+  if (c.prof.fit_strategy == KSG_REQUESTED_TO_CAPACITY_RATIO)
+    return (int64_t)std::round((double)num / (double)wsum);   // math.Round: half away from zero
+  return num / wsum;
 }
 
 int64_t ba_score(const Ctx& c, const ksg_pod& p, int n) {

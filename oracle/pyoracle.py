@@ -303,20 +303,48 @@ def go_div(a: int, b: int) -> int:
     return q if (a >= 0) == (b >= 0) else -q
 
 
+def shape_score(shape, util: int) -> int:
+    """RequestedToCapacityRatio's piecewise-linear shape at `util` percent
+    [upstream v1.32 helper/shape_score.go BuildBrokenLinearFunction, not
+    vendored: parity unpinned]; shape points (utilization, score 0..10), the
+    score scaled to MAX_NODE_SCORE (x 100 / 10, requested_to_capacity_ratio.go)."""
+    pts = [(u, s * (MAX_NODE_SCORE // 10)) for u, s in shape]
+    for i, (u, s) in enumerate(pts):
+        if util <= u:
+            if i == 0:
+                return s
+            u0, s0 = pts[i - 1]
+            return s0 + go_div((s - s0) * (util - u0), u - u0)
+    return pts[-1][1]
+
+
+def go_round(x: float) -> int:
+    """math.Round: half away from zero (x >= 0 here)."""
+    t = math.trunc(x)
+    return int(t + 1 if x - t >= 0.5 else t)
+
+
 def fit_score(pod, ni, prof: P.Profile):
     num = 0
     wsum = 0
+    rtcr = prof.fit_strategy == P.REQUESTED_TO_CAPACITY_RATIO
     for rname, w in prof.fit_resources:
         a, r = alloc_req(ni, rname, score_pod_request(pod, rname, False), False)
         if a == 0:
             continue
-        if prof.fit_strategy == P.LEAST_ALLOCATED:
+        if rtcr:   # over capacity scores as full utilization; zero scores are left out of the mean
+            s = shape_score(prof.fit_shape, MAX_NODE_SCORE if r > a else go_div(r * MAX_NODE_SCORE, a))
+            if s <= 0:
+                continue
+        elif prof.fit_strategy == P.LEAST_ALLOCATED:
             s = 0 if r > a else go_div((a - r) * MAX_NODE_SCORE, a)
         else:
             s = go_div(min(r, a) * MAX_NODE_SCORE, a)
         num += s * w
         wsum += w
-    return go_div(num, wsum) if wsum else 0
+    if not wsum:
+        return 0
+    return go_round(num / wsum) if rtcr else go_div(num, wsum)
 
 
 def ba_score(pod, ni, prof: P.Profile):
@@ -405,11 +433,14 @@ SYSTEM_DEFAULT_CONSTRAINTS = [
 
 
 def pts_constraints(pod: m.Pod, action: str, prof: P.Profile):
+    """The pod's own constraints of this action, else buildDefaultConstraints
+    [upstream v1.32 podtopologyspread/common.go, not vendored]: the profile's
+    defaults (System's pair, or defaultConstraints under defaultingType List)
+    of this action, each taking the owners' selector; none when it is empty."""
     if pod.topology_spread_constraints:
         return [TSC(c, pod) for c in pod.topology_spread_constraints if c.when_unsatisfiable == action]
-    if not prof.pts_system_defaulted:
-        return []
-    cs = [c for c in SYSTEM_DEFAULT_CONSTRAINTS if c.when_unsatisfiable == action]
+    defaults = SYSTEM_DEFAULT_CONSTRAINTS if prof.pts_system_defaulted else prof.pts_default_constraints
+    cs = [c for c in defaults if c.when_unsatisfiable == action]
     if not cs or pod.default_spread_selector is None:
         return []
     sel = Sel(pod.default_spread_selector)

@@ -6,6 +6,7 @@ package ksched
 import (
 	"fmt"
 
+	v1 "k8s.io/api/core/v1"
 	"k8s.io/apimachinery/pkg/runtime"
 	configv1 "k8s.io/kube-scheduler/config/v1"
 	"k8s.io/kubernetes/pkg/scheduler/apis/config"
@@ -66,6 +67,15 @@ func (p *ProfileArgs) ApplyPluginArgs(name string, obj runtime.Object) error {
 			switch a.ScoringStrategy.Type {
 			case config.LeastAllocated, config.MostAllocated:
 				p.FitStrategy = string(a.ScoringStrategy.Type)
+				p.FitShape = nil
+			case config.RequestedToCapacityRatio:
+				p.FitStrategy = string(a.ScoringStrategy.Type)
+				p.FitShape = nil
+				if r := a.ScoringStrategy.RequestedToCapacityRatio; r != nil {
+					for _, pt := range r.Shape {
+						p.FitShape = append(p.FitShape, [2]int32{pt.Utilization, pt.Score})
+					}
+				}
 			default:
 				return fmt.Errorf("ksched: NodeResourcesFit scoring strategy %q is not modelled", a.ScoringStrategy.Type)
 			}
@@ -91,14 +101,10 @@ func (p *ProfileArgs) ApplyPluginArgs(name string, obj runtime.Object) error {
 		p.HardPodAffinityWeight = a.HardPodAffinityWeight
 		p.IgnorePreferredTermsOfExistingPods = a.IgnorePreferredTermsOfExistingPods
 	case *config.PodTopologySpreadArgs:
-		switch {
-		case a.DefaultingType == config.SystemDefaulting:
-			p.PTSSystemDefaulted = true
-		case a.DefaultingType == config.ListDefaulting && len(a.DefaultConstraints) == 0:
-			p.PTSSystemDefaulted = false
-		default:
-			return fmt.Errorf("ksched: PodTopologySpread defaultConstraints are not modelled")
-		}
+		// the snapshot validates defaultConstraints as the scheduler does
+		// (ksg_snapshot_new refuses a System profile that lists any)
+		p.PTSSystemDefaulted = a.DefaultingType == config.SystemDefaulting
+		p.PTSDefaultConstraints = append([]v1.TopologySpreadConstraint(nil), a.DefaultConstraints...)
 	case *config.NodeAffinityArgs:
 		if a.AddedAffinity != nil {
 			return fmt.Errorf("ksched: NodeAffinity addedAffinity is not modelled")

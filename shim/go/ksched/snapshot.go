@@ -265,25 +265,7 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 		tols[i].value, tols[i].effect = a.str(t.Value), a.str(string(t.Effect))
 	}
 	v.n_tolerations, v.tolerations = C.int32_t(len(p.Spec.Tolerations)), &tols[0]
-	tsc := p.Spec.TopologySpreadConstraints
-	sp := unsafe.Slice((*C.ksg_spread_view)(a.alloc(len(tsc), C.sizeof_ksg_spread_view)), len(tsc)+1)
-	for i, c := range tsc {
-		sp[i].max_skew = C.int32_t(c.MaxSkew)
-		sp[i].topology_key = a.str(c.TopologyKey)
-		sp[i].when_unsatisfiable = a.str(string(c.WhenUnsatisfiable))
-		sp[i].selector = a.selector(c.LabelSelector)
-		if c.MinDomains != nil {
-			sp[i].min_domains = C.int32_t(*c.MinDomains)
-		}
-		if c.NodeAffinityPolicy != nil {
-			sp[i].node_affinity_policy = a.str(string(*c.NodeAffinityPolicy))
-		}
-		if c.NodeTaintsPolicy != nil {
-			sp[i].node_taints_policy = a.str(string(*c.NodeTaintsPolicy))
-		}
-		sp[i].n_match_label_keys, sp[i].match_label_keys = a.strs(c.MatchLabelKeys)
-	}
-	v.n_spread, v.spread = C.int32_t(len(tsc)), &sp[0]
+	v.n_spread, v.spread = a.spreads(p.Spec.TopologySpreadConstraints)
 	v.default_spread_selector = a.selectorOf(defaultSel)
 	if p.DeletionTimestamp != nil {
 		v.terminating = 1
@@ -368,13 +350,42 @@ const (
 type ProfileArgs struct {
 	Plugins                               []Plugin
 	Points                                [NPoints]PluginSet
-	FitStrategy                           string           // LeastAllocated / MostAllocated
+	FitStrategy                           string           // LeastAllocated / MostAllocated / RequestedToCapacityRatio
+	FitShape                              [][2]int32       // RequestedToCapacityRatio (utilization, score 0..10)
 	FitResources, BAResources             map[string]int64 // name -> weight
 	FitResourceOrder, BAResourceOrder     []string         // the args' list order
 	FitIgnoredResources, FitIgnoredGroups []string
 	HardPodAffinityWeight                 int32
 	IgnorePreferredTermsOfExistingPods    bool
 	PTSSystemDefaulted                    bool
+	PTSDefaultConstraints                 []v1.TopologySpreadConstraint // defaultingType List
+}
+
+// spreads builds ksg_spread_view entries (a pod's constraints, or
+// PodTopologySpreadArgs.defaultConstraints).
+func (a *arena) spreads(tsc []v1.TopologySpreadConstraint) (C.int32_t, *C.ksg_spread_view) {
+	nv := len(tsc)
+	if nv < 1 {
+		nv = 1
+	}
+	sp := unsafe.Slice((*C.ksg_spread_view)(a.alloc(len(tsc), C.sizeof_ksg_spread_view)), nv)
+	for i, c := range tsc {
+		sp[i].max_skew = C.int32_t(c.MaxSkew)
+		sp[i].topology_key = a.str(c.TopologyKey)
+		sp[i].when_unsatisfiable = a.str(string(c.WhenUnsatisfiable))
+		sp[i].selector = a.selector(c.LabelSelector)
+		if c.MinDomains != nil {
+			sp[i].min_domains = C.int32_t(*c.MinDomains)
+		}
+		if c.NodeAffinityPolicy != nil {
+			sp[i].node_affinity_policy = a.str(string(*c.NodeAffinityPolicy))
+		}
+		if c.NodeTaintsPolicy != nil {
+			sp[i].node_taints_policy = a.str(string(*c.NodeTaintsPolicy))
+		}
+		sp[i].n_match_label_keys, sp[i].match_label_keys = a.strs(c.MatchLabelKeys)
+	}
+	return C.int32_t(len(tsc)), &sp[0]
 }
 
 // Snapshot is one ksg_snapshot (not thread-safe; the caller serialises).
@@ -419,6 +430,17 @@ func NewSnapshot(p *ProfileArgs) (*Snapshot, error) {
 	if p.PTSSystemDefaulted {
 		pv.pts_system_defaulted = 1
 	}
+	n, nv := len(p.FitShape), len(p.FitShape)
+	if nv < 1 {
+		nv = 1
+	}
+	su := unsafe.Slice((*C.int32_t)(a.alloc(n, 4)), nv)
+	ss := unsafe.Slice((*C.int32_t)(a.alloc(n, 4)), nv)
+	for i, pt := range p.FitShape {
+		su[i], ss[i] = C.int32_t(pt[0]), C.int32_t(pt[1])
+	}
+	pv.n_shape, pv.shape_utilization, pv.shape_score = C.int32_t(n), &su[0], &ss[0]
+	pv.n_default_constraints, pv.default_constraints = a.spreads(p.PTSDefaultConstraints)
 	for k := 0; k < NPoints; k++ {
 		ps := p.Points[k]
 		en := unsafe.Slice((*C.ksg_plugin_view)(a.alloc(len(ps.Enabled), C.sizeof_ksg_plugin_view)), len(ps.Enabled)+1)

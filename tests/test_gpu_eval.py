@@ -37,6 +37,8 @@ CASES = {
     "c1-images": lambda: G.config1(n_nodes=700, n_pods=60, seed=5),
 }
 CASES.update({f"zoo-{s}": (lambda s=s: __import__("zoo").zoo(s, n_pods=60)) for s in range(4)})
+CASES.update({f"zoo-{k}-{s}": (lambda s=s, k=k: __import__("zoo").zoo_args(s, k, n_pods=60))
+              for k in ("rtcr", "pts-list") for s in (0, 2)})
 
 
 @pytest.fixture(scope="module")

@@ -67,7 +67,18 @@ CASES = [
     ("readme-kat2", G.readme_kat2),
     ("c3-60x400", lambda: G.config3(n_nodes=60, n_pods=400, apps=12, zones=4)),
     ("c3-600x3000", lambda: G.config3(n_nodes=600, n_pods=3000, apps=40, zones=8)),
-] + [(f"zoo-{s}", (lambda s=s: __import__("zoo").zoo(s))) for s in range(8)]
+] + [(f"zoo-{s}", (lambda s=s: __import__("zoo").zoo(s))) for s in range(8)] + [
+    # plugin args beyond the defaults (parity unpinned against Go: both oracles only)
+    ("c2-rtcr-1000x1500", lambda: _with_rtcr(*G.config2(n_nodes=1000, n_pods=1500, seed=13),
+                                             [(0, 2), (30, 9), (70, 10), (100, 1)])),
+] + [(f"zoo-{k}-{s}", (lambda s=s, k=k: __import__("zoo").zoo_args(s, k)))
+     for k in ("rtcr", "pts-list") for s in range(3)]
+
+
+def _with_rtcr(nodes, pods, prof, shape):
+    prof.fit_strategy = P.REQUESTED_TO_CAPACITY_RATIO
+    prof.fit_shape = shape
+    return nodes, pods, prof
 
 
 @pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
@@ -141,6 +152,18 @@ def test_readme_kat2_gpu(gpu, gpu_batched):
 def test_zoo_annotation_bytes_gpu_vs_pyoracle(gpu, seed):
     from zoo import zoo
     nodes, pods, prof = zoo(seed, n_pods=80)
+    want, _ = pyoracle_annotations(nodes, pods, prof)
+    got = scheduler_annotations(nodes, pods, prof, gpu)
+    assert want == got
+
+
+@pytest.mark.parametrize("kind,seed", [("rtcr", 0), ("rtcr", 2), ("pts-list", 0), ("pts-list", 1)])
+def test_zoo_plugin_args_annotation_bytes_gpu_vs_pyoracle(gpu, kind, seed):
+    """RequestedToCapacityRatio / PodTopologySpread defaultConstraints: every
+    annotation byte from the GPU equals the Python restatement's (parity
+    unpinned against Go: no reference fixture covers these args)."""
+    from zoo import zoo_args
+    nodes, pods, prof = zoo_args(seed, kind, n_pods=80)
     want, _ = pyoracle_annotations(nodes, pods, prof)
     got = scheduler_annotations(nodes, pods, prof, gpu)
     assert want == got

@@ -48,7 +48,10 @@ CASES = [
     ("c3-15000x3000", lambda: G.config3(n_nodes=15000, n_pods=3000)),
     ("c1-2000x800", lambda: G.config1(n_nodes=2000, n_pods=800)),
 ] + [(f"zoo-big-{s}", (lambda s=s: __import__("zoo").zoo(s, n_nodes=700, n_pods=400, apps=7, zones=5)))
-     for s in range(4)]
+     for s in range(4)] + [
+    # defaultingType List: hard and soft default constraints on the owned pods
+    (f"zoo-big-pts-list-{s}", (lambda s=s: __import__("zoo").zoo_args(s, "pts-list", n_nodes=700, n_pods=400,
+                                                                      apps=7, zones=5))) for s in range(2)]
 
 
 _ORACLE = {}   # case -> (workload, oracle placements, results, final state): both hand-offs compare to one run

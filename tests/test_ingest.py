@@ -75,11 +75,49 @@ def test_profile_from_config_multipoint_merge():
 
 
 def test_profile_from_config_refuses_unmodelled():
-    with pytest.raises(NotImplementedError):
+    # RequestedToCapacityRatio without a shape: the scheduler's validation refuses it
+    with pytest.raises(ValueError):
         I.profile_from_config({"profiles": [{"pluginConfig": [{"name": "NodeResourcesFit", "args": {
             "scoringStrategy": {"type": "RequestedToCapacityRatio"}}}]}]})
     with pytest.raises(ValueError):
         I.profile_from_config({"profiles": [{"plugins": {"multiPoint": {"enabled": [{"name": "NodeNumber"}]}}}]})
+
+
+def test_profile_from_config_rtcr_and_default_constraints():
+    """RequestedToCapacityRatio's shape and PodTopologySpread defaultingType
+    List with defaultConstraints are read, validated and written back."""
+    cfg = {"profiles": [{"pluginConfig": [
+        {"name": "NodeResourcesFit", "args": {"scoringStrategy": {
+            "type": "RequestedToCapacityRatio", "resources": [{"name": "cpu", "weight": 3}],
+            "requestedToCapacityRatio": {"shape": [{"utilization": 0, "score": 0},
+                                                   {"utilization": 100, "score": 10}]}}}},
+        {"name": "PodTopologySpread", "args": {"defaultingType": "List", "defaultConstraints": [
+            {"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "DoNotSchedule"},
+            {"maxSkew": 2, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "ScheduleAnyway"}]}}]}],
+        "percentageOfNodesToScore": 100}
+    prof, _ = I.profile_from_config(cfg)
+    assert prof.fit_strategy == P.REQUESTED_TO_CAPACITY_RATIO and prof.fit_shape == [(0, 0), (100, 10)]
+    assert not prof.pts_system_defaulted
+    assert [(c.max_skew, c.topology_key, c.when_unsatisfiable) for c in prof.pts_default_constraints] == [
+        (1, "topology.kubernetes.io/zone", "DoNotSchedule"), (2, "kubernetes.io/hostname", "ScheduleAnyway")]
+    back, _ = I.profile_from_config(I.profile_to_config(prof))
+    assert back.fit_shape == prof.fit_shape and back.pts_default_constraints == prof.pts_default_constraints
+    bad = [
+        ("NodeResourcesFit", {"scoringStrategy": {"type": "RequestedToCapacityRatio", "requestedToCapacityRatio": {
+            "shape": [{"utilization": 50, "score": 1}, {"utilization": 40, "score": 2}]}}}),
+        ("NodeResourcesFit", {"scoringStrategy": {"type": "RequestedToCapacityRatio", "requestedToCapacityRatio": {
+            "shape": [{"utilization": 0, "score": 11}]}}}),
+        ("PodTopologySpread", {"defaultingType": "System", "defaultConstraints": [
+            {"maxSkew": 1, "topologyKey": "zone", "whenUnsatisfiable": "DoNotSchedule"}]}),
+        ("PodTopologySpread", {"defaultingType": "List", "defaultConstraints": [
+            {"maxSkew": 1, "topologyKey": "zone", "whenUnsatisfiable": "DoNotSchedule",
+             "labelSelector": {"matchLabels": {"a": "b"}}}]}),
+        ("PodTopologySpread", {"defaultingType": "List", "defaultConstraints": [
+            {"maxSkew": 0, "topologyKey": "zone", "whenUnsatisfiable": "DoNotSchedule"}]}),
+    ]
+    for name, args in bad:
+        with pytest.raises(ValueError):
+            I.profile_from_config({"profiles": [{"pluginConfig": [{"name": name, "args": args}]}]})
 
 
 def _same_encoding(a, b):

@@ -54,6 +54,22 @@ def test_zoo_annotations_pyoracle_vs_oracle(seed):
         assert w == g, f"zoo seed {seed}: pod {i} annotations differ"
 
 
+@pytest.mark.parametrize("kind", ["rtcr", "pts-list"])
+@pytest.mark.parametrize("seed", range(3))
+def test_zoo_plugin_args_pyoracle_vs_oracle(kind, seed):
+    """RequestedToCapacityRatio and PodTopologySpread defaultConstraints
+    (tests/zoo.py zoo_args): both restatements agree byte for byte.  Parity
+    unpinned against Go: no reference fixture covers these args."""
+    import binding
+    from zoo import zoo_args
+    nodes, pods, prof = zoo_args(seed, kind)
+    want, recs = pyoracle_annotations(nodes, pods, prof)
+    got = scheduler_annotations(nodes, pods, prof, binding.Oracle(2))
+    for i, (w, g) in enumerate(zip(want, got)):
+        assert w == g, f"zoo {kind} seed {seed}: pod {i} annotations differ"
+    assert any(r["n_feasible"] >= 2 for r in recs)
+
+
 def test_config3_small_annotations():
     import binding
     nodes, pods, prof = G.config3(n_nodes=40, n_pods=200, apps=10, zones=4)

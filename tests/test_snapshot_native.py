@@ -73,6 +73,32 @@ def test_zoo(built, seed):
     _assert_same(nodes, pods, prof)
 
 
+@pytest.mark.parametrize("kind", ["rtcr", "pts-list"])
+@pytest.mark.parametrize("seed", range(3))
+def test_zoo_plugin_args(built, kind, seed):
+    """RequestedToCapacityRatio shapes and PodTopologySpread defaultConstraints
+    through the C ABI's profile view: the same encoding (profile fields, the
+    default constraints' programs) as encoder.py."""
+    nodes, pods, prof = zoo.zoo_args(seed, kind)
+    _assert_same(nodes, pods, prof)
+
+
+def test_profile_view_refuses_invalid_args(built):
+    """The scheduler's plugin-args validation, at ksg_snapshot_new."""
+    bad = []
+    p = P.Profile(fit_strategy=P.REQUESTED_TO_CAPACITY_RATIO, fit_shape=[])
+    bad.append(p)
+    bad.append(P.Profile(fit_strategy=P.REQUESTED_TO_CAPACITY_RATIO, fit_shape=[(50, 1), (50, 2)]))
+    bad.append(P.Profile(pts_system_defaulted=True, pts_default_constraints=[
+        m.TopologySpreadConstraint(1, m.LABEL_ZONE, m.DO_NOT_SCHEDULE, None)]))
+    bad.append(P.Profile(pts_system_defaulted=False, pts_default_constraints=[
+        m.TopologySpreadConstraint(1, m.LABEL_ZONE, m.DO_NOT_SCHEDULE, None),
+        m.TopologySpreadConstraint(2, m.LABEL_ZONE, m.DO_NOT_SCHEDULE, None)]))
+    for prof in bad:
+        with pytest.raises(S.SnapshotError):
+            S.Snapshot(prof)
+
+
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_golden_cases(built, name):
     c = CASES[name]

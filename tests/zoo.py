@@ -164,3 +164,30 @@ def zoo(seed: int, n_nodes: int = 24, n_pods: int = 160, apps: int = 5, zones: i
     if seed % 4 == 2:
         prof.hard_pod_affinity_weight = 5
     return nodes, pods, prof
+
+
+# shapes of NodeResourcesFit RequestedToCapacityRatio (utilization, score 0..10):
+# bin packing, spreading, and one starting above 0 % and ending below 100 %
+RTCR_SHAPES = [[(0, 0), (100, 10)], [(0, 10), (40, 6), (100, 0)], [(20, 3), (60, 9), (90, 2)]]
+
+
+def zoo_args(seed: int, kind: str, **kw):
+    """zoo() under a profile with the plugin args the evaluator models beyond
+    the defaults: "rtcr" (NodeResourcesFit RequestedToCapacityRatio, a shape
+    per seed) or "pts-list" (PodTopologySpread defaultingType List with
+    defaultConstraints, hard and soft, applied to the pods that have owners
+    but no constraints of their own)."""
+    nodes, pods, prof = zoo(seed, **kw)
+    if kind == "rtcr":
+        prof.fit_strategy = P.REQUESTED_TO_CAPACITY_RATIO
+        prof.fit_shape = list(RTCR_SHAPES[seed % len(RTCR_SHAPES)])
+    elif kind == "pts-list":
+        prof.pts_system_defaulted = False
+        prof.pts_default_constraints = [
+            m.TopologySpreadConstraint(1 + seed % 2, m.LABEL_ZONE, m.DO_NOT_SCHEDULE, None),
+            m.TopologySpreadConstraint(2, m.LABEL_HOSTNAME, m.SCHEDULE_ANYWAY, None,
+                                       node_taints_policy=m.POLICY_HONOR if seed % 2 else None),
+        ]
+    else:
+        raise ValueError(kind)
+    return nodes, pods, prof
