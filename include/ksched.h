@@ -133,7 +133,7 @@ typedef struct ksg_topology {
 } ksg_topology;
 
 /* ---- pods ----------------------------------------------------------------
- * Encoded pod (144 B).  Variable-length parts live in a shared int32 program
+ * Encoded pod (152 B).  Variable-length parts live in a shared int32 program
  * pool; offsets are word indices into it, -1 = absent.  See encoder.py for
  * the program grammar.                                                      */
 #define KSG_POD_TOL_UNSCHED (1u << 0)   /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
@@ -160,6 +160,8 @@ typedef struct ksg_pod {
   int32_t blob;              /* tol..ports programs are contiguous:            */
   int32_t blob_len;          /*   prog[blob, blob + blob_len) (staged into LDS) */
   int32_t ports;             /* NodePorts program: conflicting host-port ids, own ids */
+  int32_t vol;               /* volume plugins' Filter program (pods with claims) */
+  int32_t pad;
 } ksg_pod;
 
 typedef struct ksg_workload {

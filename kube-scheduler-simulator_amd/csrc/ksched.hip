@@ -517,9 +517,11 @@ int check_supported(ksg_ctx* ctx, const ksg_profile& prof, int first, int count)
 // Any pod of [first, first + count) with host ports (NodePorts reads and its
 // assume writes the node's UsedPorts: the queue kernels and the per-cycle
 // path model that; the batched, sweep and chip-wide topology paths do not).
+// Pods with claims (a volume program) take the same paths: only the queue
+// kernels' evaluator (eval_node_src) runs the volume plugins' Filter.
 bool range_has_ports(const ksg_ctx* ctx, int first, int count) {
   for (int i = first; i < first + count; i++)
-    if (ctx->h_pods[i].ports >= 0) return true;
+    if (ctx->h_pods[i].ports >= 0 || ctx->h_pods[i].vol >= 0) return true;
   return false;
 }
 
@@ -2416,7 +2418,7 @@ int dgrow(ksg_ctx* ctx, T** p, size_t* cap, size_t used, size_t need) {
 // relative to the staged blob), the blob inside the pool of `len` words.
 bool pod_offsets_ok(const ksg_pod& p, int64_t len) {
   if (p.blob < 0 || p.blob_len < 0 || (int64_t)p.blob + p.blob_len > len) return false;
-  for (int32_t off : {p.tol, p.na_req, p.na_pref, p.img, p.pts, p.ipa, p.commit, p.ports})
+  for (int32_t off : {p.tol, p.na_req, p.na_pref, p.img, p.pts, p.ipa, p.commit, p.ports, p.vol})
     if (off >= 0 && (off < p.blob || off >= p.blob + p.blob_len)) return false;
   return true;
 }
@@ -2480,6 +2482,65 @@ int flush_commit(ksg_ctx* ctx) {
   return KSG_OK;
 }
 
+// The pod's volume program (encoder.py Encoder._volume_plan grammar) lies
+// inside its blob and names only label columns < L and node indices < N:
+// vol_filter (ksched_device.h) walks it without bounds checks.
+template <class At>
+bool vol_prog_ok(const ksg_pod& p, int L, int N, At at) {
+  if (p.vol < 0) return true;
+  const int64_t end = (int64_t)p.blob + p.blob_len;
+  int64_t w = p.vol;
+  auto take = [&](int64_t& v) {
+    if (w >= end) return false;
+    v = at(w++);
+    return true;
+  };
+  auto col_ok = [&](int64_t c) { return c >= 0 && c < L; };
+  auto req_ok = [&]() {   // col op n values
+    int64_t col, op, n;
+    if (!take(col) || !take(op) || !take(n) || n < 0 || w + n > end) return false;
+    if (op != 6 && !col_ok(col)) return false;
+    w += n;
+    return true;
+  };
+  auto terms_ok = [&](int64_t nt) {
+    for (int64_t t = 0; t < nt; t++) {
+      int64_t nr;
+      if (!take(nr) || nr < 0) return false;
+      for (int64_t r = 0; r < nr; r++)
+        if (!req_ok()) return false;
+    }
+    return true;
+  };
+  int64_t flags, nb, np, nz;
+  if (!take(flags) || !take(nb) || nb < 0) return false;
+  for (int64_t b = 0; b < nb; b++) {
+    int64_t kind, nt;
+    if (!take(kind)) return false;
+    if (kind == 0) continue;
+    if (kind != 1 || !take(nt) || nt < -1 || !terms_ok(nt)) return false;
+  }
+  if (!take(np) || np < 0) return false;
+  for (int64_t k = 0; k < np; k++) {
+    int64_t sel, nt;
+    if (!take(sel) || sel < -2 || sel >= N || !take(nt) || nt < -1 || !terms_ok(nt)) return false;
+  }
+  for (int k = 0; k < 4; k++) {
+    int64_t c;
+    if (!take(c) || (c != -1 && !col_ok(c))) return false;
+  }
+  if (!take(nz) || nz < 0) return false;
+  for (int64_t k = 0; k < nz; k++) {
+    int64_t col, gcol, n;
+    if (!take(col) || !take(gcol) || !col_ok(col) || !col_ok(gcol)) return false;
+    for (int part = 0; part < 2; part++) {
+      if (!take(n) || n < 0 || w + n > end) return false;
+      w += n;
+    }
+  }
+  return true;
+}
+
 // An assume the per-cycle kernel can apply: node columns only (no selector
 // counts, template tables or host ports).
 bool commit_deferrable(const ksg_ctx* ctx, int32_t pod) {
@@ -2508,6 +2569,10 @@ int append_internal(ksg_ctx* ctx, const ksg_pod* pods, int32_t n, const int32_t*
           return k >= prog_base ? prog[k - prog_base] : ctx->h_prog[k];
         }))
       return fail(ctx, KSG_E_INVALID, "appended pod: host-port ids outside the vocabulary");
+    if (!vol_prog_ok(p, ctx->c.L, N, [&](int64_t k) -> int64_t {
+          return k >= prog_base ? prog[k - prog_base] : ctx->h_prog[k];
+        }))
+      return fail(ctx, KSG_E_INVALID, "appended pod: malformed volume program");
     used = std::max(used, pod_prog_end(p, N));
     max_blob = std::max(max_blob, p.blob_len);
   }
@@ -2812,6 +2877,8 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
     if (!pod_offsets_ok(p, wl->prog_len)) return fail(ctx, KSG_E_INVALID, "pod program outside its blob / the pool");
     if (!ports_prog_ok(p, ctx->c.PW, [&](int64_t k) -> int64_t { return prog[k]; }))
       return fail(ctx, KSG_E_INVALID, "pod " + std::to_string(i) + ": host-port ids outside the vocabulary");
+    if (!vol_prog_ok(p, ctx->c.L, ctx->c.N, [&](int64_t k) -> int64_t { return prog[k]; }))
+      return fail(ctx, KSG_E_INVALID, "pod " + std::to_string(i) + ": malformed volume program");
     if (p.node_set >= 0 && (int64_t)p.node_set + (ctx->c.N + 31) / 32 > wl->prog_len)
       return fail(ctx, KSG_E_INVALID, "node set outside the program pool");
     ctx->h_na_pref_sum[i] = na_pref_weight_sum(prog, p);

@@ -263,6 +263,24 @@ bool filter_message(const ksg_annotator* a, uint32_t st, int n, std::string& msg
       else if (reason == 3) msg = "node(s) didn't satisfy existing pods anti-affinity rules";
       else return false;
       return true;
+    case KSG_PL_VOLUME_RESTRICTIONS:
+      msg = "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode";
+      return true;
+    case KSG_PL_VOLUME_BINDING: {   // FindPodVolumes' reason order
+      static const char* const kVb[3] = {"node(s) had volume node affinity conflict",
+                                         "node(s) didn't find available persistent volumes to bind",
+                                         "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"};
+      if (!reason || reason > 7) return false;
+      for (int b = 0; b < 3; b++)
+        if (reason & (1u << b)) {
+          if (!msg.empty()) msg += ", ";
+          msg += kVb[b];
+        }
+      return true;
+    }
+    case KSG_PL_VOLUME_ZONE:
+      msg = "node(s) had no available volume zone";
+      return true;
     default:
       return false;
   }

@@ -243,6 +243,88 @@ __device__ __forceinline__ int64_t na_pref_score(const Src& nd, const int32_t* P
   return s;
 }
 
+// ---- volume plugins' Filter over the pod's volume program ----------------
+// (encoder.py Encoder._volume_plan grammar; upstream v1.32
+// volumerestrictions.Filter's ReadWriteOncePod check, volumebinding
+// FindPodVolumes (checkBoundClaims, the selected-node fast path,
+// checkVolumeProvisions), volumezone.Filter)
+struct VolVerdict {
+  bool rwop;          // VolumeRestrictions: a running pod holds a ReadWriteOncePod claim
+  uint32_t vb;        // VolumeBinding reason bits: 1 node conflict, 2 bind conflict, 4 PV missing
+  bool vz;            // VolumeZone: no available volume zone
+};
+
+template <class Src>
+__device__ __forceinline__ bool any_term(const Src& nd, const int32_t*& w, int nt) {
+  bool any = false;
+  for (int t = 0; t < nt; t++) any = eval_term(nd, w) || any;
+  return any;
+}
+
+template <class Src>
+__device__ __forceinline__ VolVerdict vol_filter(const Src& nd, const int32_t* P, int vol, int n) {
+  VolVerdict r{false, 0, false};
+  const int32_t* w = P + vol;
+  r.rwop = (*w++ & 1) != 0;
+  // bound claims, in volume order: the first missing PV or affinity mismatch ends the check
+  const int nb = *w++;
+  bool done = false;
+  for (int b = 0; b < nb; b++) {
+    const int kind = *w++;
+    if (kind == 0) {
+      if (!done) r.vb |= 4u;
+      done = true;
+      continue;
+    }
+    const int nt = *w++;
+    if (nt < 0) continue;
+    const bool ok = any_term(nd, w, nt);
+    if (!done && !ok) {
+      r.vb |= 1u;
+      done = true;
+    }
+  }
+  // unbound WaitForFirstConsumer claims: selected node, then provisioning
+  const int np = *w++;
+  bool prov_ok = true;
+  for (int k = 0; k < np; k++) {
+    const int sel = *w++;
+    const int nt = *w++;
+    if (sel != -1 && sel != n) prov_ok = false;
+    if (nt < 0) prov_ok = false;
+    else if (nt > 0 && !any_term(nd, w, nt)) prov_ok = false;
+  }
+  if (!prov_ok) r.vb |= 2u;
+  // VolumeZone: a node without any topology label passes
+  bool constrained = false;
+  for (int k = 0; k < 4; k++) {
+    const int col = w[k];
+    constrained = constrained || (col >= 0 && nd.label(col) != 0);
+  }
+  w += 4;
+  const int nz = *w++;
+  for (int k = 0; k < nz; k++) {
+    const int col = w[0], gcol = w[1];
+    const int nv = w[2];
+    const int32_t* ids = w + 3;
+    const int ng = w[3 + nv];
+    const int32_t* gids = w + 4 + nv;
+    w += 4 + nv + ng;
+    uint32_t v = nd.label(col);
+    const int32_t* set = ids;
+    int ns = nv;
+    if (!v) {   // the beta label missing: the GA one
+      v = nd.label(gcol);
+      set = gids;
+      ns = ng;
+    }
+    bool hit = false;
+    for (int i = 0; i < ns; i++) hit |= (uint32_t)set[i] == v;
+    if (constrained && (!v || !hit)) r.vz = true;
+  }
+  return r;
+}
+
 __device__ __forceinline__ bool tol_bit(const int32_t* tolp, uint32_t vid) {
   return (((uint32_t)tolp[vid >> 5]) >> (vid & 31)) & 1u;
 }

@@ -100,6 +100,7 @@ struct PodView {
   uint32_t smask;            // score plugins run (enabled and not PreScore Skip)
   int64_t w_fit, w_ba, w_img, w_t, w_a;
   int ports;                 // NodePorts program (blob-relative), -1 = none
+  int vol;                   // volume plugins' program (blob-relative), -1 = none
   const uint32_t* used_ports;   // the replica's UsedPorts bitmaps (set by kernels that evaluate NodePorts)
 };
 
@@ -119,6 +120,7 @@ __device__ __forceinline__ PodView make_view(const DevCluster& c, const ksg_prof
   v.img = rb(p.img);
   v.commit = rb(p.commit);
   v.ports = rb(p.ports);
+  v.vol = rb(p.vol);
   v.used_ports = used_ports;
   v.tolf = P + rb(p.tol);
   v.tolp = v.tolf + c.W;
@@ -544,6 +546,20 @@ __device__ __forceinline__ NodeEval eval_node_src(const DevCluster& c, const ksg
             const uint32_t r = ipa_filter_node(c, *tc, n);
             if (r) st = (uint32_t)(pl + 1) | (r << 8);
           }
+          break;
+        // volume plugins: reached only by pods with claims (PreFilter Skip
+        // otherwise); NodeVolumeLimits passes (no CSI attach limits modelled)
+        case KSG_PL_VOLUME_RESTRICTIONS:
+          if (v.vol >= 0 && (v.P[v.vol] & 1)) st = pl + 1;
+          break;
+        case KSG_PL_VOLUME_BINDING:
+          if (v.vol >= 0) {
+            const VolVerdict r = vol_filter(nd, v.P, v.vol, n);
+            if (r.vb) st = (uint32_t)(pl + 1) | (r.vb << 8);
+          }
+          break;
+        case KSG_PL_VOLUME_ZONE:
+          if (v.vol >= 0 && vol_filter(nd, v.P, v.vol, n).vz) st = pl + 1;
           break;
         default:
           break;

@@ -1289,6 +1289,8 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
   // ports := n_conf conf[n_conf] n_own own[n_own] (HostPortInfo.CheckConflict
   // over the vocabulary; own = what the pod's assume adds to UsedPorts)
   rec.ports = -1;
+  rec.vol = -1;   // claims are refused at ksg_snapshot_add_pod (volume programs: encoder.py only)
+  rec.pad = 0;
   if (!hports.empty()) {
     std::set<int32_t> conf, own;
     for (auto& hp : hports) {

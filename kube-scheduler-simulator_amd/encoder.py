@@ -75,14 +75,21 @@ POD_FLAG_NA_REQUIRED = 1 << 1
 POD_FLAG_BEST_EFFORT = 1 << 2
 POD_FLAG_PREFILTER_REJECT = 1 << 3
 
+VOLUME_PLUGINS = (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE)
+# the volume program's flag word (_vol) and VolumeBinding's Filter reason bits
+VOL_RWOP_CONFLICT = 1 << 0        # VolumeRestrictions rejects every node
+VB_NODE_CONFLICT, VB_BIND_CONFLICT, VB_PV_NOT_EXIST = 1, 2, 4
+MSG_VB_UNBOUND_IMMEDIATE = "pod has unbound immediate PersistentVolumeClaims"
+MSG_NA_CONFLICT = "pod affinity terms conflict"   # NodeAffinity PreFilter (errReasonConflict)
+
 POD_DTYPE = np.dtype([
     ("req", "<i8", (MAX_RES,)), ("nz_cpu", "<i8"), ("nz_mem", "<i8"),
     ("flags", "<u4"), ("filter_skip", "<u4"), ("score_skip", "<u4"),
     ("node_name", "<i4"), ("n_containers", "<i4"), ("tol", "<i4"), ("na_req", "<i4"),
     ("na_pref", "<i4"), ("img", "<i4"), ("node_set", "<i4"), ("pts", "<i4"), ("ipa", "<i4"),
-    ("commit", "<i4"), ("blob", "<i4"), ("blob_len", "<i4"), ("ports", "<i4"),
+    ("commit", "<i4"), ("blob", "<i4"), ("blob_len", "<i4"), ("ports", "<i4"), ("vol", "<i4"), ("pad", "<i4"),
 ])
-assert POD_DTYPE.itemsize == 144
+assert POD_DTYPE.itemsize == 152
 
 SYSTEM_DEFAULT_SPREAD = ((3, m.LABEL_HOSTNAME), (5, m.LABEL_ZONE))  # (maxSkew, key), ScheduleAnyway
 
@@ -235,10 +242,14 @@ class EncodedWorkload:
 class Encoder:
     """Encodes nodes and every pod that will ever be bound or scheduled."""
 
-    def __init__(self, nodes: Sequence[m.Node], pods: Sequence[m.Pod], prof: P.Profile):
+    def __init__(self, nodes: Sequence[m.Node], pods: Sequence[m.Pod], prof: P.Profile,
+                 bound_pods: Sequence[int] = ()):
+        """`bound_pods`: indices of the pods already running when the queue
+        starts (they count as users of their claims for VolumeRestrictions)."""
         self.nodes = list(nodes)
         self.pods = list(pods)
         self.prof = prof
+        self.bound_pods = set(int(i) for i in bound_pods)
         self.N = len(self.nodes)
         self.node_index = {n.name: i for i, n in enumerate(self.nodes)}
         if len(self.node_index) != self.N:
@@ -249,6 +260,13 @@ class Encoder:
         # NodeAffinity PreFilterResult.NodeNames per pod (sorted; upstream's
         # sets.UnsortedList order is random)
         self.prefilter_node_names: Dict[int, List[str]] = {}
+        # PreFilterResult node names per pod and plugin id (NodeAffinity,
+        # VolumeBinding), and the PreFilter that ended a pod's cycle: (plugin
+        # id, its status message; None = the plugin returned success with
+        # node names, and the framework's merge of the results left none)
+        self.prefilter_results: Dict[int, Dict[int, List[str]]] = {}
+        self.prefilter_reject: Dict[int, Tuple[int, Optional[str]]] = {}
+        self._vol_outcome: Dict[int, dict] = {}   # _volume_plan's PreFilter outcomes, consumed by _encode_pods
         self._build_resources()
         self._build_label_columns()
         self._build_taints()
@@ -306,6 +324,239 @@ class Encoder:
         own = sorted({self.port_id[t] for t in want})
         return self._emit([len(conf)] + sorted(conf) + [len(own)] + own)
 
+    # -------------------------------------------------------------- volumes
+    # VolumeRestrictions / NodeVolumeLimits / VolumeBinding / VolumeZone for
+    # pods with persistentVolumeClaim volumes [upstream v1.32
+    # plugins/volumerestrictions/volume_restrictions.go, nodevolumelimits/
+    # csi.go, volumebinding/{volume_binding,binder}.go, volumezone/
+    # volume_zone.go; not vendored: parity unpinned, DESIGN.md §9].  PreFilter
+    # is decided here, per pod; the per-node Filter predicates go to the
+    # device as the pod's volume program (_volume_plan's grammar below).
+    def _volume_label_keys(self, p: m.Pod):
+        """Node label keys the pod's volume program reads."""
+        keys = set()
+        st = p.storage
+        if not p.claim_names() or st is None:
+            return keys
+        keys.update(m.VOLUME_ZONE_LABELS)
+        for c in p.claim_names():
+            pvc = st.claim(p.namespace, c)
+            if pvc is None:
+                continue
+            pv = st.pvs.get(pvc.volume_name) if pvc.volume_name else None
+            if pv is not None:
+                for t in pv.node_affinity or ():
+                    keys.update(r.key for r in t.match_expressions)
+            cls = st.classes.get(pvc.storage_class) if pvc.storage_class else None
+            if cls is not None:
+                for term in cls.allowed_topologies:
+                    keys.update(k for k, _ in term)
+        return keys
+
+    @staticmethod
+    def _label_zones(pv: m.PersistentVolume, value: str):
+        """volumehelpers.LabelZonesToSet: "__"-separated, no blank member."""
+        zones = [z.strip() for z in value.split("__")]
+        if any(not z for z in zones):
+            raise NotImplementedError(f"PersistentVolume {pv.name}: zone label {value!r} has an empty member")
+        return sorted(set(zones))
+
+    def _volume_plan(self, i: int, p: m.Pod):
+        """(PreFilter Skip bits of the four volume plugins, the volume program
+        words or None); the plugins' PreFilter outcomes (rejection message,
+        VolumeBinding's PreFilterResult node names) go to self._vol_outcome[i]
+        for the ordered PreFilter pass in _encode_pods.
+
+        Volume program (word offsets, the pod's blob):
+          flags                    VOL_RWOP_CONFLICT
+          n_bound, n_bound x [kind, ...]   VolumeBinding checkBoundClaims, in
+                                   volume order: kind 0 = the PV does not
+                                   exist; kind 1 = nterms, terms (the PV's
+                                   required node affinity on labels only:
+                                   CheckNodeAffinity's node has no name, so
+                                   matchFields never constrain)
+          n_prov, n_prov x [sel, nterms, terms]  the unbound
+                                   WaitForFirstConsumer claims: sel = node
+                                   index of the claim's selected-node
+                                   annotation (-1 none, -2 not in the
+                                   snapshot); nterms = -1 for a class that
+                                   cannot provision (BindConflict
+                                   everywhere), else allowedTopologies as In
+                                   terms (0 terms: every node)
+          zc[4]                    label columns of volumezone.topologyLabels
+          n_zone, n_zone x [col, ga_col, n, ids..., n_ga, ids...]
+        """
+        all_skip = sum(1 << v for v in VOLUME_PLUGINS)
+        claims = p.claim_names()
+        if not claims:
+            return all_skip, None
+        st = p.storage or m.Storage()
+        ns = p.namespace
+        out = {}
+        skip = 0
+        missing = next((c for c in claims if st.claim(ns, c) is None), None)
+        nf = f'persistentvolumeclaim "{missing}" not found'
+        flags = 0
+        # VolumeRestrictions: needsRestrictionsCheck (a claim) -> readWriteOncePodPVCsForPod
+        if missing is not None:
+            out[P.VOLUME_RESTRICTIONS] = ("reject", nf)
+        else:
+            for c in claims:
+                if m.READ_WRITE_ONCE_POD not in st.claim(ns, c).access_modes:
+                    continue
+                others = self._claim_users.get((ns, c), set()) - {i}
+                if i not in self.bound_pods and any(u not in self.bound_pods for u in others):
+                    raise NotImplementedError(
+                        f"pod {ns}/{p.name}: ReadWriteOncePod claim {c!r} is shared with another queued pod "
+                        f"(whose placement decides the conflict)")
+                if others:   # StorageInfos.IsPVCUsedByPods: a running pod holds it
+                    flags |= VOL_RWOP_CONFLICT
+        # NodeVolumeLimits: PreFilter runs for claims; its Filter passes while no
+        # node publishes CSI attach limits (checked at ingest)
+        # VolumeBinding: podHasPVCs, GetPodVolumeClaims, GetEligibleNodes
+        bound, prov = [], []
+        vb = None
+        for c in claims:
+            pvc = st.claim(ns, c)
+            if pvc is None:
+                vb = ("reject", nf)
+                break
+            if pvc.deleting:
+                vb = ("reject", f'persistentvolumeclaim "{c}" is being deleted')
+                break
+        if vb is None:
+            immediate = False
+            for c in claims:
+                pvc = st.claim(ns, c)
+                if pvc.fully_bound():
+                    bound.append(pvc)
+                    continue
+                cls = st.classes.get(pvc.storage_class) if pvc.storage_class else None
+                if cls is not None and cls.binding_mode == m.BINDING_WAIT_FOR_FIRST_CONSUMER and not pvc.volume_name:
+                    prov.append((pvc, cls))
+                else:
+                    immediate = True
+            if immediate:
+                vb = ("reject", MSG_VB_UNBOUND_IMMEDIATE)
+        if vb is None:
+            eligible = None
+            for pvc in bound:   # GetEligibleNodes: local volumes' hostname In values
+                pv = st.pvs.get(pvc.volume_name)
+                if pv is None:
+                    eligible = None
+                    break
+                names = set()   # util.GetLocalPersistentVolumeNodeNames
+                for t in pv.node_affinity or ():
+                    tn = None
+                    for r in t.match_expressions:
+                        if r.key == m.LABEL_HOSTNAME and r.operator == m.IN:
+                            tn = set(r.values) if tn is None else tn & set(r.values)
+                    names |= tn or set()
+                if names:
+                    eligible = names if eligible is None else eligible & names
+            if eligible is not None:
+                vb = ("names", eligible)
+            for pvc, cls in prov:
+                for pv in st.pvs.values():
+                    if pv.storage_class == pvc.storage_class and pv.claim_ref in (None, (ns, pvc.name)):
+                        raise NotImplementedError(
+                            f"pod {ns}/{p.name}: claim {pvc.name!r} could bind statically to PersistentVolume "
+                            f"{pv.name!r} (findMatchingVolumes is not modelled)")
+                if i not in self.bound_pods and self._claim_users.get((ns, pvc.name), set()) - {i}:
+                    raise NotImplementedError(
+                        f"pod {ns}/{p.name}: unbound claim {pvc.name!r} is shared with another pod "
+                        f"(its assumed binding is not modelled)")
+        if vb is not None:
+            out[P.VOLUME_BINDING] = vb
+        # VolumeZone: getPVbyPod
+        zone = []
+        vz = None
+        for c in claims:
+            if not c:
+                vz = ("reject", "PersistentVolumeClaim had no name")
+                break
+            pvc = st.claim(ns, c)
+            if pvc is None:
+                vz = ("reject", f'persistentvolumeclaim "{c}" not found')
+                break
+            if not pvc.volume_name:
+                sc = pvc.storage_class
+                if not sc:
+                    vz = ("reject", "PersistentVolumeClaim had no pv name and storageClass name")
+                    break
+                cls = st.classes.get(sc)
+                if cls is None:
+                    vz = ("reject", f'storageclass.storage.k8s.io "{sc}" not found')
+                    break
+                if cls.binding_mode == m.BINDING_WAIT_FOR_FIRST_CONSUMER:
+                    continue
+                vz = ("reject", "PersistentVolume had no name")
+                break
+            pv = st.pvs.get(pvc.volume_name)
+            if pv is None:
+                vz = ("reject", f'persistentvolume "{pvc.volume_name}" not found')
+                break
+            for key in m.VOLUME_ZONE_LABELS:
+                if key in pv.labels:
+                    zone.append((key, self._label_zones(pv, pv.labels[key])))
+        if vz is not None:
+            out[P.VOLUME_ZONE] = vz
+        elif not zone:
+            skip |= 1 << P.VOLUME_ZONE
+        self._vol_outcome[i] = out
+        # ---- the Filter program
+        words = [flags, len(bound)]
+        for pvc in bound:
+            pv = st.pvs.get(pvc.volume_name)
+            if pv is None:
+                words.append(0)
+                continue
+            if pv.source in m.PV_SOURCES_MIGRATED:
+                raise NotImplementedError(f"PersistentVolume {pv.name}: {pv.source} (CSI translation not modelled)")
+            if pv.node_affinity is None:
+                words += [1, -1]
+                continue
+            terms = []
+            for t in pv.node_affinity:
+                if not t.match_expressions:
+                    if t.match_fields:   # fields only: the nameless node matches
+                        terms = None
+                        break
+                    terms.append([0])    # an empty term matches nothing
+                    continue
+                tw = [len(t.match_expressions)]
+                for r in t.match_expressions:
+                    tw += self._requirement(r)
+                terms.append(tw)
+            if terms is None:
+                words += [1, -1]
+            else:
+                words += [1, len(terms)] + [x for tw in terms for x in tw]
+        words.append(len(prov))
+        for pvc, cls in prov:
+            sel_name = pvc.annotations.get(m.ANN_SELECTED_NODE)
+            sel = -1 if sel_name is None else self.node_index.get(sel_name, -2)
+            if cls.provisioner in ("", m.NOT_SUPPORTED_PROVISIONER):
+                words += [sel, -1]
+                continue
+            words += [sel, len(cls.allowed_topologies)]
+            for term in cls.allowed_topologies:
+                words.append(len(term))
+                for key, vals in term:
+                    col = self.col_index[key]
+                    ids = sorted({self._value_id(col, v) for v in vals})
+                    words += [col, OP_IN, len(ids)] + ids if ids else [0, OP_NEVER, 0]
+        words += [self.col_index.get(k, -1) for k in m.VOLUME_ZONE_LABELS]
+        words.append(len(zone))
+        for key, vals in zone:
+            col = self.col_index[key]
+            ga = m.GA_LABEL.get(key, key)
+            gcol = self.col_index[ga]
+            ids = sorted({self._value_id(col, v) for v in vals})
+            gids = sorted({self._value_id(gcol, v) for v in vals})
+            words += [col, gcol, len(ids)] + ids + [len(gids)] + gids
+        return skip, words
+
     # -------------------------------------------------------------- labels
     def _pts_constraints(self, pod: m.Pod):
         """(hard, soft) lists of (max_skew, key, canon_selector, min_domains,
@@ -361,6 +612,7 @@ class Encoder:
                 keys.add(t.topology_key)
             for w in p.pod_affinity_preferred + p.pod_anti_affinity_preferred:
                 keys.add(w.term.topology_key)
+            keys.update(self._volume_label_keys(p))
         self.label_cols = sorted(keys)
         if uses_name_field:
             self.label_cols.append(m.OBJECT_NAME_FIELD)
@@ -715,16 +967,18 @@ class Encoder:
 
     def _encode_pods(self) -> EncodedWorkload:
         prof = self.prof
-        vol = {P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE}
-        vol_run = vol & (set(prof.prefilter_order()) | set(prof.filter_order()))
+        vol_run = set(VOLUME_PLUGINS) & (set(prof.prefilter_order()) | set(prof.filter_order()))
         if vol_run:
             for p in self.pods:
                 bad = p.volumes_needing_plugins()
                 if bad:
                     raise NotImplementedError(
                         f"pod {p.namespace}/{p.name}: volume {bad[0][0]!r} ({bad[0][1]}) makes the volume plugins' "
-                        f"PreFilter run; VolumeBinding / VolumeZone / NodeVolumeLimits / VolumeRestrictions are "
-                        f"modelled only as their Skip")
+                        f"PreFilter run; of the volume sources only persistentVolumeClaim is modelled")
+        self._claim_users: Dict[Tuple[str, str], set] = {}
+        for i, p in enumerate(self.pods):
+            for c in p.claim_names():
+                self._claim_users.setdefault((p.namespace, c), set()).add(i)
         rec = np.zeros(len(self.pods), POD_DTYPE)
         names = []
         ba_cols = [self.res_col[r] for r, _ in prof.ba_resources if r in self.res_col]
@@ -751,8 +1005,8 @@ class Encoder:
                 fskip |= 1 << P.NODE_AFFINITY
             if not p.host_ports():
                 fskip |= 1 << P.NODE_PORTS     # nodeports PreFilter: Skip without host ports
-            for v in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE):
-                fskip |= 1 << v   # no claim / ephemeral / in-tree disk volume (checked above): PreFilter Skip
+            vskip, vol_words = self._volume_plan(i, p) if vol_run else (sum(1 << v for v in VOLUME_PLUGINS), None)
+            fskip |= vskip   # PreFilter Skip of the volume plugins (all four for a pod without claims)
             hard, soft = self._pts_cache[i]
             if not hard:
                 fskip |= 1 << P.POD_TOPOLOGY_SPREAD
@@ -766,8 +1020,11 @@ class Encoder:
             has_pref_pod_aff = bool(p.pod_affinity_preferred or p.pod_anti_affinity_preferred)
             if prof.ignore_preferred_terms_of_existing_pods and not has_pref_pod_aff:
                 sskip |= 1 << P.INTER_POD_AFFINITY
+            # PreFilter outcomes in the profile's PreFilter order (RunPreFilterPlugins):
+            # the first rejection ends the cycle; PreFilterResults merge by
+            # intersection, and an empty merge ends it too (framework message)
+            outcome = dict(self._vol_outcome.pop(i, {}))
             # NodeAffinity PreFilter: matchFields metadata.name In -> PreFilterResult
-            e["node_set"] = -1
             if p.node_affinity_required:
                 names_u = None
                 all_named = True
@@ -782,11 +1039,26 @@ class Encoder:
                         break
                     names_u = tn if names_u is None else names_u | tn
                 if all_named and names_u is not None:
-                    if not names_u:
+                    outcome[P.NODE_AFFINITY] = ("reject", MSG_NA_CONFLICT) if not names_u else ("names", names_u)
+            e["node_set"] = -1
+            merged = None
+            for pid in prof.prefilter_order():
+                kind, val = outcome.get(pid, ("ok", None))
+                if kind == "reject":
+                    flags |= POD_FLAG_PREFILTER_REJECT
+                    self.prefilter_reject[i] = (pid, val)
+                    break
+                if kind == "names":
+                    self.prefilter_results.setdefault(i, {})[pid] = sorted(val)
+                    if pid == P.NODE_AFFINITY:
+                        self.prefilter_node_names[i] = sorted(val)
+                    merged = set(val) if merged is None else merged & set(val)
+                    if not merged:
                         flags |= POD_FLAG_PREFILTER_REJECT
-                    else:
-                        e["node_set"] = self._node_set(names_u)
-                        self.prefilter_node_names[i] = sorted(names_u)
+                        self.prefilter_reject[i] = (pid, None)
+                        break
+            if merged and not flags & POD_FLAG_PREFILTER_REJECT:
+                e["node_set"] = self._node_set(merged)
             e["flags"] = flags
             e["filter_skip"] = fskip
             e["score_skip"] = sskip
@@ -804,6 +1076,7 @@ class Encoder:
             e["ipa"] = self._ipa(i, p)
             e["commit"] = self._commit(i)
             e["ports"] = self._ports(p)
+            e["vol"] = self._emit(vol_words) if vol_words is not None else -1
             e["blob"] = blob
             e["blob_len"] = len(self.prog) - blob
             self.max_blob = max(self.max_blob, len(self.prog) - blob)

@@ -45,6 +45,20 @@ MSG_PTS_LABEL = MSG_PTS + " (missing required label)"
 MSG_IPA = {1: "node(s) didn't match pod affinity rules",
            2: "node(s) didn't match pod anti-affinity rules",
            3: "node(s) didn't satisfy existing pods anti-affinity rules"}
+# volume plugins [upstream v1.32 volumerestrictions ErrReasonReadWriteOncePodConflict,
+# volumebinding ErrReason* (FindPodVolumes order), volumezone ErrReasonConflict]
+MSG_RWOP = "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode"
+MSG_VB = ((E.VB_NODE_CONFLICT, "node(s) had volume node affinity conflict"),
+          (E.VB_BIND_CONFLICT, "node(s) didn't find available persistent volumes to bind"),
+          (E.VB_PV_NOT_EXIST, "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"))
+MSG_VZ = "node(s) had no available volume zone"
+
+
+def prefilter_framework_message(plugins: Sequence[str]) -> str:
+    """RunPreFilterPlugins' status when the merged PreFilterResults leave no node."""
+    if len(plugins) == 1:
+        return f"node(s) didn't satisfy plugin {plugins[0]}"
+    return f"node(s) didn't satisfy plugin(s) [{' '.join(plugins)}] simultaneously"
 
 
 def fit_reasons(bits: int, res_names: Sequence[str]) -> List[str]:
@@ -88,6 +102,12 @@ class Decoder:
             return MSG_PTS_LABEL if reason == 1 else MSG_PTS
         if pl == P.INTER_POD_AFFINITY:
             return MSG_IPA[reason]
+        if pl == P.VOLUME_RESTRICTIONS:
+            return MSG_RWOP
+        if pl == P.VOLUME_BINDING:
+            return ", ".join(msg for bit, msg in MSG_VB if reason & bit)
+        if pl == P.VOLUME_ZONE:
+            return MSG_VZ
         raise ValueError(f"unexpected status word {st:#x}")
 
 
@@ -104,7 +124,8 @@ def status_code(st: int, enc: E.Encoder, pod: int, node: int) -> int:
     reason = st >> 8
     if pl < 0:
         return Status.SUCCESS
-    if pl in (P.NODE_UNSCHEDULABLE, P.NODE_NAME, P.TAINT_TOLERATION, P.NODE_AFFINITY):
+    if pl in (P.NODE_UNSCHEDULABLE, P.NODE_NAME, P.TAINT_TOLERATION, P.NODE_AFFINITY, P.VOLUME_BINDING,
+              P.VOLUME_ZONE):
         return Status.UNSCHEDULABLE_AND_UNRESOLVABLE
     if pl == P.NODE_RESOURCES_FIT:
         req = enc.workload.pods[pod]["req"]
@@ -144,7 +165,7 @@ class DebuggableScheduler:
         self.nodes = list(nodes)
         self.pods = list(pods)
         self.prof = prof
-        self.enc = E.Encoder(self.nodes, self.pods, prof)
+        self.enc = E.Encoder(self.nodes, self.pods, prof, bound_pods=[pi for pi, _ in bound])
         self.engine = engine if engine is not None else native.Engine()
         self.engine.load(self.enc, E.encode_profile(prof, self.enc.cluster.res_names))
         # NodeInfo.Pods per node (pod indices): DefaultPreemption's victims
@@ -188,14 +209,16 @@ class DebuggableScheduler:
         return self._cycle(pi, record)
 
     @staticmethod
-    def rejecting_plugins(cyc: PodCycle, enc_pod) -> set:
+    def rejecting_plugins(cyc: PodCycle, enc_pod, reject=None) -> set:
         """diagnosis.UnschedulablePlugins of a failed cycle: the plugin of
-        every node's first rejection (NodeAffinity for a PreFilter reject)."""
+        every node's first rejection, or the PreFilter plugin that ended the
+        cycle (`reject` = Encoder.prefilter_reject's entry; NodeAffinity when
+        absent)."""
         w = np.asarray(cyc.fstatus)
         w = w[(w != 0) & (w != FS_NOT_EVALUATED)]
         out = {int(x) for x in np.unique(w & 0xFF) - 1}
         if int(enc_pod["flags"]) & E.POD_FLAG_PREFILTER_REJECT:
-            out.add(P.NODE_AFFINITY)
+            out.add(P.NODE_AFFINITY if reject is None else reject[0])
         return out
 
     def _cycle(self, pi: int, record: bool) -> PodCycle:
@@ -302,18 +325,19 @@ class DebuggableScheduler:
         fskip = int(rec["filter_skip"])
         if cyc.status & native.ST_IPA_PREFILTER_SKIP:
             fskip |= 1 << P.INTER_POD_AFFINITY
-        rejected = bool(rec["flags"] & E.POD_FLAG_PREFILTER_REJECT)
-        # PreFilter (wrappedplugin.go:504-512): RunPreFilterPlugins stops at an
-        # UnschedulableAndUnresolvable rejection.
+        # PreFilter (wrappedplugin.go:504-512): RunPreFilterPlugins stops at a
+        # rejection, or when the merged PreFilterResults leave no node (the
+        # plugin that emptied them recorded success and its node names)
+        reject = self.enc.prefilter_reject.get(cyc.pod) if rec["flags"] & E.POD_FLAG_PREFILTER_REJECT else None
+        names_of = self.enc.prefilter_results.get(cyc.pod, {})
         for pid in self.prof.prefilter_order():
             pname = P.PLUGIN_NAMES[pid]
-            if pid == P.NODE_AFFINITY and rejected:
-                st.AddPreFilterResult(ns, name, pname, MSG_NA_CONFLICT)
+            if reject is not None and pid == reject[0] and reject[1] is not None:
+                st.AddPreFilterResult(ns, name, pname, reject[1])
                 break
-            node_names = None
-            if pid == P.NODE_AFFINITY and int(rec["node_set"]) >= 0:
-                node_names = self.enc.prefilter_node_names[cyc.pod]
-            st.AddPreFilterResult(ns, name, pname, "" if (fskip >> pid) & 1 else A.SUCCESS, node_names)
+            st.AddPreFilterResult(ns, name, pname, "" if (fskip >> pid) & 1 else A.SUCCESS, names_of.get(pid))
+            if reject is not None and pid == reject[0]:
+                break
         # Filter
         order = [p for p in self.prof.filter_order() if not (fskip >> p) & 1]
         if self.annotator is not None:
@@ -450,8 +474,10 @@ class DevicePlugin:
         filter_skip, InterPodAffinity's from the device); NodeAffinity
         rejects a pod whose matchFields name no node."""
         rec = self.s.enc.workload.pods[cyc.pod]
-        if self.pid == P.NODE_AFFINITY and int(rec["flags"]) & E.POD_FLAG_PREFILTER_REJECT:
-            return Status(Status.UNSCHEDULABLE_AND_UNRESOLVABLE, MSG_NA_CONFLICT)
+        reject = self.s.enc.prefilter_reject.get(cyc.pod)
+        if int(rec["flags"]) & E.POD_FLAG_PREFILTER_REJECT and reject is not None and reject[0] == self.pid:
+            if reject[1] is not None:
+                return Status(Status.UNSCHEDULABLE_AND_UNRESOLVABLE, reject[1])
         fskip = int(rec["filter_skip"])
         if cyc.status & native.ST_IPA_PREFILTER_SKIP:
             fskip |= 1 << P.INTER_POD_AFFINITY

@@ -388,6 +388,49 @@ class Snapshot:
     skipped: List[str] = field(default_factory=list)   # pods bound to nodes absent from the snapshot
 
 
+# PersistentVolumeSpec fields that are not the volume source
+_PV_SPEC_FIELDS = frozenset(("capacity", "accessModes", "claimRef", "persistentVolumeReclaimPolicy",
+                             "storageClassName", "mountOptions", "volumeMode", "nodeAffinity",
+                             "volumeAttributesClassName"))
+
+
+def storage_from_k8s(doc: dict) -> m.Storage:
+    """The snapshot's pvs / pvcs / storageClasses (simulator/snapshot/
+    snapshot.go:34-36) as the volume plugins' listers return them.  Classes
+    get API defaulting (volumeBindingMode Immediate); a claim's or volume's
+    class is the beta annotation first, then spec.storageClassName
+    (storagehelpers.GetPersistentVolume[Claim]Class)."""
+    st = m.Storage()
+    for o in doc.get("storageClasses") or ():
+        meta = o.get("metadata") or {}
+        topo = tuple(tuple((e["key"], tuple(e.get("values") or ())) for e in (t.get("matchLabelExpressions") or ()))
+                     for t in o.get("allowedTopologies") or ())
+        st.classes[meta["name"]] = m.StorageClass(meta["name"], o.get("provisioner") or "",
+                                                  o.get("volumeBindingMode") or m.BINDING_IMMEDIATE, topo)
+    for o in doc.get("pvs") or ():
+        meta, spec = o.get("metadata") or {}, o.get("spec") or {}
+        ann = meta.get("annotations") or {}
+        req = (spec.get("nodeAffinity") or {}).get("required")
+        cref = spec.get("claimRef")
+        srcs = [k for k in spec if k not in _PV_SPEC_FIELDS and spec[k] is not None]
+        st.pvs[meta["name"]] = m.PersistentVolume(
+            meta["name"], labels={k: str(v) for k, v in (meta.get("labels") or {}).items()},
+            storage_class=ann.get(m.ANN_BETA_STORAGE_CLASS, spec.get("storageClassName") or ""),
+            node_affinity=None if req is None else [_term(t) for t in req.get("nodeSelectorTerms") or ()],
+            claim_ref=(cref.get("namespace") or "", cref.get("name") or "") if cref else None,
+            source=srcs[0] if srcs else "")
+    for o in doc.get("pvcs") or ():
+        meta, spec = o.get("metadata") or {}, o.get("spec") or {}
+        ann = dict(meta.get("annotations") or {})
+        ns = meta.get("namespace") or "default"
+        sc = ann[m.ANN_BETA_STORAGE_CLASS] if m.ANN_BETA_STORAGE_CLASS in ann else (spec.get("storageClassName") or "")
+        st.pvcs[(ns, meta["name"])] = m.PersistentVolumeClaim(
+            meta["name"], ns, volume_name=spec.get("volumeName") or "", storage_class=sc,
+            access_modes=tuple(spec.get("accessModes") or ()), annotations=ann,
+            deleting=bool(meta.get("deletionTimestamp")))
+    return st
+
+
 def load_snapshot(doc, n_nodes_check: bool = True) -> Snapshot:
     """ResourcesForSnap (dict or JSON text) -> Snapshot."""
     if isinstance(doc, (str, bytes)):
@@ -420,7 +463,15 @@ def load_snapshot(doc, n_nodes_check: bool = True) -> Snapshot:
     queue_objs.sort(key=lambda t: t[:3])
     pods = [pod_from_k8s(o, ns_labels or None) for o in bound_objs] + \
            [pod_from_k8s(t[3], ns_labels or None) for t in queue_objs]
+    storage = storage_from_k8s(doc)
+    if any(p.claim_names() for p in pods):
+        for n in doc.get("nodes") or ():   # NodeVolumeLimits' getVolumeLimits
+            alloc = ((n.get("status") or {}).get("allocatable") or {})
+            if any(k.startswith("attachable-volumes-csi-") for k in alloc):
+                raise NotImplementedError(f"node {n['metadata']['name']}: CSI attach limits (NodeVolumeLimits) "
+                                          "are not modelled")
     for p, o in zip(pods, bound_objs + [t[3] for t in queue_objs]):
+        p.storage = storage
         p.priority = pod_priority(o, classes, global_default)
         p.preemption_policy = pod_preemption_policy(o, class_policy)
         p.start_time = rfc3339_ns((o.get("status") or {}).get("startTime"))

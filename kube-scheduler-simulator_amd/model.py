@@ -198,6 +198,13 @@ class Pod:
     # spec.volumes: (name, the v1.VolumeSource field that is set, its JSON key,
     # persistentVolumeClaim.claimName or "")
     volumes: List[Tuple[str, str, str]] = field(default_factory=list)
+    # the cluster's PersistentVolumes / claims / StorageClasses, which the
+    # volume plugins' listers read for this pod's claims (None: none exist)
+    storage: Optional["Storage"] = None
+
+    def claim_names(self) -> List[str]:
+        """spec.volumes[].persistentVolumeClaim.claimName, in volume order."""
+        return [c for _, k, c in self.volumes if k == "persistentVolumeClaim"]
 
     def volumes_needing_plugins(self):
         """The volumes whose source makes a volume plugin's PreFilter run
@@ -205,9 +212,11 @@ class Pod:
         (podHasPVCs: claims and generic ephemeral volumes),
         nodevolumelimits/csi.go PreFilter (claims, ephemeral, in-tree volumes
         CSI migration translates), volumerestrictions (GCE PD, AWS EBS, RBD,
-        iSCSI, ReadWriteOncePod claims), volumezone (claims)]: the evaluator
-        models every other source as those plugins' Skip, and refuses these
-        (NotImplementedError) rather than record a Skip upstream would not."""
+        iSCSI, ReadWriteOncePod claims), volumezone (claims)] and that the
+        evaluator does not model: generic ephemeral and in-tree disk volumes
+        are refused (NotImplementedError) rather than recorded as a Skip
+        upstream would not return.  Claims (persistentVolumeClaim) are
+        modelled (encoder.py Encoder._volume_plan)."""
         return [(n, k) for n, k, _ in self.volumes if k in VOLUME_SOURCES_REFUSED]
 
     def has_pod_affinity(self) -> bool:
@@ -229,8 +238,78 @@ class Pod:
 
 
 VOLUME_SOURCES_REFUSED = frozenset((
-    "persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "azureFile",
+    "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "azureFile",
     "cinder", "vsphereVolume", "portworxVolume", "rbd", "iscsi"))
+
+# ---- storage: what VolumeBinding / VolumeZone / VolumeRestrictions /
+# NodeVolumeLimits read through their listers [upstream v1.32
+# pkg/scheduler/framework/plugins/{volumebinding,volumezone,volumerestrictions,
+# nodevolumelimits}; k8s.io/api storage/v1, core/v1 — not vendored]
+READ_WRITE_ONCE_POD = "ReadWriteOncePod"
+BINDING_IMMEDIATE = "Immediate"
+BINDING_WAIT_FOR_FIRST_CONSUMER = "WaitForFirstConsumer"
+NOT_SUPPORTED_PROVISIONER = "kubernetes.io/no-provisioner"
+ANN_BIND_COMPLETED = "pv.kubernetes.io/bind-completed"
+ANN_SELECTED_NODE = "volume.kubernetes.io/selected-node"
+ANN_BETA_STORAGE_CLASS = "volume.beta.kubernetes.io/storage-class"
+# volumezone.topologyLabels, in the plugin's order, and translateToGALabel
+LABEL_BETA_ZONE = "failure-domain.beta.kubernetes.io/zone"
+LABEL_BETA_REGION = "failure-domain.beta.kubernetes.io/region"
+VOLUME_ZONE_LABELS = (LABEL_BETA_ZONE, LABEL_BETA_REGION, "topology.kubernetes.io/zone",
+                      "topology.kubernetes.io/region")
+GA_LABEL = {LABEL_BETA_ZONE: "topology.kubernetes.io/zone", LABEL_BETA_REGION: "topology.kubernetes.io/region"}
+# PersistentVolume sources CSI migration translates (tryTranslatePVToCSI may
+# rewrite their node affinity): refused
+PV_SOURCES_MIGRATED = frozenset(("gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "azureFile", "cinder",
+                                 "vsphereVolume", "portworxVolume"))
+
+
+@dataclass(frozen=True)
+class StorageClass:
+    name: str
+    provisioner: str = ""
+    # volumeBindingMode after API defaulting (SetDefaults_StorageClass: Immediate)
+    binding_mode: str = BINDING_IMMEDIATE
+    # allowedTopologies: terms of (key, values) requirements (TopologySelectorTerm)
+    allowed_topologies: Tuple[Tuple[Tuple[str, Tuple[str, ...]], ...], ...] = ()
+
+
+@dataclass
+class PersistentVolume:
+    name: str
+    labels: Dict[str, str] = field(default_factory=dict)
+    storage_class: str = ""
+    # spec.nodeAffinity.required.nodeSelectorTerms; None = no required affinity
+    node_affinity: Optional[List[NodeSelectorTerm]] = None
+    claim_ref: Optional[Tuple[str, str]] = None    # (namespace, name)
+    source: str = "csi"                              # the PersistentVolumeSource field set
+
+
+@dataclass
+class PersistentVolumeClaim:
+    name: str
+    namespace: str = "default"
+    volume_name: str = ""
+    # storagehelpers.GetPersistentVolumeClaimClass: spec.storageClassName, else
+    # the beta annotation, else ""
+    storage_class: str = ""
+    access_modes: Tuple[str, ...] = ()
+    annotations: Dict[str, str] = field(default_factory=dict)
+    deleting: bool = False
+
+    def fully_bound(self) -> bool:
+        """volumeBinder.isPVCFullyBound: a volume name and bind-completed."""
+        return bool(self.volume_name) and ANN_BIND_COMPLETED in self.annotations
+
+
+@dataclass
+class Storage:
+    pvs: Dict[str, PersistentVolume] = field(default_factory=dict)
+    pvcs: Dict[Tuple[str, str], PersistentVolumeClaim] = field(default_factory=dict)   # (namespace, name)
+    classes: Dict[str, StorageClass] = field(default_factory=dict)
+
+    def claim(self, namespace: str, name: str) -> Optional[PersistentVolumeClaim]:
+        return self.pvcs.get((namespace, name))
 
 DEFAULT_BIND_ALL_HOST_IP = "0.0.0.0"
 

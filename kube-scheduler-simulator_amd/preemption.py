@@ -142,6 +142,10 @@ def check_scope(prof: P.Profile, pod: m.Pod, pods: Sequence[m.Pod]) -> None:
     """Refuse preemption the dry run cannot decide exactly: it re-runs the
     filters that read the node's pods (Fit, PodTopologySpread,
     InterPodAffinity), so every node-static filter must come before them."""
+    if pod.claim_names() and set(prof.filter_order()) & {P.VOLUME_RESTRICTIONS, P.VOLUME_BINDING, P.VOLUME_ZONE}:
+        # the dry run re-runs Fit / PTS / IPA only; VolumeRestrictions' AddPod /
+        # RemovePod extensions (ReadWriteOncePod users) are not modelled
+        raise NotImplementedError("DefaultPreemption for a preemptor with claims (volume plugins)")
     if pod.host_ports() and P.NODE_PORTS in prof.filter_order():
         # the device dry run re-runs Fit / PTS / IPA only (ksg_preempt)
         raise NotImplementedError("DefaultPreemption for a preemptor with host ports (NodePorts)")

@@ -244,7 +244,8 @@ class ScenarioRunner:
                         "pod": {"name": ps.pod.name, "namespace": ps.pod.namespace}, "nodeName": ps.node}})
                     self._wake(POD_ADD)
                 else:
-                    ps.rejectors = F.DebuggableScheduler.rejecting_plugins(cyc, sched.enc.workload.pods[i])
+                    ps.rejectors = F.DebuggableScheduler.rejecting_plugins(cyc, sched.enc.workload.pods[i],
+                                                                           sched.enc.prefilter_reject.get(i))
                 for ps2 in pending:     # pods woken by this cycle's events join activeQ now
                     if not ps2.node and ps2.rejectors is None and key_of[id(ps2)] in self.pods and ps2 is not ps:
                         entry = (-ps2.pod.priority, ps2.ordinal, index[id(ps2)])

@@ -136,6 +136,104 @@ bool eval_term(const Ctx& c, const int32_t*& w, int n) {
   return ok;
 }
 
+// ---- volume plugins (encoder.py Encoder._volume_plan program) --------------
+// Decoded once per pod, then checked per node: VolumeRestrictions' RWOP
+// conflict, VolumeBinding's reasons (1 node affinity conflict, 2 cannot bind /
+// provision, 4 bound PV missing), VolumeZone's zone check.
+struct VolTerms { bool all; const int32_t* at; int nt; };   // all: matches every node
+struct VolProg {
+  bool rwop = false;
+  std::vector<std::pair<bool, VolTerms>> bound;   // (pv exists, its node affinity)
+  std::vector<std::pair<int, VolTerms>> prov;     // (selected node, allowed topologies; nt < 0: cannot provision)
+  int zcols[4] = {-1, -1, -1, -1};
+  struct Zone { int col, gcol; std::vector<uint32_t> ids, gids; };
+  std::vector<Zone> zones;
+};
+
+const int32_t* skip_terms(const int32_t* w, int nt) {
+  for (int t = 0; t < nt; t++) {
+    int nr = *w++;
+    for (int r = 0; r < nr; r++) w += 3 + w[2];
+  }
+  return w;
+}
+
+VolProg decode_vol(const Ctx& c, const ksg_pod& p) {
+  VolProg v;
+  if (p.vol < 0) return v;
+  const int32_t* w = c.prog.data() + p.vol;
+  v.rwop = (w[0] & 1) != 0;
+  w++;
+  int nb = *w++;
+  for (int b = 0; b < nb; b++) {
+    int kind = *w++;
+    if (kind == 0) { v.bound.push_back({false, {true, nullptr, 0}}); continue; }
+    int nt = *w++;
+    if (nt < 0) { v.bound.push_back({true, {true, nullptr, 0}}); continue; }
+    v.bound.push_back({true, {false, w, nt}});
+    w = skip_terms(w, nt);
+  }
+  int np = *w++;
+  for (int k = 0; k < np; k++) {
+    int sel = *w++, nt = *w++;
+    v.prov.push_back({sel, {false, w, nt}});
+    if (nt > 0) w = skip_terms(w, nt);
+  }
+  for (int k = 0; k < 4; k++) v.zcols[k] = *w++;
+  int nz = *w++;
+  for (int k = 0; k < nz; k++) {
+    VolProg::Zone z;
+    z.col = w[0];
+    z.gcol = w[1];
+    int nv = w[2];
+    for (int i = 0; i < nv; i++) z.ids.push_back((uint32_t)w[3 + i]);
+    int ng = w[3 + nv];
+    for (int i = 0; i < ng; i++) z.gids.push_back((uint32_t)w[4 + nv + i]);
+    w += 4 + nv + ng;
+    v.zones.push_back(std::move(z));
+  }
+  return v;
+}
+
+bool terms_match(const Ctx& c, const VolTerms& t, int n) {
+  if (t.all) return true;
+  const int32_t* w = t.at;
+  bool any = false;
+  for (int k = 0; k < t.nt; k++) any = eval_term(c, w, n) || any;
+  return any;
+}
+
+// FindPodVolumes' reasons at node n: checkBoundClaims stops at the first
+// claim whose PV is missing or does not fit; then the unbound claims'
+// selected node and provisioning checks
+uint32_t volume_binding_reasons(const Ctx& c, const VolProg& v, int n) {
+  uint32_t r = 0;
+  for (auto& b : v.bound) {
+    if (!b.first) { r |= 4u; break; }
+    if (!terms_match(c, b.second, n)) { r |= 1u; break; }
+  }
+  for (auto& pr : v.prov) {
+    bool ok = pr.first == -1 || pr.first == n;
+    if (pr.second.nt < 0) ok = false;
+    else if (pr.second.nt > 0 && !terms_match(c, pr.second, n)) ok = false;
+    if (!ok) { r |= 2u; break; }
+  }
+  return r;
+}
+
+bool volume_zone_conflict(const Ctx& c, const VolProg& v, int n) {
+  bool constrained = false;
+  for (int k = 0; k < 4; k++) constrained = constrained || (v.zcols[k] >= 0 && lv(c, v.zcols[k], n) != 0);
+  if (!constrained) return false;
+  for (auto& z : v.zones) {
+    uint32_t x = lv(c, z.col, n);
+    const std::vector<uint32_t>* set = &z.ids;
+    if (!x) { x = lv(c, z.gcol, n); set = &z.gids; }
+    if (!x || std::find(set->begin(), set->end(), x) == set->end()) return true;
+  }
+  return false;
+}
+
 bool na_required_match(const Ctx& c, const ksg_pod& p, int n) {
   if (p.na_req < 0) return true;
   const int32_t* w = c.prog.data() + p.na_req;
@@ -617,21 +715,23 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
   res->status = 0;
   res->score_skip = p.score_skip;
   std::vector<uint32_t> fs(N, KSG_FS_NOT_EVALUATED);
+  // InterPodAffinity's PreFilter Skip is reported for every pod, a pod that
+  // another PreFilter rejected included (the status bit then matters only
+  // when InterPodAffinity precedes the rejecting plugin in PreFilter order)
+  IpaProg ig = ipa_prog(c, p);
+  IpaPre ipre;
+  ipre.skip = true;
+  if (p.ipa >= 0 && in_filter(c, KSG_PL_INTER_POD_AFFINITY)) ipre = ipa_prefilter(c, p, ig);
+  if (ipre.skip && in_filter(c, KSG_PL_INTER_POD_AFFINITY)) res->status |= KSG_ST_IPA_PREFILTER_SKIP;
   if (!(p.flags & KSG_POD_PREFILTER_REJECT)) {
     uint32_t fskip = p.filter_skip;
     PtsProg pg = pts_prog(c, p);
     PtsPre pre;
     if (!((fskip >> KSG_PL_POD_TOPOLOGY_SPREAD) & 1) && in_filter(c, KSG_PL_POD_TOPOLOGY_SPREAD))
       pre = pts_prefilter(c, p, pg);
-    IpaProg ig = ipa_prog(c, p);
-    IpaPre ipre;
-    ipre.skip = true;
-    if (p.ipa >= 0 && in_filter(c, KSG_PL_INTER_POD_AFFINITY)) ipre = ipa_prefilter(c, p, ig);
-    if (ipre.skip) {
-      fskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
-      if (in_filter(c, KSG_PL_INTER_POD_AFFINITY)) res->status |= KSG_ST_IPA_PREFILTER_SKIP;
-    }
+    if (ipre.skip) fskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
     const int32_t* node_set = p.node_set >= 0 ? c.prog.data() + p.node_set : nullptr;
+    const VolProg vp = decode_vol(c, p);
 #pragma omp parallel for num_threads(c.nthreads) schedule(static)
     for (int n = 0; n < N; n++) {
       if (node_set && !((((uint32_t)node_set[n >> 5]) >> (n & 31)) & 1u)) continue;
@@ -677,8 +777,19 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
             if (r) { fail = true; reason = r; }
             break;
           }
+          case KSG_PL_VOLUME_RESTRICTIONS:
+            fail = vp.rwop;
+            break;
+          case KSG_PL_VOLUME_BINDING: {
+            uint32_t r = p.vol >= 0 ? volume_binding_reasons(c, vp, n) : 0;
+            if (r) { fail = true; reason = r; }
+            break;
+          }
+          case KSG_PL_VOLUME_ZONE:
+            fail = p.vol >= 0 && volume_zone_conflict(c, vp, n);
+            break;
           default:
-            break;  // volume plugins: pass (Skip for volume-less pods)
+            break;  // NodeVolumeLimits: passes (no CSI attach limits modelled)
         }
         if (fail) st = (uint32_t)(pl + 1) | (reason << 8);
       }
@@ -699,7 +810,6 @@ int eval_pod(Ctx& c, int pi, ksg_result* res, ksg_capture* cap) {
   PtsScore pst;
   if (!((sskip >> KSG_PL_POD_TOPOLOGY_SPREAD) & 1u) && (c.prof.score_mask >> KSG_PL_POD_TOPOLOGY_SPREAD & 1u))
     pst = pts_prescore(c, p, pg, feas);
-  IpaProg ig = ipa_prog(c, p);
   IpaScore ist;
   if ((c.prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u) {
     if (!((sskip >> KSG_PL_INTER_POD_AFFINITY) & 1u)) {

@@ -722,14 +722,197 @@ def ipa_normalize(scores):
     return out
 
 
+# ---------------------------------------------------------------- volume plugins
+# Restated on the object model from upstream v1.32 volumerestrictions,
+# nodevolumelimits (csi.go), volumebinding (volume_binding.go, binder.go) and
+# volumezone (not vendored; parity unpinned).
+RWOP_MSG = "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode"
+VB_NODE_CONFLICT = "node(s) had volume node affinity conflict"
+VB_BIND_CONFLICT = "node(s) didn't find available persistent volumes to bind"
+VB_PV_NOT_EXIST = "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"
+VZ_CONFLICT = "node(s) had no available volume zone"
+
+
+def _claim(pod, name):
+    st = pod.storage
+    return None if st is None else st.pvcs.get((pod.namespace, name))
+
+
+def _class_of(pod, pvc):
+    st = pod.storage
+    return st.classes.get(pvc.storage_class) if (st is not None and pvc.storage_class) else None
+
+
+def _labels_only_match(terms, labels) -> bool:
+    """CheckNodeAffinity: MatchNodeSelectorTerms against a node that has only
+    labels (no name, so matchFields never constrain)."""
+    for t in terms:
+        if not t.match_expressions and not t.match_fields:
+            continue
+        ok = True
+        for r in t.match_expressions:
+            if r.operator in (m.IN, m.NOT_IN) and not r.values:
+                ok = False
+            elif r.operator in (m.EXISTS, m.DOES_NOT_EXIST) and r.values:
+                ok = False
+            elif r.operator in (m.GT, m.LT) and (len(r.values) != 1 or parse_int64(r.values[0]) is None):
+                ok = False
+            elif not label_req_matches(r.key, r.operator, r.values, labels):
+                ok = False
+            if not ok:
+                break
+        if ok:
+            return True
+    return False
+
+
+def _topology_match(terms, labels) -> bool:
+    """v1helper.MatchTopologySelectorTerms."""
+    if not terms:
+        return True
+    for term in terms:
+        if not term:
+            continue
+        if all(vals and k in labels and labels[k] in vals for k, vals in term):
+            return True
+    return False
+
+
+def vr_prefilter(pod, infos):
+    """VolumeRestrictions.PreFilter -> ("skip"|"reject"|"ok", message or conflicting claim count)."""
+    claims = pod.claim_names()
+    if not claims:
+        return "skip", None
+    for c in claims:
+        if _claim(pod, c) is None:
+            return "reject", f'persistentvolumeclaim "{c}" not found'
+    rwop = {c for c in claims if m.READ_WRITE_ONCE_POD in _claim(pod, c).access_modes}
+    n = 0
+    for c in rwop:   # StorageInfos().IsPVCUsedByPods
+        if any(q is not pod and q.namespace == pod.namespace and c in q.claim_names()
+               for ni in infos for q in ni.pods):
+            n += 1
+    return "ok", n
+
+
+def vb_prefilter(pod):
+    """VolumeBinding.PreFilter -> ("skip"|"reject"|"ok", message or state, eligible node names or None)."""
+    claims = pod.claim_names()
+    if not claims:
+        return "skip", None, None
+    for c in claims:
+        pvc = _claim(pod, c)
+        if pvc is None:
+            return "reject", f'persistentvolumeclaim "{c}" not found', None
+        if pvc.deleting:
+            return "reject", f'persistentvolumeclaim "{c}" is being deleted', None
+    bound, delay = [], []
+    for c in claims:
+        pvc = _claim(pod, c)
+        if pvc.volume_name and m.ANN_BIND_COMPLETED in pvc.annotations:
+            bound.append(pvc)
+            continue
+        cls = _class_of(pod, pvc)
+        if cls is not None and cls.binding_mode == m.BINDING_WAIT_FOR_FIRST_CONSUMER and not pvc.volume_name:
+            delay.append((pvc, cls))
+        else:
+            return "reject", "pod has unbound immediate PersistentVolumeClaims", None
+    eligible = None
+    for pvc in bound:
+        pv = pod.storage.pvs.get(pvc.volume_name)
+        if pv is None:
+            eligible = None
+            break
+        result = set()
+        for t in pv.node_affinity or ():
+            nodes = None
+            for r in t.match_expressions:
+                if r.key == m.LABEL_HOSTNAME and r.operator == m.IN:
+                    nodes = set(r.values) if nodes is None else nodes & set(r.values)
+            result |= nodes or set()
+        if result:
+            eligible = result if eligible is None else eligible & result
+    return "ok", (bound, delay), eligible
+
+
+def vb_filter(pod, state, node) -> Optional[str]:
+    bound, delay = state
+    reasons = []
+    for pvc in bound:   # checkBoundClaims
+        pv = pod.storage.pvs.get(pvc.volume_name)
+        if pv is None:
+            reasons.append(VB_PV_NOT_EXIST)
+            break
+        if pv.node_affinity is not None and not _labels_only_match(pv.node_affinity, node.labels):
+            reasons.append(VB_NODE_CONFLICT)
+            break
+    ok = True
+    for pvc, _ in delay:   # the selected-node fast path
+        sel = pvc.annotations.get(m.ANN_SELECTED_NODE)
+        if sel is not None and sel != node.name:
+            ok = False
+    if ok:
+        for pvc, cls in delay:   # checkVolumeProvisions
+            if cls.provisioner in ("", m.NOT_SUPPORTED_PROVISIONER) or not _topology_match(
+                    cls.allowed_topologies, node.labels):
+                ok = False
+                break
+    if not ok:
+        reasons.append(VB_BIND_CONFLICT)
+    order = [VB_NODE_CONFLICT, VB_BIND_CONFLICT, VB_PV_NOT_EXIST]
+    return ", ".join(sorted(reasons, key=order.index)) if reasons else None
+
+
+def vz_prefilter(pod):
+    """VolumeZone.PreFilter (getPVbyPod) -> ("skip"|"reject"|"ok", message or [(key, values)])."""
+    tops = []
+    for c in pod.claim_names():
+        if not c:
+            return "reject", "PersistentVolumeClaim had no name"
+        pvc = _claim(pod, c)
+        if pvc is None:
+            return "reject", f'persistentvolumeclaim "{c}" not found'
+        if not pvc.volume_name:
+            if not pvc.storage_class:
+                return "reject", "PersistentVolumeClaim had no pv name and storageClass name"
+            cls = _class_of(pod, pvc)
+            if cls is None:
+                return "reject", f'storageclass.storage.k8s.io "{pvc.storage_class}" not found'
+            if cls.binding_mode == m.BINDING_WAIT_FOR_FIRST_CONSUMER:
+                continue
+            return "reject", "PersistentVolume had no name"
+        pv = pod.storage.pvs.get(pvc.volume_name)
+        if pv is None:
+            return "reject", f'persistentvolume "{pvc.volume_name}" not found'
+        for key in m.VOLUME_ZONE_LABELS:
+            if key in pv.labels:
+                tops.append((key, {z.strip() for z in pv.labels[key].split("__")}))
+    return ("ok", tops) if tops else ("skip", None)
+
+
+def vz_filter(tops, node) -> Optional[str]:
+    if not any(k in node.labels for k in m.VOLUME_ZONE_LABELS):
+        return None
+    for key, values in tops:
+        v = node.labels.get(key)
+        if v is None:
+            v = node.labels.get(m.GA_LABEL.get(key, key))
+        if v is None or v not in values:
+            return VZ_CONFLICT
+    return None
+
+
 # ---------------------------------------------------------------- framework
 def pod_prefilter(pod, infos, prof):
-    """Returns (statuses {plugin:str}, states, rejected, node_set)."""
+    """Returns (statuses {plugin:str}, states, skip, rejected, node_set);
+    states["results"] = the PreFilterResult node names per plugin."""
     st = {}
     states = {}
     skip = set()
     node_set = None
     rejected = None
+    results = {}
+    states["results"] = results
     for pid in prof.prefilter_order():
         name = P.PLUGIN_NAMES[pid]
         if pid == P.NODE_AFFINITY:
@@ -759,7 +942,12 @@ def pod_prefilter(pod, infos, prof):
                     rejected = name
                     break
                 if names:
-                    node_set = sorted(names)
+                    results[name] = sorted(names)
+                    node_set = set(names) if node_set is None else set(node_set) & set(names)
+                    if not node_set:
+                        st[name] = "success"
+                        rejected = name
+                        break
             st[name] = "success"
         elif pid == P.NODE_PORTS:
             if not pod.host_ports():
@@ -770,8 +958,30 @@ def pod_prefilter(pod, infos, prof):
         elif pid == P.NODE_RESOURCES_FIT:
             st[name] = "success"
         elif pid in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING, P.VOLUME_ZONE):
-            st[name] = ""          # volume-less pods: Skip
-            skip.add(pid)
+            if pid == P.VOLUME_RESTRICTIONS:
+                kind, val = vr_prefilter(pod, infos)
+            elif pid == P.NODE_VOLUME_LIMITS:
+                kind, val = ("ok", None) if pod.claim_names() else ("skip", None)
+            elif pid == P.VOLUME_BINDING:
+                kind, val, eligible = vb_prefilter(pod)
+            else:
+                kind, val = vz_prefilter(pod)
+            if kind == "skip":
+                st[name] = ""
+                skip.add(pid)
+            elif kind == "reject":
+                st[name] = val
+                rejected = name
+                break
+            else:
+                states[pid] = val
+                st[name] = "success"
+                if pid == P.VOLUME_BINDING and eligible is not None:
+                    results[name] = sorted(eligible)
+                    node_set = set(eligible) if node_set is None else set(node_set) & set(eligible)
+                    if not node_set:   # the framework's merge: no node left
+                        rejected = name
+                        break
         elif pid == P.POD_TOPOLOGY_SPREAD:
             s = pts_prefilter(pod, infos, prof)
             if s is None:
@@ -825,7 +1035,14 @@ def run_filters(pod, ni, prof, states, skip, total_nodes):
             msg = pts_filter(states[pid], pod, ni)
         elif pid == P.INTER_POD_AFFINITY:
             msg = ipa_filter(states[pid], pod, ni)
-        # volume plugins pass for volume-less pods
+        elif pid == P.VOLUME_RESTRICTIONS:   # satisfyReadWriteOncePod
+            if states[pid]:
+                msg = RWOP_MSG
+        elif pid == P.VOLUME_BINDING:
+            msg = vb_filter(pod, states[pid], node)
+        elif pid == P.VOLUME_ZONE:
+            msg = vz_filter(states[pid], node)
+        # NodeVolumeLimits passes (no CSI attach limits modelled)
         if msg is None:
             out.append((name, "passed"))
         else:
@@ -840,8 +1057,7 @@ def schedule_one(pod: m.Pod, infos: List[NodeInfo], prof: P.Profile):
            "raw": {}, "norm": {}, "n_feasible": 0}
     st, states, skip, rejected, node_set = pod_prefilter(pod, infos, prof)
     rec["prefilter_status"] = st
-    if node_set is not None:
-        rec["prefilter_result"]["NodeAffinity"] = node_set
+    rec["prefilter_result"].update(states["results"])
     if rejected:
         return rec
     total_nodes = len(infos)

@@ -11,6 +11,8 @@ a SHA-256 over every pod's annotations; readme_kat.json stores the
 annotation values in full.
 """
 import hashlib
+
+import numpy as np
 import json
 import os
 import sys
@@ -50,7 +52,12 @@ def input_digest(nodes, pods, prof):
     for k in sorted(enc.cluster.arrays):
         h.update(k.encode())
         h.update(enc.cluster.arrays[k].tobytes())
-    h.update(enc.workload.pods.tobytes())
+    # the pod records as first laid out (144 B; round 5 appended the volume
+    # program offset, hashed only when a pod has one), so digests stay put
+    pods = enc.workload.pods
+    h.update(pods.view(np.uint8).reshape(len(pods), pods.dtype.itemsize)[:, :144].tobytes())
+    if (pods["vol"] >= 0).any():
+        h.update(pods["vol"].tobytes())
     h.update(enc.workload.prog.tobytes())
     return h.hexdigest()
 

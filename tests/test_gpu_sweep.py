@@ -69,7 +69,24 @@ CASES = [
     ("c5-ex-6000-r2", lambda: G.config5(n_nodes=6000, n_pods=80, n_images=500, taint_vocab=256,
                                         taints_per_node=16, images_per_node=20), None),   # S = 2, cpu/mem/gpu Fit
     ("c1-default-r2", lambda: G.config1(n_nodes=100, n_pods=300), None),            # PTS/IPA: queue kernel
-] + [(f"zoo-{s}-r4", (lambda s=s: __import__("zoo").zoo(s)), (lambda: _zoo_profiles(4))) for s in range(6)]
+] + [(f"zoo-{s}-r4", (lambda s=s: __import__("zoo").zoo(s)), (lambda: _zoo_profiles(4))) for s in range(6)] + [
+    # RequestedToCapacityRatio replicas beside Least/MostAllocated ones (generic arithmetic)
+    ("c2-3000x200-rtcr-r4", lambda: _c2(3000, 200), lambda: _rtcr_profiles(4)),
+    ("zoo-1-rtcr-r3", lambda: __import__("zoo").zoo(1), lambda: _rtcr_profiles(3, NODE_LOCAL)),
+]
+
+
+def _rtcr_profiles(k, plugins=None):
+    shapes = __import__("zoo").RTCR_SHAPES
+    out = []
+    for r, p in enumerate(G.replica_profiles(k)):
+        if plugins is not None:
+            p = P.Profile(plugins=list(plugins), fit_strategy=p.fit_strategy)
+        if r % 2 == 0:
+            p.fit_strategy = P.REQUESTED_TO_CAPACITY_RATIO
+            p.fit_shape = list(shapes[(r // 2) % len(shapes)])
+        out.append(p)
+    return out
 
 
 @pytest.mark.parametrize("name,make,profs", CASES, ids=[c[0] for c in CASES])

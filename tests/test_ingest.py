@@ -370,18 +370,30 @@ def test_volumes_parsed_from_the_export_sample():
     snap = I.load_snapshot(doc)
     byname = {p.name: p for p in snap.pods}
     assert byname["claims"].volumes == [("data", "persistentVolumeClaim", "pvc1")]
-    assert byname["claims"].volumes_needing_plugins() == [("data", "persistentVolumeClaim")]
+    assert byname["claims"].claim_names() == ["pvc1"]
+    assert byname["claims"].volumes_needing_plugins() == []    # claims are modelled (round 5)
     assert byname["scratch"].volumes == [("tmp", "emptyDir", "")]
     assert byname["scratch"].volumes_needing_plugins() == []
+    st = byname["claims"].storage
+    pvc = st.claim("default", "pvc1")
+    assert pvc.volume_name == "pv1" and pvc.fully_bound() and pvc.storage_class == ""
+    assert st.pvs["pv1"].claim_ref == ("default", "pvc1") and st.pvs["pv1"].source == "hostPath"
+    assert st.pvs["pv2"].claim_ref is None and st.pvs["pv1"].node_affinity is None
 
 
-def test_claim_volume_refused_by_both_encoders():
-    """A PVC makes VolumeBinding / NodeVolumeLimits / VolumeZone PreFilter run
-    upstream: refused, never recorded as their Skip."""
+def test_claim_volume_encoded_by_python_refused_by_native():
+    """A PVC makes the volume plugins' PreFilter run upstream: the Python
+    encoder models them (a volume program), the C ABI's native encoder still
+    refuses such pods loudly (never recording a Skip)."""
     S = pkg("snapshot")
     snap = I.load_snapshot(_volume_doc())
-    with pytest.raises(NotImplementedError, match="pvc|persistentVolumeClaim"):
-        E.Encoder(snap.nodes, snap.pods, snap.profile)
+    enc = E.Encoder(snap.nodes, snap.pods, snap.profile)
+    rec = {n: enc.workload.pods[i] for i, n in enumerate(enc.workload.names)}
+    assert int(rec["default/claims"]["vol"]) >= 0 and int(rec["default/scratch"]["vol"]) == -1
+    fskip = int(rec["default/claims"]["filter_skip"])
+    for v in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING):
+        assert not fskip >> v & 1
+    assert fskip >> P.VOLUME_ZONE & 1   # pv1 has no zone labels: VolumeZone's PreFilter Skip
     s = S.Snapshot(snap.profile, snap.nodes)
     ok = [p for p in snap.pods if p.name == "scratch"][0]
     s.add_pod(ok)

@@ -191,3 +191,103 @@ def zoo_args(seed: int, kind: str, **kw):
     else:
         raise ValueError(kind)
     return nodes, pods, prof
+
+
+def zoo_volumes(seed: int, n_nodes: int = 30, n_pods: int = 90, bound: bool = False):
+    """Pods with persistentVolumeClaim volumes over a cluster with zones and
+    regions (GA and beta labels), exercising VolumeRestrictions,
+    NodeVolumeLimits, VolumeBinding and VolumeZone: local PVs pinned by
+    hostname (VolumeBinding's PreFilterResult), zonal PVs (single and
+    "__"-joined multi-zone labels, beta keys matched against GA node labels),
+    PVs with zone node affinity, claims bound to missing PVs, claims without
+    bind-completed (unbound immediate), WaitForFirstConsumer claims against
+    classes with allowedTopologies / no provisioner / a selected node, missing
+    claims and ReadWriteOncePod claims.  bound=True also returns running pods
+    [(pod index, node index)] that hold some ReadWriteOncePod claims."""
+    rng = np.random.Generator(np.random.PCG64(seed + 4242))
+    nodes, pods, prof = zoo(seed, n_nodes=n_nodes, n_pods=n_pods)
+    zones = [f"z{k}" for k in range(3)]
+    for i, n in enumerate(nodes):
+        if not n.labels:
+            continue
+        z = zones[i % 3]
+        u = rng.random()
+        if u < 0.5:
+            n.labels[m.LABEL_ZONE] = z
+            n.labels["topology.kubernetes.io/region"] = "r0"
+        elif u < 0.7:
+            n.labels[m.LABEL_BETA_ZONE] = z
+        elif u < 0.8:
+            n.labels.pop(m.LABEL_ZONE, None)
+            n.labels.pop(m.LABEL_REGION, None)
+    st = m.Storage()
+    st.classes["fast"] = m.StorageClass("fast", "csi.example.com", m.BINDING_WAIT_FOR_FIRST_CONSUMER,
+                                        (((m.LABEL_ZONE, ("z0", "z1")),), (("topology.kubernetes.io/region", ("r9",)),)))
+    st.classes["any"] = m.StorageClass("any", "csi.example.com", m.BINDING_WAIT_FOR_FIRST_CONSUMER)
+    st.classes["local"] = m.StorageClass("local", m.NOT_SUPPORTED_PROVISIONER, m.BINDING_WAIT_FOR_FIRST_CONSUMER)
+    st.classes["imm"] = m.StorageClass("imm", "csi.example.com", m.BINDING_IMMEDIATE)
+    done = {m.ANN_BIND_COMPLETED: "yes"}
+
+    nss = sorted({p.namespace for p in pods} | {"default"})
+
+    def bound_claim(name, pv, modes=("ReadWriteOnce",)):
+        st.pvs[pv.name] = pv
+        pv.claim_ref = ("default", name)
+        for ns in nss:   # the same claim name in every namespace (all bound to the one PV)
+            st.pvcs[(ns, name)] = m.PersistentVolumeClaim(name, ns, pv.name, pv.storage_class, modes, dict(done))
+
+    hosts = [n.name for n in nodes if n.labels.get(m.LABEL_HOSTNAME)]
+    for k in range(6):   # local PVs pinned to one or two hosts
+        names = tuple(rng.choice(hosts, size=1 + k % 2, replace=False))
+        bound_claim(f"local-{k}", m.PersistentVolume(f"pv-local-{k}", storage_class="x", node_affinity=[
+            m.NodeSelectorTerm(match_expressions=(m.Requirement(m.LABEL_HOSTNAME, m.IN, names),))]))
+    for k, z in enumerate(["z0", "z1", "z0__z2", "z2"]):   # zonal PVs (labels)
+        key = m.LABEL_BETA_ZONE if k % 2 else m.LABEL_ZONE
+        bound_claim(f"zonal-{k}", m.PersistentVolume(f"pv-zonal-{k}", labels={key: z}))
+    bound_claim("zonal-region", m.PersistentVolume("pv-zonal-region", labels={m.LABEL_BETA_REGION: "r0"}))
+    bound_claim("aff-zone", m.PersistentVolume("pv-aff-zone", node_affinity=[
+        m.NodeSelectorTerm(match_expressions=(m.Requirement(m.LABEL_ZONE, m.IN, ("z1", "z2")),)),
+        m.NodeSelectorTerm(match_fields=(m.Requirement(m.OBJECT_NAME_FIELD, m.IN, ("nowhere",)),),
+                           match_expressions=(m.Requirement("rank", m.GT, ("15",)),))]))
+    bound_claim("plain", m.PersistentVolume("pv-plain"))
+    st.pvcs[("default", "ghost")] = m.PersistentVolumeClaim("ghost", "default", "pv-missing", "", ("ReadWriteOnce",),
+                                                            dict(done))
+    st.pvcs[("default", "prebound")] = m.PersistentVolumeClaim("prebound", "default", "pv-plain", "",
+                                                               ("ReadWriteOnce",))
+    st.pvcs[("default", "immediate")] = m.PersistentVolumeClaim("immediate", "default", "", "imm")
+    for k in range(3):
+        bound_claim(f"rwop-{k}", m.PersistentVolume(f"pv-rwop-{k}"), ("ReadWriteOncePod",))
+    shared = ["local-0", "local-1", "local-2", "local-3", "local-4", "local-5", "zonal-0", "zonal-1", "zonal-2",
+              "zonal-3", "zonal-region", "aff-zone", "plain", "ghost", "prebound", "immediate", "missing"]
+    for i, p in enumerate(pods):
+        p.storage = st
+        u = rng.random()
+        if u < 0.35:
+            continue
+        if u < 0.75:
+            cs = list(rng.choice(shared, size=1 + int(rng.random() < 0.3), replace=False))
+        else:   # a claim of its own: WaitForFirstConsumer (maybe with a selected node)
+            cls = ["fast", "any", "local"][int(rng.integers(3))]
+            ann = {}
+            if rng.random() < 0.2:
+                ann[m.ANN_SELECTED_NODE] = nodes[int(rng.integers(len(nodes)))].name
+            name = f"own-{i}"
+            st.pvcs[(p.namespace, name)] = m.PersistentVolumeClaim(name, p.namespace, "", cls, ("ReadWriteOnce",),
+                                                                   ann)
+            cs = [name]
+            if rng.random() < 0.3:
+                cs.append(str(rng.choice(["zonal-0", "local-2", "plain"])))
+        p.volumes = [(f"v{k}", "persistentVolumeClaim", c) for k, c in enumerate(cs)]
+    if not bound:
+        return nodes, pods, prof
+    # two running pods hold rwop-0 / rwop-1; queued pods claim rwop-0..2
+    run = []
+    for k in range(2):
+        q = m.Pod(name=f"holder-{k}", containers=[m.Container(requests={m.CPU: 100})], storage=st,
+                  volumes=[("v0", "persistentVolumeClaim", f"rwop-{k}")])
+        pods.insert(k, q)
+        run.append((k, k))
+    for j, i in enumerate(range(2, len(pods), 9)):
+        if j < 3:
+            pods[i].volumes = [("v0", "persistentVolumeClaim", f"rwop-{j}")]
+    return nodes, pods, prof, run
