@@ -240,6 +240,7 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
         sizes[i] = sum(len(v) for v in vals)
 
     bulk = B.BulkAnnotator(enc, prof, threads=threads)
+    dev = None
     try:
         eng.reset_state()
         B.annotate_queue(eng, bulk, 0, min(chunk, n_pods), sink, chunk=chunk)   # warmup
@@ -247,6 +248,47 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
         t = time.perf_counter()
         pl = B.annotate_queue(eng, bulk, 0, n_pods, sink, chunk=chunk)
         wall = time.perf_counter() - t
+        host_digests = digests.copy()
+        # The xxh3 sink holds the GIL (python-xxhash does not release it), so
+        # it caps either path at ~26 GB/s of hashing; each path is also timed
+        # with a light sink (the values' lengths only) for the serialiser's
+        # own delivery rate.  Digests come from the xxh3 runs.
+        lens = np.zeros(n_pods, np.int64)
+
+        def light(i, vals):
+            lens[i] = sum(len(v) for v in vals)
+
+        eng.reset_state()
+        t = time.perf_counter()
+        B.annotate_queue(eng, bulk, 0, n_pods, light, chunk=chunk)
+        wall_light = time.perf_counter() - t
+        # the same values serialised on the device (ksg_run_queue_json_async):
+        # the capture rows stay in HBM, the finished bytes come back on a copy
+        # stream overlapping the next chunk
+        try:
+            eng.reset_state()
+            # warmup over three chunks: the three pinned output buffers (they rotate) get sized
+            B.annotate_queue_device(eng, bulk, 0, min(3 * chunk, n_pods), light, chunk=chunk)
+            eng.reset_state()
+            t = time.perf_counter()
+            pl_d = B.annotate_queue_device(eng, bulk, 0, n_pods, light, chunk=chunk)
+            wall_dl = time.perf_counter() - t
+            eng.reset_state()
+            digests[:] = 0
+            t = time.perf_counter()
+            B.annotate_queue_device(eng, bulk, 0, n_pods, sink, chunk=chunk)
+            wall_d = time.perf_counter() - t
+            hd = xxhash.xxh3_64()
+            hd.update(digests.tobytes())
+            dev = {"pods_per_s": n_pods / wall_dl, "wall_s": wall_dl, "annotation_MB_per_s": sizes.sum() / wall_dl / 1e6,
+                   "sink": "lengths only (the values delivered to pinned host memory, per-pod views handed out)",
+                   "pods_per_s_xxh3_sink": n_pods / wall_d, "digest_xxh3": hd.hexdigest(),
+                   "bytes_equal_host": bool((digests == host_digests).all()),
+                   "placements_equal_host": bool((pl_d == pl).all()),
+                   "path": "ksg_run_queue_json_async (csrc/ksched_json.h) + sink on the annotator's threads"}
+        except Exception as e:
+            dev = {"error": str(e)}
+        digests[:] = host_digests
     finally:
         bulk.close()
     # the captured run alone (device + D2H of the capture arrays), same chunks
@@ -272,7 +314,8 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
             "annotation_MB_per_s": sizes.sum() / wall / 1e6,
             "capture_only_pods_per_s": n_pods / cap_wall, "capture_device_ms": dev_ms,
             "capture_kernels_ms": {k: round(v, 3) for k, v in ks.items()},
-            "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(), "threads": threads}
+            "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(), "threads": threads,
+            "pods_per_s_light_sink": n_pods / wall_light, "device_serialiser": dev}
 
 
 def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=None, label: str = "configs[1]",

@@ -432,6 +432,28 @@ int ksg_annotator_free(ksg_annotator* a);
  * strings are owned by the annotator and valid until its next call. */
 int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const char** json, int64_t* len);
 
+/* ---- the same values serialised on the device (round 5) -----------------
+ * ksg_annotator_attach uploads the annotator's escaped pieces (node keys in
+ * name order, plugin keys, messages) to the context, with the Store's score
+ * weights [KSG_NPLUGINS] and the plugins with ScoreExtensions.  Then
+ * ksg_run_queue_json runs ksg_run_queue(first, count) with capture and writes
+ * every pod's filter-result, score-result and finalscore-result on the device
+ * from the capture rows, byte-identical to ksg_annotate on the same capture:
+ * *json = the values back to back (pod k's three at offsets[3k .. 3k + 3]),
+ * in context-owned pinned memory.  ksg_run_queue_json_async returns once the
+ * values are written on the device, their copy back in flight on a stream
+ * of its own, with a ticket for ksg_json_wait; three buffers rotate, so a
+ * chunk's values stay valid until the third launch after it (consume chunk i
+ * while chunk i + 1 is copied back and chunk i + 2 computed).  Pods the
+ * batched / chip-wide capture paths do not take (host ports, claims) are
+ * refused (KSG_E_UNSUPPORTED): use ksg_annotate for those. */
+int ksg_annotator_attach(ksg_ctx* ctx, const ksg_annotator* a, const int64_t* weight, uint32_t normalize_mask);
+int ksg_run_queue_json(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placements, ksg_result* results,
+                       const char** json, const int64_t** offsets);
+int ksg_run_queue_json_async(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placements, ksg_result* results,
+                             int32_t* ticket);
+int ksg_json_wait(ksg_ctx* ctx, int32_t ticket, const char** json, const int64_t** offsets);
+
 #ifdef __cplusplus
 }
 #endif

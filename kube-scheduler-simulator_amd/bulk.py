@@ -129,3 +129,47 @@ def annotate_queue(engine: native.Engine, bulk: BulkAnnotator, first: int, count
         bulk.serialise(first + off, res, buf, k, sink)
     io.shutdown()
     return out
+
+
+def annotate_queue_device(engine: native.Engine, bulk: BulkAnnotator, first: int, count: int,
+                          sink: Callable[[int, tuple], None], chunk: int = 256) -> np.ndarray:
+    """annotate_queue with the values serialised on the device
+    (ksg_run_queue_json_async, csrc/ksched_json.h): per chunk one captured
+    run whose capture rows never leave HBM, the finished bytes copied back on
+    a stream of their own.  Chunk i's sink (on the annotator's worker
+    threads) overlaps chunk i + 1's copy back and chunk i + 2's run (three
+    pinned buffers rotate in the library).  Pods the capture paths do not take
+    (host ports, claims) are refused by the library: use annotate_queue."""
+    engine.attach_annotator(bulk.annotators[0], bulk.weights, bulk.norm_mask)
+    out = np.empty(count, np.int32)
+    offs_of = list(range(0, count, chunk))
+    io = ThreadPoolExecutor(max_workers=1)
+
+    def launch(j):
+        off = offs_of[j]
+        k = min(chunk, count - off)
+        pl, _, t = engine.run_queue_json_async(first + off, k)
+        out[off:off + k] = pl
+        return off, k, t
+
+    try:
+        launched = [launch(j) for j in range(min(2, len(offs_of)))]
+        for j in range(len(offs_of)):
+            off, k, t = launched[j]
+            js, offs = engine.json_wait(t, k)
+            fut = io.submit(launch, j + 2) if j + 2 < len(offs_of) else None
+
+            def emit(i, js=js, offs=offs, base=first + off):
+                o = offs[3 * i: 3 * i + 4]
+                sink(base + i, (js[o[0]:o[1]], js[o[1]:o[2]], js[o[2]:o[3]]))
+
+            if bulk.pool is None:
+                for i in range(k):
+                    emit(i)
+            else:
+                list(bulk.pool.map(emit, range(k)))
+            if fut is not None:
+                launched.append(fut.result())
+    finally:
+        io.shutdown()
+    return out

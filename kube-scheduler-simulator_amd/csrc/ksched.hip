@@ -48,6 +48,7 @@
 #include "ksched_kernels.h"
 
 #include "ksched_dev.h"
+#include "ksched_json_host.h"
 
 using namespace ksk;
 
@@ -187,6 +188,34 @@ struct ksg_ctx {
   bool ev_clean = false;                    // the arrival counter is zero
   ksg_profile* d_ev_prof = nullptr;
   int32_t* d_ev_pl = nullptr;               // eval_topo_fast's placement word
+  // the device annotation serialiser (ksg_annotator_attach / ksg_run_queue_json)
+  char* d_json_tab = nullptr;               // the uploaded tables (one block)
+  JsonTables json_t{};
+  int json_N = -1;                          // node count the tables were built for (-1: none attached)
+  int json_T = 0;
+  int64_t json_w[KSG_NPLUGINS] = {};
+  uint32_t json_norm = 0;
+  char* d_json_scratch = nullptr;           // per-lane counts, totals, offsets (grown only)
+  size_t json_scratch_bytes = 0;
+  char* d_json_arena = nullptr;             // a chunk's placements, results and capture arrays (grown only):
+  size_t json_arena_bytes = 0;              // no hipFree (a device-wide wait) between chunks
+  // three slots rotate: chunk i is read by the caller while chunk i + 1 is
+  // copied back and chunk i + 2 is computed (ksg_run_queue_json_async)
+  static constexpr int kJsonSlots = 3;
+  char* d_json_out[kJsonSlots] = {};        // a chunk's values on the device
+  size_t json_out_cap[kJsonSlots] = {};
+  char* h_json[kJsonSlots] = {};            // ... and in pinned host memory
+  size_t h_json_cap[kJsonSlots] = {};
+  std::vector<int64_t> json_off[kJsonSlots];   // [3 * count + 1]
+  uint32_t* d_json_err = nullptr;           // [kJsonSlots] error words
+  uint32_t* h_json_err = nullptr;           // ... pinned copies
+  hipEvent_t json_copied[kJsonSlots] = {};  // the slot's copy-back done
+  hipEvent_t json_written = nullptr;
+  hipStream_t json_stream = nullptr;        // the copies back
+  bool json_busy[kJsonSlots] = {};
+  int json_next = 0;
+  int json_last = -1;                       // the slot the last ksg_run_queue_json_async filled
+  bool json_want = false;                   // run_internal: serialise the capture on the device
   char* h_evt = nullptr;                    // eval_topo_fast's pinned block (its own: eval_fast polls words
   size_t h_evt_bytes = 0;                   // that topology rows would otherwise overwrite)
   char* d_hevt = nullptr;
@@ -281,6 +310,7 @@ int upc(ksg_ctx* ctx, const T*& field, const T* src, size_t count) {
 }
 
 void free_all(ksg_ctx* ctx) {
+  ctx->json_N = -1;   // the serialiser's tables name the old nodes
   for (void* p : ctx->allocs) (void)hipFree(p);
   ctx->allocs.clear();
   ctx->stage_pending = false;   // its destination arrays are gone
@@ -1692,6 +1722,112 @@ int flush_commit(ksg_ctx* ctx);
 // (coop_kernel): 262,144 nodes on 256 workgroups.
 bool coop_capture_fits(const ksg_ctx* ctx) { return ctx->c.N <= 4 * 256 * 256; }
 
+// The device serialiser over a captured chunk (ksched_json.h): lengths,
+// offsets, the values; then one copy into the pinned buffer.
+int json_serialise(ksg_ctx* ctx, const CapArgs& ca, const ksg_result* d_res, int32_t first, int32_t count) {
+  const int N = ctx->c.N;
+  if (ctx->json_N != N) return fail(ctx, KSG_E_STATE, "ksg_run_queue_json: no annotator attached for these nodes");
+  JsonArgs ja{};
+  ja.t = ctx->json_t;
+  ja.N = N;
+  ja.T = ctx->c.T;
+  ja.taints = ctx->c.taints;
+  ja.pods = ctx->d_pods;
+  ja.first = first;
+  ja.res = d_res;
+  ja.fstatus = ca.fstatus;
+  ja.raw = ca.raw;
+  ja.norm = ca.norm;
+  ja.n_rows = ca.n_rows;
+  for (int p = 0; p < KSG_NPLUGINS; p++) ja.row_of[p] = -1;
+  for (int q = 0; q < ca.n_rows; q++) ja.row_of[ca.rows[q]] = q;
+  ja.n_filter = ctx->prof.n_filter;
+  for (int i = 0; i < KSG_NPLUGINS; i++) ja.filter_order[i] = ctx->prof.filter_order[i];
+  ja.score_mask = ctx->prof.score_mask;
+  ja.normalize_mask = ctx->json_norm;
+  for (int p = 0; p < KSG_NPLUGINS; p++) ja.weight[p] = ctx->json_w[p];
+  // segments per pod: enough workgroups for the chip at small chunks
+  const int S = std::max(1, std::min(16, (1024 + count - 1) / count));
+  ja.count = count;
+  ja.S = S;
+  const size_t KS = (size_t)count * S;
+  // scratch kept across calls (grown only): per-lane counts, segment totals
+  // and prefixes, value totals, offsets, the error word
+  const size_t need = 8 * (5 * (size_t)kJsonBlock * KS + 5 * KS + 6 * KS + 3 * (size_t)count + 3 * (size_t)count + 1) + 8;
+  if (need > ctx->json_scratch_bytes) {
+    const size_t c = std::max(need, 2 * ctx->json_scratch_bytes);
+    if (ctx->d_json_scratch) (void)hipFree(ctx->d_json_scratch);
+    ctx->d_json_scratch = nullptr;
+    ctx->json_scratch_bytes = 0;
+    HIPC(ctx, hipMalloc((void**)&ctx->d_json_scratch, c));
+    ctx->json_scratch_bytes = c;
+  }
+  ja.scratch = reinterpret_cast<int64_t*>(ctx->d_json_scratch);
+  ja.segtot = ja.scratch + 5 * (size_t)kJsonBlock * KS;
+  ja.segoff = ja.segtot + 5 * KS;
+  ja.totals = ja.segoff + 6 * KS;
+  ja.offsets = ja.totals + 3 * (size_t)count;
+  ja.err = reinterpret_cast<uint32_t*>(ja.offsets + 3 * (size_t)count + 1);
+  if (!ctx->json_stream) {
+    HIPC(ctx, hipStreamCreateWithFlags(&ctx->json_stream, hipStreamNonBlocking));
+    HIPC(ctx, hipEventCreateWithFlags(&ctx->json_written, hipEventDisableTiming));
+    for (int q = 0; q < ksg_ctx::kJsonSlots; q++)
+      HIPC(ctx, hipEventCreateWithFlags(&ctx->json_copied[q], hipEventDisableTiming));
+    HIPC(ctx, hipMalloc((void**)&ctx->d_json_err, sizeof(uint32_t) * ksg_ctx::kJsonSlots));
+    HIPC(ctx, hipHostMalloc((void**)&ctx->h_json_err, sizeof(uint32_t) * ksg_ctx::kJsonSlots, hipHostMallocDefault));
+  }
+  const int slot = ctx->json_next;
+  ctx->json_next = (slot + 1) % ksg_ctx::kJsonSlots;
+  if (ctx->json_busy[slot]) {   // the copy that last filled this slot (the caller read it two calls ago)
+    HIPC(ctx, hipEventSynchronize(ctx->json_copied[slot]));
+    ctx->json_busy[slot] = false;
+  }
+  ja.err = ctx->d_json_err + slot;
+  HIPC(ctx, hipMemsetAsync(ja.err, 0, sizeof(uint32_t), ctx->stream));
+  hipLaunchKernelGGL(ksg_json_len, dim3(KS), dim3(kJsonBlock), 0, ctx->stream, ja);
+  HIPC(ctx, hipGetLastError());
+  hipLaunchKernelGGL(ksg_json_scan, dim3(1), dim3(kJsonBlock), 0, ctx->stream, ja);
+  HIPC(ctx, hipGetLastError());
+  std::vector<int64_t>& joff = ctx->json_off[slot];
+  joff.assign(3 * (size_t)count + 1, 0);
+  uint32_t err = 0;
+  HIPC(ctx, hipMemcpyAsync(joff.data(), ja.offsets, sizeof(int64_t) * joff.size(), hipMemcpyDeviceToHost,
+                           ctx->stream));
+  HIPC(ctx, hipMemcpyAsync(&err, ja.err, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  if (err) return fail(ctx, KSG_E_INVALID, "ksg_run_queue_json: a status word without a message (or a plugin that did not run)");
+  const size_t total = (size_t)joff.back();
+  if (total + 1 > ctx->json_out_cap[slot]) {
+    const size_t c = std::max(total + 1 + total / 2, ctx->json_out_cap[slot] * 2);
+    if (ctx->d_json_out[slot]) (void)hipFree(ctx->d_json_out[slot]);
+    ctx->d_json_out[slot] = nullptr;
+    ctx->json_out_cap[slot] = 0;
+    HIPC(ctx, hipMalloc((void**)&ctx->d_json_out[slot], c));
+    ctx->json_out_cap[slot] = c;
+  }
+  if (total + 1 > ctx->h_json_cap[slot]) {   // grown by half again: pinning is slow, chunks vary a little
+    const size_t c = std::max({total + 1 + total / 2, ctx->h_json_cap[slot] + ctx->h_json_cap[slot] / 2,
+                               (size_t)1 << 20});
+    if (ctx->h_json[slot]) (void)hipHostFree(ctx->h_json[slot]);
+    ctx->h_json[slot] = nullptr;
+    ctx->h_json_cap[slot] = 0;
+    HIPC(ctx, hipHostMalloc((void**)&ctx->h_json[slot], c, hipHostMallocDefault));
+    ctx->h_json_cap[slot] = c;
+  }
+  ja.out = ctx->d_json_out[slot];
+  hipLaunchKernelGGL(ksg_json_write, dim3(KS), dim3(kJsonBlock), 0, ctx->stream, ja);
+  HIPC(ctx, hipGetLastError());
+  // the copy back on its own stream: the next chunk's kernels overlap it
+  HIPC(ctx, hipEventRecord(ctx->json_written, ctx->stream));
+  HIPC(ctx, hipStreamWaitEvent(ctx->json_stream, ctx->json_written, 0));
+  HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot], ctx->d_json_out[slot], total, hipMemcpyDeviceToHost, ctx->json_stream));
+  HIPC(ctx, hipMemcpyAsync(ctx->h_json_err + slot, ja.err, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->json_stream));
+  HIPC(ctx, hipEventRecord(ctx->json_copied[slot], ctx->json_stream));
+  ctx->json_busy[slot] = true;
+  ctx->json_last = slot;
+  return KSG_OK;
+}
+
 int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int32_t* placements,
                  ksg_result* results, ksg_capture* cap) {
   int rc = check_ready(ctx);
@@ -1709,11 +1845,42 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   ksg_profile* d_prof = nullptr;
   int32_t* d_pl = nullptr;
   ksg_result* d_res = nullptr;
-  TA(tmp, &d_prof, sizeof(ksg_profile));
-  TA(tmp, &d_pl, sizeof(int32_t) * count);
-  if (results) TA(tmp, &d_res, sizeof(ksg_result) * count);
+  const bool want_json = ctx->json_want;   // ksg_run_queue_json: the capture stays on the device
+  // The serialiser's chunks carve everything from one arena kept across calls:
+  // a hipFree waits for the whole device, the previous chunk's copy back included.
+  int n_rows = 0;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++) n_rows += (ctx->prof.score_mask >> pl) & 1u;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t arena_parts[8] = {al(sizeof(ksg_profile)), al(sizeof(int32_t) * count), al(sizeof(ksg_result) * count),
+                                 al(sizeof(int32_t) * 4 * KSG_BATCH_MAX), al(sizeof(uint32_t) * N * count),
+                                 al(sizeof(int64_t) * N * count), al(sizeof(int64_t) * N * n_rows * count),
+                                 al(sizeof(int64_t) * N * n_rows * count)};
+  char* arena[8] = {};
+  if (want_json) {
+    size_t need = 0;
+    for (size_t b : arena_parts) need += b;
+    if (need > ctx->json_arena_bytes) {
+      if (ctx->d_json_arena) (void)hipFree(ctx->d_json_arena);
+      ctx->d_json_arena = nullptr;
+      ctx->json_arena_bytes = 0;
+      HIPC(ctx, hipMalloc((void**)&ctx->d_json_arena, need + need / 2));
+      ctx->json_arena_bytes = need + need / 2;
+    }
+    char* b = ctx->d_json_arena;
+    for (int i = 0; i < 8; i++) {
+      arena[i] = b;
+      b += arena_parts[i];
+    }
+    d_prof = reinterpret_cast<ksg_profile*>(arena[0]);
+    d_pl = reinterpret_cast<int32_t*>(arena[1]);
+    d_res = reinterpret_cast<ksg_result*>(arena[2]);
+  } else {
+    TA(tmp, &d_prof, sizeof(ksg_profile));
+    TA(tmp, &d_pl, sizeof(int32_t) * count);
+    if (results) TA(tmp, &d_res, sizeof(ksg_result) * count);
+  }
   HIPC(ctx, hipMemcpyAsync(d_prof, &ctx->prof, sizeof(ksg_profile), hipMemcpyHostToDevice, ctx->stream));
-  const bool want_cap = cap && (cap->fstatus || cap->raw || cap->norm || cap->total);
+  const bool want_cap = want_json || (cap && (cap->fstatus || cap->raw || cap->norm || cap->total));
   QueueArgs a = base_args(ctx);
   bool batched = do_commit && batch_eligible(ctx, first, count);
   if (ctx->force_path == 1) batched = false;
@@ -1722,6 +1889,9 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   const bool topo = !batched && needs_topo(ctx, ctx->prof, first, count);
   const bool coop = topo && ctx->topo_coop && ctx->force_path != 1 && !range_has_ports(ctx, first, count) &&
                     (!want_cap || coop_capture_fits(ctx));
+  if (want_json && !(batched || coop))
+    return fail(ctx, KSG_E_UNSUPPORTED, "ksg_run_queue_json: these pods take neither the batched nor the "
+                                        "chip-wide capture path (use ksg_annotate)");
   // captured queues take the batched path too (ksched_capture.h): the capture
   // kernels write the profile's score rows only, in a compact layout (the
   // chip-wide topology path writes the same layout)
@@ -1735,12 +1905,20 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     ca.placements = d_pl;
     for (int pl = 0; pl < KSG_NPLUGINS; pl++)
       if ((ctx->prof.score_mask >> pl) & 1u) ca.rows[ca.n_rows++] = pl;
-    TA(tmp, &ca.stats, sizeof(int32_t) * 4 * KSG_BATCH_MAX);
-    TA(tmp, &ca.fstatus, sizeof(uint32_t) * N * count);
-    TA(tmp, &ca.total, sizeof(int64_t) * N * count);
-    if (ca.n_rows) {
-      TA(tmp, &ca.raw, sizeof(int64_t) * N * ca.n_rows * count);
-      TA(tmp, &ca.norm, sizeof(int64_t) * N * ca.n_rows * count);
+    if (want_json) {
+      ca.stats = reinterpret_cast<int32_t*>(arena[3]);
+      ca.fstatus = reinterpret_cast<uint32_t*>(arena[4]);
+      ca.total = reinterpret_cast<int64_t*>(arena[5]);
+      ca.raw = ca.n_rows ? reinterpret_cast<int64_t*>(arena[6]) : nullptr;
+      ca.norm = ca.n_rows ? reinterpret_cast<int64_t*>(arena[7]) : nullptr;
+    } else {
+      TA(tmp, &ca.stats, sizeof(int32_t) * 4 * KSG_BATCH_MAX);
+      TA(tmp, &ca.fstatus, sizeof(uint32_t) * N * count);
+      TA(tmp, &ca.total, sizeof(int64_t) * N * count);
+      if (ca.n_rows) {
+        TA(tmp, &ca.raw, sizeof(int64_t) * N * ca.n_rows * count);
+        TA(tmp, &ca.norm, sizeof(int64_t) * N * ca.n_rows * count);
+      }
     }
   } else if (want_cap) {
     TA(tmp, &a.cap_fstatus, sizeof(uint32_t) * N * count);
@@ -1784,9 +1962,12 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
       return rc;
     }
   }
+  if (want_json && (rc = json_serialise(ctx, ca, d_res, first, count))) return rc;
   if (placements) HIPC(ctx, hipMemcpyAsync(placements, d_pl, sizeof(int32_t) * count, hipMemcpyDeviceToHost, ctx->stream));
   if (results) HIPC(ctx, hipMemcpyAsync(results, d_res, sizeof(ksg_result) * count, hipMemcpyDeviceToHost, ctx->stream));
-  if (want_cap && (batched || coop)) {
+  if (want_json) {
+    // nothing else to copy: the values went to the pinned buffer
+  } else if (want_cap && (batched || coop)) {
     if (cap->fstatus) HIPC(ctx, hipMemcpyAsync(cap->fstatus, ca.fstatus, sizeof(uint32_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
     if (cap->total) HIPC(ctx, hipMemcpyAsync(cap->total, ca.total, sizeof(int64_t) * N * count, hipMemcpyDeviceToHost, ctx->stream));
     for (int q = 0; q < ca.n_rows; q++) {   // compact row q -> the caller's plugin row, every pod
@@ -2741,6 +2922,19 @@ int ksg_close(ksg_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->h_ev) (void)hipHostFree(ctx->h_ev);
   if (ctx->h_evt) (void)hipHostFree(ctx->h_evt);
+  if (ctx->d_json_tab) (void)hipFree(ctx->d_json_tab);
+  if (ctx->json_stream) (void)hipStreamSynchronize(ctx->json_stream);
+  for (int q = 0; q < ksg_ctx::kJsonSlots; q++) {
+    if (ctx->d_json_out[q]) (void)hipFree(ctx->d_json_out[q]);
+    if (ctx->h_json[q]) (void)hipHostFree(ctx->h_json[q]);
+    if (ctx->json_copied[q]) (void)hipEventDestroy(ctx->json_copied[q]);
+  }
+  if (ctx->json_written) (void)hipEventDestroy(ctx->json_written);
+  if (ctx->json_stream) (void)hipStreamDestroy(ctx->json_stream);
+  if (ctx->d_json_err) (void)hipFree(ctx->d_json_err);
+  if (ctx->h_json_err) (void)hipHostFree(ctx->h_json_err);
+  if (ctx->d_json_scratch) (void)hipFree(ctx->d_json_scratch);
+  if (ctx->d_json_arena) (void)hipFree(ctx->d_json_arena);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->ev_stage) (void)hipEventDestroy(ctx->ev_stage);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -2975,6 +3169,102 @@ int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t 
     ctx->max_blob = blob0;
   }
   return rc;
+}
+
+int ksg_annotator_attach(ksg_ctx* ctx, const ksg_annotator* ann, const int64_t* weight, uint32_t normalize_mask) {
+  if (int rc_ = srv_stop(ctx)) return rc_;
+  if (!ctx || !ann || !weight) return KSG_E_INVALID;
+  if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "load nodes before attaching an annotator");
+  JsonHostTables t;
+  int rc = ksg_annotator_json_tables(ann, &t);
+  if (rc) return fail(ctx, rc, "annotator tables");
+  if ((int)t.node_order.size() != ctx->c.N) return fail(ctx, KSG_E_INVALID, "annotator and context node counts differ");
+  if (t.max_taints != ctx->c.T && ctx->c.T > 0) return fail(ctx, KSG_E_INVALID, "annotator and context taint slots differ");
+  HIPC(ctx, hipSetDevice(ctx->device));
+  // one block: node key offsets (8-aligned first), then the 4-byte arrays, then the bytes
+  std::vector<char> blob;
+  auto put = [&](const void* p, size_t n) {
+    const size_t at = (blob.size() + 7) & ~(size_t)7;
+    blob.resize(at + n);
+    if (n) std::memcpy(blob.data() + at, p, n);
+    return at;
+  };
+  const size_t o_nko = put(t.node_key_off.data(), 8 * t.node_key_off.size());
+  const size_t o_ord = put(t.node_order.data(), 4 * t.node_order.size());
+  const size_t o_pko = put(t.plugin_key_off.data(), 4 * t.plugin_key_off.size());
+  const size_t o_mo = put(t.msg_off.data(), 4 * t.msg_off.size());
+  const size_t o_tmo = put(t.taint_msg_off.data(), 4 * t.taint_msg_off.size());
+  const size_t o_fpo = put(t.fit_part_off.data(), 4 * t.fit_part_off.size());
+  const size_t o_nk = put(t.node_keys.data(), t.node_keys.size());
+  const size_t o_pk = put(t.plugin_keys.data(), t.plugin_keys.size());
+  const size_t o_m = put(t.msgs.data(), t.msgs.size());
+  const size_t o_tm = put(t.taint_msgs.data(), t.taint_msgs.size());
+  const size_t o_fp = put(t.fit_parts.data(), t.fit_parts.size());
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->d_json_tab) (void)hipFree(ctx->d_json_tab);
+  ctx->d_json_tab = nullptr;
+  ctx->json_N = -1;
+  HIPC(ctx, hipMalloc((void**)&ctx->d_json_tab, std::max<size_t>(blob.size(), 8)));
+  HIPC(ctx, hipMemcpy(ctx->d_json_tab, blob.data(), blob.size(), hipMemcpyHostToDevice));
+  char* d = ctx->d_json_tab;
+  JsonTables& j = ctx->json_t;
+  j.node_key_off = reinterpret_cast<const int64_t*>(d + o_nko);
+  j.node_order = reinterpret_cast<const int32_t*>(d + o_ord);
+  j.plugin_key_off = reinterpret_cast<const int32_t*>(d + o_pko);
+  j.msg_off = reinterpret_cast<const int32_t*>(d + o_mo);
+  j.taint_msg_off = reinterpret_cast<const int32_t*>(d + o_tmo);
+  j.fit_part_off = reinterpret_cast<const int32_t*>(d + o_fpo);
+  j.node_keys = d + o_nk;
+  j.plugin_keys = d + o_pk;
+  j.msgs = d + o_m;
+  j.taint_msgs = d + o_tm;
+  j.fit_parts = d + o_fp;
+  for (int i = 0; i < KSG_NPLUGINS; i++) j.by_name[i] = t.by_name[i];
+  j.n_res = t.n_res;
+  j.n_taint_vocab = t.n_taint_vocab;
+  for (int p = 0; p < KSG_NPLUGINS; p++) ctx->json_w[p] = weight[p];
+  ctx->json_norm = normalize_mask;
+  ctx->json_N = ctx->c.N;
+  return KSG_OK;
+}
+
+int ksg_run_queue_json_async(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placements, ksg_result* results,
+                             int32_t* ticket) {
+  if (!ctx || !ticket) return KSG_E_INVALID;
+  if (count <= 0) return fail(ctx, KSG_E_INVALID, "ksg_run_queue_json: empty pod range");
+  ctx->json_want = true;
+  const int rc = run_internal(ctx, first, count, 1, placements, results, nullptr);
+  ctx->json_want = false;
+  if (rc) return rc;
+  *ticket = ctx->json_last;
+  return KSG_OK;
+}
+
+int ksg_json_wait(ksg_ctx* ctx, int32_t ticket, const char** json, const int64_t** offsets) {
+  if (!ctx || !json || !offsets || ticket < 0 || ticket >= ksg_ctx::kJsonSlots || !ctx->h_json[ticket])
+    return KSG_E_INVALID;
+  HIPC(ctx, hipEventSynchronize(ctx->json_copied[ticket]));
+  if (ctx->h_json_err[ticket]) return fail(ctx, KSG_E_INVALID, "ksg_run_queue_json: a status word without a message");
+  const size_t total = (size_t)ctx->json_off[ticket].back();
+  ctx->h_json[ticket][total] = 0;
+  *json = ctx->h_json[ticket];
+  *offsets = ctx->json_off[ticket].data();
+  return KSG_OK;
+}
+
+int ksg_run_queue_json(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placements, ksg_result* results,
+                       const char** json, const int64_t** offsets) {
+  if (!ctx || !json || !offsets) return KSG_E_INVALID;
+  if (count == 0) {
+    static const char kEmpty[1] = {0};
+    static const int64_t kZero[1] = {0};
+    *json = kEmpty;
+    *offsets = kZero;
+    return KSG_OK;
+  }
+  int32_t t = -1;
+  const int rc = ksg_run_queue_json_async(ctx, first, count, placements, results, &t);
+  return rc ? rc : ksg_json_wait(ctx, t, json, offsets);
 }
 
 int ksg_run_queue(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* placements, ksg_result* results,

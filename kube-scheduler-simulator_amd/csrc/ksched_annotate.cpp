@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "ksched.h"
+#include "ksched_json_host.h"
 
 namespace {
 
@@ -438,5 +439,67 @@ extern "C" int ksg_annotate(ksg_annotator* a, const ksg_annotate_in* in, const c
     json[i] = a->out[i].d;
     len[i] = (int64_t)a->out[i].n;
   }
+  return KSG_OK;
+}
+
+// The device serialiser's tables (ksched_json.h): the same escaped pieces
+// this file's ksg_annotate writes, packed flat.
+int ksg_annotator_json_tables(const ksg_annotator* a, JsonHostTables* t) {
+  if (!a || !t) return KSG_E_INVALID;
+  const int N = a->N;
+  t->node_keys.clear();
+  t->node_key_off.assign(1, 0);
+  for (int n = 0; n < N; n++) {
+    t->node_keys += a->node_json[n];
+    t->node_key_off.push_back((int64_t)t->node_keys.size());
+  }
+  t->node_order = a->node_order;
+  t->plugin_keys.clear();
+  t->plugin_key_off.assign(1, 0);
+  for (int p = 0; p < KSG_NPLUGINS; p++) {
+    t->plugin_keys += a->plugin[p];
+    t->plugin_key_off.push_back((int32_t)t->plugin_keys.size());
+  }
+  int ids[KSG_NPLUGINS];
+  for (int p = 0; p < KSG_NPLUGINS; p++) ids[p] = p;
+  const std::vector<int> order = sorted_plugins(a, ids, KSG_NPLUGINS);
+  for (int i = 0; i < KSG_NPLUGINS; i++) t->by_name[i] = order[i];
+  // the messages that depend on nothing but (plugin, reason)
+  t->msgs.clear();
+  t->msg_off.assign(1, 0);
+  std::string m, q;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
+    for (int r = 0; r < 8; r++) {
+      if (pl != KSG_PL_TAINT_TOLERATION && pl != KSG_PL_NODE_RESOURCES_FIT &&
+          filter_message(a, (uint32_t)(pl + 1) | ((uint32_t)r << 8), 0, m)) {
+        q.clear();
+        go_string(q, m.c_str());
+        t->msgs += q;
+      }
+      t->msg_off.push_back((int32_t)t->msgs.size());
+    }
+  t->taint_msgs.clear();
+  t->taint_msg_off.assign(1, 0);
+  for (auto& tn : a->taint) {
+    q.clear();
+    go_string(q, ("node(s) had untolerated taint " + tn).c_str());
+    t->taint_msgs += q;
+    t->taint_msg_off.push_back((int32_t)t->taint_msgs.size());
+  }
+  auto inner = [&](const std::string& x) {   // escaped, without the quotes
+    q.clear();
+    go_string(q, x.c_str());
+    return q.substr(1, q.size() - 2);
+  };
+  t->fit_parts = inner("Too many pods");
+  t->fit_part_off.assign(1, 0);
+  t->fit_part_off.push_back((int32_t)t->fit_parts.size());
+  for (int r = 0; r < (int)a->res.size(); r++) {
+    t->fit_parts += inner(std::string("Insufficient ") + (r < 3 ? kFitRes[r] : a->res[r].c_str()));
+    t->fit_part_off.push_back((int32_t)t->fit_parts.size());
+  }
+  t->n_res = (int32_t)a->res.size();
+  t->n_taint_vocab = (int32_t)a->taint.size();
+  t->max_taints = a->max_taints;
   return KSG_OK;
 }

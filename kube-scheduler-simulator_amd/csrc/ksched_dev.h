@@ -2449,3 +2449,7 @@ __global__ __launch_bounds__(256) void ksg_range32(DevCluster c, DevState st, in
 #endif  // KSG_PART
 
 }  // namespace ksk
+
+#ifndef KSG_PART
+#include "ksched_json.h"   // the device annotation serialiser (host TU only)
+#endif

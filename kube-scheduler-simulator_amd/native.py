@@ -267,6 +267,16 @@ class Engine:
                            if hasattr(self.lib, self.PREFIX + "eval_view") else None)
         self._commit = f("commit", C.c_int, vp, C.c_int32, C.c_int32)
         self._run_queue = f("run_queue", C.c_int, vp, C.c_int32, C.c_int32, i32p, vp, C.POINTER(KsgCapture))
+        # the product library's device annotation serialiser (the CPU oracle has none)
+        self._attach = self._run_queue_json = self._run_queue_json_async = self._json_wait = None
+        if hasattr(self.lib, self.PREFIX + "annotator_attach"):
+            self._attach = f("annotator_attach", C.c_int, vp, vp, C.POINTER(C.c_int64), C.c_uint32)
+            self._run_queue_json = f("run_queue_json", C.c_int, vp, C.c_int32, C.c_int32, i32p, vp,
+                                     C.POINTER(C.c_void_p), C.POINTER(C.POINTER(C.c_int64)))
+            self._run_queue_json_async = f("run_queue_json_async", C.c_int, vp, C.c_int32, C.c_int32, i32p, vp,
+                                           C.POINTER(C.c_int32))
+            self._json_wait = f("json_wait", C.c_int, vp, C.c_int32, C.POINTER(C.c_void_p),
+                                C.POINTER(C.POINTER(C.c_int64)))
         self._read_state = f("read_state", C.c_int, vp, C.POINTER(KsgNodeState))
         self._reset_state = f("reset_state", C.c_int, vp)
         self._uncommit = f("uncommit", C.c_int, vp, C.c_int32, C.c_int32)
@@ -404,6 +414,53 @@ class Engine:
                                     res.ctypes.data if res is not None else None,
                                     C.byref(capture.struct) if capture else None))
         return pl, res
+
+    def attach_annotator(self, ann: "Annotator", weight, normalize_mask: int):
+        """ksg_annotator_attach: the annotator's escaped pieces to the device,
+        with the Store's score weights [NPLUGINS] (for run_queue_json)."""
+        if self._attach is None:
+            raise KschedError(f"{self.PREFIX}annotator_attach: this library has no device serialiser")
+        w = np.ascontiguousarray(weight, np.int64)
+        self._check(self._attach(self.ctx, ann.h, w.ctypes.data_as(C.POINTER(C.c_int64)), int(normalize_mask)))
+
+    def run_queue_json(self, first: int, count: int):
+        """ksg_run_queue_json: placements, results, the three annotation
+        values of every pod serialised on the device (one read-only
+        memoryview over the context's pinned buffer, valid until the next
+        call) and their offsets [3 * count + 1] (pod k's values at
+        offsets[3k : 3k + 4])."""
+        pl = np.zeros(count, np.int32)
+        res = np.zeros(count, RESULT_DTYPE)
+        js = C.c_void_p()
+        off = C.POINTER(C.c_int64)()
+        self._check(self._run_queue_json(self.ctx, first, count, _ptr(pl, i32p), res.ctypes.data, C.byref(js),
+                                         C.byref(off)))
+        return (pl, res) + self._json_view(js, off, count)
+
+    @staticmethod
+    def _json_view(js, off, count):
+        offsets = np.ctypeslib.as_array(off, shape=(3 * count + 1,)).copy()
+        total = int(offsets[-1])
+        buf = (C.c_char * max(total, 1)).from_address(js.value) if total else (C.c_char * 1)()
+        return memoryview(buf).cast("B")[:total].toreadonly(), offsets
+
+    def run_queue_json_async(self, first: int, count: int):
+        """ksg_run_queue_json_async: placements, results and a ticket; the
+        values' copy back is in flight (json_wait(ticket, count))."""
+        pl = np.zeros(count, np.int32)
+        res = np.zeros(count, RESULT_DTYPE)
+        t = C.c_int32()
+        self._check(self._run_queue_json_async(self.ctx, first, count, _ptr(pl, i32p), res.ctypes.data,
+                                               C.byref(t)))
+        return pl, res, t.value
+
+    def json_wait(self, ticket: int, count: int):
+        """ksg_json_wait: (values memoryview, offsets) of a launched chunk,
+        valid until the third launch after it."""
+        js = C.c_void_p()
+        off = C.POINTER(C.c_int64)()
+        self._check(self._json_wait(self.ctx, ticket, C.byref(js), C.byref(off)))
+        return self._json_view(js, off, count)
 
     def run_replicas(self, profiles, first: int, count: int):
         R = len(profiles)

@@ -1,0 +1,9 @@
+#!/bin/bash
+set -uo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r5p
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof -o run -- python3 -u scripts/annot_dev.py 2000 256 > $O/prof.log 2>&1 || { echo "prof failed"; tail -5 $O/prof.log; exit 1; }
+grep "rep" $O/prof.log
+for f in $(find $O/prof -name '*stats.csv'); do echo "== $f"; cut -d, -f1-4 "$f" | head -14; done

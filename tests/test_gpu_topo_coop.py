@@ -89,16 +89,18 @@ def test_topo_coop_matches_oracle(gpu, oracle, name, make):
     np.testing.assert_array_equal(np.concatenate([p1, p2]), po)
 
 
-@pytest.mark.parametrize("tables", ["1", "0"], ids=["tables", "pre-pass"])
-def test_configs2_30000_pods_golden(built, tables):
-    """configs[2]'s full 15,000-node cluster with a 30,000-pod queue against the
-    C++ oracle's placements, per-pod results and final pod counts
-    (tests/golden/c3_15000x30000.npz, tests/golden/make_c3_large.py: the oracle
-    takes minutes at this size): the maintained domain tables and their
-    one-pod lag over a long queue, and the pre-pass path (KSG_COOP_TABLES=0)."""
+@pytest.mark.parametrize("n_pods,tables", [(30000, "1"), (30000, "0"), (150000, "1")],
+                         ids=["30k-tables", "30k-pre-pass", "150k-tables"])
+def test_configs2_golden(built, n_pods, tables):
+    """configs[2]'s full 15,000-node cluster against the C++ oracle's
+    placements, per-pod results and final pod counts
+    (tests/golden/c3_15000x<P>.npz, tests/golden/make_c3_large.py: the oracle
+    takes minutes to hours at these sizes): a 30,000-pod queue with the
+    maintained domain tables and their one-pod lag, and with the pre-pass path
+    (KSG_COOP_TABLES=0); and BASELINE.json's full 150,000-pod queue."""
     import os
-    gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c3_15000x30000.npz"))
-    nodes, pods, prof = G.config3(n_nodes=15000, n_pods=30000)
+    gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"c3_15000x{n_pods}.npz"))
+    nodes, pods, prof = G.config3(n_nodes=15000, n_pods=n_pods)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
     old = os.environ.get("KSG_COOP_TABLES")
