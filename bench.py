@@ -318,6 +318,30 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
             "pods_per_s_light_sink": n_pods / wall_light, "device_serialiser": dev}
 
 
+def device_serialiser_long(eng, enc, prof, B, n_pods: int, chunk: int, threads: int):
+    """The device serialiser's steady state: ksg_run_queue_json_async over a
+    longer queue than the digest sample (pipeline fill and drain amortised),
+    light sink; every annotation byte still lands in pinned host memory."""
+    import numpy as np
+    lens = np.zeros(n_pods, np.int64)
+
+    def light(i, vals):
+        lens[i] = sum(len(v) for v in vals)
+
+    bulk = B.BulkAnnotator(enc, prof, threads=threads)
+    try:
+        eng.reset_state()
+        B.annotate_queue_device(eng, bulk, 0, min(3 * chunk, n_pods), light, chunk=chunk)
+        eng.reset_state()
+        t = time.perf_counter()
+        B.annotate_queue_device(eng, bulk, 0, n_pods, light, chunk=chunk)
+        wall = time.perf_counter() - t
+    finally:
+        bulk.close()
+    return {"pods": n_pods, "chunk": chunk, "pods_per_s": n_pods / wall, "wall_s": wall,
+            "annotation_bytes": int(lens.sum()), "annotation_GB_per_s": lens.sum() / wall / 1e9}
+
+
 def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=None, label: str = "configs[1]",
                       server: bool = False):
     """The drop-in's per-cycle path, the calls the Go
@@ -503,6 +527,10 @@ def main():
     ap.add_argument("--sweep-pods", type=int, default=1000)
     ap.add_argument("--annotate-pods", type=int, default=2000, help="annotation sidecar; 0 disables")
     ap.add_argument("--annotate-threads", type=int, default=16)
+    ap.add_argument("--annotate-long-pods", type=int, default=8000,
+                    help="device serialiser steady state over this many configs[1] pods; 0 disables")
+    ap.add_argument("--topo-annotate-long-pods", type=int, default=1024,
+                    help="device serialiser steady state over a configs[2] queue of this many pods; 0 disables")
     ap.add_argument("--cycle-pods", type=int, default=2000, help="per-cycle sidecar; 0 disables")
     ap.add_argument("--cycle-warm", type=int, default=500)
     ap.add_argument("--kubelet-pods", type=int, default=50000, help="kubelet-memory line; 0 disables")
@@ -651,6 +679,9 @@ def main():
             B = importlib.import_module(PKG + ".bulk")
             ann = annotation_sidecar(eng1, enc1, prof1, native, B, min(args.annotate_pods, args.configs1_pods), 256,
                                      args.annotate_threads)
+            if args.annotate_long_pods > 0 and isinstance(ann.get("device_serialiser"), dict):
+                ann["device_serialiser"]["steady_state"] = device_serialiser_long(
+                    eng1, enc1, prof1, B, min(args.annotate_long_pods, args.configs1_pods), 256, args.annotate_threads)
         except Exception as e:
             log(f"[rank {rank}] annotation sidecar unavailable: {e}")
     if eng1 is not None:
@@ -681,6 +712,14 @@ def main():
             ann3 = annotation_sidecar(eng3, enc3, prof3, native, B, len(p3), 64, args.annotate_threads,
                                       label="configs[2]")
             eng3.close()
+            if args.topo_annotate_long_pods > 0 and isinstance(ann3.get("device_serialiser"), dict):
+                n3, p3, prof3 = G.config3(n_nodes=args.topo_nodes, n_pods=args.topo_annotate_long_pods)
+                enc3 = E.Encoder(n3, p3, prof3)
+                eng3 = native.Engine(device=local_rank)
+                eng3.load(enc3, E.encode_profile(prof3, enc3.cluster.res_names))
+                ann3["device_serialiser"]["steady_state"] = device_serialiser_long(
+                    eng3, enc3, prof3, B, len(p3), 64, args.annotate_threads)
+                eng3.close()
         except Exception as e:
             log(f"[rank {rank}] configs[2] annotation sidecar unavailable: {e}")
     kub = None

@@ -212,6 +212,9 @@ struct ksg_ctx {
   hipEvent_t json_copied[kJsonSlots] = {};  // the slot's copy-back done
   hipEvent_t json_written = nullptr;
   hipStream_t json_stream = nullptr;        // the copies back
+  hipStream_t json_stream2 = nullptr;       // the second half of a split copy (a second DMA engine)
+  hipEvent_t json_half = nullptr;
+  int json_split = 0;                       // KSG_JSON_SPLIT=1: the copy back in two halves on two streams
   bool json_busy[kJsonSlots] = {};
   int json_next = 0;
   int json_last = -1;                       // the slot the last ksg_run_queue_json_async filled
@@ -1751,9 +1754,9 @@ int json_serialise(ksg_ctx* ctx, const CapArgs& ca, const ksg_result* d_res, int
   ja.count = count;
   ja.S = S;
   const size_t KS = (size_t)count * S;
-  // scratch kept across calls (grown only): per-lane counts, segment totals
-  // and prefixes, value totals, offsets, the error word
-  const size_t need = 8 * (5 * (size_t)kJsonBlock * KS + 5 * KS + 6 * KS + 3 * (size_t)count + 3 * (size_t)count + 1) + 8;
+  // scratch kept across calls (grown only): segment totals and prefixes,
+  // value totals, offsets
+  const size_t need = 8 * (5 * KS + 6 * KS + 3 * (size_t)count + 3 * (size_t)count + 1) + 8;
   if (need > ctx->json_scratch_bytes) {
     const size_t c = std::max(need, 2 * ctx->json_scratch_bytes);
     if (ctx->d_json_scratch) (void)hipFree(ctx->d_json_scratch);
@@ -1762,14 +1765,16 @@ int json_serialise(ksg_ctx* ctx, const CapArgs& ca, const ksg_result* d_res, int
     HIPC(ctx, hipMalloc((void**)&ctx->d_json_scratch, c));
     ctx->json_scratch_bytes = c;
   }
-  ja.scratch = reinterpret_cast<int64_t*>(ctx->d_json_scratch);
-  ja.segtot = ja.scratch + 5 * (size_t)kJsonBlock * KS;
+  ja.segtot = reinterpret_cast<int64_t*>(ctx->d_json_scratch);
   ja.segoff = ja.segtot + 5 * KS;
   ja.totals = ja.segoff + 6 * KS;
   ja.offsets = ja.totals + 3 * (size_t)count;
   ja.err = reinterpret_cast<uint32_t*>(ja.offsets + 3 * (size_t)count + 1);
   if (!ctx->json_stream) {
     HIPC(ctx, hipStreamCreateWithFlags(&ctx->json_stream, hipStreamNonBlocking));
+    HIPC(ctx, hipStreamCreateWithFlags(&ctx->json_stream2, hipStreamNonBlocking));
+    HIPC(ctx, hipEventCreateWithFlags(&ctx->json_half, hipEventDisableTiming));
+    if (const char* e = getenv("KSG_JSON_SPLIT")) ctx->json_split = atoi(e) != 0;
     HIPC(ctx, hipEventCreateWithFlags(&ctx->json_written, hipEventDisableTiming));
     for (int q = 0; q < ksg_ctx::kJsonSlots; q++)
       HIPC(ctx, hipEventCreateWithFlags(&ctx->json_copied[q], hipEventDisableTiming));
@@ -1815,12 +1820,22 @@ int json_serialise(ksg_ctx* ctx, const CapArgs& ca, const ksg_result* d_res, int
     ctx->h_json_cap[slot] = c;
   }
   ja.out = ctx->d_json_out[slot];
-  hipLaunchKernelGGL(ksg_json_write, dim3(KS), dim3(kJsonBlock), 0, ctx->stream, ja);
+  hipLaunchKernelGGL(ksg_json_write, dim3(KS), dim3(kJsonWBlock), 0, ctx->stream, ja);
   HIPC(ctx, hipGetLastError());
   // the copy back on its own stream: the next chunk's kernels overlap it
   HIPC(ctx, hipEventRecord(ctx->json_written, ctx->stream));
   HIPC(ctx, hipStreamWaitEvent(ctx->json_stream, ctx->json_written, 0));
-  HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot], ctx->d_json_out[slot], total, hipMemcpyDeviceToHost, ctx->json_stream));
+  if (ctx->json_split && total >= ((size_t)1 << 24)) {
+    const size_t h = (total / 2 + 4095) & ~(size_t)4095;
+    HIPC(ctx, hipStreamWaitEvent(ctx->json_stream2, ctx->json_written, 0));
+    HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot] + h, ctx->d_json_out[slot] + h, total - h, hipMemcpyDeviceToHost,
+                             ctx->json_stream2));
+    HIPC(ctx, hipEventRecord(ctx->json_half, ctx->json_stream2));
+    HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot], ctx->d_json_out[slot], h, hipMemcpyDeviceToHost, ctx->json_stream));
+    HIPC(ctx, hipStreamWaitEvent(ctx->json_stream, ctx->json_half, 0));
+  } else {
+    HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot], ctx->d_json_out[slot], total, hipMemcpyDeviceToHost, ctx->json_stream));
+  }
   HIPC(ctx, hipMemcpyAsync(ctx->h_json_err + slot, ja.err, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->json_stream));
   HIPC(ctx, hipEventRecord(ctx->json_copied[slot], ctx->json_stream));
   ctx->json_busy[slot] = true;
@@ -2924,6 +2939,7 @@ int ksg_close(ksg_ctx* ctx) {
   if (ctx->h_evt) (void)hipHostFree(ctx->h_evt);
   if (ctx->d_json_tab) (void)hipFree(ctx->d_json_tab);
   if (ctx->json_stream) (void)hipStreamSynchronize(ctx->json_stream);
+  if (ctx->json_stream2) (void)hipStreamSynchronize(ctx->json_stream2);
   for (int q = 0; q < ksg_ctx::kJsonSlots; q++) {
     if (ctx->d_json_out[q]) (void)hipFree(ctx->d_json_out[q]);
     if (ctx->h_json[q]) (void)hipHostFree(ctx->h_json[q]);
@@ -2931,6 +2947,8 @@ int ksg_close(ksg_ctx* ctx) {
   }
   if (ctx->json_written) (void)hipEventDestroy(ctx->json_written);
   if (ctx->json_stream) (void)hipStreamDestroy(ctx->json_stream);
+  if (ctx->json_stream2) (void)hipStreamDestroy(ctx->json_stream2);
+  if (ctx->json_half) (void)hipEventDestroy(ctx->json_half);
   if (ctx->d_json_err) (void)hipFree(ctx->d_json_err);
   if (ctx->h_json_err) (void)hipHostFree(ctx->h_json_err);
   if (ctx->d_json_scratch) (void)hipFree(ctx->d_json_scratch);

@@ -7,13 +7,18 @@
 //
 // Three kernels per chunk of pods:
 //   ksg_json_len    S workgroups per pod (node segments in name order), lanes
-//                   over contiguous runs of a segment: each lane's byte
-//                   counts of its nodes' fragments and how many nodes it
-//                   emits, the segment's totals;
+//                   over contiguous runs of a segment: the segment's byte
+//                   counts and emitted entries per value;
 //   ksg_json_scan   one workgroup: segment prefixes, value lengths, and the
 //                   byte offset of every value (pod-major);
-//   ksg_json_write  S workgroups per pod again: each lane's start from its
-//                   segment's prefix and a workgroup scan, then its fragments.
+//   ksg_json_write  S workgroups per pod again, rounds of kJsonWBlock
+//                   consecutive nodes (one per lane): a workgroup scan of the
+//                   entries' lengths places each entry in an LDS window, and
+//                   the window goes out as lane-consecutive (coalesced) byte
+//                   stores.  A lane writing its own run straight to HBM made
+//                   every store instruction touch 64 lines (3.7 ms per
+//                   64-pod chunk at 15,000 nodes) and slowed the concurrent
+//                   copy back of the previous chunk.
 // Every string piece (quoted node keys, plugin keys, messages) arrives
 // escaped from the host annotator; the device only copies pieces and formats
 // integers.
@@ -22,6 +27,8 @@
 namespace ksk {
 
 constexpr int kJsonBlock = 256;
+constexpr int kJsonWBlock = 128;        // ksg_json_write: nodes per round
+constexpr int kJsonWin = 40 * 1024;     // ksg_json_write: LDS window bytes
 
 struct JsonTables {
   const char* node_keys;          // node n's "<name>": at node_key_off[n]
@@ -60,7 +67,6 @@ struct JsonArgs {
   int64_t weight[KSG_NPLUGINS];   // the Store's score weights
   int32_t count;                  // pods in the chunk
   int32_t S;                      // node segments per pod (workgroups per pod)
-  int64_t* scratch;               // [count][S][kJsonBlock][5] per-lane counts
   int64_t* segtot;                // [count][S][5] per-segment counts
   int64_t* segoff;                // [count][S][6] bytes / entries before the segment, per value
   int64_t* totals;                // [count * 3] bytes of each value
@@ -307,7 +313,7 @@ __global__ __launch_bounds__(kJsonBlock) void ksg_json_len(JsonArgs a) {
   const int k = blockIdx.x / a.S, seg = blockIdx.x % a.S, tid = threadIdx.x;
   if (tid == 0) s_q = json_pod(a, k);
   __syncthreads();
-  const JsonPod q = s_q;
+  const JsonPod& q = s_q;   // read in LDS: pos[] is indexed by plugin (a private copy would live in scratch)
   const int N = a.N;
   int k0, k1;
   lane_range(a, seg, tid, k0, k1);
@@ -329,12 +335,6 @@ __global__ __launch_bounds__(kJsonBlock) void ksg_json_len(JsonArgs a) {
       cs += 1;
     }
   }
-  int64_t* sc = a.scratch + ((size_t)blockIdx.x * kJsonBlock + tid) * 5;
-  sc[0] = lf;
-  sc[1] = cf;
-  sc[2] = ls;
-  sc[3] = lt;
-  sc[4] = cs;
   if (err) atomicOr(a.err, err);
   int64_t t[5];
   (void)block_exscan(lf, s_buf, t[0]);
@@ -378,68 +378,207 @@ __global__ __launch_bounds__(kJsonBlock) void ksg_json_scan(JsonArgs a) {
   if (threadIdx.x == 0) a.offsets[n] = carry;
 }
 
-__global__ __launch_bounds__(kJsonBlock) void ksg_json_write(JsonArgs a) {
+// Bytes of one entry into an LDS window [lo, hi) of the value: pos is the
+// entry's position in the value; bytes outside the window are dropped (a
+// later window pass writes them).
+struct JsonWin {
+  char* buf;
+  int64_t lo, hi, pos;
+  __device__ __forceinline__ void c(char ch) {
+    if (pos >= lo && pos < hi) buf[pos - lo] = ch;
+    pos++;
+  }
+  __device__ __forceinline__ void s(const char* p, int64_t n) {
+    for (int64_t i = 0; i < n; i++) c(p[i]);
+  }
+  __device__ __forceinline__ void qint(int64_t v) {
+    const uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    const int d = dec_len(u);
+    c('"');
+    if (v < 0) c('-');
+    uint64_t x = u;
+    for (int i = d - 1; i >= 0; i--) {   // digits in place, last first
+      const int64_t at = pos + i;
+      if (at >= lo && at < hi) buf[at - lo] = (char)('0' + x % 10);
+      x /= 10;
+    }
+    pos += d;
+    c('"');
+  }
+};
+
+// msg_piece's bytes (its length was checked by ksg_json_len)
+__device__ __forceinline__ void emit_msg(JsonWin& w, const JsonArgs& a, uint32_t st, int n) {
+  const int pl = (int)(st & 0xFF) - 1;
+  const uint32_t reason = st >> 8;
+  const JsonTables& t = a.t;
+  if (pl == KSG_PL_TAINT_TOLERATION) {
+    if ((int)reason >= a.T) return;
+    const uint32_t id = a.taints[(size_t)reason * a.N + n];
+    if (id == 0 || (int)id > t.n_taint_vocab) return;
+    w.s(t.taint_msgs + t.taint_msg_off[id - 1], t.taint_msg_off[id] - t.taint_msg_off[id - 1]);
+    return;
+  }
+  if (pl == KSG_PL_NODE_RESOURCES_FIT) {   // fitsRequest order: pods, then columns
+    bool first = true;
+    w.c('"');
+    for (int r = -1; r < t.n_res; r++) {
+      if (!((reason >> (r + 1)) & 1u)) continue;
+      if (!first) {
+        w.c(',');
+        w.c(' ');
+      }
+      w.s(t.fit_parts + t.fit_part_off[r + 1], t.fit_part_off[r + 2] - t.fit_part_off[r + 1]);
+      first = false;
+    }
+    w.c('"');
+    return;
+  }
+  if (pl < 0 || pl >= KSG_NPLUGINS || reason >= 8) return;
+  w.s(t.msgs + t.msg_off[pl * 8 + reason], t.msg_off[pl * 8 + reason + 1] - t.msg_off[pl * 8 + reason]);
+}
+
+// filter_body's bytes
+__device__ __forceinline__ void emit_filter(JsonWin& w, const JsonArgs& a, const JsonPod& q, uint32_t st, int n) {
+  const int fail = st == 0 ? -2 : (int)(st & 0xFF) - 1;
+  const int last = st == 0 ? KSG_NPLUGINS : (fail >= 0 && fail < KSG_NPLUGINS ? q.pos[fail] : -1);
+  w.c('{');
+  if (last < 0) {   // rejected by a plugin that did not run (ksg_json_len flagged it)
+    w.c('}');
+    return;
+  }
+  bool first = true;
+  for (int i = 0; i < KSG_NPLUGINS; i++) {
+    const int pl = a.t.by_name[i];
+    if (!((q.fset >> pl) & 1u) || q.pos[pl] > last) continue;
+    if (!first) w.c(',');
+    first = false;
+    w.s(a.t.plugin_keys + a.t.plugin_key_off[pl], a.t.plugin_key_off[pl + 1] - a.t.plugin_key_off[pl]);
+    if (pl == fail) {
+      emit_msg(w, a, st, n);
+    } else {
+      w.s("\"passed\"", 8);
+    }
+  }
+  w.c('}');
+}
+
+// score_body's bytes
+__device__ __forceinline__ void emit_score(JsonWin& w, const JsonArgs& a, const JsonPod& q, int k, int n, bool fin) {
+  const size_t NN = a.N;
+  bool first = true;
+  w.c('{');
+  for (int i = 0; i < KSG_NPLUGINS; i++) {
+    const int pl = a.t.by_name[i];
+    if (!((q.sset >> pl) & 1u)) continue;
+    if (!first) w.c(',');
+    first = false;
+    w.s(a.t.plugin_keys + a.t.plugin_key_off[pl], a.t.plugin_key_off[pl + 1] - a.t.plugin_key_off[pl]);
+    const int row = a.row_of[pl];
+    int64_t raw = 0, v;
+    if (row >= 0) raw = a.raw[((size_t)k * a.n_rows + row) * NN + n];
+    if (!fin) {
+      v = raw;
+    } else {
+      const int64_t f = ((a.normalize_mask >> pl) & 1u) && row >= 0 ? a.norm[((size_t)k * a.n_rows + row) * NN + n] : raw;
+      v = (int64_t)((uint64_t)f * (uint64_t)a.weight[pl]);   // Go int64 multiplication wraps
+    }
+    w.qint(v);
+  }
+  w.c('}');
+}
+
+// Workgroup-exclusive scan of one int64 per lane (kJsonWBlock lanes).
+__device__ __forceinline__ int64_t wblock_exscan(int64_t x, int64_t* s_buf, int64_t& total) {
+  const int tid = threadIdx.x;
+  s_buf[tid] = x;
+  __syncthreads();
+  for (int d = 1; d < kJsonWBlock; d <<= 1) {
+    const int64_t y = tid >= d ? s_buf[tid - d] : 0;
+    __syncthreads();
+    s_buf[tid] += y;
+    __syncthreads();
+  }
+  total = s_buf[kJsonWBlock - 1];
+  const int64_t incl = s_buf[tid];
+  __syncthreads();
+  return incl - x;
+}
+
+// grid: count * S workgroups of kJsonWBlock lanes; workgroup (pod k, segment
+// seg).  A value is '{' + entries joined by ',' + '}': entry g (g > 0) is
+// written with its leading comma, so the value's first and last bytes (seg
+// 0's lane 0) are never touched by another workgroup.
+__global__ __launch_bounds__(kJsonWBlock) void ksg_json_write(JsonArgs a) {
   __shared__ JsonPod s_q;
-  __shared__ int64_t s_buf[kJsonBlock];
+  __shared__ int64_t s_buf[kJsonWBlock];
+  __shared__ char s_win[kJsonWin];
   const int k = blockIdx.x / a.S, seg = blockIdx.x % a.S, tid = threadIdx.x;
   if (tid == 0) s_q = json_pod(a, k);
   __syncthreads();
-  const JsonPod q = s_q;
+  const JsonPod& q = s_q;   // read in LDS: pos[] is indexed by plugin (a private copy would live in scratch)
   const int N = a.N;
-  int k0, k1;
-  lane_range(a, seg, tid, k0, k1);
-  const int64_t* sc = a.scratch + ((size_t)blockIdx.x * kJsonBlock + tid) * 5;
+  const int per_seg = (N + a.S - 1) / a.S;
+  const int s0 = min(N, seg * per_seg), s1 = min(N, s0 + per_seg);
   const int64_t* so = a.segoff + (size_t)blockIdx.x * 6;
-  int64_t tot;
-  const int64_t bf = so[0] + block_exscan(sc[0], s_buf, tot), nbf = so[1] + block_exscan(sc[1], s_buf, tot);
-  const int64_t bs = so[2] + block_exscan(sc[2], s_buf, tot), bt = so[4] + block_exscan(sc[3], s_buf, tot);
-  const int64_t nbs = so[3] + block_exscan(sc[4], s_buf, tot);
-  char* const of = a.out + a.offsets[3 * k + 0];
-  char* const os = a.out + a.offsets[3 * k + 1];
-  char* const ot = a.out + a.offsets[3 * k + 2];
-  // the lane's first byte: after '{', its predecessors' bytes and their commas
-  char* wf = of + 1 + bf + nbf;
-  char* ws = os + 1 + bs + nbs;
-  char* wt = ot + 1 + bt + nbs;
-  int64_t cf = nbf, cs = nbs;
-  uint32_t err = 0;
   const bool scored = q.nf >= 2 && q.sset != 0;
-  for (int j = k0; j < k1; j++) {
-    const int n = a.t.node_order[j];
-    const uint32_t st = a.fstatus[(size_t)k * N + n];
-    if (st == KSG_FS_NOT_EVALUATED) continue;
-    const char* key = a.t.node_keys + a.t.node_key_off[n];
-    const int64_t kl = a.t.node_key_off[n + 1] - a.t.node_key_off[n];
-    if (q.fset) {
-      if (cf > 0) *(wf - 1) = ',';
-      wf = put_bytes(wf, key, kl);
-      wf += filter_body(a, q, st, n, wf, err);
-      wf += 1;   // the next entry's comma slot
-      cf += 1;
-    }
-    if (scored && st == 0) {
-      if (cs > 0) { *(ws - 1) = ','; *(wt - 1) = ','; }
-      ws = put_bytes(ws, key, kl);
-      ws += score_body(a, q, k, n, false, ws);
-      wt = put_bytes(wt, key, kl);
-      wt += score_body(a, q, k, n, true, wt);
-      ws += 1;
-      wt += 1;
-      cs += 1;
+  constexpr int64_t kLow = ((int64_t)1 << 40) - 1;
+  for (int v = 0; v < 3; v++) {
+    if (v == 0 ? !q.fset : !scored) continue;   // "{}" (seg 0's braces below)
+    char* const out = a.out + a.offsets[3 * k + v];
+    int64_t B = so[v == 0 ? 0 : v == 1 ? 2 : 4];   // entry bytes before this round (no commas)
+    int64_t C = so[v == 0 ? 1 : v == 1 ? 3 : 5];   // entries before this round
+    for (int r0 = s0; r0 < s1; r0 += kJsonWBlock) {
+      const int j = r0 + tid;
+      int n = 0;
+      uint32_t st = 0;
+      int64_t u = 0;
+      bool e = false;
+      if (j < s1) {
+        n = a.t.node_order[j];
+        st = a.fstatus[(size_t)k * N + n];
+        e = st != KSG_FS_NOT_EVALUATED && (v == 0 || st == 0);
+        if (e) {
+          uint32_t err = 0;
+          u = (a.t.node_key_off[n + 1] - a.t.node_key_off[n]) +
+              (v == 0 ? filter_body(a, q, st, n, nullptr, err) : score_body(a, q, k, n, v == 2, nullptr));
+        }
+      }
+      int64_t tot;
+      const int64_t x = wblock_exscan(((int64_t)e << 40) | u, s_buf, tot);
+      const int64_t g = C + (x >> 40);
+      const int64_t p = 1 + B + (x & kLow) + g - (g > 0 ? 1 : 0);   // the entry's first byte (its comma)
+      const int64_t len = u + (g > 0 ? 1 : 0);
+      const int64_t Ce = C + (tot >> 40);
+      const int64_t Rlo = 1 + B + C - (C > 0 ? 1 : 0);
+      const int64_t Rhi = 1 + B + (tot & kLow) + Ce - (Ce > 0 ? 1 : 0);
+      for (int64_t lo = Rlo; lo < Rhi; lo += kJsonWin) {
+        const int64_t hi = min(Rhi, lo + (int64_t)kJsonWin);
+        if (e && p < hi && p + len > lo) {
+          JsonWin w{s_win, lo, hi, p};
+          if (g > 0) w.c(',');
+          w.s(a.t.node_keys + a.t.node_key_off[n], a.t.node_key_off[n + 1] - a.t.node_key_off[n]);
+          if (v == 0)
+            emit_filter(w, a, q, st, n);
+          else
+            emit_score(w, a, q, k, n, v == 2);
+        }
+        __syncthreads();
+        for (int64_t i = tid; i < hi - lo; i += kJsonWBlock) out[lo + i] = s_win[i];
+        __syncthreads();
+      }
+      B += tot & kLow;
+      C = Ce;
     }
   }
   if (seg == 0 && tid == 0) {
-    const int64_t lf = a.offsets[3 * k + 1] - a.offsets[3 * k + 0];
-    const int64_t ls = a.offsets[3 * k + 2] - a.offsets[3 * k + 1];
-    const int64_t lt = a.offsets[3 * k + 3] - a.offsets[3 * k + 2];
-    of[0] = '{';
-    of[lf - 1] = '}';
-    os[0] = '{';
-    os[ls - 1] = '}';
-    ot[0] = '{';
-    ot[lt - 1] = '}';
+    for (int v = 0; v < 3; v++) {
+      char* const o = a.out + a.offsets[3 * k + v];
+      const int64_t l = a.offsets[3 * k + v + 1] - a.offsets[3 * k + v];
+      o[0] = '{';
+      o[l - 1] = '}';
+    }
   }
-  if (err) atomicOr(a.err, err);
 }
 
 }  // namespace ksk

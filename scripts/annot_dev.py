@@ -1,5 +1,5 @@
 """Device serialiser alone: per-chunk time of the async launch and the wait
-(python scripts/annot_dev.py [pods] [chunk])."""
+(python scripts/annot_dev.py [pods] [chunk] [c1|c3])."""
 import importlib
 import os
 import sys
@@ -14,7 +14,9 @@ E = importlib.import_module(PKG + ".encoder")
 B = importlib.import_module(PKG + ".bulk")
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
 chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-nodes, pods, prof = G.config2(n_nodes=5000, n_pods=50000)
+cfg = sys.argv[3] if len(sys.argv) > 3 else "c1"
+nodes, pods, prof = (G.config3(n_nodes=15000, n_pods=max(n, 1024)) if cfg == "c3"
+                     else G.config2(n_nodes=5000, n_pods=50000))
 enc = E.Encoder(nodes, pods, prof)
 eng = native.Engine(device=0)
 eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
@@ -48,3 +50,6 @@ eng.set_timing(True)
 t = time.perf_counter()
 eng.run_queue(0, chunk, capture=native.CaptureBuffers(len(nodes), chunk))
 print("capture run (host copies)", round((time.perf_counter() - t) * 1e3, 1), "ms; kernels", eng.kernel_stats())
+if os.environ.get("KSG_DUMP_MAPS"):   # diagnosis of exit-time faults: which library sits where
+    with open("/proc/self/maps") as f, open(os.environ["KSG_DUMP_MAPS"], "w") as o:
+        o.write(f.read())
