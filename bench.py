@@ -39,9 +39,13 @@ Prints ONE JSON line (rank 0).  The line also carries:
   prefix of the headline queue, at 16 threads (upstream parallelism) and at
   every host core this process may use, with the CPU model and the limit
   that capped the core count;
-* `annotations` (N = 1): the simulator's product for the first 2,000 pods of
-  configs[1]: captured batched run + filter-result / score-result /
-  finalscore-result bytes (bulk.annotate_queue);
+* `annotations` / `annotations_configs2` (N = 1): the simulator's product,
+  the filter-result / score-result / finalscore-result bytes of the first
+  2,000 pods of configs[1] (256 of configs[2]): the device serialiser
+  (bulk.annotate_queue_device, values built in HBM and copied to pinned host
+  memory) with its digest checked against the host serialiser
+  (bulk.annotate_queue, captured rows + ksg_annotate on 16 threads), plus the
+  device serialiser's steady state over a longer queue;
 * `per_cycle` / `per_cycle_configs2` (N = 1): the drop-in's per-cycle C-ABI
   path, call by call from C.
 """
@@ -151,9 +155,12 @@ def pmc_traffic(kernel, name):
     for rnd in ("r5", "r4", "r3", "r2"):   # the newest round's passes first
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
-            row = json.load(open(path)).get(kernel) if kernel else None
+            tab = json.load(open(path))
         except (OSError, ValueError):
             continue
+        # the summaries key kernels by their demangled name (ksk::ksg_...),
+        # the library's timing table by the bare name
+        row = (tab.get(kernel) or tab.get("ksk::" + kernel)) if kernel else None
         if row and row.get("hbm_bytes_per_dispatch") is not None:
             return row["hbm_bytes_per_dispatch"], f"profiles/{rnd}/{name}"
     return None, None
@@ -308,14 +315,20 @@ def annotation_sidecar(eng, enc, prof, native, B, n_pods: int, chunk: int, threa
     eng.set_timing(False)
     h = xxhash.xxh3_64()
     h.update(digests.tobytes())
-    return {"workload": f"{label} cluster, first {n_pods} pods, {chunk}-pod chunks, device capture "
-                        f"+ ksg_annotate on {threads} threads",
-            "pods_per_s": n_pods / wall, "wall_s": wall, "annotation_bytes": int(sizes.sum()),
-            "annotation_MB_per_s": sizes.sum() / wall / 1e6,
+    host = {"path": f"device capture + ksg_annotate on {threads} threads (bulk.annotate_queue)",
+            "pods_per_s": n_pods / wall, "wall_s": wall, "annotation_MB_per_s": sizes.sum() / wall / 1e6,
+            "pods_per_s_light_sink": n_pods / wall_light, "threads": threads}
+    ok = isinstance(dev, dict) and "pods_per_s" in dev and dev.get("bytes_equal_host")
+    return {"workload": f"{label} cluster, first {n_pods} pods, {chunk}-pod chunks",
+            "path": ("device serialiser (bulk.annotate_queue_device): values built in HBM, copied to pinned "
+                     "host memory" if ok else "host serialiser (bulk.annotate_queue)"),
+            "pods_per_s": dev["pods_per_s"] if ok else n_pods / wall,
+            "annotation_bytes": int(sizes.sum()),
+            "annotation_MB_per_s": (dev["annotation_MB_per_s"] if ok else sizes.sum() / wall / 1e6),
             "capture_only_pods_per_s": n_pods / cap_wall, "capture_device_ms": dev_ms,
             "capture_kernels_ms": {k: round(v, 3) for k, v in ks.items()},
-            "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(), "threads": threads,
-            "pods_per_s_light_sink": n_pods / wall_light, "device_serialiser": dev}
+            "scheduled": int((pl >= 0).sum()), "digest_xxh3": h.hexdigest(),
+            "device_serialiser": dev, "host_serialiser": host}
 
 
 def device_serialiser_long(eng, enc, prof, B, n_pods: int, chunk: int, threads: int):

@@ -122,6 +122,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-placements", default=None, help="write the last run's placements (.npy)")
+    ap.add_argument("--pmc", default=None,
+                    help="committed PMC summary (profiles/rNN/<name>) whose HBM bytes per dispatch of the "
+                         "dominant kernel fill roofline.traffic")
     args = ap.parse_args()
 
     t0 = time.time()
@@ -178,6 +181,19 @@ def main():
         ks = eng.kernel_stats()
         eng.set_timing(False)
         roof = metrics.dominant_kernel_roofline(ks, per_eval)
+        if roof and args.pmc:
+            try:
+                tab = json.load(open(os.path.join(ROOT, args.pmc)))
+                row = tab.get(roof["kernel"]) or tab.get("ksk::" + roof["kernel"])
+            except (OSError, ValueError):
+                row = None
+            if row and row.get("hbm_bytes_per_dispatch") is not None:
+                roof["traffic"] = row["hbm_bytes_per_dispatch"]
+                roof["traffic_source"] = args.pmc
+                ms = roof["traffic"] / (roof["avg_launch_ms"] * 1e-3) / 1e9
+                roof["memory_side_GBps"] = ms
+                roof["memory_side_frac_of_hbm"] = ms / roof["peak"]
+                roof["traffic_over_algorithmic"] = roof["traffic"] / roof["bytes_per_launch"]
     evals = R * P * len(nodes)
     out = {
         "config": args.config, "workload": workload, "replicas": R, "nodes": len(nodes), "pods": P,
