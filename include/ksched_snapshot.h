@@ -155,18 +155,71 @@ typedef struct ksg_node_view {
 
 /* One spec.volumes[] entry (v1.Volume): kind = the JSON key of the
  * VolumeSource field that is set ("persistentVolumeClaim", "emptyDir",
- * "configMap", ...), claim_name = persistentVolumeClaim.claimName.  A pod with
- * a claim, a generic ephemeral volume or an in-tree disk volume
+ * "configMap", ...), claim_name = persistentVolumeClaim.claimName.  A claim
+ * makes VolumeBinding / NodeVolumeLimits / VolumeRestrictions / VolumeZone
+ * PreFilter run: the claim is resolved against the PersistentVolumeClaims,
+ * PersistentVolumes and StorageClasses added with ksg_snapshot_add_pvc /
+ * _add_pv / _add_storage_class (their listers), the PreFilter outcomes are
+ * decided at encode, the per-node Filter predicates go to the device as the
+ * pod's volume program.  A generic ephemeral volume or an in-tree disk volume
  * (gcePersistentDisk, awsElasticBlockStore, azureDisk, azureFile, cinder,
- * vsphereVolume, portworxVolume, rbd, iscsi) makes VolumeBinding /
- * NodeVolumeLimits / VolumeRestrictions / VolumeZone PreFilter run: while one
- * of those plugins is enabled, ksg_snapshot_add_pod refuses it
- * (KSG_E_UNSUPPORTED); every other source is their Skip, as upstream. */
+ * vsphereVolume, portworxVolume, rbd, iscsi) is refused (KSG_E_UNSUPPORTED)
+ * while a volume plugin is enabled; every other source is their Skip, as
+ * upstream. */
 typedef struct ksg_volume_view {
   const char* name;
   const char* kind;
   const char* claim_name;
 } ksg_volume_view;
+
+/* v1.PersistentVolume as VolumeBinding / VolumeZone read it
+ * (simulator/snapshot/snapshot.go:34 pvs). */
+typedef struct ksg_pv_view {
+  const char* name;
+  int32_t n_labels;
+  const ksg_str_pair* labels;                /* metadata.labels (VolumeZone) */
+  const char* storage_class;                 /* storagehelpers.GetPersistentVolumeClass: the beta
+                                                annotation, else spec.storageClassName ("" none) */
+  const char* claim_namespace;               /* spec.claimRef (claim_name NULL = no claimRef) */
+  const char* claim_name;
+  const char* source;                        /* the JSON key of the PersistentVolumeSource set ("csi", ...) */
+  int32_t has_node_affinity;                 /* spec.nodeAffinity.required != nil */
+  int32_t n_terms;
+  const ksg_node_selector_term_view* terms;  /* its nodeSelectorTerms */
+} ksg_pv_view;
+
+/* v1.PersistentVolumeClaim (snapshot.go:35 pvcs). */
+typedef struct ksg_pvc_view {
+  const char* namespace_;
+  const char* name;
+  const char* volume_name;                   /* spec.volumeName ("" unbound) */
+  const char* storage_class;                 /* GetPersistentVolumeClaimClass: the beta annotation,
+                                                else spec.storageClassName ("" none) */
+  int32_t n_access_modes;
+  const char* const* access_modes;           /* spec.accessModes */
+  int32_t n_annotations;
+  const ksg_str_pair* annotations;           /* bind-completed, selected-node */
+  int32_t deleting;                          /* metadata.deletionTimestamp != nil */
+} ksg_pvc_view;
+
+/* storagev1.StorageClass (snapshot.go:36 storageClasses), after API
+ * defaulting (volumeBindingMode "" = Immediate). */
+typedef struct ksg_topology_requirement_view {
+  const char* key;
+  int32_t n_values;
+  const char* const* values;
+} ksg_topology_requirement_view;
+typedef struct ksg_topology_term_view {
+  int32_t n_requirements;
+  const ksg_topology_requirement_view* requirements;   /* matchLabelExpressions */
+} ksg_topology_term_view;
+typedef struct ksg_storage_class_view {
+  const char* name;
+  const char* provisioner;
+  const char* binding_mode;                  /* "Immediate" / "WaitForFirstConsumer" */
+  int32_t n_allowed_topologies;
+  const ksg_topology_term_view* allowed_topologies;
+} ksg_storage_class_view;
 
 typedef struct ksg_pod_view {
   const char* namespace_;
@@ -320,6 +373,14 @@ int ksg_snapshot_add_pod(ksg_snapshot* s, const ksg_pod_view* pod, int32_t* inde
  * pod's terms (the next sync re-encodes when any changed).  Replaces the
  * reference's namespace informer feed (snapshot.go namespaces). */
 int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labels, const ksg_str_pair* labels);
+/* The volume plugins' listers (snapshot.go:34-36): a PersistentVolume,
+ * PersistentVolumeClaim or StorageClass added or replaced (same name) is read
+ * by the next encode, which is a full one (every pod's claims resolve again).
+ * A node publishing CSI attach limits (allocatable attachable-volumes-csi-*)
+ * with NodeVolumeLimits enabled and a pod with claims is refused at encode. */
+int ksg_snapshot_add_pv(ksg_snapshot* s, const ksg_pv_view* pv);
+int ksg_snapshot_add_pvc(ksg_snapshot* s, const ksg_pvc_view* pvc);
+int ksg_snapshot_add_storage_class(ksg_snapshot* s, const ksg_storage_class_view* sc);
 /* A pod the caller will add later (a pending pod of the scheduling queue, as
  * the pod informer delivers it: upstream eventhandlers.go addPodToSchedulingQueue
  * feeding the simulator's scheduler).  Its selectors, term templates, label
@@ -380,11 +441,24 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
                           int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len);
 /* PreFilter of plugin `plugin` for `pod` (given the device result's status
  * bits): *code = KSG_CODE_SUCCESS / SKIP / UNSCHEDULABLE_AND_UNRESOLVABLE
- * (NodeAffinity "pod affinity terms conflict"); NodeAffinity's
- * PreFilterResult node names (sorted) go to names[0..*n_names) when
- * *has_result = 1 (names may be NULL to query the count). */
+ * (NodeAffinity "pod affinity terms conflict", a volume plugin's claim /
+ * volume lookup: ksg_snapshot_prefilter_message); the PreFilterResult node
+ * names (sorted) of NodeAffinity or VolumeBinding go to names[0..*n_names)
+ * when *has_result = 1 (names may be NULL to query the count).  The plugins
+ * after a rejecting one in the profile's PreFilter order are not run by the
+ * framework; an empty intersection of the results is the framework's own
+ * rejection (every node is then left unevaluated on the device). */
 int ksg_snapshot_prefilter(ksg_snapshot* s, int32_t pod, int32_t plugin, uint32_t result_status, int32_t* code,
                            int32_t* has_result, const char** names, int32_t cap, int32_t* n_names);
+/* The PreFilter rejection message of `plugin` for `pod` (the status
+ * ksg_snapshot_prefilter returned as KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE:
+ * NodeAffinity "pod affinity terms conflict", VolumeRestrictions / VolumeBinding
+ * / VolumeZone claim and volume lookups), NUL-terminated, truncated to cap - 1
+ * bytes; *len = full length, 0 when the plugin did not reject.  VolumeBinding's
+ * PreFilterResult (the nodes of the pod's bound local volumes) comes through
+ * ksg_snapshot_prefilter like NodeAffinity's. */
+int ksg_snapshot_prefilter_message(ksg_snapshot* s, int32_t pod, int32_t plugin, char* msg, int32_t cap,
+                                   int32_t* len);
 
 /* Decode tables of the current encoding (for ksg_annotator_new): node names,
  * resource column names, taint strings "{key: value}". */

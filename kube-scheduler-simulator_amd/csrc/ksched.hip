@@ -138,6 +138,13 @@ struct ksg_ctx {
   bool coop_dirty = true;
   bool topo_eval_coop = false;        // the one-pod evaluation launches cooperatively (after a plain launch's
                                       // workgroups were not all resident)
+  // Queue runs of the chip-wide topology path and the multi-workgroup replica
+  // sweep: a plain launch of G workgroups within the occupancy API's
+  // residency (checked before the launch), their barriers bounded by a
+  // timeout.  env KSG_COOP_LAUNCH=1, or a barrier timeout, switches to
+  // hipLaunchCooperativeKernel (a process that made cooperative launches
+  // faulted in libamdhip64's exit-time teardown under rocprofv3).
+  bool coop_launch = false;
   int32_t* d_tables = nullptr;        // the maintained domain tables and their index (ksched_topo_tables.h)
   size_t tables_words = 0;
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
@@ -1120,12 +1127,14 @@ bool sweep_eligible(ksg_ctx* ctx, const ksg_profile* profiles, int R, int first,
 // mode: 0 generic arithmetic, 1 fast (Fit/BA over {cpu, memory}), 2 fast with
 // one scalar Fit column (instantiated for the spill-free shapes only);
 // narrow: the 16-byte records (fast modes only)
-// MULTI (group barriers): a cooperative launch, so the runtime guarantees the
-// co-residency of every workgroup (or refuses the launch)
+// MULTI (group barriers): every workgroup must be co-resident; the grid is
+// within the occupancy API's residency (run_sweep halves S until it is) and
+// the barriers are bounded by a timeout.  A cooperative launch (coop: env
+// KSG_COOP_LAUNCH=1, or after a timeout) has the runtime guarantee it.
 template <int BLOCK, bool MULTI>
 hipError_t launch_one(const void* f, const SweepArgs& s, int grid, hipStream_t st) {
   void* kargs[] = {const_cast<SweepArgs*>(&s)};
-  if (MULTI) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(BLOCK), kargs, 0, st);
+  if (MULTI && s.coop) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(BLOCK), kargs, 0, st);
   return hipLaunchKernel(f, dim3(grid), dim3(BLOCK), kargs, 0, st);
 }
 template <int BLOCK, int KN, bool MULTI>
@@ -1266,6 +1275,7 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
   s.nrcp = nrcp;   // DevCluster::rcp64 on the narrow path
   s.nmut = nmut;
   s.nx = nx;
+  s.coop = ctx->coop_launch ? 1 : 0;
   TA(tmp, &s.srec, sizeof(uint64_t) * (size_t)kBatch * N);
   // Workgroups per replica: with few replicas of a large cluster, S > 1 spreads
   // each replica over S co-resident workgroups (two group barriers per pod);
@@ -1704,10 +1714,11 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     a.count = nb;
     a.out0 = off;
     a.gen = ++ctx->coop_gen;
-    // cooperative launch: the runtime guarantees the G workgroups are
-    // co-resident (or refuses the launch), which the grid barrier needs
+    // the grid barrier needs the G workgroups co-resident: G is within the
+    // occupancy API's residency; a cooperative launch (ctx->coop_launch, or
+    // the one-pod evaluation after a timeout) has the runtime guarantee it
     void* kargs[] = {&a};
-    if (one && !ctx->topo_eval_coop)
+    if (one ? !ctx->topo_eval_coop : !ctx->coop_launch)
       HIPC(ctx, hipLaunchKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));
     else
       HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(256), kargs, 0, ctx->stream));
@@ -2019,6 +2030,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     HIPC(ctx, hipMemcpy(flags, ctx->d_coop_flags, sizeof(flags), hipMemcpyDeviceToHost));
     if (flags[4]) {
       ctx->coop_dirty = true;
+      ctx->coop_launch = true;   // not every workgroup was resident: cooperative launches from now on
       return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
     }
   }
@@ -2906,6 +2918,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_PIPE_OVERLAP")) ctx->pipe_overlap = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
+  if (const char* f = getenv("KSG_COOP_LAUNCH")) ctx->coop_launch = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SERVER")) ctx->srv_mode = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_ES")) ctx->cycle_es = atoi(f);
@@ -3544,7 +3557,10 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     unsigned to = 0;
     HIPC(ctx, hipMemcpy(&to, ctx->sweep_timeout, sizeof(to), hipMemcpyDeviceToHost));
     ctx->sweep_timeout = nullptr;
-    if (to) return fail(ctx, KSG_E_DEVICE, "replica sweep: group barrier timed out");
+    if (to) {
+      ctx->coop_launch = true;   // not every workgroup was resident: cooperative launches from now on
+      return fail(ctx, KSG_E_DEVICE, "replica sweep: group barrier timed out");
+    }
   }
   if (summaries) {
     for (size_t r = 0; r < RR; r++) {

@@ -208,6 +208,40 @@ struct Node {
   bool unsched;
   std::vector<Image> images;
 };
+// The volume plugins' objects [upstream v1.32 volumebinding / volumezone /
+// volumerestrictions listers; model.py PersistentVolume / Claim / StorageClass]
+struct PV {
+  std::string name;
+  StrMap labels;
+  std::string storage_class;
+  bool has_claim_ref = false;
+  std::string claim_ns, claim_name;
+  std::string source;
+  bool has_na = false;
+  std::vector<Term> na;
+};
+struct PVC {
+  std::string ns, name, volume_name, storage_class;
+  std::vector<std::string> modes;
+  StrMap ann;
+  bool deleting = false;
+  // volumeBinder.isPVCFullyBound: a volume name and bind-completed
+  bool fully_bound() const { return !volume_name.empty() && ann.count("pv.kubernetes.io/bind-completed"); }
+};
+struct SClass {
+  std::string name, provisioner, mode;
+  std::vector<std::vector<std::pair<std::string, std::vector<std::string>>>> topo;   // allowedTopologies
+};
+const char* const kZoneLabels[4] = {"failure-domain.beta.kubernetes.io/zone", "failure-domain.beta.kubernetes.io/region",
+                                    "topology.kubernetes.io/zone", "topology.kubernetes.io/region"};
+std::string ga_label(const std::string& k) {   // volumezone translateToGALabel
+  if (k == kZoneLabels[0]) return kZoneLabels[2];
+  if (k == kZoneLabels[1]) return kZoneLabels[3];
+  return k;
+}
+const std::string kWFFC = "WaitForFirstConsumer";
+constexpr int32_t kVolRwopConflict = 1;   // VolumeRestrictions rejects every node (encoder.py VOL_RWOP_CONFLICT)
+
 struct Pod {
   std::string ns, name, node_name;
   StrMap labels;
@@ -224,6 +258,7 @@ struct Pod {
   Sel default_sel;
   bool terminating;
   int32_t priority;
+  std::vector<std::string> claims;   // spec.volumes[].persistentVolumeClaim.claimName, in volume order
 };
 
 std::vector<Req> copy_reqs(int32_t n, const ksg_requirement_view* v) {
@@ -451,7 +486,12 @@ struct Encoded {
   std::vector<double> log_table;
   std::vector<ksg_pod> pods;
   std::vector<int32_t> prog;            // program pool (the views hand out {0} when empty)
-  std::map<int, std::vector<std::string>> prefilter_names;
+  // PreFilter outcomes per pod (profile order, encode_pod): the
+  // PreFilterResult node names per plugin (NodeAffinity, VolumeBinding) and
+  // the rejecting plugin with its message ("" = the framework's own rejection
+  // of an empty intersection)
+  std::map<int, std::map<int, std::vector<std::string>>> prefilter_names;
+  std::map<int, std::pair<int, std::string>> prefilter_reject;
   std::vector<std::string> taint_strings;
   ksg_profile prof{};
   int N = 0;
@@ -513,6 +553,14 @@ struct ksg_snapshot {
   // terms resolve against these
   bool have_namespaces = false;
   std::map<std::string, StrMap> namespaces;
+  // the volume plugins' listers (ksg_snapshot_add_pv / _add_pvc / _add_storage_class)
+  std::map<std::string, PV> pvs;
+  std::map<std::pair<std::string, std::string>, PVC> pvcs;
+  std::map<std::string, SClass> classes;
+  std::map<std::pair<std::string, std::string>, std::set<int>> claim_users;   // full encode: (ns, claim) -> pods
+  std::set<int> bound_set;          // full encode: pods with a binding (running or assumed)
+  bool vol_run = false;             // a volume plugin runs at PreFilter or Filter
+  bool csi_limits = false;          // NodeVolumeLimits runs and a node publishes CSI attach limits
   // ksg_snapshot_statuses: a status key's (code, message) is kept across
   // pods until the next full encode (status_epoch); per call, stamp/local
   // number the keys a pod meets in first-seen order
@@ -669,6 +717,31 @@ void build_resources(ksg_snapshot* s) {
   for (size_t i = 0; i < e.res_names.size(); i++) e.res_col[e.res_names[i]] = (int)i;
 }
 
+// Node label keys a pod's volume program reads (encoder.py
+// _volume_label_keys): the zone labels, its bound PVs' node-affinity keys,
+// its classes' allowedTopologies keys.
+void volume_label_keys(const ksg_snapshot* s, const Pod& p, std::set<std::string>& keys) {
+  if (p.claims.empty()) return;
+  for (const char* k : kZoneLabels) keys.insert(k);
+  for (auto& c : p.claims) {
+    auto it = s->pvcs.find({p.ns, c});
+    if (it == s->pvcs.end()) continue;
+    const PVC& pvc = it->second;
+    if (!pvc.volume_name.empty()) {
+      auto pt = s->pvs.find(pvc.volume_name);
+      if (pt != s->pvs.end() && pt->second.has_na)
+        for (auto& t : pt->second.na)
+          for (auto& r : t.expr) keys.insert(r.key);
+    }
+    if (!pvc.storage_class.empty()) {
+      auto ct = s->classes.find(pvc.storage_class);
+      if (ct != s->classes.end())
+        for (auto& term : ct->second.topo)
+          for (auto& kv : term) keys.insert(kv.first);
+    }
+  }
+}
+
 void build_label_columns(ksg_snapshot* s) {
   Encoded& e = s->e;
   std::set<std::string> keys;
@@ -691,6 +764,7 @@ void build_label_columns(ksg_snapshot* s) {
     for (auto& c : pts.second) keys.insert(c.key);
     for (auto* v : {&p.aff_req, &p.anti_req, &p.aff_pref, &p.anti_pref})
       for (auto& t : *v) keys.insert(t.key);
+    volume_label_keys(s, p, keys);
   };
   for (auto& p : s->pods) {
     s->pts_cache.push_back(pts_constraints(p, s->prof));
@@ -1016,6 +1090,9 @@ void prepare_frozen(ksg_snapshot* s, int i, Pass& ps) {
   };
   for (auto& hp : pod_host_ports(p))
     if (!e.port_id.count(hp)) ps.miss = true;
+  // a pod with claims reads the other pods' claims and the storage objects
+  // (shared ReadWriteOncePod / unbound claims): always a full encode
+  if (!p.claims.empty()) ps.miss = true;
   for (auto& t : p.anti_req) own(TMPL_REQ_ANTI, t, 1);
   for (auto& t : p.aff_req) own(TMPL_REQ_AFF, t, 1);
   for (auto& t : p.aff_pref) own(TMPL_PREF, t, t.weight);
@@ -1039,6 +1116,309 @@ void prepare_frozen(ksg_snapshot* s, int i, Pass& ps) {
 }
 
 // ---- per-pod programs --------------------------------------------------------------
+// ---- volume plugins ------------------------------------------------------------
+// A PreFilter outcome: 1 = rejection (message), 2 = PreFilterResult (names).
+struct PreOutcome {
+  int kind = 0;
+  std::string msg;
+  std::set<std::string> names;
+};
+
+std::set<std::string> set_and(const std::set<std::string>& a, const std::set<std::string>& b) {
+  std::set<std::string> out;
+  std::set_intersection(a.begin(), a.end(), b.begin(), b.end(), std::inserter(out, out.begin()));
+  return out;
+}
+
+// volumehelpers.LabelZonesToSet: "__"-separated, no blank member
+std::vector<std::string> label_zones(const PV& pv, const std::string& value) {
+  std::set<std::string> zones;
+  size_t at = 0;
+  for (;;) {
+    const size_t k = value.find("__", at);
+    std::string z = value.substr(at, k == std::string::npos ? std::string::npos : k - at);
+    const size_t b = z.find_first_not_of(" \t\n\r\f\v"), e = z.find_last_not_of(" \t\n\r\f\v");
+    z = b == std::string::npos ? std::string() : z.substr(b, e - b + 1);
+    if (z.empty())
+      throw EncodeError{KSG_E_UNSUPPORTED, "PersistentVolume " + pv.name + ": zone label '" + value +
+                                               "' has an empty member"};
+    zones.insert(z);
+    if (k == std::string::npos) break;
+    at = k + 2;
+  }
+  return std::vector<std::string>(zones.begin(), zones.end());
+}
+
+// encoder.py Encoder._volume_plan [upstream v1.32 volumerestrictions,
+// nodevolumelimits/csi.go, volumebinding, volumezone; not vendored: parity
+// unpinned, DESIGN.md §9]: the four plugins' PreFilter Skip bits, their
+// PreFilter outcomes (into `out`) and the pod's volume program (`words`, the
+// grammar of _volume_plan's docstring), value ids taken in the same order.
+uint32_t volume_plan(ksg_snapshot* s, int i, const Pod& p, Pass& ps, std::map<int, PreOutcome>& out,
+                     std::vector<int32_t>& words, bool& has_words) {
+  const uint32_t all_skip = (1u << KSG_PL_VOLUME_RESTRICTIONS) | (1u << KSG_PL_NODE_VOLUME_LIMITS) |
+                            (1u << KSG_PL_VOLUME_BINDING) | (1u << KSG_PL_VOLUME_ZONE);
+  has_words = false;
+  if (p.claims.empty()) return all_skip;
+  if (s->csi_limits)
+    throw EncodeError{KSG_E_UNSUPPORTED, "pod " + p.ns + "/" + p.name +
+                                             ": a node publishes CSI attach limits (NodeVolumeLimits) and the pod "
+                                             "has claims"};
+  const std::string& ns = p.ns;
+  const std::string who = "pod " + ns + "/" + p.name;
+  auto claim = [&](const std::string& c) -> const PVC* {
+    auto it = s->pvcs.find({ns, c});
+    return it == s->pvcs.end() ? nullptr : &it->second;
+  };
+  auto is_bound = [&](int k) { return s->bound_set.count(k) != 0; };
+  auto others_of = [&](const std::string& c) {
+    std::set<int> o;
+    auto it = s->claim_users.find({ns, c});
+    if (it != s->claim_users.end()) o = it->second;
+    o.erase(i);
+    return o;
+  };
+  uint32_t skip = 0;
+  const std::string* missing = nullptr;
+  for (auto& c : p.claims)
+    if (!claim(c)) {
+      missing = &c;
+      break;
+    }
+  const std::string nf = missing ? "persistentvolumeclaim \"" + *missing + "\" not found" : std::string();
+  int32_t flags = 0;
+  // VolumeRestrictions: readWriteOncePodPVCsForPod
+  if (missing) {
+    out[KSG_PL_VOLUME_RESTRICTIONS] = PreOutcome{1, nf, {}};
+  } else {
+    for (auto& c : p.claims) {
+      const PVC* pvc = claim(c);
+      if (std::find(pvc->modes.begin(), pvc->modes.end(), "ReadWriteOncePod") == pvc->modes.end()) continue;
+      const std::set<int> others = others_of(c);
+      if (!is_bound(i))
+        for (int u : others)
+          if (!is_bound(u))
+            throw EncodeError{KSG_E_UNSUPPORTED, who + ": ReadWriteOncePod claim '" + c +
+                                                     "' is shared with another queued pod (whose placement decides "
+                                                     "the conflict)"};
+      if (!others.empty()) flags |= kVolRwopConflict;   // StorageInfos.IsPVCUsedByPods
+    }
+  }
+  // VolumeBinding: podHasPVCs, GetPodVolumeClaims, GetEligibleNodes
+  std::vector<const PVC*> bound;
+  std::vector<std::pair<const PVC*, const SClass*>> prov;
+  bool vb_set = false;
+  PreOutcome vb;
+  for (auto& c : p.claims) {
+    const PVC* pvc = claim(c);
+    if (!pvc) {
+      vb = PreOutcome{1, nf, {}};
+      vb_set = true;
+      break;
+    }
+    if (pvc->deleting) {
+      vb = PreOutcome{1, "persistentvolumeclaim \"" + c + "\" is being deleted", {}};
+      vb_set = true;
+      break;
+    }
+  }
+  if (!vb_set) {
+    bool immediate = false;
+    for (auto& c : p.claims) {
+      const PVC* pvc = claim(c);
+      if (pvc->fully_bound()) {
+        bound.push_back(pvc);
+        continue;
+      }
+      auto ct = pvc->storage_class.empty() ? s->classes.end() : s->classes.find(pvc->storage_class);
+      if (ct != s->classes.end() && ct->second.mode == kWFFC && pvc->volume_name.empty())
+        prov.emplace_back(pvc, &ct->second);
+      else
+        immediate = true;
+    }
+    if (immediate) {
+      vb = PreOutcome{1, "pod has unbound immediate PersistentVolumeClaims", {}};
+      vb_set = true;
+    }
+  }
+  if (!vb_set) {
+    std::optional<std::set<std::string>> eligible;
+    for (const PVC* pvc : bound) {   // util.GetLocalPersistentVolumeNodeNames of every bound PV
+      auto pt = s->pvs.find(pvc->volume_name);
+      if (pt == s->pvs.end()) {
+        eligible.reset();
+        break;
+      }
+      std::set<std::string> names;
+      if (pt->second.has_na)
+        for (auto& t : pt->second.na) {
+          std::optional<std::set<std::string>> tn;
+          for (auto& r : t.expr)
+            if (r.key == kHostname && r.op == "In") {
+              std::set<std::string> sv(r.values.begin(), r.values.end());
+              tn = tn ? set_and(*tn, sv) : sv;
+            }
+          if (tn) names.insert(tn->begin(), tn->end());
+        }
+      if (!names.empty()) eligible = eligible ? set_and(*eligible, names) : names;
+    }
+    if (eligible) {
+      vb = PreOutcome{2, "", *eligible};
+      vb_set = true;
+    }
+    for (auto& pr : prov) {
+      for (auto& kv : s->pvs) {
+        const PV& pv = kv.second;
+        if (pv.storage_class == pr.first->storage_class &&
+            (!pv.has_claim_ref || (pv.claim_ns == ns && pv.claim_name == pr.first->name)))
+          throw EncodeError{KSG_E_UNSUPPORTED, who + ": claim '" + pr.first->name +
+                                                   "' could bind statically to PersistentVolume '" + pv.name +
+                                                   "' (findMatchingVolumes is not modelled)"};
+      }
+      if (!is_bound(i) && !others_of(pr.first->name).empty())
+        throw EncodeError{KSG_E_UNSUPPORTED, who + ": unbound claim '" + pr.first->name +
+                                                 "' is shared with another pod (its assumed binding is not modelled)"};
+    }
+  }
+  if (vb_set) out[KSG_PL_VOLUME_BINDING] = vb;
+  // VolumeZone: getPVbyPod
+  std::vector<std::pair<std::string, std::vector<std::string>>> zone;
+  bool vz_set = false;
+  std::string vz;
+  for (auto& c : p.claims) {
+    if (c.empty()) {
+      vz = "PersistentVolumeClaim had no name";
+      vz_set = true;
+      break;
+    }
+    const PVC* pvc = claim(c);
+    if (!pvc) {
+      vz = "persistentvolumeclaim \"" + c + "\" not found";
+      vz_set = true;
+      break;
+    }
+    if (pvc->volume_name.empty()) {
+      const std::string& sc = pvc->storage_class;
+      if (sc.empty()) {
+        vz = "PersistentVolumeClaim had no pv name and storageClass name";
+        vz_set = true;
+        break;
+      }
+      auto ct = s->classes.find(sc);
+      if (ct == s->classes.end()) {
+        vz = "storageclass.storage.k8s.io \"" + sc + "\" not found";
+        vz_set = true;
+        break;
+      }
+      if (ct->second.mode == kWFFC) continue;
+      vz = "PersistentVolume had no name";
+      vz_set = true;
+      break;
+    }
+    auto pt = s->pvs.find(pvc->volume_name);
+    if (pt == s->pvs.end()) {
+      vz = "persistentvolume \"" + pvc->volume_name + "\" not found";
+      vz_set = true;
+      break;
+    }
+    for (const char* key : kZoneLabels) {
+      auto lt = pt->second.labels.find(key);
+      if (lt != pt->second.labels.end()) zone.emplace_back(key, label_zones(pt->second, lt->second));
+    }
+  }
+  if (vz_set)
+    out[KSG_PL_VOLUME_ZONE] = PreOutcome{1, vz, {}};
+  else if (zone.empty())
+    skip |= 1u << KSG_PL_VOLUME_ZONE;
+  // the Filter program
+  words = {flags, (int32_t)bound.size()};
+  static const char* const kMigrated[] = {"gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "azureFile",
+                                          "cinder", "vsphereVolume", "portworxVolume"};
+  for (const PVC* pvc : bound) {
+    auto pt = s->pvs.find(pvc->volume_name);
+    if (pt == s->pvs.end()) {
+      words.push_back(0);
+      continue;
+    }
+    const PV& pv = pt->second;
+    for (const char* m : kMigrated)
+      if (pv.source == m)
+        throw EncodeError{KSG_E_UNSUPPORTED, "PersistentVolume " + pv.name + ": " + pv.source +
+                                                 " (CSI translation not modelled)"};
+    if (!pv.has_na) {
+      words.insert(words.end(), {1, -1});
+      continue;
+    }
+    std::vector<std::vector<int32_t>> terms;
+    bool nameless = false;   // a fields-only term: CheckNodeAffinity's nameless node matches it
+    for (auto& t : pv.na) {
+      if (t.expr.empty()) {
+        if (!t.fields.empty()) {
+          nameless = true;
+          break;
+        }
+        terms.push_back({0});   // an empty term matches nothing
+        continue;
+      }
+      std::vector<int32_t> tw = {(int32_t)t.expr.size()};
+      for (auto& r : t.expr) ps.emit(tw, ps.requirement(r, false));
+      terms.push_back(std::move(tw));
+    }
+    if (nameless) {
+      words.insert(words.end(), {1, -1});
+    } else {
+      words.insert(words.end(), {1, (int32_t)terms.size()});
+      for (auto& tw : terms) ps.emit(words, tw);
+    }
+  }
+  words.push_back((int32_t)prov.size());
+  for (auto& pr : prov) {
+    auto at = pr.first->ann.find("volume.kubernetes.io/selected-node");
+    int32_t sel = -1;
+    if (at != pr.first->ann.end()) {
+      auto nt = s->node_index.find(at->second);
+      sel = nt == s->node_index.end() ? -2 : nt->second;
+    }
+    const SClass& cls = *pr.second;
+    if (cls.provisioner.empty() || cls.provisioner == "kubernetes.io/no-provisioner") {
+      words.insert(words.end(), {sel, -1});
+      continue;
+    }
+    words.insert(words.end(), {sel, (int32_t)cls.topo.size()});
+    for (auto& term : cls.topo) {
+      words.push_back((int32_t)term.size());
+      for (auto& kv : term) {
+        const int col = ps.col(kv.first);
+        std::set<int32_t> ids;
+        for (auto& v : kv.second) ids.insert(ps.value_id(col, v));
+        if (ids.empty()) {
+          words.insert(words.end(), {0, OP_NEVER, 0});
+        } else {
+          words.insert(words.end(), {col, OP_IN, (int32_t)ids.size()});
+          words.insert(words.end(), ids.begin(), ids.end());
+        }
+      }
+    }
+  }
+  for (const char* k : kZoneLabels) {
+    auto it = s->e.col_index.find(k);
+    words.push_back(it == s->e.col_index.end() ? -1 : it->second);
+  }
+  words.push_back((int32_t)zone.size());
+  for (auto& kv : zone) {
+    const int col = ps.col(kv.first), gcol = ps.col(ga_label(kv.first));
+    std::set<int32_t> ids, gids;
+    for (auto& v : kv.second) ids.insert(ps.value_id(col, v));
+    for (auto& v : kv.second) gids.insert(ps.value_id(gcol, v));
+    words.insert(words.end(), {col, gcol, (int32_t)ids.size()});
+    words.insert(words.end(), ids.begin(), ids.end());
+    words.push_back((int32_t)gids.size());
+    words.insert(words.end(), gids.begin(), gids.end());
+  }
+  has_words = true;
+  return skip;
+}
+
 void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
   Encoded& e = s->e;
   const Pod& p = s->pods[i];
@@ -1075,8 +1455,16 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
   if (!na_required) fskip |= 1u << KSG_PL_NODE_AFFINITY;
   const std::vector<HostPort> hports = pod_host_ports(p);
   if (hports.empty()) fskip |= 1u << KSG_PL_NODE_PORTS;   // nodeports PreFilter: Skip without ports
-  for (int v : {KSG_PL_VOLUME_RESTRICTIONS, KSG_PL_NODE_VOLUME_LIMITS, KSG_PL_VOLUME_BINDING, KSG_PL_VOLUME_ZONE})
-    fskip |= 1u << v;
+  // the volume plugins' PreFilter (Skip for a pod without claims) and program
+  std::map<int, PreOutcome> outcome;
+  std::vector<int32_t> vol_words;
+  bool has_vol = false;
+  if (s->vol_run) {
+    fskip |= volume_plan(s, i, p, ps, outcome, vol_words, has_vol);
+  } else {
+    for (int v : {KSG_PL_VOLUME_RESTRICTIONS, KSG_PL_NODE_VOLUME_LIMITS, KSG_PL_VOLUME_BINDING, KSG_PL_VOLUME_ZONE})
+      fskip |= 1u << v;
+  }
   const auto& hard = s->pts_cache[i].first;
   const auto& soft = s->pts_cache[i].second;
   if (hard.empty()) fskip |= 1u << KSG_PL_POD_TOPOLOGY_SPREAD;
@@ -1087,8 +1475,6 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
   const bool pref_pod_aff = !p.aff_pref.empty() || !p.anti_pref.empty();
   if (prof.ignore_pref && !pref_pod_aff) sskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
   // NodeAffinity PreFilter: matchFields metadata.name In -> PreFilterResult
-  rec.node_set = -1;
-  e.prefilter_names.erase(i);
   if (p.has_na_req && !p.na_req.empty()) {
     std::optional<std::set<std::string>> names_u;
     bool all_named = true;
@@ -1097,13 +1483,7 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
       for (auto& rq : term.fields)
         if (rq.key == kObjectName && rq.op == "In") {
           std::set<std::string> sv(rq.values.begin(), rq.values.end());
-          if (!tn) {
-            tn = sv;
-          } else {
-            std::set<std::string> inter;
-            std::set_intersection(tn->begin(), tn->end(), sv.begin(), sv.end(), std::inserter(inter, inter.begin()));
-            tn = inter;
-          }
+          tn = tn ? set_and(*tn, sv) : sv;
         }
       if (!tn) {
         all_named = false;
@@ -1112,21 +1492,45 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
       if (!names_u) names_u = *tn;
       else names_u->insert(tn->begin(), tn->end());
     }
-    if (all_named && names_u) {
-      if (names_u->empty()) {
+    if (all_named && names_u)
+      outcome[KSG_PL_NODE_AFFINITY] = names_u->empty() ? PreOutcome{1, "pod affinity terms conflict", {}}
+                                                        : PreOutcome{2, "", *names_u};
+  }
+  // PreFilter outcomes in the profile's PreFilter order (RunPreFilterPlugins):
+  // the first rejection ends the cycle; PreFilterResults merge by
+  // intersection, and an empty merge ends it too (the framework's message)
+  rec.node_set = -1;
+  e.prefilter_names.erase(i);
+  e.prefilter_reject.erase(i);
+  std::optional<std::set<std::string>> merged;
+  for (int pid : prof.order[KSG_POINT_PREFILTER]) {
+    auto it = outcome.find(pid);
+    if (it == outcome.end()) continue;
+    const PreOutcome& o = it->second;
+    if (o.kind == 1) {
+      flags |= KSG_POD_PREFILTER_REJECT;
+      e.prefilter_reject[i] = {pid, o.msg};
+      break;
+    }
+    if (o.kind == 2) {
+      e.prefilter_names[i][pid] = std::vector<std::string>(o.names.begin(), o.names.end());
+      merged = merged ? set_and(*merged, o.names) : o.names;
+      if (merged->empty()) {
         flags |= KSG_POD_PREFILTER_REJECT;
-      } else {
-        const int N = (int)s->nodes.size(), W = (N + 31) / 32;
-        std::vector<uint32_t> bits(W, 0);
-        for (auto& nm : *names_u) {
-          auto it = s->node_index.find(nm);
-          if (it != s->node_index.end()) bits[it->second / 32] |= 1u << (it->second % 32);
-        }
-        rec.node_set = (int32_t)prog.size();
-        for (uint32_t b : bits) prog.push_back((int32_t)b);
-        e.prefilter_names[i] = std::vector<std::string>(names_u->begin(), names_u->end());
+        e.prefilter_reject[i] = {pid, std::string()};
+        break;
       }
     }
+  }
+  if (merged && !merged->empty() && !(flags & KSG_POD_PREFILTER_REJECT)) {
+    const int N = (int)s->nodes.size(), W = (N + 31) / 32;
+    std::vector<uint32_t> bits(W, 0);
+    for (auto& nm : *merged) {
+      auto it = s->node_index.find(nm);
+      if (it != s->node_index.end()) bits[it->second / 32] |= 1u << (it->second % 32);
+    }
+    rec.node_set = (int32_t)prog.size();
+    for (uint32_t b : bits) prog.push_back((int32_t)b);
   }
   rec.flags = flags;
   rec.filter_skip = fskip;
@@ -1289,7 +1693,7 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
   // ports := n_conf conf[n_conf] n_own own[n_own] (HostPortInfo.CheckConflict
   // over the vocabulary; own = what the pod's assume adds to UsedPorts)
   rec.ports = -1;
-  rec.vol = -1;   // claims are refused at ksg_snapshot_add_pod (volume programs: encoder.py only)
+  rec.vol = -1;
   rec.pad = 0;
   if (!hports.empty()) {
     std::set<int32_t> conf, own;
@@ -1313,6 +1717,10 @@ void encode_pod(ksg_snapshot* s, int i, Pass& ps) {
     prog.insert(prog.end(), conf.begin(), conf.end());
     prog.push_back((int32_t)own.size());
     prog.insert(prog.end(), own.begin(), own.end());
+  }
+  if (has_vol) {
+    rec.vol = (int32_t)prog.size();
+    ps.emit(prog, vol_words);
   }
   rec.blob = blob;
   rec.blob_len = (int32_t)prog.size() - blob;
@@ -1371,7 +1779,23 @@ void encode_all(ksg_snapshot* s) {
   }
   e.log_table.resize(N + 3);
   for (size_t i = 0; i < N + 3; i++) e.log_table[i] = go_log((double)i);
-  // pods
+  // pods: the volume plugins' view of the other pods (claim users, bindings)
+  s->claim_users.clear();
+  for (size_t i = 0; i < P; i++)
+    for (auto& c : s->pods[i].claims) s->claim_users[{s->pods[i].ns, c}].insert((int)i);
+  s->bound_set.clear();
+  for (auto& b : s->binds) s->bound_set.insert(b.first);
+  s->vol_run = false;
+  bool nvl = false;
+  for (int pt : {KSG_POINT_PREFILTER, KSG_POINT_FILTER})
+    for (int pid : s->prof.order[pt]) {
+      s->vol_run = s->vol_run || pid == KSG_PL_VOLUME_RESTRICTIONS || pid == KSG_PL_NODE_VOLUME_LIMITS ||
+                   pid == KSG_PL_VOLUME_BINDING || pid == KSG_PL_VOLUME_ZONE;
+      nvl = nvl || pid == KSG_PL_NODE_VOLUME_LIMITS;
+    }
+  s->csi_limits = false;
+  for (auto& n : s->nodes)
+    for (auto& kv : n.alloc) s->csi_limits = s->csi_limits || (nvl && starts_with(kv.first, "attachable-volumes-csi-"));
   e.pods.assign(P, ksg_pod{});
   Pass ps{s, false};
   for (size_t i = 0; i < P; i++) encode_pod(s, (int)i, ps);
@@ -1604,6 +2028,7 @@ bool extends_universe(ksg_snapshot* s, const Pod& p) {
   s->pod_selectors.resize(caches0);
   s->tmpl_match.resize(caches0);
   e.prefilter_names.erase(P);
+  e.prefilter_reject.erase(P);
   s->pods.pop_back();
   return miss;
 }
@@ -1794,6 +2219,23 @@ bool status_of(const Encoded& e, int32_t pod, uint32_t word, int32_t node, int* 
         m = reason == 1   ? "node(s) didn't match pod affinity rules"
             : reason == 2 ? "node(s) didn't match pod anti-affinity rules"
                           : "node(s) didn't satisfy existing pods anti-affinity rules";
+      break;
+    case KSG_PL_VOLUME_RESTRICTIONS:   // ErrReasonReadWriteOncePodConflict
+      c = KSG_CODE_UNSCHEDULABLE;
+      if (msg) m = "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode";
+      break;
+    case KSG_PL_VOLUME_BINDING: {   // FindPodVolumes' reasons, in order
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      static const char* const kVb[3] = {"node(s) had volume node affinity conflict",
+                                         "node(s) didn't find available persistent volumes to bind",
+                                         "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"};
+      for (int b = 0; msg && b < 3; b++)
+        if (reason & (1u << b)) m += (m.empty() ? "" : ", ") + std::string(kVb[b]);
+      break;
+    }
+    case KSG_PL_VOLUME_ZONE:
+      c = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      if (msg) m = "node(s) had no available volume zone";
       break;
     default:
       *err = "unexpected word";
@@ -1986,6 +2428,62 @@ bool resolve_namespaces(const ksg_snapshot* s, Pod& p) {
 }
 }  // namespace
 
+int ksg_snapshot_add_pv(ksg_snapshot* s, const ksg_pv_view* v) {
+  if (!s || !v || !v->name || v->n_labels < 0 || v->n_terms < 0) return KSG_E_INVALID;
+  PV pv;
+  pv.name = v->name;
+  pv.labels = copy_pairs(v->n_labels, v->labels);
+  pv.storage_class = S(v->storage_class);
+  pv.has_claim_ref = v->claim_name != nullptr;
+  pv.claim_ns = S(v->claim_namespace);
+  pv.claim_name = S(v->claim_name);
+  pv.source = S(v->source);
+  pv.has_na = v->has_node_affinity != 0;
+  for (int32_t i = 0; i < v->n_terms; i++) pv.na.push_back(copy_term(v->terms[i]));
+  s->pvs[pv.name] = std::move(pv);
+  s->encoded = false;        // every pod's claims resolve again at the next (full) encode
+  s->loaded_ctx = nullptr;
+  return KSG_OK;
+}
+
+int ksg_snapshot_add_pvc(ksg_snapshot* s, const ksg_pvc_view* v) {
+  if (!s || !v || !v->name || v->n_access_modes < 0 || v->n_annotations < 0) return KSG_E_INVALID;
+  PVC c;
+  c.ns = v->namespace_ ? S(v->namespace_) : "default";
+  c.name = v->name;
+  c.volume_name = S(v->volume_name);
+  c.storage_class = S(v->storage_class);
+  for (int32_t i = 0; i < v->n_access_modes; i++) c.modes.push_back(S(v->access_modes[i]));
+  c.ann = copy_pairs(v->n_annotations, v->annotations);
+  c.deleting = v->deleting != 0;
+  s->pvcs[{c.ns, c.name}] = std::move(c);
+  s->encoded = false;
+  s->loaded_ctx = nullptr;
+  return KSG_OK;
+}
+
+int ksg_snapshot_add_storage_class(ksg_snapshot* s, const ksg_storage_class_view* v) {
+  if (!s || !v || !v->name || v->n_allowed_topologies < 0) return KSG_E_INVALID;
+  SClass c;
+  c.name = v->name;
+  c.provisioner = S(v->provisioner);
+  c.mode = (v->binding_mode && *v->binding_mode) ? S(v->binding_mode) : std::string("Immediate");
+  for (int32_t i = 0; i < v->n_allowed_topologies; i++) {
+    const ksg_topology_term_view& t = v->allowed_topologies[i];
+    std::vector<std::pair<std::string, std::vector<std::string>>> term;
+    for (int32_t k = 0; k < t.n_requirements; k++) {
+      std::vector<std::string> vals;
+      for (int32_t j = 0; j < t.requirements[k].n_values; j++) vals.push_back(S(t.requirements[k].values[j]));
+      term.emplace_back(S(t.requirements[k].key), std::move(vals));
+    }
+    c.topo.push_back(std::move(term));
+  }
+  s->classes[c.name] = std::move(c);
+  s->encoded = false;
+  s->loaded_ctx = nullptr;
+  return KSG_OK;
+}
+
 int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labels, const ksg_str_pair* labels) {
   if (!s || !name || n_labels < 0 || (n_labels > 0 && !labels)) return KSG_E_INVALID;
   s->namespaces[S(name)] = copy_pairs(n_labels, labels);
@@ -2054,17 +2552,17 @@ int pod_from_view(ksg_snapshot* s, const ksg_pod_view* v, Pod& p) {
     for (int pid : s->prof.order[pt])
       vol_run = vol_run || pid == KSG_PL_VOLUME_RESTRICTIONS || pid == KSG_PL_NODE_VOLUME_LIMITS ||
                 pid == KSG_PL_VOLUME_BINDING || pid == KSG_PL_VOLUME_ZONE;
-  for (int32_t i = 0; vol_run && i < v->n_volumes; i++) {
-    static const char* const kRefused[] = {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk",
-                                           "awsElasticBlockStore", "azureDisk", "azureFile", "cinder",
-                                           "vsphereVolume", "portworxVolume", "rbd", "iscsi"};
+  for (int32_t i = 0; i < v->n_volumes; i++) {
+    static const char* const kRefused[] = {"ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "azureDisk",
+                                           "azureFile", "cinder", "vsphereVolume", "portworxVolume", "rbd", "iscsi"};
     const std::string kind = S(v->volumes[i].kind);
+    if (kind == "persistentVolumeClaim") p.claims.push_back(S(v->volumes[i].claim_name));
     for (const char* k : kRefused)
-      if (kind == k)
+      if (vol_run && kind == k)
         return fail(s, KSG_E_UNSUPPORTED,
                     "pod " + p.ns + "/" + p.name + ": volume '" + S(v->volumes[i].name) + "' (" + kind +
-                        ") makes the volume plugins' PreFilter run; VolumeBinding / VolumeZone / NodeVolumeLimits / "
-                        "VolumeRestrictions are modelled only as their Skip");
+                        ") makes the volume plugins' PreFilter run; of the volume sources only "
+                        "persistentVolumeClaim is modelled");
   }
   try {
     resolve_namespaces(s, p);
@@ -2370,8 +2868,10 @@ int ksg_snapshot_prefilter(ksg_snapshot* s, int32_t pod, int32_t plugin, uint32_
   if (n_names) *n_names = 0;
   uint32_t fskip = p.filter_skip;
   if (result_status & KSG_ST_IPA_PREFILTER_SKIP) fskip |= 1u << KSG_PL_INTER_POD_AFFINITY;
-  if (plugin == KSG_PL_NODE_AFFINITY && (p.flags & KSG_POD_PREFILTER_REJECT)) {
-    *code = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;   // "pod affinity terms conflict"
+  auto rj = s->e.prefilter_reject.find(pod);
+  if ((p.flags & KSG_POD_PREFILTER_REJECT) && rj != s->e.prefilter_reject.end() && rj->second.first == plugin &&
+      !rj->second.second.empty()) {
+    *code = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;   // its message: ksg_snapshot_prefilter_message
     return KSG_OK;
   }
   if ((fskip >> plugin) & 1u) {
@@ -2379,12 +2879,35 @@ int ksg_snapshot_prefilter(ksg_snapshot* s, int32_t pod, int32_t plugin, uint32_
     return KSG_OK;
   }
   *code = KSG_CODE_SUCCESS;
-  if (plugin == KSG_PL_NODE_AFFINITY && p.node_set >= 0) {
-    const auto& nm = s->e.prefilter_names.at(pod);
-    if (has_result) *has_result = 1;
-    if (n_names) *n_names = (int32_t)nm.size();
-    if (names)
-      for (int32_t k = 0; k < cap && k < (int32_t)nm.size(); k++) names[k] = nm[k].c_str();
+  auto pn = s->e.prefilter_names.find(pod);
+  if (pn != s->e.prefilter_names.end()) {
+    auto it = pn->second.find(plugin);
+    if (it != pn->second.end()) {
+      const auto& nm = it->second;
+      if (has_result) *has_result = 1;
+      if (n_names) *n_names = (int32_t)nm.size();
+      if (names)
+        for (int32_t k = 0; k < cap && k < (int32_t)nm.size(); k++) names[k] = nm[k].c_str();
+    }
+  }
+  return KSG_OK;
+}
+
+int ksg_snapshot_prefilter_message(ksg_snapshot* s, int32_t pod, int32_t plugin, char* msg, int32_t cap,
+                                   int32_t* len) {
+  if (!s || !len) return KSG_E_INVALID;
+  if (!s->encoded || pod < 0 || pod >= (int32_t)s->e.pods.size() || plugin < 0 || plugin >= KSG_NPLUGINS)
+    return fail(s, KSG_E_INVALID, "prefilter_message: index out of range");
+  std::string m;
+  auto rj = s->e.prefilter_reject.find(pod);
+  if ((s->e.pods[pod].flags & KSG_POD_PREFILTER_REJECT) && rj != s->e.prefilter_reject.end() &&
+      rj->second.first == plugin)
+    m = rj->second.second;
+  *len = (int32_t)m.size();
+  if (msg && cap > 0) {
+    const size_t n = std::min<size_t>(m.size(), (size_t)cap - 1);
+    std::memcpy(msg, m.data(), n);
+    msg[n] = 0;
   }
   return KSG_OK;
 }

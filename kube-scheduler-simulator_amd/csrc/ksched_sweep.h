@@ -40,6 +40,7 @@ struct SweepSlot {          // one workgroup's partials of the current pod (S > 
 };
 
 struct SweepArgs {
+  int32_t coop;                 // host: launch cooperatively (MULTI instances)
   DevCluster c;
   DevState st;                  // replica r's arrays at base + r * stride
   const ksg_pod* pods;

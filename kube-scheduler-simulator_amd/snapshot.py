@@ -99,6 +99,31 @@ class VolumeView(C.Structure):
     _fields_ = [("name", cp), ("kind", cp), ("claim_name", cp)]
 
 
+class PVView(C.Structure):
+    _fields_ = [("name", cp), ("n_labels", i32), ("labels", C.POINTER(StrPair)), ("storage_class", cp),
+                ("claim_namespace", cp), ("claim_name", cp), ("source", cp), ("has_node_affinity", i32),
+                ("n_terms", i32), ("terms", C.POINTER(NodeSelectorTermView))]
+
+
+class PVCView(C.Structure):
+    _fields_ = [("namespace_", cp), ("name", cp), ("volume_name", cp), ("storage_class", cp),
+                ("n_access_modes", i32), ("access_modes", C.POINTER(cp)), ("n_annotations", i32),
+                ("annotations", C.POINTER(StrPair)), ("deleting", i32)]
+
+
+class TopologyRequirementView(C.Structure):
+    _fields_ = [("key", cp), ("n_values", i32), ("values", C.POINTER(cp))]
+
+
+class TopologyTermView(C.Structure):
+    _fields_ = [("n_requirements", i32), ("requirements", C.POINTER(TopologyRequirementView))]
+
+
+class StorageClassView(C.Structure):
+    _fields_ = [("name", cp), ("provisioner", cp), ("binding_mode", cp), ("n_allowed_topologies", i32),
+                ("allowed_topologies", C.POINTER(TopologyTermView))]
+
+
 class PodView(C.Structure):
     _fields_ = [
         ("namespace_", cp), ("name", cp), ("n_labels", i32), ("labels", C.POINTER(StrPair)),
@@ -257,6 +282,38 @@ def pod_view(p: m.Pod, k: _Keep) -> PodView:
     return v
 
 
+def pv_view(pv: m.PersistentVolume, k: _Keep) -> PVView:
+    n, labels = k.pairs(pv.labels)
+    v = PVView(_b(pv.name), n, labels, _b(pv.storage_class or ""))
+    if pv.claim_ref is not None:
+        v.claim_namespace, v.claim_name = _b(pv.claim_ref[0]), _b(pv.claim_ref[1])
+    v.source = _b(pv.source or "")
+    if pv.node_affinity is not None:
+        v.has_node_affinity = 1
+        v.n_terms, v.terms = k.arr(NodeSelectorTermView, [k.term(t) for t in pv.node_affinity])
+    return v
+
+
+def pvc_view(c: m.PersistentVolumeClaim, k: _Keep) -> PVCView:
+    nm, modes = k.strs(list(c.access_modes))
+    na, ann = k.pairs(c.annotations)
+    return PVCView(_b(c.namespace), _b(c.name), _b(c.volume_name or ""), _b(c.storage_class or ""), nm, modes,
+                   na, ann, 1 if c.deleting else 0)
+
+
+def storage_class_view(sc: m.StorageClass, k: _Keep) -> StorageClassView:
+    terms = []
+    for term in sc.allowed_topologies:
+        reqs = []
+        for key, vals in term:
+            nv, vs = k.strs(list(vals))
+            reqs.append(TopologyRequirementView(_b(key), nv, vs))
+        nr, ra = k.arr(TopologyRequirementView, reqs)
+        terms.append(TopologyTermView(nr, ra))
+    nt, ta = k.arr(TopologyTermView, terms)
+    return StorageClassView(_b(sc.name), _b(sc.provisioner or ""), _b(sc.binding_mode or ""), nt, ta)
+
+
 def _spread_view(c: m.TopologySpreadConstraint, k: _Keep) -> SpreadView:
     nk, keys = k.strs(list(c.match_label_keys))
     return SpreadView(c.max_skew, _b(c.topology_key), _b(c.when_unsatisfiable), k.sel(c.label_selector),
@@ -314,6 +371,10 @@ class Snapshot:
         self._add_node = f("add_node", C.c_int, vp, C.POINTER(NodeView), C.POINTER(i32))
         self._add_pod = f("add_pod", C.c_int, vp, C.POINTER(PodView), C.POINTER(i32))
         self._add_ns = f("add_namespace", C.c_int, vp, cp, i32, C.POINTER(StrPair))
+        self._add_pv = f("add_pv", C.c_int, vp, C.POINTER(PVView))
+        self._add_pvc = f("add_pvc", C.c_int, vp, C.POINTER(PVCView))
+        self._add_sc = f("add_storage_class", C.c_int, vp, C.POINTER(StorageClassView))
+        self._prefilter_msg = f("prefilter_message", C.c_int, vp, i32, i32, C.c_char_p, i32, C.POINTER(i32))
         self._hint_pod = f("hint_pod", C.c_int, vp, C.POINTER(PodView))
         self._unhint_pod = f("unhint_pod", C.c_int, vp, cp, cp)
         self._bind_ = f("bind", C.c_int, vp, i32, i32)
@@ -344,6 +405,10 @@ class Snapshot:
             self.add_namespace(name, labels)
         for n in nodes:
             self.add_node(n)
+        # the volume plugins' listers: the storage objects the pods' claims
+        # resolve against (model.Pod.storage; one Storage shared by the pods)
+        for st in {id(p.storage): p.storage for p in pods if p.storage is not None}.values():
+            self.add_storage(st)
         for p in pods:
             self.add_pod(p)
         for pi, ni in bound:
@@ -375,6 +440,26 @@ class Snapshot:
         k = _Keep()
         n, arr = k.pairs(labels)
         self._check(self._add_ns(self.h, _b(name), n, arr), "add_namespace")
+
+    def add_storage(self, st: m.Storage) -> None:
+        """ksg_snapshot_add_pv / _add_pvc / _add_storage_class of every object."""
+        for sc in st.classes.values():
+            k = _Keep()
+            self._check(self._add_sc(self.h, C.byref(storage_class_view(sc, k))), "add_storage_class")
+        for pv in st.pvs.values():
+            k = _Keep()
+            self._check(self._add_pv(self.h, C.byref(pv_view(pv, k))), "add_pv")
+        for c in st.pvcs.values():
+            k = _Keep()
+            self._check(self._add_pvc(self.h, C.byref(pvc_view(c, k))), "add_pvc")
+
+    def prefilter_message(self, pod: int, plugin: int) -> str:
+        """ksg_snapshot_prefilter_message: the plugin's PreFilter rejection ("" none)."""
+        n = i32()
+        self._check(self._prefilter_msg(self.h, pod, plugin, None, 0, C.byref(n)), "prefilter_message")
+        buf = C.create_string_buffer(n.value + 1)
+        self._check(self._prefilter_msg(self.h, pod, plugin, buf, n.value + 1, C.byref(n)), "prefilter_message")
+        return buf.value.decode()
 
     def add_pod(self, p: m.Pod) -> int:
         k = _Keep()

@@ -190,9 +190,9 @@ def main():
             if row and row.get("hbm_bytes_per_dispatch") is not None:
                 roof["traffic"] = row["hbm_bytes_per_dispatch"]
                 roof["traffic_source"] = args.pmc
-                ms = roof["traffic"] / (roof["avg_launch_ms"] * 1e-3) / 1e9
-                roof["memory_side_GBps"] = ms
-                roof["memory_side_frac_of_hbm"] = ms / roof["peak"]
+                side = roof["traffic"] / (roof["avg_launch_ms"] * 1e-3) / 1e9
+                roof["memory_side_GBps"] = side
+                roof["memory_side_frac_of_hbm"] = side / roof["peak"]
                 roof["traffic_over_algorithmic"] = roof["traffic"] / roof["bytes_per_launch"]
     evals = R * P * len(nodes)
     out = {

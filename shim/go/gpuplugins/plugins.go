@@ -65,7 +65,8 @@ type nominatedVerdict struct {
 
 type preFilterResult struct {
 	code  int
-	names []string // NodeAffinity's PreFilterResult, nil = none
+	names []string // NodeAffinity's / VolumeBinding's PreFilterResult, nil = none
+	msg   string   // a rejection's message (ksg_snapshot_prefilter_message)
 }
 
 func (s *podState) Clone() framework.StateData { return s }
@@ -108,6 +109,10 @@ type Evaluator struct {
 	nsDirty   bool                // a namespace was added or its labels changed
 	attached  sync.Once
 	nsList    func() ([]*v1.Namespace, error) // the handle's namespace lister, nil before attach
+	// the volume plugins' listers (PVs, claims, classes): every object is handed
+	// to the snapshot when one changed (the next encode is then a full one)
+	stDirty bool
+	stSync  func(*ksched.Snapshot) error
 }
 
 // staleLimit: rebuild once this many superseded snapshot pods accumulated
@@ -144,6 +149,50 @@ func (e *Evaluator) attach(h framework.Handle) {
 			AddFunc:    func(interface{}) { e.markNamespaces() },
 			UpdateFunc: func(o, n interface{}) { e.markNamespaces() },
 		})
+		pvInf, pvcInf, scInf := f.Core().V1().PersistentVolumes(), f.Core().V1().PersistentVolumeClaims(),
+			f.Storage().V1().StorageClasses()
+		pvL, pvcL, scL := pvInf.Lister(), pvcInf.Lister(), scInf.Lister()
+		e.side.Lock()
+		e.stSync = func(snap *ksched.Snapshot) error {
+			scs, err := scL.List(labels.Everything())
+			if err != nil {
+				return err
+			}
+			for _, sc := range scs {
+				if err := snap.AddStorageClass(sc); err != nil {
+					return err
+				}
+			}
+			pvs, err := pvL.List(labels.Everything())
+			if err != nil {
+				return err
+			}
+			for _, pv := range pvs {
+				if err := snap.AddPV(pv); err != nil {
+					return err
+				}
+			}
+			pvcs, err := pvcL.List(labels.Everything())
+			if err != nil {
+				return err
+			}
+			for _, c := range pvcs {
+				if err := snap.AddPVC(c); err != nil {
+					return err
+				}
+			}
+			return nil
+		}
+		e.stDirty = true
+		e.side.Unlock()
+		mark := cache.ResourceEventHandlerFuncs{
+			AddFunc:    func(interface{}) { e.markStorage() },
+			UpdateFunc: func(o, n interface{}) { e.markStorage() },
+			DeleteFunc: func(interface{}) { e.markStorage() },
+		}
+		for _, inf := range []cache.SharedIndexInformer{pvInf.Informer(), pvcInf.Informer(), scInf.Informer()} {
+			_, _ = inf.AddEventHandler(mark)
+		}
 		_, _ = f.Core().V1().Pods().Informer().AddEventHandler(cache.ResourceEventHandlerFuncs{
 			AddFunc:    func(o interface{}) { e.notePod(o) },
 			UpdateFunc: func(_, n interface{}) { e.notePod(n) },
@@ -162,6 +211,27 @@ func (e *Evaluator) attach(h framework.Handle) {
 		e.subscribed = true
 		e.side.Unlock()
 	})
+}
+
+func (e *Evaluator) markStorage() {
+	e.side.Lock()
+	e.stDirty = true
+	e.side.Unlock()
+}
+
+// syncStorage (under mu) hands the PVs, claims and classes to the snapshot
+// when one changed (or at a rebuild): pods with claims resolve against them.
+// A deleted object stays in the snapshot until the next rebuild; the claims
+// that named it are then unresolved, as upstream's listers would have them.
+func (e *Evaluator) syncStorage(force bool) error {
+	e.side.Lock()
+	dirty, sync := e.stDirty || force, e.stSync
+	e.stDirty = false
+	e.side.Unlock()
+	if !dirty || sync == nil || e.snap == nil {
+		return nil
+	}
+	return sync(e.snap)
 }
 
 func (e *Evaluator) markNamespaces() {
@@ -310,6 +380,9 @@ func (e *Evaluator) rebuild(infos []*framework.NodeInfo) error {
 	}
 	// every namespace before the first pod: a bound pod's namespaceSelector
 	// term needs them to encode
+	if err := e.syncStorage(true); err != nil {
+		return err
+	}
 	if err := e.syncNamespaces(true); err != nil {
 		return err
 	}
@@ -342,6 +415,9 @@ func (e *Evaluator) syncCluster(infos []*framework.NodeInfo) error {
 	}
 	if !same {
 		return e.rebuild(infos)
+	}
+	if err := e.syncStorage(false); err != nil {
+		return err
 	}
 	if err := e.syncNamespaces(false); err != nil {
 		return err
@@ -453,7 +529,13 @@ func (e *Evaluator) evalPod(cs *framework.CycleState, pod *v1.Pod, infos []*fram
 		if err != nil {
 			return nil, err
 		}
-		st.pre[id] = preFilterResult{code: code, names: names}
+		msg := ""
+		if code == ksched.CodeUnschedulableAndUnresolvable {
+			if msg, err = e.snap.PreFilterMessage(idx, id); err != nil {
+				return nil, err
+			}
+		}
+		st.pre[id] = preFilterResult{code: code, names: names, msg: msg}
 	}
 	cs.Write(stateKey, st)
 	return st, nil
@@ -674,7 +756,7 @@ func (b *base) preFilter(cs *framework.CycleState, pod *v1.Pod) (*framework.PreF
 	case ksched.CodeSkip:
 		return nil, framework.NewStatus(framework.Skip) // recorded as "" (store.go:522)
 	case ksched.CodeUnschedulableAndUnresolvable: // nodeaffinity errReasonConflict
-		return nil, framework.NewStatus(framework.UnschedulableAndUnresolvable, "pod affinity terms conflict")
+		return nil, framework.NewStatus(framework.UnschedulableAndUnresolvable, st.pre[b.id].msg)
 	}
 	if names != nil {
 		return &framework.PreFilterResult{NodeNames: sets.New[string](names...)}, nil

@@ -15,6 +15,7 @@ import (
 	"unsafe"
 
 	v1 "k8s.io/api/core/v1"
+	storagev1 "k8s.io/api/storage/v1"
 	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
 	"k8s.io/apimachinery/pkg/labels"
 	"k8s.io/apimachinery/pkg/selection"
@@ -54,7 +55,7 @@ func (a *arena) free() {
 }
 
 func (a *arena) strs(ss []string) (C.int32_t, **C.char) {
-	arr := unsafe.Slice((**C.char)(a.alloc(len(ss), C.size_t(unsafe.Sizeof((*C.char)(nil))))), len(ss)+1)
+	arr := unsafe.Slice((**C.char)(a.alloc(len(ss)+1, C.size_t(unsafe.Sizeof((*C.char)(nil))))), len(ss)+1)
 	for i, s := range ss {
 		arr[i] = a.str(s)
 	}
@@ -62,7 +63,7 @@ func (a *arena) strs(ss []string) (C.int32_t, **C.char) {
 }
 
 func (a *arena) pairs(m map[string]string) (C.int32_t, *C.ksg_str_pair) {
-	arr := unsafe.Slice((*C.ksg_str_pair)(a.alloc(len(m), C.sizeof_ksg_str_pair)), len(m)+1)
+	arr := unsafe.Slice((*C.ksg_str_pair)(a.alloc(len(m)+1, C.sizeof_ksg_str_pair)), len(m)+1)
 	i := 0
 	for k, v := range m { // order is irrelevant: the encoder keys by name
 		arr[i].key, arr[i].value = a.str(k), a.str(v)
@@ -73,7 +74,7 @@ func (a *arena) pairs(m map[string]string) (C.int32_t, *C.ksg_str_pair) {
 
 // quantity: cpu in millicores (Quantity.MilliValue), the rest in base units.
 func (a *arena) resources(rl v1.ResourceList) (C.int32_t, *C.ksg_quantity) {
-	arr := unsafe.Slice((*C.ksg_quantity)(a.alloc(len(rl), C.sizeof_ksg_quantity)), len(rl)+1)
+	arr := unsafe.Slice((*C.ksg_quantity)(a.alloc(len(rl)+1, C.sizeof_ksg_quantity)), len(rl)+1)
 	i := 0
 	for name, q := range rl {
 		arr[i].name = a.str(string(name))
@@ -88,7 +89,7 @@ func (a *arena) resources(rl v1.ResourceList) (C.int32_t, *C.ksg_quantity) {
 }
 
 func (a *arena) nodeReqs(rs []v1.NodeSelectorRequirement) (C.int32_t, *C.ksg_requirement_view) {
-	arr := unsafe.Slice((*C.ksg_requirement_view)(a.alloc(len(rs), C.sizeof_ksg_requirement_view)), len(rs)+1)
+	arr := unsafe.Slice((*C.ksg_requirement_view)(a.alloc(len(rs)+1, C.sizeof_ksg_requirement_view)), len(rs)+1)
 	for i, r := range rs {
 		arr[i].key, arr[i].op = a.str(r.Key), a.str(string(r.Operator))
 		arr[i].n_values, arr[i].values = a.strs(r.Values)
@@ -97,7 +98,7 @@ func (a *arena) nodeReqs(rs []v1.NodeSelectorRequirement) (C.int32_t, *C.ksg_req
 }
 
 func (a *arena) labelReqs(rs []metav1.LabelSelectorRequirement) (C.int32_t, *C.ksg_requirement_view) {
-	arr := unsafe.Slice((*C.ksg_requirement_view)(a.alloc(len(rs), C.sizeof_ksg_requirement_view)), len(rs)+1)
+	arr := unsafe.Slice((*C.ksg_requirement_view)(a.alloc(len(rs)+1, C.sizeof_ksg_requirement_view)), len(rs)+1)
 	for i, r := range rs {
 		arr[i].key, arr[i].op = a.str(r.Key), a.str(string(r.Operator))
 		arr[i].n_values, arr[i].values = a.strs(r.Values)
@@ -153,7 +154,7 @@ func (a *arena) selectorOf(sel labels.Selector) C.ksg_label_selector_view {
 
 func (a *arena) affinity(ts []v1.PodAffinityTerm, ws []v1.WeightedPodAffinityTerm) (C.int32_t, *C.ksg_affinity_term_view) {
 	n := len(ts) + len(ws)
-	arr := unsafe.Slice((*C.ksg_affinity_term_view)(a.alloc(n, C.sizeof_ksg_affinity_term_view)), n+1)
+	arr := unsafe.Slice((*C.ksg_affinity_term_view)(a.alloc(n+1, C.sizeof_ksg_affinity_term_view)), n+1)
 	fill := func(i int, w int32, t v1.PodAffinityTerm) {
 		arr[i].weight = C.int32_t(w)
 		arr[i].selector = a.selector(t.LabelSelector)
@@ -171,14 +172,14 @@ func (a *arena) affinity(ts []v1.PodAffinityTerm, ws []v1.WeightedPodAffinityTer
 }
 
 func (a *arena) containers(cs []v1.Container, init bool) (C.int32_t, *C.ksg_container_view) {
-	arr := unsafe.Slice((*C.ksg_container_view)(a.alloc(len(cs), C.sizeof_ksg_container_view)), len(cs)+1)
+	arr := unsafe.Slice((*C.ksg_container_view)(a.alloc(len(cs)+1, C.sizeof_ksg_container_view)), len(cs)+1)
 	for i, c := range cs {
 		arr[i].image = a.str(c.Image)
 		arr[i].n_requests, arr[i].requests = a.resources(c.Resources.Requests)
 		if init && c.RestartPolicy != nil && *c.RestartPolicy == v1.ContainerRestartPolicyAlways {
 			arr[i].restartable = 1
 		}
-		hp := unsafe.Slice((*C.ksg_host_port_view)(a.alloc(len(c.Ports), C.sizeof_ksg_host_port_view)), len(c.Ports)+1)
+		hp := unsafe.Slice((*C.ksg_host_port_view)(a.alloc(len(c.Ports)+1, C.sizeof_ksg_host_port_view)), len(c.Ports)+1)
 		n := 0
 		for _, p := range c.Ports {
 			if p.HostPort > 0 { // schedutil.GetHostPorts; "" ip / protocol sanitised natively
@@ -196,7 +197,7 @@ func (a *arena) node(n *v1.Node) *C.ksg_node_view {
 	v := (*C.ksg_node_view)(a.alloc(1, C.sizeof_ksg_node_view))
 	v.name = a.str(n.Name)
 	v.n_labels, v.labels = a.pairs(n.Labels)
-	ts := unsafe.Slice((*C.ksg_taint_view)(a.alloc(len(n.Spec.Taints), C.sizeof_ksg_taint_view)), len(n.Spec.Taints)+1)
+	ts := unsafe.Slice((*C.ksg_taint_view)(a.alloc(len(n.Spec.Taints)+1, C.sizeof_ksg_taint_view)), len(n.Spec.Taints)+1)
 	for i, t := range n.Spec.Taints {
 		ts[i].key, ts[i].value, ts[i].effect = a.str(t.Key), a.str(t.Value), a.str(string(t.Effect))
 	}
@@ -205,7 +206,7 @@ func (a *arena) node(n *v1.Node) *C.ksg_node_view {
 	if n.Spec.Unschedulable {
 		v.unschedulable = 1
 	}
-	im := unsafe.Slice((*C.ksg_image_view)(a.alloc(len(n.Status.Images), C.sizeof_ksg_image_view)), len(n.Status.Images)+1)
+	im := unsafe.Slice((*C.ksg_image_view)(a.alloc(len(n.Status.Images)+1, C.sizeof_ksg_image_view)), len(n.Status.Images)+1)
 	for i, img := range n.Status.Images {
 		im[i].n_names, im[i].names = a.strs(img.Names)
 		im[i].size_bytes = C.int64_t(img.SizeBytes)
@@ -233,7 +234,7 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 		if na := aff.NodeAffinity; na != nil {
 			if req := na.RequiredDuringSchedulingIgnoredDuringExecution; req != nil {
 				v.has_na_required = 1
-				terms := unsafe.Slice((*C.ksg_node_selector_term_view)(a.alloc(len(req.NodeSelectorTerms),
+				terms := unsafe.Slice((*C.ksg_node_selector_term_view)(a.alloc(len(req.NodeSelectorTerms)+1,
 					C.sizeof_ksg_node_selector_term_view)), len(req.NodeSelectorTerms)+1)
 				for i, t := range req.NodeSelectorTerms {
 					terms[i] = a.term(t)
@@ -242,7 +243,7 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 			}
 			if pref := na.PreferredDuringSchedulingIgnoredDuringExecution; pref != nil {
 				v.has_na_preferred = 1
-				pts := unsafe.Slice((*C.ksg_preferred_term_view)(a.alloc(len(pref), C.sizeof_ksg_preferred_term_view)), len(pref)+1)
+				pts := unsafe.Slice((*C.ksg_preferred_term_view)(a.alloc(len(pref)+1, C.sizeof_ksg_preferred_term_view)), len(pref)+1)
 				for i, t := range pref {
 					pts[i].weight = C.int32_t(t.Weight)
 					pts[i].preference = a.term(t.Preference)
@@ -259,7 +260,7 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 			v.n_pod_anti_affinity_preferred, v.pod_anti_affinity_preferred = a.affinity(nil, pa.PreferredDuringSchedulingIgnoredDuringExecution)
 		}
 	}
-	tols := unsafe.Slice((*C.ksg_toleration_view)(a.alloc(len(p.Spec.Tolerations), C.sizeof_ksg_toleration_view)), len(p.Spec.Tolerations)+1)
+	tols := unsafe.Slice((*C.ksg_toleration_view)(a.alloc(len(p.Spec.Tolerations)+1, C.sizeof_ksg_toleration_view)), len(p.Spec.Tolerations)+1)
 	for i, t := range p.Spec.Tolerations {
 		tols[i].key, tols[i].op = a.str(t.Key), a.str(string(t.Operator))
 		tols[i].value, tols[i].effect = a.str(t.Value), a.str(string(t.Effect))
@@ -278,7 +279,7 @@ func (a *arena) pod(p *v1.Pod, defaultSel labels.Selector) *C.ksg_pod_view {
 	if nv < 1 {
 		nv = 1
 	}
-	vols := unsafe.Slice((*C.ksg_volume_view)(a.alloc(len(p.Spec.Volumes), C.sizeof_ksg_volume_view)), nv)
+	vols := unsafe.Slice((*C.ksg_volume_view)(a.alloc(len(p.Spec.Volumes)+1, C.sizeof_ksg_volume_view)), nv)
 	for i, vol := range p.Spec.Volumes {
 		vols[i].name, vols[i].kind = a.str(vol.Name), a.str(volumeKind(&vol.VolumeSource))
 		if vol.PersistentVolumeClaim != nil {
@@ -368,7 +369,7 @@ func (a *arena) spreads(tsc []v1.TopologySpreadConstraint) (C.int32_t, *C.ksg_sp
 	if nv < 1 {
 		nv = 1
 	}
-	sp := unsafe.Slice((*C.ksg_spread_view)(a.alloc(len(tsc), C.sizeof_ksg_spread_view)), nv)
+	sp := unsafe.Slice((*C.ksg_spread_view)(a.alloc(len(tsc)+1, C.sizeof_ksg_spread_view)), nv)
 	for i, c := range tsc {
 		sp[i].max_skew = C.int32_t(c.MaxSkew)
 		sp[i].topology_key = a.str(c.TopologyKey)
@@ -406,14 +407,14 @@ func NewSnapshot(p *ProfileArgs) (*Snapshot, error) {
 	var a arena
 	defer a.free()
 	var pv C.ksg_profile_view
-	pls := unsafe.Slice((*C.ksg_plugin_view)(a.alloc(len(p.Plugins), C.sizeof_ksg_plugin_view)), len(p.Plugins)+1)
+	pls := unsafe.Slice((*C.ksg_plugin_view)(a.alloc(len(p.Plugins)+1, C.sizeof_ksg_plugin_view)), len(p.Plugins)+1)
 	for i, pl := range p.Plugins {
 		pls[i].name, pls[i].weight = a.str(pl.Name), C.int32_t(pl.Weight)
 	}
 	pv.n_plugins, pv.plugins = C.int32_t(len(p.Plugins)), &pls[0]
 	pv.fit_strategy = a.str(p.FitStrategy)
 	list := func(order []string, w map[string]int64) (C.int32_t, *C.ksg_quantity) {
-		arr := unsafe.Slice((*C.ksg_quantity)(a.alloc(len(order), C.sizeof_ksg_quantity)), len(order)+1)
+		arr := unsafe.Slice((*C.ksg_quantity)(a.alloc(len(order)+1, C.sizeof_ksg_quantity)), len(order)+1)
 		for i, n := range order {
 			arr[i].name, arr[i].value = a.str(n), C.int64_t(w[n])
 		}
@@ -443,7 +444,7 @@ func NewSnapshot(p *ProfileArgs) (*Snapshot, error) {
 	pv.n_default_constraints, pv.default_constraints = a.spreads(p.PTSDefaultConstraints)
 	for k := 0; k < NPoints; k++ {
 		ps := p.Points[k]
-		en := unsafe.Slice((*C.ksg_plugin_view)(a.alloc(len(ps.Enabled), C.sizeof_ksg_plugin_view)), len(ps.Enabled)+1)
+		en := unsafe.Slice((*C.ksg_plugin_view)(a.alloc(len(ps.Enabled)+1, C.sizeof_ksg_plugin_view)), len(ps.Enabled)+1)
 		for i, pl := range ps.Enabled {
 			en[i].name, en[i].weight = a.str(pl.Name), C.int32_t(pl.Weight)
 		}
@@ -502,6 +503,120 @@ func (x *Snapshot) AddNamespace(ns *v1.Namespace) error {
 	defer a.free()
 	n, l := a.pairs(ns.Labels)
 	return x.check(C.ksg_snapshot_add_namespace(x.s, a.str(ns.Name), n, l))
+}
+
+// pvSource is the JSON key of the PersistentVolumeSource that is set (the
+// in-tree sources CSI migration translates are refused at encode).
+func pvSource(s *v1.PersistentVolumeSource) string {
+	switch {
+	case s.CSI != nil:
+		return "csi"
+	case s.HostPath != nil:
+		return "hostPath"
+	case s.Local != nil:
+		return "local"
+	case s.NFS != nil:
+		return "nfs"
+	case s.GCEPersistentDisk != nil:
+		return "gcePersistentDisk"
+	case s.AWSElasticBlockStore != nil:
+		return "awsElasticBlockStore"
+	case s.AzureDisk != nil:
+		return "azureDisk"
+	case s.AzureFile != nil:
+		return "azureFile"
+	case s.Cinder != nil:
+		return "cinder"
+	case s.VsphereVolume != nil:
+		return "vsphereVolume"
+	case s.PortworxVolume != nil:
+		return "portworxVolume"
+	}
+	return "other"
+}
+
+const annBetaStorageClass = "volume.beta.kubernetes.io/storage-class"
+
+// AddPV adds or replaces a PersistentVolume (the volume plugins' PV lister;
+// snapshot.go:34 pvs); the next encode is a full one.
+func (x *Snapshot) AddPV(pv *v1.PersistentVolume) error {
+	var a arena
+	defer a.free()
+	v := (*C.ksg_pv_view)(a.alloc(1, C.sizeof_ksg_pv_view))
+	v.name = a.str(pv.Name)
+	v.n_labels, v.labels = a.pairs(pv.Labels)
+	sc := pv.Spec.StorageClassName // storagehelpers.GetPersistentVolumeClass
+	if c, ok := pv.Annotations[annBetaStorageClass]; ok {
+		sc = c
+	}
+	v.storage_class = a.str(sc)
+	if r := pv.Spec.ClaimRef; r != nil {
+		v.claim_namespace, v.claim_name = a.str(r.Namespace), a.str(r.Name)
+	}
+	v.source = a.str(pvSource(&pv.Spec.PersistentVolumeSource))
+	if na := pv.Spec.NodeAffinity; na != nil && na.Required != nil {
+		v.has_node_affinity = 1
+		ts := na.Required.NodeSelectorTerms
+		terms := unsafe.Slice((*C.ksg_node_selector_term_view)(a.alloc(len(ts)+1,
+			C.sizeof_ksg_node_selector_term_view)), len(ts)+1)
+		for i, t := range ts {
+			terms[i] = a.term(t)
+		}
+		v.n_terms, v.terms = C.int32_t(len(ts)), &terms[0]
+	}
+	return x.check(C.ksg_snapshot_add_pv(x.s, v))
+}
+
+// AddPVC adds or replaces a PersistentVolumeClaim (snapshot.go:35 pvcs).
+func (x *Snapshot) AddPVC(c *v1.PersistentVolumeClaim) error {
+	var a arena
+	defer a.free()
+	v := (*C.ksg_pvc_view)(a.alloc(1, C.sizeof_ksg_pvc_view))
+	v.namespace_, v.name = a.str(c.Namespace), a.str(c.Name)
+	v.volume_name = a.str(c.Spec.VolumeName)
+	sc := "" // storagehelpers.GetPersistentVolumeClaimClass
+	if cl, ok := c.Annotations[annBetaStorageClass]; ok {
+		sc = cl
+	} else if c.Spec.StorageClassName != nil {
+		sc = *c.Spec.StorageClassName
+	}
+	v.storage_class = a.str(sc)
+	modes := make([]string, len(c.Spec.AccessModes))
+	for i, m := range c.Spec.AccessModes {
+		modes[i] = string(m)
+	}
+	v.n_access_modes, v.access_modes = a.strs(modes)
+	v.n_annotations, v.annotations = a.pairs(c.Annotations)
+	if c.DeletionTimestamp != nil {
+		v.deleting = 1
+	}
+	return x.check(C.ksg_snapshot_add_pvc(x.s, v))
+}
+
+// AddStorageClass adds or replaces a StorageClass (snapshot.go:36).
+func (x *Snapshot) AddStorageClass(sc *storagev1.StorageClass) error {
+	var a arena
+	defer a.free()
+	v := (*C.ksg_storage_class_view)(a.alloc(1, C.sizeof_ksg_storage_class_view))
+	v.name, v.provisioner = a.str(sc.Name), a.str(sc.Provisioner)
+	mode := string(storagev1.VolumeBindingImmediate)
+	if sc.VolumeBindingMode != nil {
+		mode = string(*sc.VolumeBindingMode)
+	}
+	v.binding_mode = a.str(mode)
+	terms := unsafe.Slice((*C.ksg_topology_term_view)(a.alloc(len(sc.AllowedTopologies)+1,
+		C.sizeof_ksg_topology_term_view)), len(sc.AllowedTopologies)+1)
+	for i, t := range sc.AllowedTopologies {
+		reqs := unsafe.Slice((*C.ksg_topology_requirement_view)(a.alloc(len(t.MatchLabelExpressions)+1,
+			C.sizeof_ksg_topology_requirement_view)), len(t.MatchLabelExpressions)+1)
+		for k, r := range t.MatchLabelExpressions {
+			reqs[k].key = a.str(r.Key)
+			reqs[k].n_values, reqs[k].values = a.strs(r.Values)
+		}
+		terms[i].n_requirements, terms[i].requirements = C.int32_t(len(t.MatchLabelExpressions)), &reqs[0]
+	}
+	v.n_allowed_topologies, v.allowed_topologies = C.int32_t(len(sc.AllowedTopologies)), &terms[0]
+	return x.check(C.ksg_snapshot_add_storage_class(x.s, v))
 }
 
 // Bind records a pod already running on a node (replayed at load).
@@ -662,6 +777,24 @@ func (x *Snapshot) PreFilter(pod, plugin int, resultStatus uint32) (int, []strin
 }
 
 // NodeIndex returns the column of a node (-1: unknown).
+// PreFilterMessage is the message of a PreFilter rejection of plugin
+// (NodeAffinity's conflict, a volume plugin's claim / volume lookup; "" none).
+func (x *Snapshot) PreFilterMessage(pod, plugin int) (string, error) {
+	var n C.int32_t
+	if err := x.check(C.ksg_snapshot_prefilter_message(x.s, C.int32_t(pod), C.int32_t(plugin), nil, 0, &n)); err != nil {
+		return "", err
+	}
+	if n == 0 {
+		return "", nil
+	}
+	buf := (*C.char)(C.malloc(C.size_t(n) + 1))
+	defer C.free(unsafe.Pointer(buf))
+	if err := x.check(C.ksg_snapshot_prefilter_message(x.s, C.int32_t(pod), C.int32_t(plugin), buf, n+1, &n)); err != nil {
+		return "", err
+	}
+	return C.GoStringN(buf, n), nil
+}
+
 func (x *Snapshot) NodeIndex(name string) int {
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))

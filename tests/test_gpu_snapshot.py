@@ -27,7 +27,8 @@ def oracle():
 CASES = [("c2", lambda: G.config2(n_nodes=500, n_pods=600)),
          ("c3", lambda: G.config3(n_nodes=300, n_pods=500)),
          ("c1", lambda: G.config1(n_nodes=100, n_pods=300))] + \
-        [(f"zoo-{s}", (lambda s=s: zoo.zoo(s))) for s in range(3)]
+        [(f"zoo-{s}", (lambda s=s: zoo.zoo(s))) for s in range(3)] + \
+        [(f"zoo-volumes-{s}", (lambda s=s: zoo.zoo_volumes(s))) for s in range(3)]
 
 
 @pytest.mark.parametrize("name,make", CASES, ids=[c[0] for c in CASES])
@@ -115,4 +116,28 @@ def test_eval_then_commit_topology(built, oracle):
             gpu.commit(j, r.selected)
     oracle.load(enc, pf)
     want, _ = oracle.run_queue(0, len(pods))
+    np.testing.assert_array_equal(np.array(got, np.int32), want)
+
+
+def test_per_cycle_sync_path_volumes(built):
+    """The per-cycle loop with claims: a pod with claims makes the sync
+    re-encode (shared claims and storage objects are read from the whole
+    snapshot); placements equal one device queue of the same snapshot."""
+    nodes, pods, prof = zoo.zoo_volumes(1)
+    full = S.Snapshot(prof, nodes, pods)
+    g1 = native.Engine(device=0)
+    full.load(g1)
+    want, _ = g1.run_queue(0, len(pods))
+    snap = S.Snapshot(prof, nodes, pods[:1])
+    g2 = native.Engine(device=0)
+    snap.load(g2)
+    got = []
+    for j, p in enumerate(pods):
+        if j > 0:
+            snap.add_pod(p)
+            snap.sync(g2)
+        r = g2.eval(j)
+        got.append(r.selected)
+        if r.selected >= 0:
+            snap.assume(g2, j, r.selected)
     np.testing.assert_array_equal(np.array(got, np.int32), want)

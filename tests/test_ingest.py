@@ -381,10 +381,10 @@ def test_volumes_parsed_from_the_export_sample():
     assert st.pvs["pv2"].claim_ref is None and st.pvs["pv1"].node_affinity is None
 
 
-def test_claim_volume_encoded_by_python_refused_by_native():
-    """A PVC makes the volume plugins' PreFilter run upstream: the Python
-    encoder models them (a volume program), the C ABI's native encoder still
-    refuses such pods loudly (never recording a Skip)."""
+def test_claim_volume_encoded_by_python_and_native():
+    """A PVC makes the volume plugins' PreFilter run upstream: both encoders
+    model them (a volume program) and produce the same bytes; the native one
+    resolves the claim against the storage objects added through the C ABI."""
     S = pkg("snapshot")
     snap = I.load_snapshot(_volume_doc())
     enc = E.Encoder(snap.nodes, snap.pods, snap.profile)
@@ -394,11 +394,11 @@ def test_claim_volume_encoded_by_python_refused_by_native():
     for v in (P.VOLUME_RESTRICTIONS, P.NODE_VOLUME_LIMITS, P.VOLUME_BINDING):
         assert not fskip >> v & 1
     assert fskip >> P.VOLUME_ZONE & 1   # pv1 has no zone labels: VolumeZone's PreFilter Skip
-    s = S.Snapshot(snap.profile, snap.nodes)
-    ok = [p for p in snap.pods if p.name == "scratch"][0]
-    s.add_pod(ok)
-    with pytest.raises(S.SnapshotError, match="persistentVolumeClaim"):
-        s.add_pod([p for p in snap.pods if p.name == "claims"][0])
+    s = S.Snapshot(snap.profile, snap.nodes, snap.pods)
+    s.encode()
+    got = s.arrays()
+    assert got["pods"].tobytes() == enc.workload.pods.tobytes()
+    np.testing.assert_array_equal(got["prog"], enc.workload.prog)
 
 
 def test_volume_sources_the_plugins_skip_encode():

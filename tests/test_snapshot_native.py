@@ -496,3 +496,111 @@ def test_hint_without_new_terms_keeps_appending(built):
     o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
     want, _ = o.run_queue(0, len(order), results=False)
     np.testing.assert_array_equal(_oracle_on_views(snap, len(order)), want)
+
+
+# ---- volume plugins (round 5): claims through the native encoder -----------
+def _assert_same_bound(nodes, pods, prof, bound):
+    """_assert_same with running pods: the Python encoder's bound_pods and the
+    native snapshot's bindings (VolumeRestrictions counts their claims)."""
+    enc = E.Encoder(nodes, pods, prof, bound_pods=[pi for pi, _ in bound])
+    snap = S.Snapshot(prof, nodes, pods, bound)
+    snap.encode()
+    got, want = snap.arrays(), _py_arrays(enc)
+    for k, v in want.items():
+        if k == "log_table":
+            assert got[k].tobytes() == np.asarray(v, np.float64).tobytes(), k
+        else:
+            np.testing.assert_array_equal(got[k], np.asarray(v), err_msg=k)
+    assert got["pods"].tobytes() == enc.workload.pods.tobytes()
+    return snap, enc
+
+
+def _prefilter_outcomes_match(snap, enc, prof, n_pods):
+    """ksg_snapshot_prefilter / _prefilter_message against the Python
+    encoder's ordered PreFilter outcomes (rejection + message, node names)."""
+    for i in range(n_pods):
+        rec = enc.workload.pods[i]
+        rej = enc.prefilter_reject.get(i) if int(rec["flags"]) & E.POD_FLAG_PREFILTER_REJECT else None
+        names_of = enc.prefilter_results.get(i, {})
+        for pid in prof.prefilter_order():
+            code, names = snap.prefilter(i, pid, 0)
+            if rej is not None and rej[0] == pid and rej[1] is not None:
+                assert code == S.CODE_UNRESOLVABLE, (i, pid)
+                assert snap.prefilter_message(i, pid) == rej[1]
+                break
+            assert snap.prefilter_message(i, pid) == ""
+            skip = (int(rec["filter_skip"]) >> pid) & 1
+            assert code == (S.CODE_SKIP if skip else S.CODE_SUCCESS), (i, pid)
+            want = names_of.get(pid)
+            assert (names if names is not None else None) == (sorted(want) if want is not None else None), (i, pid)
+            if rej is not None and rej[0] == pid:
+                break
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_zoo_volumes_native(built, seed):
+    """Pods with claims (local, zonal, affinity-pinned, missing and unbound
+    PVs, WaitForFirstConsumer classes) through ksg_snapshot_add_pv / _pvc /
+    _storage_class and the pods' volume views: the same columns (the zone
+    label columns, allowedTopologies and zone value ids), records (filter
+    skips, PreFilter reject flag, node sets) and volume programs as
+    encoder.py, and the same PreFilter outcomes."""
+    nodes, pods, prof = zoo.zoo_volumes(seed)
+    snap, enc = _assert_same(nodes, pods, prof)
+    assert (enc.workload.pods["vol"] >= 0).sum() > 10
+    _prefilter_outcomes_match(snap, enc, prof, len(pods))
+
+
+def test_zoo_volumes_rwop_native(built):
+    nodes, pods, prof, run = zoo.zoo_volumes(1, bound=True)
+    snap, enc = _assert_same_bound(nodes, pods, prof, run)
+    assert any(enc.prog[int(r["vol"])] & 1 for r in enc.workload.pods if r["vol"] >= 0)   # a RWOP conflict
+    _prefilter_outcomes_match(snap, enc, prof, len(pods))
+
+
+def test_volume_status_messages_native(built):
+    """The volume plugins' Filter messages and codes from ksg_snapshot_status
+    equal framework.Decoder / status_code."""
+    nodes, pods, prof = zoo.zoo_volumes(2)
+    snap, enc = _assert_same(nodes, pods, prof)
+    dec = F.Decoder(enc)
+    for pl, reasons in ((P.VOLUME_RESTRICTIONS, (0,)), (P.VOLUME_BINDING, (1, 2, 3, 4, 5, 6, 7)),
+                        (P.VOLUME_ZONE, (0,))):
+        for r in reasons:
+            w = (pl + 1) | (r << 8)
+            code, msg = snap.status(0, w, 0)
+            assert msg == dec.message(w, 0)
+            assert code == F.status_code(w, enc, 0, 0)
+
+
+def test_volume_refusals_native(built):
+    """encoder.py's refusals hold through the C ABI (KSG_E_UNSUPPORTED at
+    encode): a ReadWriteOncePod claim shared by queued pods, a claim a free PV
+    could bind statically; ephemeral volumes at add_pod."""
+    nodes, pods, prof = zoo.zoo_volumes(0)
+    st = pods[0].storage
+    pods[3].volumes = [("v", "persistentVolumeClaim", "rwop-0")]
+    pods[4].volumes = [("v", "persistentVolumeClaim", "rwop-0")]
+    snap = S.Snapshot(prof, nodes, pods)
+    with pytest.raises(S.SnapshotError, match="ReadWriteOncePod"):
+        snap.encode()
+    pods[4].volumes = []
+    st.pvs["pv-free"] = m.PersistentVolume("pv-free", storage_class="any")
+    st.pvcs[("default", "free")] = m.PersistentVolumeClaim("free", "default", "", "any")
+    pods[5].volumes = [("v", "persistentVolumeClaim", "free")]
+    snap = S.Snapshot(prof, nodes, pods)
+    with pytest.raises(S.SnapshotError, match="statically"):
+        snap.encode()
+    pods[5].volumes = [("v", "ephemeral", "")]
+    with pytest.raises(S.SnapshotError, match="ephemeral"):
+        S.Snapshot(prof, nodes, pods)
+
+
+def test_export_case2_claim_native(built):
+    """The reference's export sample case 2 plus pods claiming pvc1 / a missing
+    claim (tests/test_volumes.py) through the native encoder."""
+    from test_volumes import export_case2_with_claim
+    I = pkg("ingest")
+    snap_doc = I.load_snapshot(export_case2_with_claim())
+    snap, enc = _assert_same(snap_doc.nodes, snap_doc.pods, snap_doc.profile)
+    _prefilter_outcomes_match(snap, enc, snap_doc.profile, len(snap_doc.pods))
