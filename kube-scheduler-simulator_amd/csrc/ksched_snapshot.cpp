@@ -399,9 +399,11 @@ Canon canon_selector(const Sel& ls, const StrMap* extra = nullptr) {
   return std::vector<CReq>(reqs.begin(), reqs.end());
 }
 
-bool selector_matches(const Canon& c, const StrMap& labels) {
-  if (!c) return false;
-  for (auto& r : *c) {
+bool reqs_match(const std::vector<CReq>& reqs, const StrMap& labels);
+bool selector_matches(const Canon& c, const StrMap& labels) { return c && reqs_match(*c, labels); }
+// a canonical selector's requirements (labels.Selector.Matches)
+bool reqs_match(const std::vector<CReq>& reqs, const StrMap& labels) {
+  for (auto& r : reqs) {
     const auto it = labels.find(std::get<0>(r));
     const bool has = it != labels.end();
     const auto& vals = std::get<2>(r);
@@ -559,6 +561,13 @@ struct ksg_snapshot {
   std::map<std::string, SClass> classes;
   std::map<std::pair<std::string, std::string>, std::set<int>> claim_users;   // full encode: (ns, claim) -> pods
   std::set<int> bound_set;          // full encode: pods with a binding (running or assumed)
+  // match_pod's inverted index of the universe (rebuilt at every full
+  // encode): selector / template ids by one (key, value) their match needs;
+  // the rest (no In requirement, or matching everything) are scanned
+  struct SelIndex {
+    std::map<std::pair<std::string, std::string>, std::vector<int>> kv[3];   // pts, ipa, templates
+    std::vector<int> scan[3];
+  } sel_index;
   bool vol_run = false;             // a volume plugin runs at PreFilter or Filter
   bool csi_limits = false;          // NodeVolumeLimits runs and a node publishes CSI attach limits
   // ksg_snapshot_statuses: a status key's (code, message) is kept across
@@ -1025,26 +1034,70 @@ void build_topology_universe(ksg_snapshot* s) {
   }
 }
 
+// match_pod's index: every selector (PodTopologySpread), conjunction
+// (InterPodAffinity: its first scope) and template of the universe under one
+// (key, value) an In requirement of its selector needs, else in the scan list;
+// labels.Nothing() matches no pod and is left out.
+void build_sel_index(ksg_snapshot* s) {
+  Encoded& e = s->e;
+  auto& ix = s->sel_index;
+  for (int k = 0; k < 3; k++) {
+    ix.kv[k].clear();
+    ix.scan[k].clear();
+  }
+  auto put = [&](int which, const std::vector<CReq>& reqs, int id) {
+    for (auto& r : reqs)
+      if (std::get<1>(r) == OP_IN && !std::get<2>(r).empty()) {
+        for (auto& v : std::get<2>(r)) ix.kv[which][{std::get<0>(r), v}].push_back(id);
+        return;
+      }
+    ix.scan[which].push_back(id);
+  };
+  for (size_t k = 0; k < e.pts_order.size(); k++) put(0, e.pts_order[k].first, (int)k);
+  for (size_t k = 0; k < e.ipa_order.size(); k++) {
+    const auto& conj = e.ipa_order[k];
+    if (conj.empty()) ix.scan[1].push_back((int)k);
+    else if (conj[0].canon) put(1, *conj[0].canon, (int)k);
+  }
+  for (size_t t = 0; t < e.tmpl_order.size(); t++) {
+    const Scope& sc = std::get<1>(e.tmpl_order[t]);
+    if (sc.canon) put(2, *sc.canon, (int)t);
+  }
+}
+
 // Selector / template membership of one pod against the current universe
-// (the incremental path: the full pass computes it with the pod index).
+// (the incremental path: the full pass computes it with the pod index): the
+// candidates under the pod's (key, value) labels plus the scan lists, each
+// checked in full, in id order.
 void match_pod(ksg_snapshot* s, int i) {
   Encoded& e = s->e;
   const Pod& q = s->pods[i];
+  const auto& ix = s->sel_index;
+  auto candidates = [&](int which) {
+    std::vector<int> c(ix.scan[which]);
+    for (auto& kv : q.labels) {
+      auto it = ix.kv[which].find({kv.first, kv.second});
+      if (it != ix.kv[which].end()) c.insert(c.end(), it->second.begin(), it->second.end());
+    }
+    std::sort(c.begin(), c.end());
+    c.erase(std::unique(c.begin(), c.end()), c.end());
+    return c;
+  };
   const int n_pts = (int)e.pts_order.size();
   std::vector<int> sels;
-  for (size_t k = 0; k < e.pts_order.size(); k++)
-    if (q.ns == e.pts_order[k].second && !q.terminating && selector_matches(Canon(e.pts_order[k].first), q.labels))
-      sels.push_back((int)k);
-  for (size_t k = 0; k < e.ipa_order.size(); k++) {
+  if (!q.terminating)
+    for (int k : candidates(0))
+      if (q.ns == e.pts_order[k].second && reqs_match(e.pts_order[k].first, q.labels)) sels.push_back(k);
+  for (int k : candidates(1)) {
     bool all = true;
     for (auto& sc : e.ipa_order[k]) all = all && sc.ns_match(q.ns) && selector_matches(sc.canon, q.labels);
-    if (all) sels.push_back(n_pts + (int)k);
+    if (all) sels.push_back(n_pts + k);
   }
   s->pod_selectors[i] = sels;
   std::array<std::vector<int>, 3> tm;
-  for (size_t t = 0; t < e.tmpl_order.size(); t++) {
+  for (int t : candidates(2)) {
     const Scope& sc = std::get<1>(e.tmpl_order[t]);
-    if (sc.ns_match(q.ns) && selector_matches(sc.canon, q.labels)) tm[std::get<0>(e.tmpl_order[t])].push_back((int)t);
+    if (sc.ns_match(q.ns) && selector_matches(sc.canon, q.labels)) tm[std::get<0>(e.tmpl_order[t])].push_back(t);
   }
   s->tmpl_match[i] = tm;
 }
@@ -1748,6 +1801,7 @@ void encode_all(ksg_snapshot* s) {
   build_images(s);
   build_ports(s);
   build_topology_universe(s);
+  build_sel_index(s);
   // node columns
   const size_t R = e.res_names.size();
   e.alloc.assign(R * N, 0);
