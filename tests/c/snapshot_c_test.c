@@ -407,6 +407,104 @@ static void check_kat(void) {
   ksg_snapshot_free(snap);
 }
 
+/* The volume plugins through the C ABI alone (ksg_snapshot_add_pv / _pvc /
+ * _storage_class): a local PV pinned to node-0001 (VolumeBinding's
+ * PreFilterResult), a missing claim (VolumeRestrictions' PreFilter
+ * rejection and its message), a zonal PV in z0 (VolumeZone at Filter), an
+ * unbound WaitForFirstConsumer claim whose class allows z1 only
+ * (VolumeBinding's BindConflict at Filter); decisions from the oracle on the
+ * native encoding, messages from ksg_snapshot_status. */
+static void check_volumes(void) {
+  scenario s = scenario_kat();   /* the in-tree default plugin set, volume plugins included */
+  s.n_nodes = 4;
+  s.nodes = A(4, sizeof *s.nodes);
+  for (int i = 0; i < 4; i++) {
+    ksg_node_view* n = &s.nodes[i];
+    n->name = S("node-%04d", i);
+    ksg_str_pair* l = A(2, sizeof *l);
+    l[0] = (ksg_str_pair){"kubernetes.io/hostname", n->name};
+    l[1] = (ksg_str_pair){"topology.kubernetes.io/zone", i < 2 ? "z0" : "z1"};
+    n->n_labels = 2; n->labels = l;
+    ksg_quantity* q = A(3, sizeof *q);
+    q[0] = (ksg_quantity){"cpu", 4000};
+    q[1] = (ksg_quantity){"memory", 32 * GI};
+    q[2] = (ksg_quantity){"pods", 110};
+    n->n_alloc = 3; n->allocatable = q;
+  }
+  ksg_snapshot* snap = build(&s, 0);
+  static ksg_str_pair done[1] = {{"pv.kubernetes.io/bind-completed", "yes"}};
+  static const char* rwo[1] = {"ReadWriteOnce"};
+  /* pv-local: required node affinity hostname In [node-0001] */
+  static const char* host1[1] = {"node-0001"};
+  ksg_node_selector_term_view term = {1, req_in("kubernetes.io/hostname", 1, host1), 0, NULL};
+  ksg_pv_view pv_local = {"pv-local", 0, NULL, "", "default", "pvc-local", "local", 1, 1, &term};
+  static ksg_str_pair zl[1] = {{"topology.kubernetes.io/zone", "z0"}};
+  ksg_pv_view pv_zonal = {"pv-zonal", 1, zl, "", "default", "pvc-zonal", "csi", 0, 0, NULL};
+  OK(ksg_snapshot_add_pv(snap, &pv_local));
+  OK(ksg_snapshot_add_pv(snap, &pv_zonal));
+  ksg_pvc_view c_local = {"default", "pvc-local", "pv-local", "", 1, rwo, 1, done, 0};
+  ksg_pvc_view c_zonal = {"default", "pvc-zonal", "pv-zonal", "", 1, rwo, 1, done, 0};
+  ksg_pvc_view c_wffc = {"default", "pvc-wffc", "", "wffc", 1, rwo, 0, NULL, 0};
+  OK(ksg_snapshot_add_pvc(snap, &c_local));
+  OK(ksg_snapshot_add_pvc(snap, &c_zonal));
+  OK(ksg_snapshot_add_pvc(snap, &c_wffc));
+  static const char* z1[1] = {"z1"};
+  ksg_topology_requirement_view treq = {"topology.kubernetes.io/zone", 1, z1};
+  ksg_topology_term_view tterm = {1, &treq};
+  ksg_storage_class_view sc = {"wffc", "csi.example.com", "WaitForFirstConsumer", 1, &tterm};
+  OK(ksg_snapshot_add_storage_class(snap, &sc));
+  static const char* claims[4] = {"pvc-local", "missing", "pvc-zonal", "pvc-wffc"};
+  ksg_pod_view pods[4];
+  for (int j = 0; j < 4; j++) {
+    pods[j] = s.pods[0];
+    pods[j].name = S("claims-%d", j);
+    ksg_volume_view* v = A(1, sizeof *v);
+    v->name = "data"; v->kind = "persistentVolumeClaim"; v->claim_name = claims[j];
+    pods[j].n_volumes = 1; pods[j].volumes = v;
+    OK(ksg_snapshot_add_pod(snap, &pods[j], NULL));
+  }
+  OK(ksg_snapshot_encode(snap));
+  s.n_pods = 0;
+  kso_ctx* o = oracle_of(snap, &s);
+  uint32_t fs[4][4];
+  ksg_result r[4];
+  for (int j = 0; j < 4; j++) {
+    int64_t raw[KSG_NPLUGINS * 4], norm[KSG_NPLUGINS * 4], tot[4];
+    ksg_capture cap = {fs[j], raw, norm, tot};
+    OK(kso_eval(o, j, &r[j], &cap));
+  }
+  int32_t code, has, n;
+  const char* names[4];
+  OK(ksg_snapshot_prefilter(snap, 0, KSG_PL_VOLUME_BINDING, r[0].status, &code, &has, names, 4, &n));
+  CHECK(code == KSG_CODE_SUCCESS && has == 1 && n == 1 && strcmp(names[0], "node-0001") == 0,
+        "volumes: VolumeBinding PreFilterResult code %d has %d n %d", code, has, n);
+  CHECK(r[0].n_feasible == 1 && r[0].selected == 1, "volumes: local PV pod feasible %d selected %d",
+        r[0].n_feasible, r[0].selected);
+  OK(ksg_snapshot_prefilter(snap, 1, KSG_PL_VOLUME_RESTRICTIONS, r[1].status, &code, &has, NULL, 0, &n));
+  CHECK(code == KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, "volumes: missing claim PreFilter code %d", code);
+  char msg[256];
+  int32_t len;
+  OK(ksg_snapshot_prefilter_message(snap, 1, KSG_PL_VOLUME_RESTRICTIONS, msg, sizeof msg, &len));
+  CHECK(strcmp(msg, "persistentvolumeclaim \"missing\" not found") == 0, "volumes: message '%s'", msg);
+  CHECK(r[1].n_feasible == 0 && fs[1][0] == KSG_FS_NOT_EVALUATED, "volumes: rejected pod evaluated a node");
+  /* pv-zonal in z0: nodes 2, 3 fail VolumeZone */
+  CHECK(r[2].n_feasible == 2 && fs[2][0] == 0 && (fs[2][2] & 0xff) == KSG_PL_VOLUME_ZONE + 1,
+        "volumes: zonal feasible %d word %#x", r[2].n_feasible, fs[2][2]);
+  OK(ksg_snapshot_status(snap, 2, fs[2][2], 2, &code, msg, sizeof msg, &len));
+  CHECK(code == KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE && strcmp(msg, "node(s) had no available volume zone") == 0,
+        "volumes: zone status %d '%s'", code, msg);
+  /* the class allows z1: nodes 0, 1 cannot provision */
+  CHECK(r[3].n_feasible == 2 && fs[3][3] == 0 && (fs[3][0] & 0xff) == KSG_PL_VOLUME_BINDING + 1,
+        "volumes: WaitForFirstConsumer feasible %d word %#x", r[3].n_feasible, fs[3][0]);
+  OK(ksg_snapshot_status(snap, 3, fs[3][0], 0, &code, msg, sizeof msg, &len));
+  CHECK(strcmp(msg, "node(s) didn't find available persistent volumes to bind") == 0, "volumes: bind status '%s'",
+        msg);
+  printf("ok volumes: VolumeBinding result {node-0001}, VolumeRestrictions rejection, VolumeZone and "
+         "BindConflict at Filter\n");
+  kso_close(o);
+  ksg_snapshot_free(snap);
+}
+
 /* Incremental encoding (pods added after the first encode) against one full
  * encode: identical pod records and program pool when appended. */
 static void check_incremental_bytes(const scenario* s) {
@@ -440,6 +538,7 @@ static void oracle_queue(kso_ctx* o, const scenario* s, int32_t* pl, ksg_result*
 
 static int run_cpu(void) {
   check_kat();
+  check_volumes();
   scenario sc[2] = {scenario_c2(96, 400, 24), scenario_c3(64, 300, 16, 8)};
   for (int k = 0; k < 2; k++) {
     const scenario* s = &sc[k];
