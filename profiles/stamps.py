@@ -12,7 +12,11 @@ E = importlib.import_module("kube-scheduler-simulator_amd.encoder")
 native = importlib.import_module("kube-scheduler-simulator_amd.native")
 
 n_pods = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
-nodes, pods, prof = G.config2(n_pods=n_pods)
+# argv[2] "default": the headline's default profile (generator.config1 at 5,000 nodes)
+if len(sys.argv) > 2 and sys.argv[2] == "default":
+    nodes, pods, prof = G.config1(n_nodes=5000, n_pods=n_pods)
+else:
+    nodes, pods, prof = G.config2(n_pods=n_pods)
 enc = E.Encoder(nodes, pods, prof)
 eng = native.Engine(lib_path=os.path.join(ROOT, "kube-scheduler-simulator_amd", "libksched_stamps.so"))
 eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
