@@ -17,12 +17,34 @@ nodes, pods, prof = G.config3(n_pods=n_pods)
 enc = E.Encoder(nodes, pods, prof)
 eng = native.Engine(lib_path=os.path.join(ROOT, "kube-scheduler-simulator_amd", "libksched_stamps.so"))
 eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
-eng.run_queue(0, n_pods, results=False)
-ms = eng.last_kernel_ms()
+if len(sys.argv) > 2 and sys.argv[2] == "eval":
+    # the per-cycle form: one ksg_eval (the topology kernel on one pod, phase 1
+    # included) and one ksg_commit per pod, after n_pods // 2 queued pods
+    warm = n_pods // 2
+    eng.run_queue(0, warm, results=False)
+    st0 = (C.c_ulonglong * 16)()
+    f0 = eng.lib.ksg_debug_stamps
+    f0.argtypes = [C.c_void_p, C.c_void_p]
+    assert f0(eng.ctx, st0) == 0
+    import time
+    t = time.perf_counter()
+    for j in range(warm, n_pods):
+        r = eng.eval(j)
+        if r.selected >= 0:
+            eng.commit(j, r.selected)
+    ms = (time.perf_counter() - t) * 1e3
+    n_pods = n_pods - warm
+else:
+    st0 = None
+    eng.run_queue(0, n_pods, results=False)
+    ms = eng.last_kernel_ms()
 st = (C.c_ulonglong * 16)()
 fn = eng.lib.ksg_debug_stamps
 fn.argtypes = [C.c_void_p, C.c_void_p]
 assert fn(eng.ctx, st) == 0
+if st0 is not None:   # the per-cycle calls only
+    for i in range(16):
+        st[i] -= st0[i]
 tot = sum(st)
 names = ["setup (stage pod, layout)", "phase 1: merge / publish", "barrier 1", "2a: merged counts to LDS",
          "2b: reset next set, IPA skips", "2c3: sweep A, IPA score", "2d: reductions, marks", "barrier 2",
