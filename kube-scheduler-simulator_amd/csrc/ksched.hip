@@ -147,6 +147,15 @@ struct ksg_ctx {
   bool coop_launch = false;
   int32_t* d_tables = nullptr;        // the maintained domain tables and their index (ksched_topo_tables.h)
   size_t tables_words = 0;
+  // The per-cycle tables (ksg_eval of topology pods): the whole selector
+  // universe's tables, built once, kept exact by ksg_commit's kernel,
+  // invalidated by anything else that moves the counts (queue runs, reset,
+  // reload, bulk bindings).  env KSG_PC_TABLES=0: the pre-pass every call.
+  int32_t* d_pct = nullptr;
+  size_t pct_words = 0;
+  TopoTables pct{};
+  bool pct_valid = false;
+  bool pc_tables = true;
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched, 3 int64 sweep state
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
@@ -362,6 +371,9 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_coop_srec = nullptr;
   ctx->d_tables = nullptr;
   ctx->tables_words = 0;
+  ctx->d_pct = nullptr;
+  ctx->pct_words = 0;
+  ctx->pct_valid = false;
   ctx->pc_node = -1;   // a deferred assume onto the freed state
   ctx->d_coop_notables = nullptr;
   ctx->coop_cfg_N = -1;
@@ -1419,7 +1431,11 @@ const void* coop_kernel(int kn, bool ll, int cap) {
 // parse_topo), laid out in one device block and rebuilt from cnt and the
 // labels by ksg_topo_tables_init.  Returns false (tables unused) when the
 // layout would not fit its limits.
-bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* out, int* rc) {
+// universe: every (selector, non-unique column) pair and every selector's
+// count-of-counts, no per-pod scope (the per-cycle tables: the topology
+// kernel computes each pod's scope itself, tables_fill), into ctx->d_pct.
+bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* out, int* rc,
+                       bool universe = false) {
   *rc = KSG_OK;
   const int S = ctx->c.S, L = ctx->c.L, N = ctx->c.N;
   if (S <= 0 || L <= 0 || (size_t)S * L > (1u << 24)) return false;
@@ -1452,6 +1468,17 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
     want_tot[sel] = 1;
   };
   const int32_t* P = ctx->h_prog.data();
+  if (universe) {
+    count = 0;
+    bool any_unique = false;
+    for (int col = 0; col < L; col++) any_unique = any_unique || ctx->h_col_unique[col];
+    for (int sel = 0; sel < S; sel++) {
+      for (int col = 0; col < L; col++)
+        if (!ctx->h_col_unique[col]) pair(sel, col);
+      if (any_unique) cc(sel);
+      want_tot[sel] = 1;
+    }
+  }
   for (int i = first; i < first + count; i++) {
     const ksg_pod& p = ctx->h_pods[i];
     if (p.pts >= 0) {
@@ -1509,19 +1536,21 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
                o_fo = (o_elig + ((size_t)count + 3) / 4 + 3) & ~(size_t)3,
                o_tasks = o_fo + (size_t)count * kTopoFill * 4,
                words = o_tasks + tasks.size() * (sizeof(TopoTableTask) / 4);
-  if (words > ctx->tables_words) {
-    if (ctx->d_tables) {
-      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_tables);
+  int32_t*& buf = universe ? ctx->d_pct : ctx->d_tables;
+  size_t& buf_words = universe ? ctx->pct_words : ctx->tables_words;
+  if (words > buf_words) {
+    if (buf) {
+      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)buf);
       if (it != ctx->allocs.end()) ctx->allocs.erase(it);
       if (hipStreamSynchronize(ctx->stream) != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: sync"); return false; }
-      (void)hipFree(ctx->d_tables);
-      ctx->d_tables = nullptr;
-      ctx->tables_words = 0;
+      (void)hipFree(buf);
+      buf = nullptr;
+      buf_words = 0;
     }
-    if ((*rc = dalloc(ctx, &ctx->d_tables, words))) return false;
-    ctx->tables_words = words;
+    if ((*rc = dalloc(ctx, &buf, words))) return false;
+    buf_words = words;
   }
-  int32_t* b = ctx->d_tables;
+  int32_t* b = buf;
   auto up = [&](size_t off, const void* src, size_t bytes) {
     return hipMemcpyAsync(b + off, src, bytes, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
   };
@@ -1554,10 +1583,12 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
   hipLaunchKernelGGL(ksg_topo_tables_init, dim3((unsigned)tasks.size()), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
                      t, reinterpret_cast<const TopoTableTask*>(b + o_tasks));
   if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: init launch"); return false; }
-  hipLaunchKernelGGL(ksg_topo_tables_elig, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, ctx->stream, ctx->c, t,
-                     ctx->d_pods, ctx->d_prog, count, reinterpret_cast<uint8_t*>(b + o_elig),
-                     reinterpret_cast<int4*>(b + o_fo));
-  if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: scope launch"); return false; }
+  if (count > 0) {
+    hipLaunchKernelGGL(ksg_topo_tables_elig, dim3((unsigned)((count + 63) / 64)), dim3(64), 0, ctx->stream, ctx->c, t,
+                       ctx->d_pods, ctx->d_prog, count, reinterpret_cast<uint8_t*>(b + o_elig),
+                       reinterpret_cast<int4*>(b + o_fo));
+    if (hipGetLastError() != hipSuccess) { *rc = fail(ctx, KSG_E_DEVICE, "tables: scope launch"); return false; }
+  }
   (void)N;
   *out = t;
   return true;
@@ -1638,6 +1669,7 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   // the maintained tables: placement runs (they are rebuilt per run from the
   // state; a single-pod evaluation runs phase 1 instead of paying the rebuild)
   if (ctx->coop_tables && do_commit && count > 1) {
+    ctx->pct_valid = false;   // the run moves the counts without the per-cycle tables
     TopoTables t{};
     if (build_topo_tables(ctx, first, count, &t, &rc)) {
       a.tt = t;
@@ -1645,6 +1677,27 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     } else if (rc) {
       return rc;
     }
+  } else if (ctx->coop_tables && ctx->pc_tables && !do_commit && count == 1 && cap && cap->mode == 2) {
+    // the per-cycle evaluation: the universe's tables, built once per
+    // encoding and kept exact by every ksg_commit / ksg_uncommit since
+    if (!ctx->pct_valid) {
+      TopoTables t{};
+      if (build_topo_tables(ctx, 0, 0, &t, &rc, true)) {
+        ctx->pct = t;
+        ctx->pct_valid = true;
+      } else if (rc) {
+        return rc;
+      } else {
+        ctx->pc_tables = false;   // the layout does not fit its limits: the pre-pass from now on
+      }
+    }
+    if (ctx->pct_valid) {
+      a.tt = ctx->pct;
+      a.use_tables = 1;
+      a.tables_inkernel = 1;
+    }
+  } else if (do_commit) {
+    ctx->pct_valid = false;
   }
   if (!a.use_tables) {   // the kernel reads tt.invalid and the index arrays at setup: a valid empty set
     if (!ctx->d_coop_notables) {
@@ -1866,6 +1919,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   HIPC(ctx, hipSetDevice(ctx->device));
   if ((rc = flush_stage(ctx))) return rc;
   if ((rc = flush_commit(ctx))) return rc;
+  if (do_commit) ctx->pct_valid = false;   // the queue's assumes bypass the per-cycle tables
   const size_t N = ctx->c.N;
   Tmp tmp;
   ksg_profile* d_prof = nullptr;
@@ -2685,7 +2739,7 @@ int flush_commit(ksg_ctx* ctx) {
   const int pod = ctx->pc_pod, node = ctx->pc_node;
   ctx->pc_node = -1;
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
-                     ctx->d_prog, pod, node, 1);
+                     ctx->d_prog, pod, node, 1, ctx->pct, ctx->pct_valid ? 1 : 0);
   HIPC(ctx, hipGetLastError());
   return KSG_OK;
 }
@@ -2919,6 +2973,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_COOP_LAUNCH")) ctx->coop_launch = atoi(f) != 0;
+  if (const char* f = getenv("KSG_PC_TABLES")) ctx->pc_tables = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SERVER")) ctx->srv_mode = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_ES")) ctx->cycle_es = atoi(f);
@@ -3091,6 +3146,7 @@ int ksg_load_workload(ksg_ctx* ctx, const ksg_workload* wl) {
     const int rc = flush_commit(ctx);
     if (rc) return rc;
   }
+  ctx->pct_valid = false;
   ctx->stage_pending = false;   // a staged append of the replaced workload
   ctx->h_pods.assign(wl->pods, wl->pods + wl->n_pods);
   std::vector<int32_t> prog(wl->prog, wl->prog + wl->prog_len);
@@ -3317,7 +3373,7 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
   }
   if ((rc = srv_stop(ctx))) return rc;
   hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
-                     ctx->d_prog, pod, node, sign);
+                     ctx->d_prog, pod, node, sign, ctx->pct, ctx->pct_valid ? 1 : 0);
   // stream-ordered: the next evaluation on ctx->stream sees the update, and
   // every read-back synchronises the stream; no host wait per assume
   HIPC(ctx, hipGetLastError());
@@ -3335,6 +3391,7 @@ int ksg_commit_batch(ksg_ctx* ctx, const int32_t* pods, const int32_t* nodes, in
     if (pods[i] < 0 || pods[i] >= ctx->n_pods || nodes[i] < 0 || nodes[i] >= ctx->c.N)
       return fail(ctx, KSG_E_INVALID, "commit batch: pod or node out of range");
   if (n == 0) return KSG_OK;
+  ctx->pct_valid = false;   // the bulk bindings move the counts without the per-cycle tables
   HIPC(ctx, hipSetDevice(ctx->device));
   if ((rc = flush_stage(ctx))) return rc;
   if ((rc = flush_commit(ctx))) return rc;
@@ -3441,6 +3498,7 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
   if ((rc = flush_commit(ctx))) return rc;
   for (int r = 0; r < n_replicas; r++)
     if ((rc = check_supported(ctx, profiles[r], first, count))) return rc;
+  ctx->pct_valid = false;   // (replica state is a copy; conservatively rebuilt)
   HIPC(ctx, hipSetDevice(ctx->device));
   const DevCluster& c = ctx->c;
   const size_t N = c.N, R = c.R, S = std::max(c.S, 1), NT = std::max(c.n_tmpl, 1);
@@ -3601,6 +3659,7 @@ int ksg_reset_state(ksg_ctx* ctx) {
   if (!ctx->have_nodes) return fail(ctx, KSG_E_STATE, "no nodes loaded");
   HIPC(ctx, hipSetDevice(ctx->device));
   ctx->pc_node = -1;   // a deferred assume is reset with the rest
+  ctx->pct_valid = false;
   const size_t N = ctx->c.N, R = ctx->c.R;
   HIPC(ctx, hipMemcpyAsync(ctx->st.requested, ctx->d_req0, 8 * R * N, hipMemcpyDeviceToDevice, ctx->stream));
   HIPC(ctx, hipMemcpyAsync(ctx->st.nonzero, ctx->d_nz0, 16 * N, hipMemcpyDeviceToDevice, ctx->stream));

@@ -2301,12 +2301,36 @@ __global__ __launch_bounds__(256) void ksg_replica_sums(const int64_t* requested
 #endif  // KSG_PART
 
 #ifndef KSG_PART
+// tables (the per-cycle domain tables, ksg_eval of topology pods): the
+// assume's effect on them as lag_apply adds it, for sign +1 (assume) and -1
+// (a victim's deletion), from the selectors' counts before the update.
 __global__ void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods, const int32_t* prog, int pod,
-                                  int node, int sign) {
+                                  int node, int sign, TopoTables t, int tables) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const ksg_pod& p = pods[pod];
-  commit_node(c, st.requested, st.nonzero, st.pod_count, st.cnt, st.tab, st.tmpl_total, p,
-              p.commit >= 0 ? prog + p.commit : nullptr, node, sign, st.ports,
+  const int32_t* cw = p.commit >= 0 ? prog + p.commit : nullptr;
+  const int N = c.N;
+  const int n_sel = tables && cw ? cw[0] : 0;
+  for (int i = 0; i < n_sel; i++) {
+    const int sel = cw[1 + i];
+    const int old = st.cnt[(size_t)sel * N + node];
+    for (int k = t.sp_off[sel]; k < t.sp_off[sel + 1]; k++) {
+      const uint32_t v = c.label_val[(size_t)t.sp[2 * k] * N + node];
+      if (v) t.dom[t.sp[2 * k + 1] + v] += sign;
+    }
+    t.tot[sel] += sign;
+    const int co = t.cc_off[sel];
+    if (co >= 0) {
+      const int k = old + sign;   // the node's count after the update
+      if (old >= t.Kc - 1 || k < 0 || k >= t.Kc - 1) {
+        *t.invalid = 1u;
+      } else {
+        t.cc[co + old] -= 1;
+        t.cc[co + k] += 1;
+      }
+    }
+  }
+  commit_node(c, st.requested, st.nonzero, st.pod_count, st.cnt, st.tab, st.tmpl_total, p, cw, node, sign, st.ports,
               p.ports >= 0 ? prog + p.ports : nullptr);
 }
 #endif  // KSG_PART

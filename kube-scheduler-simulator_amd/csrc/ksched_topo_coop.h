@@ -130,6 +130,8 @@ struct CoopArgs {
   // the maintained domain tables (ksched_topo_tables.h)
   TopoTables tt;
   int32_t use_tables;          // 1: pods within their scope skip phase 1 and barrier 1
+  int32_t tables_inkernel;     // 1 (the per-cycle tables): elig and the fill tasks of each pod computed at
+                               // its setup (tables_fill) instead of read from tt.elig / tt.fo
   unsigned gen;                // barrier flag generation: flags are (gen << 16) + epoch, monotonic across
                                // launches, so nothing is reset per launch
   int32_t fused_static;        // 1 (one pod): every lane computes its node's static record itself
@@ -415,7 +417,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.profile)[i_];
   for (int i = tid; i < a.count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
-  for (int i = tid; i < a.count; i += BLOCK) s_elig[i] = a.use_tables ? tt.elig[a.first - tt.first + i] : 0;
+  if (!a.tables_inkernel)
+    for (int i = tid; i < a.count; i += BLOCK) s_elig[i] = a.use_tables ? tt.elig[a.first - tt.first + i] : 0;
   const bool lab_lds = LL || (KN == 1 && cg.L <= kCoopLabCols);
   const bool col_lds = LL || cg.L <= kCoopLabCols;
   const bool tmpl_lds = LL || cg.n_tmpl <= kCoopTmpl;
@@ -575,6 +578,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       // start), the tables exact (no count-of-counts overflow in the previous
       // pod's lag_apply: s_inv) and the histograms within their limits.
       const TopoProg& g0 = s_g;
+      if (a.tables_inkernel)   // the per-cycle tables: this pod's scope and fill tasks here
+        s_elig[kq] = s_tables_ok && tables_fill(a.c, tt, p, a.prog, s_fo) ? 1 : 0;
       const bool e = s_tables_ok != 0 && s_t.ok && s_elig[kq] && !s_inv;
       const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
       s_skip = !s_prev_imm && (!has_pre || e);
@@ -605,7 +610,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const bool tab_read = s_skip && s_tables_ok && ok;
     if (tab_read) {
       const TopoProg& g1 = s_g;
-      if (tid < kTopoFill) s_fo[tid] = tt.fo[(size_t)(a.first - tt.first + kq) * kTopoFill + tid];
+      if (tid < kTopoFill && !a.tables_inkernel) s_fo[tid] = tt.fo[(size_t)(a.first - tt.first + kq) * kTopoFill + tid];
       if (g1.ipa && tid >= 64 && tid < 64 + 1 + g1.n_pref) {
         const int sel = tid == 64 ? g1.sel_all : g1.pref[3 * (tid - 65) + 1];
         s_totv[tid - 64] = sel >= 0 ? (long long)gld(tt.tot + sel) : 0;

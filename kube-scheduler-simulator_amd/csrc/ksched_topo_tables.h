@@ -96,21 +96,13 @@ __device__ __forceinline__ bool tables_scope(const DevCluster& c, const TopoTabl
 
 constexpr int kTopoFill = 24;   // fill tasks per pod: kMaxHard + kMaxSoft + kMaxAff + kMaxAnti + kMaxPref
 
-// One lane per pod of the run: tables_scope into elig (after ksg_topo_tables_init)
-// and the pod's fill tasks: every non-unique slot's table offsets in the order
-// the topology kernel lays its histograms out (hard, soft without a hostname
-// key, affinity, anti-affinity, preferred), so the kernel's fill needs no
-// dependent index load.
-#ifndef KSG_PART
-__global__ __launch_bounds__(64) void ksg_topo_tables_elig(DevCluster c, TopoTables t, const ksg_pod* pods,
-                                                           const int32_t* prog, int count, uint8_t* elig,
-                                                           int4* fo) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= count) return;
-  const ksg_pod& p = pods[t.first + i];
+// tables_scope of pod p and its fill tasks: every non-unique slot's table
+// offsets in the order the topology kernel lays its histograms out (hard,
+// soft without a hostname key, affinity, anti-affinity, preferred), so the
+// kernel's fill needs no dependent index load.  out: kTopoFill entries.
+__device__ __forceinline__ bool tables_fill(const DevCluster& c, const TopoTables& t, const ksg_pod& p,
+                                            const int32_t* prog, int4* out) {
   const bool e = tables_scope(c, t, p, prog);
-  elig[i] = e ? 1 : 0;
-  int4* out = fo + (size_t)i * kTopoFill;
   int k = 0;
   auto task = [&](int sel, int col, bool pres) {
     if (k >= kTopoFill || col < 0 || col >= t.L || c.col_unique[col]) return;
@@ -138,6 +130,17 @@ __global__ __launch_bounds__(64) void ksg_topo_tables_elig(DevCluster c, TopoTab
     for (int j = 0; j < npref && j < kMaxPref; j++) task(w[3 * j + 1], w[3 * j], true);
   }
   for (; k < kTopoFill; k++) out[k] = make_int4(-1, -1, -1, -1);
+  return e;
+}
+
+// One lane per pod of the run: tables_fill into elig and fo (after ksg_topo_tables_init).
+#ifndef KSG_PART
+__global__ __launch_bounds__(64) void ksg_topo_tables_elig(DevCluster c, TopoTables t, const ksg_pod* pods,
+                                                           const int32_t* prog, int count, uint8_t* elig,
+                                                           int4* fo) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= count) return;
+  elig[i] = tables_fill(c, t, pods[t.first + i], prog, fo + (size_t)i * kTopoFill) ? 1 : 0;
 }
 #endif  // KSG_PART
 

@@ -350,3 +350,47 @@ def test_commit_batch_equals_sequential_commits(built):
         assert (ra.selected, ra.n_feasible, ra.status) == (rb.selected, rb.n_feasible, rb.status), i
         np.testing.assert_array_equal(ca.fstatus, cb.fstatus)
         np.testing.assert_array_equal(ca.total, cb.total)
+
+
+def test_topology_cycles_with_tables_across_invalidations(gpu, oracle):
+    """The per-cycle topology tables (built once, kept exact by ksg_commit /
+    ksg_uncommit, rebuilt after anything else moved the counts): evaluate +
+    assume, uncommit a few assumes, a queue run, a reset, more cycles; every
+    cycle equal to the oracle's, the node state too."""
+    nodes, pods, prof = G.config3(n_nodes=400, n_pods=160, apps=10, zones=4)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    oracle.load(enc, pf)
+    N, R = len(nodes), len(enc.cluster.res_names)
+
+    def cycles(lo, hi, placed):
+        for i in range(lo, hi):
+            cg, co = native.CaptureBuffers(N, 1), native.CaptureBuffers(N, 1)
+            rg, ro = gpu.eval(i, cg), oracle.eval(i, co)
+            assert gpu.last_run_info()[0] == 6
+            assert (rg.selected, rg.n_feasible, rg.status) == (ro.selected, ro.n_feasible, ro.status), i
+            np.testing.assert_array_equal(cg.fstatus, co.fstatus, err_msg=f"pod {i}")
+            np.testing.assert_array_equal(cg.total, co.total, err_msg=f"pod {i}")
+            if rg.selected >= 0:
+                gpu.commit(i, rg.selected)
+                oracle.commit(i, ro.selected)
+                placed.append((i, rg.selected))
+
+    placed = []
+    cycles(0, 40, placed)
+    for i, n in placed[::3][:6]:   # victims' deletions (ksg_uncommit: the tables follow)
+        gpu.uncommit(i, n)
+        oracle.uncommit(i, n)
+    cycles(40, 70, placed)
+    pl_g, _ = gpu.run_queue(70, 30)   # a queue run moves the counts: the tables are rebuilt
+    pl_o, _ = oracle.run_queue(70, 30)
+    np.testing.assert_array_equal(pl_g, pl_o)
+    cycles(100, 130, placed)
+    for a, b in zip(gpu.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(a, b)
+    gpu.reset_state()
+    oracle.reset_state()
+    cycles(130, 160, [])
+    for a, b in zip(gpu.read_state(R), oracle.read_state(R)):
+        np.testing.assert_array_equal(a, b)
