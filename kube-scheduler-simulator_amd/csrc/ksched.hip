@@ -113,7 +113,7 @@ struct ksg_ctx {
   ksg_profile* d_preprof = nullptr;
   // chip-wide topology path buffers (lazily allocated)
   CoopAcc* d_coop_acc = nullptr;
-  unsigned* d_coop_flags = nullptr;   // [4] timeout
+  unsigned* d_coop_flags = nullptr;   // [4] timeout, [6] the one-pod completion counter
   unsigned* d_coop_wgflags = nullptr; // [256][32] per-workgroup barrier flags
   int coop_pmode = 0;                 // env KSG_COOP_PMODE: 0 merge with atomics (33.3 k vs 32.1 k pods/s on
                                       // config 3), 1 every workgroup folds every partial slot
@@ -156,6 +156,9 @@ struct ksg_ctx {
   TopoTables pct{};
   bool pct_valid = false;
   bool pc_tables = true;
+  bool cycle_last = true;             // the one-pod topology evaluation completes on its last arrival
+  bool commit_args = true;            // ksg_commit's kernel takes the pod's commit program by value
+  bool topo_stage = true;             // ... and reads a staged append in place (KSG_TOPO_STAGE=0: copies first)
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched, 3 int64 sweep state
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
@@ -1409,6 +1412,10 @@ struct CoopCap {
   unsigned* h_flag = nullptr;
   unsigned* h_ovf = nullptr;
   unsigned seq = 0;
+  // mode 2, the pod's append still staged: read from the staging buffer (its
+  // device address) and copied to the device pool by workgroup 0
+  const char* stage = nullptr;
+  int64_t stage_base = 0, stage_len = 0;
 };
 
 // ksg_topo_coop<KN, LL, CAP>: capture instances exist for KN <= 4 (up to
@@ -1626,12 +1633,13 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     ctx->coop_G = G;
     ctx->coop_ll = ll;
     ctx->coop_cfg_N = N;
+    ctx->coop_dirty = true;   // (the one-pod completion counter counts arrivals modulo G)
   }
   const int kn = ctx->coop_kn, G = ctx->coop_G;
   const bool ll = ctx->coop_ll;
   if (!ctx->d_coop_acc) {
     if ((rc = dalloc(ctx, &ctx->d_coop_acc, 2))) return rc;
-    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [4] timeout
+    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [4] timeout, [6] one-pod completion counter
     if ((rc = dalloc(ctx, &ctx->d_coop_wgflags, (size_t)256 * 32))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_parts, 256))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_phist, (size_t)256 * kCoopPHist))) return rc;
@@ -1665,6 +1673,8 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   a.bar = ctx->d_coop_wgflags;
   a.pmode = ctx->coop_pmode;
   a.timeout = ctx->d_coop_flags + 4;
+  a.arrive = ctx->d_coop_flags + 6;
+  a.last_arrive = ctx->cycle_last ? 1 : 0;
   a.commit = do_commit;
   // the maintained tables: placement runs (they are rebuilt per run from the
   // state; a single-pod evaluation runs phase 1 instead of paying the rebuild)
@@ -1725,6 +1735,15 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     a.h_flag = cap->h_flag;
     a.h_ovf = cap->h_ovf;
     a.seq = cap->seq;
+    if (cap->stage) {   // pods + first and prog + blob address the staged record and programs
+      const int32_t* sprog = reinterpret_cast<const int32_t*>(cap->stage + sizeof(ksg_pod));
+      a.pods = reinterpret_cast<const ksg_pod*>(cap->stage) - first;
+      a.prog = sprog - cap->stage_base;
+      a.wpods = ctx->d_pods + first;
+      a.wprog = ctx->d_prog + cap->stage_base;
+      a.sprog = sprog;
+      a.slen = cap->stage_len;
+    }
   }
   // one pod evaluated (the per-cycle path): the static records in place, a
   // plain launch (every workgroup one per CU, the barrier's poll is bounded;
@@ -2540,7 +2559,15 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
   const size_t h_need = o_raw + 8 * N * (n_rows + 1 + std::max(n_normrows, 1)) + 64;
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
-  if ((rc = flush_stage(ctx))) return rc;   // the topology kernel reads the pod from the device pool
+  // the pod's append still staged: the kernel reads it from the staging
+  // buffer and copies it to the device pool (no copy launches in front of it)
+  const ksg_pod& hp = ctx->h_pods[pod];
+  const bool staged = ctx->stage_pending && ctx->stage_n == 1 && ctx->stage_first == pod && ctx->d_stage &&
+                      hp.blob >= ctx->stage_base && (int64_t)hp.blob + hp.blob_len <= ctx->stage_base + ctx->stage_len &&
+                      (hp.node_set < 0 || (hp.node_set >= ctx->stage_base &&
+                                           (int64_t)hp.node_set + ((int64_t)N + 31) / 32 <= ctx->stage_base + ctx->stage_len)) &&
+                      ctx->topo_stage;
+  if (!staged && (rc = flush_stage(ctx))) return rc;
   if ((rc = flush_commit(ctx))) return rc;
   if (!ctx->d_ev_prof && (rc = dalloc(ctx, &ctx->d_ev_prof, 1))) return rc;
   if (!ctx->d_ev_pl && (rc = dalloc(ctx, &ctx->d_ev_pl, 4))) return rc;
@@ -2581,10 +2608,16 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
   cc.h_ovf = reinterpret_cast<unsigned*>(db + 24);
   cc.h_flag = reinterpret_cast<unsigned*>(db + 28);
   cc.seq = seq;
+  if (staged) {
+    cc.stage = ctx->d_stage;
+    cc.stage_base = ctx->stage_base;
+    cc.stage_len = ctx->stage_len;
+  }
   if ((rc = run_topo_coop(ctx, pod, 1, ctx->d_ev_pl, nullptr, ctx->d_ev_prof, 0, &cc, false))) {
     ctx->coop_dirty = true;
     return rc;
   }
+  if (staged) ctx->stage_pending = false;   // the kernel's workgroup 0 writes it to the device pool
   for (unsigned spins = 0; *flag != seq; spins++) {
     __builtin_ia32_pause();
     if ((spins & 1023) == 1023) {
@@ -2717,6 +2750,41 @@ int32_t na_pref_weight_sum(const std::vector<int32_t>& prog, const ksg_pod& p);
 // Issue a pending staged append (append_internal) as two stream-ordered
 // copies.  Every entry point that launches kernels reading d_pods / d_prog
 // calls this first, except the per-cycle evaluation of the staged pod.
+// One assume (sign 1) or its removal (-1) on the stream: the record and the
+// commit program by value when they fit CommitArgs, else read by the kernel.
+int launch_commit(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
+  const ksg_pod& p = ctx->h_pods[pod];
+  CommitArgs k{};
+  k.node = node;
+  k.sign = sign;
+  for (int r = 0; r < KSG_MAX_RES; r++) k.req[r] = p.req[r];
+  k.nz_cpu = p.nz_cpu;
+  k.nz_mem = p.nz_mem;
+  k.ports = p.ports >= 0 ? ctx->d_prog + p.ports : nullptr;
+  bool inl = ctx->commit_args;
+  if (p.commit >= 0) {
+    const int32_t* w = ctx->h_prog.data() + p.commit;
+    k.ns = w[0];
+    k.nt = w[1 + k.ns];
+    inl = inl && k.ns <= kCommitSel && k.nt <= kCommitTmpl;
+    if (inl) {
+      for (int i = 0; i < k.ns; i++) k.sel[i] = w[1 + i];
+      for (int i = 0; i < k.nt; i++) {
+        k.tm[i] = w[2 + k.ns + 2 * i];
+        k.tw[i] = w[3 + k.ns + 2 * i];
+      }
+    }
+  }
+  if (inl)
+    hipLaunchKernelGGL(ksg_commit_args_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, k, ctx->pct,
+                       ctx->pct_valid ? 1 : 0);
+  else
+    hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
+                       ctx->d_prog, pod, node, sign, ctx->pct, ctx->pct_valid ? 1 : 0);
+  HIPC(ctx, hipGetLastError());
+  return KSG_OK;
+}
+
 int flush_stage(ksg_ctx* ctx) {
   if (!ctx->stage_pending) return KSG_OK;
   if (int rc = srv_stop(ctx)) return rc;
@@ -2738,10 +2806,7 @@ int flush_commit(ksg_ctx* ctx) {
   if (int rc = srv_stop(ctx)) return rc;
   const int pod = ctx->pc_pod, node = ctx->pc_node;
   ctx->pc_node = -1;
-  hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
-                     ctx->d_prog, pod, node, 1, ctx->pct, ctx->pct_valid ? 1 : 0);
-  HIPC(ctx, hipGetLastError());
-  return KSG_OK;
+  return launch_commit(ctx, pod, node, 1);
 }
 
 // The pod's volume program (encoder.py Encoder._volume_plan grammar) lies
@@ -2974,6 +3039,9 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_COOP_LAUNCH")) ctx->coop_launch = atoi(f) != 0;
   if (const char* f = getenv("KSG_PC_TABLES")) ctx->pc_tables = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_LAST")) ctx->cycle_last = atoi(f) != 0;
+  if (const char* f = getenv("KSG_TOPO_STAGE")) ctx->topo_stage = atoi(f) != 0;
+  if (const char* f = getenv("KSG_COMMIT_ARGS")) ctx->commit_args = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SERVER")) ctx->srv_mode = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_ES")) ctx->cycle_es = atoi(f);
@@ -3372,8 +3440,7 @@ static int commit_signed(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
     return KSG_OK;
   }
   if ((rc = srv_stop(ctx))) return rc;
-  hipLaunchKernelGGL(ksg_commit_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->c, ctx->st, ctx->d_pods,
-                     ctx->d_prog, pod, node, sign, ctx->pct, ctx->pct_valid ? 1 : 0);
+  if ((rc = launch_commit(ctx, pod, node, sign))) return rc;
   // stream-ordered: the next evaluation on ctx->stream sees the update, and
   // every read-back synchronises the stream; no host wait per assume
   HIPC(ctx, hipGetLastError());

@@ -2304,34 +2304,106 @@ __global__ __launch_bounds__(256) void ksg_replica_sums(const int64_t* requested
 // tables (the per-cycle domain tables, ksg_eval of topology pods): the
 // assume's effect on them as lag_apply adds it, for sign +1 (assume) and -1
 // (a victim's deletion), from the selectors' counts before the update.
-__global__ void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods, const int32_t* prog, int pod,
-                                  int node, int sign, TopoTables t, int tables) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// ksg_commit_kernel's assume with the pod's record and commit program passed
+// by value from the host copies (ksg_commit / ksg_uncommit when they fit):
+// no dependent loads of the record and program in front of the updates.
+constexpr int kCommitSel = 48, kCommitTmpl = 24;
+struct CommitArgs {
+  int32_t node, sign, ns, nt;
+  int64_t req[KSG_MAX_RES];
+  int64_t nz_cpu, nz_mem;
+  const int32_t* ports;        // the pod's ports program (device pool), or null
+  int32_t sel[kCommitSel];
+  int32_t tm[kCommitTmpl], tw[kCommitTmpl];
+};
+__global__ __launch_bounds__(64) void ksg_commit_args_kernel(DevCluster c, DevState st, CommitArgs a, TopoTables t,
+                                                             int tables) {
+  const int lane = threadIdx.x, N = c.N, node = a.node, sign = a.sign;
+  if (lane == 0 && a.ports && st.ports) ports_commit(st.ports, N, node, a.ports, sign);
+  if (lane < c.R) st.requested[(size_t)lane * N + node] += sign * a.req[lane];
+  if (lane == KSG_MAX_RES) st.nonzero[node] += sign * a.nz_cpu;
+  if (lane == KSG_MAX_RES + 1) st.nonzero[(size_t)N + node] += sign * a.nz_mem;
+  if (lane == KSG_MAX_RES + 2) st.pod_count[node] += sign;
+  if (lane < a.ns) {
+    const int sel = a.sel[lane];
+    const int old = atomicAdd(st.cnt + (size_t)sel * N + node, sign);
+    if (tables) {
+      for (int k = t.sp_off[sel]; k < t.sp_off[sel + 1]; k++) {
+        const uint32_t v = c.label_val[(size_t)t.sp[2 * k] * N + node];
+        if (v) atomicAdd(t.dom + t.sp[2 * k + 1] + v, sign);
+      }
+      atomicAdd(t.tot + sel, sign);
+      const int co = t.cc_off[sel];
+      if (co >= 0) {
+        const int k = old + sign;
+        if (old >= t.Kc - 1 || k < 0 || k >= t.Kc - 1) {
+          *t.invalid = 1u;
+        } else {
+          atomicSub(t.cc + co + old, 1);
+          atomicAdd(t.cc + co + k, 1);
+        }
+      }
+    }
+  }
+  if (lane < a.nt) {
+    const int tm = a.tm[lane];
+    const uint32_t val = c.label_val[(size_t)c.tmpl_col[tm] * N + node];
+    if (val) {
+      atomicAdd(st.tab + c.tmpl_off[tm] + val, sign * (c.tmpl_kind[tm] == KSG_TMPL_PREF ? a.tw[lane] : 1));
+      atomicAdd(st.tmpl_total + tm, sign);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void ksg_commit_kernel(DevCluster c, DevState st, const ksg_pod* pods,
+                                                        const int32_t* prog, int pod, int node, int sign,
+                                                        TopoTables t, int tables) {
+  // commit_node's updates spread over the wave: the node's columns over lanes
+  // 0 .. R + 2, one lane per matched selector (its count and, with the
+  // tables, its domain / total / count-of-counts entries), one per template;
+  // atomics, so a program naming an entry twice adds twice as the serial
+  // form does.  (Round 5: one lane walked it all, 4-7 us of dependent loads.)
+  const int lane = threadIdx.x;
+  if (blockIdx.x != 0) return;
   const ksg_pod& p = pods[pod];
-  const int32_t* cw = p.commit >= 0 ? prog + p.commit : nullptr;
   const int N = c.N;
-  const int n_sel = tables && cw ? cw[0] : 0;
-  for (int i = 0; i < n_sel; i++) {
+  if (lane == 0 && p.ports >= 0 && st.ports) ports_commit(st.ports, N, node, prog + p.ports, sign);
+  if (lane < c.R) st.requested[(size_t)lane * N + node] += sign * p.req[lane];
+  if (lane == KSG_MAX_RES) st.nonzero[node] += sign * p.nz_cpu;
+  if (lane == KSG_MAX_RES + 1) st.nonzero[(size_t)N + node] += sign * p.nz_mem;
+  if (lane == KSG_MAX_RES + 2) st.pod_count[node] += sign;
+  if (p.commit < 0) return;
+  const int32_t* cw = prog + p.commit;
+  const int ns = cw[0];
+  for (int i = lane; i < ns; i += 64) {
     const int sel = cw[1 + i];
-    const int old = st.cnt[(size_t)sel * N + node];
+    const int old = atomicAdd(st.cnt + (size_t)sel * N + node, sign);
+    if (!tables) continue;
     for (int k = t.sp_off[sel]; k < t.sp_off[sel + 1]; k++) {
       const uint32_t v = c.label_val[(size_t)t.sp[2 * k] * N + node];
-      if (v) t.dom[t.sp[2 * k + 1] + v] += sign;
+      if (v) atomicAdd(t.dom + t.sp[2 * k + 1] + v, sign);
     }
-    t.tot[sel] += sign;
+    atomicAdd(t.tot + sel, sign);
     const int co = t.cc_off[sel];
     if (co >= 0) {
       const int k = old + sign;   // the node's count after the update
       if (old >= t.Kc - 1 || k < 0 || k >= t.Kc - 1) {
         *t.invalid = 1u;
       } else {
-        t.cc[co + old] -= 1;
-        t.cc[co + k] += 1;
+        atomicSub(t.cc + co + old, 1);
+        atomicAdd(t.cc + co + k, 1);
       }
     }
   }
-  commit_node(c, st.requested, st.nonzero, st.pod_count, st.cnt, st.tab, st.tmpl_total, p, cw, node, sign, st.ports,
-              p.ports >= 0 ? prog + p.ports : nullptr);
+  const int32_t* w = cw + 1 + ns;
+  const int nt = w[0];
+  for (int i = lane; i < nt; i += 64) {
+    const int tm = w[1 + 2 * i];
+    const uint32_t val = c.label_val[(size_t)c.tmpl_col[tm] * N + node];
+    if (!val) continue;
+    atomicAdd(st.tab + c.tmpl_off[tm] + val, sign * (c.tmpl_kind[tm] == KSG_TMPL_PREF ? w[2 + 2 * i] : 1));
+    atomicAdd(st.tmpl_total + tm, sign);
+  }
 }
 #endif  // KSG_PART
 

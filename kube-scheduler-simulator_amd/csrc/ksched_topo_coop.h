@@ -139,6 +139,15 @@ struct CoopArgs {
   int32_t cap_es;              // CAP == 2: bytes per row value (2, 4, 8); a value that does not fit
                                // sets *h_ovf and the host evaluates again wider
   unsigned* h_ovf;
+  int32_t last_arrive;         // CAP == 2: 1 (default) the last arrival completes the call, 0 barrier 3 and
+                               // phase 4 (KSG_CYCLE_LAST=0, measurement knob)
+  ksg_pod* wpods;              // CAP == 2, a staged append read in place (pods / prog point into the
+                               // staging buffer): workgroup 0 copies it here (pod `first`) ...
+  int32_t* wprog;              // ... and its programs here; null: none
+  const int32_t* sprog;
+  int64_t slen;
+  unsigned* arrive;            // CAP == 2: the completion counter (never reset between launches: the last
+                               // of each launch's G arrivals stores the result; zeroed with the flags)
 };
 
 // Hand-offs between the G workgroups without cache maintenance (MI355X guide,
@@ -390,7 +399,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ int s_lag_tab;      // 1: s_lag's template-table entries are pending (readers add them)
   __shared__ int s_prev_imm;     // the previous pod wrote its template tables at once: barrier 1 orders them
   __shared__ int s_tables_ok;    // the tables are exact for this launch
-  __shared__ int s_skip;         // this pod: no phase 1, no barrier 1 (tables, or nothing to count)
+  __shared__ int s_last;         // CAP == 2: this workgroup arrived last (stores the result)
   __shared__ int s_lsel[kLagSel];   // this pod's matched selectors (commit program) ...
   __shared__ int s_nlsel;           // ... and their number (may exceed kLagSel)
   __shared__ int s_wmin;            // this workgroup's lowest feasible node (phase 2)
@@ -419,6 +428,11 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
   if (!a.tables_inkernel)
     for (int i = tid; i < a.count; i += BLOCK) s_elig[i] = a.use_tables ? tt.elig[a.first - tt.first + i] : 0;
+  if (CAP == 2 && a.wpods && wg == 0) {   // the staged append to the device pool (read by later launches)
+    for (int i = tid; i < (int)(sizeof(ksg_pod) / 4); i += BLOCK)
+      reinterpret_cast<int32_t*>(a.wpods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
+    for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
+  }
   const bool lab_lds = LL || (KN == 1 && cg.L <= kCoopLabCols);
   const bool col_lds = LL || cg.L <= kCoopLabCols;
   const bool tmpl_lds = LL || cg.n_tmpl <= kCoopTmpl;
@@ -577,13 +591,11 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       // Tables scope (tables_scope, one flag per pod computed at the run's
       // start), the tables exact (no count-of-counts overflow in the previous
       // pod's lag_apply: s_inv) and the histograms within their limits.
-      const TopoProg& g0 = s_g;
-      if (a.tables_inkernel)   // the per-cycle tables: this pod's scope and fill tasks here
-        s_elig[kq] = s_tables_ok && tables_fill(a.c, tt, p, a.prog, s_fo) ? 1 : 0;
-      const bool e = s_tables_ok != 0 && s_t.ok && s_elig[kq] && !s_inv;
-      const bool has_pre = s_t.ok && (g0.pts_filter || g0.pts_score || g0.ipa);
-      s_skip = !s_prev_imm && (!has_pre || e);
     }
+    // the per-cycle tables: this pod's scope and fill tasks, from its LDS
+    // program beside tid 0's parse (another wave)
+    if (a.tables_inkernel && tid == 192)
+      s_elig[kq] = s_tables_ok && tables_fill(c, tt, p, s_blob, s_fo, p.blob) ? 1 : 0;
     uint64_t srk[KN];
     if (a.fused_static) {   // one pod: the record of ksg_sweep_static, computed in place
       const PodView vs = make_view(c, prof, s_pod, s_blob, a.prog);
@@ -603,11 +615,15 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     KSG_CSTAMP(2);    // (stamps build: tid 0's parse and layout; segment 2 is barrier 1 otherwise)
     const bool ok = s_t.ok;
     const int words = ok ? s_t.words : 0;
+    // this pod skips phase 1 and barrier 1: it reads the tables (their scope,
+    // exact), or has nothing to count
+    const bool pre_skip = !s_prev_imm && (!(ok && (s_g.pts_filter || s_g.pts_score || s_g.ipa)) ||
+                                        (s_tables_ok != 0 && ok && s_elig[kq] && !s_inv));
     // a pod reading the tables: its fill tasks, the totals its affinity /
     // preferred terms read and the existing pods' template totals, loaded now
     // (every write they see is lagged or was applied before barrier 3 of the
     // previous pod), in flight through the rest of the setup
-    const bool tab_read = s_skip && s_tables_ok && ok;
+    const bool tab_read = pre_skip && s_tables_ok && ok;
     if (tab_read) {
       const TopoProg& g1 = s_g;
       if (tid < kTopoFill && !a.tables_inkernel) s_fo[tid] = tt.fo[(size_t)(a.first - tt.first + kq) * kTopoFill + tid];
@@ -627,7 +643,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     }
     const bool pmode = a.pmode && words <= kCoopPHist && words * G <= 32768;
     for (int i = tid; i < words; i += BLOCK) s_hist[i] = 0;
-    if (pmode && !s_skip) {   // word kinds of the partial slot (fold_all, phase 1's hand-off)
+    if (pmode && !pre_skip) {   // word kinds of the partial slot (fold_all, phase 1's hand-off)
       for (int w = tid; w < words; w += BLOCK) {
         int kind = 0;
         auto in = [&](const Slot& sl) {
@@ -665,7 +681,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     // and barrier 1 is not needed either, every cross-workgroup write of the
     // previous pod being lagged)
     const bool pre = ok && (g.pts_filter || g.pts_score || g.ipa);
-    const bool skip = s_skip != 0;
+    const bool skip = pre_skip != 0;
     if (pre && !skip) {
       long long lmin[kMaxHard], ldom[kMaxHard], lempty[kMaxSoft], laff = 0, lany = 0;
 #pragma unroll
@@ -1365,6 +1381,74 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       gst(&mine->best, b);
       gst(&mine->err, e);
       s_wbest = b;
+    }
+    if (CAP == 2 && a.last_arrive) {
+      // The per-cycle evaluation (one pod, no assume): no barrier 3.  Each
+      // workgroup's host rows and argmax slot are performed (system-scope
+      // stores: vmcnt(0)), it arrives on a counter, and the last of the G
+      // arrivals selects the host and stores the result and then the flag
+      // (ksg_eval_cycle's completion), so the rows' PCIe drain no longer
+      // waits in a grid barrier before a phase 4 and the other workgroups end.
+      KSG_CSTAMP(8);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)a.arrive, 1u,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (old + 1) % (unsigned)G == 0 ? 1 : 0;
+      }
+      __syncthreads();
+      KSG_CSTAMP(9);
+      if (s_last) {
+        // the atomics set of this pod, read by every workgroup before its
+        // arrival: clean for the next launch
+        for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&acc->hist[i], 0);
+        if (tid < 64) {
+          unsigned long long b = 0;
+          int32_t e = 0;
+          for (int l = tid; l < G; l += 64) {
+            b = max(b, (unsigned long long)gld(&a.parts[l].best));
+            e |= gld(&a.parts[l].err);
+          }
+          b = wreduce(b, OpMaxU64{});
+          e = wreduce(e, OpOrI{});
+          if (tid == 0) {
+            int selected = -1;
+            uint32_t status = 0;
+            if (!ok) {
+              status |= KSG_ST_SCORE_ERROR;
+            } else if (gnfeas == 1) {
+              selected = gminidx;
+            } else if (scored) {
+              status |= KSG_ST_SCORED;
+              if (e & 1) status |= KSG_ST_SCORE_ERROR;   // (bit 1: a capture value wider than the rows)
+              else selected = key_node(b);
+            }
+            uint32_t score_skip = p.score_skip;
+            if (ipa_in_filter && s_t.ipa_skip_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
+            if (scored && ipa_in_score && !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u) && s_t.ipa_skip_score) {
+              status |= KSG_ST_IPA_PRESCORE_SKIP;
+              score_skip |= bit(KSG_PL_INTER_POD_AFFINITY);
+            }
+            a.placements[a.out0 + kq] = selected;
+            ksg_result res;
+            res.selected = selected;
+            res.n_feasible = ok ? gnfeas : 0;
+            res.status = status;
+            res.score_skip = score_skip;
+            if (a.results) a.results[a.out0 + kq] = res;
+            hst<true>(a.h_ovf, (unsigned)((e >> 1) & 1));
+            hst<true>(&a.h_res->selected, res.selected);
+            hst<true>(&a.h_res->n_feasible, res.n_feasible);
+            hst<true>(&a.h_res->status, res.status);
+            hst<true>(&a.h_res->score_skip, res.score_skip);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.h_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+      }
+      KSG_CSTAMP(10);
+      continue;   // (one pod)
     }
     if (a.commit && s_nlsel > 0) {   // the counts the assume will change (the winner's become the lag's)
       __syncthreads();

@@ -51,12 +51,12 @@ struct TopoTables {
 // table and presence bitmap, each unique hard key's count-of-counts.  P: the
 // program pool (absolute offsets).  Same program layout as parse_topo.
 __device__ __forceinline__ bool tables_scope(const DevCluster& c, const TopoTables& tt, const ksg_pod& p,
-                                             const int32_t* P) {
+                                             const int32_t* P, int base = 0) {
   auto pair = [&](int sel, int col) { return sel >= 0 ? tt.pair_off[(size_t)sel * tt.L + col] : -1; };
   auto all = [&](int col) { return tt.col_missing[col] == 0; };
   bool e = true;
   if (p.pts >= 0) {
-    const int32_t* w = P + p.pts;
+    const int32_t* w = P + (p.pts - base);
     const int nh = w[0], ns = w[1];
     const int32_t* hard = w + 3;
     for (int i = 0; e && i < nh; i++) {
@@ -72,7 +72,7 @@ __device__ __forceinline__ bool tables_scope(const DevCluster& c, const TopoTabl
     }
   }
   if (p.ipa >= 0) {
-    const int32_t* w = P + p.ipa;
+    const int32_t* w = P + (p.ipa - base);
     const int na = w[0], sel_all = w[1];
     for (int i = 0; e && i < na; i++) {
       const int col = w[3 + i];
@@ -100,9 +100,11 @@ constexpr int kTopoFill = 24;   // fill tasks per pod: kMaxHard + kMaxSoft + kMa
 // offsets in the order the topology kernel lays its histograms out (hard,
 // soft without a hostname key, affinity, anti-affinity, preferred), so the
 // kernel's fill needs no dependent index load.  out: kTopoFill entries.
+// prog + (offset - base) is the pod's program word at that offset (base 0:
+// the pool; the pod's blob offset: its LDS copy).
 __device__ __forceinline__ bool tables_fill(const DevCluster& c, const TopoTables& t, const ksg_pod& p,
-                                            const int32_t* prog, int4* out) {
-  const bool e = tables_scope(c, t, p, prog);
+                                            const int32_t* prog, int4* out, int base = 0) {
+  const bool e = tables_scope(c, t, p, prog, base);
   int k = 0;
   auto task = [&](int sel, int col, bool pres) {
     if (k >= kTopoFill || col < 0 || col >= t.L || c.col_unique[col]) return;
@@ -110,7 +112,7 @@ __device__ __forceinline__ bool tables_fill(const DevCluster& c, const TopoTable
     out[k++] = make_int4(off, pres ? t.pres_off[col] : -1, col, sel);
   };
   if (e && p.pts >= 0) {
-    const int32_t* w = prog + p.pts;
+    const int32_t* w = prog + (p.pts - base);
     const int nh = w[0], ns = w[1];
     const int32_t* hard = w + 3;
     for (int j = 0; j < nh && j < kMaxHard; j++) task(hard[7 * j + 1], hard[7 * j], true);
@@ -119,7 +121,7 @@ __device__ __forceinline__ bool tables_fill(const DevCluster& c, const TopoTable
       if (!soft[6 * j + 5]) task(soft[6 * j + 1], soft[6 * j], false);
   }
   if (e && p.ipa >= 0) {
-    const int32_t* w = prog + p.ipa;
+    const int32_t* w = prog + (p.ipa - base);
     const int na = w[0], sel_all = w[1];
     for (int j = 0; j < na && j < kMaxAff; j++) task(sel_all, w[3 + j], true);
     w += 3 + na;

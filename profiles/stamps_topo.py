@@ -18,8 +18,9 @@ enc = E.Encoder(nodes, pods, prof)
 eng = native.Engine(lib_path=os.path.join(ROOT, "kube-scheduler-simulator_amd", "libksched_stamps.so"))
 eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
 if len(sys.argv) > 2 and sys.argv[2] == "eval":
-    # the per-cycle form: one ksg_eval (the topology kernel on one pod, phase 1
-    # included) and one ksg_commit per pod, after n_pods // 2 queued pods
+    # the per-cycle form: one ksg_eval_view (the topology kernel on one pod,
+    # reading the per-cycle domain tables) and one ksg_commit per pod, after
+    # n_pods // 2 queued pods
     warm = n_pods // 2
     eng.run_queue(0, warm, results=False)
     st0 = (C.c_ulonglong * 16)()
@@ -29,7 +30,9 @@ if len(sys.argv) > 2 and sys.argv[2] == "eval":
     import time
     t = time.perf_counter()
     for j in range(warm, n_pods):
-        r = eng.eval(j)
+        # ksg_eval_view (capture mode 2, the per-cycle tables), rows left in the library
+        r, v = native.KsgResult(), native.KsgEvalRows()
+        eng._check(eng._eval_view(eng.ctx, j, C.byref(r), C.byref(v)))
         if r.selected >= 0:
             eng.commit(j, r.selected)
     ms = (time.perf_counter() - t) * 1e3

@@ -16,3 +16,7 @@ for k in ("per_cycle", "per_cycle_server", "per_cycle_configs2"):
     print(k, v and (round(v["us_per_cycle_mean"], 1), round(v["us_per_cycle_p50"], 1),
                     {a: round(b, 1) for a, b in v["breakdown_us_mean"].items()}, v.get("placements_equal_run_queue")))
 PY
+if [ -f kube-scheduler-simulator_amd/libksched_stamps.so ]; then
+  timeout -k 10 300 python3 -u profiles/stamps_topo.py 1600 eval > "$O/stamps_eval.txt" 2>&1 || { echo "stamps failed"; tail -5 "$O/stamps_eval.txt"; exit 1; }
+  cat "$O/stamps_eval.txt"
+fi
