@@ -2309,9 +2309,14 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
                                     : (kn == 1 ? (const void*)ksg_cycle_server<1, false>
                                       : kn == 2 ? (const void*)ksg_cycle_server<2, false>
                                                 : (const void*)ksg_cycle_server<4, false>);
-    // cooperative: every workgroup resident (or the launch is refused), as the
-    // exchanges need for the server's whole life
-    HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(64), sargs, 0, ctx->stream));
+    // plain, G within the occupancy API's residency, as the per-cycle launch
+    // (a process that made cooperative launches faults in the runtime's exit
+    // teardown under rocprofv3); an exchange timeout ends the server and the
+    // next one launches cooperatively (the runtime's residency guarantee)
+    if (ctx->cycle_coop)
+      HIPC(ctx, hipLaunchCooperativeKernel(kf, dim3(G), dim3(64), sargs, 0, ctx->stream));
+    else
+      HIPC(ctx, hipLaunchKernel(kf, dim3(G), dim3(64), sargs, 0, ctx->stream));
     HIPC(ctx, hipGetLastError());
     ctx->srv_running = true;
     ctx->srv_last = std::chrono::steady_clock::now();
@@ -2456,6 +2461,10 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     if (server) {            // every workgroup of the server leaves on a timed-out exchange
       (void)hipStreamSynchronize(ctx->stream);
       ctx->srv_running = false;
+      if (!ctx->cycle_coop) {   // not every workgroup was resident: a cooperative server from now on
+        ctx->cycle_coop = true;
+        return eval_fast(ctx, pod, res, cap, view);
+      }
       return fail(ctx, KSG_E_DEVICE, "per-cycle server: workgroup exchange timed out");
     }
     if (!ctx->cycle_coop) {   // not every workgroup was resident: the cooperative launch from now on
