@@ -356,7 +356,7 @@ def device_serialiser_long(eng, enc, prof, B, n_pods: int, chunk: int, threads: 
 
 
 def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=None, label: str = "configs[1]",
-                      server: bool = False):
+                      server: bool = False, hint_ahead: int = 0):
     """The drop-in's per-cycle path, the calls the Go
     shim makes per scheduling cycle, through the C ABI of libksched.so:
     ksg_snapshot_add_pod -> ksg_snapshot_sync (append to the device
@@ -376,7 +376,9 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=N
     # the queue's pending pods are announced up front, as the Go shim's pod
     # informer does (ksg_snapshot_hint_pod): their selectors and templates are
     # in the encoding universe before their cycles, so adding them appends
-    for p in pods:
+    # (hint_ahead > 0: only the first warm + hint_ahead up front, then cycle i
+    # hints pod i + hint_ahead, as for pods created while the queue runs)
+    for p in (pods if hint_ahead <= 0 else pods[:warm + hint_ahead]):
         snap.hint_pod(p)
     prev = os.environ.get("KSG_CYCLE_SERVER")
     os.environ["KSG_CYCLE_SERVER"] = "1" if server else "0"   # read once, when the context opens
@@ -401,13 +403,13 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=N
     i32p = C.POINTER(C.c_int32)
     drv.cycle_run.restype = C.c_int
     drv.cycle_run.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(S.PodView), C.c_int32, C.c_int32, C.c_void_p,
-                              C.c_int32, i32p, C.POINTER(C.c_int64), i32p, i32p, i32p]
+                              C.c_int32, i32p, C.POINTER(C.c_int64), i32p, i32p, i32p, C.c_int32]
     placed = np.full(warm + n_pods, -1, np.int32)
     phases = np.zeros((n_pods, 5), np.int64)
     ap, rl, where = C.c_int32(), C.c_int32(), C.c_int32(-1)
     rc = drv.cycle_run(snap.h, eng.ctx, arr, len(views), warm, C.addressof(rows), N,
                        placed.ctypes.data_as(i32p), phases.ctypes.data_as(C.POINTER(C.c_int64)),
-                       C.byref(ap), C.byref(rl), C.byref(where))
+                       C.byref(ap), C.byref(rl), C.byref(where), hint_ahead)
     if rc != 0:
         raise RuntimeError(f"cycle driver: rc={rc} in phase {where.value}: {snap._err(snap.h).decode()}")
     # the same pods as one device-resident queue
@@ -425,7 +427,7 @@ def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=N
     return {"workload": f"{label} cluster ({N} nodes), per-cycle C-ABI path, {n_pods} cycles timed after {warm}",
             "driver": "C (tests/c/cycle_driver.c), CLOCK_MONOTONIC per call",
             "mode": "persistent server (KSG_CYCLE_SERVER=1)" if server else "one launch per cycle",
-            "pending_pods_hinted": True,
+            "pending_pods_hinted": True if hint_ahead <= 0 else f"one per cycle, {hint_ahead} pods ahead (timed in add_pod)",
             "us_per_cycle_mean": float(per.mean()), "us_per_cycle_p50": float(np.percentile(per, 50)),
             "us_per_cycle_p99": float(np.percentile(per, 99)), "pods_per_s": float(1e6 / per.mean()),
             "breakdown_us_mean": {k: float(us[:, j].mean()) for j, k in enumerate(names)},
@@ -699,12 +701,14 @@ def main():
             log(f"[rank {rank}] annotation sidecar unavailable: {e}")
     if eng1 is not None:
         eng1.close()
-    cyc = cyc_srv = None
+    cyc = cyc_srv = cyc_hint = None
     if world == 1 and args.cycle_pods > 0:
         try:
             S = importlib.import_module(PKG + ".snapshot")
             cyc = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods)
             cyc_srv = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods, server=True)
+            # pods created while the queue runs, one hint per cycle
+            cyc_hint = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods, hint_ahead=8)
         except Exception as e:
             log(f"[rank {rank}] per-cycle sidecar unavailable: {e}")
     cyc3 = ann3 = None
@@ -770,7 +774,7 @@ def main():
         out["source_hash"] = {"library": ge.library_hash(), "tree": ge.source_hash()}
         out["source_hash"]["matches"] = out["source_hash"]["library"] == out["source_hash"]["tree"]
         for key, val in (("configs1", c1), ("replica_sweep", sweep), ("annotations", ann), ("per_cycle", cyc),
-                         ("per_cycle_server", cyc_srv),
+                         ("per_cycle_server", cyc_srv), ("per_cycle_hinted", cyc_hint),
                          ("kubelet_memory", kub), ("per_cycle_configs2", cyc3), ("annotations_configs2", ann3)):
             if val is not None:
                 out[key] = val

@@ -5,6 +5,10 @@
  *   ksg_snapshot_add_pod -> ksg_snapshot_sync -> ksg_eval_view (the rows
  *   in library memory) -> ksg_snapshot_statuses -> ksg_snapshot_assume
  *
+ * hint_ahead > 0: cycle i first announces pod i + hint_ahead
+ * (ksg_snapshot_hint_pod, timed with add_pod), as the Go shim's pod informer
+ * does for a pod created while the queue runs.
+ *
  * Bench infrastructure, not product: links libksched.so only. */
 #include <stdint.h>
 #include <stdlib.h>
@@ -26,7 +30,7 @@ static int64_t now_ns(void) {
  * naming the phase. */
 int cycle_run(ksg_snapshot* s, ksg_ctx* ctx, const ksg_pod_view* views, int32_t n, int32_t warm,
               ksg_eval_rows* rows, int32_t n_nodes, int32_t* placed, int64_t* phase_ns, int32_t* appended,
-              int32_t* reloads, int32_t* where) {
+              int32_t* reloads, int32_t* where, int32_t hint_ahead) {
   int32_t* code = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_nodes);
   int32_t* msg = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_nodes);
   const int64_t cap_bytes = 1 << 16;
@@ -38,6 +42,10 @@ int cycle_run(ksg_snapshot* s, ksg_ctx* ctx, const ksg_pod_view* views, int32_t 
     int64_t len = 0;
     ksg_result r;
     const int64_t t0 = now_ns();
+    if (hint_ahead > 0 && i + hint_ahead < n && (rc = ksg_snapshot_hint_pod(s, &views[i + hint_ahead]))) {
+      *where = 0;
+      break;
+    }
     if ((rc = ksg_snapshot_add_pod(s, &views[i], &idx))) { *where = 0; break; }
     const int64_t t1 = now_ns();
     if ((rc = ksg_snapshot_sync(s, ctx, &ap))) { *where = 1; break; }
