@@ -47,7 +47,8 @@ Prints ONE JSON line (rank 0).  The line also carries:
   (bulk.annotate_queue, captured rows + ksg_annotate on 16 threads), plus the
   device serialiser's steady state over a longer queue;
 * `per_cycle` / `per_cycle_configs2` (N = 1): the drop-in's per-cycle C-ABI
-  path, call by call from C.
+  path, call by call from C; `per_cycle_server` the persistent server mode,
+  `per_cycle_hinted` one pending-pod hint per cycle instead of all up front.
 """
 from __future__ import annotations
 
