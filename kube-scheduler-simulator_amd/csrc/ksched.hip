@@ -156,6 +156,7 @@ struct ksg_ctx {
   TopoTables pct{};
   bool pct_valid = false;
   bool pc_tables = true;
+  bool cycle_early = true;            // ... writes its phase-2 rows after barrier 2
   bool cycle_last = true;             // the one-pod topology evaluation completes on its last arrival
   bool commit_args = true;            // ksg_commit's kernel takes the pod's commit program by value
   bool topo_stage = true;             // ... and reads a staged append in place (KSG_TOPO_STAGE=0: copies first)
@@ -1675,6 +1676,7 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   a.timeout = ctx->d_coop_flags + 4;
   a.arrive = ctx->d_coop_flags + 6;
   a.last_arrive = ctx->cycle_last ? 1 : 0;
+  a.early_rows = ctx->cycle_early ? 1 : 0;
   a.commit = do_commit;
   // the maintained tables: placement runs (they are rebuilt per run from the
   // state; a single-pod evaluation runs phase 1 instead of paying the rebuild)
@@ -3049,6 +3051,7 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_COOP_LAUNCH")) ctx->coop_launch = atoi(f) != 0;
   if (const char* f = getenv("KSG_PC_TABLES")) ctx->pc_tables = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_LAST")) ctx->cycle_last = atoi(f) != 0;
+  if (const char* f = getenv("KSG_CYCLE_EARLY")) ctx->cycle_early = atoi(f) != 0;
   if (const char* f = getenv("KSG_TOPO_STAGE")) ctx->topo_stage = atoi(f) != 0;
   if (const char* f = getenv("KSG_COMMIT_ARGS")) ctx->commit_args = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;

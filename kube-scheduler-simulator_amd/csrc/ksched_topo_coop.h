@@ -139,6 +139,8 @@ struct CoopArgs {
   int32_t cap_es;              // CAP == 2: bytes per row value (2, 4, 8); a value that does not fit
                                // sets *h_ovf and the host evaluates again wider
   unsigned* h_ovf;
+  int32_t early_rows;          // CAP == 2: 1 (default) the rows final since phase 2 are written after barrier 2
+                               // (KSG_CYCLE_EARLY=0: all in 3c; measurement knob)
   int32_t last_arrive;         // CAP == 2: 1 (default) the last arrival completes the call, 0 barrier 3 and
                                // phase 4 (KSG_CYCLE_LAST=0, measurement knob)
   ksg_pod* wpods;              // CAP == 2, a staged append read in place (pods / prog point into the
@@ -1136,6 +1138,44 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     KSG_CSTAMP(6);
     if (!coop_barrier(a.bar, a.timeout, G, target)) return;
     KSG_CSTAMP(7);
+    // CAP 2: the rows final since phase 2 (the status words and the raw
+    // scores of every plugin but PodTopologySpread, whose raw count needs
+    // phase 3's weights), written as if the pod is scored, go to the host now:
+    // their PCIe transfer overlaps phase 3.  3c writes the rest, and zeroes
+    // these when the pod turns out unscored (< 2 feasible nodes).
+    uint32_t early_err = 0;
+    const bool early = CAP == 2 && a.early_rows;
+    if constexpr (CAP == 2) {
+      if (early) {
+        const size_t NN = N;
+        const int es = a.cap_es;
+        for (int k = 0; k < KN; k++) {
+          const int n = node_of(k);
+          if (n >= N) break;
+          hst<true>(a.cap_fs + (size_t)kq * NN + n, ok ? ev[k].st : (uint32_t)KSG_FS_NOT_EVALUATED);
+          const bool feas = ok && ev[k].st == 0;
+          for (int q = 0; q < a.cap_n_rows; q++) {
+            const int pl = a.cap_rows[q];
+            if (pl == KSG_PL_POD_TOPOLOGY_SPREAD) continue;
+            int64_t raw = 0;
+            if (feas && ((v.smask >> pl) & 1u)) {
+              switch (pl) {
+                case KSG_PL_NODE_RESOURCES_FIT: raw = fitr[k]; break;
+                case KSG_PL_BALANCED_ALLOCATION: raw = bar[k]; break;
+                case KSG_PL_IMAGE_LOCALITY: raw = (int64_t)((srk[k] >> 32) & 0xff); break;
+                case KSG_PL_TAINT_TOLERATION: raw = ev[k].rt; break;
+                case KSG_PL_NODE_AFFINITY: raw = ev[k].ra; break;
+                case KSG_PL_INTER_POD_AFFINITY: if (ipa_may_score) raw = yv[k]; break;
+                default: break;
+              }
+            }
+            cyc_put_es<true>(a.cap_raw, ((size_t)kq * a.cap_n_rows + q) * NN + n, raw, es);
+            const bool f = es == 8 || (es == 4 ? raw == (int64_t)(int32_t)raw : raw == (int64_t)(int16_t)raw);
+            early_err |= f ? 0u : 2u;
+          }
+        }
+      }
+    }
 
     // ---- phase 3: fold phase 2; sizes, normalisation, argmax --------------------
     // every reader of the tables and template tables for this pod is past
@@ -1340,9 +1380,11 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         const int n = node_of(k);
         if (n >= N) break;
         const bool feas = scored && ev[k].st == 0;
-        hst<SYS>(a.cap_fs + (size_t)kq * NN + n, ok ? ev[k].st : (uint32_t)KSG_FS_NOT_EVALUATED);
+        if (!early) hst<SYS>(a.cap_fs + (size_t)kq * NN + n, ok ? ev[k].st : (uint32_t)KSG_FS_NOT_EVALUATED);
         for (int q = 0; q < a.cap_n_rows; q++) {
           const int pl = a.cap_rows[q];
+          // (written after barrier 2 with the same value when the pod is scored)
+          const bool raw_done = early && scored && pl != KSG_PL_POD_TOPOLOGY_SPREAD;
           int64_t raw = 0, nrm = 0;
           if (feas && ((v.smask >> pl) & 1u)) {
             switch (pl) {
@@ -1357,8 +1399,10 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
             }
           }
           const size_t row = ((size_t)kq * a.cap_n_rows + q) * NN + n;
-          cyc_put_es<SYS>(a.cap_raw, row, raw, es);
-          err |= fits(raw) ? 0u : 2u;
+          if (!raw_done) {
+            cyc_put_es<SYS>(a.cap_raw, row, raw, es);
+            err |= fits(raw) ? 0u : 2u;
+          }
           if (q < a.cap_n_normrows) {
             cyc_put_es<SYS>(a.cap_norm, ((size_t)kq * a.cap_n_normrows + q) * NN + n, nrm, es);
             err |= fits(nrm) ? 0u : 2u;
@@ -1369,6 +1413,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         err |= fits(tv) ? 0u : 2u;
       }
     }
+    err |= early_err;
     best = wreduce(best, OpMaxU64{});
     err = wreduce(err, OpOr32{});
     __syncthreads();   // every wave is past its get_*() reads of s_l / s_i
