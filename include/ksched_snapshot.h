@@ -439,6 +439,15 @@ int ksg_snapshot_status(ksg_snapshot* s, int32_t pod, uint32_t word, int32_t nod
  * and call again. */
 int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
                           int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len);
+/* ksg_snapshot_statuses for a caller that keeps its code / msg arrays between
+ * calls (the Go shim's per-cycle buffers): same outputs, but when code, msg
+ * and n_nodes are those of this snapshot's last successful delta call, the
+ * arrays are taken to still hold that call's output, so only the nodes it
+ * rejected are reset and only this call's rejected nodes are written (no
+ * dense pass over the passing nodes).  Any other call (different arrays, a
+ * failed call, ksg_snapshot_statuses in between) writes every node. */
+int ksg_snapshot_statuses_delta(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes,
+                                int32_t* code, int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len);
 /* PreFilter of plugin `plugin` for `pod` (given the device result's status
  * bits): *code = KSG_CODE_SUCCESS / SKIP / UNSCHEDULABLE_AND_UNRESOLVABLE
  * (NodeAffinity "pod affinity terms conflict", a volume plugin's claim /

@@ -586,6 +586,14 @@ struct ksg_snapshot {
     uint64_t dm_key[kDm];
     int32_t dm_id[kDm];
   } status;
+  // ksg_snapshot_statuses_delta: the output arrays of the last call and the
+  // nodes it rejected (the only entries it left other than Success / -1)
+  struct StatusDelta {
+    const int32_t* code = nullptr;
+    const int32_t* msg = nullptr;
+    int32_t n = -1;
+    std::vector<int32_t> rej;
+  } sdelta;
 };
 
 namespace {
@@ -2203,6 +2211,18 @@ uint64_t scan_block_sse2(const uint32_t* w, int32_t* code, int32_t* msg) {
   return mask;
 }
 
+// scan_block_sse2's mask without the stores (ksg_snapshot_statuses_delta)
+uint64_t mask_block_sse2(const uint32_t* w) {
+  const __m128i v_pass = _mm_setzero_si128(), v_ne = _mm_set1_epi32((int)KSG_FS_NOT_EVALUATED);
+  uint64_t mask = 0;
+  for (int i = 0; i < 64; i += 4) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(w + i));
+    const __m128i ok = _mm_or_si128(_mm_cmpeq_epi32(v, v_pass), _mm_cmpeq_epi32(v, v_ne));
+    mask |= (uint64_t)(~_mm_movemask_ps(_mm_castsi128_ps(ok)) & 0xf) << i;
+  }
+  return mask;
+}
+
 // framework.Status (code, Message()) of a Filter status word at `node` for
 // `pod`; msg may be null when only the code is wanted.
 bool status_of(const Encoded& e, int32_t pod, uint32_t word, int32_t node, int* code, std::string* msg,
@@ -2795,8 +2815,43 @@ int ksg_snapshot_status(ksg_snapshot* s, int32_t pod, uint32_t word, int32_t nod
   return KSG_OK;
 }
 
+// ksg_snapshot_statuses and its delta form: dense stores the passed defaults
+// of every node; otherwise only the rejected nodes are written.  rej (or
+// null) collects the rejected nodes.
+static int statuses_impl(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
+                         int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len, bool dense,
+                         std::vector<int32_t>* rej);
+
 int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
                           int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len) {
+  if (s) s->sdelta.code = nullptr;   // a delta call after this one starts dense
+  return statuses_impl(s, pod, words, n_nodes, code, msg, buf, cap, n_msgs, len, true, nullptr);
+}
+
+int ksg_snapshot_statuses_delta(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes,
+                                int32_t* code, int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len) {
+  if (!s || !code || !msg) return KSG_E_INVALID;
+  auto& d = s->sdelta;
+  const bool reuse = d.code == code && d.msg == msg && d.n == n_nodes;
+  if (reuse)   // the last call's rejections back to the defaults
+    for (int32_t n : d.rej) {
+      code[n] = KSG_CODE_SUCCESS;
+      msg[n] = -1;
+    }
+  d.code = nullptr;   // (set again only when this call succeeds)
+  d.rej.clear();
+  const int rc = statuses_impl(s, pod, words, n_nodes, code, msg, buf, cap, n_msgs, len, !reuse, &d.rej);
+  if (rc == KSG_OK) {
+    d.code = code;
+    d.msg = msg;
+    d.n = n_nodes;
+  }
+  return rc;
+}
+
+static int statuses_impl(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
+                         int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len, bool dense,
+                         std::vector<int32_t>* rej) {
   if (!s || !words || !code || !msg) return KSG_E_INVALID;
   if (!s->encoded || pod < 0 || pod >= (int32_t)s->e.pods.size() || n_nodes != s->e.N)
     return fail(s, KSG_E_INVALID, "statuses: index out of range");
@@ -2840,12 +2895,14 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     const int32_t m = std::min(kB, n_nodes - b);
     uint64_t mask = 0;   // the block's rejected nodes: four words per compare
     if (m == kB) {
-      mask = scan_block_sse2(words + b, code + b, msg + b);
+      mask = dense ? scan_block_sse2(words + b, code + b, msg + b) : mask_block_sse2(words + b);
     } else {
       for (int32_t i = 0; i < m; i++) {
         const uint32_t w = words[b + i];
-        code[b + i] = KSG_CODE_SUCCESS;
-        msg[b + i] = -1;
+        if (dense) {
+          code[b + i] = KSG_CODE_SUCCESS;
+          msg[b + i] = -1;
+        }
         mask |= (uint64_t)(w != 0 && w != KSG_FS_NOT_EVALUATED) << i;
       }
     }
@@ -2894,6 +2951,7 @@ int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, i
     }
     code[n] = c;
     msg[n] = last_idx;
+    if (rej) rej->push_back(n);
     }
   }
   int64_t total = 0;

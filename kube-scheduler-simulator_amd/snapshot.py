@@ -393,6 +393,8 @@ class Snapshot:
         self._profile_info = f("profile_info", C.c_int, vp, C.POINTER(ProfileInfo))
         self._statuses = f("statuses", C.c_int, vp, i32, C.POINTER(C.c_uint32), i32, C.POINTER(i32),
                            C.POINTER(i32), C.c_char_p, i64, C.POINTER(i32), C.POINTER(i64))
+        self._statuses_delta = f("statuses_delta", C.c_int, vp, i32, C.POINTER(C.c_uint32), i32, C.POINTER(i32),
+                                 C.POINTER(i32), C.c_char_p, i64, C.POINTER(i32), C.POINTER(i64))
         self.h = vp()
         k = _Keep()
         rc = self._new(C.byref(profile_view(prof, k)), C.byref(self.h))

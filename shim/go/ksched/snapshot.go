@@ -682,6 +682,49 @@ func (x *Snapshot) Status(pod int, word uint32, node int) (int, string, error) {
 	return int(code), C.GoString(buf), nil
 }
 
+// StatusesInto is Statuses into slices the caller keeps from cycle to cycle
+// (ksg_snapshot_statuses_delta): while codes and msg are the slices of this
+// Snapshot's previous StatusesInto call, untouched since, only the nodes that
+// call rejected and the nodes this one rejects are written.
+func (x *Snapshot) StatusesInto(pod int, words []uint32, codes, msg []int32) (msgs []string, err error) {
+	n := len(words)
+	if n == 0 || len(codes) < n || len(msg) < n {
+		c, m, t, e := x.Statuses(pod, words)
+		copy(codes, c)
+		copy(msg, m)
+		return t, e
+	}
+	if len(x.msgBuf) == 0 {
+		x.msgBuf = make([]byte, 1<<16)
+	}
+	var nm C.int32_t
+	var ln C.int64_t
+	call := func() error {
+		return x.check(C.ksg_snapshot_statuses_delta(x.s, C.int32_t(pod), (*C.uint32_t)(unsafe.Pointer(&words[0])),
+			C.int32_t(n), (*C.int32_t)(unsafe.Pointer(&codes[0])), (*C.int32_t)(unsafe.Pointer(&msg[0])),
+			(*C.char)(unsafe.Pointer(&x.msgBuf[0])), C.int64_t(len(x.msgBuf)), &nm, &ln))
+	}
+	if err = call(); err != nil {
+		return nil, err
+	}
+	if int64(ln) > int64(len(x.msgBuf)) { // the texts did not fit: once more (the arrays already hold this call's output)
+		x.msgBuf = make([]byte, int64(ln)+1)
+		if err = call(); err != nil {
+			return nil, err
+		}
+	}
+	raw := x.msgBuf[:ln]
+	msgs = make([]string, 0, int(nm))
+	start := 0
+	for i := 0; i < len(raw) && len(msgs) < int(nm); i++ {
+		if raw[i] == 0 {
+			msgs = append(msgs, string(raw[start:i]))
+			start = i + 1
+		}
+	}
+	return msgs, nil
+}
+
 // Statuses decodes every node's Filter status word of a pod at once
 // (ksg_snapshot_statuses): codes[n] (Code*), msg[n] = index into msgs, -1
 // for success / not evaluated.  One C call writes straight into the result

@@ -3,7 +3,8 @@
  * so the measured cost is the C ABI's alone (no Python / ctypes in the loop):
  *
  *   ksg_snapshot_add_pod -> ksg_snapshot_sync -> ksg_eval_view (the rows
- *   in library memory) -> ksg_snapshot_statuses -> ksg_snapshot_assume
+ *   in library memory) -> ksg_snapshot_statuses_delta (the shim's buffers kept
+ *   across cycles) -> ksg_snapshot_assume
  *
  * hint_ahead > 0: cycle i first announces pod i + hint_ahead
  * (ksg_snapshot_hint_pod, timed with add_pod), as the Go shim's pod informer
@@ -36,6 +37,7 @@ int cycle_run(ksg_snapshot* s, ksg_ctx* ctx, const ksg_pod_view* views, int32_t 
   const int64_t cap_bytes = 1 << 16;
   char* buf = (char*)malloc((size_t)cap_bytes);
   int rc = 0;
+  const int dense = getenv("KSG_DRIVER_DENSE") != NULL;   /* measurement: the dense statuses form */
   *appended = *reloads = 0;
   for (int32_t i = 0; i < n && rc == 0; i++) {
     int32_t idx = -1, ap = 0, n_msgs = 0;
@@ -52,7 +54,8 @@ int cycle_run(ksg_snapshot* s, ksg_ctx* ctx, const ksg_pod_view* views, int32_t 
     const int64_t t2 = now_ns();
     if ((rc = ksg_eval_view(ctx, idx, &r, rows))) { *where = 2; break; }
     const int64_t t3 = now_ns();
-    if ((rc = ksg_snapshot_statuses(s, idx, rows->fstatus, n_nodes, code, msg, buf, cap_bytes, &n_msgs, &len))) {
+    if ((rc = (dense ? ksg_snapshot_statuses : ksg_snapshot_statuses_delta)(s, idx, rows->fstatus, n_nodes, code, msg, buf,
+                                                                           cap_bytes, &n_msgs, &len))) {
       *where = 3;
       break;
     }

@@ -604,3 +604,45 @@ def test_export_case2_claim_native(built):
     snap_doc = I.load_snapshot(export_case2_with_claim())
     snap, enc = _assert_same(snap_doc.nodes, snap_doc.pods, snap_doc.profile)
     _prefilter_outcomes_match(snap, enc, snap_doc.profile, len(snap_doc.pods))
+
+
+def test_statuses_delta_matches_dense(built):
+    """ksg_snapshot_statuses_delta with arrays kept across calls gives, call
+    after call, exactly the dense form's codes / message indices / messages;
+    a dense call in between (or other arrays) makes the next delta call dense."""
+    import ctypes as C
+    nodes, pods, prof = zoo.zoo(2)
+    enc = E.Encoder(nodes, pods, prof)
+    snap = S.Snapshot(prof, nodes, pods)
+    snap.encode()
+    ref = S.Snapshot(prof, nodes, pods)
+    ref.encode()
+    import binding
+    o = binding.Oracle(1)
+    o.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    n = len(nodes)
+    code = np.full(n, 7, np.int32)   # garbage before the first (dense) call
+    msg = np.full(n, 7, np.int32)
+    buf = C.create_string_buffer(1 << 16)
+    nm, ln = C.c_int32(), C.c_int64()
+    i32p = C.POINTER(C.c_int32)
+    for pi in range(40):
+        cap = pkg("native").CaptureBuffers(n, 1)
+        o.eval(pi, cap)
+        w = np.ascontiguousarray(cap.fstatus[0], np.uint32)
+        # the dense form on another snapshot of the same objects (a dense call
+        # on `snap` would restart its delta state), and on `snap` itself now
+        # and then, after which the delta call writes every node again
+        want_c, want_m, want_t = ref.statuses(pi, w)
+        if pi % 13 == 5:
+            snap.statuses(pi, w)
+        assert snap._statuses_delta(snap.h, pi, w.ctypes.data_as(C.POINTER(C.c_uint32)), n,
+                                    code.ctypes.data_as(i32p), msg.ctypes.data_as(i32p), buf, len(buf),
+                                    C.byref(nm), C.byref(ln)) == 0
+        texts = [t.decode() for t in buf.raw[:ln.value].split(b"\0")[:nm.value]]
+        assert np.array_equal(code, want_c) and np.array_equal(msg, want_m) and texts == want_t, pi
+        assert snap._statuses_delta(snap.h, pi, w.ctypes.data_as(C.POINTER(C.c_uint32)), n,
+                                    code.ctypes.data_as(i32p), msg.ctypes.data_as(i32p), buf, len(buf),
+                                    C.byref(nm), C.byref(ln)) == 0
+        assert np.array_equal(code, want_c) and np.array_equal(msg, want_m), pi
+        o.commit(pi, max(0, int(np.argmin(cap.fstatus[0]))))
