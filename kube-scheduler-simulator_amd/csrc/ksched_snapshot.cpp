@@ -2832,7 +2832,10 @@ int ksg_snapshot_statuses_delta(ksg_snapshot* s, int32_t pod, const uint32_t* wo
                                 int32_t* code, int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len) {
   if (!s || !code || !msg) return KSG_E_INVALID;
   auto& d = s->sdelta;
-  const bool reuse = d.code == code && d.msg == msg && d.n == n_nodes;
+  // (the sparse form pays per rejected node: past an eighth of the nodes
+  // rejected by the last call, the dense pass is the cheaper one; measured on
+  // configs[1] ~30 % rejected, configs[2] ~15 %)
+  const bool reuse = d.code == code && d.msg == msg && d.n == n_nodes && d.rej.size() * 8 <= (size_t)n_nodes;
   if (reuse)   // the last call's rejections back to the defaults
     for (int32_t n : d.rej) {
       code[n] = KSG_CODE_SUCCESS;
