@@ -97,9 +97,13 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(enc, pf, n_threads: int, budget_s: float):
+def cpu_baseline(enc, pf, n_threads: int, budget_s: float, check=None):
     """C++ restatement of the reference algorithm (oracle/, "port"), timed on a
-    bounded prefix of the same queue on the same cluster."""
+    bounded prefix of the same queue on the same cluster.  With `check` (the
+    GPU's placements of the whole queue), the oracle also finishes the queue
+    untimed and the line reports whether every placement agrees (VERDICT r5
+    item 1: the headline pinned at its own size)."""
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import binding
     o = binding.Oracle(n_threads)
@@ -107,19 +111,32 @@ def cpu_baseline(enc, pf, n_threads: int, budget_s: float):
     n_pods = len(enc.workload.pods)
     done = 0
     chunk = 500
+    got = []
     t0 = time.perf_counter()
     while done < n_pods and time.perf_counter() - t0 < budget_s:
         k = min(chunk, n_pods - done)
-        o.run_queue(done, k, results=False)
+        got.append(o.run_queue(done, k, results=False)[0])
         done += k
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "pods/s", "cores": n_threads, "kind": "port",
-            "sample": f"first {done} pods of the {n_pods}-pod queue on the same {len(enc.cluster.node_names)}-node "
-                      f"cluster ({dt:.1f} s, OpenMP over nodes like the upstream 16-worker Parallelizer)",
-            "node_evals_per_sec": done * len(enc.cluster.node_names) / dt}
+    out = {"value": done / dt, "unit": "pods/s", "cores": n_threads, "kind": "port",
+           "sample": f"first {done} pods of the {n_pods}-pod queue on the same {len(enc.cluster.node_names)}-node "
+                     f"cluster ({dt:.1f} s, OpenMP over nodes like the upstream 16-worker Parallelizer)",
+           "node_evals_per_sec": done * len(enc.cluster.node_names) / dt}
+    if check is not None:
+        if done < n_pods:   # the rest of the queue, untimed: the check covers every pod
+            got.append(o.run_queue(done, n_pods - done, results=False)[0])
+        po = np.concatenate(got)
+        bad = np.nonzero(po != np.asarray(check))[0]
+        out["placements_checked"] = int(n_pods)
+        out["placements_equal_oracle"] = bool(bad.size == 0 and len(check) == n_pods)
+        if bad.size:
+            out["first_mismatch"] = {"pod": int(bad[0]), "gpu": int(check[bad[0]]), "oracle": int(po[bad[0]]),
+                                     "mismatches": int(bad.size)}
+    o.close()
+    return out
 
 
-def cpu_baselines(enc, pf, budget_s: float):
+def cpu_baselines(enc, pf, budget_s: float, check=None):
     """BASELINE.md / SURVEY §8(d): 16 threads (upstream parallelism: 16) and
     every host core this process may use (the limit that applied is named);
     when the affinity mask holds more cores than that limit grants, the port
@@ -127,7 +144,7 @@ def cpu_baselines(enc, pf, budget_s: float):
     oversubscribed (north star: "then all host cores")."""
     usable, limit = usable_cores()
     affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    out = cpu_baseline(enc, pf, 16, budget_s)
+    out = cpu_baseline(enc, pf, 16, budget_s, check=check)
     out["cpu_model"] = cpu_model()
     out["nproc"] = os.cpu_count()
     out["affinity_cores"] = affinity
@@ -780,7 +797,9 @@ def main():
             if val is not None:
                 out[key] = val
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baselines(enc, pf, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baselines(enc, pf, args.cpu_budget, check=pl)
+            # the headline's placements against the oracle over the whole queue
+            out["placements_equal_oracle"] = out["cpu_baseline"].get("placements_equal_oracle")
         print(json.dumps(out), flush=True)
     eng.close()
     dist.barrier()

@@ -1,10 +1,14 @@
-"""Golden vectors for the large configs[2] parity cases (VERDICT r3 item 4,
-r4 item 4): the C++ oracle's placements and per-pod results for
-generator.config3 at 15,000 nodes x P pods (seed 3), saved as
-tests/golden/c3_15000x<P>.npz (P = 30,000, and the full 150,000-pod queue).
-The oracle takes minutes to hours at these sizes, so the GPU tests compare
-against these files instead of re-running it.
-Regenerate: python tests/golden/make_c3_large.py [threads] [pods]"""
+"""Golden vectors for the large parity cases: the C++ oracle's placements and
+per-pod results, so the GPU tests compare against these files instead of
+re-running the oracle (minutes to hours at these sizes).
+
+* configs[2]: generator.config3 at 15,000
+  nodes x P pods (seed 3) -> tests/golden/c3_15000x<P>.npz (P = 30,000, and
+  the full 150,000-pod queue).
+  Regenerate: python tests/golden/make_c3_large.py [threads] [pods]
+* the headline: generator.config1, the in-tree default
+  profile, at 5,000 nodes x 50,000 pods (seed 1) -> c1_5000x50000.npz.
+  Regenerate: python tests/golden/make_c3_large.py [threads] 50000 config1 5000"""
 import os
 import sys
 import time
@@ -27,8 +31,11 @@ N_NODES = 15000
 def main():
     threads = int(sys.argv[1]) if len(sys.argv) > 1 else os.cpu_count()
     N_PODS = int(sys.argv[2]) if len(sys.argv) > 2 else 30000
+    gen = sys.argv[3] if len(sys.argv) > 3 else "config3"
+    n_nodes = int(sys.argv[4]) if len(sys.argv) > 4 else N_NODES
+    tag = {"config3": "c3", "config1": "c1"}[gen]
     t = time.time()
-    nodes, pods, prof = G.config3(n_nodes=N_NODES, n_pods=N_PODS)
+    nodes, pods, prof = getattr(G, gen)(n_nodes=n_nodes, n_pods=N_PODS)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
     o = binding.Oracle(threads)
@@ -39,12 +46,12 @@ def main():
         print(f"  {lo + len(chunks[-1][0])} pods, {time.time() - t:.0f} s", flush=True)
     pl = np.concatenate([c[0] for c in chunks])
     res = {k: np.concatenate([np.asarray(c[1][k]) for c in chunks]) for k in ("n_feasible", "status", "score_skip")}
-    np.savez_compressed(os.path.join(HERE, f"c3_15000x{N_PODS}.npz"), placements=np.asarray(pl, np.int32),
+    np.savez_compressed(os.path.join(HERE, f"{tag}_{n_nodes}x{N_PODS}.npz"), placements=np.asarray(pl, np.int32),
                         n_feasible=np.asarray(res["n_feasible"], np.int32),
                         status=np.asarray(res["status"], np.uint32),
                         score_skip=np.asarray(res["score_skip"], np.uint32),
                         pod_count=np.asarray(o.read_state(len(enc.cluster.res_names))[2], np.int32))
-    print(f"{N_PODS} pods x {N_NODES} nodes: {int((np.asarray(pl) >= 0).sum())} scheduled, "
+    print(f"{gen}: {N_PODS} pods x {n_nodes} nodes: {int((np.asarray(pl) >= 0).sum())} scheduled, "
           f"{time.time() - t:.0f} s at {threads} threads")
 
 
