@@ -381,6 +381,12 @@ int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labe
 int ksg_snapshot_add_pv(ksg_snapshot* s, const ksg_pv_view* pv);
 int ksg_snapshot_add_pvc(ksg_snapshot* s, const ksg_pvc_view* pvc);
 int ksg_snapshot_add_storage_class(ksg_snapshot* s, const ksg_storage_class_view* sc);
+/* Drops every PersistentVolume, claim and StorageClass (the listers' state
+ * before a resync: the Go shim clears, then re-adds what its listers hold, so
+ * a deleted object leaves the snapshot and a pod naming a deleted claim is
+ * rejected at PreFilter as upstream's lister lookup would reject it).  The
+ * next encode is a full one when anything was dropped. */
+int ksg_snapshot_clear_storage(ksg_snapshot* s);
 /* A pod the caller will add later (a pending pod of the scheduling queue, as
  * the pod informer delivers it: upstream eventhandlers.go addPodToSchedulingQueue
  * feeding the simulator's scheduler).  Its selectors, term templates, label
@@ -439,15 +445,23 @@ int ksg_snapshot_status(ksg_snapshot* s, int32_t pod, uint32_t word, int32_t nod
  * and call again. */
 int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
                           int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len);
-/* ksg_snapshot_statuses for a caller that keeps its code / msg arrays between
- * calls (the Go shim's per-cycle buffers): same outputs, but when code, msg
- * and n_nodes are those of this snapshot's last successful delta call, the
- * arrays are taken to still hold that call's output, so only the nodes it
- * rejected are reset and only this call's rejected nodes are written (no
- * dense pass over the passing nodes).  Any other call (different arrays, a
- * failed call, ksg_snapshot_statuses in between) writes every node. */
-int ksg_snapshot_statuses_delta(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes,
-                                int32_t* code, int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len);
+/* ksg_snapshot_statuses into arrays the snapshot owns (the per-cycle form;
+ * replaces round 5's ksg_snapshot_statuses_delta, which recognised the
+ * caller's kept arrays by their addresses): *code / *msg point at n_nodes
+ * entries, read-only to the caller, valid until the next
+ * ksg_snapshot_statuses_kept call on this snapshot or ksg_snapshot_free.
+ * After a complete call they hold exactly its output, so the next call
+ * resets only the nodes that call rejected and writes only its own rejected
+ * nodes (no pass over the passing nodes); it writes every node when the last
+ * call failed, n_nodes changed, or the last call rejected more than an eighth
+ * of the nodes.  buf / cap / *n_msgs / *len as ksg_snapshot_statuses.  A
+ * caller that retains the statuses past the next cycle copies them. */
+int ksg_snapshot_statuses_kept(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes,
+                               const int32_t** code, const int32_t** msg, char* buf, int64_t cap, int32_t* n_msgs,
+                               int64_t* len);
+/* Calls of ksg_snapshot_statuses_kept that took the sparse / the dense form
+ * (diagnostics and tests). */
+int ksg_snapshot_statuses_kept_stats(ksg_snapshot* s, int64_t* sparse_calls, int64_t* dense_calls);
 /* PreFilter of plugin `plugin` for `pod` (given the device result's status
  * bits): *code = KSG_CODE_SUCCESS / SKIP / UNSCHEDULABLE_AND_UNRESOLVABLE
  * (NodeAffinity "pod affinity terms conflict", a volume plugin's claim /

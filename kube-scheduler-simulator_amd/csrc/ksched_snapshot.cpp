@@ -586,14 +586,15 @@ struct ksg_snapshot {
     uint64_t dm_key[kDm];
     int32_t dm_id[kDm];
   } status;
-  // ksg_snapshot_statuses_delta: the output arrays of the last call and the
-  // nodes it rejected (the only entries it left other than Success / -1)
-  struct StatusDelta {
-    const int32_t* code = nullptr;
-    const int32_t* msg = nullptr;
-    int32_t n = -1;
+  // ksg_snapshot_statuses_kept: the arrays it returns (owned here, read-only
+  // to the caller), whether they hold the last call's complete output, and
+  // the nodes that call rejected (the only entries other than Success / -1)
+  struct StatusKept {
+    std::vector<int32_t> code, msg;
+    bool valid = false;
     std::vector<int32_t> rej;
-  } sdelta;
+    int64_t sparse_calls = 0, dense_calls = 0;
+  } skept;
 };
 
 namespace {
@@ -2211,7 +2212,7 @@ uint64_t scan_block_sse2(const uint32_t* w, int32_t* code, int32_t* msg) {
   return mask;
 }
 
-// scan_block_sse2's mask without the stores (ksg_snapshot_statuses_delta)
+// scan_block_sse2's mask without the stores (ksg_snapshot_statuses_kept's sparse form)
 uint64_t mask_block_sse2(const uint32_t* w) {
   const __m128i v_pass = _mm_setzero_si128(), v_ne = _mm_set1_epi32((int)KSG_FS_NOT_EVALUATED);
   uint64_t mask = 0;
@@ -2558,6 +2559,17 @@ int ksg_snapshot_add_storage_class(ksg_snapshot* s, const ksg_storage_class_view
   return KSG_OK;
 }
 
+int ksg_snapshot_clear_storage(ksg_snapshot* s) {
+  if (!s) return KSG_E_INVALID;
+  if (s->pvs.empty() && s->pvcs.empty() && s->classes.empty()) return KSG_OK;
+  s->pvs.clear();
+  s->pvcs.clear();
+  s->classes.clear();
+  s->encoded = false;   // claims resolve again (a deleted object's claims now fail) at the next encode
+  s->loaded_ctx = nullptr;
+  return KSG_OK;
+}
+
 int ksg_snapshot_add_namespace(ksg_snapshot* s, const char* name, int32_t n_labels, const ksg_str_pair* labels) {
   if (!s || !name || n_labels < 0 || (n_labels > 0 && !labels)) return KSG_E_INVALID;
   s->namespaces[S(name)] = copy_pairs(n_labels, labels);
@@ -2824,32 +2836,49 @@ static int statuses_impl(ksg_snapshot* s, int32_t pod, const uint32_t* words, in
 
 int ksg_snapshot_statuses(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,
                           int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len) {
-  if (s) s->sdelta.code = nullptr;   // a delta call after this one starts dense
   return statuses_impl(s, pod, words, n_nodes, code, msg, buf, cap, n_msgs, len, true, nullptr);
 }
 
-int ksg_snapshot_statuses_delta(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes,
-                                int32_t* code, int32_t* msg, char* buf, int64_t cap, int32_t* n_msgs, int64_t* len) {
+int ksg_snapshot_statuses_kept(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes,
+                               const int32_t** code, const int32_t** msg, char* buf, int64_t cap, int32_t* n_msgs,
+                               int64_t* len) {
   if (!s || !code || !msg) return KSG_E_INVALID;
-  auto& d = s->sdelta;
-  // (the sparse form pays per rejected node: past an eighth of the nodes
-  // rejected by the last call, the dense pass is the cheaper one; measured on
-  // configs[1] ~30 % rejected, configs[2] ~15 %)
-  const bool reuse = d.code == code && d.msg == msg && d.n == n_nodes && d.rej.size() * 8 <= (size_t)n_nodes;
-  if (reuse)   // the last call's rejections back to the defaults
-    for (int32_t n : d.rej) {
-      code[n] = KSG_CODE_SUCCESS;
-      msg[n] = -1;
-    }
-  d.code = nullptr;   // (set again only when this call succeeds)
-  d.rej.clear();
-  const int rc = statuses_impl(s, pod, words, n_nodes, code, msg, buf, cap, n_msgs, len, !reuse, &d.rej);
-  if (rc == KSG_OK) {
-    d.code = code;
-    d.msg = msg;
-    d.n = n_nodes;
+  *code = *msg = nullptr;
+  if (n_nodes < 0) return fail(s, KSG_E_INVALID, "statuses: index out of range");
+  auto& d = s->skept;
+  // The arrays are the snapshot's own and read-only to the caller, so after a
+  // complete call they hold exactly its output: the next call resets the
+  // nodes that call rejected and writes only its own rejected nodes.  (The
+  // sparse form pays per rejected node: past an eighth of the nodes rejected
+  // by the last call, the dense pass is the cheaper one; measured on
+  // configs[1] ~30 % rejected, configs[2] ~15 %.)
+  const bool sparse = d.valid && d.code.size() == (size_t)n_nodes && d.rej.size() * 8 <= (size_t)n_nodes;
+  if (d.code.size() != (size_t)n_nodes) {
+    d.code.assign((size_t)n_nodes, KSG_CODE_SUCCESS);
+    d.msg.assign((size_t)n_nodes, -1);
   }
-  return rc;
+  if (sparse)
+    for (int32_t n : d.rej) {
+      d.code[n] = KSG_CODE_SUCCESS;
+      d.msg[n] = -1;
+    }
+  d.valid = false;   // (set again only when this call completes)
+  d.rej.clear();
+  (sparse ? d.sparse_calls : d.dense_calls)++;
+  const int rc = statuses_impl(s, pod, words, n_nodes, d.code.data(), d.msg.data(), buf, cap, n_msgs, len, !sparse,
+                               &d.rej);
+  if (rc != KSG_OK) return rc;
+  d.valid = true;
+  *code = d.code.data();
+  *msg = d.msg.data();
+  return KSG_OK;
+}
+
+int ksg_snapshot_statuses_kept_stats(ksg_snapshot* s, int64_t* sparse_calls, int64_t* dense_calls) {
+  if (!s) return KSG_E_INVALID;
+  if (sparse_calls) *sparse_calls = s->skept.sparse_calls;
+  if (dense_calls) *dense_calls = s->skept.dense_calls;
+  return KSG_OK;
 }
 
 static int statuses_impl(ksg_snapshot* s, int32_t pod, const uint32_t* words, int32_t n_nodes, int32_t* code,

@@ -393,8 +393,11 @@ class Snapshot:
         self._profile_info = f("profile_info", C.c_int, vp, C.POINTER(ProfileInfo))
         self._statuses = f("statuses", C.c_int, vp, i32, C.POINTER(C.c_uint32), i32, C.POINTER(i32),
                            C.POINTER(i32), C.c_char_p, i64, C.POINTER(i32), C.POINTER(i64))
-        self._statuses_delta = f("statuses_delta", C.c_int, vp, i32, C.POINTER(C.c_uint32), i32, C.POINTER(i32),
-                                 C.POINTER(i32), C.c_char_p, i64, C.POINTER(i32), C.POINTER(i64))
+        self._statuses_kept = f("statuses_kept", C.c_int, vp, i32, C.POINTER(C.c_uint32), i32,
+                                C.POINTER(C.POINTER(i32)), C.POINTER(C.POINTER(i32)), C.c_char_p, i64,
+                                C.POINTER(i32), C.POINTER(i64))
+        self._kept_stats = f("statuses_kept_stats", C.c_int, vp, C.POINTER(i64), C.POINTER(i64))
+        self._clear_storage = f("clear_storage", C.c_int, vp)
         self.h = vp()
         k = _Keep()
         rc = self._new(C.byref(profile_view(prof, k)), C.byref(self.h))
@@ -454,6 +457,11 @@ class Snapshot:
         for c in st.pvcs.values():
             k = _Keep()
             self._check(self._add_pvc(self.h, C.byref(pvc_view(c, k))), "add_pvc")
+
+    def clear_storage(self) -> None:
+        """ksg_snapshot_clear_storage: drop every PV, claim and StorageClass
+        (a lister resync: clear, then add_storage of what is left)."""
+        self._check(self._clear_storage(self.h), "clear_storage")
 
     def prefilter_message(self, pod: int, plugin: int) -> str:
         """ksg_snapshot_prefilter_message: the plugin's PreFilter rejection ("" none)."""
@@ -604,6 +612,33 @@ class Snapshot:
             self._check(self._statuses(*args, buf, len(buf), C.byref(nm), C.byref(ln)), "statuses")
         texts = buf.raw[:ln.value].split(b"\0")[:nm.value]
         return code, msg, [t.decode("utf-8") for t in texts]
+
+    def statuses_kept(self, pod: int, words) -> Tuple[np.ndarray, np.ndarray, List[str]]:
+        """ksg_snapshot_statuses_kept: ksg_snapshot_statuses into the
+        snapshot's own arrays (only the previous and the current rejected
+        nodes written when the last call rejected few); returns copies."""
+        w = np.ascontiguousarray(words, np.uint32)
+        n = len(w)
+        pc, pm = C.POINTER(i32)(), C.POINTER(i32)()
+        nm, ln = i32(), i64()
+        buf = getattr(self, "_status_buf", None)
+        if buf is None:
+            buf = self._status_buf = C.create_string_buffer(1 << 16)
+        args = (self.h, pod, w.ctypes.data_as(C.POINTER(C.c_uint32)), n, C.byref(pc), C.byref(pm))
+        self._check(self._statuses_kept(*args, buf, len(buf), C.byref(nm), C.byref(ln)), "statuses_kept")
+        if ln.value > len(buf):   # the arrays already hold this call's output; the texts once more
+            buf = self._status_buf = C.create_string_buffer(ln.value)
+            self._check(self._statuses_kept(*args, buf, len(buf), C.byref(nm), C.byref(ln)), "statuses_kept")
+        code = np.ctypeslib.as_array(pc, (n,)).copy() if n else np.zeros(0, np.int32)
+        msg = np.ctypeslib.as_array(pm, (n,)).copy() if n else np.zeros(0, np.int32)
+        texts = buf.raw[:ln.value].split(b"\0")[:nm.value]
+        return code, msg, [t.decode("utf-8") for t in texts]
+
+    def statuses_kept_stats(self) -> Tuple[int, int]:
+        """(sparse, dense) ksg_snapshot_statuses_kept calls so far."""
+        a, b = i64(), i64()
+        self._check(self._kept_stats(self.h, C.byref(a), C.byref(b)), "statuses_kept_stats")
+        return a.value, b.value
 
     def prefilter(self, pod: int, plugin: int, result_status: int = 0):
         """(code, node names or None) of plugin's PreFilter for the pod."""

@@ -158,6 +158,12 @@ func (e *Evaluator) attach(h framework.Handle) {
 			if err != nil {
 				return err
 			}
+			// the listers' state replaces the snapshot's: a deleted PV / claim /
+			// class leaves it (a pod naming a deleted claim is then rejected at
+			// PreFilter, as upstream's lister lookup rejects it)
+			if err := snap.ClearStorage(); err != nil {
+				return err
+			}
 			for _, sc := range scs {
 				if err := snap.AddStorageClass(sc); err != nil {
 					return err
@@ -221,8 +227,9 @@ func (e *Evaluator) markStorage() {
 
 // syncStorage (under mu) hands the PVs, claims and classes to the snapshot
 // when one changed (or at a rebuild): pods with claims resolve against them.
-// A deleted object stays in the snapshot until the next rebuild; the claims
-// that named it are then unresolved, as upstream's listers would have them.
+// The snapshot's storage is cleared first, so a deleted object leaves it at
+// the next sync and the claims that named it are unresolved, as upstream's
+// listers would have them.
 func (e *Evaluator) syncStorage(force bool) error {
 	e.side.Lock()
 	dirty, sync := e.stDirty || force, e.stSync

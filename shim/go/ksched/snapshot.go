@@ -593,6 +593,13 @@ func (x *Snapshot) AddPVC(c *v1.PersistentVolumeClaim) error {
 	return x.check(C.ksg_snapshot_add_pvc(x.s, v))
 }
 
+// ClearStorage drops every PV, claim and StorageClass
+// (ksg_snapshot_clear_storage): a lister resync clears, then re-adds what the
+// listers hold, so deleted objects leave the snapshot.
+func (x *Snapshot) ClearStorage() error {
+	return x.check(C.ksg_snapshot_clear_storage(x.s))
+}
+
 // AddStorageClass adds or replaces a StorageClass (snapshot.go:36).
 func (x *Snapshot) AddStorageClass(sc *storagev1.StorageClass) error {
 	var a arena
@@ -682,37 +689,38 @@ func (x *Snapshot) Status(pod int, word uint32, node int) (int, string, error) {
 	return int(code), C.GoString(buf), nil
 }
 
-// StatusesInto is Statuses into slices the caller keeps from cycle to cycle
-// (ksg_snapshot_statuses_delta): while codes and msg are the slices of this
-// Snapshot's previous StatusesInto call, untouched since, only the nodes that
-// call rejected and the nodes this one rejects are written.
-func (x *Snapshot) StatusesInto(pod int, words []uint32, codes, msg []int32) (msgs []string, err error) {
+// StatusesKept is Statuses into arrays the C snapshot owns and keeps across
+// calls (ksg_snapshot_statuses_kept): when the previous call rejected few
+// nodes, only that call's and this call's rejected nodes are written.  codes
+// and msg alias C memory: they are read-only and valid until the next
+// StatusesKept call or Free, so a caller that keeps them past the cycle (in
+// CycleState) copies them first.
+func (x *Snapshot) StatusesKept(pod int, words []uint32) (codes, msg []int32, msgs []string, err error) {
 	n := len(words)
-	if n == 0 || len(codes) < n || len(msg) < n {
-		c, m, t, e := x.Statuses(pod, words)
-		copy(codes, c)
-		copy(msg, m)
-		return t, e
+	if n == 0 {
+		return x.Statuses(pod, words)
 	}
 	if len(x.msgBuf) == 0 {
 		x.msgBuf = make([]byte, 1<<16)
 	}
 	var nm C.int32_t
 	var ln C.int64_t
+	var pc, pm *C.int32_t
 	call := func() error {
-		return x.check(C.ksg_snapshot_statuses_delta(x.s, C.int32_t(pod), (*C.uint32_t)(unsafe.Pointer(&words[0])),
-			C.int32_t(n), (*C.int32_t)(unsafe.Pointer(&codes[0])), (*C.int32_t)(unsafe.Pointer(&msg[0])),
-			(*C.char)(unsafe.Pointer(&x.msgBuf[0])), C.int64_t(len(x.msgBuf)), &nm, &ln))
+		return x.check(C.ksg_snapshot_statuses_kept(x.s, C.int32_t(pod), (*C.uint32_t)(unsafe.Pointer(&words[0])),
+			C.int32_t(n), &pc, &pm, (*C.char)(unsafe.Pointer(&x.msgBuf[0])), C.int64_t(len(x.msgBuf)), &nm, &ln))
 	}
 	if err = call(); err != nil {
-		return nil, err
+		return nil, nil, nil, err
 	}
 	if int64(ln) > int64(len(x.msgBuf)) { // the texts did not fit: once more (the arrays already hold this call's output)
 		x.msgBuf = make([]byte, int64(ln)+1)
 		if err = call(); err != nil {
-			return nil, err
+			return nil, nil, nil, err
 		}
 	}
+	codes = unsafe.Slice((*int32)(unsafe.Pointer(pc)), n)
+	msg = unsafe.Slice((*int32)(unsafe.Pointer(pm)), n)
 	raw := x.msgBuf[:ln]
 	msgs = make([]string, 0, int(nm))
 	start := 0
@@ -722,7 +730,7 @@ func (x *Snapshot) StatusesInto(pod int, words []uint32, codes, msg []int32) (ms
 			start = i + 1
 		}
 	}
-	return msgs, nil
+	return codes, msg, msgs, nil
 }
 
 // Statuses decodes every node's Filter status word of a pod at once

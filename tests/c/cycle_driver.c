@@ -3,8 +3,8 @@
  * so the measured cost is the C ABI's alone (no Python / ctypes in the loop):
  *
  *   ksg_snapshot_add_pod -> ksg_snapshot_sync -> ksg_eval_view (the rows
- *   in library memory) -> ksg_snapshot_statuses_delta (the shim's buffers kept
- *   across cycles) -> ksg_snapshot_assume
+ *   in library memory) -> ksg_snapshot_statuses_kept (the snapshot's arrays,
+ *   kept across cycles) -> ksg_snapshot_assume
  *
  * hint_ahead > 0: cycle i first announces pod i + hint_ahead
  * (ksg_snapshot_hint_pod, timed with add_pod), as the Go shim's pod informer
@@ -54,8 +54,10 @@ int cycle_run(ksg_snapshot* s, ksg_ctx* ctx, const ksg_pod_view* views, int32_t 
     const int64_t t2 = now_ns();
     if ((rc = ksg_eval_view(ctx, idx, &r, rows))) { *where = 2; break; }
     const int64_t t3 = now_ns();
-    if ((rc = (dense ? ksg_snapshot_statuses : ksg_snapshot_statuses_delta)(s, idx, rows->fstatus, n_nodes, code, msg, buf,
-                                                                           cap_bytes, &n_msgs, &len))) {
+    const int32_t *kcode = NULL, *kmsg = NULL;
+    if ((rc = dense ? ksg_snapshot_statuses(s, idx, rows->fstatus, n_nodes, code, msg, buf, cap_bytes, &n_msgs, &len)
+                    : ksg_snapshot_statuses_kept(s, idx, rows->fstatus, n_nodes, &kcode, &kmsg, buf, cap_bytes,
+                                                 &n_msgs, &len))) {
       *where = 3;
       break;
     }
