@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define KSG_ABI_VERSION 3
+#define KSG_ABI_VERSION 4
 
 #define KSG_OK 0
 #define KSG_E_INVALID (-1)     /* bad argument / inconsistent sizes            */
@@ -280,8 +280,19 @@ typedef struct ksg_eval_rows {
   int32_t elem_bytes;
   const uint32_t* fstatus;                /* [n_nodes] Filter status words */
   const void* raw[KSG_NPLUGINS];
-  const void* norm[KSG_NPLUGINS];
-  const void* total;                      /* [n_nodes] weighted totals (0: not scored) */
+  const void* norm[KSG_NPLUGINS];         /* NULL for a plugin in norm_from_raw */
+  const void* total;                      /* [n_nodes] weighted totals (0: not scored); NULL when the
+                                           * evaluation did not materialise them (the node-local per-cycle
+                                           * kernel: the framework sums the weights itself) */
+  /* Normalised rows the caller derives (round 6: the node-local per-cycle
+   * kernel no longer stores them): for plugin p in norm_from_raw, at a
+   * feasible node of a scored pod (p in norm_scored), DefaultNormalizeScore
+   * of raw[p] with the maximum norm_max[p] over the feasible nodes:
+   * TaintToleration (reverse) max ? 100 - 100 * raw / max : 100,
+   * NodeAffinity max ? 100 * raw / max : raw (integer division); 0 elsewhere. */
+  uint32_t norm_from_raw;
+  uint32_t norm_scored;
+  int64_t norm_max[KSG_NPLUGINS];
 } ksg_eval_rows;
 /* ksg_eval with the rows left in library memory (the per-cycle call of the Go
  * shim; replaces the framework's per-(pod, node, plugin) Filter / Score /
@@ -349,10 +360,21 @@ int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
  * checked narrow forms that ran (exact either way; for tests and reports). */
 #define KSG_RUN_NARROW_SWEEP 1   /* replica sweep on the 16-byte records */
 #define KSG_RUN_SLOT32 2         /* slot walk with 32-bit Fit / BalancedAllocation */
-#define KSG_RUN_TCOL 4           /* phase 2 was the transposed walk (ksg_batch_phase2t) */
+/* 4: the transposed walk (KSG_RUN_TCOL, retired in ABI 4) */
 #define KSG_RUN_SPEC 8           /* phase 2 was the speculate-and-verify walk (ksg_batch_phase2v) */
 #define KSG_RUN_WIDE_MEM 16      /* ... in its wide-memory instance (memory not whole MiB: int64 bytes) */
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
+
+/* Grid-barrier timeouts this context recovered from since it opened.  The
+ * chip-wide topology path, the multi-workgroup replica sweep and the
+ * per-cycle kernels launch plainly with a grid inside the occupancy API's
+ * co-resident count and bound their barrier polls; a timeout (a workgroup was
+ * not resident) restores the node state the call started from (a topology
+ * queue's partial commits included), switches the context to cooperative
+ * launches and runs the same call again, so the caller sees the exact
+ * result.  A timeout under a cooperative launch is KSG_E_DEVICE.  (No
+ * reference counterpart: device residency.) */
+int ksg_recoveries(ksg_ctx* ctx, int32_t* n);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event
  * record per launch).  With timing on, ksg_kernel_stats() returns, per kernel
@@ -367,22 +389,16 @@ enum {
   KSG_K_QUEUE_TOPO = 1,
   KSG_K_BATCH_PHASE1 = 2,
   KSG_K_BATCH_TOPK = 3,
-  KSG_K_BATCH_PHASE2 = 4,
-  KSG_K_BATCH_PHASE2_SCAN = 5,
-  KSG_K_BATCH_PHASE2S = 6,
-  KSG_K_SWEEP_STATIC = 7,
-  KSG_K_SWEEP = 8,
-  KSG_K_TOPO_COOP = 9,
-  KSG_K_BATCH_PHASE2P = 10,
-  KSG_K_SWEEP_NARROW = 11,
-  KSG_K_CAPTURE_EVAL = 12,
-  KSG_K_CAPTURE_NORM = 13,
-  KSG_K_BATCH_PHASE2T = 14,
-  KSG_K_BATCH_TRANSPOSE = 15,
-  KSG_K_TCOL_CARRY = 16,
-  KSG_K_EVAL_CYCLE = 17,
-  KSG_K_BATCH_PHASE2V = 18,
-  KSG_NKERNELS = 19
+  KSG_K_BATCH_PHASE2S = 4,
+  KSG_K_SWEEP_STATIC = 5,
+  KSG_K_SWEEP = 6,
+  KSG_K_TOPO_COOP = 7,
+  KSG_K_SWEEP_NARROW = 8,
+  KSG_K_CAPTURE_EVAL = 9,
+  KSG_K_CAPTURE_NORM = 10,
+  KSG_K_EVAL_CYCLE = 11,
+  KSG_K_BATCH_PHASE2V = 12,
+  KSG_NKERNELS = 13
 };
 typedef struct ksg_kernel_stat {
   char name[48];

@@ -156,34 +156,29 @@ struct ksg_ctx {
   TopoTables pct{};
   bool pct_valid = false;
   bool pc_tables = true;
-  bool cycle_early = true;            // ... writes its phase-2 rows after barrier 2
-  bool cycle_last = true;             // the one-pod topology evaluation completes on its last arrival
-  bool commit_args = true;            // ksg_commit's kernel takes the pod's commit program by value
-  bool topo_stage = true;             // ... and reads a staged append in place (KSG_TOPO_STAGE=0: copies first)
   unsigned* sweep_timeout = nullptr;  // the last replica sweep's group-barrier timeout word (S > 1)
   int force_path = 0;  // env KSG_FORCE_PATH: 1 queue kernel, 2 batched, 3 int64 sweep state
   bool last_narrow = false;   // the last replica sweep ran on the narrow records
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
-  bool last_tcol = false;     // the last batched run's phase 2 was the transposed walk
   bool last_spec = false;     // ... the speculate-and-verify walk
   bool last_mw = false;       // ... in its wide-memory instance
   bool pipe_overlap = true;   // env KSG_PIPE_OVERLAP=0: the window pipeline on one stream (same arithmetic;
                               // for counter passes, which serialise kernels: a walk polling for the
                               // other stream's top-k would wait out its poll bound)
-  uint64_t* d_rect = nullptr; // transposed walk: node-major record / static copies
-  int32_t* d_statt = nullptr;
-  uint64_t* d_prect[2] = {nullptr, nullptr};   // the same, per window parity
-  int32_t* d_pstatt[2] = {nullptr, nullptr};
-  uint32_t* d_tccol = nullptr;                 // carried columns [64][64]
-  uint64_t* d_tcinit = nullptr;                // TcInit [64] (4 words each)
+  uint64_t* d_prect[2] = {nullptr, nullptr};   // the spec walk: node-major record copies, per window parity
+  int32_t* d_pimgt[2] = {nullptr, nullptr};    // ... and weight x ImageLocality
   unsigned* d_flag = nullptr; // range-check flag (ksg_range32)
-  // env KSG_BATCH_MODE: 0 "scan", 1 "topset", 2 "slot", 4 "window", 5 "tcol" (the transposed
-  // walk where the N32 check and tcol_candidate pass, else the slot walk), 6 "spec"
+  // env KSG_BATCH_MODE: 2 "slot" (one launch chain per batch), 4 "window" (the
+  // slot walk in the two-stream pipeline), 6 "spec" (default: the
+  // speculate-and-verify walk in the pipeline, the window slot walk outside
+  // its scope).  Round 6 retired "scan", "topset" and "tcol" (never faster
+  // than the window walk; the spec walk superseded them).
   // (default: the speculate-and-verify walk where the N32 check and spec_candidate pass,
   // else the window slot walk; both with the next batch's phase 1 + top-k overlapped
   // through the two-batch window)
   int batch_mode = 6;
-  int slot_block = 64;   // env KSG_SLOT_BLOCK: lanes (= max batch) of ksg_batch_phase2s: 64, 128, 256 (64: the window walk at 64-pod batches, 2 waves, 416 k vs 408 k pods/s at 128, profiles/r2/phase2_window_blocks.log)
+  int slot_block = 64;   // env KSG_SLOT_BLOCK: pods per batch of the unwindowed slot walk: 64 or 128 (the window walk
+                         // runs 64-pod batches, 416 k vs 408 k pods/s at 128, profiles/r2/phase2_window_blocks.log)
   // per-kernel timing (ksg_set_timing): one event before the first and after
   // every launch of a run, on the launch stream
   bool timing = false;
@@ -232,9 +227,6 @@ struct ksg_ctx {
   hipEvent_t json_copied[kJsonSlots] = {};  // the slot's copy-back done
   hipEvent_t json_written = nullptr;
   hipStream_t json_stream = nullptr;        // the copies back
-  hipStream_t json_stream2 = nullptr;       // the second half of a split copy (a second DMA engine)
-  hipEvent_t json_half = nullptr;
-  int json_split = 0;                       // KSG_JSON_SPLIT=1: the copy back in two halves on two streams
   bool json_busy[kJsonSlots] = {};
   int json_next = 0;
   int json_last = -1;                       // the slot the last ksg_run_queue_json_async filled
@@ -245,6 +237,16 @@ struct ksg_ctx {
   bool ev_prof_dirty = true;
   bool eval_fast = true;                    // env KSG_EVAL_FAST=0: ksg_eval takes the queue kernel
   int inject_walk_err = 0;                  // env KSG_TEST_INJECT_WALK_ERR=1 (tests: the walk's guard reaches the host)
+  // env KSG_TEST_INJECT_TIMEOUT (tests): a mask of grid-barrier launches whose
+  // next plain launch starts with its sticky timeout word set, so its barriers
+  // give up as if a workgroup were not resident (partial commits included):
+  // 1 the topology queue, 2 the one-pod topology evaluation, 4 the replica
+  // sweep (S > 1), 8 the per-cycle launch.  Each bit is consumed by its
+  // launch.
+  int inject_timeout = 0;
+  int32_t recoveries = 0;                   // grid-barrier timeouts recovered by a cooperative relaunch
+  char* d_state_bak = nullptr;              // the node state before a plain topology queue launch (its
+  size_t state_bak_bytes = 0;               // timeout restores it and relaunches cooperatively)
   CycArgs cyc_args{};                       // ksg_eval_cycle's launch arguments, rebuilt in place per call
   unsigned cyc_last_G = 0;                  // the grid of the last per-cycle call (its counter counts multiples of it)
   // the persistent per-cycle server (env KSG_CYCLE_SERVER=1, ksched_cycle.h ksg_cycle_server)
@@ -261,7 +263,6 @@ struct ksg_ctx {
   int cycle_kn = 1;                         // env KSG_CYCLE_KN (1/2/4): the smallest nodes-per-lane tried (tests)
   bool cycle_sys = true;                    // system-scope host stores + a vmcnt wait (no L2 write-back); env
                                             // KSG_CYCLE_SYS=0: plain stores + __threadfence_system (round 4)
-  int cycle_es = 0;                         // env KSG_CYCLE_ES=2/4/8: force the row width (measurements)
   bool cycle_coop = false;                  // per-cycle launch: plain (G within the occupancy API's residency,
                                             // ~7 us less host time); cooperative after an exchange timeout,
                                             // or always with env KSG_CYCLE_COOP=1
@@ -348,12 +349,8 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_rec = nullptr;
   ctx->d_img = nullptr;
   ctx->d_stat = nullptr;
-  ctx->d_rect = nullptr;
-  ctx->d_statt = nullptr;
   ctx->d_prect[0] = ctx->d_prect[1] = nullptr;
-  ctx->d_pstatt[0] = ctx->d_pstatt[1] = nullptr;
-  ctx->d_tccol = nullptr;
-  ctx->d_tcinit = nullptr;
+  ctx->d_pimgt[0] = ctx->d_pimgt[1] = nullptr;
   ctx->d_pmax = nullptr;
   ctx->d_p1 = nullptr;
   ctx->d_top = nullptr;
@@ -375,6 +372,8 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_coop_srec = nullptr;
   ctx->d_tables = nullptr;
   ctx->tables_words = 0;
+  ctx->d_state_bak = nullptr;
+  ctx->state_bak_bytes = 0;
   ctx->d_pct = nullptr;
   ctx->pct_words = 0;
   ctx->pct_valid = false;
@@ -394,11 +393,9 @@ void free_all(ksg_ctx* ctx) {
 
 // ---- per-kernel timing -------------------------------------------------------
 const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_batch_phase1",
-                                          "ksg_batch_topk", "ksg_batch_phase2", "ksg_batch_phase2_scan",
-                                          "ksg_batch_phase2s", "ksg_sweep_static", "ksg_sweep",
-                                          "ksg_topo_coop", "ksg_batch_phase2p", "ksg_sweep_narrow",
-                                          "ksg_capture_eval", "ksg_capture_norm", "ksg_batch_phase2t",
-                                          "ksg_batch_transpose", "ksg_tcol_carry", "ksg_eval_cycle",
+                                          "ksg_batch_topk", "ksg_batch_phase2s", "ksg_sweep_static",
+                                          "ksg_sweep", "ksg_topo_coop", "ksg_sweep_narrow",
+                                          "ksg_capture_eval", "ksg_capture_norm", "ksg_eval_cycle",
                                           "ksg_batch_phase2v"};
 
 int tmark(ksg_ctx* ctx) {
@@ -624,15 +621,17 @@ struct Tmp {
     if (_e != hipSuccess) return fail(ctx, KSG_E_NOMEM, hipGetErrorString(_e));        \
   } while (0)
 
-// ksg_batch_phase2s instances: (RM 4 | KSG_MAX_RES) x (64 | 128 | 256 lanes)
-static const std::array<const void*, 9>& slot_kernels() {
-  static const std::array<const void*, 9> k = {
+// ksg_batch_phase2s instances: (RM 4 | KSG_MAX_RES | 4 with N32) x (64 | 128 lanes)
+static const std::array<const void*, 6>& slot_kernels() {
+  static const std::array<const void*, 6> k = {
       (const void*)ksg_batch_phase2s<4, 64>,           (const void*)ksg_batch_phase2s<4, 128>,
-      (const void*)ksg_batch_phase2s<4, 256>,          (const void*)ksg_batch_phase2s<KSG_MAX_RES, 64>,
-      (const void*)ksg_batch_phase2s<KSG_MAX_RES, 128>, (const void*)ksg_batch_phase2s<KSG_MAX_RES, 256>,
-      (const void*)ksg_batch_phase2s<4, 64, true>,     (const void*)ksg_batch_phase2s<4, 128, true>,
-      (const void*)ksg_batch_phase2s<4, 256, true>};
+      (const void*)ksg_batch_phase2s<KSG_MAX_RES, 64>, (const void*)ksg_batch_phase2s<KSG_MAX_RES, 128>,
+      (const void*)ksg_batch_phase2s<4, 64, true>,     (const void*)ksg_batch_phase2s<4, 128, true>};
   return k;
+}
+// index into slot_kernels(): the instance for (n32, RM, lanes <= 128)
+static int slot_kernel_index(bool n32, int slot_rm, int lanes) {
+  return (n32 ? 4 : slot_rm == 4 ? 0 : 2) + (lanes <= 64 ? 0 : 1);
 }
 
 bool profile_cm_fast(const ksg_profile& prof);
@@ -722,31 +721,14 @@ int decide_mw(ksg_ctx* ctx, int32_t first, int32_t count, bool* mw) {
 // LDS budget attribute of the phase-2 instances (once per process)
 int set_phase2_attrs(ksg_ctx* ctx, size_t budget) {
   int rc;
-  if ((rc = func_lds_attr(ctx, (const void*)ksg_batch_phase2, budget))) return rc;
-  if ((rc = func_lds_attr(ctx, (const void*)ksg_batch_phase2_scan<512>, budget))) return rc;
   for (const void* f : slot_kernels())
     if ((rc = func_lds_attr(ctx, f, budget))) return rc;
   return KSG_OK;
 }
 
-// ksg_batch_phase2t instances: P = 1 (<= 64 pods per batch), 2 (<= 128)
-static const std::array<const void*, 2>& tcol_kernels() {
-  static const std::array<const void*, 2> k = {(const void*)ksg_batch_phase2t<1>, (const void*)ksg_batch_phase2t<2>};
-  return k;
-}
-constexpr size_t kTcolLds = 128 * 1024;   // dynamic LDS of the transposed walk (static part ~14 KB)
 constexpr size_t kSpecLds = 130 * 1024;   // ... of the speculate-and-verify walk (static part ~16 KB): the
                                           // launch always asks for all of it, so that no other kernel's
                                           // workgroup shares the walk's CU
-
-// Host half of the transposed walk's scope (ksched_phase2t.h): on top of the
-// N32 check, every weighted total fits the column word's 14 bits.
-bool tcol_candidate(const ksg_ctx* ctx) {
-  int64_t wsum = 0;
-  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
-    if ((ctx->prof.score_mask >> pl) & 1u) wsum += ctx->prof.weight[pl];
-  return ctx->c.R <= 4 && wsum * 100 < (1 << 14);
-}
 
 // Host half of the speculate-and-verify walk's scope (ksched_phase2v.h): on top
 // of the N32 check, every weighted total fits the column word's 27 bits.
@@ -760,9 +742,8 @@ bool spec_candidate(const ksg_ctx* ctx) {
 int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const CapArgs* cap,
                 const ksg_profile* d_prof) {
   const int N = ctx->c.N;
-  // the window mode (4) runs its slot walk here without the pipeline (capture
-  // runs); the transposed walk (5) falls back to the slot walk out of its scope
-  const int bmode = ctx->batch_mode >= 4 ? 2 : ctx->batch_mode;
+  // the slot walk, one launch chain per batch (captured queues, the "slot"
+  // mode, the window pipeline off)
   if (!ctx->d_rec) {
     int rc;
     if ((rc = dalloc(ctx, &ctx->d_rec, (size_t)KSG_BATCH_MAX * N))) return rc;
@@ -800,45 +781,28 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   constexpr size_t kLdsBudget = 120 * 1024;
   const size_t cm_words = (size_t)((((N + 31) / 32) + 3) & ~3);
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;   // ksg_batch_phase2s<RM> instance
-  const size_t slot_bytes = bmode == 2 ? 8 * (size_t)(2 * slot_rm + 10) : 8 * (size_t)(2 * ctx->c.R + 4);
-  const bool topset = bmode >= 1;   // top-set variants keep one slot per pod
   {
     int rc;
     if ((rc = set_phase2_attrs(ctx, kLdsBudget))) return rc;
   }
   bool n32 = false;
-  if (bmode == 2) {
+  {
     int rc;
     if ((rc = decide_n32(ctx, first, count, &n32))) return rc;
   }
   b.stat = n32 ? ctx->d_stat : nullptr;
-  const bool tcol = ctx->batch_mode == 5 && n32 && tcol_candidate(ctx);
-  if (tcol)
-    for (const void* f : tcol_kernels()) {
-      int rc;
-      if ((rc = func_lds_attr(ctx, f, kTcolLds))) return rc;
-    }
-  ctx->last_tcol = tcol;
   ctx->last_spec = false;
   ctx->last_mw = false;
-  if (tcol && !ctx->d_rect) {
-    int rc;
-    if ((rc = dalloc(ctx, &ctx->d_rect, (size_t)128 * N))) return rc;
-    if ((rc = dalloc(ctx, &ctx->d_statt, (size_t)128 * N))) return rc;
-  }
-  b.rect = ctx->d_rect;
-  b.statt = ctx->d_statt;
   (void)hipGetLastError();
   treset(ctx);
   HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
   int trc;
   if ((trc = tmark(ctx))) return trc;
   for (int off = 0; off < count;) {
-    int nb = std::min(bmode == 2 ? (tcol ? std::min(ctx->slot_block, 128) : ctx->slot_block) : KSG_BATCH_MAX,
-                      count - off);
+    int nb = std::min(ctx->slot_block, count - off);
     int64_t lo = 0, hi = 0;
     size_t bytes = 0;
-    const size_t budget = tcol ? kTcolLds : kLdsBudget;
+    const size_t budget = kLdsBudget;
     for (;;) {
       lo = ctx->h_pods[first + off].blob;
       hi = lo;
@@ -848,9 +812,7 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
         hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
       }
       const size_t words = (cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3;
-      // the transposed walk: one slot row per pod + the [slot][pod] column store
-      bytes = 4 * words + (tcol ? (size_t)nb * slot_bytes + (size_t)nb * (nb > 64 ? 128 : 64) * 4
-                                : topset ? (size_t)nb * slot_bytes : 0);
+      bytes = 4 * words;
       if (bytes <= budget || nb == 1) break;
       nb = std::max(1, nb / 2);
     }
@@ -863,30 +825,12 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
     const double units = (double)b.nb * N;   // (pod, node) pairs of the batch
     hipLaunchKernelGGL(ksg_batch_phase1, dim3((N + 255) / 256, b.nb), dim3(256), 0, ctx->stream, b);
     if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return trc;
-    if (topset) {
-      hipLaunchKernelGGL(ksg_batch_topk<1024>, dim3(b.nb), dim3(1024), 0, ctx->stream, b);
-      if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
-      // units: top-set entries + changed-node records read, Σ_j (j + 1) <= nb (nb + 1) / 2
-      if (tcol) {
-        b.qs = b.nb > 64 ? 128 : 64;
-        hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, ctx->stream, b);
-        if ((trc = tlaunched(ctx, KSG_K_BATCH_TRANSPOSE, units))) return trc;
-        hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(tcol_kernels()[b.nb > 64 ? 1 : 0])),
-                           dim3(1), dim3(64), bytes, ctx->stream, b);
-        if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2T, 0.5 * b.nb * (b.nb + 1)))) return trc;
-      } else if (bmode == 2) {
-        const int si = (n32 ? 6 : slot_rm == 4 ? 0 : 3) + (ctx->slot_block == 64 ? 0 : ctx->slot_block == 128 ? 1 : 2);
-        hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(slot_kernels()[si])), dim3(1),
-                           dim3(ctx->slot_block), bytes, ctx->stream, b);
-        if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2S, 0.5 * b.nb * (b.nb + 1)))) return trc;
-      } else {
-        hipLaunchKernelGGL(ksg_batch_phase2, dim3(1), dim3(kP2Block), bytes, ctx->stream, b);
-        if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2, 0.5 * b.nb * (b.nb + 1)))) return trc;
-      }
-    } else {
-      hipLaunchKernelGGL(ksg_batch_phase2_scan<512>, dim3(1), dim3(512), bytes, ctx->stream, b);
-      if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2_SCAN, units))) return trc;
-    }
+    hipLaunchKernelGGL(ksg_batch_topk<1024>, dim3(b.nb), dim3(1024), 0, ctx->stream, b);
+    if ((trc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return trc;
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(
+                           const_cast<void*>(slot_kernels()[slot_kernel_index(n32, slot_rm, ctx->slot_block)])),
+                       dim3(1), dim3(ctx->slot_block), bytes, ctx->stream, b);
+    if ((trc = tlaunched(ctx, KSG_K_BATCH_PHASE2S, 0.5 * b.nb * (b.nb + 1)))) return trc;
     if (cap) {   // the batch's capture, on the post-batch state (ksched_capture.h)
       CapArgs ca = *cap;
       ca.b0 = b.b0;
@@ -916,7 +860,6 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
 int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const ksg_profile* d_prof) {
   const int N = ctx->c.N;
   int rc;
-  ctx->last_tcol = false;
   ctx->last_spec = false;
   ctx->last_mw = false;
   if (!ctx->d_prec[0]) {
@@ -945,14 +888,11 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   const bool window = ctx->pipe_window != 0;
   const bool overlap = window && !ctx->timing && ctx->pipe_overlap;
   const int slot_rm = ctx->c.R <= 4 ? 4 : KSG_MAX_RES;
-  // mode 4: the slot walk inside this pipeline (one lane per slot); mode 5:
-  // the transposed walk (ksched_phase2t.h) with the previous batch's nodes as
-  // carried columns, 64-pod batches, else the slot walk.  (The round-2
-  // two-version walk and a round-3 one-wave walk with two slots per lane, both
-  // measured slower, were removed.)
+  // mode 4: the slot walk inside this pipeline (one lane per slot).  (The
+  // round-2 two-version walk, a round-3 one-wave walk with two slots per lane
+  // and the transposed walk, all measured no faster, were removed.)
   bool n32 = false, mw = false;
   if (ctx->batch_mode >= 4 && (rc = decide_n32(ctx, first, count, &n32))) return rc;
-  const bool tcolw = ctx->batch_mode == 5 && window && n32 && tcol_candidate(ctx);
   // mode 6: the speculate-and-verify walk (ksched_phase2v.h), N32 scope, 64-pod
   // batches; memory outside the N32 ranges (not whole MiB, as kubelets report
   // it, or too large) takes its wide-memory instance (MW: memory in int64
@@ -960,34 +900,27 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   if (ctx->batch_mode == 6 && window && !n32 && spec_candidate(ctx) && (rc = decide_mw(ctx, first, count, &mw)))
     return rc;
   const bool specw = ctx->batch_mode == 6 && window && (n32 || mw) && spec_candidate(ctx);
-  ctx->last_tcol = tcolw;
   ctx->last_spec = specw;
   ctx->last_mw = specw && mw;
   const void* spec_kern = mw ? (const void*)ksg_batch_phase2v<64 * kSvWaves, true>
                              : (const void*)ksg_batch_phase2v<64 * kSvWaves, false>;
-  if ((tcolw || specw) && !ctx->d_prect[0]) {
+  if (specw && !ctx->d_prect[0]) {   // the node-major copies phase 1 writes (records, ImageLocality)
     for (int q = 0; q < 2; q++) {
       if ((rc = dalloc(ctx, &ctx->d_prect[q], (size_t)64 * N))) return rc;
-      if ((rc = dalloc(ctx, &ctx->d_pstatt[q], (size_t)64 * N))) return rc;
+      if ((rc = dalloc(ctx, &ctx->d_pimgt[q], (size_t)64 * N))) return rc;
     }
   }
   if (specw && (rc = func_lds_attr(ctx, spec_kern, kSpecLds))) return rc;
-  if (tcolw) {
-    if (!ctx->d_tccol) {
-      if ((rc = dalloc(ctx, &ctx->d_tccol, (size_t)64 * 64))) return rc;
-      if ((rc = dalloc(ctx, &ctx->d_tcinit, (size_t)4 * 64))) return rc;
-    }
-    for (const void* f : tcol_kernels())
-      if ((rc = func_lds_attr(ctx, f, kTcolLds))) return rc;
-  }
-  const int B = tcolw || specw ? 64 : window ? std::min(ctx->slot_block, KSG_BATCH_MAX / 2) : ctx->slot_block;
+  // batches: 64 pods in the window (the spec walk, or the slot walk with the
+  // previous batch's 64 slots carried beside this batch's), else slot_block
+  const int B = specw || window ? 64 : ctx->slot_block;
   const int slots = window ? 2 * B : B;   // carried + this batch's slots
-  const int sblock = slots <= 64 ? 64 : slots <= 128 ? 128 : 256;
-  const void* kern = slot_kernels()[(n32 ? 6 : slot_rm == 4 ? 0 : 3) + (sblock == 64 ? 0 : sblock == 128 ? 1 : 2)];
+  const int sblock = slots <= 64 ? 64 : 128;
+  const void* kern = slot_kernels()[slot_kernel_index(n32, slot_rm, sblock)];
   const int block = sblock;
-  const size_t kLdsBudget = tcolw ? kTcolLds : specw ? kSpecLds : 120 * 1024;
+  const size_t kLdsBudget = specw ? kSpecLds : 120 * 1024;
   const size_t slot_bytes = 8 * (size_t)(2 * slot_rm + 10);   // SlotLayout<RM>::STRIDE int64 words
-  if (!tcolw && (rc = set_phase2_attrs(ctx, 120 * 1024))) return rc;   // the slot-walk instances (fallback)
+  if ((rc = set_phase2_attrs(ctx, 120 * 1024))) return rc;   // the slot-walk instances (fallback)
   BatchArgs b{};
   b.c = ctx->c;
   b.st = ctx->st;
@@ -1027,9 +960,6 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
       if (specw)   // row versions + T as node indices ([pod][nb + carried])
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
                 (size_t)kSvSlots * kSvRow * 8 + (size_t)kSvSlots * 64 * 4 + (size_t)64 * (nb + prev_nb) * 4;
-      else if (tcolw)   // slot rows + the [slot][64] column store for this batch's and the carried slots
-        bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
-                (size_t)(nb + prev_nb) * (slot_bytes + 64 * 4);
       else
         bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
                 (size_t)sblock * slot_bytes;
@@ -1045,14 +975,9 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.rec = ctx->d_prec[par];
     b.img = ctx->d_pimg[par];
     b.stat = n32 && !specw ? ctx->d_pstat[par] : nullptr;   // (the spec walk computes its statics)
-    const bool xpose = tcolw;   // the transpose launch (the spec walk's copies come from phase 1)
-    b.rect = xpose || specw ? ctx->d_prect[par] : nullptr;
-    b.statt = xpose ? ctx->d_pstatt[par] : nullptr;
-    b.imgt = specw ? ctx->d_pstatt[par] : nullptr;
+    b.rect = specw ? ctx->d_prect[par] : nullptr;
+    b.imgt = specw ? ctx->d_pimgt[par] : nullptr;
     b.xcd_grid = specw ? 1 : 0;
-    b.qs = 64;
-    b.tc_colinit = ctx->d_tccol;
-    b.tc_init = ctx->d_tcinit;
     b.pmax = ctx->d_ppmax[par];
     b.p1 = ctx->d_pp1[par];
     b.top = ctx->d_ptop[par];
@@ -1062,18 +987,17 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     b.carry_out = window ? ctx->d_carry + par * KSG_BATCH_MAX : nullptr;
     b.carry_out_n = window ? carry_n + par : nullptr;
     const double units = (double)nb * N;
-    // the walk waits for this batch's top-k: the slot walk polls a flag the
-    // last top-k workgroup stores (no cross-stream event in front of it on the
-    // critical stream); the transposed walk's kernels wait on an event
-    // (the speculate-and-verify walk also reads the transpose: the transpose signals)
-    const bool tk_flag = overlap && !tcolw;
+    // the walk waits for this batch's top-k: it polls a flag the last top-k
+    // workgroup stores (no cross-stream event in front of it on the critical
+    // stream)
+    const bool tk_flag = overlap;
     b.tk_arrive = tk_flag ? tk : nullptr;
     b.tk_done = tk_flag ? tk + 1 : nullptr;
     b.tk_timeout = tk_flag ? tk + 2 : nullptr;
     b.walk_err = tk + 3;
     b.inject_walk_err = ctx->inject_walk_err;
     b.tk_seq = (unsigned)bi + 1;
-    BatchArgs bt = b;   // the top-k launch: signals (no transpose follows it in the spec walk)
+    BatchArgs bt = b;   // the top-k launch: signals
     bt.tk_sc = specw && tk_flag ? 1 : 0;
     b.tk_sc = bt.tk_sc;
     // phase 1 of batch b reads the state as of the end of batch b - 2 at least,
@@ -1086,25 +1010,10 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE1, units))) return rc;
     hipLaunchKernelGGL(ksg_batch_topk<1024>, dim3(nb), dim3(1024), 0, s1, bt);
     if ((rc = tlaunched(ctx, KSG_K_BATCH_TOPK, units))) return rc;
-    if (xpose) {
-      BatchArgs bx = b;
-      bx.tk_done = nullptr;
-      hipLaunchKernelGGL(ksg_batch_transpose, dim3((N + 31) / 32), dim3(256), 0, s1, bx);
-      if ((rc = tlaunched(ctx, KSG_K_BATCH_TRANSPOSE, units))) return rc;
-    }
-    if (overlap && !tk_flag) {
-      HIPC(ctx, hipEventRecord(ctx->ev_tk[par], s1));
-      HIPC(ctx, hipStreamWaitEvent(s2, ctx->ev_tk[par], 0));
-    }
     if (specw) {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(spec_kern)), dim3(1),
                          dim3(64 * kSvWaves), kSpecLds, s2, b);
       if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2V, 0.5 * nb * (nb + 1)))) return rc;
-    } else if (tcolw) {   // the carried columns on the state after the previous walk, then the walk
-      hipLaunchKernelGGL(ksg_tcol_carry<1>, dim3(nb), dim3(64), 0, s2, b);
-      if ((rc = tlaunched(ctx, KSG_K_TCOL_CARRY, (double)nb * prev_nb))) return rc;
-      hipLaunchKernelGGL(ksg_batch_phase2t<1>, dim3(1), dim3(64), bytes, s2, b);
-      if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2T, 0.5 * nb * (nb + 1)))) return rc;
     } else {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BatchArgs)>(const_cast<void*>(kern)), dim3(1), dim3(block), bytes, s2, b);
       if ((rc = tlaunched(ctx, KSG_K_BATCH_PHASE2S, 0.5 * nb * (nb + 1)))) return rc;
@@ -1339,6 +1248,10 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     TA(tmp, &s.gbar, sizeof(unsigned) * 16 * (size_t)R);
     TA(tmp, &s.timeout, 16);
     HIPC(ctx, hipMemsetAsync(s.timeout, 0, 16, ctx->stream));
+    if ((ctx->inject_timeout & 4) && !s.coop) {   // test injection: the group barriers find it set
+      ctx->inject_timeout &= ~4;
+      HIPC(ctx, hipMemsetAsync(s.timeout, 0x01, sizeof(unsigned), ctx->stream));
+    }
   }
   (void)hipGetLastError();
   treset(ctx);
@@ -1611,14 +1524,12 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     int cus = 0;
     HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     if (!ctx->coop_gmax) ctx->coop_gmax = std::min(cus, 256);   // one workgroup per CU: lanes wait on memory
-    // Measurement knob: cap on the group size (fewer workgroups, more nodes per lane).
-    if (const char* f = getenv("KSG_COOP_GMAX")) ctx->coop_gmax = std::max(1, std::min(atoi(f), std::min(cus, 256)));
     int kn = 1;
     while ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N && kn < 32) kn *= 2;
     if ((size_t)kn * 256 * ctx->coop_gmax < (size_t)N) return fail(ctx, KSG_E_UNSUPPORTED, "topology path: too many nodes");
     const int G = (int)((N + 256 * kn - 1) / (256 * kn));
     // the variant whose label / vocabulary / template tables are LDS at compile time
-    const bool ll = kn == 1 && ctx->c.L <= kCoopLabCols && ctx->c.n_tmpl <= kCoopTmpl && !getenv("KSG_COOP_NO_LL");
+    const bool ll = kn == 1 && ctx->c.L <= kCoopLabCols && ctx->c.n_tmpl <= kCoopTmpl;
     int occ = 0;
     switch (kn) {
       case 1: rc = ll ? coop_occupancy<1, true>(ctx, &occ) : coop_occupancy<1>(ctx, &occ); break;
@@ -1675,8 +1586,6 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   a.pmode = ctx->coop_pmode;
   a.timeout = ctx->d_coop_flags + 4;
   a.arrive = ctx->d_coop_flags + 6;
-  a.last_arrive = ctx->cycle_last ? 1 : 0;
-  a.early_rows = ctx->cycle_early ? 1 : 0;
   a.commit = do_commit;
   // the maintained tables: placement runs (they are rebuilt per run from the
   // state; a single-pod evaluation runs phase 1 instead of paying the rebuild)
@@ -1788,6 +1697,15 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     a.count = nb;
     a.out0 = off;
     a.gen = ++ctx->coop_gen;
+    {   // test injection: the barriers of this launch (the second of a queue
+        // run, so the first 64 pods are committed) find the timeout word set
+      const int bit = one ? 2 : 1;
+      if ((ctx->inject_timeout & bit) && !(one ? ctx->topo_eval_coop : ctx->coop_launch) &&
+          off == (count > kCoopBatch ? kCoopBatch : 0)) {
+        ctx->inject_timeout &= ~bit;
+        HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags + 4, 0x01, sizeof(unsigned), ctx->stream));
+      }
+    }
     // the grid barrier needs the G workgroups co-resident: G is within the
     // occupancy API's residency; a cooperative launch (ctx->coop_launch, or
     // the one-pod evaluation after a timeout) has the runtime guarantee it
@@ -1805,6 +1723,50 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
 
 int flush_stage(ksg_ctx* ctx);
 int flush_commit(ksg_ctx* ctx);
+
+// The mutable node state of the context (requested, non-zero requested, pod
+// counts, selector counts, domain tables, template totals, host ports) into
+// (save) or back from (restore) one device buffer kept across calls: a plain
+// topology queue launch whose grid barrier times out has committed some of
+// its pods; the call restores the state and relaunches cooperatively.
+int state_copy(ksg_ctx* ctx, bool save) {
+  const size_t N = ctx->c.N, R = ctx->c.R;
+  const struct { void* p; size_t bytes; } part[] = {
+      {ctx->st.requested, 8 * R * N},
+      {ctx->st.nonzero, 16 * N},
+      {ctx->st.pod_count, 4 * N},
+      {ctx->st.cnt, 4 * (size_t)std::max(ctx->c.S, 1) * N},
+      {ctx->st.tab, 4 * ctx->tab_words},
+      {ctx->st.tmpl_total, 4 * (size_t)std::max(ctx->c.n_tmpl, 1)},
+      {ctx->st.ports, 4 * (size_t)ctx->c.PW * N},
+  };
+  size_t total = 0;
+  for (const auto& q : part) total += q.p ? (q.bytes + 255) & ~(size_t)255 : 0;
+  if (save && total > ctx->state_bak_bytes) {
+    if (ctx->d_state_bak) {
+      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_state_bak);
+      if (it != ctx->allocs.end()) ctx->allocs.erase(it);
+      HIPC(ctx, hipStreamSynchronize(ctx->stream));
+      (void)hipFree(ctx->d_state_bak);
+      ctx->d_state_bak = nullptr;
+      ctx->state_bak_bytes = 0;
+    }
+    int rc;
+    if ((rc = dalloc(ctx, &ctx->d_state_bak, total))) return rc;
+    ctx->state_bak_bytes = total;
+  }
+  if (!ctx->d_state_bak || total > ctx->state_bak_bytes)
+    return fail(ctx, KSG_E_STATE, "state restore without a saved state");
+  size_t off = 0;
+  for (const auto& q : part) {
+    if (!q.p) continue;
+    char* b = ctx->d_state_bak + off;
+    HIPC(ctx, hipMemcpyAsync(save ? (void*)b : q.p, save ? q.p : (const void*)b, q.bytes, hipMemcpyDeviceToDevice,
+                             ctx->stream));
+    off += (q.bytes + 255) & ~(size_t)255;
+  }
+  return KSG_OK;
+}
 
 // The capture instances of ksg_topo_coop cover up to 4 nodes per lane
 // (coop_kernel): 262,144 nodes on 256 workgroups.
@@ -1857,9 +1819,6 @@ int json_serialise(ksg_ctx* ctx, const CapArgs& ca, const ksg_result* d_res, int
   ja.err = reinterpret_cast<uint32_t*>(ja.offsets + 3 * (size_t)count + 1);
   if (!ctx->json_stream) {
     HIPC(ctx, hipStreamCreateWithFlags(&ctx->json_stream, hipStreamNonBlocking));
-    HIPC(ctx, hipStreamCreateWithFlags(&ctx->json_stream2, hipStreamNonBlocking));
-    HIPC(ctx, hipEventCreateWithFlags(&ctx->json_half, hipEventDisableTiming));
-    if (const char* e = getenv("KSG_JSON_SPLIT")) ctx->json_split = atoi(e) != 0;
     HIPC(ctx, hipEventCreateWithFlags(&ctx->json_written, hipEventDisableTiming));
     for (int q = 0; q < ksg_ctx::kJsonSlots; q++)
       HIPC(ctx, hipEventCreateWithFlags(&ctx->json_copied[q], hipEventDisableTiming));
@@ -1910,17 +1869,7 @@ int json_serialise(ksg_ctx* ctx, const CapArgs& ca, const ksg_result* d_res, int
   // the copy back on its own stream: the next chunk's kernels overlap it
   HIPC(ctx, hipEventRecord(ctx->json_written, ctx->stream));
   HIPC(ctx, hipStreamWaitEvent(ctx->json_stream, ctx->json_written, 0));
-  if (ctx->json_split && total >= ((size_t)1 << 24)) {
-    const size_t h = (total / 2 + 4095) & ~(size_t)4095;
-    HIPC(ctx, hipStreamWaitEvent(ctx->json_stream2, ctx->json_written, 0));
-    HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot] + h, ctx->d_json_out[slot] + h, total - h, hipMemcpyDeviceToHost,
-                             ctx->json_stream2));
-    HIPC(ctx, hipEventRecord(ctx->json_half, ctx->json_stream2));
-    HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot], ctx->d_json_out[slot], h, hipMemcpyDeviceToHost, ctx->json_stream));
-    HIPC(ctx, hipStreamWaitEvent(ctx->json_stream, ctx->json_half, 0));
-  } else {
-    HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot], ctx->d_json_out[slot], total, hipMemcpyDeviceToHost, ctx->json_stream));
-  }
+  HIPC(ctx, hipMemcpyAsync(ctx->h_json[slot], ctx->d_json_out[slot], total, hipMemcpyDeviceToHost, ctx->json_stream));
   HIPC(ctx, hipMemcpyAsync(ctx->h_json_err + slot, ja.err, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->json_stream));
   HIPC(ctx, hipEventRecord(ctx->json_copied[slot], ctx->json_stream));
   ctx->json_busy[slot] = true;
@@ -2032,7 +1981,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   }
   if (batched) {
     ctx->last_path = 2;
-    if ((ctx->batch_mode == 4 || (ctx->batch_mode >= 5 && ctx->pipe_window)) && !want_cap) {
+    if ((ctx->batch_mode == 4 || (ctx->batch_mode == 6 && ctx->pipe_window)) && !want_cap) {
       if ((rc = run_pipe(ctx, first, count, d_pl, d_res, d_prof))) return rc;
     } else if ((rc = run_batched(ctx, first, count, d_pl, d_res, want_cap ? &ca : nullptr, d_prof))) {
       return rc;
@@ -2058,6 +2007,11 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
         for (int q = 0; q < ca.n_rows; q++) cc.rows[q] = ca.rows[q];
         cc.n_rows = cc.n_normrows = ca.n_rows;
       }
+      // a plain launch relies on the occupancy API for the grid barrier's
+      // residency: keep the pre-call node state so that a timeout (the
+      // workgroups were not all resident) restores it and relaunches
+      // cooperatively instead of failing over partial commits
+      if (do_commit && !ctx->coop_launch && (rc = state_copy(ctx, true))) return rc;
       if ((rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof, do_commit, want_cap ? &cc : nullptr))) return rc;
     } else if ((rc = launch_queue(ctx, a, 1, block, topo))) {
       return rc;
@@ -2105,8 +2059,13 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     HIPC(ctx, hipMemcpy(flags, ctx->d_coop_flags, sizeof(flags), hipMemcpyDeviceToHost));
     if (flags[4]) {
       ctx->coop_dirty = true;
-      ctx->coop_launch = true;   // not every workgroup was resident: cooperative launches from now on
-      return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out");
+      if (ctx->coop_launch) return fail(ctx, KSG_E_DEVICE, "topology path: grid barrier timed out (cooperative launch)");
+      // not every workgroup was resident: the pre-call state back, then the
+      // same call once more with cooperative launches (from now on)
+      ctx->coop_launch = true;
+      if (do_commit && (rc = state_copy(ctx, false))) return rc;
+      ctx->recoveries++;
+      return run_internal(ctx, first, count, do_commit, placements, results, cap);
     }
   }
   return KSG_OK;
@@ -2147,26 +2106,20 @@ bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
 int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_eval_rows* view = nullptr) {
   const size_t N = ctx->c.N;
   const ksg_profile& prof = ctx->prof;
-  // score rows, the normalising plugins first (only their norm rows differ
-  // from the raw ones, so only those are written)
-  int rows[KSG_NPLUGINS], n_rows = 0, n_normrows = 0;
-  for (int pl : {KSG_PL_TAINT_TOLERATION, KSG_PL_NODE_AFFINITY})
+  // score rows: the raw values of every plugin the profile scores.  The
+  // normalised TaintToleration / NodeAffinity rows are derived on the host
+  // from them and the maxima of the result line, and the totals are not
+  // materialised for the view (no reader: the framework sums the weights
+  // itself), round 6.
+  int rows[KSG_NPLUGINS], n_rows = 0;
+  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
     if ((prof.score_mask >> pl) & 1u) rows[n_rows++] = pl;
-  n_normrows = n_rows;
-  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
-    if (((prof.score_mask >> pl) & 1u) && pl != KSG_PL_TAINT_TOLERATION && pl != KSG_PL_NODE_AFFINITY)
-      rows[n_rows++] = pl;
   // Row width: the narrowest exact one.  Raw Fit / BalancedAllocation /
-  // ImageLocality and every normalised score are in [0, 100]; raw
-  // TaintToleration is at most the node's taint count, raw NodeAffinity at
-  // most the pod's summed preferred weights; totals at most Σ|weight| x 100.
+  // ImageLocality are in [0, 100]; raw TaintToleration is at most the node's
+  // taint count, raw NodeAffinity at most the pod's summed preferred weights.
   const ksg_pod& hp = ctx->h_pods[pod];
-  int64_t wabs = 0;
-  for (int pl = 0; pl < KSG_NPLUGINS; pl++)
-    if ((prof.score_mask >> pl) & 1u) wabs += prof.weight[pl] < 0 ? -(int64_t)prof.weight[pl] : prof.weight[pl];
-  int64_t bound = std::max<int64_t>({wabs * 100, 100, ctx->c.T, na_pref_bound(ctx, hp)});
+  int64_t bound = std::max<int64_t>({(int64_t)100, (int64_t)ctx->c.T, na_pref_bound(ctx, hp)});
   size_t es = bound < (1 << 15) ? 2 : bound < (1ll << 31) ? 4 : 8;
-  if (ctx->cycle_es == 4 || ctx->cycle_es == 8) es = std::max<size_t>(es, ctx->cycle_es);
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
   // one-wave workgroups, KN nodes per lane: the smallest KN whose grid is
@@ -2197,11 +2150,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   }
   const unsigned G = (unsigned)((N + 64 * kn - 1) / (64 * kn));
   const size_t Gm = (N + 63) / 64;   // the largest grid (KN = 1): no reallocation on a KN change
-  // host block: result line (stats[4], best key, error bits, done) | pad | fstatus[N] | raw[n_rows][N] | total[N] |
-  // norm[n_normrows][N]
+  // host block: result line (stats[4], best key, error bits, done) | pad | fstatus[N] | raw[n_rows][N]
   const size_t o_fs = 64, o_raw = o_fs + ((4 * N + 7) & ~(size_t)7);
-  const size_t o_tot = o_raw + ((es * N * n_rows + 7) & ~(size_t)7), o_norm = o_tot + ((es * N + 7) & ~(size_t)7);
-  const size_t h_need = o_norm + es * N * std::max(n_normrows, 1);
+  const size_t h_need = o_raw + es * N * std::max(n_rows, 1);
   // device block: exchange lines [Gm][32] | timeout | completion counter | key slot, error slot
   const size_t d_flags = 0, d_to = d_flags + 128 * Gm, d_arr = d_to + 128, d_key = d_arr + 128;
   const size_t d_need = d_key + 128;
@@ -2284,6 +2235,12 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
         idle > 0.25 || std::memcmp(&ctx->srv_static, &cs, sizeof(CycStatic)) != 0)
       if ((rc = srv_stop(ctx))) return rc;
   }
+  // test injection: this launch's exchange finds the sticky timeout word set
+  // (the one-launch form; a server polls the word while idle and would leave)
+  if ((ctx->inject_timeout & 8) && !server && !ctx->cycle_coop) {
+    ctx->inject_timeout &= ~8;
+    HIPC(ctx, hipMemsetAsync(ctx->d_ev + d_to, 0x01, sizeof(unsigned), ctx->stream));
+  }
   if (server && !ctx->srv_running) {   // the persistent form: started once, fed through the mailbox
     if (!ctx->h_mb) {
       HIPC(ctx, hipHostMalloc((void**)&ctx->h_mb, sizeof(SrvMailbox), hipHostMallocMapped | hipHostMallocCoherent));
@@ -2304,6 +2261,11 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     sa.d_go = reinterpret_cast<unsigned*>(ctx->d_srv + sizeof(CycCall) + sizeof(int32_t) * KSG_BLOB_MAX);
     sa.last = __atomic_load_n(&ctx->h_mb->seq, __ATOMIC_ACQUIRE);
     sa.want_img = want_img;
+    // the relay's go word starts at the last sequence number served: the
+    // workgroups other than 0 take any other value for a relayed call (a relay
+    // block reallocated and zeroed by a reload, with the mailbox's sequence
+    // past 0, read as one: a zeroed call, an illegal address)
+    HIPC(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sa.d_go), (int)sa.last, 1, ctx->stream));
     void* sargs[] = {&sa};
     const void* kf = ctx->cycle_sys ? (kn == 1 ? (const void*)ksg_cycle_server<1, true>
                                       : kn == 2 ? (const void*)ksg_cycle_server<2, true>
@@ -2371,15 +2333,12 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   }
   ck.gprof = ctx->d_ev_prof;
   ck.n_rows = n_rows;
-  ck.n_normrows = n_normrows;
   ck.es = (int32_t)es;
   ck.kn = kn;
   ck.rows = 0;
   for (int q = 0; q < n_rows; q++) ck.rows |= (uint64_t)(rows[q] & 15) << (4 * q);
   ck.h_fs = reinterpret_cast<uint32_t*>(db + o_fs);
   ck.h_raw = db + o_raw;
-  ck.h_tot = db + o_tot;
-  ck.h_norm = db + o_norm;
   ck.h_stats = reinterpret_cast<int32_t*>(db);
   ck.seq = seq;
   ck.op = 0;
@@ -2465,12 +2424,14 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       ctx->srv_running = false;
       if (!ctx->cycle_coop) {   // not every workgroup was resident: a cooperative server from now on
         ctx->cycle_coop = true;
+        ctx->recoveries++;
         return eval_fast(ctx, pod, res, cap, view);
       }
       return fail(ctx, KSG_E_DEVICE, "per-cycle server: workgroup exchange timed out");
     }
     if (!ctx->cycle_coop) {   // not every workgroup was resident: the cooperative launch from now on
       ctx->cycle_coop = true;
+      ctx->recoveries++;
       return eval_fast(ctx, pod, res, cap, view);
     }
     return fail(ctx, KSG_E_DEVICE, "per-cycle evaluation: workgroup exchange timed out");
@@ -2501,37 +2462,59 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   res->n_feasible = nfeas;
   res->status = status;
   res->score_skip = score_skip;
-  auto put_row = [&](int64_t* dst, size_t off) {   // one row into the caller's int64 array
-    if (es == 2) {
-      const int16_t* src = reinterpret_cast<const int16_t*>(hb + off);
-      for (size_t n = 0; n < N; n++) dst[n] = src[n];
-    } else if (es == 4) {
-      const int32_t* src = reinterpret_cast<const int32_t*>(hb + off);
-      for (size_t n = 0; n < N; n++) dst[n] = src[n];
-    } else {
-      std::memcpy(dst, hb + off, 8 * N);
-    }
+  auto row_at = [&](int q, size_t n) -> int64_t {   // raw row q at node n
+    const char* r = hb + o_raw + es * N * q;
+    return es == 2 ? reinterpret_cast<const int16_t*>(r)[n]
+                   : es == 4 ? reinterpret_cast<const int32_t*>(r)[n] : reinterpret_cast<const int64_t*>(r)[n];
   };
+  // DefaultNormalizeScore of TaintToleration (reverse) / NodeAffinity from
+  // the raw value and the device's maximum over the feasible nodes (the
+  // kernel's total_score arithmetic); 0 where nothing was scored
+  const int64_t max_t = st[1], max_a = st[2];
+  const uint32_t smask = prof.score_mask & ~hp.score_skip;
+  auto norm_of = [&](int pl, int64_t raw) -> int64_t {
+    if (!((smask >> pl) & 1u)) return 0;
+    if (pl == KSG_PL_TAINT_TOLERATION) return max_t != 0 ? 100 - (100 * raw) / max_t : 100;
+    if (pl == KSG_PL_NODE_AFFINITY) return max_a != 0 ? (100 * raw) / max_a : raw;
+    return raw;
+  };
+  const bool scored = (status & KSG_ST_SCORED) != 0;
   if (view) {   // the rows where the kernel wrote them
     *view = ksg_eval_rows{};
     view->n_nodes = (int32_t)N;
     view->elem_bytes = (int32_t)es;
     view->fstatus = reinterpret_cast<const uint32_t*>(hb + o_fs);
     for (int q = 0; q < n_rows; q++) {
-      view->raw[rows[q]] = hb + o_raw + es * N * q;
-      view->norm[rows[q]] = q < n_normrows ? hb + o_norm + es * N * q : view->raw[rows[q]];
+      const int pl = rows[q];
+      view->raw[pl] = hb + o_raw + es * N * q;
+      const bool derived = pl == KSG_PL_TAINT_TOLERATION || pl == KSG_PL_NODE_AFFINITY;
+      view->norm[pl] = derived ? nullptr : view->raw[pl];
+      if (derived) {
+        view->norm_from_raw |= 1u << pl;
+        view->norm_max[pl] = pl == KSG_PL_TAINT_TOLERATION ? max_t : max_a;
+      }
     }
-    view->total = hb + o_tot;
+    view->norm_scored = scored ? smask : 0u;
+    view->total = nullptr;
   }
-  const bool want_fs = cap && cap->fstatus, want_raw = cap && cap->raw, want_norm = cap && cap->norm,
-             want_tot = cap && cap->total;
-  if (want_fs) std::memcpy(cap->fstatus, hb + o_fs, 4 * N);
+  const bool want_raw = cap && cap->raw, want_norm = cap && cap->norm, want_tot = cap && cap->total;
+  if (cap && cap->fstatus) std::memcpy(cap->fstatus, hb + o_fs, 4 * N);
+  if (want_tot) std::memset(cap->total, 0, 8 * N);
+  const uint32_t* fs = reinterpret_cast<const uint32_t*>(hb + o_fs);
   for (int q = 0; q < n_rows; q++) {
-    if (want_raw) put_row(cap->raw + (size_t)rows[q] * N, o_raw + es * N * q);
-    // plugins without ScoreExtensions record the raw score as the final one
-    if (want_norm) put_row(cap->norm + (size_t)rows[q] * N, q < n_normrows ? o_norm + es * N * q : o_raw + es * N * q);
+    const int pl = rows[q];
+    int64_t* dr = want_raw ? cap->raw + (size_t)pl * N : nullptr;
+    int64_t* dn = want_norm ? cap->norm + (size_t)pl * N : nullptr;
+    const int64_t w = prof.weight[pl];
+    for (size_t n = 0; n < N; n++) {
+      const int64_t raw = row_at(q, n);
+      if (dr) dr[n] = raw;
+      // plugins without ScoreExtensions record the raw score as the final one
+      const int64_t v = scored && fs[n] == 0 ? norm_of(pl, raw) : 0;
+      if (dn) dn[n] = v;
+      if (want_tot) cap->total[n] += v * w;
+    }
   }
-  if (want_tot) put_row(cap->total, o_tot);
   ctx->last_path = 5;
   return KSG_OK;
 }
@@ -2576,8 +2559,7 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
   const bool staged = ctx->stage_pending && ctx->stage_n == 1 && ctx->stage_first == pod && ctx->d_stage &&
                       hp.blob >= ctx->stage_base && (int64_t)hp.blob + hp.blob_len <= ctx->stage_base + ctx->stage_len &&
                       (hp.node_set < 0 || (hp.node_set >= ctx->stage_base &&
-                                           (int64_t)hp.node_set + ((int64_t)N + 31) / 32 <= ctx->stage_base + ctx->stage_len)) &&
-                      ctx->topo_stage;
+                                           (int64_t)hp.node_set + ((int64_t)N + 31) / 32 <= ctx->stage_base + ctx->stage_len));
   if (!staged && (rc = flush_stage(ctx))) return rc;
   if ((rc = flush_commit(ctx))) return rc;
   if (!ctx->d_ev_prof && (rc = dalloc(ctx, &ctx->d_ev_prof, 1))) return rc;
@@ -2637,6 +2619,7 @@ int eval_topo_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap,
         ctx->coop_dirty = true;   // a grid barrier timed out: the flags and atomics sets are reset next time
         if (!ctx->topo_eval_coop) {   // not every workgroup was resident: cooperative launches from now on
           ctx->topo_eval_coop = true;
+          ctx->recoveries++;
           return eval_topo_fast(ctx, pod, res, cap, view, es);
         }
         return fail(ctx, KSG_E_DEVICE, "per-cycle topology evaluation: kernel finished without its completion flag "
@@ -2772,7 +2755,7 @@ int launch_commit(ksg_ctx* ctx, int32_t pod, int32_t node, int sign) {
   k.nz_cpu = p.nz_cpu;
   k.nz_mem = p.nz_mem;
   k.ports = p.ports >= 0 ? ctx->d_prog + p.ports : nullptr;
-  bool inl = ctx->commit_args;
+  bool inl = true;   // the commit program by value when it fits the arguments
   if (p.commit >= 0) {
     const int32_t* w = ctx->h_prog.data() + p.commit;
     k.ns = w[0];
@@ -3042,29 +3025,25 @@ int ksg_open(int device, ksg_ctx** out) {
   if (const char* f = getenv("KSG_DEFER_COMMIT")) ctx->defer_commit = atoi(f) != 0;
   if (const char* f = getenv("KSG_BATCH_MODE")) {
     const std::string m(f);
-    ctx->batch_mode = m == "scan" ? 0 : m == "topset" ? 1 : m == "slot" ? 2 : m == "tcol" ? 5 : m == "spec" ? 6 : 4;
+    ctx->batch_mode = m == "slot" ? 2 : m == "window" ? 4 : 6;
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_PIPE_OVERLAP")) ctx->pipe_overlap = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
-  if (const char* f = getenv("KSG_COOP_LAUNCH")) ctx->coop_launch = atoi(f) != 0;
+  if (const char* f = getenv("KSG_COOP_LAUNCH")) ctx->coop_launch = ctx->topo_eval_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_PC_TABLES")) ctx->pc_tables = atoi(f) != 0;
-  if (const char* f = getenv("KSG_CYCLE_LAST")) ctx->cycle_last = atoi(f) != 0;
-  if (const char* f = getenv("KSG_CYCLE_EARLY")) ctx->cycle_early = atoi(f) != 0;
-  if (const char* f = getenv("KSG_TOPO_STAGE")) ctx->topo_stage = atoi(f) != 0;
-  if (const char* f = getenv("KSG_COMMIT_ARGS")) ctx->commit_args = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SYS")) ctx->cycle_sys = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_SERVER")) ctx->srv_mode = atoi(f) != 0;
-  if (const char* f = getenv("KSG_CYCLE_ES")) ctx->cycle_es = atoi(f);
   if (const char* f = getenv("KSG_CYCLE_KN")) {
     const int v = atoi(f);
     ctx->cycle_kn = v >= 4 ? 4 : v >= 2 ? 2 : 1;
   }
   if (const char* f = getenv("KSG_TEST_INJECT_WALK_ERR")) ctx->inject_walk_err = atoi(f) != 0;
+  if (const char* f = getenv("KSG_TEST_INJECT_TIMEOUT")) ctx->inject_timeout = atoi(f);
   if (const char* f = getenv("KSG_SLOT_BLOCK")) {
     const int v = atoi(f);
-    ctx->slot_block = v <= 64 ? 64 : v <= 128 ? 128 : KSG_BATCH_MAX;
+    ctx->slot_block = v <= 64 ? 64 : 128;
   }
   *out = ctx;
   return KSG_OK;
@@ -3087,7 +3066,6 @@ int ksg_close(ksg_ctx* ctx) {
   if (ctx->h_evt) (void)hipHostFree(ctx->h_evt);
   if (ctx->d_json_tab) (void)hipFree(ctx->d_json_tab);
   if (ctx->json_stream) (void)hipStreamSynchronize(ctx->json_stream);
-  if (ctx->json_stream2) (void)hipStreamSynchronize(ctx->json_stream2);
   for (int q = 0; q < ksg_ctx::kJsonSlots; q++) {
     if (ctx->d_json_out[q]) (void)hipFree(ctx->d_json_out[q]);
     if (ctx->h_json[q]) (void)hipHostFree(ctx->h_json[q]);
@@ -3095,8 +3073,6 @@ int ksg_close(ksg_ctx* ctx) {
   }
   if (ctx->json_written) (void)hipEventDestroy(ctx->json_written);
   if (ctx->json_stream) (void)hipStreamDestroy(ctx->json_stream);
-  if (ctx->json_stream2) (void)hipStreamDestroy(ctx->json_stream2);
-  if (ctx->json_half) (void)hipEventDestroy(ctx->json_half);
   if (ctx->d_json_err) (void)hipFree(ctx->d_json_err);
   if (ctx->h_json_err) (void)hipHostFree(ctx->h_json_err);
   if (ctx->d_json_scratch) (void)hipFree(ctx->d_json_scratch);
@@ -3695,8 +3671,13 @@ int ksg_run_replicas(ksg_ctx* ctx, const ksg_profile* profiles, int32_t n_replic
     HIPC(ctx, hipMemcpy(&to, ctx->sweep_timeout, sizeof(to), hipMemcpyDeviceToHost));
     ctx->sweep_timeout = nullptr;
     if (to) {
-      ctx->coop_launch = true;   // not every workgroup was resident: cooperative launches from now on
-      return fail(ctx, KSG_E_DEVICE, "replica sweep: group barrier timed out");
+      if (ctx->coop_launch) return fail(ctx, KSG_E_DEVICE, "replica sweep: group barrier timed out (cooperative launch)");
+      // not every workgroup was resident: every replica starts from the
+      // context's state, which the sweep does not change, so the same call
+      // runs once more with cooperative launches (from now on)
+      ctx->coop_launch = true;
+      ctx->recoveries++;
+      return ksg_run_replicas(ctx, profiles, n_replicas, first, count, placements, summaries);
     }
   }
   if (summaries) {
@@ -3799,11 +3780,17 @@ int ksg_kernel_stats(ksg_ctx* ctx, ksg_kernel_stat* out, int32_t max, int32_t* n
   return KSG_OK;
 }
 
+int ksg_recoveries(ksg_ctx* ctx, int32_t* n) {
+  if (!ctx || !n) return KSG_E_INVALID;
+  *n = ctx->recoveries;
+  return KSG_OK;
+}
+
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
   if (!ctx || !path || !flags) return KSG_E_INVALID;
   *path = ctx->last_path;
   *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0) |
-           (ctx->last_tcol ? KSG_RUN_TCOL : 0) | (ctx->last_spec ? KSG_RUN_SPEC : 0) |
+           (ctx->last_spec ? KSG_RUN_SPEC : 0) |
            (ctx->last_mw ? KSG_RUN_WIDE_MEM : 0);
   return KSG_OK;
 }

@@ -33,9 +33,13 @@
 //              own slot; grid exchange on per-workgroup flags tagged with the
 //              call's sequence number (agent-scope stores and loads, no reset
 //              between calls); every workgroup folds the G slots.
-//   rows       status words, raw, normalised and total rows (2, 4 or 8 bytes)
-//              to the host block (SYS, the default: system-scope stores and a
-//              vmcnt wait; else plain stores and __threadfence_system); the
+//   rows       status words and raw rows (2, 4 or 8 bytes) to the host block
+//              (SYS, the default: system-scope stores and a vmcnt wait; else
+//              plain stores and __threadfence_system); the normalised rows
+//              and the totals are not stored (round 6: the host derives the
+//              normalised TaintToleration / NodeAffinity values from the raw
+//              rows and the maxima of the result line; nothing reads the
+//              totals); the
 //              selectHost keys and error bits fold into device slots by
 //              atomics, and the last workgroup to arrive stores the result
 //              line and its done word: the host polls one word.
@@ -103,12 +107,11 @@ struct CycCall {
   int32_t* wprog;
   const int32_t* sprog;
   int64_t slen;
-  int32_t n_rows, n_normrows, es, kn;
-  uint64_t rows;                     // score row q's plugin in bits 4q..4q+3 (the normalising ones first)
+  int32_t n_rows, es, kn;
+  uint64_t rows;                     // score row q's plugin in bits 4q..4q+3
   uint32_t* h_fs;                    // [N]          (fine-grained pinned host memory, device addresses)
-  char* h_raw;                       // [n_rows][N]
-  char* h_tot;                       // [N]
-  char* h_norm;                      // [n_normrows][N]
+  char* h_raw;                       // [n_rows][N]  (the normalised rows and the totals are not stored: the
+                                     // host derives them from these and the maxima in h_stats)
   int32_t* h_stats;                  // [8] nfeas, max taint, max node affinity, max (N - n), best key (2 words),
                                      // error bits, done (= seq; stored last, by the last workgroup)
   unsigned seq;
@@ -568,7 +571,8 @@ __device__ __forceinline__ void cyc_serve(const CycStatic& S, const CycCall& K, 
   const int32_t nfeas = gs[0], max_t = gs[1], max_a = gs[2], low = gs[3];
   KSG_YSTAMP(4);
 
-  // ---- the rows that need the fold: normalized and total scores ------------------------
+  // ---- selectHost over the normalised totals (not stored: the host derives the
+  // normalised rows from the raw ones and the maxima, round 6) ---------------------------
   const bool scored = nfeas >= 2;   // fewer than two feasible nodes: no Score ran, nothing recorded
   PodView v{};                       // total_score's inputs
   v.smask = sm;
@@ -581,19 +585,13 @@ __device__ __forceinline__ void cyc_serve(const CycStatic& S, const CycCall& K, 
     const int n = nk[k];
     if (n >= N) continue;
     const bool ok = st[k] == 0;
-    int64_t total = 0, nt = 0, na = 0;
     if (scored && ok) {
-      total = total_score(v, part[k], rt[k], ra[k], max_t, max_a, err, &nt, &na);
+      const int64_t total = total_score(v, part[k], rt[k], ra[k], max_t, max_a, err, nullptr, nullptr);
       const uint64_t kk = argmax_key(total, n);
       key = kk > key ? kk : key;
     }
     if (!scored && ok)   // no Score ran: nothing recorded for it
       for (int q = 0; q < K.n_rows; q++) cyc_put_es<SYS>(K.h_raw, (size_t)q * NN + n, 0, es);
-    for (int q = 0; q < K.n_normrows; q++) {
-      const int pl = (int)((K.rows >> (4 * q)) & 15u);
-      cyc_put_es<SYS>(K.h_norm, (size_t)q * NN + n, pl == KSG_PL_TAINT_TOLERATION ? nt : na, es);
-    }
-    cyc_put_es<SYS>(K.h_tot, n, total, es);
   }
   key = wreduce(key, OpMaxU64{});
   err = wreduce(err, OpOr32{});

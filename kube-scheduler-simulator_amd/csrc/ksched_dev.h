@@ -223,18 +223,13 @@ struct BatchArgs {
   const int32_t* carry_n;   // their count (device), or null
   int32_t* carry_out;       // this batch's changed nodes, for the next batch
   int32_t* carry_out_n;
-  // transposed walk (ksched_phase2t.h): node-major copies [N][qs] of rec / stat
-  uint64_t* rect;
-  int32_t* statt;
-  int32_t qs;
   // speculate-and-verify walk (ksched_phase2v.h): phase 1 itself writes the
-  // node-major copies rect and imgt ([N][64], weight x ImageLocality) from a
-  // 1-D XCD-ordered grid (every pod of a node tile on one XCD, so the partial
-  // lines of a node's row merge in that XCD's L2); no transpose launch
+  // node-major copies rect and imgt ([N][64]: the phase-1 records and weight x
+  // ImageLocality) from a 1-D XCD-ordered grid (every pod of a node tile on
+  // one XCD, so the partial lines of a node's row merge in that XCD's L2)
+  uint64_t* rect;
   int32_t* imgt;
   int32_t xcd_grid;
-  uint32_t* tc_colinit;     // [carried slot][qs] column words of the carried nodes (ksg_tcol_carry)
-  void* tc_init;            // [qs] TcInit: per-pod maxima / counters over the carried columns
   // the window pipeline's top-k -> walk hand-off without a cross-stream event
   // (run_pipe): the last top-k workgroup of batch b stores tk_seq = b + 1 into
   // *tk_done; the walk of batch b polls it, then acquires.  Null: stream order.
@@ -334,209 +329,6 @@ __global__ __launch_bounds__(256) void ksg_batch_phase1(BatchArgs a) {
 #else
 #define KSG_STAMP(seg) do {} while (0)
 #endif
-
-// Phase 2, scan variant (KSG_BATCH_MODE=scan): one workgroup walks the batch
-// in queue order, re-evaluates the changed nodes from global memory and scans
-// all N phase-1 records of every pod (three barriers per pod).  Kept as the
-// reference implementation of the batched scheme next to the top-set variant
-// below.
-// Diagnostic build (-DKSG_STAMPS): lane 0 of wave 0 sums s_memtime deltas per
-// segment of the phase-2 loop.  Never compiled into the measured library.
-constexpr int kRPT = 10;  // phase-1 records held in registers per lane (N <= 5120 at 512 lanes)
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2_scan(BatchArgs a) {
-  constexpr int NW = BLOCK / 64;
-  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
-  __shared__ ksg_profile s_prof;
-  __shared__ int32_t s_clist[KSG_BATCH_MAX];
-  __shared__ NodeEval s_ce[KSG_BATCH_MAX];
-  __shared__ int32_t s_pmax[2 * KSG_BATCH_MAX];
-  __shared__ int32_t s_nc;
-  __shared__ Red s_red[NW];
-  __shared__ uint64_t s_best[NW];
-  __shared__ uint32_t s_err[NW];
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const DevCluster& c = a.c;
-  const int N = c.N;
-  int64_t* requested = a.st.requested;
-  int64_t* nonzero = a.st.nonzero;
-  int32_t* pod_count = a.st.pod_count;
-  const int cm_words = (((N + 31) / 32) + 3) & ~3;
-  constexpr int POD_WORDS = sizeof(ksg_pod) / 4;
-  uint32_t* s_cmask = reinterpret_cast<uint32_t*>(s_dyn);
-  ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
-  int32_t* s_prog = s_dyn + cm_words + a.nb * POD_WORDS;
-
-  for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
-  for (int i = tid; i < a.nb * POD_WORDS; i += BLOCK)
-    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
-  for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
-  for (int i = tid; i < 2 * a.nb; i += BLOCK) s_pmax[i] = a.pmax[i];
-  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
-    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
-  if (tid == 0) s_nc = 0;
-
-  uint64_t rr[kRPT];
-  auto prefetch = [&](int j) {
-    const uint64_t* rec = a.rec + (size_t)j * N;
-#pragma unroll
-    for (int q = 0; q < kRPT; q++) {
-      const int n = tid + q * BLOCK;
-      rr[q] = n < N ? rec[n] : 0;
-    }
-  };
-  prefetch(0);
-  __syncthreads();
-
-#ifdef KSG_STAMPS
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
-#endif
-  KSG_STAMP(0);
-  for (int j = 0; j < a.nb; j++) {
-    const ksg_pod& p = s_pods[j];
-    const ksg_profile& prof = s_prof;
-    const PodView v = make_view(c, prof, p, s_prog + (p.blob - a.prog_lo), a.prog);
-    const int nc = s_nc;
-    // re-evaluate the nodes assumed onto earlier in this batch, on live state
-    for (int i = tid; i < nc; i += BLOCK)
-      s_ce[i] = eval_node(c, prof, v, requested, nonzero, pod_count, s_clist[i], nullptr, nullptr);
-    KSG_STAMP(1);
-    __syncthreads();
-    KSG_STAMP(2);
-    const int64_t mt1 = s_pmax[2 * j], ma1 = s_pmax[2 * j + 1];
-    const uint64_t* rec = a.rec + (size_t)j * N;
-    Red r{0, 0, 0, 0x7fffffff};
-    uint64_t best = 0;
-    uint32_t err = 0;
-    auto visit = [&](uint64_t x, int n, int64_t mt, int64_t ma, bool stats) {
-      if (!(x >> 63)) return;
-      const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
-      if (stats) {
-        r.nfeas += 1;
-        r.minidx = min(r.minidx, n);
-        r.max_t = max(r.max_t, rt);
-        r.max_a = max(r.max_a, ra);
-      }
-      const uint64_t key = argmax_key(total_score(v, part, rt, ra, mt, ma, err, nullptr, nullptr), n);
-      best = key > best ? key : best;
-    };
-    auto visit_changed = [&](int64_t mt, int64_t ma, bool stats) {
-      for (int i = tid; i < nc; i += BLOCK) {
-        const NodeEval e = s_ce[i];
-        if (e.st != 0) continue;
-        const int n = s_clist[i];
-        if (stats) {
-          r.nfeas += 1;
-          r.minidx = min(r.minidx, n);
-          r.max_t = max(r.max_t, e.rt);
-          r.max_a = max(r.max_a, e.ra);
-        }
-        const uint64_t key = argmax_key(total_score(v, e.part, e.rt, e.ra, mt, ma, err, nullptr, nullptr), n);
-        best = key > best ? key : best;
-      }
-    };
-    auto scan = [&](int64_t mt, int64_t ma, bool stats) {
-#pragma unroll
-      for (int q = 0; q < kRPT; q++) {
-        const int n = tid + q * BLOCK;
-        if (n < N && !((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rr[q], n, mt, ma, stats);
-      }
-      for (int n = tid + kRPT * BLOCK; n < N; n += BLOCK)
-        if (!((s_cmask[n >> 5] >> (n & 31)) & 1u)) visit(rec[n], n, mt, ma, stats);
-      visit_changed(mt, ma, stats);
-    };
-    scan(mt1, ma1, true);
-    KSG_STAMP(3);
-    {
-      Red w;
-      w.max_t = wave_max64(r.max_t);
-      w.max_a = wave_max64(r.max_a);
-      w.nfeas = wave_sum32(r.nfeas);
-      w.minidx = wave_min32(r.minidx);
-      best = wave_max_u64(best);
-      err = wave_or32(err);
-      if (lane == 0) { s_red[wv] = w; s_best[wv] = best; s_err[wv] = err; }
-    }
-    __syncthreads();
-    Red g{0, 0, 0, 0x7fffffff};
-    uint64_t gb = 0;
-    uint32_t ge = 0;
-#pragma unroll
-    for (int i = 0; i < NW; i++) {
-      const Red w = s_red[i];
-      g.max_t = max(g.max_t, w.max_t);
-      g.max_a = max(g.max_a, w.max_a);
-      g.nfeas += w.nfeas;
-      g.minidx = min(g.minidx, w.minidx);
-      gb = s_best[i] > gb ? s_best[i] : gb;
-      ge |= s_err[i];
-    }
-    const bool stale_t = (v.smask & bit(KSG_PL_TAINT_TOLERATION)) && g.max_t != mt1;
-    const bool stale_a = (v.smask & bit(KSG_PL_NODE_AFFINITY)) && g.max_a != ma1;
-    if (g.nfeas >= 2 && (stale_t || stale_a)) {
-      // a holder of a phase-1 maximum was assumed full: renormalise with the
-      // live maxima (second scan; rare)
-      __syncthreads();
-      best = 0;
-      err = 0;
-      scan(g.max_t, g.max_a, false);
-      best = wave_max_u64(best);
-      err = wave_or32(err);
-      if (lane == 0) { s_best[wv] = best; s_err[wv] = err; }
-      __syncthreads();
-      gb = 0;
-      ge = 0;
-#pragma unroll
-      for (int i = 0; i < NW; i++) {
-        gb = s_best[i] > gb ? s_best[i] : gb;
-        ge |= s_err[i];
-      }
-    }
-    KSG_STAMP(4);
-    if (j + 1 < a.nb) prefetch(j + 1);   // overlaps the commit barrier
-    int selected = -1;
-    uint32_t status = 0;
-    if (g.nfeas == 1) {
-      selected = g.minidx;
-    } else if (g.nfeas >= 2) {
-      status |= KSG_ST_SCORED;
-      if (ge) status |= KSG_ST_SCORE_ERROR;
-      else selected = key_node(gb);
-    }
-    uint32_t score_skip;
-    ipa_skip_bits(prof, p, status, score_skip);
-    if (tid == 0) {
-      if (selected >= 0) {
-        commit_node(c, requested, nonzero, pod_count, a.st.cnt, a.st.tab, a.st.tmpl_total, p,
-                    v.commit >= 0 ? v.P + v.commit : nullptr, selected);
-        if (!((s_cmask[selected >> 5] >> (selected & 31)) & 1u)) {
-          s_cmask[selected >> 5] |= 1u << (selected & 31);
-          s_clist[s_nc] = selected;
-          s_nc = s_nc + 1;
-        }
-      }
-      const int o = a.out0 + j;
-      a.placements[o] = selected;
-      if (a.results) {
-        ksg_result res;
-        res.selected = selected;
-        res.n_feasible = g.nfeas;
-        res.status = status;
-        res.score_skip = score_skip;
-        a.results[o] = res;
-      }
-    }
-    __syncthreads();
-    KSG_STAMP(5);
-  }
-  for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
-#ifdef KSG_STAMPS
-  if (tid == 0 && a.stamps)
-    for (int i = 0; i < 6; i++) atomicAdd(&a.stamps[i], st_acc[i]);
-#endif
-}
 
 // Phase 1b, one workgroup per pod j: the statistics phase 2 needs to update
 // pod j's result incrementally, and the top set T_j = the min(j + 1, nfeas)
@@ -772,391 +564,14 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_topk(BatchArgs a) {
   }
 }
 
-// Phase 2: one workgroup walks the batch in queue order and keeps every node
-// assumed onto during the batch (the changed set C, |C| <= j before pod j) in
-// an LDS slot holding its live resource columns.  Per pod j:
-//   A  lanes 0..255     re-evaluate C: static filters/scores from the phase-1
-//                       record (they do not depend on the assumed pods),
-//                       NodeResourcesFit + BalancedAllocation from the slot;
-//      lanes 256..511   best key of T_j \ C (= the best unchanged node);
-//      lanes 512..767   best two keys of T_{j+1} \ C (prediction of pod j+1's
-//                       choice, so its columns are fetched a pod ahead);
-//   B  feasible count = phase-1 count corrected over C; the normalisation
-//      maxima are unchanged while a holder survives (else, or on a range
-//      error, a full rescan of the records, rare); select; the last wave
-//      assumes the pod into its slot and stores the node's new columns.
-// Two barriers per pod; the next pod's records and top set are fetched into
-// registers during A and written to LDS during B.
-
+// The slot walk's per-wave partials (ksg_batch_phase2s).
 struct WRed {
   uint64_t k0, k1;
   int32_t feas1, live, lost_t, lost_a, cmin, err;
 };
 
-__device__ __forceinline__ void top2_merge(uint64_t& a, uint64_t& b, uint64_t oa, uint64_t ob) {
-  const uint64_t hi = a > oa ? a : oa, lo = a > oa ? oa : a;
-  uint64_t s = b > ob ? b : ob;
-  s = s > lo ? s : lo;
-  a = hi;
-  b = s;
-}
-
-__device__ __forceinline__ void slot_cols(const int64_t* sl, int R, NodeCols& L) {
-#pragma unroll
-  for (int r = 0; r < KSG_MAX_RES; r++) {
-    L.alloc[r] = r < R ? sl[r] : 0;
-    L.req[r] = r < R ? sl[R + r] : 0;
-  }
-  L.nz_cpu = sl[2 * R];
-  L.nz_mem = sl[2 * R + 1];
-  L.pod_count = (int32_t)sl[2 * R + 2];
-  L.allowed = (int32_t)sl[2 * R + 3];
-}
-
-constexpr int kP2Block = 768;   // three groups of 256 lanes; the last wave also assumes pods
-
-#ifndef KSG_PART
-__global__ __launch_bounds__(kP2Block) void ksg_batch_phase2(BatchArgs a) {
-  constexpr int BLOCK = kP2Block, NW = BLOCK / 64;
-  constexpr int LOADER = NW - 1;   // wave that assumes pods and fetches node columns (after its A work)
-  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
-  __shared__ ksg_profile s_prof;
-  __shared__ P1Stats s_p1[KSG_BATCH_MAX];
-  __shared__ int32_t s_clist[KSG_BATCH_MAX];
-  __shared__ uint64_t s_top[2][KSG_BATCH_MAX];
-  __shared__ uint64_t s_crec[2][KSG_BATCH_MAX];
-  __shared__ int32_t s_cimg[2][KSG_BATCH_MAX];
-  __shared__ uint64_t s_ce[KSG_BATCH_MAX];     // live record of each changed node (rescan path)
-  __shared__ WRed s_w[NW];
-  __shared__ int32_t s_nc;
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, grp = tid >> 8, gi = tid & 255;
-  const DevCluster& c = a.c;
-  const int N = c.N, R = c.R, S = 2 * R + 4;
-  const int cm_words = (((N + 31) / 32) + 3) & ~3;
-  constexpr int POD_WORDS = sizeof(ksg_pod) / 4;
-  uint32_t* s_cmask = reinterpret_cast<uint32_t*>(s_dyn);
-  ksg_pod* s_pods = reinterpret_cast<ksg_pod*>(s_dyn + cm_words);
-  int32_t* s_prog = s_dyn + cm_words + a.nb * POD_WORDS;
-  int64_t* s_slot = reinterpret_cast<int64_t*>(s_dyn + ((cm_words + a.nb * POD_WORDS + a.prog_len + 3) & ~3));
-
-  for (int i = tid; i < cm_words; i += BLOCK) s_cmask[i] = 0;
-  for (int i = tid; i < a.nb * POD_WORDS; i += BLOCK)
-    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.b0)[i];
-  for (int i = tid; i < a.prog_len; i += BLOCK) s_prog[i] = a.prog[a.prog_lo + i];
-  for (int i = tid; i < a.nb * (int)(sizeof(P1Stats) / 4); i += BLOCK)
-    reinterpret_cast<int32_t*>(s_p1)[i] = reinterpret_cast<const int32_t*>(a.p1)[i];
-  for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
-    reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.prof)[i_];
-  if (tid < KSG_BATCH_MAX) {
-    s_top[0][tid] = a.top[tid];
-    if (a.nb > 1) s_top[1][tid] = a.top[KSG_BATCH_MAX + tid];
-  }
-  if (tid == 0) s_nc = 0;
-
-  bool fit_filter_on = false;
-  for (int kf = 0; kf < a.prof->n_filter; kf++) fit_filter_on |= a.prof->filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
-
-  // loader wave: columns of the predicted next choice.  Lane l < S holds slot
-  // word l (alloc[R], requested[R], nonzero[2], pod_count, allowed); lane S
-  // the record and lane S + 1 the image part of the pod after it.
-  int spec_node = -1;
-  int64_t spec_val = 0;
-  auto fetch = [&](int n, int jrec, int64_t& val) {
-    val = 0;
-    if (lane < R) val = c.alloc[(size_t)lane * N + n];
-    else if (lane < 2 * R) val = a.st.requested[(size_t)(lane - R) * N + n];
-    else if (lane < 2 * R + 2) val = a.st.nonzero[(size_t)(lane - 2 * R) * N + n];
-    else if (lane == 2 * R + 2) val = a.st.pod_count[n];
-    else if (lane == 2 * R + 3) val = c.allowed[n];
-    else if (lane == S && jrec < a.nb) val = (int64_t)a.rec[(size_t)jrec * N + n];
-    else if (lane == S + 1 && jrec < a.nb) val = a.img[(size_t)jrec * N + n];
-  };
-  if (wv == LOADER) {
-    if (a.p1[0].K > 0) {
-      spec_node = key_node(a.top[0]);
-      fetch(spec_node, 1, spec_val);
-    }
-  }
-  __syncthreads();
-
-#ifdef KSG_STAMPS
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
-#endif
-  KSG_STAMP(0);
-  for (int j = 0; j < a.nb; j++) {
-    const ksg_pod& p = s_pods[j];
-    const ksg_profile& prof = s_prof;
-    const PodView v = make_view(c, prof, p, s_prog + (p.blob - a.prog_lo), a.prog);
-    const P1Stats s1 = s_p1[j];
-    const int nc = s_nc;
-    const int cur = j & 1, nxt = cur ^ 1;
-    const int64_t mt1 = s1.mt, ma1 = s1.ma;
-    auto changed = [&](int n) { return ((s_cmask[n >> 5] >> (n & 31)) & 1u) != 0; };
-
-    // ---- A --------------------------------------------------------------
-    uint64_t pre_rec = 0;   // grp 0: next pod's record of changed node gi; grp 1: T_{j+2} entry gi
-    int32_t pre_img = 0;
-    if (grp == 0) {
-      WRed w{0, 0, 0, 0, 0, 0, 0x7fffffff, 0};
-      if (gi < nc) {
-        const int n = s_clist[gi];
-        if (j + 1 < a.nb) {
-          pre_rec = a.rec[(size_t)(j + 1) * N + n];
-          pre_img = a.img[(size_t)(j + 1) * N + n];
-        }
-        const uint64_t x = s_crec[cur][gi];
-        uint64_t live = 0;
-        if (x >> 63) {
-          w.feas1 = 1;
-          const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff;
-          NodeCols L;
-          slot_cols(s_slot + (size_t)gi * S, R, L);
-          const bool fits = !(fit_filter_on && !((v.fskip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) &&
-                              fit_filter(c, p, L, prof.fit_ignored_res) != 0);
-          if (!fits) {
-            w.lost_t = rt == mt1;
-            w.lost_a = ra == ma1;
-          } else {
-            int64_t part = s_cimg[cur][gi];
-            if (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) part += fit_score(prof, p, L) * v.w_fit;
-            if (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) part += ba_score(prof, p, L) * v.w_ba;
-            uint32_t e = 0;
-            w.k0 = argmax_key(total_score(v, part, rt, ra, mt1, ma1, e, nullptr, nullptr), n);
-            w.err = (int32_t)e;
-            w.live = 1;
-            w.cmin = n;
-            live = pack_rec(part, rt, ra);
-          }
-        }
-        s_ce[gi] = live;
-      }
-      w.k0 = wave_max_u64(w.k0);
-      w.feas1 = wave_sum32(w.feas1);
-      w.live = wave_sum32(w.live);
-      w.lost_t = wave_sum32(w.lost_t);
-      w.lost_a = wave_sum32(w.lost_a);
-      w.cmin = wave_min32(w.cmin);
-      w.err = (int32_t)wave_or32((uint32_t)w.err);
-      if (lane == 0) s_w[wv] = w;
-    } else if (grp == 1) {
-      uint64_t best = 0;
-      if (gi < s1.K) {
-        const uint64_t key = s_top[cur][gi];
-        if (!changed(key_node(key))) best = key;
-      }
-      if (j + 2 < a.nb && gi < s_p1[j + 2].K) pre_rec = a.top[(size_t)(j + 2) * KSG_BATCH_MAX + gi];
-      best = wave_max_u64(best);
-      if (lane == 0) s_w[wv].k0 = best;
-    } else if (grp == 2) {
-      uint64_t t1 = 0, t2 = 0;
-      if (j + 1 < a.nb && gi < s_p1[j + 1].K) {
-        const uint64_t key = s_top[nxt][gi];
-        if (!changed(key_node(key))) t1 = key;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t o1 = __shfl_xor(t1, o, 64), o2 = __shfl_xor(t2, o, 64);
-        top2_merge(t1, t2, o1, o2);
-      }
-      if (lane == 0) { s_w[wv].k0 = t1; s_w[wv].k1 = t2; }
-    }
-    KSG_STAMP(1);
-    __syncthreads();
-    KSG_STAMP(2);
-
-    // ---- B --------------------------------------------------------------
-    WRed g{0, 0, 0, 0, 0, 0, 0x7fffffff, 0};
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const WRed w = s_w[i];
-      g.k0 = w.k0 > g.k0 ? w.k0 : g.k0;
-      g.feas1 += w.feas1;
-      g.live += w.live;
-      g.lost_t += w.lost_t;
-      g.lost_a += w.lost_a;
-      g.cmin = min(g.cmin, w.cmin);
-      g.err |= w.err;
-    }
-    const int unch = s1.nfeas - g.feas1;          // unchanged feasible nodes
-    int nfeas = unch + g.live;
-    const bool stale = nfeas >= 2 && (((v.smask & bit(KSG_PL_TAINT_TOLERATION)) && s1.ht - g.lost_t <= 0) ||
-                                      ((v.smask & bit(KSG_PL_NODE_AFFINITY)) && s1.ha - g.lost_a <= 0));
-    const bool rescan = nfeas >= 2 && (s1.err || g.err || stale);
-    uint64_t bu = 0, s1k = 0, s2k = 0;   // loader: best of T_j \ C; best two of T_{j+1} \ C
-    if (wv == LOADER) {
-#pragma unroll
-      for (int i = 4; i < 8; i++) bu = s_w[i].k0 > bu ? s_w[i].k0 : bu;
-#pragma unroll
-      for (int i = 8; i < 12; i++) top2_merge(s1k, s2k, s_w[i].k0, s_w[i].k1);
-    }
-    int selected = -1;
-    uint32_t status = 0;
-    if (rescan) {
-      // full pass over pod j's records with the live maxima (rare)
-      const uint64_t* rec = a.rec + (size_t)j * N;
-      Red r{0, 0, 0, 0x7fffffff};
-      for (int pass = 0; pass < 2; pass++) {
-        uint64_t best = 0;
-        uint32_t err = 0;
-        auto visit = [&](uint64_t x, int n) {
-          if (!(x >> 63)) return;
-          const int64_t rt = (x >> 48) & 0xff, ra = (x >> 32) & 0xffff, part = (uint32_t)x;
-          if (pass == 0) {
-            r.nfeas += 1;
-            r.minidx = min(r.minidx, n);
-            r.max_t = max(r.max_t, rt);
-            r.max_a = max(r.max_a, ra);
-          } else {
-            const uint64_t key = argmax_key(total_score(v, part, rt, ra, r.max_t, r.max_a, err, nullptr, nullptr), n);
-            best = key > best ? key : best;
-          }
-        };
-        for (int n = tid; n < N; n += BLOCK)
-          if (!changed(n)) visit(rec[n], n);
-        for (int i = tid; i < nc; i += BLOCK) visit(s_ce[i], s_clist[i]);
-        __syncthreads();   // s_w reads of this pod are done / previous pass consumed
-        if (pass == 0) {
-          WRed w{0, 0, 0, 0, 0, 0, 0, 0};
-          w.k0 = (uint64_t)wave_max64(r.max_t);
-          w.k1 = (uint64_t)wave_max64(r.max_a);
-          w.live = wave_sum32(r.nfeas);
-          w.cmin = wave_min32(r.minidx);
-          if (lane == 0) s_w[wv] = w;
-          __syncthreads();
-          r = Red{0, 0, 0, 0x7fffffff};
-#pragma unroll
-          for (int i = 0; i < NW; i++) {
-            const WRed w2 = s_w[i];
-            r.max_t = max(r.max_t, (int64_t)w2.k0);
-            r.max_a = max(r.max_a, (int64_t)w2.k1);
-            r.nfeas += w2.live;
-            r.minidx = min(r.minidx, w2.cmin);
-          }
-        } else {
-          WRed w{0, 0, 0, 0, 0, 0, 0, 0};
-          w.k0 = wave_max_u64(best);
-          w.err = (int32_t)wave_or32(err);
-          if (lane == 0) s_w[wv] = w;
-          __syncthreads();
-          uint64_t gb = 0;
-          uint32_t ge = 0;
-#pragma unroll
-          for (int i = 0; i < NW; i++) {
-            gb = s_w[i].k0 > gb ? s_w[i].k0 : gb;
-            ge |= (uint32_t)s_w[i].err;
-          }
-          nfeas = r.nfeas;
-          status |= KSG_ST_SCORED;
-          if (ge) status |= KSG_ST_SCORE_ERROR;
-          else selected = key_node(gb);
-        }
-      }
-    } else if (nfeas == 1) {
-      selected = unch == 1 ? -2 : g.cmin;   // -2: the unchanged best (resolved below)
-    } else if (nfeas >= 2) {
-      status |= KSG_ST_SCORED;
-      selected = -3;                          // max(best unchanged, best changed)
-    }
-    KSG_STAMP(3);
-    if (grp == 0 && gi < nc && j + 1 < a.nb) {
-      s_crec[nxt][gi] = pre_rec;
-      s_cimg[nxt][gi] = pre_img;
-    } else if (grp == 1 && j + 2 < a.nb && gi < s_p1[j + 2].K) {
-      s_top[cur][gi] = pre_rec;
-    }
-    if (wv == LOADER) {
-      if (selected == -2) selected = key_node(bu);
-      else if (selected == -3) selected = key_node(bu > g.k0 ? bu : g.k0);
-      uint32_t score_skip;
-      ipa_skip_bits(prof, p, status, score_skip);
-      if (selected >= 0) {
-        // assume: live columns of the selected node into its slot + global
-        int idx = -1;
-        if (changed(selected)) {
-          for (int b = 0; b < nc; b += 64) {
-            const uint64_t m = __ballot(b + lane < nc && s_clist[b + lane] == selected);
-            if (m) { idx = b + __builtin_ctzll(m); break; }
-          }
-        }
-        int64_t val;
-        if (idx >= 0) {
-          val = lane < S ? s_slot[(size_t)idx * S + lane] : 0;
-        } else if (selected == spec_node) {
-          val = spec_val;
-        } else {
-          fetch(selected, j + 1, val);
-        }
-        if (lane < S) {
-          int64_t d = 0;
-          if (lane >= R && lane < 2 * R) d = p.req[lane - R];
-          else if (lane == 2 * R) d = p.nz_cpu;
-          else if (lane == 2 * R + 1) d = p.nz_mem;
-          else if (lane == 2 * R + 2) d = 1;
-          val += d;
-          const int slot = idx >= 0 ? idx : nc;
-          s_slot[(size_t)slot * S + lane] = val;
-          if (lane >= R && lane < 2 * R) a.st.requested[(size_t)(lane - R) * N + selected] = val;
-          else if (lane == 2 * R || lane == 2 * R + 1) a.st.nonzero[(size_t)(lane - 2 * R) * N + selected] = val;
-          else if (lane == 2 * R + 2) a.st.pod_count[selected] = (int32_t)val;
-        }
-        if (idx < 0) {
-          if (lane == S) s_crec[nxt][nc] = (uint64_t)val;
-          if (lane == S + 1) s_cimg[nxt][nc] = (int32_t)val;
-          if (lane == 0) {
-            s_cmask[selected >> 5] |= 1u << (selected & 31);
-            s_clist[nc] = selected;
-            s_nc = nc + 1;
-          }
-        }
-        if (lane == 0 && v.commit >= 0) {   // PodTopologySpread / InterPodAffinity count tables
-          const int32_t* w = v.P + v.commit;
-          const int ns = *w++;
-          for (int i = 0; i < ns; i++) a.st.cnt[(size_t)w[i] * N + selected] += 1;
-          w += ns;
-          const int nt = *w++;
-          for (int i = 0; i < nt; i++) {
-            const int t = w[2 * i];
-            const uint32_t lv = c.label_val[(size_t)c.tmpl_col[t] * N + selected];
-            if (!lv) continue;
-            a.st.tab[c.tmpl_off[t] + lv] += c.tmpl_kind[t] == KSG_TMPL_PREF ? w[2 * i + 1] : 1;
-            a.st.tmpl_total[t] += 1;
-          }
-        }
-      }
-      if (lane == 0) {
-        const int o = a.out0 + j;
-        a.placements[o] = selected;
-        if (a.results) {
-          ksg_result res;
-          res.selected = selected;
-          res.n_feasible = nfeas;
-          res.status = status;
-          res.score_skip = score_skip;
-          a.results[o] = res;
-        }
-      }
-      // predict pod j+1's choice: its best unchanged node once `selected` is in C
-      spec_node = -1;
-      if (j + 1 < a.nb) {
-        const int n1 = s1k ? key_node(s1k) : -1, n2 = s2k ? key_node(s2k) : -1;
-        spec_node = n1 != selected ? n1 : n2;
-        if (spec_node >= 0) fetch(spec_node, j + 2, spec_val);
-      }
-    }
-    KSG_STAMP(4);
-    __syncthreads();
-    KSG_STAMP(5);
-  }
-  for (int i = tid; i < 2 * a.nb; i += BLOCK) a.pmax[i] = 0;   // ready for the next batch's phase 1
-#ifdef KSG_STAMPS
-  if (tid == 0 && a.stamps)
-    for (int i = 0; i < 6; i++) atomicAdd(&a.stamps[i], st_acc[i]);
-#endif
-}
-#endif  // KSG_PART
-
-// Phase 2, slot-parallel variant (KSG_BATCH_MODE=slot, default).  256 lanes;
+// Phase 2, the slot walk (the fallback outside the speculate-and-verify walk's
+// scope, and the captured queues).  256 lanes;
 // lane i owns changed slot i (the i-th node assumed onto in this batch) and
 // keeps that node's phase-1 records in registers, one pod ahead.  Per pod j:
 //   X  every lane: spec = the first entry of the sorted top set T_j outside C
@@ -1851,7 +1266,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2s(BatchArgs a) {
 }
 
 #if !defined(KSG_PART) || defined(KSG_WITH_BATCH)
-#include "ksched_phase2t.h"
+#include "ksched_n32.h"
 #endif
 #if !defined(KSG_PART) || defined(KSG_WITH_BATCH)
 #include "ksched_phase2v.h"

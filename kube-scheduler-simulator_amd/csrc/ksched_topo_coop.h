@@ -139,10 +139,6 @@ struct CoopArgs {
   int32_t cap_es;              // CAP == 2: bytes per row value (2, 4, 8); a value that does not fit
                                // sets *h_ovf and the host evaluates again wider
   unsigned* h_ovf;
-  int32_t early_rows;          // CAP == 2: 1 (default) the rows final since phase 2 are written after barrier 2
-                               // (KSG_CYCLE_EARLY=0: all in 3c; measurement knob)
-  int32_t last_arrive;         // CAP == 2: 1 (default) the last arrival completes the call, 0 barrier 3 and
-                               // phase 4 (KSG_CYCLE_LAST=0, measurement knob)
   ksg_pod* wpods;              // CAP == 2, a staged append read in place (pods / prog point into the
                                // staging buffer): workgroup 0 copies it here (pod `first`) ...
   int32_t* wprog;              // ... and its programs here; null: none
@@ -1144,7 +1140,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     // their PCIe transfer overlaps phase 3.  3c writes the rest, and zeroes
     // these when the pod turns out unscored (< 2 feasible nodes).
     uint32_t early_err = 0;
-    const bool early = CAP == 2 && a.early_rows;
+    const bool early = CAP == 2;
     if constexpr (CAP == 2) {
       if (early) {
         const size_t NN = N;
@@ -1427,7 +1423,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       gst(&mine->err, e);
       s_wbest = b;
     }
-    if (CAP == 2 && a.last_arrive) {
+    if (CAP == 2) {
       // The per-cycle evaluation (one pod, no assume): no barrier 3.  Each
       // workgroup's host rows and argmax slot are performed (system-scope
       // stores: vmcnt(0)), it arrives on a counter, and the last of the G

@@ -92,13 +92,9 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
         return 24
     if name == "ksg_eval_cycle":     # ksg_capture_eval + ksg_capture_norm in one launch (per-cycle path)
         return bytes_per_eval + 12 + 24
-    if name in ("ksg_batch_topk", "ksg_batch_phase2_scan"):
+    if name == "ksg_batch_topk":
         return 8
-    if name == "ksg_tcol_carry":
-        return 140   # live columns of a carried node (128 B) + record and static (12 B) per (pod, carried node)
-    if name == "ksg_batch_transpose":
-        return 24   # 12 B read + 12 B written per (pod, node)
-    if name in ("ksg_batch_phase2", "ksg_batch_phase2s", "ksg_batch_phase2p", "ksg_batch_phase2t", "ksg_batch_phase2v"):
+    if name in ("ksg_batch_phase2s", "ksg_batch_phase2v"):
         return 20
     if name in ("ksg_sweep_static", "ksg_sweep"):
         if not isinstance(cols, dict):
@@ -131,8 +127,7 @@ def dominant_kernel_roofline(kstats, bytes_per_eval):
             "bytes_per_launch": dom["bytes_per_launch"], "kernels": rows}
 
 
-PHASE2_KERNELS = ("ksg_batch_phase2s", "ksg_batch_phase2t", "ksg_batch_phase2v", "ksg_batch_phase2p",
-                  "ksg_batch_phase2")
+PHASE2_KERNELS = ("ksg_batch_phase2s", "ksg_batch_phase2v")
 
 
 def price_decided_node_evals(roof, bytes_per_eval: int, node_evals: int):

@@ -21,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libksched.so")
 
 NPLUGINS = 14
+PL_TAINT_TOLERATION, PL_NODE_AFFINITY = 2, 3   # KSG_PL_* of include/ksched.h
 MAX_RES = 8
 MAX_SHAPE = 16     # KSG_MAX_SHAPE
 
@@ -115,7 +116,26 @@ class KsgCapture(C.Structure):
 class KsgEvalRows(C.Structure):
     """ksg_eval_rows: the per-cycle rows in library memory."""
     _fields_ = [("n_nodes", C.c_int32), ("elem_bytes", C.c_int32), ("fstatus", u32p),
-                ("raw", C.c_void_p * NPLUGINS), ("norm", C.c_void_p * NPLUGINS), ("total", C.c_void_p)]
+                ("raw", C.c_void_p * NPLUGINS), ("norm", C.c_void_p * NPLUGINS), ("total", C.c_void_p),
+                ("norm_from_raw", C.c_uint32), ("norm_scored", C.c_uint32), ("norm_max", C.c_int64 * NPLUGINS)]
+
+
+def derive_norm(plugin: int, raw: np.ndarray, mx: int, fstatus: np.ndarray, scored: bool) -> np.ndarray:
+    """DefaultNormalizeScore of a row the per-cycle kernel leaves to the host
+    (ksg_eval_rows.norm_from_raw): TaintToleration reversed, NodeAffinity
+    plain, integer division by the maximum over the feasible nodes; 0 at
+    infeasible nodes and when the pod was not scored."""
+    out = np.zeros(len(raw), np.int64)
+    if not scored:
+        return out
+    feas = fstatus == 0
+    r = raw.astype(np.int64)
+    if plugin == PL_TAINT_TOLERATION:
+        v = 100 - (100 * r) // mx if mx else np.full(len(r), 100, np.int64)
+    else:
+        v = (100 * r) // mx if mx else r
+    out[feas] = v[feas]
+    return out
 
 
 class KsgNodeState(C.Structure):
@@ -202,7 +222,7 @@ def make_profile(fields: dict) -> KsgProfile:
     return p
 
 
-RUN_NARROW_SWEEP, RUN_SLOT32, RUN_TCOL, RUN_SPEC, RUN_WIDE_MEM = 1, 2, 4, 8, 16   # ksg_last_run_info flags
+RUN_NARROW_SWEEP, RUN_SLOT32, RUN_SPEC, RUN_WIDE_MEM = 1, 2, 8, 16   # ksg_last_run_info flags
 
 
 class CaptureBuffers:
@@ -293,6 +313,7 @@ class Engine:
                            C.POINTER(KsgCapture))
         self._last_ms = f("last_kernel_ms", C.c_int, vp, C.POINTER(C.c_double))
         self._run_info = f("last_run_info", C.c_int, vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32))
+        self._recoveries = f("recoveries", C.c_int, vp, C.POINTER(C.c_int32))
         self._set_timing = f("set_timing", C.c_int, vp, C.c_int)
         self._kernel_stats = f("kernel_stats", C.c_int, vp, C.POINTER(KsgKernelStat), C.c_int32,
                                C.POINTER(C.c_int32))
@@ -352,10 +373,14 @@ class Engine:
 
         def row(ptr):
             return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), (n,)).astype(np.int64)
-        out = {"fstatus": np.ctypeslib.as_array(v.fstatus, (n,)).copy(), "elem_bytes": v.elem_bytes,
-               "raw": {p: row(v.raw[p]) for p in range(NPLUGINS) if v.raw[p]},
-               "norm": {p: row(v.norm[p]) for p in range(NPLUGINS) if v.norm[p]},
-               "total": row(v.total)}
+        fs = np.ctypeslib.as_array(v.fstatus, (n,)).copy()
+        raw = {p: row(v.raw[p]) for p in range(NPLUGINS) if v.raw[p]}
+        norm = {p: row(v.norm[p]) for p in range(NPLUGINS) if v.norm[p]}
+        for p in range(NPLUGINS):   # the rows the caller derives (ksg_eval_rows.norm_from_raw)
+            if (v.norm_from_raw >> p) & 1:
+                norm[p] = derive_norm(p, raw[p], v.norm_max[p], fs, (v.norm_scored >> p) & 1)
+        out = {"fstatus": fs, "elem_bytes": v.elem_bytes, "raw": raw, "norm": norm,
+               "total": row(v.total) if v.total else None}
         return r, out
 
     def append_pods(self, pods: np.ndarray, prog: np.ndarray, prog_base: int):
@@ -493,6 +518,12 @@ class Engine:
         p, fl = C.c_int32(), C.c_int32()
         self._check(self._run_info(self.ctx, C.byref(p), C.byref(fl)))
         return p.value, fl.value
+
+    def recoveries(self) -> int:
+        """Grid-barrier timeouts recovered by a cooperative relaunch (ksg_recoveries)."""
+        n = C.c_int32()
+        self._check(self._recoveries(self.ctx, C.byref(n)))
+        return n.value
 
     def last_kernel_ms(self) -> float:
         v = C.c_double()

@@ -17,13 +17,9 @@ G = importlib.import_module("kube-scheduler-simulator_amd.generator")
 E = importlib.import_module("kube-scheduler-simulator_amd.encoder")
 native = importlib.import_module("kube-scheduler-simulator_amd.native")
 
-MODES = [("window", {"KSG_BATCH_MODE": "window"}),
-         ("window-128", {"KSG_BATCH_MODE": "window", "KSG_SLOT_BLOCK": "128"}),
-         ("slot", {"KSG_BATCH_MODE": "slot"}), ("slot-64", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "64"}),
-         ("tcol", {"KSG_BATCH_MODE": "tcol"}),
-         ("tcol-nowindow-64", {"KSG_BATCH_MODE": "tcol", "KSG_PIPE_WINDOW": "0", "KSG_SLOT_BLOCK": "64"}),
-         ("spec", {"KSG_BATCH_MODE": "spec"}),
-         ("spec-xpose", {"KSG_BATCH_MODE": "spec", "KSG_SPEC_TRANSPOSE": "1"})]
+MODES = [("spec", {"KSG_BATCH_MODE": "spec"}),
+         ("window", {"KSG_BATCH_MODE": "window"}),
+         ("slot", {"KSG_BATCH_MODE": "slot"}), ("slot-128", {"KSG_BATCH_MODE": "slot", "KSG_SLOT_BLOCK": "128"})]
 
 
 def main():
@@ -35,7 +31,7 @@ def main():
     nodes, pods, prof = G.config2(n_nodes=a.nodes, n_pods=a.pods)
     enc = E.Encoder(nodes, pods, prof)
     pf = E.encode_profile(prof, enc.cluster.res_names)
-    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK", "KSG_SPEC_TRANSPOSE")
+    keys = ("KSG_BATCH_MODE", "KSG_PIPE_WINDOW", "KSG_SLOT_BLOCK")
     want = set(a.modes.split(","))
     ref = None
     for name, env in MODES:

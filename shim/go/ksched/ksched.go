@@ -169,6 +169,10 @@ type PodEval struct {
 	raw, norm           [NPlugins]unsafe.Pointer
 	total               unsafe.Pointer
 	keep                [][]int64 // Eval: the Go rows the pointers above refer to
+	// the normalised rows the per-cycle kernel leaves to the caller
+	// (ksg_eval_rows.norm_from_raw): derived from raw and normMax
+	normFromRaw, normScored uint32
+	normMax                 [NPlugins]int64
 }
 
 func (e *PodEval) at(p unsafe.Pointer, node int) int64 {
@@ -187,10 +191,33 @@ func (e *PodEval) at(p unsafe.Pointer, node int) int64 {
 // Raw is plugin's Score() value at node (0 for a plugin the profile does not score).
 func (e *PodEval) Raw(plugin, node int) int64 { return e.at(e.raw[plugin], node) }
 
-// Norm is plugin's value after NormalizeScore at node.
-func (e *PodEval) Norm(plugin, node int) int64 { return e.at(e.norm[plugin], node) }
+// Norm is plugin's value after NormalizeScore at node.  TaintToleration and
+// NodeAffinity on the node-local per-cycle path are DefaultNormalizeScore of
+// the raw value with the device's maximum over the feasible nodes (reverse
+// for TaintToleration), computed here: the kernel no longer stores them.
+func (e *PodEval) Norm(plugin, node int) int64 {
+	if e.normFromRaw>>uint(plugin)&1 == 0 {
+		return e.at(e.norm[plugin], node)
+	}
+	if e.normScored>>uint(plugin)&1 == 0 || e.FStatus[node] != 0 {
+		return 0
+	}
+	raw, mx := e.at(e.raw[plugin], node), e.normMax[plugin]
+	if plugin == TaintToleration {
+		if mx == 0 {
+			return 100
+		}
+		return 100 - 100*raw/mx
+	}
+	if mx == 0 {
+		return raw
+	}
+	return 100 * raw / mx
+}
 
-// Total is the weighted sum at node (0: not scored).
+// Total is the weighted sum at node (0: not scored, or not materialised:
+// the node-local per-cycle path leaves it out, the framework sums the
+// weights itself).
 func (e *PodEval) Total(node int) int64 { return e.at(e.total, node) }
 
 // NumNodes is the number of node columns.
@@ -214,6 +241,10 @@ func (x *Ctx) EvalView(pod int) (*PodEval, error) {
 		e.raw[p], e.norm[p] = unsafe.Pointer(rows.raw[p]), unsafe.Pointer(rows.norm[p])
 	}
 	e.total = unsafe.Pointer(rows.total)
+	e.normFromRaw, e.normScored = uint32(rows.norm_from_raw), uint32(rows.norm_scored)
+	for p := 0; p < NPlugins; p++ {
+		e.normMax[p] = int64(rows.norm_max[p])
+	}
 	e.Selected, e.NFeasible = int(res.selected), int(res.n_feasible)
 	e.Status, e.ScoreSkip = uint32(res.status), uint32(res.score_skip)
 	return e, nil

@@ -32,7 +32,7 @@ def test_library_exports_every_symbol(built):
     missing = [s for s in declared_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     lib.ksg_abi_version.restype = ctypes.c_int
-    assert lib.ksg_abi_version() == 3
+    assert lib.ksg_abi_version() == 4
 
 
 def test_struct_layouts_match(tmp_path):

@@ -1,12 +1,13 @@
-"""GPU parity of every phase-2 variant of the batched placement path
-(KSG_BATCH_MODE): "slot" at each block size,
-"tcol" (the transposed walk, ksched_phase2t.h: in the two-stream
-pipeline with the previous batch's nodes as carried columns, serialised with
-timing on, and without the window at 128- and 64-pod batches; the slot walk
-where its scope check fails), "window" (the default: the slot walk inside the two-stream pipeline with
-the two-batch window; also without the window, at 128-pod batches and with
-per-kernel timing on, which runs the same arithmetic without overlap), and (opt-in) "topset" and "scan".  Same bar as the default path: placements, per-pod results and node
-state bit-exact against the C++ oracle, including split calls."""
+"""GPU parity of every phase-2 form of the batched placement path
+(KSG_BATCH_MODE): "spec" (the default: the speculate-and-verify
+walk in the two-stream pipeline, serialised with timing on), "window" (the
+slot walk inside the pipeline with the two-batch window: the spec walk's
+fallback outside its scope; also without the window and with per-kernel timing
+on, which runs the same arithmetic without overlap) and "slot" (one launch
+chain per batch, at 64- and 128-pod batches: the captured queues' form).
+Same bar as the default path: placements, per-pod results and node state
+bit-exact against the C++ oracle, including split calls.  (Round 6 retired
+"scan", "topset" and "tcol".)"""
 import numpy as np
 import pytest
 
@@ -27,21 +28,12 @@ def _have_gpu():
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _have_gpu(), reason="needs an MI355X")]
 
-# (mode, extra env).  "window" is the default (the slot walk, one lane per
-# slot, at 64-pod batches).
-# "topset" and "scan" (the round-1 forms, 7.5 and 13 us per pod) and the
-# extra slot block sizes run only with KSG_TEST_ALL_VARIANTS=1: they are not
-# on any default path and cost GPU minutes.
-import os
+# (mode, extra env).  "spec" is the default; "window" its fallback (the slot
+# walk, one lane per slot, at 64-pod batches).
 MODES = {"window": ("window", {}), "window-timed": ("window", {"_timing": 1}),
-         "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "window128": ("window", {"KSG_SLOT_BLOCK": 128}),
-         "slot": ("slot", {}),
-         "tcol": ("tcol", {}), "tcol-nowindow64": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 64}),
+         "window-nowindow": ("window", {"KSG_PIPE_WINDOW": 0}), "slot": ("slot", {}),
+         "slot128": ("slot", {"KSG_SLOT_BLOCK": 128}),
          "spec": ("spec", {}), "spec-timed": ("spec", {"_timing": 1})}
-if os.environ.get("KSG_TEST_ALL_VARIANTS") == "1":
-    MODES.update({"slot128": ("slot", {"KSG_SLOT_BLOCK": 128}), "slot256": ("slot", {"KSG_SLOT_BLOCK": 256}),
-                  "topset": ("topset", {}), "scan": ("scan", {}), "tcol-timed": ("tcol", {"_timing": 1}),
-                  "tcol-nowindow": ("tcol", {"KSG_PIPE_WINDOW": 0, "KSG_SLOT_BLOCK": 128})})
 
 
 @pytest.fixture(scope="module", params=list(MODES))
@@ -126,48 +118,7 @@ def test_slot32_refused_on_sub_mib_memory(oracle):
     oracle.load(enc, pf)
     pl, _ = a.run_queue(0, len(pods))
     path, flags = a.last_run_info()
-    assert path == 2 and not flags & (native.RUN_TCOL | native.RUN_SLOT32)   # the int64 slot walk
-    np.testing.assert_array_equal(pl, oracle.run_queue(0, len(pods))[0])
-
-
-# ---- the transposed walk (KSG_RUN_TCOL) -----------------------------------------
-@pytest.mark.parametrize("strategy", ["least", "most"])
-def test_tcol_runs_and_matches_oracle(oracle, strategy):
-    """Config 2 runs phase 2 as the transposed walk (one wave, lane = pod, a
-    column per changed node); MostAllocated re-chooses nodes within a batch, so
-    the column rewrites and the rescans of the running maxima run too."""
-    P = pkg("profile")
-    nodes, pods, prof = G.config2(n_nodes=1500, n_pods=2500, seed=21)
-    if strategy == "most":
-        prof = P.config2_profile(strategy=P.MOST_ALLOCATED)
-    enc = E.Encoder(nodes, pods, prof)
-    pf = E.encode_profile(prof, enc.cluster.res_names)
-    a = _engine_with_batch_mode("tcol")
-    a.load(enc, pf)
-    oracle.load(enc, pf)
-    pl, res = a.run_queue(0, len(pods))
-    assert a.last_run_info() == (2, native.RUN_SLOT32 | native.RUN_TCOL)
-    po, ro = oracle.run_queue(0, len(pods))
-    np.testing.assert_array_equal(pl, po)
-    for f in ("n_feasible", "status", "score_skip"):
-        np.testing.assert_array_equal(res[f], ro[f], err_msg=f)
-    R = len(enc.cluster.res_names)
-    for x, y in zip(a.read_state(R), oracle.read_state(R)):
-        np.testing.assert_array_equal(x, y)
-
-
-def test_tcol_out_of_scope_falls_back(oracle):
-    """Sub-MiB memory fails the N32 check: the slot walk's int64 instances run."""
-    nodes, pods, prof = G.config2(n_nodes=300, n_pods=400, seed=9)
-    nodes[3].allocatable["memory"] += 4096
-    enc = E.Encoder(nodes, pods, prof)
-    pf = E.encode_profile(prof, enc.cluster.res_names)
-    a = _engine_with_batch_mode("tcol")
-    a.load(enc, pf)
-    oracle.load(enc, pf)
-    pl, _ = a.run_queue(0, len(pods))
-    path, flags = a.last_run_info()
-    assert path == 2 and not flags & (native.RUN_TCOL | native.RUN_SLOT32)   # the int64 slot walk
+    assert path == 2 and not flags & native.RUN_SLOT32   # the int64 slot walk
     np.testing.assert_array_equal(pl, oracle.run_queue(0, len(pods))[0])
 
 

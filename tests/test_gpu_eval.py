@@ -89,6 +89,19 @@ def test_eval_cycle_server_matches_oracle(oracle, monkeypatch, name):
         eng.close()
 
 
+def test_eval_cycle_server_across_reloads(oracle, monkeypatch):
+    """One context, two workloads, the persistent server running for both: a
+    reload stops the server and reallocates its relay block, and the next
+    server must not take the zeroed relay for a call (round 6 fix)."""
+    monkeypatch.setenv("KSG_CYCLE_SERVER", "1")
+    eng = native.Engine(device=0)
+    try:
+        for name in ("c2-1000x120", "c1-100x150", "zoo-1"):
+            _check_cycles(eng, oracle, name, *CASES[name]())
+    finally:
+        eng.close()
+
+
 def test_eval_cycle_server_interleaved_with_queue_runs(oracle, monkeypatch):
     """Calls that need the stream (a queue run, a non-deferrable assume, a
     reload) stop the server and the next evaluation starts it again, reading
@@ -239,7 +252,12 @@ def test_cycles_from_an_empty_snapshot(built):
 def test_eval_view_equals_eval_with_capture(gpu, built):
     """ksg_eval_view leaves the rows in library memory: the same status words,
     raw / normalised rows and totals as ksg_eval with capture buffers, on the
-    per-cycle path and (topology pods) its chip-wide topology form."""
+    per-cycle path and (topology pods) its chip-wide topology form.  The
+    node-local per-cycle kernel stores no normalised rows and no totals
+    (round 6): the view's TaintToleration / NodeAffinity rows are derived from
+    the raw rows and the maxima (native.derive_norm), as the Go shim derives
+    them, and must equal the capture's (which test_eval_cycle_matches_oracle
+    compares with the oracle's)."""
     import zoo
     for nodes, pods, prof in (G.config2(n_nodes=1500, n_pods=30, seed=3), zoo.zoo(2, n_pods=40)):
         enc = E.Encoder(nodes, pods, prof)
@@ -257,7 +275,10 @@ def test_eval_view_equals_eval_with_capture(gpu, built):
             for p in rows:
                 np.testing.assert_array_equal(cap.raw[0, p], v["raw"][p])
                 np.testing.assert_array_equal(cap.norm[0, p], v["norm"][p])
-            np.testing.assert_array_equal(cap.total[0], v["total"])
+            if v["total"] is not None:   # (the node-local per-cycle kernel leaves the totals out)
+                np.testing.assert_array_equal(cap.total[0], v["total"])
+            else:
+                assert gpu.last_run_info()[0] == 5
             if ra.selected >= 0:
                 gpu.commit(i, ra.selected)
 
