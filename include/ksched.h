@@ -333,13 +333,14 @@ int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out);
  * pods on it with lower priority than `pod`, most important first:
  * util.MoreImportantPod order) are vic_pod[vic_off[k] .. vic_off[k+1]).
  * Per candidate: remove every potential victim, re-run the filters that read
- * the node's pods for `pod` (NodeResourcesFit; PodTopologySpread and
- * InterPodAffinity with the PreFilter counts of the candidate's domains moved
- * by the removals, as the RemovePod / AddPod extensions move them upstream)
+ * the node's pods for `pod` (NodeResourcesFit; NodePorts on the UsedPorts
+ * the removals leave; PodTopologySpread and InterPodAffinity with the
+ * PreFilter counts of the candidate's domains moved by the removals, as the
+ * RemovePod / AddPod extensions move them upstream)
  * (fits[k] = 0: the node cannot help), then reprieve the victims in order,
  * each staying evicted (victim[i] = 1) only if `pod` no longer fits with it
  * back.  Node-static filters are not re-run: the caller
- * (preemption.check_scope) requires them ordered before those three.
+ * (preemption.check_scope) requires them ordered before those four.
  * KSG_E_UNSUPPORTED when the preemptor's terms exceed the dry run's limits. */
 int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int32_t n_cand,
                         const int32_t* vic_off, const int32_t* vic_pod, int32_t* fits, uint8_t* victim);

@@ -3475,8 +3475,6 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
   if ((rc = check_blobs(ctx, pod, 1))) return rc;
   if ((rc = flush_stage(ctx))) return rc;
   if ((rc = flush_commit(ctx))) return rc;
-  if (ctx->h_pods[pod].ports >= 0)   // the dry run re-runs Fit / PTS / IPA only
-    return fail(ctx, KSG_E_UNSUPPORTED, "preemption: a preemptor with host ports (NodePorts) is not modelled");
   if (n_cand == 0) return KSG_OK;
   const int32_t nv = vic_off[n_cand];
   if (vic_off[0] != 0 || nv < 0 || (nv > 0 && (!vic_pod || !victim)))
@@ -3492,6 +3490,15 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
   bool fit_on = false;
   for (int kf = 0; kf < ctx->prof.n_filter; kf++) fit_on |= ctx->prof.filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
   fit_on = fit_on && !((p.filter_skip >> KSG_PL_NODE_RESOURCES_FIT) & 1u);
+  // NodePorts re-runs on the UsedPorts the removals leave (PrePorts)
+  bool ports_on = false;
+  for (int kf = 0; kf < ctx->prof.n_filter; kf++) ports_on |= ctx->prof.filter_order[kf] == KSG_PL_NODE_PORTS;
+  ports_on = ports_on && !((p.filter_skip >> KSG_PL_NODE_PORTS) & 1u) && p.ports >= 0 && ctx->st.ports;
+  if (ports_on) {
+    if ((size_t)p.ports >= ctx->h_prog.size() || ctx->h_prog[p.ports] > kPreMaxConf)
+      return fail(ctx, KSG_E_UNSUPPORTED, "preemption: more than " + std::to_string(kPreMaxConf) +
+                                              " conflicting host-port entries for the preemptor");
+  }
   // one scratch block: cand | off | vic | fits | victim
   const size_t words = (size_t)n_cand + (n_cand + 1) + nv + n_cand + (nv + 3) / 4;
   if (words > ctx->pre_words) {
@@ -3526,12 +3533,12 @@ int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int
                        ctx->d_prog, ctx->d_preprof, pod, ctx->d_pretopo);
     hipLaunchKernelGGL(ksg_preempt_topo, dim3((n_cand + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
                        ctx->d_pods, ctx->d_prog, ctx->d_preprof, pod, ctx->d_pretopo, d_cand, n_cand, d_off, d_vic,
-                       d_fits, d_victim);
+                       d_fits, d_victim, ports_on ? 1 : 0);
     HIPC(ctx, hipMemcpyAsync(&topo_ok, &ctx->d_pretopo->ok, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
   } else {
     hipLaunchKernelGGL(ksg_preempt_kernel, dim3((n_cand + 255) / 256), dim3(256), 0, ctx->stream, ctx->c, ctx->st,
-                       ctx->d_pods, pod, ctx->prof.fit_ignored_res, fit_on ? 1 : 0, d_cand, n_cand, d_off, d_vic,
-                       d_fits, d_victim);
+                       ctx->d_pods, ctx->d_prog, pod, ctx->prof.fit_ignored_res, fit_on ? 1 : 0, ports_on ? 1 : 0,
+                       d_cand, n_cand, d_off, d_vic, d_fits, d_victim);
   }
   HIPC(ctx, hipGetLastError());
   HIPC(ctx, hipMemcpyAsync(fits, d_fits, sizeof(int32_t) * n_cand, hipMemcpyDeviceToHost, ctx->stream));

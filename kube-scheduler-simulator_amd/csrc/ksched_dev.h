@@ -1873,16 +1873,48 @@ __global__ __launch_bounds__(256) void ksg_commit_batch_kernel(DevCluster c, Dev
 // pass is off the per-pod critical path (it runs for pods with no feasible
 // node only).
 #ifndef KSG_PART
-__global__ __launch_bounds__(256) void ksg_preempt_kernel(DevCluster c, DevState st, const ksg_pod* pods, int pod,
-                                                          uint32_t ignored, int fit_on, const int32_t* cand,
-                                                          int n_cand, const int32_t* off, const int32_t* vic,
-                                                          int32_t* fits, uint8_t* victim) {
+// NodePorts in the preemption dry run: which of the preemptor's conflict ids
+// (ksg_pod.ports, at most kPreMaxConf: the host refuses more) are set in the
+// node's UsedPorts, as a bit mask.  A victim's removal clears the ids it owns
+// and its re-addition sets them (set semantics, as ports_commit and upstream
+// HostPortInfo: a removal drops an entry another pod on the node may share).
+constexpr int kPreMaxConf = 64;
+struct PrePorts {
+  const int32_t* conf = nullptr;
+  int nconf = 0;
+  uint64_t bits = 0;
+  __device__ void init(const int32_t* w, const uint32_t* used, int N, int n) {
+    if (!w || !used) return;
+    nconf = w[0] < kPreMaxConf ? w[0] : kPreMaxConf;
+    conf = w + 1;
+    for (int j = 0; j < nconf; j++) {
+      const uint32_t id = (uint32_t)conf[j];
+      if ((used[(size_t)(id >> 5) * N + n] >> (id & 31)) & 1u) bits |= 1ull << j;
+    }
+  }
+  __device__ void move(const int32_t* w, int sign) {   // the pod's own ids (w: its ports program)
+    if (!conf || !w) return;
+    const int32_t* own = w + 1 + w[0];
+    for (int i = 0; i < own[0]; i++)
+      for (int j = 0; j < nconf; j++)
+        if (conf[j] == own[1 + i]) bits = sign > 0 ? bits | (1ull << j) : bits & ~(1ull << j);
+  }
+  __device__ bool ok() const { return bits == 0; }
+};
+
+__global__ __launch_bounds__(256) void ksg_preempt_kernel(DevCluster c, DevState st, const ksg_pod* pods,
+                                                          const int32_t* prog, int pod, uint32_t ignored, int fit_on,
+                                                          int ports_on, const int32_t* cand, int n_cand,
+                                                          const int32_t* off, const int32_t* vic, int32_t* fits,
+                                                          uint8_t* victim) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_cand) return;
   const int n = cand[k];
   NodeCols L;
   load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
   const ksg_pod& p = pods[pod];
+  PrePorts pp;
+  pp.init(ports_on ? prog + p.ports : nullptr, st.ports, c.N, n);
   const int b = off[k], e = off[k + 1];
   auto move = [&](const ksg_pod& v, int sign) {
 #pragma unroll
@@ -1891,15 +1923,17 @@ __global__ __launch_bounds__(256) void ksg_preempt_kernel(DevCluster c, DevState
     L.nz_cpu += sign * v.nz_cpu;
     L.nz_mem += sign * v.nz_mem;
     L.pod_count += sign;
+    pp.move(v.ports >= 0 ? prog + v.ports : nullptr, sign);
   };
+  auto passes = [&]() { return pp.ok() && (!fit_on || fit_filter(c, p, L, ignored) == 0); };
   for (int i = b; i < e; i++) move(pods[vic[i]], -1);
-  const bool ok = !fit_on || fit_filter(c, p, L, ignored) == 0;
+  const bool ok = passes();
   fits[k] = ok ? 1 : 0;
   for (int i = b; i < e; i++) {
     uint8_t out = 0;
     if (ok) {
       move(pods[vic[i]], +1);
-      if (fit_on && fit_filter(c, p, L, ignored) != 0) {
+      if (!passes()) {
         move(pods[vic[i]], -1);
         out = 1;
       }

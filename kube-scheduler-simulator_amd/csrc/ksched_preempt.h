@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void ksg_preempt_topo(DevCluster c, DevState s
                                                         const int32_t* prog, const ksg_profile* profp, int pod,
                                                         const PreemptTopo* topo, const int32_t* cand, int n_cand,
                                                         const int32_t* off, const int32_t* vic, int32_t* fits,
-                                                        uint8_t* victim) {
+                                                        uint8_t* victim, int ports_on) {
   __shared__ int32_t s_blob[KSG_BLOB_MAX];
   __shared__ ksg_pod s_pod;
   __shared__ ksg_profile s_prof;
@@ -281,9 +281,12 @@ __global__ __launch_bounds__(256) void ksg_preempt_topo(DevCluster c, DevState s
   NodeCols L;
   load_cols(c, st.requested, st.nonzero, st.pod_count, n, L);
   PreDelta d{};
+  PrePorts pp;
+  pp.init(ports_on ? prog + p.ports : nullptr, st.ports, N, n);
   const int b = off[k], e = off[k + 1];
   auto move = [&](int q, int sign) {
     const ksg_pod& w = pods[q];
+    pp.move(w.ports >= 0 ? prog + w.ports : nullptr, sign);
 #pragma unroll
     for (int r = 0; r < KSG_MAX_RES; r++)
       if (r < c.R) L.req[r] += sign * w.req[r];
@@ -294,6 +297,7 @@ __global__ __launch_bounds__(256) void ksg_preempt_topo(DevCluster c, DevState s
   };
   const bool all = pts_on && has_all(c, g.hard, g.n_hard, 7, n);
   auto passes = [&]() -> bool {
+    if (!pp.ok()) return false;
     if (fit_on && fit_filter(c, p, L, prof.fit_ignored_res) != 0) return false;
     if (pts_on) {
       for (int i = 0; i < g.n_hard; i++) {

@@ -372,6 +372,31 @@ def preemption_topo_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 1
     return nodes, pods, bound, prof
 
 
+def preemption_ports_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, seed: int = 31):
+    """preemption_case with host ports: a third of the running pods and half
+    of the queued pods hold a host port from a small set (8080/TCP on every
+    IP, 9090/TCP, 53/UDP, 127.0.0.1:7000), so that queued pods meet NodePorts
+    rejections a lower-priority victim's eviction resolves (DefaultPreemption
+    with NodePorts re-run in the dry run)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes, pods, bound, prof = preemption_case(n_nodes=n_nodes, n_bound=n_bound, n_queue=n_queue, seed=seed)
+    choices = [("", "", 8080), ("", "TCP", 9090), ("", "UDP", 53), ("127.0.0.1", "TCP", 7000)]
+    nb = len(bound)
+    used = {}   # node -> set of sanitised ports held by the running pods (no conflicts among them)
+    for pi, ni in bound:
+        if rng.random() < 0.33:
+            hp = choices[int(rng.integers(len(choices)))]
+            key = (m.sanitize_host_port(hp[0], hp[1]), hp[2])
+            if key in used.setdefault(ni, set()):
+                continue
+            used[ni].add(key)
+            pods[pi].containers[0].host_ports = (hp,)
+    for p in pods[nb:]:
+        if rng.random() < 0.5:
+            p.containers[0].host_ports = (choices[int(rng.integers(len(choices)))],)
+    return nodes, pods, bound, prof
+
+
 def host_ports_case(n_nodes: int = 40, n_queue: int = 240, seed: int = 9, daemonset: bool = True):
     """NodePorts parity case.  Every node runs a DaemonSet-style pod already
     bound to it (hostPort 9100/TCP, as a node exporter; `daemonset`), ingested

@@ -30,8 +30,10 @@ steps, and where each one runs here:
    `evaluateNominatedNode`): when it passes, it is the only feasible node and
    the pod binds there without scoring.
 
-The dry run re-runs the filters that read the node's pods: NodeResourcesFit
-and, for a preemptor with hard spread constraints or required inter-pod terms
+The dry run re-runs the filters that read the node's pods: NodeResourcesFit,
+NodePorts (a preemptor with host ports: the node's UsedPorts as the removed /
+reprieved victims leave them, set semantics as upstream's HostPortInfo) and,
+for a preemptor with hard spread constraints or required inter-pod terms
 (or matched by existing pods' anti-affinity), PodTopologySpread and
 InterPodAffinity with the PreFilter counts of the candidate's domains moved by
 the removed / reprieved pods (ksched_preempt.h; the oracles recompute the
@@ -135,20 +137,17 @@ def pick_one_node(cands: Sequence[Tuple[int, Sequence[m.Pod], int]]) -> int:
     return pool[0][0]
 
 
-_POD_DEPENDENT = (P.NODE_RESOURCES_FIT, P.POD_TOPOLOGY_SPREAD, P.INTER_POD_AFFINITY)
+_POD_DEPENDENT = (P.NODE_RESOURCES_FIT, P.NODE_PORTS, P.POD_TOPOLOGY_SPREAD, P.INTER_POD_AFFINITY)
 
 
 def check_scope(prof: P.Profile, pod: m.Pod, pods: Sequence[m.Pod]) -> None:
     """Refuse preemption the dry run cannot decide exactly: it re-runs the
-    filters that read the node's pods (Fit, PodTopologySpread,
+    filters that read the node's pods (Fit, NodePorts, PodTopologySpread,
     InterPodAffinity), so every node-static filter must come before them."""
     if pod.claim_names() and set(prof.filter_order()) & {P.VOLUME_RESTRICTIONS, P.VOLUME_BINDING, P.VOLUME_ZONE}:
         # the dry run re-runs Fit / PTS / IPA only; VolumeRestrictions' AddPod /
         # RemovePod extensions (ReadWriteOncePod users) are not modelled
         raise NotImplementedError("DefaultPreemption for a preemptor with claims (volume plugins)")
-    if pod.host_ports() and P.NODE_PORTS in prof.filter_order():
-        # the device dry run re-runs Fit / PTS / IPA only (ksg_preempt)
-        raise NotImplementedError("DefaultPreemption for a preemptor with host ports (NodePorts)")
     order = prof.filter_order()
     first = min((order.index(p) for p in _POD_DEPENDENT if p in order), default=None)
     if first is not None:

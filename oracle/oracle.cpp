@@ -942,9 +942,10 @@ void uncommit(Ctx& c, int pi, int n) {
 // and re-addition through the plugins' RemovePod / AddPod extensions; here the
 // PodTopologySpread and InterPodAffinity PreFilter states are recomputed from
 // scratch on the modified cluster (the same counts, by their definition), with
-// the PreFilter Skip decisions of the original cycle.  The node's pods are
-// restored afterwards.  Node-static filters are not re-run: the caller only
-// passes nodes whose first rejection came from Fit / PTS / IPA with every
+// the PreFilter Skip decisions of the original cycle; NodePorts reads the
+// node's UsedPorts as the removals leave them.  The node's pods are restored
+// afterwards.  Node-static filters are not re-run: the caller only passes
+// nodes whose first rejection came from Fit / NodePorts / PTS / IPA with every
 // static filter ordered before them (preemption.check_scope).
 void select_victims(Ctx& c, int pi, int n, const int32_t* vic, int nv, int32_t& fits, uint8_t* victim) {
   const ksg_pod& p = c.pods[pi];
@@ -956,7 +957,15 @@ void select_victims(Ctx& c, int pi, int n, const int32_t* vic, int nv, int32_t& 
   const IpaProg ig = ipa_prog(c, p);
   bool ipa_on = false;
   if (p.ipa >= 0 && on(KSG_PL_INTER_POD_AFFINITY)) ipa_on = !ipa_prefilter(c, p, ig).skip;
+  // NodePorts on the node's UsedPorts as the removals / re-additions leave
+  // them (uncommit / commit: set semantics, upstream HostPortInfo)
+  const bool ports_on = on(KSG_PL_NODE_PORTS) && p.ports >= 0;
   auto passes = [&]() {
+    if (ports_on) {
+      const int32_t* w = c.prog.data() + p.ports;
+      for (int i = 0; i < w[0]; i++)
+        if (c.used_ports[n].count(w[1 + i])) return false;
+    }
     if (fit_on && fit_filter(c, p, n) != 0) return false;
     if (pts_on && pts_filter(c, pg, pts_prefilter(c, p, pg), n) != 0) return false;
     if (ipa_on && ipa_filter(c, ig, ipa_prefilter(c, p, ig), n) != 0) return false;

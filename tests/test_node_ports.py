@@ -217,14 +217,29 @@ def test_native_status_message(built):
     assert code == F.Status.UNSCHEDULABLE and msg == MSG
 
 
-def test_preemptor_with_host_ports_refused():
+@pytest.mark.parametrize("engine", ["oracle", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_preemptor_with_host_ports_kat(engine, request):
+    """Worked by hand: n0 runs "low" (priority 0, hostPort 80) and "keep"
+    (priority 0, hostPort 81); "high" (priority 100) wants 80.  NodePorts
+    rejects n0 (Unschedulable: preemption may help); the dry run removes both
+    lower-priority pods, reprieves "low" first (the more important by name
+    order at equal priority and start) -- 80 is then held again, so "low"
+    stays evicted -- then "keep", which fits.  One victim, "low"; the retry
+    binds "high" on n0.  (Round 5 refused every preemptor with host ports.)"""
+    import binding
     nodes = _one_node()
-    run = _pod("low", [("", "TCP", 80)], node="n0")
-    run.priority = 0
+    low, keep = _pod("low", [("", "TCP", 80)], node="n0"), _pod("keep", [("", "TCP", 81)], node="n0")
     cand = _pod("high", [("", "TCP", 80)])
+    low.priority = keep.priority = 0
     cand.priority = 100
-    with pytest.raises(NotImplementedError, match="host ports"):
-        PR.check_scope(P.default_profile(), cand, [run, cand])
+    pods = [low, keep, cand]
+    PR.check_scope(P.default_profile(), cand, pods)   # in scope now
+    eng = binding.Oracle(1) if engine == "oracle" else (request.getfixturevalue("built") and native.Engine(device=0))
+    s = F.DebuggableScheduler(nodes, pods, P.default_profile(), engine=eng, bound=[(0, 0), (1, 0)])
+    placed = s.schedule_one(2)
+    (pi, nom, victims), = s.preemptions
+    assert (pi, nom, [pods[v].name for v in victims]) == (2, 0, ["low"])
+    assert placed == 0
 
 
 # ---- GPU: the UsedPorts bitmap on the device -------------------------------------

@@ -177,7 +177,45 @@ def test_topology_preemption_framework_vs_pyoracle(seed):
     assert ann == ora
 
 
+def _port_preemptions(s, pods):
+    return [pi for pi, _, _ in s.preemptions if pods[pi].host_ports()]
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33])
+def test_host_port_preemption_framework_vs_pyoracle(seed):
+    """Preemptors with host ports: the dry run re-runs
+    NodePorts on the UsedPorts the removed / reprieved victims leave (C++
+    oracle: set semantics, as upstream's HostPortInfo) against pyoracle's
+    trial NodeInfo, annotation bytes included.  Parity vs Go unpinned."""
+    nodes, pods, bound, prof = G.preemption_ports_case(seed=seed)
+    s, placed, ann = _run_framework(_oracle_engine(), nodes, pods, bound, prof)
+    nb = len(bound)
+    ora, recs = pyoracle_annotations(nodes, pods[nb:], prof, bound=[(pods[i], nodes[n].name) for i, n in bound])
+    assert _port_preemptions(s, pods), "no preemption by a pod with host ports"
+    assert [r["selected_index"] for r in recs] == placed
+    pre = [(pi - nb, s.node_names[n], [(pods[v].namespace, pods[v].name) for v in vs]) for pi, n, vs in s.preemptions]
+    ref = [(k, r["first_attempt"]["nominated"], r["first_attempt"]["victims"])
+           for k, r in enumerate(recs) if "first_attempt" in r]
+    assert pre == ref
+    assert ann == ora
+
+
 # ---- GPU: the dry run and the deletions on the device ------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [31, 32, 34])
+def test_gpu_host_port_preemption_matches_pyoracle(built, seed):
+    """The device's dry run with NodePorts (PrePorts: the preemptor's conflict
+    ids tracked through the removals and reprieves) against pyoracle."""
+    nodes, pods, bound, prof = G.preemption_ports_case(seed=seed, n_nodes=60, n_bound=260, n_queue=160)
+    s, placed, ann = _run_framework(native.Engine(device=0), nodes, pods, bound, prof)
+    nb = len(bound)
+    ora, recs = pyoracle_annotations(nodes, pods[nb:], prof, bound=[(pods[i], nodes[n].name) for i, n in bound])
+    assert _port_preemptions(s, pods)
+    assert [r["selected_index"] for r in recs] == placed
+    assert ann == ora
+
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [7, 8, 9, 10])
 def test_gpu_preemption_matches_pyoracle(built, seed):
