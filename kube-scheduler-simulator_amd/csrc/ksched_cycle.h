@@ -146,6 +146,8 @@ struct SrvArgs {
   unsigned* d_go;                    // 128-byte line: the relayed call's sequence number
   unsigned last;                     // the last sequence number served before this launch
   int32_t want_img;                  // the profile scores ImageLocality: keep the image slots
+  int32_t direct;                    // 1: the mailbox is fine-grained device memory: every workgroup polls
+                                     // it and reads the call itself (no relay)
 };
 
 // The node a lane evaluates, its columns prefetched: the first kCycLab label
@@ -702,7 +704,11 @@ __device__ __forceinline__ T sys_ld(const T* p) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The persistent form.  Workgroup 0 alone polls the host mailbox (lane 0,
+// The persistent form.  With the mailbox in fine-grained device memory
+// (SrvArgs::direct, the default where the CPU maps it: round 6) every
+// workgroup polls its sequence word and reads the call in place: HBM, not
+// PCIe, so no relay.  Otherwise (pinned host memory):
+// workgroup 0 alone polls the host mailbox (lane 0,
 // one PCIe read in flight at a time), reads the call and its programs, and
 // relays them into device memory behind a go word (agent-scope stores); the
 // other workgroups poll the go word and read the relayed copy, so PCIe carries
@@ -722,7 +728,8 @@ __global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
   const int G = (int)gridDim.x;
   const CycStatic& S = a.s;
   const int N = S.c.N;
-  const bool relay = blockIdx.x == 0;
+  const bool direct = a.direct != 0;
+  const bool relay = !direct && blockIdx.x == 0;
   int nk[KN];
   NodeCols L[KN];
   PNode nd[KN];
@@ -742,7 +749,7 @@ __global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
     if (lane == 0) {
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
-        seq = relay ? sys_ld(&mb->seq) : gld(a.d_go);
+        seq = relay || direct ? sys_ld(&mb->seq) : gld(a.d_go);
         if (seq != last) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kSrvIdle || gld(S.timeout)) break;
         __builtin_amdgcn_s_sleep(1);
@@ -751,7 +758,13 @@ __global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
     seq = (unsigned)__builtin_amdgcn_readfirstlane((int)seq);
     if (seq == last) break;   // idle or a timed-out exchange elsewhere: leave
     // ---- the call and its programs into LDS (workgroup 0: from the host, relayed) -------
-    if (relay) {
+    if (direct) {   // the mailbox in device memory: read it in place (system scope: the CPU wrote it)
+      const int32_t* src = reinterpret_cast<const int32_t*>(&mb->k);
+      for (int i = lane; i < KW; i += 64) reinterpret_cast<int32_t*>(&s_k)[i] = sys_ld(src + i);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const int blen = s_k.op != 0 ? 0 : s_k.blob_len;
+      for (int i = lane; i < blen; i += 64) s_blob[i] = sys_ld(mb->blob + i);
+    } else if (relay) {
       const int32_t* src = reinterpret_cast<const int32_t*>(&mb->k);
       int32_t* dst = reinterpret_cast<int32_t*>(a.d_call);
       for (int i = lane; i < KW; i += 64) {
