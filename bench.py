@@ -47,7 +47,8 @@ Prints ONE JSON line (rank 0).  The line also carries:
   (bulk.annotate_queue, captured rows + ksg_annotate on 16 threads), plus the
   device serialiser's steady state over a longer queue;
 * `per_cycle` / `per_cycle_configs2` (N = 1): the drop-in's per-cycle C-ABI
-  path, call by call from C; `per_cycle_server` the persistent server mode,
+  path, call by call from C (the persistent server, the default since round
+  6); `per_cycle_launch` one kernel launch per cycle,
   `per_cycle_hinted` one pending-pod hint per cycle instead of all up front.
 """
 from __future__ import annotations
@@ -374,7 +375,7 @@ def device_serialiser_long(eng, enc, prof, B, n_pods: int, chunk: int, threads: 
 
 
 def per_cycle_sidecar(native, G, S, n_nodes: int, warm: int, n_pods: int, make=None, label: str = "configs[1]",
-                      server: bool = False, hint_ahead: int = 0):
+                      server: bool = True, hint_ahead: int = 0):
     """The drop-in's per-cycle path, the calls the Go
     shim makes per scheduling cycle, through the C ABI of libksched.so:
     ksg_snapshot_add_pod -> ksg_snapshot_sync (append to the device
@@ -719,12 +720,12 @@ def main():
             log(f"[rank {rank}] annotation sidecar unavailable: {e}")
     if eng1 is not None:
         eng1.close()
-    cyc = cyc_srv = cyc_hint = None
+    cyc = cyc_launch = cyc_hint = None
     if world == 1 and args.cycle_pods > 0:
         try:
             S = importlib.import_module(PKG + ".snapshot")
             cyc = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods)
-            cyc_srv = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods, server=True)
+            cyc_launch = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods, server=False)
             # pods created while the queue runs, one hint per cycle
             cyc_hint = per_cycle_sidecar(native, G, S, args.nodes, args.cycle_warm, args.cycle_pods, hint_ahead=8)
         except Exception as e:
@@ -792,7 +793,7 @@ def main():
         out["source_hash"] = {"library": ge.library_hash(), "tree": ge.source_hash()}
         out["source_hash"]["matches"] = out["source_hash"]["library"] == out["source_hash"]["tree"]
         for key, val in (("configs1", c1), ("replica_sweep", sweep), ("annotations", ann), ("per_cycle", cyc),
-                         ("per_cycle_server", cyc_srv), ("per_cycle_hinted", cyc_hint),
+                         ("per_cycle_launch", cyc_launch), ("per_cycle_hinted", cyc_hint),
                          ("kubelet_memory", kub), ("per_cycle_configs2", cyc3), ("annotations_configs2", ann3)):
             if val is not None:
                 out[key] = val

@@ -364,6 +364,7 @@ int ksg_last_kernel_ms(ksg_ctx* ctx, double* ms);
 /* 4: the transposed walk (KSG_RUN_TCOL, retired in ABI 4) */
 #define KSG_RUN_SPEC 8           /* phase 2 was the speculate-and-verify walk (ksg_batch_phase2v) */
 #define KSG_RUN_WIDE_MEM 16      /* ... in its wide-memory instance (memory not whole MiB: int64 bytes) */
+#define KSG_RUN_TOPO_WINDOW 32   /* path 4 ran the speculative topology queue (window rows + walk) */
 int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
 
 /* Grid-barrier timeouts this context recovered from since it opened.  The
@@ -376,6 +377,12 @@ int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags);
  * result.  A timeout under a cooperative launch is KSG_E_DEVICE.  (No
  * reference counterpart: device residency.) */
 int ksg_recoveries(ksg_ctx* ctx, int32_t* n);
+
+/* The last placement run's speculative topology queue (KSG_RUN_TOPO_WINDOW):
+ * windows walked, pods decided, windows a changed node ended early.  All 0
+ * when the run took another path.  (No reference counterpart: the reference
+ * schedules one pod per cycle.) */
+int ksg_topo_window_stats(ksg_ctx* ctx, int64_t* windows, int64_t* pods, int64_t* cut);
 
 /* Per-kernel timing of the next runs (off by default: it adds one event
  * record per launch).  With timing on, ksg_kernel_stats() returns, per kernel
@@ -399,7 +406,9 @@ enum {
   KSG_K_CAPTURE_NORM = 10,
   KSG_K_EVAL_CYCLE = 11,
   KSG_K_BATCH_PHASE2V = 12,
-  KSG_NKERNELS = 13
+  KSG_K_TOPO_WIN_ROWS = 13,
+  KSG_K_TOPO_WALK = 14,
+  KSG_NKERNELS = 15
 };
 typedef struct ksg_kernel_stat {
   char name[48];

@@ -64,6 +64,7 @@ struct ksg_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
   int last_path = 0;   // 1 = queue kernel, 2 = batched, 3 = replica sweep, 4 = chip-wide topology
+  bool last_window = false;   // path 4 ran the speculative topology queue (ksched_topo_win.h)
   ksg_profile prof{};
   bool have_prof = false, have_nodes = false, have_wl = false;
   // cluster
@@ -145,6 +146,13 @@ struct ksg_ctx {
   // hipLaunchCooperativeKernel (a process that made cooperative launches
   // faulted in libamdhip64's exit-time teardown under rocprofv3).
   bool coop_launch = false;
+  // the speculative topology queue (ksched_topo_win.h; env KSG_TOPO_WINDOW=0
+  // disables): one device block for the rows' outputs, flags and partials
+  bool topo_window = true;
+  char* d_win = nullptr;
+  size_t win_bytes = 0;
+  int win_kmax = kWinMax;              // env KSG_TOPO_WINDOW_K: pods per window (1 .. kWinMax)
+  unsigned long long win_stats[3] = {0, 0, 0};   // the last run: windows, pods decided, windows cut short
   int32_t* d_tables = nullptr;        // the maintained domain tables and their index (ksched_topo_tables.h)
   size_t tables_words = 0;
   // The per-cycle tables (ksg_eval of topology pods): the whole selector
@@ -249,8 +257,9 @@ struct ksg_ctx {
   size_t state_bak_bytes = 0;               // timeout restores it and relaunches cooperatively)
   CycArgs cyc_args{};                       // ksg_eval_cycle's launch arguments, rebuilt in place per call
   unsigned cyc_last_G = 0;                  // the grid of the last per-cycle call (its counter counts multiples of it)
-  // the persistent per-cycle server (env KSG_CYCLE_SERVER=1, ksched_cycle.h ksg_cycle_server)
-  bool srv_mode = false;
+  // the persistent per-cycle server (ksched_cycle.h ksg_cycle_server; the default since round 6,
+  // KSG_CYCLE_SERVER=0: one launch per cycle)
+  bool srv_mode = true;
   bool srv_running = false;
   int srv_kn = 0;
   unsigned srv_G = 0;
@@ -375,6 +384,8 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_coop_srec = nullptr;
   ctx->d_tables = nullptr;
   ctx->tables_words = 0;
+  ctx->d_win = nullptr;
+  ctx->win_bytes = 0;
   ctx->d_state_bak = nullptr;
   ctx->state_bak_bytes = 0;
   ctx->d_pct = nullptr;
@@ -399,7 +410,7 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_topk", "ksg_batch_phase2s", "ksg_sweep_static",
                                           "ksg_sweep", "ksg_topo_coop", "ksg_sweep_narrow",
                                           "ksg_capture_eval", "ksg_capture_norm", "ksg_eval_cycle",
-                                          "ksg_batch_phase2v"};
+                                          "ksg_batch_phase2v", "ksg_topo_coop_window", "ksg_topo_walk"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -1541,9 +1552,9 @@ bool build_topo_tables(ksg_ctx* ctx, int32_t first, int32_t count, TopoTables* o
   return true;
 }
 
-int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
-                  const ksg_profile* d_prof, int do_commit = 1, const CoopCap* cap = nullptr,
-                  bool timed = true) {
+// The chip-wide topology path's group shape (nodes per lane, G, the LDS
+// variant), once per node set.
+int coop_shape(ksg_ctx* ctx) {
   const int N = ctx->c.N;
   int rc;
   if (ctx->coop_cfg_N != N) {   // the group shape, once per node set
@@ -1573,11 +1584,21 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
     ctx->coop_cfg_N = N;
     ctx->coop_dirty = true;   // (the one-pod completion counter counts arrivals modulo G)
   }
+  return KSG_OK;
+}
+
+int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
+                  const ksg_profile* d_prof, int do_commit = 1, const CoopCap* cap = nullptr,
+                  bool timed = true) {
+  const int N = ctx->c.N;
+  int rc;
+  if ((rc = coop_shape(ctx))) return rc;
   const int kn = ctx->coop_kn, G = ctx->coop_G;
   const bool ll = ctx->coop_ll;
   if (!ctx->d_coop_acc) {
     if ((rc = dalloc(ctx, &ctx->d_coop_acc, 2))) return rc;
-    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [4] timeout, [6] one-pod completion counter
+    if (!ctx->d_coop_flags && (rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;   // [4] timeout, [6] one-pod
+                                                                                      // completion counter
     if ((rc = dalloc(ctx, &ctx->d_coop_wgflags, (size_t)256 * 32))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_parts, 256))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_coop_phist, (size_t)256 * kCoopPHist))) return rc;
@@ -1744,6 +1765,228 @@ int run_topo_coop(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg
   }
   HIPC(ctx, hipGetLastError());
   if (timed) HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  return KSG_OK;
+}
+
+// The speculative topology queue (ksched_topo_win.h) over pods [first, first +
+// count) of a placement run.  *used = false (nothing launched) when the run is
+// outside its scope: one node per lane, no host ports or volumes (an assume
+// that changes what a node-local plugin reads outside the walk's
+// re-evaluation), the maintained tables, at least two rows of G workgroups
+// co-resident; the caller then runs ksg_topo_coop.
+//
+// Window lengths come from the pods' programs alone: pod j joins the window
+// of the pods before it when none of them writes (commit program: matched
+// selectors, owned templates) what j reads (its constraints' and terms'
+// selectors, the templates matching it).  The launches are device-driven: the
+// host enqueues one (rows, walk) pair per window the lengths predict, then
+// reads the cursor once; a window the walk ended early leaves pods for a
+// second, shorter round.
+int run_topo_window(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res,
+                    const ksg_profile* d_prof, bool* used) {
+  *used = false;
+  int rc;
+  if (!ctx->topo_window || ctx->coop_launch || !ctx->coop_tables || count < 2) return KSG_OK;
+  if ((rc = coop_shape(ctx))) return rc;
+  if (ctx->coop_kn != 1) return KSG_OK;
+  for (int32_t i = first; i < first + count; i++)
+    if (ctx->h_pods[i].ports >= 0 || ctx->h_pods[i].vol >= 0) return KSG_OK;
+  const int N = ctx->c.N, G = ctx->coop_G;
+  const bool ll = ctx->coop_ll;
+  const void* kf = ll ? (const void*)ksg_topo_coop<1, true, 3> : (const void*)ksg_topo_coop<1, false, 3>;
+  int occ = 0, cus = 0;
+  HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kf, 256, 0));
+  HIPC(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  const int kmax = std::min(ctx->win_kmax, (occ * cus) / std::max(G, 1));
+  if (kmax < 2) return KSG_OK;
+  TopoTables tt{};
+  if (!build_topo_tables(ctx, first, count, &tt, &rc)) return rc;
+  ctx->pct_valid = false;   // the run moves the counts without the per-cycle tables
+  // ---- window lengths -------------------------------------------------------
+  const int S = ctx->c.S, T = ctx->c.n_tmpl;
+  const int32_t* P = ctx->h_prog.data();
+  std::vector<int32_t> rd_off(count + 1, 0), wr_off(count + 1, 0), rd, wr;
+  for (int32_t k = 0; k < count; k++) {
+    const ksg_pod& p = ctx->h_pods[first + k];
+    auto sel = [&](std::vector<int32_t>& v, int32_t s) { if (s >= 0 && s < S) v.push_back(s); };
+    auto tmpl = [&](std::vector<int32_t>& v, int32_t t) { if (t >= 0 && t < T) v.push_back(S + t); };
+    if (p.pts >= 0) {
+      const int32_t* w = P + p.pts;
+      const int nh = w[0], ns = w[1];
+      for (int q = 0; q < nh; q++) sel(rd, w[3 + 7 * q + 1]);
+      for (int q = 0; q < ns; q++) sel(rd, w[3 + 7 * nh + 6 * q + 1]);
+    }
+    if (p.ipa >= 0) {
+      const int32_t* w = P + p.ipa;
+      const int na = w[0];
+      if (na > 0) sel(rd, w[1]);
+      w += 3 + na;
+      const int nanti = *w++;
+      for (int q = 0; q < nanti; q++) sel(rd, w[2 * q + 1]);
+      w += 2 * nanti;
+      const int npref = *w++;
+      for (int q = 0; q < npref; q++) sel(rd, w[3 * q + 1]);
+      w += 3 * npref;
+      for (int lst = 0; lst < 3; lst++) {
+        const int nm = *w++;
+        for (int q = 0; q < nm; q++) tmpl(rd, w[q]);
+        w += nm;
+      }
+    }
+    if (p.commit >= 0) {
+      const int32_t* w = P + p.commit;
+      const int ns = w[0];
+      for (int q = 0; q < ns; q++) sel(wr, w[1 + q]);
+      const int nt = w[1 + ns];
+      for (int q = 0; q < nt; q++) tmpl(wr, w[2 + ns + 2 * q]);
+    }
+    rd_off[k + 1] = (int32_t)rd.size();
+    wr_off[k + 1] = (int32_t)wr.size();
+  }
+  std::vector<int32_t> wlen(count), stamp((size_t)S + T, -1);
+  for (int32_t s0 = 0; s0 < count; s0++) {
+    int len = 0;
+    for (int32_t j = s0; j < count && len < kmax; j++, len++) {
+      bool clash = false;
+      for (int32_t q = rd_off[j]; q < rd_off[j + 1] && !clash; q++) clash = stamp[rd[q]] == s0;
+      if (clash) break;
+      for (int32_t q = wr_off[j]; q < wr_off[j + 1]; q++) stamp[wr[q]] = s0;
+    }
+    wlen[s0] = std::max(len, 1);
+  }
+  auto windows_from = [&](int32_t pos) {   // launches if no window ends early
+    int n = 0;
+    while (pos < count) { pos += wlen[pos]; n++; }
+    return n;
+  };
+  // ---- the device block ------------------------------------------------------
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_cur = 0, o_stats = 128, o_len = 256, o_tot = o_len + al(sizeof(int32_t) * count),
+               o_top = o_tot + al(sizeof(int32_t) * kmax * N),
+               o_pod = o_top + al(sizeof(unsigned long long) * kmax * G * kmax),
+               o_parts = o_pod + al(sizeof(WinPod) * kmax), o_phist = o_parts + al(sizeof(CoopPart) * kmax * G),
+               o_acc = o_phist + al(sizeof(int32_t) * kmax * G * kCoopPHist),
+               o_bar = o_acc + al(sizeof(CoopAcc) * 2 * kmax), o_arr = o_bar + al(sizeof(unsigned) * kmax * G * 32),
+               bytes = o_arr + al(sizeof(unsigned) * kmax * 32);
+  if (!ctx->d_coop_flags) {   // the timeout word (shared with ksg_topo_coop)
+    if ((rc = dalloc(ctx, &ctx->d_coop_flags, 8))) return rc;
+    ctx->coop_dirty = true;
+  }
+  if (bytes > ctx->win_bytes) {
+    if (ctx->d_win) {
+      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_win);
+      if (it != ctx->allocs.end()) ctx->allocs.erase(it);
+      HIPC(ctx, hipStreamSynchronize(ctx->stream));
+      (void)hipFree(ctx->d_win);
+      ctx->d_win = nullptr;
+      ctx->win_bytes = 0;
+    }
+    if ((rc = dalloc(ctx, &ctx->d_win, bytes))) return rc;
+    ctx->win_bytes = bytes;
+  }
+  char* b = ctx->d_win;
+  // flags, partials, atomics sets, counters: zero per run (barrier epochs
+  // start from the run's first generation)
+  HIPC(ctx, hipMemsetAsync(b, 0, o_tot, ctx->stream));
+  HIPC(ctx, hipMemsetAsync(b + o_pod, 0, bytes - o_pod, ctx->stream));
+  HIPC(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b + o_cur), first, 1, ctx->stream));
+  HIPC(ctx, hipMemcpyAsync(b + o_len, wlen.data(), sizeof(int32_t) * count, hipMemcpyHostToDevice, ctx->stream));
+  if (ctx->coop_dirty) {   // the timeout word (shared with ksg_topo_coop)
+    HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags, 0, 32, ctx->stream));
+  }
+  CoopArgs a{};
+  a.c = ctx->c;
+  a.st = ctx->st;
+  a.pods = ctx->d_pods;
+  a.prog = ctx->d_prog;
+  a.profile = d_prof;
+  a.G = G;
+  a.parts = reinterpret_cast<CoopPart*>(b + o_parts);
+  a.phist = reinterpret_cast<int32_t*>(b + o_phist);
+  a.acc = reinterpret_cast<CoopAcc*>(b + o_acc);
+  a.bar = reinterpret_cast<unsigned*>(b + o_bar);
+  a.arrive = reinterpret_cast<unsigned*>(b + o_arr);
+  a.pmode = ctx->coop_pmode;
+  a.timeout = ctx->d_coop_flags + 4;
+  a.commit = 0;
+  a.tt = tt;
+  a.use_tables = 1;
+  a.fused_static = 1;
+  a.win_cursor = reinterpret_cast<const int32_t*>(b + o_cur);
+  a.win_len = reinterpret_cast<const int32_t*>(b + o_len);
+  a.win_base = first;
+  a.win_end = first + count;
+  a.win_kmax = kmax;
+  a.win_tot = reinterpret_cast<int32_t*>(b + o_tot);
+  a.win_top = reinterpret_cast<unsigned long long*>(b + o_top);
+  a.win_pod = reinterpret_cast<WinPod*>(b + o_pod);
+  WalkArgs w{};
+  w.c = ctx->c;
+  w.st = ctx->st;
+  w.tt = tt;
+  w.use_tables = 1;
+  w.pods = ctx->d_pods;
+  w.profile = d_prof;
+  w.cursor = reinterpret_cast<int32_t*>(b + o_cur);
+  w.win_len = a.win_len;
+  w.win_base = first;
+  w.win_end = first + count;
+  w.win_kmax = kmax;
+  w.G = G;
+  w.win_tot = a.win_tot;
+  w.win_top = a.win_top;
+  w.win_pod = a.win_pod;
+  w.prog = ctx->d_prog;
+  w.placements = d_pl;
+  w.results = d_res;
+  w.timeout = a.timeout;
+  w.wstats = reinterpret_cast<unsigned long long*>(b + o_stats);
+#ifdef KSG_STAMPS
+  if (!ctx->d_stamps) {
+    if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
+    HIPC(ctx, hipMemsetAsync(ctx->d_stamps, 0, 128, ctx->stream));
+  }
+  a.stamps = ctx->d_stamps;
+#endif
+  *used = true;
+  (void)hipGetLastError();
+  treset(ctx);
+  HIPC(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  if ((rc = tmark(ctx))) return rc;
+  unsigned gen = 0;
+  int steps = windows_from(0);
+  int32_t pos = 0;   // the predicted window's start (the timing's units: node-evals of its rows)
+  for (;;) {
+    for (int s = 0; s < steps; s++) {
+      const int32_t wl = pos < count ? wlen[pos] : 0;
+      pos += wl;
+      if (++gen >= 0xffffu) {   // barrier epochs are (gen << 16) + k: reset the flags before they wrap
+        HIPC(ctx, hipMemsetAsync(b + o_bar, 0, sizeof(unsigned) * kmax * G * 32, ctx->stream));
+        gen = 1;
+      }
+      a.gen = gen;
+      if ((ctx->inject_timeout & 1) && pos > 16 && pos - wl < count) {   // test injection: after some windows,
+        ctx->inject_timeout &= ~1;                                      // the rows find the timeout word set
+        HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags + 4, 0x01, sizeof(unsigned), ctx->stream));
+      }
+      void* kargs[] = {&a};
+      HIPC(ctx, hipLaunchKernel(kf, dim3(G, kmax), dim3(256), kargs, 0, ctx->stream));
+      if ((rc = tlaunched(ctx, KSG_K_TOPO_WIN_ROWS, (double)wl * N))) return rc;
+      hipLaunchKernelGGL(ksg_topo_walk, dim3(1), dim3(256), 0, ctx->stream, w);
+      if ((rc = tlaunched(ctx, KSG_K_TOPO_WALK, (double)wl))) return rc;
+    }
+    HIPC(ctx, hipGetLastError());
+    int32_t cur = 0;
+    unsigned to = 0;
+    HIPC(ctx, hipMemcpyAsync(&cur, b + o_cur, sizeof(cur), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(ctx, hipMemcpyAsync(&to, ctx->d_coop_flags + 4, sizeof(to), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(ctx, hipStreamSynchronize(ctx->stream));
+    if (to || cur >= first + count) break;   // done, or a row's barrier timed out (run_internal recovers)
+    steps = windows_from(cur - first);
+    pos = cur - first;
+  }
+  HIPC(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  HIPC(ctx, hipMemcpyAsync(ctx->win_stats, b + o_stats, sizeof(ctx->win_stats), hipMemcpyDeviceToHost, ctx->stream));
   return KSG_OK;
 }
 
@@ -1916,6 +2159,7 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
   if ((rc = flush_stage(ctx))) return rc;
   if ((rc = flush_commit(ctx))) return rc;
   if (do_commit) ctx->pct_valid = false;   // the queue's assumes bypass the per-cycle tables
+  ctx->last_window = false;
   const size_t N = ctx->c.N;
   Tmp tmp;
   ksg_profile* d_prof = nullptr;
@@ -2038,7 +2282,11 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
       // workgroups were not all resident) restores it and relaunches
       // cooperatively instead of failing over partial commits
       if (do_commit && !ctx->coop_launch && (rc = state_copy(ctx, true))) return rc;
-      if ((rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof, do_commit, want_cap ? &cc : nullptr))) return rc;
+      bool win = false;
+      if (do_commit && !want_cap && (rc = run_topo_window(ctx, first, count, d_pl, d_res, d_prof, &win))) return rc;
+      ctx->last_window = win;
+      if (!win && (rc = run_topo_coop(ctx, first, count, d_pl, d_res, d_prof, do_commit, want_cap ? &cc : nullptr)))
+        return rc;
     } else if ((rc = launch_queue(ctx, a, 1, block, topo))) {
       return rc;
     }
@@ -2258,7 +2506,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   if (ctx->srv_running) {   // a server launched for other arguments, or idle long enough to be near its own exit
     const double idle = std::chrono::duration<double>(std::chrono::steady_clock::now() - ctx->srv_last).count();
     if (!server || ctx->srv_kn != kn || ctx->srv_G != G || ctx->srv_img != want_img || ctx->srv_sys != ctx->cycle_sys ||
-        idle > 0.25 || std::memcmp(&ctx->srv_static, &cs, sizeof(CycStatic)) != 0)
+        idle > 0.05 || std::memcmp(&ctx->srv_static, &cs, sizeof(CycStatic)) != 0)
       if ((rc = srv_stop(ctx))) return rc;
   }
   // test injection: this launch's exchange finds the sticky timeout word set
@@ -3075,6 +3323,8 @@ int ksg_open(int device, ksg_ctx** out) {
   }
   if (const char* f = getenv("KSG_FORCE_PATH")) ctx->force_path = atoi(f);
   if (const char* f = getenv("KSG_TOPO_COOP")) ctx->topo_coop = atoi(f) != 0;
+  if (const char* f = getenv("KSG_TOPO_WINDOW")) ctx->topo_window = atoi(f) != 0;
+  if (const char* f = getenv("KSG_TOPO_WINDOW_K")) ctx->win_kmax = std::max(1, std::min(atoi(f), kWinMax));
   if (const char* f = getenv("KSG_COOP_PMODE")) ctx->coop_pmode = atoi(f) != 0;
   if (const char* f = getenv("KSG_COOP_TABLES")) ctx->coop_tables = atoi(f) != 0;
   if (const char* f = getenv("KSG_DEFER_COMMIT")) ctx->defer_commit = atoi(f) != 0;
@@ -3842,6 +4092,15 @@ int ksg_kernel_stats(ksg_ctx* ctx, ksg_kernel_stat* out, int32_t max, int32_t* n
   return KSG_OK;
 }
 
+int ksg_topo_window_stats(ksg_ctx* ctx, int64_t* windows, int64_t* pods, int64_t* cut) {
+  if (!ctx || !windows || !pods || !cut) return KSG_E_INVALID;
+  const bool w = ctx->last_window;
+  *windows = w ? (int64_t)ctx->win_stats[0] : 0;
+  *pods = w ? (int64_t)ctx->win_stats[1] : 0;
+  *cut = w ? (int64_t)ctx->win_stats[2] : 0;
+  return KSG_OK;
+}
+
 int ksg_recoveries(ksg_ctx* ctx, int32_t* n) {
   if (!ctx || !n) return KSG_E_INVALID;
   *n = ctx->recoveries;
@@ -3853,7 +4112,7 @@ int ksg_last_run_info(ksg_ctx* ctx, int32_t* path, int32_t* flags) {
   *path = ctx->last_path;
   *flags = (ctx->last_narrow ? KSG_RUN_NARROW_SWEEP : 0) | (ctx->last_n32 ? KSG_RUN_SLOT32 : 0) |
            (ctx->last_spec ? KSG_RUN_SPEC : 0) |
-           (ctx->last_mw ? KSG_RUN_WIDE_MEM : 0);
+           (ctx->last_mw ? KSG_RUN_WIDE_MEM : 0) | (ctx->last_window ? KSG_RUN_TOPO_WINDOW : 0);
   return KSG_OK;
 }
 

@@ -49,7 +49,7 @@
 // registers / LDS, and each cycle's call (CycCall + programs) arrives in a
 // pinned host mailbox the workgroups poll, so a cycle pays neither a launch
 // nor the entry latencies.  It leaves on a stop request, after kSrvIdle of
-// idleness (the host never calls a server idle for more than 0.25 s: it
+// idleness (the host never calls a server idle for more than 0.05 s: it
 // restarts it instead, so a call never races the idle exit), or when an
 // exchange times out, so every wave always ends.
 //
@@ -67,8 +67,11 @@ constexpr int kCycTnt = 8;       // taint slots prefetched into registers
 constexpr int kCycImg = 8;       // image slots prefetched into registers (ImageLocality pods)
 constexpr int kCycEff = 4096;    // taint-effect bytes staged in LDS
 constexpr int kCycMaxKN = 4;     // nodes per lane
-constexpr unsigned long long kSrvIdle = 1000000000ull;   // server: 10 s of the 100 MHz real-time clock
-                                                        // (the host restarts a server idle for 0.25 s)
+constexpr unsigned long long kSrvIdle = 10000000ull;   // server: 0.1 s of the 100 MHz real-time clock (the
+                                                      // host restarts a server idle for 0.05 s).  Short: a
+                                                      // running server holds back every device-wide
+                                                      // synchronisation of the process (hipFree) until it
+                                                      // leaves
 
 // What does not change between calls on a loaded context.
 struct CycStatic {

@@ -1681,6 +1681,7 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
 #endif
 #if !defined(KSG_PART) || defined(KSG_WITH_TOPO)
 #include "ksched_topo_coop.h"
+#include "ksched_topo_win.h"
 #endif
 
 // dst[r * stride + i] = src[i] for every replica r = blockIdx.y (replica state

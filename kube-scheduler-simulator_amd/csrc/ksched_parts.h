@@ -21,6 +21,10 @@ KSG_INST ksg_topo_coop<1, true, 0>(CoopArgs);
 KSG_INST ksg_topo_coop<1, true, 1>(CoopArgs);
 KSG_INST ksg_topo_coop<1, true, 2>(CoopArgs);
 #endif
+#if !defined(KSG_PART) || KSG_PART == 4
+KSG_INST ksg_topo_coop<1, false, 3>(CoopArgs);
+KSG_INST ksg_topo_coop<1, true, 3>(CoopArgs);
+#endif
 #if !defined(KSG_PART) || KSG_PART == 2
 KSG_INST ksg_topo_coop<2, false, 0>(CoopArgs);
 KSG_INST ksg_topo_coop<2, false, 1>(CoopArgs);

@@ -81,6 +81,19 @@ struct CoopAcc {    // atomics fallback for large histograms
   int32_t hist[KSG_HIST_MAX];
 };
 
+// A window pod's facts at the window's start (CAP == 3 writes them, the walk
+// reads them): what phase 4 would decide from, less the argmax.
+struct WinPod {
+  int32_t ok, nfeas, minidx, scored;
+  uint32_t err;          // ScoreError bits of every workgroup (or-ed; the walk zeroes it)
+  uint32_t status;       // KSG_ST_IPA_* flags
+  uint32_t score_skip;
+  uint32_t smask;        // the pod's Score plugins (make_view)
+  int32_t w_fit, w_ba;
+  int32_t fit_on;        // NodeResourcesFit's Filter runs for the pod
+  int32_t pad;
+};
+
 // gld / gst / gadd / gor and arrive_and_wait_sc1: ksched_sweep.h
 
 #ifdef KSG_STAMPS
@@ -146,6 +159,20 @@ struct CoopArgs {
   int64_t slen;
   unsigned* arrive;            // CAP == 2: the completion counter (never reset between launches: the last
                                // of each launch's G arrivals stores the result; zeroed with the flags)
+                               // CAP == 3: one per window row, 32 words apart
+  // CAP == 3, a window of the speculative topology queue (ksched_topo_win.h):
+  // grid (G, kmax); row y evaluates pod *win_cursor + y against the state the
+  // window starts from, with its own barrier flags / partial slots / atomics
+  // set (bar, parts, phist, acc offset by the row), and stores, instead of
+  // selecting and assuming, its nodes' static totals, its G tiles' best keys
+  // and the pod's facts for ksg_topo_walk
+  const int32_t* win_cursor;   // the run's first undecided pod (ksg_topo_walk advances it)
+  const int32_t* win_len;      // [pods of the run]: the window starting at that pod
+  int32_t win_base, win_end;   // the run's pods [win_base, win_end)
+  int32_t win_kmax;            // rows of the grid (gridDim.y)
+  int32_t* win_tot;            // [kmax][N]
+  unsigned long long* win_top; // [kmax][G][kmax]
+  WinPod* win_pod;             // [kmax]
 };
 
 // Hand-offs between the G workgroups without cache maintenance (MI355X guide,
@@ -402,6 +429,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   __shared__ int s_nlsel;           // ... and their number (may exceed kLagSel)
   __shared__ int s_wmin;            // this workgroup's lowest feasible node (phase 2)
   __shared__ unsigned long long s_wbest;   // this workgroup's best key (phase 3)
+  __shared__ unsigned long long s_wtop[NW];   // CAP == 3: the tile's best keys, one round at a time
   __shared__ uint8_t s_elig[kCoopBatch];    // tables_scope of the batch's pods
   __shared__ int s_inv;                     // the tables were invalidated (read per pod)
   __shared__ int4 s_fo[kTopoFill];          // the pod's fill tasks (tables' fo), loaded at setup
@@ -413,6 +441,23 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   const int N = cg.N;
   const DevState& st = a.st;
   const TopoTables& tt = a.tt;
+  // the pods of this launch: [first, first + count); CAP == 3 reads them from
+  // the window cursor, and row blockIdx.y takes pod first + blockIdx.y alone
+  static_assert(CAP != 3 || KN == 1, "window rows: one node per lane");
+  int first = a.first, count = a.count, kq_lo = 0;
+  if constexpr (CAP == 3) {
+    first = *a.win_cursor;
+    if (first >= a.win_end) return;
+    count = min(min(a.win_len[first - a.win_base], a.win_kmax), a.win_end - first);
+    kq_lo = (int)blockIdx.y;
+    if (kq_lo >= count) return;
+  }
+  const int kq_hi = CAP == 3 ? kq_lo + 1 : count;
+  const int row = CAP == 3 ? kq_lo : 0;   // this row's flags, partial slots and atomics set
+  CoopPart* const parts = a.parts + (size_t)row * G;
+  int32_t* const phist = a.phist + (size_t)row * G * kCoopPHist;
+  CoopAcc* const accs = a.acc + 2 * row;
+  unsigned* const rbar = a.bar + (size_t)row * G * 32;   // this row's barrier flags
   if (tid == 0) {
     s_lag.node = -1;
     s_lag.n_sel = s_lag.n_tmpl = 0;
@@ -422,13 +467,13 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   }
   for (int i_ = tid; i_ < (int)(sizeof(ksg_profile) / 4); i_ += (int)blockDim.x)
     reinterpret_cast<int32_t*>(&s_prof)[i_] = reinterpret_cast<const int32_t*>(a.profile)[i_];
-  for (int i = tid; i < a.count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
-    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
+  for (int i = tid; i < count * (int)(sizeof(ksg_pod) / 4); i += BLOCK)
+    reinterpret_cast<int32_t*>(s_pods)[i] = reinterpret_cast<const int32_t*>(a.pods + first)[i];
   if (!a.tables_inkernel)
-    for (int i = tid; i < a.count; i += BLOCK) s_elig[i] = a.use_tables ? tt.elig[a.first - tt.first + i] : 0;
+    for (int i = tid; i < count; i += BLOCK) s_elig[i] = a.use_tables ? tt.elig[first - tt.first + i] : 0;
   if (CAP == 2 && a.wpods && wg == 0) {   // the staged append to the device pool (read by later launches)
     for (int i = tid; i < (int)(sizeof(ksg_pod) / 4); i += BLOCK)
-      reinterpret_cast<int32_t*>(a.wpods)[i] = reinterpret_cast<const int32_t*>(a.pods + a.first)[i];
+      reinterpret_cast<int32_t*>(a.wpods)[i] = reinterpret_cast<const int32_t*>(a.pods + first)[i];
     for (int64_t i = tid; i < a.slen; i += BLOCK) a.wprog[i] = a.sprog[i];
   }
   const bool lab_lds = LL || (KN == 1 && cg.L <= kCoopLabCols);
@@ -468,8 +513,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   const bool ipa_in_score = (prof.score_mask >> KSG_PL_INTER_POD_AFFINITY) & 1u;
   unsigned target = a.gen << 16;   // this launch's barrier epochs
   int prev_fallback_words = 0;   // words of the previous pod's atomics-merged histograms (0: partial slots)
-  CoopPart* const mine = a.parts + wg;
-  int32_t* const myhist = a.phist + (size_t)wg * kCoopPHist;
+  CoopPart* const mine = parts + wg;
+  int32_t* const myhist = phist + (size_t)wg * kCoopPHist;
 #ifdef KSG_STAMPS
   unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
                      st_last = __builtin_amdgcn_s_memtime();
@@ -488,7 +533,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         const int x = x0 + u * BLOCK;
         w[u] = x / G;
         const int qg = x - w[u] * G;
-        y[u] = x < total ? gld(a.phist + (size_t)qg * kCoopPHist + base + w[u]) : 0;
+        y[u] = x < total ? gld(phist + (size_t)qg * kCoopPHist + base + w[u]) : 0;
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {
@@ -511,7 +556,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         const int x = x0 + u * BLOCK;
         const int qg = x / nw;
         w[u] = x - qg * nw;
-        y[u] = x < total && s_wkind[w[u]] != 2 ? gld(a.phist + (size_t)qg * kCoopPHist + w[u]) : 0;
+        y[u] = x < total && s_wkind[w[u]] != 2 ? gld(phist + (size_t)qg * kCoopPHist + w[u]) : 0;
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) {
@@ -544,15 +589,15 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   constexpr int kCoopPrefetch = 4;   // program words per lane prefetched for the next pod
   int32_t nb[kCoopPrefetch] = {0, 0, 0, 0};
   int nb_len = 0;
-  for (int kq = 0; kq < a.count; kq++) {
-    CoopAcc* acc = a.acc + (kq & 1);
-    CoopAcc* nxt = a.acc + ((kq + 1) & 1);
+  for (int kq = kq_lo; kq < kq_hi; kq++) {
+    CoopAcc* acc = accs + (kq & 1);
+    CoopAcc* nxt = accs + ((kq + 1) & 1);
     const uint64_t* srow = a.srec + (size_t)kq * N;
     __syncthreads();
     if (tid < (int)(sizeof(ksg_pod) / 4))
       reinterpret_cast<int32_t*>(&s_pod)[tid] = reinterpret_cast<const int32_t*>(&s_pods[kq])[tid];
     if (tid == BLOCK - 1) s_inv = s_tables_ok ? gld(tt.invalid) != 0 : 1;   // read beside the pod's staging
-    if (kq == 0 || nb_len > kCoopPrefetch * BLOCK) {
+    if (kq == kq_lo || nb_len > kCoopPrefetch * BLOCK) {   // (CAP 3: each row's first and only pod)
       const int boff = s_pods[kq].blob, blen = s_pods[kq].blob_len;
       for (int i = tid; i < blen; i += BLOCK) s_blob[i] = a.prog[boff + i];
     } else {   // prefetched during the previous pod's last barrier
@@ -624,7 +669,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
     const bool tab_read = pre_skip && s_tables_ok && ok;
     if (tab_read) {
       const TopoProg& g1 = s_g;
-      if (tid < kTopoFill && !a.tables_inkernel) s_fo[tid] = tt.fo[(size_t)(a.first - tt.first + kq) * kTopoFill + tid];
+      if (tid < kTopoFill && !a.tables_inkernel) s_fo[tid] = tt.fo[(size_t)(first - tt.first + kq) * kTopoFill + tid];
       if (g1.ipa && tid >= 64 && tid < 64 + 1 + g1.n_pref) {
         const int sel = tid == 64 ? g1.sel_all : g1.pref[3 * (tid - 65) + 1];
         s_totv[tid - 64] = sel >= 0 ? (long long)gld(tt.tot + sel) : 0;
@@ -809,7 +854,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     KSG_CSTAMP(1);
-    if (!skip && !coop_barrier(a.bar, a.timeout, G, target)) return;
+    if (!skip && !coop_barrier(rbar, a.timeout, G, target)) return;
     KSG_CSTAMP(2);
 
     // ---- phase 2: fold the partials into LDS; sweep A --------------------------
@@ -914,7 +959,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
 #pragma unroll
         for (int i = 0; i < kMaxSoft; i++) se[i] = 0;
         if (tid < G) {
-          const CoopPart* q = a.parts + tid;
+          const CoopPart* q = parts + tid;
 #pragma unroll
           for (int i = 0; i < kMaxHard; i++)
             if (need_hmin && i < g.n_hard) { hm[i] = gld(&q->hard_min[i]); hd[i] = gld(&q->hard_dom[i]); }
@@ -1030,7 +1075,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       ev[k] = eval_node_rec(c, prof, v, L, n, tn, cmp);
       KSG_CSTAMP(11);
       if (ev[k].st != 0) continue;
-      if constexpr (CAP != 0) {
+      if constexpr (CAP == 1 || CAP == 2) {
         fitr[k] = (v.smask & bit(KSG_PL_NODE_RESOURCES_FIT)) ? (int32_t)fit_score(prof, p, L) : 0;
         bar[k] = (v.smask & bit(KSG_PL_BALANCED_ALLOCATION)) ? (int32_t)ba_score(prof, p, L) : 0;
       }
@@ -1132,7 +1177,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         }
       }
     KSG_CSTAMP(6);
-    if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+    if (!coop_barrier(rbar, a.timeout, G, target)) return;
     KSG_CSTAMP(7);
     // CAP 2: the rows final since phase 2 (the status words and the raw
     // scores of every plugin but PodTopologySpread, whose raw count needs
@@ -1197,7 +1242,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       int32_t f_pr[kMaxSoft] = {0, 0, 0, 0}, f_se[kMaxSoft] = {0, 0, 0, 0};
       long long f_mmin = BIG, f_mmax = -BIG - 1, f_imin = BIG, f_imax = -BIG - 1;
       if (tid < G) {
-        const CoopPart* q = a.parts + tid;
+        const CoopPart* q = parts + tid;
         f_n = gld(&q->nfeas);
         f_min = gld(&q->minidx);
         f_mt = (int32_t)gld(&q->max_t);
@@ -1302,11 +1347,11 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           gst(&mine->pmin, get_l(6, OpMinL{}));
           gst(&mine->pmax, get_l(7, OpMaxL{}));
         }
-        if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+        if (!coop_barrier(rbar, a.timeout, G, target)) return;
         long long l2 = BIG, h2 = -BIG - 1;
         if (tid < G) {
-          l2 = gld(&a.parts[tid].pmin);
-          h2 = gld(&a.parts[tid].pmax);
+          l2 = gld(&parts[tid].pmin);
+          h2 = gld(&parts[tid].pmax);
         }
         bfold_l(l2, OpMinL{}, 8);
         bfold_l(h2, OpMaxL{}, 9);
@@ -1367,7 +1412,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         if constexpr (CAP != 0) ctot[k] = total;
       }
     }
-    if constexpr (CAP != 0) {   // every row of this lane's nodes (ksg_capture semantics: < 2 feasible nodes record no scores)
+    if constexpr (CAP == 1 || CAP == 2) {   // every row of this lane's nodes (ksg_capture semantics: < 2 feasible nodes record no scores)
       constexpr bool SYS = CAP == 2;
       const size_t NN = N;
       const int es = CAP == 2 ? a.cap_es : (a.cap_narrow ? 4 : 8);
@@ -1422,6 +1467,66 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       gst(&mine->best, b);
       gst(&mine->err, e);
       s_wbest = b;
+      if constexpr (CAP == 3)
+        if (e) __hip_atomic_fetch_or((__attribute__((address_space(1))) uint32_t*)&a.win_pod[row].err, (uint32_t)e,
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if constexpr (CAP == 3) {
+      // A window row ends here, before any select or assume (ksg_topo_walk
+      // decides): every node's static total, i.e. the weighted total less its
+      // NodeResourcesFit / BalancedAllocation part, the only part an earlier
+      // pod of the window can change (or -1: filtered out; 0: feasible, pod
+      // not scored); this tile's kq + 1 best keys (the walk's best unchanged
+      // node is among them when at most kq nodes changed); the pod's facts.
+      const int n0 = node_of(0);
+      const bool feas0 = ok && n0 < N && ev[0].st == 0;
+      if (n0 < N)
+        a.win_tot[(size_t)row * N + n0] = feas0 ? (scored ? (int32_t)(ctot[0] - (ev[0].part - ev[0].img)) : 0) : -1;
+      uint64_t key = scored && feas0 ? argmax_key(ctot[0], n0) : 0;
+      for (int r = 0; r <= row; r++) {
+        const uint64_t m = wreduce(key, OpMaxU64{});
+        if (lane == 0) s_wtop[wv] = m;
+        __syncthreads();
+        uint64_t b = s_wtop[0];
+        for (int i = 1; i < NW; i++) b = max(b, s_wtop[i]);
+        if (tid == 0) a.win_top[((size_t)row * G + wg) * a.win_kmax + r] = b;
+        if (key == b) key = 0;
+        __syncthreads();
+      }
+      if (wg == 0 && tid == 0) {
+        WinPod& w = a.win_pod[row];
+        uint32_t status = 0, score_skip = p.score_skip;
+        if (ipa_in_filter && s_t.ipa_skip_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
+        if (scored && ipa_in_score && !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u) && s_t.ipa_skip_score) {
+          status |= KSG_ST_IPA_PRESCORE_SKIP;
+          score_skip |= bit(KSG_PL_INTER_POD_AFFINITY);
+        }
+        bool fit_in = false;
+        for (int kf = 0; kf < prof.n_filter; kf++) fit_in |= prof.filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
+        w.ok = ok ? 1 : 0;
+        w.nfeas = ok ? gnfeas : 0;
+        w.minidx = gminidx;
+        w.scored = scored ? 1 : 0;
+        w.status = status;
+        w.score_skip = score_skip;
+        w.smask = v.smask;
+        w.w_fit = v.w_fit;
+        w.w_ba = v.w_ba;
+        w.fit_on = fit_in && !((v.fskip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) ? 1 : 0;
+      }
+      // this row's atomics set (soft marks; pre-pass histograms), read by
+      // every workgroup of the row in phase 3: the last to arrive zeroes it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)(a.arrive + row * 32),
+                                                    1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (old + 1) % (unsigned)G == 0 ? 1 : 0;
+      }
+      __syncthreads();
+      if (s_last)
+        for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&acc->hist[i], 0);
+      continue;
     }
     if (CAP == 2) {
       // The per-cycle evaluation (one pod, no assume): no barrier 3.  Each
@@ -1448,8 +1553,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
           unsigned long long b = 0;
           int32_t e = 0;
           for (int l = tid; l < G; l += 64) {
-            b = max(b, (unsigned long long)gld(&a.parts[l].best));
-            e |= gld(&a.parts[l].err);
+            b = max(b, (unsigned long long)gld(&parts[l].best));
+            e |= gld(&parts[l].err);
           }
           b = wreduce(b, OpMaxU64{});
           e = wreduce(e, OpOrI{});
@@ -1506,15 +1611,15 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       }
     }
     // the next pod's program words, loaded while this pod's last barrier waits
-    nb_len = kq + 1 < a.count ? s_pods[kq + 1].blob_len : 0;
+    nb_len = kq + 1 < count ? s_pods[kq + 1].blob_len : 0;
     if (nb_len <= kCoopPrefetch * BLOCK) {
-      const int boff = kq + 1 < a.count ? s_pods[kq + 1].blob : 0;
+      const int boff = kq + 1 < count ? s_pods[kq + 1].blob : 0;
 #pragma unroll
       for (int u = 0; u < kCoopPrefetch; u++)
         nb[u] = tid + u * BLOCK < nb_len ? a.prog[boff + tid + u * BLOCK] : 0;
     }
     KSG_CSTAMP(8);
-    if (!coop_barrier(a.bar, a.timeout, G, target)) return;
+    if (!coop_barrier(rbar, a.timeout, G, target)) return;
     KSG_CSTAMP(9);
 
     // ---- phase 4: select and assume --------------------------------------------
@@ -1522,8 +1627,8 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       unsigned long long b = 0;
       int32_t e = 0;
       if (tid < G) {
-        b = gld(&a.parts[tid].best);
-        e = gld(&a.parts[tid].err);
+        b = gld(&parts[tid].best);
+        e = gld(&parts[tid].err);
       }
       b = wreduce(b, OpMaxU64{});
       e = wreduce(e, OpOrI{});
@@ -1571,7 +1676,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       const int n_tm = any && !tab_now ? n_own_tmpl : 0;
       if (tid < n_sel) {
         const int owner = (selected / BLOCK) % G;
-        const int32_t* cnts = scored ? a.parts[owner].best_cnt : a.parts[owner].min_cnt;
+        const int32_t* cnts = scored ? parts[owner].best_cnt : parts[owner].min_cnt;
         d.sel[tid] = s_lsel[tid];
         d.old_cnt[tid] = gld(cnts + tid);
       }
@@ -1596,7 +1701,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         }
       }
     }
-    if (wg == 0 && kq == a.count - 1)   // the last pod's atomics set, read by everyone before barrier 3:
+    if (wg == 0 && kq == count - 1)   // the last pod's atomics set, read by everyone before barrier 3:
       for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&acc->hist[i], 0);   // clean for the next launch
     if (wg == 0 && tid == 0) {
       uint32_t score_skip = p.score_skip;

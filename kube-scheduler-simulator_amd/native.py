@@ -222,7 +222,7 @@ def make_profile(fields: dict) -> KsgProfile:
     return p
 
 
-RUN_NARROW_SWEEP, RUN_SLOT32, RUN_SPEC, RUN_WIDE_MEM = 1, 2, 8, 16   # ksg_last_run_info flags
+RUN_NARROW_SWEEP, RUN_SLOT32, RUN_SPEC, RUN_WIDE_MEM, RUN_TOPO_WINDOW = 1, 2, 8, 16, 32   # ksg_last_run_info flags
 
 
 class CaptureBuffers:
@@ -314,6 +314,8 @@ class Engine:
         self._last_ms = f("last_kernel_ms", C.c_int, vp, C.POINTER(C.c_double))
         self._run_info = f("last_run_info", C.c_int, vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32))
         self._recoveries = f("recoveries", C.c_int, vp, C.POINTER(C.c_int32))
+        self._win_stats = f("topo_window_stats", C.c_int, vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                            C.POINTER(C.c_int64))
         self._set_timing = f("set_timing", C.c_int, vp, C.c_int)
         self._kernel_stats = f("kernel_stats", C.c_int, vp, C.POINTER(KsgKernelStat), C.c_int32,
                                C.POINTER(C.c_int32))
@@ -524,6 +526,13 @@ class Engine:
         n = C.c_int32()
         self._check(self._recoveries(self.ctx, C.byref(n)))
         return n.value
+
+    def topo_window_stats(self):
+        """(windows, pods decided, windows ended early) of the last run's
+        speculative topology queue (ksg_topo_window_stats; zeros on other paths)."""
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        self._check(self._win_stats(self.ctx, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
 
     def last_kernel_ms(self) -> float:
         v = C.c_double()

@@ -195,13 +195,19 @@ def main():
                 roof["memory_side_frac_of_hbm"] = side / roof["peak"]
                 roof["traffic_over_algorithmic"] = roof["traffic"] / roof["bytes_per_launch"]
     evals = R * P * len(nodes)
+    path, flags = eng.last_run_info()
     out = {
         "config": args.config, "workload": workload, "replicas": R, "nodes": len(nodes), "pods": P,
         "device_ms": kms, "wall_ms": min(ms),
         "pods_per_s": R * P / (kms * 1e-3), "node_evals_per_s": evals / (kms * 1e-3),
         "scheduled": int((pl >= 0).sum()), "bytes_per_node_eval": bpe, "columns": per_eval,
         "roofline": roof,
+        "run_path": path, "run_flags": flags,
     }
+    if args.config == 3 and flags & native.RUN_TOPO_WINDOW:
+        w, d, c = eng.topo_window_stats()
+        out["topo_window"] = {"windows": w, "pods_decided": d, "windows_ended_early": c,
+                              "mean_pods_per_window": d / max(w, 1)}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baselines(enc, pf, profiles, P, args.cpu_budget)
     if args.save_placements:

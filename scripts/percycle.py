@@ -1,5 +1,5 @@
 """Run bench.py's per-cycle sidecar alone (C driver):
-python scripts/percycle.py [nodes] [warm] [pods] [c2|c3] [server|launch] [hint_ahead]"""
+python scripts/percycle.py [nodes] [warm] [pods] [c2|c3] [server (default)|launch] [hint_ahead]"""
 import importlib
 import json
 import os
@@ -16,7 +16,7 @@ S = importlib.import_module(PKG + ".snapshot")
 a = [int(x) for x in sys.argv[1:4]] + [5000, 500, 2000][len(sys.argv[1:4]):]
 kind = sys.argv[4] if len(sys.argv) > 4 else "c2"
 make, label = (G.config3, "configs[2]") if kind == "c3" else (G.config2, "configs[1]")
-srv = len(sys.argv) > 5 and sys.argv[5] == "server"
+srv = not (len(sys.argv) > 5 and sys.argv[5] == "launch")
 ahead = int(sys.argv[6]) if len(sys.argv) > 6 else 0
 print(json.dumps(bench.per_cycle_sidecar(native, G, S, a[0], a[1], a[2], make=make, label=label, server=srv,
                                          hint_ahead=ahead)), flush=True)

@@ -76,12 +76,11 @@ def test_eval_cycle_nodes_per_lane(oracle, monkeypatch, kn, name):
 
 @pytest.mark.parametrize("name", ["c2-1000x120", "c1-100x150", "c5-small", "c5-vocab8k", "zoo-0", "zoo-3",
                                   "readme-kat2"])
-def test_eval_cycle_server_matches_oracle(oracle, monkeypatch, name):
-    """The persistent per-cycle server (KSG_CYCLE_SERVER=1: node columns held
-    in registers across cycles, calls through the pinned mailbox) equals the
-    oracle pod by pod, deferred assumes included; read_state at the end stops
-    it, so the state it wrote back is what the oracle holds."""
-    monkeypatch.setenv("KSG_CYCLE_SERVER", "1")
+def test_eval_cycle_launch_matches_oracle(oracle, monkeypatch, name):
+    """One ksg_eval_cycle launch per cycle (KSG_CYCLE_SERVER=0; the persistent
+    server, which test_eval_cycle_matches_oracle runs, is the default since
+    round 6) equals the oracle pod by pod, deferred assumes included."""
+    monkeypatch.setenv("KSG_CYCLE_SERVER", "0")
     eng = native.Engine(device=0)
     try:
         _check_cycles(eng, oracle, name, *CASES[name]())

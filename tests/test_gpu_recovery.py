@@ -120,13 +120,17 @@ def test_coop_cycle(oracle, monkeypatch, server):
 
 # ---- a forced timeout: restore, cooperative relaunch, the oracle's result ------------
 
-def test_timeout_topology_queue_recovers(oracle, monkeypatch):
-    """The second launch of the first call times out after 64 committed pods:
-    the call restores the pre-call state and runs again cooperatively."""
-    eng = _engine(monkeypatch, KSG_TEST_INJECT_TIMEOUT=1)
+@pytest.mark.parametrize("window", [1, 0], ids=["windows", "pod-by-pod"])
+def test_timeout_topology_queue_recovers(oracle, monkeypatch, window):
+    """A barrier of the first call times out after pods were committed (pod by
+    pod: the second launch, after 64 pods; the speculative topology queue:
+    the rows of the 17th window): the call restores the pre-call state and
+    runs again cooperatively (pod by pod from then on)."""
+    eng = _engine(monkeypatch, KSG_TEST_INJECT_TIMEOUT=1, KSG_TOPO_WINDOW=window)
     try:
         _topo_queue(eng, oracle)
         assert eng.recoveries() == 1
+        assert not eng.last_run_info()[1] & native.RUN_TOPO_WINDOW   # cooperative launches: pod by pod
     finally:
         eng.close()
 
@@ -153,7 +157,7 @@ def test_timeout_cycle_recovers(oracle, monkeypatch):
     """The per-cycle kernel's exchange gives up on the first cycle (its
     deferred assume and staged append already applied): the cycle is
     evaluated again cooperatively, the rest run cooperatively."""
-    eng = _engine(monkeypatch, KSG_TEST_INJECT_TIMEOUT=8)
+    eng = _engine(monkeypatch, KSG_TEST_INJECT_TIMEOUT=8, KSG_CYCLE_SERVER=0)   # (the one-launch form)
     try:
         _cycles(eng, oracle, "c2-1000x120")
         assert eng.recoveries() == 1

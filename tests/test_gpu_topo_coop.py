@@ -17,21 +17,29 @@ native = pkg("native")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[0, 1], ids=["atomic-merge", "partial-slots"])
+@pytest.fixture(scope="module", params=[(0, 1), (1, 1), (0, 0)], ids=["atomic-merge", "partial-slots", "pod-by-pod"])
 def gpu(built, request):
     """Both histogram hand-offs (KSG_COOP_PMODE, read at ksg_open): 0 (default)
     merges each workgroup's partial histograms into an accumulator with
-    agent-scope atomics, 1 folds every workgroup's partial slot."""
+    agent-scope atomics, 1 folds every workgroup's partial slot; placement
+    runs take the speculative topology queue (windows of independent pods,
+    ksched_topo_win.h, the default since round 6), or ksg_topo_coop pod by
+    pod (KSG_TOPO_WINDOW=0)."""
     import os
-    old = os.environ.get("KSG_COOP_PMODE")
-    os.environ["KSG_COOP_PMODE"] = str(request.param)
+    pmode, window = request.param
+    env = {"KSG_COOP_PMODE": str(pmode), "KSG_TOPO_WINDOW": str(window)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        return native.Engine(device=0)
+        eng = native.Engine(device=0)
+        eng.window = bool(window)
+        return eng
     finally:
-        if old is None:
-            del os.environ["KSG_COOP_PMODE"]
-        else:
-            os.environ["KSG_COOP_PMODE"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
@@ -75,6 +83,9 @@ def test_topo_coop_matches_oracle(gpu, oracle, name, make):
     enc, pf, P, po, ro, ostate = _case(oracle, name, make)
     gpu.load(enc, pf)
     pg, rg = gpu.run_queue(0, P)
+    path, flags = gpu.last_run_info()
+    if path == 4:   # (configs[0]'s pods need no topology kernel: the batched path)
+        assert bool(flags & native.RUN_TOPO_WINDOW) == gpu.window, (path, flags)
     bad = np.nonzero(pg != po)[0]
     assert bad.size == 0, f"{name}: first mismatches at pods {bad[:5]}: gpu {pg[bad[:5]]} oracle {po[bad[:5]]}"
     for f in ("n_feasible", "status", "score_skip"):
@@ -114,8 +125,34 @@ def test_configs2_golden(built, n_pods, tables):
             os.environ["KSG_COOP_TABLES"] = old
     eng.load(enc, pf)
     pg, rg = eng.run_queue(0, len(pods))
+    # the speculative topology queue needs the maintained tables
+    assert bool(eng.last_run_info()[1] & native.RUN_TOPO_WINDOW) == (tables == "1")
     bad = np.nonzero(pg != gold["placements"])[0]
     assert bad.size == 0, f"first mismatches at pods {bad[:5]}: gpu {pg[bad[:5]]} oracle {gold['placements'][bad[:5]]}"
     for f in ("n_feasible", "status", "score_skip"):
         np.testing.assert_array_equal(np.asarray(rg[f]).astype(gold[f].dtype), gold[f], err_msg=f)
     np.testing.assert_array_equal(eng.read_state(len(enc.cluster.res_names))[2], gold["pod_count"])
+
+
+@pytest.mark.parametrize("k", [2, 5])
+def test_topo_window_sizes(built, oracle, k):
+    """Windows of at most k pods (KSG_TOPO_WINDOW_K) place exactly as the
+    oracle; the walk ends some windows early (a changed node left a pod's
+    feasible set) on a cluster tight enough to fill nodes."""
+    import os
+    enc, pf, P, po, ro, ostate = _case(oracle, "c3-4000x1200", CASES[0][1])
+    os.environ["KSG_TOPO_WINDOW_K"] = str(k)
+    try:
+        eng = native.Engine(device=0)
+    finally:
+        del os.environ["KSG_TOPO_WINDOW_K"]
+    eng.load(enc, pf)
+    pg, rg = eng.run_queue(0, P)
+    assert eng.last_run_info()[1] & native.RUN_TOPO_WINDOW
+    windows, decided, cut = eng.topo_window_stats()
+    assert decided == P and P / k <= windows <= P, (windows, decided, cut)
+    np.testing.assert_array_equal(pg, po)
+    for f in ("n_feasible", "status", "score_skip"):
+        np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
+    for a, b in zip(eng.read_state(len(enc.cluster.res_names)), ostate):
+        np.testing.assert_array_equal(a, b)
