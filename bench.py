@@ -46,6 +46,9 @@ Prints ONE JSON line (rank 0).  The line also carries:
   memory) with its digest checked against the host serialiser
   (bulk.annotate_queue, captured rows + ksg_annotate on 16 threads), plus the
   device serialiser's steady state over a longer queue;
+* `configs2` (N = 1): BASELINE configs[2], 15,000 nodes x 150,000 pods with
+  PodTopologySpread + InterPodAffinity, the whole queue per run on the
+  speculative topology queue, placements against the committed golden vector;
 * `per_cycle` / `per_cycle_configs2` (N = 1): the drop-in's per-cycle C-ABI
   path, call by call from C (the persistent server, the default since round
   6); `per_cycle_launch` one kernel launch per cycle,
@@ -544,6 +547,46 @@ def kubelet_memory_line(native, G, E, n_nodes: int, n_pods: int, steps: int, con
             "scheduled": int((pl >= 0).sum())}
 
 
+def topo_queue_line(native, G, E, metrics, n_nodes: int, n_pods: int):
+    """BASELINE configs[2]: 15,000 nodes x 150,000 pods with PodTopologySpread
+    + InterPodAffinity (generator.config3), the whole queue in one
+    ksg_run_queue on a fresh cluster (the speculative topology queue,
+    ksched_topo_win.h).  A first run with per-kernel timing (the roofline),
+    then the timed run; placements against the committed C++-oracle golden
+    vector of the same queue when it exists (tests/golden/c3_15000x150000.npz,
+    tests/golden/make_golden.py)."""
+    import numpy as np
+    nodes, pods, prof = G.config3(n_nodes=n_nodes, n_pods=n_pods)
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    eng = native.Engine(device=0)
+    eng.load(enc, pf)
+    eng.set_timing(True)
+    eng.run_queue(0, n_pods, results=False)
+    ks = eng.kernel_stats()
+    eng.set_timing(False)
+    eng.reset_state()
+    t = time.perf_counter()
+    pl, _ = eng.run_queue(0, n_pods, results=False)
+    wall = time.perf_counter() - t
+    kms = eng.last_kernel_ms()
+    path, flags = eng.last_run_info()
+    win = eng.topo_window_stats()
+    eng.close()
+    per_eval = metrics.bytes_per_node_eval(enc, prof)
+    out = {"workload": f"configs[2]: {n_nodes} nodes x {n_pods} pods, PodTopologySpread + InterPodAffinity "
+                       "(generator.config3, config3 profile), the whole queue per run",
+           "pods_per_s": n_pods / (kms * 1e-3), "pods_per_s_wall": n_pods / wall, "device_ms": kms,
+           "scheduled": int((pl >= 0).sum()), "run_flags": flags,
+           "speculative_topology_queue": bool(flags & native.RUN_TOPO_WINDOW),
+           "windows": {"windows": win[0], "pods_decided": win[1], "ended_early": win[2]},
+           "roofline": metrics.dominant_kernel_roofline(ks, per_eval)}
+    gold = os.path.join(ROOT, "tests", "golden", f"c3_{n_nodes}x{n_pods}.npz")
+    if os.path.exists(gold):
+        out["placements_equal_golden"] = bool(np.array_equal(pl, np.load(gold)["placements"]))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -570,6 +613,7 @@ def main():
     ap.add_argument("--kubelet-pods", type=int, default=50000, help="kubelet-memory line; 0 disables")
     ap.add_argument("--topo-nodes", type=int, default=15000, help="configs[2] cluster of the topology legs")
     ap.add_argument("--topo-cycle-pods", type=int, default=400, help="configs[2] per-cycle leg; 0 disables")
+    ap.add_argument("--topo-queue-pods", type=int, default=150000, help="configs[2] full-queue line; 0 disables")
     ap.add_argument("--topo-annotate-pods", type=int, default=256, help="configs[2] annotation leg; 0 disables")
     ap.add_argument("--no-build-check", action="store_true",
                     help="skip the check that libksched.so embeds the tree's source hash")
@@ -758,6 +802,12 @@ def main():
                 eng3.close()
         except Exception as e:
             log(f"[rank {rank}] configs[2] annotation sidecar unavailable: {e}")
+    topo = None
+    if world == 1 and args.topo_queue_pods > 0:
+        try:
+            topo = topo_queue_line(native, G, E, metrics, args.topo_nodes, args.topo_queue_pods)
+        except Exception as e:
+            log(f"[rank {rank}] configs[2] queue line unavailable: {e}")
     kub = None
     if world == 1 and args.kubelet_pods > 0 and c1 is not None:
         try:
@@ -794,7 +844,8 @@ def main():
         out["source_hash"]["matches"] = out["source_hash"]["library"] == out["source_hash"]["tree"]
         for key, val in (("configs1", c1), ("replica_sweep", sweep), ("annotations", ann), ("per_cycle", cyc),
                          ("per_cycle_launch", cyc_launch), ("per_cycle_hinted", cyc_hint),
-                         ("kubelet_memory", kub), ("per_cycle_configs2", cyc3), ("annotations_configs2", ann3)):
+                         ("kubelet_memory", kub), ("configs2", topo), ("per_cycle_configs2", cyc3),
+                         ("annotations_configs2", ann3)):
             if val is not None:
                 out[key] = val
         if not args.no_cpu_baseline and world == 1:

@@ -406,9 +406,8 @@ enum {
   KSG_K_CAPTURE_NORM = 10,
   KSG_K_EVAL_CYCLE = 11,
   KSG_K_BATCH_PHASE2V = 12,
-  KSG_K_TOPO_WIN_ROWS = 13,
-  KSG_K_TOPO_WALK = 14,
-  KSG_NKERNELS = 15
+  KSG_K_TOPO_WIN_ROWS = 13,   /* the window rows (walk included: the last workgroup decides) */
+  KSG_NKERNELS = 14
 };
 typedef struct ksg_kernel_stat {
   char name[48];

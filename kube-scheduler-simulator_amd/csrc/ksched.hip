@@ -410,7 +410,7 @@ const char* kKernelNames[KSG_NKERNELS] = {"ksg_queue_kernel", "ksg_queue_topo_ke
                                           "ksg_batch_topk", "ksg_batch_phase2s", "ksg_sweep_static",
                                           "ksg_sweep", "ksg_topo_coop", "ksg_sweep_narrow",
                                           "ksg_capture_eval", "ksg_capture_norm", "ksg_eval_cycle",
-                                          "ksg_batch_phase2v", "ksg_topo_coop_window", "ksg_topo_walk"};
+                                          "ksg_batch_phase2v", "ksg_topo_coop_window"};
 
 int tmark(ksg_ctx* ctx) {
   if (!ctx->timing) return KSG_OK;
@@ -1920,27 +1920,10 @@ int run_topo_window(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, k
   a.win_tot = reinterpret_cast<int32_t*>(b + o_tot);
   a.win_top = reinterpret_cast<unsigned long long*>(b + o_top);
   a.win_pod = reinterpret_cast<WinPod*>(b + o_pod);
-  WalkArgs w{};
-  w.c = ctx->c;
-  w.st = ctx->st;
-  w.tt = tt;
-  w.use_tables = 1;
-  w.pods = ctx->d_pods;
-  w.profile = d_prof;
-  w.cursor = reinterpret_cast<int32_t*>(b + o_cur);
-  w.win_len = a.win_len;
-  w.win_base = first;
-  w.win_end = first + count;
-  w.win_kmax = kmax;
-  w.G = G;
-  w.win_tot = a.win_tot;
-  w.win_top = a.win_top;
-  w.win_pod = a.win_pod;
-  w.prog = ctx->d_prog;
-  w.placements = d_pl;
-  w.results = d_res;
-  w.timeout = a.timeout;
-  w.wstats = reinterpret_cast<unsigned long long*>(b + o_stats);
+  a.placements = d_pl;
+  a.results = d_res;
+  a.win_done = reinterpret_cast<unsigned*>(b + o_stats + 64);
+  a.win_stats = reinterpret_cast<unsigned long long*>(b + o_stats);
 #ifdef KSG_STAMPS
   if (!ctx->d_stamps) {
     if ((rc = dalloc(ctx, &ctx->d_stamps, 16))) return rc;
@@ -1969,11 +1952,12 @@ int run_topo_window(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, k
         ctx->inject_timeout &= ~1;                                      // the rows find the timeout word set
         HIPC(ctx, hipMemsetAsync(ctx->d_coop_flags + 4, 0x01, sizeof(unsigned), ctx->stream));
       }
+      // rows: the predicted window's length (the rows take min(win_len at the
+      // cursor, rows): a window the walk ended early leaves the prediction
+      // behind until the host reads the cursor, and a shorter window is valid)
       void* kargs[] = {&a};
-      HIPC(ctx, hipLaunchKernel(kf, dim3(G, kmax), dim3(256), kargs, 0, ctx->stream));
+      HIPC(ctx, hipLaunchKernel(kf, dim3(G, std::max(wl, 1)), dim3(256), kargs, 0, ctx->stream));
       if ((rc = tlaunched(ctx, KSG_K_TOPO_WIN_ROWS, (double)wl * N))) return rc;
-      hipLaunchKernelGGL(ksg_topo_walk, dim3(1), dim3(256), 0, ctx->stream, w);
-      if ((rc = tlaunched(ctx, KSG_K_TOPO_WALK, (double)wl))) return rc;
     }
     HIPC(ctx, hipGetLastError());
     int32_t cur = 0;

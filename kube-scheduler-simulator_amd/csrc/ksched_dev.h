@@ -1680,8 +1680,8 @@ __global__ __launch_bounds__(BLOCK) void ksg_queue_topo_kernel(QueueArgs a) {
 #include "ksched_topo_tables.h"
 #endif
 #if !defined(KSG_PART) || defined(KSG_WITH_TOPO)
-#include "ksched_topo_coop.h"
 #include "ksched_topo_win.h"
+#include "ksched_topo_coop.h"
 #endif
 
 // dst[r * stride + i] = src[i] for every replica r = blockIdx.y (replica state

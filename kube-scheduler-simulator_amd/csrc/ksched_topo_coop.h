@@ -81,18 +81,6 @@ struct CoopAcc {    // atomics fallback for large histograms
   int32_t hist[KSG_HIST_MAX];
 };
 
-// A window pod's facts at the window's start (CAP == 3 writes them, the walk
-// reads them): what phase 4 would decide from, less the argmax.
-struct WinPod {
-  int32_t ok, nfeas, minidx, scored;
-  uint32_t err;          // ScoreError bits of every workgroup (or-ed; the walk zeroes it)
-  uint32_t status;       // KSG_ST_IPA_* flags
-  uint32_t score_skip;
-  uint32_t smask;        // the pod's Score plugins (make_view)
-  int32_t w_fit, w_ba;
-  int32_t fit_on;        // NodeResourcesFit's Filter runs for the pod
-  int32_t pad;
-};
 
 // gld / gst / gadd / gor and arrive_and_wait_sc1: ksched_sweep.h
 
@@ -173,6 +161,8 @@ struct CoopArgs {
   int32_t* win_tot;            // [kmax][N]
   unsigned long long* win_top; // [kmax][G][kmax]
   WinPod* win_pod;             // [kmax]
+  unsigned* win_done;          // arrivals of the launch's workgroups (the last walks the window and zeroes it)
+  unsigned long long* win_stats;   // [3] windows, pods decided, windows ended early
 };
 
 // Hand-offs between the G workgroups without cache maintenance (MI355X guide,
@@ -448,7 +438,7 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
   if constexpr (CAP == 3) {
     first = *a.win_cursor;
     if (first >= a.win_end) return;
-    count = min(min(a.win_len[first - a.win_base], a.win_kmax), a.win_end - first);
+    count = min(min(a.win_len[first - a.win_base], (int)gridDim.y), a.win_end - first);
     kq_lo = (int)blockIdx.y;
     if (kq_lo >= count) return;
   }
@@ -1472,29 +1462,33 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if constexpr (CAP == 3) {
-      // A window row ends here, before any select or assume (ksg_topo_walk
-      // decides): every node's static total, i.e. the weighted total less its
-      // NodeResourcesFit / BalancedAllocation part, the only part an earlier
-      // pod of the window can change (or -1: filtered out; 0: feasible, pod
-      // not scored); this tile's kq + 1 best keys (the walk's best unchanged
-      // node is among them when at most kq nodes changed); the pod's facts.
+      // A window row ends here, before any select or assume: every node's
+      // static total, i.e. the weighted total less its NodeResourcesFit /
+      // BalancedAllocation part, the only part an earlier pod of the window
+      // can change (or -1: filtered out; 0: feasible, pod not scored); this
+      // tile's kq + 1 best keys (the walk's best unchanged node is among them
+      // when at most kq nodes changed); the pod's facts.  Agent-scope stores:
+      // the walk reads them in this launch, from another workgroup.
+      __shared__ WalkLds s_walk;
+      __shared__ int s_final;
       const int n0 = node_of(0);
       const bool feas0 = ok && n0 < N && ev[0].st == 0;
       if (n0 < N)
-        a.win_tot[(size_t)row * N + n0] = feas0 ? (scored ? (int32_t)(ctot[0] - (ev[0].part - ev[0].img)) : 0) : -1;
+        gst(a.win_tot + (size_t)row * N + n0, feas0 ? (scored ? (int32_t)(ctot[0] - (ev[0].part - ev[0].img)) : 0) : -1);
       uint64_t key = scored && feas0 ? argmax_key(ctot[0], n0) : 0;
+      KSG_CSTAMP(8);
       for (int r = 0; r <= row; r++) {
         const uint64_t m = wreduce(key, OpMaxU64{});
         if (lane == 0) s_wtop[wv] = m;
         __syncthreads();
         uint64_t b = s_wtop[0];
         for (int i = 1; i < NW; i++) b = max(b, s_wtop[i]);
-        if (tid == 0) a.win_top[((size_t)row * G + wg) * a.win_kmax + r] = b;
+        if (tid == 0) gst(a.win_top + ((size_t)row * G + wg) * a.win_kmax + r, (unsigned long long)b);
         if (key == b) key = 0;
         __syncthreads();
       }
       if (wg == 0 && tid == 0) {
-        WinPod& w = a.win_pod[row];
+        WinPod* w = a.win_pod + row;
         uint32_t status = 0, score_skip = p.score_skip;
         if (ipa_in_filter && s_t.ipa_skip_filter) status |= KSG_ST_IPA_PREFILTER_SKIP;
         if (scored && ipa_in_score && !((p.score_skip >> KSG_PL_INTER_POD_AFFINITY) & 1u) && s_t.ipa_skip_score) {
@@ -1503,16 +1497,16 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
         }
         bool fit_in = false;
         for (int kf = 0; kf < prof.n_filter; kf++) fit_in |= prof.filter_order[kf] == KSG_PL_NODE_RESOURCES_FIT;
-        w.ok = ok ? 1 : 0;
-        w.nfeas = ok ? gnfeas : 0;
-        w.minidx = gminidx;
-        w.scored = scored ? 1 : 0;
-        w.status = status;
-        w.score_skip = score_skip;
-        w.smask = v.smask;
-        w.w_fit = v.w_fit;
-        w.w_ba = v.w_ba;
-        w.fit_on = fit_in && !((v.fskip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) ? 1 : 0;
+        gst(&w->ok, ok ? 1 : 0);
+        gst(&w->nfeas, ok ? gnfeas : 0);
+        gst(&w->minidx, gminidx);
+        gst(&w->scored, scored ? 1 : 0);
+        gst(&w->status, status);
+        gst(&w->score_skip, score_skip);
+        gst(&w->smask, v.smask);
+        gst(&w->w_fit, v.w_fit);
+        gst(&w->w_ba, v.w_ba);
+        gst(&w->fit_on, fit_in && !((v.fskip >> KSG_PL_NODE_RESOURCES_FIT) & 1u) ? 1 : 0);
       }
       // this row's atomics set (soft marks; pre-pass histograms), read by
       // every workgroup of the row in phase 3: the last to arrive zeroes it
@@ -1526,6 +1520,36 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       __syncthreads();
       if (s_last)
         for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&acc->hist[i], 0);
+      KSG_CSTAMP(9);
+      // every row's outputs are performed (vmcnt above): the last workgroup of
+      // the launch to arrive walks the window
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)a.win_done, 1u,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_final = old + 1 == (unsigned)(count * G) ? 1 : 0;
+      }
+      __syncthreads();
+      if (s_final) {
+        WalkArgs w;
+        w.c = cg;
+        w.st = st;
+        w.tt = tt;
+        w.use_tables = a.use_tables;
+        w.cursor = const_cast<int32_t*>(a.win_cursor);
+        w.win_base = a.win_base;
+        w.G = G;
+        w.K = a.win_kmax;
+        w.win_tot = a.win_tot;
+        w.win_top = a.win_top;
+        w.win_pod = a.win_pod;
+        w.prog = a.prog;
+        w.placements = a.placements;
+        w.results = a.results;
+        w.wstats = a.win_stats;
+        walk_window(w, first, count, prof, s_pods, s_walk);
+        if (tid == 0) gst(a.win_done, 0u);
+      }
+      KSG_CSTAMP(10);
       continue;
     }
     if (CAP == 2) {

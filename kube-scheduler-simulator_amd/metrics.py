@@ -85,9 +85,7 @@ def kernel_bytes_per_unit(name: str, cols) -> int:
     if name in ("ksg_queue_kernel", "ksg_queue_topo_kernel", "ksg_topo_coop"):
         return bytes_per_eval
     if name == "ksg_topo_coop_window":   # a window row's node-eval + its 4-byte static total written
-        return bytes_per_eval + 4
-    if name == "ksg_topo_walk":   # unit = a decided pod: its changed nodes' columns and tile lists, O(window)
-        return 0
+        return bytes_per_eval + 4      # (the walk's reads are O(window), not O(nodes))
     if name == "ksg_batch_phase1":
         return bytes_per_eval + 12
     if name == "ksg_capture_eval":   # node columns on the post-batch state + status word and record written

@@ -49,11 +49,16 @@ if st0 is not None:   # the per-cycle calls only
     for i in range(16):
         st[i] -= st0[i]
 tot = sum(st)
+win = bool(eng.last_run_info()[1] & native.RUN_TOPO_WINDOW)
 names = ["setup (stage pod, layout)", "phase 1: merge / publish", "barrier 1", "2a: merged counts to LDS",
          "2b: reset next set, IPA skips", "2c3: sweep A, IPA score", "2d: reductions, marks", "barrier 2",
          "3c: normalise, argmax", "barrier 3", "phase 4 (select, assume)", "2c1: sweep A, load + filters",
          "2c2: sweep A, PTS soft", "3a: fold phase-2 partials", "3b: marks, sizes, weights", "phase 1: node loop"]
+if win:   # the speculative topology queue: a row ends after 3c (ksched_topo_win.h)
+    names[8] = "3c: normalise (static totals)"
+    names[9] = "window: tile lists, facts, row arrival"
+    names[10] = "window: launch arrival + walk (wg 0)"
 order = [0, 15, 1, 2, 3, 4, 11, 12, 5, 6, 7, 13, 14, 8, 9, 10]
-print(f"[topo coop] {n_pods} pods x {len(nodes)} nodes, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped)")
+print(f"[topo coop{' window rows' if win else ''}] {n_pods} pods x {len(nodes)} nodes, kernel {ms:.1f} ms, {ms * 1e3 / n_pods:.2f} us/pod (stamped)")
 for i in order:
     print(f"  {names[i]:34s} {st[i] / n_pods:10.0f} cycles/pod  {100 * st[i] / max(tot, 1):5.1f} %")
