@@ -1521,12 +1521,18 @@ __global__ __launch_bounds__(256) void ksg_topo_coop(CoopArgs a) {
       if (s_last)
         for (int i = tid; i < prev_fallback_words; i += BLOCK) gst(&acc->hist[i], 0);
       KSG_CSTAMP(9);
-      // every row's outputs are performed (vmcnt above): the last workgroup of
-      // the launch to arrive walks the window
+      // the last workgroup of each row (its row's outputs are performed: every
+      // workgroup drained its stores before arriving) arrives on the launch's
+      // counter, and the last row's walks the window.  (Every workgroup on
+      // one counter: 185 atomics on one word serialise, ~5 us.)
       if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)a.win_done, 1u,
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_final = old + 1 == (unsigned)(count * G) ? 1 : 0;
+        int fin = 0;
+        if (s_last) {
+          const unsigned old = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)a.win_done, 1u,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          fin = old + 1 == (unsigned)count ? 1 : 0;
+        }
+        s_final = fin;
       }
       __syncthreads();
       if (s_final) {
