@@ -762,11 +762,19 @@ __global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
     if (seq == last) break;   // idle or a timed-out exchange elsewhere: leave
     // ---- the call and its programs into LDS (workgroup 0: from the host, relayed) -------
     if (direct) {   // the mailbox in device memory: read it in place (system scope: the CPU wrote it)
+      // the call and the first kCycBlob program words in one round trip (the
+      // words past the call's blob_len are read and dropped)
       const int32_t* src = reinterpret_cast<const int32_t*>(&mb->k);
+      int32_t bw[kCycBlob / 64];
+#pragma unroll
+      for (int u = 0; u < kCycBlob / 64; u++) bw[u] = sys_ld(mb->blob + lane + 64 * u);
       for (int i = lane; i < KW; i += 64) reinterpret_cast<int32_t*>(&s_k)[i] = sys_ld(src + i);
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       const int blen = s_k.op != 0 ? 0 : s_k.blob_len;
-      for (int i = lane; i < blen; i += 64) s_blob[i] = sys_ld(mb->blob + i);
+#pragma unroll
+      for (int u = 0; u < kCycBlob / 64; u++)
+        if (lane + 64 * u < blen) s_blob[lane + 64 * u] = bw[u];
+      for (int i = kCycBlob + lane; i < blen; i += 64) s_blob[i] = sys_ld(mb->blob + i);
     } else if (relay) {
       const int32_t* src = reinterpret_cast<const int32_t*>(&mb->k);
       int32_t* dst = reinterpret_cast<int32_t*>(a.d_call);
@@ -793,10 +801,15 @@ __global__ __launch_bounds__(64) void ksg_cycle_server(SrvArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if (s_k.op != 0) break;   // stop
-    const int32_t* nsrc = s_k.pod.node_set >= 0 ? s_k.gprog + s_k.pod.node_set : S.c.allowed;
+    if (s_k.pod.node_set >= 0) {   // the PreFilterResult's node bitmap (one more round trip, only then)
+      const int32_t* nsrc = s_k.gprog + s_k.pod.node_set;
 #pragma unroll
-    for (int k = 0; k < KN; k++) nsw[k] = (uint32_t)nsrc[(nk[k] < N ? nk[k] : N - 1) >> 5];
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      for (int k = 0; k < KN; k++) nsw[k] = (uint32_t)nsrc[(nk[k] < N ? nk[k] : N - 1) >> 5];
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+#pragma unroll
+      for (int k = 0; k < KN; k++) nsw[k] = 0xffffffffu;
+    }
 #ifdef KSG_STAMPS
     y_last = __builtin_amdgcn_s_memtime();
 #endif
