@@ -174,7 +174,7 @@ def pmc_traffic(kernel, name):
     """HBM bytes per dispatch of `kernel` from a committed PMC summary
     (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE +
     WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
-    for rnd in ("r5", "r4", "r3", "r2"):   # the newest round's passes first
+    for rnd in ("r6", "r5", "r4", "r3", "r2"):   # the newest round's passes first
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             tab = json.load(open(path))

@@ -28,10 +28,15 @@ def kernel_key(name: str) -> str:
     (ksg_sweep<..., NARROW = true>, the sixth argument) are ksg_sweep_narrow."""
     name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0].strip()
     base = name.split("<")[0].strip()
-    if base == "ksg_sweep" and "<" in name:
+    ns = base[:base.rindex("::") + 2] if "::" in base else ""   # (ksk::)
+    if base == ns + "ksg_sweep" and "<" in name:
         args = [a.strip() for a in name[name.index("<") + 1:name.rindex(">")].split(",")]
         if len(args) >= 6 and args[5] == "true":
-            return "ksg_sweep_narrow"
+            return ns + "ksg_sweep_narrow"
+    if base == ns + "ksg_topo_coop" and "<" in name:   # CAP = 3: the speculative topology queue's window rows
+        args = [a.strip() for a in name[name.index("<") + 1:name.rindex(">")].split(",")]
+        if len(args) >= 3 and args[2] == "3":
+            return ns + "ksg_topo_coop_window"
     return base
 
 
