@@ -339,11 +339,21 @@ int ksg_read_state(ksg_ctx* ctx, ksg_node_state* out);
  * RemovePod / AddPod extensions move them upstream)
  * (fits[k] = 0: the node cannot help), then reprieve the victims in order,
  * each staying evicted (victim[i] = 1) only if `pod` no longer fits with it
- * back.  Node-static filters are not re-run: the caller
- * (preemption.check_scope) requires them ordered before those four.
+ * back.  Node-static filters are not re-run: the caller drops the nodes
+ * whose static filters reject `pod` first (ksg_eval_skipping below).
  * KSG_E_UNSUPPORTED when the preemptor's terms exceed the dry run's limits. */
 int ksg_preempt_victims(ksg_ctx* ctx, int32_t pod, const int32_t* cand_node, int32_t n_cand,
                         const int32_t* vic_off, const int32_t* vic_pod, int32_t* fits, uint8_t* victim);
+/* ksg_eval of loaded pod `pod` with the Filter plugins in `filter_skip`
+ * (bit = plugin id) skipped as a PreFilter Skip would skip them; the pod's
+ * record is restored before the call returns.  DefaultPreemption asks it
+ * with the four pod-dependent filters skipped: a node whose status word is
+ * then 0 passes every node-static filter (VolumeBinding, VolumeZone, ...
+ * ordered after NodeResourcesFit included), the part of
+ * SelectVictimsOnNode's RunFilterPluginsWithNominatedPods (upstream v1.32
+ * preemption.go, called from default_preemption.go:SelectVictimsOnNode) no
+ * removal can change. */
+int ksg_eval_skipping(ksg_ctx* ctx, int32_t pod, uint32_t filter_skip, ksg_result* res, ksg_capture* cap);
 /* A victim's deletion: the inverse of ksg_commit (NodeInfo.RemovePod and the
  * count tables), applied by DefaultPreemption's prepareCandidate. */
 int ksg_uncommit(ksg_ctx* ctx, int32_t pod, int32_t node);

@@ -3585,7 +3585,7 @@ int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t 
   const int64_t base = (int64_t)ctx->h_prog.size();
   ksg_pod p = *pod;
   for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob,
-                     &p.ports})
+                     &p.ports, &p.vol})
     if (*f >= 0) *f = (int32_t)(*f + base);
   const int32_t n0 = ctx->n_pods, blob0 = ctx->max_blob;
   const int64_t used0 = ctx->prog_used;
@@ -3601,6 +3601,28 @@ int ksg_eval_pod(ksg_ctx* ctx, const ksg_pod* pod, const int32_t* prog, int64_t 
     ctx->max_blob = blob0;
   }
   return rc;
+}
+
+int ksg_eval_skipping(ksg_ctx* ctx, int32_t pod, uint32_t filter_skip, ksg_result* res, ksg_capture* cap) {
+  if (!ctx || !res) return ctx ? fail(ctx, KSG_E_INVALID, "null result") : KSG_E_INVALID;
+  int rc = check_ready(ctx);
+  if (rc) return rc;
+  if (pod < 0 || pod >= ctx->n_pods) return fail(ctx, KSG_E_INVALID, "pod index");
+  if ((rc = flush_stage(ctx)) || (rc = srv_stop(ctx))) return rc;
+  // the record with the extra Skip bits, on the host (the dispatch reads it)
+  // and the device; the original goes back once the evaluation has synced
+  const ksg_pod keep = ctx->h_pods[pod];
+  ctx->h_pods[pod].filter_skip |= filter_skip;
+  HIPC(ctx, hipMemcpyAsync(ctx->d_pods + pod, &ctx->h_pods[pod], sizeof(ksg_pod), hipMemcpyHostToDevice,
+                           ctx->stream));
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  rc = eval_internal(ctx, pod, res, cap);
+  int rc2 = srv_stop(ctx);
+  ctx->h_pods[pod] = keep;
+  HIPC(ctx, hipMemcpyAsync(ctx->d_pods + pod, &ctx->h_pods[pod], sizeof(ksg_pod), hipMemcpyHostToDevice,
+                           ctx->stream));
+  HIPC(ctx, hipStreamSynchronize(ctx->stream));
+  return rc ? rc : rc2;
 }
 
 int ksg_annotator_attach(ksg_ctx* ctx, const ksg_annotator* ann, const int64_t* weight, uint32_t normalize_mask) {

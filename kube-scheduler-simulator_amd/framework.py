@@ -231,6 +231,10 @@ class DebuggableScheduler:
         if nominated >= 0:
             # prepareCandidate: delete the victims; then the retry (module
             # docstring of preemption.py, step 6)
+            if any(self._rwop_shared(v) for v in victims):
+                # the encoded VolumeRestrictions conflict of the claim's
+                # other users would go stale (encoder.py VOL_RWOP_CONFLICT)
+                raise NotImplementedError("a preemption victim holds a ReadWriteOncePod claim another pod uses")
             for v in victims:
                 self.engine.uncommit(v, nominated)
                 self.on_node[nominated].remove(v)
@@ -252,6 +256,13 @@ class DebuggableScheduler:
             self.on_node[cyc.selected].append(pi)
         return cyc
 
+    def _rwop_shared(self, q: int) -> bool:
+        """Whether pod q holds a ReadWriteOncePod claim another pod also uses."""
+        pod = self.pods[q]
+        if not pod.claim_names():
+            return False
+        return bool(PR.rwop_holders(pod, [(i, 0, o) for i, o in enumerate(self.pods) if i != q]))
+
     def preempt(self, pi: int, cyc: PodCycle):
         """DefaultPreemption.PostFilter for a pod with no feasible node:
         returns (nominated node or -1, victims most important first).  The
@@ -271,7 +282,19 @@ class DebuggableScheduler:
                 lists.append((n, sorted(low, key=lambda q: PR.importance_key(self.pods[q]))))
         if not lists:
             return -1, []
-        PR.check_scope(self.prof, pod, self.pods)
+        holders = PR.rwop_holders(pod, [(q, n, self.pods[q]) for n, v in enumerate(self.on_node) for q in v])
+        if PR.rwop_outcome(pod, holders, self.pods) == -1:
+            return -1, []
+        if PR.needs_static_verdict(self.prof, pod):
+            # SelectVictimsOnNode re-runs every filter: a node-static one
+            # ordered after the recorded rejection fails the node whatever
+            # is removed (ksg_eval_skipping with the dry run's four skipped)
+            cap = native.CaptureBuffers(len(self.nodes), 1)
+            self.engine.eval_skipping(pi, PR.static_skip_mask(), cap)
+            ok = np.asarray(cap.fstatus[0]) == 0
+            lists = [(n, v) for n, v in lists if ok[n]]
+            if not lists:
+                return -1, []
         off = np.zeros(len(lists) + 1, np.int32)
         off[1:] = np.cumsum([len(v) for _, v in lists])
         vic = np.array([q for _, v in lists for q in v], np.int32)

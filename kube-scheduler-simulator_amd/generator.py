@@ -335,6 +335,47 @@ def preemption_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, s
     return nodes, pods, bound, P.default_profile()
 
 
+def preemption_volume_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, seed: int = 31):
+    """preemption_case with claims: about half of the queued pods claim a
+    zonal PV (VolumeZone), a local PV pinned to one or two hosts
+    (VolumeBinding's node affinity), a plain PV or a ReadWriteOncePod claim
+    that a running pod of higher priority than any preemptor holds
+    (VolumeRestrictions).  In the default order VolumeRestrictions,
+    VolumeBinding and VolumeZone follow NodeResourcesFit, so a node whose
+    recorded rejection is Fit can still fail them in the dry run."""
+    nodes, pods, bound, prof = preemption_case(n_nodes, n_bound, n_queue, seed)
+    rng = np.random.Generator(np.random.PCG64(seed + 9191))
+    st = m.Storage()
+    done = {m.ANN_BIND_COMPLETED: "yes"}
+
+    def claim(name, pv, modes=("ReadWriteOnce",)):
+        st.pvs[pv.name] = pv
+        pv.claim_ref = ("default", name)
+        st.pvcs[("default", name)] = m.PersistentVolumeClaim(name, "default", pv.name, "", modes, dict(done))
+    for z in range(4):
+        claim(f"zonal-{z}", m.PersistentVolume(f"pv-zonal-{z}", labels={m.LABEL_ZONE: f"zone-{z}"}))
+    for k in range(6):
+        hosts = tuple(nodes[int(i)].name for i in rng.choice(len(nodes), size=1 + k % 2, replace=False))
+        claim(f"local-{k}", m.PersistentVolume(f"pv-local-{k}", node_affinity=[
+            m.NodeSelectorTerm(match_expressions=(m.Requirement(m.LABEL_HOSTNAME, m.IN, hosts),))]))
+    claim("plain", m.PersistentVolume("pv-plain"))
+    claim("rwop-0", m.PersistentVolume("pv-rwop-0"), ("ReadWriteOncePod",))
+    shared = [f"zonal-{z}" for z in range(4)] + [f"local-{k}" for k in range(6)] + ["plain"]
+    for p in pods:
+        p.storage = st
+    # the holder of rwop-0: a running pod no preemptor outranks
+    holder = next(i for i, _ in bound if pods[i].node_name)
+    pods[holder].priority = 5000
+    pods[holder].volumes = [("v0", "persistentVolumeClaim", "rwop-0")]
+    for p in pods[len(bound):]:
+        if rng.random() < 0.5:
+            p.volumes = [("v0", "persistentVolumeClaim", str(rng.choice(shared)))]
+    # one queued claimant (the encoder refuses two queued users of one
+    # ReadWriteOncePod claim)
+    pods[len(bound)].volumes = [("v0", "persistentVolumeClaim", "rwop-0")]
+    return nodes, pods, bound, prof
+
+
 def preemption_topo_case(n_nodes: int = 40, n_bound: int = 160, n_queue: int = 120, seed: int = 21):
     """preemption_case with topology: running pods of six apps (a fifth with
     required hostname anti-affinity against another app), queued pods of

@@ -302,6 +302,8 @@ class Engine:
         self._uncommit = f("uncommit", C.c_int, vp, C.c_int32, C.c_int32)
         self._preempt = f("preempt_victims", C.c_int, vp, C.c_int32, i32p, C.c_int32, i32p, i32p, i32p,
                           C.POINTER(C.c_uint8))
+        self._eval_skipping = f("eval_skipping", C.c_int, vp, C.c_int32, C.c_uint32, C.POINTER(KsgResult),
+                                C.POINTER(KsgCapture))
         self._append = f("append_pods", C.c_int, vp, C.POINTER(KsgWorkload), C.c_int64)
         self._declare_extra(f)
 
@@ -363,6 +365,14 @@ class Engine:
     def eval(self, pod: int, capture: Optional[CaptureBuffers] = None) -> KsgResult:
         r = KsgResult()
         self._check(self._eval(self.ctx, pod, C.byref(r), C.byref(capture.struct) if capture else None))
+        return r
+
+    def eval_skipping(self, pod: int, filter_skip: int, capture: Optional[CaptureBuffers] = None) -> KsgResult:
+        """ksg_eval_skipping: ksg_eval with the Filter plugins in the
+        `filter_skip` bit mask skipped (DefaultPreemption's node-static verdict)."""
+        r = KsgResult()
+        self._check(self._eval_skipping(self.ctx, pod, filter_skip, C.byref(r),
+                                        C.byref(capture.struct) if capture else None))
         return r
 
     def eval_view(self, pod: int):

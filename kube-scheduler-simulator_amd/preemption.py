@@ -37,10 +37,20 @@ for a preemptor with hard spread constraints or required inter-pod terms
 (or matched by existing pods' anti-affinity), PodTopologySpread and
 InterPodAffinity with the PreFilter counts of the candidate's domains moved by
 the removed / reprieved pods (ksched_preempt.h; the oracles recompute the
-PreFilter state instead).  Scope (refused with NotImplementedError, never
-computed wrongly): profiles that order a node-static filter after one of those
-three.  There are no PodDisruptionBudgets in a snapshot, so every victim is
-non-violating.
+PreFilter state instead).  The node-static filters (NodeUnschedulable,
+NodeName, TaintToleration, NodeAffinity and the volume plugins) are not
+re-run: no removal changes them.  When one of them is ordered after a
+pod-dependent filter (VolumeBinding / VolumeZone after NodeResourcesFit in
+the default order, for a preemptor with claims), a node whose recorded
+rejection is the pod-dependent one may still fail it; the candidate lists
+then keep only the nodes `ksg_eval_skipping` passes with the pod-dependent
+filters skipped (`static_skip_mask`).  VolumeRestrictions is node-static
+except for a ReadWriteOncePod conflict, which removing the claim's holders
+clears (its RemovePod extension): `rwop_outcome` decides the cases where no
+node can clear it and refuses the one the dry run does not model (every
+holder of lower priority on a single node).  Scope (refused with
+NotImplementedError, never computed wrongly): that case.  There are no
+PodDisruptionBudgets in a snapshot, so every victim is non-violating.
 """
 from __future__ import annotations
 
@@ -57,7 +67,6 @@ SUCCESS, ERROR, UNSCHEDULABLE, UNSCHEDULABLE_AND_UNRESOLVABLE = 0, 1, 2, 3
 NOW = 1 << 62
 INT32_SPAN = 1 << 31          # math.MaxInt32 + 1 (minSumPrioritiesScoreFunc)
 
-_STATIC_FILTERS = (P.NODE_UNSCHEDULABLE, P.NODE_NAME, P.TAINT_TOLERATION, P.NODE_AFFINITY)
 
 
 def status_code(word: int, req=None, alloc=None) -> int:
@@ -84,7 +93,9 @@ def status_code(word: int, req=None, alloc=None) -> int:
         return UNSCHEDULABLE_AND_UNRESOLVABLE if reason == 1 else UNSCHEDULABLE
     if pl == P.INTER_POD_AFFINITY:             # ErrReasonAffinityRulesNotMatch is unresolvable
         return UNSCHEDULABLE_AND_UNRESOLVABLE if reason == 1 else UNSCHEDULABLE
-    return UNSCHEDULABLE_AND_UNRESOLVABLE      # NodeUnschedulable, NodeName, TaintToleration, NodeAffinity
+    if pl == P.VOLUME_RESTRICTIONS:            # satisfyReadWriteOncePod: Unschedulable
+        return UNSCHEDULABLE
+    return UNSCHEDULABLE_AND_UNRESOLVABLE      # node-static filters, VolumeBinding, VolumeZone
 
 
 def start_of(pod: m.Pod) -> int:
@@ -140,20 +151,61 @@ def pick_one_node(cands: Sequence[Tuple[int, Sequence[m.Pod], int]]) -> int:
 _POD_DEPENDENT = (P.NODE_RESOURCES_FIT, P.NODE_PORTS, P.POD_TOPOLOGY_SPREAD, P.INTER_POD_AFFINITY)
 
 
-def check_scope(prof: P.Profile, pod: m.Pod, pods: Sequence[m.Pod]) -> None:
-    """Refuse preemption the dry run cannot decide exactly: it re-runs the
-    filters that read the node's pods (Fit, NodePorts, PodTopologySpread,
-    InterPodAffinity), so every node-static filter must come before them."""
-    if pod.claim_names() and set(prof.filter_order()) & {P.VOLUME_RESTRICTIONS, P.VOLUME_BINDING, P.VOLUME_ZONE}:
-        # the dry run re-runs Fit / PTS / IPA only; VolumeRestrictions' AddPod /
-        # RemovePod extensions (ReadWriteOncePod users) are not modelled
-        raise NotImplementedError("DefaultPreemption for a preemptor with claims (volume plugins)")
+def static_skip_mask() -> int:
+    """ksg_eval_skipping's filter_skip for the node-static verdict: the four
+    filters the dry run re-runs skipped, so a node's status word is 0 iff
+    every other Filter plugin passes it."""
+    return sum(1 << p for p in _POD_DEPENDENT)
+
+
+def needs_static_verdict(prof: P.Profile, pod: m.Pod) -> bool:
+    """Whether a potential node (its recorded rejection pod-dependent) can
+    still fail a node-static filter ordered after that rejection: some
+    static filter follows a pod-dependent one in the profile's order.  The
+    volume plugins count only for a preemptor with claims (Skip or pass
+    without them)."""
     order = prof.filter_order()
     first = min((order.index(p) for p in _POD_DEPENDENT if p in order), default=None)
-    if first is not None:
-        late = [P.PLUGIN_NAMES[p] for p in order[first + 1:] if p in _STATIC_FILTERS]
-        if late:
-            raise NotImplementedError(f"DefaultPreemption with {late} ordered after {P.PLUGIN_NAMES[order[first]]}")
+    if first is None:
+        return False
+    late = [p for p in order[first + 1:] if p not in _POD_DEPENDENT]
+    if not pod.claim_names():
+        late = [p for p in late if p not in E.VOLUME_PLUGINS]
+    return bool(late)
+
+
+def rwop_holders(pod: m.Pod, placed: Sequence[Tuple[int, int, m.Pod]]) -> List[Tuple[int, int]]:
+    """(pod index, node) of the placed pods holding one of `pod`'s
+    ReadWriteOncePod claims: VolumeRestrictions' conflictingPVCRefCount
+    (upstream volumerestrictions PreFilter, StorageInfos.IsPVCUsedByPods).
+    `placed` = (index, node, pod) of every placed pod."""
+    if pod.storage is None:
+        return []
+    rwop = set()
+    for c in pod.claim_names():
+        pvc = pod.storage.claim(pod.namespace, c)
+        if pvc is not None and m.READ_WRITE_ONCE_POD in pvc.access_modes:
+            rwop.add(c)
+    if not rwop:
+        return []
+    return [(q, n) for q, n, o in placed
+            if o is not pod and o.namespace == pod.namespace and rwop & set(o.claim_names())]
+
+
+def rwop_outcome(pod: m.Pod, holders: Sequence[Tuple[int, int]], pods: Sequence[m.Pod]) -> Optional[int]:
+    """A preemptor with a ReadWriteOncePod conflict: removing victims from one
+    node clears the conflict (VolumeRestrictions RemovePod) only when every
+    holder runs on that node and is a potential victim (lower priority).
+    Otherwise VolumeRestrictions rejects the preemptor on every node of the
+    dry run and there is no candidate: returns -1.  The remaining case is
+    refused: the dry run would have to keep the holders evicted through the
+    reprieve."""
+    if not holders:
+        return None
+    if len({n for _, n in holders}) > 1 or any(pods[q].priority >= pod.priority for q, _ in holders):
+        return -1
+    raise NotImplementedError("DefaultPreemption for a preemptor whose ReadWriteOncePod claim a lower-priority "
+                              "pod holds (VolumeRestrictions RemovePod)")
 
 
 def potential_nodes(fstatus, req=None, alloc=None) -> List[int]:

@@ -39,6 +39,8 @@ class Oracle(native.Engine):
 
     def _declare_extra(self, f):
         self._set_threads = f("set_threads", C.c_int, C.c_void_p, C.c_int)
+        self._eval_pod = f("eval_pod", C.c_int, C.c_void_p, C.c_void_p, native.i32p, C.c_int64,
+                           C.POINTER(native.KsgResult), C.POINTER(native.KsgCapture))
         self.abi_version = native.NPLUGINS and 1
 
     def set_threads(self, n: int):

@@ -1066,7 +1066,7 @@ int kso_eval_pod(kso_ctx* c, const ksg_pod* pod, const int32_t* prog, int64_t pr
   const int64_t base = (int64_t)c->prog.size();
   ksg_pod p = *pod;
   for (int32_t* f : {&p.tol, &p.na_req, &p.na_pref, &p.img, &p.node_set, &p.pts, &p.ipa, &p.commit, &p.blob,
-                     &p.ports})
+                     &p.ports, &p.vol})
     if (*f >= 0) *f = (int32_t)(*f + base);
   c->prog.insert(c->prog.end(), prog, prog + prog_len);
   c->pods.push_back(p);
@@ -1087,6 +1087,17 @@ int kso_eval(kso_ctx* c, int32_t pod, ksg_result* res, ksg_capture* cap) {
   if (!c || !res || !c->have_nodes || !c->have_wl || !c->have_prof) return KSG_E_STATE;
   if (pod < 0 || pod >= (int)c->pods.size()) return KSG_E_INVALID;
   return eval_pod(*c, pod, res, cap);
+}
+
+// ksg_eval_skipping: the Filter plugins in filter_skip skipped for this call
+int kso_eval_skipping(kso_ctx* c, int32_t pod, uint32_t filter_skip, ksg_result* res, ksg_capture* cap) {
+  if (!c || !res || !c->have_nodes || !c->have_wl || !c->have_prof) return KSG_E_STATE;
+  if (pod < 0 || pod >= (int)c->pods.size()) return KSG_E_INVALID;
+  const uint32_t keep = c->pods[pod].filter_skip;
+  c->pods[pod].filter_skip |= filter_skip;
+  const int rc = eval_pod(*c, pod, res, cap);
+  c->pods[pod].filter_skip = keep;
+  return rc;
 }
 
 int kso_commit(kso_ctx* c, int32_t pod, int32_t node) {

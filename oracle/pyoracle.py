@@ -1201,7 +1201,7 @@ def _filter_code(plugin: str, msg: str, pod=None, node=None) -> str:
                 if req.get(r, 0) > node.allocatable.get(r, 0):
                     return "UnschedulableAndUnresolvable"
         return "Unschedulable"
-    if plugin == "NodePorts":
+    if plugin in ("NodePorts", "VolumeRestrictions"):   # ErrReasonReadWriteOncePodConflict: Unschedulable
         return "Unschedulable"
     if plugin == "PodTopologySpread":
         return "UnschedulableAndUnresolvable" if msg.endswith("(missing required label)") else "Unschedulable"

@@ -13,8 +13,12 @@
 //  2. potential nodes = Unschedulable (not UnschedulableAndUnresolvable)
 //     filter statuses, from the device's status words;
 //  3. SelectVictimsOnNode for all of them in one ksg_preempt_victims call
-//     (Fit, and PodTopologySpread / InterPodAffinity with the victims'
-//     domain counts moved, for preemptors with topology terms);
+//     (Fit, NodePorts, and PodTopologySpread / InterPodAffinity with the
+//     victims' domain counts moved, for preemptors with topology terms), on
+//     the nodes whose node-static filters pass (ksg_eval_skipping with those
+//     four skipped: VolumeBinding / VolumeZone ordered after Fit), after the
+//     ReadWriteOncePod holders decided what no removal can clear
+//     (preemption.rwop_outcome);
 //  4. the first calculateNumCandidates candidates in node order,
 //     pickOneNodeForPreemption's criteria, lowest column on a final tie;
 //  5. prepareCandidate: delete the victims through the API (their deletion
@@ -172,6 +176,26 @@ func (p *preemption) PostFilter(ctx context.Context, cs *framework.CycleState, p
 	if len(lists) == 0 {
 		return nil, framework.NewStatus(framework.Unschedulable, "preemption: 0/"+fmt.Sprint(len(infos))+" nodes are available")
 	}
+	if out, s := p.rwopOutcome(pod, infos, prio); s != nil {
+		return nil, s
+	} else if out < 0 {
+		return nil, framework.NewStatus(framework.Unschedulable, "preemption: no candidate node")
+	}
+	// node-static verdict: the dry run re-runs only the four filters removals
+	// change; a static one ordered after the recorded rejection stays failed
+	fs, err := e.ctx.EvalSkipping(st.pod, staticSkip)
+	if err != nil {
+		return nil, framework.AsStatus(err)
+	}
+	kept := lists[:0]
+	for _, c := range lists {
+		if fs[c.col] == 0 {
+			kept = append(kept, c)
+		}
+	}
+	if lists = kept; len(lists) == 0 {
+		return nil, framework.NewStatus(framework.Unschedulable, "preemption: no candidate node")
+	}
 	cand, off, vic := make([]int32, 0, len(lists)), []int32{0}, []int32{}
 	for _, c := range lists {
 		cand = append(cand, int32(c.col))
@@ -226,6 +250,69 @@ func (p *preemption) PostFilter(ctx context.Context, cs *framework.CycleState, p
 	}
 	return &framework.PostFilterResult{NominatingInfo: &framework.NominatingInfo{
 		NominatedNodeName: best.node, NominatingMode: framework.ModeOverride}}, framework.NewStatus(framework.Success)
+}
+
+// staticSkip: the filters SelectVictimsOnNode's removals can change.
+const staticSkip = uint32(1)<<ksched.NodeResourcesFit | uint32(1)<<ksched.NodePorts |
+	uint32(1)<<ksched.PodTopologySpread | uint32(1)<<ksched.InterPodAffinity
+
+// rwopOutcome is preemption.rwop_outcome: the pods holding one of pod's
+// ReadWriteOncePod claims (VolumeRestrictions' conflictingPVCRefCount).
+// Removing victims clears the conflict only on a node that runs every holder
+// with each of lower priority; otherwise no candidate exists (-1).  That one
+// node is refused (an Error status): the dry run does not keep the holders
+// evicted through the reprieve.  0: no holder.
+func (p *preemption) rwopOutcome(pod *v1.Pod, infos []*framework.NodeInfo, prio int32) (int, *framework.Status) {
+	f := p.h.SharedInformerFactory()
+	if f == nil {
+		return 0, nil
+	}
+	pvcs := f.Core().V1().PersistentVolumeClaims().Lister().PersistentVolumeClaims(pod.Namespace)
+	rwop := map[string]struct{}{}
+	for _, vol := range pod.Spec.Volumes {
+		if vol.PersistentVolumeClaim == nil {
+			continue
+		}
+		c, err := pvcs.Get(vol.PersistentVolumeClaim.ClaimName)
+		if err != nil {
+			continue // a missing claim is VolumeRestrictions' PreFilter rejection
+		}
+		for _, m := range c.Spec.AccessModes {
+			if m == v1.ReadWriteOncePod {
+				rwop[c.Name] = struct{}{}
+			}
+		}
+	}
+	if len(rwop) == 0 {
+		return 0, nil
+	}
+	holderNode, holders := "", 0
+	for _, ni := range infos {
+		for _, pi := range ni.Pods {
+			q := pi.Pod
+			if q.UID == pod.UID || q.Namespace != pod.Namespace {
+				continue
+			}
+			for _, vol := range q.Spec.Volumes {
+				if vol.PersistentVolumeClaim == nil {
+					continue
+				}
+				if _, ok := rwop[vol.PersistentVolumeClaim.ClaimName]; !ok {
+					continue
+				}
+				if podPriority(q) >= prio || (holders > 0 && holderNode != ni.Node().Name) {
+					return -1, nil
+				}
+				holderNode, holders = ni.Node().Name, holders+1
+				break
+			}
+		}
+	}
+	if holders == 0 {
+		return 0, nil
+	}
+	return 0, framework.AsStatus(fmt.Errorf("DefaultPreemption: a lower-priority pod on %s holds a ReadWriteOncePod claim of %s/%s (not modelled)",
+		holderNode, pod.Namespace, pod.Name))
 }
 
 // PreemptionFactory returns the DefaultPreemption replacement (register it

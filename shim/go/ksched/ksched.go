@@ -307,6 +307,23 @@ func (x *Ctx) PreemptVictims(pod int, cand, off, vic []int32) (fits []int32, vic
 	return fits, victim, err
 }
 
+// EvalSkipping evaluates loaded pod `pod` with the Filter plugins in the
+// skip bit mask skipped (ksg_eval_skipping) and returns the filter status
+// words: DefaultPreemption's node-static verdict (status 0 = every filter
+// outside the mask passes the node).
+func (x *Ctx) EvalSkipping(pod int, skip uint32) ([]uint32, error) {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	n := x.nN
+	fs, raw, norm, total := make([]uint32, n), make([]int64, NPlugins*n), make([]int64, NPlugins*n), make([]int64, n)
+	var res C.ksg_result
+	cap := C.ksg_capture{fstatus: pu32(fs), raw: p64(raw), norm: p64(norm), total: p64(total)}
+	if err := x.check(C.ksg_eval_skipping(x.c, C.int32_t(pod), C.uint32_t(skip), &res, &cap)); err != nil {
+		return nil, err
+	}
+	return fs, nil
+}
+
 // RunQueue schedules pods [first, first+count) on the device in queue order.
 func (x *Ctx) RunQueue(first, count int) ([]int32, error) {
 	x.mu.Lock()

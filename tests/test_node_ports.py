@@ -233,7 +233,7 @@ def test_preemptor_with_host_ports_kat(engine, request):
     low.priority = keep.priority = 0
     cand.priority = 100
     pods = [low, keep, cand]
-    PR.check_scope(P.default_profile(), cand, pods)   # in scope now
+    assert not PR.needs_static_verdict(P.default_profile(), cand)   # no claims: the dry run decides alone
     eng = binding.Oracle(1) if engine == "oracle" else (request.getfixturevalue("built") and native.Engine(device=0))
     s = F.DebuggableScheduler(nodes, pods, P.default_profile(), engine=eng, bound=[(0, 0), (1, 0)])
     placed = s.schedule_one(2)

@@ -142,14 +142,108 @@ def test_framework_run_queue_matches_single_cycles():
     assert list(pl) == placed and s2.preemptions == s1.preemptions
 
 
-def test_scope_refusals():
-    """A node-static filter ordered after a pod-dependent one is refused."""
+def _vs_pyoracle(nodes, pods, bound, prof, engine=None):
+    s, placed, ann = _run_framework(engine or _oracle_engine(), nodes, pods, bound, prof)
+    nb = len(bound)
+    ora, recs = pyoracle_annotations(nodes, pods[nb:], prof, bound=[(pods[i], nodes[n].name) for i, n in bound])
+    assert [r["selected_index"] for r in recs] == placed
+    pre = [(pi - nb, s.node_names[n], [(pods[v].namespace, pods[v].name) for v in vs]) for pi, n, vs in s.preemptions]
+    ref = [(k, r["first_attempt"]["nominated"], r["first_attempt"]["victims"])
+           for k, r in enumerate(recs) if "first_attempt" in r]
+    assert pre == ref
+    assert ann == ora
+    return s
+
+
+def test_static_filter_after_fit_vs_pyoracle():
+    """TaintToleration ordered after NodeResourcesFit: node-2 (tainted) holds
+    the cheapest victim and its recorded rejection is Fit (Unschedulable),
+    but the dry run's TaintToleration still rejects it; the node-static
+    verdict (ksg_eval_skipping) keeps it out of the candidates."""
     nodes, pods, bound, prof = _kat(100)
+    f = m.Pod(name="f", containers=[m.Container(image="pause", requests={m.CPU: 4000, m.MEMORY: GI})])
+    f.priority, f.start_time, f.node_name = 0, 5, "node-2"
+    pods.insert(5, f)
+    bound.append((5, 2))
     names = [n for n, _ in prof.plugins]
     i, j = names.index("TaintToleration"), names.index("NodeResourcesFit")
     prof.plugins[i], prof.plugins[j] = prof.plugins[j], prof.plugins[i]
+    assert PR.needs_static_verdict(prof, pods[-1])
+    s = _vs_pyoracle(nodes, pods, bound, prof)
+    (pi, nom, victims), = s.preemptions
+    assert s.node_names[nom] == "node-0" and [pods[v].name for v in victims] == ["a"]
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_volume_preemptors_vs_pyoracle(seed):
+    """Preemptors with claims (zonal / local / plain PVs, one ReadWriteOncePod
+    claim a higher-priority running pod holds): VolumeBinding / VolumeZone
+    ordered after Fit filter the candidates, VolumeRestrictions' conflict
+    leaves none."""
+    nodes, pods, bound, prof = G.preemption_volume_case(seed=seed)
+    nb = len(bound)
+    s = _vs_pyoracle(nodes, pods, bound, prof)
+    claimants = [pi for pi, _, _ in s.preemptions if pods[pi].claim_names()]
+    assert len(claimants) >= 5
+    assert pods[nb].claim_names() == ["rwop-0"] and nb not in {pi for pi, _, _ in s.preemptions}
+
+
+def test_eval_skipping_and_eval_pod_with_claims():
+    """The oracle's ksg_eval_skipping: no status word names a skipped plugin,
+    every node ksg_eval passes still passes, and the record is restored; its
+    ksg_eval_pod of a pod with claims (the volume program rebased) equals
+    ksg_eval."""
+    E = pkg("encoder")
+    nodes, pods, bound, prof = G.preemption_volume_case(seed=31)
+    enc = E.Encoder(nodes, pods, prof, bound_pods=[i for i, _ in bound])
+    eng = _oracle_engine()
+    eng.load(enc, E.encode_profile(prof, enc.cluster.res_names))
+    N, mask = len(nodes), PR.static_skip_mask()
+    n_vol = 0
+    for pi in range(len(bound), len(pods), 2):
+        a, b, c = (native.CaptureBuffers(N) for _ in range(3))
+        r0 = eng.eval(pi, a)
+        eng.eval_skipping(pi, mask, b)
+        fa, fb = np.asarray(a.fstatus[0]), np.asarray(b.fstatus[0])
+        assert not any((mask >> ((int(w) & 0xFF) - 1)) & 1 for w in fb if w and w != 0xFFFFFFFF)
+        assert np.all(fb[fa == 0] == 0)
+        r1 = eng.eval(pi, c)
+        assert (r0.selected, r0.n_feasible, r0.status) == (r1.selected, r1.n_feasible, r1.status)
+        rec = enc.workload.pods[pi].copy()
+        if int(rec["vol"]) < 0 or int(rec["node_set"]) >= 0:
+            continue
+        n_vol += 1
+        lo, hi = int(rec["blob"]), int(rec["blob"]) + int(rec["blob_len"])
+        for f in ("tol", "na_req", "na_pref", "img", "pts", "ipa", "commit", "blob", "ports", "vol"):
+            if int(rec[f]) >= 0:
+                rec[f] = int(rec[f]) - lo
+        d = native.CaptureBuffers(N)
+        r2 = eng.eval_pod(rec, enc.workload.prog[lo:hi], d)
+        assert (r2.selected, r2.n_feasible, r2.status) == (r0.selected, r0.n_feasible, r0.status)
+        np.testing.assert_array_equal(d.fstatus, a.fstatus)
+    assert n_vol >= 5
+
+
+def test_rwop_holder_refusal():
+    """The one case refused: every holder of the preemptor's
+    ReadWriteOncePod claim a potential victim on one node."""
+    nodes, pods, bound, prof = _kat(100)
+    st = m.Storage()
+    pv = m.PersistentVolume("pv-r", claim_ref=("default", "r"))
+    st.pvs[pv.name] = pv
+    st.pvcs[("default", "r")] = m.PersistentVolumeClaim("r", "default", "pv-r", "", ("ReadWriteOncePod",),
+                                                        {m.ANN_BIND_COMPLETED: "yes"})
+    for p in pods:
+        p.storage = st
+    pods[0].volumes = [("v0", "persistentVolumeClaim", "r")]     # a (prio 1) on node-0
+    pods[-1].volumes = [("v0", "persistentVolumeClaim", "r")]
+    assert PR.status_code(1 + P.VOLUME_RESTRICTIONS) == PR.UNSCHEDULABLE
     with pytest.raises(NotImplementedError):
         _run_framework(_oracle_engine(), nodes, pods, bound, prof)
+    pods[0].priority = 10                                         # the holder outranks nobody: no candidate
+    pods[-1].priority = 10
+    s, placed, _ = _run_framework(_oracle_engine(), nodes, pods, bound, prof)
+    assert placed == [-1] and not s.preemptions
 
 
 def _topo_preemptors(s, pods):
@@ -214,6 +308,54 @@ def test_gpu_host_port_preemption_matches_pyoracle(built, seed):
     assert [r["selected_index"] for r in recs] == placed
     assert ann == ora
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [31, 32, 33])
+def test_gpu_volume_preemptors_match_pyoracle(built, seed):
+    """Preemptors with claims on the device: ksg_eval_skipping's node-static
+    verdict (VolumeBinding / VolumeZone after Fit) against pyoracle."""
+    nodes, pods, bound, prof = G.preemption_volume_case(seed=seed, n_nodes=60, n_bound=260, n_queue=160)
+    s = _vs_pyoracle(nodes, pods, bound, prof, native.Engine(device=0))
+    assert [pi for pi, _, _ in s.preemptions if pods[pi].claim_names()]
+
+
+@pytest.mark.gpu
+def test_gpu_static_filter_after_fit(built):
+    nodes, pods, bound, prof = _kat(100)
+    f = m.Pod(name="f", containers=[m.Container(image="pause", requests={m.CPU: 4000, m.MEMORY: GI})])
+    f.priority, f.start_time, f.node_name = 0, 5, "node-2"
+    pods.insert(5, f)
+    bound.append((5, 2))
+    names = [n for n, _ in prof.plugins]
+    i, j = names.index("TaintToleration"), names.index("NodeResourcesFit")
+    prof.plugins[i], prof.plugins[j] = prof.plugins[j], prof.plugins[i]
+    s = _vs_pyoracle(nodes, pods, bound, prof, native.Engine(device=0))
+    assert [s.node_names[n] for _, n, _ in s.preemptions] == ["node-0"]
+
+
+@pytest.mark.gpu
+def test_gpu_eval_skipping_equals_oracle(built):
+    """ksg_eval_skipping on every pod of a volume case, equal to the oracle's
+    twin and leaving the record as it was (a plain ksg_eval after it)."""
+    E = pkg("encoder")
+    nodes, pods, bound, prof = G.preemption_volume_case(seed=33)
+    enc = E.Encoder(nodes, pods, prof, bound_pods={i for i, _ in bound})
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu, cpu = native.Engine(device=0), _oracle_engine()
+    gpu.load(enc, pf)
+    cpu.load(enc, pf)
+    N = len(nodes)
+    for pi in range(len(bound), len(pods), 3):
+        a, b = native.CaptureBuffers(N), native.CaptureBuffers(N)
+        ra = gpu.eval_skipping(pi, PR.static_skip_mask(), a)
+        rb = cpu.eval_skipping(pi, PR.static_skip_mask(), b)
+        assert (ra.selected, ra.n_feasible) == (rb.selected, rb.n_feasible)
+        np.testing.assert_array_equal(a.fstatus, b.fstatus)
+        a2, b2 = native.CaptureBuffers(N), native.CaptureBuffers(N)
+        r2, r3 = gpu.eval(pi, a2), cpu.eval(pi, b2)
+        assert (r2.selected, r2.n_feasible, r2.status) == (r3.selected, r3.n_feasible, r3.status)
+        np.testing.assert_array_equal(a2.fstatus, b2.fstatus)
 
 
 @pytest.mark.gpu
