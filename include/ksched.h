@@ -268,9 +268,10 @@ int ksg_eval(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap);
 
 /* The per-cycle results of ksg_eval_view, in library memory (no copy into
  * caller arrays): valid until the next ksg_eval / ksg_eval_view / ksg_eval_pod
- * on the context.  Rows hold elem_bytes-wide signed integers (2 when every
- * raw score, normalised score and weighted total fits 16 bits, 4 when they fit
- * 32 bits, else 8), one per node; raw[pl] / norm[pl] are
+ * on the context.  Rows hold elem_bytes-wide integers, one per node: 1 =
+ * unsigned byte (the node-local per-cycle path when every raw score is in
+ * [0, 255]), else signed (2 when every raw score, normalised score and
+ * weighted total fits 16 bits, 4 when they fit 32 bits, else 8); raw[pl] / norm[pl] are
  * NULL for a plugin the profile does not score (norm[pl] == raw[pl] for the
  * plugins without ScoreExtensions).  A pod with fewer than two feasible nodes
  * has all-zero rows (no Score runs).  The Go shim's Score / NormalizeScore

@@ -2374,10 +2374,12 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     if ((prof.score_mask >> pl) & 1u) rows[n_rows++] = pl;
   // Row width: the narrowest exact one.  Raw Fit / BalancedAllocation /
   // ImageLocality are in [0, 100]; raw TaintToleration is at most the node's
-  // taint count, raw NodeAffinity at most the pod's summed preferred weights.
+  // taint count, raw NodeAffinity at most the pod's summed preferred weights;
+  // none is negative, so one unsigned byte holds them up to 255 (the rows are
+  // most of the bytes a cycle writes across the host link).
   const ksg_pod& hp = ctx->h_pods[pod];
   int64_t bound = std::max<int64_t>({(int64_t)100, (int64_t)ctx->c.T, na_pref_bound(ctx, hp)});
-  size_t es = bound < (1 << 15) ? 2 : bound < (1ll << 31) ? 4 : 8;
+  size_t es = bound <= 255 ? 1 : bound < (1 << 15) ? 2 : bound < (1ll << 31) ? 4 : 8;
   int rc;
   HIPC(ctx, hipSetDevice(ctx->device));
   // one-wave workgroups, KN nodes per lane: the smallest KN whose grid is
@@ -2748,8 +2750,9 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
   res->score_skip = score_skip;
   auto row_at = [&](int q, size_t n) -> int64_t {   // raw row q at node n
     const char* r = hb + o_raw + es * N * q;
-    return es == 2 ? reinterpret_cast<const int16_t*>(r)[n]
-                   : es == 4 ? reinterpret_cast<const int32_t*>(r)[n] : reinterpret_cast<const int64_t*>(r)[n];
+    return es == 1   ? reinterpret_cast<const uint8_t*>(r)[n]
+           : es == 2 ? reinterpret_cast<const int16_t*>(r)[n]
+           : es == 4 ? reinterpret_cast<const int32_t*>(r)[n] : reinterpret_cast<const int64_t*>(r)[n];
   };
   // DefaultNormalizeScore of TaintToleration (reverse) / NodeAffinity from
   // the raw value and the device's maximum over the feasible nodes (the

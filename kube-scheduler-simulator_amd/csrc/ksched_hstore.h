@@ -20,7 +20,8 @@ __device__ __forceinline__ void cyc_put(char* base, size_t idx, int64_t v, bool 
 }
 template <bool SYS>
 __device__ __forceinline__ void cyc_put_es(char* base, size_t idx, int64_t v, int es) {
-  if (es == 2) hst<SYS>(reinterpret_cast<int16_t*>(base) + idx, (int16_t)v);
+  if (es == 1) hst<SYS>(reinterpret_cast<uint8_t*>(base) + idx, (uint8_t)v);
+  else if (es == 2) hst<SYS>(reinterpret_cast<int16_t*>(base) + idx, (int16_t)v);
   else cyc_put<SYS>(base, idx, v, es == 4);
 }
 

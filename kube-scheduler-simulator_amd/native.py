@@ -381,7 +381,7 @@ class Engine:
         r, v = KsgResult(), KsgEvalRows()
         self._check(self._eval_view(self.ctx, pod, C.byref(r), C.byref(v)))
         n = v.n_nodes
-        ct = {2: C.c_int16, 4: C.c_int32, 8: C.c_int64}[v.elem_bytes]
+        ct = {1: C.c_uint8, 2: C.c_int16, 4: C.c_int32, 8: C.c_int64}[v.elem_bytes]
 
         def row(ptr):
             return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), (n,)).astype(np.int64)

@@ -180,6 +180,8 @@ func (e *PodEval) at(p unsafe.Pointer, node int) int64 {
 		return 0
 	}
 	switch e.elem {
+	case 1:
+		return int64(*(*uint8)(unsafe.Add(p, node)))
 	case 2:
 		return int64(*(*int16)(unsafe.Add(p, 2*node)))
 	case 4:

@@ -16,6 +16,7 @@ G = pkg("generator")
 E = pkg("encoder")
 P = pkg("profile")
 native = pkg("native")
+m = pkg("model")
 
 pytestmark = pytest.mark.gpu
 
@@ -258,7 +259,12 @@ def test_eval_view_equals_eval_with_capture(gpu, built):
     them, and must equal the capture's (which test_eval_cycle_matches_oracle
     compares with the oracle's)."""
     import zoo
-    for nodes, pods, prof in (G.config2(n_nodes=1500, n_pods=30, seed=3), zoo.zoo(2, n_pods=40)):
+    wide = G.config2(n_nodes=1500, n_pods=30, seed=3)
+    for p in wide[1][::3]:   # preferred weights summing past one byte: 2-byte rows for these pods
+        p.node_affinity_preferred = [m.PreferredSchedulingTerm(100, m.NodeSelectorTerm(match_expressions=(
+            m.Requirement("pool", m.IN, (pool,)),))) for pool in G.POOLS[:3]]
+    widths = set()
+    for nodes, pods, prof in (G.config2(n_nodes=1500, n_pods=30, seed=3), zoo.zoo(2, n_pods=40), wide):
         enc = E.Encoder(nodes, pods, prof)
         pf = E.encode_profile(prof, enc.cluster.res_names)
         gpu.load(enc, pf)
@@ -267,6 +273,7 @@ def test_eval_view_equals_eval_with_capture(gpu, built):
             cap = native.CaptureBuffers(len(nodes), 1)
             ra = gpu.eval(i, cap)
             rv, v = gpu.eval_view(i)
+            widths.add(v["elem_bytes"])
             assert (ra.selected, ra.n_feasible, ra.status, ra.score_skip) == (rv.selected, rv.n_feasible, rv.status,
                                                                                rv.score_skip)
             np.testing.assert_array_equal(cap.fstatus[0], v["fstatus"])
@@ -280,6 +287,7 @@ def test_eval_view_equals_eval_with_capture(gpu, built):
                 assert gpu.last_run_info()[0] == 5
             if ra.selected >= 0:
                 gpu.commit(i, ra.selected)
+    assert {1, 2} <= widths   # one-byte rows when every raw score fits, two when one does not
 
 
 def _engine_with(env):
