@@ -25,3 +25,23 @@ def built():
     ge = importlib.import_module("__graft_entry__")
     ge.build()
     return True
+
+
+@pytest.fixture(autouse=True)
+def _device_sync_after_test(request):
+    """KSG_TEST_DEVICE_SYNC=1 (diagnosis only): after every GPU test, let the
+    persistent servers idle out and synchronise the device, so an
+    asynchronous fault is reported by the test whose kernels raised it."""
+    yield
+    if not os.environ.get("KSG_TEST_DEVICE_SYNC") or request.node.get_closest_marker("gpu") is None:
+        return
+    import ctypes
+    import gc
+    import time
+    gc.collect()
+    time.sleep(0.15)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipGetErrorString.restype = ctypes.c_char_p
+    rc = hip.hipDeviceSynchronize()
+    if rc != 0:
+        pytest.fail(f"device fault after {request.node.nodeid}: {hip.hipGetErrorString(rc).decode()}")
