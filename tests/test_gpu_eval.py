@@ -259,35 +259,52 @@ def test_eval_view_equals_eval_with_capture(gpu, built):
     them, and must equal the capture's (which test_eval_cycle_matches_oracle
     compares with the oracle's)."""
     import zoo
-    wide = G.config2(n_nodes=1500, n_pods=30, seed=3)
-    for p in wide[1][::3]:   # preferred weights summing past one byte: 2-byte rows for these pods
+    for nodes, pods, prof in (G.config2(n_nodes=1500, n_pods=30, seed=3), zoo.zoo(2, n_pods=40)):
+        _view_equals_capture(gpu, nodes, pods, prof)
+
+
+def test_eval_view_row_widths(built):
+    """The per-cycle rows are one byte wide while every raw score fits in
+    [0, 255], two bytes for a pod whose preferred node-affinity weights sum
+    past it; both equal ksg_eval's capture.  (Its own engine, closed at the
+    end: no server of it outlives the test.)"""
+    nodes, pods, prof = G.config2(n_nodes=1500, n_pods=30, seed=3)
+    for p in pods[::3]:
         p.node_affinity_preferred = [m.PreferredSchedulingTerm(100, m.NodeSelectorTerm(match_expressions=(
             m.Requirement("pool", m.IN, (pool,)),))) for pool in G.POOLS[:3]]
+    eng = native.Engine(device=0)
+    try:
+        widths = _view_equals_capture(eng, nodes, pods, prof)
+    finally:
+        eng.close()
+    assert widths == {1, 2}
+
+
+def _view_equals_capture(gpu, nodes, pods, prof):
     widths = set()
-    for nodes, pods, prof in (G.config2(n_nodes=1500, n_pods=30, seed=3), zoo.zoo(2, n_pods=40), wide):
-        enc = E.Encoder(nodes, pods, prof)
-        pf = E.encode_profile(prof, enc.cluster.res_names)
-        gpu.load(enc, pf)
-        rows = _score_rows(pf)
-        for i in range(len(pods)):
-            cap = native.CaptureBuffers(len(nodes), 1)
-            ra = gpu.eval(i, cap)
-            rv, v = gpu.eval_view(i)
-            widths.add(v["elem_bytes"])
-            assert (ra.selected, ra.n_feasible, ra.status, ra.score_skip) == (rv.selected, rv.n_feasible, rv.status,
-                                                                               rv.score_skip)
-            np.testing.assert_array_equal(cap.fstatus[0], v["fstatus"])
-            assert sorted(v["raw"]) == sorted(rows)
-            for p in rows:
-                np.testing.assert_array_equal(cap.raw[0, p], v["raw"][p])
-                np.testing.assert_array_equal(cap.norm[0, p], v["norm"][p])
-            if v["total"] is not None:   # (the node-local per-cycle kernel leaves the totals out)
-                np.testing.assert_array_equal(cap.total[0], v["total"])
-            else:
-                assert gpu.last_run_info()[0] == 5
-            if ra.selected >= 0:
-                gpu.commit(i, ra.selected)
-    assert {1, 2} <= widths   # one-byte rows when every raw score fits, two when one does not
+    enc = E.Encoder(nodes, pods, prof)
+    pf = E.encode_profile(prof, enc.cluster.res_names)
+    gpu.load(enc, pf)
+    rows = _score_rows(pf)
+    for i in range(len(pods)):
+        cap = native.CaptureBuffers(len(nodes), 1)
+        ra = gpu.eval(i, cap)
+        rv, v = gpu.eval_view(i)
+        widths.add(v["elem_bytes"])
+        assert (ra.selected, ra.n_feasible, ra.status, ra.score_skip) == (rv.selected, rv.n_feasible, rv.status,
+                                                                           rv.score_skip)
+        np.testing.assert_array_equal(cap.fstatus[0], v["fstatus"])
+        assert sorted(v["raw"]) == sorted(rows)
+        for p in rows:
+            np.testing.assert_array_equal(cap.raw[0, p], v["raw"][p])
+            np.testing.assert_array_equal(cap.norm[0, p], v["norm"][p])
+        if v["total"] is not None:   # (the node-local per-cycle kernel leaves the totals out)
+            np.testing.assert_array_equal(cap.total[0], v["total"])
+        else:
+            assert gpu.last_run_info()[0] == 5
+        if ra.selected >= 0:
+            gpu.commit(i, ra.selected)
+    return widths
 
 
 def _engine_with(env):
