@@ -506,6 +506,14 @@ int launch_queue(ksg_ctx* ctx, QueueArgs& a, int n_replicas, int block, bool top
 // Whether [p, p + len) lies in a writable mapping of this process
 // (/proc/self/maps): a device allocation the CPU may store to (large BAR)
 // rather than a GPU-only virtual range.
+// Kernel arguments in device memory (HIP_FORCE_DEV_KERNARG=1) unless the
+// process set it: the batched walk dispatches one single-workgroup kernel per
+// 64-pod batch, and reading each argument block from host memory at dispatch
+// cost 8-16 % of the headline (scripts/gpu_kernarg_ab.sh, round 6).  The
+// runtime reads its environment at the first HIP call, after this library is
+// loaded in the Go shim and in native.py (which sets the same default).
+__attribute__((constructor)) void ksg_env_defaults() { setenv("HIP_FORCE_DEV_KERNARG", "1", 0); }
+
 bool host_writable(const void* p, size_t len) {
   FILE* f = std::fopen("/proc/self/maps", "r");
   if (!f) return false;

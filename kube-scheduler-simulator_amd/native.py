@@ -15,6 +15,13 @@ from typing import Optional
 
 import numpy as np
 
+# Kernel arguments in device memory: the batched walk launches one
+# single-workgroup kernel per 64-pod batch, and fetching each launch's
+# argument block from host memory cost 8-16 % of the headline
+# (scripts/gpu_kernarg_ab.sh).  The HIP runtime reads it at its first call;
+# a caller's own setting wins (libksched.so sets the same default at load).
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 from . import encoder as E
 
 HERE = os.path.dirname(os.path.abspath(__file__))
