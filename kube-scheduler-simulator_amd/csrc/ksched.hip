@@ -170,6 +170,12 @@ struct ksg_ctx {
   bool last_n32 = false;      // the last batched run's slot walk ran the 32-bit instances
   bool last_spec = false;     // ... the speculate-and-verify walk
   bool last_mw = false;       // ... in its wide-memory instance
+  bool spec_persist = true;   // env KSG_SPEC_PERSIST=0: one spec-walk launch per batch (else one for the run)
+  unsigned* h_p2done = nullptr;   // the persistent walk's batches-walked counter (pinned, mapped)
+  unsigned* d_p2done = nullptr;
+  int32_t* d_btab = nullptr;      // its batch table ([batch][6]; grown, freed with the context)
+  size_t btab_cap = 0;
+  std::vector<int32_t> h_btab;
   bool pipe_overlap = true;   // env KSG_PIPE_OVERLAP=0: the window pipeline on one stream (same arithmetic;
                               // for counter passes, which serialise kernels: a walk polling for the
                               // other stream's top-k would wait out its poll bound)
@@ -403,6 +409,8 @@ void free_all(ksg_ctx* ctx) {
   ctx->d_ev_pl = nullptr;
   ctx->ev_prof_dirty = true;
   ctx->d_srv = nullptr;   // (the server was stopped before anything freed)
+  ctx->d_btab = nullptr;
+  ctx->btab_cap = 0;
 }
 
 // ---- per-kernel timing -------------------------------------------------------
@@ -895,6 +903,143 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
   return KSG_OK;
 }
 
+// The window pipeline with the persistent spec walk (ksg_batch_phase2v_run):
+// the batch table first (the same LDS-fitting batches as the per-batch
+// launches), the walk launched once on the main stream, then phase 1 / top-k
+// of batch b on the second stream as soon as the walk has finished batch
+// b - 2 (the walk's counter in pinned host memory; each of those launches
+// acquires at its dispatch what the walk released).  The walk polls each
+// batch's top-k flag as before.  The host's wait is bounded: a walk that
+// ended early (a timed-out hand-off, a broken invariant) stops the launches
+// and run_internal reports its words.
+int run_spec_persistent(ksg_ctx* ctx, const BatchArgs& b0, int32_t first, int32_t count, size_t cm_words, bool mw,
+                        unsigned* tk, int32_t* carry_n) {
+  const int N = ctx->c.N;
+  constexpr int B = 64;
+  std::vector<int32_t>& tab = ctx->h_btab;
+  tab.clear();
+  for (int off = 0, prev_nb = 0; off < count;) {
+    int nb = std::min(B, count - off);
+    int64_t lo = 0, hi = 0;
+    size_t bytes = 0;
+    for (;;) {
+      lo = ctx->h_pods[first + off].blob;
+      hi = lo;
+      for (int k = 0; k < nb; k++) {
+        const ksg_pod& q = ctx->h_pods[first + off + k];
+        lo = std::min<int64_t>(lo, q.blob);
+        hi = std::max<int64_t>(hi, (int64_t)q.blob + q.blob_len);
+      }
+      bytes = 4 * ((cm_words + (size_t)nb * (sizeof(ksg_pod) / 4) + (size_t)(hi - lo) + 3) & ~(size_t)3) +
+              (size_t)kSvSlots * kSvRow * 8 + (size_t)kSvSlots * 64 * 4 + (size_t)64 * (nb + prev_nb) * 4;
+      if (bytes <= kSpecLds || nb == 1) break;
+      nb = std::max(1, nb / 2);
+    }
+    if (bytes > kSpecLds) return fail(ctx, KSG_E_UNSUPPORTED, "batch does not fit the LDS budget");
+    for (int32_t v : {first + off, off, nb, (int32_t)lo, (int32_t)(hi - lo), prev_nb}) tab.push_back(v);
+    prev_nb = nb;
+    off += nb;
+  }
+  const int nbatch = (int)(tab.size() / 6);
+  int rc;
+  if (tab.size() > ctx->btab_cap) {
+    if (ctx->d_btab) {
+      auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), (void*)ctx->d_btab);
+      if (it != ctx->allocs.end()) ctx->allocs.erase(it);
+      HIPC(ctx, hipStreamSynchronize(ctx->stream));
+      (void)hipFree(ctx->d_btab);
+      ctx->d_btab = nullptr;
+    }
+    if ((rc = dalloc(ctx, &ctx->d_btab, tab.size()))) return rc;
+    ctx->btab_cap = tab.size();
+  }
+  if (!ctx->h_p2done) {
+    HIPC(ctx, hipHostMalloc((void**)&ctx->h_p2done, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    void* dp = nullptr;
+    HIPC(ctx, hipHostGetDevicePointer(&dp, ctx->h_p2done, 0));
+    ctx->d_p2done = static_cast<unsigned*>(dp);
+  }
+  hipStream_t s1 = ctx->stream2, s2 = ctx->stream;
+  HIPC(ctx, hipMemcpyAsync(ctx->d_btab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice, s2));
+  volatile unsigned* done = ctx->h_p2done;
+  *done = 0;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  SpecRun r{};
+  r.btab = ctx->d_btab;
+  r.nbatch = nbatch;
+  for (int q = 0; q < 2; q++) {
+    r.rec[q] = ctx->d_prec[q];
+    r.img[q] = ctx->d_pimg[q];
+    r.rect[q] = ctx->d_prect[q];
+    r.imgt[q] = ctx->d_pimgt[q];
+    r.pmax[q] = ctx->d_ppmax[q];
+    r.p1[q] = ctx->d_pp1[q];
+    r.top[q] = ctx->d_ptop[q];
+  }
+  r.carry = ctx->d_carry;
+  r.carry_n = carry_n;
+  r.done = ctx->d_p2done;
+  BatchArgs base = b0;
+  base.tk_arrive = tk;
+  base.tk_done = tk + 1;
+  base.tk_timeout = tk + 2;
+  base.walk_err = tk + 3;
+  base.inject_walk_err = ctx->inject_walk_err;
+  base.tk_sc = 1;
+  base.stat = nullptr;
+  base.xcd_grid = 1;
+  const void* run_kern = mw ? (const void*)ksg_batch_phase2v_run<64 * kSvWaves, true>
+                            : (const void*)ksg_batch_phase2v_run<64 * kSvWaves, false>;
+  if ((rc = func_lds_attr(ctx, run_kern, kSpecLds))) return rc;
+  void* kargs[] = {&base, &r};
+  HIPC(ctx, hipLaunchKernel(run_kern, dim3(1), dim3(64 * kSvWaves), kargs, kSpecLds, s2));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int bi = 0; bi < nbatch; bi++) {
+    if (bi >= 2) {   // phase 1 of batch bi reads what the walk of batch bi - 2 wrote, into its buffers
+      for (unsigned spins = 0; *done < (unsigned)(bi - 1); spins++) {
+        __builtin_ia32_pause();
+        if ((spins & 4095) == 4095) {
+          const hipError_t e = hipStreamQuery(s2);
+          if (e != hipErrorNotReady && *done < (unsigned)(bi - 1)) {
+            if (e != hipSuccess) return fail(ctx, KSG_E_DEVICE, std::string("spec walk: ") + hipGetErrorString(e));
+            bi = nbatch;   // the walk ended early: run_internal reports its words
+            break;
+          }
+          if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 120.0)
+            return fail(ctx, KSG_E_DEVICE, "spec walk: no progress for 120 s");
+        }
+      }
+      if (bi >= nbatch) break;
+    }
+    const int32_t* d = tab.data() + 6 * bi;
+    const int par = bi & 1;
+    BatchArgs b = base;
+    b.b0 = d[0];
+    b.out0 = d[1];
+    b.nb = d[2];
+    b.prog_lo = d[3];
+    b.prog_len = d[4];
+    b.k_extra = d[5];
+    b.rec = r.rec[par];
+    b.img = r.img[par];
+    b.rect = r.rect[par];
+    b.imgt = r.imgt[par];
+    b.pmax = r.pmax[par];
+    b.p1 = r.p1[par];
+    b.top = r.top[par];
+    b.carry = r.carry + (par ^ 1) * KSG_BATCH_MAX;
+    b.carry_n = carry_n + (par ^ 1);
+    b.carry_out = r.carry + par * KSG_BATCH_MAX;
+    b.carry_out_n = carry_n + par;
+    b.tk_seq = (unsigned)bi + 1;
+    hipLaunchKernelGGL(ksg_batch_phase1, dim3(((((N + 255) / 256) + 7) & ~7) * b.nb), dim3(256), 0, s1, b);
+    hipLaunchKernelGGL(ksg_batch_topk<1024>, dim3(b.nb), dim3(1024), 0, s1, b);
+  }
+  HIPC(ctx, hipGetLastError());
+  HIPC(ctx, hipEventRecord(ctx->ev1, s2));
+  return KSG_OK;
+}
+
 // Pipelined batched path (the two-batch window).  Batch b's phase 1 + top-k run on
 // a second stream while batch b - 1's phase 2 runs: phase 1 of batch b reads
 // the state at least as of the end of batch b - 2 (it waits for that phase 2),
@@ -988,6 +1133,8 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   HIPC(ctx, hipEventRecord(ctx->ev0, s2));
   if (overlap) HIPC(ctx, hipStreamWaitEvent(s1, ctx->ev0, 0));
   if ((rc = tmark(ctx))) return rc;
+  if (specw && overlap && ctx->spec_persist)
+    return run_spec_persistent(ctx, b, first, count, cm_words, mw, tk, carry_n);
   int prev_nb = 0;
   for (int off = 0, bi = 0; off < count; bi++) {
     const int par = bi & 1;
@@ -3329,6 +3476,7 @@ int ksg_open(int device, ksg_ctx** out) {
   }
   if (const char* f = getenv("KSG_PIPE_WINDOW")) ctx->pipe_window = atoi(f) != 0;
   if (const char* f = getenv("KSG_PIPE_OVERLAP")) ctx->pipe_overlap = atoi(f) != 0;
+  if (const char* f = getenv("KSG_SPEC_PERSIST")) ctx->spec_persist = atoi(f) != 0;
   if (const char* f = getenv("KSG_EVAL_FAST")) ctx->eval_fast = atoi(f) != 0;
   if (const char* f = getenv("KSG_CYCLE_COOP")) ctx->cycle_coop = atoi(f) != 0;
   if (const char* f = getenv("KSG_COOP_LAUNCH")) ctx->coop_launch = ctx->topo_eval_coop = atoi(f) != 0;
@@ -3363,6 +3511,7 @@ int ksg_close(ksg_ctx* ctx) {
   }
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->h_ev) (void)hipHostFree(ctx->h_ev);
+  if (ctx->h_p2done) (void)hipHostFree(ctx->h_p2done);
   if (ctx->h_evt) (void)hipHostFree(ctx->h_evt);
   if (ctx->d_json_tab) (void)hipFree(ctx->d_json_tab);
   if (ctx->json_stream) (void)hipStreamSynchronize(ctx->json_stream);

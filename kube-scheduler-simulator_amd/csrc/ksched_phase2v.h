@@ -67,8 +67,9 @@ struct SvItem {
   int32_t t;               // the pod whose assume made the version (-1: none, the carried live row)
 };
 
+// One batch's walk (the body of both kernels below).
 template <int BLOCK, bool MW = false>
-__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
+__device__ __forceinline__ void spec_walk_batch(const BatchArgs& a) {
   using SL = SlotLayout<4>;
   constexpr int NW = BLOCK / 64;
   constexpr int SW = SL::W;
@@ -713,4 +714,76 @@ __global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
   if (tid == 0 && a.stamps)
     for (int i = 0; i < 16; i++) atomicAdd(&a.stamps[i], st_acc[i]);
 #endif
+}
+
+// One launch per batch (stream-ordered runs, the counter passes).
+template <int BLOCK, bool MW = false>
+__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v(BatchArgs a) {
+  spec_walk_batch<BLOCK, MW>(a);
+}
+
+// The persistent walk (round 6): one launch walks every batch of the run, so
+// the single-workgroup walk no longer pays a dispatch, its kernel-boundary
+// cache operations and an event between batches (a 6.6 us median gap per
+// 64-pod batch on the headline, profiles/r6).  Batch b's arguments come from
+// the host's table; its top-k hand-off is the same flag poll.  After each
+// batch every wave drains its stores, one lane writes the XCD's L2 back (agent
+// release: the node state, the zeroed maxima and the carry that phase 1 of
+// batch b + 2 reads from other XCDs) and stores b + 1 into the host-visible
+// counter; the host launches phase 1 / top-k of batch b + 2 once it reads it
+// (their dispatch acquires).  A timed-out hand-off or a broken invariant ends
+// the loop (the host reports it).
+struct SpecRun {
+  const int32_t* btab;   // [nbatch][6]: b0, out0, nb, prog_lo, prog_len, k_extra
+  int32_t nbatch;
+  uint64_t* rec[2];
+  int32_t* img[2];
+  uint64_t* rect[2];
+  int32_t* imgt[2];
+  int32_t* pmax[2];
+  P1Stats* p1[2];
+  uint64_t* top[2];
+  int32_t* carry;        // [2][KSG_BATCH_MAX]
+  int32_t* carry_n;      // [2]
+  unsigned* done;        // batches walked (pinned host memory, the device address)
+};
+
+template <int BLOCK, bool MW = false>
+__global__ __launch_bounds__(BLOCK) void ksg_batch_phase2v_run(BatchArgs base, SpecRun r) {
+  __shared__ int s_stop;
+  using G1 = __attribute__((address_space(1))) unsigned;
+  for (int bi = 0; bi < r.nbatch; bi++) {
+    BatchArgs a = base;
+    const int32_t* d = r.btab + 6 * bi;
+    a.b0 = d[0];
+    a.out0 = d[1];
+    a.nb = d[2];
+    a.prog_lo = d[3];
+    a.prog_len = d[4];
+    a.k_extra = d[5];
+    const int par = bi & 1;
+    a.rec = r.rec[par];
+    a.img = r.img[par];
+    a.rect = r.rect[par];
+    a.imgt = r.imgt[par];
+    a.pmax = r.pmax[par];
+    a.p1 = r.p1[par];
+    a.top = r.top[par];
+    a.carry = r.carry + (par ^ 1) * KSG_BATCH_MAX;
+    a.carry_n = r.carry_n + (par ^ 1);
+    a.carry_out = r.carry + par * KSG_BATCH_MAX;
+    a.carry_out_n = r.carry_n + par;
+    a.tk_seq = (unsigned)bi + 1;
+    spec_walk_batch<BLOCK, MW>(a);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store((G1*)r.done, (unsigned)bi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_stop = (__hip_atomic_load((G1*)base.tk_timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                __hip_atomic_load((G1*)base.walk_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
+    }
+    __syncthreads();
+    if (s_stop) break;
+  }
 }
