@@ -470,6 +470,11 @@ def queue_roofline(metrics, kstats, bpe: int, node_evals: int, kms: float, pmc_f
     roof = metrics.price_decided_node_evals(roof, bpe, node_evals)
     roof["step"] = metrics.roofline(bpe, node_evals, kms)
     roof["step"]["kernel_ms"] = kms
+    # the timed steps run the persistent walk (one ksg_batch_phase2v_run launch
+    # per step, phase 1 / top-k beside it); the per-kernel pass runs with HIP
+    # events around every launch, which takes the one-launch-per-batch form of
+    # the same walk on one stream
+    roof["timing_pass"] = "per-batch launches, one stream (ksg_set_timing); timed steps: persistent walk"
     # HBM bytes per launch of the dominant kernel from the committed PMC passes
     # (profiles/run_pmc.sh -> profiles/pmc_summary.py: 2 x FETCH_SIZE +
     # WRITE_SIZE per dispatch, gfx950-corrected), null when not collected
