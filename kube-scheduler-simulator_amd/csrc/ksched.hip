@@ -541,7 +541,19 @@ bool host_writable(const void* p, size_t len) {
   return ok;
 }
 
+// At most one persistent per-cycle server per process.  Two contexts' servers
+// alive together, one of them idling towards its exit while the other context
+// starts its own, faulted a GPU test sequence (round 6, tests/test_gpu_eval.py
+// with the module engine's server outliving its test; not reproduced with the
+// servers serialised).  A context starting its server stops the other's first,
+// under a process-wide lock that every server call holds from its post to its
+// completion, so no call of the other context is in flight.
+std::recursive_mutex g_srv_mu;
+ksg_ctx* g_srv_ctx = nullptr;
+
 int srv_stop(ksg_ctx* ctx) {
+  std::lock_guard<std::recursive_mutex> lk(g_srv_mu);
+  if (ctx && g_srv_ctx == ctx) g_srv_ctx = nullptr;
   if (!ctx || !ctx->srv_running) return KSG_OK;
   ctx->srv_running = false;
   SrvMailbox* mb = ctx->h_mb;
@@ -2517,6 +2529,8 @@ bool eval_fast_eligible(ksg_ctx* ctx, int32_t pod) {
 }
 
 int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_eval_rows* view = nullptr) {
+  std::unique_lock<std::recursive_mutex> srv_lk(g_srv_mu, std::defer_lock);
+  if (ctx->srv_mode) srv_lk.lock();   // (g_srv_mu) the whole call: no other context stops this server mid-call
   const size_t N = ctx->c.N;
   const ksg_profile& prof = ctx->prof;
   // score rows: the raw values of every plugin the profile scores.  The
@@ -2657,6 +2671,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
     HIPC(ctx, hipMemsetAsync(ctx->d_ev + d_to, 0x01, sizeof(unsigned), ctx->stream));
   }
   if (server && !ctx->srv_running) {   // the persistent form: started once, fed through the mailbox
+    if (g_srv_ctx && g_srv_ctx != ctx && (rc = srv_stop(g_srv_ctx))) return rc;   // one server per process
     if (!ctx->h_mb) {
       // The mailbox in fine-grained device memory when the CPU can write it
       // (large BAR: the allocation is mapped writable into this process):
@@ -2724,6 +2739,7 @@ int eval_fast(ksg_ctx* ctx, int32_t pod, ksg_result* res, ksg_capture* cap, ksg_
       HIPC(ctx, hipLaunchKernel(kf, dim3(G), dim3(64), sargs, 0, ctx->stream));
     HIPC(ctx, hipGetLastError());
     ctx->srv_running = true;
+    g_srv_ctx = ctx;
     ctx->srv_last = std::chrono::steady_clock::now();
     ctx->srv_kn = kn;
     ctx->srv_G = G;
