@@ -800,7 +800,7 @@ bool spec_candidate(const ksg_ctx* ctx) {
   int64_t wsum = 0;
   for (int pl = 0; pl < KSG_NPLUGINS; pl++)
     if ((ctx->prof.score_mask >> pl) & 1u) wsum += ctx->prof.weight[pl];
-  return ctx->c.R <= 4 && wsum * 100 < (1 << kSvTotalBits) && ctx->c.N < (1 << 26);   // (owner entries: lane << 26 | node)
+  return ctx->c.R <= 4 && wsum * 100 < (1 << kSvTotalBits);
 }
 
 int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_result* d_res, const CapArgs* cap,

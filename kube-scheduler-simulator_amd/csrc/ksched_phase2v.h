@@ -88,8 +88,7 @@ __device__ __forceinline__ void spec_walk_batch(const BatchArgs& a) {
   __shared__ uint8_t s_snap[64 * 64];     // [macro-step][pod] T pointers at the macro-step's start
   __shared__ uint8_t s_mstep[64];         // pod's macro-step in the current round
   __shared__ uint8_t s_dptr[64];          // pod's T pointer when it was decided
-  __shared__ uint32_t s_owner[kSvOwner];  // lowest (lane << 26 | node) among the lanes whose node hashes here,
-                                          // 0xffffffff = none
+  __shared__ uint32_t s_owner[kSvOwner];  // lowest lane holding a node (hashed), 0xffffffff = none
   __shared__ SvItem s_item[64 + 1];       // a round's special items: carried slots / the correction
   __shared__ int32_t s_ctl[8];            // round: start, nv_c, ns_c, n_special; progress; next item
   __shared__ P1Stats s_p1[64];
@@ -361,12 +360,9 @@ __device__ __forceinline__ void spec_walk_batch(const BatchArgs& a) {
         s_snap[mi * 64 + lane] = (uint8_t)ptr;
         const bool act = lane >= cur && lane < nb && cnode >= 0;
         const int hsh = cnode & (kSvOwner - 1);
-        const unsigned me = ((unsigned)lane << 26) | (unsigned)cnode;   // (node < 2^26: spec_candidate)
-        if (act) atomicMin(&s_owner[hsh], me);
+        if (act) atomicMin(&s_owner[hsh], (unsigned)lane);
         // (one wave: the LDS executes its DS instructions in order, so this read sees every lane's min)
-        const unsigned ow = act ? s_owner[hsh] : me;
-        const unsigned o = ow >> 26;                                    // the bucket's lowest lane
-        const bool same = (ow & ((1u << 26) - 1)) == (unsigned)cnode;    // ... holds this lane's node
+        const unsigned o = act ? s_owner[hsh] : (unsigned)lane;
         const uint64_t dup = __ballot(act && o != (unsigned)lane);
         const int f = dup ? __builtin_ctzll(dup) : nb;
 #ifdef KSG_STAMPS
@@ -382,16 +378,9 @@ __device__ __forceinline__ void spec_walk_batch(const BatchArgs& a) {
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
           __hip_atomic_store(&s_ctl[4], f - start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        // later pods whose candidate the run took: a run lane is the lowest of
-        // its bucket, so a lane whose bucket's lowest lane is past the run
-        // keeps its node, and one whose lowest lane is in the run holding the
-        // same node loses it; only a hash collision with a run lane reads the
-        // bitmap (round 6: one LDS round trip fewer per macro-step)
-        const bool hit = lane >= f && lane < nb && cnode >= 0 && o < (unsigned)f;
-        bool conflict = hit && same;
-        if (__ballot(hit && !same)) {
-          if (hit && !same) conflict = sv_changed(s_cmask, cnode);
-        }
+        // later pods whose candidate the run took (the owner prefilter has no
+        // false negatives; the bitmap decides, hashing collisions included)
+        bool conflict = lane >= f && lane < nb && cnode >= 0 && o < (unsigned)f && sv_changed(s_cmask, cnode);
         while (__ballot(conflict)) {
 #ifdef KSG_STAMPS
           if (tid == 0) st_acc[13] += 1;   // step-on iterations
