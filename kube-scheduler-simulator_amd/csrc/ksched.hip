@@ -171,6 +171,7 @@ struct ksg_ctx {
   bool last_spec = false;     // ... the speculate-and-verify walk
   bool last_mw = false;       // ... in its wide-memory instance
   bool spec_persist = true;   // env KSG_SPEC_PERSIST=0: one spec-walk launch per batch (else one for the run)
+  bool last_persist = false;  // the last batched run took the persistent walk (its state saved first)
   unsigned* h_p2done = nullptr;   // the persistent walk's batches-walked counter (pinned, mapped)
   unsigned* d_p2done = nullptr;
   int32_t* d_btab = nullptr;      // its batch table ([batch][6]; grown, freed with the context)
@@ -924,6 +925,8 @@ int run_batched(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_r
 // batch's top-k flag as before.  The host's wait is bounded: a walk that
 // ended early (a timed-out hand-off, a broken invariant) stops the launches
 // and run_internal reports its words.
+int state_copy(ksg_ctx* ctx, bool save);
+
 int run_spec_persistent(ksg_ctx* ctx, const BatchArgs& b0, int32_t first, int32_t count, size_t cm_words, bool mw,
                         unsigned* tk, int32_t* carry_n) {
   const int N = ctx->c.N;
@@ -972,7 +975,15 @@ int run_spec_persistent(ksg_ctx* ctx, const BatchArgs& b0, int32_t first, int32_
     ctx->d_p2done = static_cast<unsigned*>(dp);
   }
   hipStream_t s1 = ctx->stream2, s2 = ctx->stream;
+  // the pre-call state, for a walk whose top-k poll gives up (run_internal
+  // restores it and runs the per-batch form)
+  if ((rc = state_copy(ctx, true))) return rc;
+  ctx->last_persist = true;
   HIPC(ctx, hipMemcpyAsync(ctx->d_btab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice, s2));
+  if (ctx->inject_timeout & 16) {   // test injection: the walk finds its poll's give-up word set after batch 0
+    ctx->inject_timeout &= ~16;
+    HIPC(ctx, hipMemsetAsync(tk + 2, 0x01, 1, s2));
+  }
   volatile unsigned* done = ctx->h_p2done;
   *done = 0;
   std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -1064,6 +1075,7 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
   int rc;
   ctx->last_spec = false;
   ctx->last_mw = false;
+  ctx->last_persist = false;
   if (!ctx->d_prec[0]) {
     for (int q = 0; q < 2; q++) {
       if ((rc = dalloc(ctx, &ctx->d_prec[q], (size_t)KSG_BATCH_MAX * N))) return rc;
@@ -1077,7 +1089,13 @@ int run_pipe(ksg_ctx* ctx, int32_t first, int32_t count, int32_t* d_pl, ksg_resu
     if ((rc = dalloc(ctx, &ctx->d_carry, (size_t)2 * KSG_BATCH_MAX + 6))) return rc;   // + carry_n[2], tk[4]
   }
   if (!ctx->stream2) {
-    HIPC(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    // the second stream at another priority than the main one: the runtime
+    // keeps a queue pool per priority, so the two never share a hardware
+    // queue, where the persistent walk would sit in front of the phase 1 /
+    // top-k launches it waits for
+    int least = 0, greatest = 0;
+    HIPC(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPC(ctx, hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, greatest));
     for (int q = 0; q < 2; q++) {
       HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_tk[q], hipEventDisableTiming));
       HIPC(ctx, hipEventCreateWithFlags(&ctx->ev_p2[q], hipEventDisableTiming));
@@ -2474,6 +2492,17 @@ int run_internal(ksg_ctx* ctx, int32_t first, int32_t count, int do_commit, int3
     unsigned tkf[4] = {0, 0, 0, 0};
     HIPC(ctx, hipMemcpy(tkf, ctx->pipe_tk, sizeof(tkf), hipMemcpyDeviceToHost));
     ctx->pipe_tk = nullptr;
+    if (tkf[2] == 1 && ctx->last_persist) {
+      // the persistent walk waited out its poll for a top-k (a launch it
+      // depends on queued behind it): the pre-call state back, then the
+      // per-batch form, which launches each walk after its top-k
+      if (ctx->stream2) HIPC(ctx, hipStreamSynchronize(ctx->stream2));
+      if (do_commit && (rc = state_copy(ctx, false))) return rc;
+      ctx->last_persist = false;
+      ctx->spec_persist = false;
+      ctx->recoveries++;
+      return run_internal(ctx, first, count, do_commit, placements, results, cap);
+    }
     if (tkf[2] == 1) return fail(ctx, KSG_E_DEVICE, "batched path: top-k hand-off poll timed out");
     if (tkf[2] || tkf[3])
       return fail(ctx, KSG_E_DEVICE, "batched path: speculate-and-verify walk invariant broken (code " +

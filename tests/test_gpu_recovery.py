@@ -144,6 +144,31 @@ def test_timeout_topology_one_pod_recovers(oracle, monkeypatch):
         eng.close()
 
 
+def test_persistent_walk_recovers(oracle, monkeypatch):
+    """The persistent spec walk gives up waiting for a top-k (injected: its
+    give-up word set after batch 0): the call restores the pre-call state and
+    runs the per-batch form (from then on), equal to the oracle."""
+    eng = _engine(monkeypatch, KSG_TEST_INJECT_TIMEOUT=16)
+    try:
+        nodes, pods, prof = G.config2(n_nodes=1500, n_pods=1000, seed=21)
+        enc = E.Encoder(nodes, pods, prof)
+        pf = E.encode_profile(prof, enc.cluster.res_names)
+        eng.load(enc, pf)
+        oracle.load(enc, pf)
+        pg, rg = eng.run_queue(0, len(pods))
+        po, ro = oracle.run_queue(0, len(pods))
+        np.testing.assert_array_equal(pg, po)
+        for f in ("n_feasible", "status", "score_skip"):
+            np.testing.assert_array_equal(rg[f], ro[f], err_msg=f)
+        R = len(enc.cluster.res_names)
+        for x, y in zip(eng.read_state(R), oracle.read_state(R)):
+            np.testing.assert_array_equal(x, y)
+        assert eng.recoveries() == 1
+        assert eng.last_run_info()[1] & native.RUN_SPEC
+    finally:
+        eng.close()
+
+
 def test_timeout_replica_sweep_recovers(oracle, monkeypatch):
     eng = _engine(monkeypatch, KSG_TEST_INJECT_TIMEOUT=4)
     try:
