@@ -1291,6 +1291,15 @@ hipError_t launch_sweep(const SweepArgs& s, int grid, int mode, bool narrow, hip
                               : (const void*)ksg_sweep<BLOCK, KN, false, MULTI>;
   return launch_one<BLOCK, MULTI>(f, s, grid, st);
 }
+// The narrow fast sweep of a few replicas over a large cluster with every
+// result in registers: 512-lane workgroups at 8 waves per CU (256 VGPRs),
+// 64 nodes per lane, so a group of S = N / 32,768 workgroups needs no
+// scratch row (configs[4]: S = 4 instead of 8 with the row).
+const void* sweep_wide_kernel(int mode) {
+  return mode == 2 ? (const void*)ksg_sweep<512, 64, true, true, true, true>
+                   : (const void*)ksg_sweep<512, 64, true, true, false, true>;
+}
+
 template <int BLOCK, int KN, bool MULTI>
 hipError_t launch_sweep_ex(const SweepArgs& s, int grid, bool narrow, hipStream_t st) {
   const void* f = narrow ? (const void*)ksg_sweep<BLOCK, KN, true, MULTI, true, true>
@@ -1463,6 +1472,20 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     if ((long long)R * S <= (long long)occ * cus) break;   // every workgroup of a group co-resident
     S = S / 2;
   }
+  // the register-resident wide form when the scratch form was chosen for the
+  // narrow fast state and its groups are co-resident
+  bool wide = false;
+  if (kn == 0 && S > 1 && mode >= 1 && narrow && !getenv("KSG_SWEEP_NO_WIDE")) {
+    const int S2 = (N + 512 * 64 - 1) / (512 * 64);
+    int occ = 0;
+    HIPC(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, sweep_wide_kernel(mode), 512, 0));
+    if (S2 > 1 && (long long)R * S2 <= (long long)occ * cus) {
+      wide = true;
+      S = S2;
+      block = 512;
+      kn = 64;
+    }
+  }
   s.S = S;
   if (kn == 0) TA(tmp, &s.scratch, sizeof(uint64_t) * (size_t)R * N);
   if (S > 1) {
@@ -1490,7 +1513,9 @@ int run_sweep(ksg_ctx* ctx, const QueueArgs& a, const ksg_profile* profiles, con
     const int grid = R * S;
     const int key = block * 100 + kn;
     hipError_t le;
-    if (mode == 2) {
+    if (wide) {
+      le = launch_one<512, true>(sweep_wide_kernel(mode), s, grid, ctx->stream);
+    } else if (mode == 2) {
       if (S > 1) {
         if (key == 25608) le = launch_sweep_ex<256, 8, true>(s, grid, narrow, ctx->stream);
         else le = launch_sweep_ex<256, 0, true>(s, grid, narrow, ctx->stream);
